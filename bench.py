@@ -1,0 +1,212 @@
+#!/usr/bin/env python
+"""Benchmark: log-likelihood evaluations / s on the N=16384 dense Matérn-3/2
+covariance (BASELINE.json metric), one process per GPU.
+
+A step = one block of ``--eta-per-rank`` eta values of the 64-point grid
+logspace(-3, 3, 64) per rank: one batched device call factorizes
+K + eta_b I (fp64 MFMA Cholesky, fused forward solve of [X | z], logdet and
+Gram), the host forms the direct log-likelihood (sigma = 1, sigma0 = sqrt(eta)),
+and ONE all-gather (RCCL over xGMI at N > 1) collects the [logdet, lp] curve.
+K is assembled on each GPU from the points before the timed region (inputs
+resident in HBM). Per-rank work is fixed: scaling "weak".
+
+Launch: python bench.py [--gpus 1 --steps K --warmup W]
+        python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+"""
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG_ROOT = os.path.join(REPO, 'gaussian-process-param-estimation_amd')
+for p in (REPO, PKG_ROOT):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+FP64_MFMA_PEAK_TFLOPS = 78.6    # MI355X fp64 matrix, dense (AMD spec)
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=5)
+    ap.add_argument('--warmup', type=int, default=2)
+    ap.add_argument('--grid', type=int, default=128, help='points per axis (n = grid^2)')
+    ap.add_argument('--nu', type=float, default=1.5)
+    ap.add_argument('--eta-per-rank', type=int, default=8)
+    ap.add_argument('--outer', type=int, default=2, help='outer panel width / 128')
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-timing', action='store_true',
+                    help='skip the per-kernel HIP-event roofline timing')
+    return ap.parse_args()
+
+
+def cpu_baseline(points, z, X, nu, etas):
+    """The reference's CPU call pattern, timed on this host (rank 0, N=1):
+    Likelihood -> MixedCorrelation(imate_method='eigenvalue') -> per eval
+    2 x scipy.linalg.solve(K + eta I, ., assume_a='pos') + O(n) eigen logdet
+    (_direct_likelihood.py:59-71, mixed_correlation.py:239-299). Sample: ONE
+    evaluation at the full N (the one-time eigh setup is excluded and reported
+    separately as not timed). Uses the oracle restatement (kind 'port')."""
+    from oracle import matern
+    import scipy.linalg
+    try:
+        from threadpoolctl import threadpool_info
+        threads = max([i.get('num_threads', 1) for i in threadpool_info()
+                       if i.get('user_api') == 'blas'] or [os.cpu_count()])
+    except Exception:
+        threads = os.cpu_count()
+    K = matern.dense_correlation(points, 0.1, nu)
+    eta = float(etas[0])
+    n = K.shape[0]
+    t0 = time.perf_counter()
+    Kn = K.copy()
+    Kn[numpy.diag_indices(n)] += eta
+    Y = scipy.linalg.solve(Kn, X, assume_a='pos')          # solve(eta, X)  :62
+    Kn = K.copy()
+    Kn[numpy.diag_indices(n)] += eta
+    w = scipy.linalg.solve(Kn, z, assume_a='pos')          # solve(eta, z)  :332
+    _ = (X.T @ Y, w)
+    dt = time.perf_counter() - t0
+    cpu = platform.processor() or platform.machine()
+    try:
+        with open('/proc/cpuinfo') as fh:
+            for line in fh:
+                if line.startswith('model name'):
+                    cpu = line.split(':', 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {'value': 1.0 / dt, 'unit': 'evals/s', 'cores': int(threads), 'kind': 'port',
+            'sample': 'one direct log-likelihood eval at N=%d (2 x scipy.linalg.solve '
+                      'assume_a=pos, eigen-logdet setup excluded), %.1f s; host %s, '
+                      'os.cpu_count()=%d' % (n, dt, cpu, os.cpu_count())}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    from gaussian_proc import generate_correlation, _data
+    from gaussian_proc._mixed_correlation import MixedCorrelation
+    from gaussian_proc._likelihood._direct_likelihood import _lp_from_terms
+
+    points = _data.generate_points(args.grid, 2, True)
+    z = _data.generate_data(points, 0.2)
+    X = _data.generate_basis_functions(points, 2)
+    n, m = X.shape
+    B = args.eta_per_rank
+    D = generate_correlation(points, 0.1, args.nu, device_resident=True, device=local,
+                             max_batch=B)
+    op = MixedCorrelation(D)
+    op.op.set_outer(args.outer)
+    op.set_rhs(X, z)
+    grid = numpy.logspace(-3, 3, 64)
+
+    def step_etas(s):
+        idx = [(s * world * B + rank * B + j) % grid.size for j in range(B)]
+        return grid[idx]
+
+    def step(s, timing_acc=None):
+        etas = step_etas(s)
+        ld, G = op.loglik_terms(etas, X, z)
+        if timing_acc is not None:
+            t = op.op.last_timing()
+            timing_acc['syrk_ms'] += t['syrk_ms']
+            timing_acc['syrk_flops'] += t['syrk_flops']
+            timing_acc['syrk_launches'] += t['syrk_launches']
+            timing_acc['total_ms'] += t['total_ms']
+        lp = numpy.array([_lp_from_terms(n, m, 1.0, l, g) for l, g in zip(ld, G)])
+        res = torch.from_numpy(numpy.stack([etas, ld, lp], axis=1)).cuda()
+        if world > 1:
+            out = torch.empty((world * B, 3), dtype=torch.float64, device=res.device)
+            dist.all_gather_into_tensor(out, res)
+            return out
+        return res
+
+    for s in range(args.warmup):
+        step(s)
+    timing = {'syrk_ms': 0.0, 'syrk_flops': 0.0, 'syrk_launches': 0, 'total_ms': 0.0}
+    op.op.set_timing(not args.no_timing)
+    barrier()
+    t0 = time.perf_counter()
+    last = None
+    for s in range(args.steps):
+        last = step(args.warmup + s, None if args.no_timing else timing)
+    barrier()
+    dt = time.perf_counter() - t0
+    op.op.set_timing(False)
+    t_max = torch.tensor([dt], dtype=torch.float64, device='cuda')
+    if world > 1:
+        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+    dt = float(t_max.item())
+    evals = world * B * args.steps
+    flops_eval = n ** 3 / 3.0 + 2.0 * n ** 2 * (m + 1) + n ** 2
+    result = None
+    if rank == 0:
+        roof = None
+        if not args.no_timing and timing['syrk_ms'] > 0:
+            achieved = timing['syrk_flops'] / (timing['syrk_ms'] * 1e-3) / 1e12
+            roof = {'bound': 'mfma', 'achieved': round(achieved, 3),
+                    'peak': FP64_MFMA_PEAK_TFLOPS, 'unit': 'TFLOP/s',
+                    'frac': round(achieved / FP64_MFMA_PEAK_TFLOPS, 4), 'traffic': None,
+                    'kernel': 'syrk_kernel (trailing update, fp64 MFMA 16x16x4)',
+                    'launches': timing['syrk_launches'],
+                    'avg_launch_ms': round(timing['syrk_ms'] / max(1, timing['syrk_launches']), 4)}
+        whole = flops_eval * evals / world / dt / 1e12
+        result = {
+            'metric': 'log-likelihood evals/sec (N=16384 dense Matern-3/2)',
+            'value': evals / dt,
+            'unit': 'evals/s',
+            'n_gpus': world,
+            'steps': args.steps,
+            'warmup': args.warmup,
+            'ms_per_step': dt / args.steps * 1e3,
+            'higher_is_better': True,
+            'scaling': 'weak',
+            'vs_baseline': None,
+            'dtype': 'f64',
+            'data': 'synthetic (reference data_utilities: 2D grid, sin + 0.2 noise seed 31, '
+                    'deg-2 basis)',
+            'config': {'workload': 'cfg3: N=%d 2D grid Matern nu=%g rho=0.1, eta grid '
+                                   'logspace(-3,3,64), %d eta/rank/step' % (n, args.nu, B),
+                       'n': n, 'm': m, 'eta_per_rank_per_step': B,
+                       'outer_panel': 128 * args.outer,
+                       'parallelism': 'eta-shard x%d + all-gather' % world},
+            'roofline': roof,
+            'whole_eval_tflops_per_gpu': round(whole, 3),
+            'whole_eval_mfma_frac': round(whole / FP64_MFMA_PEAK_TFLOPS, 4),
+            'flops_per_eval': flops_eval,
+            'lp_sample': [float(v) for v in last[0].tolist()] if last is not None else None,
+            'cpu_baseline': None,
+        }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result['cpu_baseline'] = cpu_baseline(points, z, X, args.nu, step_etas(0))
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

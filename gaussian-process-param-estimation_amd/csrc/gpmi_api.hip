@@ -1,0 +1,612 @@
+// C-ABI (include/gpmi.h) and host orchestration of the gpmi kernels.
+//
+// One gpmi_op = one device-resident correlation matrix K (padded to n_pad, a
+// multiple of 128, identity in the pad) plus workspace for max_batch
+// concurrent factorizations of K + eta_b I. All work of an op runs in order on
+// the op's own HIP stream; the host blocks only when it reads results back.
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "gpmi_internal.h"
+#include "../../include/gpmi.h"
+
+using namespace gpmi;
+
+namespace {
+
+thread_local char g_err[512] = "";
+
+int set_err(int code, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+  return code;
+}
+
+#define HIP_TRY(expr)                                                              \
+  do {                                                                             \
+    hipError_t e_ = (expr);                                                        \
+    if (e_ != hipSuccess)                                                          \
+      return set_err(-(int)e_, "%s failed: %s", #expr, hipGetErrorString(e_));     \
+  } while (0)
+
+#define LAUNCH_CHECK(name)                                                         \
+  do {                                                                             \
+    hipError_t e_ = hipGetLastError();                                             \
+    if (e_ != hipSuccess)                                                          \
+      return set_err(-(int)e_, "launch of %s failed: %s", name,                    \
+                     hipGetErrorString(e_));                                       \
+  } while (0)
+
+constexpr int TS = GPMI_TS;
+constexpr int RLD = GPMI_RHS_LD;
+constexpr int OUT_LD = 1 + RLD * RLD;
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    (void)hipGetDevice(&prev);
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    (void)hipGetDevice(&cur);
+    if (prev >= 0 && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+}  // namespace
+
+struct gpmi_op {
+  int device = 0;
+  int64_t n = 0, n_pad = 0;
+  int nt = 0;
+  int max_batch = 1;
+  int outer = 2;
+  hipStream_t stream = nullptr;
+  double* K = nullptr;       // [n_pad][n_pad]
+  double* A = nullptr;       // [max_batch][n_pad][n_pad]
+  double* R = nullptr;       // [max_batch][n_pad][16]
+  double* X = nullptr;       // [max_batch][n_pad][16]
+  double* U = nullptr;       // [max_batch][128][16]
+  double* Linv = nullptr;    // [max_batch][nt][128][128]
+  double* logdiag = nullptr; // [max_batch][nt]
+  double* gram = nullptr;    // [max_batch][nt][256]
+  double* out = nullptr;     // [max_batch][OUT_LD]
+  double* etas = nullptr;    // [max_batch]
+  double* rhs_src = nullptr; // [n_pad][16]
+  double* scratch = nullptr; // [n_pad][16] (matvec input)
+  double* scratch2 = nullptr;// [n_pad][16] (matvec output)
+  double* tracebuf = nullptr;// [n_pad][2]
+  int* info = nullptr;       // [max_batch]
+  int nrhs = 0;
+  bool has_K = false;
+  // factor cache: batch slot 0 holds the factor of K + cached_eta I
+  bool cache_valid = false;
+  double cached_eta = 0.0;
+  // timing
+  bool timing = false;
+  std::vector<hipEvent_t> ev;
+  hipEvent_t ev_begin = nullptr, ev_end = nullptr;
+  double last_syrk_ms = 0.0, last_syrk_flops = 0.0, last_total_ms = 0.0;
+  int last_syrk_launches = 0;
+  std::vector<std::pair<int, double>> syrk_log;  // (event index, flops)
+
+  BatchPtrs ptrs() const {
+    BatchPtrs p;
+    p.A = A;
+    p.sA = n_pad * n_pad;
+    p.R = R;
+    p.sR = n_pad * RLD;
+    p.U = U;
+    p.sU = (int64_t)TS * RLD;
+    p.Linv = Linv;
+    p.sL = (int64_t)nt * TS * TS;
+    p.logdiag = logdiag;
+    p.sLD = nt;
+    p.gram = gram;
+    p.sG = (int64_t)nt * 256;
+    p.info = info;
+    return p;
+  }
+};
+
+namespace {
+
+int launch_syrk(gpmi_op* op, int nb, int tc0, int w, int t, int p0, int kdim) {
+  const int tri = w * (w + 1) / 2;
+  const int tiles = tri + (t - w) * w;
+  if (tiles <= 0) return 0;
+  int evi = -1;
+  if (op->timing) {
+    evi = (int)op->syrk_log.size() * 2;
+    if ((int)op->ev.size() < evi + 2) {
+      for (int k = 0; k < 64; ++k) {
+        hipEvent_t e;
+        HIP_TRY(hipEventCreate(&e));
+        op->ev.push_back(e);
+      }
+    }
+    HIP_TRY(hipEventRecord(op->ev[evi], op->stream));
+  }
+  hipLaunchKernelGGL(syrk_kernel, dim3(tiles, nb), dim3(256), 0, op->stream, op->A,
+                     (int64_t)op->n_pad, op->n_pad * op->n_pad, tc0, w, t, p0, kdim);
+  LAUNCH_CHECK("syrk_kernel");
+  if (op->timing) {
+    HIP_TRY(hipEventRecord(op->ev[evi + 1], op->stream));
+    // algorithmic flops: lower triangle only (diagonal tiles count 128*129/2 entries)
+    const double offd = (double)(tiles - std::min(tiles, w)) * TS * TS;
+    const double diag = (double)std::min(tiles, w) * TS * (TS + 1) / 2.0;
+    const double fl = 2.0 * (offd + diag) * kdim * nb;
+    op->syrk_log.push_back({evi, fl});
+  }
+  return 0;
+}
+
+// Factor K + eta_b I for b < nb, with the fused forward substitution of the
+// RHS block (copied from rhs_src). Results stay on the device.
+int run_factor(gpmi_op* op, const double* etas_host, int nb, const double* rhs_dev) {
+  if (!op->has_K) return set_err(-1000, "operator has no matrix (load or assemble first)");
+  if (nb < 1 || nb > op->max_batch)
+    return set_err(-1001, "batch %d outside [1, %d]", nb, op->max_batch);
+  DeviceGuard g(op->device);
+  hipStream_t s = op->stream;
+  const int nt = op->nt;
+  const int64_t lda = op->n_pad;
+  BatchPtrs P = op->ptrs();
+  op->syrk_log.clear();
+  op->cache_valid = false;
+  if (op->timing) {
+    if (!op->ev_begin) {
+      HIP_TRY(hipEventCreate(&op->ev_begin));
+      HIP_TRY(hipEventCreate(&op->ev_end));
+    }
+    HIP_TRY(hipEventRecord(op->ev_begin, s));
+  }
+  HIP_TRY(hipMemcpyAsync(op->etas, etas_host, sizeof(double) * nb, hipMemcpyHostToDevice, s));
+  hipLaunchKernelGGL(shift_copy_kernel, dim3(nt * (nt + 1) / 2), dim3(256), 0, s, op->K, lda,
+                     op->A, lda, P.sA, op->etas, nb, op->n, nt);
+  LAUNCH_CHECK("shift_copy_kernel");
+  for (int b = 0; b < nb; ++b)
+    HIP_TRY(hipMemcpyAsync(op->R + b * P.sR, rhs_dev, sizeof(double) * P.sR,
+                           hipMemcpyDeviceToDevice, s));
+  HIP_TRY(hipMemsetAsync(op->info, 0, sizeof(int) * nb, s));
+  int kb = 0;
+  while (kb < nt) {
+    const int S = std::min(op->outer, nt - kb);
+    for (int sp = 0; sp < S; ++sp) {
+      const int j = kb + sp;
+      if (sp > 0) {
+        int rc = launch_syrk(op, nb, j, 1, nt - j, kb * TS, sp * TS);
+        if (rc) return rc;
+      }
+      hipLaunchKernelGGL(diag_block_kernel, dim3(nb), dim3(256), 0, s, P, lda, j, nt);
+      LAUNCH_CHECK("diag_block_kernel");
+      if (j + 1 < nt) {
+        hipLaunchKernelGGL(panel_kernel, dim3(nt - j - 1, nb), dim3(256), 0, s, P, lda, j);
+        LAUNCH_CHECK("panel_kernel");
+      }
+    }
+    const int tc0 = kb + S;
+    if (tc0 < nt) {
+      const int t = nt - tc0;
+      int rc = launch_syrk(op, nb, tc0, t, t, kb * TS, S * TS);
+      if (rc) return rc;
+    }
+    kb += S;
+  }
+  hipLaunchKernelGGL(finalize_kernel, dim3(nb), dim3(256), 0, s, P, nt, op->out, OUT_LD);
+  LAUNCH_CHECK("finalize_kernel");
+  if (op->timing) HIP_TRY(hipEventRecord(op->ev_end, s));
+  return 0;
+}
+
+int collect_timing(gpmi_op* op) {
+  if (!op->timing) return 0;
+  HIP_TRY(hipEventSynchronize(op->ev_end));
+  double tot = 0.0, fl = 0.0;
+  for (auto& pr : op->syrk_log) {
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, op->ev[pr.first], op->ev[pr.first + 1]));
+    tot += ms;
+    fl += pr.second;
+  }
+  float all = 0.f;
+  HIP_TRY(hipEventElapsedTime(&all, op->ev_begin, op->ev_end));
+  op->last_syrk_ms = tot;
+  op->last_syrk_flops = fl;
+  op->last_syrk_launches = (int)op->syrk_log.size();
+  op->last_total_ms = all;
+  return 0;
+}
+
+int upload_rhs(gpmi_op* op, double* dst, const double* rhs, int64_t ld, int nrhs, int col0) {
+  // pack columns [col0, col0 + nrhs) of an [n][ld] host block into [n_pad][16]
+  std::vector<double> h((size_t)op->n_pad * RLD, 0.0);
+  for (int64_t i = 0; i < op->n; ++i)
+    for (int c = 0; c < nrhs; ++c) h[(size_t)i * RLD + c] = rhs[i * ld + col0 + c];
+  HIP_TRY(hipMemcpyAsync(dst, h.data(), sizeof(double) * h.size(),
+                         hipMemcpyHostToDevice, op->stream));
+  HIP_TRY(hipStreamSynchronize(op->stream));
+  return 0;
+}
+
+int ensure_factor(gpmi_op* op, double eta, const double* rhs_dev, bool* fresh) {
+  *fresh = false;
+  if (op->cache_valid && op->cached_eta == eta) return 0;
+  int rc = run_factor(op, &eta, 1, rhs_dev);
+  if (rc) return rc;
+  op->cache_valid = true;
+  op->cached_eta = eta;
+  *fresh = true;
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gpmi_version(void) { return 100; }
+
+int gpmi_last_error(char* buf, size_t len) {
+  if (!buf || !len) return 0;
+  strncpy(buf, g_err, len - 1);
+  buf[len - 1] = 0;
+  return 0;
+}
+
+int gpmi_device_count(int* count) {
+  HIP_TRY(hipGetDeviceCount(count));
+  return 0;
+}
+
+static int matern_params(double nu, MaternParams* P) {
+  if (!(nu > 0.0)) return set_err(-1002, "nu must be positive (got %g)", nu);
+  P->nu = nu;
+  P->sqrt2nu = std::sqrt(2.0 * nu);
+  P->prefactor = std::pow(2.0, 1.0 - nu) / std::tgamma(nu);
+  if (nu == 0.5) P->mode = MATERN_HALF;
+  else if (nu == 1.5) P->mode = MATERN_3HALF;
+  else if (nu == 2.5) P->mode = MATERN_5HALF;
+  else if (nu < 100) P->mode = MATERN_GENERAL;
+  else P->mode = MATERN_GAUSS;
+  return 0;
+}
+
+static int assemble(int device, hipStream_t s, const double* points, int64_t n, int d,
+                    const double* scale, double nu, double* Kdev, int64_t ldk,
+                    int64_t n_pad) {
+  if (d < 1 || d > GPMI_MAX_DIM)
+    return set_err(-1003, "dimension %d outside [1, %d]", d, GPMI_MAX_DIM);
+  MaternParams P;
+  int rc = matern_params(nu, &P);
+  if (rc) return rc;
+  DeviceGuard g(device);
+  double *dp = nullptr, *ds = nullptr;
+  HIP_TRY(hipMalloc(&dp, sizeof(double) * std::max<int64_t>(1, n * d)));
+  HIP_TRY(hipMalloc(&ds, sizeof(double) * d));
+  HIP_TRY(hipMemcpyAsync(dp, points, sizeof(double) * n * d, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(ds, scale, sizeof(double) * d, hipMemcpyHostToDevice, s));
+  dim3 grid((unsigned)((n_pad + 255) / 256), (unsigned)((n_pad + 15) / 16));
+  hipLaunchKernelGGL(matern_dense_kernel, grid, dim3(256), 0, s, dp, n, d, ds, P, Kdev, ldk,
+                     n_pad);
+  LAUNCH_CHECK("matern_dense_kernel");
+  HIP_TRY(hipStreamSynchronize(s));
+  HIP_TRY(hipFree(dp));
+  HIP_TRY(hipFree(ds));
+  return 0;
+}
+
+int gpmi_matern_dense(int device, const double* points, int64_t n, int d,
+                      const double* scale, double nu, double* K_out, int64_t ldk) {
+  if (n <= 0) return 0;
+  DeviceGuard g(device);
+  double* dK = nullptr;
+  HIP_TRY(hipMalloc(&dK, sizeof(double) * n * n));
+  int rc = assemble(device, nullptr, points, n, d, scale, nu, dK, n, n);
+  if (rc) {
+    (void)hipFree(dK);
+    return rc;
+  }
+  HIP_TRY(hipMemcpy2D(K_out, sizeof(double) * ldk, dK, sizeof(double) * n, sizeof(double) * n,
+                      n, hipMemcpyDeviceToHost));
+  HIP_TRY(hipFree(dK));
+  return 0;
+}
+
+int gpmi_op_create(int device, int64_t n, int max_batch, gpmi_op** out) {
+  if (!out) return set_err(-1004, "null output handle");
+  if (n <= 0) return set_err(-1005, "matrix size must be positive");
+  if (max_batch < 1) max_batch = 1;
+  DeviceGuard g(device);
+  gpmi_op* op = new gpmi_op();
+  op->device = device;
+  op->n = n;
+  op->n_pad = (n + TS - 1) / TS * TS;
+  op->nt = (int)(op->n_pad / TS);
+  op->max_batch = max_batch;
+  const int64_t np = op->n_pad;
+  auto fail = [&](hipError_t e, const char* what) {
+    gpmi_op_destroy(op);
+    return set_err(-(int)e, "allocation of %s failed: %s", what, hipGetErrorString(e));
+  };
+  hipError_t e;
+  if ((e = hipStreamCreateWithFlags(&op->stream, hipStreamNonBlocking)) != hipSuccess)
+    return fail(e, "stream");
+#define ALLOC(ptr, count)                                                           \
+  if ((e = hipMalloc(&op->ptr, sizeof(*op->ptr) * (size_t)(count))) != hipSuccess)  \
+    return fail(e, #ptr);
+  ALLOC(K, np * np);
+  ALLOC(A, (size_t)max_batch * np * np);
+  ALLOC(R, (size_t)max_batch * np * RLD);
+  ALLOC(X, (size_t)max_batch * np * RLD);
+  ALLOC(U, (size_t)max_batch * TS * RLD);
+  ALLOC(Linv, (size_t)max_batch * op->nt * TS * TS);
+  ALLOC(logdiag, (size_t)max_batch * op->nt);
+  ALLOC(gram, (size_t)max_batch * op->nt * 256);
+  ALLOC(out, (size_t)max_batch * OUT_LD);
+  ALLOC(etas, max_batch);
+  ALLOC(rhs_src, np * RLD);
+  ALLOC(scratch, np * RLD);
+  ALLOC(scratch2, np * RLD);
+  ALLOC(tracebuf, np * 2);
+  ALLOC(info, max_batch);
+#undef ALLOC
+  if ((e = hipMemsetAsync(op->rhs_src, 0, sizeof(double) * np * RLD, op->stream)) != hipSuccess)
+    return fail(e, "rhs memset");
+  if ((e = hipStreamSynchronize(op->stream)) != hipSuccess) return fail(e, "sync");
+  *out = op;
+  return 0;
+}
+
+int gpmi_op_destroy(gpmi_op* op) {
+  if (!op) return 0;
+  DeviceGuard g(op->device);
+  if (op->stream) (void)hipStreamSynchronize(op->stream);
+  double* bufs[] = {op->K, op->A, op->R, op->X, op->U, op->Linv, op->logdiag, op->gram,
+                    op->out, op->etas, op->rhs_src, op->scratch, op->scratch2, op->tracebuf};
+  for (double* p : bufs)
+    if (p) (void)hipFree(p);
+  if (op->info) (void)hipFree(op->info);
+  for (auto e : op->ev) (void)hipEventDestroy(e);
+  if (op->ev_begin) (void)hipEventDestroy(op->ev_begin);
+  if (op->ev_end) (void)hipEventDestroy(op->ev_end);
+  if (op->stream) (void)hipStreamDestroy(op->stream);
+  delete op;
+  return 0;
+}
+
+int gpmi_op_size(const gpmi_op* op, int64_t* n, int64_t* n_pad) {
+  if (!op) return set_err(-1006, "null handle");
+  if (n) *n = op->n;
+  if (n_pad) *n_pad = op->n_pad;
+  return 0;
+}
+
+int gpmi_op_load_matrix(gpmi_op* op, const double* K_host, int64_t ldk) {
+  if (!op) return set_err(-1006, "null handle");
+  DeviceGuard g(op->device);
+  const int64_t np = op->n_pad, n = op->n;
+  // identity pad, then the n x n block
+  std::vector<double> pad_rows;
+  HIP_TRY(hipMemsetAsync(op->K, 0, sizeof(double) * np * np, op->stream));
+  HIP_TRY(hipMemcpy2DAsync(op->K, sizeof(double) * np, K_host, sizeof(double) * ldk,
+                           sizeof(double) * n, n, hipMemcpyHostToDevice, op->stream));
+  if (np > n) {
+    std::vector<double> one(1, 1.0);
+    for (int64_t i = n; i < np; ++i)
+      HIP_TRY(hipMemcpyAsync(op->K + i * np + i, one.data(), sizeof(double),
+                             hipMemcpyHostToDevice, op->stream));
+  }
+  HIP_TRY(hipStreamSynchronize(op->stream));
+  op->has_K = true;
+  op->cache_valid = false;
+  return 0;
+}
+
+int gpmi_op_assemble_matern(gpmi_op* op, const double* points, int d, const double* scale,
+                            double nu) {
+  if (!op) return set_err(-1006, "null handle");
+  int rc = assemble(op->device, op->stream, points, op->n, d, scale, nu, op->K, op->n_pad,
+                    op->n_pad);
+  if (rc) return rc;
+  op->has_K = true;
+  op->cache_valid = false;
+  return 0;
+}
+
+int gpmi_op_get_matrix(gpmi_op* op, double* K_out, int64_t ldk) {
+  if (!op) return set_err(-1006, "null handle");
+  DeviceGuard g(op->device);
+  HIP_TRY(hipMemcpy2DAsync(K_out, sizeof(double) * ldk, op->K, sizeof(double) * op->n_pad,
+                           sizeof(double) * op->n, op->n, hipMemcpyDeviceToHost, op->stream));
+  HIP_TRY(hipStreamSynchronize(op->stream));
+  return 0;
+}
+
+int gpmi_op_set_rhs(gpmi_op* op, const double* rhs, int64_t ld, int nrhs) {
+  if (!op) return set_err(-1006, "null handle");
+  if (nrhs < 0 || nrhs > RLD) return set_err(-1007, "nrhs %d outside [0, %d]", nrhs, RLD);
+  DeviceGuard g(op->device);
+  int rc = upload_rhs(op, op->rhs_src, rhs, ld, nrhs, 0);
+  if (rc) return rc;
+  op->nrhs = nrhs;
+  return 0;
+}
+
+int gpmi_op_loglik_batch(gpmi_op* op, const double* etas, int neta, double* logdet,
+                         double* gram, int* info) {
+  if (!op) return set_err(-1006, "null handle");
+  DeviceGuard g(op->device);
+  int rc = run_factor(op, etas, neta, op->rhs_src);
+  if (rc) return rc;
+  std::vector<double> hout((size_t)neta * OUT_LD);
+  std::vector<int> hinfo(neta);
+  HIP_TRY(hipMemcpyAsync(hout.data(), op->out, sizeof(double) * hout.size(),
+                         hipMemcpyDeviceToHost, op->stream));
+  HIP_TRY(hipMemcpyAsync(hinfo.data(), op->info, sizeof(int) * neta, hipMemcpyDeviceToHost,
+                         op->stream));
+  HIP_TRY(hipStreamSynchronize(op->stream));
+  rc = collect_timing(op);
+  if (rc) return rc;
+  const int m = op->nrhs;
+  int status = 0;
+  for (int e = 0; e < neta; ++e) {
+    if (logdet) logdet[e] = hout[(size_t)e * OUT_LD];
+    if (gram)
+      for (int a = 0; a < m; ++a)
+        for (int c = 0; c < m; ++c)
+          gram[((size_t)e * m + a) * m + c] = hout[(size_t)e * OUT_LD + 1 + a * RLD + c];
+    if (info) info[e] = hinfo[e];
+    if (hinfo[e] && !status) status = hinfo[e];
+  }
+  op->cache_valid = (neta >= 1 && hinfo[0] == 0);
+  op->cached_eta = etas[0];
+  if (status) set_err(status, "matrix K + eta I is not positive definite (pivot %d)", status);
+  return 0;
+}
+
+int gpmi_op_logdet(gpmi_op* op, double eta, double* logdet) {
+  if (!op) return set_err(-1006, "null handle");
+  DeviceGuard g(op->device);
+  bool fresh;
+  int rc = ensure_factor(op, eta, op->rhs_src, &fresh);
+  if (rc) return rc;
+  double ld = 0.0;
+  int inf = 0;
+  HIP_TRY(hipMemcpyAsync(&ld, op->out, sizeof(double), hipMemcpyDeviceToHost, op->stream));
+  HIP_TRY(hipMemcpyAsync(&inf, op->info, sizeof(int), hipMemcpyDeviceToHost, op->stream));
+  HIP_TRY(hipStreamSynchronize(op->stream));
+  if (inf) {
+    op->cache_valid = false;
+    return set_err(inf, "matrix K + eta I is not positive definite (pivot %d)", inf);
+  }
+  *logdet = ld;
+  return 0;
+}
+
+int gpmi_op_solve(gpmi_op* op, double eta, const double* rhs, int64_t ld, int nrhs,
+                  double* sol, int64_t ldsol) {
+  if (!op) return set_err(-1006, "null handle");
+  DeviceGuard g(op->device);
+  const int nt = op->nt;
+  const int64_t lda = op->n_pad;
+  BatchPtrs P = op->ptrs();
+  std::vector<double> h((size_t)op->n_pad * RLD);
+  for (int c0 = 0; c0 < nrhs; c0 += RLD) {
+    const int nc = std::min(RLD, nrhs - c0);
+    int rc = upload_rhs(op, op->scratch, rhs, ld, nc, c0);
+    if (rc) return rc;
+    bool fresh;
+    rc = ensure_factor(op, eta, op->scratch, &fresh);
+    if (rc) return rc;
+    int inf = 0;
+    HIP_TRY(hipMemcpyAsync(&inf, op->info, sizeof(int), hipMemcpyDeviceToHost, op->stream));
+    HIP_TRY(hipStreamSynchronize(op->stream));
+    if (inf) {
+      op->cache_valid = false;
+      return set_err(inf, "matrix K + eta I is not positive definite (pivot %d)", inf);
+    }
+    if (!fresh) {
+      // cached factor: forward substitution of the new RHS block
+      HIP_TRY(hipMemcpyAsync(op->R, op->scratch, sizeof(double) * P.sR,
+                             hipMemcpyDeviceToDevice, op->stream));
+      for (int kb = 0; kb < nt; ++kb) {
+        hipLaunchKernelGGL(fwd_step_kernel, dim3(nt - kb, 1), dim3(256), 0, op->stream, P, lda,
+                           kb);
+        LAUNCH_CHECK("fwd_step_kernel");
+      }
+    }
+    for (int kb = nt - 1; kb >= 0; --kb) {
+      hipLaunchKernelGGL(bwd_step_kernel, dim3(std::max(kb, 1), 1), dim3(256), 0, op->stream, P,
+                         lda, kb, op->X, P.sR);
+      LAUNCH_CHECK("bwd_step_kernel");
+    }
+    HIP_TRY(hipMemcpyAsync(h.data(), op->X, sizeof(double) * h.size(), hipMemcpyDeviceToHost,
+                           op->stream));
+    HIP_TRY(hipStreamSynchronize(op->stream));
+    for (int64_t i = 0; i < op->n; ++i)
+      for (int c = 0; c < nc; ++c) sol[i * ldsol + c0 + c] = h[(size_t)i * RLD + c];
+  }
+  return 0;
+}
+
+int gpmi_op_matvec(gpmi_op* op, const double* x, int64_t ld, int ncol, double* y,
+                   int64_t ldy) {
+  if (!op) return set_err(-1006, "null handle");
+  if (!op->has_K) return set_err(-1000, "operator has no matrix");
+  DeviceGuard g(op->device);
+  std::vector<double> h((size_t)op->n_pad * RLD, 0.0);
+  for (int c0 = 0; c0 < ncol; c0 += RLD) {
+    const int nc = std::min(RLD, ncol - c0);
+    std::fill(h.begin(), h.end(), 0.0);
+    for (int64_t i = 0; i < op->n; ++i)
+      for (int c = 0; c < nc; ++c) h[(size_t)i * RLD + c] = x[i * ld + c0 + c];
+    HIP_TRY(hipMemcpyAsync(op->scratch, h.data(), sizeof(double) * h.size(),
+                           hipMemcpyHostToDevice, op->stream));
+    hipLaunchKernelGGL(gemv_sym_kernel, dim3((unsigned)((op->n + 3) / 4)), dim3(256), 0,
+                       op->stream, op->K, op->n_pad, op->n, op->scratch, (int64_t)RLD, nc,
+                       op->scratch2, 0.0, 1);
+    LAUNCH_CHECK("gemv_sym_kernel");
+    HIP_TRY(hipMemcpyAsync(h.data(), op->scratch2, sizeof(double) * h.size(),
+                           hipMemcpyDeviceToHost, op->stream));
+    HIP_TRY(hipStreamSynchronize(op->stream));
+    for (int64_t i = 0; i < op->n; ++i)
+      for (int c = 0; c < nc; ++c) y[i * ldy + c0 + c] = h[(size_t)i * RLD + c];
+  }
+  return 0;
+}
+
+int gpmi_op_trace(gpmi_op* op, double* trace_k, double* trace_k2) {
+  if (!op) return set_err(-1006, "null handle");
+  if (!op->has_K) return set_err(-1000, "operator has no matrix");
+  DeviceGuard g(op->device);
+  hipLaunchKernelGGL(trace_kernel, dim3((unsigned)op->n), dim3(256), 0, op->stream, op->K,
+                     op->n_pad, op->n, op->tracebuf);
+  LAUNCH_CHECK("trace_kernel");
+  std::vector<double> h((size_t)op->n * 2);
+  HIP_TRY(hipMemcpyAsync(h.data(), op->tracebuf, sizeof(double) * h.size(),
+                         hipMemcpyDeviceToHost, op->stream));
+  HIP_TRY(hipStreamSynchronize(op->stream));
+  double a = 0.0, f = 0.0;
+  for (int64_t i = 0; i < op->n; ++i) {
+    a += h[2 * i];
+    f += h[2 * i + 1];
+  }
+  if (trace_k) *trace_k = a;
+  if (trace_k2) *trace_k2 = f;
+  return 0;
+}
+
+int gpmi_op_set_timing(gpmi_op* op, int enable) {
+  if (!op) return set_err(-1006, "null handle");
+  op->timing = enable != 0;
+  return 0;
+}
+
+int gpmi_op_last_timing(gpmi_op* op, double* syrk_ms, int* syrk_launches, double* syrk_flops,
+                        double* total_ms) {
+  if (!op) return set_err(-1006, "null handle");
+  if (syrk_ms) *syrk_ms = op->last_syrk_ms;
+  if (syrk_launches) *syrk_launches = op->last_syrk_launches;
+  if (syrk_flops) *syrk_flops = op->last_syrk_flops;
+  if (total_ms) *total_ms = op->last_total_ms;
+  return 0;
+}
+
+int gpmi_op_set_outer(gpmi_op* op, int s) {
+  if (!op) return set_err(-1006, "null handle");
+  if (s < 1 || s > 8) return set_err(-1008, "outer panel width %d outside [1, 8]", s);
+  op->outer = s;
+  return 0;
+}
+
+}  // extern "C"

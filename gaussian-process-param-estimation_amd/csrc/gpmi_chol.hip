@@ -1,0 +1,530 @@
+// Batched blocked Cholesky of K + eta_b I on gfx950 fp64 MFMA, with the
+// forward substitution of a resident RHS block, logdet and Gram partials fused
+// into the factorization loop.
+//
+// Replaces, per eta, the reference's dense numerics behind the MixedCorrelation
+// duck type:
+//   MixedCorrelation.logdet   gaussian_proc/_mixed_correlation/mixed_correlation.py:221-274
+//   MixedCorrelation.solve    mixed_correlation.py:280-299 -> _linear_solver.py:71
+//                             (scipy.linalg.solve(assume_a='pos') = LAPACK ?posv)
+// which the reference runs 2-3 times per DirectLikelihood.log_likelihood
+// (_direct_likelihood.py:59,62,332); here one factorization serves all of them.
+//
+// Algorithm (lower, row-major A, 128-wide diagonal blocks, outer panels of
+// S sub-panels, see gpmi_api.hip): per sub-panel k
+//   diag_block_kernel : L_kk = chol(A_kk) in LDS, Linv_kk = L_kk^-1, logdet
+//                       partial, y_k = Linv_kk r_k, u_k = Linv_kk^T y_k, Gram y_k^T y_k
+//   panel_kernel      : L_ik = A_ik Linv_kk^T  and  r_i -= A_ik u_k  (= L_ik y_k)
+//   syrk_kernel       : A_ij -= sum_p L_ip L_jp^T over the lower-triangular tiles
+// All three are batched over the eta values (blockIdx.y / blockIdx.x = member).
+
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "gpmi_internal.h"
+
+namespace gpmi {
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+typedef double d2 __attribute__((ext_vector_type(2)));
+
+constexpr int TS = GPMI_TS;      // 128
+constexpr int BK = 16;           // k-depth of one LDS stage
+constexpr int LDSK = 18;         // padded row stride (doubles) of a staged [row][k] slab
+constexpr int STAGE = TS * LDSK; // doubles per staged operand buffer
+constexpr int RLD = GPMI_RHS_LD; // 16
+
+__device__ __forceinline__ d4 mfma64(double a, double b, d4 c) {
+  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+// 128 x 16 slab of rows base[row * ld + p .. p + 15]: each wave-instruction
+// reads 32 full 128-B row segments (16 B / lane).
+__device__ __forceinline__ void gload_slab(const double* __restrict__ base, int64_t ld,
+                                           int p, d2 (&r)[4]) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int idx = i * 256 + t;
+    const int row = idx >> 3, c2 = idx & 7;
+    r[i] = *reinterpret_cast<const d2*>(base + (int64_t)row * ld + p + 2 * c2);
+  }
+}
+
+__device__ __forceinline__ void sstore_slab(double* s, const d2 (&r)[4]) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int idx = i * 256 + t;
+    const int row = idx >> 3, c2 = idx & 7;
+    *reinterpret_cast<d2*>(s + row * LDSK + 2 * c2) = r[i];
+  }
+}
+
+// acc (wave tile 64 x 64 at (wr, wc)) += P1[0:128, 0:kdim] * P2[0:128, 0:kdim]^T.
+// f64 MFMA 16x16x4 operand maps: A[i = lane&15][k = lane>>4], B[k = lane>>4][j = lane&15].
+// WITH_RHS additionally accumulates racc (rows wr*64 + wc*32 + [0,32), 16 cols)
+// += P1 * U with U[kdim][16] staged in LDS.
+template <bool WITH_RHS>
+__device__ __forceinline__ void tile_mma(const double* __restrict__ P1, int64_t ld1,
+                                         const double* __restrict__ P2, int64_t ld2,
+                                         int kdim, double* sA, double* sB,
+                                         d4 (&acc)[4][4], const double* sU,
+                                         d4 (&racc)[2]) {
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int wr = w >> 1, wc = w & 1;
+  const int fr = lane & 15, fk = lane >> 4;
+  d2 ra[4], rb[4];
+  gload_slab(P1, ld1, 0, ra);
+  gload_slab(P2, ld2, 0, rb);
+  sstore_slab(sA, ra);
+  sstore_slab(sB, rb);
+  __syncthreads();
+  const int nsteps = kdim / BK;
+  for (int s = 0; s < nsteps; ++s) {
+    const int cur = s & 1;
+    const double* cA = sA + cur * STAGE;
+    const double* cB = sB + cur * STAGE;
+    if (s + 1 < nsteps) {
+      gload_slab(P1, ld1, (s + 1) * BK, ra);
+      gload_slab(P2, ld2, (s + 1) * BK, rb);
+    }
+#pragma unroll
+    for (int kk = 0; kk < BK / 4; ++kk) {
+      double a[4], b[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = cA[(wr * 64 + i * 16 + fr) * LDSK + kk * 4 + fk];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = cB[(wc * 64 + j * 16 + fr) * LDSK + kk * 4 + fk];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma64(a[i], b[j], acc[i][j]);
+      if (WITH_RHS) {
+        const double u = sU[(s * BK + kk * 4 + fk) * RLD + fr];
+        const double a0 = wc ? a[2] : a[0];
+        const double a1 = wc ? a[3] : a[1];
+        racc[0] = mfma64(a0, u, racc[0]);
+        racc[1] = mfma64(a1, u, racc[1]);
+      }
+    }
+    if (s + 1 < nsteps) {
+      sstore_slab(sA + (cur ^ 1) * STAGE, ra);
+      sstore_slab(sB + (cur ^ 1) * STAGE, rb);
+    }
+    __syncthreads();
+  }
+}
+
+// Bijective XCD-aware remap (consecutive logical tiles -> one XCD's L2).
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
+// Lower-triangular tile enumeration of a band of w tile columns over t tile
+// rows (row-major): rows i < w hold a triangle, rows i >= w hold w tiles.
+__device__ __forceinline__ void tri_decode(int q, int w, int* pi, int* pj) {
+  const int tri = w * (w + 1) / 2;
+  int i, j;
+  if (q < tri) {
+    i = (int)((sqrt(8.0 * (double)q + 1.0) - 1.0) * 0.5);
+    while ((i + 1) * (i + 2) / 2 <= q) ++i;
+    while (i * (i + 1) / 2 > q) --i;
+    j = q - i * (i + 1) / 2;
+  } else {
+    const int r = q - tri;
+    i = w + r / w;
+    j = r % w;
+  }
+  *pi = i;
+  *pj = j;
+}
+
+// ---------------------------------------------------------------------------
+// A_b = K + eta_b * I on the lower-triangular 128-tiles (diagonal tiles whole).
+// K is read once per launch and written to every batch member. The shift is
+// applied only to the first n diagonal entries; pads stay identity.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void shift_copy_kernel(
+    const double* __restrict__ K, int64_t ldk, double* __restrict__ A, int64_t lda,
+    int64_t sA, const double* __restrict__ etas, int nb, int64_t n, int nt) {
+  int I, J;
+  tri_decode(blockIdx.x, nt, &I, &J);
+  const int t = threadIdx.x;
+  for (int e = t; e < TS * TS / 2; e += 256) {
+    const int r = e >> 6, c = (e & 63) * 2;
+    const int64_t gi = (int64_t)I * TS + r, gj = (int64_t)J * TS + c;
+    const d2 v = *reinterpret_cast<const d2*>(K + gi * ldk + gj);
+    for (int b = 0; b < nb; ++b) {
+      d2 o = v;
+      if (gi < n) {
+        if (gi == gj) o[0] += etas[b];
+        if (gi == gj + 1) o[1] += etas[b];
+      }
+      *reinterpret_cast<d2*>(A + b * sA + gi * lda + gj) = o;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Diagonal block k (one workgroup per batch member): in-LDS Cholesky,
+// triangular inverse, logdet partial and the RHS forward step.
+// ---------------------------------------------------------------------------
+constexpr int DLD = TS + 1;   // LDS row stride of the 128x128 block (bank-conflict-free columns)
+
+__global__ __launch_bounds__(256) void diag_block_kernel(BatchPtrs P, int64_t lda, int kb,
+                                                         int nt) {
+  __shared__ double Ls[TS * DLD];
+  __shared__ double Ys[TS * RLD];
+  __shared__ double tmp[TS];
+  __shared__ int s_fail;
+  const int t = threadIdx.x;
+  const int b = blockIdx.x;
+  const int64_t k0 = (int64_t)kb * TS;
+  double* A = P.A + b * P.sA;
+  double* R = P.R + b * P.sR;
+  if (t == 0) s_fail = 0;
+  for (int e = t; e < TS * TS; e += 256) {
+    const int r = e >> 7, c = e & 127;
+    Ls[r * DLD + c] = (c <= r) ? A[(k0 + r) * lda + k0 + c] : 0.0;
+  }
+  for (int e = t; e < TS * RLD; e += 256) Ys[e] = R[k0 * RLD + e];
+  __syncthreads();
+
+  // --- right-looking Cholesky, one column per step ---
+  double logsum = 0.0;
+  const int row = t & 127, half = t >> 7;
+  for (int j = 0; j < TS; ++j) {
+    const double djj = Ls[j * DLD + j];
+    const double ljj = sqrt(djj);
+    if (t == 0) {
+      if (!(djj > 0.0) && s_fail == 0) s_fail = j + 1;
+      logsum += log(ljj);
+    }
+    __syncthreads();
+    if (t < TS) {
+      if (t > j) Ls[t * DLD + j] = Ls[t * DLD + j] / ljj;
+      else if (t == j) Ls[t * DLD + j] = ljj;
+    }
+    __syncthreads();
+    if (row > j) {
+      const double lrj = Ls[row * DLD + j];
+      for (int c = j + 1 + half; c <= row; c += 2)
+        Ls[row * DLD + c] -= lrj * Ls[c * DLD + j];
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    P.logdiag[b * P.sLD + kb] = 2.0 * logsum;
+    if (s_fail && P.info[b] == 0) P.info[b] = (int)k0 + s_fail;
+  }
+  for (int e = t; e < TS * TS; e += 256) {
+    const int r = e >> 7, c = e & 127;
+    if (c <= r) A[(k0 + r) * lda + k0 + c] = Ls[r * DLD + c];
+  }
+  __syncthreads();
+
+  // --- in-place inverse of the lower-triangular block (column sweep, j descending) ---
+  for (int j = TS - 1; j >= 0; --j) {
+    if (t < TS && t > j) tmp[t] = Ls[t * DLD + j];
+    if (t == 0) Ls[j * DLD + j] = 1.0 / Ls[j * DLD + j];
+    __syncthreads();
+    if (t < TS && t > j) {
+      const double ajj = -Ls[j * DLD + j];
+      double s = 0.0;
+      for (int p = j + 1; p <= t; ++p) s += Ls[t * DLD + p] * tmp[p];
+      Ls[t * DLD + j] = ajj * s;
+    }
+    __syncthreads();
+  }
+  double* Li = P.Linv + b * P.sL + (int64_t)kb * TS * TS;
+  for (int e = t; e < TS * TS; e += 256) {
+    const int r = e >> 7, c = e & 127;
+    Li[e] = (c <= r) ? Ls[r * DLD + c] : 0.0;
+  }
+
+  // --- y = Linv r_k ; u = Linv^T y ; Gram = y^T y ---
+  double yv[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) yv[q] = 0.0;
+  for (int p = 0; p <= row; ++p) {
+    const double l = Ls[row * DLD + p];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) yv[q] += l * Ys[p * RLD + half * 8 + q];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    Ys[row * RLD + half * 8 + q] = yv[q];
+    R[(k0 + row) * RLD + half * 8 + q] = yv[q];
+  }
+  __syncthreads();
+  {
+    const int c = row;
+    double uv[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) uv[q] = 0.0;
+    for (int r = c; r < TS; ++r) {
+      const double l = Ls[r * DLD + c];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) uv[q] += l * Ys[r * RLD + half * 8 + q];
+    }
+    double* U = P.U + b * P.sU;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) U[c * RLD + half * 8 + q] = uv[q];
+  }
+  {
+    const int a = t >> 4, q = t & 15;
+    double g = 0.0;
+    for (int r = 0; r < TS; ++r) g += Ys[r * RLD + a] * Ys[r * RLD + q];
+    P.gram[b * P.sG + (int64_t)kb * 256 + t] = g;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Panel: for row tile I = kb + 1 + blockIdx.x of member b = blockIdx.y:
+//   L_Ik = A_Ik Linv_kk^T (in place)  and  r_I -= A_Ik u_k.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void panel_kernel(BatchPtrs P, int64_t lda, int kb) {
+  __shared__ double smem[4 * STAGE + TS * RLD];
+  double* sA = smem;
+  double* sB = smem + 2 * STAGE;
+  double* sU = smem + 4 * STAGE;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int wr = w >> 1, wc = w & 1, fr = lane & 15, fk = lane >> 4;
+  const int b = blockIdx.y;
+  const int I = kb + 1 + blockIdx.x;
+  double* A = P.A + b * P.sA;
+  const double* U = P.U + b * P.sU;
+  for (int e = t; e < TS * RLD; e += 256) sU[e] = U[e];
+  double* Aik = A + (int64_t)I * TS * lda + (int64_t)kb * TS;
+  const double* Li = P.Linv + b * P.sL + (int64_t)kb * TS * TS;
+  d4 acc[4][4];
+  d4 racc[2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = d4{0.0, 0.0, 0.0, 0.0};
+  racc[0] = racc[1] = d4{0.0, 0.0, 0.0, 0.0};
+  tile_mma<true>(Aik, lda, Li, TS, TS, sA, sB, acc, sU, racc);
+  // C/D map of v_mfma_f64_16x16x4f64: row = (lane>>4) + 4*r, col = lane&15.
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        Aik[(int64_t)(wr * 64 + i * 16 + fk + 4 * r) * lda + wc * 64 + j * 16 + fr] =
+            acc[i][j][r];
+  double* R = P.R + b * P.sR + (int64_t)I * TS * RLD;
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      R[(wr * 64 + wc * 32 + h * 16 + fk + 4 * r) * RLD + fr] -= racc[h][r];
+}
+
+// ---------------------------------------------------------------------------
+// Trailing update on a band of tile columns [tc0, tc0 + w) over tile rows
+// [tc0, tc0 + t): A_IJ -= sum_{p in [p0, p0+kdim)} A_Ip A_Jp^T, J <= I.
+// blockIdx.y = batch member.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256, 2) void syrk_kernel(double* A, int64_t lda, int64_t sA,
+                                                      int tc0, int w, int t, int p0,
+                                                      int kdim) {
+  __shared__ double smem[4 * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wr = wv >> 1, wc = wv & 1, fr = lane & 15, fk = lane >> 4;
+  const int q = xcd_remap(blockIdx.x, gridDim.x);
+  int i, j;
+  tri_decode(q, w, &i, &j);
+  (void)t;
+  const int I = tc0 + i, J = tc0 + j;
+  double* Ab = A + blockIdx.y * sA;
+  const double* P1 = Ab + (int64_t)I * TS * lda + p0;
+  const double* P2 = Ab + (int64_t)J * TS * lda + p0;
+  d4 acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[a][c] = d4{0.0, 0.0, 0.0, 0.0};
+  d4 dummy[2];
+  tile_mma<false>(P1, lda, P2, lda, kdim, smem, smem + 2 * STAGE, acc, nullptr, dummy);
+  double* C = Ab + (int64_t)I * TS * lda + (int64_t)J * TS;
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        C[(int64_t)(wr * 64 + a * 16 + fk + 4 * r) * lda + wc * 64 + c * 16 + fr] -=
+            acc[a][c][r];
+}
+
+// out[b][0] = logdet = sum of block partials; out[b][1 + e] = Gram entry e (16x16).
+__global__ __launch_bounds__(256) void finalize_kernel(BatchPtrs P, int nt, double* out,
+                                                       int out_ld) {
+  const int b = blockIdx.x, t = threadIdx.x;
+  double g = 0.0;
+  for (int k = 0; k < nt; ++k) g += P.gram[b * P.sG + (int64_t)k * 256 + t];
+  out[b * out_ld + 1 + t] = g;
+  if (t == 0) {
+    double s = 0.0;
+    for (int k = 0; k < nt; ++k) s += P.logdiag[b * P.sLD + k];
+    out[b * out_ld] = s;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Backward substitution L^T X = Y (Y = forward-substituted R), step kb
+// (descending). Every workgroup recomputes x_kb = Linv_kb^T y_kb in LDS;
+// workgroup j < kb then applies y_j -= L_{kb,j}^T x_kb; workgroup 0 stores x_kb.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void bwd_step_kernel(BatchPtrs P, int64_t lda, int kb,
+                                                       double* X, int64_t sX) {
+  __shared__ double Ys[TS * RLD];
+  __shared__ double Xs[TS * RLD];
+  const int t = threadIdx.x, b = blockIdx.y, jblk = blockIdx.x;
+  const int row = t & 127, half = t >> 7;
+  double* R = P.R + b * P.sR;
+  const double* A = P.A + b * P.sA;
+  const double* Li = P.Linv + b * P.sL + (int64_t)kb * TS * TS;
+  for (int e = t; e < TS * RLD; e += 256) Ys[e] = R[(int64_t)kb * TS * RLD + e];
+  __syncthreads();
+  {
+    double xv[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) xv[q] = 0.0;
+    for (int r = row; r < TS; ++r) {
+      const double l = Li[r * TS + row];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) xv[q] += l * Ys[r * RLD + half * 8 + q];
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) Xs[row * RLD + half * 8 + q] = xv[q];
+  }
+  __syncthreads();
+  if (jblk == 0) {
+    double* Xb = X + b * sX + (int64_t)kb * TS * RLD;
+    for (int e = t; e < TS * RLD; e += 256) Xb[e] = Xs[e];
+  }
+  if (kb == 0) return;
+  // y_j[c][q] -= sum_r L_{kb,j}[r][c] x[r][q]
+  const double* Lkj = A + (int64_t)kb * TS * lda + (int64_t)jblk * TS;
+  const int c = row;
+  double yv[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) yv[q] = 0.0;
+  for (int r = 0; r < TS; ++r) {
+    const double l = Lkj[(int64_t)r * lda + c];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) yv[q] += l * Xs[r * RLD + half * 8 + q];
+  }
+  double* Yj = R + (int64_t)jblk * TS * RLD;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) Yj[c * RLD + half * 8 + q] -= yv[q];
+}
+
+// y[:, c] = K x[:, c]  (one wave per row, lanes stride the columns of K).
+__global__ __launch_bounds__(256) void gemv_sym_kernel(const double* __restrict__ K,
+                                                       int64_t ldk, int64_t n,
+                                                       const double* __restrict__ x,
+                                                       int64_t ldx, int ncol,
+                                                       double* __restrict__ y, double eta,
+                                                       int exponent) {
+  (void)eta;
+  (void)exponent;
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= n) return;
+  for (int c = 0; c < ncol; ++c) {
+    double s = 0.0;
+    for (int64_t j = lane; j < n; j += 64) s += K[row * ldk + j] * x[j * ldx + c];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+    if (lane == 0) y[row * ldx + c] = s;
+  }
+}
+
+// Per-block partial sums of trace(K) and ||K||_F^2 (host adds the partials).
+__global__ __launch_bounds__(256) void trace_kernel(const double* __restrict__ K, int64_t ldk,
+                                                    int64_t n, double* __restrict__ out) {
+  __shared__ double s0[256], s1[256];
+  const int t = threadIdx.x;
+  const int64_t row = blockIdx.x;
+  double a = 0.0, f = 0.0;
+  if (row < n) {
+    if (t == 0) a = K[row * ldk + row];
+    for (int64_t j = t; j < n; j += 256) {
+      const double v = K[row * ldk + j];
+      f += v * v;
+    }
+  }
+  s0[t] = a;
+  s1[t] = f;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if (t < off) {
+      s0[t] += s0[t + off];
+      s1[t] += s1[t + off];
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    out[2 * row] = s0[0];
+    out[2 * row + 1] = s1[0];
+  }
+}
+
+}  // namespace gpmi
+
+namespace gpmi {
+
+// Forward substitution step kb with a cached factor (L y = r, descending blocks
+// already done): every workgroup recomputes y_kb = Linv_kb r_kb in LDS;
+// workgroup 0 stores it, workgroup i > 0 applies r_{kb+i} -= L_{kb+i,kb} y_kb.
+__global__ __launch_bounds__(256) void fwd_step_kernel(BatchPtrs P, int64_t lda, int kb) {
+  __shared__ double Rs[TS * RLD];
+  __shared__ double Ys[TS * RLD];
+  const int t = threadIdx.x, b = blockIdx.y, iblk = blockIdx.x;
+  const int row = t & 127, half = t >> 7;
+  double* R = P.R + b * P.sR;
+  const double* A = P.A + b * P.sA;
+  const double* Li = P.Linv + b * P.sL + (int64_t)kb * TS * TS;
+  for (int e = t; e < TS * RLD; e += 256) Rs[e] = R[(int64_t)kb * TS * RLD + e];
+  __syncthreads();
+  {
+    double yv[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) yv[q] = 0.0;
+    for (int p = 0; p <= row; ++p) {
+      const double l = Li[row * TS + p];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) yv[q] += l * Rs[p * RLD + half * 8 + q];
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) Ys[row * RLD + half * 8 + q] = yv[q];
+  }
+  __syncthreads();
+  if (iblk == 0) {
+    for (int e = t; e < TS * RLD; e += 256) R[(int64_t)kb * TS * RLD + e] = Ys[e];
+    return;
+  }
+  const int I = kb + iblk;
+  const double* Lik = A + (int64_t)I * TS * lda + (int64_t)kb * TS;
+  double yv[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) yv[q] = 0.0;
+  for (int c = 0; c < TS; ++c) {
+    const double l = Lik[(int64_t)row * lda + c];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) yv[q] += l * Ys[c * RLD + half * 8 + q];
+  }
+  double* Ri = R + (int64_t)I * TS * RLD;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) Ri[row * RLD + half * 8 + q] -= yv[q];
+}
+
+}  // namespace gpmi

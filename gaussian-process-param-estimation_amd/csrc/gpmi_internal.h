@@ -1,0 +1,54 @@
+// Internal declarations shared by the gpmi HIP translation units.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define GPMI_MAX_DIM 8     // max point dimension handled by the assembly kernel
+#define GPMI_TS 128        // tile / diagonal-block size of the blocked Cholesky
+#define GPMI_RHS_LD 16     // leading dimension (max columns) of a resident RHS block
+
+namespace gpmi {
+
+enum MaternMode { MATERN_HALF = 0, MATERN_3HALF = 1, MATERN_5HALF = 2,
+                  MATERN_GENERAL = 3, MATERN_GAUSS = 4 };
+
+struct MaternParams {
+  int mode;
+  double nu;
+  double sqrt2nu;     // sqrt(2 nu)
+  double prefactor;   // 2^(1-nu) / Gamma(nu)
+};
+
+__global__ void matern_dense_kernel(const double* points, int64_t n, int d,
+                                    const double* scale_dev, MaternParams P,
+                                    double* K, int64_t ldk, int64_t n_pad);
+
+// Batched factorization kernels (gpmi_chol.hip). All matrices are row-major
+// n_pad x n_pad with leading dimension lda; batch member b lives at base + b*stride.
+struct BatchPtrs {
+  double* A;        int64_t sA;       // working matrices K + eta_b I -> L
+  double* R;        int64_t sR;       // RHS blocks [n_pad][16] -> L^-1 R
+  double* U;        int64_t sU;       // per-step u_k = A_kk^-1 r_k  [128][16]
+  double* Linv;     int64_t sL;       // inverses of the diagonal blocks [nt][128][128]
+  double* logdiag;  int64_t sLD;      // per diagonal block: 2 sum log L_ii  [nt]
+  double* gram;     int64_t sG;       // per diagonal block Gram partials [nt][16][16]
+  int* info;                          // first non-positive pivot (1-based), per member
+};
+
+__global__ void shift_copy_kernel(const double* K, int64_t ldk, double* A, int64_t lda,
+                                  int64_t sA, const double* etas, int nb, int64_t n,
+                                  int nt);
+__global__ void diag_block_kernel(BatchPtrs P, int64_t lda, int kb, int nt);
+__global__ void panel_kernel(BatchPtrs P, int64_t lda, int kb);
+__global__ void syrk_kernel(double* A, int64_t lda, int64_t sA, int tc0, int w, int t,
+                            int p0, int kdim);
+__global__ void finalize_kernel(BatchPtrs P, int nt, double* out, int out_ld);
+__global__ void bwd_step_kernel(BatchPtrs P, int64_t lda, int kb, double* X, int64_t sX);
+__global__ void fwd_step_kernel(BatchPtrs P, int64_t lda, int kb);
+__global__ void gemv_sym_kernel(const double* K, int64_t ldk, int64_t n,
+                                const double* x, int64_t ldx, int ncol, double* y,
+                                double eta, int exponent);
+__global__ void trace_kernel(const double* K, int64_t ldk, int64_t n, double* out);
+
+}  // namespace gpmi

@@ -1,0 +1,245 @@
+"""ctypes binding of libgpmi.so (the C ABI declared in include/gpmi.h).
+
+There is no CPU fallback: if the library (built for gfx950 by
+``__graft_entry__.build()``) is missing, or no HIP device is visible when a
+device call is made, the call raises. The CPU restatement lives in
+``oracle/`` and is test infrastructure only.
+"""
+
+import ctypes
+import os
+
+import numpy
+
+_LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), '_lib')
+LIB_PATH = os.path.join(_LIB_DIR, 'libgpmi.so')
+MAX_RHS = 16
+
+_lib = None
+
+c_double_p = ctypes.POINTER(ctypes.c_double)
+c_int_p = ctypes.POINTER(ctypes.c_int)
+c_i64 = ctypes.c_int64
+c_op_p = ctypes.c_void_p
+
+# name -> (restype, argtypes); mirrors include/gpmi.h
+SIGNATURES = {
+    'gpmi_version': (ctypes.c_int, []),
+    'gpmi_last_error': (ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t]),
+    'gpmi_device_count': (ctypes.c_int, [c_int_p]),
+    'gpmi_matern_dense': (ctypes.c_int, [ctypes.c_int, c_double_p, c_i64, ctypes.c_int,
+                                         c_double_p, ctypes.c_double, c_double_p, c_i64]),
+    'gpmi_op_create': (ctypes.c_int, [ctypes.c_int, c_i64, ctypes.c_int,
+                                      ctypes.POINTER(c_op_p)]),
+    'gpmi_op_destroy': (ctypes.c_int, [c_op_p]),
+    'gpmi_op_size': (ctypes.c_int, [c_op_p, ctypes.POINTER(c_i64), ctypes.POINTER(c_i64)]),
+    'gpmi_op_load_matrix': (ctypes.c_int, [c_op_p, c_double_p, c_i64]),
+    'gpmi_op_assemble_matern': (ctypes.c_int, [c_op_p, c_double_p, ctypes.c_int, c_double_p,
+                                               ctypes.c_double]),
+    'gpmi_op_get_matrix': (ctypes.c_int, [c_op_p, c_double_p, c_i64]),
+    'gpmi_op_set_rhs': (ctypes.c_int, [c_op_p, c_double_p, c_i64, ctypes.c_int]),
+    'gpmi_op_loglik_batch': (ctypes.c_int, [c_op_p, c_double_p, ctypes.c_int, c_double_p,
+                                            c_double_p, c_int_p]),
+    'gpmi_op_logdet': (ctypes.c_int, [c_op_p, ctypes.c_double, c_double_p]),
+    'gpmi_op_solve': (ctypes.c_int, [c_op_p, ctypes.c_double, c_double_p, c_i64, ctypes.c_int,
+                                     c_double_p, c_i64]),
+    'gpmi_op_matvec': (ctypes.c_int, [c_op_p, c_double_p, c_i64, ctypes.c_int, c_double_p,
+                                      c_i64]),
+    'gpmi_op_trace': (ctypes.c_int, [c_op_p, c_double_p, c_double_p]),
+    'gpmi_op_set_timing': (ctypes.c_int, [c_op_p, ctypes.c_int]),
+    'gpmi_op_last_timing': (ctypes.c_int, [c_op_p, c_double_p, c_int_p, c_double_p,
+                                           c_double_p]),
+    'gpmi_op_set_outer': (ctypes.c_int, [c_op_p, ctypes.c_int]),
+}
+
+
+class GPMIError(RuntimeError):
+    """Error reported by libgpmi (HIP error or invalid argument)."""
+
+
+def load():
+    """Load libgpmi.so (once). Raises if it has not been built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.isfile(LIB_PATH):
+        raise ImportError(
+            'libgpmi.so not found at %s: build the HIP library first '
+            '(python -c "import __graft_entry__ as g; g.build()")' % LIB_PATH)
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def last_error():
+    buf = ctypes.create_string_buffer(512)
+    load().gpmi_last_error(buf, 512)
+    return buf.value.decode(errors='replace')
+
+
+def check(rc, what):
+    """Map a C status to Python: <0 -> GPMIError; >0 -> LinAlgError (not SPD)."""
+    if rc == 0:
+        return
+    if rc > 0:
+        raise numpy.linalg.LinAlgError(
+            '%s: matrix K + eta I is not positive definite (pivot %d)' % (what, rc))
+    raise GPMIError('%s failed (%d): %s' % (what, rc, last_error()))
+
+
+def device_count():
+    n = ctypes.c_int(0)
+    check(load().gpmi_device_count(ctypes.byref(n)), 'gpmi_device_count')
+    return n.value
+
+
+def require_device(device):
+    cnt = device_count()
+    if cnt < 1:
+        raise GPMIError('no HIP device visible: gaussian_proc runs only on MI355X (gfx950)')
+    if not 0 <= device < cnt:
+        raise GPMIError('device %d outside [0, %d)' % (device, cnt))
+
+
+def default_device():
+    return int(os.environ.get('LOCAL_RANK', '0'))
+
+
+def dptr(a):
+    return a.ctypes.data_as(c_double_p)
+
+
+def as_c(a):
+    return numpy.ascontiguousarray(a, dtype=numpy.float64)
+
+
+class Operator(object):
+    """Owning wrapper of a ``gpmi_op`` handle (device-resident K + workspace)."""
+
+    def __init__(self, n, device=None, max_batch=1):
+        self.lib = load()
+        self.device = default_device() if device is None else int(device)
+        require_device(self.device)
+        self.n = int(n)
+        self.max_batch = int(max_batch)
+        h = c_op_p()
+        check(self.lib.gpmi_op_create(self.device, self.n, self.max_batch, ctypes.byref(h)),
+              'gpmi_op_create')
+        self.h = h
+        npad = c_i64()
+        check(self.lib.gpmi_op_size(self.h, None, ctypes.byref(npad)), 'gpmi_op_size')
+        self.n_pad = npad.value
+        self.nrhs = 0
+
+    def close(self):
+        if getattr(self, 'h', None) is not None and self.h.value:
+            self.lib.gpmi_op_destroy(self.h)
+            self.h = c_op_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def load_matrix(self, K):
+        K = as_c(K)
+        if K.shape != (self.n, self.n):
+            raise ValueError('K must be %d x %d' % (self.n, self.n))
+        check(self.lib.gpmi_op_load_matrix(self.h, dptr(K), self.n), 'gpmi_op_load_matrix')
+
+    def assemble_matern(self, points, scale, nu):
+        points = as_c(points)
+        scale = as_c(scale)
+        check(self.lib.gpmi_op_assemble_matern(self.h, dptr(points), points.shape[1],
+                                               dptr(scale), float(nu)),
+              'gpmi_op_assemble_matern')
+
+    def get_matrix(self):
+        K = numpy.empty((self.n, self.n))
+        check(self.lib.gpmi_op_get_matrix(self.h, dptr(K), self.n), 'gpmi_op_get_matrix')
+        return K
+
+    def set_rhs(self, R):
+        R = as_c(R)
+        if R.ndim == 1:
+            R = R[:, None]
+        if R.shape[0] != self.n or R.shape[1] > MAX_RHS:
+            raise ValueError('RHS must be %d x k with k <= %d' % (self.n, MAX_RHS))
+        check(self.lib.gpmi_op_set_rhs(self.h, dptr(R), R.shape[1], R.shape[1]),
+              'gpmi_op_set_rhs')
+        self.nrhs = R.shape[1]
+
+    def loglik_batch(self, etas):
+        """-> (logdet[neta], gram[neta, nrhs, nrhs], info[neta])"""
+        etas = as_c(numpy.atleast_1d(etas))
+        ne = etas.shape[0]
+        ld = numpy.empty(ne)
+        g = numpy.empty((ne, self.nrhs, self.nrhs))
+        info = numpy.zeros(ne, dtype=numpy.int32)
+        check(self.lib.gpmi_op_loglik_batch(self.h, dptr(etas), ne, dptr(ld), dptr(g),
+                                            info.ctypes.data_as(c_int_p)),
+              'gpmi_op_loglik_batch')
+        return ld, g, info
+
+    def logdet(self, eta):
+        out = ctypes.c_double()
+        check(self.lib.gpmi_op_logdet(self.h, float(eta), ctypes.byref(out)), 'gpmi_op_logdet')
+        return out.value
+
+    def solve(self, eta, Y):
+        Y = as_c(Y)
+        Y2 = Y[:, None] if Y.ndim == 1 else Y
+        sol = numpy.empty_like(Y2)
+        check(self.lib.gpmi_op_solve(self.h, float(eta), dptr(Y2), Y2.shape[1], Y2.shape[1],
+                                     dptr(sol), sol.shape[1]), 'gpmi_op_solve')
+        return sol[:, 0] if Y.ndim == 1 else sol
+
+    def matvec(self, x):
+        x = as_c(x)
+        x2 = x[:, None] if x.ndim == 1 else x
+        y = numpy.empty_like(x2)
+        check(self.lib.gpmi_op_matvec(self.h, dptr(x2), x2.shape[1], x2.shape[1], dptr(y),
+                                      y.shape[1]), 'gpmi_op_matvec')
+        return y[:, 0] if x.ndim == 1 else y
+
+    def trace(self):
+        a = ctypes.c_double()
+        b = ctypes.c_double()
+        check(self.lib.gpmi_op_trace(self.h, ctypes.byref(a), ctypes.byref(b)), 'gpmi_op_trace')
+        return a.value, b.value
+
+    def set_timing(self, on):
+        check(self.lib.gpmi_op_set_timing(self.h, int(bool(on))), 'gpmi_op_set_timing')
+
+    def last_timing(self):
+        ms = ctypes.c_double()
+        nl = ctypes.c_int()
+        fl = ctypes.c_double()
+        tot = ctypes.c_double()
+        check(self.lib.gpmi_op_last_timing(self.h, ctypes.byref(ms), ctypes.byref(nl),
+                                           ctypes.byref(fl), ctypes.byref(tot)),
+              'gpmi_op_last_timing')
+        return dict(syrk_ms=ms.value, syrk_launches=nl.value, syrk_flops=fl.value,
+                    total_ms=tot.value)
+
+    def set_outer(self, s):
+        check(self.lib.gpmi_op_set_outer(self.h, int(s)), 'gpmi_op_set_outer')
+
+
+def matern_dense(points, scale, nu, device=None):
+    """Dense Matérn K on the device, returned as a host ndarray."""
+    lib = load()
+    device = default_device() if device is None else int(device)
+    require_device(device)
+    points = as_c(points)
+    scale = as_c(scale)
+    n, d = points.shape
+    K = numpy.empty((n, n))
+    check(lib.gpmi_matern_dense(device, dptr(points), n, d, dptr(scale), float(nu), dptr(K),
+                                n), 'gpmi_matern_dense')
+    return K

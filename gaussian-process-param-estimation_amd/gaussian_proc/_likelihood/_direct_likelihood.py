@@ -1,0 +1,197 @@
+"""Restricted GP log-likelihood in the direct parameters (sigma, sigma0).
+
+Drop-in for ``DirectLikelihood`` of the reference
+(gaussian_proc/_likelihood/_direct_likelihood.py:25-405).
+
+Hot path. The reference evaluates one ``log_likelihood`` with
+``K_mixed.logdet(eta)`` and two dense solves (:59, :62, :332), i.e. 2-3 dense
+factorizations. Here, when ``K_mixed`` is the device operator, one Cholesky
+K + eta I = L L^T gives everything: with R = [X | z] and
+G = R^T (K + eta I)^-1 R = (L^-1 R)^T (L^-1 R),
+
+  logdet_S = n log sigma^2 + logdet(K + eta I)              (:60)
+  B        = X^T S^-1 X = G_XX / sigma^2                     (:65, :69)
+  z^T M z  = (G_zz - G_Xz^T G_XX^-1 G_Xz) / sigma^2          (:71-72, :335-338)
+  lp       = -(n-m)/2 log 2pi - logdet_S/2 - log det B / 2 - z^T M z / 2   (:75-76)
+
+The sigma ~ 0 branch (|sigma| < 1e-8, :49-55) never touches K and is evaluated
+as in the reference. The Jacobian / Hessian keep the reference formulas
+(derivatives w.r.t. sigma^2 and sigma0^2 — reference quirk) on top
+of the operator duck type.
+"""
+
+import numpy
+import scipy.optimize
+from functools import partial
+
+__all__ = ['DirectLikelihood']
+
+_TOL = 1e-8          # _direct_likelihood.py:49,106,324
+_TOL_HESS = 1e-16    # _direct_likelihood.py:179
+
+
+def _lp_from_terms(n, m, sigma, logdet_kn, G):
+    """log-likelihood from logdet(K + eta I) and G = R^T (K + eta I)^-1 R."""
+    s2 = sigma ** 2
+    Gxx = G[:m, :m]
+    gxz = G[:m, m]
+    gzz = G[m, m]
+    logdet_S = n * numpy.log(s2) + logdet_kn
+    B = Gxx / s2
+    logdet_B = numpy.log(numpy.linalg.det(B))
+    zMz = (gzz - gxz @ numpy.linalg.solve(Gxx, gxz)) / s2
+    return -0.5 * (n - m) * numpy.log(2.0 * numpy.pi) - 0.5 * logdet_S \
+        - 0.5 * logdet_B - 0.5 * zMz
+
+
+def _lp_small_sigma(z, X, sigma0):
+    """|sigma| < tol branch (_direct_likelihood.py:50-55, M_dot :325-328)."""
+    n, m = X.shape
+    s02 = sigma0 ** 2
+    logdet_S = n * numpy.log(s02)
+    Y = X / s02
+    B = X.T @ Y
+    logdet_B = numpy.log(numpy.linalg.det(B))
+    Binv = numpy.linalg.inv(B)
+    Mz = z / s02 - Y @ (Binv @ (Y.T @ z))
+    return -0.5 * (n - m) * numpy.log(2.0 * numpy.pi) - 0.5 * logdet_S \
+        - 0.5 * logdet_B - 0.5 * numpy.dot(z, Mz)
+
+
+class DirectLikelihood(object):
+
+    @staticmethod
+    def log_likelihood(z, X, K_mixed, sign_switch, hyperparam):
+        sigma, sigma0 = hyperparam[0], hyperparam[1]
+        n, m = X.shape
+        if numpy.abs(sigma) < _TOL:
+            lp = _lp_small_sigma(z, X, sigma0)
+        elif hasattr(K_mixed, 'loglik_terms'):
+            eta = (sigma0 / sigma) ** 2
+            ld, G = K_mixed.loglik_terms([eta], X, z)
+            lp = _lp_from_terms(n, m, sigma, ld[0], G[0])
+        else:
+            # generic operator duck type (reference call pattern)
+            eta = (sigma0 / sigma) ** 2
+            logdet_S = n * numpy.log(sigma ** 2) + K_mixed.logdet(eta)
+            Y = K_mixed.solve(eta, X) / sigma ** 2
+            B = X.T @ Y
+            logdet_B = numpy.log(numpy.linalg.det(B))
+            Binv = numpy.linalg.inv(B)
+            zMz = numpy.dot(z, DirectLikelihood.M_dot(K_mixed, Binv, Y, sigma, sigma0, z))
+            lp = -0.5 * (n - m) * numpy.log(2.0 * numpy.pi) - 0.5 * logdet_S \
+                - 0.5 * logdet_B - 0.5 * zMz
+        return -lp if sign_switch else lp
+
+    @staticmethod
+    def log_likelihood_batch(z, X, K_mixed, hyperparams, sign_switch=False):
+        """Vectorised log_likelihood over many (sigma, sigma0): all etas are
+        factorized in batches of ``K_mixed.op.max_batch`` per device call."""
+        hp = numpy.atleast_2d(numpy.asarray(hyperparams, dtype=float))
+        n, m = X.shape
+        out = numpy.empty(hp.shape[0])
+        big = numpy.abs(hp[:, 0]) >= _TOL
+        if numpy.any(big):
+            etas = (hp[big, 1] / hp[big, 0]) ** 2
+            ld, G = K_mixed.loglik_terms(etas, X, z)
+            out[big] = [_lp_from_terms(n, m, s, l, g)
+                        for s, l, g in zip(hp[big, 0], ld, G)]
+        for i in numpy.flatnonzero(~big):
+            out[i] = _lp_small_sigma(z, X, hp[i, 1])
+        return -out if sign_switch else out
+
+    @staticmethod
+    def M_dot(K_mixed, Binv, Y, sigma, sigma0, z):                 # :276-340
+        if numpy.abs(sigma) < _TOL:
+            w = z / sigma0 ** 2
+        else:
+            eta = (sigma0 / sigma) ** 2
+            w = K_mixed.solve(eta, z) / sigma ** 2
+        return w - Y @ (Binv @ (Y.T @ z))
+
+    @staticmethod
+    def log_likelihood_jacobian(z, X, K_mixed, sign_switch, hyperparam):   # :89-157
+        sigma, sigma0 = hyperparam[0], hyperparam[1]
+        n, m = X.shape
+        small = numpy.abs(sigma) < _TOL
+        if small:
+            Y = X / sigma0 ** 2
+        else:
+            eta = (sigma0 / sigma) ** 2
+            Y = K_mixed.solve(eta, X) / sigma ** 2
+        Binv = numpy.linalg.inv(X.T @ Y)
+        Mz = DirectLikelihood.M_dot(K_mixed, Binv, Y, sigma, sigma0, z)
+        KMz = K_mixed.dot(0, Mz)
+        zMMz = numpy.dot(Mz, Mz)
+        zMKMz = numpy.dot(Mz, KMz)
+        if small:
+            trace_M = (n - m) / sigma0 ** 2
+            YtKY = Y.T @ K_mixed.dot(0, Y)
+            trace_KM = K_mixed.trace(0) / sigma0 ** 2 - numpy.trace(Binv @ YtKY)
+        else:
+            trace_M = K_mixed.traceinv(eta) / sigma ** 2 - numpy.trace(Binv @ (Y.T @ Y))
+            trace_KM = (n - m) / sigma ** 2 - eta * trace_M
+        jac = numpy.array([-0.5 * trace_KM + 0.5 * zMKMz,
+                           -0.5 * trace_M + 0.5 * zMMz], dtype=float)
+        return -jac if sign_switch else jac
+
+    @staticmethod
+    def log_likelihood_hessian(z, X, K_mixed, sign_switch, hyperparam):    # :163-270
+        sigma, sigma0 = hyperparam[0], hyperparam[1]
+        n, m = X.shape
+        small = numpy.abs(sigma) < _TOL_HESS
+        if small:
+            Y = X / sigma0 ** 2
+            V = Y / sigma0 ** 2
+        else:
+            eta = (sigma0 / sigma) ** 2
+            Y = K_mixed.solve(eta, X) / sigma ** 2
+            V = K_mixed.solve(eta, Y) / sigma ** 2
+        Binv = numpy.linalg.inv(X.T @ Y)
+        A = Binv @ (Y.T @ Y)
+        Mz = DirectLikelihood.M_dot(K_mixed, Binv, Y, sigma, sigma0, z)
+        MMz = DirectLikelihood.M_dot(K_mixed, Binv, Y, sigma, sigma0, Mz)
+        KMz = K_mixed.dot(0, Mz)
+        MKMz = DirectLikelihood.M_dot(K_mixed, Binv, Y, sigma, sigma0, KMz)
+        zMMMz = numpy.dot(Mz, MMz)
+        zMMKMz = numpy.dot(MMz, KMz)
+        zMKMKMz = numpy.dot(KMz, MKMz)
+        if small:
+            trace_M = (n - m) / sigma0 ** 2
+            trace_S2inv = n / sigma0 ** 4
+        else:
+            trace_M = K_mixed.traceinv(eta) / sigma ** 2 - numpy.trace(A)
+            trace_S2inv = K_mixed.traceinv(eta, exponent=2) / sigma ** 4
+        trace_M2 = trace_S2inv - 2.0 * numpy.trace(Binv @ (Y.T @ V)) + numpy.trace(A @ A)
+        if small:
+            E = K_mixed.dot(0, X, exponent=2) @ (X.T @ X)
+            trace_KMKM = (K_mixed.trace(0, exponent=2) - 2.0 * numpy.trace(E) +
+                          numpy.trace(E @ E)) / sigma0 ** 4
+            YtKY = Y.T @ K_mixed.dot(0, Y)
+            trace_KM = K_mixed.trace(0) / sigma0 ** 2 - numpy.trace(Binv @ YtKY)
+            trace_KMM = trace_KM / sigma0 ** 2
+        else:
+            trace_KMKM = (n - m) / sigma ** 4 - (2 * eta / sigma ** 2) * trace_M + \
+                (eta ** 2) * trace_M2
+            trace_KMM = trace_M / sigma ** 2 - eta * trace_M2
+        h_ss = 0.5 * (trace_KMKM - 2.0 * zMKMKMz)
+        h_s0 = 0.5 * (trace_KMM - 2.0 * zMMKMz)
+        h_00 = 0.5 * (trace_M2 - 2.0 * zMMMz)
+        hess = numpy.array([[h_ss, h_s0], [h_s0, h_00]], dtype=float)
+        return -hess if sign_switch else hess
+
+    @staticmethod
+    def maximize_log_likelihood(z, X, K_mixed, tol=1e-3, hyperparam_guess=[0.2, 0.2],
+                                method='Nelder-Mead'):                      # :346-405
+        print('Maximize log likelihood with sigma sigma0 ...')
+        f = partial(DirectLikelihood.log_likelihood, z, X, K_mixed, True)
+        jac = partial(DirectLikelihood.log_likelihood_jacobian, z, X, K_mixed, True)
+        hess = partial(DirectLikelihood.log_likelihood_hessian, z, X, K_mixed, True)
+        # The reference overrides ``method`` with trust-exact (:378).
+        res = scipy.optimize.minimize(f, hyperparam_guess, method='trust-exact', tol=tol,
+                                      jac=jac, hess=hess)
+        print(res)
+        print('Iter: %d, Eval: %d, Success: %s' % (res.nit, res.nfev, res.success))
+        sigma, sigma0 = res.x[0], res.x[1]
+        return {'sigma': sigma, 'sigma0': sigma0, 'eta': (sigma0 / sigma) ** 2,
+                'max_lp': -res.fun}

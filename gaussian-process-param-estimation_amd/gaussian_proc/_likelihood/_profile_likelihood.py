@@ -1,0 +1,140 @@
+"""Profiled GP log-likelihood in (sigma, eta).
+
+Drop-in for ``ProfileLikelihood`` of the reference
+(gaussian_proc/_likelihood/_profile_likelihood.py:32-415).
+
+``log_likelihood`` (:38-85) uses the same single-factorization terms as the
+direct likelihood: with G = [X z]^T (K + eta I)^-1 [X z],
+  lp = -(n-m)/2 log sigma^2 - logdet(K + eta I)/2 - log det G_XX / 2
+       - (G_zz - G_Xz^T G_XX^-1 G_Xz) / (2 sigma^2).
+The reference materialises Y B^-1 Y^T as an n x n matrix (:73); the value is the
+same. The eta-derivatives (:91-192) keep the reference formulas on the operator
+duck type.
+"""
+
+import numpy
+from scipy.optimize import minimize
+from functools import partial
+
+from ._root_finding import find_interval_with_sign_change, chandrupatla_method
+
+__all__ = ['ProfileLikelihood']
+
+
+class ProfileLikelihood(object):
+
+    @staticmethod
+    def log_likelihood(z, X, K_mixed, sign_switch, hyperparam):
+        sigma, eta = hyperparam[0], hyperparam[1]
+        n, m = X.shape
+        if hasattr(K_mixed, 'loglik_terms'):
+            ld, G = K_mixed.loglik_terms([eta], X, z)
+            ld, G = ld[0], G[0]
+            Gxx, gxz, gzz = G[:m, :m], G[:m, m], G[m, m]
+            logdet_B = numpy.log(numpy.linalg.det(Gxx))
+            zMz = gzz - gxz @ numpy.linalg.solve(Gxx, gxz)
+        else:
+            ld = K_mixed.logdet(eta)
+            Y = K_mixed.solve(eta, X)
+            w = K_mixed.solve(eta, z)
+            B = X.T @ Y
+            logdet_B = numpy.log(numpy.linalg.det(B))
+            zMz = numpy.dot(z, w - Y @ (numpy.linalg.inv(B) @ (Y.T @ z)))
+        lp = -0.5 * (n - m) * numpy.log(sigma ** 2) - 0.5 * ld - 0.5 * logdet_B \
+            - (0.5 / (sigma ** 2)) * zMz
+        return -lp if sign_switch else lp
+
+    @staticmethod
+    def _mz(z, X, K_mixed, eta):
+        Y = K_mixed.solve(eta, X)
+        w = K_mixed.solve(eta, z)
+        Binv = numpy.linalg.inv(X.T @ Y)
+        return Y, Binv, w - Y @ (Binv @ (Y.T @ z))
+
+    @staticmethod
+    def log_likelihood_der1_eta(z, X, K_mixed, log_eta):           # :91-132
+        eta = 0.0 if numpy.isneginf(log_eta) else 10.0 ** log_eta
+        n, m = X.shape
+        Y, Binv, Mz = ProfileLikelihood._mz(z, X, K_mixed, eta)
+        trace_M = K_mixed.traceinv(eta) - numpy.trace(Binv @ (Y.T @ Y))
+        zMz = numpy.dot(z, Mz)
+        zM2z = numpy.dot(Mz, Mz)
+        sigma02 = zMz / (n - m)
+        return -0.5 * (trace_M - zM2z / sigma02)
+
+    @staticmethod
+    def log_likelihood_der2_eta(z, X, K_mixed, eta):               # :138-192
+        n, m = X.shape
+        Y, Binv, Mz = ProfileLikelihood._mz(z, X, K_mixed, eta)
+        V = K_mixed.solve(eta, Y)
+        A = Binv @ (Y.T @ Y)
+        trace_M = K_mixed.traceinv(eta) - numpy.trace(A)
+        trace_M2 = K_mixed.traceinv(eta, exponent=2) - \
+            2.0 * numpy.trace(Binv @ (Y.T @ V)) + numpy.trace(A @ A)
+        MMz = K_mixed.solve(eta, Mz) - Y @ (Binv @ (Y.T @ Mz))
+        zMz = numpy.dot(z, Mz)
+        zM3z = numpy.dot(Mz, MMz)
+        sigma02 = zMz / (n - m)
+        return (0.5 / sigma02) * ((trace_M2 / (n - m) + (trace_M / (n - m)) ** 2) * zMz -
+                                  2.0 * zM3z)
+
+    @staticmethod
+    def maximize_log_likelihood_with_sigma_eta(z, X, K_mixed, tol=1e-6,
+                                               hyperparam_guess=[0.1, 0.1],
+                                               method='Nelder-Mead'):   # :198-238
+        print('Maximize log likelihood with sigma eta ...')
+        f = partial(ProfileLikelihood.log_likelihood, z, X, K_mixed, True)
+        res = minimize(f, hyperparam_guess, method='Nelder-Mead', tol=tol)
+        print('Iter: %d, Eval: %d, success: %s' % (res.nit, res.nfev, res.success))
+        sigma, eta = res.x[0], res.x[1]
+        return {'sigma': sigma, 'sigma0': numpy.sqrt(eta) * sigma, 'eta': eta,
+                'max_lp': -res.fun}
+
+    @staticmethod
+    def find_log_likelihood_der1_zeros(z, X, K_mixed, interval_eta, tol=1e-6,
+                                       max_iterations=100, num_bracket_trials=3):  # :244-415
+        n, m = X.shape
+
+        def optimal_sigma(eta):
+            Y, Binv, Mz = ProfileLikelihood._mz(z, X, K_mixed, eta)
+            return numpy.sqrt(numpy.dot(z, Mz) / (n - m))
+
+        def optimal_sigma0():
+            Binv = numpy.linalg.inv(X.T @ X)
+            v = X @ (Binv @ (X.T @ z))
+            return numpy.sqrt(numpy.dot(z, z - v) / (n - m))
+
+        print('Find root of log likelihood derivative ...')
+        der1 = partial(ProfileLikelihood.log_likelihood_der1_eta, z, X, K_mixed)
+        bracket = [numpy.log10(interval_eta[0]), numpy.log10(interval_eta[1])]
+        found, bracket, values = find_interval_with_sign_change(
+            der1, bracket, num_bracket_trials, args=())
+        if found:
+            res = chandrupatla_method(der1, bracket, values, verbose=False, eps_m=tol,
+                                      eps_a=tol, maxiter=max_iterations)
+            print('Iter: %d' % (res['iterations']))
+            eta = 10 ** res['root']
+            sigma = optimal_sigma(eta)
+            sigma0 = numpy.sqrt(eta) * sigma
+            success = True
+        else:
+            d2 = ProfileLikelihood.log_likelihood_der2_eta(z, X, K_mixed, 0.0)
+            left, right = values[0], values[1]
+            print('dL/deta   at eta = %0.2e:\t %0.2f' % (bracket[0], left))
+            print('dL/deta   at eta = %0.2e:\t %0.16f' % (bracket[1], right))
+            print('d2L/deta2 at eta = 0.0:\t %0.2f' % d2)
+            eta = None
+            if left > 0 and right > 0:
+                eta = 0.0 if d2 > 0 else numpy.inf
+            elif left < 0 and right < 0:
+                eta = 0.0 if d2 < 0 else numpy.inf
+            if eta == 0:
+                sigma0 = 0
+                sigma = optimal_sigma(eta)
+            elif eta == numpy.inf:
+                sigma = 0
+                sigma0 = optimal_sigma0()
+            else:
+                raise ValueError('eta must be zero or inf at this point.')
+            success = True
+        return {'sigma': sigma, 'sigma0': sigma0, 'eta': eta, 'success': success}

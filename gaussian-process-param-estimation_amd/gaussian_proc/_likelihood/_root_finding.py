@@ -1,0 +1,98 @@
+"""Scalar bracketing and Chandrupatla root finding (host-side drivers).
+
+Restates the reference's gaussian_proc/_likelihood/_root_finding.py:
+  find_interval_with_sign_change  :21-148  (midpoint probe, then one outward step)
+  chandrupatla_method             :155-309 (IQI / bisection hybrid)
+The decision rules and return values match the reference for scalar f; the
+per-iteration diagnostic prints of the bracket search are kept.
+"""
+
+import numpy
+
+__all__ = ['find_interval_with_sign_change', 'chandrupatla_method']
+
+
+def find_interval_with_sign_change(f, bracket, num_bracket_trials, args=()):
+    x0, x1 = bracket[0], bracket[1]
+    f0, f1 = f(x0, *args), f(x1, *args)
+    for it in range(1, num_bracket_trials + 1):
+        if numpy.sign(f0) != numpy.sign(f1):
+            return True, [x0, x1], [f0, f1]
+        print('bracket was not found. Search for bracket. Iteration: %d' % it)
+        print('x0: %0.2f, f0: %0.16f' % (x0, f0))
+        print('x1: %0.2f, f1: %0.16f' % (x1, f1))
+        xm = 0.5 * x0 + 0.5 * x1
+        fm = f(xm, *args)
+        print('x_new: %0.2f, f_new: %0.16f' % (xm, fm))
+        left_smaller = numpy.abs(f0) < numpy.abs(f1)
+        if numpy.sign(f0) != numpy.sign(fm):
+            if left_smaller:
+                return True, [x0, xm], [f0, fm]
+            return True, [xm, x1], [fm, f1]
+        if numpy.abs(fm) < min(numpy.abs(f0), numpy.abs(f1)):
+            # shrink toward the side with the smaller |f|
+            if left_smaller:
+                x1, f1 = xm, fm
+            else:
+                x0, f0 = xm, fm
+            continue
+        # probe one half-width outside, on the side of the smaller |f|
+        right = numpy.abs(f0) > numpy.abs(f1)
+        t = 1.5 if right else -0.5
+        xo = x0 * (1.0 - t) + x1 * t
+        fo = f(xo, *args)
+        if numpy.sign(f0) != numpy.sign(fo):
+            if right:
+                return True, [xo, x0], [fo, f0]
+            return True, [x1, xo], [f1, fo]
+        if right:
+            x0, f0, x1, f1 = x1, f1, xo, fo
+        else:
+            x1, f1, x0, f0 = x0, f0, xo, fo
+    return False, [x0, x1], [f0, f1]
+
+
+def chandrupatla_method(f, bracket, bracket_values, verbose=False, eps_m=None, eps_a=None,
+                        maxiter=50, args=()):
+    b, a = float(bracket[0]), float(bracket[1])
+    if bracket_values is None:
+        fa, fb = f(a, *args), f(b, *args)
+    else:
+        fa, fb = bracket_values[1], bracket_values[0]
+    assert numpy.sign(fa) * numpy.sign(fb) <= 0
+    c, fc = a, fa
+    eps = numpy.finfo(float).eps
+    eps_m = eps if eps_m is None else eps_m
+    eps_a = 2 * eps if eps_a is None else eps_a
+    t = 0.5
+    iterations = 0
+    xm = b
+    while maxiter > 0:
+        maxiter -= 1
+        xt = a + t * (b - a)
+        ft = f(xt, *args)
+        if numpy.sign(ft) == numpy.sign(fa):
+            c, fc = a, fa
+        else:
+            c, fc = b, fb
+            b, fb = a, fa
+        a, fa = xt, ft
+        if numpy.abs(fa) < numpy.abs(fb):
+            xm, fm = a, fa
+        else:
+            xm, fm = b, fb
+        tol = 2 * eps_m * numpy.abs(xm) + eps_a
+        tlim = tol / numpy.abs(b - c)
+        if verbose:
+            print('xt=%r ft=%r fm=%r tlim=%r' % (xt, ft, fm, tlim))
+        if fm == 0 or tlim > 0.5:
+            break
+        iterations += 1
+        xi = (a - b) / (c - b)
+        phi = (fa - fb) / (fc - fb)
+        if phi ** 2 < xi and (1 - phi) ** 2 < 1 - xi:
+            t = fa / (fb - fa) * fc / (fb - fc) + (c - a) / (b - a) * fa / (fc - fa) * fb / (fc - fb)
+        else:
+            t = 0.5
+        t = min(1 - tlim, max(tlim, t))
+    return {'root': xm, 'iterations': iterations}

@@ -1,0 +1,166 @@
+"""The mixed-correlation operator K + eta I, device-resident.
+
+Drop-in for ``MixedCorrelation`` of the reference
+(gaussian_proc/_mixed_correlation/mixed_correlation.py:25-335). K lives in HBM
+once per operator; every eta-dependent quantity comes from one fp64 MFMA
+Cholesky of K + eta I (csrc/gpmi_chol.hip), cached per eta so that
+``logdet(eta)`` followed by ``solve(eta, .)`` factorizes once.
+
+All exact ``imate_method`` values ('eigenvalue', 'cholesky', and 'hutchinson'
+for logdet, which the reference maps to Cholesky at :236-246) are computed
+exactly from the Cholesky factor; they agree with the reference's eigenvalue
+path to rounding. The stochastic estimators ('hutchinson' traceinv, 'slq') and
+traceinv interpolation are not implemented yet and raise
+``NotImplementedError``.
+
+Error conventions follow the reference: ``ValueError`` for an unknown method
+(:146,212,271) or a bad ``dot`` exponent (:323-326), ``TypeError`` for
+``interpolate`` without points (:53-55), and ``numpy.linalg.LinAlgError`` when
+K + eta I is not positive definite (scipy's posv behaviour).
+"""
+
+import numpy
+
+from .. import _hip
+from ..generate_correlation.generate_correlation import DeviceCorrelation
+
+__all__ = ['MixedCorrelation']
+
+_METHODS = ('eigenvalue', 'cholesky', 'hutchinson', 'slq')
+
+
+class MixedCorrelation(object):
+    """K + eta I without forming sigma^2 K + sigma0^2 I."""
+
+    def __init__(self, K, interpolate=False, interpolant_points=None,
+                 imate_method='cholesky', imate_options={}, device=None, max_batch=None):
+        self.interpolate = interpolate
+        self.interpolant_points = interpolant_points
+        self.imate_method = imate_method
+        self.imate_options = imate_options
+        if self.interpolate:
+            if self.interpolant_points is None:
+                raise TypeError('When "interpolate" is set to "True", the '
+                                '"interpolant_points" cannot be None.')
+            raise NotImplementedError('traceinv interpolation is not implemented yet')
+        if isinstance(K, DeviceCorrelation):
+            if max_batch is not None and max_batch > K.op.max_batch:
+                raise ValueError('DeviceCorrelation was created with max_batch=%d'
+                                 % K.op.max_batch)
+            self.K = K
+            self.op = K.op
+        else:
+            if hasattr(K, 'toarray') and not isinstance(K, numpy.ndarray):
+                raise NotImplementedError('sparse K is not implemented on the device yet')
+            K = numpy.ascontiguousarray(K, dtype=float)
+            if K.ndim != 2 or K.shape[0] != K.shape[1]:
+                raise ValueError('K must be a square matrix')
+            self.K = K
+            self.op = _hip.Operator(K.shape[0], device=device, max_batch=max_batch or 1)
+            self.op.load_matrix(K)
+        self.n = self.op.n
+        self._trace_cache = None
+        self._rhs_cache = None
+
+    # ---- reference duck type -------------------------------------------------
+
+    def get_matrix_size(self):                                     # :85-90
+        return self.n
+
+    def _traces(self):
+        if self._trace_cache is None:
+            self._trace_cache = self.op.trace()
+        return self._trace_cache
+
+    def trace(self, eta, exponent=1):                              # :96-149
+        if exponent == 0:
+            return float(self.n)
+        if exponent == 1:
+            t = self._traces()[0]
+            if eta != 0:
+                t += eta * self.n
+            return t
+        if exponent == 2:
+            tk, tk2 = self._traces()
+            if eta == 0:
+                return tk2
+            return tk2 + 2.0 * eta * tk + eta ** 2 * self.n
+        if self.imate_method in ('eigenvalue', 'slq'):
+            raise NotImplementedError('trace with exponent %r needs the eigenvalue '
+                                      'operator (not implemented yet)' % exponent)
+        raise ValueError('Existing methods are "exact", "eigenvalue", and "slq".')
+
+    def traceinv(self, eta, exponent=1):                           # :155-215
+        if self.imate_method not in ('eigenvalue', 'cholesky'):
+            if self.imate_method in _METHODS:
+                raise NotImplementedError('stochastic traceinv (%s) is not implemented yet'
+                                          % self.imate_method)
+            raise ValueError('Existing methods are "eigenvalue", "cholesky,"'
+                             '"hutchinson", and "slq".')
+        # exact: tr((K + eta I)^-p) from the inverse (columns solved on the device)
+        Ainv = self.op.solve(eta, numpy.eye(self.n))
+        if exponent == 1:
+            return float(numpy.trace(Ainv))
+        if exponent == 2:
+            return float(numpy.sum(Ainv * Ainv))
+        return float(numpy.trace(numpy.linalg.matrix_power(Ainv, exponent)))
+
+    def logdet(self, eta, exponent=1):                             # :221-274
+        if self.imate_method not in ('eigenvalue', 'cholesky', 'hutchinson'):
+            if self.imate_method == 'slq':
+                raise NotImplementedError('slq logdet is not implemented yet')
+            raise ValueError('Existing methods are "eigenvalue", "cholesky",'
+                             ' and "slq".')
+        return exponent * self.op.logdet(eta)
+
+    def solve(self, eta, Y):                                       # :280-299
+        return self.op.solve(eta, Y)
+
+    def dot(self, eta, x, exponent=1):                             # :305-335
+        if not isinstance(exponent, int):
+            raise ValueError('"exponent" should be an integer.')
+        elif exponent < 0:
+            raise ValueError('"exponent" should be a non-negative integer.')
+        y = numpy.zeros_like(x, dtype=float)
+        if exponent == 0:
+            return y
+        Kx = self.op.matvec(x)
+        for _ in range(exponent):
+            y += Kx
+            if eta != 0:
+                y += eta * x
+        return y
+
+    # ---- fused hot path (extension) -----------------------------------------
+
+    def set_rhs(self, X, z):
+        """Make [X | z] the resident RHS block (skipped if unchanged)."""
+        X = numpy.asarray(X, dtype=float)
+        z = numpy.asarray(z, dtype=float)
+        c = self._rhs_cache
+        if c is not None and c[0].shape == X.shape and numpy.array_equal(c[0], X) and \
+                numpy.array_equal(c[1], z):
+            return
+        if X.shape[1] + 1 > _hip.MAX_RHS:
+            raise ValueError('at most %d basis functions' % (_hip.MAX_RHS - 1))
+        self.op.set_rhs(numpy.column_stack([X, z]))
+        self._rhs_cache = (X.copy(), z.copy())
+
+    def loglik_terms(self, etas, X, z):
+        """For each eta: logdet(K + eta I) and G = [X z]^T (K + eta I)^-1 [X z]
+        from ONE Cholesky per eta, batched over up to ``max_batch`` etas per
+        device call. Returns (logdet[neta], G[neta, m+1, m+1])."""
+        self.set_rhs(X, z)
+        etas = numpy.atleast_1d(numpy.asarray(etas, dtype=float))
+        lds, gs = [], []
+        mb = self.op.max_batch
+        for i in range(0, etas.size, mb):
+            ld, g, info = self.op.loglik_batch(etas[i:i + mb])
+            if numpy.any(info):
+                bad = int(numpy.flatnonzero(info)[0])
+                raise numpy.linalg.LinAlgError(
+                    'K + eta I is not positive definite for eta = %r (pivot %d)'
+                    % (etas[i + bad], info[bad]))
+            lds.append(ld)
+            gs.append(g)
+        return numpy.concatenate(lds), numpy.concatenate(gs)

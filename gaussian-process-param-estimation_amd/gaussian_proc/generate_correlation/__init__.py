@@ -1,0 +1,3 @@
+from .generate_correlation import generate_correlation, DeviceCorrelation   # noqa: F401
+
+__all__ = ['generate_correlation']

@@ -1,0 +1,114 @@
+/*
+ * gpmi — MI355X-native (gfx950) Gaussian-process log-likelihood evaluator.
+ * C ABI of libgpmi.so: plain pointers and sizes, int status codes, no C++
+ * exceptions and no framework types across the boundary.
+ *
+ * Status: 0 = OK; > 0 = LAPACK-style info (1-based index of the first
+ * non-positive pivot of K + eta I, i.e. "not positive definite");
+ * < 0 = error (message via gpmi_last_error).
+ *
+ * The reference (ameli/gaussian-process-param-estimation v0.0.1) has no FFI on
+ * this path: its hot path is Python calling Cython/scipy/imate. Each entry point
+ * below replaces the reference interface cited next to it; the Python package
+ * gaussian_proc (gaussian-process-param-estimation_amd/gaussian_proc) binds them
+ * with ctypes.
+ *
+ * Layouts: host matrices are row-major (C order) fp64. Device state lives in an
+ * opaque gpmi_op handle (one per GPU per operator); calls on one handle must be
+ * serialised by the caller.
+ */
+#ifndef GPMI_H_
+#define GPMI_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct gpmi_op gpmi_op;
+
+#define GPMI_MAX_RHS 16   /* columns of the resident RHS block (m + 1 <= 16) */
+
+/* Library version (major*10000 + minor*100 + patch). */
+int gpmi_version(void);
+
+/* Copy the calling thread's last error message into buf (always NUL-terminated). */
+int gpmi_last_error(char* buf, size_t len);
+
+/* Number of visible HIP devices. */
+int gpmi_device_count(int* count);
+
+/* Dense Matérn correlation matrix, host in / host out.
+ * Replaces generate_correlation(points, correlation_scale, nu, sparse=False)
+ *   gaussian_proc/generate_correlation/generate_correlation.py:32-222
+ *   -> _generate_dense_correlation.pyx:98-162 -> _kernels.pyx:17-136.
+ * points: [n][d] (d <= 8); scale: [d] (already broadcast); K_out: [n][ldk]. */
+int gpmi_matern_dense(int device, const double* points, int64_t n, int d,
+                      const double* scale, double nu, double* K_out, int64_t ldk);
+
+/* Create the device-resident K + eta I operator for an n x n correlation matrix,
+ * with workspace for max_batch concurrent eta values.
+ * Replaces MixedCorrelation.__init__  mixed_correlation.py:34-79. */
+int gpmi_op_create(int device, int64_t n, int max_batch, gpmi_op** out);
+int gpmi_op_destroy(gpmi_op* op);
+/* n and the padded size (multiple of 128) used on the device. */
+int gpmi_op_size(const gpmi_op* op, int64_t* n, int64_t* n_pad);
+
+/* Fill K from a host matrix [n][ldk] (symmetric; the lower triangle is used). */
+int gpmi_op_load_matrix(gpmi_op* op, const double* K_host, int64_t ldk);
+/* Assemble K on the device from points (no host round trip):
+ * generate_correlation(points, scale, nu) fused into the operator. */
+int gpmi_op_assemble_matern(gpmi_op* op, const double* points, int d,
+                            const double* scale, double nu);
+/* Copy K back to the host ([n][ldk]). */
+int gpmi_op_get_matrix(gpmi_op* op, double* K_out, int64_t ldk);
+
+/* Upload the resident RHS block R = [X | z] ([n][ld], nrhs <= 16 columns). */
+int gpmi_op_set_rhs(gpmi_op* op, const double* rhs, int64_t ld, int nrhs);
+
+/* Batched likelihood terms for neta <= max_batch values of eta, one dense
+ * Cholesky per eta (K + eta I = L L^T) on fp64 MFMA:
+ *   logdet[e]            = log det(K + eta_e I)
+ *   gram[e][nrhs][nrhs]  = (L^-1 R)^T (L^-1 R) = R^T (K + eta_e I)^-1 R
+ *   info[e]              = 0, or 1-based first non-positive pivot.
+ * Replaces the logdet + 2 x solve of DirectLikelihood.log_likelihood
+ * (_direct_likelihood.py:59,62,332 -> mixed_correlation.py:221-299). */
+int gpmi_op_loglik_batch(gpmi_op* op, const double* etas, int neta,
+                         double* logdet, double* gram, int* info);
+
+/* logdet(K + eta I) (mixed_correlation.py:221-274, exact). Caches the factor. */
+int gpmi_op_logdet(gpmi_op* op, double eta, double* logdet);
+
+/* Solve (K + eta I) X = RHS for an [n][ld] host RHS with nrhs columns
+ * (any count; processed in blocks of 16). Reuses the cached factor for eta.
+ * Replaces MixedCorrelation.solve mixed_correlation.py:280-299
+ *   -> linear_solver _linear_solver.py:24-73 (scipy.linalg.solve, assume_a='pos'). */
+int gpmi_op_solve(gpmi_op* op, double eta, const double* rhs, int64_t ld, int nrhs,
+                  double* sol, int64_t ldsol);
+
+/* y = K x for an [n][ld] host block with ncol columns.
+ * Building block of MixedCorrelation.dot mixed_correlation.py:305-335. */
+int gpmi_op_matvec(gpmi_op* op, const double* x, int64_t ld, int ncol, double* y,
+                   int64_t ldy);
+
+/* trace(K) and trace(K^2) = ||K||_F^2 (K symmetric).
+ * Building blocks of MixedCorrelation.trace mixed_correlation.py:96-149. */
+int gpmi_op_trace(gpmi_op* op, double* trace_k, double* trace_k2);
+
+/* Kernel-level timing of the last gpmi_op_loglik_batch when enabled:
+ * dominant kernel (trailing-update SYRK) total device ms, launches and
+ * algorithmic flops; whole-call device ms. HIP events on the op's stream. */
+int gpmi_op_set_timing(gpmi_op* op, int enable);
+int gpmi_op_last_timing(gpmi_op* op, double* syrk_ms, int* syrk_launches,
+                        double* syrk_flops, double* total_ms);
+
+/* Outer panel width in 128-column sub-panels (trailing update depth = 128*S). */
+int gpmi_op_set_outer(gpmi_op* op, int s);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GPMI_H_ */

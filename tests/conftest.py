@@ -1,0 +1,22 @@
+import os
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG_ROOT = os.path.join(REPO, 'gaussian-process-param-estimation_amd')
+for p in (REPO, PKG_ROOT):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+GOLDEN = os.path.join(REPO, 'tests', 'golden')
+
+
+def pytest_configure(config):
+    config.addinivalue_line('markers', 'gpu: needs an MI355X (gfx950) HIP device')
+    config.addinivalue_line('markers', 'slow: long-running (large N)')
+
+
+@pytest.fixture(scope='session')
+def golden_dir():
+    return GOLDEN

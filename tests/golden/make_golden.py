@@ -1,0 +1,253 @@
+#!/usr/bin/env python
+"""Generate the golden fixtures under tests/golden/ by running the REFERENCE
+(ameli/gaussian-process-param-estimation v0.0.1) in the development container.
+
+Recipe:
+  1. copy /root/reference/gaussian_proc to a scratch dir under /tmp (never into
+     the repo), cythonize its three .pyx modules there with the directives of the
+     reference setup.py:993-999 (+ legacy_implicit_noexcept for speed only; the
+     results are identical) and -O3 -fopenmp, language c++;
+  2. install ``oracle.imate_exact`` (the restated exact imate methods; imate is
+     unpinned in requirements.txt:5 and absent here) as module ``imate``;
+  3. stub ``mpl_toolkits.axes_grid1.inset_locator.InsetPosition`` (removed in
+     matplotlib 3.10, only used by plotting code);
+  4. import the reference and its examples/_utilities/data_utilities.py, and
+     record inputs/outputs as JSON / npz (allow_pickle=False) fixtures.
+
+Outputs are data only (inputs and expected outputs). The reference never
+travels with the repo. Run:  python tests/golden/make_golden.py [--big]
+"""
+
+import argparse
+import json
+import os
+import shutil
+import subprocess
+import sys
+import textwrap
+
+import numpy
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = '/root/reference'
+SCRATCH = '/tmp/gp_ref_build'
+
+
+def build_reference():
+    pkg_dst = os.path.join(SCRATCH, 'pkg')
+    gc_dir = os.path.join(pkg_dst, 'gaussian_proc', 'generate_correlation')
+    if os.path.isdir(gc_dir) and any(f.endswith('.so') for f in os.listdir(gc_dir)):
+        return pkg_dst
+    if os.path.isdir(SCRATCH):
+        shutil.rmtree(SCRATCH)
+    os.makedirs(pkg_dst)
+    shutil.copytree(os.path.join(REF, 'gaussian_proc'),
+                    os.path.join(pkg_dst, 'gaussian_proc'))
+    setup_py = textwrap.dedent('''
+        from setuptools import setup, Extension
+        from Cython.Build import cythonize
+        import numpy
+        names = ['_kernels', '_generate_dense_correlation',
+                 '_generate_sparse_correlation']
+        exts = [Extension('gaussian_proc.generate_correlation.' + n,
+                          ['gaussian_proc/generate_correlation/' + n + '.pyx'],
+                          language='c++', include_dirs=[numpy.get_include()],
+                          extra_compile_args=['-O3', '-fopenmp'],
+                          extra_link_args=['-fopenmp'])
+                for n in names]
+        setup(ext_modules=cythonize(exts, language_level=3, compiler_directives={
+            'boundscheck': False, 'wraparound': False, 'cdivision': True,
+            'nonecheck': False, 'legacy_implicit_noexcept': True}))
+    ''')
+    with open(os.path.join(pkg_dst, 'setup.py'), 'w') as f:
+        f.write(setup_py)
+    subprocess.check_call([sys.executable, 'setup.py', 'build_ext', '--inplace'],
+                          cwd=pkg_dst, stdout=subprocess.DEVNULL)
+    return pkg_dst
+
+
+def import_reference():
+    pkg = build_reference()
+    sys.path.insert(0, REPO)
+    import oracle.imate_exact
+    sys.modules['imate'] = oracle.imate_exact
+    import matplotlib
+    matplotlib.use('Agg')
+    import mpl_toolkits.axes_grid1.inset_locator as il
+    if not hasattr(il, 'InsetPosition'):
+        il.InsetPosition = object
+    sys.path.insert(0, pkg)
+    sys.path.insert(0, os.path.join(REF, 'examples'))
+    import gaussian_proc
+    from gaussian_proc._mixed_correlation import MixedCorrelation
+    from gaussian_proc._likelihood._direct_likelihood import DirectLikelihood
+    from gaussian_proc._likelihood._profile_likelihood import ProfileLikelihood
+    from gaussian_proc._likelihood import Likelihood
+    from _utilities import data_utilities as du
+    return dict(gp=gaussian_proc, MC=MixedCorrelation, DL=DirectLikelihood,
+                PL=ProfileLikelihood, Likelihood=Likelihood, du=du)
+
+
+def f(x):
+    return float(x)
+
+
+ETAS = [1e-3, 1e-1, 1.0, 10.0]
+HYPERS = [[0.1, 0.2], [1.0, 0.1], [0.5, 0.05], [1.0, 1.0], [1e-9, 0.3]]
+LOG_ETAS = [-1.0, 0.0, 1.0]
+
+
+def sample_idx(n, k=64, seed=7):
+    rng = numpy.random.RandomState(seed)
+    return numpy.sort(rng.choice(n, size=min(k, n), replace=False))
+
+
+def config_case(R, name, num_points, dim, nu, scale=0.1, full_arrays=False,
+                optimize=False):
+    du = R['du']
+    pts = du.generate_points(num_points, dim, True)
+    z = du.generate_data(pts, 0.2)
+    X = du.generate_basis_functions(pts, 2)
+    K = R['gp'].generate_correlation(pts, scale, nu, True)
+    n, m = X.shape
+    ii = sample_idx(n)
+    jj = sample_idx(n, seed=11)
+    out = dict(name=name, num_points=num_points, dimension=dim, nu=nu,
+               correlation_scale=scale, n=n, m=m,
+               K_sum=f(K.sum()), K_diag_sum=f(numpy.trace(K)),
+               K_samples=dict(i=ii.tolist(), j=jj.tolist(),
+                              v=K[ii, jj].tolist()),
+               K_row_sums_sample=K.sum(axis=1)[ii].tolist(),
+               z_sum=f(z.sum()), z_samples=z[ii].tolist(),
+               X_col_sums=X.sum(axis=0).tolist(), sample_rows=ii.tolist())
+    arrays = {}
+    mcs = {'eigenvalue': R['MC'](K, imate_method='eigenvalue'),
+           'cholesky': R['MC'](K, imate_method='cholesky')}
+    ops = {}
+    for meth, op in mcs.items():
+        d = {}
+        d['logdet'] = [f(op.logdet(e)) for e in ETAS]
+        d['logdet_exp2'] = [f(op.logdet(e, exponent=2)) for e in ETAS[:2]]
+        d['traceinv'] = [f(op.traceinv(e)) for e in ETAS]
+        d['traceinv_exp2'] = [f(op.traceinv(e, exponent=2)) for e in ETAS]
+        d['trace'] = {str(p): [f(op.trace(e, exponent=p)) for e in [0.0] + ETAS]
+                      for p in (0, 1, 2)}
+        ops[meth] = d
+    out['etas'] = ETAS
+    out['operator'] = ops
+    op = mcs['eigenvalue']
+    DL, PL = R['DL'], R['PL']
+    out['hypers'] = HYPERS
+    out['direct_lp'] = [f(DL.log_likelihood(z, X, op, False, h)) for h in HYPERS]
+    out['direct_lp_chol'] = [f(DL.log_likelihood(z, X, mcs['cholesky'], False, h))
+                             for h in HYPERS]
+    out['direct_jac'] = [DL.log_likelihood_jacobian(z, X, op, False, h).tolist()
+                         for h in HYPERS]
+    out['direct_hess'] = [DL.log_likelihood_hessian(z, X, op, False, h).tolist()
+                          for h in HYPERS]
+    out['profile_hypers'] = [[0.1, 1.0], [1.0, 0.01], [0.3, 10.0]]
+    out['profile_lp'] = [f(PL.log_likelihood(z, X, op, False, h))
+                         for h in out['profile_hypers']]
+    out['log_etas'] = LOG_ETAS
+    out['profile_der1_eta'] = [f(PL.log_likelihood_der1_eta(z, X, op, le))
+                               for le in LOG_ETAS]
+    out['profile_der2_eta_etas'] = [0.1, 1.0]
+    out['profile_der2_eta'] = [f(PL.log_likelihood_der2_eta(z, X, op, e))
+                               for e in out['profile_der2_eta_etas']]
+    # operator solve / dot samples
+    w = op.solve(1.0, z)
+    Y = op.solve(0.1, X)
+    out['solve_eta1_z_samples'] = w[ii].tolist()
+    out['solve_eta1_z_sum'] = f(w.sum())
+    out['solve_eta01_X_colsums'] = Y.sum(axis=0).tolist()
+    d2 = op.dot(0.5, z, exponent=2)
+    out['dot_eta05_exp2_z_samples'] = d2[ii].tolist()
+    out['dot_eta05_exp2_z_sum'] = f(d2.sum())
+    if full_arrays:
+        arrays['K'] = K
+        arrays['solve_eta1_z'] = w
+        arrays['solve_eta01_X'] = Y
+        arrays['points'] = pts
+        arrays['z'] = z
+        arrays['X'] = X
+    if optimize:
+        import io
+        import contextlib
+        buf = io.StringIO()
+        with contextlib.redirect_stdout(buf):
+            rd = R['Likelihood'](X, K, 'direct').maximize_log_likelihood(z)
+            rp = R['Likelihood'](X, K, 'profiled').maximize_log_likelihood(z)
+        out['maximize_direct'] = {k: f(v) for k, v in rd.items()}
+        out['maximize_profiled'] = {k: (f(v) if not isinstance(v, bool) else v)
+                                    for k, v in rp.items()}
+    return out, arrays
+
+
+def matern_cases(R):
+    gp = R['gp']
+    rng = numpy.random.RandomState(2024)
+    cases = [(1, 0.1, 0.5), (2, 0.1, 1.5), (2, 0.25, 2.5), (3, 0.3, 1.5),
+             (2, [0.1, 0.3], 1.5), (3, [0.2, 0.1, 0.4], 2.5), (2, 0.2, 3.2),
+             (2, 0.2, 0.8), (2, 0.2, 150.0), (1, 0.05, 1.5)]
+    arrays = {}
+    meta = []
+    for c, (d, scale, nu) in enumerate(cases):
+        pts = rng.rand(48, d)
+        if c == 0:
+            pts[5] = pts[3]                     # duplicate point -> distance 0
+        sc = numpy.array(scale, dtype=float) if isinstance(scale, list) else scale
+        K = gp.generate_correlation(pts, sc, nu, grid=False)
+        arrays['points_%d' % c] = pts
+        arrays['K_%d' % c] = K
+        meta.append(dict(case=c, dimension=d, correlation_scale=scale, nu=nu))
+    return meta, arrays
+
+
+def big_case(R):
+    """N=16384 (2D 128x128 grid, nu=1.5): 'cholesky' imate method (3 dense
+    factorizations per lp) — the eigenvalue method needs a 227 s eigh."""
+    du = R['du']
+    pts = du.generate_points(128, 2, True)
+    z = du.generate_data(pts, 0.2)
+    X = du.generate_basis_functions(pts, 2)
+    K = R['gp'].generate_correlation(pts, 0.1, 1.5, True)
+    op = R['MC'](K, imate_method='cholesky')
+    etas = [0.01, 1.0, 4.0]
+    out = dict(name='cfg3_n16384_nu1.5', n=16384, m=X.shape[1], nu=1.5,
+               correlation_scale=0.1, K_sum=f(K.sum()),
+               etas=etas, logdet=[f(op.logdet(e)) for e in etas],
+               hypers=[[0.1, 0.2], [1.0, 0.1]])
+    out['direct_lp'] = [f(R['DL'].log_likelihood(z, X, op, False, h))
+                        for h in out['hypers']]
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--big', action='store_true', help='also the N=16384 case (~5 min)')
+    args = ap.parse_args()
+    R = import_reference()
+    meta, arr = matern_cases(R)
+    numpy.savez_compressed(os.path.join(HERE, 'matern_small.npz'), **arr)
+    with open(os.path.join(HERE, 'matern_small.json'), 'w') as fh:
+        json.dump(meta, fh, indent=1)
+    c1, a1 = config_case(R, 'cfg1_n256_1d', 256, 1, 1.5, full_arrays=True,
+                         optimize=True)
+    numpy.savez_compressed(os.path.join(HERE, 'cfg1_arrays.npz'), **a1)
+    with open(os.path.join(HERE, 'cfg1.json'), 'w') as fh:
+        json.dump(c1, fh, indent=1)
+    c2, _ = config_case(R, 'cfg2_n4096_2d', 64, 2, 1.5)
+    with open(os.path.join(HERE, 'cfg2.json'), 'w') as fh:
+        json.dump(c2, fh, indent=1)
+    c25, _ = config_case(R, 'n1024_2d_nu2.5', 32, 2, 2.5)
+    with open(os.path.join(HERE, 'n1024_nu25.json'), 'w') as fh:
+        json.dump(c25, fh, indent=1)
+    if args.big:
+        with open(os.path.join(HERE, 'cfg3_big.json'), 'w') as fh:
+            json.dump(big_case(R), fh, indent=1)
+    print('golden fixtures written to', HERE)
+
+
+if __name__ == '__main__':
+    main()

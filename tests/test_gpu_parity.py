@@ -1,0 +1,245 @@
+"""HIP path vs the oracle / golden vectors on an MI355X (gfx950).
+
+Tolerances (north_star): logdet <= 1e-8 relative, log-likelihood <= 1e-6
+relative; the tests use tighter bars where fp64 allows. Matérn entries:
+closed forms within a few ulp of the reference Cython build.
+"""
+
+import numpy
+import pytest
+
+from oracle import matern, likelihood as olk
+from oracle.mixed_correlation import MixedCorrelation as OracleMC
+from _util import load_json, load_npz, config_inputs, rel
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope='module')
+def gp():
+    import gaussian_proc
+    from gaussian_proc import _hip
+    _hip.require_device(0)
+    return gaussian_proc
+
+
+# ---------------------------------------------------------------- assembly --
+
+def test_matern_dense_matches_reference_cython(gp):
+    meta = load_json('matern_small.json')
+    arr = load_npz('matern_small.npz')
+    for case in meta:
+        c = case['case']
+        pts = arr['points_%d' % c]
+        K_ref = arr['K_%d' % c]
+        K = gp.generate_correlation(pts, case['correlation_scale'], case['nu'], grid=False)
+        err = numpy.max(numpy.abs(K - K_ref))
+        tol = 4e-16 if case['nu'] in (0.5, 1.5, 2.5) or case['nu'] >= 100 else 1e-13
+        assert err <= tol, (case, err)
+        numpy.testing.assert_array_equal(K, K.T)
+        assert numpy.all(numpy.diag(K) == 1.0)
+
+
+@pytest.mark.parametrize('nu', [0.3, 0.5, 0.75, 1.0, 1.5, 2.0, 2.5, 3.2, 7.5, 40.0, 150.0])
+def test_matern_general_nu_vs_scipy(gp, nu):
+    rng = numpy.random.RandomState(5)
+    pts = rng.rand(200, 2)
+    K = gp.generate_correlation(pts, 0.15, nu, grid=False)
+    K_ref = matern.dense_correlation(pts, 0.15, nu)
+    assert numpy.max(numpy.abs(K - K_ref)) <= 2e-14
+
+
+def test_device_resident_correlation_roundtrip(gp):
+    cfg = load_json('cfg1.json')
+    pts, _, _ = config_inputs(cfg)
+    D = gp.generate_correlation(pts, 0.1, 1.5, device_resident=True)
+    K = D.toarray()
+    K_ref = load_npz('cfg1_arrays.npz')['K']
+    assert numpy.max(numpy.abs(K - K_ref)) <= 4e-16
+
+
+# ---------------------------------------------------------------- operator --
+
+def _op(gp, K, **kw):
+    from gaussian_proc._mixed_correlation import MixedCorrelation
+    return MixedCorrelation(K, imate_method='cholesky', **kw)
+
+
+@pytest.mark.parametrize('name', ['cfg1.json', 'n1024_nu25.json'])
+def test_operator_exact_methods(gp, name):
+    cfg = load_json(name)
+    pts, z, X = config_inputs(cfg)
+    K = gp.generate_correlation(pts, cfg['correlation_scale'], cfg['nu'])
+    assert rel(K.sum(), cfg['K_sum']) < 1e-13
+    op = _op(gp, K)
+    g = cfg['operator']['cholesky']
+    assert rel([op.logdet(e) for e in cfg['etas']], g['logdet']) < 1e-10
+    assert rel([op.logdet(e, exponent=2) for e in cfg['etas'][:2]], g['logdet_exp2']) < 1e-10
+    for p in ('0', '1', '2'):
+        assert rel([op.trace(e, int(p)) for e in [0.0] + cfg['etas']], g['trace'][p]) < 1e-12
+    assert rel([op.traceinv(e) for e in cfg['etas']], g['traceinv']) < 1e-8
+    assert rel([op.traceinv(e, 2) for e in cfg['etas']], g['traceinv_exp2']) < 1e-8
+    w = op.solve(1.0, z)
+    numpy.testing.assert_allclose(w[cfg['sample_rows']], cfg['solve_eta1_z_samples'],
+                                  rtol=1e-9, atol=1e-12)
+    Y = op.solve(0.1, X)
+    assert rel(Y.sum(axis=0), cfg['solve_eta01_X_colsums']) < 1e-8
+    d2 = op.dot(0.5, z, exponent=2)
+    numpy.testing.assert_allclose(d2[cfg['sample_rows']], cfg['dot_eta05_exp2_z_samples'],
+                                  rtol=1e-12)
+
+
+def test_solve_full_vectors_cfg1(gp):
+    a = load_npz('cfg1_arrays.npz')
+    op = _op(gp, a['K'])
+    numpy.testing.assert_allclose(op.solve(1.0, a['z']), a['solve_eta1_z'], rtol=1e-10,
+                                  atol=1e-12)
+    numpy.testing.assert_allclose(op.solve(0.1, a['X']), a['solve_eta01_X'], rtol=1e-9,
+                                  atol=1e-11)
+
+
+@pytest.mark.parametrize('n', [1, 5, 127, 128, 129, 300, 1000])
+def test_ragged_sizes_vs_oracle(gp, n):
+    rng = numpy.random.RandomState(n)
+    pts = rng.rand(n, 2)
+    K = matern.dense_correlation(pts, 0.2, 1.5)
+    X = numpy.column_stack([numpy.ones(n), pts])
+    z = numpy.sin(3 * pts[:, 0]) + 0.1 * rng.randn(n)
+    op = _op(gp, K)
+    ref = OracleMC(K, 'cholesky')
+    for eta in (1e-2, 1.0):
+        assert rel(op.logdet(eta), ref.logdet(eta)) < 1e-10
+        numpy.testing.assert_allclose(op.solve(eta, z), ref.solve(eta, z), rtol=1e-8,
+                                      atol=1e-10)
+        numpy.testing.assert_allclose(op.solve(eta, X), ref.solve(eta, X), rtol=1e-8,
+                                      atol=1e-10)
+    ld, G = op.loglik_terms([0.05, 0.5, 5.0], X, z)
+    R = numpy.column_stack([X, z])
+    for e, l, g in zip([0.05, 0.5, 5.0], ld, G):
+        assert rel(l, ref.logdet(e)) < 1e-10
+        numpy.testing.assert_allclose(g, R.T @ ref.solve(e, R), rtol=1e-8, atol=1e-10)
+
+
+def test_solve_many_columns(gp):
+    rng = numpy.random.RandomState(1)
+    pts = rng.rand(400, 2)
+    K = matern.dense_correlation(pts, 0.1, 2.5)
+    B = rng.randn(400, 37)
+    op = _op(gp, K)
+    numpy.testing.assert_allclose(op.solve(0.3, B), OracleMC(K).solve(0.3, B), rtol=1e-9,
+                                  atol=1e-10)
+
+
+def test_not_positive_definite_raises_linalg_error(gp):
+    n = 200
+    rng = numpy.random.RandomState(3)
+    A = rng.randn(n, n)
+    K = A + A.T                                    # indefinite
+    op = _op(gp, K)
+    with pytest.raises(numpy.linalg.LinAlgError):
+        op.logdet(0.0)
+    with pytest.raises(numpy.linalg.LinAlgError):
+        op.solve(0.0, numpy.ones(n))
+    # a large shift makes it SPD again
+    ref = OracleMC(K)
+    assert rel(op.logdet(100.0), ref.logdet(100.0)) < 1e-10
+
+
+def test_method_errors_match_reference(gp):
+    from gaussian_proc._mixed_correlation import MixedCorrelation
+    K = numpy.eye(4)
+    with pytest.raises(TypeError):
+        MixedCorrelation(K, interpolate=True)
+    op = MixedCorrelation(K, imate_method='bogus')
+    with pytest.raises(ValueError):
+        op.logdet(1.0)
+    with pytest.raises(ValueError):
+        op.traceinv(1.0)
+    op2 = MixedCorrelation(K)
+    with pytest.raises(ValueError):
+        op2.dot(0, numpy.ones(4), exponent=1.5)
+    with pytest.raises(ValueError):
+        op2.dot(0, numpy.ones(4), exponent=-1)
+
+
+# -------------------------------------------------------------- likelihood --
+
+@pytest.mark.parametrize('name', ['cfg1.json', 'n1024_nu25.json'])
+def test_direct_and_profile_likelihood(gp, name):
+    from gaussian_proc._likelihood import Likelihood
+    from gaussian_proc._likelihood._direct_likelihood import DirectLikelihood
+    from gaussian_proc._likelihood._profile_likelihood import ProfileLikelihood
+    cfg = load_json(name)
+    pts, z, X = config_inputs(cfg)
+    K = gp.generate_correlation(pts, cfg['correlation_scale'], cfg['nu'])
+    lik = Likelihood(X, K, max_batch=4)
+    lps = [lik.likelihood(z, h) for h in cfg['hypers']]
+    assert rel(lps, cfg['direct_lp']) < 1e-9
+    assert rel(lik.likelihood_batch(z, cfg['hypers']), cfg['direct_lp']) < 1e-9
+    op = lik.K_mixed
+    for h, jref, href in zip(cfg['hypers'], cfg['direct_jac'], cfg['direct_hess']):
+        assert rel(DirectLikelihood.log_likelihood_jacobian(z, X, op, False, h), jref) < 1e-7
+        if h[0] >= 1e-8:
+            assert rel(DirectLikelihood.log_likelihood_hessian(z, X, op, False, h), href) < 1e-6
+    assert rel([ProfileLikelihood.log_likelihood(z, X, op, False, h)
+                for h in cfg['profile_hypers']], cfg['profile_lp']) < 1e-9
+    assert rel([ProfileLikelihood.log_likelihood_der1_eta(z, X, op, le)
+                for le in cfg['log_etas']], cfg['profile_der1_eta']) < 1e-7
+    assert rel([ProfileLikelihood.log_likelihood_der2_eta(z, X, op, e)
+                for e in cfg['profile_der2_eta_etas']], cfg['profile_der2_eta']) < 1e-6
+
+
+def test_cfg2_n4096_likelihood_and_logdet(gp):
+    cfg = load_json('cfg2.json')
+    pts, z, X = config_inputs(cfg)
+    D = gp.generate_correlation(pts, 0.1, 1.5, device_resident=True, max_batch=4)
+    from gaussian_proc._likelihood import Likelihood
+    lik = Likelihood(X, D)
+    assert rel(lik.likelihood_batch(z, cfg['hypers']), cfg['direct_lp']) < 1e-8
+    op = lik.K_mixed
+    assert rel([op.logdet(e) for e in cfg['etas']],
+               cfg['operator']['eigenvalue']['logdet']) < 1e-9
+    ld, _ = op.loglik_terms(cfg['etas'], X, z)
+    assert rel(ld, cfg['operator']['eigenvalue']['logdet']) < 1e-9
+
+
+def test_maximize_cfg1_matches_reference(gp, capsys):
+    from gaussian_proc._likelihood import Likelihood
+    cfg = load_json('cfg1.json')
+    pts, z, X = config_inputs(cfg)
+    K = gp.generate_correlation(pts, 0.1, 1.5)
+    rd = Likelihood(X, K, 'direct').maximize_log_likelihood(z)
+    ref = cfg['maximize_direct']
+    assert rel([rd['sigma'], rd['sigma0'], rd['max_lp']],
+               [ref['sigma'], ref['sigma0'], ref['max_lp']]) < 1e-6
+    rp = Likelihood(X, K, 'profiled').maximize_log_likelihood(z)
+    refp = cfg['maximize_profiled']
+    assert rp['eta'] == numpy.inf and rp['sigma'] == 0
+    assert rel(rp['sigma0'], refp['sigma0']) < 1e-12
+
+
+def test_gaussian_process_train_smoke(gp, capsys):
+    cfg = load_json('cfg1.json')
+    pts, z, X = config_inputs(cfg)
+    K = gp.generate_correlation(pts, 0.1, 1.5)
+    gp.GaussianProcess(X, K).train(z)
+    out = capsys.readouterr().out
+    assert "'sigma'" in out and "'max_lp'" in out
+
+
+@pytest.mark.slow
+def test_cfg3_n16384_logdet_and_lp(gp):
+    cfg = load_json('cfg3_big.json')
+    from oracle import data
+    pts = data.generate_points(128, 2, True)
+    z = data.generate_data(pts, 0.2)
+    X = data.generate_basis_functions(pts, 2)
+    D = gp.generate_correlation(pts, 0.1, 1.5, device_resident=True, max_batch=3)
+    assert rel(D.op.trace()[0], 16384.0) < 1e-15
+    from gaussian_proc._mixed_correlation import MixedCorrelation
+    op = MixedCorrelation(D)
+    ld, _ = op.loglik_terms(cfg['etas'], X, z)
+    assert rel(ld, cfg['logdet']) < 1e-9
+    from gaussian_proc._likelihood._direct_likelihood import DirectLikelihood
+    lp = DirectLikelihood.log_likelihood_batch(z, X, op, cfg['hypers'])
+    assert rel(lp, cfg['direct_lp']) < 1e-8
