@@ -41,7 +41,7 @@ def parse():
     ap.add_argument('--grid', type=int, default=128, help='points per axis (n = grid^2)')
     ap.add_argument('--nu', type=float, default=1.5)
     ap.add_argument('--eta-per-rank', type=int, default=8)
-    ap.add_argument('--outer', type=int, default=2, help='outer panel width / 128')
+    ap.add_argument('--outer', type=int, default=4, help='outer panel width / 128')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-timing', action='store_true',
                     help='skip the per-kernel HIP-event roofline timing')

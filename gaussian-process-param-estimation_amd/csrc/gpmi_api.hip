@@ -70,7 +70,7 @@ struct gpmi_op {
   int64_t n = 0, n_pad = 0;
   int nt = 0;
   int max_batch = 1;
-  int outer = 2;
+  int outer = 4;
   hipStream_t stream = nullptr;
   double* K = nullptr;       // [n_pad][n_pad]
   double* A = nullptr;       // [max_batch][n_pad][n_pad]

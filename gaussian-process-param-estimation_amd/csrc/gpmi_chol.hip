@@ -24,20 +24,9 @@
 
 #include "gpmi_internal.h"
 
+#include "gpmi_device.h"
+
 namespace gpmi {
-
-typedef double d4 __attribute__((ext_vector_type(4)));
-typedef double d2 __attribute__((ext_vector_type(2)));
-
-constexpr int TS = GPMI_TS;      // 128
-constexpr int BK = 16;           // k-depth of one LDS stage
-constexpr int LDSK = 18;         // padded row stride (doubles) of a staged [row][k] slab
-constexpr int STAGE = TS * LDSK; // doubles per staged operand buffer
-constexpr int RLD = GPMI_RHS_LD; // 16
-
-__device__ __forceinline__ d4 mfma64(double a, double b, d4 c) {
-  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
-}
 
 // 128 x 16 slab of rows base[row * ld + p .. p + 15]: each wave-instruction
 // reads 32 full 128-B row segments (16 B / lane).
@@ -165,121 +154,6 @@ __global__ __launch_bounds__(256) void shift_copy_kernel(
       }
       *reinterpret_cast<d2*>(A + b * sA + gi * lda + gj) = o;
     }
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Diagonal block k (one workgroup per batch member): in-LDS Cholesky,
-// triangular inverse, logdet partial and the RHS forward step.
-// ---------------------------------------------------------------------------
-constexpr int DLD = TS + 1;   // LDS row stride of the 128x128 block (bank-conflict-free columns)
-
-__global__ __launch_bounds__(256) void diag_block_kernel(BatchPtrs P, int64_t lda, int kb,
-                                                         int nt) {
-  __shared__ double Ls[TS * DLD];
-  __shared__ double Ys[TS * RLD];
-  __shared__ double tmp[TS];
-  __shared__ int s_fail;
-  const int t = threadIdx.x;
-  const int b = blockIdx.x;
-  const int64_t k0 = (int64_t)kb * TS;
-  double* A = P.A + b * P.sA;
-  double* R = P.R + b * P.sR;
-  if (t == 0) s_fail = 0;
-  for (int e = t; e < TS * TS; e += 256) {
-    const int r = e >> 7, c = e & 127;
-    Ls[r * DLD + c] = (c <= r) ? A[(k0 + r) * lda + k0 + c] : 0.0;
-  }
-  for (int e = t; e < TS * RLD; e += 256) Ys[e] = R[k0 * RLD + e];
-  __syncthreads();
-
-  // --- right-looking Cholesky, one column per step ---
-  double logsum = 0.0;
-  const int row = t & 127, half = t >> 7;
-  for (int j = 0; j < TS; ++j) {
-    const double djj = Ls[j * DLD + j];
-    const double ljj = sqrt(djj);
-    if (t == 0) {
-      if (!(djj > 0.0) && s_fail == 0) s_fail = j + 1;
-      logsum += log(ljj);
-    }
-    __syncthreads();
-    if (t < TS) {
-      if (t > j) Ls[t * DLD + j] = Ls[t * DLD + j] / ljj;
-      else if (t == j) Ls[t * DLD + j] = ljj;
-    }
-    __syncthreads();
-    if (row > j) {
-      const double lrj = Ls[row * DLD + j];
-      for (int c = j + 1 + half; c <= row; c += 2)
-        Ls[row * DLD + c] -= lrj * Ls[c * DLD + j];
-    }
-    __syncthreads();
-  }
-  if (t == 0) {
-    P.logdiag[b * P.sLD + kb] = 2.0 * logsum;
-    if (s_fail && P.info[b] == 0) P.info[b] = (int)k0 + s_fail;
-  }
-  for (int e = t; e < TS * TS; e += 256) {
-    const int r = e >> 7, c = e & 127;
-    if (c <= r) A[(k0 + r) * lda + k0 + c] = Ls[r * DLD + c];
-  }
-  __syncthreads();
-
-  // --- in-place inverse of the lower-triangular block (column sweep, j descending) ---
-  for (int j = TS - 1; j >= 0; --j) {
-    if (t < TS && t > j) tmp[t] = Ls[t * DLD + j];
-    if (t == 0) Ls[j * DLD + j] = 1.0 / Ls[j * DLD + j];
-    __syncthreads();
-    if (t < TS && t > j) {
-      const double ajj = -Ls[j * DLD + j];
-      double s = 0.0;
-      for (int p = j + 1; p <= t; ++p) s += Ls[t * DLD + p] * tmp[p];
-      Ls[t * DLD + j] = ajj * s;
-    }
-    __syncthreads();
-  }
-  double* Li = P.Linv + b * P.sL + (int64_t)kb * TS * TS;
-  for (int e = t; e < TS * TS; e += 256) {
-    const int r = e >> 7, c = e & 127;
-    Li[e] = (c <= r) ? Ls[r * DLD + c] : 0.0;
-  }
-
-  // --- y = Linv r_k ; u = Linv^T y ; Gram = y^T y ---
-  double yv[8];
-#pragma unroll
-  for (int q = 0; q < 8; ++q) yv[q] = 0.0;
-  for (int p = 0; p <= row; ++p) {
-    const double l = Ls[row * DLD + p];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) yv[q] += l * Ys[p * RLD + half * 8 + q];
-  }
-  __syncthreads();
-#pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    Ys[row * RLD + half * 8 + q] = yv[q];
-    R[(k0 + row) * RLD + half * 8 + q] = yv[q];
-  }
-  __syncthreads();
-  {
-    const int c = row;
-    double uv[8];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) uv[q] = 0.0;
-    for (int r = c; r < TS; ++r) {
-      const double l = Ls[r * DLD + c];
-#pragma unroll
-      for (int q = 0; q < 8; ++q) uv[q] += l * Ys[r * RLD + half * 8 + q];
-    }
-    double* U = P.U + b * P.sU;
-#pragma unroll
-    for (int q = 0; q < 8; ++q) U[c * RLD + half * 8 + q] = uv[q];
-  }
-  {
-    const int a = t >> 4, q = t & 15;
-    double g = 0.0;
-    for (int r = 0; r < TS; ++r) g += Ys[r * RLD + a] * Ys[r * RLD + q];
-    P.gram[b * P.sG + (int64_t)kb * 256 + t] = g;
   }
 }
 
