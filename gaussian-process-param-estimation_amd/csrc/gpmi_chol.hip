@@ -55,7 +55,7 @@ __device__ __forceinline__ void sstore_slab(double* s, const d2 (&r)[4]) {
 // f64 MFMA 16x16x4 operand maps: A[i = lane&15][k = lane>>4], B[k = lane>>4][j = lane&15].
 // WITH_RHS additionally accumulates racc (rows wr*64 + wc*32 + [0,32), 16 cols)
 // += P1 * U with U[kdim][16] staged in LDS.
-template <bool WITH_RHS>
+template <bool WITH_RHS, bool NEG = false>
 __device__ __forceinline__ void tile_mma(const double* __restrict__ P1, int64_t ld1,
                                          const double* __restrict__ P2, int64_t ld2,
                                          int kdim, double* sA, double* sB,
@@ -83,7 +83,10 @@ __device__ __forceinline__ void tile_mma(const double* __restrict__ P1, int64_t 
     for (int kk = 0; kk < BK / 4; ++kk) {
       double a[4], b[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) a[i] = cA[(wr * 64 + i * 16 + fr) * LDSK + kk * 4 + fk];
+      for (int i = 0; i < 4; ++i) {
+        a[i] = cA[(wr * 64 + i * 16 + fr) * LDSK + kk * 4 + fk];
+        if (NEG) a[i] = -a[i];
+      }
 #pragma unroll
       for (int j = 0; j < 4; ++j) b[j] = cB[(wc * 64 + j * 16 + fr) * LDSK + kk * 4 + fk];
 #pragma unroll
@@ -219,22 +222,27 @@ __global__ __launch_bounds__(256, 2) void syrk_kernel(double* A, int64_t lda, in
   double* Ab = A + blockIdx.y * sA;
   const double* P1 = Ab + (int64_t)I * TS * lda + p0;
   const double* P2 = Ab + (int64_t)J * TS * lda + p0;
-  d4 acc[4][4];
-#pragma unroll
-  for (int a = 0; a < 4; ++a)
-#pragma unroll
-    for (int c = 0; c < 4; ++c) acc[a][c] = d4{0.0, 0.0, 0.0, 0.0};
-  d4 dummy[2];
-  tile_mma<false>(P1, lda, P2, lda, kdim, smem, smem + 2 * STAGE, acc, nullptr, dummy);
+  // The C tile is loaded into the accumulators up front (its latency overlaps
+  // the first operand stage) and the update runs as acc += (-P1) P2^T, so the
+  // epilogue is store-only.
   double* C = Ab + (int64_t)I * TS * lda + (int64_t)J * TS;
+  d4 acc[4][4];
 #pragma unroll
   for (int a = 0; a < 4; ++a)
 #pragma unroll
     for (int c = 0; c < 4; ++c)
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        C[(int64_t)(wr * 64 + a * 16 + fk + 4 * r) * lda + wc * 64 + c * 16 + fr] -=
-            acc[a][c][r];
+        acc[a][c][r] = C[(int64_t)(wr * 64 + a * 16 + fk + 4 * r) * lda + wc * 64 + c * 16 + fr];
+  d4 dummy[2];
+  tile_mma<false, true>(P1, lda, P2, lda, kdim, smem, smem + 2 * STAGE, acc, nullptr, dummy);
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        C[(int64_t)(wr * 64 + a * 16 + fk + 4 * r) * lda + wc * 64 + c * 16 + fr] = acc[a][c][r];
 }
 
 // out[b][0] = logdet = sum of block partials; out[b][1 + e] = Gram entry e (16x16).
