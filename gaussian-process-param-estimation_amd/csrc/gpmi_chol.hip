@@ -175,7 +175,14 @@ __global__ __launch_bounds__(256) void panel_kernel(BatchPtrs P, int64_t lda, in
   const int I = kb + 1 + blockIdx.x;
   double* A = P.A + b * P.sA;
   const double* U = P.U + b * P.sU;
-  for (int e = t; e < TS * RLD; e += 256) sU[e] = U[e];
+  {
+    d2 v[4];
+#pragma unroll
+    for (int it = 0; it < 4; ++it)
+      v[it] = *reinterpret_cast<const d2*>(U + 2 * (it * 256 + t));
+#pragma unroll
+    for (int it = 0; it < 4; ++it) *reinterpret_cast<d2*>(&sU[2 * (it * 256 + t)]) = v[it];
+  }
   double* Aik = A + (int64_t)I * TS * lda + (int64_t)kb * TS;
   const double* Li = P.Linv + b * P.sL + (int64_t)kb * TS * TS;
   d4 acc[4][4];
