@@ -71,7 +71,10 @@ struct gpmi_op {
   int nt = 0;
   int max_batch = 1;
   int outer = 4;
+  int lanes = 1;                       // concurrent half-batches (streams) per call
   hipStream_t stream = nullptr;
+  hipStream_t stream2 = nullptr;       // second lane
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   double* K = nullptr;       // [n_pad][n_pad]
   double* A = nullptr;       // [max_batch][n_pad][n_pad]
   double* R = nullptr;       // [max_batch][n_pad][16]
@@ -99,6 +102,7 @@ struct gpmi_op {
   double last_syrk_ms = 0.0, last_syrk_flops = 0.0, last_total_ms = 0.0;
   int last_syrk_launches = 0;
   std::vector<std::pair<int, double>> syrk_log;  // (event index, flops)
+  double last_syrk_busy_ms = 0.0;                // union of syrk launch intervals
 
   BatchPtrs ptrs() const {
     BatchPtrs p;
@@ -121,10 +125,11 @@ struct gpmi_op {
 
 namespace {
 
-int launch_syrk(gpmi_op* op, int nb, int tc0, int w, int t, int p0, int kdim) {
+int launch_syrk(gpmi_op* op, hipStream_t st, int b0, int nb, int tc0, int w, int t, int p0,
+                int kdim) {
   const int tri = w * (w + 1) / 2;
   const int tiles = tri + (t - w) * w;
-  if (tiles <= 0) return 0;
+  if (tiles <= 0 || nb <= 0) return 0;
   int evi = -1;
   if (op->timing) {
     evi = (int)op->syrk_log.size() * 2;
@@ -135,13 +140,14 @@ int launch_syrk(gpmi_op* op, int nb, int tc0, int w, int t, int p0, int kdim) {
         op->ev.push_back(e);
       }
     }
-    HIP_TRY(hipEventRecord(op->ev[evi], op->stream));
+    HIP_TRY(hipEventRecord(op->ev[evi], st));
   }
-  hipLaunchKernelGGL(syrk_kernel, dim3(tiles, nb), dim3(256), 0, op->stream, op->A,
-                     (int64_t)op->n_pad, op->n_pad * op->n_pad, tc0, w, t, p0, kdim);
+  hipLaunchKernelGGL(syrk_kernel, dim3(tiles, nb), dim3(256), 0, st,
+                     op->A + (int64_t)b0 * op->n_pad * op->n_pad, (int64_t)op->n_pad,
+                     op->n_pad * op->n_pad, tc0, w, t, p0, kdim);
   LAUNCH_CHECK("syrk_kernel");
   if (op->timing) {
-    HIP_TRY(hipEventRecord(op->ev[evi + 1], op->stream));
+    HIP_TRY(hipEventRecord(op->ev[evi + 1], st));
     // algorithmic flops: lower triangle only (diagonal tiles count 128*129/2 entries)
     const double offd = (double)(tiles - std::min(tiles, w)) * TS * TS;
     const double diag = (double)std::min(tiles, w) * TS * (TS + 1) / 2.0;
@@ -149,6 +155,18 @@ int launch_syrk(gpmi_op* op, int nb, int tc0, int w, int t, int p0, int kdim) {
     op->syrk_log.push_back({evi, fl});
   }
   return 0;
+}
+
+BatchPtrs offset_ptrs(const BatchPtrs& P, int b0) {
+  BatchPtrs q = P;
+  q.A += b0 * P.sA;
+  q.R += b0 * P.sR;
+  q.U += b0 * P.sU;
+  q.Linv += b0 * P.sL;
+  q.logdiag += b0 * P.sLD;
+  q.gram += b0 * P.sG;
+  q.info += b0;
+  return q;
 }
 
 // Factor K + eta_b I for b < nb, with the fused forward substitution of the
@@ -179,29 +197,52 @@ int run_factor(gpmi_op* op, const double* etas_host, int nb, const double* rhs_d
     HIP_TRY(hipMemcpyAsync(op->R + b * P.sR, rhs_dev, sizeof(double) * P.sR,
                            hipMemcpyDeviceToDevice, s));
   HIP_TRY(hipMemsetAsync(op->info, 0, sizeof(int) * nb, s));
+  // lanes: the batch is split into halves factorized on two streams, so one
+  // half's latency-bound diagonal/panel chain overlaps the other's trailing update.
+  const int L = (op->lanes > 1 && nb > 1 && op->stream2) ? 2 : 1;
+  const int nb0 = L == 2 ? (nb + 1) / 2 : nb;
+  const int lb0[2] = {0, nb0};
+  const int lnb[2] = {nb0, nb - nb0};
+  hipStream_t ls[2] = {s, op->stream2};
+  if (L == 2) {
+    HIP_TRY(hipEventRecord(op->ev_fork, s));
+    HIP_TRY(hipStreamWaitEvent(op->stream2, op->ev_fork, 0));
+  }
   int kb = 0;
   while (kb < nt) {
     const int S = std::min(op->outer, nt - kb);
     for (int sp = 0; sp < S; ++sp) {
       const int j = kb + sp;
-      if (sp > 0) {
-        int rc = launch_syrk(op, nb, j, 1, nt - j, kb * TS, sp * TS);
-        if (rc) return rc;
+      if (sp > 0)
+        for (int l = 0; l < L; ++l) {
+          int rc = launch_syrk(op, ls[l], lb0[l], lnb[l], j, 1, nt - j, kb * TS, sp * TS);
+          if (rc) return rc;
+        }
+      for (int l = 0; l < L; ++l) {
+        hipLaunchKernelGGL(diag_block_kernel, dim3(lnb[l]), dim3(256), 0, ls[l],
+                           offset_ptrs(P, lb0[l]), lda, j, nt);
+        LAUNCH_CHECK("diag_block_kernel");
       }
-      hipLaunchKernelGGL(diag_block_kernel, dim3(nb), dim3(256), 0, s, P, lda, j, nt);
-      LAUNCH_CHECK("diag_block_kernel");
-      if (j + 1 < nt) {
-        hipLaunchKernelGGL(panel_kernel, dim3(nt - j - 1, nb), dim3(256), 0, s, P, lda, j);
-        LAUNCH_CHECK("panel_kernel");
-      }
+      if (j + 1 < nt)
+        for (int l = 0; l < L; ++l) {
+          hipLaunchKernelGGL(panel_kernel, dim3(nt - j - 1, lnb[l]), dim3(256), 0, ls[l],
+                             offset_ptrs(P, lb0[l]), lda, j);
+          LAUNCH_CHECK("panel_kernel");
+        }
     }
     const int tc0 = kb + S;
     if (tc0 < nt) {
       const int t = nt - tc0;
-      int rc = launch_syrk(op, nb, tc0, t, t, kb * TS, S * TS);
-      if (rc) return rc;
+      for (int l = 0; l < L; ++l) {
+        int rc = launch_syrk(op, ls[l], lb0[l], lnb[l], tc0, t, t, kb * TS, S * TS);
+        if (rc) return rc;
+      }
     }
     kb += S;
+  }
+  if (L == 2) {
+    HIP_TRY(hipEventRecord(op->ev_join, op->stream2));
+    HIP_TRY(hipStreamWaitEvent(s, op->ev_join, 0));
   }
   hipLaunchKernelGGL(finalize_kernel, dim3(nb), dim3(256), 0, s, P, nt, op->out, OUT_LD);
   LAUNCH_CHECK("finalize_kernel");
@@ -213,15 +254,32 @@ int collect_timing(gpmi_op* op) {
   if (!op->timing) return 0;
   HIP_TRY(hipEventSynchronize(op->ev_end));
   double tot = 0.0, fl = 0.0;
+  std::vector<std::pair<double, double>> iv;
   for (auto& pr : op->syrk_log) {
-    float ms = 0.f;
+    float ms = 0.f, t0 = 0.f, t1 = 0.f;
     HIP_TRY(hipEventElapsedTime(&ms, op->ev[pr.first], op->ev[pr.first + 1]));
+    HIP_TRY(hipEventElapsedTime(&t0, op->ev_begin, op->ev[pr.first]));
+    HIP_TRY(hipEventElapsedTime(&t1, op->ev_begin, op->ev[pr.first + 1]));
+    iv.push_back({t0, t1});
     tot += ms;
     fl += pr.second;
   }
+  std::sort(iv.begin(), iv.end());
+  double busy = 0.0, cs = -1.0, ce = -1.0;
+  for (auto& x : iv) {
+    if (x.first > ce) {
+      if (ce > cs) busy += ce - cs;
+      cs = x.first;
+      ce = x.second;
+    } else if (x.second > ce) {
+      ce = x.second;
+    }
+  }
+  if (ce > cs) busy += ce - cs;
   float all = 0.f;
   HIP_TRY(hipEventElapsedTime(&all, op->ev_begin, op->ev_end));
   op->last_syrk_ms = tot;
+  op->last_syrk_busy_ms = busy;
   op->last_syrk_flops = fl;
   op->last_syrk_launches = (int)op->syrk_log.size();
   op->last_total_ms = all;
@@ -341,6 +399,12 @@ int gpmi_op_create(int device, int64_t n, int max_batch, gpmi_op** out) {
   hipError_t e;
   if ((e = hipStreamCreateWithFlags(&op->stream, hipStreamNonBlocking)) != hipSuccess)
     return fail(e, "stream");
+  if ((e = hipStreamCreateWithFlags(&op->stream2, hipStreamNonBlocking)) != hipSuccess)
+    return fail(e, "stream2");
+  if ((e = hipEventCreateWithFlags(&op->ev_fork, hipEventDisableTiming)) != hipSuccess)
+    return fail(e, "event");
+  if ((e = hipEventCreateWithFlags(&op->ev_join, hipEventDisableTiming)) != hipSuccess)
+    return fail(e, "event");
 #define ALLOC(ptr, count)                                                           \
   if ((e = hipMalloc(&op->ptr, sizeof(*op->ptr) * (size_t)(count))) != hipSuccess)  \
     return fail(e, #ptr);
@@ -371,6 +435,7 @@ int gpmi_op_destroy(gpmi_op* op) {
   if (!op) return 0;
   DeviceGuard g(op->device);
   if (op->stream) (void)hipStreamSynchronize(op->stream);
+  if (op->stream2) (void)hipStreamSynchronize(op->stream2);
   double* bufs[] = {op->K, op->A, op->R, op->X, op->U, op->Linv, op->logdiag, op->gram,
                     op->out, op->etas, op->rhs_src, op->scratch, op->scratch2, op->tracebuf};
   for (double* p : bufs)
@@ -379,6 +444,9 @@ int gpmi_op_destroy(gpmi_op* op) {
   for (auto e : op->ev) (void)hipEventDestroy(e);
   if (op->ev_begin) (void)hipEventDestroy(op->ev_begin);
   if (op->ev_end) (void)hipEventDestroy(op->ev_end);
+  if (op->ev_fork) (void)hipEventDestroy(op->ev_fork);
+  if (op->ev_join) (void)hipEventDestroy(op->ev_join);
+  if (op->stream2) (void)hipStreamDestroy(op->stream2);
   if (op->stream) (void)hipStreamDestroy(op->stream);
   delete op;
   return 0;
@@ -593,12 +661,20 @@ int gpmi_op_set_timing(gpmi_op* op, int enable) {
 }
 
 int gpmi_op_last_timing(gpmi_op* op, double* syrk_ms, int* syrk_launches, double* syrk_flops,
-                        double* total_ms) {
+                        double* total_ms, double* syrk_busy_ms) {
   if (!op) return set_err(-1006, "null handle");
+  if (syrk_busy_ms) *syrk_busy_ms = op->last_syrk_busy_ms;
   if (syrk_ms) *syrk_ms = op->last_syrk_ms;
   if (syrk_launches) *syrk_launches = op->last_syrk_launches;
   if (syrk_flops) *syrk_flops = op->last_syrk_flops;
   if (total_ms) *total_ms = op->last_total_ms;
+  return 0;
+}
+
+int gpmi_op_set_lanes(gpmi_op* op, int lanes) {
+  if (!op) return set_err(-1006, "null handle");
+  if (lanes < 1 || lanes > 2) return set_err(-1009, "lanes %d outside [1, 2]", lanes);
+  op->lanes = lanes;
   return 0;
 }
 

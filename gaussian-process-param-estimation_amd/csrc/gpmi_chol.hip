@@ -47,7 +47,7 @@ __device__ __forceinline__ void sstore_slab(double* s, const d2 (&r)[4]) {
   for (int i = 0; i < 4; ++i) {
     const int idx = i * 256 + t;
     const int row = idx >> 3, c2 = idx & 7;
-    *reinterpret_cast<d2*>(s + row * LDSK + 2 * c2) = r[i];
+    *reinterpret_cast<d2*>(s + row * BK + 2 * (c2 ^ ((row >> 1) & 7))) = r[i];
   }
 }
 
@@ -84,11 +84,11 @@ __device__ __forceinline__ void tile_mma(const double* __restrict__ P1, int64_t 
       double a[4], b[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        a[i] = cA[(wr * 64 + i * 16 + fr) * LDSK + kk * 4 + fk];
+        a[i] = cA[slab_off(wr * 64 + i * 16 + fr, kk * 4 + fk)];
         if (NEG) a[i] = -a[i];
       }
 #pragma unroll
-      for (int j = 0; j < 4; ++j) b[j] = cB[(wc * 64 + j * 16 + fr) * LDSK + kk * 4 + fk];
+      for (int j = 0; j < 4; ++j) b[j] = cB[slab_off(wc * 64 + j * 16 + fr, kk * 4 + fk)];
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -164,7 +164,7 @@ __global__ __launch_bounds__(256) void shift_copy_kernel(
 // Panel: for row tile I = kb + 1 + blockIdx.x of member b = blockIdx.y:
 //   L_Ik = A_Ik Linv_kk^T (in place)  and  r_I -= A_Ik u_k.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void panel_kernel(BatchPtrs P, int64_t lda, int kb) {
+__global__ __launch_bounds__(256, 2) void panel_kernel(BatchPtrs P, int64_t lda, int kb) {
   __shared__ double smem[4 * STAGE + TS * RLD];
   double* sA = smem;
   double* sB = smem + 2 * STAGE;

@@ -48,7 +48,8 @@ SIGNATURES = {
     'gpmi_op_trace': (ctypes.c_int, [c_op_p, c_double_p, c_double_p]),
     'gpmi_op_set_timing': (ctypes.c_int, [c_op_p, ctypes.c_int]),
     'gpmi_op_last_timing': (ctypes.c_int, [c_op_p, c_double_p, c_int_p, c_double_p,
-                                           c_double_p]),
+                                           c_double_p, c_double_p]),
+    'gpmi_op_set_lanes': (ctypes.c_int, [c_op_p, ctypes.c_int]),
     'gpmi_op_set_outer': (ctypes.c_int, [c_op_p, ctypes.c_int]),
 }
 
@@ -221,11 +222,16 @@ class Operator(object):
         nl = ctypes.c_int()
         fl = ctypes.c_double()
         tot = ctypes.c_double()
+        busy = ctypes.c_double()
         check(self.lib.gpmi_op_last_timing(self.h, ctypes.byref(ms), ctypes.byref(nl),
-                                           ctypes.byref(fl), ctypes.byref(tot)),
+                                           ctypes.byref(fl), ctypes.byref(tot),
+                                           ctypes.byref(busy)),
               'gpmi_op_last_timing')
         return dict(syrk_ms=ms.value, syrk_launches=nl.value, syrk_flops=fl.value,
-                    total_ms=tot.value)
+                    total_ms=tot.value, syrk_busy_ms=busy.value)
+
+    def set_lanes(self, lanes):
+        check(self.lib.gpmi_op_set_lanes(self.h, int(lanes)), 'gpmi_op_set_lanes')
 
     def set_outer(self, s):
         check(self.lib.gpmi_op_set_outer(self.h, int(s)), 'gpmi_op_set_outer')

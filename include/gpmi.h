@@ -102,7 +102,12 @@ int gpmi_op_trace(gpmi_op* op, double* trace_k, double* trace_k2);
  * algorithmic flops; whole-call device ms. HIP events on the op's stream. */
 int gpmi_op_set_timing(gpmi_op* op, int enable);
 int gpmi_op_last_timing(gpmi_op* op, double* syrk_ms, int* syrk_launches,
-                        double* syrk_flops, double* total_ms);
+                        double* syrk_flops, double* total_ms, double* syrk_busy_ms);
+
+/* Split each batch into two halves factorized concurrently on two HIP streams
+ * (lanes = 2), so one half's latency-bound diagonal/panel chain overlaps the
+ * other half's trailing update. Default 1. */
+int gpmi_op_set_lanes(gpmi_op* op, int lanes);
 
 /* Outer panel width in 128-column sub-panels (trailing update depth = 128*S). */
 int gpmi_op_set_outer(gpmi_op* op, int s);
