@@ -310,6 +310,11 @@ int ensure_factor(gpmi_op* op, double eta, const double* rhs_dev, bool* fresh) {
 
 }  // namespace
 
+namespace gpmi {
+int matern_params_host(double nu, MaternParams* P);
+int set_error(int code, const char* msg) { return set_err(code, "%s", msg); }
+}  // namespace gpmi
+
 extern "C" {
 
 int gpmi_version(void) { return 100; }
@@ -336,6 +341,25 @@ static int matern_params(double nu, MaternParams* P) {
   else if (nu == 2.5) P->mode = MATERN_5HALF;
   else if (nu < 100) P->mode = MATERN_GENERAL;
   else P->mode = MATERN_GAUSS;
+  return 0;
+}
+
+int gpmi_matern_values(int device, const double* x, int64_t m, double nu, double* out) {
+  if (m <= 0) return 0;
+  MaternParams P;
+  int rc = matern_params(nu, &P);
+  if (rc) return rc;
+  DeviceGuard g(device);
+  double *dx = nullptr, *dv = nullptr;
+  HIP_TRY(hipMalloc(&dx, sizeof(double) * m));
+  HIP_TRY(hipMalloc(&dv, sizeof(double) * m));
+  HIP_TRY(hipMemcpy(dx, x, sizeof(double) * m, hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(matern_eval_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, 0, dx,
+                     m, P, dv);
+  LAUNCH_CHECK("matern_eval_kernel");
+  HIP_TRY(hipMemcpy(out, dv, sizeof(double) * m, hipMemcpyDeviceToHost));
+  HIP_TRY(hipFree(dx));
+  HIP_TRY(hipFree(dv));
   return 0;
 }
 
@@ -686,3 +710,7 @@ int gpmi_op_set_outer(gpmi_op* op, int s) {
 }
 
 }  // extern "C"
+
+namespace gpmi {
+int matern_params_host(double nu, MaternParams* P) { return matern_params(nu, P); }
+}  // namespace gpmi

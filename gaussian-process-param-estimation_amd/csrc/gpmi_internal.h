@@ -50,5 +50,6 @@ __global__ void gemv_sym_kernel(const double* K, int64_t ldk, int64_t n,
                                 const double* x, int64_t ldx, int ncol, double* y,
                                 double eta, int exponent);
 __global__ void trace_kernel(const double* K, int64_t ldk, int64_t n, double* out);
+__global__ void matern_eval_kernel(const double* x, int64_t m, MaternParams P, double* out);
 
 }  // namespace gpmi

@@ -1,0 +1,483 @@
+// C-ABI of the sparse path (include/gpmi.h, gpmi_sp_*): tapered Matérn CSR
+// assembly, SpMM, blocked Lanczos with full (CGS2) reorthogonalisation for
+// stochastic Lanczos quadrature, and blocked CG.
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "gpmi_internal.h"
+#include "../../include/gpmi.h"
+
+using namespace gpmi;
+
+namespace gpmi {
+__global__ void csr_count_kernel(const double*, int64_t, int, const double*, MaternParams, double,
+                                 double, int*);
+__global__ void csr_fill_kernel(const double*, int64_t, int, const double*, MaternParams, double,
+                                double, const int64_t*, int*, double*);
+__global__ void matern_eval_kernel(const double*, int64_t, MaternParams, double*);
+__global__ void csr_spmm_kernel(const int64_t*, const int*, const double*, int64_t, const double*,
+                                int64_t, double*, int64_t, int, int, double);
+__global__ void col_dot_partial_kernel(const double*, int64_t, const double*, int64_t, int,
+                                       double*);
+__global__ void col_dot_reduce_kernel(const double*, int, int, int, double*);
+__global__ void col_gs_update_kernel(double*, const double*, int64_t, const double*, int, int64_t,
+                                     int);
+__global__ void col_axpby_kernel(const double*, double*, const double*, const double*, int64_t,
+                                 int);
+__global__ void rademacher_kernel(double*, int64_t, int, unsigned long long, int, double);
+int matern_params_host(double nu, MaternParams* P);   // gpmi_api.hip
+int set_error(int code, const char* msg);             // gpmi_api.hip
+}  // namespace gpmi
+
+namespace {
+
+#define SP_TRY(expr)                                                                   \
+  do {                                                                                 \
+    hipError_t e_ = (expr);                                                            \
+    if (e_ != hipSuccess) {                                                            \
+      char b_[400];                                                                    \
+      snprintf(b_, sizeof(b_), "%s failed: %s", #expr, hipGetErrorString(e_));        \
+      return set_error(-(int)e_, b_);                                                  \
+    }                                                                                  \
+  } while (0)
+
+#define SP_LAUNCH(name)                                                                \
+  do {                                                                                 \
+    hipError_t e_ = hipGetLastError();                                                 \
+    if (e_ != hipSuccess) {                                                            \
+      char b_[400];                                                                    \
+      snprintf(b_, sizeof(b_), "launch of %s failed: %s", name, hipGetErrorString(e_)); \
+      return set_error(-(int)e_, b_);                                                  \
+    }                                                                                  \
+  } while (0)
+
+constexpr int NBLK = 256;   // fixed reduction grid (deterministic sums)
+constexpr int MAXS = 32;    // vector-block width per device pass
+
+struct Guard {
+  int prev = -1;
+  explicit Guard(int d) {
+    (void)hipGetDevice(&prev);
+    if (prev != d) (void)hipSetDevice(d);
+  }
+  ~Guard() {
+    int c = -1;
+    (void)hipGetDevice(&c);
+    if (prev >= 0 && c != prev) (void)hipSetDevice(prev);
+  }
+};
+
+int next_pow2(int s) {
+  int p = 1;
+  while (p < s) p <<= 1;
+  return p;
+}
+
+}  // namespace
+
+struct gpmi_sp {
+  int device = 0;
+  int64_t n = 0, nnz = 0;
+  double tau = 0.0;
+  hipStream_t stream = nullptr;
+  int64_t* indptr = nullptr;
+  int* indices = nullptr;
+  double* data = nullptr;
+  // workspace (grown on demand)
+  size_t ws_doubles = 0;
+  double* ws = nullptr;
+  double* partial = nullptr;   // [NBLK][J][s]
+  size_t partial_doubles = 0;
+  double* small = nullptr;     // coefficient / reduction arrays
+};
+
+namespace {
+
+int ensure_ws(gpmi_sp* sp, size_t doubles) {
+  if (sp->ws_doubles >= doubles) return 0;
+  if (sp->ws) SP_TRY(hipFree(sp->ws));
+  sp->ws = nullptr;
+  SP_TRY(hipMalloc(&sp->ws, sizeof(double) * doubles));
+  sp->ws_doubles = doubles;
+  return 0;
+}
+
+int ensure_partial(gpmi_sp* sp, size_t doubles) {
+  if (sp->partial_doubles >= doubles) return 0;
+  if (sp->partial) SP_TRY(hipFree(sp->partial));
+  sp->partial = nullptr;
+  SP_TRY(hipMalloc(&sp->partial, sizeof(double) * doubles));
+  sp->partial_doubles = doubles;
+  return 0;
+}
+
+int spmm(gpmi_sp* sp, const double* X, double* Y, int s, double eta) {
+  hipLaunchKernelGGL(csr_spmm_kernel, dim3((unsigned)((sp->n + 3) / 4)), dim3(256), 0,
+                     sp->stream, sp->indptr, sp->indices, sp->data, sp->n, X, (int64_t)s, Y,
+                     (int64_t)s, s, next_pow2(s), eta);
+  SP_LAUNCH("csr_spmm_kernel");
+  return 0;
+}
+
+// out[j][c] = sum_i A_j[i][c] B[i][c], j < J  (device out)
+int col_dots(gpmi_sp* sp, const double* A, int64_t strideA, int J, const double* B, int s,
+             double* out) {
+  int rc = ensure_partial(sp, (size_t)NBLK * J * s);
+  if (rc) return rc;
+  hipLaunchKernelGGL(col_dot_partial_kernel, dim3(NBLK, J), dim3(256), 0, sp->stream, A, strideA,
+                     B, sp->n, s, sp->partial);
+  SP_LAUNCH("col_dot_partial_kernel");
+  hipLaunchKernelGGL(col_dot_reduce_kernel, dim3((J * s + 255) / 256), dim3(256), 0, sp->stream,
+                     sp->partial, NBLK, J, s, out);
+  SP_LAUNCH("col_dot_reduce_kernel");
+  return 0;
+}
+
+unsigned grid_ns(int64_t n, int s) { return (unsigned)((n * s + 255) / 256); }
+
+// Lanczos of K on s probe columns starting from V0 (already in V block 0).
+// alpha/beta: host [s][steps] (column-major by probe). CGS2 reorthogonalisation.
+int lanczos_block(gpmi_sp* sp, double* V, double* W, int s, int steps, double* h_alpha,
+                  double* h_beta) {
+  const int64_t ns = sp->n * s;
+  double* H = sp->small;                 // [(steps+1)][s]
+  double* coefa = sp->small + (size_t)(steps + 2) * MAXS;
+  double* coefb = coefa + MAXS;
+  std::vector<double> hH((size_t)(steps + 1) * s), hnorm(s), ha(s), hb(s);
+  std::vector<double> beta_prev(s, 0.0);
+  std::vector<int> dead(s, 0);
+  for (int k = 0; k < steps; ++k) {
+    double* Vk = V + (int64_t)k * ns;
+    int rc = spmm(sp, Vk, W, s, 0.0);
+    if (rc) return rc;
+    if (k > 0) {
+      for (int c = 0; c < s; ++c) {
+        ha[c] = -beta_prev[c];
+        hb[c] = 1.0;
+      }
+      SP_TRY(hipMemcpyAsync(coefa, ha.data(), sizeof(double) * s, hipMemcpyHostToDevice,
+                            sp->stream));
+      SP_TRY(hipMemcpyAsync(coefb, hb.data(), sizeof(double) * s, hipMemcpyHostToDevice,
+                            sp->stream));
+      hipLaunchKernelGGL(col_axpby_kernel, dim3(grid_ns(sp->n, s)), dim3(256), 0, sp->stream,
+                         V + (int64_t)(k - 1) * ns, W, coefa, coefb, sp->n, s);
+      SP_LAUNCH("col_axpby_kernel");
+    }
+    double alpha_sum[MAXS] = {0};
+    for (int pass = 0; pass < 2; ++pass) {
+      rc = col_dots(sp, V, ns, k + 1, W, s, H);
+      if (rc) return rc;
+      hipLaunchKernelGGL(col_gs_update_kernel, dim3(grid_ns(sp->n, s)), dim3(256), 0, sp->stream,
+                         W, V, ns, H, k + 1, sp->n, s);
+      SP_LAUNCH("col_gs_update_kernel");
+      SP_TRY(hipMemcpyAsync(hH.data(), H + (size_t)k * s, sizeof(double) * s,
+                            hipMemcpyDeviceToHost, sp->stream));
+      SP_TRY(hipStreamSynchronize(sp->stream));
+      for (int c = 0; c < s; ++c) alpha_sum[c] += hH[c];
+    }
+    rc = col_dots(sp, W, 0, 1, W, s, H);
+    if (rc) return rc;
+    SP_TRY(hipMemcpyAsync(hnorm.data(), H, sizeof(double) * s, hipMemcpyDeviceToHost,
+                          sp->stream));
+    SP_TRY(hipStreamSynchronize(sp->stream));
+    for (int c = 0; c < s; ++c) {
+      const double a = dead[c] ? 0.0 : alpha_sum[c];
+      double b = dead[c] ? 0.0 : std::sqrt(std::max(hnorm[c], 0.0));
+      if (!dead[c] && !(b > 1e-13 * std::max(1.0, std::fabs(a)))) {
+        dead[c] = 1;   // invariant subspace reached: the rest of this column is padding
+        b = 0.0;
+      }
+      h_alpha[(size_t)c * steps + k] = a;
+      h_beta[(size_t)c * steps + k] = b;
+      beta_prev[c] = b;
+      ha[c] = b > 0.0 ? 1.0 / b : 0.0;
+      hb[c] = 0.0;
+    }
+    if (k + 1 < steps) {
+      // V_{k+1} = W / beta  (b = 0 -> X * 0 + 0 * Y; Y is zero-initialised below)
+      double* Vn = V + (int64_t)(k + 1) * ns;
+      SP_TRY(hipMemsetAsync(Vn, 0, sizeof(double) * ns, sp->stream));
+      SP_TRY(hipMemcpyAsync(coefa, ha.data(), sizeof(double) * s, hipMemcpyHostToDevice,
+                            sp->stream));
+      SP_TRY(hipMemcpyAsync(coefb, hb.data(), sizeof(double) * s, hipMemcpyHostToDevice,
+                            sp->stream));
+      hipLaunchKernelGGL(col_axpby_kernel, dim3(grid_ns(sp->n, s)), dim3(256), 0, sp->stream, W,
+                         Vn, coefa, coefb, sp->n, s);
+      SP_LAUNCH("col_axpby_kernel");
+    }
+  }
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gpmi_sp_create_csr(int device, int64_t n, const int64_t* indptr, const int* indices,
+                       const double* data, gpmi_sp** out) {
+  if (!out || n <= 0) return set_error(-1100, "invalid arguments");
+  Guard g(device);
+  gpmi_sp* sp = new gpmi_sp();
+  sp->device = device;
+  sp->n = n;
+  sp->nnz = indptr[n];
+  SP_TRY(hipStreamCreateWithFlags(&sp->stream, hipStreamNonBlocking));
+  SP_TRY(hipMalloc(&sp->indptr, sizeof(int64_t) * (n + 1)));
+  SP_TRY(hipMalloc(&sp->indices, sizeof(int) * std::max<int64_t>(1, sp->nnz)));
+  SP_TRY(hipMalloc(&sp->data, sizeof(double) * std::max<int64_t>(1, sp->nnz)));
+  SP_TRY(hipMalloc(&sp->small, sizeof(double) * 16384));
+  SP_TRY(hipMemcpy(sp->indptr, indptr, sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice));
+  SP_TRY(hipMemcpy(sp->indices, indices, sizeof(int) * sp->nnz, hipMemcpyHostToDevice));
+  SP_TRY(hipMemcpy(sp->data, data, sizeof(double) * sp->nnz, hipMemcpyHostToDevice));
+  *out = sp;
+  return 0;
+}
+
+int gpmi_sp_create_matern(int device, const double* points, int64_t n, int d,
+                          const double* scale, double nu, double tau, gpmi_sp** out) {
+  if (!out || n <= 0) return set_error(-1100, "invalid arguments");
+  if (d < 1 || d > GPMI_MAX_DIM) return set_error(-1003, "dimension outside [1, 8]");
+  MaternParams P;
+  int rc = matern_params_host(nu, &P);
+  if (rc) return rc;
+  Guard g(device);
+  gpmi_sp* sp = new gpmi_sp();
+  sp->device = device;
+  sp->n = n;
+  sp->tau = tau;
+  SP_TRY(hipStreamCreateWithFlags(&sp->stream, hipStreamNonBlocking));
+  SP_TRY(hipMalloc(&sp->small, sizeof(double) * 16384));
+  hipStream_t st = sp->stream;
+  // Scaled-distance cutoff: smallest grid x with matern(x) <= tau, with margin.
+  // matern is decreasing, so every pair beyond xcut has matern < tau.
+  const int M = 4096;
+  double xmax = 1.0, xcut = 0.0;
+  std::vector<double> hx(M), hv(M);
+  double* dx = sp->small;
+  double* dv = sp->small + M;
+  for (int it = 0; it < 60; ++it) {
+    for (int i = 0; i < M; ++i) hx[i] = xmax * (i + 1) / M;
+    SP_TRY(hipMemcpyAsync(dx, hx.data(), sizeof(double) * M, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(matern_eval_kernel, dim3(M / 256), dim3(256), 0, st, dx, (int64_t)M, P, dv);
+    SP_LAUNCH("matern_eval_kernel");
+    SP_TRY(hipMemcpyAsync(hv.data(), dv, sizeof(double) * M, hipMemcpyDeviceToHost, st));
+    SP_TRY(hipStreamSynchronize(st));
+    int first = -1;
+    for (int i = 0; i < M; ++i)
+      if (hv[i] <= tau) {
+        first = i;
+        break;
+      }
+    if (first >= 0) {
+      xcut = hx[first] * (1.0 + 1e-6) + xmax / M;
+      break;
+    }
+    xmax *= 2.0;
+  }
+  if (xcut == 0.0) return set_error(-1101, "taper threshold not reached (tau too small)");
+  double *dp = nullptr, *ds = nullptr;
+  int* dcnt = nullptr;
+  SP_TRY(hipMalloc(&dp, sizeof(double) * n * d));
+  SP_TRY(hipMalloc(&ds, sizeof(double) * d));
+  SP_TRY(hipMalloc(&dcnt, sizeof(int) * n));
+  SP_TRY(hipMemcpyAsync(dp, points, sizeof(double) * n * d, hipMemcpyHostToDevice, st));
+  SP_TRY(hipMemcpyAsync(ds, scale, sizeof(double) * d, hipMemcpyHostToDevice, st));
+  const unsigned grid = (unsigned)((n + 3) / 4);
+  hipLaunchKernelGGL(csr_count_kernel, dim3(grid), dim3(256), 0, st, dp, n, d, ds, P, tau, xcut,
+                     dcnt);
+  SP_LAUNCH("csr_count_kernel");
+  std::vector<int> cnt(n);
+  SP_TRY(hipMemcpyAsync(cnt.data(), dcnt, sizeof(int) * n, hipMemcpyDeviceToHost, st));
+  SP_TRY(hipStreamSynchronize(st));
+  std::vector<int64_t> ip(n + 1, 0);
+  for (int64_t i = 0; i < n; ++i) ip[i + 1] = ip[i] + cnt[i];
+  sp->nnz = ip[n];
+  SP_TRY(hipMalloc(&sp->indptr, sizeof(int64_t) * (n + 1)));
+  SP_TRY(hipMalloc(&sp->indices, sizeof(int) * std::max<int64_t>(1, sp->nnz)));
+  SP_TRY(hipMalloc(&sp->data, sizeof(double) * std::max<int64_t>(1, sp->nnz)));
+  SP_TRY(hipMemcpyAsync(sp->indptr, ip.data(), sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice,
+                        st));
+  hipLaunchKernelGGL(csr_fill_kernel, dim3(grid), dim3(256), 0, st, dp, n, d, ds, P, tau, xcut,
+                     sp->indptr, sp->indices, sp->data);
+  SP_LAUNCH("csr_fill_kernel");
+  SP_TRY(hipStreamSynchronize(st));
+  SP_TRY(hipFree(dp));
+  SP_TRY(hipFree(ds));
+  SP_TRY(hipFree(dcnt));
+  *out = sp;
+  return 0;
+}
+
+int gpmi_sp_destroy(gpmi_sp* sp) {
+  if (!sp) return 0;
+  Guard g(sp->device);
+  if (sp->stream) (void)hipStreamSynchronize(sp->stream);
+  if (sp->indptr) (void)hipFree(sp->indptr);
+  if (sp->indices) (void)hipFree(sp->indices);
+  if (sp->data) (void)hipFree(sp->data);
+  if (sp->ws) (void)hipFree(sp->ws);
+  if (sp->partial) (void)hipFree(sp->partial);
+  if (sp->small) (void)hipFree(sp->small);
+  if (sp->stream) (void)hipStreamDestroy(sp->stream);
+  delete sp;
+  return 0;
+}
+
+int gpmi_sp_info(const gpmi_sp* sp, int64_t* n, int64_t* nnz) {
+  if (!sp) return set_error(-1006, "null handle");
+  if (n) *n = sp->n;
+  if (nnz) *nnz = sp->nnz;
+  return 0;
+}
+
+int gpmi_sp_get_csr(gpmi_sp* sp, int64_t* indptr, int* indices, double* data) {
+  if (!sp) return set_error(-1006, "null handle");
+  Guard g(sp->device);
+  SP_TRY(hipMemcpy(indptr, sp->indptr, sizeof(int64_t) * (sp->n + 1), hipMemcpyDeviceToHost));
+  SP_TRY(hipMemcpy(indices, sp->indices, sizeof(int) * sp->nnz, hipMemcpyDeviceToHost));
+  SP_TRY(hipMemcpy(data, sp->data, sizeof(double) * sp->nnz, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int gpmi_sp_spmm(gpmi_sp* sp, double eta, const double* X, int64_t ld, int ncol, double* Y,
+                 int64_t ldy) {
+  if (!sp) return set_error(-1006, "null handle");
+  Guard g(sp->device);
+  const int64_t n = sp->n;
+  for (int c0 = 0; c0 < ncol; c0 += MAXS) {
+    const int s = std::min(MAXS, ncol - c0);
+    int rc = ensure_ws(sp, (size_t)2 * n * s);
+    if (rc) return rc;
+    std::vector<double> h((size_t)n * s);
+    for (int64_t i = 0; i < n; ++i)
+      for (int c = 0; c < s; ++c) h[(size_t)i * s + c] = X[i * ld + c0 + c];
+    SP_TRY(hipMemcpyAsync(sp->ws, h.data(), sizeof(double) * h.size(), hipMemcpyHostToDevice,
+                          sp->stream));
+    rc = spmm(sp, sp->ws, sp->ws + n * s, s, eta);
+    if (rc) return rc;
+    SP_TRY(hipMemcpyAsync(h.data(), sp->ws + n * s, sizeof(double) * h.size(),
+                          hipMemcpyDeviceToHost, sp->stream));
+    SP_TRY(hipStreamSynchronize(sp->stream));
+    for (int64_t i = 0; i < n; ++i)
+      for (int c = 0; c < s; ++c) Y[i * ldy + c0 + c] = h[(size_t)i * s + c];
+  }
+  return 0;
+}
+
+int gpmi_sp_lanczos(gpmi_sp* sp, int nprobe, int steps, uint64_t seed, int probe_offset,
+                    double* alpha, double* beta) {
+  if (!sp) return set_error(-1006, "null handle");
+  if (steps < 1 || steps > 256 || nprobe < 1)
+    return set_error(-1102, "steps must be in [1, 256] and nprobe >= 1");
+  Guard g(sp->device);
+  const int64_t n = sp->n;
+  for (int p0 = 0; p0 < nprobe; p0 += MAXS) {
+    const int s = std::min(MAXS, nprobe - p0);
+    int rc = ensure_ws(sp, (size_t)(steps + 2) * n * s);
+    if (rc) return rc;
+    double* V = sp->ws;
+    double* W = sp->ws + (size_t)(steps + 1) * n * s;
+    hipLaunchKernelGGL(rademacher_kernel, dim3(grid_ns(n, s)), dim3(256), 0, sp->stream, V, n, s,
+                       (unsigned long long)seed, probe_offset + p0, 1.0 / std::sqrt((double)n));
+    SP_LAUNCH("rademacher_kernel");
+    rc = lanczos_block(sp, V, W, s, steps, alpha + (size_t)p0 * steps, beta + (size_t)p0 * steps);
+    if (rc) return rc;
+  }
+  return 0;
+}
+
+int gpmi_sp_cg(gpmi_sp* sp, double eta, const double* rhs, int64_t ld, int nrhs, double rtol,
+               int maxiter, double* sol, int64_t ldsol, int* iterations) {
+  if (!sp) return set_error(-1006, "null handle");
+  Guard g(sp->device);
+  const int64_t n = sp->n;
+  int max_it_used = 0;
+  for (int c0 = 0; c0 < nrhs; c0 += MAXS) {
+    const int s = std::min(MAXS, nrhs - c0);
+    const int64_t ns = n * s;
+    int rc = ensure_ws(sp, (size_t)4 * ns);
+    if (rc) return rc;
+    double* X = sp->ws;
+    double* Rr = X + ns;
+    double* Pp = Rr + ns;
+    double* Q = Pp + ns;
+    double* dots = sp->small;
+    double* ca = sp->small + 2 * MAXS;
+    double* cb = ca + MAXS;
+    std::vector<double> h((size_t)ns);
+    for (int64_t i = 0; i < n; ++i)
+      for (int c = 0; c < s; ++c) h[(size_t)i * s + c] = rhs[i * ld + c0 + c];
+    SP_TRY(hipMemcpyAsync(Rr, h.data(), sizeof(double) * ns, hipMemcpyHostToDevice, sp->stream));
+    SP_TRY(hipMemcpyAsync(Pp, Rr, sizeof(double) * ns, hipMemcpyDeviceToDevice, sp->stream));
+    SP_TRY(hipMemsetAsync(X, 0, sizeof(double) * ns, sp->stream));
+    std::vector<double> rr(s), bn(s), pq(s), rrn(s), ha(s), hb(s);
+    rc = col_dots(sp, Rr, 0, 1, Rr, s, dots);
+    if (rc) return rc;
+    SP_TRY(hipMemcpyAsync(rr.data(), dots, sizeof(double) * s, hipMemcpyDeviceToHost, sp->stream));
+    SP_TRY(hipStreamSynchronize(sp->stream));
+    for (int c = 0; c < s; ++c) bn[c] = std::sqrt(rr[c]);
+    std::vector<int> done(s, 0);
+    int it = 0;
+    for (; it < maxiter; ++it) {
+      bool all = true;
+      for (int c = 0; c < s; ++c) {
+        if (!(std::sqrt(rr[c]) > rtol * bn[c])) done[c] = 1;
+        all = all && done[c];
+      }
+      if (all) break;
+      rc = spmm(sp, Pp, Q, s, eta);
+      if (rc) return rc;
+      rc = col_dots(sp, Pp, 0, 1, Q, s, dots);
+      if (rc) return rc;
+      SP_TRY(hipMemcpyAsync(pq.data(), dots, sizeof(double) * s, hipMemcpyDeviceToHost,
+                            sp->stream));
+      SP_TRY(hipStreamSynchronize(sp->stream));
+      for (int c = 0; c < s; ++c) {
+        const double a = done[c] ? 0.0 : rr[c] / pq[c];
+        ha[c] = a;
+        hb[c] = 1.0;
+      }
+      SP_TRY(hipMemcpyAsync(ca, ha.data(), sizeof(double) * s, hipMemcpyHostToDevice, sp->stream));
+      SP_TRY(hipMemcpyAsync(cb, hb.data(), sizeof(double) * s, hipMemcpyHostToDevice, sp->stream));
+      hipLaunchKernelGGL(col_axpby_kernel, dim3(grid_ns(n, s)), dim3(256), 0, sp->stream, Pp, X, ca,
+                         cb, n, s);   // x += a p
+      SP_LAUNCH("col_axpby_kernel");
+      for (int c = 0; c < s; ++c) ha[c] = -ha[c];
+      SP_TRY(hipMemcpyAsync(ca, ha.data(), sizeof(double) * s, hipMemcpyHostToDevice, sp->stream));
+      hipLaunchKernelGGL(col_axpby_kernel, dim3(grid_ns(n, s)), dim3(256), 0, sp->stream, Q, Rr, ca,
+                         cb, n, s);   // r -= a q
+      SP_LAUNCH("col_axpby_kernel");
+      rc = col_dots(sp, Rr, 0, 1, Rr, s, dots);
+      if (rc) return rc;
+      SP_TRY(hipMemcpyAsync(rrn.data(), dots, sizeof(double) * s, hipMemcpyDeviceToHost,
+                            sp->stream));
+      SP_TRY(hipStreamSynchronize(sp->stream));
+      for (int c = 0; c < s; ++c) {
+        ha[c] = 1.0;
+        hb[c] = done[c] ? 1.0 : rrn[c] / rr[c];
+        if (!done[c]) rr[c] = rrn[c];
+      }
+      SP_TRY(hipMemcpyAsync(ca, ha.data(), sizeof(double) * s, hipMemcpyHostToDevice, sp->stream));
+      SP_TRY(hipMemcpyAsync(cb, hb.data(), sizeof(double) * s, hipMemcpyHostToDevice, sp->stream));
+      hipLaunchKernelGGL(col_axpby_kernel, dim3(grid_ns(n, s)), dim3(256), 0, sp->stream, Rr, Pp, ca,
+                         cb, n, s);   // p = r + b p
+      SP_LAUNCH("col_axpby_kernel");
+    }
+    max_it_used = std::max(max_it_used, it);
+    SP_TRY(hipMemcpyAsync(h.data(), X, sizeof(double) * ns, hipMemcpyDeviceToHost, sp->stream));
+    SP_TRY(hipStreamSynchronize(sp->stream));
+    for (int64_t i = 0; i < n; ++i)
+      for (int c = 0; c < s; ++c) sol[i * ldsol + c0 + c] = h[(size_t)i * s + c];
+  }
+  if (iterations) *iterations = max_it_used;
+  return 0;
+}
+
+}  // extern "C"

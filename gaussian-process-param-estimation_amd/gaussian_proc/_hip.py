@@ -51,6 +51,22 @@ SIGNATURES = {
                                            c_double_p, c_double_p]),
     'gpmi_op_set_lanes': (ctypes.c_int, [c_op_p, ctypes.c_int]),
     'gpmi_op_set_outer': (ctypes.c_int, [c_op_p, ctypes.c_int]),
+    'gpmi_matern_values': (ctypes.c_int, [ctypes.c_int, c_double_p, c_i64, ctypes.c_double,
+                                          c_double_p]),
+    'gpmi_sp_create_matern': (ctypes.c_int, [ctypes.c_int, c_double_p, c_i64, ctypes.c_int,
+                                             c_double_p, ctypes.c_double, ctypes.c_double,
+                                             ctypes.POINTER(c_op_p)]),
+    'gpmi_sp_create_csr': (ctypes.c_int, [ctypes.c_int, c_i64, ctypes.POINTER(c_i64),
+                                          c_int_p, c_double_p, ctypes.POINTER(c_op_p)]),
+    'gpmi_sp_destroy': (ctypes.c_int, [c_op_p]),
+    'gpmi_sp_info': (ctypes.c_int, [c_op_p, ctypes.POINTER(c_i64), ctypes.POINTER(c_i64)]),
+    'gpmi_sp_get_csr': (ctypes.c_int, [c_op_p, ctypes.POINTER(c_i64), c_int_p, c_double_p]),
+    'gpmi_sp_spmm': (ctypes.c_int, [c_op_p, ctypes.c_double, c_double_p, c_i64, ctypes.c_int,
+                                    c_double_p, c_i64]),
+    'gpmi_sp_lanczos': (ctypes.c_int, [c_op_p, ctypes.c_int, ctypes.c_int, ctypes.c_uint64,
+                                       ctypes.c_int, c_double_p, c_double_p]),
+    'gpmi_sp_cg': (ctypes.c_int, [c_op_p, ctypes.c_double, c_double_p, c_i64, ctypes.c_int,
+                                  ctypes.c_double, ctypes.c_int, c_double_p, c_i64, c_int_p]),
 }
 
 
@@ -249,3 +265,105 @@ def matern_dense(points, scale, nu, device=None):
     check(lib.gpmi_matern_dense(device, dptr(points), n, d, dptr(scale), float(nu), dptr(K),
                                 n), 'gpmi_matern_dense')
     return K
+
+
+def matern_values(x, nu, device=None):
+    """matern(x) evaluated by the device kernel (used for the taper threshold)."""
+    lib = load()
+    device = default_device() if device is None else int(device)
+    require_device(device)
+    x = as_c(numpy.atleast_1d(x))
+    out = numpy.empty_like(x)
+    check(lib.gpmi_matern_values(device, dptr(x), x.size, float(nu), dptr(out)),
+          'gpmi_matern_values')
+    return out
+
+
+class SparseOperator(object):
+    """Owning wrapper of a ``gpmi_sp`` handle (device CSR + Krylov workspace)."""
+
+    def __init__(self, handle, device):
+        self.lib = load()
+        self.h = handle
+        self.device = device
+        n = c_i64()
+        nnz = c_i64()
+        check(self.lib.gpmi_sp_info(self.h, ctypes.byref(n), ctypes.byref(nnz)), 'gpmi_sp_info')
+        self.n, self.nnz = n.value, nnz.value
+
+    @classmethod
+    def from_points(cls, points, scale, nu, tau, device=None):
+        lib = load()
+        device = default_device() if device is None else int(device)
+        require_device(device)
+        points = as_c(points)
+        scale = as_c(scale)
+        h = c_op_p()
+        check(lib.gpmi_sp_create_matern(device, dptr(points), points.shape[0], points.shape[1],
+                                        dptr(scale), float(nu), float(tau), ctypes.byref(h)),
+              'gpmi_sp_create_matern')
+        return cls(h, device)
+
+    @classmethod
+    def from_csr(cls, K, device=None):
+        lib = load()
+        device = default_device() if device is None else int(device)
+        require_device(device)
+        K = K.tocsr()
+        K.sort_indices()
+        ip = numpy.ascontiguousarray(K.indptr, dtype=numpy.int64)
+        ix = numpy.ascontiguousarray(K.indices, dtype=numpy.int32)
+        dv = as_c(K.data)
+        h = c_op_p()
+        check(lib.gpmi_sp_create_csr(device, K.shape[0], ip.ctypes.data_as(ctypes.POINTER(c_i64)),
+                                     ix.ctypes.data_as(c_int_p), dptr(dv), ctypes.byref(h)),
+              'gpmi_sp_create_csr')
+        return cls(h, device)
+
+    def close(self):
+        if getattr(self, 'h', None) is not None and self.h.value:
+            self.lib.gpmi_sp_destroy(self.h)
+            self.h = c_op_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def csr(self):
+        import scipy.sparse
+        ip = numpy.empty(self.n + 1, dtype=numpy.int64)
+        ix = numpy.empty(self.nnz, dtype=numpy.int32)
+        dv = numpy.empty(self.nnz)
+        check(self.lib.gpmi_sp_get_csr(self.h, ip.ctypes.data_as(ctypes.POINTER(c_i64)),
+                                       ix.ctypes.data_as(c_int_p), dptr(dv)), 'gpmi_sp_get_csr')
+        return scipy.sparse.csr_matrix((dv, ix, ip), shape=(self.n, self.n))
+
+    def spmm(self, eta, X):
+        X = as_c(X)
+        X2 = X[:, None] if X.ndim == 1 else X
+        Y = numpy.empty_like(X2)
+        check(self.lib.gpmi_sp_spmm(self.h, float(eta), dptr(X2), X2.shape[1], X2.shape[1],
+                                    dptr(Y), Y.shape[1]), 'gpmi_sp_spmm')
+        return Y[:, 0] if X.ndim == 1 else Y
+
+    def lanczos(self, nprobe, steps, seed=0, probe_offset=0):
+        """-> alpha[nprobe, steps], beta[nprobe, steps] (beta = 0 ends a tridiagonal)."""
+        a = numpy.zeros((nprobe, steps))
+        b = numpy.zeros((nprobe, steps))
+        check(self.lib.gpmi_sp_lanczos(self.h, int(nprobe), int(steps), int(seed),
+                                       int(probe_offset), dptr(a), dptr(b)), 'gpmi_sp_lanczos')
+        return a, b
+
+    def cg(self, eta, B, rtol=1e-6, maxiter=None):
+        B = as_c(B)
+        B2 = B[:, None] if B.ndim == 1 else B
+        X = numpy.empty_like(B2)
+        it = ctypes.c_int(0)
+        maxiter = 10 * self.n if maxiter is None else int(maxiter)
+        check(self.lib.gpmi_sp_cg(self.h, float(eta), dptr(B2), B2.shape[1], B2.shape[1],
+                                  float(rtol), maxiter, dptr(X), X.shape[1], ctypes.byref(it)),
+              'gpmi_sp_cg')
+        self.last_cg_iterations = it.value
+        return X[:, 0] if B.ndim == 1 else X

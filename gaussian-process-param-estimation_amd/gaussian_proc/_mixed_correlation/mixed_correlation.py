@@ -20,9 +20,12 @@ K + eta I is not positive definite (scipy's posv behaviour).
 """
 
 import numpy
+import scipy.sparse
 
 from .. import _hip
-from ..generate_correlation.generate_correlation import DeviceCorrelation
+from .. import _slq
+from ..generate_correlation.generate_correlation import DeviceCorrelation, \
+    DeviceSparseCorrelation
 
 __all__ = ['MixedCorrelation']
 
@@ -43,6 +46,10 @@ class MixedCorrelation(object):
                 raise TypeError('When "interpolate" is set to "True", the '
                                 '"interpolant_points" cannot be None.')
             raise NotImplementedError('traceinv interpolation is not implemented yet')
+        self.sparse = False
+        if isinstance(K, DeviceSparseCorrelation) or scipy.sparse.issparse(K):
+            self._init_sparse(K, device)
+            return
         if isinstance(K, DeviceCorrelation):
             if max_batch is not None and max_batch > K.op.max_batch:
                 raise ValueError('DeviceCorrelation was created with max_batch=%d'
@@ -62,12 +69,65 @@ class MixedCorrelation(object):
         self._trace_cache = None
         self._rhs_cache = None
 
+    # ---- sparse K (tapered Matérn, CSR on the device) -------------------------
+
+    def _init_sparse(self, K, device):
+        """Sparse K: logdet / traceinv by stochastic Lanczos quadrature
+        ('slq'; one device Lanczos run per probe, cached, serves every eta) or
+        Hutchinson ('hutchinson' traceinv, CG solves); solve by blocked CG with
+        the reference's tolerance (_linear_solver.py:24,57-68: rtol 1e-6)."""
+        self.sparse = True
+        if isinstance(K, DeviceSparseCorrelation):
+            self.K = K
+            self.sop = K.op
+        else:
+            self.K = K.tocsr()
+            self.sop = _hip.SparseOperator.from_csr(self.K, device=device)
+        self.n = self.sop.n
+        self.op = None
+        self._trace_cache = None
+        self._rhs_cache = None
+        opts = dict(self.imate_options or {})
+        self.num_samples = int(opts.get('num_samples', opts.get('max_num_samples', 20)))
+        self.lanczos_degree = int(opts.get('lanczos_degree', 30))
+        self.seed = int(opts.get('seed', 0))
+        self.cg_rtol = float(opts.get('cg_rtol', 1e-6))
+        self._nodes = None
+
+    def slq_nodes(self):
+        """Ritz nodes of every probe (computed once; eta-independent)."""
+        if self._nodes is None:
+            a, b = self.sop.lanczos(self.num_samples, self.lanczos_degree, self.seed)
+            self._nodes = _slq.nodes(a, b)
+        return self._nodes
+
+    def _slq(self, eta, what):
+        q = _slq.quadrature(self.slq_nodes(), [eta], _slq.FUNCS[what])
+        return float(self.n * q[:, 0].mean())
+
+    def _sparse_traces(self):
+        if self._trace_cache is None:
+            Kc = self.sop.csr()
+            self._trace_cache = (float(Kc.diagonal().sum()), float(numpy.sum(Kc.data ** 2)))
+        return self._trace_cache
+
+    def _sparse_method(self, allowed):
+        if self.imate_method not in allowed:
+            if self.imate_method in _METHODS:
+                raise NotImplementedError(
+                    'imate_method %r on a sparse K needs a sparse direct factorization '
+                    '(not implemented); use "slq"' % self.imate_method)
+            raise ValueError('Existing methods are "eigenvalue", "cholesky", '
+                             '"hutchinson", and "slq".')
+
     # ---- reference duck type -------------------------------------------------
 
     def get_matrix_size(self):                                     # :85-90
         return self.n
 
     def _traces(self):
+        if self.sparse:
+            return self._sparse_traces()
         if self._trace_cache is None:
             self._trace_cache = self.op.trace()
         return self._trace_cache
@@ -91,6 +151,17 @@ class MixedCorrelation(object):
         raise ValueError('Existing methods are "exact", "eigenvalue", and "slq".')
 
     def traceinv(self, eta, exponent=1):                           # :155-215
+        if self.sparse:
+            self._sparse_method(('slq', 'hutchinson'))
+            if self.imate_method == 'slq' and exponent in (1, 2):
+                return self._slq(eta, 'traceinv' if exponent == 1 else 'traceinv2')
+            if self.imate_method == 'hutchinson' and exponent in (1, 2):
+                V = _slq.rademacher(self.n, self.num_samples, self.seed)
+                W = self.sop.cg(eta, V, rtol=self.cg_rtol)
+                if exponent == 1:
+                    return float(numpy.sum(V * W) / self.num_samples)
+                return float(numpy.sum(W * W) / self.num_samples)
+            raise NotImplementedError('sparse traceinv with exponent %r' % exponent)
         if self.imate_method not in ('eigenvalue', 'cholesky'):
             if self.imate_method in _METHODS:
                 raise NotImplementedError('stochastic traceinv (%s) is not implemented yet'
@@ -106,6 +177,9 @@ class MixedCorrelation(object):
         return float(numpy.trace(numpy.linalg.matrix_power(Ainv, exponent)))
 
     def logdet(self, eta, exponent=1):                             # :221-274
+        if self.sparse:
+            self._sparse_method(('slq',))
+            return exponent * self._slq(eta, 'logdet')
         if self.imate_method not in ('eigenvalue', 'cholesky', 'hutchinson'):
             if self.imate_method == 'slq':
                 raise NotImplementedError('slq logdet is not implemented yet')
@@ -114,6 +188,8 @@ class MixedCorrelation(object):
         return exponent * self.op.logdet(eta)
 
     def solve(self, eta, Y):                                       # :280-299
+        if self.sparse:
+            return self.sop.cg(eta, Y, rtol=self.cg_rtol)
         return self.op.solve(eta, Y)
 
     def dot(self, eta, x, exponent=1):                             # :305-335
@@ -124,7 +200,7 @@ class MixedCorrelation(object):
         y = numpy.zeros_like(x, dtype=float)
         if exponent == 0:
             return y
-        Kx = self.op.matvec(x)
+        Kx = self.sop.spmm(0.0, x) if self.sparse else self.op.matvec(x)
         for _ in range(exponent):
             y += Kx
             if eta != 0:
@@ -150,8 +226,15 @@ class MixedCorrelation(object):
         """For each eta: logdet(K + eta I) and G = [X z]^T (K + eta I)^-1 [X z]
         from ONE Cholesky per eta, batched over up to ``max_batch`` etas per
         device call. Returns (logdet[neta], G[neta, m+1, m+1])."""
-        self.set_rhs(X, z)
         etas = numpy.atleast_1d(numpy.asarray(etas, dtype=float))
+        if self.sparse:
+            R = numpy.column_stack([numpy.asarray(X, dtype=float), numpy.asarray(z, dtype=float)])
+            lds, gs = [], []
+            for e in etas:
+                lds.append(self.logdet(e))
+                gs.append(R.T @ self.sop.cg(e, R, rtol=self.cg_rtol))
+            return numpy.array(lds), numpy.array(gs)
+        self.set_rhs(X, z)
         lds, gs = [], []
         mb = self.op.max_batch
         for i in range(0, etas.size, mb):

@@ -16,7 +16,7 @@ import numpy
 
 from .. import _hip
 
-__all__ = ['generate_correlation', 'DeviceCorrelation']
+__all__ = ['generate_correlation', 'DeviceCorrelation', 'DeviceSparseCorrelation']
 
 
 class DeviceCorrelation(object):
@@ -40,6 +40,33 @@ class DeviceCorrelation(object):
         return self.op.get_matrix()
 
 
+class DeviceSparseCorrelation(object):
+    """A tapered (compact-support) Matérn correlation kept on one GPU in CSR:
+    the entries with matern(x_ij) > tau, tau from the reference's density
+    heuristic (``generate_correlation(..., sparse=True)``)."""
+
+    def __init__(self, points, correlation_scale, nu, density, device=None):
+        from . import _taper
+        self.points = _hip.as_c(points)
+        self.correlation_scale = _hip.as_c(correlation_scale)
+        self.nu = float(nu)
+        self.density = float(density)
+        n, d = self.points.shape
+        self.shape = (n, n)
+        self.tau = _taper.kernel_threshold(n, d, density, self.correlation_scale, nu,
+                                           device=device)
+        self.op = _hip.SparseOperator.from_points(self.points, self.correlation_scale, self.nu,
+                                                  self.tau, device=device)
+        self.nnz = self.op.nnz
+
+    @property
+    def device(self):
+        return self.op.device
+
+    def tocsr(self):
+        return self.op.csr()
+
+
 def _broadcast_scale(points, correlation_scale):
     # generate_correlation.py:191-196
     if numpy.isscalar(correlation_scale):
@@ -56,17 +83,22 @@ def generate_correlation(points, correlation_scale=0.1, nu=0.5, grid=True, spars
                          device_resident=False, max_batch=1):
     """Matérn correlation matrix of ``points`` (n x d, d <= 8).
 
-    ``grid``, ``density`` and ``plot`` are accepted for signature parity; ``grid``
-    does not change the result in the reference either (the points are given).
+    Dense: ``numpy.ndarray`` (n, n). ``sparse=True``: the tapered matrix as a
+    ``scipy.sparse.csr_matrix`` (sorted indices), entries with
+    matern(x_ij) > tau where tau follows the reference's ``density`` heuristic
+    (_generate_sparse_correlation.pyx:294-413, with the argument fixes of
+    SURVEY §0.4). ``grid`` and ``plot`` are accepted for signature parity.
     """
     points = numpy.ascontiguousarray(points, dtype=float)
     if points.ndim != 2:
         raise ValueError('points must be a 2D array (num_points, dimension)')
     scale = _broadcast_scale(points, correlation_scale)
     if sparse:
-        raise NotImplementedError(
-            'sparse (tapered) correlation is not implemented on the device yet '
-            '(reference: _generate_sparse_correlation.pyx, see DESIGN.md "next")')
+        K = DeviceSparseCorrelation(points, scale, nu, density, device=device)
+        if verbose:
+            print('Generated sparse correlation matrix of size: %d, nnz: %d, density: %s.'
+                  % (points.shape[0], K.nnz, K.nnz / float(points.shape[0]) ** 2))
+        return K if device_resident else K.tocsr()
     if device_resident:
         K = DeviceCorrelation(points, scale, nu, device=device, max_batch=max_batch)
     else:

@@ -112,6 +112,47 @@ int gpmi_op_set_lanes(gpmi_op* op, int lanes);
 /* Outer panel width in 128-column sub-panels (trailing update depth = 128*S). */
 int gpmi_op_set_outer(gpmi_op* op, int s);
 
+/* ------------------------------------------------------------------ sparse --
+ * Tapered (compact-support) Matérn correlation in CSR on the device, and the
+ * Krylov primitives of the sparse likelihood path. Replaces
+ *   generate_correlation(sparse=True)  -> _generate_sparse_correlation.pyx:472-594
+ *     (with the two argument fixes of SURVEY §0.4; the threshold heuristic
+ *      :294-465 runs on the host, gaussian_proc/generate_correlation)
+ *   MixedCorrelation.logdet / traceinv with imate 'slq'
+ *     (mixed_correlation.py:138-143,204-209,263-268)
+ *   linear_solver for sparse A: scipy.sparse.linalg.cg (_linear_solver.py:57-68).
+ */
+typedef struct gpmi_sp gpmi_sp;
+
+/* matern(x_i) for m scaled distances (the device kernel the assembly uses). */
+int gpmi_matern_values(int device, const double* x, int64_t m, double nu, double* out);
+
+/* CSR of the entries with matern(x_ij) > tau (x_ij the scaled distance), sorted
+ * columns, deterministic; int64 row pointers, int32 columns. */
+int gpmi_sp_create_matern(int device, const double* points, int64_t n, int d,
+                          const double* scale, double nu, double tau, gpmi_sp** out);
+/* From a host CSR (indptr[n+1] int64, indices int32, data fp64). */
+int gpmi_sp_create_csr(int device, int64_t n, const int64_t* indptr, const int* indices,
+                       const double* data, gpmi_sp** out);
+int gpmi_sp_destroy(gpmi_sp* sp);
+int gpmi_sp_info(const gpmi_sp* sp, int64_t* n, int64_t* nnz);
+int gpmi_sp_get_csr(gpmi_sp* sp, int64_t* indptr, int* indices, double* data);
+
+/* Y = (K + eta I) X for an [n][ld] host block with ncol columns. */
+int gpmi_sp_spmm(gpmi_sp* sp, double eta, const double* X, int64_t ld, int ncol, double* Y,
+                 int64_t ldy);
+
+/* Lanczos tridiagonals of K for nprobe Rademacher probes (counter-based,
+ * probe index probe_offset + p, seed), full CGS2 reorthogonalisation.
+ * alpha, beta: [nprobe][steps]; a column that reaches an invariant subspace is
+ * padded with zeros (beta = 0 marks the end of its tridiagonal). */
+int gpmi_sp_lanczos(gpmi_sp* sp, int nprobe, int steps, uint64_t seed, int probe_offset,
+                    double* alpha, double* beta);
+
+/* Blocked CG for (K + eta I) X = RHS, per-column stop ||r|| <= rtol ||b||. */
+int gpmi_sp_cg(gpmi_sp* sp, double eta, const double* rhs, int64_t ld, int nrhs, double rtol,
+               int maxiter, double* sol, int64_t ldsol, int* iterations);
+
 #ifdef __cplusplus
 }
 #endif

@@ -44,6 +44,23 @@ def build_reference():
     os.makedirs(pkg_dst)
     shutil.copytree(os.path.join(REF, 'gaussian_proc'),
                     os.path.join(pkg_dst, 'gaussian_proc'))
+    # The shipped sparse generator raises TypeError before doing any work
+    # (SURVEY §0.4). Apply the two argument fixes to the SCRATCH copy only:
+    #   :390  _ball_volume(geometric_mean_radius) -> (..., dimension)
+    #   :542  _estimate_max_nnz(matrix_size, dimension, density)
+    #         -> (matrix_size, correlation_scale, dimension, density)
+    sp = os.path.join(pkg_dst, 'gaussian_proc', 'generate_correlation',
+                      '_generate_sparse_correlation.pyx')
+    src = open(sp).read()
+    a = '_ball_volume(geometric_mean_radius)'
+    assert src.count(a) == 1
+    src = src.replace(a, '_ball_volume(geometric_mean_radius, dimension)')
+    import re
+    m = re.search(r'max_nnz = _estimate_max_nnz\(\s*matrix_size,\s*dimension,\s*density\)', src)
+    assert m, 'estimate_max_nnz call site not found'
+    src = src[:m.start()] + ('max_nnz = _estimate_max_nnz(matrix_size, correlation_scale, '
+                             'dimension, density)') + src[m.end():]
+    open(sp, 'w').write(src)
     setup_py = textwrap.dedent('''
         from setuptools import setup, Extension
         from Cython.Build import cythonize
@@ -204,6 +221,34 @@ def matern_cases(R):
     return meta, arrays
 
 
+def sparse_cases(R, big=False):
+    """Tapered (sparse) Matérn from the reference generator + 2 arg fixes."""
+    gp = R['gp']
+    du = R['du']
+    cases = [('sp2d_n1024', 32, 2, 0.05, 1.5, 0.02), ('sp3d_n1000', 10, 3, 0.1, 1.5, 0.03),
+             ('sp2d_n4096_nu05', 64, 2, 0.02, 0.5, 0.005)]
+    if big:
+        cases.append(('sp2d_n65536_cfg4', 256, 2, 0.005, 1.5, 1e-3))
+    meta, arrays = [], {}
+    import io
+    import contextlib
+    for name, npts, d, rho, nu, dens in cases:
+        pts = du.generate_points(npts, d, True)
+        with contextlib.redirect_stdout(io.StringIO()):
+            K = gp.generate_correlation(pts, rho, nu, True, sparse=True, density=dens)
+        K = K.tocsr()
+        K.sort_indices()
+        meta.append(dict(name=name, num_points=npts, dimension=d, correlation_scale=rho,
+                         nu=nu, density=dens, n=K.shape[0], nnz=int(K.nnz),
+                         data_sum=float(K.data.sum()), min_kept=float(K.data.min()),
+                         note='reference + 2 arg fixes (SURVEY 0.4)'))
+        if K.shape[0] <= 4096:
+            arrays[name + '_indptr'] = K.indptr.astype(numpy.int64)
+            arrays[name + '_indices'] = K.indices.astype(numpy.int64)
+            arrays[name + '_data'] = K.data
+    return meta, arrays
+
+
 def big_case(R):
     """N=16384 (2D 128x128 grid, nu=1.5): 'cholesky' imate method (3 dense
     factorizations per lp) — the eigenvalue method needs a 227 s eigh."""
@@ -226,8 +271,16 @@ def big_case(R):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--big', action='store_true', help='also the N=16384 case (~5 min)')
+    ap.add_argument('--sparse-only', action='store_true')
+    ap.add_argument('--sparse-big', action='store_true', help='also config 4 (~5 min)')
     args = ap.parse_args()
     R = import_reference()
+    smeta, sarr = sparse_cases(R, args.sparse_big)
+    numpy.savez_compressed(os.path.join(HERE, 'sparse_small.npz'), **sarr)
+    with open(os.path.join(HERE, 'sparse.json'), 'w') as fh:
+        json.dump(smeta, fh, indent=1)
+    if args.sparse_only:
+        return
     meta, arr = matern_cases(R)
     numpy.savez_compressed(os.path.join(HERE, 'matern_small.npz'), **arr)
     with open(os.path.join(HERE, 'matern_small.json'), 'w') as fh:
