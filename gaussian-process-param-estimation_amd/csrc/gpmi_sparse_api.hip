@@ -480,4 +480,34 @@ int gpmi_sp_cg(gpmi_sp* sp, double eta, const double* rhs, int64_t ld, int nrhs,
   return 0;
 }
 
+int gpmi_sp_bench_spmm(gpmi_sp* sp, int s, int reps, double eta, double* avg_ms) {
+  if (!sp) return set_error(-1006, "null handle");
+  if (s < 1 || s > 64 || reps < 1) return set_error(-1103, "s in [1, 64], reps >= 1");
+  Guard g(sp->device);
+  const int64_t ns = sp->n * s;
+  int rc = ensure_ws(sp, (size_t)2 * ns);
+  if (rc) return rc;
+  hipLaunchKernelGGL(rademacher_kernel, dim3(grid_ns(sp->n, s)), dim3(256), 0, sp->stream, sp->ws,
+                     sp->n, s, 12345ull, 0, 1.0);
+  SP_LAUNCH("rademacher_kernel");
+  hipEvent_t e0, e1;
+  SP_TRY(hipEventCreate(&e0));
+  SP_TRY(hipEventCreate(&e1));
+  rc = spmm(sp, sp->ws, sp->ws + ns, s, eta);   // warm-up
+  if (rc) return rc;
+  SP_TRY(hipEventRecord(e0, sp->stream));
+  for (int r = 0; r < reps; ++r) {
+    rc = spmm(sp, sp->ws, sp->ws + ns, s, eta);
+    if (rc) return rc;
+  }
+  SP_TRY(hipEventRecord(e1, sp->stream));
+  SP_TRY(hipEventSynchronize(e1));
+  float ms = 0.f;
+  SP_TRY(hipEventElapsedTime(&ms, e0, e1));
+  *avg_ms = ms / reps;
+  SP_TRY(hipEventDestroy(e0));
+  SP_TRY(hipEventDestroy(e1));
+  return 0;
+}
+
 }  // extern "C"

@@ -65,6 +65,8 @@ SIGNATURES = {
                                     c_double_p, c_i64]),
     'gpmi_sp_lanczos': (ctypes.c_int, [c_op_p, ctypes.c_int, ctypes.c_int, ctypes.c_uint64,
                                        ctypes.c_int, c_double_p, c_double_p]),
+    'gpmi_sp_bench_spmm': (ctypes.c_int, [c_op_p, ctypes.c_int, ctypes.c_int, ctypes.c_double,
+                                          c_double_p]),
     'gpmi_sp_cg': (ctypes.c_int, [c_op_p, ctypes.c_double, c_double_p, c_i64, ctypes.c_int,
                                   ctypes.c_double, ctypes.c_int, c_double_p, c_i64, c_int_p]),
 }
@@ -355,6 +357,12 @@ class SparseOperator(object):
         check(self.lib.gpmi_sp_lanczos(self.h, int(nprobe), int(steps), int(seed),
                                        int(probe_offset), dptr(a), dptr(b)), 'gpmi_sp_lanczos')
         return a, b
+
+    def bench_spmm(self, s, reps, eta=0.0):
+        ms = ctypes.c_double()
+        check(self.lib.gpmi_sp_bench_spmm(self.h, int(s), int(reps), float(eta),
+                                          ctypes.byref(ms)), 'gpmi_sp_bench_spmm')
+        return ms.value
 
     def cg(self, eta, B, rtol=1e-6, maxiter=None):
         B = as_c(B)

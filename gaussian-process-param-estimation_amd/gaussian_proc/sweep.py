@@ -68,3 +68,49 @@ def eta_sweep(K_mixed, X, z, etas, sigma=1.0, group=None):
         t_all = torch.cat(parts)
     allv = t_all.cpu().numpy()[:etas.size]
     return allv[:, 0].copy(), allv[:, 1].copy()
+
+
+def slq_sweep(K_mixed, etas, group=None):
+    """Stochastic-Lanczos-quadrature curves over an eta grid for a sparse
+    ``MixedCorrelation`` (imate_method 'slq'), probes sharded over the ranks.
+
+    Rank r runs the device Lanczos for the probe block [lo, hi) of the global
+    probe set (counter-based probes: the union over ranks is exactly the
+    single-GPU probe set), evaluates its per-probe quadrature for every eta, and
+    ONE all-gather collects the [probe, eta] blocks. Returns
+    dict(logdet, traceinv, traceinv2), each [neta], identical on every rank."""
+    from . import _slq
+    etas = numpy.atleast_1d(numpy.asarray(etas, dtype=float))
+    s = K_mixed.num_samples
+    world, rank, dist = 1, 0, None
+    if group is not False:
+        try:
+            import torch.distributed as dist_mod
+            if dist_mod.is_available() and dist_mod.is_initialized():
+                dist = dist_mod
+                world = dist.get_world_size(group)
+                rank = dist.get_rank(group)
+        except ImportError:
+            dist = None
+    lo, hi, per = shard(s, world, rank)
+    names = ('logdet', 'traceinv', 'traceinv2')
+    local = numpy.zeros((per, len(names), etas.size))
+    if hi > lo:
+        a, b = K_mixed.sop.lanczos(hi - lo, K_mixed.lanczos_degree, K_mixed.seed,
+                                   probe_offset=lo)
+        nodes = _slq.nodes(a, b)
+        for f, name in enumerate(names):
+            local[:hi - lo, f] = _slq.quadrature(nodes, etas, _slq.FUNCS[name])
+    if dist is not None and world > 1:
+        import torch
+        backend = dist.get_backend(group)
+        dev = torch.device('cuda', torch.cuda.current_device()) if backend == 'nccl' \
+            else torch.device('cpu')
+        t_local = torch.from_numpy(local.reshape(per, -1)).to(dev)
+        parts = [torch.empty_like(t_local) for _ in range(world)]
+        dist.all_gather(parts, t_local, group=group)
+        allq = torch.cat(parts).cpu().numpy().reshape(world * per, len(names), etas.size)[:s]
+    else:
+        allq = local[:s]
+    n = K_mixed.n
+    return {name: n * allq[:, f].mean(axis=0) for f, name in enumerate(names)}

@@ -153,6 +153,10 @@ int gpmi_sp_lanczos(gpmi_sp* sp, int nprobe, int steps, uint64_t seed, int probe
 int gpmi_sp_cg(gpmi_sp* sp, double eta, const double* rhs, int64_t ld, int nrhs, double rtol,
                int maxiter, double* sol, int64_t ldsol, int* iterations);
 
+/* Device-resident SpMM timing: reps launches of Y = (K + eta I) X with an
+ * [n][s] block already in HBM; average ms per launch (HIP events). */
+int gpmi_sp_bench_spmm(gpmi_sp* sp, int s, int reps, double eta, double* avg_ms);
+
 #ifdef __cplusplus
 }
 #endif

@@ -53,6 +53,67 @@ def _worker(rank, world, port, etas, out_q):
     dist.destroy_process_group()
 
 
+class _FakeSparse(object):
+    """Exact numpy Lanczos with the counter-based probes (stand-in for the
+    device SparseOperator.lanczos in a CPU-only process)."""
+
+    def __init__(self, K, steps):
+        self.K = K
+        self.steps = steps
+
+    def lanczos(self, nprobe, steps, seed=0, probe_offset=0):
+        from oracle import sparse as osp
+        P = osp.rademacher_probes(self.K.shape[0], probe_offset + nprobe, seed)[:, probe_offset:]
+        a = numpy.zeros((nprobe, steps))
+        b = numpy.zeros((nprobe, steps))
+        for p in range(nprobe):
+            ao, bo = osp.lanczos(self.K, P[:, p], steps)
+            a[p, :ao.size] = ao
+            b[p, :bo.size] = bo
+        return a, b
+
+
+class _SparseMixed(object):
+    def __init__(self, K):
+        self.sop = _FakeSparse(K, 12)
+        self.num_samples = 5
+        self.lanczos_degree = 12
+        self.seed = 3
+        self.n = K.shape[0]
+
+
+def _slq_worker(rank, world, port, etas, out_q):
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    from gaussian_proc.sweep import slq_sweep
+    K, _, _ = _problem()
+    res = slq_sweep(_SparseMixed(K + 0.5 * numpy.eye(K.shape[0])), etas)
+    out_q.put((rank, res))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_slq_sweep_probe_sharding_gloo():
+    from gaussian_proc.sweep import slq_sweep
+    etas = numpy.array([0.5, 1.0, 4.0])
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_slq_worker, args=(r, 2, port, etas, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    K, _, _ = _problem()
+    ref = slq_sweep(_SparseMixed(K + 0.5 * numpy.eye(K.shape[0])), etas, group=False)
+    for _, r in res:
+        for k in ('logdet', 'traceinv', 'traceinv2'):
+            numpy.testing.assert_allclose(r[k], ref[k], rtol=1e-12)
+
+
 def _free_port():
     s = socket.socket()
     s.bind(('127.0.0.1', 0))
