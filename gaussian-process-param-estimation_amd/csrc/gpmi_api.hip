@@ -89,12 +89,20 @@ struct gpmi_op {
   double* scratch = nullptr; // [n_pad][16] (matvec input)
   double* scratch2 = nullptr;// [n_pad][16] (matvec output)
   double* tracebuf = nullptr;// [n_pad][2]
+  double* W = nullptr;       // [n_pad][n_pad] L^-T workspace (traceinv, allocated lazily)
+  double* tpart = nullptr;   // [nt * (nt + 1) / 2 + nt * nt] traceinv partials
+  double* Td = nullptr;      // [nt][128][128] diagonal tiles of A^-1 (traceinv exponent 2)
   int* info = nullptr;       // [max_batch]
   int nrhs = 0;
   bool has_K = false;
   // factor cache: batch slot 0 holds the factor of K + cached_eta I
   bool cache_valid = false;
   double cached_eta = 0.0;
+  uint64_t factor_gen = 0;             // bumped by every factorization
+  // traceinv cache (valid for factor generation tinv_gen)
+  uint64_t tinv_gen = ~0ull;
+  int tinv_have = 0;                   // bit 0: tr(A^-1), bit 1: tr(A^-2)
+  double tinv[2] = {0.0, 0.0};
   // timing
   bool timing = false;
   std::vector<hipEvent_t> ev;
@@ -182,6 +190,7 @@ int run_factor(gpmi_op* op, const double* etas_host, int nb, const double* rhs_d
   BatchPtrs P = op->ptrs();
   op->syrk_log.clear();
   op->cache_valid = false;
+  ++op->factor_gen;
   if (op->timing) {
     if (!op->ev_begin) {
       HIP_TRY(hipEventCreate(&op->ev_begin));
@@ -461,7 +470,8 @@ int gpmi_op_destroy(gpmi_op* op) {
   if (op->stream) (void)hipStreamSynchronize(op->stream);
   if (op->stream2) (void)hipStreamSynchronize(op->stream2);
   double* bufs[] = {op->K, op->A, op->R, op->X, op->U, op->Linv, op->logdiag, op->gram,
-                    op->out, op->etas, op->rhs_src, op->scratch, op->scratch2, op->tracebuf};
+                    op->out, op->etas, op->rhs_src, op->scratch, op->scratch2, op->tracebuf,
+                    op->W, op->tpart, op->Td};
   for (double* p : bufs)
     if (p) (void)hipFree(p);
   if (op->info) (void)hipFree(op->info);
@@ -675,6 +685,94 @@ int gpmi_op_trace(gpmi_op* op, double* trace_k, double* trace_k2) {
   }
   if (trace_k) *trace_k = a;
   if (trace_k2) *trace_k2 = f;
+  return 0;
+}
+
+int gpmi_op_traceinv(gpmi_op* op, double eta, int exponent, double* value) {
+  if (!op) return set_err(-1006, "null handle");
+  if (!value) return set_err(-1004, "null output");
+  if (exponent < 1 || exponent > 2)
+    return set_err(-1010, "traceinv exponent %d outside [1, 2]", exponent);
+  DeviceGuard g(op->device);
+  bool fresh;
+  int rc = ensure_factor(op, eta, op->rhs_src, &fresh);
+  if (rc) return rc;
+  int inf = 0;
+  HIP_TRY(hipMemcpyAsync(&inf, op->info, sizeof(int), hipMemcpyDeviceToHost, op->stream));
+  HIP_TRY(hipStreamSynchronize(op->stream));
+  if (inf) {
+    op->cache_valid = false;
+    return set_err(inf, "matrix K + eta I is not positive definite (pivot %d)", inf);
+  }
+  if (op->tinv_gen != op->factor_gen) {
+    op->tinv_gen = op->factor_gen;
+    op->tinv_have = 0;
+  }
+  const int bit = 1 << (exponent - 1);
+  if (!(op->tinv_have & bit)) {
+    const int nt = op->nt;
+    const int64_t np = op->n_pad;
+    const int ntri = nt * (nt + 1) / 2;
+    if (!op->W) {
+      HIP_TRY(hipMalloc(&op->W, sizeof(double) * (size_t)np * np));
+      HIP_TRY(hipMalloc(&op->tpart, sizeof(double) * (size_t)(ntri + nt * nt)));
+      HIP_TRY(hipMalloc(&op->Td, sizeof(double) * (size_t)nt * TS * TS));
+    }
+    hipStream_t s = op->stream;
+    double* p1 = op->tpart + ntri;   // [nt][nt]: ||Y_kj||^2 at [k * nt + j]
+    if (!(op->tinv_have & 1)) {
+      // W = L^-T from the cached factor in slot 0 (needed by both exponents)
+      for (int kb = 0; kb < nt; kb += op->outer) {
+        const int ke = std::min(nt, kb + op->outer);
+        for (int k = kb; k < ke; ++k) {
+          if (k > kb) {
+            hipLaunchKernelGGL(trinv_update_kernel, dim3(k), dim3(256), 0, s, op->A, np, op->W,
+                               np, k, k, kb, k);
+            LAUNCH_CHECK("trinv_update_kernel");
+          }
+          hipLaunchKernelGGL(trinv_diag_kernel, dim3(k + 1), dim3(256), 0, s, op->Linv, op->W,
+                             np, k, p1 + (int64_t)k * nt);
+          LAUNCH_CHECK("trinv_diag_kernel");
+        }
+        if (ke < nt) {
+          hipLaunchKernelGGL(trinv_update_kernel, dim3((nt - ke) * ke), dim3(256), 0, s, op->A,
+                             np, op->W, np, ke, ke, kb, ke);
+          LAUNCH_CHECK("trinv_update_kernel");
+        }
+      }
+      std::vector<double> h((size_t)nt * nt);
+      HIP_TRY(hipMemcpyAsync(h.data(), p1, sizeof(double) * h.size(), hipMemcpyDeviceToHost, s));
+      HIP_TRY(hipStreamSynchronize(s));
+      double acc = 0.0;
+      for (int k = 0; k < nt; ++k)
+        for (int j = 0; j <= k; ++j) acc += h[(size_t)k * nt + j];
+      // the identity pad contributes n_pad - n
+      op->tinv[0] = acc - (double)(np - op->n);
+      op->tinv_have |= 1;
+    }
+    if (exponent == 2) {
+      // T = W W^T over k-panels of 4 tiles; panel [p0, p0 + kd) updates tile rows I < imax
+      for (int p0 = 0; p0 < (int)np; p0 += 4 * TS) {
+        const int kd = std::min<int>(4 * TS, (int)np - p0);
+        const int imax = (p0 + kd) / TS;
+        hipLaunchKernelGGL(gram_panel_kernel, dim3(imax * (imax + 1) / 2), dim3(256), 0, s,
+                           op->W, np, op->Td, p0, kd, imax);
+        LAUNCH_CHECK("gram_panel_kernel");
+      }
+      hipLaunchKernelGGL(gram_sumsq_kernel, dim3(nt), dim3(256), 0, s, op->W, np, op->Td,
+                         op->tpart);
+      LAUNCH_CHECK("gram_sumsq_kernel");
+      std::vector<double> h((size_t)nt);
+      HIP_TRY(hipMemcpyAsync(h.data(), op->tpart, sizeof(double) * h.size(),
+                             hipMemcpyDeviceToHost, s));
+      HIP_TRY(hipStreamSynchronize(s));
+      double acc = 0.0;
+      for (int q = 0; q < nt; ++q) acc += h[q];
+      op->tinv[1] = acc - (double)(np - op->n);
+      op->tinv_have |= 2;
+    }
+  }
+  *value = op->tinv[exponent - 1];
   return 0;
 }
 

@@ -28,4 +28,111 @@ __device__ __forceinline__ d4 mfma64(double a, double b, d4 c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
 
+
+// 128 x 16 slab of rows base[row * ld + p .. p + 15]: each wave-instruction
+// reads 32 full 128-B row segments (16 B / lane).
+__device__ __forceinline__ void gload_slab(const double* __restrict__ base, int64_t ld,
+                                           int p, d2 (&r)[4]) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int idx = i * 256 + t;
+    const int row = idx >> 3, c2 = idx & 7;
+    r[i] = *reinterpret_cast<const d2*>(base + (int64_t)row * ld + p + 2 * c2);
+  }
+}
+
+__device__ __forceinline__ void sstore_slab(double* s, const d2 (&r)[4]) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int idx = i * 256 + t;
+    const int row = idx >> 3, c2 = idx & 7;
+    *reinterpret_cast<d2*>(s + row * BK + 2 * (c2 ^ ((row >> 1) & 7))) = r[i];
+  }
+}
+
+// acc (wave tile 64 x 64 at (wr, wc)) += P1[0:128, 0:kdim] * P2[0:128, 0:kdim]^T.
+// f64 MFMA 16x16x4 operand maps: A[i = lane&15][k = lane>>4], B[k = lane>>4][j = lane&15].
+// WITH_RHS additionally accumulates racc (rows wr*64 + wc*32 + [0,32), 16 cols)
+// += P1 * U with U[kdim][16] staged in LDS.
+template <bool WITH_RHS, bool NEG = false>
+__device__ __forceinline__ void tile_mma(const double* __restrict__ P1, int64_t ld1,
+                                         const double* __restrict__ P2, int64_t ld2,
+                                         int kdim, double* sA, double* sB,
+                                         d4 (&acc)[4][4], const double* sU,
+                                         d4 (&racc)[2]) {
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int wr = w >> 1, wc = w & 1;
+  const int fr = lane & 15, fk = lane >> 4;
+  d2 ra[4], rb[4];
+  gload_slab(P1, ld1, 0, ra);
+  gload_slab(P2, ld2, 0, rb);
+  sstore_slab(sA, ra);
+  sstore_slab(sB, rb);
+  __syncthreads();
+  const int nsteps = kdim / BK;
+  for (int s = 0; s < nsteps; ++s) {
+    const int cur = s & 1;
+    const double* cA = sA + cur * STAGE;
+    const double* cB = sB + cur * STAGE;
+    if (s + 1 < nsteps) {
+      gload_slab(P1, ld1, (s + 1) * BK, ra);
+      gload_slab(P2, ld2, (s + 1) * BK, rb);
+    }
+#pragma unroll
+    for (int kk = 0; kk < BK / 4; ++kk) {
+      double a[4], b[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        a[i] = cA[slab_off(wr * 64 + i * 16 + fr, kk * 4 + fk)];
+        if (NEG) a[i] = -a[i];
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = cB[slab_off(wc * 64 + j * 16 + fr, kk * 4 + fk)];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma64(a[i], b[j], acc[i][j]);
+      if (WITH_RHS) {
+        const double u = sU[(s * BK + kk * 4 + fk) * RLD + fr];
+        const double a0 = wc ? a[2] : a[0];
+        const double a1 = wc ? a[3] : a[1];
+        racc[0] = mfma64(a0, u, racc[0]);
+        racc[1] = mfma64(a1, u, racc[1]);
+      }
+    }
+    if (s + 1 < nsteps) {
+      sstore_slab(sA + (cur ^ 1) * STAGE, ra);
+      sstore_slab(sB + (cur ^ 1) * STAGE, rb);
+    }
+    __syncthreads();
+  }
+}
+
+// Bijective XCD-aware remap (consecutive logical tiles -> one XCD's L2).
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
+// Lower-triangular tile enumeration of a band of w tile columns over t tile
+// rows (row-major): rows i < w hold a triangle, rows i >= w hold w tiles.
+__device__ __forceinline__ void tri_decode(int q, int w, int* pi, int* pj) {
+  const int tri = w * (w + 1) / 2;
+  int i, j;
+  if (q < tri) {
+    i = (int)((sqrt(8.0 * (double)q + 1.0) - 1.0) * 0.5);
+    while ((i + 1) * (i + 2) / 2 <= q) ++i;
+    while (i * (i + 1) / 2 > q) --i;
+    j = q - i * (i + 1) / 2;
+  } else {
+    const int r = q - tri;
+    i = w + r / w;
+    j = r % w;
+  }
+  *pi = i;
+  *pj = j;
+}
+
 }  // namespace gpmi

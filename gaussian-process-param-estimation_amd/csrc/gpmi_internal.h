@@ -50,6 +50,14 @@ __global__ void gemv_sym_kernel(const double* K, int64_t ldk, int64_t n,
                                 const double* x, int64_t ldx, int ncol, double* y,
                                 double eta, int exponent);
 __global__ void trace_kernel(const double* K, int64_t ldk, int64_t n, double* out);
+__global__ void trinv_diag_kernel(const double* Linv, double* W, int64_t ldw, int k,
+                                  double* partial);
+__global__ void trinv_update_kernel(const double* L, int64_t lda, double* W, int64_t ldw, int i0,
+                                    int nj, int kb, int ke);
+__global__ void gram_panel_kernel(double* W, int64_t ldw, double* Td, int p0, int kdim,
+                                  int imax);
+__global__ void gram_sumsq_kernel(const double* W, int64_t ldw, const double* Td,
+                                  double* partial);
 __global__ void matern_eval_kernel(const double* x, int64_t m, MaternParams P, double* out);
 
 }  // namespace gpmi

@@ -46,6 +46,7 @@ SIGNATURES = {
     'gpmi_op_matvec': (ctypes.c_int, [c_op_p, c_double_p, c_i64, ctypes.c_int, c_double_p,
                                       c_i64]),
     'gpmi_op_trace': (ctypes.c_int, [c_op_p, c_double_p, c_double_p]),
+    'gpmi_op_traceinv': (ctypes.c_int, [c_op_p, ctypes.c_double, ctypes.c_int, c_double_p]),
     'gpmi_op_set_timing': (ctypes.c_int, [c_op_p, ctypes.c_int]),
     'gpmi_op_last_timing': (ctypes.c_int, [c_op_p, c_double_p, c_int_p, c_double_p,
                                            c_double_p, c_double_p]),
@@ -231,6 +232,14 @@ class Operator(object):
         b = ctypes.c_double()
         check(self.lib.gpmi_op_trace(self.h, ctypes.byref(a), ctypes.byref(b)), 'gpmi_op_trace')
         return a.value, b.value
+
+    def traceinv(self, eta, exponent=1):
+        """Exact tr((K + eta I)^-exponent), exponent 1 or 2 (device triangular
+        inverse of the cached Cholesky factor)."""
+        v = ctypes.c_double()
+        check(self.lib.gpmi_op_traceinv(self.h, float(eta), int(exponent), ctypes.byref(v)),
+              'gpmi_op_traceinv')
+        return v.value
 
     def set_timing(self, on):
         check(self.lib.gpmi_op_set_timing(self.h, int(bool(on))), 'gpmi_op_set_timing')

@@ -168,12 +168,13 @@ class MixedCorrelation(object):
                                           % self.imate_method)
             raise ValueError('Existing methods are "eigenvalue", "cholesky,"'
                              '"hutchinson", and "slq".')
-        # exact: tr((K + eta I)^-p) from the inverse (columns solved on the device)
+        if exponent == 0:
+            return float(self.n)
+        if exponent in (1, 2):
+            # exact, from the device triangular inverse of the cached factor
+            return self.op.traceinv(eta, exponent)
+        # higher powers (not used by the likelihoods): columns of A^-1 solved on the device
         Ainv = self.op.solve(eta, numpy.eye(self.n))
-        if exponent == 1:
-            return float(numpy.trace(Ainv))
-        if exponent == 2:
-            return float(numpy.sum(Ainv * Ainv))
         return float(numpy.trace(numpy.linalg.matrix_power(Ainv, exponent)))
 
     def logdet(self, eta, exponent=1):                             # :221-274

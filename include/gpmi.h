@@ -97,6 +97,14 @@ int gpmi_op_matvec(gpmi_op* op, const double* x, int64_t ld, int ncol, double* y
  * Building blocks of MixedCorrelation.trace mixed_correlation.py:96-149. */
 int gpmi_op_trace(gpmi_op* op, double* trace_k, double* trace_k2);
 
+/* Exact tr((K + eta I)^-exponent), exponent 1 or 2, from the (cached) Cholesky
+ * factor: tr(A^-1) = ||L^-1||_F^2 and tr(A^-2) = ||L^-T L^-1||_F^2, with L^-1
+ * built by a blocked triangular solve on the device (n_pad^2 extra doubles,
+ * allocated on first use). Results are cached per factorization.
+ * Replaces MixedCorrelation.traceinv mixed_correlation.py:155-215 for
+ * imate_method 'eigenvalue' / 'cholesky' (imate.traceinv, exact). */
+int gpmi_op_traceinv(gpmi_op* op, double eta, int exponent, double* value);
+
 /* Kernel-level timing of the last gpmi_op_loglik_batch when enabled:
  * dominant kernel (trailing-update SYRK) total device ms, launches and
  * algorithmic flops; whole-call device ms. HIP events on the op's stream. */

@@ -120,6 +120,27 @@ def test_ragged_sizes_vs_oracle(gp, n):
         numpy.testing.assert_allclose(g, R.T @ ref.solve(e, R), rtol=1e-8, atol=1e-10)
 
 
+@pytest.mark.parametrize('n', [5, 128, 300, 1000])
+def test_traceinv_device_vs_inverse(gp, n):
+    """tr(A^-1) = ||L^-1||_F^2 and tr(A^-2) = ||A^-1||_F^2 from the device
+    triangular inverse vs numpy's explicit inverse (rel <= 1e-10)."""
+    rng = numpy.random.RandomState(n + 7)
+    pts = rng.rand(n, 2)
+    K = matern.dense_correlation(pts, 0.15, 0.5)
+    op = _op(gp, K)
+    X = numpy.column_stack([numpy.ones(n), pts])
+    z = rng.randn(n)
+    for eta in (1e-2, 0.7):
+        Ainv = numpy.linalg.inv(K + eta * numpy.eye(n))
+        assert rel(op.traceinv(eta), numpy.trace(Ainv)) < 1e-10
+        assert rel(op.traceinv(eta, 2), numpy.sum(Ainv * Ainv)) < 1e-10
+        assert rel(op.traceinv(eta, 1), numpy.trace(Ainv)) < 1e-10   # cached
+        # a batched call re-uses slot 0: the traceinv cache must not go stale
+        op.loglik_terms([3.0, 0.2], X, z)
+        assert rel(op.traceinv(eta, 2), numpy.sum(Ainv * Ainv)) < 1e-10
+        assert op.traceinv(eta, 0) == n
+
+
 def test_solve_many_columns(gp):
     rng = numpy.random.RandomState(1)
     pts = rng.rand(400, 2)
@@ -201,6 +222,12 @@ def test_cfg2_n4096_likelihood_and_logdet(gp):
                cfg['operator']['eigenvalue']['logdet']) < 1e-9
     ld, _ = op.loglik_terms(cfg['etas'], X, z)
     assert rel(ld, cfg['operator']['eigenvalue']['logdet']) < 1e-9
+    g = cfg['operator']['eigenvalue']
+    assert rel([op.traceinv(e) for e in cfg['etas']], g['traceinv']) < 1e-9
+    assert rel([op.traceinv(e, 2) for e in cfg['etas']], g['traceinv_exp2']) < 1e-9
+    from gaussian_proc._likelihood._profile_likelihood import ProfileLikelihood
+    assert rel([ProfileLikelihood.log_likelihood_der1_eta(z, X, op, le)
+                for le in cfg['log_etas']], cfg['profile_der1_eta']) < 1e-7
 
 
 def test_maximize_cfg1_matches_reference(gp, capsys):
