@@ -60,4 +60,19 @@ __global__ void gram_sumsq_kernel(const double* W, int64_t ldw, const double* Td
                                   double* partial);
 __global__ void matern_eval_kernel(const double* x, int64_t m, MaternParams P, double* out);
 
+// Multi-shift CG Gram state (gpmi_sparse.hip, gpmi_sparse_api.hip); device pointers.
+constexpr int MS_MAXS = 16;   // RHS columns per multi-shift block
+struct MsState {
+  double* rr;      // [s]   r_c . r_c
+  double* a;       // [s]   alpha_c of this iteration (0 once converged)
+  double* a_prev;  // [s]
+  double* beta;    // [s]   beta used to form the current p
+  double* bn2;     // [s]   ||b_c||^2
+  int* active;     // [s]
+  double* z;       // [S][s]    zeta_j of the current residual
+  double* z_prev;  // [S][s]
+  double* bp;      // [S][s'][s] b_c' . p_{j,c}
+  double* g;       // [S][s'][s] accumulated G_j[c'][c]
+};
+
 }  // namespace gpmi

@@ -32,6 +32,14 @@ __global__ void col_gs_update_kernel(double*, const double*, int64_t, const doub
 __global__ void col_axpby_kernel(const double*, double*, const double*, const double*, int64_t,
                                  int);
 __global__ void rademacher_kernel(double*, int64_t, int, unsigned long long, int, double);
+__global__ void ms_dots_partial_kernel(const double*, const double*, int64_t, int, double*);
+__global__ void ms_alpha_kernel(MsState, const double*, int);
+__global__ void ms_r_update_kernel(double*, const double*, const double*, int64_t, int);
+__global__ void ms_scalar_kernel(MsState, const double*, int, const double*, int, int, double,
+                                 double*);
+__global__ void ms_p_update_kernel(double*, const double*, const double*, const int*, int64_t,
+                                   int);
+__global__ void ms_init_kernel(MsState, const double*, int, int, int);
 int matern_params_host(double nu, MaternParams* P);   // gpmi_api.hip
 int set_error(int code, const char* msg);             // gpmi_api.hip
 }  // namespace gpmi
@@ -96,6 +104,8 @@ struct gpmi_sp {
   double* partial = nullptr;   // [NBLK][J][s]
   size_t partial_doubles = 0;
   double* small = nullptr;     // coefficient / reduction arrays
+  double* msbuf = nullptr;     // multi-shift CG scalar state
+  size_t msbuf_doubles = 0;
 };
 
 namespace {
@@ -325,6 +335,7 @@ int gpmi_sp_destroy(gpmi_sp* sp) {
   if (sp->ws) (void)hipFree(sp->ws);
   if (sp->partial) (void)hipFree(sp->partial);
   if (sp->small) (void)hipFree(sp->small);
+  if (sp->msbuf) (void)hipFree(sp->msbuf);
   if (sp->stream) (void)hipStreamDestroy(sp->stream);
   delete sp;
   return 0;
@@ -477,6 +488,104 @@ int gpmi_sp_cg(gpmi_sp* sp, double eta, const double* rhs, int64_t ld, int nrhs,
       for (int c = 0; c < s; ++c) sol[i * ldsol + c0 + c] = h[(size_t)i * s + c];
   }
   if (iterations) *iterations = max_it_used;
+  return 0;
+}
+
+int gpmi_sp_msgram(gpmi_sp* sp, const double* etas, int neta, const double* rhs, int64_t ld,
+                   int nrhs, double rtol, int maxiter, double* G, int* iterations) {
+  if (!sp) return set_error(-1006, "null handle");
+  if (neta < 1 || nrhs < 1 || nrhs > MS_MAXS || neta * nrhs > 1024)
+    return set_error(-1104, "msgram: need 1 <= nrhs <= 16 and neta * nrhs <= 1024");
+  Guard g(sp->device);
+  const int64_t n = sp->n;
+  const int s = nrhs, S = neta;
+  const int64_t ns = n * s;
+  const double eta0 = *std::min_element(etas, etas + neta);
+  int rc = ensure_ws(sp, (size_t)4 * ns);
+  if (rc) return rc;
+  const int ne = s * s + s;
+  rc = ensure_partial(sp, (size_t)NBLK * std::max(ne, s));
+  if (rc) return rc;
+  const size_t need = (size_t)6 * s + 2 * (size_t)S * s + 2 * (size_t)S * s * s + S + s + s;
+  if (sp->msbuf_doubles < need) {
+    if (sp->msbuf) SP_TRY(hipFree(sp->msbuf));
+    sp->msbuf = nullptr;
+    SP_TRY(hipMalloc(&sp->msbuf, sizeof(double) * need));
+    sp->msbuf_doubles = need;
+  }
+  double* q = sp->msbuf;
+  MsState st;
+  st.rr = q; q += s;
+  st.a = q; q += s;
+  st.a_prev = q; q += s;
+  st.beta = q; q += s;
+  st.bn2 = q; q += s;
+  double* pq = q; q += s;
+  st.z = q; q += (size_t)S * s;
+  st.z_prev = q; q += (size_t)S * s;
+  st.bp = q; q += (size_t)S * s * s;
+  st.g = q; q += (size_t)S * s * s;
+  double* dshift = q; q += S;
+  double* beta_out = q; q += s;
+  st.active = reinterpret_cast<int*>(q);   // s ints in s doubles
+  double* Bd = sp->ws;
+  double* Rd = Bd + ns;
+  double* Pd = Rd + ns;
+  double* Qd = Pd + ns;
+  hipStream_t str = sp->stream;
+  {
+    std::vector<double> h((size_t)ns);
+    for (int64_t i = 0; i < n; ++i)
+      for (int c = 0; c < s; ++c) h[(size_t)i * s + c] = rhs[i * ld + c];
+    SP_TRY(hipMemcpyAsync(Bd, h.data(), sizeof(double) * ns, hipMemcpyHostToDevice, str));
+    std::vector<double> hd(S);
+    for (int j = 0; j < S; ++j) hd[j] = etas[j] - eta0;
+    SP_TRY(hipMemcpyAsync(dshift, hd.data(), sizeof(double) * S, hipMemcpyHostToDevice, str));
+    SP_TRY(hipMemcpyAsync(Rd, Bd, sizeof(double) * ns, hipMemcpyDeviceToDevice, str));
+    SP_TRY(hipMemcpyAsync(Pd, Bd, sizeof(double) * ns, hipMemcpyDeviceToDevice, str));
+    SP_TRY(hipStreamSynchronize(str));
+  }
+  const unsigned sthreads = (unsigned)((S * s + 63) / 64 * 64);
+  hipLaunchKernelGGL(ms_dots_partial_kernel, dim3(NBLK), dim3(256), 0, str, Bd, Rd, n, s,
+                     sp->partial);
+  SP_LAUNCH("ms_dots_partial_kernel");
+  hipLaunchKernelGGL(ms_init_kernel, dim3(1), dim3(sthreads), 0, str, st, sp->partial, NBLK, S,
+                     s);
+  SP_LAUNCH("ms_init_kernel");
+  int it = 0;
+  std::vector<int> hact(s);
+  for (; it < maxiter; ++it) {
+    if (it % 8 == 0) {
+      SP_TRY(hipMemcpyAsync(hact.data(), st.active, sizeof(int) * s, hipMemcpyDeviceToHost, str));
+      SP_TRY(hipStreamSynchronize(str));
+      bool any = false;
+      for (int c = 0; c < s; ++c) any = any || hact[c];
+      if (!any) break;
+    }
+    rc = spmm(sp, Pd, Qd, s, eta0);
+    if (rc) return rc;
+    rc = col_dots(sp, Pd, 0, 1, Qd, s, pq);
+    if (rc) return rc;
+    hipLaunchKernelGGL(ms_alpha_kernel, dim3(1), dim3(64), 0, str, st, pq, s);
+    SP_LAUNCH("ms_alpha_kernel");
+    hipLaunchKernelGGL(ms_r_update_kernel, dim3(grid_ns(n, s)), dim3(256), 0, str, Rd, Qd, st.a,
+                       n, s);
+    SP_LAUNCH("ms_r_update_kernel");
+    hipLaunchKernelGGL(ms_dots_partial_kernel, dim3(NBLK), dim3(256), 0, str, Bd, Rd, n, s,
+                       sp->partial);
+    SP_LAUNCH("ms_dots_partial_kernel");
+    hipLaunchKernelGGL(ms_scalar_kernel, dim3(1), dim3(sthreads), 0, str, st, sp->partial, NBLK,
+                       dshift, S, s, rtol * rtol, beta_out);
+    SP_LAUNCH("ms_scalar_kernel");
+    hipLaunchKernelGGL(ms_p_update_kernel, dim3(grid_ns(n, s)), dim3(256), 0, str, Pd, Rd, st.beta,
+                       st.active, n, s);
+    SP_LAUNCH("ms_p_update_kernel");
+  }
+  std::vector<double> hg((size_t)S * s * s);
+  SP_TRY(hipMemcpyAsync(hg.data(), st.g, sizeof(double) * hg.size(), hipMemcpyDeviceToHost, str));
+  SP_TRY(hipStreamSynchronize(str));
+  std::copy(hg.begin(), hg.end(), G);
+  if (iterations) *iterations = it;
   return 0;
 }
 

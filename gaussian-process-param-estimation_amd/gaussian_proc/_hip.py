@@ -70,6 +70,9 @@ SIGNATURES = {
                                           c_double_p]),
     'gpmi_sp_cg': (ctypes.c_int, [c_op_p, ctypes.c_double, c_double_p, c_i64, ctypes.c_int,
                                   ctypes.c_double, ctypes.c_int, c_double_p, c_i64, c_int_p]),
+    'gpmi_sp_msgram': (ctypes.c_int, [c_op_p, c_double_p, ctypes.c_int, c_double_p, c_i64,
+                                      ctypes.c_int, ctypes.c_double, ctypes.c_int, c_double_p,
+                                      c_int_p]),
 }
 
 
@@ -384,3 +387,26 @@ class SparseOperator(object):
               'gpmi_sp_cg')
         self.last_cg_iterations = it.value
         return X[:, 0] if B.ndim == 1 else X
+
+    MS_MAXS = 16
+
+    def msgram(self, etas, B, rtol=1e-6, maxiter=None):
+        """G[j] = B^T (K + etas[j] I)^-1 B for all etas from one multi-shift CG
+        (B: [n, s], s <= 16). Returns G [neta, s, s]."""
+        B = as_c(B)
+        B2 = B[:, None] if B.ndim == 1 else B
+        etas = as_c(numpy.atleast_1d(etas))
+        s = B2.shape[1]
+        G = numpy.empty((etas.size, s, s))
+        it = ctypes.c_int(0)
+        maxiter = 10 * self.n if maxiter is None else int(maxiter)
+        step = max(1, 1024 // s)
+        for j0 in range(0, etas.size, step):
+            e = as_c(etas[j0:j0 + step])
+            Gj = numpy.empty((e.size, s, s))
+            check(self.lib.gpmi_sp_msgram(self.h, dptr(e), e.size, dptr(B2), s, s, float(rtol),
+                                          maxiter, dptr(Gj), ctypes.byref(it)),
+                  'gpmi_sp_msgram')
+            G[j0:j0 + e.size] = Gj
+        self.last_cg_iterations = it.value
+        return G

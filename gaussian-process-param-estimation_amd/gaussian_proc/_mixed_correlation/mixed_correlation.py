@@ -229,12 +229,11 @@ class MixedCorrelation(object):
         device call. Returns (logdet[neta], G[neta, m+1, m+1])."""
         etas = numpy.atleast_1d(numpy.asarray(etas, dtype=float))
         if self.sparse:
+            # SLQ logdet per eta (cached Ritz nodes) and all Gram blocks from one
+            # multi-shift CG on K + min(eta) I (tolerance as _linear_solver.py:24)
             R = numpy.column_stack([numpy.asarray(X, dtype=float), numpy.asarray(z, dtype=float)])
-            lds, gs = [], []
-            for e in etas:
-                lds.append(self.logdet(e))
-                gs.append(R.T @ self.sop.cg(e, R, rtol=self.cg_rtol))
-            return numpy.array(lds), numpy.array(gs)
+            lds = numpy.array([self.logdet(e) for e in etas])
+            return lds, self.sop.msgram(etas, R, rtol=self.cg_rtol)
         self.set_rhs(X, z)
         lds, gs = [], []
         mb = self.op.max_batch

@@ -161,6 +161,17 @@ int gpmi_sp_lanczos(gpmi_sp* sp, int nprobe, int steps, uint64_t seed, int probe
 int gpmi_sp_cg(gpmi_sp* sp, double eta, const double* rhs, int64_t ld, int nrhs, double rtol,
                int maxiter, double* sol, int64_t ldsol, int* iterations);
 
+/* Multi-shift CG Gram: G[j] = RHS^T (K + etas[j] I)^-1 RHS for every eta from
+ * ONE blocked CG on K + min(etas) I (shifted systems share its Krylov space;
+ * the Gram entries follow scalar recurrences, no per-eta vectors). Per-column
+ * stop ||r|| <= rtol ||b|| on the base (slowest) system. nrhs <= 16,
+ * neta * nrhs <= 1024; G: [neta][nrhs][nrhs]. Every K + eta_j I must be SPD.
+ * Replaces the per-eta sparse solves of DirectLikelihood.log_likelihood
+ * _direct_likelihood.py:59,62 -> MixedCorrelation.solve mixed_correlation.py:280-299
+ * -> _linear_solver.py:57-68 (scipy.sparse.linalg.cg, tol 1e-6). */
+int gpmi_sp_msgram(gpmi_sp* sp, const double* etas, int neta, const double* rhs, int64_t ld,
+                   int nrhs, double rtol, int maxiter, double* G, int* iterations);
+
 /* Device-resident SpMM timing: reps launches of Y = (K + eta I) X with an
  * [n][s] block already in HBM; average ms per launch (HIP events). */
 int gpmi_sp_bench_spmm(gpmi_sp* sp, int s, int reps, double eta, double* avg_ms);

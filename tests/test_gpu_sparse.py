@@ -76,6 +76,36 @@ def test_spmm_and_cg(gp):
     numpy.testing.assert_allclose(Y, scipy.sparse.linalg.spsolve(A, X), rtol=1e-8, atol=1e-9)
 
 
+def _nrel(a, b):
+    return float(numpy.max(numpy.abs(a - b)) / numpy.max(numpy.abs(b)))
+
+
+def test_multishift_gram_vs_exact(gp):
+    """One multi-shift CG on K + min(eta) I gives B^T (K + eta I)^-1 B for every
+    eta; vs scipy's sparse direct solve (Gram error is quadratic in the CG
+    residual: rel <= 1e-9 at rtol 1e-8, <= 1e-6 at the reference's 1e-6)."""
+    from gaussian_proc import _hip
+    _, K = _small_sparse()
+    n = K.shape[0]
+    sop = _hip.SparseOperator.from_csr(K)
+    rng = numpy.random.RandomState(5)
+    B = rng.randn(n, 7)
+    etas = numpy.array([10.0, 2.5, 4.0, 100.0])
+    for rtol, tol in ((1e-8, 1e-9), (1e-6, 1e-6)):
+        G = sop.msgram(etas, B, rtol=rtol)
+        for e, g in zip(etas, G):
+            A = (K + e * scipy.sparse.eye(n)).tocsc()
+            ex = B.T @ scipy.sparse.linalg.spsolve(A, B)
+            assert _nrel(g, ex) < tol, (rtol, e)
+    # 11 columns (3D degree-2 basis + z) and a 1-column RHS
+    B11 = rng.randn(n, 11)
+    G = sop.msgram([3.0], B11, rtol=1e-10)
+    ex = B11.T @ scipy.sparse.linalg.spsolve((K + 3.0 * scipy.sparse.eye(n)).tocsc(), B11)
+    assert _nrel(G[0], ex) < 1e-10
+    g1 = sop.msgram([3.0, 7.0], B[:, 0], rtol=1e-10)
+    assert g1.shape == (2, 1, 1)
+
+
 def test_lanczos_and_slq_match_oracle_same_probes(gp):
     from gaussian_proc import _hip, _slq
     _, K = _small_sparse()
