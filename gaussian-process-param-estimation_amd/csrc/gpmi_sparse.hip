@@ -17,26 +17,58 @@
 
 namespace gpmi {
 
-// Y[:, 0:s] = (K + eta I) X[:, 0:s]; one wave per row; lanes = (slot, column)
-// with sp2 = next pow2 >= s columns and 64 / sp2 nonzero slots.
+// Y[:, 0:s] = (K + eta I) X[:, 0:s]; one wave per row (blocks of 4 rows,
+// contiguous row ranges per XCD so neighbouring rows share X rows in L2). The
+// wave loads its row's (column, value) pairs, up to 64 per chunk, in one
+// coalesced read and broadcasts them with ds_bpermute to lanes = (slot, column),
+// slots = 64 / s nonzeros at a time, four independent gathers per lane; the
+// slots are summed with shuffles in a fixed order. (Runs of rows per wave with
+// the next row prefetched measured 1.5x slower: fewer waves in flight.) The gathers (nnz * s doubles) come from
+// L2 / MALL; HBM sees the CSR arrays once.
+__device__ __forceinline__ void spmm_chunk(const int myidx, const double myval, int cnt,
+                                           const double* __restrict__ X, int64_t ldx, int slots,
+                                           int slot, int c, bool on, double (&acc)[4]) {
+  // wave-uniform trip count: every lane takes part in every ds_bpermute
+  for (int jb = 0; jb < cnt; jb += 4 * slots) {
+    int ix[4];
+    double vx[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int j = (jb + u * slots + slot) & 63;
+      ix[u] = __shfl(myidx, j);
+      vx[u] = __shfl(myval, j);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (on && jb + u * slots + slot < cnt) acc[u] += vx[u] * X[(int64_t)ix[u] * ldx + c];
+  }
+}
+
 __global__ __launch_bounds__(256) void csr_spmm_kernel(const int64_t* __restrict__ indptr,
                                                        const int* __restrict__ indices,
                                                        const double* __restrict__ data,
                                                        int64_t n, const double* __restrict__ X,
                                                        int64_t ldx, double* __restrict__ Y,
-                                                       int64_t ldy, int s, int sp2, double eta) {
-  const int lane = threadIdx.x & 63;
-  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+                                                       int64_t ldy, int s, int slots, double eta) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  // contiguous row ranges per XCD: neighbouring rows share X rows in that XCD's L2
+  const int64_t row = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * 4 + wv;
   if (row >= n) return;
-  const int c = lane & (sp2 - 1);
-  const int slot = lane / sp2;
-  const int slots = 64 / sp2;
+  const int slot = lane / s;
+  const int c = lane - slot * s;
+  const bool on = slot < slots;
   const int64_t k0 = indptr[row], k1 = indptr[row + 1];
-  double acc = 0.0;
-  if (c < s)
-    for (int64_t k = k0 + slot; k < k1; k += slots) acc += data[k] * X[(int64_t)indices[k] * ldx + c];
-  for (int off = sp2; off < 64; off <<= 1) acc += __shfl_xor(acc, off);
-  if (slot == 0 && c < s) Y[row * ldy + c] = acc + eta * X[row * ldx + c];
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int64_t kb = k0; kb < k1; kb += 64) {
+    const int cnt = (int)((k1 - kb) < 64 ? (k1 - kb) : 64);
+    const int myidx = lane < cnt ? indices[kb + lane] : 0;
+    const double myval = lane < cnt ? data[kb + lane] : 0.0;
+    spmm_chunk(myidx, myval, cnt, X, ldx, slots, slot, c, on, acc);
+  }
+  const double part = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+  double tot = 0.0;
+  for (int u = 0; u < slots; ++u) tot += __shfl(part, (c + u * s) & 63);
+  if (slot == 0) Y[row * ldy + c] = tot + eta * X[row * ldx + c];
 }
 
 // partial[b][j][c] = sum over this block's rows of A_j[i][c] * B[i][c],
@@ -65,14 +97,29 @@ __global__ __launch_bounds__(256) void col_dot_partial_kernel(const double* __re
   }
 }
 
-// out[j][c] = sum_b partial[b][j][c]   (one thread per (j, c), fixed order)
-__global__ void col_dot_reduce_kernel(const double* __restrict__ partial, int nblk, int J, int s,
-                                      double* __restrict__ out) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= J * s) return;
+// Fixed-order wave reduction of v over the 64 lanes (xor butterfly).
+__device__ __forceinline__ double wave_sum(double v) {
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  return v;
+}
+
+// sum_b partial[b * stride + e], b < nblk, by one wave (nblk strided over lanes).
+__device__ __forceinline__ double wave_reduce_partials(const double* __restrict__ partial,
+                                                       int nblk, int64_t stride, int e) {
+  const int lane = threadIdx.x & 63;
   double v = 0.0;
-  for (int b = 0; b < nblk; ++b) v += partial[(int64_t)b * J * s + e];
-  out[e] = v;
+  for (int b = lane; b < nblk; b += 64) v += partial[(int64_t)b * stride + e];
+  return wave_sum(v);
+}
+
+// out[j][c] = sum_b partial[b][j][c]: one wave per output element (fixed order).
+__global__ __launch_bounds__(256) void col_dot_reduce_kernel(const double* __restrict__ partial,
+                                                             int nblk, int J, int s,
+                                                             double* __restrict__ out) {
+  const int e = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (e >= J * s) return;
+  const double v = wave_reduce_partials(partial, nblk, (int64_t)J * s, e);
+  if ((threadIdx.x & 63) == 0) out[e] = v;
 }
 
 // W[i][c] = alpha * W[i][c] - sum_{j<J} A_j[i][c] * H[j][c]   (H on the device)
@@ -132,39 +179,79 @@ __global__ __launch_bounds__(256) void rademacher_kernel(double* __restrict__ V,
 //
 // Scalar state (device, double): see MsState below; one column c per CG.
 // ---------------------------------------------------------------------------
-// partial[blk][e]: e = c' * s + c < s*s -> sum_i B[i][c'] R[i][c]; e = s*s + c -> R_c . R_c.
-// Rows are staged through LDS 64 at a time; thread e (and e + 256) owns one output.
+// partial[blk][e]: e = c' * S + c < S*S -> sum_i B[i][c'] R[i][c]; e = S*S + c -> R_c . R_c.
+// One thread per row (grid-stride), the row's S values of R in registers;
+// blockIdx.y selects four B columns c' (group 0 also forms R.R), so a thread
+// holds at most 4*S + S accumulators. Block sums: wave butterflies, then the
+// four waves in order (deterministic).
+template <int S>
 __global__ __launch_bounds__(256) void ms_dots_partial_kernel(const double* __restrict__ B,
                                                               const double* __restrict__ R,
-                                                              int64_t n, int s,
+                                                              int64_t n,
                                                               double* __restrict__ partial) {
-  __shared__ double sB[64 * MS_MAXS], sR[64 * MS_MAXS];
-  const int t = threadIdx.x;
-  const int ne = s * s + s;
-  double acc0 = 0.0, acc1 = 0.0;
-  for (int64_t r0 = (int64_t)blockIdx.x * 64; r0 < n; r0 += (int64_t)gridDim.x * 64) {
-    const int rows = (int)((n - r0) < 64 ? (n - r0) : 64);
-    for (int e = t; e < rows * s; e += 256) {
-      sB[e] = B[r0 * s + e];
-      sR[e] = R[r0 * s + e];
-    }
-    __syncthreads();
-    for (int h = 0; h < 2; ++h) {
-      const int e = t + h * 256;
-      if (e < ne) {
-        const double* X = e < s * s ? sB : sR;
-        const int cx = e < s * s ? e / s : e - s * s;
-        const int cy = e < s * s ? e % s : e - s * s;
-        double v = 0.0;
-        for (int r = 0; r < rows; ++r) v += X[r * s + cx] * sR[r * s + cy];
-        if (h == 0) acc0 += v;
-        else acc1 += v;
-      }
-    }
-    __syncthreads();
+  constexpr int NE = S * S + S;
+  __shared__ double red[4][4 * S + S];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int c0 = blockIdx.y * 4;
+  double acc[4][S], rr[S];
+#pragma unroll
+  for (int c = 0; c < S; ++c) {
+    rr[c] = 0.0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[q][c] = 0.0;
   }
-  if (t < ne) partial[(int64_t)blockIdx.x * ne + t] = acc0;
-  if (t + 256 < ne) partial[(int64_t)blockIdx.x * ne + t + 256] = acc1;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + t; i < n; i += (int64_t)gridDim.x * 256) {
+    double r[S], b[4];
+#pragma unroll
+    for (int c = 0; c < S; ++c) r[c] = R[i * S + c];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) b[q] = (c0 + q < S) ? B[i * S + c0 + q] : 0.0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int c = 0; c < S; ++c) acc[q][c] += b[q] * r[c];
+    if (blockIdx.y == 0) {
+#pragma unroll
+      for (int c = 0; c < S; ++c) rr[c] += r[c] * r[c];
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int c = 0; c < S; ++c) {
+      const double v = wave_sum(acc[q][c]);
+      if (lane == 0) red[wv][q * S + c] = v;
+    }
+#pragma unroll
+  for (int c = 0; c < S; ++c) {
+    const double v = wave_sum(rr[c]);
+    if (lane == 0) red[wv][4 * S + c] = v;
+  }
+  __syncthreads();
+  if (t < 5 * S) {
+    const double v = (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]);
+    if (t < 4 * S) {
+      const int q = t / S, c = t - q * S;
+      if (c0 + q < S) partial[(int64_t)blockIdx.x * NE + (c0 + q) * S + c] = v;
+    } else if (blockIdx.y == 0) {
+      partial[(int64_t)blockIdx.x * NE + S * S + (t - 4 * S)] = v;
+    }
+  }
+}
+
+// Host-side dispatch over the instantiated widths.
+void launch_ms_dots(const double* B, const double* R, int64_t n, int s, double* partial,
+                    int nblk, hipStream_t st) {
+  const dim3 grid(nblk, (s + 3) / 4), blk(256);
+  switch (s) {
+#define MS_CASE(k) \
+  case k: hipLaunchKernelGGL(ms_dots_partial_kernel<k>, grid, blk, 0, st, B, R, n, partial); break;
+    MS_CASE(1) MS_CASE(2) MS_CASE(3) MS_CASE(4) MS_CASE(5) MS_CASE(6) MS_CASE(7) MS_CASE(8)
+    MS_CASE(9) MS_CASE(10) MS_CASE(11) MS_CASE(12) MS_CASE(13) MS_CASE(14) MS_CASE(15)
+    MS_CASE(16)
+#undef MS_CASE
+    default: break;
+  }
 }
 
 // Scalar step 1 (one thread per column): alpha_c = rr_c / (p_c . A p_c).
@@ -192,10 +279,12 @@ __global__ void ms_scalar_kernel(MsState st, const double* __restrict__ partial,
                                  double* __restrict__ beta_out) {
   __shared__ double br[MS_MAXS * MS_MAXS + MS_MAXS];
   const int ne = s * s + s;
-  for (int e = threadIdx.x; e < ne; e += blockDim.x) {
-    double v = 0.0;
-    for (int b = 0; b < nblk; ++b) v += partial[(int64_t)b * ne + e];
-    br[e] = v;
+  {
+    const int nw = blockDim.x >> 6, wv = threadIdx.x >> 6;
+    for (int e = wv; e < ne; e += nw) {
+      const double v = wave_reduce_partials(partial, nblk, ne, e);
+      if ((threadIdx.x & 63) == 0) br[e] = v;
+    }
   }
   __syncthreads();
   const int t = threadIdx.x;
@@ -247,10 +336,12 @@ __global__ void ms_init_kernel(MsState st, const double* __restrict__ partial, i
                                int s) {
   __shared__ double br[MS_MAXS * MS_MAXS + MS_MAXS];
   const int ne = s * s + s;
-  for (int e = threadIdx.x; e < ne; e += blockDim.x) {
-    double v = 0.0;
-    for (int b = 0; b < nblk; ++b) v += partial[(int64_t)b * ne + e];
-    br[e] = v;
+  {
+    const int nw = blockDim.x >> 6, wv = threadIdx.x >> 6;
+    for (int e = wv; e < ne; e += nw) {
+      const double v = wave_reduce_partials(partial, nblk, ne, e);
+      if ((threadIdx.x & 63) == 0) br[e] = v;
+    }
   }
   __syncthreads();
   const int t = threadIdx.x;

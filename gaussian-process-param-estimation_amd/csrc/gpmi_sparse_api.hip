@@ -32,7 +32,8 @@ __global__ void col_gs_update_kernel(double*, const double*, int64_t, const doub
 __global__ void col_axpby_kernel(const double*, double*, const double*, const double*, int64_t,
                                  int);
 __global__ void rademacher_kernel(double*, int64_t, int, unsigned long long, int, double);
-__global__ void ms_dots_partial_kernel(const double*, const double*, int64_t, int, double*);
+void launch_ms_dots(const double* B, const double* R, int64_t n, int s, double* partial, int nblk,
+                    hipStream_t st);
 __global__ void ms_alpha_kernel(MsState, const double*, int);
 __global__ void ms_r_update_kernel(double*, const double*, const double*, int64_t, int);
 __global__ void ms_scalar_kernel(MsState, const double*, int, const double*, int, int, double,
@@ -68,6 +69,7 @@ namespace {
 
 constexpr int NBLK = 256;   // fixed reduction grid (deterministic sums)
 constexpr int MAXS = 32;    // vector-block width per device pass
+constexpr int MS_NBLK = 128; // row blocks of the multi-shift dot partials
 
 struct Guard {
   int prev = -1;
@@ -82,11 +84,6 @@ struct Guard {
   }
 };
 
-int next_pow2(int s) {
-  int p = 1;
-  while (p < s) p <<= 1;
-  return p;
-}
 
 }  // namespace
 
@@ -131,7 +128,7 @@ int ensure_partial(gpmi_sp* sp, size_t doubles) {
 int spmm(gpmi_sp* sp, const double* X, double* Y, int s, double eta) {
   hipLaunchKernelGGL(csr_spmm_kernel, dim3((unsigned)((sp->n + 3) / 4)), dim3(256), 0,
                      sp->stream, sp->indptr, sp->indices, sp->data, sp->n, X, (int64_t)s, Y,
-                     (int64_t)s, s, next_pow2(s), eta);
+                     (int64_t)s, s, 64 / s, eta);
   SP_LAUNCH("csr_spmm_kernel");
   return 0;
 }
@@ -144,7 +141,7 @@ int col_dots(gpmi_sp* sp, const double* A, int64_t strideA, int J, const double*
   hipLaunchKernelGGL(col_dot_partial_kernel, dim3(NBLK, J), dim3(256), 0, sp->stream, A, strideA,
                      B, sp->n, s, sp->partial);
   SP_LAUNCH("col_dot_partial_kernel");
-  hipLaunchKernelGGL(col_dot_reduce_kernel, dim3((J * s + 255) / 256), dim3(256), 0, sp->stream,
+  hipLaunchKernelGGL(col_dot_reduce_kernel, dim3((J * s + 3) / 4), dim3(256), 0, sp->stream,
                      sp->partial, NBLK, J, s, out);
   SP_LAUNCH("col_dot_reduce_kernel");
   return 0;
@@ -546,10 +543,9 @@ int gpmi_sp_msgram(gpmi_sp* sp, const double* etas, int neta, const double* rhs,
     SP_TRY(hipStreamSynchronize(str));
   }
   const unsigned sthreads = (unsigned)((S * s + 63) / 64 * 64);
-  hipLaunchKernelGGL(ms_dots_partial_kernel, dim3(NBLK), dim3(256), 0, str, Bd, Rd, n, s,
-                     sp->partial);
+  launch_ms_dots(Bd, Rd, n, s, sp->partial, MS_NBLK, str);
   SP_LAUNCH("ms_dots_partial_kernel");
-  hipLaunchKernelGGL(ms_init_kernel, dim3(1), dim3(sthreads), 0, str, st, sp->partial, NBLK, S,
+  hipLaunchKernelGGL(ms_init_kernel, dim3(1), dim3(sthreads), 0, str, st, sp->partial, MS_NBLK, S,
                      s);
   SP_LAUNCH("ms_init_kernel");
   int it = 0;
@@ -571,10 +567,9 @@ int gpmi_sp_msgram(gpmi_sp* sp, const double* etas, int neta, const double* rhs,
     hipLaunchKernelGGL(ms_r_update_kernel, dim3(grid_ns(n, s)), dim3(256), 0, str, Rd, Qd, st.a,
                        n, s);
     SP_LAUNCH("ms_r_update_kernel");
-    hipLaunchKernelGGL(ms_dots_partial_kernel, dim3(NBLK), dim3(256), 0, str, Bd, Rd, n, s,
-                       sp->partial);
+    launch_ms_dots(Bd, Rd, n, s, sp->partial, MS_NBLK, str);
     SP_LAUNCH("ms_dots_partial_kernel");
-    hipLaunchKernelGGL(ms_scalar_kernel, dim3(1), dim3(sthreads), 0, str, st, sp->partial, NBLK,
+    hipLaunchKernelGGL(ms_scalar_kernel, dim3(1), dim3(sthreads), 0, str, st, sp->partial, MS_NBLK,
                        dshift, S, s, rtol * rtol, beta_out);
     SP_LAUNCH("ms_scalar_kernel");
     hipLaunchKernelGGL(ms_p_update_kernel, dim3(grid_ns(n, s)), dim3(256), 0, str, Pd, Rd, st.beta,
