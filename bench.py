@@ -40,10 +40,12 @@ def parse():
     ap.add_argument('--warmup', type=int, default=2)
     ap.add_argument('--grid', type=int, default=128, help='points per axis (n = grid^2)')
     ap.add_argument('--nu', type=float, default=1.5)
-    ap.add_argument('--eta-per-rank', type=int, default=8)
-    ap.add_argument('--outer', type=int, default=4, help='outer panel width / 128')
-    ap.add_argument('--lanes', type=int, default=1,
-                    help='1 or 2 concurrent half-batches (HIP streams) per device call')
+    ap.add_argument('--eta-per-rank', type=int, default=16,
+                    help='eta values factorized together per device call (one step)')
+    ap.add_argument('--outer', type=int, default=16, help='outer panel width / 128')
+    ap.add_argument('--lookahead', type=int, default=0,
+                    help='1: panel factorization on a second stream overlaps the bulk '
+                         'trailing update; 0: one stream, in order')
     ap.add_argument('--config', default='dense', choices=['dense', 'sparse4', 'sparse5'],
                     help='dense: the headline N=16384 metric; sparse4/sparse5: BASELINE '
                          'configs 4 and 5 (tapered Matern, SLQ + CG)')
@@ -51,6 +53,26 @@ def parse():
     ap.add_argument('--no-timing', action='store_true',
                     help='skip the per-kernel HIP-event roofline timing')
     return ap.parse_args()
+
+
+def pmc_traffic(outer, batch, kernel='gpmi::syrk_kernel'):
+    """HBM-side bytes per launch of `kernel` from the committed rocprofv3 PMC
+    summary of this configuration (profiles/r*/pmc_traffic_outer{outer}_b{batch}.json,
+    FETCH_SIZE and WRITE_SIZE collected in separate passes; FETCH_SIZE doubled
+    for gfx950 wide streaming reads per MI355X_MICROARCH.md 'HBM'). PMC counters
+    cannot be collected inside the timed run, hence the committed file; None
+    when no summary matches."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, 'profiles', 'r*',
+                                          'pmc_traffic_outer%d_b%d.json' % (outer, batch))))
+    if not files:
+        return None, None
+    with open(files[-1]) as fh:
+        k = json.load(fh)['kernels'].get(kernel)
+    if not k:
+        return None, None
+    pd = k['per_dispatch']
+    return (2.0 * pd['FETCH_SIZE'] + pd['WRITE_SIZE']) * 1024.0, os.path.relpath(files[-1], REPO)
 
 
 def cpu_baseline(points, z, X, nu, etas):
@@ -234,7 +256,7 @@ def main():
                              max_batch=B)
     op = MixedCorrelation(D)
     op.op.set_outer(args.outer)
-    op.op.set_lanes(args.lanes)
+    op.op.set_lookahead(args.lookahead)
     op.set_rhs(X, z)
     grid = numpy.logspace(-3, 3, 64)
 
@@ -283,12 +305,20 @@ def main():
     if rank == 0:
         roof = None
         if not args.no_timing and timing['syrk_ms'] > 0:
-            # flops over the union of the syrk launch intervals (= the sum of the
-            # launch durations when lanes = 1, launches never overlap)
-            achieved = timing['syrk_flops'] / (timing['syrk_busy_ms'] * 1e-3) / 1e12
+            # algorithmic flops per launch / average launch duration (HIP events on
+            # the launching stream) = total flops / summed launch time; with
+            # --lookahead 1 launches on the two streams can overlap and busy_ms
+            # (their union) is the shorter wall time
+            achieved = timing['syrk_flops'] / (timing['syrk_ms'] * 1e-3) / 1e12
+            traffic, tsrc = pmc_traffic(args.outer, B)
             roof = {'bound': 'mfma', 'achieved': round(achieved, 3),
                     'peak': FP64_MFMA_PEAK_TFLOPS, 'unit': 'TFLOP/s',
-                    'frac': round(achieved / FP64_MFMA_PEAK_TFLOPS, 4), 'traffic': None,
+                    'frac': round(achieved / FP64_MFMA_PEAK_TFLOPS, 4),
+                    'traffic': None if traffic is None else round(traffic),
+                    'traffic_unit': 'bytes per launch (HBM side, PMC)',
+                    'traffic_source': tsrc,
+                    'algorithmic_flops_per_launch': round(timing['syrk_flops']
+                                                          / max(1, timing['syrk_launches'])),
                     'kernel': 'syrk_kernel (trailing update, fp64 MFMA 16x16x4)',
                     'launches': timing['syrk_launches'],
                     'avg_launch_ms': round(timing['syrk_ms'] / max(1, timing['syrk_launches']), 4),
@@ -313,7 +343,7 @@ def main():
             'config': {'workload': 'cfg3: N=%d 2D grid Matern nu=%g rho=0.1, eta grid '
                                    'logspace(-3,3,64), %d eta/rank/step' % (n, args.nu, B),
                        'n': n, 'm': m, 'eta_per_rank_per_step': B,
-                       'outer_panel': 128 * args.outer, 'lanes': args.lanes,
+                       'outer_panel': 128 * args.outer, 'lookahead': args.lookahead,
                        'parallelism': 'eta-shard x%d + all-gather' % world},
             'roofline': roof,
             'whole_eval_tflops_per_gpu': round(whole, 3),

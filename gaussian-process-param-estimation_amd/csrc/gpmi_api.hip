@@ -11,7 +11,10 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <array>
+#include <map>
 #include <vector>
 
 #include "gpmi_internal.h"
@@ -70,11 +73,14 @@ struct gpmi_op {
   int64_t n = 0, n_pad = 0;
   int nt = 0;
   int max_batch = 1;
-  int outer = 4;
-  int lanes = 1;                       // concurrent half-batches (streams) per call
+  int outer = 16;                      // outer panel width in 128-column tiles
+  int lookahead = 0;                   // 1: panel chain on stream2 beside the bulk update
   hipStream_t stream = nullptr;
-  hipStream_t stream2 = nullptr;       // second lane
+  hipStream_t stream2 = nullptr;       // high-priority panel stream (look-ahead)
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  std::vector<hipEvent_t> ev_panel, ev_rest;  // per outer panel (look-ahead)
+  bool dry = false;                    // schedule dry run: collect SYRK shapes only
+  std::vector<std::pair<int, int>> shapes;
   double* K = nullptr;       // [n_pad][n_pad]
   double* A = nullptr;       // [max_batch][n_pad][n_pad]
   double* R = nullptr;       // [max_batch][n_pad][16]
@@ -93,6 +99,10 @@ struct gpmi_op {
   double* tpart = nullptr;   // [nt * (nt + 1) / 2 + nt * nt] traceinv partials
   double* Td = nullptr;      // [nt][128][128] diagonal tiles of A^-1 (traceinv exponent 2)
   int* info = nullptr;       // [max_batch]
+  // grouped syrk tile orders, one per trailing-update shape (w, t) of the schedule
+  uint32_t* order = nullptr;
+  int order_nt = -1, order_outer = -1, order_la = -1, group = 8;
+  std::map<std::pair<int, int>, int64_t> order_off;
   int nrhs = 0;
   bool has_K = false;
   // factor cache: batch slot 0 holds the factor of K + cached_eta I
@@ -110,6 +120,7 @@ struct gpmi_op {
   double last_syrk_ms = 0.0, last_syrk_flops = 0.0, last_total_ms = 0.0;
   int last_syrk_launches = 0;
   std::vector<std::pair<int, double>> syrk_log;  // (event index, flops)
+  std::vector<std::array<int, 3>> syrk_shape;    // (w, t, kdim) per logged launch
   double last_syrk_busy_ms = 0.0;                // union of syrk launch intervals
 
   BatchPtrs ptrs() const {
@@ -133,11 +144,29 @@ struct gpmi_op {
 
 namespace {
 
+// Lower-triangular tiles of a band (w tile columns over t tile rows) in row
+// groups of G rows, column-major inside a group, packed (i << 16) | j. The
+// 32 CUs x 2 workgroups in flight on one XCD then cover ~G rows x (64/G)
+// columns, so each operand slab is re-read from that XCD's L2, not from the
+// Infinity Cache / HBM.
+void grouped_order(int w, int t, int G, std::vector<uint32_t>* out) {
+  for (int r0 = 0; r0 < t; r0 += G) {
+    const int r1 = std::min(t, r0 + G);
+    const int jmax = std::min(r1 - 1, w - 1);
+    for (int j = 0; j <= jmax; ++j)
+      for (int i = std::max(r0, j); i < r1; ++i) out->push_back(((uint32_t)i << 16) | j);
+  }
+}
+
 int launch_syrk(gpmi_op* op, hipStream_t st, int b0, int nb, int tc0, int w, int t, int p0,
                 int kdim) {
   const int tri = w * (w + 1) / 2;
   const int tiles = tri + (t - w) * w;
   if (tiles <= 0 || nb <= 0) return 0;
+  if (op->dry) {
+    op->shapes.push_back({w, t});
+    return 0;
+  }
   int evi = -1;
   if (op->timing) {
     evi = (int)op->syrk_log.size() * 2;
@@ -150,9 +179,14 @@ int launch_syrk(gpmi_op* op, hipStream_t st, int b0, int nb, int tc0, int w, int
     }
     HIP_TRY(hipEventRecord(op->ev[evi], st));
   }
+  const uint32_t* order = nullptr;
+  if (op->order && w > 1) {
+    auto it = op->order_off.find({w, t});
+    if (it != op->order_off.end()) order = op->order + it->second;
+  }
   hipLaunchKernelGGL(syrk_kernel, dim3(tiles, nb), dim3(256), 0, st,
                      op->A + (int64_t)b0 * op->n_pad * op->n_pad, (int64_t)op->n_pad,
-                     op->n_pad * op->n_pad, tc0, w, t, p0, kdim);
+                     op->n_pad * op->n_pad, tc0, w, t, p0, kdim, order);
   LAUNCH_CHECK("syrk_kernel");
   if (op->timing) {
     HIP_TRY(hipEventRecord(op->ev[evi + 1], st));
@@ -161,20 +195,128 @@ int launch_syrk(gpmi_op* op, hipStream_t st, int b0, int nb, int tc0, int w, int
     const double diag = (double)std::min(tiles, w) * TS * (TS + 1) / 2.0;
     const double fl = 2.0 * (offd + diag) * kdim * nb;
     op->syrk_log.push_back({evi, fl});
+    op->syrk_shape.push_back({w, t, kdim});
   }
   return 0;
 }
 
-BatchPtrs offset_ptrs(const BatchPtrs& P, int b0) {
-  BatchPtrs q = P;
-  q.A += b0 * P.sA;
-  q.R += b0 * P.sR;
-  q.U += b0 * P.sU;
-  q.Linv += b0 * P.sL;
-  q.logdiag += b0 * P.sLD;
-  q.gram += b0 * P.sG;
-  q.info += b0;
-  return q;
+// Recursive panel factorization of tile columns [c0, c0 + W) (all contributions
+// of columns < c0 already applied): factor the left half, update the right half
+// from it (a band SYRK with kdim = half width), factor the right half. A single
+// column is the diagonal-block kernel (Cholesky, inverse, fused forward solve,
+// logdet / Gram partials) followed by the panel kernel (L_ik and r_i updates).
+int factor_panel(gpmi_op* op, const BatchPtrs& P, int nb, hipStream_t st, int c0, int W) {
+  const int nt = op->nt;
+  if (W == 1) {
+    if (op->dry) return 0;
+    hipLaunchKernelGGL(diag_block_kernel, dim3(nb), dim3(256), 0, st, P, (int64_t)op->n_pad,
+                       c0, nt);
+    LAUNCH_CHECK("diag_block_kernel");
+    if (c0 + 1 < nt) {
+      hipLaunchKernelGGL(panel_kernel, dim3(nt - c0 - 1, nb), dim3(256), 0, st, P,
+                         (int64_t)op->n_pad, c0);
+      LAUNCH_CHECK("panel_kernel");
+    }
+    return 0;
+  }
+  const int h = W / 2;
+  int rc = factor_panel(op, P, nb, st, c0, h);
+  if (rc) return rc;
+  rc = launch_syrk(op, st, 0, nb, c0 + h, W - h, nt - c0 - h, c0 * TS, h * TS);
+  if (rc) return rc;
+  return factor_panel(op, P, nb, st, c0 + h, W - h);
+}
+
+int get_event(std::vector<hipEvent_t>* v, size_t i, hipEvent_t* out) {
+  while (v->size() <= i) {
+    hipEvent_t e;
+    HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    v->push_back(e);
+  }
+  *out = (*v)[i];
+  return 0;
+}
+
+// The blocked factorization schedule over outer panels P_k of `outer` tile
+// columns. Without look-ahead everything runs in order on op->stream: factor
+// P_k, then one trailing SYRK over all columns right of it (kdim = 128 * outer).
+// With look-ahead the panel chain runs on the high-priority op->stream2:
+//   stream2: factor(P_k) -> [wait U_rest(k-1)] -> U_next(k): P_{k+1}'s columns
+//   stream : [wait factor(P_k)] -> U_rest(k): columns right of P_{k+1}
+// so the latency-bound factorization of P_{k+1} overlaps the bulk update U_rest(k).
+// U_rest(k-1) and U_next(k) both write P_{k+1}'s columns, hence the wait.
+int schedule(gpmi_op* op, const BatchPtrs& P, int nb) {
+  const int nt = op->nt, O = op->outer;
+  const bool la = op->lookahead && !op->dry;
+  hipStream_t A = op->stream, B = la ? op->stream2 : op->stream;
+  bool have_rest_prev = false;
+  hipEvent_t ev_rest_prev = nullptr;
+  int np = 0;
+  for (int c0 = 0; c0 < nt; c0 += O, ++np) {
+    const int W = std::min(O, nt - c0);
+    int rc = factor_panel(op, P, nb, B, c0, W);
+    if (rc) return rc;
+    const int c1 = c0 + W;
+    if (c1 >= nt) break;
+    if (!op->lookahead) {
+      rc = launch_syrk(op, A, 0, nb, c1, nt - c1, nt - c1, c0 * TS, W * TS);
+      if (rc) return rc;
+      continue;
+    }
+    const int c2 = c1 + std::min(O, nt - c1);
+    bool have_rest = false;
+    hipEvent_t ev_f = nullptr, ev_r = nullptr;
+    if (c2 < nt) {
+      if (la) {
+        if ((rc = get_event(&op->ev_panel, np, &ev_f))) return rc;
+        HIP_TRY(hipEventRecord(ev_f, B));
+        HIP_TRY(hipStreamWaitEvent(A, ev_f, 0));
+      }
+      rc = launch_syrk(op, A, 0, nb, c2, nt - c2, nt - c2, c0 * TS, W * TS);
+      if (rc) return rc;
+      if (la) {
+        if ((rc = get_event(&op->ev_rest, np, &ev_r))) return rc;
+        HIP_TRY(hipEventRecord(ev_r, A));
+      }
+      have_rest = true;
+    }
+    if (la && have_rest_prev) HIP_TRY(hipStreamWaitEvent(B, ev_rest_prev, 0));
+    rc = launch_syrk(op, B, 0, nb, c1, c2 - c1, nt - c1, c0 * TS, W * TS);
+    if (rc) return rc;
+    have_rest_prev = have_rest;
+    ev_rest_prev = ev_r;
+  }
+  return 0;
+}
+
+// Trailing-update shapes (w, t) the schedule launches, from a dry run.
+int ensure_order(gpmi_op* op) {
+  if (op->group <= 0) return 0;
+  if (op->order && op->order_nt == op->nt && op->order_outer == op->outer &&
+      op->order_la == op->lookahead)
+    return 0;
+  if (op->order) HIP_TRY(hipFree(op->order));
+  op->order = nullptr;
+  op->order_off.clear();
+  op->dry = true;
+  op->shapes.clear();
+  BatchPtrs P = op->ptrs();
+  int rc = schedule(op, P, 1);
+  op->dry = false;
+  if (rc) return rc;
+  std::vector<uint32_t> h;
+  for (auto& wt : op->shapes) {
+    if (wt.first < 2 || op->order_off.count(wt)) continue;
+    op->order_off[wt] = (int64_t)h.size();
+    grouped_order(wt.first, wt.second, op->group, &h);
+  }
+  if (h.empty()) h.push_back(0);
+  HIP_TRY(hipMalloc(&op->order, sizeof(uint32_t) * h.size()));
+  HIP_TRY(hipMemcpy(op->order, h.data(), sizeof(uint32_t) * h.size(), hipMemcpyHostToDevice));
+  op->order_nt = op->nt;
+  op->order_outer = op->outer;
+  op->order_la = op->lookahead;
+  return 0;
 }
 
 // Factor K + eta_b I for b < nb, with the fused forward substitution of the
@@ -188,7 +330,12 @@ int run_factor(gpmi_op* op, const double* etas_host, int nb, const double* rhs_d
   const int nt = op->nt;
   const int64_t lda = op->n_pad;
   BatchPtrs P = op->ptrs();
+  {
+    int rc = ensure_order(op);
+    if (rc) return rc;
+  }
   op->syrk_log.clear();
+  op->syrk_shape.clear();
   op->cache_valid = false;
   ++op->factor_gen;
   if (op->timing) {
@@ -206,50 +353,13 @@ int run_factor(gpmi_op* op, const double* etas_host, int nb, const double* rhs_d
     HIP_TRY(hipMemcpyAsync(op->R + b * P.sR, rhs_dev, sizeof(double) * P.sR,
                            hipMemcpyDeviceToDevice, s));
   HIP_TRY(hipMemsetAsync(op->info, 0, sizeof(int) * nb, s));
-  // lanes: the batch is split into halves factorized on two streams, so one
-  // half's latency-bound diagonal/panel chain overlaps the other's trailing update.
-  const int L = (op->lanes > 1 && nb > 1 && op->stream2) ? 2 : 1;
-  const int nb0 = L == 2 ? (nb + 1) / 2 : nb;
-  const int lb0[2] = {0, nb0};
-  const int lnb[2] = {nb0, nb - nb0};
-  hipStream_t ls[2] = {s, op->stream2};
-  if (L == 2) {
+  if (op->lookahead) {
     HIP_TRY(hipEventRecord(op->ev_fork, s));
     HIP_TRY(hipStreamWaitEvent(op->stream2, op->ev_fork, 0));
   }
-  int kb = 0;
-  while (kb < nt) {
-    const int S = std::min(op->outer, nt - kb);
-    for (int sp = 0; sp < S; ++sp) {
-      const int j = kb + sp;
-      if (sp > 0)
-        for (int l = 0; l < L; ++l) {
-          int rc = launch_syrk(op, ls[l], lb0[l], lnb[l], j, 1, nt - j, kb * TS, sp * TS);
-          if (rc) return rc;
-        }
-      for (int l = 0; l < L; ++l) {
-        hipLaunchKernelGGL(diag_block_kernel, dim3(lnb[l]), dim3(256), 0, ls[l],
-                           offset_ptrs(P, lb0[l]), lda, j, nt);
-        LAUNCH_CHECK("diag_block_kernel");
-      }
-      if (j + 1 < nt)
-        for (int l = 0; l < L; ++l) {
-          hipLaunchKernelGGL(panel_kernel, dim3(nt - j - 1, lnb[l]), dim3(256), 0, ls[l],
-                             offset_ptrs(P, lb0[l]), lda, j);
-          LAUNCH_CHECK("panel_kernel");
-        }
-    }
-    const int tc0 = kb + S;
-    if (tc0 < nt) {
-      const int t = nt - tc0;
-      for (int l = 0; l < L; ++l) {
-        int rc = launch_syrk(op, ls[l], lb0[l], lnb[l], tc0, t, t, kb * TS, S * TS);
-        if (rc) return rc;
-      }
-    }
-    kb += S;
-  }
-  if (L == 2) {
+  int rc = schedule(op, P, nb);
+  if (rc) return rc;
+  if (op->lookahead) {
     HIP_TRY(hipEventRecord(op->ev_join, op->stream2));
     HIP_TRY(hipStreamWaitEvent(s, op->ev_join, 0));
   }
@@ -272,6 +382,24 @@ int collect_timing(gpmi_op* op) {
     iv.push_back({t0, t1});
     tot += ms;
     fl += pr.second;
+  }
+  if (std::getenv("GPMI_SYRK_TRACE")) {
+    // dev aid: SYRK time by class (bulk trailing update w == t vs band w < t) and kdim
+    std::map<std::pair<int, int>, std::array<double, 3>> cls;
+    for (size_t i = 0; i < op->syrk_log.size(); ++i) {
+      const auto& sh = op->syrk_shape[i];
+      float ms = 0.f;
+      HIP_TRY(hipEventElapsedTime(&ms, op->ev[op->syrk_log[i].first],
+                                  op->ev[op->syrk_log[i].first + 1]));
+      auto& c = cls[{sh[0] == sh[1] ? 1 : 0, sh[2]}];
+      c[0] += 1;
+      c[1] += ms;
+      c[2] += op->syrk_log[i].second;
+    }
+    for (auto& kv : cls)
+      fprintf(stderr, "[gpmi syrk] %s kdim=%4d launches=%3.0f ms=%8.3f TF/s=%6.2f\n",
+              kv.first.first ? "bulk" : "band", kv.first.second, kv.second[0], kv.second[1],
+              kv.second[2] / (kv.second[1] * 1e-3) / 1e12);
   }
   std::sort(iv.begin(), iv.end());
   double busy = 0.0, cs = -1.0, ce = -1.0;
@@ -424,6 +552,7 @@ int gpmi_op_create(int device, int64_t n, int max_batch, gpmi_op** out) {
   op->n_pad = (n + TS - 1) / TS * TS;
   op->nt = (int)(op->n_pad / TS);
   op->max_batch = max_batch;
+  if (const char* g = std::getenv("GPMI_SYRK_GROUP")) op->group = std::atoi(g);
   const int64_t np = op->n_pad;
   auto fail = [&](hipError_t e, const char* what) {
     gpmi_op_destroy(op);
@@ -432,8 +561,12 @@ int gpmi_op_create(int device, int64_t n, int max_batch, gpmi_op** out) {
   hipError_t e;
   if ((e = hipStreamCreateWithFlags(&op->stream, hipStreamNonBlocking)) != hipSuccess)
     return fail(e, "stream");
-  if ((e = hipStreamCreateWithFlags(&op->stream2, hipStreamNonBlocking)) != hipSuccess)
-    return fail(e, "stream2");
+  {
+    int lo = 0, hi = 0;
+    if ((e = hipDeviceGetStreamPriorityRange(&lo, &hi)) != hipSuccess) return fail(e, "priority");
+    if ((e = hipStreamCreateWithPriority(&op->stream2, hipStreamNonBlocking, hi)) != hipSuccess)
+      return fail(e, "stream2");
+  }
   if ((e = hipEventCreateWithFlags(&op->ev_fork, hipEventDisableTiming)) != hipSuccess)
     return fail(e, "event");
   if ((e = hipEventCreateWithFlags(&op->ev_join, hipEventDisableTiming)) != hipSuccess)
@@ -475,9 +608,12 @@ int gpmi_op_destroy(gpmi_op* op) {
   for (double* p : bufs)
     if (p) (void)hipFree(p);
   if (op->info) (void)hipFree(op->info);
+  if (op->order) (void)hipFree(op->order);
   for (auto e : op->ev) (void)hipEventDestroy(e);
   if (op->ev_begin) (void)hipEventDestroy(op->ev_begin);
   if (op->ev_end) (void)hipEventDestroy(op->ev_end);
+  for (auto e : op->ev_panel) (void)hipEventDestroy(e);
+  for (auto e : op->ev_rest) (void)hipEventDestroy(e);
   if (op->ev_fork) (void)hipEventDestroy(op->ev_fork);
   if (op->ev_join) (void)hipEventDestroy(op->ev_join);
   if (op->stream2) (void)hipStreamDestroy(op->stream2);
@@ -793,16 +929,15 @@ int gpmi_op_last_timing(gpmi_op* op, double* syrk_ms, int* syrk_launches, double
   return 0;
 }
 
-int gpmi_op_set_lanes(gpmi_op* op, int lanes) {
+int gpmi_op_set_lookahead(gpmi_op* op, int enable) {
   if (!op) return set_err(-1006, "null handle");
-  if (lanes < 1 || lanes > 2) return set_err(-1009, "lanes %d outside [1, 2]", lanes);
-  op->lanes = lanes;
+  op->lookahead = enable != 0;
   return 0;
 }
 
 int gpmi_op_set_outer(gpmi_op* op, int s) {
   if (!op) return set_err(-1006, "null handle");
-  if (s < 1 || s > 8) return set_err(-1008, "outer panel width %d outside [1, 8]", s);
+  if (s < 1 || s > 32) return set_err(-1008, "outer panel width %d outside [1, 32]", s);
   op->outer = s;
   return 0;
 }

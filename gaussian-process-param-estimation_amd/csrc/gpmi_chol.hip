@@ -111,13 +111,21 @@ __global__ __launch_bounds__(256, 2) void panel_kernel(BatchPtrs P, int64_t lda,
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256, 2) void syrk_kernel(double* A, int64_t lda, int64_t sA,
                                                       int tc0, int w, int t, int p0,
-                                                      int kdim) {
+                                                      int kdim, const uint32_t* order) {
   __shared__ double smem[4 * STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int wr = wv >> 1, wc = wv & 1, fr = lane & 15, fk = lane >> 4;
   const int q = xcd_remap(blockIdx.x, gridDim.x);
   int i, j;
-  tri_decode(q, w, &i, &j);
+  if (order) {
+    // host-built grouped order (row groups, column-major inside a group): the
+    // tiles in flight on one XCD share a few row and column slabs in its L2
+    const uint32_t o = order[q];
+    i = (int)(o >> 16);
+    j = (int)(o & 0xffffu);
+  } else {
+    tri_decode(q, w, &i, &j);
+  }
   (void)t;
   const int I = tc0 + i, J = tc0 + j;
   double* Ab = A + blockIdx.y * sA;

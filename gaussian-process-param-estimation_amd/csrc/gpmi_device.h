@@ -16,9 +16,11 @@ constexpr int BK = 16;           // k-depth of one LDS stage
 constexpr int STAGE = TS * BK;   // doubles per staged operand buffer (128 rows x 16, 16 KB)
 
 // Staged slabs are stored unpadded, [row][16 doubles], with the 16-byte chunk c
-// of row r placed at chunk position c ^ ((r >> 1) & 7). MFMA fragment reads
-// (16 consecutive rows at one k) then hit 32 distinct banks per 32-lane group,
-// and the staging ds_write_b128 of a row stays one contiguous 128-byte line.
+// of row r placed at chunk position c ^ ((r >> 1) & 7); the staging
+// ds_write_b128 of a row stays one contiguous 128-byte line. The compiler merges
+// fragment reads 16 rows apart into ds_read2st64_b64, whose 16-lane groups see
+// this layout 2-way conflicted; measured faster than the conflict-free
+// k ^ (r & 15) layout (with or without the merge) all the same.
 __device__ __forceinline__ int slab_off(int row, int k) {
   return row * BK + 2 * ((k >> 1) ^ ((row >> 1) & 7)) + (k & 1);
 }
@@ -26,6 +28,12 @@ constexpr int RLD = GPMI_RHS_LD; // 16
 
 __device__ __forceinline__ d4 mfma64(double a, double b, d4 c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+// c - a b: for f64 MFMA the BLGP field is the NEG modifier (bit 0 negates A),
+// so the subtraction costs no VALU op.
+__device__ __forceinline__ d4 mfma64_neg(double a, double b, d4 c) {
+  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 1);
 }
 
 
@@ -52,6 +60,7 @@ __device__ __forceinline__ void sstore_slab(double* s, const d2 (&r)[4]) {
   }
 }
 
+
 // acc (wave tile 64 x 64 at (wr, wc)) += P1[0:128, 0:kdim] * P2[0:128, 0:kdim]^T.
 // f64 MFMA 16x16x4 operand maps: A[i = lane&15][k = lane>>4], B[k = lane>>4][j = lane&15].
 // WITH_RHS additionally accumulates racc (rows wr*64 + wc*32 + [0,32), 16 cols)
@@ -71,6 +80,11 @@ __device__ __forceinline__ void tile_mma(const double* __restrict__ P1, int64_t 
   sstore_slab(sA, ra);
   sstore_slab(sB, rb);
   __syncthreads();
+  // Drain every global load issued before the loop (the caller's accumulator
+  // preload) here, once. Otherwise the waitcnt pass places vmcnt(3..0) waits
+  // on the first accumulator uses INSIDE the loop, which also drain the
+  // next-stage prefetch every iteration (vmcnt counts in order).
+  __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0) expcnt(7) lgkmcnt(15)
   const int nsteps = kdim / BK;
   for (int s = 0; s < nsteps; ++s) {
     const int cur = s & 1;
@@ -84,16 +98,14 @@ __device__ __forceinline__ void tile_mma(const double* __restrict__ P1, int64_t 
     for (int kk = 0; kk < BK / 4; ++kk) {
       double a[4], b[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        a[i] = cA[slab_off(wr * 64 + i * 16 + fr, kk * 4 + fk)];
-        if (NEG) a[i] = -a[i];
-      }
+      for (int i = 0; i < 4; ++i) a[i] = cA[slab_off(wr * 64 + i * 16 + fr, kk * 4 + fk)];
 #pragma unroll
       for (int j = 0; j < 4; ++j) b[j] = cB[slab_off(wc * 64 + j * 16 + fr, kk * 4 + fk)];
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = mfma64(a[i], b[j], acc[i][j]);
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = NEG ? mfma64_neg(a[i], b[j], acc[i][j]) : mfma64(a[i], b[j], acc[i][j]);
       if (WITH_RHS) {
         const double u = sU[(s * BK + kk * 4 + fk) * RLD + fr];
         const double a0 = wc ? a[2] : a[0];

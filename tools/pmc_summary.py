@@ -1,0 +1,45 @@
+"""Summarize rocprofv3 --pmc CSV passes per kernel (dev tool).
+
+usage: python tools/pmc_summary.py OUT.json NOTE dir1 [dir2 ...]
+Each dir holds one pass's *_counter_collection.csv. Per kernel name (template
+and argument list stripped) it reports dispatch count, the summed counter
+values and the per-dispatch mean; FETCH_SIZE / WRITE_SIZE are in KB as
+rocprofv3 reports them (gfx950: FETCH_SIZE counts half the bytes of wide
+coalesced streaming reads, MI355X_MICROARCH.md "HBM")."""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+
+def short(name):
+    return name.split('(')[0]
+
+
+def main():
+    out, note, dirs = sys.argv[1], sys.argv[2], sys.argv[3:]
+    acc = defaultdict(lambda: defaultdict(float))
+    disp = defaultdict(set)
+    for d in dirs:
+        for f in glob.glob(os.path.join(d, '*counter_collection.csv')):
+            with open(f) as fh:
+                for row in csv.DictReader(fh):
+                    k = short(row['Kernel_Name'])
+                    acc[k][row['Counter_Name']] += float(row['Counter_Value'])
+                    disp[k].add((f, row['Dispatch_Id']))
+    res = {'note': note, 'kernels': {}}
+    for k, cs in acc.items():
+        nd = max(1, len(disp[k]) // max(1, len(dirs)))
+        res['kernels'][k] = {'dispatches': nd,
+                             'sum': {c: v for c, v in sorted(cs.items())},
+                             'per_dispatch': {c: v / nd for c, v in sorted(cs.items())}}
+    with open(out, 'w') as fh:
+        json.dump(res, fh, indent=1)
+    for k, v in res['kernels'].items():
+        print(k, v['dispatches'], {c: '%.4g' % x for c, x in v['sum'].items()})
+
+
+if __name__ == '__main__':
+    main()
