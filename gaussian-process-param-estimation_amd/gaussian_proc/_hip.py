@@ -12,7 +12,9 @@ import os
 import numpy
 
 _LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), '_lib')
-LIB_PATH = os.path.join(_LIB_DIR, 'libgpmi.so')
+# GPMI_LIB_VARIANT=<name> loads _lib/libgpmi_<name>.so instead (kernel experiments)
+LIB_PATH = os.path.join(_LIB_DIR, 'libgpmi%s.so' % (
+    '_' + os.environ['GPMI_LIB_VARIANT'] if os.environ.get('GPMI_LIB_VARIANT') else ''))
 MAX_RHS = 16
 
 _lib = None

@@ -12,9 +12,14 @@ __global__ __launch_bounds__(256) void peak_kernel(double* out, int iters, doubl
   d4 acc[16];
   for (int i = 0; i < 16; ++i) acc[i] = d4{0.0, 0.0, 0.0, 0.0};
   double a = seed + threadIdx.x * 1e-3, b = seed - threadIdx.x * 1e-3;
-  for (int it = 0; it < iters; ++it) {
+  // 8 x 16 MFMAs per trip, so the loop-carried accumulator copies the compiler
+  // adds at the back edge are amortized
+  for (int it = 0; it < iters; it += 8) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) acc[i] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[i], 0, 0, 0);
+    for (int u = 0; u < 8; ++u)
+#pragma unroll
+      for (int i = 0; i < 16; ++i)
+        acc[i] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[i], 0, 0, 0);
   }
   double s = 0.0;
   for (int i = 0; i < 16; ++i) s += acc[i][0] + acc[i][1] + acc[i][2] + acc[i][3];
