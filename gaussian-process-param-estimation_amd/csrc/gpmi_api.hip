@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "gpmi_internal.h"
+#include "gpmi_band.h"
 #include "../../include/gpmi.h"
 
 using namespace gpmi;
@@ -450,6 +451,15 @@ int ensure_factor(gpmi_op* op, double eta, const double* rhs_dev, bool* fresh) {
 namespace gpmi {
 int matern_params_host(double nu, MaternParams* P);
 int set_error(int code, const char* msg) { return set_err(code, "%s", msg); }
+int op_view(const gpmi_op* op, OpView* v) {
+  if (!op) return set_err(-1006, "null handle");
+  v->device = op->device;
+  v->n = op->n;
+  v->n_pad = op->n_pad;
+  v->K = op->K;
+  v->has_K = op->has_K;
+  return 0;
+}
 }  // namespace gpmi
 
 extern "C" {

@@ -1,0 +1,49 @@
+// Band path (gpmi_band.hip, gpmi_band_api.hip): constants and kernel declarations.
+#pragma once
+
+#include "gpmi_internal.h"
+
+namespace gpmi {
+
+enum { KFAST = 0, KSLOW = 1 };
+
+constexpr int HH_ROWS = 256;       // panel rows per hh_col workgroup (16 waves x 16 rows)
+constexpr int HH_RPW = 16;
+constexpr int HH_MAXG = 128;       // max hh_col workgroups (n_pad <= 32768)
+constexpr int HH_PART_LD = 136;    // partial record: S_j (j < 128), sum x^2 at [128]
+constexpr int TN_CH = 1024;        // rows per tn_partial chunk
+constexpr int SY_CH = 16;          // tile columns per symm split-K chunk
+constexpr int BAND_ULD = 384;      // U = [W | V | W]
+constexpr int BAND_MAX_NPAD = HH_MAXG * HH_ROWS;
+
+__global__ void hh_col_kernel(double* P, int64_t lda, int m, int c, double* part, double* pivrow,
+                              double* tau);
+__global__ void vcopy_kernel(const double* P, int64_t lda, int m, double* U, int64_t ldu);
+__global__ void tn_partial_kernel(const double* P1, int64_t ld1, const double* P2, int64_t ld2,
+                                  int m, double* part);
+__global__ void tn_reduce_kernel(const double* part, int nch, double* out, double scale);
+__global__ void tbuild_kernel(const double* VtV, const double* tau, double* T);
+__global__ void symm_kernel(const double* A, int64_t lda, const double* U, int64_t ldu, int tr0,
+                            int mt, double* Xp);
+__global__ void psum_kernel(const double* Xp, int nch, double* X);
+__global__ void xt_kernel(double* X, const double* T);
+__global__ void z_kernel(const double* T, const double* M, double* Zh);
+__global__ void w_kernel(const double* X, double* U, int64_t ldu, const double* Zh);
+__global__ void syr2k_kernel(double* A, int64_t lda, const double* U, int64_t ldu, int tr0,
+                             int mt);
+__global__ void qt_partial_kernel(const double* P, int64_t lda, int m, const double* Y,
+                                  double* part);
+__global__ void qt_reduce_kernel(const double* part, int G, const double* T, double* b);
+__global__ void qt_apply_kernel(const double* P, int64_t lda, int m, double* Y, const double* b);
+__global__ void band_chol_kernel(const double* B, int64_t lda, int nt, int64_t n, const double* Y,
+                                 const double* etas, double* out, int out_ld, int* info);
+
+// Read-only view of an operator for the band path (gpmi_api.hip).
+struct OpView {
+  int device;
+  int64_t n, n_pad;
+  const double* K;
+  bool has_K;
+};
+
+}  // namespace gpmi

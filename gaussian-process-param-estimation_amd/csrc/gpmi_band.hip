@@ -1,0 +1,698 @@
+// Band path: one orthogonal reduction of the correlation matrix to symmetric
+// band form, K = Q B Q^T with bandwidth 128, then every eta is a banded
+// Cholesky of B + eta I (K + eta I = Q (B + eta I) Q^T for every eta).
+//
+// This is the device form of the reference's one-time spectral setup
+// (MixedCorrelation.__init__ with imate_method='eigenvalue' runs eigh(K) once,
+// gaussian_proc/_mixed_correlation/mixed_correlation.py:76-79, so that every
+// later logdet / traceinv is cheap, :172-181,239-248). Here the once-per-K work
+// is the band reduction (4/3 n^3 flops, fp64 MFMA), after which one likelihood
+// evaluation costs O(n b^2) instead of the O(n^3) factorization per eta:
+//   logdet(K + eta I)            = logdet(B + eta I)
+//   R^T (K + eta I)^-1 R         = Y^T (B + eta I)^-1 Y,   Y = Q^T R (once per RHS)
+//
+// Stage 1 (dense -> band), per panel j of 128 columns (rows r0 = 128 (j + 1) on):
+//   hh_col_kernel x 128    Householder QR of the m x 128 panel, one launch per
+//                          column (partial sums of the next column published per
+//                          workgroup; the panel rows live in registers)
+//   vcopy + tn_partial/reduce + tbuild    V (unit lower) and the compact-WY T:
+//                          T[0:c, c] = -tau_c T[0:c, 0:c] (V^T V)[0:c, c]
+//   symm -> psum -> xt     X = A22 V T (A22 lower-stored: transposed tile reads above
+//                          the diagonal), split-K partials summed deterministically
+//   tn_partial/reduce(V,X) -> z -> w      W = X - 1/2 V (T^T V^T X)
+//   syr2k                  A22 -= W V^T + V W^T on the lower tiles (kdim 256)
+// Stage 2 (per eta, band_chol_kernel): one workgroup per eta walks the 128-blocks:
+//   D_k = B_kk + eta I - C_k C_k^T;  L_kk = chol(D_k), Linv_kk (LDS, shared with
+//   the diagonal-block kernel, gpmi_lds_chol.h);  y_k = Linv_kk (Y_k - C_k y_{k-1});
+//   C_{k+1} = E_k Linv_kk^T with E_k = triu(B_{k+1,k}); logdet and Gram y^T y
+//   accumulated in registers. Nothing leaves the workgroup until the end.
+
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "gpmi_internal.h"
+#include "gpmi_device.h"
+#include "gpmi_lds_chol.h"
+#include "gpmi_band.h"
+
+namespace gpmi {
+
+// ---------------------------------------------------------------------------
+// Generic 128 x 128 tile product on fp64 MFMA with either operand layout:
+//   KFAST: op(P)[r][k] = P[r * ld + k]   (staged as the swizzled [row][16] slab)
+//   KSLOW: op(P)[r][k] = P[k * ld + r]   (staged as [16][SLD], k-major; the
+//          fragment reads of lanes 0-15 and 16-31 land 32 banks apart)
+// acc (wave tile 64 x 64 at (wr, wc)) (+|-)= op(P1)[0:128, 0:kdim] op(P2)[0:128, 0:kdim]^T.
+// Ends with a workgroup barrier (back-to-back calls may reuse smem).
+// ---------------------------------------------------------------------------
+constexpr int SLD = 144;
+constexpr int GSTAGE = 16 * SLD;   // doubles per staged operand (>= STAGE)
+
+template <int L>
+__device__ __forceinline__ void gl_op(const double* __restrict__ base, int64_t ld, int k0,
+                                      d2 (&r)[4]) {
+  if (L == KFAST) {
+    gload_slab(base, ld, k0, r);
+    return;
+  }
+  const int t = threadIdx.x, kk = t >> 4, c0 = (t & 15) * 8;
+  const double* p = base + (int64_t)(k0 + kk) * ld + c0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) r[q] = *reinterpret_cast<const d2*>(p + 2 * q);
+}
+
+template <int L>
+__device__ __forceinline__ void st_op(double* s, const d2 (&r)[4]) {
+  if (L == KFAST) {
+    sstore_slab(s, r);
+    return;
+  }
+  const int t = threadIdx.x, kk = t >> 4, c0 = (t & 15) * 8;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) *reinterpret_cast<d2*>(s + kk * SLD + c0 + 2 * q) = r[q];
+}
+
+template <int L>
+__device__ __forceinline__ double fr_op(const double* s, int row, int k) {
+  return L == KFAST ? s[slab_off(row, k)] : s[k * SLD + row];
+}
+
+template <int AL, int BL, bool NEG>
+__device__ __forceinline__ void gemm_tile(const double* __restrict__ P1, int64_t ld1,
+                                          const double* __restrict__ P2, int64_t ld2, int kdim,
+                                          double* smem, d4 (&acc)[4][4]) {
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int wr = w >> 1, wc = w & 1, fr = lane & 15, fk = lane >> 4;
+  double* sA = smem;
+  double* sB = smem + 2 * GSTAGE;
+  d2 ra[4], rb[4];
+  gl_op<AL>(P1, ld1, 0, ra);
+  gl_op<BL>(P2, ld2, 0, rb);
+  st_op<AL>(sA, ra);
+  st_op<BL>(sB, rb);
+  __syncthreads();
+  const int nsteps = kdim / BK;
+  for (int s = 0; s < nsteps; ++s) {
+    const int cur = s & 1;
+    const double* cA = sA + cur * GSTAGE;
+    const double* cB = sB + cur * GSTAGE;
+    if (s + 1 < nsteps) {
+      gl_op<AL>(P1, ld1, (s + 1) * BK, ra);
+      gl_op<BL>(P2, ld2, (s + 1) * BK, rb);
+    }
+#pragma unroll
+    for (int kk = 0; kk < BK / 4; ++kk) {
+      double a[4], b[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = fr_op<AL>(cA, wr * 64 + i * 16 + fr, kk * 4 + fk);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = fr_op<BL>(cB, wc * 64 + j * 16 + fr, kk * 4 + fk);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = NEG ? mfma64_neg(a[i], b[j], acc[i][j]) : mfma64(a[i], b[j], acc[i][j]);
+    }
+    if (s + 1 < nsteps) {
+      st_op<AL>(sA + (cur ^ 1) * GSTAGE, ra);
+      st_op<BL>(sB + (cur ^ 1) * GSTAGE, rb);
+    }
+    __syncthreads();
+  }
+}
+
+__device__ __forceinline__ void zero_tile(d4 (&acc)[4][4]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = d4{0.0, 0.0, 0.0, 0.0};
+}
+
+// C/D map of v_mfma_f64_16x16x4f64: row = (lane>>4) + 4 r, col = lane & 15.
+__device__ __forceinline__ void load_tile(const double* C, int64_t ldc, d4 (&acc)[4][4]) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int wr = w >> 1, wc = w & 1, fr = lane & 15, fk = lane >> 4;
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        acc[a][c][r] = C[(int64_t)(wr * 64 + a * 16 + fk + 4 * r) * ldc + wc * 64 + c * 16 + fr];
+}
+
+__device__ __forceinline__ void store_tile(double* C, int64_t ldc, const d4 (&acc)[4][4],
+                                           double scale) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int wr = w >> 1, wc = w & 1, fr = lane & 15, fk = lane >> 4;
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        C[(int64_t)(wr * 64 + a * 16 + fk + 4 * r) * ldc + wc * 64 + c * 16 + fr] =
+            scale * acc[a][c][r];
+}
+
+// ---------------------------------------------------------------------------
+// Householder QR of the m x 128 panel P (row-major, ld lda), column c.
+// Workgroup g owns panel rows [256 g, 256 g + 256) (16 waves x 16 rows, lanes
+// over the columns, two columns per lane); its rows are loaded into registers
+// before the reduction of the previous launch's partials completes.
+// Inputs (written by launch c - 1): part[c & 1][g'] = partial sums over the rows
+// of workgroup g' of x_i P_ij (j >= c, x = column c, rows >= c) and, at [128],
+// of x_i^2 (rows > c); pivrow[c & 1] = row c of the panel.
+// Reflector (LAPACK dlarfg convention): alpha = -sign(x0) ||x||,
+// tau = (alpha - x0) / alpha, v = x / (x0 - alpha) with v_c = 1; tau = 0 when the
+// sub-column is exactly zero. w_j = v^T P_j = (S_j - alpha P_cj) / (x0 - alpha).
+// Then P_ij -= tau v_i w_j (j > c), column c <- (alpha; v), and the partials of
+// column c + 1 are published. c = -1 publishes the partials of column 0 only.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void hh_col_kernel(double* __restrict__ P, int64_t lda,
+                                                      int m, int c, double* __restrict__ part,
+                                                      double* __restrict__ pivrow,
+                                                      double* __restrict__ tau) {
+  __shared__ double sS[HH_PART_LD];
+  __shared__ double sw[TS];
+  __shared__ double sacc[16][HH_PART_LD];
+  __shared__ double sscal[3];
+  const int G = gridDim.x, g = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int j0 = lane, j1 = lane + 64;
+  const int rbase = g * HH_ROWS + w * HH_RPW;
+  double p0[HH_RPW], p1[HH_RPW];
+#pragma unroll
+  for (int q = 0; q < HH_RPW; ++q) {
+    const int i = rbase + q;
+    p0[q] = 0.0;
+    p1[q] = 0.0;
+    if (i < m && i >= c) {
+      const double* row = P + (int64_t)i * lda;
+      if (j0 >= c) p0[q] = row[j0];
+      if (j1 >= c) p1[q] = row[j1];
+    }
+  }
+  double tau_c = 0.0, scale = 0.0, alpha = 0.0;
+  if (c >= 0) {
+    const double* pp = part + (size_t)(c & 1) * HH_MAXG * HH_PART_LD;
+    double s0 = 0.0, s1 = 0.0, sn = 0.0;
+    for (int q = w; q < G; q += 16) {
+      s0 += pp[q * HH_PART_LD + j0];
+      s1 += pp[q * HH_PART_LD + j1];
+      sn += pp[q * HH_PART_LD + 128];
+    }
+    sacc[w][j0] = s0;
+    sacc[w][j1] = s1;
+    if (lane == 0) sacc[w][128] = sn;
+    __syncthreads();
+    if (t <= 128) {
+      double s = 0.0;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) s += sacc[q][t];
+      sS[t] = s;
+    }
+    __syncthreads();
+    if (t == 0) {
+      const double x0 = pivrow[(c & 1) * TS + c];
+      const double nb2 = sS[128];
+      double tc = 0.0, sc = 0.0, al = x0;
+      if (nb2 > 0.0) {
+        const double nrm = sqrt(x0 * x0 + nb2);
+        al = x0 >= 0.0 ? -nrm : nrm;
+        tc = (al - x0) / al;
+        sc = 1.0 / (x0 - al);
+      }
+      sscal[0] = tc;
+      sscal[1] = sc;
+      sscal[2] = al;
+      if (g == 0) tau[c] = tc;
+    }
+    __syncthreads();
+    tau_c = sscal[0];
+    scale = sscal[1];
+    alpha = sscal[2];
+    if (t < TS && t > c) sw[t] = (sS[t] - alpha * pivrow[(c & 1) * TS + t]) * scale;
+    __syncthreads();
+  }
+  const bool act = tau_c != 0.0;
+  const int c1 = c + 1;
+  const double w0 = (act && j0 > c) ? sw[j0] : 0.0;
+  const double w1 = (act && j1 > c) ? sw[j1] : 0.0;
+  double a0 = 0.0, a1 = 0.0, nb = 0.0;
+#pragma unroll
+  for (int q = 0; q < HH_RPW; ++q) {
+    const int i = rbase + q;
+    if (i >= m || i < c) continue;
+    double* row = P + (int64_t)i * lda;
+    if (act) {
+      const double xc = __shfl(c < 64 ? p0[q] : p1[q], c & 63);
+      const double vi = (i == c) ? 1.0 : xc * scale;
+      const double tv = tau_c * vi;
+      p0[q] -= tv * w0;
+      p1[q] -= tv * w1;
+      if (j0 == c) p0[q] = (i == c) ? alpha : vi;
+      if (j1 == c) p1[q] = (i == c) ? alpha : vi;
+      if (j0 >= c) row[j0] = p0[q];
+      if (j1 >= c) row[j1] = p1[q];
+    }
+    if (c1 < TS && i >= c1) {
+      const double x = __shfl(c1 < 64 ? p0[q] : p1[q], c1 & 63);
+      if (j0 >= c1) a0 += x * p0[q];
+      if (j1 >= c1) a1 += x * p1[q];
+      if (i > c1) nb += x * x;
+      if (i == c1) {
+        if (j0 >= c1) pivrow[(c1 & 1) * TS + j0] = p0[q];
+        if (j1 >= c1) pivrow[(c1 & 1) * TS + j1] = p1[q];
+      }
+    }
+  }
+  if (c1 >= TS) return;
+  __syncthreads();
+  sacc[w][j0] = a0;
+  sacc[w][j1] = a1;
+  if (lane == 0) sacc[w][128] = nb;
+  __syncthreads();
+  if (t <= 128 && t >= c1) {
+    double s = 0.0;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) s += sacc[q][t];
+    part[((size_t)(c1 & 1) * HH_MAXG + g) * HH_PART_LD + t] = s;
+  }
+}
+
+// U[r0 + i][128 + q] = V[i][q] (unit lower trapezoidal), i < m.
+__global__ __launch_bounds__(256) void vcopy_kernel(const double* __restrict__ P, int64_t lda,
+                                                    int m, double* __restrict__ U, int64_t ldu) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t i = e >> 7;
+  const int q = (int)(e & 127);
+  if (i >= m) return;
+  const double v = (i > q) ? P[i * lda + q] : (i == q ? 1.0 : 0.0);
+  U[i * ldu + TS + q] = v;
+}
+
+// part[ch] = P1[rows]^T P2[rows] (128 x 128), rows = [ch * TN_CH, +TN_CH) of m.
+__global__ __launch_bounds__(256, 2) void tn_partial_kernel(const double* __restrict__ P1,
+                                                            int64_t ld1,
+                                                            const double* __restrict__ P2,
+                                                            int64_t ld2, int m,
+                                                            double* __restrict__ part) {
+  __shared__ double smem[4 * GSTAGE];
+  const int ch = blockIdx.x;
+  const int i0 = ch * TN_CH, kd = min(TN_CH, m - i0);
+  d4 acc[4][4];
+  zero_tile(acc);
+  gemm_tile<KSLOW, KSLOW, false>(P1 + (int64_t)i0 * ld1, ld1, P2 + (int64_t)i0 * ld2, ld2, kd,
+                                 smem, acc);
+  store_tile(part + (int64_t)ch * TS * TS, TS, acc, 1.0);
+}
+
+// out = scale * sum_ch part[ch] (128 x 128), fixed order.
+__global__ __launch_bounds__(256) void tn_reduce_kernel(const double* __restrict__ part, int nch,
+                                                        double* __restrict__ out, double scale) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  double s = 0.0;
+  for (int c = 0; c < nch; ++c) s += part[(int64_t)c * TS * TS + e];
+  out[e] = scale * s;
+}
+
+// Compact-WY T (upper) of the panel's 128 reflectors from V^T V (one workgroup):
+// T[c][c] = tau_c, T[0:c, c] = -tau_c T[0:c, 0:c] (V^T V)[0:c, c]. Thread r owns
+// row r of T in LDS.
+__global__ __launch_bounds__(128) void tbuild_kernel(const double* __restrict__ VtV,
+                                                     const double* __restrict__ tau,
+                                                     double* __restrict__ T) {
+  __shared__ double sT[TS * (TS + 1)];
+  __shared__ double sv[TS];
+  const int r = threadIdx.x;
+  double* row = sT + r * (TS + 1);
+  for (int k = 0; k < TS; ++k) row[k] = 0.0;
+  for (int c = 0; c < TS; ++c) {
+    sv[r] = VtV[r * TS + c];
+    __syncthreads();
+    const double tc = tau[c];
+    if (r < c) {
+      double s = 0.0;
+      for (int k = r; k < c; ++k) s += row[k] * sv[k];
+      row[c] = -tc * s;
+    } else if (r == c) {
+      row[c] = tc;
+    }
+    __syncthreads();
+  }
+  for (int k = 0; k < TS; ++k) T[r * TS + k] = row[k];
+}
+
+// Split-K symmetric product: Xp[il][ch] = sum_{J in chunk ch} A22_IJ V_J, with
+// A22_IJ = A_IJ (J <= I, stored) or A_JI^T (J > I, read transposed).
+__global__ __launch_bounds__(256, 2) void symm_kernel(const double* __restrict__ A, int64_t lda,
+                                                      const double* __restrict__ U, int64_t ldu,
+                                                      int tr0, int mt,
+                                                      double* __restrict__ Xp) {
+  __shared__ double smem[4 * GSTAGE];
+  const int il = blockIdx.x, ch = blockIdx.y, nch = gridDim.y;
+  const int I = tr0 + il;
+  const int jl0 = ch * SY_CH, jl1 = min(mt, (ch + 1) * SY_CH);
+  const int jsplit = min(jl1, max(jl0, il + 1));   // tiles [jl0, jsplit) have J <= I
+  d4 acc[4][4];
+  zero_tile(acc);
+  for (int jl = jl0; jl < jsplit; ++jl) {
+    const int J = tr0 + jl;
+    gemm_tile<KFAST, KSLOW, false>(A + (int64_t)I * TS * lda + (int64_t)J * TS, lda,
+                                   U + (int64_t)J * TS * ldu + TS, ldu, TS, smem, acc);
+  }
+  for (int jl = jsplit; jl < jl1; ++jl) {
+    const int J = tr0 + jl;
+    gemm_tile<KSLOW, KSLOW, false>(A + (int64_t)J * TS * lda + (int64_t)I * TS, lda,
+                                   U + (int64_t)J * TS * ldu + TS, ldu, TS, smem, acc);
+  }
+  store_tile(Xp + ((int64_t)il * nch + ch) * TS * TS, TS, acc, 1.0);
+}
+
+// X[tile il] = sum_ch Xp[il][ch]   (elementwise, 2 doubles per thread)
+__global__ __launch_bounds__(256) void psum_kernel(const double* __restrict__ Xp, int nch,
+                                                   double* __restrict__ X) {
+  const int il = blockIdx.y;
+  const int e = (blockIdx.x * 256 + threadIdx.x) * 2;
+  d2 s = {0.0, 0.0};
+  for (int c = 0; c < nch; ++c)
+    s += *reinterpret_cast<const d2*>(Xp + ((int64_t)il * nch + c) * TS * TS + e);
+  *reinterpret_cast<d2*>(X + (int64_t)il * TS * TS + e) = s;
+}
+
+// X_I <- X_I T (in place; one tile row per workgroup).
+__global__ __launch_bounds__(256, 2) void xt_kernel(double* __restrict__ X,
+                                                    const double* __restrict__ T) {
+  __shared__ double smem[4 * GSTAGE];
+  double* Xi = X + (int64_t)blockIdx.x * TS * TS;
+  d4 acc[4][4];
+  zero_tile(acc);
+  gemm_tile<KFAST, KSLOW, false>(Xi, TS, T, TS, TS, smem, acc);
+  store_tile(Xi, TS, acc, 1.0);
+}
+
+// Zh = 1/2 T^T M (one workgroup).
+__global__ __launch_bounds__(256) void z_kernel(const double* __restrict__ T,
+                                                const double* __restrict__ M,
+                                                double* __restrict__ Zh) {
+  __shared__ double smem[4 * GSTAGE];
+  d4 acc[4][4];
+  zero_tile(acc);
+  gemm_tile<KSLOW, KSLOW, false>(T, TS, M, TS, TS, smem, acc);
+  store_tile(Zh, TS, acc, 0.5);
+}
+
+// W_I = X_I - V_I Zh  ->  U[rows I][0:128] and U[rows I][256:384].
+__global__ __launch_bounds__(256, 2) void w_kernel(const double* __restrict__ X,
+                                                   double* __restrict__ U, int64_t ldu,
+                                                   const double* __restrict__ Zh) {
+  __shared__ double smem[4 * GSTAGE];
+  const int il = blockIdx.x;
+  double* Ui = U + (int64_t)il * TS * ldu;
+  d4 acc[4][4];
+  load_tile(X + (int64_t)il * TS * TS, TS, acc);
+  gemm_tile<KFAST, KSLOW, true>(Ui + TS, ldu, Zh, TS, TS, smem, acc);
+  store_tile(Ui, ldu, acc, 1.0);
+  store_tile(Ui + 2 * TS, ldu, acc, 1.0);
+}
+
+// A_IJ -= [W_I V_I] [V_J W_J]^T on the lower tiles of the trailing mt x mt tiles.
+__global__ __launch_bounds__(256, 2) void syr2k_kernel(double* __restrict__ A, int64_t lda,
+                                                       const double* __restrict__ U,
+                                                       int64_t ldu, int tr0, int mt) {
+  __shared__ double smem[4 * GSTAGE];
+  const int q = xcd_remap(blockIdx.x, gridDim.x);
+  int i, j;
+  tri_decode(q, mt, &i, &j);
+  const int I = tr0 + i, J = tr0 + j;
+  double* C = A + (int64_t)I * TS * lda + (int64_t)J * TS;
+  d4 acc[4][4];
+  load_tile(C, lda, acc);
+  gemm_tile<KFAST, KFAST, true>(U + (int64_t)I * TS * ldu, ldu, U + (int64_t)J * TS * ldu + TS,
+                                ldu, 2 * TS, smem, acc);
+  store_tile(C, lda, acc, 1.0);
+}
+
+// ---------------------------------------------------------------------------
+// Y <- Q_j^T Y for one panel (Y rows r0.., 16 columns): Y -= V (T^T (V^T Y)).
+// V is read from the reduced matrix (unit lower trapezoidal below the band).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void qt_partial_kernel(const double* __restrict__ P,
+                                                         int64_t lda, int m,
+                                                         const double* __restrict__ Y,
+                                                         double* __restrict__ part) {
+  const int g = blockIdx.x, t = threadIdx.x;
+  const int a = t & 127, h = t >> 7;
+  double s[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  const int i1 = min(m, (g + 1) * 256);
+  for (int i = g * 256; i < i1; ++i) {
+    const double v = (i > a) ? P[(int64_t)i * lda + a] : (i == a ? 1.0 : 0.0);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) s[q] += v * Y[(int64_t)i * RLD + 8 * h + q];
+  }
+#pragma unroll
+  for (int q = 0; q < 8; ++q) part[((int64_t)g * TS + a) * RLD + 8 * h + q] = s[q];
+}
+
+// b = T^T (sum_g part[g])  (128 x 16, one workgroup)
+__global__ __launch_bounds__(256) void qt_reduce_kernel(const double* __restrict__ part, int G,
+                                                        const double* __restrict__ T,
+                                                        double* __restrict__ b) {
+  __shared__ double sa[TS * RLD];
+  const int t = threadIdx.x;
+  for (int e = t; e < TS * RLD; e += 256) {
+    double s = 0.0;
+    for (int g = 0; g < G; ++g) s += part[(int64_t)g * TS * RLD + e];
+    sa[e] = s;
+  }
+  __syncthreads();
+  const int k = t & 127, h = t >> 7;
+  double o[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  for (int a = 0; a <= k; ++a) {
+    const double tv = T[a * TS + k];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) o[q] += tv * sa[a * RLD + 8 * h + q];
+  }
+#pragma unroll
+  for (int q = 0; q < 8; ++q) b[k * RLD + 8 * h + q] = o[q];
+}
+
+// Y[i] -= V[i] b for the rows of this workgroup (16 lanes share a row).
+__global__ __launch_bounds__(256) void qt_apply_kernel(const double* __restrict__ P, int64_t lda,
+                                                       int m, double* __restrict__ Y,
+                                                       const double* __restrict__ b) {
+  __shared__ double sb[TS * RLD];
+  const int t = threadIdx.x;
+  for (int e = t; e < TS * RLD; e += 256) sb[e] = b[e];
+  __syncthreads();
+  const int col = t & 15;
+  for (int i = blockIdx.x * 256 + (t >> 4); i < min(m, (int)(blockIdx.x + 1) * 256); i += 16) {
+    double s = 0.0;
+    const double* row = P + (int64_t)i * lda;
+    const int amax = min(i, TS);
+    for (int a = 0; a < amax; ++a) s += row[a] * sb[a * RLD + col];
+    if (i < TS) s += sb[i * RLD + col];   // unit diagonal of V
+    Y[(int64_t)i * RLD + col] -= s;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Banded Cholesky of B + eta I per workgroup (eta = etas[blockIdx.x]) with the
+// forward substitution of Y, logdet and Gram. B = the reduced matrix: diagonal
+// tiles (full) and the upper triangles of the subdiagonal tiles (bandwidth 128).
+// out[e][0] = logdet (rows < n only; the identity pad is decoupled),
+// out[e][1 + a * 16 + c] = (L^-1 Y)^T (L^-1 Y); info[e] = first bad pivot.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void band_chol_kernel(const double* __restrict__ B,
+                                                        int64_t lda, int nt, int64_t n,
+                                                        const double* __restrict__ Y,
+                                                        const double* __restrict__ etas,
+                                                        double* __restrict__ out, int out_ld,
+                                                        int* __restrict__ info) {
+  __shared__ double Ls[TS * DL];
+  __shared__ double Aux[TS * RLD];
+  __shared__ double sdiag[TS];
+  __shared__ double sred[2];
+  __shared__ int s_fail;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int wr = w >> 1, wc = w & 1, fr = lane & 15, fk = lane >> 4;
+  const int e = blockIdx.x;
+  const double eta = etas[e];
+  double logdet = 0.0;
+  int fail = 0;
+  d4 Gacc = {0.0, 0.0, 0.0, 0.0};
+  d4 Rr[2];
+  // D_0 = B_00 + eta I (lower), r_0 = Y_0
+  for (int q = t; q < TS * TS; q += 256) {
+    const int r = q >> 7, c = q & 127;
+    Ls[r * DL + c] = (c <= r) ? B[(int64_t)r * lda + c] + (r == c ? eta : 0.0) : 0.0;
+  }
+#pragma unroll
+  for (int slot = 0; slot < 2; ++slot) {
+    const int ti = slot == 0 ? w : NDB - 1 - w;
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) Rr[slot][rr] = Y[(int64_t)(ti * DB + fk + 4 * rr) * RLD + fr];
+  }
+  if (t == 0) s_fail = 0;
+  __syncthreads();
+  for (int k = 0; k < nt; ++k) {
+    lds_chol_block(Ls, Aux, sdiag, &s_fail);
+    if (w < 2) {
+      double v = ((int64_t)k * TS + t < n) ? log(sdiag[t]) : 0.0;
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+      if (lane == 0) sred[w] = v;
+    }
+    __syncthreads();
+    if (t == 0) {
+      logdet += 2.0 * (sred[0] + sred[1]);
+      if (s_fail && !fail) fail = k * TS + s_fail;
+      s_fail = 0;
+    }
+    lds_inv_block(Ls, Aux);
+    __syncthreads();
+    // r_k -> Aux (k-major [128][16])
+#pragma unroll
+    for (int slot = 0; slot < 2; ++slot) {
+      const int ti = slot == 0 ? w : NDB - 1 - w;
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) Aux[(ti * DB + fk + 4 * rr) * RLD + fr] = Rr[slot][rr];
+    }
+    __syncthreads();
+    // y_k = Linv r_k
+    d4 Yv[2];
+#pragma unroll
+    for (int slot = 0; slot < 2; ++slot) {
+      const int ti = slot == 0 ? w : NDB - 1 - w;
+      d4 a0 = {0.0, 0.0, 0.0, 0.0}, a1 = {0.0, 0.0, 0.0, 0.0};
+      for (int kt = 0; kt <= ti; ++kt) {
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+          const double av = Ls[(ti * DB + fr) * DL + kt * DB + 4 * kk + fk];
+          const double bv = Aux[(kt * DB + 4 * kk + fk) * RLD + fr];
+          if (kk & 1) a1 = mfma64(av, bv, a1);
+          else a0 = mfma64(av, bv, a0);
+        }
+      }
+      Yv[slot] = a0 + a1;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int slot = 0; slot < 2; ++slot) {
+      const int ti = slot == 0 ? w : NDB - 1 - w;
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) Aux[(ti * DB + fk + 4 * rr) * RLD + fr] = Yv[slot][rr];
+    }
+    __syncthreads();
+    // Gram += y^T y over this wave's two 16-row slices
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int kt = 2 * w + h;
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const double v = Aux[(kt * DB + 4 * kk + fk) * RLD + fr];
+        Gacc = mfma64(v, v, Gacc);
+      }
+    }
+    if (k + 1 == nt) break;
+    // C = E_k Linv^T, E_k = triu(B_{k+1,k})
+    const double* E = B + (int64_t)(k + 1) * TS * lda + (int64_t)k * TS;
+    d4 acc[4][4];
+    zero_tile(acc);
+    for (int kq = 0; kq < TS / 4; ++kq) {
+      const int qk = kq * 4 + fk;
+      double a[4], b[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = wr * 64 + i * 16 + fr;
+        a[i] = (r <= qk) ? E[(int64_t)r * lda + qk] : 0.0;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c = wc * 64 + j * 16 + fr;
+        b[j] = (qk <= c) ? Ls[c * DL + qk] : 0.0;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma64(a[i], b[j], acc[i][j]);
+    }
+    __syncthreads();   // every wave is done with Linv
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          Ls[(wr * 64 + i * 16 + fk + 4 * r) * DL + wc * 64 + j * 16 + fr] = acc[i][j][r];
+    __syncthreads();
+    // r_{k+1} = Y_{k+1} - C y_k
+    const int64_t g1 = (int64_t)(k + 1) * TS;
+#pragma unroll
+    for (int slot = 0; slot < 2; ++slot) {
+      const int ti = slot == 0 ? w : NDB - 1 - w;
+      d4 a0;
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) a0[rr] = Y[(g1 + ti * DB + fk + 4 * rr) * RLD + fr];
+      for (int kt = 0; kt < NDB; ++kt) {
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+          const double av = -Ls[(ti * DB + fr) * DL + kt * DB + 4 * kk + fk];
+          const double bv = Aux[(kt * DB + 4 * kk + fk) * RLD + fr];
+          a0 = mfma64(av, bv, a0);
+        }
+      }
+      Rr[slot] = a0;
+    }
+    // D_{k+1} = B_{k+1,k+1} + eta I - C C^T on the 36 lower 16x16 tiles (9 per wave)
+    d4 S[9];
+#pragma unroll
+    for (int s9 = 0; s9 < 9; ++s9) {
+      const int qt = w + 4 * s9;
+      int ti = 0;
+      while ((ti + 1) * (ti + 2) / 2 <= qt) ++ti;
+      const int tj = qt - ti * (ti + 1) / 2;
+      const int r0 = ti * DB, c0 = tj * DB;
+      d4 a;
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int r = r0 + fk + 4 * rr, c = c0 + fr;
+        a[rr] = B[(g1 + r) * lda + g1 + c] + (r == c ? eta : 0.0);
+      }
+      for (int kq = 0; kq < TS / 4; ++kq) {
+        const double av = -Ls[(r0 + fr) * DL + 4 * kq + fk];
+        const double bv = Ls[(c0 + fr) * DL + 4 * kq + fk];
+        a = mfma64(av, bv, a);
+      }
+      S[s9] = a;
+    }
+    __syncthreads();   // every wave is done with C
+#pragma unroll
+    for (int s9 = 0; s9 < 9; ++s9) {
+      const int qt = w + 4 * s9;
+      int ti = 0;
+      while ((ti + 1) * (ti + 2) / 2 <= qt) ++ti;
+      const int tj = qt - ti * (ti + 1) / 2;
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr)
+        Ls[(ti * DB + fk + 4 * rr) * DL + tj * DB + fr] = S[s9][rr];
+    }
+    __syncthreads();
+  }
+  __syncthreads();
+  d4* sg = reinterpret_cast<d4*>(Ls);
+  sg[w * 64 + lane] = Gacc;
+  __syncthreads();
+  if (w == 0) {
+    const d4 Gs = ((sg[lane] + sg[64 + lane]) + sg[128 + lane]) + sg[192 + lane];
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) out[(int64_t)e * out_ld + 1 + (fk + 4 * rr) * RLD + fr] = Gs[rr];
+  }
+  if (t == 0) {
+    out[(int64_t)e * out_ld] = logdet;
+    info[e] = fail;
+  }
+}
+
+}  // namespace gpmi

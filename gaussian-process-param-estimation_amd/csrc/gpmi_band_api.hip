@@ -1,0 +1,352 @@
+// C-ABI of the band path (include/gpmi.h, gpmi_band_*): reduction of an
+// operator's K to symmetric band form (bandwidth 128) on the device, Q^T applied
+// to a resident RHS block, and batched banded-Cholesky likelihood terms for any
+// number of eta values (kernels: gpmi_band.hip).
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <vector>
+
+#include "gpmi_internal.h"
+#include "gpmi_band.h"
+#include "../../include/gpmi.h"
+
+using namespace gpmi;
+
+namespace gpmi {
+int set_error(int code, const char* msg);   // gpmi_api.hip
+int op_view(const gpmi_op* op, OpView* v);  // gpmi_api.hip
+}  // namespace gpmi
+
+namespace {
+
+#define BD_TRY(expr)                                                                   \
+  do {                                                                                 \
+    hipError_t e_ = (expr);                                                            \
+    if (e_ != hipSuccess) {                                                            \
+      char b_[400];                                                                    \
+      snprintf(b_, sizeof(b_), "%s failed: %s", #expr, hipGetErrorString(e_));        \
+      return set_error(-(int)e_, b_);                                                  \
+    }                                                                                  \
+  } while (0)
+
+#define BD_LAUNCH(name)                                                                \
+  do {                                                                                 \
+    hipError_t e_ = hipGetLastError();                                                 \
+    if (e_ != hipSuccess) {                                                            \
+      char b_[400];                                                                    \
+      snprintf(b_, sizeof(b_), "launch of %s failed: %s", name, hipGetErrorString(e_)); \
+      return set_error(-(int)e_, b_);                                                  \
+    }                                                                                  \
+  } while (0)
+
+constexpr int TS = GPMI_TS;
+constexpr int RLD = GPMI_RHS_LD;
+constexpr int OUT_LD = 1 + RLD * RLD;
+
+struct Guard {
+  int prev = -1;
+  explicit Guard(int d) {
+    (void)hipGetDevice(&prev);
+    if (prev != d) (void)hipSetDevice(d);
+  }
+  ~Guard() {
+    int c = -1;
+    (void)hipGetDevice(&c);
+    if (prev >= 0 && c != prev) (void)hipSetDevice(prev);
+  }
+};
+
+}  // namespace
+
+struct gpmi_band {
+  int device = 0;
+  int64_t n = 0, n_pad = 0;
+  int nt = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  double* Ab = nullptr;      // [n_pad][n_pad]: band (diagonal tiles, triu of subdiagonal
+                             // tiles) + Householder vectors below the band
+  double* U = nullptr;       // [n_pad][384] = [W | V | W] of the current panel
+  double* X = nullptr;       // [n_pad][128] (rows relative to the panel's trailing block)
+  double* Xp = nullptr;      // symm split-K partials
+  double* part = nullptr;    // [2][HH_MAXG][HH_PART_LD] column partials
+  double* pivrow = nullptr;  // [2][128]
+  double* tau = nullptr;     // [nt][128]
+  double* Tm = nullptr;      // [nt][128][128] compact-WY T per panel
+  double* tnp = nullptr;     // tn partials [nch][128][128]
+  double* VtV = nullptr;     // [128][128]
+  double* M = nullptr;       // [128][128]
+  double* Zh = nullptr;      // [128][128]
+  double* Y = nullptr;       // [n_pad][16] = Q^T R
+  double* qtp = nullptr;     // [HH_MAXG][128][16]
+  double* qb = nullptr;      // [128][16]
+  double* etas = nullptr;    // [cap]
+  double* out = nullptr;     // [cap][OUT_LD]
+  int* info = nullptr;       // [cap]
+  int cap = 0;
+  int nrhs = 0;
+  double reduce_ms = 0.0, rhs_ms = 0.0, loglik_ms = 0.0;
+};
+
+namespace {
+
+int band_free(gpmi_band* b) {
+  double* bufs[] = {b->Ab, b->U, b->X, b->Xp, b->part, b->pivrow, b->tau, b->Tm, b->tnp,
+                    b->VtV, b->M, b->Zh, b->Y, b->qtp, b->qb, b->etas, b->out};
+  for (double* p : bufs)
+    if (p) (void)hipFree(p);
+  if (b->info) (void)hipFree(b->info);
+  if (b->ev0) (void)hipEventDestroy(b->ev0);
+  if (b->ev1) (void)hipEventDestroy(b->ev1);
+  if (b->stream) (void)hipStreamDestroy(b->stream);
+  delete b;
+  return 0;
+}
+
+// Dense -> band: panels j = 0 .. nt-2 of 128 columns (see gpmi_band.hip).
+int band_reduce(gpmi_band* b, const double* K) {
+  hipStream_t s = b->stream;
+  const int64_t np = b->n_pad;
+  const int nt = b->nt;
+  BD_TRY(hipEventRecord(b->ev0, s));
+  BD_TRY(hipMemcpyAsync(b->Ab, K, sizeof(double) * np * np, hipMemcpyDeviceToDevice, s));
+  for (int j = 0; j + 1 < nt; ++j) {
+    const int64_t r0 = (int64_t)(j + 1) * TS, c0 = (int64_t)j * TS;
+    const int m = (int)(np - r0), mt = nt - j - 1;
+    const int G = (m + HH_ROWS - 1) / HH_ROWS;
+    double* P = b->Ab + r0 * np + c0;
+    double* tau = b->tau + (int64_t)j * TS;
+    double* T = b->Tm + (int64_t)j * TS * TS;
+    for (int c = -1; c < TS; ++c) {
+      hipLaunchKernelGGL(hh_col_kernel, dim3(G), dim3(1024), 0, s, P, np, m, c, b->part,
+                         b->pivrow, tau);
+      BD_LAUNCH("hh_col_kernel");
+    }
+    double* Ur = b->U + r0 * BAND_ULD;
+    hipLaunchKernelGGL(vcopy_kernel, dim3((unsigned)((int64_t)m * TS / 256)), dim3(256), 0, s, P,
+                       np, m, Ur, (int64_t)BAND_ULD);
+    BD_LAUNCH("vcopy_kernel");
+    const int nch = (m + TN_CH - 1) / TN_CH;
+    hipLaunchKernelGGL(tn_partial_kernel, dim3(nch), dim3(256), 0, s, Ur + TS,
+                       (int64_t)BAND_ULD, Ur + TS, (int64_t)BAND_ULD, m, b->tnp);
+    BD_LAUNCH("tn_partial_kernel");
+    hipLaunchKernelGGL(tn_reduce_kernel, dim3(TS * TS / 256), dim3(256), 0, s, b->tnp, nch,
+                       b->VtV, 1.0);
+    BD_LAUNCH("tn_reduce_kernel");
+    hipLaunchKernelGGL(tbuild_kernel, dim3(1), dim3(TS), 0, s, b->VtV, tau, T);
+    BD_LAUNCH("tbuild_kernel");
+    const int sch = (mt + SY_CH - 1) / SY_CH;
+    hipLaunchKernelGGL(symm_kernel, dim3(mt, sch), dim3(256), 0, s, b->Ab, np, b->U,
+                       (int64_t)BAND_ULD, j + 1, mt, b->Xp);
+    BD_LAUNCH("symm_kernel");
+    hipLaunchKernelGGL(psum_kernel, dim3(TS * TS / 512, mt), dim3(256), 0, s, b->Xp, sch, b->X);
+    BD_LAUNCH("psum_kernel");
+    hipLaunchKernelGGL(xt_kernel, dim3(mt), dim3(256), 0, s, b->X, T);
+    BD_LAUNCH("xt_kernel");
+    hipLaunchKernelGGL(tn_partial_kernel, dim3(nch), dim3(256), 0, s, Ur + TS,
+                       (int64_t)BAND_ULD, b->X, (int64_t)TS, m, b->tnp);
+    BD_LAUNCH("tn_partial_kernel");
+    hipLaunchKernelGGL(tn_reduce_kernel, dim3(TS * TS / 256), dim3(256), 0, s, b->tnp, nch, b->M,
+                       1.0);
+    BD_LAUNCH("tn_reduce_kernel");
+    hipLaunchKernelGGL(z_kernel, dim3(1), dim3(256), 0, s, T, b->M, b->Zh);
+    BD_LAUNCH("z_kernel");
+    hipLaunchKernelGGL(w_kernel, dim3(mt), dim3(256), 0, s, b->X, Ur, (int64_t)BAND_ULD, b->Zh);
+    BD_LAUNCH("w_kernel");
+    hipLaunchKernelGGL(syr2k_kernel, dim3(mt * (mt + 1) / 2), dim3(256), 0, s, b->Ab, np, b->U,
+                       (int64_t)BAND_ULD, j + 1, mt);
+    BD_LAUNCH("syr2k_kernel");
+  }
+  BD_TRY(hipEventRecord(b->ev1, s));
+  BD_TRY(hipEventSynchronize(b->ev1));
+  float ms = 0.f;
+  BD_TRY(hipEventElapsedTime(&ms, b->ev0, b->ev1));
+  b->reduce_ms = ms;
+  return 0;
+}
+
+int ensure_cap(gpmi_band* b, int neta) {
+  if (b->cap >= neta) return 0;
+  if (b->etas) BD_TRY(hipFree(b->etas));
+  if (b->out) BD_TRY(hipFree(b->out));
+  if (b->info) BD_TRY(hipFree(b->info));
+  b->etas = b->out = nullptr;
+  b->info = nullptr;
+  b->cap = 0;
+  const int cap = std::max(neta, 64);
+  BD_TRY(hipMalloc(&b->etas, sizeof(double) * cap));
+  BD_TRY(hipMalloc(&b->out, sizeof(double) * cap * OUT_LD));
+  BD_TRY(hipMalloc(&b->info, sizeof(int) * cap));
+  b->cap = cap;
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gpmi_band_create(gpmi_op* op, gpmi_band** out) {
+  if (!out) return set_error(-1004, "null output handle");
+  OpView v;
+  int rc = op_view(op, &v);
+  if (rc) return rc;
+  if (!v.has_K) return set_error(-1000, "operator has no matrix (load or assemble first)");
+  if (v.n_pad > BAND_MAX_NPAD) return set_error(-1200, "band path supports n <= 32768");
+  Guard g(v.device);
+  gpmi_band* b = new gpmi_band();
+  b->device = v.device;
+  b->n = v.n;
+  b->n_pad = v.n_pad;
+  b->nt = (int)(v.n_pad / TS);
+  const int64_t np = b->n_pad;
+  const int nt = b->nt;
+  const int sch = std::max(1, (nt - 1 + SY_CH - 1) / SY_CH);
+  const int nch = (int)std::max<int64_t>(1, (np + TN_CH - 1) / TN_CH);
+  hipError_t e;
+  auto fail = [&](hipError_t err, const char* what) {
+    band_free(b);
+    char msg[200];
+    snprintf(msg, sizeof(msg), "allocation of %s failed: %s", what, hipGetErrorString(err));
+    return set_error(-(int)err, msg);
+  };
+  if ((e = hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking)) != hipSuccess)
+    return fail(e, "stream");
+  if ((e = hipEventCreate(&b->ev0)) != hipSuccess) return fail(e, "event");
+  if ((e = hipEventCreate(&b->ev1)) != hipSuccess) return fail(e, "event");
+#define BALLOC(ptr, count)                                                          \
+  if ((e = hipMalloc(&b->ptr, sizeof(double) * (size_t)(count))) != hipSuccess)     \
+    return fail(e, #ptr);
+  BALLOC(Ab, np * np);
+  BALLOC(U, np * BAND_ULD);
+  BALLOC(X, np * TS);
+  BALLOC(Xp, (size_t)std::max(1, nt - 1) * sch * TS * TS);
+  BALLOC(part, 2 * HH_MAXG * HH_PART_LD);
+  BALLOC(pivrow, 2 * TS);
+  BALLOC(tau, (size_t)nt * TS);
+  BALLOC(Tm, (size_t)nt * TS * TS);
+  BALLOC(tnp, (size_t)nch * TS * TS);
+  BALLOC(VtV, TS * TS);
+  BALLOC(M, TS * TS);
+  BALLOC(Zh, TS * TS);
+  BALLOC(Y, np * RLD);
+  BALLOC(qtp, (size_t)HH_MAXG * TS * RLD);
+  BALLOC(qb, TS * RLD);
+#undef BALLOC
+  if ((e = hipMemsetAsync(b->U, 0, sizeof(double) * np * BAND_ULD, b->stream)) != hipSuccess)
+    return fail(e, "U memset");
+  if ((e = hipMemsetAsync(b->Y, 0, sizeof(double) * np * RLD, b->stream)) != hipSuccess)
+    return fail(e, "Y memset");
+  rc = band_reduce(b, v.K);
+  if (rc) {
+    band_free(b);
+    return rc;
+  }
+  *out = b;
+  return 0;
+}
+
+int gpmi_band_destroy(gpmi_band* b) {
+  if (!b) return 0;
+  Guard g(b->device);
+  if (b->stream) (void)hipStreamSynchronize(b->stream);
+  return band_free(b);
+}
+
+int gpmi_band_set_rhs(gpmi_band* b, const double* rhs, int64_t ld, int nrhs) {
+  if (!b) return set_error(-1006, "null handle");
+  if (nrhs < 0 || nrhs > RLD) return set_error(-1007, "nrhs outside [0, 16]");
+  Guard g(b->device);
+  hipStream_t s = b->stream;
+  const int64_t np = b->n_pad;
+  std::vector<double> h((size_t)np * RLD, 0.0);
+  for (int64_t i = 0; i < b->n; ++i)
+    for (int c = 0; c < nrhs; ++c) h[(size_t)i * RLD + c] = rhs[i * ld + c];
+  BD_TRY(hipEventRecord(b->ev0, s));
+  BD_TRY(hipMemcpyAsync(b->Y, h.data(), sizeof(double) * h.size(), hipMemcpyHostToDevice, s));
+  for (int j = 0; j + 1 < b->nt; ++j) {
+    const int64_t r0 = (int64_t)(j + 1) * TS, c0 = (int64_t)j * TS;
+    const int m = (int)(np - r0);
+    const int G = (m + 255) / 256;
+    const double* P = b->Ab + r0 * np + c0;
+    double* Yr = b->Y + r0 * RLD;
+    hipLaunchKernelGGL(qt_partial_kernel, dim3(G), dim3(256), 0, s, P, np, m, Yr, b->qtp);
+    BD_LAUNCH("qt_partial_kernel");
+    hipLaunchKernelGGL(qt_reduce_kernel, dim3(1), dim3(256), 0, s, b->qtp, G,
+                       b->Tm + (int64_t)j * TS * TS, b->qb);
+    BD_LAUNCH("qt_reduce_kernel");
+    hipLaunchKernelGGL(qt_apply_kernel, dim3(G), dim3(256), 0, s, P, np, m, Yr, b->qb);
+    BD_LAUNCH("qt_apply_kernel");
+  }
+  BD_TRY(hipEventRecord(b->ev1, s));
+  BD_TRY(hipEventSynchronize(b->ev1));
+  float ms = 0.f;
+  BD_TRY(hipEventElapsedTime(&ms, b->ev0, b->ev1));
+  b->rhs_ms = ms;
+  b->nrhs = nrhs;
+  return 0;
+}
+
+int gpmi_band_loglik(gpmi_band* b, const double* etas, int neta, double* logdet, double* gram,
+                     int* info) {
+  if (!b) return set_error(-1006, "null handle");
+  if (neta <= 0) return 0;
+  Guard g(b->device);
+  int rc = ensure_cap(b, neta);
+  if (rc) return rc;
+  hipStream_t s = b->stream;
+  BD_TRY(hipMemcpyAsync(b->etas, etas, sizeof(double) * neta, hipMemcpyHostToDevice, s));
+  BD_TRY(hipEventRecord(b->ev0, s));
+  hipLaunchKernelGGL(band_chol_kernel, dim3(neta), dim3(256), 0, s, b->Ab, b->n_pad, b->nt, b->n,
+                     b->Y, b->etas, b->out, OUT_LD, b->info);
+  BD_LAUNCH("band_chol_kernel");
+  BD_TRY(hipEventRecord(b->ev1, s));
+  std::vector<double> hout((size_t)neta * OUT_LD);
+  std::vector<int> hinfo(neta);
+  BD_TRY(hipMemcpyAsync(hout.data(), b->out, sizeof(double) * hout.size(), hipMemcpyDeviceToHost,
+                        s));
+  BD_TRY(hipMemcpyAsync(hinfo.data(), b->info, sizeof(int) * neta, hipMemcpyDeviceToHost, s));
+  BD_TRY(hipStreamSynchronize(s));
+  float ms = 0.f;
+  BD_TRY(hipEventElapsedTime(&ms, b->ev0, b->ev1));
+  b->loglik_ms = ms;
+  const int m = b->nrhs;
+  for (int e = 0; e < neta; ++e) {
+    if (logdet) logdet[e] = hout[(size_t)e * OUT_LD];
+    if (gram)
+      for (int a = 0; a < m; ++a)
+        for (int c = 0; c < m; ++c)
+          gram[((size_t)e * m + a) * m + c] = hout[(size_t)e * OUT_LD + 1 + a * RLD + c];
+    if (info) info[e] = hinfo[e];
+  }
+  return 0;
+}
+
+int gpmi_band_get(gpmi_band* b, double* B_out, int64_t ld) {
+  if (!b) return set_error(-1006, "null handle");
+  Guard g(b->device);
+  const int64_t np = b->n_pad, n = b->n;
+  std::vector<double> h((size_t)np * np);
+  BD_TRY(hipMemcpyAsync(h.data(), b->Ab, sizeof(double) * h.size(), hipMemcpyDeviceToHost,
+                        b->stream));
+  BD_TRY(hipStreamSynchronize(b->stream));
+  for (int64_t i = 0; i < n; ++i)
+    for (int64_t j = 0; j < n; ++j) {
+      const int64_t hi = std::max(i, j), lo = std::min(i, j);
+      B_out[i * ld + j] = (hi - lo <= TS) ? h[(size_t)hi * np + lo] : 0.0;
+    }
+  return 0;
+}
+
+int gpmi_band_last_timing(gpmi_band* b, double* reduce_ms, double* rhs_ms, double* loglik_ms) {
+  if (!b) return set_error(-1006, "null handle");
+  if (reduce_ms) *reduce_ms = b->reduce_ms;
+  if (rhs_ms) *rhs_ms = b->rhs_ms;
+  if (loglik_ms) *loglik_ms = b->loglik_ms;
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,231 @@
+// 128x128 SPD block factorization and inversion in LDS, shared by the
+// diagonal-block kernel of the blocked Cholesky (gpmi_diag.hip) and the banded
+// Cholesky of the band path (gpmi_band.hip). One 256-thread workgroup.
+//
+//   lds_chol_block : Ls (lower, row stride DL) <- L = chol(Ls), blocked by 16:
+//                    in-register 16x16 factor (wave 0, rsq + Newton pivots),
+//                    16-wide panel solve, MFMA trailing update. inv(L_jj) of the
+//                    eight 16x16 diagonal blocks are left in Aux[8][16][16],
+//                    diag(L) in sdiag, the first non-positive pivot (1-based)
+//                    in *s_fail.
+//   lds_inv_block  : Ls <- L^-1 (lower), column blocks in parallel over the 4
+//                    waves, X_ij = -X_ii sum_k L_ik X_kj on fp64 MFMA with the X
+//                    column held in registers.
+//
+// f64 MFMA 16x16x4 maps: A[i = lane&15][k = lane>>4], B[k = lane>>4][j = lane&15],
+// C/D: lane holds rows (lane>>4) + 4 r (r = 0..3) of column lane&15.
+#pragma once
+
+#include "gpmi_device.h"
+
+namespace gpmi {
+
+constexpr int DB = 16;         // inner block
+constexpr int NDB = TS / DB;   // 8
+constexpr int DL = 130;        // LDS row stride in doubles (conflict-free MFMA A reads)
+
+// Broadcast a double from a compile-time-uniform source lane (v_readlane, no LDS).
+__device__ __forceinline__ double readlane_d(double v, int lane) {
+  const long long b = __double_as_longlong(v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(b & 0xffffffffLL), lane);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(b >> 32), lane);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+// 1/sqrt(d) to double precision: hardware estimate + two Newton steps.
+__device__ __forceinline__ double rsqrt_nr(double d) {
+  double r = __builtin_amdgcn_rsq(d);
+  r = r * (1.5 - 0.5 * d * r * r);
+  r = r * (1.5 - 0.5 * d * r * r);
+  return r;
+}
+
+// Column block J of X = L^-1 (rows J..7), X_JJ already in the LDS diagonal tile.
+// Xc[i - J] holds X_iJ in C/D layout (= B-operand layout, k = row).
+template <int J>
+__device__ __forceinline__ void inv_colblock(const double* Ls, d4 (&Xc)[NDB - J], int fr,
+                                             int fk) {
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) Xc[0][rr] = Ls[(J * DB + fk + 4 * rr) * DL + J * DB + fr];
+#pragma unroll
+  for (int i = J + 1; i < NDB; ++i) {
+    d4 T0 = {0.0, 0.0, 0.0, 0.0}, T1 = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int k = J; k < i; ++k) {
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const double av = Ls[(i * DB + fr) * DL + k * DB + 4 * kk + fk];
+        if (kk & 1) T1 = mfma64(av, Xc[k - J][kk], T1);
+        else T0 = mfma64(av, Xc[k - J][kk], T0);
+      }
+    }
+    const d4 T = T0 + T1;
+    d4 Xt = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const double av = -Ls[(i * DB + fr) * DL + i * DB + 4 * kk + fk];
+      Xt = mfma64(av, T[kk], Xt);
+    }
+    Xc[i - J] = Xt;
+  }
+}
+
+template <int J>
+__device__ __forceinline__ void store_colblock(double* Ls, const d4 (&Xc)[NDB - J], int fr,
+                                               int fk) {
+#pragma unroll
+  for (int i = J; i < NDB; ++i)
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) Ls[(i * DB + fk + 4 * rr) * DL + J * DB + fr] = Xc[i - J][rr];
+}
+
+
+__device__ __forceinline__ void lds_chol_block(double* Ls, double* Aux, double* sdiag,
+                                               int* s_fail) {
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int fr = lane & 15, fk = lane >> 4;
+  for (int jb = 0; jb < NDB; ++jb) {
+    const int j0 = jb * DB;
+    // ---- F1: factor and invert the 16x16 diagonal block in registers (wave 0)
+    if (w == 0) {
+      const int r = lane >> 2, g = lane & 3;
+      double a[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) a[k] = Ls[(j0 + r) * DL + j0 + 4 * g + k];
+      double myrinv = 0.0;
+#pragma unroll
+      for (int j = 0; j < DB; ++j) {
+        const int sk = j & 3, sg = j >> 2;
+        const double d = readlane_d(a[sk], (j << 2) | sg);
+        const double crj = __shfl(a[sk], (r << 2) | sg);
+        double lcj[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) lcj[k] = __shfl(a[sk], ((4 * g + k) << 2) | sg);
+        const double rinv = rsqrt_nr(d);
+        const double ljj = d * rinv;
+        if (lane == 0) {
+          if (!(d > 0.0) && *s_fail == 0) *s_fail = j0 + j + 1;
+          sdiag[j0 + j] = ljj;
+        }
+        if (r == j) myrinv = rinv;
+        const double lrj = (r > j) ? crj * rinv : ((r == j) ? ljj : 0.0);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int c = 4 * g + k;
+          if (c > j && c <= r) a[k] -= lrj * (lcj[k] * rinv);
+        }
+        if (g == sg) a[sk] = lrj;
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) Ls[(j0 + r) * DL + j0 + 4 * g + k] = a[k];
+      // X = inv(L_jj): row p of X is final once the rows above it are.
+      double lrow[DB];   // L[r][p], p = 0..15
+#pragma unroll
+      for (int p = 0; p < DB; ++p) lrow[p] = __shfl(a[p & 3], (r << 2) | (p >> 2));
+      double s[4] = {0.0, 0.0, 0.0, 0.0}, x[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int p = 0; p < DB; ++p) {
+        if (r == p) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) x[k] = (((4 * g + k) == p ? 1.0 : 0.0) - s[k]) * myrinv;
+        }
+        double xp[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) xp[k] = __shfl(x[k], (p << 2) | g);
+        if (r > p) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) s[k] += lrow[p] * xp[k];
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) Aux[jb * 256 + r * 16 + 4 * g + k] = x[k];
+    }
+    __syncthreads();
+    // ---- F2: panel rows below: L[i][j0 + c] = sum_p A[i][j0 + p] X[c][p]
+    {
+      const int row = j0 + DB + (t >> 1), h = t & 1;
+      double av[DB];
+      if (row < TS) {
+#pragma unroll
+        for (int p = 0; p < DB; ++p) av[p] = Ls[row * DL + j0 + p];
+      }
+      __syncthreads();
+      if (row < TS) {
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          const double* xr = &Aux[jb * 256 + (8 * h + c) * 16];
+          double o = 0.0;
+#pragma unroll
+          for (int p = 0; p < DB; ++p) o += av[p] * xr[p];
+          Ls[row * DL + j0 + 8 * h + c] = o;
+        }
+      }
+    }
+    __syncthreads();
+    // ---- F3: trailing update of tiles (ti, tj), jb < tj <= ti < 8, K = 16 (MFMA)
+    {
+      const int m = NDB - 1 - jb;               // trailing tiles per side
+      const int ntile = m * (m + 1) / 2;
+      for (int q = w; q < ntile; q += 4) {
+        int ti = 0;
+        while ((ti + 1) * (ti + 2) / 2 <= q) ++ti;
+        const int tj = q - ti * (ti + 1) / 2;
+        const int r0 = (jb + 1 + ti) * DB, c0 = (jb + 1 + tj) * DB;
+        d4 acc;
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) acc[rr] = Ls[(r0 + fk + 4 * rr) * DL + c0 + fr];
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+          const double av = -Ls[(r0 + fr) * DL + j0 + 4 * kk + fk];
+          const double bv = Ls[(c0 + fr) * DL + j0 + 4 * kk + fk];
+          acc = mfma64(av, bv, acc);
+        }
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) Ls[(r0 + fk + 4 * rr) * DL + c0 + fr] = acc[rr];
+      }
+    }
+    __syncthreads();
+  }
+}
+
+__device__ __forceinline__ void lds_inv_block(double* Ls, const double* Aux) {
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int fr = lane & 15, fk = lane >> 4;
+  for (int e = t; e < NDB * 256; e += 256) {
+    const int jb = e >> 8, r = (e >> 4) & 15, c = e & 15;
+    Ls[(jb * DB + r) * DL + jb * DB + c] = Aux[e];
+  }
+  __syncthreads();
+  // balanced column-block ownership: {0}, {1,7}, {2,6}, {3,4,5}
+  if (w == 0) {
+    d4 X0[8];
+    inv_colblock<0>(Ls, X0, fr, fk);
+    __syncthreads();
+    store_colblock<0>(Ls, X0, fr, fk);
+  } else if (w == 1) {
+    d4 X1[7], X7[1];
+    inv_colblock<1>(Ls, X1, fr, fk);
+    inv_colblock<7>(Ls, X7, fr, fk);
+    __syncthreads();
+    store_colblock<1>(Ls, X1, fr, fk);
+    store_colblock<7>(Ls, X7, fr, fk);
+  } else if (w == 2) {
+    d4 X2[6], X6[2];
+    inv_colblock<2>(Ls, X2, fr, fk);
+    inv_colblock<6>(Ls, X6, fr, fk);
+    __syncthreads();
+    store_colblock<2>(Ls, X2, fr, fk);
+    store_colblock<6>(Ls, X6, fr, fk);
+  } else {
+    d4 X3[5], X4[4], X5[3];
+    inv_colblock<3>(Ls, X3, fr, fk);
+    inv_colblock<4>(Ls, X4, fr, fk);
+    inv_colblock<5>(Ls, X5, fr, fk);
+    __syncthreads();
+    store_colblock<3>(Ls, X3, fr, fk);
+    store_colblock<4>(Ls, X4, fr, fk);
+    store_colblock<5>(Ls, X5, fr, fk);
+  }
+}
+
+}  // namespace gpmi

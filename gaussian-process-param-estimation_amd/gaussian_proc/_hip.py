@@ -75,6 +75,13 @@ SIGNATURES = {
     'gpmi_sp_msgram': (ctypes.c_int, [c_op_p, c_double_p, ctypes.c_int, c_double_p, c_i64,
                                       ctypes.c_int, ctypes.c_double, ctypes.c_int, c_double_p,
                                       c_int_p]),
+    'gpmi_band_create': (ctypes.c_int, [c_op_p, ctypes.POINTER(c_op_p)]),
+    'gpmi_band_destroy': (ctypes.c_int, [c_op_p]),
+    'gpmi_band_set_rhs': (ctypes.c_int, [c_op_p, c_double_p, c_i64, ctypes.c_int]),
+    'gpmi_band_loglik': (ctypes.c_int, [c_op_p, c_double_p, ctypes.c_int, c_double_p,
+                                        c_double_p, c_int_p]),
+    'gpmi_band_get': (ctypes.c_int, [c_op_p, c_double_p, c_i64]),
+    'gpmi_band_last_timing': (ctypes.c_int, [c_op_p, c_double_p, c_double_p, c_double_p]),
 }
 
 
@@ -267,6 +274,76 @@ class Operator(object):
 
     def set_outer(self, s):
         check(self.lib.gpmi_op_set_outer(self.h, int(s)), 'gpmi_op_set_outer')
+
+
+class Band(object):
+    """Owning wrapper of a ``gpmi_band`` handle: the operator's K reduced once on
+    the device to band form K = Q B Q^T (bandwidth 128); afterwards logdet and
+    the Gram block R^T (K + eta I)^-1 R for any number of eta cost one banded
+    Cholesky each (all eta concurrently, one workgroup per eta)."""
+
+    CHUNK = 4096   # eta values per device call
+
+    def __init__(self, op):
+        self.lib = load()
+        self.op = op   # keeps the operator (and its device) alive
+        self.n = op.n
+        self.device = op.device
+        h = c_op_p()
+        check(self.lib.gpmi_band_create(op.h, ctypes.byref(h)), 'gpmi_band_create')
+        self.h = h
+        self.nrhs = 0
+
+    def close(self):
+        if getattr(self, 'h', None) is not None and self.h.value:
+            self.lib.gpmi_band_destroy(self.h)
+            self.h = c_op_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_rhs(self, R):
+        R = as_c(R)
+        if R.ndim == 1:
+            R = R[:, None]
+        if R.shape[0] != self.n or R.shape[1] > MAX_RHS:
+            raise ValueError('RHS must be %d x k with k <= %d' % (self.n, MAX_RHS))
+        check(self.lib.gpmi_band_set_rhs(self.h, dptr(R), R.shape[1], R.shape[1]),
+              'gpmi_band_set_rhs')
+        self.nrhs = R.shape[1]
+
+    def loglik(self, etas):
+        """-> (logdet[neta], gram[neta, nrhs, nrhs], info[neta])"""
+        etas = as_c(numpy.atleast_1d(etas))
+        ne = etas.shape[0]
+        ld = numpy.empty(ne)
+        g = numpy.empty((ne, self.nrhs, self.nrhs))
+        info = numpy.zeros(ne, dtype=numpy.int32)
+        for i in range(0, ne, self.CHUNK):
+            e = as_c(etas[i:i + self.CHUNK])
+            k = e.shape[0]
+            ldk = numpy.empty(k)
+            gk = numpy.empty((k, self.nrhs, self.nrhs))
+            ik = numpy.zeros(k, dtype=numpy.int32)
+            check(self.lib.gpmi_band_loglik(self.h, dptr(e), k, dptr(ldk), dptr(gk),
+                                            ik.ctypes.data_as(c_int_p)), 'gpmi_band_loglik')
+            ld[i:i + k], g[i:i + k], info[i:i + k] = ldk, gk, ik
+        return ld, g, info
+
+    def band(self):
+        """B as a dense symmetric n x n host matrix (tests)."""
+        B = numpy.empty((self.n, self.n))
+        check(self.lib.gpmi_band_get(self.h, dptr(B), self.n), 'gpmi_band_get')
+        return B
+
+    def last_timing(self):
+        a, b, c = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+        check(self.lib.gpmi_band_last_timing(self.h, ctypes.byref(a), ctypes.byref(b),
+                                             ctypes.byref(c)), 'gpmi_band_last_timing')
+        return dict(reduce_ms=a.value, rhs_ms=b.value, loglik_ms=c.value)
 
 
 def matern_dense(points, scale, nu, device=None):

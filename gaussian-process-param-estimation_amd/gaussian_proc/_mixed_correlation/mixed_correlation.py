@@ -68,6 +68,40 @@ class MixedCorrelation(object):
         self.n = self.op.n
         self._trace_cache = None
         self._rhs_cache = None
+        self._band = None
+        self._band_rhs = None
+
+    # ---- 'eigenvalue': one-time band reduction -----------------------------
+
+    def band(self):
+        """The one-time spectral setup of imate_method='eigenvalue' (the
+        reference's eigh(K) in __init__, mixed_correlation.py:76-79), on the
+        device: K = Q B Q^T with B banded (bandwidth 128), computed on first use.
+        Afterwards logdet(eta) and the likelihood terms cost one banded Cholesky
+        of B + eta I per eta (csrc/gpmi_band.hip)."""
+        if self._band is None:
+            self._band = _hip.Band(self.op)
+        return self._band
+
+    def _band_terms(self, etas, X=None, z=None):
+        b = self.band()
+        if X is not None:
+            X = numpy.asarray(X, dtype=float)
+            z = numpy.asarray(z, dtype=float)
+            c = self._band_rhs
+            if c is None or c[0].shape != X.shape or not numpy.array_equal(c[0], X) or \
+                    not numpy.array_equal(c[1], z):
+                if X.shape[1] + 1 > _hip.MAX_RHS:
+                    raise ValueError('at most %d basis functions' % (_hip.MAX_RHS - 1))
+                b.set_rhs(numpy.column_stack([X, z]))
+                self._band_rhs = (X.copy(), z.copy())
+        ld, g, info = b.loglik(etas)
+        if numpy.any(info):
+            bad = int(numpy.flatnonzero(info)[0])
+            raise numpy.linalg.LinAlgError(
+                'K + eta I is not positive definite for eta = %r (pivot %d)'
+                % (numpy.atleast_1d(etas)[bad], info[bad]))
+        return ld, g
 
     # ---- sparse K (tapered Matérn, CSR on the device) -------------------------
 
@@ -186,6 +220,8 @@ class MixedCorrelation(object):
                 raise NotImplementedError('slq logdet is not implemented yet')
             raise ValueError('Existing methods are "eigenvalue", "cholesky",'
                              ' and "slq".')
+        if self.imate_method == 'eigenvalue':
+            return exponent * float(self._band_terms([eta])[0][0])
         return exponent * self.op.logdet(eta)
 
     def solve(self, eta, Y):                                       # :280-299
@@ -234,6 +270,8 @@ class MixedCorrelation(object):
             R = numpy.column_stack([numpy.asarray(X, dtype=float), numpy.asarray(z, dtype=float)])
             lds = numpy.array([self.logdet(e) for e in etas])
             return lds, self.sop.msgram(etas, R, rtol=self.cg_rtol)
+        if self.imate_method == 'eigenvalue':
+            return self._band_terms(etas, X, z)
         self.set_rhs(X, z)
         lds, gs = [], []
         mb = self.op.max_batch

@@ -179,6 +179,42 @@ int gpmi_sp_msgram(gpmi_sp* sp, const double* etas, int neta, const double* rhs,
  * [n][s] block already in HBM; average ms per launch (HIP events). */
 int gpmi_sp_bench_spmm(gpmi_sp* sp, int s, int reps, double eta, double* avg_ms);
 
+/* -------------------------------------------------------------------- band --
+ * One-time orthogonal reduction of an operator's K to symmetric band form,
+ * K = Q B Q^T with bandwidth 128 (blocked Householder panels, two-sided
+ * updates on fp64 MFMA, 4/3 n^3 flops), after which every eta costs one banded
+ * Cholesky of B + eta I, O(n 128^2), since K + eta I = Q (B + eta I) Q^T.
+ * This is the device form of the reference's one-time spectral setup:
+ *   MixedCorrelation.__init__ with imate_method='eigenvalue' runs eigh(K) once
+ *   (mixed_correlation.py:76-79) so that logdet(eta) is cheap for every eta
+ *   (:239-248); Likelihood builds its operator that way (likelihood.py:41-49).
+ * n <= 32768. */
+typedef struct gpmi_band gpmi_band;
+
+/* Reduce the operator's current K (the operator stays usable; the band form is
+ * a copy). Blocks until the reduction is done. */
+int gpmi_band_create(gpmi_op* op, gpmi_band** out);
+int gpmi_band_destroy(gpmi_band* b);
+
+/* Y = Q^T R for an [n][ld] host block R with nrhs <= 16 columns (resident). */
+int gpmi_band_set_rhs(gpmi_band* b, const double* rhs, int64_t ld, int nrhs);
+
+/* For any number of eta values (one workgroup per eta, all concurrent):
+ *   logdet[e]           = log det(K + eta_e I) = log det(B + eta_e I)
+ *   gram[e][nrhs][nrhs] = R^T (K + eta_e I)^-1 R = Y^T (B + eta_e I)^-1 Y
+ *   info[e]             = 0, or 1-based first non-positive pivot.
+ * Replaces the logdet + 2 x solve of DirectLikelihood.log_likelihood
+ * (_direct_likelihood.py:59,62,332) on the 'eigenvalue' operator. */
+int gpmi_band_loglik(gpmi_band* b, const double* etas, int neta, double* logdet,
+                     double* gram, int* info);
+
+/* The band matrix B as a dense symmetric [n][ld] host matrix (tests). */
+int gpmi_band_get(gpmi_band* b, double* B_out, int64_t ld);
+
+/* Device ms of the last reduction, Q^T application and loglik call (HIP events). */
+int gpmi_band_last_timing(gpmi_band* b, double* reduce_ms, double* rhs_ms,
+                          double* loglik_ms);
+
 #ifdef __cplusplus
 }
 #endif
