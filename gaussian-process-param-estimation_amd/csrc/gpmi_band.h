@@ -7,17 +7,23 @@ namespace gpmi {
 
 enum { KFAST = 0, KSLOW = 1 };
 
-constexpr int HH_ROWS = 256;       // panel rows per hh_col workgroup (16 waves x 16 rows)
+constexpr int HH_WAVES = 8;        // hh_col workgroup: 8 waves x 16 rows = 128 panel rows
+constexpr int HH_THREADS = 64 * HH_WAVES;
 constexpr int HH_RPW = 16;
-constexpr int HH_MAXG = 128;       // max hh_col workgroups (n_pad <= 32768)
+constexpr int HH_ROWS = HH_WAVES * HH_RPW;
+constexpr int HH_MAXG = 256;       // max hh_col workgroups (n_pad <= 32768)
+constexpr int HH_PANEL_MAXG = 128;  // hh_panel (single-launch) workgroups: m <= 16384
+constexpr int HH_PANEL_LDS = 96 * 1024;  // dynamic LDS: one hh_panel workgroup per CU
 constexpr int HH_PART_LD = 136;    // partial record: S_j (j < 128), sum x^2 at [128]
-constexpr int TN_CH = 1024;        // rows per tn_partial chunk
+constexpr int TN_CH = 256;         // rows per tn_partial chunk
 constexpr int SY_CH = 16;          // tile columns per symm split-K chunk
 constexpr int BAND_ULD = 384;      // U = [W | V | W]
 constexpr int BAND_MAX_NPAD = HH_MAXG * HH_ROWS;
 
 __global__ void hh_col_kernel(double* P, int64_t lda, int m, int c, double* part, double* pivrow,
                               double* tau);
+__global__ void hh_panel_kernel(double* P, int64_t lda, int m, double* part, double* pivrow,
+                                unsigned* counter, double* tau, int* err);
 __global__ void vcopy_kernel(const double* P, int64_t lda, int m, double* U, int64_t ldu);
 __global__ void tn_partial_kernel(const double* P1, int64_t ld1, const double* P2, int64_t ld2,
                                   int m, double* part);

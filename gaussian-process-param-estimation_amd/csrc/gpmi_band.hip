@@ -16,7 +16,7 @@
 //                          column (partial sums of the next column published per
 //                          workgroup; the panel rows live in registers)
 //   vcopy + tn_partial/reduce + tbuild    V (unit lower) and the compact-WY T:
-//                          T[0:c, c] = -tau_c T[0:c, 0:c] (V^T V)[0:c, c]
+//                          T = (diag(1/tau) + striu(V^T V))^-1 (LDS MFMA inverse)
 //   symm -> psum -> xt     X = A22 V T (A22 lower-stored: transposed tile reads above
 //                          the diagonal), split-K partials summed deterministically
 //   tn_partial/reduce(V,X) -> z -> w      W = X - 1/2 V (T^T V^T X)
@@ -158,7 +158,7 @@ __device__ __forceinline__ void store_tile(double* C, int64_t ldc, const d4 (&ac
 
 // ---------------------------------------------------------------------------
 // Householder QR of the m x 128 panel P (row-major, ld lda), column c.
-// Workgroup g owns panel rows [256 g, 256 g + 256) (16 waves x 16 rows, lanes
+// Workgroup g owns panel rows [128 g, 128 g + 128) (8 waves x 16 rows, lanes
 // over the columns, two columns per lane); its rows are loaded into registers
 // before the reduction of the previous launch's partials completes.
 // Inputs (written by launch c - 1): part[c & 1][g'] = partial sums over the rows
@@ -170,17 +170,15 @@ __device__ __forceinline__ void store_tile(double* C, int64_t ldc, const d4 (&ac
 // Then P_ij -= tau v_i w_j (j > c), column c <- (alpha; v), and the partials of
 // column c + 1 are published. c = -1 publishes the partials of column 0 only.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(1024) void hh_col_kernel(double* __restrict__ P, int64_t lda,
+__global__ __launch_bounds__(HH_THREADS) void hh_col_kernel(double* __restrict__ P, int64_t lda,
                                                       int m, int c, double* __restrict__ part,
                                                       double* __restrict__ pivrow,
                                                       double* __restrict__ tau) {
-  __shared__ double sS[HH_PART_LD];
-  __shared__ double sw[TS];
-  __shared__ double sacc[16][HH_PART_LD];
-  __shared__ double sscal[3];
+  __shared__ double sacc[HH_WAVES][HH_PART_LD];
   const int G = gridDim.x, g = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int j0 = lane, j1 = lane + 64;
   const int rbase = g * HH_ROWS + w * HH_RPW;
+  // every independent load first: own rows, the pivot row, the partial records
   double p0[HH_RPW], p1[HH_RPW];
 #pragma unroll
   for (int q = 0; q < HH_RPW; ++q) {
@@ -193,52 +191,48 @@ __global__ __launch_bounds__(1024) void hh_col_kernel(double* __restrict__ P, in
       if (j1 >= c) p1[q] = row[j1];
     }
   }
-  double tau_c = 0.0, scale = 0.0, alpha = 0.0;
+  double tau_c = 0.0, scale = 0.0, alpha = 0.0, w0 = 0.0, w1 = 0.0;
   if (c >= 0) {
+    const double pv0 = pivrow[(c & 1) * TS + j0];
+    const double pv1 = pivrow[(c & 1) * TS + j1];
     const double* pp = part + (size_t)(c & 1) * HH_MAXG * HH_PART_LD;
     double s0 = 0.0, s1 = 0.0, sn = 0.0;
-    for (int q = w; q < G; q += 16) {
-      s0 += pp[q * HH_PART_LD + j0];
-      s1 += pp[q * HH_PART_LD + j1];
-      sn += pp[q * HH_PART_LD + 128];
+#pragma unroll 4
+    for (int u = 0; u < HH_MAXG / HH_WAVES; ++u) {
+      const int q = w + HH_WAVES * u;
+      if (q < G) {
+        s0 += pp[q * HH_PART_LD + j0];
+        s1 += pp[q * HH_PART_LD + j1];
+        sn += pp[q * HH_PART_LD + 128];
+      }
     }
     sacc[w][j0] = s0;
     sacc[w][j1] = s1;
     if (lane == 0) sacc[w][128] = sn;
     __syncthreads();
-    if (t <= 128) {
-      double s = 0.0;
+    double S0 = 0.0, S1 = 0.0, nb2 = 0.0;
 #pragma unroll
-      for (int q = 0; q < 16; ++q) s += sacc[q][t];
-      sS[t] = s;
+    for (int q = 0; q < HH_WAVES; ++q) {
+      S0 += sacc[q][j0];
+      S1 += sacc[q][j1];
+      nb2 += sacc[q][128];
     }
-    __syncthreads();
-    if (t == 0) {
-      const double x0 = pivrow[(c & 1) * TS + c];
-      const double nb2 = sS[128];
-      double tc = 0.0, sc = 0.0, al = x0;
-      if (nb2 > 0.0) {
-        const double nrm = sqrt(x0 * x0 + nb2);
-        al = x0 >= 0.0 ? -nrm : nrm;
-        tc = (al - x0) / al;
-        sc = 1.0 / (x0 - al);
-      }
-      sscal[0] = tc;
-      sscal[1] = sc;
-      sscal[2] = al;
-      if (g == 0) tau[c] = tc;
+    // the reflector, computed identically by every thread (no broadcast step)
+    const double x0 = readlane_d(c < 64 ? pv0 : pv1, c & 63);
+    if (nb2 > 0.0) {
+      const double nrm = sqrt(x0 * x0 + nb2);
+      alpha = x0 >= 0.0 ? -nrm : nrm;
+      tau_c = (alpha - x0) / alpha;
+      scale = 1.0 / (x0 - alpha);
+    } else {
+      alpha = x0;
     }
-    __syncthreads();
-    tau_c = sscal[0];
-    scale = sscal[1];
-    alpha = sscal[2];
-    if (t < TS && t > c) sw[t] = (sS[t] - alpha * pivrow[(c & 1) * TS + t]) * scale;
-    __syncthreads();
+    if (g == 0 && t == 0) tau[c] = tau_c;
+    if (j0 > c) w0 = (S0 - alpha * pv0) * scale;
+    if (j1 > c) w1 = (S1 - alpha * pv1) * scale;
   }
   const bool act = tau_c != 0.0;
   const int c1 = c + 1;
-  const double w0 = (act && j0 > c) ? sw[j0] : 0.0;
-  const double w1 = (act && j1 > c) ? sw[j1] : 0.0;
   double a0 = 0.0, a1 = 0.0, nb = 0.0;
 #pragma unroll
   for (int q = 0; q < HH_RPW; ++q) {
@@ -246,7 +240,7 @@ __global__ __launch_bounds__(1024) void hh_col_kernel(double* __restrict__ P, in
     if (i >= m || i < c) continue;
     double* row = P + (int64_t)i * lda;
     if (act) {
-      const double xc = __shfl(c < 64 ? p0[q] : p1[q], c & 63);
+      const double xc = readlane_d(c < 64 ? p0[q] : p1[q], c & 63);
       const double vi = (i == c) ? 1.0 : xc * scale;
       const double tv = tau_c * vi;
       p0[q] -= tv * w0;
@@ -257,9 +251,9 @@ __global__ __launch_bounds__(1024) void hh_col_kernel(double* __restrict__ P, in
       if (j1 >= c) row[j1] = p1[q];
     }
     if (c1 < TS && i >= c1) {
-      const double x = __shfl(c1 < 64 ? p0[q] : p1[q], c1 & 63);
-      if (j0 >= c1) a0 += x * p0[q];
-      if (j1 >= c1) a1 += x * p1[q];
+      const double x = readlane_d(c1 < 64 ? p0[q] : p1[q], c1 & 63);
+      a0 += x * p0[q];
+      a1 += x * p1[q];
       if (i > c1) nb += x * x;
       if (i == c1) {
         if (j0 >= c1) pivrow[(c1 & 1) * TS + j0] = p0[q];
@@ -276,8 +270,189 @@ __global__ __launch_bounds__(1024) void hh_col_kernel(double* __restrict__ P, in
   if (t <= 128 && t >= c1) {
     double s = 0.0;
 #pragma unroll
-    for (int q = 0; q < 16; ++q) s += sacc[q][t];
+    for (int q = 0; q < HH_WAVES; ++q) s += sacc[q][t];
     part[((size_t)(c1 & 1) * HH_MAXG + g) * HH_PART_LD + t] = s;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// The same panel QR in ONE launch (G <= HH_PANEL_MAXG workgroups, one per CU,
+// all co-resident): the panel rows stay in registers for all 128 columns and
+// the per-column reduction is exchanged inside the launch. Hand-off (the
+// write-through form of the guide's publish/consume recipe): every partial
+// record and pivot-row word is stored sc1 (agent-scope relaxed atomic store),
+// each storing wave drains vmcnt, the workgroup barrier follows, then ONE lane
+// adds to the monotonic counter (agent scope). Consumers: ONE lane polls the
+// counter with sc1 loads until it reaches G (c + 1), a workgroup barrier, then
+// every read of a record is an sc1 load. Records are double-buffered by column
+// parity: a workgroup publishing column c + 1 has seen every workgroup publish
+// column c, i.e. finish reading the slot it overwrites. Every spin is bounded;
+// a timeout sets *err and all workgroups leave (the host reports the error).
+// counter[0] must be zero at launch (the host memsets it per panel).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void st_sc1(double* p, double v) {
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p),
+                     (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_sc1(const double* p) {
+  return __longlong_as_double((long long)__hip_atomic_load(
+      reinterpret_cast<const unsigned long long*>(p), __ATOMIC_RELAXED,
+      __HIP_MEMORY_SCOPE_AGENT));
+}
+
+__global__ __launch_bounds__(HH_THREADS) void hh_panel_kernel(double* __restrict__ P,
+                                                              int64_t lda, int m,
+                                                              double* __restrict__ part,
+                                                              double* __restrict__ pivrow,
+                                                              unsigned* __restrict__ counter,
+                                                              double* __restrict__ tau,
+                                                              int* __restrict__ err) {
+  extern __shared__ double dyn_lds[];   // sized by the host to keep one workgroup per CU
+  double(*sacc)[HH_PART_LD] = reinterpret_cast<double(*)[HH_PART_LD]>(dyn_lds);
+  __shared__ int s_bail;
+  const int G = gridDim.x, g = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int j0 = lane, j1 = lane + 64;
+  const int rbase = g * HH_ROWS + w * HH_RPW;
+  double p0[HH_RPW], p1[HH_RPW];
+#pragma unroll
+  for (int q = 0; q < HH_RPW; ++q) {
+    const int i = rbase + q;
+    p0[q] = 0.0;
+    p1[q] = 0.0;
+    if (i < m) {
+      const double* row = P + (int64_t)i * lda;
+      p0[q] = row[j0];
+      p1[q] = row[j1];
+    }
+  }
+  if (t == 0) s_bail = 0;
+  const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
+      part, (short)0, (int)(2 * HH_MAXG * HH_PART_LD * sizeof(double)), 0x00020000);
+  // publish the partials of column c1 (slot c1 & 1) from the registers
+  auto publish = [&](int c1) {
+    double a0 = 0.0, a1 = 0.0, nb = 0.0;
+#pragma unroll
+    for (int q = 0; q < HH_RPW; ++q) {
+      const int i = rbase + q;
+      if (i >= m || i < c1) continue;
+      const double x = readlane_d(c1 < 64 ? p0[q] : p1[q], c1 & 63);
+      a0 += x * p0[q];
+      a1 += x * p1[q];
+      if (i > c1) nb += x * x;
+      if (i == c1) {
+        if (j0 >= c1) st_sc1(pivrow + (c1 & 1) * TS + j0, p0[q]);
+        if (j1 >= c1) st_sc1(pivrow + (c1 & 1) * TS + j1, p1[q]);
+      }
+    }
+    __syncthreads();   // sacc is free (previous readers done)
+    sacc[w][j0] = a0;
+    sacc[w][j1] = a1;
+    if (lane == 0) sacc[w][128] = nb;
+    __syncthreads();
+    if (t <= 128 && t >= c1) {
+      double s = 0.0;
+#pragma unroll
+      for (int q = 0; q < HH_WAVES; ++q) s += sacc[q][t];
+      st_sc1(part + ((size_t)(c1 & 1) * HH_MAXG + g) * HH_PART_LD + t, s);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t == 0) __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  publish(0);
+  for (int c = 0; c < TS; ++c) {
+    // wait until every workgroup has published column c
+    if (t == 0) {
+      const unsigned target = (unsigned)G * (unsigned)(c + 1);
+      unsigned spins = 0;
+      while (__hip_atomic_load(counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+        __builtin_amdgcn_s_sleep(2);
+        if ((++spins & 1023u) == 0 &&
+            (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0 ||
+             spins > (1u << 24))) {
+          __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          s_bail = 1;
+          break;
+        }
+      }
+    }
+    __syncthreads();
+    if (s_bail) return;
+    // records of slot c & 1: lane l reads columns (2l, 2l + 1) of every record this
+    // wave owns with 16-byte sc1 loads, all in flight together; lane 0 also reads
+    // the x^2 sum at [128]
+    const uint32_t slot_off = (uint32_t)((c & 1) * HH_MAXG * HH_PART_LD * 8);
+    const double pv0 = ld_sc1(pivrow + (c & 1) * TS + j0);
+    const double pv1 = ld_sc1(pivrow + (c & 1) * TS + j1);
+    d2 rv[HH_PANEL_MAXG / HH_WAVES];
+    double rn[HH_PANEL_MAXG / HH_WAVES];
+#pragma unroll
+    for (int u = 0; u < HH_PANEL_MAXG / HH_WAVES; ++u) {
+      const int q = w + HH_WAVES * u;
+      rv[u] = d2{0.0, 0.0};
+      rn[u] = 0.0;
+      if (q < G) {
+        const uint32_t roff = slot_off + (uint32_t)(q * HH_PART_LD * 8);
+        rv[u] = __builtin_bit_cast(
+            d2, __builtin_amdgcn_raw_buffer_load_b128(prs, roff + 16 * lane, 0, 16));
+        if (lane == 0) rn[u] = ld_sc1(part + (roff >> 3) + 128);
+      }
+    }
+    d2 sv = {0.0, 0.0};
+    double sn = 0.0;
+#pragma unroll
+    for (int u = 0; u < HH_PANEL_MAXG / HH_WAVES; ++u) {
+      sv += rv[u];
+      sn += rn[u];
+    }
+    __syncthreads();   // sacc readers of the previous publish are done
+    sacc[w][2 * lane] = sv[0];
+    sacc[w][2 * lane + 1] = sv[1];
+    if (lane == 0) sacc[w][128] = sn;
+    __syncthreads();
+    double S0 = 0.0, S1 = 0.0, nb2 = 0.0;
+#pragma unroll
+    for (int q = 0; q < HH_WAVES; ++q) {
+      S0 += sacc[q][j0];
+      S1 += sacc[q][j1];
+      nb2 += sacc[q][128];
+    }
+    const double x0 = readlane_d(c < 64 ? pv0 : pv1, c & 63);
+    double tau_c = 0.0, scale = 0.0, alpha = x0;
+    if (nb2 > 0.0) {
+      const double nrm = sqrt(x0 * x0 + nb2);
+      alpha = x0 >= 0.0 ? -nrm : nrm;
+      tau_c = (alpha - x0) / alpha;
+      scale = 1.0 / (x0 - alpha);
+    }
+    if (g == 0 && t == 0) tau[c] = tau_c;
+    if (tau_c != 0.0) {
+      const double w0 = (j0 > c) ? (S0 - alpha * pv0) * scale : 0.0;
+      const double w1 = (j1 > c) ? (S1 - alpha * pv1) * scale : 0.0;
+#pragma unroll
+      for (int q = 0; q < HH_RPW; ++q) {
+        const int i = rbase + q;
+        if (i >= m || i < c) continue;
+        const double xc = readlane_d(c < 64 ? p0[q] : p1[q], c & 63);
+        const double vi = (i == c) ? 1.0 : xc * scale;
+        const double tv = tau_c * vi;
+        p0[q] -= tv * w0;
+        p1[q] -= tv * w1;
+        if (j0 == c) p0[q] = (i == c) ? alpha : vi;
+        if (j1 == c) p1[q] = (i == c) ? alpha : vi;
+      }
+    }
+    if (c + 1 < TS) publish(c + 1);
+  }
+#pragma unroll
+  for (int q = 0; q < HH_RPW; ++q) {
+    const int i = rbase + q;
+    if (i < m) {
+      double* row = P + (int64_t)i * lda;
+      row[j0] = p0[q];
+      row[j1] = p1[q];
+    }
   }
 }
 
@@ -317,31 +492,65 @@ __global__ __launch_bounds__(256) void tn_reduce_kernel(const double* __restrict
   out[e] = scale * s;
 }
 
-// Compact-WY T (upper) of the panel's 128 reflectors from V^T V (one workgroup):
-// T[c][c] = tau_c, T[0:c, c] = -tau_c T[0:c, 0:c] (V^T V)[0:c, c]. Thread r owns
-// row r of T in LDS.
-__global__ __launch_bounds__(128) void tbuild_kernel(const double* __restrict__ VtV,
+// Compact-WY T (upper) of the panel's 128 reflectors, one workgroup:
+//   T = (diag(1/tau) + striu(V^T V))^-1 = (Lm^-1)^T,  Lm = diag(1/tau) + stril(V^T V),
+// which equals LAPACK's forward recurrence T[0:c, c] = -tau_c T[0:c, 0:c] (V^T V)[0:c, c].
+// Lm^-1 reuses the LDS block inverse of the Cholesky kernels (16 x 16 diagonal
+// blocks by forward substitution, then MFMA column blocks). An identity reflector
+// (tau_c = 0) is decoupled: unit diagonal, no coupling, and T_cc = 0.
+__global__ __launch_bounds__(256) void tbuild_kernel(const double* __restrict__ VtV,
                                                      const double* __restrict__ tau,
                                                      double* __restrict__ T) {
-  __shared__ double sT[TS * (TS + 1)];
-  __shared__ double sv[TS];
-  const int r = threadIdx.x;
-  double* row = sT + r * (TS + 1);
-  for (int k = 0; k < TS; ++k) row[k] = 0.0;
-  for (int c = 0; c < TS; ++c) {
-    sv[r] = VtV[r * TS + c];
-    __syncthreads();
-    const double tc = tau[c];
-    if (r < c) {
-      double s = 0.0;
-      for (int k = r; k < c; ++k) s += row[k] * sv[k];
-      row[c] = -tc * s;
-    } else if (r == c) {
-      row[c] = tc;
-    }
-    __syncthreads();
+  __shared__ double Ls[TS * DL];
+  __shared__ double Aux[TS * RLD];
+  __shared__ double stau[TS];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  if (t < TS) stau[t] = tau[t];
+  __syncthreads();
+  for (int e = t; e < TS * TS; e += 256) {
+    const int r = e >> 7, c = e & 127;
+    double v = 0.0;
+    if (c == r) v = stau[r] != 0.0 ? 1.0 / stau[r] : 1.0;
+    else if (c < r && stau[r] != 0.0 && stau[c] != 0.0) v = VtV[e];
+    Ls[r * DL + c] = v;
   }
-  for (int k = 0; k < TS; ++k) T[r * TS + k] = row[k];
+  __syncthreads();
+  // inverses of the eight 16 x 16 diagonal blocks (wave w: blocks w and w + 4)
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int j0 = (w + 4 * h) * DB;
+    const int r = lane >> 2, g = lane & 3;
+    double lrow[DB];
+#pragma unroll
+    for (int p = 0; p < DB; ++p) lrow[p] = Ls[(j0 + r) * DL + j0 + p];
+    const double rinv = 1.0 / Ls[(j0 + r) * DL + j0 + r];
+    double s[4] = {0.0, 0.0, 0.0, 0.0}, x[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int p = 0; p < DB; ++p) {
+      if (r == p) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) x[k] = (((4 * g + k) == p ? 1.0 : 0.0) - s[k]) * rinv;
+      }
+      double xp[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) xp[k] = __shfl(x[k], (p << 2) | g);
+      if (r > p) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) s[k] += lrow[p] * xp[k];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) Aux[(j0 / DB) * 256 + r * 16 + 4 * g + k] = x[k];
+  }
+  __syncthreads();
+  lds_inv_block(Ls, Aux);
+  __syncthreads();
+  for (int e = t; e < TS * TS; e += 256) {
+    const int r = e >> 7, c = e & 127;
+    double v = 0.0;
+    if (r <= c && !(r == c && stau[c] == 0.0)) v = Ls[c * DL + r];
+    T[e] = v;
+  }
 }
 
 // Split-K symmetric product: Xp[il][ch] = sum_{J in chunk ch} A22_IJ V_J, with

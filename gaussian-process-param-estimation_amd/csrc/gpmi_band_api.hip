@@ -87,6 +87,8 @@ struct gpmi_band {
   double* etas = nullptr;    // [cap]
   double* out = nullptr;     // [cap][OUT_LD]
   int* info = nullptr;       // [cap]
+  unsigned* ctr = nullptr;   // hh_panel hand-off counter (16 bytes)
+  int* err = nullptr;        // hh_panel timeout flag
   int cap = 0;
   int nrhs = 0;
   double reduce_ms = 0.0, rhs_ms = 0.0, loglik_ms = 0.0;
@@ -100,6 +102,8 @@ int band_free(gpmi_band* b) {
   for (double* p : bufs)
     if (p) (void)hipFree(p);
   if (b->info) (void)hipFree(b->info);
+  if (b->ctr) (void)hipFree(b->ctr);
+  if (b->err) (void)hipFree(b->err);
   if (b->ev0) (void)hipEventDestroy(b->ev0);
   if (b->ev1) (void)hipEventDestroy(b->ev1);
   if (b->stream) (void)hipStreamDestroy(b->stream);
@@ -121,10 +125,18 @@ int band_reduce(gpmi_band* b, const double* K) {
     double* P = b->Ab + r0 * np + c0;
     double* tau = b->tau + (int64_t)j * TS;
     double* T = b->Tm + (int64_t)j * TS * TS;
-    for (int c = -1; c < TS; ++c) {
-      hipLaunchKernelGGL(hh_col_kernel, dim3(G), dim3(1024), 0, s, P, np, m, c, b->part,
-                         b->pivrow, tau);
-      BD_LAUNCH("hh_col_kernel");
+    if (G <= HH_PANEL_MAXG) {
+      // one launch per panel (rows in registers, in-launch reductions)
+      BD_TRY(hipMemsetAsync(b->ctr, 0, 16, s));
+      hipLaunchKernelGGL(hh_panel_kernel, dim3(G), dim3(HH_THREADS), HH_PANEL_LDS, s, P, np, m,
+                         b->part, b->pivrow, b->ctr, tau, b->err);
+      BD_LAUNCH("hh_panel_kernel");
+    } else {
+      for (int c = -1; c < TS; ++c) {
+        hipLaunchKernelGGL(hh_col_kernel, dim3(G), dim3(HH_THREADS), 0, s, P, np, m, c,
+                           b->part, b->pivrow, tau);
+        BD_LAUNCH("hh_col_kernel");
+      }
     }
     double* Ur = b->U + r0 * BAND_ULD;
     hipLaunchKernelGGL(vcopy_kernel, dim3((unsigned)((int64_t)m * TS / 256)), dim3(256), 0, s, P,
@@ -137,7 +149,7 @@ int band_reduce(gpmi_band* b, const double* K) {
     hipLaunchKernelGGL(tn_reduce_kernel, dim3(TS * TS / 256), dim3(256), 0, s, b->tnp, nch,
                        b->VtV, 1.0);
     BD_LAUNCH("tn_reduce_kernel");
-    hipLaunchKernelGGL(tbuild_kernel, dim3(1), dim3(TS), 0, s, b->VtV, tau, T);
+    hipLaunchKernelGGL(tbuild_kernel, dim3(1), dim3(256), 0, s, b->VtV, tau, T);
     BD_LAUNCH("tbuild_kernel");
     const int sch = (mt + SY_CH - 1) / SY_CH;
     hipLaunchKernelGGL(symm_kernel, dim3(mt, sch), dim3(256), 0, s, b->Ab, np, b->U,
@@ -162,7 +174,11 @@ int band_reduce(gpmi_band* b, const double* K) {
     BD_LAUNCH("syr2k_kernel");
   }
   BD_TRY(hipEventRecord(b->ev1, s));
+  int herr = 0;
+  BD_TRY(hipMemcpyAsync(&herr, b->err, sizeof(int), hipMemcpyDeviceToHost, s));
   BD_TRY(hipEventSynchronize(b->ev1));
+  BD_TRY(hipStreamSynchronize(s));
+  if (herr) return set_error(-1201, "band reduction: panel hand-off timed out (workgroups not co-resident?)");
   float ms = 0.f;
   BD_TRY(hipEventElapsedTime(&ms, b->ev0, b->ev1));
   b->reduce_ms = ms;
@@ -236,6 +252,19 @@ int gpmi_band_create(gpmi_op* op, gpmi_band** out) {
   BALLOC(qtp, (size_t)HH_MAXG * TS * RLD);
   BALLOC(qb, TS * RLD);
 #undef BALLOC
+  if ((e = hipMalloc(&b->ctr, 16)) != hipSuccess) return fail(e, "ctr");
+  if ((e = hipMalloc(&b->err, 16)) != hipSuccess) return fail(e, "err");
+  if ((e = hipMemsetAsync(b->err, 0, 16, b->stream)) != hipSuccess) return fail(e, "err memset");
+  {
+    static bool attr_set = false;
+    if (!attr_set) {
+      if ((e = hipFuncSetAttribute(reinterpret_cast<const void*>(&hh_panel_kernel),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, HH_PANEL_LDS)) !=
+          hipSuccess)
+        return fail(e, "hh_panel LDS attribute");
+      attr_set = true;
+    }
+  }
   if ((e = hipMemsetAsync(b->U, 0, sizeof(double) * np * BAND_ULD, b->stream)) != hipSuccess)
     return fail(e, "U memset");
   if ((e = hipMemsetAsync(b->Y, 0, sizeof(double) * np * RLD, b->stream)) != hipSuccess)

@@ -8,7 +8,8 @@ import time
 
 import numpy
 
-sys.path[:0] = ['.', 'gaussian-process-param-estimation_amd']
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, 'gaussian-process-param-estimation_amd')]
 from gaussian_proc import generate_correlation, _data  # noqa: E402
 from gaussian_proc._mixed_correlation import MixedCorrelation  # noqa: E402
 
@@ -33,6 +34,6 @@ for rep in range(3):
     print('rep %d: %d etas wall %.1f ms (rhs %.2f ms, loglik device %.2f ms)' % (
         rep, neta, 1e3 * (t1 - t0), t['rhs_ms'], t['loglik_ms']), flush=True)
 if grid == 128:
-    cfg = json.load(open(os.path.join('tests', 'golden', 'cfg3_big.json')))
+    cfg = json.load(open(os.path.join(REPO, 'tests', 'golden', 'cfg3_big.json')))
     ld3, _ = op.loglik_terms(cfg['etas'], X, z)
     print('cfg3 logdet rel err', numpy.abs(ld3 - cfg['logdet']) / numpy.abs(cfg['logdet']))
