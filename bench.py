@@ -50,6 +50,10 @@ def parse():
                     help='dense: the headline N=16384 metric; sparse4/sparse5: BASELINE '
                          'configs 4 and 5 (tapered Matern, SLQ + CG)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-band', action='store_true',
+                    help='skip the band-mode (eigenvalue operator) measurement of the dense run')
+    ap.add_argument('--band-etas', type=int, default=64,
+                    help='band mode: eta values per rank per step (one reduction per step)')
     ap.add_argument('--no-timing', action='store_true',
                     help='skip the per-kernel HIP-event roofline timing')
     return ap.parse_args()
@@ -224,6 +228,89 @@ def run_sparse(args, world, rank, local, dist, torch):
         dist.destroy_process_group()
 
 
+def golden_logdet_err(op_logdet_fn, nu, n):
+    """max relative error of logdet(K + eta I) vs the reference's own values
+    (tests/golden/cfg3_big.json: eigh/Cholesky of the reference at N=16384,
+    nu=1.5, etas 0.01, 1, 4); None for other configurations."""
+    path = os.path.join(REPO, 'tests', 'golden', 'cfg3_big.json')
+    if n != 16384 or nu != 1.5 or not os.path.isfile(path):
+        return None
+    with open(path) as fh:
+        cfg = json.load(fh)
+    ld = numpy.asarray(op_logdet_fn(cfg['etas']))
+    ref = numpy.asarray(cfg['logdet'])
+    return float(numpy.max(numpy.abs(ld - ref) / numpy.abs(ref)))
+
+
+def band_mode(args, D, X, z, world, rank, dist, torch, ld_ref=None):
+    """The eigenvalue operator's path (MixedCorrelation imate_method='eigenvalue'):
+    per step ONE device band reduction K = Q B Q^T of the resident K (redone every
+    step), Q^T [X z], and the banded-Cholesky terms of ``--band-etas`` eta values,
+    then the host lp and one all-gather. Same eta grid and lp as the dense line."""
+    from gaussian_proc._mixed_correlation import MixedCorrelation
+    from gaussian_proc._likelihood._direct_likelihood import _lp_from_terms
+    n, m = X.shape
+    E = args.band_etas
+    grid = numpy.logspace(-3, 3, 64)
+    op = MixedCorrelation(D, imate_method='eigenvalue')
+    b = op.band()
+    acc = {'reduce_ms': 0.0, 'rhs_ms': 0.0, 'loglik_ms': 0.0}
+
+    def step(s, record):
+        idx = [(s * world * E + rank * E + j) % grid.size for j in range(E)]
+        etas = grid[idx]
+        b.refresh()
+        op._band_rhs = None
+        ld, G = op.loglik_terms(etas, X, z)
+        if record:
+            for k, v in b.last_timing().items():
+                acc[k] += v
+        lp = numpy.array([_lp_from_terms(n, m, 1.0, l, g) for l, g in zip(ld, G)])
+        res = torch.from_numpy(numpy.stack([etas, ld, lp], axis=1)).cuda()
+        if world > 1:
+            out = torch.empty((world * E, 3), dtype=torch.float64, device=res.device)
+            dist.all_gather_into_tensor(out, res)
+            return out
+        return res
+
+    for s in range(args.warmup):
+        step(s, False)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        last = step(args.warmup + s, True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    t_max = torch.tensor([dt], dtype=torch.float64, device='cuda')
+    if world > 1:
+        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+    dt = float(t_max.item())
+    K = args.steps
+    red = acc['reduce_ms'] / K
+    flops_red = 4.0 * n ** 3 / 3.0
+    out = {
+        'value': world * E * K / dt, 'unit': 'evals/s', 'ms_per_step': dt / K * 1e3,
+        'eta_per_rank_per_step': E,
+        'step': 'band reduction of K + Q^T [X z] + %d banded Cholesky evals + host lp' % E,
+        'reduce_ms': round(red, 3), 'rhs_ms': round(acc['rhs_ms'] / K, 3),
+        'loglik_ms': round(acc['loglik_ms'] / K, 3),
+        'marginal_evals_per_s_per_gpu': round(E / (acc['loglik_ms'] / K * 1e-3), 1),
+        'reduction_tflops': round(flops_red / (red * 1e-3) / 1e12, 3),
+        'reduction_mfma_frac': round(flops_red / (red * 1e-3) / 1e12 / FP64_MFMA_PEAK_TFLOPS, 4),
+        'lp_sample': [float(v) for v in last[0].tolist()],
+        'logdet_rel_err_vs_reference': golden_logdet_err(
+            lambda e: op.loglik_terms(e, X, z)[0], args.nu, n),
+    }
+    if ld_ref is not None:
+        out['logdet_rel_err_vs_cholesky'] = float(numpy.max(
+            numpy.abs(op.loglik_terms(ld_ref[0], X, z)[0] - ld_ref[1]) / numpy.abs(ld_ref[1])))
+    return out
+
+
 def main():
     args = parse()
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -352,6 +439,14 @@ def main():
             'lp_sample': [float(v) for v in last[0].tolist()] if last is not None else None,
             'cpu_baseline': None,
         }
+    ld_err = golden_logdet_err(lambda e: op.loglik_terms(e, X, z)[0], args.nu, n)
+    if rank == 0:
+        result['logdet_rel_err_vs_reference'] = ld_err
+    if not args.no_band:
+        ld_ref = (last[:, 0].cpu().numpy()[:B], last[:, 1].cpu().numpy()[:B])
+        bm = band_mode(args, D, X, z, world, rank, dist, torch, ld_ref)
+        if rank == 0:
+            result['band_mode'] = bm
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result['cpu_baseline'] = cpu_baseline(points, z, X, args.nu, step_etas(0))
     if rank == 0:

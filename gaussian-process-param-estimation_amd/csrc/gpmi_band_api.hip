@@ -278,6 +278,19 @@ int gpmi_band_create(gpmi_op* op, gpmi_band** out) {
   return 0;
 }
 
+int gpmi_band_refresh(gpmi_band* b, gpmi_op* op) {
+  if (!b) return set_error(-1006, "null handle");
+  OpView v;
+  int rc = op_view(op, &v);
+  if (rc) return rc;
+  if (!v.has_K) return set_error(-1000, "operator has no matrix (load or assemble first)");
+  if (v.n != b->n || v.device != b->device)
+    return set_error(-1202, "operator size or device differs from the band's");
+  Guard g(b->device);
+  b->nrhs = 0;
+  return band_reduce(b, v.K);
+}
+
 int gpmi_band_destroy(gpmi_band* b) {
   if (!b) return 0;
   Guard g(b->device);

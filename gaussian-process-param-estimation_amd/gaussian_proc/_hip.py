@@ -77,6 +77,7 @@ SIGNATURES = {
                                       c_int_p]),
     'gpmi_band_create': (ctypes.c_int, [c_op_p, ctypes.POINTER(c_op_p)]),
     'gpmi_band_destroy': (ctypes.c_int, [c_op_p]),
+    'gpmi_band_refresh': (ctypes.c_int, [c_op_p, c_op_p]),
     'gpmi_band_set_rhs': (ctypes.c_int, [c_op_p, c_double_p, c_i64, ctypes.c_int]),
     'gpmi_band_loglik': (ctypes.c_int, [c_op_p, c_double_p, ctypes.c_int, c_double_p,
                                         c_double_p, c_int_p]),
@@ -304,6 +305,11 @@ class Band(object):
             self.close()
         except Exception:
             pass
+
+    def refresh(self):
+        """Reduce the operator's current K again (buffers reused; RHS reset)."""
+        check(self.lib.gpmi_band_refresh(self.h, self.op.h), 'gpmi_band_refresh')
+        self.nrhs = 0
 
     def set_rhs(self, R):
         R = as_c(R)

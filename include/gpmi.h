@@ -195,6 +195,9 @@ typedef struct gpmi_band gpmi_band;
  * a copy). Blocks until the reduction is done. */
 int gpmi_band_create(gpmi_op* op, gpmi_band** out);
 int gpmi_band_destroy(gpmi_band* b);
+/* Re-run the reduction on the operator's current K (same n and device), reusing
+ * the band's buffers; the resident RHS must be set again afterwards. */
+int gpmi_band_refresh(gpmi_band* b, gpmi_op* op);
 
 /* Y = Q^T R for an [n][ld] host block R with nrhs <= 16 columns (resident). */
 int gpmi_band_set_rhs(gpmi_band* b, const double* rhs, int64_t ld, int nrhs);
