@@ -15,6 +15,7 @@ constexpr int HH_MAXG = 256;       // max hh_col workgroups (n_pad <= 32768)
 constexpr int HH_PANEL_MAXG = 128;  // hh_panel (single-launch) workgroups: m <= 16384
 constexpr int HH_PANEL_LDS = 96 * 1024;  // dynamic LDS: one hh_panel workgroup per CU
 constexpr int HH_PART_LD = 136;    // partial record: S_j (j < 128), sum x^2 at [128]
+constexpr int QT_ROWS = 64;        // rows per qt_partial / qt_apply workgroup
 constexpr int TN_CH = 256;         // rows per tn_partial chunk
 constexpr int SY_CH = 16;          // tile columns per symm split-K chunk
 constexpr int BAND_ULD = 384;      // U = [W | V | W]
@@ -39,7 +40,8 @@ __global__ void syr2k_kernel(double* A, int64_t lda, const double* U, int64_t ld
                              int mt);
 __global__ void qt_partial_kernel(const double* P, int64_t lda, int m, const double* Y,
                                   double* part);
-__global__ void qt_reduce_kernel(const double* part, int G, const double* T, double* b);
+__global__ void qt_reduce_kernel(const double* part, int G, double* a);
+__global__ void qt_tb_kernel(const double* a, const double* T, double* b);
 __global__ void qt_apply_kernel(const double* P, int64_t lda, int m, double* Y, const double* b);
 __global__ void band_chol_kernel(const double* B, int64_t lda, int nt, int64_t n, const double* Y,
                                  const double* etas, double* out, int out_ld, int* info);

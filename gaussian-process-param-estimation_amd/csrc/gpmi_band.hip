@@ -282,13 +282,13 @@ __global__ __launch_bounds__(HH_THREADS) void hh_col_kernel(double* __restrict__
 // write-through form of the guide's publish/consume recipe): every partial
 // record and pivot-row word is stored sc1 (agent-scope relaxed atomic store),
 // each storing wave drains vmcnt, the workgroup barrier follows, then ONE lane
-// adds to the monotonic counter (agent scope). Consumers: ONE lane polls the
-// counter with sc1 loads until it reaches G (c + 1), a workgroup barrier, then
-// every read of a record is an sc1 load. Records are double-buffered by column
+// adds to the monotonic counter (agent scope; 8 shards, one per g % 8). Consumers:
+// every wave polls the shards with sc1 loads until their sum reaches G (c + 1)
+// and then reads the records with sc1 loads only. Records are double-buffered by column
 // parity: a workgroup publishing column c + 1 has seen every workgroup publish
 // column c, i.e. finish reading the slot it overwrites. Every spin is bounded;
 // a timeout sets *err and all workgroups leave (the host reports the error).
-// counter[0] must be zero at launch (the host memsets it per panel).
+// counter[0..127] must be zero at launch (the host memsets it per panel).
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void st_sc1(double* p, double v) {
   __hip_atomic_store(reinterpret_cast<unsigned long long*>(p),
@@ -358,27 +358,39 @@ __global__ __launch_bounds__(HH_THREADS) void hh_panel_kernel(double* __restrict
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (t == 0) __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // arrival on this workgroup's shard (8 shards, 64 bytes apart: fan-in <= G / 8)
+    if (t == 0)
+      __hip_atomic_fetch_add(counter + 16 * (g & 7), 1u, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
   };
   publish(0);
   for (int c = 0; c < TS; ++c) {
-    // wait until every workgroup has published column c
-    if (t == 0) {
+    // wait until every workgroup has published column c: each wave polls the 8
+    // shards itself (lane k < 8 reads shard k) and loads only after its own poll
+    {
       const unsigned target = (unsigned)G * (unsigned)(c + 1);
       unsigned spins = 0;
-      while (__hip_atomic_load(counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-        __builtin_amdgcn_s_sleep(2);
+      for (;;) {
+        unsigned v = 0;
+        if (lane < 8) v = __hip_atomic_load(counter + 16 * lane, __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+        for (int off = 4; off > 0; off >>= 1) v += __shfl_xor(v, off);
+        if (__builtin_amdgcn_readfirstlane(v) >= target) break;
+        __builtin_amdgcn_s_sleep(1);
         if ((++spins & 1023u) == 0 &&
             (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0 ||
              spins > (1u << 24))) {
-          __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (lane == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           s_bail = 1;
           break;
         }
       }
     }
-    __syncthreads();
-    if (s_bail) return;
+    if (s_bail) {
+      __syncthreads();
+      return;
+    }
     // records of slot c & 1: lane l reads columns (2l, 2l + 1) of every record this
     // wave owns with 16-byte sc1 loads, all in flight together; lane 0 also reads
     // the x^2 sum at [128]
@@ -406,7 +418,6 @@ __global__ __launch_bounds__(HH_THREADS) void hh_panel_kernel(double* __restrict
       sv += rv[u];
       sn += rn[u];
     }
-    __syncthreads();   // sacc readers of the previous publish are done
     sacc[w][2 * lane] = sv[0];
     sacc[w][2 * lane + 1] = sv[1];
     if (lane == 0) sacc[w][128] = sn;
@@ -646,64 +657,90 @@ __global__ __launch_bounds__(256, 2) void syr2k_kernel(double* __restrict__ A, i
 // ---------------------------------------------------------------------------
 // Y <- Q_j^T Y for one panel (Y rows r0.., 16 columns): Y -= V (T^T (V^T Y)).
 // V is read from the reduced matrix (unit lower trapezoidal below the band).
+//   qt_partial : workgroup g: part[g] = V[rows]^T Y[rows] over QT_ROWS rows
+//   qt_reduce  : a = sum_g part[g] (128 x 16), 8 workgroups
+//   qt_tb      : b = T^T a (one workgroup)
+//   qt_apply   : Y[rows] -= V[rows] b
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void qt_partial_kernel(const double* __restrict__ P,
                                                          int64_t lda, int m,
                                                          const double* __restrict__ Y,
                                                          double* __restrict__ part) {
+  __shared__ double sy[QT_ROWS * RLD];
   const int g = blockIdx.x, t = threadIdx.x;
+  const int i0 = g * QT_ROWS, i1 = min(m, i0 + QT_ROWS);
+  for (int e = t; e < QT_ROWS * RLD; e += 256)
+    sy[e] = (i0 + e / RLD < i1) ? Y[(int64_t)i0 * RLD + e] : 0.0;
+  __syncthreads();
   const int a = t & 127, h = t >> 7;
   double s[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-  const int i1 = min(m, (g + 1) * 256);
-  for (int i = g * 256; i < i1; ++i) {
+  for (int i = i0; i < i1; ++i) {
     const double v = (i > a) ? P[(int64_t)i * lda + a] : (i == a ? 1.0 : 0.0);
+    const double* yr = sy + (i - i0) * RLD + 8 * h;
 #pragma unroll
-    for (int q = 0; q < 8; ++q) s[q] += v * Y[(int64_t)i * RLD + 8 * h + q];
+    for (int q = 0; q < 8; ++q) s[q] += v * yr[q];
   }
 #pragma unroll
   for (int q = 0; q < 8; ++q) part[((int64_t)g * TS + a) * RLD + 8 * h + q] = s[q];
 }
 
-// b = T^T (sum_g part[g])  (128 x 16, one workgroup)
+// a[e] = sum_g part[g][e], e < 128 * 16 (fixed order)
 __global__ __launch_bounds__(256) void qt_reduce_kernel(const double* __restrict__ part, int G,
-                                                        const double* __restrict__ T,
-                                                        double* __restrict__ b) {
+                                                        double* __restrict__ a) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  double s = 0.0;
+  for (int g = 0; g < G; ++g) s += part[(int64_t)g * TS * RLD + e];
+  a[e] = s;
+}
+
+// b = T^T a  (128 x 16, one workgroup; T upper triangular)
+__global__ __launch_bounds__(256) void qt_tb_kernel(const double* __restrict__ a,
+                                                    const double* __restrict__ T,
+                                                    double* __restrict__ b) {
   __shared__ double sa[TS * RLD];
   const int t = threadIdx.x;
-  for (int e = t; e < TS * RLD; e += 256) {
-    double s = 0.0;
-    for (int g = 0; g < G; ++g) s += part[(int64_t)g * TS * RLD + e];
-    sa[e] = s;
-  }
+  for (int e = t; e < TS * RLD; e += 256) sa[e] = a[e];
   __syncthreads();
   const int k = t & 127, h = t >> 7;
   double o[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-  for (int a = 0; a <= k; ++a) {
-    const double tv = T[a * TS + k];
+  for (int r = 0; r <= k; ++r) {
+    const double tv = T[r * TS + k];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) o[q] += tv * sa[a * RLD + 8 * h + q];
+    for (int q = 0; q < 8; ++q) o[q] += tv * sa[r * RLD + 8 * h + q];
   }
 #pragma unroll
   for (int q = 0; q < 8; ++q) b[k * RLD + 8 * h + q] = o[q];
 }
 
-// Y[i] -= V[i] b for the rows of this workgroup (16 lanes share a row).
+// Y[i] -= V[i] b for the QT_ROWS rows of this workgroup (4 threads per row, 4
+// columns each; the row of V is staged through LDS).
 __global__ __launch_bounds__(256) void qt_apply_kernel(const double* __restrict__ P, int64_t lda,
                                                        int m, double* __restrict__ Y,
                                                        const double* __restrict__ b) {
   __shared__ double sb[TS * RLD];
+  __shared__ double sv[QT_ROWS * (TS + 1)];
   const int t = threadIdx.x;
+  const int i0 = blockIdx.x * QT_ROWS, i1 = min(m, i0 + QT_ROWS);
   for (int e = t; e < TS * RLD; e += 256) sb[e] = b[e];
-  __syncthreads();
-  const int col = t & 15;
-  for (int i = blockIdx.x * 256 + (t >> 4); i < min(m, (int)(blockIdx.x + 1) * 256); i += 16) {
-    double s = 0.0;
-    const double* row = P + (int64_t)i * lda;
-    const int amax = min(i, TS);
-    for (int a = 0; a < amax; ++a) s += row[a] * sb[a * RLD + col];
-    if (i < TS) s += sb[i * RLD + col];   // unit diagonal of V
-    Y[(int64_t)i * RLD + col] -= s;
+  for (int e = t; e < QT_ROWS * TS; e += 256) {
+    const int r = e >> 7, a = e & 127, i = i0 + r;
+    double v = 0.0;
+    if (i < i1) v = (i > a) ? P[(int64_t)i * lda + a] : (i == a ? 1.0 : 0.0);
+    sv[r * (TS + 1) + a] = v;
   }
+  __syncthreads();
+  const int r = t >> 2, c4 = (t & 3) * 4;
+  const int i = i0 + r;
+  if (i >= i1) return;
+  double s[4] = {0.0, 0.0, 0.0, 0.0};
+  const double* vr = sv + r * (TS + 1);
+  for (int a = 0; a < TS; ++a) {
+    const double v = vr[a];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) s[q] += v * sb[a * RLD + c4 + q];
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) Y[(int64_t)i * RLD + c4 + q] -= s[q];
 }
 
 // ---------------------------------------------------------------------------

@@ -83,11 +83,12 @@ struct gpmi_band {
   double* Zh = nullptr;      // [128][128]
   double* Y = nullptr;       // [n_pad][16] = Q^T R
   double* qtp = nullptr;     // [HH_MAXG][128][16]
+  double* qa = nullptr;      // [128][16]
   double* qb = nullptr;      // [128][16]
   double* etas = nullptr;    // [cap]
   double* out = nullptr;     // [cap][OUT_LD]
   int* info = nullptr;       // [cap]
-  unsigned* ctr = nullptr;   // hh_panel hand-off counter (16 bytes)
+  unsigned* ctr = nullptr;   // hh_panel hand-off counter: 8 shards, 64 B apart (512 bytes)
   int* err = nullptr;        // hh_panel timeout flag
   int cap = 0;
   int nrhs = 0;
@@ -98,7 +99,7 @@ namespace {
 
 int band_free(gpmi_band* b) {
   double* bufs[] = {b->Ab, b->U, b->X, b->Xp, b->part, b->pivrow, b->tau, b->Tm, b->tnp,
-                    b->VtV, b->M, b->Zh, b->Y, b->qtp, b->qb, b->etas, b->out};
+                    b->VtV, b->M, b->Zh, b->Y, b->qtp, b->qa, b->qb, b->etas, b->out};
   for (double* p : bufs)
     if (p) (void)hipFree(p);
   if (b->info) (void)hipFree(b->info);
@@ -127,7 +128,7 @@ int band_reduce(gpmi_band* b, const double* K) {
     double* T = b->Tm + (int64_t)j * TS * TS;
     if (G <= HH_PANEL_MAXG) {
       // one launch per panel (rows in registers, in-launch reductions)
-      BD_TRY(hipMemsetAsync(b->ctr, 0, 16, s));
+      BD_TRY(hipMemsetAsync(b->ctr, 0, 512, s));
       hipLaunchKernelGGL(hh_panel_kernel, dim3(G), dim3(HH_THREADS), HH_PANEL_LDS, s, P, np, m,
                          b->part, b->pivrow, b->ctr, tau, b->err);
       BD_LAUNCH("hh_panel_kernel");
@@ -249,10 +250,11 @@ int gpmi_band_create(gpmi_op* op, gpmi_band** out) {
   BALLOC(M, TS * TS);
   BALLOC(Zh, TS * TS);
   BALLOC(Y, np * RLD);
-  BALLOC(qtp, (size_t)HH_MAXG * TS * RLD);
+  BALLOC(qtp, (size_t)(np / QT_ROWS + 1) * TS * RLD);
+  BALLOC(qa, TS * RLD);
   BALLOC(qb, TS * RLD);
 #undef BALLOC
-  if ((e = hipMalloc(&b->ctr, 16)) != hipSuccess) return fail(e, "ctr");
+  if ((e = hipMalloc(&b->ctr, 512)) != hipSuccess) return fail(e, "ctr");
   if ((e = hipMalloc(&b->err, 16)) != hipSuccess) return fail(e, "err");
   if ((e = hipMemsetAsync(b->err, 0, 16, b->stream)) != hipSuccess) return fail(e, "err memset");
   {
@@ -312,14 +314,17 @@ int gpmi_band_set_rhs(gpmi_band* b, const double* rhs, int64_t ld, int nrhs) {
   for (int j = 0; j + 1 < b->nt; ++j) {
     const int64_t r0 = (int64_t)(j + 1) * TS, c0 = (int64_t)j * TS;
     const int m = (int)(np - r0);
-    const int G = (m + 255) / 256;
+    const int G = (m + QT_ROWS - 1) / QT_ROWS;
     const double* P = b->Ab + r0 * np + c0;
     double* Yr = b->Y + r0 * RLD;
     hipLaunchKernelGGL(qt_partial_kernel, dim3(G), dim3(256), 0, s, P, np, m, Yr, b->qtp);
     BD_LAUNCH("qt_partial_kernel");
-    hipLaunchKernelGGL(qt_reduce_kernel, dim3(1), dim3(256), 0, s, b->qtp, G,
-                       b->Tm + (int64_t)j * TS * TS, b->qb);
+    hipLaunchKernelGGL(qt_reduce_kernel, dim3(TS * RLD / 256), dim3(256), 0, s, b->qtp, G,
+                       b->qa);
     BD_LAUNCH("qt_reduce_kernel");
+    hipLaunchKernelGGL(qt_tb_kernel, dim3(1), dim3(256), 0, s, b->qa,
+                       b->Tm + (int64_t)j * TS * TS, b->qb);
+    BD_LAUNCH("qt_tb_kernel");
     hipLaunchKernelGGL(qt_apply_kernel, dim3(G), dim3(256), 0, s, P, np, m, Yr, b->qb);
     BD_LAUNCH("qt_apply_kernel");
   }
