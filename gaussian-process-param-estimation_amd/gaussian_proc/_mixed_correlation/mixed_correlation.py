@@ -2,16 +2,21 @@
 
 Drop-in for ``MixedCorrelation`` of the reference
 (gaussian_proc/_mixed_correlation/mixed_correlation.py:25-335). K lives in HBM
-once per operator; every eta-dependent quantity comes from one fp64 MFMA
-Cholesky of K + eta I (csrc/gpmi_chol.hip), cached per eta so that
-``logdet(eta)`` followed by ``solve(eta, .)`` factorizes once.
+once per operator.
 
-All exact ``imate_method`` values ('eigenvalue', 'cholesky', and 'hutchinson'
-for logdet, which the reference maps to Cholesky at :236-246) are computed
-exactly from the Cholesky factor; they agree with the reference's eigenvalue
-path to rounding. The stochastic estimators ('hutchinson' traceinv, 'slq') and
-traceinv interpolation are not implemented yet and raise
-``NotImplementedError``.
+* imate_method='eigenvalue' (the reference's one-time eigh in __init__,
+  :76-79, then cheap per-eta logdet, :239-248): the device reduces K once to
+  band form K = Q B Q^T (bandwidth 128, csrc/gpmi_band.hip, on first use);
+  logdet(eta) and the likelihood terms are then one banded Cholesky of
+  B + eta I per eta. traceinv uses the exact dense path below.
+* 'cholesky' (and 'hutchinson' for logdet, which the reference maps to
+  Cholesky at :250-261): one fp64 MFMA Cholesky of K + eta I
+  (csrc/gpmi_chol.hip), cached per eta so that logdet(eta) followed by
+  solve(eta, .) factorizes once; exact traceinv from its device triangular
+  inverse.
+* 'hutchinson' traceinv (:193-203): Rademacher probes solved with the device
+  Cholesky (stochastic; parity unpinned against imate, which is absent).
+* sparse K: 'slq' / 'hutchinson' with device Lanczos and CG.
 
 Error conventions follow the reference: ``ValueError`` for an unknown method
 (:146,212,271) or a bad ``dot`` exponent (:323-326), ``TypeError`` for
@@ -196,6 +201,16 @@ class MixedCorrelation(object):
                     return float(numpy.sum(V * W) / self.num_samples)
                 return float(numpy.sum(W * W) / self.num_samples)
             raise NotImplementedError('sparse traceinv with exponent %r' % exponent)
+        if self.imate_method == 'hutchinson' and exponent in (1, 2):
+            # Hutchinson estimator (imate 'hutchinson', assume_matrix='sym_pos'):
+            # tr(A^-1) ~ mean v^T A^-1 v, tr(A^-2) ~ mean |A^-1 v|^2, Rademacher v
+            opts = dict(self.imate_options or {})
+            s = int(opts.get('num_samples', opts.get('max_num_samples', 20)))
+            V = _slq.rademacher(self.n, s, int(opts.get('seed', 0)))
+            W = self.op.solve(eta, V)
+            if exponent == 1:
+                return float(numpy.sum(V * W) / s)
+            return float(numpy.sum(W * W) / s)
         if self.imate_method not in ('eigenvalue', 'cholesky'):
             if self.imate_method in _METHODS:
                 raise NotImplementedError('stochastic traceinv (%s) is not implemented yet'

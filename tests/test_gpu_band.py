@@ -120,3 +120,21 @@ def test_band_cfg3_n16384(gp):
     from gaussian_proc._likelihood._direct_likelihood import DirectLikelihood
     lp = DirectLikelihood.log_likelihood_batch(z, X, op, cfg['hypers'])
     assert rel(lp, cfg['direct_lp']) < 1e-8
+
+
+def test_dense_hutchinson_traceinv_within_mc_error(gp):
+    """'hutchinson' traceinv on a dense K (Rademacher probes, device Cholesky
+    solves): stochastic, so checked against the exact trace within 4 standard
+    errors of the estimator (imate is absent: parity unpinned)."""
+    from gaussian_proc._mixed_correlation import MixedCorrelation
+    K, _, _ = _inputs(400, 9)
+    s = 200
+    op = MixedCorrelation(K, imate_method='hutchinson', imate_options={'num_samples': s})
+    for eta in (0.1, 1.0):
+        Ainv = numpy.linalg.inv(K + eta * numpy.eye(400))
+        exact = numpy.trace(Ainv)
+        # Var of the Rademacher estimator: 2 (||A^-1||_F^2 - sum diag^2) / s
+        se = numpy.sqrt(2.0 * (numpy.sum(Ainv ** 2) - numpy.sum(numpy.diag(Ainv) ** 2)) / s)
+        assert abs(op.traceinv(eta) - exact) < 4 * se + 1e-12
+        assert op.logdet(eta) == pytest.approx(numpy.linalg.slogdet(K + eta * numpy.eye(400))[1],
+                                               rel=1e-10)
