@@ -46,6 +46,12 @@ __global__ void qt_apply_kernel(const double* P, int64_t lda, int m, double* Y, 
 __global__ void band_chol_kernel(const double* B, int64_t lda, int nt, int64_t n, const double* Y,
                                  const double* etas, double* out, int out_ld, int* info);
 
+__global__ void chase_copy_kernel(const double* Ab, double* A, int64_t lda, int n);
+__global__ void chase_task_kernel(double* A, int64_t lda, int n, int t, int s_hi);
+__global__ void tridiag_extract_kernel(const double* A, int64_t lda, int n, double* d, double* e2);
+__global__ void bisect_kernel(const double* d, const double* e2, int n, double lo0, double hi0,
+                              double pivmin, double* lam);
+
 // Read-only view of an operator for the band path (gpmi_api.hip).
 struct OpView {
   int device;

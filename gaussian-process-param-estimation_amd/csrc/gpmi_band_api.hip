@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 #include "gpmi_internal.h"
@@ -93,13 +94,17 @@ struct gpmi_band {
   int cap = 0;
   int nrhs = 0;
   double reduce_ms = 0.0, rhs_ms = 0.0, loglik_ms = 0.0;
+  // eigenvalues (bulge chase + bisection), computed on request
+  double* Ac = nullptr;      // [n_pad][n_pad] chase copy of the band (lower)
+  double* td = nullptr;      // [n] diagonal, then [n] squared subdiagonal, then [n] eigenvalues
+  double eig_ms = 0.0;
 };
 
 namespace {
 
 int band_free(gpmi_band* b) {
   double* bufs[] = {b->Ab, b->U, b->X, b->Xp, b->part, b->pivrow, b->tau, b->Tm, b->tnp,
-                    b->VtV, b->M, b->Zh, b->Y, b->qtp, b->qa, b->qb, b->etas, b->out};
+                    b->VtV, b->M, b->Zh, b->Y, b->qtp, b->qa, b->qb, b->etas, b->out, b->Ac, b->td};
   for (double* p : bufs)
     if (p) (void)hipFree(p);
   if (b->info) (void)hipFree(b->info);
@@ -372,6 +377,65 @@ int gpmi_band_loglik(gpmi_band* b, const double* etas, int neta, double* logdet,
   return 0;
 }
 
+int gpmi_band_eigenvalues(gpmi_band* b, double* lam) {
+  if (!b) return set_error(-1006, "null handle");
+  Guard g(b->device);
+  hipStream_t s = b->stream;
+  const int64_t np = b->n_pad;
+  const int n = (int)b->n;
+  if (!b->Ac) {
+    BD_TRY(hipMalloc(&b->Ac, sizeof(double) * np * np));
+    BD_TRY(hipMalloc(&b->td, sizeof(double) * 3 * np));
+  }
+  BD_TRY(hipEventRecord(b->ev0, s));
+  hipLaunchKernelGGL(chase_copy_kernel, dim3(n), dim3(256), 0, s, b->Ab, b->Ac, np, n);
+  BD_LAUNCH("chase_copy_kernel");
+  // wavefront t = 3 s + k: tasks s in [s_lo, s_hi], one workgroup each
+  const int kmax = (n - 2) / TS + 1;
+  const int tmax = 3 * std::max(0, n - 3) + kmax;
+  for (int t = 0; t <= tmax && n > 2; ++t) {
+    const int s_hi = std::min(t / 3, n - 3);
+    const int s_lo = std::max(0, (t - kmax + 2) / 3);
+    if (s_hi < s_lo) continue;
+    hipLaunchKernelGGL(chase_task_kernel, dim3(s_hi - s_lo + 1), dim3(256), 0, s, b->Ac, np, n,
+                       t, s_hi);
+    BD_LAUNCH("chase_task_kernel");
+  }
+  double* d = b->td;
+  double* e2 = b->td + np;
+  double* dl = b->td + 2 * np;
+  hipLaunchKernelGGL(tridiag_extract_kernel, dim3((n + 255) / 256), dim3(256), 0, s, b->Ac, np, n,
+                     d, e2);
+  BD_LAUNCH("tridiag_extract_kernel");
+  std::vector<double> hd(n), he2(n);
+  BD_TRY(hipMemcpyAsync(hd.data(), d, sizeof(double) * n, hipMemcpyDeviceToHost, s));
+  BD_TRY(hipMemcpyAsync(he2.data(), e2, sizeof(double) * n, hipMemcpyDeviceToHost, s));
+  BD_TRY(hipStreamSynchronize(s));
+  // Gershgorin interval and the dstebz pivot floor
+  double lo = hd[0], hi = hd[0], emax = 0.0;
+  for (int i = 0; i < n; ++i) {
+    const double el = i > 0 ? std::sqrt(he2[i - 1]) : 0.0;
+    const double er = i + 1 < n ? std::sqrt(he2[i]) : 0.0;
+    lo = std::min(lo, hd[i] - el - er);
+    hi = std::max(hi, hd[i] + el + er);
+    emax = std::max(emax, he2[i]);
+  }
+  const double span = std::max(hi - lo, std::fabs(hi)) * 1e-15 + 1e-300;
+  lo -= span;
+  hi += span;
+  const double pivmin = 2.2250738585072014e-308 * std::max(1.0, emax);
+  hipLaunchKernelGGL(bisect_kernel, dim3((n + 255) / 256), dim3(256), 0, s, d, e2, n, lo, hi,
+                     pivmin, dl);
+  BD_LAUNCH("bisect_kernel");
+  BD_TRY(hipMemcpyAsync(lam, dl, sizeof(double) * n, hipMemcpyDeviceToHost, s));
+  BD_TRY(hipEventRecord(b->ev1, s));
+  BD_TRY(hipStreamSynchronize(s));
+  float ms = 0.f;
+  BD_TRY(hipEventElapsedTime(&ms, b->ev0, b->ev1));
+  b->eig_ms = ms;
+  return 0;
+}
+
 int gpmi_band_get(gpmi_band* b, double* B_out, int64_t ld) {
   if (!b) return set_error(-1006, "null handle");
   Guard g(b->device);
@@ -390,6 +454,7 @@ int gpmi_band_get(gpmi_band* b, double* B_out, int64_t ld) {
 
 int gpmi_band_last_timing(gpmi_band* b, double* reduce_ms, double* rhs_ms, double* loglik_ms) {
   if (!b) return set_error(-1006, "null handle");
+  if (std::getenv("GPMI_BAND_TRACE")) fprintf(stderr, "[gpmi band] eigenvalues %.3f ms\n", b->eig_ms);
   if (reduce_ms) *reduce_ms = b->reduce_ms;
   if (rhs_ms) *rhs_ms = b->rhs_ms;
   if (loglik_ms) *loglik_ms = b->loglik_ms;

@@ -82,6 +82,7 @@ SIGNATURES = {
     'gpmi_band_loglik': (ctypes.c_int, [c_op_p, c_double_p, ctypes.c_int, c_double_p,
                                         c_double_p, c_int_p]),
     'gpmi_band_get': (ctypes.c_int, [c_op_p, c_double_p, c_i64]),
+    'gpmi_band_eigenvalues': (ctypes.c_int, [c_op_p, c_double_p]),
     'gpmi_band_last_timing': (ctypes.c_int, [c_op_p, c_double_p, c_double_p, c_double_p]),
 }
 
@@ -338,6 +339,12 @@ class Band(object):
                                             ik.ctypes.data_as(c_int_p)), 'gpmi_band_loglik')
             ld[i:i + k], g[i:i + k], info[i:i + k] = ldk, gk, ik
         return ld, g, info
+
+    def eigenvalues(self):
+        """The n eigenvalues of K, ascending (device bulge chase + bisection)."""
+        lam = numpy.empty(self.n)
+        check(self.lib.gpmi_band_eigenvalues(self.h, dptr(lam)), 'gpmi_band_eigenvalues')
+        return lam
 
     def band(self):
         """B as a dense symmetric n x n host matrix (tests)."""

@@ -75,8 +75,17 @@ class MixedCorrelation(object):
         self._rhs_cache = None
         self._band = None
         self._band_rhs = None
+        self._eig = None
 
     # ---- 'eigenvalue': one-time band reduction -----------------------------
+
+    def eigenvalues(self):
+        """Eigenvalues of K (ascending), the reference's K_eigenvalues
+        (mixed_correlation.py:76-79): band form on the device, then bulge
+        chasing to tridiagonal and bisection (computed once, on first use)."""
+        if self._eig is None:
+            self._eig = self.band().eigenvalues()
+        return self._eig
 
     def band(self):
         """The one-time spectral setup of imate_method='eigenvalue' (the
@@ -184,9 +193,11 @@ class MixedCorrelation(object):
             if eta == 0:
                 return tk2
             return tk2 + 2.0 * eta * tk + eta ** 2 * self.n
-        if self.imate_method in ('eigenvalue', 'slq'):
-            raise NotImplementedError('trace with exponent %r needs the eigenvalue '
-                                      'operator (not implemented yet)' % exponent)
+        if self.imate_method == 'eigenvalue' and not self.sparse:
+            # sum over the eigenvalues (imate 'eigenvalue', :127-133)
+            return float(numpy.sum((self.eigenvalues() + eta) ** float(exponent)))
+        if self.imate_method == 'slq':
+            raise NotImplementedError('trace with exponent %r on the slq operator' % exponent)
         raise ValueError('Existing methods are "exact", "eigenvalue", and "slq".')
 
     def traceinv(self, eta, exponent=1):                           # :155-215
@@ -219,6 +230,9 @@ class MixedCorrelation(object):
                              '"hutchinson", and "slq".')
         if exponent == 0:
             return float(self.n)
+        if self.imate_method == 'eigenvalue':
+            # sum over the eigenvalues (imate 'eigenvalue', :172-181)
+            return float(numpy.sum((self.eigenvalues() + eta) ** (-float(exponent))))
         if exponent in (1, 2):
             # exact, from the device triangular inverse of the cached factor
             return self.op.traceinv(eta, exponent)

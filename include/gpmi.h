@@ -211,6 +211,13 @@ int gpmi_band_set_rhs(gpmi_band* b, const double* rhs, int64_t ld, int nrhs);
 int gpmi_band_loglik(gpmi_band* b, const double* etas, int neta, double* logdet,
                      double* gram, int* info);
 
+/* The n eigenvalues of K (ascending): B -> tridiagonal by bulge chasing on the
+ * device (one launch per wavefront of 128-row tasks), then bisection on Sturm
+ * counts (one thread per eigenvalue). Completes the eigenvalue operator:
+ * trace / traceinv / logdet of K + eta I as sums over lambda_i + eta
+ * (mixed_correlation.py:127-133,172-181,239-248). Allocates n_pad^2 doubles. */
+int gpmi_band_eigenvalues(gpmi_band* b, double* lam);
+
 /* The band matrix B as a dense symmetric [n][ld] host matrix (tests). */
 int gpmi_band_get(gpmi_band* b, double* B_out, int64_t ld);
 

@@ -138,3 +138,41 @@ def test_dense_hutchinson_traceinv_within_mc_error(gp):
         assert abs(op.traceinv(eta) - exact) < 4 * se + 1e-12
         assert op.logdet(eta) == pytest.approx(numpy.linalg.slogdet(K + eta * numpy.eye(400))[1],
                                                rel=1e-10)
+
+
+@pytest.mark.parametrize('n', [2, 5, 129, 300, 1000])
+def test_eigenvalues_vs_numpy(gp, n):
+    """Device bulge chase + bisection: the spectrum of K to 1e-12 ||K||."""
+    K, _, _ = _inputs(n, n + 2)
+    lam = _mc(K).eigenvalues()
+    ref = numpy.linalg.eigvalsh(K)
+    assert lam.shape == (n,)
+    assert numpy.all(numpy.diff(lam) >= 0)
+    assert numpy.max(numpy.abs(lam - ref)) <= 1e-12 * numpy.abs(ref).max()
+
+
+def test_eigenvalue_operator_traces(gp):
+    """'eigenvalue' traceinv (exponent 1, 2, 3) and trace (exponent 3) as sums over
+    the device eigenvalues vs explicit matrix functions (rel <= 1e-9)."""
+    K, _, _ = _inputs(500, 21, nu=2.5, scale=0.1)
+    op = _mc(K)
+    for eta in (1e-2, 0.3, 4.0):
+        A = K + eta * numpy.eye(500)
+        Ainv = numpy.linalg.inv(A)
+        assert rel(op.traceinv(eta), numpy.trace(Ainv)) < 1e-9
+        assert rel(op.traceinv(eta, 2), numpy.sum(Ainv * Ainv)) < 1e-9
+        assert rel(op.traceinv(eta, 3), numpy.trace(Ainv @ Ainv @ Ainv)) < 1e-9
+        assert rel(op.trace(eta, 3), numpy.trace(A @ A @ A)) < 1e-9
+        assert op.traceinv(eta, 0) == 500
+
+
+def test_eigenvalue_operator_cfg2_golden(gp):
+    """N=4096: traceinv of the reference's eigenvalue operator (golden)."""
+    cfg = load_json('cfg2.json')
+    pts, z, X = config_inputs(cfg)
+    D = gp.generate_correlation(pts, 0.1, 1.5, device_resident=True)
+    op = _mc(D)
+    g = cfg['operator']['eigenvalue']
+    assert rel([op.traceinv(e) for e in cfg['etas']], g['traceinv']) < 1e-9
+    assert rel([op.traceinv(e, 2) for e in cfg['etas']], g['traceinv_exp2']) < 1e-9
+    assert rel([op.logdet(e) for e in cfg['etas']], g['logdet']) < 1e-9
