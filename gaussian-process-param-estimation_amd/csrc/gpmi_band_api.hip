@@ -397,7 +397,7 @@ int gpmi_band_eigenvalues(gpmi_band* b, double* lam) {
     const int s_hi = std::min(t / 3, n - 3);
     const int s_lo = std::max(0, (t - kmax + 2) / 3);
     if (s_hi < s_lo) continue;
-    hipLaunchKernelGGL(chase_task_kernel, dim3(s_hi - s_lo + 1), dim3(256), 0, s, b->Ac, np, n,
+    hipLaunchKernelGGL(chase_task_kernel, dim3(s_hi - s_lo + 1), dim3(512), 0, s, b->Ac, np, n,
                        t, s_hi);
     BD_LAUNCH("chase_task_kernel");
   }

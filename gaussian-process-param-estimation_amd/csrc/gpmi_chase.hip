@@ -16,7 +16,9 @@
 //   F <- H F, D = A[J_k, J_k] <- H D H (symmetric rank-2 form on the lower
 //   triangle, D staged whole in LDS), E = A[J_{k+1}, J_k] <- E H.
 // The matrix is a dense n_pad x n_pad lower-triangle copy of B; every access is
-// within 2b of the diagonal.
+// within 2b of the diagonal. The three blocks (F, D, E) are loaded into
+// registers at the start (all 16-byte loads of the task in flight together),
+// staged through LDS only for the matrix-vector products, and written back whole.
 //
 // bisect_kernel: thread i finds the i-th smallest eigenvalue of the symmetric
 // tridiagonal (d, e) by bisection on the Sturm count (LDL^T pivots of T - x I,
@@ -28,6 +30,7 @@
 
 #include "gpmi_internal.h"
 #include "gpmi_band.h"
+#include "gpmi_device.h"
 
 namespace gpmi {
 
@@ -44,14 +47,68 @@ __device__ __forceinline__ double block_sum(double v, double* red) {
   return (red[0] + red[1]) + (red[2] + red[3]);
 }
 
-__global__ __launch_bounds__(256) void chase_task_kernel(double* __restrict__ A, int64_t lda,
-                                                         int n, int t, int s_hi) {
-  __shared__ double D[CB * CLD];
+constexpr int CT = 512;             // chase workgroup: 8 waves
+constexpr int CPT = CB * CB / 2 / CT;   // 16-byte pairs per thread per 128 x 128 block
+
+__device__ __forceinline__ double block_sum8(double v, double* red) {
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  __syncthreads();
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  return ((red[0] + red[1]) + (red[2] + red[3])) + ((red[4] + red[5]) + (red[6] + red[7]));
+}
+
+// Rows [0, nr) x columns [0, nc) of a row-major block into registers (pair u of
+// thread t: element index e = u * CT + t, row e >> 6, columns 2 (e & 63) + {0,1};
+// outside the block: 0). All CPT loads are in flight together.
+__device__ __forceinline__ void load_block(const double* __restrict__ src, int64_t lda, int nr,
+                                           int nc, d2 (&r)[CPT]) {
+#pragma unroll
+  for (int u = 0; u < CPT; ++u) {
+    const int e = u * CT + threadIdx.x;
+    const int i = e >> 6, c2 = 2 * (e & 63);
+    const double* p = src + (int64_t)i * lda + c2;
+    r[u] = d2{0.0, 0.0};
+    if (i < nr) {
+      if (c2 + 1 < nc) r[u] = *reinterpret_cast<const d2*>(p);
+      else if (c2 < nc) r[u][0] = p[0];
+    }
+  }
+}
+
+__device__ __forceinline__ void block_to_lds(const d2 (&r)[CPT], double* __restrict__ buf) {
+#pragma unroll
+  for (int u = 0; u < CPT; ++u) {
+    const int e = u * CT + threadIdx.x;
+    const int i = e >> 6, c2 = 2 * (e & 63);
+    buf[i * CLD + c2] = r[u][0];
+    buf[i * CLD + c2 + 1] = r[u][1];
+  }
+}
+
+// out[c] = sum_{j < nj} M[c][j] v[j] (rows c < nr) or, with TRANS, sum_{i < nj}
+// v[i] M[i][c]; 4 partial sums per output (thread (c, h), h = 0..3), reduced in sp.
+template <bool TRANS>
+__device__ __forceinline__ void lds_matvec(const double* __restrict__ buf, int nr, int nj,
+                                           const double* __restrict__ v, double (*sp)[CB]) {
+  const int c = threadIdx.x & 127, h = threadIdx.x >> 7;
+  double acc = 0.0;
+  if (TRANS || c < nr)
+    for (int j = h; j < nj; j += 4) acc += (TRANS ? buf[j * CLD + c] : buf[c * CLD + j]) * v[j];
+  sp[h][c] = acc;
+}
+
+__global__ __launch_bounds__(CT) void chase_task_kernel(double* __restrict__ A, int64_t lda,
+                                                        int n, int t, int s_hi) {
+  __shared__ double buf[CB * CLD];
   __shared__ double sv[CB];
   __shared__ double sw[CB];
-  __shared__ double sp[2][CB];
-  __shared__ double red[4];
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  __shared__ double sp[4][CB];
+  __shared__ double red[8];
+  __shared__ double sx0;
+  const int tid = threadIdx.x;
   const int s = s_hi - (int)blockIdx.x;
   const int k = t - 3 * s;
   if (s < 0 || k < 0) return;
@@ -59,11 +116,16 @@ __global__ __launch_bounds__(256) void chase_task_kernel(double* __restrict__ A,
   if (r0 >= n) return;
   const int r1 = min(r0 + CB, n), L = r1 - r0;
   const int col = (k == 0) ? s : s + 1 + (k - 1) * CB;
-  // ---- reflector from x = A[r0:r1, col]
-  __shared__ double sx0;
+  const int e1 = min(r1 + CB, n), LE = e1 - r1;
+  // every load of the task first: x, then the F, D and E blocks into registers
   const double xi = (tid < L) ? A[(int64_t)(r0 + tid) * lda + col] : 0.0;
+  d2 Fr[CPT], Dr[CPT], Er[CPT];
+  if (k >= 1) load_block(A + (int64_t)r0 * lda + col, lda, L, CB, Fr);
+  load_block(A + (int64_t)r0 * lda + r0, lda, L, L, Dr);
+  if (LE > 0) load_block(A + (int64_t)r1 * lda + r0, lda, LE, L, Er);
+  // ---- reflector (LAPACK dlarfg)
   if (tid == 0) sx0 = xi;
-  const double nb2 = block_sum((tid > 0 && tid < L) ? xi * xi : 0.0, red);
+  const double nb2 = block_sum8((tid > 0 && tid < L) ? xi * xi : 0.0, red);
   const double xx0 = sx0;
   double tau = 0.0, beta = xx0, scale = 0.0;
   if (nb2 > 0.0) {
@@ -73,67 +135,77 @@ __global__ __launch_bounds__(256) void chase_task_kernel(double* __restrict__ A,
     scale = 1.0 / (xx0 - beta);
   }
   if (tid < CB) sv[tid] = (tid == 0) ? 1.0 : ((tid < L) ? xi * scale : 0.0);
-  __syncthreads();
-  // ---- the annihilated column
-  if (k == 0) {
-    if (tid < L) A[(int64_t)(r0 + tid) * lda + s] = (tid == 0) ? beta : 0.0;
-  }
+  if (k == 0 && tid < L) A[(int64_t)(r0 + tid) * lda + s] = (tid == 0) ? beta : 0.0;
   if (tau == 0.0) return;   // identity reflector: nothing else changes
-  // ---- F <- H F, F = A[r0:r1, col:col + CB] (k >= 1)
+  // ---- F <- H F (k >= 1): w = tau F^T v; column col becomes (beta, 0 ...)
   if (k >= 1) {
-    const int c = tid & 127, h = tid >> 7;
-    double acc = 0.0;
-    for (int i = h; i < L; i += 2) acc += sv[i] * A[(int64_t)(r0 + i) * lda + col + c];
-    sp[h][c] = acc;
+    block_to_lds(Fr, buf);
     __syncthreads();
-    if (tid < CB) sw[tid] = tau * (sp[0][tid] + sp[1][tid]);
+    lds_matvec<true>(buf, CB, L, sv, sp);
     __syncthreads();
-    for (int i = h; i < L; i += 2) {
-      double* p = A + (int64_t)(r0 + i) * lda + col + c;
-      if (c == 0) *p = (i == 0) ? beta : 0.0;
-      else *p -= sv[i] * sw[c];
+    if (tid < CB) sw[tid] = tau * ((sp[0][tid] + sp[1][tid]) + (sp[2][tid] + sp[3][tid]));
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < CPT; ++u) {
+      const int e = u * CT + tid;
+      const int i = e >> 6, c2 = 2 * (e & 63);
+      if (i >= L) continue;
+      d2 o;
+      o[0] = (c2 == 0) ? (i == 0 ? beta : 0.0) : Fr[u][0] - sv[i] * sw[c2];
+      o[1] = Fr[u][1] - sv[i] * sw[c2 + 1];
+      *reinterpret_cast<d2*>(A + (int64_t)(r0 + i) * lda + col + c2) = o;
     }
   }
-  // ---- D <- H D H on the lower triangle of A[r0:r1, r0:r1], staged symmetric in LDS
-  for (int e = tid; e < L * CB; e += 256) {
+  // ---- D <- H D H: p = tau D v (D symmetrized from its lower part),
+  //      w = p - tau/2 (v.p) v, D -= v w^T + w v^T
+  __syncthreads();
+  block_to_lds(Dr, buf);
+  __syncthreads();
+  for (int e = tid; e < CB * CB; e += CT) {
     const int i = e >> 7, j = e & 127;
-    if (j <= i) {
-      const double v = A[(int64_t)(r0 + i) * lda + r0 + j];
-      D[i * CLD + j] = v;
-      D[j * CLD + i] = v;
-    }
+    if (j > i && j < L) buf[i * CLD + j] = buf[j * CLD + i];
   }
   __syncthreads();
-  {
-    // p = tau D v (thread pair per row)
-    const int i = tid & 127, h = tid >> 7;
-    double acc = 0.0;
-    if (i < L)
-      for (int j = h; j < L; j += 2) acc += D[i * CLD + j] * sv[j];
-    sp[h][i] = acc;
-  }
+  lds_matvec<false>(buf, L, L, sv, sp);
   __syncthreads();
-  const double pi = (tid < L) ? tau * (sp[0][tid] + sp[1][tid]) : 0.0;
-  const double vp = block_sum((tid < L) ? pi * sv[tid] : 0.0, red);
+  const double pi =
+      (tid < L) ? tau * ((sp[0][tid] + sp[1][tid]) + (sp[2][tid] + sp[3][tid])) : 0.0;
+  const double vp = block_sum8((tid < L) ? pi * sv[tid] : 0.0, red);
   if (tid < CB) sw[tid] = (tid < L) ? pi - 0.5 * tau * vp * sv[tid] : 0.0;
   __syncthreads();
-  for (int e = tid; e < L * CB; e += 256) {
-    const int i = e >> 7, j = e & 127;
-    if (j <= i)
-      A[(int64_t)(r0 + i) * lda + r0 + j] = D[i * CLD + j] - sv[i] * sw[j] - sw[i] * sv[j];
-  }
-  // ---- E <- E H, E = A[r1:e1, r0:r1]
-  const int e1 = min(r1 + CB, n);
-  for (int i = r1 + wv; i < e1; i += 4) {
-    double* row = A + (int64_t)i * lda + r0;
-    const double a0 = (lane < L) ? row[lane] : 0.0;
-    const double a1 = (lane + 64 < L) ? row[lane + 64] : 0.0;
-    double q = a0 * sv[lane] + a1 * sv[lane + 64];
+  // whole rows back (the upper part of A's band region is never read)
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) q += __shfl_xor(q, off);
-    q *= tau;
-    if (lane < L) row[lane] = a0 - q * sv[lane];
-    if (lane + 64 < L) row[lane + 64] = a1 - q * sv[lane + 64];
+  for (int u = 0; u < CPT; ++u) {
+    const int e = u * CT + tid;
+    const int i = e >> 6, c2 = 2 * (e & 63);
+    if (i >= L || c2 >= L) continue;
+    const double a0 = i < L ? buf[i * CLD + c2] : 0.0;   // symmetrized value
+    const double a1 = buf[i * CLD + c2 + 1];
+    d2 o;
+    o[0] = a0 - sv[i] * sw[c2] - sw[i] * sv[c2];
+    o[1] = a1 - sv[i] * sw[c2 + 1] - sw[i] * sv[c2 + 1];
+    if (c2 + 1 < L) *reinterpret_cast<d2*>(A + (int64_t)(r0 + i) * lda + r0 + c2) = o;
+    else A[(int64_t)(r0 + i) * lda + r0 + c2] = o[0];
+  }
+  if (LE <= 0) return;
+  // ---- E <- E H: q = tau E v, E -= q v^T
+  __syncthreads();
+  block_to_lds(Er, buf);
+  __syncthreads();
+  lds_matvec<false>(buf, LE, L, sv, sp);
+  __syncthreads();
+  if (tid < CB) sw[tid] = tau * ((sp[0][tid] + sp[1][tid]) + (sp[2][tid] + sp[3][tid]));
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < CPT; ++u) {
+    const int e = u * CT + tid;
+    const int i = e >> 6, c2 = 2 * (e & 63);
+    if (i >= LE || c2 >= L) continue;
+    d2 o;
+    o[0] = Er[u][0] - sw[i] * sv[c2];
+    o[1] = Er[u][1] - sw[i] * sv[c2 + 1];
+    if (c2 + 1 < L) *reinterpret_cast<d2*>(A + (int64_t)(r1 + i) * lda + r0 + c2) = o;
+    else A[(int64_t)(r1 + i) * lda + r0 + c2] = o[0];
   }
 }
 
