@@ -50,6 +50,8 @@ def parse():
                     help='dense: the headline N=16384 metric; sparse4/sparse5: BASELINE '
                          'configs 4 and 5 (tapered Matern, SLQ + CG)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-der', action='store_true',
+                    help='skip the der1 eta-sweep measurement of the band mode')
     ap.add_argument('--no-band', action='store_true',
                     help='skip the band-mode (eigenvalue operator) measurement of the dense run')
     ap.add_argument('--band-etas', type=int, default=64,
@@ -308,7 +310,29 @@ def band_mode(args, D, X, z, world, rank, dist, torch, ld_ref=None):
     if ld_ref is not None:
         out['logdet_rel_err_vs_cholesky'] = float(numpy.max(
             numpy.abs(op.loglik_terms(ld_ref[0], X, z)[0] - ld_ref[1]) / numpy.abs(ld_ref[1])))
+    if not args.no_der:
+        out['der1_sweep'] = der1_sweep(op, X, z, E, rank, torch)
     return out
+
+
+def der1_sweep(op, X, z, E, rank, torch):
+    """ProfileLikelihood.log_likelihood_der1_eta over this rank's E points of
+    the grid in one call (band Gram blocks G1..G3 + eigenvalue traceinv), after
+    the one-time eigenvalues of K (timed separately)."""
+    from gaussian_proc._likelihood._profile_likelihood import ProfileLikelihood
+    log_etas = numpy.linspace(-3, 3, 64)[[(rank * E + j) % 64 for j in range(E)]]
+    t0 = time.perf_counter()
+    op.eigenvalues()
+    eig_ms = (time.perf_counter() - t0) * 1e3
+    ProfileLikelihood.log_likelihood_der1_eta_batch(z, X, op, log_etas)   # warm (buffers)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    d1 = ProfileLikelihood.log_likelihood_der1_eta_batch(z, X, op, log_etas)
+    dt = time.perf_counter() - t0
+    return {'etas': E, 'wall_ms': round(dt * 1e3, 3), 'device_ms': round(op.band().der_ms(), 3),
+            'der1_evals_per_s_per_gpu': round(E / dt, 1),
+            'eigenvalues_ms_once': round(eig_ms, 1),
+            'der1_sample': [float(log_etas[0]), float(d1[0])]}
 
 
 def main():

@@ -78,6 +78,9 @@ struct gpmi_op {
   int lookahead = 0;                   // 1: panel chain on stream2 beside the bulk update
   hipStream_t stream = nullptr;
   hipStream_t stream2 = nullptr;       // high-priority panel stream (look-ahead)
+  hipStream_t stream3 = nullptr;       // second batch group (groups == 2)
+  int groups = 1;                      // 2: the batch runs as two halves on two streams
+  hipEvent_t ev_g = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   std::vector<hipEvent_t> ev_panel, ev_rest;  // per outer panel (look-ahead)
   bool dry = false;                    // schedule dry run: collect SYRK shapes only
@@ -161,6 +164,7 @@ void grouped_order(int w, int t, int G, std::vector<uint32_t>* out) {
 
 int launch_syrk(gpmi_op* op, hipStream_t st, int b0, int nb, int tc0, int w, int t, int p0,
                 int kdim) {
+  // b0: first batch member of the launch (a batch group's offset)
   const int tri = w * (w + 1) / 2;
   const int tiles = tri + (t - w) * w;
   if (tiles <= 0 || nb <= 0) return 0;
@@ -206,7 +210,8 @@ int launch_syrk(gpmi_op* op, hipStream_t st, int b0, int nb, int tc0, int w, int
 // from it (a band SYRK with kdim = half width), factor the right half. A single
 // column is the diagonal-block kernel (Cholesky, inverse, fused forward solve,
 // logdet / Gram partials) followed by the panel kernel (L_ik and r_i updates).
-int factor_panel(gpmi_op* op, const BatchPtrs& P, int nb, hipStream_t st, int c0, int W) {
+int factor_panel(gpmi_op* op, const BatchPtrs& P, int b0, int nb, hipStream_t st, int c0,
+                 int W) {
   const int nt = op->nt;
   if (W == 1) {
     if (op->dry) return 0;
@@ -221,11 +226,11 @@ int factor_panel(gpmi_op* op, const BatchPtrs& P, int nb, hipStream_t st, int c0
     return 0;
   }
   const int h = W / 2;
-  int rc = factor_panel(op, P, nb, st, c0, h);
+  int rc = factor_panel(op, P, b0, nb, st, c0, h);
   if (rc) return rc;
-  rc = launch_syrk(op, st, 0, nb, c0 + h, W - h, nt - c0 - h, c0 * TS, h * TS);
+  rc = launch_syrk(op, st, b0, nb, c0 + h, W - h, nt - c0 - h, c0 * TS, h * TS);
   if (rc) return rc;
-  return factor_panel(op, P, nb, st, c0 + h, W - h);
+  return factor_panel(op, P, b0, nb, st, c0 + h, W - h);
 }
 
 int get_event(std::vector<hipEvent_t>* v, size_t i, hipEvent_t* out) {
@@ -246,21 +251,22 @@ int get_event(std::vector<hipEvent_t>* v, size_t i, hipEvent_t* out) {
 //   stream : [wait factor(P_k)] -> U_rest(k): columns right of P_{k+1}
 // so the latency-bound factorization of P_{k+1} overlaps the bulk update U_rest(k).
 // U_rest(k-1) and U_next(k) both write P_{k+1}'s columns, hence the wait.
-int schedule(gpmi_op* op, const BatchPtrs& P, int nb) {
+// P points at batch member b0 (a batch group); `main` replaces op->stream.
+int schedule(gpmi_op* op, const BatchPtrs& P, int b0, int nb, hipStream_t main = nullptr) {
   const int nt = op->nt, O = op->outer;
   const bool la = op->lookahead && !op->dry;
-  hipStream_t A = op->stream, B = la ? op->stream2 : op->stream;
+  hipStream_t A = main ? main : op->stream, B = la ? op->stream2 : A;
   bool have_rest_prev = false;
   hipEvent_t ev_rest_prev = nullptr;
   int np = 0;
   for (int c0 = 0; c0 < nt; c0 += O, ++np) {
     const int W = std::min(O, nt - c0);
-    int rc = factor_panel(op, P, nb, B, c0, W);
+    int rc = factor_panel(op, P, b0, nb, B, c0, W);
     if (rc) return rc;
     const int c1 = c0 + W;
     if (c1 >= nt) break;
     if (!op->lookahead) {
-      rc = launch_syrk(op, A, 0, nb, c1, nt - c1, nt - c1, c0 * TS, W * TS);
+      rc = launch_syrk(op, A, b0, nb, c1, nt - c1, nt - c1, c0 * TS, W * TS);
       if (rc) return rc;
       continue;
     }
@@ -273,7 +279,7 @@ int schedule(gpmi_op* op, const BatchPtrs& P, int nb) {
         HIP_TRY(hipEventRecord(ev_f, B));
         HIP_TRY(hipStreamWaitEvent(A, ev_f, 0));
       }
-      rc = launch_syrk(op, A, 0, nb, c2, nt - c2, nt - c2, c0 * TS, W * TS);
+      rc = launch_syrk(op, A, b0, nb, c2, nt - c2, nt - c2, c0 * TS, W * TS);
       if (rc) return rc;
       if (la) {
         if ((rc = get_event(&op->ev_rest, np, &ev_r))) return rc;
@@ -282,7 +288,7 @@ int schedule(gpmi_op* op, const BatchPtrs& P, int nb) {
       have_rest = true;
     }
     if (la && have_rest_prev) HIP_TRY(hipStreamWaitEvent(B, ev_rest_prev, 0));
-    rc = launch_syrk(op, B, 0, nb, c1, c2 - c1, nt - c1, c0 * TS, W * TS);
+    rc = launch_syrk(op, B, b0, nb, c1, c2 - c1, nt - c1, c0 * TS, W * TS);
     if (rc) return rc;
     have_rest_prev = have_rest;
     ev_rest_prev = ev_r;
@@ -302,7 +308,7 @@ int ensure_order(gpmi_op* op) {
   op->dry = true;
   op->shapes.clear();
   BatchPtrs P = op->ptrs();
-  int rc = schedule(op, P, 1);
+  int rc = schedule(op, P, 0, 1);
   op->dry = false;
   if (rc) return rc;
   std::vector<uint32_t> h;
@@ -318,6 +324,18 @@ int ensure_order(gpmi_op* op) {
   op->order_outer = op->outer;
   op->order_la = op->lookahead;
   return 0;
+}
+
+BatchPtrs shifted(const BatchPtrs& P, int b0) {
+  BatchPtrs q = P;
+  q.A += b0 * P.sA;
+  q.R += b0 * P.sR;
+  q.U += b0 * P.sU;
+  q.Linv += b0 * P.sL;
+  q.logdiag += b0 * P.sLD;
+  q.gram += b0 * P.sG;
+  q.info += b0;
+  return q;
 }
 
 // Factor K + eta_b I for b < nb, with the fused forward substitution of the
@@ -358,7 +376,24 @@ int run_factor(gpmi_op* op, const double* etas_host, int nb, const double* rhs_d
     HIP_TRY(hipEventRecord(op->ev_fork, s));
     HIP_TRY(hipStreamWaitEvent(op->stream2, op->ev_fork, 0));
   }
-  int rc = schedule(op, P, nb);
+  int rc = 0;
+  if (op->groups == 2 && nb >= 2 && !op->lookahead) {
+    // two independent halves of the batch on two streams: one half's
+    // latency-bound diagonal-block / panel kernels run beside the other's SYRK
+    const int h = nb / 2;
+    if (!op->stream3) {
+      HIP_TRY(hipStreamCreateWithFlags(&op->stream3, hipStreamNonBlocking));
+      HIP_TRY(hipEventCreateWithFlags(&op->ev_g, hipEventDisableTiming));
+    }
+    HIP_TRY(hipEventRecord(op->ev_fork, s));
+    HIP_TRY(hipStreamWaitEvent(op->stream3, op->ev_fork, 0));
+    if ((rc = schedule(op, P, 0, h, s))) return rc;
+    if ((rc = schedule(op, shifted(P, h), h, nb - h, op->stream3))) return rc;
+    HIP_TRY(hipEventRecord(op->ev_g, op->stream3));
+    HIP_TRY(hipStreamWaitEvent(s, op->ev_g, 0));
+  } else {
+    rc = schedule(op, P, 0, nb);
+  }
   if (rc) return rc;
   if (op->lookahead) {
     HIP_TRY(hipEventRecord(op->ev_join, op->stream2));
@@ -563,6 +598,7 @@ int gpmi_op_create(int device, int64_t n, int max_batch, gpmi_op** out) {
   op->nt = (int)(op->n_pad / TS);
   op->max_batch = max_batch;
   if (const char* g = std::getenv("GPMI_SYRK_GROUP")) op->group = std::atoi(g);
+  if (const char* g = std::getenv("GPMI_GROUPS")) op->groups = std::atoi(g);
   const int64_t np = op->n_pad;
   auto fail = [&](hipError_t e, const char* what) {
     gpmi_op_destroy(op);
@@ -612,6 +648,7 @@ int gpmi_op_destroy(gpmi_op* op) {
   DeviceGuard g(op->device);
   if (op->stream) (void)hipStreamSynchronize(op->stream);
   if (op->stream2) (void)hipStreamSynchronize(op->stream2);
+  if (op->stream3) (void)hipStreamSynchronize(op->stream3);
   double* bufs[] = {op->K, op->A, op->R, op->X, op->U, op->Linv, op->logdiag, op->gram,
                     op->out, op->etas, op->rhs_src, op->scratch, op->scratch2, op->tracebuf,
                     op->W, op->tpart, op->Td};
@@ -627,6 +664,8 @@ int gpmi_op_destroy(gpmi_op* op) {
   if (op->ev_fork) (void)hipEventDestroy(op->ev_fork);
   if (op->ev_join) (void)hipEventDestroy(op->ev_join);
   if (op->stream2) (void)hipStreamDestroy(op->stream2);
+  if (op->stream3) (void)hipStreamDestroy(op->stream3);
+  if (op->ev_g) (void)hipEventDestroy(op->ev_g);
   if (op->stream) (void)hipStreamDestroy(op->stream);
   delete op;
   return 0;

@@ -44,7 +44,9 @@ __global__ void qt_reduce_kernel(const double* part, int G, double* a);
 __global__ void qt_tb_kernel(const double* a, const double* T, double* b);
 __global__ void qt_apply_kernel(const double* P, int64_t lda, int m, double* Y, const double* b);
 __global__ void band_chol_kernel(const double* B, int64_t lda, int nt, int64_t n, const double* Y,
-                                 const double* etas, double* out, int out_ld, int* info);
+                                 const double* etas, double* out, int out_ld, int* info,
+                                 double* fac, double* ysol);
+__global__ void band_der_kernel(const double* fac, int nt, double* ysol, double* der);
 
 __global__ void chase_copy_kernel(const double* Ab, double* A, int64_t lda, int n);
 __global__ void chase_task_kernel(double* A, int64_t lda, int n, int t, int s_hi);

@@ -755,7 +755,9 @@ __global__ __launch_bounds__(256) void band_chol_kernel(const double* __restrict
                                                         const double* __restrict__ Y,
                                                         const double* __restrict__ etas,
                                                         double* __restrict__ out, int out_ld,
-                                                        int* __restrict__ info) {
+                                                        int* __restrict__ info,
+                                                        double* __restrict__ fac,
+                                                        double* __restrict__ ysol) {
   __shared__ double Ls[TS * DL];
   __shared__ double Aux[TS * RLD];
   __shared__ double sdiag[TS];
@@ -765,6 +767,9 @@ __global__ __launch_bounds__(256) void band_chol_kernel(const double* __restrict
   const int wr = w >> 1, wc = w & 1, fr = lane & 15, fk = lane >> 4;
   const int e = blockIdx.x;
   const double eta = etas[e];
+  // optional factor store for band_der_kernel: [nt][2][128][128] per eta
+  double* const fac_e = fac ? fac + (int64_t)e * nt * 2 * TS * TS : nullptr;
+  double* const ysol_e = ysol ? ysol + (int64_t)e * nt * TS * RLD : nullptr;
   double logdet = 0.0;
   int fail = 0;
   d4 Gacc = {0.0, 0.0, 0.0, 0.0};
@@ -798,6 +803,13 @@ __global__ __launch_bounds__(256) void band_chol_kernel(const double* __restrict
     }
     lds_inv_block(Ls, Aux);
     __syncthreads();
+    if (fac_e) {
+      double* dst = fac_e + (int64_t)(2 * k) * TS * TS;
+      for (int q = t; q < TS * TS; q += 256) {
+        const int r = q >> 7, c = q & 127;
+        dst[q] = (c <= r) ? Ls[r * DL + c] : 0.0;
+      }
+    }
     // r_k -> Aux (k-major [128][16])
 #pragma unroll
     for (int slot = 0; slot < 2; ++slot) {
@@ -831,6 +843,8 @@ __global__ __launch_bounds__(256) void band_chol_kernel(const double* __restrict
       for (int rr = 0; rr < 4; ++rr) Aux[(ti * DB + fk + 4 * rr) * RLD + fr] = Yv[slot][rr];
     }
     __syncthreads();
+    if (ysol_e)
+      for (int q = t; q < TS * RLD; q += 256) ysol_e[(int64_t)k * TS * RLD + q] = Aux[q];
     // Gram += y^T y over this wave's two 16-row slices
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -873,6 +887,10 @@ __global__ __launch_bounds__(256) void band_chol_kernel(const double* __restrict
         for (int r = 0; r < 4; ++r)
           Ls[(wr * 64 + i * 16 + fk + 4 * r) * DL + wc * 64 + j * 16 + fr] = acc[i][j][r];
     __syncthreads();
+    if (fac_e) {
+      double* dst = fac_e + (int64_t)(2 * k + 1) * TS * TS;
+      for (int q = t; q < TS * TS; q += 256) dst[q] = Ls[(q >> 7) * DL + (q & 127)];
+    }
     // r_{k+1} = Y_{k+1} - C y_k
     const int64_t g1 = (int64_t)(k + 1) * TS;
 #pragma unroll
@@ -939,6 +957,151 @@ __global__ __launch_bounds__(256) void band_chol_kernel(const double* __restrict
     out[(int64_t)e * out_ld] = logdet;
     info[e] = fail;
   }
+}
+
+// ---------------------------------------------------------------------------
+// Higher inverse powers for the eta-derivatives (ProfileLikelihood der1 / der2,
+// _profile_likelihood.py:91-192, need R^T (K + eta I)^-p R for p = 2, 3):
+// with the factor blocks band_chol_kernel stored (Linv_k at fac[2k], the
+// subdiagonal block L_{k+1,k} = C_k at fac[2k+1]) and y = L^-1 Y in ysol,
+//   backward  x = L^-T y   (x_k = Linv_k^T (y_k - C_k^T x_{k+1})),  G2 = x^T x
+//   forward   u = L^-1 x   (u_k = Linv_k (x_k - C_{k-1} u_{k-1})),  G3 = u^T u
+// so G2 = Y^T (B + eta I)^-2 Y and G3 = Y^T (B + eta I)^-3 Y. One workgroup per
+// eta; x overwrites y in ysol. der[e][0:256] = G2, der[e][256:512] = G3.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void block_to_ls(const double* __restrict__ src, double* Ls) {
+  for (int q = threadIdx.x; q < TS * TS; q += 256) Ls[(q >> 7) * DL + (q & 127)] = src[q];
+}
+
+// out[slot] (rows ti * 16 + fk + 4 rr, column fr) = sum_k op(M)[row][k] V[k][fr];
+// op(M) = M or M^T of the 128 x 128 block in Ls; LOWER: M is lower triangular.
+template <bool TRANS, bool LOWER>
+__device__ __forceinline__ void ls_mm(const double* Ls, const double* V, d4 (&out)[2]) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, fr = lane & 15, fk = lane >> 4;
+#pragma unroll
+  for (int slot = 0; slot < 2; ++slot) {
+    const int ti = slot == 0 ? w : NDB - 1 - w;
+    int k0 = 0, k1 = NDB;
+    if (LOWER) {
+      if (TRANS) k0 = ti;
+      else k1 = ti + 1;
+    }
+    d4 a0 = {0.0, 0.0, 0.0, 0.0}, a1 = {0.0, 0.0, 0.0, 0.0};
+    for (int kt = k0; kt < k1; ++kt) {
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const int row = ti * DB + fr, kx = kt * DB + 4 * kk + fk;
+        const double av = TRANS ? Ls[kx * DL + row] : Ls[row * DL + kx];
+        const double bv = V[kx * RLD + fr];
+        if (kk & 1) a1 = mfma64(av, bv, a1);
+        else a0 = mfma64(av, bv, a0);
+      }
+    }
+    out[slot] = a0 + a1;
+  }
+}
+
+__device__ __forceinline__ void slots_to_aux(const d4 (&v)[2], double* Aux) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, fr = lane & 15, fk = lane >> 4;
+#pragma unroll
+  for (int slot = 0; slot < 2; ++slot) {
+    const int ti = slot == 0 ? w : NDB - 1 - w;
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) Aux[(ti * DB + fk + 4 * rr) * RLD + fr] = v[slot][rr];
+  }
+}
+
+__device__ __forceinline__ void load_slots(const double* __restrict__ src, d4 (&v)[2]) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, fr = lane & 15, fk = lane >> 4;
+#pragma unroll
+  for (int slot = 0; slot < 2; ++slot) {
+    const int ti = slot == 0 ? w : NDB - 1 - w;
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) v[slot][rr] = src[(ti * DB + fk + 4 * rr) * RLD + fr];
+  }
+}
+
+__device__ __forceinline__ void gram_acc(const double* Aux, d4& G) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, fr = lane & 15, fk = lane >> 4;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int kt = 2 * w + h;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const double v = Aux[(kt * DB + 4 * kk + fk) * RLD + fr];
+      G = mfma64(v, v, G);
+    }
+  }
+}
+
+__device__ __forceinline__ void gram_out(d4 G, double* Ls, double* dst) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, fr = lane & 15, fk = lane >> 4;
+  d4* sg = reinterpret_cast<d4*>(Ls);
+  __syncthreads();
+  sg[w * 64 + lane] = G;
+  __syncthreads();
+  if (w == 0) {
+    const d4 Gs = ((sg[lane] + sg[64 + lane]) + sg[128 + lane]) + sg[192 + lane];
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) dst[(fk + 4 * rr) * RLD + fr] = Gs[rr];
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(256) void band_der_kernel(const double* __restrict__ fac, int nt,
+                                                       double* __restrict__ ysol,
+                                                       double* __restrict__ der) {
+  __shared__ double Ls[TS * DL];
+  __shared__ double Aux[TS * RLD];
+  const int e = blockIdx.x;
+  const double* fe = fac + (int64_t)e * nt * 2 * TS * TS;
+  double* ye = ysol + (int64_t)e * nt * TS * RLD;
+  d4 G2 = {0.0, 0.0, 0.0, 0.0}, G3 = {0.0, 0.0, 0.0, 0.0};
+  d4 v[2], p[2];
+  // backward: x_k = Linv_k^T (y_k - C_k^T x_{k+1}); Aux holds x_{k+1}
+  for (int k = nt - 1; k >= 0; --k) {
+    load_slots(ye + (int64_t)k * TS * RLD, v);
+    if (k + 1 < nt) {
+      block_to_ls(fe + (int64_t)(2 * k + 1) * TS * TS, Ls);
+      __syncthreads();
+      ls_mm<true, false>(Ls, Aux, p);
+#pragma unroll
+      for (int q = 0; q < 2; ++q) v[q] -= p[q];
+    }
+    __syncthreads();
+    slots_to_aux(v, Aux);
+    block_to_ls(fe + (int64_t)(2 * k) * TS * TS, Ls);
+    __syncthreads();
+    ls_mm<true, true>(Ls, Aux, p);
+    __syncthreads();
+    slots_to_aux(p, Aux);
+    __syncthreads();
+    for (int q = threadIdx.x; q < TS * RLD; q += 256) ye[(int64_t)k * TS * RLD + q] = Aux[q];
+    gram_acc(Aux, G2);
+  }
+  __syncthreads();
+  // forward: u_k = Linv_k (x_k - C_{k-1} u_{k-1}); Aux holds u_{k-1}
+  for (int k = 0; k < nt; ++k) {
+    load_slots(ye + (int64_t)k * TS * RLD, v);
+    if (k > 0) {
+      block_to_ls(fe + (int64_t)(2 * k - 1) * TS * TS, Ls);
+      __syncthreads();
+      ls_mm<false, false>(Ls, Aux, p);
+#pragma unroll
+      for (int q = 0; q < 2; ++q) v[q] -= p[q];
+    }
+    __syncthreads();
+    slots_to_aux(v, Aux);
+    block_to_ls(fe + (int64_t)(2 * k) * TS * TS, Ls);
+    __syncthreads();
+    ls_mm<false, true>(Ls, Aux, p);
+    __syncthreads();
+    slots_to_aux(p, Aux);
+    __syncthreads();
+    gram_acc(Aux, G3);
+  }
+  gram_out(G2, Ls, der + (int64_t)e * 2 * RLD * RLD);
+  gram_out(G3, Ls, der + (int64_t)e * 2 * RLD * RLD + RLD * RLD);
 }
 
 }  // namespace gpmi

@@ -93,7 +93,13 @@ struct gpmi_band {
   int* err = nullptr;        // hh_panel timeout flag
   int cap = 0;
   int nrhs = 0;
-  double reduce_ms = 0.0, rhs_ms = 0.0, loglik_ms = 0.0;
+  double reduce_ms = 0.0, rhs_ms = 0.0, loglik_ms = 0.0, der_ms = 0.0;
+  // eta-derivative terms (allocated on first use): per eta of a chunk, the
+  // banded factor blocks, the solution block and the two higher Grams
+  double* fac = nullptr;     // [dcap][nt][2][128][128]
+  double* ysol = nullptr;    // [dcap][n_pad][16]
+  double* der = nullptr;     // [dcap][2][16][16]
+  int dcap = 0;
   // eigenvalues (bulge chase + bisection), computed on request
   double* Ac = nullptr;      // [n_pad][n_pad] chase copy of the band (lower)
   double* td = nullptr;      // [n] diagonal, then [n] squared subdiagonal, then [n] eigenvalues
@@ -104,7 +110,8 @@ namespace {
 
 int band_free(gpmi_band* b) {
   double* bufs[] = {b->Ab, b->U, b->X, b->Xp, b->part, b->pivrow, b->tau, b->Tm, b->tnp,
-                    b->VtV, b->M, b->Zh, b->Y, b->qtp, b->qa, b->qb, b->etas, b->out, b->Ac, b->td};
+                    b->VtV, b->M, b->Zh, b->Y, b->qtp, b->qa, b->qb, b->etas, b->out, b->Ac, b->td,
+                    b->fac, b->ysol, b->der};
   for (double* p : bufs)
     if (p) (void)hipFree(p);
   if (b->info) (void)hipFree(b->info);
@@ -353,7 +360,7 @@ int gpmi_band_loglik(gpmi_band* b, const double* etas, int neta, double* logdet,
   BD_TRY(hipMemcpyAsync(b->etas, etas, sizeof(double) * neta, hipMemcpyHostToDevice, s));
   BD_TRY(hipEventRecord(b->ev0, s));
   hipLaunchKernelGGL(band_chol_kernel, dim3(neta), dim3(256), 0, s, b->Ab, b->n_pad, b->nt, b->n,
-                     b->Y, b->etas, b->out, OUT_LD, b->info);
+                     b->Y, b->etas, b->out, OUT_LD, b->info, nullptr, nullptr);
   BD_LAUNCH("band_chol_kernel");
   BD_TRY(hipEventRecord(b->ev1, s));
   std::vector<double> hout((size_t)neta * OUT_LD);
@@ -372,6 +379,63 @@ int gpmi_band_loglik(gpmi_band* b, const double* etas, int neta, double* logdet,
       for (int a = 0; a < m; ++a)
         for (int c = 0; c < m; ++c)
           gram[((size_t)e * m + a) * m + c] = hout[(size_t)e * OUT_LD + 1 + a * RLD + c];
+    if (info) info[e] = hinfo[e];
+  }
+  return 0;
+}
+
+int gpmi_band_der_terms(gpmi_band* b, const double* etas, int neta, double* logdet,
+                        double* g1, double* g2, double* g3, int* info) {
+  if (!b) return set_error(-1006, "null handle");
+  if (neta <= 0) return 0;
+  if (neta > GPMI_BAND_DER_MAX)
+    return set_error(-1202, "gpmi_band_der_terms: at most GPMI_BAND_DER_MAX etas per call");
+  Guard g(b->device);
+  int rc = ensure_cap(b, neta);
+  if (rc) return rc;
+  const int64_t np = b->n_pad;
+  const int nt = b->nt;
+  if (b->dcap < neta) {
+    if (b->fac) BD_TRY(hipFree(b->fac));
+    if (b->ysol) BD_TRY(hipFree(b->ysol));
+    if (b->der) BD_TRY(hipFree(b->der));
+    b->fac = b->ysol = b->der = nullptr;
+    b->dcap = 0;
+    BD_TRY(hipMalloc(&b->fac, sizeof(double) * neta * nt * 2 * TS * TS));
+    BD_TRY(hipMalloc(&b->ysol, sizeof(double) * neta * np * RLD));
+    BD_TRY(hipMalloc(&b->der, sizeof(double) * neta * 2 * RLD * RLD));
+    b->dcap = neta;
+  }
+  hipStream_t s = b->stream;
+  BD_TRY(hipMemcpyAsync(b->etas, etas, sizeof(double) * neta, hipMemcpyHostToDevice, s));
+  BD_TRY(hipEventRecord(b->ev0, s));
+  hipLaunchKernelGGL(band_chol_kernel, dim3(neta), dim3(256), 0, s, b->Ab, np, nt, b->n, b->Y,
+                     b->etas, b->out, OUT_LD, b->info, b->fac, b->ysol);
+  BD_LAUNCH("band_chol_kernel");
+  hipLaunchKernelGGL(band_der_kernel, dim3(neta), dim3(256), 0, s, b->fac, nt, b->ysol, b->der);
+  BD_LAUNCH("band_der_kernel");
+  BD_TRY(hipEventRecord(b->ev1, s));
+  std::vector<double> hout((size_t)neta * OUT_LD), hder((size_t)neta * 2 * RLD * RLD);
+  std::vector<int> hinfo(neta);
+  BD_TRY(hipMemcpyAsync(hout.data(), b->out, sizeof(double) * hout.size(), hipMemcpyDeviceToHost,
+                        s));
+  BD_TRY(hipMemcpyAsync(hder.data(), b->der, sizeof(double) * hder.size(), hipMemcpyDeviceToHost,
+                        s));
+  BD_TRY(hipMemcpyAsync(hinfo.data(), b->info, sizeof(int) * neta, hipMemcpyDeviceToHost, s));
+  BD_TRY(hipStreamSynchronize(s));
+  float ms = 0.f;
+  BD_TRY(hipEventElapsedTime(&ms, b->ev0, b->ev1));
+  b->der_ms = ms;
+  const int m = b->nrhs;
+  for (int e = 0; e < neta; ++e) {
+    if (logdet) logdet[e] = hout[(size_t)e * OUT_LD];
+    for (int a = 0; a < m; ++a)
+      for (int c = 0; c < m; ++c) {
+        const size_t o = ((size_t)e * m + a) * m + c;
+        if (g1) g1[o] = hout[(size_t)e * OUT_LD + 1 + a * RLD + c];
+        if (g2) g2[o] = hder[(size_t)e * 2 * RLD * RLD + a * RLD + c];
+        if (g3) g3[o] = hder[(size_t)e * 2 * RLD * RLD + RLD * RLD + a * RLD + c];
+      }
     if (info) info[e] = hinfo[e];
   }
   return 0;
@@ -458,6 +522,12 @@ int gpmi_band_last_timing(gpmi_band* b, double* reduce_ms, double* rhs_ms, doubl
   if (reduce_ms) *reduce_ms = b->reduce_ms;
   if (rhs_ms) *rhs_ms = b->rhs_ms;
   if (loglik_ms) *loglik_ms = b->loglik_ms;
+  return 0;
+}
+
+int gpmi_band_der_ms(gpmi_band* b, double* der_ms) {
+  if (!b) return set_error(-1006, "null handle");
+  if (der_ms) *der_ms = b->der_ms;
   return 0;
 }
 

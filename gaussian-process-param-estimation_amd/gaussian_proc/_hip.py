@@ -83,6 +83,9 @@ SIGNATURES = {
                                         c_double_p, c_int_p]),
     'gpmi_band_get': (ctypes.c_int, [c_op_p, c_double_p, c_i64]),
     'gpmi_band_eigenvalues': (ctypes.c_int, [c_op_p, c_double_p]),
+    'gpmi_band_der_terms': (ctypes.c_int, [c_op_p, c_double_p, ctypes.c_int, c_double_p,
+                                           c_double_p, c_double_p, c_double_p, c_int_p]),
+    'gpmi_band_der_ms': (ctypes.c_int, [c_op_p, c_double_p]),
     'gpmi_band_last_timing': (ctypes.c_int, [c_op_p, c_double_p, c_double_p, c_double_p]),
 }
 
@@ -339,6 +342,35 @@ class Band(object):
                                             ik.ctypes.data_as(c_int_p)), 'gpmi_band_loglik')
             ld[i:i + k], g[i:i + k], info[i:i + k] = ldk, gk, ik
         return ld, g, info
+
+    DER_CHUNK = 256   # GPMI_BAND_DER_MAX
+
+    def der_terms(self, etas):
+        """-> (logdet[neta], g1, g2, g3 [neta, nrhs, nrhs], info[neta]) with
+        gp = R^T (K + eta I)^-p R for the resident RHS R."""
+        etas = as_c(numpy.atleast_1d(etas))
+        ne, m = etas.shape[0], self.nrhs
+        ld = numpy.empty(ne)
+        g = [numpy.empty((ne, m, m)) for _ in range(3)]
+        info = numpy.zeros(ne, dtype=numpy.int32)
+        for i in range(0, ne, self.DER_CHUNK):
+            e = as_c(etas[i:i + self.DER_CHUNK])
+            k = e.shape[0]
+            ldk = numpy.empty(k)
+            gk = [numpy.empty((k, m, m)) for _ in range(3)]
+            ik = numpy.zeros(k, dtype=numpy.int32)
+            check(self.lib.gpmi_band_der_terms(self.h, dptr(e), k, dptr(ldk), dptr(gk[0]),
+                                               dptr(gk[1]), dptr(gk[2]),
+                                               ik.ctypes.data_as(c_int_p)), 'gpmi_band_der_terms')
+            ld[i:i + k], info[i:i + k] = ldk, ik
+            for q in range(3):
+                g[q][i:i + k] = gk[q]
+        return ld, g[0], g[1], g[2], info
+
+    def der_ms(self):
+        v = ctypes.c_double()
+        check(self.lib.gpmi_band_der_ms(self.h, ctypes.byref(v)), 'gpmi_band_der_ms')
+        return v.value
 
     def eigenvalues(self):
         """The n eigenvalues of K, ascending (device bulge chase + bisection)."""

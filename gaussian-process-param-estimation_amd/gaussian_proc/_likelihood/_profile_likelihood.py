@@ -9,7 +9,10 @@ direct likelihood: with G = [X z]^T (K + eta I)^-1 [X z],
        - (G_zz - G_Xz^T G_XX^-1 G_Xz) / (2 sigma^2).
 The reference materialises Y B^-1 Y^T as an n x n matrix (:73); the value is the
 same. The eta-derivatives (:91-192) keep the reference formulas on the operator
-duck type.
+duck type; on the dense eigenvalue operator they come instead from the Gram
+blocks Gp = [X z]^T (K + eta I)^-p [X z], p = 1..3, of the band path
+(MixedCorrelation.der_terms, any number of eta per call) and traceinv from the
+eigenvalues, with the same algebra written in those blocks (_der_from_terms).
 """
 
 import numpy
@@ -19,6 +22,35 @@ from functools import partial
 from ._root_finding import find_interval_with_sign_change, chandrupatla_method
 
 __all__ = ['ProfileLikelihood']
+
+
+def _use_band(K_mixed):
+    return hasattr(K_mixed, 'der_terms') and getattr(K_mixed, 'imate_method', None) == \
+        'eigenvalue' and not getattr(K_mixed, 'sparse', False)
+
+
+def _der_from_terms(n, m, G1, G2, G3, tr1, tr2=None):
+    """der1 (and der2 when tr2 is given) of the profiled likelihood from
+    Gp = [X z]^T S^-p [X z], S = K + eta I, and tr(S^-1), tr(S^-2); the terms of
+    _profile_likelihood.py:91-192 in those blocks: Mz = S^-1 (z - X a) with
+    a = B^-1 X^T S^-1 z, B = X^T S^-1 X."""
+    B = G1[:m, :m]
+    a = numpy.linalg.solve(B, G1[:m, m])
+    zMz = G1[m, m] - G1[:m, m] @ a
+    zM2z = G2[m, m] - 2.0 * (a @ G2[:m, m]) + a @ G2[:m, :m] @ a
+    A = numpy.linalg.solve(B, G2[:m, :m])            # B^-1 Y^T Y
+    trace_M = tr1 - numpy.trace(A)
+    sigma02 = zMz / (n - m)
+    der1 = -0.5 * (trace_M - zM2z / sigma02)
+    if tr2 is None:
+        return der1, None
+    trace_M2 = tr2 - 2.0 * numpy.trace(numpy.linalg.solve(B, G3[:m, :m])) + numpy.trace(A @ A)
+    MzS1Mz = G3[m, m] - 2.0 * (a @ G3[:m, m]) + a @ G3[:m, :m] @ a
+    YtMz = G2[:m, m] - G2[:m, :m] @ a
+    zM3z = MzS1Mz - YtMz @ numpy.linalg.solve(B, YtMz)
+    der2 = (0.5 / sigma02) * ((trace_M2 / (n - m) + (trace_M / (n - m)) ** 2) * zMz -
+                              2.0 * zM3z)
+    return der1, der2
 
 
 class ProfileLikelihood(object):
@@ -55,6 +87,9 @@ class ProfileLikelihood(object):
     def log_likelihood_der1_eta(z, X, K_mixed, log_eta):           # :91-132
         eta = 0.0 if numpy.isneginf(log_eta) else 10.0 ** log_eta
         n, m = X.shape
+        if _use_band(K_mixed):
+            return float(ProfileLikelihood.log_likelihood_der1_eta_batch(z, X, K_mixed,
+                                                                         [log_eta])[0])
         Y, Binv, Mz = ProfileLikelihood._mz(z, X, K_mixed, eta)
         trace_M = K_mixed.traceinv(eta) - numpy.trace(Binv @ (Y.T @ Y))
         zMz = numpy.dot(z, Mz)
@@ -63,8 +98,27 @@ class ProfileLikelihood(object):
         return -0.5 * (trace_M - zM2z / sigma02)
 
     @staticmethod
+    def log_likelihood_der1_eta_batch(z, X, K_mixed, log_etas):
+        """der1 at many log10(eta) in one device call (dense eigenvalue
+        operator; otherwise one log_likelihood_der1_eta per point)."""
+        log_etas = numpy.atleast_1d(numpy.asarray(log_etas, dtype=float))
+        if not _use_band(K_mixed):
+            return numpy.array([ProfileLikelihood.log_likelihood_der1_eta(z, X, K_mixed, le)
+                                for le in log_etas])
+        n, m = X.shape
+        etas = numpy.where(numpy.isneginf(log_etas), 0.0, 10.0 ** log_etas)
+        _, G1, G2, G3 = K_mixed.der_terms(etas, X, z)
+        return numpy.array([_der_from_terms(n, m, G1[i], G2[i], G3[i],
+                                            K_mixed.traceinv(etas[i]))[0]
+                            for i in range(etas.size)])
+
+    @staticmethod
     def log_likelihood_der2_eta(z, X, K_mixed, eta):               # :138-192
         n, m = X.shape
+        if _use_band(K_mixed):
+            _, G1, G2, G3 = K_mixed.der_terms([eta], X, z)
+            return float(_der_from_terms(n, m, G1[0], G2[0], G3[0], K_mixed.traceinv(eta),
+                                         K_mixed.traceinv(eta, exponent=2))[1])
         Y, Binv, Mz = ProfileLikelihood._mz(z, X, K_mixed, eta)
         V = K_mixed.solve(eta, Y)
         A = Binv @ (Y.T @ Y)

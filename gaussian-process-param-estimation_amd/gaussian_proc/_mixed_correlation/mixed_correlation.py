@@ -97,7 +97,7 @@ class MixedCorrelation(object):
             self._band = _hip.Band(self.op)
         return self._band
 
-    def _band_terms(self, etas, X=None, z=None):
+    def _band_rhs_set(self, X, z):
         b = self.band()
         if X is not None:
             X = numpy.asarray(X, dtype=float)
@@ -109,13 +109,34 @@ class MixedCorrelation(object):
                     raise ValueError('at most %d basis functions' % (_hip.MAX_RHS - 1))
                 b.set_rhs(numpy.column_stack([X, z]))
                 self._band_rhs = (X.copy(), z.copy())
-        ld, g, info = b.loglik(etas)
+        return b
+
+    @staticmethod
+    def _check_info(etas, info):
         if numpy.any(info):
             bad = int(numpy.flatnonzero(info)[0])
             raise numpy.linalg.LinAlgError(
                 'K + eta I is not positive definite for eta = %r (pivot %d)'
                 % (numpy.atleast_1d(etas)[bad], info[bad]))
+
+    def _band_terms(self, etas, X=None, z=None):
+        ld, g, info = self._band_rhs_set(X, z).loglik(etas)
+        self._check_info(etas, info)
         return ld, g
+
+    def der_terms(self, etas, X, z):
+        """The eigenvalue operator's eta-derivative terms: for each eta,
+        logdet(K + eta I) and Gp = [X z]^T (K + eta I)^-p [X z] for p = 1, 2, 3,
+        from one banded Cholesky and two more banded triangular sweeps per eta
+        (csrc/gpmi_band.hip band_der_kernel). They replace the 2-5 dense solves
+        per eta of ProfileLikelihood.log_likelihood_der1_eta / der2_eta
+        (_profile_likelihood.py:91-192). Returns (logdet, G1, G2, G3)."""
+        if self.sparse or self.imate_method != 'eigenvalue':
+            raise NotImplementedError('der_terms needs the dense eigenvalue operator')
+        etas = numpy.atleast_1d(numpy.asarray(etas, dtype=float))
+        ld, g1, g2, g3, info = self._band_rhs_set(X, z).der_terms(etas)
+        self._check_info(etas, info)
+        return ld, g1, g2, g3
 
     # ---- sparse K (tapered Matérn, CSR on the device) -------------------------
 

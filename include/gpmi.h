@@ -211,6 +211,25 @@ int gpmi_band_set_rhs(gpmi_band* b, const double* rhs, int64_t ld, int nrhs);
 int gpmi_band_loglik(gpmi_band* b, const double* etas, int neta, double* logdet,
                      double* gram, int* info);
 
+/* Most etas per gpmi_band_der_terms call (its factor store is
+ * 2 * n_pad * 128 doubles per eta: 33.5 MB at n = 16384). */
+#define GPMI_BAND_DER_MAX 256
+
+/* The eta-derivative terms of the profiled likelihood for neta <= GPMI_BAND_DER_MAX
+ * etas (one workgroup per eta): logdet and info as gpmi_band_loglik, and
+ *   g1[e] = R^T (K + eta_e I)^-1 R,  g2[e] = R^T (K + eta_e I)^-2 R,
+ *   g3[e] = R^T (K + eta_e I)^-3 R   (each [nrhs][nrhs]),
+ * from the banded factor (forward solve, backward solve, forward solve).
+ * With traceinv from gpmi_band_eigenvalues these give
+ * ProfileLikelihood.log_likelihood_der1_eta / der2_eta
+ * (_profile_likelihood.py:91-192), which the reference evaluates with 2-5
+ * dense solves per eta. Any output pointer may be NULL. */
+int gpmi_band_der_terms(gpmi_band* b, const double* etas, int neta, double* logdet,
+                        double* g1, double* g2, double* g3, int* info);
+
+/* Device ms of the last gpmi_band_der_terms call (HIP events). */
+int gpmi_band_der_ms(gpmi_band* b, double* der_ms);
+
 /* The n eigenvalues of K (ascending): B -> tridiagonal by bulge chasing on the
  * device (one launch per wavefront of 128-row tasks), then bisection on Sturm
  * counts (one thread per eigenvalue). Completes the eigenvalue operator:

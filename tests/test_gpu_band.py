@@ -176,3 +176,61 @@ def test_eigenvalue_operator_cfg2_golden(gp):
     assert rel([op.traceinv(e) for e in cfg['etas']], g['traceinv']) < 1e-9
     assert rel([op.traceinv(e, 2) for e in cfg['etas']], g['traceinv_exp2']) < 1e-9
     assert rel([op.logdet(e) for e in cfg['etas']], g['logdet']) < 1e-9
+
+
+@pytest.mark.parametrize('n', [5, 128, 129, 300, 1000])
+def test_band_der_terms_vs_numpy(gp, n):
+    """G_p = [X z]^T (K + eta I)^-p [X z], p = 1, 2, 3, from the banded factor
+    (forward, backward, forward sweeps) vs numpy, ragged n, rtol 1e-9."""
+    K, X, z = _inputs(n, n + 5)
+    op = _mc(K)
+    etas = [1e-2, 0.3, 7.0]
+    ld, G1, G2, G3 = op.der_terms(etas, X, z)
+    R = numpy.column_stack([X, z])
+    ref = OracleMC(K, 'cholesky')
+    for i, e in enumerate(etas):
+        Si = numpy.linalg.inv(K + e * numpy.eye(n))
+        assert rel(ld[i], ref.logdet(e)) < 1e-10
+        for G, P in ((G1, Si), (G2, Si @ Si), (G3, Si @ Si @ Si)):
+            Gr = R.T @ P @ R
+            numpy.testing.assert_allclose(G[i], Gr, rtol=1e-9, atol=1e-11 * numpy.abs(Gr).max())
+    # same logdet / G1 as the likelihood call
+    ld_l, G_l = op.loglik_terms(etas, X, z)
+    numpy.testing.assert_array_equal(ld, ld_l)
+    numpy.testing.assert_array_equal(G1, G_l)
+
+
+def test_band_der1_der2_vs_oracle(gp):
+    """ProfileLikelihood der1 (batch and scalar) and der2 on the eigenvalue
+    operator (band Gram blocks + eigenvalue traces) vs the oracle's restatement
+    of the reference formulas."""
+    from gaussian_proc._likelihood._profile_likelihood import ProfileLikelihood
+    from oracle import likelihood as olik
+    K, X, z = _inputs(700, 31, nu=2.5, scale=0.1)
+    op = _mc(K)
+    ref = OracleMC(K, 'cholesky')
+    log_etas = numpy.linspace(-3, 2, 11)
+    d1 = ProfileLikelihood.log_likelihood_der1_eta_batch(z, X, op, log_etas)
+    d1_ref = [olik.profile_der1_eta(z, X, ref, le) for le in log_etas]
+    assert rel(d1, d1_ref) < 1e-8
+    assert rel(ProfileLikelihood.log_likelihood_der1_eta(z, X, op, -1.0),
+               olik.profile_der1_eta(z, X, ref, -1.0)) < 1e-8
+    for eta in (0.01, 1.0):
+        assert rel(ProfileLikelihood.log_likelihood_der2_eta(z, X, op, eta),
+                   olik.profile_der2_eta(z, X, ref, eta)) < 1e-7
+    with pytest.raises(NotImplementedError):
+        from gaussian_proc._mixed_correlation import MixedCorrelation
+        MixedCorrelation(K, imate_method='cholesky').der_terms([1.0], X, z)
+
+
+def test_band_der1_cfg2_golden(gp):
+    """N=4096: der1 / der2 of the reference's eigenvalue operator (golden)."""
+    from gaussian_proc._likelihood._profile_likelihood import ProfileLikelihood
+    cfg = load_json('cfg2.json')
+    pts, z, X = config_inputs(cfg)
+    D = gp.generate_correlation(pts, 0.1, 1.5, device_resident=True)
+    op = _mc(D)
+    d1 = ProfileLikelihood.log_likelihood_der1_eta_batch(z, X, op, cfg['log_etas'])
+    assert rel(d1, cfg['profile_der1_eta']) < 1e-7
+    assert rel([ProfileLikelihood.log_likelihood_der2_eta(z, X, op, e)
+                for e in cfg['profile_der2_eta_etas']], cfg['profile_der2_eta']) < 1e-6

@@ -5,7 +5,13 @@ Each dir holds one pass's *_counter_collection.csv. Per kernel name (template
 and argument list stripped) it reports dispatch count, the summed counter
 values and the per-dispatch mean; FETCH_SIZE / WRITE_SIZE are in KB as
 rocprofv3 reports them (gfx950: FETCH_SIZE counts half the bytes of wide
-coalesced streaming reads, MI355X_MICROARCH.md "HBM")."""
+coalesced streaming reads, MI355X_MICROARCH.md "HBM").
+
+When a pass holds SQ_VALU_MFMA_BUSY_CYCLES, GRBM_GUI_ACTIVE and
+SQ_INSTS_VALU_MFMA_MOPS_F64 and a kernel trace sits beside the counters, it also
+derives per kernel: mfma_busy_frac = MFMA busy cycles / (4 SIMDs x 256 CUs x
+GRBM_GUI_ACTIVE / 8 XCDs), the effective clock GRBM_GUI_ACTIVE / 8 / kernel
+time, and the executed fp64 MFMA rate (one MOPS = 512 flop)."""
 import csv
 import glob
 import json
@@ -35,6 +41,23 @@ def main():
         res['kernels'][k] = {'dispatches': nd,
                              'sum': {c: v for c, v in sorted(cs.items())},
                              'per_dispatch': {c: v / nd for c, v in sorted(cs.items())}}
+    times = defaultdict(float)
+    for d in dirs:
+        for f in glob.glob(os.path.join(d, '*kernel_trace.csv')):
+            with open(f) as fh:
+                for row in csv.DictReader(fh):
+                    times[short(row['Kernel_Name'])] += (int(row['End_Timestamp']) -
+                                                         int(row['Start_Timestamp'])) * 1e-9
+    for k, v in res['kernels'].items():
+        cs = v['sum']
+        if times.get(k) and cs.get('GRBM_GUI_ACTIVE') and 'SQ_VALU_MFMA_BUSY_CYCLES' in cs:
+            per_xcd = cs['GRBM_GUI_ACTIVE'] / 8.0
+            v['derived'] = {
+                'kernel_time_s': times[k],
+                'effective_clock_ghz': per_xcd / times[k] / 1e9,
+                'mfma_busy_frac': cs['SQ_VALU_MFMA_BUSY_CYCLES'] / (4 * 256 * per_xcd),
+                'mfma_f64_tflops_executed': cs.get('SQ_INSTS_VALU_MFMA_MOPS_F64', 0.0) * 512 / times[k] / 1e12,
+            }
     with open(out, 'w') as fh:
         json.dump(res, fh, indent=1)
     for k, v in res['kernels'].items():
