@@ -17,17 +17,22 @@ G = R^T (K + eta I)^-1 R = (L^-1 R)^T (L^-1 R),
 The sigma ~ 0 branch (|sigma| < 1e-8, :49-55) never touches K and is evaluated
 as in the reference. The Jacobian / Hessian keep the reference formulas
 (derivatives w.r.t. sigma^2 and sigma0^2 — reference quirk) on top
-of the operator duck type.
+of the operator duck type; on the dense eigenvalue operator (sigma not ~ 0) the
+same quantities come from the band Gram blocks Gp = R^T (K + eta I)^-p R,
+p = 1..3, and the eigenvalue traces (_jac_hess_from_terms), with no dense solve.
 """
 
 import numpy
 import scipy.optimize
 from functools import partial
 
+from ._profile_likelihood import _use_band
+
 __all__ = ['DirectLikelihood']
 
 _TOL = 1e-8          # _direct_likelihood.py:49,106,324
 _TOL_HESS = 1e-16    # _direct_likelihood.py:179
+_CANCEL = 1e-4       # band-path derivative forms: least kept fraction (_jac_hess_from_terms)
 
 
 def _lp_from_terms(n, m, sigma, logdet_kn, G):
@@ -56,6 +61,60 @@ def _lp_small_sigma(z, X, sigma0):
     Mz = z / s02 - Y @ (Binv @ (Y.T @ z))
     return -0.5 * (n - m) * numpy.log(2.0 * numpy.pi) - 0.5 * logdet_S \
         - 0.5 * logdet_B - 0.5 * numpy.dot(z, Mz)
+
+
+def _jac_hess_from_terms(n, m, sigma, eta, G1, G2, G3, tr1, tr2=None):
+    """Jacobian (and Hessian when tr2 = tr((K + eta I)^-2) is given) of the
+    direct likelihood for |sigma| >= tol from Gp = R^T A^-p R, A = K + eta I,
+    S = sigma^2 A. With a = G1_XX^-1 G1_Xz and r = z - X a (so X^T A^-1 r = 0):
+    M z = A^-1 r / sigma^2, K M z = (r - eta A^-1 r) / sigma^2, and every term of
+    _direct_likelihood.py:89-270 is a quadratic form Qp = r^T A^-p r or uses
+    t2 = X^T A^-2 r, c = G1_XX^-1 t2.
+
+    The reference forms K M z as a product with K; here it is r - eta A^-1 r, so
+    the K-weighted forms are differences such as Q1 - eta Q2. When eta is large
+    against the spectrum carrying r they cancel: if a difference keeps less than
+    _CANCEL of its largest term, this returns None and the caller takes the
+    reference's solve path."""
+    s2 = sigma ** 2
+    Gxx = G1[:m, :m]
+    a = numpy.linalg.solve(Gxx, G1[:m, m])
+
+    def quad(G):
+        return G[m, m] - 2.0 * (a @ G[:m, m]) + a @ G[:m, :m] @ a
+
+    def kept(total, *terms):
+        return abs(total) >= _CANCEL * max(abs(t) for t in terms)
+
+    Q1, Q2 = quad(G1), quad(G2)
+    P2 = numpy.linalg.solve(Gxx, G2[:m, :m])          # G1_XX^-1 G2_XX
+    trace_M = (tr1 - numpy.trace(P2)) / s2
+    trace_KM = (n - m) / s2 - eta * trace_M
+    zMMz = Q2 / s2 ** 2
+    zMKMz = (Q1 - eta * Q2) / s2 ** 2
+    if not kept(Q1 - eta * Q2, Q1, eta * Q2):
+        return None, None
+    jac = numpy.array([-0.5 * trace_KM + 0.5 * zMKMz, -0.5 * trace_M + 0.5 * zMMz], dtype=float)
+    if tr2 is None:
+        return jac, None
+    Q3 = quad(G3)
+    t2 = G2[:m, m] - G2[:m, :m] @ a
+    tc = t2 @ numpy.linalg.solve(Gxx, t2)             # t2^T c
+    zMMMz = (Q3 - tc) / s2 ** 3
+    zMMKMz = (Q2 - eta * Q3 + eta * tc) / s2 ** 3
+    zMKMKMz = (Q1 - 2.0 * eta * Q2 + eta ** 2 * (Q3 - tc)) / s2 ** 3
+    if not (kept(Q2 - eta * Q3 + eta * tc, Q2, eta * Q3, eta * tc) and
+            kept(Q1 - 2.0 * eta * Q2 + eta ** 2 * (Q3 - tc), Q1, 2.0 * eta * Q2, eta ** 2 * Q3,
+                 eta ** 2 * tc)):
+        return jac, None
+    trace_M2 = (tr2 - 2.0 * numpy.trace(numpy.linalg.solve(Gxx, G3[:m, :m])) +
+                numpy.trace(P2 @ P2)) / s2 ** 2
+    trace_KMKM = (n - m) / s2 ** 2 - (2 * eta / s2) * trace_M + (eta ** 2) * trace_M2
+    trace_KMM = trace_M / s2 - eta * trace_M2
+    h_ss = 0.5 * (trace_KMKM - 2.0 * zMKMKMz)
+    h_s0 = 0.5 * (trace_KMM - 2.0 * zMMKMz)
+    h_00 = 0.5 * (trace_M2 - 2.0 * zMMMz)
+    return jac, numpy.array([[h_ss, h_s0], [h_s0, h_00]], dtype=float)
 
 
 class DirectLikelihood(object):
@@ -114,6 +173,13 @@ class DirectLikelihood(object):
         sigma, sigma0 = hyperparam[0], hyperparam[1]
         n, m = X.shape
         small = numpy.abs(sigma) < _TOL
+        if not small and _use_band(K_mixed):
+            eta = (sigma0 / sigma) ** 2
+            _, G1, G2, G3 = K_mixed.der_terms([eta], X, z)
+            jac = _jac_hess_from_terms(n, m, sigma, eta, G1[0], G2[0], G3[0],
+                                       K_mixed.traceinv(eta))[0]
+            if jac is not None:
+                return -jac if sign_switch else jac
         if small:
             Y = X / sigma0 ** 2
         else:
@@ -140,6 +206,13 @@ class DirectLikelihood(object):
         sigma, sigma0 = hyperparam[0], hyperparam[1]
         n, m = X.shape
         small = numpy.abs(sigma) < _TOL_HESS
+        if not small and _use_band(K_mixed):
+            eta = (sigma0 / sigma) ** 2
+            _, G1, G2, G3 = K_mixed.der_terms([eta], X, z)
+            hess = _jac_hess_from_terms(n, m, sigma, eta, G1[0], G2[0], G3[0],
+                                        K_mixed.traceinv(eta), K_mixed.traceinv(eta, 2))[1]
+            if hess is not None:
+                return -hess if sign_switch else hess
         if small:
             Y = X / sigma0 ** 2
             V = Y / sigma0 ** 2

@@ -234,3 +234,20 @@ def test_band_der1_cfg2_golden(gp):
     assert rel(d1, cfg['profile_der1_eta']) < 1e-7
     assert rel([ProfileLikelihood.log_likelihood_der2_eta(z, X, op, e)
                 for e in cfg['profile_der2_eta_etas']], cfg['profile_der2_eta']) < 1e-6
+
+
+def test_band_direct_jac_hess_vs_oracle(gp):
+    """DirectLikelihood Jacobian / Hessian on the eigenvalue operator (band Gram
+    blocks, no dense solve) vs the oracle's reference formulas; the sigma ~ 0
+    branch still takes the reference path."""
+    from gaussian_proc._likelihood._direct_likelihood import DirectLikelihood
+    from oracle import likelihood as olik
+    K, X, z = _inputs(500, 41, nu=1.5, scale=0.15)
+    op = _mc(K)
+    ref = OracleMC(K, 'cholesky')
+    for h in ([0.8, 0.1], [1.5, 1.2], [0.3, 1.0], [1e-9, 0.4]):
+        assert rel(DirectLikelihood.log_likelihood_jacobian(z, X, op, False, h),
+                   olik.direct_jac(z, X, ref, h)) < 1e-8
+        if h[0] >= 1e-8:   # the reference's own Hessian formula cancels at eta ~ 1e17
+            assert rel(DirectLikelihood.log_likelihood_hessian(z, X, op, True, h),
+                       -olik.direct_hess(z, X, ref, h)) < 1e-7
