@@ -79,6 +79,9 @@ struct gpmi_band {
   double* tau = nullptr;     // [nt][128]
   double* Tm = nullptr;      // [nt][128][128] compact-WY T per panel
   double* tnp = nullptr;     // tn partials [nch][128][128]
+  double* tnp2 = nullptr;    // tn partials of V^T V (side stream) [nch][128][128]
+  hipStream_t side = nullptr;          // V^T V and T of a panel, beside its SYMM
+  hipEvent_t ev_v = nullptr, ev_t = nullptr;
   double* VtV = nullptr;     // [128][128]
   double* M = nullptr;       // [128][128]
   double* Zh = nullptr;      // [128][128]
@@ -109,7 +112,7 @@ struct gpmi_band {
 namespace {
 
 int band_free(gpmi_band* b) {
-  double* bufs[] = {b->Ab, b->U, b->X, b->Xp, b->part, b->pivrow, b->tau, b->Tm, b->tnp,
+  double* bufs[] = {b->Ab, b->U, b->X, b->Xp, b->part, b->pivrow, b->tau, b->Tm, b->tnp, b->tnp2,
                     b->VtV, b->M, b->Zh, b->Y, b->qtp, b->qa, b->qb, b->etas, b->out, b->Ac, b->td,
                     b->fac, b->ysol, b->der};
   for (double* p : bufs)
@@ -120,6 +123,9 @@ int band_free(gpmi_band* b) {
   if (b->ev0) (void)hipEventDestroy(b->ev0);
   if (b->ev1) (void)hipEventDestroy(b->ev1);
   if (b->stream) (void)hipStreamDestroy(b->stream);
+  if (b->side) (void)hipStreamDestroy(b->side);
+  if (b->ev_v) (void)hipEventDestroy(b->ev_v);
+  if (b->ev_t) (void)hipEventDestroy(b->ev_t);
   delete b;
   return 0;
 }
@@ -156,20 +162,25 @@ int band_reduce(gpmi_band* b, const double* K) {
                        np, m, Ur, (int64_t)BAND_ULD);
     BD_LAUNCH("vcopy_kernel");
     const int nch = (m + TN_CH - 1) / TN_CH;
-    hipLaunchKernelGGL(tn_partial_kernel, dim3(nch), dim3(256), 0, s, Ur + TS,
-                       (int64_t)BAND_ULD, Ur + TS, (int64_t)BAND_ULD, m, b->tnp);
+    // T from V^T V on the side stream, beside the SYMM (which needs only V)
+    BD_TRY(hipEventRecord(b->ev_v, s));
+    BD_TRY(hipStreamWaitEvent(b->side, b->ev_v, 0));
+    hipLaunchKernelGGL(tn_partial_kernel, dim3(nch), dim3(256), 0, b->side, Ur + TS,
+                       (int64_t)BAND_ULD, Ur + TS, (int64_t)BAND_ULD, m, b->tnp2);
     BD_LAUNCH("tn_partial_kernel");
-    hipLaunchKernelGGL(tn_reduce_kernel, dim3(TS * TS / 256), dim3(256), 0, s, b->tnp, nch,
-                       b->VtV, 1.0);
+    hipLaunchKernelGGL(tn_reduce_kernel, dim3(TS * TS / 256), dim3(256), 0, b->side, b->tnp2,
+                       nch, b->VtV, 1.0);
     BD_LAUNCH("tn_reduce_kernel");
-    hipLaunchKernelGGL(tbuild_kernel, dim3(1), dim3(256), 0, s, b->VtV, tau, T);
+    hipLaunchKernelGGL(tbuild_kernel, dim3(1), dim3(256), 0, b->side, b->VtV, tau, T);
     BD_LAUNCH("tbuild_kernel");
+    BD_TRY(hipEventRecord(b->ev_t, b->side));
     const int sch = (mt + SY_CH - 1) / SY_CH;
     hipLaunchKernelGGL(symm_kernel, dim3(mt, sch), dim3(256), 0, s, b->Ab, np, b->U,
                        (int64_t)BAND_ULD, j + 1, mt, b->Xp);
     BD_LAUNCH("symm_kernel");
     hipLaunchKernelGGL(psum_kernel, dim3(TS * TS / 512, mt), dim3(256), 0, s, b->Xp, sch, b->X);
     BD_LAUNCH("psum_kernel");
+    BD_TRY(hipStreamWaitEvent(s, b->ev_t, 0));
     hipLaunchKernelGGL(xt_kernel, dim3(mt), dim3(256), 0, s, b->X, T);
     BD_LAUNCH("xt_kernel");
     hipLaunchKernelGGL(tn_partial_kernel, dim3(nch), dim3(256), 0, s, Ur + TS,
@@ -246,6 +257,11 @@ int gpmi_band_create(gpmi_op* op, gpmi_band** out) {
     return fail(e, "stream");
   if ((e = hipEventCreate(&b->ev0)) != hipSuccess) return fail(e, "event");
   if ((e = hipEventCreate(&b->ev1)) != hipSuccess) return fail(e, "event");
+  if ((e = hipStreamCreateWithFlags(&b->side, hipStreamNonBlocking)) != hipSuccess)
+    return fail(e, "side stream");
+  if ((e = hipEventCreateWithFlags(&b->ev_v, hipEventDisableTiming)) != hipSuccess ||
+      (e = hipEventCreateWithFlags(&b->ev_t, hipEventDisableTiming)) != hipSuccess)
+    return fail(e, "event");
 #define BALLOC(ptr, count)                                                          \
   if ((e = hipMalloc(&b->ptr, sizeof(double) * (size_t)(count))) != hipSuccess)     \
     return fail(e, #ptr);
@@ -258,6 +274,7 @@ int gpmi_band_create(gpmi_op* op, gpmi_band** out) {
   BALLOC(tau, (size_t)nt * TS);
   BALLOC(Tm, (size_t)nt * TS * TS);
   BALLOC(tnp, (size_t)nch * TS * TS);
+  BALLOC(tnp2, (size_t)nch * TS * TS);
   BALLOC(VtV, TS * TS);
   BALLOC(M, TS * TS);
   BALLOC(Zh, TS * TS);

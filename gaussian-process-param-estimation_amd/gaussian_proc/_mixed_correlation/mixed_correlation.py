@@ -134,8 +134,15 @@ class MixedCorrelation(object):
         if self.sparse or self.imate_method != 'eigenvalue':
             raise NotImplementedError('der_terms needs the dense eigenvalue operator')
         etas = numpy.atleast_1d(numpy.asarray(etas, dtype=float))
-        ld, g1, g2, g3, info = self._band_rhs_set(X, z).der_terms(etas)
+        b = self._band_rhs_set(X, z)
+        c = getattr(self, '_der_cache', None)
+        # the Jacobian and Hessian of one point ask for the same eta: reuse
+        if c is not None and c[0] is self._band_rhs and c[1] is b and \
+                numpy.array_equal(c[2], etas):
+            return c[3]
+        ld, g1, g2, g3, info = b.der_terms(etas)
         self._check_info(etas, info)
+        self._der_cache = (self._band_rhs, b, etas.copy(), (ld, g1, g2, g3))
         return ld, g1, g2, g3
 
     # ---- sparse K (tapered Matérn, CSR on the device) -------------------------
