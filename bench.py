@@ -325,6 +325,7 @@ def der1_sweep(op, X, z, E, rank, torch):
     op.eigenvalues()
     eig_ms = (time.perf_counter() - t0) * 1e3
     ProfileLikelihood.log_likelihood_der1_eta_batch(z, X, op, log_etas)   # warm (buffers)
+    op._der_cache = None   # time the device work, not the operator's last-call cache
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     d1 = ProfileLikelihood.log_likelihood_der1_eta_batch(z, X, op, log_etas)

@@ -16,7 +16,7 @@ constexpr int HH_PANEL_MAXG = 128;  // hh_panel (single-launch) workgroups: m <=
 constexpr int HH_PANEL_LDS = 96 * 1024;  // dynamic LDS: one hh_panel workgroup per CU
 constexpr int HH_PART_LD = 136;    // partial record: S_j (j < 128), sum x^2 at [128]
 constexpr int QT_ROWS = 64;        // rows per qt_partial / qt_apply workgroup
-constexpr int TN_CH = 256;         // rows per tn_partial chunk
+constexpr int TN_CH = 128;         // rows per tn_partial chunk
 constexpr int SY_CH = 16;          // tile columns per symm split-K chunk
 constexpr int BAND_ULD = 384;      // U = [W | V | W]
 constexpr int BAND_MAX_NPAD = HH_MAXG * HH_ROWS;

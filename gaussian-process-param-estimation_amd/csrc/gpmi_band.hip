@@ -499,6 +499,7 @@ __global__ __launch_bounds__(256) void tn_reduce_kernel(const double* __restrict
                                                         double* __restrict__ out, double scale) {
   const int e = blockIdx.x * 256 + threadIdx.x;
   double s = 0.0;
+#pragma unroll 8
   for (int c = 0; c < nch; ++c) s += part[(int64_t)c * TS * TS + e];
   out[e] = scale * s;
 }
