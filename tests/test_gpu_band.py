@@ -251,3 +251,22 @@ def test_band_direct_jac_hess_vs_oracle(gp):
         if h[0] >= 1e-8:   # the reference's own Hessian formula cancels at eta ~ 1e17
             assert rel(DirectLikelihood.log_likelihood_hessian(z, X, op, True, h),
                        -olik.direct_hess(z, X, ref, h)) < 1e-7
+
+
+@pytest.mark.slow
+def test_band_past_single_launch_panel_limit(gp):
+    """n = 16640: the first panel has 129 row blocks, past the single-launch panel
+    QR (<= 128 workgroups), so it runs the per-column hh_col path; logdet and the
+    Gram block vs the dense device Cholesky (an independent factorization)."""
+    from gaussian_proc._mixed_correlation import MixedCorrelation
+    n = 16640
+    rng = numpy.random.RandomState(7)
+    pts = rng.rand(n, 2)
+    D = gp.generate_correlation(pts, 0.05, 1.5, device_resident=True, max_batch=2)
+    X = numpy.column_stack([numpy.ones(n), pts])
+    z = numpy.cos(4 * pts[:, 1]) + 0.1 * rng.randn(n)
+    etas = [0.05, 2.0]
+    ld_b, G_b = MixedCorrelation(D, imate_method='eigenvalue').loglik_terms(etas, X, z)
+    ld_c, G_c = MixedCorrelation(D, imate_method='cholesky').loglik_terms(etas, X, z)
+    assert rel(ld_b, ld_c) < 1e-10
+    numpy.testing.assert_allclose(G_b, G_c, rtol=1e-8, atol=1e-10 * numpy.abs(G_c).max())
