@@ -63,6 +63,7 @@ __device__ __forceinline__ double block_sum8(double v, double* red) {
 // Rows [0, nr) x columns [0, nc) of a row-major block into registers (pair u of
 // thread t: element index e = u * CT + t, row e >> 6, columns 2 (e & 63) + {0,1};
 // outside the block: 0). All CPT loads are in flight together.
+template <bool LOWER = false>
 __device__ __forceinline__ void load_block(const double* __restrict__ src, int64_t lda, int nr,
                                            int nc, d2 (&r)[CPT]) {
 #pragma unroll
@@ -71,7 +72,7 @@ __device__ __forceinline__ void load_block(const double* __restrict__ src, int64
     const int i = e >> 6, c2 = 2 * (e & 63);
     const double* p = src + (int64_t)i * lda + c2;
     r[u] = d2{0.0, 0.0};
-    if (i < nr) {
+    if (i < nr && (!LOWER || c2 <= i)) {   // LOWER: pairs starting on or left of the diagonal
       if (c2 + 1 < nc) r[u] = *reinterpret_cast<const d2*>(p);
       else if (c2 < nc) r[u][0] = p[0];
     }
@@ -95,8 +96,23 @@ __device__ __forceinline__ void lds_matvec(const double* __restrict__ buf, int n
                                            const double* __restrict__ v, double (*sp)[CB]) {
   const int c = threadIdx.x & 127, h = threadIdx.x >> 7;
   double acc = 0.0;
-  if (TRANS || c < nr)
+  if (TRANS || c < nr) {
+#pragma unroll 8
     for (int j = h; j < nj; j += 4) acc += (TRANS ? buf[j * CLD + c] : buf[c * CLD + j]) * v[j];
+  }
+  sp[h][c] = acc;
+}
+
+// out[c] = sum_{j < nj} D[c][j] v[j] for the symmetric D whose lower triangle is
+// in buf (D[c][j] = buf[max(c,j)][min(c,j)]); 4 partial sums per output.
+__device__ __forceinline__ void lds_symv_lower(const double* __restrict__ buf, int nj,
+                                               const double* __restrict__ v, double (*sp)[CB]) {
+  const int c = threadIdx.x & 127, h = threadIdx.x >> 7;
+  double acc = 0.0;
+  if (c < nj) {
+#pragma unroll 8
+    for (int j = h; j < nj; j += 4) acc += (j <= c ? buf[c * CLD + j] : buf[j * CLD + c]) * v[j];
+  }
   sp[h][c] = acc;
 }
 
@@ -121,7 +137,7 @@ __global__ __launch_bounds__(CT) void chase_task_kernel(double* __restrict__ A, 
   const double xi = (tid < L) ? A[(int64_t)(r0 + tid) * lda + col] : 0.0;
   d2 Fr[CPT], Dr[CPT], Er[CPT];
   if (k >= 1) load_block(A + (int64_t)r0 * lda + col, lda, L, CB, Fr);
-  load_block(A + (int64_t)r0 * lda + r0, lda, L, L, Dr);
+  load_block<true>(A + (int64_t)r0 * lda + r0, lda, L, L, Dr);
   if (LE > 0) load_block(A + (int64_t)r1 * lda + r0, lda, LE, L, Er);
   // ---- reflector (LAPACK dlarfg)
   if (tid == 0) sx0 = xi;
@@ -161,26 +177,22 @@ __global__ __launch_bounds__(CT) void chase_task_kernel(double* __restrict__ A, 
   __syncthreads();
   block_to_lds(Dr, buf);
   __syncthreads();
-  for (int e = tid; e < CB * CB; e += CT) {
-    const int i = e >> 7, j = e & 127;
-    if (j > i && j < L) buf[i * CLD + j] = buf[j * CLD + i];
-  }
-  __syncthreads();
-  lds_matvec<false>(buf, L, L, sv, sp);
+  lds_symv_lower(buf, L, sv, sp);
   __syncthreads();
   const double pi =
       (tid < L) ? tau * ((sp[0][tid] + sp[1][tid]) + (sp[2][tid] + sp[3][tid])) : 0.0;
   const double vp = block_sum8((tid < L) ? pi * sv[tid] : 0.0, red);
   if (tid < CB) sw[tid] = (tid < L) ? pi - 0.5 * tau * vp * sv[tid] : 0.0;
   __syncthreads();
-  // whole rows back (the upper part of A's band region is never read)
+  // the lower triangle back (pairs starting on or left of the diagonal; the
+  // partner above the diagonal lands in the band's never-read upper part)
 #pragma unroll
   for (int u = 0; u < CPT; ++u) {
     const int e = u * CT + tid;
     const int i = e >> 6, c2 = 2 * (e & 63);
-    if (i >= L || c2 >= L) continue;
-    const double a0 = i < L ? buf[i * CLD + c2] : 0.0;   // symmetrized value
-    const double a1 = buf[i * CLD + c2 + 1];
+    if (i >= L || c2 >= L || c2 > i) continue;
+    const double a0 = Dr[u][0];
+    const double a1 = Dr[u][1];
     d2 o;
     o[0] = a0 - sv[i] * sw[c2] - sw[i] * sv[c2];
     o[1] = a1 - sv[i] * sw[c2 + 1] - sw[i] * sv[c2 + 1];
