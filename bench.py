@@ -261,8 +261,7 @@ def band_mode(args, D, X, z, world, rank, dist, torch, ld_ref=None):
     def step(s, record):
         idx = [(s * world * E + rank * E + j) % grid.size for j in range(E)]
         etas = grid[idx]
-        b.refresh()
-        op._band_rhs = None
+        op.refresh_band(X, z)   # reduction of K with Q^T [X z] applied alongside
         ld, G = op.loglik_terms(etas, X, z)
         if record:
             for k, v in b.last_timing().items():
@@ -297,7 +296,8 @@ def band_mode(args, D, X, z, world, rank, dist, torch, ld_ref=None):
     out = {
         'value': world * E * K / dt, 'unit': 'evals/s', 'ms_per_step': dt / K * 1e3,
         'eta_per_rank_per_step': E,
-        'step': 'band reduction of K + Q^T [X z] + %d banded Cholesky evals + host lp' % E,
+        'step': 'band reduction of K (Q^T [X z] applied alongside) + %d banded Cholesky evals + '
+                'host lp' % E,
         'reduce_ms': round(red, 3), 'rhs_ms': round(acc['rhs_ms'] / K, 3),
         'loglik_ms': round(acc['loglik_ms'] / K, 3),
         'marginal_evals_per_s_per_gpu': round(E / (acc['loglik_ms'] / K * 1e-3), 1),

@@ -81,7 +81,8 @@ struct gpmi_band {
   double* tnp = nullptr;     // tn partials [nch][128][128]
   double* tnp2 = nullptr;    // tn partials of V^T V (side stream) [nch][128][128]
   hipStream_t side = nullptr;          // V^T V and T of a panel, beside its SYMM
-  hipEvent_t ev_v = nullptr, ev_t = nullptr;
+  hipStream_t qs = nullptr;            // Q^T R during the reduction (gpmi_band_refresh_rhs)
+  hipEvent_t ev_v = nullptr, ev_t = nullptr, ev_q = nullptr;
   double* VtV = nullptr;     // [128][128]
   double* M = nullptr;       // [128][128]
   double* Zh = nullptr;      // [128][128]
@@ -124,18 +125,54 @@ int band_free(gpmi_band* b) {
   if (b->ev1) (void)hipEventDestroy(b->ev1);
   if (b->stream) (void)hipStreamDestroy(b->stream);
   if (b->side) (void)hipStreamDestroy(b->side);
+  if (b->qs) (void)hipStreamDestroy(b->qs);
+  if (b->ev_q) (void)hipEventDestroy(b->ev_q);
   if (b->ev_v) (void)hipEventDestroy(b->ev_v);
   if (b->ev_t) (void)hipEventDestroy(b->ev_t);
   delete b;
   return 0;
 }
 
+// Y <- Q_j^T Y for panel j (Y = b->Y, rows from 128 (j + 1)) on stream st.
+int qt_panel(gpmi_band* b, int j, hipStream_t st) {
+  const int64_t np = b->n_pad;
+  const int64_t r0 = (int64_t)(j + 1) * TS, c0 = (int64_t)j * TS;
+  const int m = (int)(np - r0);
+  const int G = (m + QT_ROWS - 1) / QT_ROWS;
+  const double* P = b->Ab + r0 * np + c0;
+  double* Yr = b->Y + r0 * RLD;
+  hipLaunchKernelGGL(qt_partial_kernel, dim3(G), dim3(256), 0, st, P, np, m, Yr, b->qtp);
+  BD_LAUNCH("qt_partial_kernel");
+  hipLaunchKernelGGL(qt_reduce_kernel, dim3(TS * RLD / 256), dim3(256), 0, st, b->qtp, G, b->qa);
+  BD_LAUNCH("qt_reduce_kernel");
+  hipLaunchKernelGGL(qt_tb_kernel, dim3(1), dim3(256), 0, st, b->qa, b->Tm + (int64_t)j * TS * TS,
+                     b->qb);
+  BD_LAUNCH("qt_tb_kernel");
+  hipLaunchKernelGGL(qt_apply_kernel, dim3(G), dim3(256), 0, st, P, np, m, Yr, b->qb);
+  BD_LAUNCH("qt_apply_kernel");
+  return 0;
+}
+
+// RHS [n][ld] (nrhs columns) -> the padded [n_pad][16] host layout of Y.
+std::vector<double> pack_rhs(const gpmi_band* b, const double* rhs, int64_t ld, int nrhs) {
+  std::vector<double> h((size_t)b->n_pad * RLD, 0.0);
+  for (int64_t i = 0; i < b->n; ++i)
+    for (int c = 0; c < nrhs; ++c) h[(size_t)i * RLD + c] = rhs[i * ld + c];
+  return h;
+}
+
 // Dense -> band: panels j = 0 .. nt-2 of 128 columns (see gpmi_band.hip).
-int band_reduce(gpmi_band* b, const double* K) {
+// With yh (the packed RHS), Y = Q^T R is applied panel by panel on the qs
+// stream as soon as each panel's T exists, beside the rest of the reduction.
+int band_reduce(gpmi_band* b, const double* K, const std::vector<double>* yh = nullptr) {
   hipStream_t s = b->stream;
   const int64_t np = b->n_pad;
   const int nt = b->nt;
   BD_TRY(hipEventRecord(b->ev0, s));
+  if (yh) {
+    BD_TRY(hipMemcpyAsync(b->Y, yh->data(), sizeof(double) * yh->size(), hipMemcpyHostToDevice,
+                          b->qs));
+  }
   BD_TRY(hipMemcpyAsync(b->Ab, K, sizeof(double) * np * np, hipMemcpyDeviceToDevice, s));
   for (int j = 0; j + 1 < nt; ++j) {
     const int64_t r0 = (int64_t)(j + 1) * TS, c0 = (int64_t)j * TS;
@@ -174,6 +211,11 @@ int band_reduce(gpmi_band* b, const double* K) {
     hipLaunchKernelGGL(tbuild_kernel, dim3(1), dim3(256), 0, b->side, b->VtV, tau, T);
     BD_LAUNCH("tbuild_kernel");
     BD_TRY(hipEventRecord(b->ev_t, b->side));
+    if (yh) {
+      BD_TRY(hipStreamWaitEvent(b->qs, b->ev_t, 0));
+      int rc = qt_panel(b, j, b->qs);
+      if (rc) return rc;
+    }
     const int sch = (mt + SY_CH - 1) / SY_CH;
     hipLaunchKernelGGL(symm_kernel, dim3(mt, sch), dim3(256), 0, s, b->Ab, np, b->U,
                        (int64_t)BAND_ULD, j + 1, mt, b->Xp);
@@ -196,6 +238,10 @@ int band_reduce(gpmi_band* b, const double* K) {
     hipLaunchKernelGGL(syr2k_kernel, dim3(mt * (mt + 1) / 2), dim3(256), 0, s, b->Ab, np, b->U,
                        (int64_t)BAND_ULD, j + 1, mt);
     BD_LAUNCH("syr2k_kernel");
+  }
+  if (yh) {
+    BD_TRY(hipEventRecord(b->ev_q, b->qs));
+    BD_TRY(hipStreamWaitEvent(s, b->ev_q, 0));
   }
   BD_TRY(hipEventRecord(b->ev1, s));
   int herr = 0;
@@ -259,6 +305,10 @@ int gpmi_band_create(gpmi_op* op, gpmi_band** out) {
   if ((e = hipEventCreate(&b->ev1)) != hipSuccess) return fail(e, "event");
   if ((e = hipStreamCreateWithFlags(&b->side, hipStreamNonBlocking)) != hipSuccess)
     return fail(e, "side stream");
+  if ((e = hipStreamCreateWithFlags(&b->qs, hipStreamNonBlocking)) != hipSuccess)
+    return fail(e, "rhs stream");
+  if ((e = hipEventCreateWithFlags(&b->ev_q, hipEventDisableTiming)) != hipSuccess)
+    return fail(e, "event");
   if ((e = hipEventCreateWithFlags(&b->ev_v, hipEventDisableTiming)) != hipSuccess ||
       (e = hipEventCreateWithFlags(&b->ev_t, hipEventDisableTiming)) != hipSuccess)
     return fail(e, "event");
@@ -322,6 +372,25 @@ int gpmi_band_refresh(gpmi_band* b, gpmi_op* op) {
   return band_reduce(b, v.K);
 }
 
+int gpmi_band_refresh_rhs(gpmi_band* b, gpmi_op* op, const double* rhs, int64_t ld, int nrhs) {
+  if (!b) return set_error(-1006, "null handle");
+  if (nrhs < 0 || nrhs > RLD) return set_error(-1007, "nrhs outside [0, 16]");
+  OpView v;
+  int rc = op_view(op, &v);
+  if (rc) return rc;
+  if (!v.has_K) return set_error(-1000, "operator has no matrix (load or assemble first)");
+  if (v.n != b->n || v.device != b->device)
+    return set_error(-1202, "operator size or device differs from the band's");
+  Guard g(b->device);
+  b->nrhs = 0;
+  const std::vector<double> h = pack_rhs(b, rhs, ld, nrhs);
+  rc = band_reduce(b, v.K, &h);
+  if (rc) return rc;
+  b->nrhs = nrhs;
+  b->rhs_ms = 0.0;   // overlapped with the reduction
+  return 0;
+}
+
 int gpmi_band_destroy(gpmi_band* b) {
   if (!b) return 0;
   Guard g(b->device);
@@ -335,27 +404,13 @@ int gpmi_band_set_rhs(gpmi_band* b, const double* rhs, int64_t ld, int nrhs) {
   Guard g(b->device);
   hipStream_t s = b->stream;
   const int64_t np = b->n_pad;
-  std::vector<double> h((size_t)np * RLD, 0.0);
-  for (int64_t i = 0; i < b->n; ++i)
-    for (int c = 0; c < nrhs; ++c) h[(size_t)i * RLD + c] = rhs[i * ld + c];
+  (void)np;
+  const std::vector<double> h = pack_rhs(b, rhs, ld, nrhs);
   BD_TRY(hipEventRecord(b->ev0, s));
   BD_TRY(hipMemcpyAsync(b->Y, h.data(), sizeof(double) * h.size(), hipMemcpyHostToDevice, s));
   for (int j = 0; j + 1 < b->nt; ++j) {
-    const int64_t r0 = (int64_t)(j + 1) * TS, c0 = (int64_t)j * TS;
-    const int m = (int)(np - r0);
-    const int G = (m + QT_ROWS - 1) / QT_ROWS;
-    const double* P = b->Ab + r0 * np + c0;
-    double* Yr = b->Y + r0 * RLD;
-    hipLaunchKernelGGL(qt_partial_kernel, dim3(G), dim3(256), 0, s, P, np, m, Yr, b->qtp);
-    BD_LAUNCH("qt_partial_kernel");
-    hipLaunchKernelGGL(qt_reduce_kernel, dim3(TS * RLD / 256), dim3(256), 0, s, b->qtp, G,
-                       b->qa);
-    BD_LAUNCH("qt_reduce_kernel");
-    hipLaunchKernelGGL(qt_tb_kernel, dim3(1), dim3(256), 0, s, b->qa,
-                       b->Tm + (int64_t)j * TS * TS, b->qb);
-    BD_LAUNCH("qt_tb_kernel");
-    hipLaunchKernelGGL(qt_apply_kernel, dim3(G), dim3(256), 0, s, P, np, m, Yr, b->qb);
-    BD_LAUNCH("qt_apply_kernel");
+    int rc = qt_panel(b, j, s);
+    if (rc) return rc;
   }
   BD_TRY(hipEventRecord(b->ev1, s));
   BD_TRY(hipEventSynchronize(b->ev1));
@@ -406,7 +461,7 @@ int gpmi_band_der_terms(gpmi_band* b, const double* etas, int neta, double* logd
   if (!b) return set_error(-1006, "null handle");
   if (neta <= 0) return 0;
   if (neta > GPMI_BAND_DER_MAX)
-    return set_error(-1202, "gpmi_band_der_terms: at most GPMI_BAND_DER_MAX etas per call");
+    return set_error(-1203, "gpmi_band_der_terms: at most GPMI_BAND_DER_MAX etas per call");
   Guard g(b->device);
   int rc = ensure_cap(b, neta);
   if (rc) return rc;

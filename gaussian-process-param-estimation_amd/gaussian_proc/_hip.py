@@ -78,6 +78,7 @@ SIGNATURES = {
     'gpmi_band_create': (ctypes.c_int, [c_op_p, ctypes.POINTER(c_op_p)]),
     'gpmi_band_destroy': (ctypes.c_int, [c_op_p]),
     'gpmi_band_refresh': (ctypes.c_int, [c_op_p, c_op_p]),
+    'gpmi_band_refresh_rhs': (ctypes.c_int, [c_op_p, c_op_p, c_double_p, c_i64, ctypes.c_int]),
     'gpmi_band_set_rhs': (ctypes.c_int, [c_op_p, c_double_p, c_i64, ctypes.c_int]),
     'gpmi_band_loglik': (ctypes.c_int, [c_op_p, c_double_p, ctypes.c_int, c_double_p,
                                         c_double_p, c_int_p]),
@@ -88,6 +89,16 @@ SIGNATURES = {
     'gpmi_band_der_ms': (ctypes.c_int, [c_op_p, c_double_p]),
     'gpmi_band_last_timing': (ctypes.c_int, [c_op_p, c_double_p, c_double_p, c_double_p]),
 }
+
+
+def rhs_block(R, n):
+    """R as a C-contiguous n x k block (k <= MAX_RHS) for the resident RHS."""
+    R = as_c(R)
+    if R.ndim == 1:
+        R = R[:, None]
+    if R.shape[0] != n or R.shape[1] > MAX_RHS:
+        raise ValueError('RHS must be %d x k with k <= %d' % (n, MAX_RHS))
+    return R
 
 
 class GPMIError(RuntimeError):
@@ -202,11 +213,7 @@ class Operator(object):
         return K
 
     def set_rhs(self, R):
-        R = as_c(R)
-        if R.ndim == 1:
-            R = R[:, None]
-        if R.shape[0] != self.n or R.shape[1] > MAX_RHS:
-            raise ValueError('RHS must be %d x k with k <= %d' % (self.n, MAX_RHS))
+        R = rhs_block(R, self.n)
         check(self.lib.gpmi_op_set_rhs(self.h, dptr(R), R.shape[1], R.shape[1]),
               'gpmi_op_set_rhs')
         self.nrhs = R.shape[1]
@@ -310,10 +317,20 @@ class Band(object):
         except Exception:
             pass
 
-    def refresh(self):
-        """Reduce the operator's current K again (buffers reused; RHS reset)."""
-        check(self.lib.gpmi_band_refresh(self.h, self.op.h), 'gpmi_band_refresh')
-        self.nrhs = 0
+    def refresh(self, R=None):
+        """Reduce the operator's current K again (buffers reused). Without R the
+        resident RHS is reset; with R, Q^T R is applied during the reduction."""
+        if R is None:
+            check(self.lib.gpmi_band_refresh(self.h, self.op.h), 'gpmi_band_refresh')
+            self.nrhs = 0
+            return
+        R = self._check_rhs(R)
+        check(self.lib.gpmi_band_refresh_rhs(self.h, self.op.h, dptr(R), R.shape[1], R.shape[1]),
+              'gpmi_band_refresh_rhs')
+        self.nrhs = R.shape[1]
+
+    def _check_rhs(self, R):
+        return rhs_block(R, self.n)
 
     def set_rhs(self, R):
         R = as_c(R)

@@ -97,6 +97,23 @@ class MixedCorrelation(object):
             self._band = _hip.Band(self.op)
         return self._band
 
+    def refresh_band(self, X=None, z=None):
+        """Redo the one-time band reduction of K (same K: the timing form of the
+        setup); with X, z the Q^T [X z] the likelihood terms need is applied
+        during the reduction instead of after it."""
+        b = self.band()
+        self._der_cache = None
+        if X is None:
+            b.refresh()
+            self._band_rhs = None
+            return
+        X = numpy.asarray(X, dtype=float)
+        z = numpy.asarray(z, dtype=float)
+        if X.shape[1] + 1 > _hip.MAX_RHS:
+            raise ValueError('at most %d basis functions' % (_hip.MAX_RHS - 1))
+        b.refresh(numpy.column_stack([X, z]))
+        self._band_rhs = (X.copy(), z.copy())
+
     def _band_rhs_set(self, X, z):
         b = self.band()
         if X is not None:

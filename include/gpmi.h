@@ -198,6 +198,10 @@ int gpmi_band_destroy(gpmi_band* b);
 /* Re-run the reduction on the operator's current K (same n and device), reusing
  * the band's buffers; the resident RHS must be set again afterwards. */
 int gpmi_band_refresh(gpmi_band* b, gpmi_op* op);
+/* gpmi_band_refresh + gpmi_band_set_rhs in one call: Y = Q^T R is applied panel by
+ * panel on a separate stream while the reduction proceeds (same results). */
+int gpmi_band_refresh_rhs(gpmi_band* b, gpmi_op* op, const double* rhs, int64_t ld,
+                          int nrhs);
 
 /* Y = Q^T R for an [n][ld] host block R with nrhs <= 16 columns (resident). */
 int gpmi_band_set_rhs(gpmi_band* b, const double* rhs, int64_t ld, int nrhs);

@@ -270,3 +270,19 @@ def test_band_past_single_launch_panel_limit(gp):
     ld_c, G_c = MixedCorrelation(D, imate_method='cholesky').loglik_terms(etas, X, z)
     assert rel(ld_b, ld_c) < 1e-10
     numpy.testing.assert_allclose(G_b, G_c, rtol=1e-8, atol=1e-10 * numpy.abs(G_c).max())
+
+
+def test_band_refresh_with_rhs_matches_set_rhs(gp):
+    """Q^T [X z] applied during the reduction (third stream) equals the separate
+    set_rhs pass bit for bit (same kernels, same order)."""
+    K, X, z = _inputs(900, 77)
+    op = _mc(K)
+    etas = [1e-3, 0.2, 3.0]
+    ld0, G0 = op.loglik_terms(etas, X, z)
+    op.refresh_band(X, z)
+    ld1, G1 = op.loglik_terms(etas, X, z)
+    numpy.testing.assert_array_equal(ld0, ld1)
+    numpy.testing.assert_array_equal(G0, G1)
+    op.refresh_band()
+    ld2, G2 = op.loglik_terms(etas, X, z)
+    numpy.testing.assert_array_equal(G0, G2)
