@@ -37,7 +37,9 @@ __global__ void xt_kernel(double* X, const double* T);
 __global__ void z_kernel(const double* T, const double* M, double* Zh);
 __global__ void w_kernel(const double* X, double* U, int64_t ldu, const double* Zh);
 __global__ void syr2k_kernel(double* A, int64_t lda, const double* U, int64_t ldu, int tr0,
-                             int mt);
+                             int mt, int sub);
+__global__ void syr2k_rest_kernel(double* A, int64_t lda, const double* U, int64_t ldu, int tr0,
+                                  int mt);
 __global__ void qt_partial_kernel(const double* P, int64_t lda, int m, const double* Y,
                                   double* part);
 __global__ void qt_reduce_kernel(const double* part, int G, double* a);

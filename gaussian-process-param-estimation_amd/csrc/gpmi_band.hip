@@ -639,20 +639,40 @@ __global__ __launch_bounds__(256, 2) void w_kernel(const double* __restrict__ X,
 }
 
 // A_IJ -= [W_I V_I] [V_J W_J]^T on the lower tiles of the trailing mt x mt tiles.
-__global__ __launch_bounds__(256, 2) void syr2k_kernel(double* __restrict__ A, int64_t lda,
-                                                       const double* __restrict__ U,
-                                                       int64_t ldu, int tr0, int mt) {
-  __shared__ double smem[4 * GSTAGE];
-  const int q = xcd_remap(blockIdx.x, gridDim.x);
-  int i, j;
-  tri_decode(q, mt, &i, &j);
-  const int I = tr0 + i, J = tr0 + j;
+__device__ __forceinline__ void syr2k_tile(double* __restrict__ A, int64_t lda,
+                                           const double* __restrict__ U, int64_t ldu, int I, int J,
+                                           double* smem) {
   double* C = A + (int64_t)I * TS * lda + (int64_t)J * TS;
   d4 acc[4][4];
   load_tile(C, lda, acc);
   gemm_tile<KFAST, KFAST, true>(U + (int64_t)I * TS * ldu, ldu, U + (int64_t)J * TS * ldu + TS,
                                 ldu, 2 * TS, smem, acc);
   store_tile(C, lda, acc, 1.0);
+}
+
+// sub 0: every lower tile of the trailing mt x mt block (XCD-aware order);
+// sub 1: tile column 0 only (the next panel's columns, look-ahead).
+__global__ __launch_bounds__(256, 2) void syr2k_kernel(double* __restrict__ A, int64_t lda,
+                                                       const double* __restrict__ U,
+                                                       int64_t ldu, int tr0, int mt, int sub) {
+  __shared__ double smem[4 * GSTAGE];
+  int i = blockIdx.x, j = 0;
+  if (sub == 0) tri_decode(xcd_remap(blockIdx.x, gridDim.x), mt, &i, &j);
+  syr2k_tile(A, lda, U, ldu, tr0 + i, tr0 + j, smem);
+}
+
+// Look-ahead: the lower tiles right of tile column 0, looped over by a capped
+// grid so that CUs stay free for the next panel's QR.
+__global__ __launch_bounds__(256, 2) void syr2k_rest_kernel(double* __restrict__ A, int64_t lda,
+                                                            const double* __restrict__ U,
+                                                            int64_t ldu, int tr0, int mt) {
+  __shared__ double smem[4 * GSTAGE];
+  const int ntiles = (mt - 1) * mt / 2;
+  for (int q = blockIdx.x; q < ntiles; q += gridDim.x) {
+    int i, j;
+    tri_decode(q, mt - 1, &i, &j);
+    syr2k_tile(A, lda, U, ldu, tr0 + i + 1, tr0 + j + 1, smem);
+  }
 }
 
 // ---------------------------------------------------------------------------

@@ -82,6 +82,11 @@ struct gpmi_band {
   double* tnp2 = nullptr;    // tn partials of V^T V (side stream) [nch][128][128]
   hipStream_t side = nullptr;          // V^T V and T of a panel, beside its SYMM
   hipStream_t qs = nullptr;            // Q^T R during the reduction (gpmi_band_refresh_rhs)
+  // look-ahead: the next panel's QR (high-priority stream) beside the rest of the
+  // SYR2K on a capped grid
+  int lookahead = 1, la_grid = 128, ncu = 256;
+  hipStream_t s_pan = nullptr;
+  hipEvent_t ev_col = nullptr, ev_pan = nullptr;
   hipEvent_t ev_v = nullptr, ev_t = nullptr, ev_q = nullptr;
   double* VtV = nullptr;     // [128][128]
   double* M = nullptr;       // [128][128]
@@ -126,6 +131,9 @@ int band_free(gpmi_band* b) {
   if (b->stream) (void)hipStreamDestroy(b->stream);
   if (b->side) (void)hipStreamDestroy(b->side);
   if (b->qs) (void)hipStreamDestroy(b->qs);
+  if (b->s_pan) (void)hipStreamDestroy(b->s_pan);
+  for (hipEvent_t e : {b->ev_col, b->ev_pan})
+    if (e) (void)hipEventDestroy(e);
   if (b->ev_q) (void)hipEventDestroy(b->ev_q);
   if (b->ev_v) (void)hipEventDestroy(b->ev_v);
   if (b->ev_t) (void)hipEventDestroy(b->ev_t);
@@ -153,6 +161,30 @@ int qt_panel(gpmi_band* b, int j, hipStream_t st) {
   return 0;
 }
 
+// Householder QR of panel j (columns [128 j, +128), rows from 128 (j + 1)) on st.
+int panel_qr(gpmi_band* b, int j, hipStream_t st) {
+  const int64_t np = b->n_pad;
+  const int64_t r0 = (int64_t)(j + 1) * TS, c0 = (int64_t)j * TS;
+  const int m = (int)(np - r0);
+  const int G = (m + HH_ROWS - 1) / HH_ROWS;
+  double* P = b->Ab + r0 * np + c0;
+  double* tau = b->tau + (int64_t)j * TS;
+  if (G <= HH_PANEL_MAXG) {
+    // one launch per panel (rows in registers, in-launch reductions)
+    BD_TRY(hipMemsetAsync(b->ctr, 0, 512, st));
+    hipLaunchKernelGGL(hh_panel_kernel, dim3(G), dim3(HH_THREADS), HH_PANEL_LDS, st, P, np, m,
+                       b->part, b->pivrow, b->ctr, tau, b->err);
+    BD_LAUNCH("hh_panel_kernel");
+  } else {
+    for (int c = -1; c < TS; ++c) {
+      hipLaunchKernelGGL(hh_col_kernel, dim3(G), dim3(HH_THREADS), 0, st, P, np, m, c, b->part,
+                         b->pivrow, tau);
+      BD_LAUNCH("hh_col_kernel");
+    }
+  }
+  return 0;
+}
+
 // RHS [n][ld] (nrhs columns) -> the padded [n_pad][16] host layout of Y.
 std::vector<double> pack_rhs(const gpmi_band* b, const double* rhs, int64_t ld, int nrhs) {
   std::vector<double> h((size_t)b->n_pad * RLD, 0.0);
@@ -174,26 +206,19 @@ int band_reduce(gpmi_band* b, const double* K, const std::vector<double>* yh = n
                           b->qs));
   }
   BD_TRY(hipMemcpyAsync(b->Ab, K, sizeof(double) * np * np, hipMemcpyDeviceToDevice, s));
+  const bool la = b->lookahead && b->s_pan;
+  bool ahead = false;   // panel j already factored by the previous look-ahead
   for (int j = 0; j + 1 < nt; ++j) {
     const int64_t r0 = (int64_t)(j + 1) * TS, c0 = (int64_t)j * TS;
     const int m = (int)(np - r0), mt = nt - j - 1;
-    const int G = (m + HH_ROWS - 1) / HH_ROWS;
     double* P = b->Ab + r0 * np + c0;
     double* tau = b->tau + (int64_t)j * TS;
     double* T = b->Tm + (int64_t)j * TS * TS;
-    if (G <= HH_PANEL_MAXG) {
-      // one launch per panel (rows in registers, in-launch reductions)
-      BD_TRY(hipMemsetAsync(b->ctr, 0, 512, s));
-      hipLaunchKernelGGL(hh_panel_kernel, dim3(G), dim3(HH_THREADS), HH_PANEL_LDS, s, P, np, m,
-                         b->part, b->pivrow, b->ctr, tau, b->err);
-      BD_LAUNCH("hh_panel_kernel");
-    } else {
-      for (int c = -1; c < TS; ++c) {
-        hipLaunchKernelGGL(hh_col_kernel, dim3(G), dim3(HH_THREADS), 0, s, P, np, m, c,
-                           b->part, b->pivrow, tau);
-        BD_LAUNCH("hh_col_kernel");
-      }
+    if (!ahead) {
+      int rc = panel_qr(b, j, s);
+      if (rc) return rc;
     }
+    ahead = false;
     double* Ur = b->U + r0 * BAND_ULD;
     hipLaunchKernelGGL(vcopy_kernel, dim3((unsigned)((int64_t)m * TS / 256)), dim3(256), 0, s, P,
                        np, m, Ur, (int64_t)BAND_ULD);
@@ -235,9 +260,34 @@ int band_reduce(gpmi_band* b, const double* K, const std::vector<double>* yh = n
     BD_LAUNCH("z_kernel");
     hipLaunchKernelGGL(w_kernel, dim3(mt), dim3(256), 0, s, b->X, Ur, (int64_t)BAND_ULD, b->Zh);
     BD_LAUNCH("w_kernel");
-    hipLaunchKernelGGL(syr2k_kernel, dim3(mt * (mt + 1) / 2), dim3(256), 0, s, b->Ab, np, b->U,
-                       (int64_t)BAND_ULD, j + 1, mt);
-    BD_LAUNCH("syr2k_kernel");
+    const int next_g = (int)((np - r0 - TS + HH_ROWS - 1) / HH_ROWS);   // panel j + 1's grid
+    if (la && j + 2 < nt && next_g <= HH_PANEL_MAXG) {
+      // tile column 0 of the update (panel j + 1's columns) first; then that
+      // panel's QR beside the rest of the update on a grid capped to la_grid
+      // workgroups, so that the panel's workgroups find free CUs
+      hipLaunchKernelGGL(syr2k_kernel, dim3(mt), dim3(256), 0, s, b->Ab, np, b->U,
+                         (int64_t)BAND_ULD, j + 1, mt, 1);
+      BD_LAUNCH("syr2k_kernel");
+      BD_TRY(hipEventRecord(b->ev_col, s));
+      BD_TRY(hipStreamWaitEvent(b->s_pan, b->ev_col, 0));
+      int rc = panel_qr(b, j + 1, b->s_pan);
+      if (rc) return rc;
+      BD_TRY(hipEventRecord(b->ev_pan, b->s_pan));
+      const int rest = (mt - 1) * mt / 2;
+      // la_grid 0: leave exactly the panel's workgroup count of CUs free (measured:
+      // slower than a fixed 128-workgroup cap at N = 16384, 302 vs 262 ms)
+      const int cap = b->la_grid > 0 ? b->la_grid : std::max(64, b->ncu - next_g);
+      hipLaunchKernelGGL(syr2k_rest_kernel, dim3(std::min(rest, cap)), dim3(256), 0, s, b->Ab,
+                         np, b->U, (int64_t)BAND_ULD, j + 1, mt);
+      BD_LAUNCH("syr2k_rest_kernel");
+      BD_TRY(hipStreamWaitEvent(s, b->ev_pan, 0));
+      ahead = true;
+    } else {
+      const int tiles = mt * (mt + 1) / 2;
+      hipLaunchKernelGGL(syr2k_kernel, dim3(tiles), dim3(256), 0, s, b->Ab, np, b->U,
+                         (int64_t)BAND_ULD, j + 1, mt, 0);
+      BD_LAUNCH("syr2k_kernel");
+    }
   }
   if (yh) {
     BD_TRY(hipEventRecord(b->ev_q, b->qs));
@@ -307,6 +357,20 @@ int gpmi_band_create(gpmi_op* op, gpmi_band** out) {
     return fail(e, "side stream");
   if ((e = hipStreamCreateWithFlags(&b->qs, hipStreamNonBlocking)) != hipSuccess)
     return fail(e, "rhs stream");
+  if (const char* la = std::getenv("GPMI_BAND_LA")) b->lookahead = std::atoi(la);
+  if (const char* lg = std::getenv("GPMI_BAND_LA_GRID")) b->la_grid = std::max(0, std::atoi(lg));
+  if ((e = hipDeviceGetAttribute(&b->ncu, hipDeviceAttributeMultiprocessorCount, v.device)) !=
+      hipSuccess)
+    return fail(e, "CU count");
+  if (b->lookahead) {
+    int lo = 0, hi = 0;
+    if ((e = hipDeviceGetStreamPriorityRange(&lo, &hi)) != hipSuccess) return fail(e, "prio");
+    if ((e = hipStreamCreateWithPriority(&b->s_pan, hipStreamNonBlocking, hi)) != hipSuccess)
+      return fail(e, "panel stream");
+    for (hipEvent_t* ev : {&b->ev_col, &b->ev_pan})
+      if ((e = hipEventCreateWithFlags(ev, hipEventDisableTiming)) != hipSuccess)
+        return fail(e, "event");
+  }
   if ((e = hipEventCreateWithFlags(&b->ev_q, hipEventDisableTiming)) != hipSuccess)
     return fail(e, "event");
   if ((e = hipEventCreateWithFlags(&b->ev_v, hipEventDisableTiming)) != hipSuccess ||
