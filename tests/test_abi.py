@@ -3,6 +3,8 @@
 import os
 import re
 
+import numpy
+
 import pytest
 
 from gaussian_proc import _hip
@@ -38,3 +40,25 @@ def test_error_paths_without_device():
     # invalid arguments are rejected before any device work
     assert lib.gpmi_op_set_timing(None, 1) < 0
     assert 'null handle' in _hip.last_error()
+
+
+def test_missing_library_fails_loudly(monkeypatch):
+    """No CPU fallback: without libgpmi.so the operator raises ImportError."""
+    monkeypatch.setattr(_hip, '_lib', None)
+    monkeypatch.setattr(_hip, 'LIB_PATH', '/nonexistent/libgpmi.so')
+    with pytest.raises(ImportError):
+        _hip.load()
+    from gaussian_proc._mixed_correlation import MixedCorrelation
+    with pytest.raises(ImportError):
+        MixedCorrelation(numpy.eye(4), imate_method='cholesky')
+
+
+def test_no_device_raises(monkeypatch):
+    """On a host without a HIP device the operator raises GPMIError (the CPU
+    container), never computes on the host."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip('a device is present')
+    from gaussian_proc._mixed_correlation import MixedCorrelation
+    with pytest.raises(_hip.GPMIError):
+        MixedCorrelation(numpy.eye(4), imate_method='cholesky')
