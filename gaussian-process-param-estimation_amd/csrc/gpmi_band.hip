@@ -991,7 +991,18 @@ __global__ __launch_bounds__(256) void band_chol_kernel(const double* __restrict
 // eta; x overwrites y in ysol. der[e][0:256] = G2, der[e][256:512] = G3.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void block_to_ls(const double* __restrict__ src, double* Ls) {
-  for (int q = threadIdx.x; q < TS * TS; q += 256) Ls[(q >> 7) * DL + (q & 127)] = src[q];
+  // all 32 16-byte loads of this thread in flight before the LDS stores
+  constexpr int NP = TS * TS / 2 / 256;
+  d2 r[NP];
+#pragma unroll
+  for (int u = 0; u < NP; ++u)
+    r[u] = *reinterpret_cast<const d2*>(src + 2 * (u * 256 + threadIdx.x));
+#pragma unroll
+  for (int u = 0; u < NP; ++u) {
+    const int q = 2 * (u * 256 + threadIdx.x);
+    Ls[(q >> 7) * DL + (q & 127)] = r[u][0];
+    Ls[(q >> 7) * DL + (q & 127) + 1] = r[u][1];
+  }
 }
 
 // out[slot] (rows ti * 16 + fk + 4 rr, column fr) = sum_k op(M)[row][k] V[k][fr];

@@ -1,6 +1,6 @@
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 120 python tools/chol_probe.py > gpurun_out/cp_base.log 2>&1 || exit 1
-GPMI_LIB_VARIANT=noe timeout -k 10 120 python tools/chol_probe.py > gpurun_out/cp_noe.log 2>&1 || exit 1
-GPMI_LIB_VARIANT=noeb timeout -k 10 120 python tools/chol_probe.py > gpurun_out/cp_noeb.log 2>&1
+timeout -k 10 120 python tools/chol_probe.py > gpurun_out/cp_base.log 2>&1
+
+
