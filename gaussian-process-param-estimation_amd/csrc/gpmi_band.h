@@ -17,7 +17,16 @@ constexpr int HH_PANEL_LDS = 96 * 1024;  // dynamic LDS: one hh_panel workgroup 
 constexpr int HH_PART_LD = 136;    // partial record: S_j (j < 128), sum x^2 at [128]
 constexpr int QT_ROWS = 64;        // rows per qt_partial / qt_apply workgroup
 constexpr int TN_CH = 128;         // rows per tn_partial chunk
-constexpr int SY_CH = 16;          // tile columns per symm split-K chunk
+#ifndef GPMI_SYMM_DIV
+#define GPMI_SYMM_DIV 1024
+#endif
+constexpr int SY_CH = 16;          // tile columns per symm split-K chunk (at most)
+// symm split-K chunk for an mt-tile trailing block: SY_CH tile columns, fewer
+// when mt is small so that mt x chunks still gives ~2 workgroups per CU
+inline int symm_chunk(int mt) {
+  int ch = mt * mt / GPMI_SYMM_DIV;
+  return ch < 1 ? 1 : (ch > SY_CH ? SY_CH : ch);
+}
 constexpr int BAND_ULD = 384;      // U = [W | V | W]
 constexpr int BAND_MAX_NPAD = HH_MAXG * HH_ROWS;
 
@@ -31,7 +40,7 @@ __global__ void tn_partial_kernel(const double* P1, int64_t ld1, const double* P
 __global__ void tn_reduce_kernel(const double* part, int nch, double* out, double scale);
 __global__ void tbuild_kernel(const double* VtV, const double* tau, double* T);
 __global__ void symm_kernel(const double* A, int64_t lda, const double* U, int64_t ldu, int tr0,
-                            int mt, double* Xp);
+                            int mt, int chunk, double* Xp);
 __global__ void psum_kernel(const double* Xp, int nch, double* X);
 __global__ void xt_kernel(double* X, const double* T);
 __global__ void z_kernel(const double* T, const double* M, double* Zh);

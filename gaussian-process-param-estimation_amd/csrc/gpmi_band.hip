@@ -569,12 +569,12 @@ __global__ __launch_bounds__(256) void tbuild_kernel(const double* __restrict__ 
 // A22_IJ = A_IJ (J <= I, stored) or A_JI^T (J > I, read transposed).
 __global__ __launch_bounds__(256, 2) void symm_kernel(const double* __restrict__ A, int64_t lda,
                                                       const double* __restrict__ U, int64_t ldu,
-                                                      int tr0, int mt,
+                                                      int tr0, int mt, int chunk,
                                                       double* __restrict__ Xp) {
   __shared__ double smem[4 * GSTAGE];
   const int il = blockIdx.x, ch = blockIdx.y, nch = gridDim.y;
   const int I = tr0 + il;
-  const int jl0 = ch * SY_CH, jl1 = min(mt, (ch + 1) * SY_CH);
+  const int jl0 = ch * chunk, jl1 = min(mt, (ch + 1) * chunk);
   const int jsplit = min(jl1, max(jl0, il + 1));   // tiles [jl0, jsplit) have J <= I
   d4 acc[4][4];
   zero_tile(acc);

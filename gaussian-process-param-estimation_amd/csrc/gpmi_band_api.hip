@@ -241,9 +241,10 @@ int band_reduce(gpmi_band* b, const double* K, const std::vector<double>* yh = n
       int rc = qt_panel(b, j, b->qs);
       if (rc) return rc;
     }
-    const int sch = (mt + SY_CH - 1) / SY_CH;
+    const int chunk = symm_chunk(mt);
+    const int sch = (mt + chunk - 1) / chunk;
     hipLaunchKernelGGL(symm_kernel, dim3(mt, sch), dim3(256), 0, s, b->Ab, np, b->U,
-                       (int64_t)BAND_ULD, j + 1, mt, b->Xp);
+                       (int64_t)BAND_ULD, j + 1, mt, chunk, b->Xp);
     BD_LAUNCH("symm_kernel");
     hipLaunchKernelGGL(psum_kernel, dim3(TS * TS / 512, mt), dim3(256), 0, s, b->Xp, sch, b->X);
     BD_LAUNCH("psum_kernel");
@@ -340,7 +341,11 @@ int gpmi_band_create(gpmi_op* op, gpmi_band** out) {
   b->nt = (int)(v.n_pad / TS);
   const int64_t np = b->n_pad;
   const int nt = b->nt;
-  const int sch = std::max(1, (nt - 1 + SY_CH - 1) / SY_CH);
+  int64_t xp_tiles = 1;   // the largest mt x split-K chunks over the panels
+  for (int mt = 1; mt < nt; ++mt) {
+    const int ch = symm_chunk(mt);
+    xp_tiles = std::max<int64_t>(xp_tiles, (int64_t)mt * ((mt + ch - 1) / ch));
+  }
   const int nch = (int)std::max<int64_t>(1, (np + TN_CH - 1) / TN_CH);
   hipError_t e;
   auto fail = [&](hipError_t err, const char* what) {
@@ -382,7 +387,7 @@ int gpmi_band_create(gpmi_op* op, gpmi_band** out) {
   BALLOC(Ab, np * np);
   BALLOC(U, np * BAND_ULD);
   BALLOC(X, np * TS);
-  BALLOC(Xp, (size_t)std::max(1, nt - 1) * sch * TS * TS);
+  BALLOC(Xp, (size_t)xp_tiles * TS * TS);
   BALLOC(part, 2 * HH_MAXG * HH_PART_LD);
   BALLOC(pivrow, 2 * TS);
   BALLOC(tau, (size_t)nt * TS);
