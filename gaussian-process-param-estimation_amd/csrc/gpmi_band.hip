@@ -36,6 +36,10 @@
 #include "gpmi_lds_chol.h"
 #include "gpmi_band.h"
 
+#ifndef GPMI_BAND_STAMPS
+#define GPMI_BAND_STAMPS 0   // probe builds: phase stamps of band_chol_kernel (printf)
+#endif
+
 namespace gpmi {
 
 // ---------------------------------------------------------------------------
@@ -788,6 +792,19 @@ __global__ __launch_bounds__(256) void band_chol_kernel(const double* __restrict
   const int wr = w >> 1, wc = w & 1, fr = lane & 15, fk = lane >> 4;
   const int e = blockIdx.x;
   const double eta = etas[e];
+#if GPMI_BAND_STAMPS
+  unsigned long long bst[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define BSTAMP(i) \
+  if (e == 0 && (k == 8 || k == 64) && t == 0) bst[i] = wall_clock64()
+#define BSTAMP_PRINT() \
+  if (e == 0 && (k == 8 || k == 64) && t == 0)                                          \
+    printf("band_chol k=%d stamps(10ns): chol %llu ld %llu inv %llu y %llu C %llu r %llu D %llu\n", \
+           k, bst[1] - bst[0], bst[2] - bst[1], bst[3] - bst[2], bst[4] - bst[3],          \
+           bst[5] - bst[4], bst[6] - bst[5], bst[7] - bst[6])
+#else
+#define BSTAMP(i)
+#define BSTAMP_PRINT()
+#endif
   // optional factor store for band_der_kernel: [nt][2][128][128] per eta
   double* const fac_e = fac ? fac + (int64_t)e * nt * 2 * TS * TS : nullptr;
   double* const ysol_e = ysol ? ysol + (int64_t)e * nt * TS * RLD : nullptr;
@@ -809,7 +826,9 @@ __global__ __launch_bounds__(256) void band_chol_kernel(const double* __restrict
   if (t == 0) s_fail = 0;
   __syncthreads();
   for (int k = 0; k < nt; ++k) {
+    BSTAMP(0);
     lds_chol_block(Ls, Aux, sdiag, &s_fail);
+    BSTAMP(1);
     if (w < 2) {
       double v = ((int64_t)k * TS + t < n) ? log(sdiag[t]) : 0.0;
 #pragma unroll
@@ -822,8 +841,10 @@ __global__ __launch_bounds__(256) void band_chol_kernel(const double* __restrict
       if (s_fail && !fail) fail = k * TS + s_fail;
       s_fail = 0;
     }
+    BSTAMP(2);
     lds_inv_block(Ls, Aux);
     __syncthreads();
+    BSTAMP(3);
     if (fac_e) {
       double* dst = fac_e + (int64_t)(2 * k) * TS * TS;
       for (int q = t; q < TS * TS; q += 256) {
@@ -876,6 +897,7 @@ __global__ __launch_bounds__(256) void band_chol_kernel(const double* __restrict
         Gacc = mfma64(v, v, Gacc);
       }
     }
+    BSTAMP(4);
     if (k + 1 == nt) break;
     // C = E_k Linv^T, E_k = triu(B_{k+1,k})
     const double* E = B + (int64_t)(k + 1) * TS * lda + (int64_t)k * TS;
@@ -908,6 +930,7 @@ __global__ __launch_bounds__(256) void band_chol_kernel(const double* __restrict
         for (int r = 0; r < 4; ++r)
           Ls[(wr * 64 + i * 16 + fk + 4 * r) * DL + wc * 64 + j * 16 + fr] = acc[i][j][r];
     __syncthreads();
+    BSTAMP(5);
     if (fac_e) {
       double* dst = fac_e + (int64_t)(2 * k + 1) * TS * TS;
       for (int q = t; q < TS * TS; q += 256) dst[q] = Ls[(q >> 7) * DL + (q & 127)];
@@ -930,6 +953,7 @@ __global__ __launch_bounds__(256) void band_chol_kernel(const double* __restrict
       }
       Rr[slot] = a0;
     }
+    BSTAMP(6);
     // D_{k+1} = B_{k+1,k+1} + eta I - C C^T on the 36 lower 16x16 tiles (9 per wave)
     d4 S[9];
 #pragma unroll
@@ -964,6 +988,8 @@ __global__ __launch_bounds__(256) void band_chol_kernel(const double* __restrict
         Ls[(ti * DB + fk + 4 * rr) * DL + tj * DB + fr] = S[s9][rr];
     }
     __syncthreads();
+    BSTAMP(7);
+    BSTAMP_PRINT();
   }
   __syncthreads();
   d4* sg = reinterpret_cast<d4*>(Ls);

@@ -1,6 +1,9 @@
 """Summarize rocprofv3 --pmc CSV passes per kernel (dev tool).
 
 usage: python tools/pmc_summary.py OUT.json NOTE dir1 [dir2 ...]
+PMC_FIRST=K (environment): also report, per kernel, the mean over its first K
+dispatches of each pass ('per_dispatch_first'), e.g. the timed call of a run
+that makes a second, differently sized call afterwards.
 Each dir holds one pass's *_counter_collection.csv. Per kernel name (template
 and argument list stripped) it reports dispatch count, the summed counter
 values and the per-dispatch mean; FETCH_SIZE / WRITE_SIZE are in KB as
@@ -28,6 +31,8 @@ def main():
     out, note, dirs = sys.argv[1], sys.argv[2], sys.argv[3:]
     acc = defaultdict(lambda: defaultdict(float))
     disp = defaultdict(set)
+    first_k = int(os.environ.get('PMC_FIRST', '0'))
+    rows_by = defaultdict(lambda: defaultdict(lambda: defaultdict(float)))
     for d in dirs:
         for f in glob.glob(os.path.join(d, '*counter_collection.csv')):
             with open(f) as fh:
@@ -35,12 +40,23 @@ def main():
                     k = short(row['Kernel_Name'])
                     acc[k][row['Counter_Name']] += float(row['Counter_Value'])
                     disp[k].add((f, row['Dispatch_Id']))
+                    rows_by[(f, k)][int(row['Dispatch_Id'])][row['Counter_Name']] += \
+                        float(row['Counter_Value'])
+    first = defaultdict(lambda: defaultdict(float))
+    if first_k:
+        for (f, k), by in rows_by.items():
+            for did in sorted(by)[:first_k]:
+                for c, v in by[did].items():
+                    first[k][c] += v / first_k
     res = {'note': note, 'kernels': {}}
     for k, cs in acc.items():
         nd = max(1, len(disp[k]) // max(1, len(dirs)))
         res['kernels'][k] = {'dispatches': nd,
                              'sum': {c: v for c, v in sorted(cs.items())},
                              'per_dispatch': {c: v / nd for c, v in sorted(cs.items())}}
+        if first_k and k in first:
+            res['kernels'][k]['first_dispatches'] = first_k
+            res['kernels'][k]['per_dispatch_first'] = dict(sorted(first[k].items()))
     times = defaultdict(float)
     for d in dirs:
         for f in glob.glob(os.path.join(d, '*kernel_trace.csv')):
