@@ -768,6 +768,85 @@ __global__ __launch_bounds__(256) void qt_apply_kernel(const double* __restrict_
   for (int q = 0; q < 4; ++q) Y[(int64_t)i * RLD + c4 + q] -= s[q];
 }
 
+// Tile row I of the subdiagonal factor block C = E Linv^T (band_chol_kernel):
+// E = triu(B_{k+1,k}) (global) and Linv^T are upper triangular, so C is, and
+// tile (I, j), j >= I, sums only the k-tiles q = I..j (120 of the 512 tile
+// products of a full 128^3 product). The wave's E fragments of row I are all
+// loaded first (one batch of global loads), Linv is read from LDS.
+template <int I>
+__device__ __forceinline__ void c_row(const double* __restrict__ E, int64_t lda, const double* Ls,
+                                      d4 (&Ct)[NDB - I], int fr, int fk) {
+  double ef[NDB - I][4];
+#pragma unroll
+  for (int q = I; q < NDB; ++q)
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int r = I * DB + fr, qk = q * DB + 4 * kk + fk;
+      ef[q - I][kk] = (q > I || r <= qk) ? E[(int64_t)r * lda + qk] : 0.0;
+    }
+#pragma unroll
+  for (int j = I; j < NDB; ++j) {
+    d4 a0 = {0.0, 0.0, 0.0, 0.0}, a1 = {0.0, 0.0, 0.0, 0.0};
+    const int c = j * DB + fr;
+#pragma unroll
+    for (int q = I; q <= j; ++q)
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const int qk = q * DB + 4 * kk + fk;
+        const double bv = (q < j || qk <= c) ? Ls[c * DL + qk] : 0.0;
+        if (kk & 1) a1 = mfma64(ef[q - I][kk], bv, a1);
+        else a0 = mfma64(ef[q - I][kk], bv, a0);
+      }
+    Ct[j - I] = a0 + a1;
+  }
+}
+
+// Row I of C into Ls (zeros left of the diagonal tile).
+template <int I>
+__device__ __forceinline__ void c_store(double* Ls, const d4 (&Ct)[NDB - I], int fr, int fk) {
+#pragma unroll
+  for (int j = 0; j < NDB; ++j)
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr)
+      Ls[(I * DB + fk + 4 * rr) * DL + j * DB + fr] = (j < I) ? 0.0 : Ct[j - I < 0 ? 0 : j - I][rr];
+}
+
+// Ls (Linv) <- C = E Linv^T. Tile rows per wave {0}, {1,6}, {2,5}, {3,4,7}:
+// 36 / 31 / 27 / 26 tile products. Ends with a workgroup barrier.
+__device__ __forceinline__ void c_rows(const double* __restrict__ E, int64_t lda, double* Ls,
+                                       int w, int fr, int fk) {
+  if (w == 0) {
+    d4 C0[8];
+    c_row<0>(E, lda, Ls, C0, fr, fk);
+    __syncthreads();   // every wave is done with Linv
+    c_store<0>(Ls, C0, fr, fk);
+  } else if (w == 1) {
+    d4 C1[7], C6[2];
+    c_row<1>(E, lda, Ls, C1, fr, fk);
+    c_row<6>(E, lda, Ls, C6, fr, fk);
+    __syncthreads();
+    c_store<1>(Ls, C1, fr, fk);
+    c_store<6>(Ls, C6, fr, fk);
+  } else if (w == 2) {
+    d4 C2[6], C5[3];
+    c_row<2>(E, lda, Ls, C2, fr, fk);
+    c_row<5>(E, lda, Ls, C5, fr, fk);
+    __syncthreads();
+    c_store<2>(Ls, C2, fr, fk);
+    c_store<5>(Ls, C5, fr, fk);
+  } else {
+    d4 C3[5], C4[4], C7[1];
+    c_row<3>(E, lda, Ls, C3, fr, fk);
+    c_row<4>(E, lda, Ls, C4, fr, fk);
+    c_row<7>(E, lda, Ls, C7, fr, fk);
+    __syncthreads();
+    c_store<3>(Ls, C3, fr, fk);
+    c_store<4>(Ls, C4, fr, fk);
+    c_store<7>(Ls, C7, fr, fk);
+  }
+  __syncthreads();
+}
+
 // ---------------------------------------------------------------------------
 // Banded Cholesky of B + eta I per workgroup (eta = etas[blockIdx.x]) with the
 // forward substitution of Y, logdet and Gram. B = the reduced matrix: diagonal
@@ -789,7 +868,7 @@ __global__ __launch_bounds__(256) void band_chol_kernel(const double* __restrict
   __shared__ double sred[2];
   __shared__ int s_fail;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int wr = w >> 1, wc = w & 1, fr = lane & 15, fk = lane >> 4;
+  const int fr = lane & 15, fk = lane >> 4;
   const int e = blockIdx.x;
   const double eta = etas[e];
 #if GPMI_BAND_STAMPS
@@ -899,37 +978,9 @@ __global__ __launch_bounds__(256) void band_chol_kernel(const double* __restrict
     }
     BSTAMP(4);
     if (k + 1 == nt) break;
-    // C = E_k Linv^T, E_k = triu(B_{k+1,k})
-    const double* E = B + (int64_t)(k + 1) * TS * lda + (int64_t)k * TS;
-    d4 acc[4][4];
-    zero_tile(acc);
-    for (int kq = 0; kq < TS / 4; ++kq) {
-      const int qk = kq * 4 + fk;
-      double a[4], b[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int r = wr * 64 + i * 16 + fr;
-        a[i] = (r <= qk) ? E[(int64_t)r * lda + qk] : 0.0;
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int c = wc * 64 + j * 16 + fr;
-        b[j] = (qk <= c) ? Ls[c * DL + qk] : 0.0;
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = mfma64(a[i], b[j], acc[i][j]);
-    }
-    __syncthreads();   // every wave is done with Linv
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          Ls[(wr * 64 + i * 16 + fk + 4 * r) * DL + wc * 64 + j * 16 + fr] = acc[i][j][r];
-    __syncthreads();
+    // C = E_k Linv^T, E_k = triu(B_{k+1,k}): upper triangular, like both factors
+    // (tile rows per wave: c_rows)
+    c_rows(B + (int64_t)(k + 1) * TS * lda + (int64_t)k * TS, lda, Ls, w, fr, fk);
     BSTAMP(5);
     if (fac_e) {
       double* dst = fac_e + (int64_t)(2 * k + 1) * TS * TS;
@@ -943,7 +994,7 @@ __global__ __launch_bounds__(256) void band_chol_kernel(const double* __restrict
       d4 a0;
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) a0[rr] = Y[(g1 + ti * DB + fk + 4 * rr) * RLD + fr];
-      for (int kt = 0; kt < NDB; ++kt) {
+      for (int kt = ti; kt < NDB; ++kt) {   // C upper triangular
 #pragma unroll
         for (int kk = 0; kk < 4; ++kk) {
           const double av = -Ls[(ti * DB + fr) * DL + kt * DB + 4 * kk + fk];
@@ -969,7 +1020,7 @@ __global__ __launch_bounds__(256) void band_chol_kernel(const double* __restrict
         const int r = r0 + fk + 4 * rr, c = c0 + fr;
         a[rr] = B[(g1 + r) * lda + g1 + c] + (r == c ? eta : 0.0);
       }
-      for (int kq = 0; kq < TS / 4; ++kq) {
+      for (int kq = 4 * ti; kq < TS / 4; ++kq) {   // C rows of tile ti: columns >= r0
         const double av = -Ls[(r0 + fr) * DL + 4 * kq + fk];
         const double bv = Ls[(c0 + fr) * DL + 4 * kq + fk];
         a = mfma64(av, bv, a);
@@ -1032,18 +1083,18 @@ __device__ __forceinline__ void block_to_ls(const double* __restrict__ src, doub
 }
 
 // out[slot] (rows ti * 16 + fk + 4 rr, column fr) = sum_k op(M)[row][k] V[k][fr];
-// op(M) = M or M^T of the 128 x 128 block in Ls; LOWER: M is lower triangular.
-template <bool TRANS, bool LOWER>
+// op(M) = M or M^T of the 128 x 128 block in Ls; M lower (Linv) or upper (C)
+// triangular: only the nonzero k-tiles are summed.
+constexpr int TRI_LOWER = 1, TRI_UPPER = 2;
+template <bool TRANS, int TRI>
 __device__ __forceinline__ void ls_mm(const double* Ls, const double* V, d4 (&out)[2]) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, fr = lane & 15, fk = lane >> 4;
 #pragma unroll
   for (int slot = 0; slot < 2; ++slot) {
     const int ti = slot == 0 ? w : NDB - 1 - w;
     int k0 = 0, k1 = NDB;
-    if (LOWER) {
-      if (TRANS) k0 = ti;
-      else k1 = ti + 1;
-    }
+    if ((TRI == TRI_LOWER) == TRANS) k0 = ti;
+    else k1 = ti + 1;
     d4 a0 = {0.0, 0.0, 0.0, 0.0}, a1 = {0.0, 0.0, 0.0, 0.0};
     for (int kt = k0; kt < k1; ++kt) {
 #pragma unroll
@@ -1122,7 +1173,7 @@ __global__ __launch_bounds__(256) void band_der_kernel(const double* __restrict_
     if (k + 1 < nt) {
       block_to_ls(fe + (int64_t)(2 * k + 1) * TS * TS, Ls);
       __syncthreads();
-      ls_mm<true, false>(Ls, Aux, p);
+      ls_mm<true, TRI_UPPER>(Ls, Aux, p);   // C_k^T x_{k+1}
 #pragma unroll
       for (int q = 0; q < 2; ++q) v[q] -= p[q];
     }
@@ -1130,7 +1181,7 @@ __global__ __launch_bounds__(256) void band_der_kernel(const double* __restrict_
     slots_to_aux(v, Aux);
     block_to_ls(fe + (int64_t)(2 * k) * TS * TS, Ls);
     __syncthreads();
-    ls_mm<true, true>(Ls, Aux, p);
+    ls_mm<true, TRI_LOWER>(Ls, Aux, p);
     __syncthreads();
     slots_to_aux(p, Aux);
     __syncthreads();
@@ -1144,7 +1195,7 @@ __global__ __launch_bounds__(256) void band_der_kernel(const double* __restrict_
     if (k > 0) {
       block_to_ls(fe + (int64_t)(2 * k - 1) * TS * TS, Ls);
       __syncthreads();
-      ls_mm<false, false>(Ls, Aux, p);
+      ls_mm<false, TRI_UPPER>(Ls, Aux, p);   // C_{k-1} u_{k-1}
 #pragma unroll
       for (int q = 0; q < 2; ++q) v[q] -= p[q];
     }
@@ -1152,7 +1203,7 @@ __global__ __launch_bounds__(256) void band_der_kernel(const double* __restrict_
     slots_to_aux(v, Aux);
     block_to_ls(fe + (int64_t)(2 * k) * TS * TS, Ls);
     __syncthreads();
-    ls_mm<false, true>(Ls, Aux, p);
+    ls_mm<false, TRI_LOWER>(Ls, Aux, p);
     __syncthreads();
     slots_to_aux(p, Aux);
     __syncthreads();
