@@ -906,6 +906,24 @@ __global__ __launch_bounds__(256) void band_chol_kernel(const double* __restrict
   __syncthreads();
   for (int k = 0; k < nt; ++k) {
     BSTAMP(0);
+    // B_{k+1,k+1} + eta I on this wave's 9 lower 16x16 tiles, loaded now so the
+    // loads complete during the block factorization (the D update below)
+    const int64_t g1 = (int64_t)(k + 1) * TS;
+    d4 S[9];
+    if (k + 1 < nt) {
+#pragma unroll
+      for (int s9 = 0; s9 < 9; ++s9) {
+        const int qt = w + 4 * s9;
+        int ti = 0;
+        while ((ti + 1) * (ti + 2) / 2 <= qt) ++ti;
+        const int tj = qt - ti * (ti + 1) / 2;
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          const int r = ti * DB + fk + 4 * rr, c = tj * DB + fr;
+          S[s9][rr] = B[(g1 + r) * lda + g1 + c] + (r == c ? eta : 0.0);
+        }
+      }
+    }
     lds_chol_block(Ls, Aux, sdiag, &s_fail);
     BSTAMP(1);
     if (w < 2) {
@@ -987,7 +1005,6 @@ __global__ __launch_bounds__(256) void band_chol_kernel(const double* __restrict
       for (int q = t; q < TS * TS; q += 256) dst[q] = Ls[(q >> 7) * DL + (q & 127)];
     }
     // r_{k+1} = Y_{k+1} - C y_k
-    const int64_t g1 = (int64_t)(k + 1) * TS;
 #pragma unroll
     for (int slot = 0; slot < 2; ++slot) {
       const int ti = slot == 0 ? w : NDB - 1 - w;
@@ -1006,7 +1023,6 @@ __global__ __launch_bounds__(256) void band_chol_kernel(const double* __restrict
     }
     BSTAMP(6);
     // D_{k+1} = B_{k+1,k+1} + eta I - C C^T on the 36 lower 16x16 tiles (9 per wave)
-    d4 S[9];
 #pragma unroll
     for (int s9 = 0; s9 < 9; ++s9) {
       const int qt = w + 4 * s9;
@@ -1014,12 +1030,7 @@ __global__ __launch_bounds__(256) void band_chol_kernel(const double* __restrict
       while ((ti + 1) * (ti + 2) / 2 <= qt) ++ti;
       const int tj = qt - ti * (ti + 1) / 2;
       const int r0 = ti * DB, c0 = tj * DB;
-      d4 a;
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        const int r = r0 + fk + 4 * rr, c = c0 + fr;
-        a[rr] = B[(g1 + r) * lda + g1 + c] + (r == c ? eta : 0.0);
-      }
+      d4 a = S[s9];
       for (int kq = 4 * ti; kq < TS / 4; ++kq) {   // C rows of tile ti: columns >= r0
         const double av = -Ls[(r0 + fr) * DL + 4 * kq + fk];
         const double bv = Ls[(c0 + fr) * DL + 4 * kq + fk];

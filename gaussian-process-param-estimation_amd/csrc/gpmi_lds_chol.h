@@ -32,6 +32,39 @@ __device__ __forceinline__ double readlane_d(double v, int lane) {
   return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
 
+#ifndef GPMI_F1_LDS
+#define GPMI_F1_LDS 1   // 16x16 factor: DPP quad broadcast + LDS line (0: ds_bpermute shuffles)
+#endif
+
+// v broadcast from lane SG of each quad (DPP quad_perm [SG,SG,SG,SG], VALU only).
+template <int SG>
+__device__ __forceinline__ double quad_bcast(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_mov_dpp((int)(b & 0xffffffffLL), SG * 0x55, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), SG * 0x55, 0xF, 0xF, false);
+  return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) |
+                                          (unsigned)lo));
+}
+
+// Lanes of one wave exchanging values through LDS: the write must stay before the
+// read (the compiler, reasoning per lane, could otherwise forward or hoist). LDS
+// executes one wave's instructions in order, so no s_barrier is needed.
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// sg known after unrolling: the switch folds to one DPP pair
+__device__ __forceinline__ double quad_bcast_sel(double v, int sg) {
+  switch (sg) {
+    case 0: return quad_bcast<0>(v);
+    case 1: return quad_bcast<1>(v);
+    case 2: return quad_bcast<2>(v);
+    default: return quad_bcast<3>(v);
+  }
+}
+
 // 1/sqrt(d) to double precision: hardware estimate + two Newton steps.
 __device__ __forceinline__ double rsqrt_nr(double d) {
   double r = __builtin_amdgcn_rsq(d);
@@ -80,77 +113,134 @@ __device__ __forceinline__ void store_colblock(double* Ls, const d4 (&Xc)[NDB - 
 }
 
 
+// F1 of block jb (wave 0): factor the 16x16 diagonal block in registers and
+// invert it into Aux[jb][16][16]; diag(L) to sdiag, first bad pivot to *s_fail.
+__device__ __forceinline__ void f1_factor(double* Ls, double* Aux, double* sdiag, int* s_fail,
+                                          int jb, double* colbuf) {
+  const int lane = threadIdx.x & 63;
+  const int j0 = jb * DB;
+    const int r = lane >> 2, g = lane & 3;
+    double a[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) a[k] = Ls[(j0 + r) * DL + j0 + 4 * g + k];
+    double myrinv = 0.0;
+#pragma unroll
+    for (int j = 0; j < DB; ++j) {
+      const int sk = j & 3, sg = j >> 2;
+      const double d = readlane_d(a[sk], (j << 2) | sg);
+#if GPMI_F1_LDS
+      // column j: A[r][j] to every lane of quad r by DPP; the column through a
+      // 16-double LDS line (one wave: LDS order, no barrier) overlaps the rsq chain
+      const double crj = quad_bcast_sel(a[sk], sg);
+      if (g == 0) colbuf[r] = crj;
+      wave_lds_sync();
+      double lcj[4];
+      {
+        const d2 c01 = *reinterpret_cast<const d2*>(&colbuf[4 * g]);
+        const d2 c23 = *reinterpret_cast<const d2*>(&colbuf[4 * g + 2]);
+        lcj[0] = c01[0]; lcj[1] = c01[1]; lcj[2] = c23[0]; lcj[3] = c23[1];
+      }
+#else
+      const double crj = __shfl(a[sk], (r << 2) | sg);
+      double lcj[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) lcj[k] = __shfl(a[sk], ((4 * g + k) << 2) | sg);
+#endif
+      const double rinv = rsqrt_nr(d);
+      const double ljj = d * rinv;
+      if (lane == 0) {
+        if (!(d > 0.0) && *s_fail == 0) *s_fail = j0 + j + 1;
+        sdiag[j0 + j] = ljj;
+      }
+      if (r == j) myrinv = rinv;
+      const double lrj = (r > j) ? crj * rinv : ((r == j) ? ljj : 0.0);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int c = 4 * g + k;
+        if (c > j && c <= r) a[k] -= lrj * (lcj[k] * rinv);
+      }
+      if (g == sg) a[sk] = lrj;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) Ls[(j0 + r) * DL + j0 + 4 * g + k] = a[k];
+    // X = inv(L_jj): row p of X is final once the rows above it are.
+    double lrow[DB];   // L[r][p], p = 0..15
+#pragma unroll
+    for (int p = 0; p < DB; ++p) lrow[p] = __shfl(a[p & 3], (r << 2) | (p >> 2));
+    double s[4] = {0.0, 0.0, 0.0, 0.0}, x[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int p = 0; p < DB; ++p) {
+      if (r == p) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) x[k] = (((4 * g + k) == p ? 1.0 : 0.0) - s[k]) * myrinv;
+      }
+      double xp[4];
+#if GPMI_F1_LDS
+      // row p of X through the LDS line (the four lanes of quad p write it)
+      if (r == p) {
+        *reinterpret_cast<d2*>(&colbuf[4 * g]) = d2{x[0], x[1]};
+        *reinterpret_cast<d2*>(&colbuf[4 * g + 2]) = d2{x[2], x[3]};
+      }
+      wave_lds_sync();
+      {
+        const d2 c01 = *reinterpret_cast<const d2*>(&colbuf[4 * g]);
+        const d2 c23 = *reinterpret_cast<const d2*>(&colbuf[4 * g + 2]);
+        xp[0] = c01[0]; xp[1] = c01[1]; xp[2] = c23[0]; xp[3] = c23[1];
+      }
+#else
+#pragma unroll
+      for (int k = 0; k < 4; ++k) xp[k] = __shfl(x[k], (p << 2) | g);
+#endif
+      if (r > p) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) s[k] += lrow[p] * xp[k];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) Aux[jb * 256 + r * 16 + 4 * g + k] = x[k];
+}
+
+// F3 tile q of the trailing update after block jb: (ti, tj), jb < tj <= ti < 8, K = 16.
+__device__ __forceinline__ void f3_tile(double* Ls, int jb, int q, int fr, int fk) {
+  const int j0 = jb * DB;
+  int ti = 0;
+  while ((ti + 1) * (ti + 2) / 2 <= q) ++ti;
+  const int tj = q - ti * (ti + 1) / 2;
+  const int r0 = (jb + 1 + ti) * DB, c0 = (jb + 1 + tj) * DB;
+  d4 acc;
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) acc[rr] = Ls[(r0 + fk + 4 * rr) * DL + c0 + fr];
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk) {
+    const double av = -Ls[(r0 + fr) * DL + j0 + 4 * kk + fk];
+    const double bv = Ls[(c0 + fr) * DL + j0 + 4 * kk + fk];
+    acc = mfma64(av, bv, acc);
+  }
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) Ls[(r0 + fk + 4 * rr) * DL + c0 + fr] = acc[rr];
+}
+
+// Blocked by 16 with a look-ahead: wave 0 updates trailing tile 0 (the next
+// diagonal block) and factors it (F1 of jb + 1) while waves 1-3 update the other
+// trailing tiles, so F3 hides behind the F1 chain. The two lanes of an F2 row are
+// in one wave (LDS order: both read the row before either writes it).
 __device__ __forceinline__ void lds_chol_block(double* Ls, double* Aux, double* sdiag,
                                                int* s_fail) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int fr = lane & 15, fk = lane >> 4;
+  __shared__ __attribute__((aligned(16))) double colbuf[DB];   // F1 broadcast line (wave 0)
+  if (w == 0) f1_factor(Ls, Aux, sdiag, s_fail, 0, colbuf);
   for (int jb = 0; jb < NDB; ++jb) {
     const int j0 = jb * DB;
-    // ---- F1: factor and invert the 16x16 diagonal block in registers (wave 0)
-    if (w == 0) {
-      const int r = lane >> 2, g = lane & 3;
-      double a[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) a[k] = Ls[(j0 + r) * DL + j0 + 4 * g + k];
-      double myrinv = 0.0;
-#pragma unroll
-      for (int j = 0; j < DB; ++j) {
-        const int sk = j & 3, sg = j >> 2;
-        const double d = readlane_d(a[sk], (j << 2) | sg);
-        const double crj = __shfl(a[sk], (r << 2) | sg);
-        double lcj[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) lcj[k] = __shfl(a[sk], ((4 * g + k) << 2) | sg);
-        const double rinv = rsqrt_nr(d);
-        const double ljj = d * rinv;
-        if (lane == 0) {
-          if (!(d > 0.0) && *s_fail == 0) *s_fail = j0 + j + 1;
-          sdiag[j0 + j] = ljj;
-        }
-        if (r == j) myrinv = rinv;
-        const double lrj = (r > j) ? crj * rinv : ((r == j) ? ljj : 0.0);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int c = 4 * g + k;
-          if (c > j && c <= r) a[k] -= lrj * (lcj[k] * rinv);
-        }
-        if (g == sg) a[sk] = lrj;
-      }
-#pragma unroll
-      for (int k = 0; k < 4; ++k) Ls[(j0 + r) * DL + j0 + 4 * g + k] = a[k];
-      // X = inv(L_jj): row p of X is final once the rows above it are.
-      double lrow[DB];   // L[r][p], p = 0..15
-#pragma unroll
-      for (int p = 0; p < DB; ++p) lrow[p] = __shfl(a[p & 3], (r << 2) | (p >> 2));
-      double s[4] = {0.0, 0.0, 0.0, 0.0}, x[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-      for (int p = 0; p < DB; ++p) {
-        if (r == p) {
-#pragma unroll
-          for (int k = 0; k < 4; ++k) x[k] = (((4 * g + k) == p ? 1.0 : 0.0) - s[k]) * myrinv;
-        }
-        double xp[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) xp[k] = __shfl(x[k], (p << 2) | g);
-        if (r > p) {
-#pragma unroll
-          for (int k = 0; k < 4; ++k) s[k] += lrow[p] * xp[k];
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < 4; ++k) Aux[jb * 256 + r * 16 + 4 * g + k] = x[k];
-    }
-    __syncthreads();
+    __syncthreads();   // F1 of jb done
     // ---- F2: panel rows below: L[i][j0 + c] = sum_p A[i][j0 + p] X[c][p]
     {
       const int row = j0 + DB + (t >> 1), h = t & 1;
-      double av[DB];
       if (row < TS) {
+        double av[DB];
 #pragma unroll
         for (int p = 0; p < DB; ++p) av[p] = Ls[row * DL + j0 + p];
-      }
-      __syncthreads();
-      if (row < TS) {
+        wave_lds_sync();   // both lanes of the row read it before either writes
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
           const double* xr = &Aux[jb * 256 + (8 * h + c) * 16];
@@ -162,30 +252,20 @@ __device__ __forceinline__ void lds_chol_block(double* Ls, double* Aux, double* 
       }
     }
     __syncthreads();
-    // ---- F3: trailing update of tiles (ti, tj), jb < tj <= ti < 8, K = 16 (MFMA)
-    {
-      const int m = NDB - 1 - jb;               // trailing tiles per side
-      const int ntile = m * (m + 1) / 2;
-      for (int q = w; q < ntile; q += 4) {
-        int ti = 0;
-        while ((ti + 1) * (ti + 2) / 2 <= q) ++ti;
-        const int tj = q - ti * (ti + 1) / 2;
-        const int r0 = (jb + 1 + ti) * DB, c0 = (jb + 1 + tj) * DB;
-        d4 acc;
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) acc[rr] = Ls[(r0 + fk + 4 * rr) * DL + c0 + fr];
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) {
-          const double av = -Ls[(r0 + fr) * DL + j0 + 4 * kk + fk];
-          const double bv = Ls[(c0 + fr) * DL + j0 + 4 * kk + fk];
-          acc = mfma64(av, bv, acc);
-        }
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) Ls[(r0 + fk + 4 * rr) * DL + c0 + fr] = acc[rr];
+    // ---- F3 (+ F1 of jb + 1 on wave 0)
+    const int m = NDB - 1 - jb;               // trailing tiles per side
+    const int ntile = m * (m + 1) / 2;
+    if (w == 0) {
+      if (ntile > 0) {
+        f3_tile(Ls, jb, 0, fr, fk);
+        wave_lds_sync();   // the tile written by other lanes of this wave
+        f1_factor(Ls, Aux, sdiag, s_fail, jb + 1, colbuf);
       }
+    } else {
+      for (int q = w; q < ntile; q += 3) f3_tile(Ls, jb, q, fr, fk);
     }
-    __syncthreads();
   }
+  __syncthreads();
 }
 
 __device__ __forceinline__ void lds_inv_block(double* Ls, const double* Aux) {
