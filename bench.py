@@ -2,8 +2,10 @@
 """Benchmark: log-likelihood evaluations / s on the N=16384 dense Matérn-3/2
 covariance (BASELINE.json metric), one process per GPU.
 
-A step = one block of ``--eta-per-rank`` eta values of the 64-point grid
-logspace(-3, 3, 64) per rank: one batched device call factorizes
+A step = one block of ``--eta-per-rank`` (64) eta values per rank of the grid
+logspace(-3, 3, max(64, N * 64)) (at N=1 exactly the 64-point cfg3 curve; at
+N > 1 a finer grid over the same range, no eta repeated across ranks): one
+batched device call factorizes
 K + eta_b I (fp64 MFMA Cholesky, fused forward solve of [X | z], logdet and
 Gram), the host forms the direct log-likelihood (sigma = 1, sigma0 = sqrt(eta)),
 and ONE all-gather (RCCL over xGMI at N > 1) collects the [logdet, lp] curve.
@@ -260,7 +262,7 @@ def band_mode(args, D, X, z, world, rank, dist, torch, ld_ref=None):
     from gaussian_proc._likelihood._direct_likelihood import _lp_from_terms
     n, m = X.shape
     E = args.band_etas
-    grid = numpy.logspace(-3, 3, 64)
+    grid = numpy.logspace(-3, 3, max(64, world * E))
     op = MixedCorrelation(D, imate_method='eigenvalue')
     b = op.band()
     acc = {'reduce_ms': 0.0, 'rhs_ms': 0.0, 'loglik_ms': 0.0}
