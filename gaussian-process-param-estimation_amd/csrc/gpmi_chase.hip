@@ -14,11 +14,11 @@
 //   reflector H (LAPACK dlarfg) from A[J_0, s] (k = 0) or from the first column
 //   c = s + 1 + (k - 1) b of the bulge block F = A[J_k, J_{k-1}] (k >= 1);
 //   F <- H F, D = A[J_k, J_k] <- H D H (symmetric rank-2 form on the lower
-//   triangle, D staged whole in LDS), E = A[J_{k+1}, J_k] <- E H.
+//   triangle), E = A[J_{k+1}, J_k] <- E H.
 // The matrix is a dense n_pad x n_pad lower-triangle copy of B; every access is
-// within 2b of the diagonal. The three blocks (F, D, E) are loaded into
-// registers at the start (all 16-byte loads of the task in flight together),
-// staged through LDS only for the matrix-vector products, and written back whole.
+// within 2b of the diagonal. The three blocks (F, D, E) are loaded at the start
+// (all 16-byte loads of the task in flight together; F parked in LDS), the three
+// matrix-vector products taken in one pass, and the blocks written back whole.
 //
 // bisect_kernel: thread i finds the i-th smallest eigenvalue of the symmetric
 // tridiagonal (d, e) by bisection on the Sturm count (LDL^T pivots of T - x I,
@@ -35,17 +35,6 @@
 namespace gpmi {
 
 constexpr int CB = GPMI_TS;        // band width of B = 128
-constexpr int CLD = CB + 1;        // LDS row stride of the staged diagonal block
-
-__device__ __forceinline__ double block_sum(double v, double* red) {
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-  __syncthreads();
-  if (lane == 0) red[w] = v;
-  __syncthreads();
-  return (red[0] + red[1]) + (red[2] + red[3]);
-}
 
 constexpr int CT = 512;             // chase workgroup: 8 waves
 constexpr int CPT = CB * CB / 2 / CT;   // 16-byte pairs per thread per 128 x 128 block
@@ -79,52 +68,45 @@ __device__ __forceinline__ void load_block(const double* __restrict__ src, int64
   }
 }
 
-__device__ __forceinline__ void block_to_lds(const d2 (&r)[CPT], double* __restrict__ buf) {
-#pragma unroll
-  for (int u = 0; u < CPT; ++u) {
-    const int e = u * CT + threadIdx.x;
-    const int i = e >> 6, c2 = 2 * (e & 63);
-    buf[i * CLD + c2] = r[u][0];
-    buf[i * CLD + c2 + 1] = r[u][1];
+// Butterfly reduce-scatter over 8 values: returns in every lane the 64-lane sum of
+// value index (lane >> 3) & 7 (10 shuffles for 8 sums, fixed order).
+__device__ __forceinline__ double butterfly8(double (&v)[8]) {
+  const int lane = threadIdx.x & 63;
+#define GPMI_BFLY_STEP(O, NN)                                      \
+  {                                                                \
+    const bool up = (lane & (O)) != 0;                             \
+    _Pragma("unroll") for (int q = 0; q < (NN) / 2; ++q) {         \
+      const double keep = up ? v[q + (NN) / 2] : v[q];             \
+      const double send = up ? v[q] : v[q + (NN) / 2];             \
+      v[q] = keep + __shfl_xor(send, (O));                         \
+    }                                                              \
   }
+  GPMI_BFLY_STEP(32, 8)
+  GPMI_BFLY_STEP(16, 4)
+  GPMI_BFLY_STEP(8, 2)
+#undef GPMI_BFLY_STEP
+  double r = v[0];
+  r += __shfl_xor(r, 4);
+  r += __shfl_xor(r, 2);
+  r += __shfl_xor(r, 1);
+  return r;
 }
 
-// out[c] = sum_{j < nj} M[c][j] v[j] (rows c < nr) or, with TRANS, sum_{i < nj}
-// v[i] M[i][c]; 4 partial sums per output (thread (c, h), h = 0..3), reduced in sp.
-template <bool TRANS>
-__device__ __forceinline__ void lds_matvec(const double* __restrict__ buf, int nr, int nj,
-                                           const double* __restrict__ v, double (*sp)[CB]) {
-  const int c = threadIdx.x & 127, h = threadIdx.x >> 7;
-  double acc = 0.0;
-  if (TRANS || c < nr) {
-#pragma unroll 8
-    for (int j = h; j < nj; j += 4) acc += (TRANS ? buf[j * CLD + c] : buf[c * CLD + j]) * v[j];
-  }
-  sp[h][c] = acc;
-}
-
-// out[c] = sum_{j < nj} D[c][j] v[j] for the symmetric D whose lower triangle is
-// in buf (D[c][j] = buf[max(c,j)][min(c,j)]); 4 partial sums per output.
-__device__ __forceinline__ void lds_symv_lower(const double* __restrict__ buf, int nj,
-                                               const double* __restrict__ v, double (*sp)[CB]) {
-  const int c = threadIdx.x & 127, h = threadIdx.x >> 7;
-  double acc = 0.0;
-  if (c < nj) {
-#pragma unroll 8
-    for (int j = h; j < nj; j += 4) acc += (j <= c ? buf[c * CLD + j] : buf[j * CLD + c]) * v[j];
-  }
-  sp[h][c] = acc;
-}
-
+// One chase task with the three products F^T v, D v and E v taken in ONE pass over
+// the blocks held in registers (wave w holds rows 8u + w, lane the columns 2 lane,
+// 2 lane + 1): row sums by butterfly reductions, column sums as per-wave partials
+// in LDS summed in wave order. Only F is parked in LDS (in thread order, to fit the
+// register file); 5 barriers per task.
 __global__ __launch_bounds__(CT) void chase_task_kernel(double* __restrict__ A, int64_t lda,
                                                         int n, int t, int s_hi) {
-  __shared__ double buf[CB * CLD];
   __shared__ double sv[CB];
-  __shared__ double sw[CB];
-  __shared__ double sp[4][CB];
+  __shared__ double cpart[2][8][CB];   // per-wave column partials: F^T v, strict-lower(D)^T v
+  __shared__ double srow[2][CB];       // row sums: lower(D) v, E v
+  __shared__ double sf[CB], sw[CB], sq[CB];
   __shared__ double red[8];
   __shared__ double sx0;
-  const int tid = threadIdx.x;
+  __shared__ d2 fbuf[CPT * CT];        // F (k >= 1) in thread order: frees 64 VGPRs
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int s = s_hi - (int)blockIdx.x;
   const int k = t - 3 * s;
   if (s < 0 || k < 0) return;
@@ -133,10 +115,14 @@ __global__ __launch_bounds__(CT) void chase_task_kernel(double* __restrict__ A, 
   const int r1 = min(r0 + CB, n), L = r1 - r0;
   const int col = (k == 0) ? s : s + 1 + (k - 1) * CB;
   const int e1 = min(r1 + CB, n), LE = e1 - r1;
-  // every load of the task first: x, then the F, D and E blocks into registers
   const double xi = (tid < L) ? A[(int64_t)(r0 + tid) * lda + col] : 0.0;
-  d2 Fr[CPT], Dr[CPT], Er[CPT];
-  if (k >= 1) load_block(A + (int64_t)r0 * lda + col, lda, L, CB, Fr);
+  d2 Dr[CPT], Er[CPT];
+  if (k >= 1) {
+    d2 Fr[CPT];
+    load_block(A + (int64_t)r0 * lda + col, lda, L, CB, Fr);
+#pragma unroll
+    for (int u = 0; u < CPT; ++u) fbuf[u * CT + tid] = Fr[u];   // own slots: no barrier
+  }
   load_block<true>(A + (int64_t)r0 * lda + r0, lda, L, L, Dr);
   if (LE > 0) load_block(A + (int64_t)r1 * lda + r0, lda, LE, L, Er);
   // ---- reflector (LAPACK dlarfg)
@@ -153,71 +139,112 @@ __global__ __launch_bounds__(CT) void chase_task_kernel(double* __restrict__ A, 
   if (tid < CB) sv[tid] = (tid == 0) ? 1.0 : ((tid < L) ? xi * scale : 0.0);
   if (k == 0 && tid < L) A[(int64_t)(r0 + tid) * lda + s] = (tid == 0) ? beta : 0.0;
   if (tau == 0.0) return;   // identity reflector: nothing else changes
-  // ---- F <- H F (k >= 1): w = tau F^T v; column col becomes (beta, 0 ...)
+  __syncthreads();
+  // ---- one pass: D (lower pairs; the pair starting on the diagonal carries an
+  //      unread upper element), E, F
+  const int c0 = 2 * lane;
+  const double vc0 = sv[c0], vc1 = sv[c0 + 1];
+  double dc0 = 0.0, dc1 = 0.0;
+  // row sums in two halves of 8 rows (half the live partials): lane holds row
+  // u = 8 h + ((lane >> 3) & 7) of each
+  double prow[2], qrow[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    double rowv[8];
+#pragma unroll
+    for (int uu = 0; uu < 8; ++uu) {
+      const int u = 8 * h + uu;
+      const int i = 8 * u + w;
+      const double vi = sv[i];
+      const double d0 = (c0 <= i) ? Dr[u][0] : 0.0;
+      const double d1 = (c0 + 1 <= i) ? Dr[u][1] : 0.0;
+      rowv[uu] = d0 * vc0 + d1 * vc1;
+      if (c0 < i) dc0 += d0 * vi;
+      if (c0 + 1 < i) dc1 += d1 * vi;
+    }
+    prow[h] = butterfly8(rowv);
+#pragma unroll
+    for (int uu = 0; uu < 8; ++uu)
+      rowv[uu] = Er[8 * h + uu][0] * vc0 + Er[8 * h + uu][1] * vc1;
+    qrow[h] = butterfly8(rowv);
+  }
+  double fc0 = 0.0, fc1 = 0.0;
   if (k >= 1) {
-    block_to_lds(Fr, buf);
-    __syncthreads();
-    lds_matvec<true>(buf, CB, L, sv, sp);
-    __syncthreads();
-    if (tid < CB) sw[tid] = tau * ((sp[0][tid] + sp[1][tid]) + (sp[2][tid] + sp[3][tid]));
-    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < CPT; ++u) {
+      const double vi = sv[8 * u + w];
+      const d2 f = fbuf[u * CT + tid];
+      fc0 += f[0] * vi;
+      fc1 += f[1] * vi;
+    }
+  }
+  cpart[0][w][c0] = fc0;
+  cpart[0][w][c0 + 1] = fc1;
+  cpart[1][w][c0] = dc0;
+  cpart[1][w][c0 + 1] = dc1;
+  if ((lane & 7) == 0) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int i = 8 * (8 * h + ((lane >> 3) & 7)) + w;
+      srow[0][i] = prow[h];
+      srow[1][i] = qrow[h];
+    }
+  }
+  __syncthreads();
+  double pi = 0.0;
+  if (tid < CB) {
+    double sd = srow[0][tid], sfv = 0.0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      sd += cpart[1][q][tid];
+      sfv += cpart[0][q][tid];
+    }
+    pi = (tid < L) ? tau * sd : 0.0;
+    sf[tid] = tau * sfv;
+    sq[tid] = tau * srow[1][tid];
+  }
+  const double vp = block_sum8((tid < L) ? pi * sv[tid] : 0.0, red);
+  if (tid < CB) sw[tid] = (tid < L) ? pi - 0.5 * tau * vp * sv[tid] : 0.0;
+  __syncthreads();
+  // ---- F <- H F: column col becomes (beta, 0 ...)
+  if (k >= 1) {
 #pragma unroll
     for (int u = 0; u < CPT; ++u) {
       const int e = u * CT + tid;
       const int i = e >> 6, c2 = 2 * (e & 63);
       if (i >= L) continue;
+      const d2 f = fbuf[u * CT + tid];
       d2 o;
-      o[0] = (c2 == 0) ? (i == 0 ? beta : 0.0) : Fr[u][0] - sv[i] * sw[c2];
-      o[1] = Fr[u][1] - sv[i] * sw[c2 + 1];
+      o[0] = (c2 == 0) ? (i == 0 ? beta : 0.0) : f[0] - sv[i] * sf[c2];
+      o[1] = f[1] - sv[i] * sf[c2 + 1];
       *reinterpret_cast<d2*>(A + (int64_t)(r0 + i) * lda + col + c2) = o;
     }
   }
-  // ---- D <- H D H: p = tau D v (D symmetrized from its lower part),
-  //      w = p - tau/2 (v.p) v, D -= v w^T + w v^T
-  __syncthreads();
-  block_to_lds(Dr, buf);
-  __syncthreads();
-  lds_symv_lower(buf, L, sv, sp);
-  __syncthreads();
-  const double pi =
-      (tid < L) ? tau * ((sp[0][tid] + sp[1][tid]) + (sp[2][tid] + sp[3][tid])) : 0.0;
-  const double vp = block_sum8((tid < L) ? pi * sv[tid] : 0.0, red);
-  if (tid < CB) sw[tid] = (tid < L) ? pi - 0.5 * tau * vp * sv[tid] : 0.0;
-  __syncthreads();
-  // the lower triangle back (pairs starting on or left of the diagonal; the
-  // partner above the diagonal lands in the band's never-read upper part)
+  // ---- D <- H D H = D - v w^T - w v^T (lower triangle back)
 #pragma unroll
   for (int u = 0; u < CPT; ++u) {
     const int e = u * CT + tid;
     const int i = e >> 6, c2 = 2 * (e & 63);
     if (i >= L || c2 >= L || c2 > i) continue;
-    const double a0 = Dr[u][0];
-    const double a1 = Dr[u][1];
     d2 o;
-    o[0] = a0 - sv[i] * sw[c2] - sw[i] * sv[c2];
-    o[1] = a1 - sv[i] * sw[c2 + 1] - sw[i] * sv[c2 + 1];
+    o[0] = Dr[u][0] - sv[i] * sw[c2] - sw[i] * sv[c2];
+    o[1] = Dr[u][1] - sv[i] * sw[c2 + 1] - sw[i] * sv[c2 + 1];
     if (c2 + 1 < L) *reinterpret_cast<d2*>(A + (int64_t)(r0 + i) * lda + r0 + c2) = o;
     else A[(int64_t)(r0 + i) * lda + r0 + c2] = o[0];
   }
-  if (LE <= 0) return;
-  // ---- E <- E H: q = tau E v, E -= q v^T
-  __syncthreads();
-  block_to_lds(Er, buf);
-  __syncthreads();
-  lds_matvec<false>(buf, LE, L, sv, sp);
-  __syncthreads();
-  if (tid < CB) sw[tid] = tau * ((sp[0][tid] + sp[1][tid]) + (sp[2][tid] + sp[3][tid]));
-  __syncthreads();
+  // ---- E <- E H = E - q v^T
+  if (LE > 0) {
 #pragma unroll
-  for (int u = 0; u < CPT; ++u) {
-    const int e = u * CT + tid;
-    const int i = e >> 6, c2 = 2 * (e & 63);
-    if (i >= LE || c2 >= L) continue;
-    d2 o;
-    o[0] = Er[u][0] - sw[i] * sv[c2];
-    o[1] = Er[u][1] - sw[i] * sv[c2 + 1];
-    if (c2 + 1 < L) *reinterpret_cast<d2*>(A + (int64_t)(r1 + i) * lda + r0 + c2) = o;
-    else A[(int64_t)(r1 + i) * lda + r0 + c2] = o[0];
+    for (int u = 0; u < CPT; ++u) {
+      const int e = u * CT + tid;
+      const int i = e >> 6, c2 = 2 * (e & 63);
+      if (i >= LE || c2 >= L) continue;
+      d2 o;
+      o[0] = Er[u][0] - sq[i] * sv[c2];
+      o[1] = Er[u][1] - sq[i] * sv[c2 + 1];
+      if (c2 + 1 < L) *reinterpret_cast<d2*>(A + (int64_t)(r1 + i) * lda + r0 + c2) = o;
+      else A[(int64_t)(r1 + i) * lda + r0 + c2] = o[0];
+    }
   }
 }
 
