@@ -300,6 +300,113 @@ __global__ __launch_bounds__(256) void csr_fill_kernel(const double* __restrict_
   }
 }
 
+// ---------------------------------------------------------------------------
+// Cell-list form of the same assembly (d <= 3): points binned in cells of width
+// >= xcut * scale_k per dimension, so every kept pair (scaled distance <= xcut)
+// lies in the same or an adjacent cell. perm = point indices grouped by cell
+// (cell_start[c] .. cell_start[c + 1]), cell[i] = cell of point i, gdim = cells
+// per dimension. One wave per row visits the 3^d neighbour cells: O(n * candidates)
+// instead of O(n^2). The fill pass collects the kept (j, value) pairs of its row
+// in LDS and writes them in ascending j (rank = number of smaller kept j), so the
+// CSR is identical to the brute-force kernels' (same taper_keep, same order).
+// ---------------------------------------------------------------------------
+constexpr int CELL_CAP = 512;   // kept entries per row held by the fill pass
+
+template <typename F>
+__device__ __forceinline__ void for_each_candidate(int64_t row, int d, const int* __restrict__ cell,
+                                                   const int* __restrict__ gdim,
+                                                   const int* __restrict__ cell_start,
+                                                   const int* __restrict__ perm, F&& f) {
+  const int lane = threadIdx.x & 63;
+  int cc[3] = {0, 0, 0};
+  {
+    int c = cell[row];
+    for (int k = 0; k < d; ++k) {
+      cc[k] = c % gdim[k];
+      c /= gdim[k];
+    }
+  }
+  const int nb = (d == 1) ? 3 : (d == 2 ? 9 : 27);
+  for (int o = 0; o < nb; ++o) {
+    int id = 0, mul = 1, oo = o;
+    bool ok = true;
+    for (int k = 0; k < d; ++k) {
+      const int q = cc[k] + (oo % 3) - 1;
+      oo /= 3;
+      ok = ok && q >= 0 && q < gdim[k];
+      id += q * mul;
+      mul *= gdim[k];
+    }
+    if (!ok) continue;   // wave-uniform
+    const int b0 = cell_start[id], b1 = cell_start[id + 1];
+    for (int b = b0; b < b1; b += 64) {
+      const int k = b + lane;
+      f(k < b1 ? perm[k] : -1);
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void csr_cell_count_kernel(
+    const double* __restrict__ points, int64_t n, int d, const double* __restrict__ scale,
+    MaternParams P, double tau, double xcut, const int* __restrict__ cell,
+    const int* __restrict__ gdim, const int* __restrict__ cell_start,
+    const int* __restrict__ perm, int* __restrict__ row_nnz) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= n) return;
+  double pi[GPMI_MAX_DIM];
+#pragma unroll
+  for (int k = 0; k < GPMI_MAX_DIM; ++k) pi[k] = (k < d) ? points[row * d + k] : 0.0;
+  int cnt = 0;
+  for_each_candidate(row, d, cell, gdim, cell_start, perm, [&](int j) {
+    double v = 0.0;
+    const bool keep = (j >= 0) && taper_keep(pi, points, j, d, scale, P, tau, xcut, &v);
+    cnt += __popcll(__ballot(keep));
+  });
+  if (lane == 0) row_nnz[row] = cnt;
+}
+
+__global__ __launch_bounds__(256) void csr_cell_fill_kernel(
+    const double* __restrict__ points, int64_t n, int d, const double* __restrict__ scale,
+    MaternParams P, double tau, double xcut, const int* __restrict__ cell,
+    const int* __restrict__ gdim, const int* __restrict__ cell_start,
+    const int* __restrict__ perm, const int64_t* __restrict__ indptr, int* __restrict__ indices,
+    double* __restrict__ data) {
+  __shared__ int sj[4][CELL_CAP];
+  __shared__ double sv[4][CELL_CAP];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t row = (int64_t)blockIdx.x * 4 + w;
+  if (row >= n) return;
+  double pi[GPMI_MAX_DIM];
+#pragma unroll
+  for (int k = 0; k < GPMI_MAX_DIM; ++k) pi[k] = (k < d) ? points[row * d + k] : 0.0;
+  const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  int cnt = 0;   // the host checked max(row_nnz) <= CELL_CAP
+  for_each_candidate(row, d, cell, gdim, cell_start, perm, [&](int j) {
+    double v = 0.0;
+    const bool keep = (j >= 0) && taper_keep(pi, points, j, d, scale, P, tau, xcut, &v);
+    const unsigned long long m = __ballot(keep);
+    if (keep) {
+      const int pos = cnt + __popcll(m & below);
+      sj[w][pos] = j;
+      sv[w][pos] = v;
+    }
+    cnt += __popcll(m);
+  });
+  // one wave owns sj[w] / sv[w]: LDS order, fences keep the writes before the reads
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const int64_t base = indptr[row];
+  for (int e = lane; e < cnt; e += 64) {
+    const int je = sj[w][e];
+    int rank = 0;
+    for (int f = 0; f < cnt; ++f) rank += sj[w][f] < je;
+    indices[base + rank] = je;
+    data[base + rank] = sv[w][e];
+  }
+}
+
 // Matérn of one scaled distance (host-side threshold / cutoff helper).
 __global__ void matern_eval_kernel(const double* x, int64_t m, MaternParams P, double* out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;

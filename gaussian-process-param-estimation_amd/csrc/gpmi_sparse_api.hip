@@ -8,6 +8,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -22,6 +23,13 @@ __global__ void csr_count_kernel(const double*, int64_t, int, const double*, Mat
 __global__ void csr_fill_kernel(const double*, int64_t, int, const double*, MaternParams, double,
                                 double, const int64_t*, int*, double*);
 __global__ void matern_eval_kernel(const double*, int64_t, MaternParams, double*);
+__global__ void csr_cell_count_kernel(const double*, int64_t, int, const double*, MaternParams,
+                                      double, double, const int*, const int*, const int*,
+                                      const int*, int*);
+__global__ void csr_cell_fill_kernel(const double*, int64_t, int, const double*, MaternParams,
+                                     double, double, const int*, const int*, const int*,
+                                     const int*, const int64_t*, int*, double*);
+constexpr int CELL_CAP_HOST = 512;   // = CELL_CAP (gpmi_matern.hip)
 __global__ void csr_spmm_kernel(const int64_t*, const int*, const double*, int64_t, const double*,
                                 int64_t, double*, int64_t, int, int, double);
 __global__ void col_dot_partial_kernel(const double*, int64_t, const double*, int64_t, int,
@@ -297,12 +305,79 @@ int gpmi_sp_create_matern(int device, const double* points, int64_t n, int d,
   SP_TRY(hipMemcpyAsync(dp, points, sizeof(double) * n * d, hipMemcpyHostToDevice, st));
   SP_TRY(hipMemcpyAsync(ds, scale, sizeof(double) * d, hipMemcpyHostToDevice, st));
   const unsigned grid = (unsigned)((n + 3) / 4);
-  hipLaunchKernelGGL(csr_count_kernel, dim3(grid), dim3(256), 0, st, dp, n, d, ds, P, tau, xcut,
-                     dcnt);
-  SP_LAUNCH("csr_count_kernel");
+  // Cell list (d <= 3): cells of width >= xcut * scale_k, so a kept pair is in the
+  // same or an adjacent cell; coarsened while there are more cells than 4 n.
+  // GPMI_SPARSE_BRUTE=1 forces the all-pairs kernels (A/B and tests).
+  const char* brute_env = std::getenv("GPMI_SPARSE_BRUTE");
+  bool cells = d <= 3 && n < (int64_t)1 << 28 && !(brute_env && std::atoi(brute_env) != 0);
+  int* dcell = nullptr;   // [n] cell of each point, then gdim [d], cell_start, perm
+  int *dgdim = nullptr, *dstart = nullptr, *dperm = nullptr;
+  if (cells) {
+    double pmin[3], pmax[3], wid[3];
+    int64_t G[3] = {1, 1, 1};
+    for (int k = 0; k < d; ++k) {
+      pmin[k] = pmax[k] = points[k];
+      for (int64_t i = 1; i < n; ++i) {
+        pmin[k] = std::min(pmin[k], points[i * d + k]);
+        pmax[k] = std::max(pmax[k], points[i * d + k]);
+      }
+      wid[k] = xcut * std::fabs(scale[k]) * (1.0 + 1e-9);
+      if (!(wid[k] > 0.0) || !std::isfinite(wid[k])) cells = false;
+    }
+    int64_t total = 0;
+    for (int it = 0; cells && it < 64; ++it) {
+      total = 1;
+      for (int k = 0; k < d; ++k) {
+        const double g = std::floor((pmax[k] - pmin[k]) / wid[k]) + 1.0;
+        G[k] = g > 1e9 ? (int64_t)1e9 : (int64_t)g;
+        total = std::min<int64_t>(total * G[k], (int64_t)1 << 40);
+      }
+      if (total <= std::max<int64_t>(4 * n, 1024)) break;
+      for (int k = 0; k < d; ++k) wid[k] *= 2.0;
+    }
+    if (cells && total > std::max<int64_t>(4 * n, 1024)) cells = false;
+    if (cells) {
+      std::vector<int> hcell(n), hstart(total + 1, 0), hperm(n), hg(d);
+      for (int k = 0; k < d; ++k) hg[k] = (int)G[k];
+      for (int64_t i = 0; i < n; ++i) {
+        int64_t c = 0, mul = 1;
+        for (int k = 0; k < d; ++k) {
+          int64_t q = (int64_t)std::floor((points[i * d + k] - pmin[k]) / wid[k]);
+          q = std::min<int64_t>(std::max<int64_t>(q, 0), G[k] - 1);
+          c += q * mul;
+          mul *= G[k];
+        }
+        hcell[i] = (int)c;
+        ++hstart[c + 1];
+      }
+      for (int64_t c = 0; c < total; ++c) hstart[c + 1] += hstart[c];
+      std::vector<int> fillp(hstart.begin(), hstart.end() - 1);
+      for (int64_t i = 0; i < n; ++i) hperm[fillp[hcell[i]]++] = (int)i;   // ascending i per cell
+      SP_TRY(hipMalloc(&dcell, sizeof(int) * (2 * n + d + total + 1)));
+      dgdim = dcell + n;
+      dstart = dgdim + d;
+      dperm = dstart + total + 1;
+      SP_TRY(hipMemcpyAsync(dcell, hcell.data(), sizeof(int) * n, hipMemcpyHostToDevice, st));
+      SP_TRY(hipMemcpyAsync(dgdim, hg.data(), sizeof(int) * d, hipMemcpyHostToDevice, st));
+      SP_TRY(hipMemcpyAsync(dstart, hstart.data(), sizeof(int) * (total + 1),
+                            hipMemcpyHostToDevice, st));
+      SP_TRY(hipMemcpyAsync(dperm, hperm.data(), sizeof(int) * n, hipMemcpyHostToDevice, st));
+      SP_TRY(hipStreamSynchronize(st));   // host vectors go out of scope
+    }
+  }
+  if (cells) {
+    hipLaunchKernelGGL(csr_cell_count_kernel, dim3(grid), dim3(256), 0, st, dp, n, d, ds, P, tau,
+                       xcut, dcell, dgdim, dstart, dperm, dcnt);
+    SP_LAUNCH("csr_cell_count_kernel");
+  } else {
+    hipLaunchKernelGGL(csr_count_kernel, dim3(grid), dim3(256), 0, st, dp, n, d, ds, P, tau, xcut,
+                       dcnt);
+    SP_LAUNCH("csr_count_kernel");
+  }
   std::vector<int> cnt(n);
   SP_TRY(hipMemcpyAsync(cnt.data(), dcnt, sizeof(int) * n, hipMemcpyDeviceToHost, st));
   SP_TRY(hipStreamSynchronize(st));
+  if (cells && *std::max_element(cnt.begin(), cnt.end()) > CELL_CAP_HOST) cells = false;
   std::vector<int64_t> ip(n + 1, 0);
   for (int64_t i = 0; i < n; ++i) ip[i + 1] = ip[i] + cnt[i];
   sp->nnz = ip[n];
@@ -311,10 +386,17 @@ int gpmi_sp_create_matern(int device, const double* points, int64_t n, int d,
   SP_TRY(hipMalloc(&sp->data, sizeof(double) * std::max<int64_t>(1, sp->nnz)));
   SP_TRY(hipMemcpyAsync(sp->indptr, ip.data(), sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice,
                         st));
-  hipLaunchKernelGGL(csr_fill_kernel, dim3(grid), dim3(256), 0, st, dp, n, d, ds, P, tau, xcut,
-                     sp->indptr, sp->indices, sp->data);
-  SP_LAUNCH("csr_fill_kernel");
+  if (cells) {
+    hipLaunchKernelGGL(csr_cell_fill_kernel, dim3(grid), dim3(256), 0, st, dp, n, d, ds, P, tau,
+                       xcut, dcell, dgdim, dstart, dperm, sp->indptr, sp->indices, sp->data);
+    SP_LAUNCH("csr_cell_fill_kernel");
+  } else {   // all pairs (d > 3, or a row holds more than CELL_CAP kept entries)
+    hipLaunchKernelGGL(csr_fill_kernel, dim3(grid), dim3(256), 0, st, dp, n, d, ds, P, tau, xcut,
+                       sp->indptr, sp->indices, sp->data);
+    SP_LAUNCH("csr_fill_kernel");
+  }
   SP_TRY(hipStreamSynchronize(st));
+  if (dcell) SP_TRY(hipFree(dcell));
   SP_TRY(hipFree(dp));
   SP_TRY(hipFree(ds));
   SP_TRY(hipFree(dcnt));

@@ -167,3 +167,20 @@ def test_sparse_likelihood_vs_oracle(gp):
         lp = DirectLikelihood.log_likelihood(z, X, op, False, hp)
         lp_ref = olk.direct_lp(z, X, ref, hp)
         assert abs(lp - lp_ref) < 0.01 * abs(lp_ref) + 1.0
+
+
+@pytest.mark.parametrize('dim,npts,rho,dens', [(1, 3000, 0.01, 1e-2), (2, 2500, 0.02, 5e-3),
+                                               (3, 4096, 0.03, 4e-3)])
+def test_cell_list_assembly_equals_all_pairs(gp, monkeypatch, dim, npts, rho, dens):
+    """The cell-list CSR (default for d <= 3) is bit-identical to the all-pairs
+    kernels on scattered (non-grid) points, ragged cell occupancy included."""
+    rng = numpy.random.RandomState(7 + dim)
+    pts = rng.rand(npts, dim)
+    pts[:7] = pts[0]                     # coincident points share a cell
+    K = gp.generate_correlation(pts, rho, 1.5, grid=False, sparse=True, density=dens)
+    monkeypatch.setenv('GPMI_SPARSE_BRUTE', '1')
+    B = gp.generate_correlation(pts, rho, 1.5, grid=False, sparse=True, density=dens)
+    numpy.testing.assert_array_equal(K.indptr, B.indptr)
+    numpy.testing.assert_array_equal(K.indices, B.indices)
+    numpy.testing.assert_array_equal(K.data, B.data)
+    assert K.nnz > npts
