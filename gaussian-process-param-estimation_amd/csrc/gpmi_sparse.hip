@@ -148,6 +148,36 @@ __global__ __launch_bounds__(256) void col_axpby_kernel(const double* __restrict
   Y[e] = a[c] * X[e] + b[c] * Y[e];
 }
 
+// Lanczos step k scalars on the device (no host round trip): alpha = the two
+// CGS2 passes' projections on V_k, beta = ||W||, a column whose beta falls below
+// 1e-13 max(1, |alpha|) is dead (invariant subspace: padding from then on).
+// Writes alpha/beta[c][k], and the axpby coefficients for V_{k+1} = W / beta
+// (ca/cb) and for the next step's W -= beta V_k (na/nb).
+__global__ void lanczos_scalar_kernel(const double* __restrict__ H1k,
+                                      const double* __restrict__ H2k,
+                                      const double* __restrict__ nrm, int s, int k, int steps,
+                                      int* __restrict__ dead, double* __restrict__ alpha,
+                                      double* __restrict__ beta, double* __restrict__ ca,
+                                      double* __restrict__ cb, double* __restrict__ na,
+                                      double* __restrict__ nb) {
+  const int c = threadIdx.x;
+  if (c >= s) return;
+  if (k == 0) dead[c] = 0;
+  const int dd = dead[c];
+  const double a = dd ? 0.0 : (0.0 + H1k[c]) + H2k[c];
+  double b = dd ? 0.0 : sqrt(fmax(nrm[c], 0.0));
+  if (!dd && !(b > 1e-13 * fmax(1.0, fabs(a)))) {
+    dead[c] = 1;
+    b = 0.0;
+  }
+  alpha[(int64_t)c * steps + k] = a;
+  beta[(int64_t)c * steps + k] = b;
+  ca[c] = b > 0.0 ? 1.0 / b : 0.0;
+  cb[c] = 0.0;
+  na[c] = -b;
+  nb[c] = 1.0;
+}
+
 // Normalised Rademacher probes: V[i][c] = +-1/sqrt(n), bit 63 of
 // splitmix64(seed * G + (c + c0) * H + i) (matches oracle/sparse.py).
 __global__ __launch_bounds__(256) void rademacher_kernel(double* __restrict__ V, int64_t n, int s,

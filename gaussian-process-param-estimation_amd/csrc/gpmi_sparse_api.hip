@@ -40,6 +40,9 @@ __global__ void col_gs_update_kernel(double*, const double*, int64_t, const doub
 __global__ void col_axpby_kernel(const double*, double*, const double*, const double*, int64_t,
                                  int);
 __global__ void rademacher_kernel(double*, int64_t, int, unsigned long long, int, double);
+__global__ void lanczos_scalar_kernel(const double*, const double*, const double*, int, int, int,
+                                      int*, double*, double*, double*, double*, double*,
+                                      double*);
 void launch_ms_dots(const double* B, const double* R, int64_t n, int s, double* partial, int nblk,
                     hipStream_t st);
 __global__ void ms_alpha_kernel(MsState, const double*, int);
@@ -110,6 +113,8 @@ struct gpmi_sp {
   size_t partial_doubles = 0;
   double* small = nullptr;     // coefficient / reduction arrays
   double* msbuf = nullptr;     // multi-shift CG scalar state
+  double* lz = nullptr;        // Lanczos scalars (lanczos_block)
+  size_t lz_doubles = 0;
   size_t msbuf_doubles = 0;
 };
 
@@ -162,72 +167,63 @@ unsigned grid_ns(int64_t n, int s) { return (unsigned)((n * s + 255) / 256); }
 int lanczos_block(gpmi_sp* sp, double* V, double* W, int s, int steps, double* h_alpha,
                   double* h_beta) {
   const int64_t ns = sp->n * s;
-  double* H = sp->small;                 // [(steps+1)][s]
-  double* coefa = sp->small + (size_t)(steps + 2) * MAXS;
-  double* coefb = coefa + MAXS;
-  std::vector<double> hH((size_t)(steps + 1) * s), hnorm(s), ha(s), hb(s);
-  std::vector<double> beta_prev(s, 0.0);
-  std::vector<int> dead(s, 0);
+  // device scalars: H1, H2 [(steps+1)][MAXS] (the two CGS2 passes), norms, the
+  // alpha/beta tables [s][steps], two axpby coefficient pairs and the dead flags
+  const size_t need = (size_t)2 * (steps + 1) * MAXS + MAXS + (size_t)2 * MAXS * steps +
+                      4 * MAXS + MAXS;
+  if (sp->lz_doubles < need) {
+    if (sp->lz) SP_TRY(hipFree(sp->lz));
+    sp->lz = nullptr;
+    SP_TRY(hipMalloc(&sp->lz, sizeof(double) * need));
+    sp->lz_doubles = need;
+  }
+  double* H1 = sp->lz;
+  double* H2 = H1 + (size_t)(steps + 1) * MAXS;
+  double* nrm = H2 + (size_t)(steps + 1) * MAXS;
+  double* dalpha = nrm + MAXS;
+  double* dbeta = dalpha + (size_t)MAXS * steps;
+  double* ca = dbeta + (size_t)MAXS * steps;
+  double* cb = ca + MAXS;
+  double* na = cb + MAXS;
+  double* nb = na + MAXS;
+  int* dead = reinterpret_cast<int*>(nb + MAXS);
   for (int k = 0; k < steps; ++k) {
     double* Vk = V + (int64_t)k * ns;
     int rc = spmm(sp, Vk, W, s, 0.0);
     if (rc) return rc;
-    if (k > 0) {
-      for (int c = 0; c < s; ++c) {
-        ha[c] = -beta_prev[c];
-        hb[c] = 1.0;
-      }
-      SP_TRY(hipMemcpyAsync(coefa, ha.data(), sizeof(double) * s, hipMemcpyHostToDevice,
-                            sp->stream));
-      SP_TRY(hipMemcpyAsync(coefb, hb.data(), sizeof(double) * s, hipMemcpyHostToDevice,
-                            sp->stream));
+    if (k > 0) {   // W -= beta_{k-1} V_{k-1}
       hipLaunchKernelGGL(col_axpby_kernel, dim3(grid_ns(sp->n, s)), dim3(256), 0, sp->stream,
-                         V + (int64_t)(k - 1) * ns, W, coefa, coefb, sp->n, s);
+                         V + (int64_t)(k - 1) * ns, W, na, nb, sp->n, s);
       SP_LAUNCH("col_axpby_kernel");
     }
-    double alpha_sum[MAXS] = {0};
-    for (int pass = 0; pass < 2; ++pass) {
+    for (int pass = 0; pass < 2; ++pass) {   // CGS2 against V_0 .. V_k
+      double* H = pass == 0 ? H1 : H2;
       rc = col_dots(sp, V, ns, k + 1, W, s, H);
       if (rc) return rc;
       hipLaunchKernelGGL(col_gs_update_kernel, dim3(grid_ns(sp->n, s)), dim3(256), 0, sp->stream,
                          W, V, ns, H, k + 1, sp->n, s);
       SP_LAUNCH("col_gs_update_kernel");
-      SP_TRY(hipMemcpyAsync(hH.data(), H + (size_t)k * s, sizeof(double) * s,
-                            hipMemcpyDeviceToHost, sp->stream));
-      SP_TRY(hipStreamSynchronize(sp->stream));
-      for (int c = 0; c < s; ++c) alpha_sum[c] += hH[c];
     }
-    rc = col_dots(sp, W, 0, 1, W, s, H);
+    rc = col_dots(sp, W, 0, 1, W, s, nrm);
     if (rc) return rc;
-    SP_TRY(hipMemcpyAsync(hnorm.data(), H, sizeof(double) * s, hipMemcpyDeviceToHost,
-                          sp->stream));
-    SP_TRY(hipStreamSynchronize(sp->stream));
-    for (int c = 0; c < s; ++c) {
-      const double a = dead[c] ? 0.0 : alpha_sum[c];
-      double b = dead[c] ? 0.0 : std::sqrt(std::max(hnorm[c], 0.0));
-      if (!dead[c] && !(b > 1e-13 * std::max(1.0, std::fabs(a)))) {
-        dead[c] = 1;   // invariant subspace reached: the rest of this column is padding
-        b = 0.0;
-      }
-      h_alpha[(size_t)c * steps + k] = a;
-      h_beta[(size_t)c * steps + k] = b;
-      beta_prev[c] = b;
-      ha[c] = b > 0.0 ? 1.0 / b : 0.0;
-      hb[c] = 0.0;
-    }
+    hipLaunchKernelGGL(lanczos_scalar_kernel, dim3(1), dim3(64), 0, sp->stream,
+                       H1 + (size_t)k * s, H2 + (size_t)k * s, nrm, s, k, steps, dead, dalpha,
+                       dbeta, ca, cb, na, nb);
+    SP_LAUNCH("lanczos_scalar_kernel");
     if (k + 1 < steps) {
       // V_{k+1} = W / beta  (b = 0 -> X * 0 + 0 * Y; Y is zero-initialised below)
       double* Vn = V + (int64_t)(k + 1) * ns;
       SP_TRY(hipMemsetAsync(Vn, 0, sizeof(double) * ns, sp->stream));
-      SP_TRY(hipMemcpyAsync(coefa, ha.data(), sizeof(double) * s, hipMemcpyHostToDevice,
-                            sp->stream));
-      SP_TRY(hipMemcpyAsync(coefb, hb.data(), sizeof(double) * s, hipMemcpyHostToDevice,
-                            sp->stream));
       hipLaunchKernelGGL(col_axpby_kernel, dim3(grid_ns(sp->n, s)), dim3(256), 0, sp->stream, W,
-                         Vn, coefa, coefb, sp->n, s);
+                         Vn, ca, cb, sp->n, s);
       SP_LAUNCH("col_axpby_kernel");
     }
   }
+  SP_TRY(hipMemcpyAsync(h_alpha, dalpha, sizeof(double) * s * steps, hipMemcpyDeviceToHost,
+                        sp->stream));
+  SP_TRY(hipMemcpyAsync(h_beta, dbeta, sizeof(double) * s * steps, hipMemcpyDeviceToHost,
+                        sp->stream));
+  SP_TRY(hipStreamSynchronize(sp->stream));
   return 0;
 }
 
@@ -415,6 +411,7 @@ int gpmi_sp_destroy(gpmi_sp* sp) {
   if (sp->partial) (void)hipFree(sp->partial);
   if (sp->small) (void)hipFree(sp->small);
   if (sp->msbuf) (void)hipFree(sp->msbuf);
+  if (sp->lz) (void)hipFree(sp->lz);
   if (sp->stream) (void)hipStreamDestroy(sp->stream);
   delete sp;
   return 0;
