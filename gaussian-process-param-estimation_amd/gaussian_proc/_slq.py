@@ -37,8 +37,8 @@ def quadrature(node_list, etas, fn):
     """Per-probe sums sum_i tau_i^2 fn(theta_i + eta) -> [nprobe, neta]."""
     etas = numpy.atleast_1d(numpy.asarray(etas, dtype=float))
     q = numpy.empty((len(node_list), etas.size))
-    for p, (theta, w) in enumerate(node_list):
-        q[p] = [numpy.sum(w * fn(theta + e)) for e in etas]
+    for p, (theta, w) in enumerate(node_list):   # all eta of a probe in one array op
+        q[p] = numpy.sum(w[None, :] * fn(theta[None, :] + etas[:, None]), axis=1)
     return q
 
 
