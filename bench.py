@@ -86,6 +86,23 @@ def pmc_traffic(outer, batch, kernel='gpmi::syrk_kernel'):
     return (2.0 * pd['FETCH_SIZE'] + pd['WRITE_SIZE']) * 1024.0, os.path.relpath(files[-1], REPO)
 
 
+def pmc_traffic_sparse(config, kernel='gpmi::csr_spmm_kernel'):
+    """HBM-side bytes per timed SpMM launch from the committed PMC summary of this
+    sparse config (profiles/r*/pmc_traffic_{config}.json, per_dispatch_last = the
+    bench's timed s=20 launches; FETCH_SIZE doubled as in pmc_traffic)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, 'profiles', 'r*',
+                                          'pmc_traffic_%s.json' % config)))
+    if not files:
+        return None, None
+    with open(files[-1]) as fh:
+        k = json.load(fh)['kernels'].get(kernel)
+    if not k or 'per_dispatch_last' not in k:
+        return None, None
+    pd = k['per_dispatch_last']
+    return (2.0 * pd['FETCH_SIZE'] + pd['WRITE_SIZE']) * 1024.0, os.path.relpath(files[-1], REPO)
+
+
 def cpu_baseline(points, z, X, nu, etas):
     """The reference's CPU call pattern, timed on this host (rank 0, N=1):
     Likelihood -> MixedCorrelation(imate_method='eigenvalue') -> per eval
@@ -204,6 +221,7 @@ def run_sparse(args, world, rank, local, dist, torch):
     nnz = op.sop.nnz
     alg_bytes = 12.0 * nnz + 8.0 * (n + 1) + 16.0 * n * s_blk
     gbs = alg_bytes / (ms * 1e-3) / 1e9
+    sp_traffic, sp_tsrc = pmc_traffic_sparse(args.config) if s_blk == 20 else (None, None)
     if rank == 0:
         res = {
             'metric': 'log-likelihood evals/sec (%s, sparse tapered Matern, SLQ + CG)'
@@ -221,7 +239,10 @@ def run_sparse(args, world, rank, local, dist, torch):
                        'assembly_s': t_asm,
                        'parallelism': 'probe + eta shards x%d + all-gather' % world},
             'roofline': {'bound': 'hbm', 'achieved': round(gbs, 1), 'peak': HBM_PEAK_GBS,
-                         'unit': 'GB/s', 'frac': round(gbs / HBM_PEAK_GBS, 4), 'traffic': None,
+                         'unit': 'GB/s', 'frac': round(gbs / HBM_PEAK_GBS, 4),
+                         'traffic': None if sp_traffic is None else round(sp_traffic),
+                         'traffic_unit': 'bytes per launch (HBM side, PMC)',
+                         'traffic_source': sp_tsrc,
                          'kernel': 'csr_spmm_kernel (s=%d columns)' % s_blk,
                          'avg_launch_ms': round(ms, 4),
                          # every nonzero gathers s contiguous doubles of X: cache-side bytes

@@ -48,6 +48,13 @@ def main():
             for did in sorted(by)[:first_k]:
                 for c, v in by[did].items():
                     first[k][c] += v / first_k
+    last_k = int(os.environ.get('PMC_LAST', '0'))   # the same over the last K dispatches
+    last = defaultdict(lambda: defaultdict(float))
+    if last_k:
+        for (f, k), by in rows_by.items():
+            for did in sorted(by)[-last_k:]:
+                for c, v in by[did].items():
+                    last[k][c] += v / last_k
     res = {'note': note, 'kernels': {}}
     for k, cs in acc.items():
         nd = max(1, len(disp[k]) // max(1, len(dirs)))
@@ -57,6 +64,9 @@ def main():
         if first_k and k in first:
             res['kernels'][k]['first_dispatches'] = first_k
             res['kernels'][k]['per_dispatch_first'] = dict(sorted(first[k].items()))
+        if last_k and k in last:
+            res['kernels'][k]['last_dispatches'] = last_k
+            res['kernels'][k]['per_dispatch_last'] = dict(sorted(last[k].items()))
     times = defaultdict(float)
     for d in dirs:
         for f in glob.glob(os.path.join(d, '*kernel_trace.csv')):
