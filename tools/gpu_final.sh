@@ -9,3 +9,7 @@ timeout -k 10 200 python tools/pcie_probe.py 128 > gpurun_out/pcie.log 2>&1 || {
 cat gpurun_out/pcie.log
 timeout -k 10 400 python bench.py > gpurun_out/bench_default.log 2>&1 || { tail -5 gpurun_out/bench_default.log; exit 1; }
 tail -1 gpurun_out/bench_default.log | cut -c1-250
+for cfg in sparse4 sparse5; do
+  timeout -k 10 300 python bench.py --config $cfg > gpurun_out/bench_$cfg.log 2>&1 || { tail -5 gpurun_out/bench_$cfg.log; exit 1; }
+  tail -1 gpurun_out/bench_$cfg.log | cut -c1-160
+done
