@@ -284,21 +284,23 @@ void launch_ms_dots(const double* B, const double* R, int64_t n, int s, double* 
   }
 }
 
-// Scalar step 1 (one thread per column): alpha_c = rr_c / (p_c . A p_c).
-__global__ void ms_alpha_kernel(MsState st, const double* __restrict__ pq, int s) {
-  const int c = threadIdx.x;
-  if (c >= s) return;
-  st.a[c] = st.active[c] ? st.rr[c] / pq[c] : 0.0;
-}
-
-// r[i][c] -= a[c] q[i][c]
+// r[i][c] -= a[c] q[i][c] with the base step a[c] = rr[c] / (p . q)[c] (0 once the
+// column stopped) formed per element; the first workgroup also stores a for the
+// scalar kernel (the separate alpha launch folded in).
 __global__ __launch_bounds__(256) void ms_r_update_kernel(double* __restrict__ R,
                                                           const double* __restrict__ Q,
-                                                          const double* __restrict__ a,
+                                                          MsState st,
+                                                          const double* __restrict__ pq,
                                                           int64_t n, int s) {
   const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (blockIdx.x == 0 && threadIdx.x < s) {
+    const int c = threadIdx.x;
+    st.a[c] = st.active[c] ? st.rr[c] / pq[c] : 0.0;
+  }
   if (e >= n * s) return;
-  R[e] -= a[(int)(e % s)] * Q[e];
+  const int c = (int)(e % s);
+  const double a = st.active[c] ? st.rr[c] / pq[c] : 0.0;
+  R[e] -= a * Q[e];
 }
 
 // Scalar step 2 (thread (j, c), j < S shifts): with BR = B^T r_new and rr_new

@@ -45,8 +45,7 @@ __global__ void lanczos_scalar_kernel(const double*, const double*, const double
                                       double*);
 void launch_ms_dots(const double* B, const double* R, int64_t n, int s, double* partial, int nblk,
                     hipStream_t st);
-__global__ void ms_alpha_kernel(MsState, const double*, int);
-__global__ void ms_r_update_kernel(double*, const double*, const double*, int64_t, int);
+__global__ void ms_r_update_kernel(double*, const double*, MsState, const double*, int64_t, int);
 __global__ void ms_scalar_kernel(MsState, const double*, int, const double*, int, int, double,
                                  double*);
 __global__ void ms_p_update_kernel(double*, const double*, const double*, const int*, int64_t,
@@ -641,10 +640,8 @@ int gpmi_sp_msgram(gpmi_sp* sp, const double* etas, int neta, const double* rhs,
     if (rc) return rc;
     rc = col_dots(sp, Pd, 0, 1, Qd, s, pq);
     if (rc) return rc;
-    hipLaunchKernelGGL(ms_alpha_kernel, dim3(1), dim3(64), 0, str, st, pq, s);
-    SP_LAUNCH("ms_alpha_kernel");
-    hipLaunchKernelGGL(ms_r_update_kernel, dim3(grid_ns(n, s)), dim3(256), 0, str, Rd, Qd, st.a,
-                       n, s);
+    hipLaunchKernelGGL(ms_r_update_kernel, dim3(grid_ns(n, s)), dim3(256), 0, str, Rd, Qd, st,
+                       pq, n, s);
     SP_LAUNCH("ms_r_update_kernel");
     launch_ms_dots(Bd, Rd, n, s, sp->partial, MS_NBLK, str);
     SP_LAUNCH("ms_dots_partial_kernel");
