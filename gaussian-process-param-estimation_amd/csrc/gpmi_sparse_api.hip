@@ -318,6 +318,7 @@ int gpmi_sp_create_matern(int device, const double* points, int64_t n, int d,
       }
       wid[k] = xcut * std::fabs(scale[k]) * (1.0 + 1e-9);
       if (!(wid[k] > 0.0) || !std::isfinite(wid[k])) cells = false;
+      if (!std::isfinite(pmin[k]) || !std::isfinite(pmax[k])) cells = false;   // NaN / inf points
     }
     int64_t total = 0;
     for (int it = 0; cells && it < 64; ++it) {
