@@ -312,13 +312,14 @@ int gpmi_sp_create_matern(int device, const double* points, int64_t n, int d,
     int64_t G[3] = {1, 1, 1};
     for (int k = 0; k < d; ++k) {
       pmin[k] = pmax[k] = points[k];
-      for (int64_t i = 1; i < n; ++i) {
-        pmin[k] = std::min(pmin[k], points[i * d + k]);
-        pmax[k] = std::max(pmax[k], points[i * d + k]);
+      for (int64_t i = 0; i < n; ++i) {
+        const double v = points[i * d + k];
+        if (!std::isfinite(v)) cells = false;   // NaN / inf points: all-pairs kernels
+        pmin[k] = std::min(pmin[k], v);
+        pmax[k] = std::max(pmax[k], v);
       }
       wid[k] = xcut * std::fabs(scale[k]) * (1.0 + 1e-9);
       if (!(wid[k] > 0.0) || !std::isfinite(wid[k])) cells = false;
-      if (!std::isfinite(pmin[k]) || !std::isfinite(pmax[k])) cells = false;   // NaN / inf points
     }
     int64_t total = 0;
     for (int it = 0; cells && it < 64; ++it) {
