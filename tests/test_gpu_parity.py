@@ -270,3 +270,33 @@ def test_cfg3_n16384_logdet_and_lp(gp):
     from gaussian_proc._likelihood._direct_likelihood import DirectLikelihood
     lp = DirectLikelihood.log_likelihood_batch(z, X, op, cfg['hypers'])
     assert rel(lp, cfg['direct_lp']) < 1e-8
+
+
+def test_bench_batch64_call_vs_single_and_oracle(gp):
+    """The bench's configuration in small: ONE batched device call over a 64-point
+    eta grid (ragged n = 2304, outer panel 2048) against batch-1 calls of the same
+    operator and, for every fourth eta, the oracle's Cholesky logdet and Gram."""
+    from oracle import data
+    from gaussian_proc._mixed_correlation import MixedCorrelation
+    pts = data.generate_points(48, 2, True)
+    z = data.generate_data(pts, 0.2)
+    X = data.generate_basis_functions(pts, 2)
+    etas = numpy.logspace(-3, 3, 64)
+    D = gp.generate_correlation(pts, 0.1, 1.5, device_resident=True, max_batch=64)
+    op = MixedCorrelation(D)
+    op.op.set_outer(16)
+    ld, G = op.loglik_terms(etas, X, z)
+    assert ld.shape == (64,) and G.shape[0] == 64
+    one = MixedCorrelation(gp.generate_correlation(pts, 0.1, 1.5, device_resident=True,
+                                                   max_batch=1))
+    for i in (0, 17, 40, 63):
+        l1, g1 = one.loglik_terms([etas[i]], X, z)
+        assert abs(l1[0] - ld[i]) <= 1e-12 * abs(ld[i])
+        assert numpy.max(numpy.abs(g1[0] - G[i])) <= 1e-12 * numpy.max(numpy.abs(G[i]))
+    K = matern.dense_correlation(pts, 0.1, 1.5)
+    ref = OracleMC(K, 'cholesky')
+    R = numpy.column_stack([X, z])
+    for i in range(0, 64, 4):
+        assert rel(ld[i], ref.logdet(etas[i])) < 1e-10, i
+        Gref = R.T @ ref.solve(etas[i], R)
+        assert numpy.max(numpy.abs(G[i] - Gref)) <= 1e-8 * numpy.max(numpy.abs(Gref)), i
