@@ -32,8 +32,11 @@ __device__ __forceinline__ double readlane_d(double v, int lane) {
   return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
 
-#ifndef GPMI_F1_LDS
-#define GPMI_F1_LDS 1   // 16x16 factor: DPP quad broadcast + LDS line (0: ds_bpermute shuffles)
+#ifndef GPMI_CHOL_STAMPS
+#define GPMI_CHOL_STAMPS 0   // probe builds: per-block phase stamps of one lds_chol_block call
+#endif
+#if GPMI_CHOL_STAMPS
+__device__ int g_chol_calls;
 #endif
 
 // v broadcast from lane SG of each quad (DPP quad_perm [SG,SG,SG,SG], VALU only).
@@ -115,89 +118,69 @@ __device__ __forceinline__ void store_colblock(double* Ls, const d4 (&Xc)[NDB - 
 
 // F1 of block jb (wave 0): factor the 16x16 diagonal block in registers and
 // invert it into Aux[jb][16][16]; diag(L) to sdiag, first bad pivot to *s_fail.
+// Lane (r, g) holds row r, columns 4g..4g+3. Pivot step j: column j to every lane
+// of quad r by DPP and across quads through the LDS line colbuf (one wave: LDS
+// order plus wave-scope fences, no barrier), overlapping the rsq chain; row j of
+// X = L^-1 is formed in the same step (rows above it are final) and passed
+// through xbuf, so the inverse chain runs in the shadow of the factor chain.
 __device__ __forceinline__ void f1_factor(double* Ls, double* Aux, double* sdiag, int* s_fail,
-                                          int jb, double* colbuf) {
+                                          int jb, double* colbuf, double* xbuf) {
   const int lane = threadIdx.x & 63;
   const int j0 = jb * DB;
-    const int r = lane >> 2, g = lane & 3;
-    double a[4];
+  const int r = lane >> 2, g = lane & 3;
+  double a[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) a[k] = Ls[(j0 + r) * DL + j0 + 4 * g + k];
-    double myrinv = 0.0;
+  for (int k = 0; k < 4; ++k) a[k] = Ls[(j0 + r) * DL + j0 + 4 * g + k];
+  double myrinv = 0.0;
+  double s[4] = {0.0, 0.0, 0.0, 0.0}, x[4] = {0.0, 0.0, 0.0, 0.0};
+  int fail = 0;
 #pragma unroll
-    for (int j = 0; j < DB; ++j) {
-      const int sk = j & 3, sg = j >> 2;
-      const double d = readlane_d(a[sk], (j << 2) | sg);
-#if GPMI_F1_LDS
-      // column j: A[r][j] to every lane of quad r by DPP; the column through a
-      // 16-double LDS line (one wave: LDS order, no barrier) overlaps the rsq chain
-      const double crj = quad_bcast_sel(a[sk], sg);
-      if (g == 0) colbuf[r] = crj;
-      wave_lds_sync();
-      double lcj[4];
-      {
-        const d2 c01 = *reinterpret_cast<const d2*>(&colbuf[4 * g]);
-        const d2 c23 = *reinterpret_cast<const d2*>(&colbuf[4 * g + 2]);
-        lcj[0] = c01[0]; lcj[1] = c01[1]; lcj[2] = c23[0]; lcj[3] = c23[1];
-      }
-#else
-      const double crj = __shfl(a[sk], (r << 2) | sg);
-      double lcj[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) lcj[k] = __shfl(a[sk], ((4 * g + k) << 2) | sg);
-#endif
-      const double rinv = rsqrt_nr(d);
-      const double ljj = d * rinv;
-      if (lane == 0) {
-        if (!(d > 0.0) && *s_fail == 0) *s_fail = j0 + j + 1;
-        sdiag[j0 + j] = ljj;
-      }
-      if (r == j) myrinv = rinv;
-      const double lrj = (r > j) ? crj * rinv : ((r == j) ? ljj : 0.0);
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int c = 4 * g + k;
-        if (c > j && c <= r) a[k] -= lrj * (lcj[k] * rinv);
-      }
-      if (g == sg) a[sk] = lrj;
+  for (int j = 0; j < DB; ++j) {
+    const int sk = j & 3, sg = j >> 2;
+    const double d = readlane_d(a[sk], (j << 2) | sg);
+    const double crj = quad_bcast_sel(a[sk], sg);
+    if (g == 0) colbuf[r] = crj;
+    wave_lds_sync();
+    double lcj[4];
+    {
+      const d2 c01 = *reinterpret_cast<const d2*>(&colbuf[4 * g]);
+      const d2 c23 = *reinterpret_cast<const d2*>(&colbuf[4 * g + 2]);
+      lcj[0] = c01[0]; lcj[1] = c01[1]; lcj[2] = c23[0]; lcj[3] = c23[1];
     }
+    const double rinv = rsqrt_nr(d);
+    const double ljj = d * rinv;
+    if (!(d > 0.0) && fail == 0) fail = j0 + j + 1;   // d is wave-uniform
+    if (lane == 0) sdiag[j0 + j] = ljj;
+    if (r == j) myrinv = rinv;
+    const double lrj = (r > j) ? crj * rinv : ((r == j) ? ljj : 0.0);
 #pragma unroll
-    for (int k = 0; k < 4; ++k) Ls[(j0 + r) * DL + j0 + 4 * g + k] = a[k];
-    // X = inv(L_jj): row p of X is final once the rows above it are.
-    double lrow[DB];   // L[r][p], p = 0..15
-#pragma unroll
-    for (int p = 0; p < DB; ++p) lrow[p] = __shfl(a[p & 3], (r << 2) | (p >> 2));
-    double s[4] = {0.0, 0.0, 0.0, 0.0}, x[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-    for (int p = 0; p < DB; ++p) {
-      if (r == p) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) x[k] = (((4 * g + k) == p ? 1.0 : 0.0) - s[k]) * myrinv;
-      }
-      double xp[4];
-#if GPMI_F1_LDS
-      // row p of X through the LDS line (the four lanes of quad p write it)
-      if (r == p) {
-        *reinterpret_cast<d2*>(&colbuf[4 * g]) = d2{x[0], x[1]};
-        *reinterpret_cast<d2*>(&colbuf[4 * g + 2]) = d2{x[2], x[3]};
-      }
-      wave_lds_sync();
-      {
-        const d2 c01 = *reinterpret_cast<const d2*>(&colbuf[4 * g]);
-        const d2 c23 = *reinterpret_cast<const d2*>(&colbuf[4 * g + 2]);
-        xp[0] = c01[0]; xp[1] = c01[1]; xp[2] = c23[0]; xp[3] = c23[1];
-      }
-#else
-#pragma unroll
-      for (int k = 0; k < 4; ++k) xp[k] = __shfl(x[k], (p << 2) | g);
-#endif
-      if (r > p) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) s[k] += lrow[p] * xp[k];
-      }
+    for (int k = 0; k < 4; ++k) {
+      const int c = 4 * g + k;
+      if (c > j && c <= r) a[k] -= lrj * (lcj[k] * rinv);
     }
+    if (g == sg) a[sk] = lrj;
+    // row j of X: (e_j - sum_{p < j} L[j][p] X[p]) / L[j][j]; lrj = L[r][j] is final
+    if (r == j) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) Aux[jb * 256 + r * 16 + 4 * g + k] = x[k];
+      for (int k = 0; k < 4; ++k) x[k] = (((4 * g + k) == j ? 1.0 : 0.0) - s[k]) * myrinv;
+      *reinterpret_cast<d2*>(&xbuf[4 * g]) = d2{x[0], x[1]};
+      *reinterpret_cast<d2*>(&xbuf[4 * g + 2]) = d2{x[2], x[3]};
+    }
+    wave_lds_sync();
+    if (r > j) {
+      const d2 c01 = *reinterpret_cast<const d2*>(&xbuf[4 * g]);
+      const d2 c23 = *reinterpret_cast<const d2*>(&xbuf[4 * g + 2]);
+      s[0] += lrj * c01[0];
+      s[1] += lrj * c01[1];
+      s[2] += lrj * c23[0];
+      s[3] += lrj * c23[1];
+    }
+  }
+  if (lane == 0 && fail && *s_fail == 0) *s_fail = fail;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) Ls[(j0 + r) * DL + j0 + 4 * g + k] = a[k];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) Aux[jb * 256 + r * 16 + 4 * g + k] = x[k];
 }
 
 // F3 tile q of the trailing update after block jb: (ti, tj), jb < tj <= ti < 8, K = 16.
@@ -228,11 +211,24 @@ __device__ __forceinline__ void lds_chol_block(double* Ls, double* Aux, double* 
                                                int* s_fail) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int fr = lane & 15, fk = lane >> 4;
-  __shared__ __attribute__((aligned(16))) double colbuf[DB];   // F1 broadcast line (wave 0)
-  if (w == 0) f1_factor(Ls, Aux, sdiag, s_fail, 0, colbuf);
+  __shared__ __attribute__((aligned(16))) double colbuf[DB];   // F1 column line (wave 0)
+  __shared__ __attribute__((aligned(16))) double xbuf[DB];     // F1 inverse-row line
+#if GPMI_CHOL_STAMPS
+  unsigned long long cs[NDB + 1][3];
+  bool cst = false;
+  if (t == 0 && blockIdx.x == 0) cst = atomicAdd(&g_chol_calls, 1) == 8;
+#define CHST(jb, i) \
+  if (cst) cs[jb][i] = wall_clock64()
+#else
+#define CHST(jb, i)
+#endif
+  CHST(0, 2);
+  if (w == 0) f1_factor(Ls, Aux, sdiag, s_fail, 0, colbuf, xbuf);
+  CHST(0, 1);
   for (int jb = 0; jb < NDB; ++jb) {
     const int j0 = jb * DB;
     __syncthreads();   // F1 of jb done
+    CHST(jb, 0);
     // ---- F2: panel rows below: L[i][j0 + c] = sum_p A[i][j0 + p] X[c][p]
     {
       const int row = j0 + DB + (t >> 1), h = t & 1;
@@ -252,6 +248,7 @@ __device__ __forceinline__ void lds_chol_block(double* Ls, double* Aux, double* 
       }
     }
     __syncthreads();
+    CHST(jb + 1, 1);
     // ---- F3 (+ F1 of jb + 1 on wave 0)
     const int m = NDB - 1 - jb;               // trailing tiles per side
     const int ntile = m * (m + 1) / 2;
@@ -259,13 +256,20 @@ __device__ __forceinline__ void lds_chol_block(double* Ls, double* Aux, double* 
       if (ntile > 0) {
         f3_tile(Ls, jb, 0, fr, fk);
         wave_lds_sync();   // the tile written by other lanes of this wave
-        f1_factor(Ls, Aux, sdiag, s_fail, jb + 1, colbuf);
+        f1_factor(Ls, Aux, sdiag, s_fail, jb + 1, colbuf, xbuf);
+        CHST(jb + 1, 2);
       }
     } else {
       for (int q = w; q < ntile; q += 3) f3_tile(Ls, jb, q, fr, fk);
     }
   }
   __syncthreads();
+#if GPMI_CHOL_STAMPS
+  if (cst)
+    for (int jb = 1; jb < NDB; ++jb)
+      printf("lds_chol jb=%d (10ns): F2 %llu  F3t0+F1 %llu  wait %llu\n", jb - 1,
+             cs[jb][1] - cs[jb - 1][0], cs[jb][2] - cs[jb][1], cs[jb][0] - cs[jb][2]);
+#endif
 }
 
 __device__ __forceinline__ void lds_inv_block(double* Ls, const double* Aux) {
