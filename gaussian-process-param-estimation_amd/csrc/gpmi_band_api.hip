@@ -595,16 +595,30 @@ int gpmi_band_eigenvalues(gpmi_band* b, double* lam) {
   BD_TRY(hipEventRecord(b->ev0, s));
   hipLaunchKernelGGL(chase_copy_kernel, dim3(n), dim3(256), 0, s, b->Ab, b->Ac, np, n);
   BD_LAUNCH("chase_copy_kernel");
-  // wavefront t = 3 s + k: tasks s in [s_lo, s_hi], one workgroup each
+  // wavefront t = 3 s + k: tasks s in [s_lo, s_hi]. GPMI_CHASE_SPLIT=0: one
+  // workgroup per task (chase_task_kernel) instead of reflector + per-block launches
+  static const bool chase_split = [] {
+    const char* v = std::getenv("GPMI_CHASE_SPLIT");
+    return !(v && std::atoi(v) == 0);
+  }();
   const int kmax = (n - 2) / TS + 1;
   const int tmax = 3 * std::max(0, n - 3) + kmax;
   for (int t = 0; t <= tmax && n > 2; ++t) {
     const int s_hi = std::min(t / 3, n - 3);
     const int s_lo = std::max(0, (t - kmax + 2) / 3);
     if (s_hi < s_lo) continue;
-    hipLaunchKernelGGL(chase_task_kernel, dim3(s_hi - s_lo + 1), dim3(512), 0, s, b->Ac, np, n,
-                       t, s_hi);
-    BD_LAUNCH("chase_task_kernel");
+    if (chase_split) {   // reflectors (scratch: td, free until the chase ends), then F/D/E
+      hipLaunchKernelGGL(chase_reflect_kernel, dim3(s_hi - s_lo + 1), dim3(TS), 0, s, b->Ac, np,
+                         n, t, s_hi, b->td);
+      BD_LAUNCH("chase_reflect_kernel");
+      hipLaunchKernelGGL(chase_apply_kernel, dim3(3 * (s_hi - s_lo + 1)), dim3(512), 0, s, b->Ac,
+                         np, n, t, s_hi, b->td);
+      BD_LAUNCH("chase_apply_kernel");
+    } else {
+      hipLaunchKernelGGL(chase_task_kernel, dim3(s_hi - s_lo + 1), dim3(512), 0, s, b->Ac, np, n,
+                         t, s_hi);
+      BD_LAUNCH("chase_task_kernel");
+    }
   }
   double* d = b->td;
   double* e2 = b->td + np;

@@ -248,6 +248,194 @@ __global__ __launch_bounds__(CT) void chase_task_kernel(double* __restrict__ A, 
   }
 }
 
+// ---------------------------------------------------------------------------
+// Split form of the task (default): the F, D and E updates of a task need only its
+// reflector, so a small launch forms every task's (v, tau, beta) into a scratch
+// slot (and writes the annihilated column s when k = 0), then one workgroup per
+// block applies it: three workgroups per task, none exchanging data, each moving a
+// third of the task's bytes through its CU. Same arithmetic and order as
+// chase_task_kernel, so the result is bit-identical.
+// ---------------------------------------------------------------------------
+constexpr int SLOT = CB + 2;   // v[128], tau, beta
+
+__global__ __launch_bounds__(CB) void chase_reflect_kernel(double* __restrict__ A, int64_t lda,
+                                                           int n, int t, int s_hi,
+                                                           double* __restrict__ scr) {
+  __shared__ double red[2];
+  __shared__ double sx0;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int s = s_hi - (int)blockIdx.x;
+  const int k = t - 3 * s;
+  if (s < 0 || k < 0) return;
+  const int r0 = s + 1 + k * CB;
+  if (r0 >= n) return;
+  const int L = min(r0 + CB, n) - r0;
+  const int col = (k == 0) ? s : s + 1 + (k - 1) * CB;
+  double* sl = scr + (int64_t)blockIdx.x * SLOT;
+  const double xi = (tid < L) ? A[(int64_t)(r0 + tid) * lda + col] : 0.0;
+  if (tid == 0) sx0 = xi;
+  double v = (tid > 0 && tid < L) ? xi * xi : 0.0;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  const double nb2 = red[0] + red[1];
+  const double xx0 = sx0;
+  double tau = 0.0, beta = xx0, scale = 0.0;
+  if (nb2 > 0.0) {
+    const double nrm = sqrt(xx0 * xx0 + nb2);
+    beta = xx0 >= 0.0 ? -nrm : nrm;
+    tau = (beta - xx0) / beta;
+    scale = 1.0 / (xx0 - beta);
+  }
+  sl[tid] = (tid == 0) ? 1.0 : ((tid < L) ? xi * scale : 0.0);
+  if (tid == 0) {
+    sl[CB] = tau;
+    sl[CB + 1] = beta;
+  }
+  if (k == 0 && tid < L) A[(int64_t)(r0 + tid) * lda + s] = (tid == 0) ? beta : 0.0;
+}
+
+__global__ __launch_bounds__(CT) void chase_apply_kernel(double* __restrict__ A, int64_t lda,
+                                                         int n, int t, int s_hi,
+                                                         const double* __restrict__ scr) {
+  __shared__ double sv[CB];
+  __shared__ double cpart[8][CB];
+  __shared__ double srow[CB];
+  __shared__ double sx[CB];
+  __shared__ double red[8];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int slot = (int)blockIdx.x / 3, part = (int)blockIdx.x % 3;   // 0 F, 1 D, 2 E
+  const int s = s_hi - slot;
+  const int k = t - 3 * s;
+  if (s < 0 || k < 0) return;
+  const int r0 = s + 1 + k * CB;
+  if (r0 >= n) return;
+  const int r1 = min(r0 + CB, n), L = r1 - r0;
+  const int col = (k == 0) ? s : s + 1 + (k - 1) * CB;
+  const int e1 = min(r1 + CB, n), LE = e1 - r1;
+  if (part == 0 && k == 0) return;     // no bulge block in the first task of a sweep
+  if (part == 2 && LE <= 0) return;
+  const double* sl = scr + (int64_t)slot * SLOT;
+  const double tau = sl[CB], beta = sl[CB + 1];
+  if (tau == 0.0) return;              // identity reflector
+  d2 Br[CPT];
+  if (part == 0) load_block(A + (int64_t)r0 * lda + col, lda, L, CB, Br);
+  else if (part == 1) load_block<true>(A + (int64_t)r0 * lda + r0, lda, L, L, Br);
+  else load_block(A + (int64_t)r1 * lda + r0, lda, LE, L, Br);
+  if (tid < CB) sv[tid] = sl[tid];
+  __syncthreads();
+  const int c0 = 2 * lane;
+  const double vc0 = sv[c0], vc1 = sv[c0 + 1];
+  if (part == 0) {
+    // ---- F <- H F: w = tau F^T v; column col becomes (beta, 0 ...)
+    double fc0 = 0.0, fc1 = 0.0;
+#pragma unroll
+    for (int u = 0; u < CPT; ++u) {
+      const double vi = sv[8 * u + w];
+      fc0 += Br[u][0] * vi;
+      fc1 += Br[u][1] * vi;
+    }
+    cpart[w][c0] = fc0;
+    cpart[w][c0 + 1] = fc1;
+    __syncthreads();
+    if (tid < CB) {
+      double sfv = 0.0;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) sfv += cpart[q][tid];
+      sx[tid] = tau * sfv;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < CPT; ++u) {
+      const int e = u * CT + tid;
+      const int i = e >> 6, c2 = 2 * (e & 63);
+      if (i >= L) continue;
+      d2 o;
+      o[0] = (c2 == 0) ? (i == 0 ? beta : 0.0) : Br[u][0] - sv[i] * sx[c2];
+      o[1] = Br[u][1] - sv[i] * sx[c2 + 1];
+      *reinterpret_cast<d2*>(A + (int64_t)(r0 + i) * lda + col + c2) = o;
+    }
+  } else if (part == 1) {
+    // ---- D <- H D H = D - v w^T - w v^T, w = p - tau/2 (v.p) v, p = tau D v
+    double dc0 = 0.0, dc1 = 0.0;
+    double prow[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      double rowv[8];
+#pragma unroll
+      for (int uu = 0; uu < 8; ++uu) {
+        const int u = 8 * h + uu;
+        const int i = 8 * u + w;
+        const double vi = sv[i];
+        const double d0 = (c0 <= i) ? Br[u][0] : 0.0;
+        const double d1 = (c0 + 1 <= i) ? Br[u][1] : 0.0;
+        rowv[uu] = d0 * vc0 + d1 * vc1;
+        if (c0 < i) dc0 += d0 * vi;
+        if (c0 + 1 < i) dc1 += d1 * vi;
+      }
+      prow[h] = butterfly8(rowv);
+    }
+    cpart[w][c0] = dc0;
+    cpart[w][c0 + 1] = dc1;
+    if ((lane & 7) == 0) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) srow[8 * (8 * h + ((lane >> 3) & 7)) + w] = prow[h];
+    }
+    __syncthreads();
+    double pi = 0.0;
+    if (tid < CB) {
+      double sd = srow[tid];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) sd += cpart[q][tid];
+      pi = (tid < L) ? tau * sd : 0.0;
+    }
+    const double vp = block_sum8((tid < L) ? pi * sv[tid] : 0.0, red);
+    if (tid < CB) sx[tid] = (tid < L) ? pi - 0.5 * tau * vp * sv[tid] : 0.0;
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < CPT; ++u) {
+      const int e = u * CT + tid;
+      const int i = e >> 6, c2 = 2 * (e & 63);
+      if (i >= L || c2 >= L || c2 > i) continue;
+      d2 o;
+      o[0] = Br[u][0] - sv[i] * sx[c2] - sx[i] * sv[c2];
+      o[1] = Br[u][1] - sv[i] * sx[c2 + 1] - sx[i] * sv[c2 + 1];
+      if (c2 + 1 < L) *reinterpret_cast<d2*>(A + (int64_t)(r0 + i) * lda + r0 + c2) = o;
+      else A[(int64_t)(r0 + i) * lda + r0 + c2] = o[0];
+    }
+  } else {
+    // ---- E <- E H = E - q v^T, q = tau E v
+    double qrow[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      double rowv[8];
+#pragma unroll
+      for (int uu = 0; uu < 8; ++uu)
+        rowv[uu] = Br[8 * h + uu][0] * vc0 + Br[8 * h + uu][1] * vc1;
+      qrow[h] = butterfly8(rowv);
+    }
+    if ((lane & 7) == 0) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) srow[8 * (8 * h + ((lane >> 3) & 7)) + w] = qrow[h];
+    }
+    __syncthreads();
+    if (tid < CB) sx[tid] = tau * srow[tid];
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < CPT; ++u) {
+      const int e = u * CT + tid;
+      const int i = e >> 6, c2 = 2 * (e & 63);
+      if (i >= LE || c2 >= L) continue;
+      d2 o;
+      o[0] = Br[u][0] - sx[i] * sv[c2];
+      o[1] = Br[u][1] - sx[i] * sv[c2 + 1];
+      if (c2 + 1 < L) *reinterpret_cast<d2*>(A + (int64_t)(r1 + i) * lda + r0 + c2) = o;
+      else A[(int64_t)(r1 + i) * lda + r0 + c2] = o[0];
+    }
+  }
+}
+
 // Copy of the band for the chase: B's lower band (0 <= i - j <= 128) of the
 // reduced matrix, zero for 128 < i - j <= 2 * 128 + 1 (the bulge envelope; the
 // reduced matrix keeps Householder vectors there). Row i per workgroup.
