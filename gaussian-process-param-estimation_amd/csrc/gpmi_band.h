@@ -61,9 +61,9 @@ __global__ void band_der_kernel(const double* fac, int nt, double* ysol, double*
 
 __global__ void chase_copy_kernel(const double* Ab, double* A, int64_t lda, int n);
 __global__ void chase_task_kernel(double* A, int64_t lda, int n, int t, int s_hi);
-__global__ void chase_reflect_kernel(double* A, int64_t lda, int n, int t, int s_hi, double* scr);
+__global__ void chase_reflect_kernel(double* A, int64_t lda, int n, int s, double* sl);
 __global__ void chase_apply_kernel(double* A, int64_t lda, int n, int t, int s_hi,
-                                   const double* scr);
+                                   const double* rd, double* wr, int ns);
 __global__ void tridiag_extract_kernel(const double* A, int64_t lda, int n, double* d, double* e2);
 __global__ void bisect_kernel(const double* d, const double* e2, int n, double lo0, double hi0,
                               double pivmin, double* lam);

@@ -590,7 +590,9 @@ int gpmi_band_eigenvalues(gpmi_band* b, double* lam) {
   const int n = (int)b->n;
   if (!b->Ac) {
     BD_TRY(hipMalloc(&b->Ac, sizeof(double) * np * np));
-    BD_TRY(hipMalloc(&b->td, sizeof(double) * 3 * np));
+    // td: [n] diagonal, [n] squared subdiagonal, [n] eigenvalues, then the chase's
+    // reflector slots (two wavefront parities x ((n - 2) / 128 + 3) slots of 130)
+    BD_TRY(hipMalloc(&b->td, sizeof(double) * (3 * np + 2 * ((np - 2) / TS + 3) * (TS + 2))));
   }
   BD_TRY(hipEventRecord(b->ev0, s));
   hipLaunchKernelGGL(chase_copy_kernel, dim3(n), dim3(256), 0, s, b->Ab, b->Ac, np, n);
@@ -607,12 +609,22 @@ int gpmi_band_eigenvalues(gpmi_band* b, double* lam) {
     const int s_hi = std::min(t / 3, n - 3);
     const int s_lo = std::max(0, (t - kmax + 2) / 3);
     if (s_hi < s_lo) continue;
-    if (chase_split) {   // reflectors (scratch: td, free until the chase ends), then F/D/E
-      hipLaunchKernelGGL(chase_reflect_kernel, dim3(s_hi - s_lo + 1), dim3(TS), 0, s, b->Ac, np,
-                         n, t, s_hi, b->td);
-      BD_LAUNCH("chase_reflect_kernel");
+    if (chase_split) {
+      // reflector slots by sweep (s % ns), double-buffered by wavefront parity: the
+      // E workgroup of (s, k) writes the reflector of (s, k + 1) for wavefront t + 1;
+      // a sweep's first task (t = 3 s) gets its own small launch
+      const int ns = kmax + 2;
+      double* scr = b->td + 3 * np;
+      double* rd = scr + (int64_t)(t & 1) * ns * (TS + 2);
+      double* wr = scr + (int64_t)((t + 1) & 1) * ns * (TS + 2);
+      if (t % 3 == 0 && t / 3 >= s_lo && t / 3 <= s_hi) {
+        const int s0 = t / 3;
+        hipLaunchKernelGGL(chase_reflect_kernel, dim3(1), dim3(TS), 0, s, b->Ac, np, n, s0,
+                           rd + (int64_t)(s0 % ns) * (TS + 2));
+        BD_LAUNCH("chase_reflect_kernel");
+      }
       hipLaunchKernelGGL(chase_apply_kernel, dim3(3 * (s_hi - s_lo + 1)), dim3(512), 0, s, b->Ac,
-                         np, n, t, s_hi, b->td);
+                         np, n, t, s_hi, rd, wr, ns);
       BD_LAUNCH("chase_apply_kernel");
     } else {
       hipLaunchKernelGGL(chase_task_kernel, dim3(s_hi - s_lo + 1), dim3(512), 0, s, b->Ac, np, n,

@@ -258,20 +258,20 @@ __global__ __launch_bounds__(CT) void chase_task_kernel(double* __restrict__ A, 
 // ---------------------------------------------------------------------------
 constexpr int SLOT = CB + 2;   // v[128], tau, beta
 
+// Reflector of the first task (s, 0) of sweep s into slot sl; writes the
+// annihilated column s. (The reflector of (s, k + 1) comes from the E workgroup of
+// (s, k) one wavefront earlier: chase_apply_kernel.)
 __global__ __launch_bounds__(CB) void chase_reflect_kernel(double* __restrict__ A, int64_t lda,
-                                                           int n, int t, int s_hi,
-                                                           double* __restrict__ scr) {
+                                                           int n, int s,
+                                                           double* __restrict__ sl) {
   __shared__ double red[2];
   __shared__ double sx0;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int s = s_hi - (int)blockIdx.x;
-  const int k = t - 3 * s;
-  if (s < 0 || k < 0) return;
-  const int r0 = s + 1 + k * CB;
+  const int k = 0;
+  const int r0 = s + 1;
   if (r0 >= n) return;
   const int L = min(r0 + CB, n) - r0;
-  const int col = (k == 0) ? s : s + 1 + (k - 1) * CB;
-  double* sl = scr + (int64_t)blockIdx.x * SLOT;
+  const int col = s;
   const double xi = (tid < L) ? A[(int64_t)(r0 + tid) * lda + col] : 0.0;
   if (tid == 0) sx0 = xi;
   double v = (tid > 0 && tid < L) ? xi * xi : 0.0;
@@ -298,8 +298,10 @@ __global__ __launch_bounds__(CB) void chase_reflect_kernel(double* __restrict__ 
 
 __global__ __launch_bounds__(CT) void chase_apply_kernel(double* __restrict__ A, int64_t lda,
                                                          int n, int t, int s_hi,
-                                                         const double* __restrict__ scr) {
+                                                         const double* __restrict__ rd,
+                                                         double* __restrict__ wr, int ns) {
   __shared__ double sv[CB];
+  __shared__ double red2[2];
   __shared__ double cpart[8][CB];
   __shared__ double srow[CB];
   __shared__ double sx[CB];
@@ -316,9 +318,9 @@ __global__ __launch_bounds__(CT) void chase_apply_kernel(double* __restrict__ A,
   const int e1 = min(r1 + CB, n), LE = e1 - r1;
   if (part == 0 && k == 0) return;     // no bulge block in the first task of a sweep
   if (part == 2 && LE <= 0) return;
-  const double* sl = scr + (int64_t)slot * SLOT;
+  const double* sl = rd + (int64_t)(s % ns) * SLOT;
   const double tau = sl[CB], beta = sl[CB + 1];
-  if (tau == 0.0) return;              // identity reflector
+  if (tau == 0.0 && part != 2) return;   // identity reflector (E still forms the next one)
   d2 Br[CPT];
   if (part == 0) load_block(A + (int64_t)r0 * lda + col, lda, L, CB, Br);
   else if (part == 1) load_block<true>(A + (int64_t)r0 * lda + r0, lda, L, L, Br);
@@ -406,6 +408,7 @@ __global__ __launch_bounds__(CT) void chase_apply_kernel(double* __restrict__ A,
     }
   } else {
     // ---- E <- E H = E - q v^T, q = tau E v
+    if (tau != 0.0) {
     double qrow[2];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -432,6 +435,42 @@ __global__ __launch_bounds__(CT) void chase_apply_kernel(double* __restrict__ A,
       o[1] = Br[u][1] - sx[i] * sv[c2 + 1];
       if (c2 + 1 < L) *reinterpret_cast<d2*>(A + (int64_t)(r1 + i) * lda + r0 + c2) = o;
       else A[(int64_t)(r1 + i) * lda + r0 + c2] = o[0];
+      Br[u] = o;
+    }
+    }
+    // ---- reflector of task (s, k + 1): its x is E's (updated) first column; the
+    //      same arithmetic as chase_reflect_kernel, into this sweep's slot of wr
+    __syncthreads();   // sx, srow reuse below
+    if (lane == 0) {
+#pragma unroll
+      for (int u = 0; u < CPT; ++u) srow[8 * u + w] = (8 * u + w < LE) ? Br[u][0] : 0.0;
+    }
+    __syncthreads();
+    double xi = 0.0, v2 = 0.0;
+    if (tid < CB) {
+      xi = srow[tid];
+      v2 = (tid > 0 && tid < LE) ? xi * xi : 0.0;
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) v2 += __shfl_xor(v2, off);
+      if (lane == 0) red2[w] = v2;
+    }
+    __syncthreads();
+    if (tid < CB) {
+      const double nb2 = red2[0] + red2[1];
+      const double xx0 = srow[0];
+      double tn = 0.0, bn = xx0, sc = 0.0;
+      if (nb2 > 0.0) {
+        const double nrm = sqrt(xx0 * xx0 + nb2);
+        bn = xx0 >= 0.0 ? -nrm : nrm;
+        tn = (bn - xx0) / bn;
+        sc = 1.0 / (xx0 - bn);
+      }
+      double* wl = wr + (int64_t)(s % ns) * SLOT;
+      wl[tid] = (tid == 0) ? 1.0 : ((tid < LE) ? xi * sc : 0.0);
+      if (tid == 0) {
+        wl[CB] = tn;
+        wl[CB + 1] = bn;
+      }
     }
   }
 }
