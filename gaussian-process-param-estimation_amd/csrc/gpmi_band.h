@@ -33,7 +33,7 @@ constexpr int BAND_MAX_NPAD = HH_MAXG * HH_ROWS;
 __global__ void hh_col_kernel(double* P, int64_t lda, int m, int c, double* part, double* pivrow,
                               double* tau);
 __global__ void hh_panel_kernel(double* P, int64_t lda, int m, double* part, double* pivrow,
-                                unsigned* counter, double* tau, int* err);
+                                unsigned* counter, double* tau, int* err, unsigned spin_limit);
 __global__ void vcopy_kernel(const double* P, int64_t lda, int m, double* U, int64_t ldu);
 __global__ void tn_partial_kernel(const double* P1, int64_t ld1, const double* P2, int64_t ld2,
                                   int m, double* part);

@@ -290,8 +290,9 @@ __global__ __launch_bounds__(HH_THREADS) void hh_col_kernel(double* __restrict__
 // every wave polls the shards with sc1 loads until their sum reaches G (c + 1)
 // and then reads the records with sc1 loads only. Records are double-buffered by column
 // parity: a workgroup publishing column c + 1 has seen every workgroup publish
-// column c, i.e. finish reading the slot it overwrites. Every spin is bounded;
-// a timeout sets *err and all workgroups leave (the host reports the error).
+// column c, i.e. finish reading the slot it overwrites. Every spin is bounded
+// (spin_limit polls); a timeout sets *err, every workgroup leaves, and the host
+// redoes the reduction with the per-column launches (hh_col_kernel).
 // counter[0..127] must be zero at launch (the host memsets it per panel).
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void st_sc1(double* p, double v) {
@@ -311,7 +312,8 @@ __global__ __launch_bounds__(HH_THREADS) void hh_panel_kernel(double* __restrict
                                                               double* __restrict__ pivrow,
                                                               unsigned* __restrict__ counter,
                                                               double* __restrict__ tau,
-                                                              int* __restrict__ err) {
+                                                              int* __restrict__ err,
+                                                              unsigned spin_limit) {
   extern __shared__ double dyn_lds[];   // sized by the host to keep one workgroup per CU
   double(*sacc)[HH_PART_LD] = reinterpret_cast<double(*)[HH_PART_LD]>(dyn_lds);
   __shared__ int s_bail;
@@ -382,18 +384,14 @@ __global__ __launch_bounds__(HH_THREADS) void hh_panel_kernel(double* __restrict
         for (int off = 4; off > 0; off >>= 1) v += __shfl_xor(v, off);
         if (__builtin_amdgcn_readfirstlane(v) >= target) break;
         __builtin_amdgcn_s_sleep(1);
-        if ((++spins & 1023u) == 0 &&
-            (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0 ||
-             spins > (1u << 24))) {
+        if (++spins > spin_limit ||
+            ((spins & 1023u) == 0 &&
+             __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)) {
           if (lane == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           s_bail = 1;
           break;
         }
       }
-    }
-    if (s_bail) {
-      __syncthreads();
-      return;
     }
     // records of slot c & 1: lane l reads columns (2l, 2l + 1) of every record this
     // wave owns with 16-byte sc1 loads, all in flight together; lane 0 also reads
@@ -426,6 +424,9 @@ __global__ __launch_bounds__(HH_THREADS) void hh_panel_kernel(double* __restrict
     sacc[w][2 * lane + 1] = sv[1];
     if (lane == 0) sacc[w][128] = sn;
     __syncthreads();
+    // a timed-out wave reached this barrier too (its loads read stale but valid
+    // memory); every wave sees s_bail here and the workgroup leaves together
+    if (s_bail) return;
     double S0 = 0.0, S1 = 0.0, nb2 = 0.0;
 #pragma unroll
     for (int q = 0; q < HH_WAVES; ++q) {

@@ -100,6 +100,12 @@ struct gpmi_band {
   int* info = nullptr;       // [cap]
   unsigned* ctr = nullptr;   // hh_panel hand-off counter: 8 shards, 64 B apart (512 bytes)
   int* err = nullptr;        // hh_panel timeout flag
+  // hh_panel_kernel needs all G workgroups co-resident: used only for G <= panel_maxg
+  // (CU count x resident workgroups per CU, at most HH_PANEL_MAXG); a timed-out
+  // hand-off makes band_reduce redo the reduction with hh_col_kernel launches
+  int panel_maxg = HH_PANEL_MAXG;
+  unsigned spin_limit = 1u << 24;
+  int panel_fallbacks = 0;
   int cap = 0;
   int nrhs = 0;
   double reduce_ms = 0.0, rhs_ms = 0.0, loglik_ms = 0.0, der_ms = 0.0;
@@ -161,19 +167,20 @@ int qt_panel(gpmi_band* b, int j, hipStream_t st) {
   return 0;
 }
 
-// Householder QR of panel j (columns [128 j, +128), rows from 128 (j + 1)) on st.
-int panel_qr(gpmi_band* b, int j, hipStream_t st) {
+// Householder QR of panel j (columns [128 j, +128), rows from 128 (j + 1)) on st;
+// single = false forces the per-column launches.
+int panel_qr(gpmi_band* b, int j, hipStream_t st, bool single) {
   const int64_t np = b->n_pad;
   const int64_t r0 = (int64_t)(j + 1) * TS, c0 = (int64_t)j * TS;
   const int m = (int)(np - r0);
   const int G = (m + HH_ROWS - 1) / HH_ROWS;
   double* P = b->Ab + r0 * np + c0;
   double* tau = b->tau + (int64_t)j * TS;
-  if (G <= HH_PANEL_MAXG) {
+  if (single && G <= b->panel_maxg) {
     // one launch per panel (rows in registers, in-launch reductions)
     BD_TRY(hipMemsetAsync(b->ctr, 0, 512, st));
     hipLaunchKernelGGL(hh_panel_kernel, dim3(G), dim3(HH_THREADS), HH_PANEL_LDS, st, P, np, m,
-                       b->part, b->pivrow, b->ctr, tau, b->err);
+                       b->part, b->pivrow, b->ctr, tau, b->err, b->spin_limit);
     BD_LAUNCH("hh_panel_kernel");
   } else {
     for (int c = -1; c < TS; ++c) {
@@ -196,17 +203,19 @@ std::vector<double> pack_rhs(const gpmi_band* b, const double* rhs, int64_t ld, 
 // Dense -> band: panels j = 0 .. nt-2 of 128 columns (see gpmi_band.hip).
 // With yh (the packed RHS), Y = Q^T R is applied panel by panel on the qs
 // stream as soon as each panel's T exists, beside the rest of the reduction.
-int band_reduce(gpmi_band* b, const double* K, const std::vector<double>* yh = nullptr) {
+// single = false: every panel by per-column launches, no look-ahead.
+int band_reduce_pass(gpmi_band* b, const double* K, const std::vector<double>* yh, bool single) {
   hipStream_t s = b->stream;
   const int64_t np = b->n_pad;
   const int nt = b->nt;
+  BD_TRY(hipMemsetAsync(b->err, 0, 16, s));
   BD_TRY(hipEventRecord(b->ev0, s));
   if (yh) {
     BD_TRY(hipMemcpyAsync(b->Y, yh->data(), sizeof(double) * yh->size(), hipMemcpyHostToDevice,
                           b->qs));
   }
   BD_TRY(hipMemcpyAsync(b->Ab, K, sizeof(double) * np * np, hipMemcpyDeviceToDevice, s));
-  const bool la = b->lookahead && b->s_pan;
+  const bool la = single && b->lookahead && b->s_pan;
   bool ahead = false;   // panel j already factored by the previous look-ahead
   for (int j = 0; j + 1 < nt; ++j) {
     const int64_t r0 = (int64_t)(j + 1) * TS, c0 = (int64_t)j * TS;
@@ -215,7 +224,7 @@ int band_reduce(gpmi_band* b, const double* K, const std::vector<double>* yh = n
     double* tau = b->tau + (int64_t)j * TS;
     double* T = b->Tm + (int64_t)j * TS * TS;
     if (!ahead) {
-      int rc = panel_qr(b, j, s);
+      int rc = panel_qr(b, j, s, single);
       if (rc) return rc;
     }
     ahead = false;
@@ -262,7 +271,7 @@ int band_reduce(gpmi_band* b, const double* K, const std::vector<double>* yh = n
     hipLaunchKernelGGL(w_kernel, dim3(mt), dim3(256), 0, s, b->X, Ur, (int64_t)BAND_ULD, b->Zh);
     BD_LAUNCH("w_kernel");
     const int next_g = (int)((np - r0 - TS + HH_ROWS - 1) / HH_ROWS);   // panel j + 1's grid
-    if (la && j + 2 < nt && next_g <= HH_PANEL_MAXG) {
+    if (la && j + 2 < nt && next_g <= b->panel_maxg) {
       // tile column 0 of the update (panel j + 1's columns) first; then that
       // panel's QR beside the rest of the update on a grid capped to la_grid
       // workgroups, so that the panel's workgroups find free CUs
@@ -271,7 +280,7 @@ int band_reduce(gpmi_band* b, const double* K, const std::vector<double>* yh = n
       BD_LAUNCH("syr2k_kernel");
       BD_TRY(hipEventRecord(b->ev_col, s));
       BD_TRY(hipStreamWaitEvent(b->s_pan, b->ev_col, 0));
-      int rc = panel_qr(b, j + 1, b->s_pan);
+      int rc = panel_qr(b, j + 1, b->s_pan, single);
       if (rc) return rc;
       BD_TRY(hipEventRecord(b->ev_pan, b->s_pan));
       const int rest = (mt - 1) * mt / 2;
@@ -304,6 +313,16 @@ int band_reduce(gpmi_band* b, const double* K, const std::vector<double>* yh = n
   BD_TRY(hipEventElapsedTime(&ms, b->ev0, b->ev1));
   b->reduce_ms = ms;
   return 0;
+}
+
+// The reduction with the single-launch panel QR; if a hand-off times out (its
+// workgroups were not all resident, e.g. the GPU is shared or partitioned), the
+// whole reduction is redone from K with the per-column panel launches.
+int band_reduce(gpmi_band* b, const double* K, const std::vector<double>* yh = nullptr) {
+  int rc = band_reduce_pass(b, K, yh, true);
+  if (rc != -1201) return rc;
+  ++b->panel_fallbacks;
+  return band_reduce_pass(b, K, yh, false);
 }
 
 int ensure_cap(gpmi_band* b, int neta) {
@@ -405,16 +424,22 @@ int gpmi_band_create(gpmi_op* op, gpmi_band** out) {
   if ((e = hipMalloc(&b->ctr, 512)) != hipSuccess) return fail(e, "ctr");
   if ((e = hipMalloc(&b->err, 16)) != hipSuccess) return fail(e, "err");
   if ((e = hipMemsetAsync(b->err, 0, 16, b->stream)) != hipSuccess) return fail(e, "err memset");
+  // per device (this one is current): cheap, so set on every create
+  if ((e = hipFuncSetAttribute(reinterpret_cast<const void*>(&hh_panel_kernel),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, HH_PANEL_LDS)) !=
+      hipSuccess)
+    return fail(e, "hh_panel LDS attribute");
   {
-    static bool attr_set = false;
-    if (!attr_set) {
-      if ((e = hipFuncSetAttribute(reinterpret_cast<const void*>(&hh_panel_kernel),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, HH_PANEL_LDS)) !=
-          hipSuccess)
-        return fail(e, "hh_panel LDS attribute");
-      attr_set = true;
-    }
+    int per_cu = 0;
+    if ((e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+             &per_cu, reinterpret_cast<const void*>(&hh_panel_kernel), HH_THREADS,
+             HH_PANEL_LDS)) != hipSuccess)
+      return fail(e, "hh_panel occupancy");
+    b->panel_maxg = std::min(HH_PANEL_MAXG, std::max(0, per_cu) * b->ncu);
   }
+  // test hook: GPMI_HH_SPIN_LIMIT=0 makes the first unsuccessful poll a timeout
+  if (const char* sl = std::getenv("GPMI_HH_SPIN_LIMIT"))
+    b->spin_limit = (unsigned)std::strtoul(sl, nullptr, 10);
   if ((e = hipMemsetAsync(b->U, 0, sizeof(double) * np * BAND_ULD, b->stream)) != hipSuccess)
     return fail(e, "U memset");
   if ((e = hipMemsetAsync(b->Y, 0, sizeof(double) * np * RLD, b->stream)) != hipSuccess)
@@ -689,6 +714,13 @@ int gpmi_band_last_timing(gpmi_band* b, double* reduce_ms, double* rhs_ms, doubl
   if (reduce_ms) *reduce_ms = b->reduce_ms;
   if (rhs_ms) *rhs_ms = b->rhs_ms;
   if (loglik_ms) *loglik_ms = b->loglik_ms;
+  return 0;
+}
+
+int gpmi_band_stats(gpmi_band* b, int* panel_fallbacks, int* panel_maxg) {
+  if (!b) return set_error(-1006, "null handle");
+  if (panel_fallbacks) *panel_fallbacks = b->panel_fallbacks;
+  if (panel_maxg) *panel_maxg = b->panel_maxg;
   return 0;
 }
 

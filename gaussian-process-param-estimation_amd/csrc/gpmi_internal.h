@@ -73,6 +73,7 @@ struct MsState {
   double* z_prev;  // [S][s]
   double* bp;      // [S][s'][s] b_c' . p_{j,c}
   double* g;       // [S][s'][s] accumulated G_j[c'][c]
+  int* flags;      // [1]   set when an active column meets p^T (K + eta_0 I) p <= 0
 };
 
 }  // namespace gpmi

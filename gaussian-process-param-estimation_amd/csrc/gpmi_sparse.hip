@@ -296,6 +296,8 @@ __global__ __launch_bounds__(256) void ms_r_update_kernel(double* __restrict__ R
   if (blockIdx.x == 0 && threadIdx.x < s) {
     const int c = threadIdx.x;
     st.a[c] = st.active[c] ? st.rr[c] / pq[c] : 0.0;
+    // negative curvature: K + eta_0 I is not positive definite
+    if (st.active[c] && !(pq[c] > 0.0)) st.flags[0] = 1;
   }
   if (e >= n * s) return;
   const int c = (int)(e % s);
@@ -395,6 +397,7 @@ __global__ void ms_init_kernel(MsState st, const double* __restrict__ partial, i
     st.beta[t] = 0.0;
     st.active[t] = br[s * s + t] > 0.0 ? 1 : 0;
   }
+  if (t == 0) st.flags[0] = 0;
 }
 
 }  // namespace gpmi

@@ -115,6 +115,7 @@ struct gpmi_sp {
   double* lz = nullptr;        // Lanczos scalars (lanczos_block)
   size_t lz_doubles = 0;
   size_t msbuf_doubles = 0;
+  int last_converged = 1;      // last gpmi_sp_cg / gpmi_sp_msgram met rtol in every column
 };
 
 namespace {
@@ -487,6 +488,8 @@ int gpmi_sp_cg(gpmi_sp* sp, double eta, const double* rhs, int64_t ld, int nrhs,
   Guard g(sp->device);
   const int64_t n = sp->n;
   int max_it_used = 0;
+  bool converged = true;
+  sp->last_converged = 0;
   for (int c0 = 0; c0 < nrhs; c0 += MAXS) {
     const int s = std::min(MAXS, nrhs - c0);
     const int64_t ns = n * s;
@@ -528,6 +531,8 @@ int gpmi_sp_cg(gpmi_sp* sp, double eta, const double* rhs, int64_t ld, int nrhs,
                             sp->stream));
       SP_TRY(hipStreamSynchronize(sp->stream));
       for (int c = 0; c < s; ++c) {
+        if (!done[c] && !(pq[c] > 0.0))
+          return set_error(1, "CG: p^T (K + eta I) p <= 0 (K + eta I is not positive definite)");
         const double a = done[c] ? 0.0 : rr[c] / pq[c];
         ha[c] = a;
         hb[c] = 1.0;
@@ -559,12 +564,15 @@ int gpmi_sp_cg(gpmi_sp* sp, double eta, const double* rhs, int64_t ld, int nrhs,
       SP_LAUNCH("col_axpby_kernel");
     }
     max_it_used = std::max(max_it_used, it);
+    for (int c = 0; c < s; ++c)
+      if (!(std::sqrt(rr[c]) <= rtol * bn[c])) converged = false;
     SP_TRY(hipMemcpyAsync(h.data(), X, sizeof(double) * ns, hipMemcpyDeviceToHost, sp->stream));
     SP_TRY(hipStreamSynchronize(sp->stream));
     for (int64_t i = 0; i < n; ++i)
       for (int c = 0; c < s; ++c) sol[i * ldsol + c0 + c] = h[(size_t)i * s + c];
   }
   if (iterations) *iterations = max_it_used;
+  sp->last_converged = converged ? 1 : 0;
   return 0;
 }
 
@@ -583,7 +591,7 @@ int gpmi_sp_msgram(gpmi_sp* sp, const double* etas, int neta, const double* rhs,
   const int ne = s * s + s;
   rc = ensure_partial(sp, (size_t)NBLK * std::max(ne, s));
   if (rc) return rc;
-  const size_t need = (size_t)6 * s + 2 * (size_t)S * s + 2 * (size_t)S * s * s + S + s + s;
+  const size_t need = (size_t)6 * s + 2 * (size_t)S * s + 2 * (size_t)S * s * s + S + s + s + 1;
   if (sp->msbuf_doubles < need) {
     if (sp->msbuf) SP_TRY(hipFree(sp->msbuf));
     sp->msbuf = nullptr;
@@ -605,6 +613,9 @@ int gpmi_sp_msgram(gpmi_sp* sp, const double* etas, int neta, const double* rhs,
   double* dshift = q; q += S;
   double* beta_out = q; q += s;
   st.active = reinterpret_cast<int*>(q);   // s ints in s doubles
+  q += s;
+  st.flags = reinterpret_cast<int*>(q);    // 1 int in 1 double
+  sp->last_converged = 0;
   double* Bd = sp->ws;
   double* Rd = Bd + ns;
   double* Pd = Rd + ns;
@@ -629,13 +640,23 @@ int gpmi_sp_msgram(gpmi_sp* sp, const double* etas, int neta, const double* rhs,
                      s);
   SP_LAUNCH("ms_init_kernel");
   int it = 0;
-  std::vector<int> hact(s);
+  std::vector<int> hact(2 * s + 2);
+  auto poll = [&](bool* any) -> int {
+    // active[0..s) and flags[0] (2 doubles after active's s) in one copy
+    SP_TRY(hipMemcpyAsync(hact.data(), st.active, sizeof(int) * (2 * s + 2), hipMemcpyDeviceToHost,
+                          str));
+    SP_TRY(hipStreamSynchronize(str));
+    *any = false;
+    for (int c = 0; c < s; ++c) *any = *any || hact[c];
+    return hact[2 * s] ? set_error(1, "multi-shift CG: p^T (K + min(eta) I) p <= 0 (not positive "
+                                      "definite)")
+                       : 0;
+  };
   for (; it < maxiter; ++it) {
     if (it % 8 == 0) {
-      SP_TRY(hipMemcpyAsync(hact.data(), st.active, sizeof(int) * s, hipMemcpyDeviceToHost, str));
-      SP_TRY(hipStreamSynchronize(str));
       bool any = false;
-      for (int c = 0; c < s; ++c) any = any || hact[c];
+      rc = poll(&any);
+      if (rc) return rc;
       if (!any) break;
     }
     rc = spmm(sp, Pd, Qd, s, eta0);
@@ -654,11 +675,23 @@ int gpmi_sp_msgram(gpmi_sp* sp, const double* etas, int neta, const double* rhs,
                        st.active, n, s);
     SP_LAUNCH("ms_p_update_kernel");
   }
+  {
+    bool any = false;
+    rc = poll(&any);
+    if (rc) return rc;
+    sp->last_converged = any ? 0 : 1;
+  }
   std::vector<double> hg((size_t)S * s * s);
   SP_TRY(hipMemcpyAsync(hg.data(), st.g, sizeof(double) * hg.size(), hipMemcpyDeviceToHost, str));
   SP_TRY(hipStreamSynchronize(str));
   std::copy(hg.begin(), hg.end(), G);
   if (iterations) *iterations = it;
+  return 0;
+}
+
+int gpmi_sp_last_status(const gpmi_sp* sp, int* converged) {
+  if (!sp) return set_error(-1006, "null handle");
+  if (converged) *converged = sp->last_converged;
   return 0;
 }
 

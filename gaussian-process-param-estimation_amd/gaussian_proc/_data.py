@@ -26,8 +26,8 @@ def generate_data(points, noise_magnitude):
     return z + noise_magnitude * numpy.random.RandomState(31).randn(points.shape[0])
 
 
-def generate_basis_functions(points, polynomial_degree=2):
-    d = points.shape[1]
+def generate_basis_functions(points, polynomial_degree=2, trigonometric=False):
+    n, d = points.shape
     grids = numpy.meshgrid(*([numpy.arange(polynomial_degree + 1)] * d))
     powers = numpy.array([g.ravel() for g in grids])
     powers = powers[:, powers.sum(axis=0) <= polynomial_degree]
@@ -35,4 +35,12 @@ def generate_basis_functions(points, polynomial_degree=2):
     for j in range(powers.shape[1]):
         for i in range(d):
             X[:, j] *= points[:, i] ** powers[i, j]
+    if trigonometric:
+        # reference :175-183, its column index quirk included (i + 0 / i + 1
+        # overlap for d > 1, so sin of axis i is overwritten by cos of axis i - 1)
+        T = numpy.empty((n, 2 * d))
+        for i in range(d):
+            T[:, i] = numpy.sin(points[:, i] * numpy.pi)
+            T[:, i + 1] = numpy.cos(points[:, i] * numpy.pi)
+        X = numpy.c_[X, T]
     return X

@@ -87,6 +87,8 @@ SIGNATURES = {
     'gpmi_band_der_terms': (ctypes.c_int, [c_op_p, c_double_p, ctypes.c_int, c_double_p,
                                            c_double_p, c_double_p, c_double_p, c_int_p]),
     'gpmi_band_der_ms': (ctypes.c_int, [c_op_p, c_double_p]),
+    'gpmi_band_stats': (ctypes.c_int, [c_op_p, c_int_p, c_int_p]),
+    'gpmi_sp_last_status': (ctypes.c_int, [c_op_p, c_int_p]),
     'gpmi_band_last_timing': (ctypes.c_int, [c_op_p, c_double_p, c_double_p, c_double_p]),
 }
 
@@ -384,6 +386,13 @@ class Band(object):
                 g[q][i:i + k] = gk[q]
         return ld, g[0], g[1], g[2], info
 
+    def stats(self):
+        """-> dict(panel_fallbacks, panel_maxg) (see gpmi_band_stats)."""
+        fb, mg = ctypes.c_int(), ctypes.c_int()
+        check(self.lib.gpmi_band_stats(self.h, ctypes.byref(fb), ctypes.byref(mg)),
+              'gpmi_band_stats')
+        return dict(panel_fallbacks=fb.value, panel_maxg=mg.value)
+
     def der_ms(self):
         v = ctypes.c_double()
         check(self.lib.gpmi_band_der_ms(self.h, ctypes.byref(v)), 'gpmi_band_der_ms')
@@ -527,6 +536,7 @@ class SparseOperator(object):
                                   float(rtol), maxiter, dptr(X), X.shape[1], ctypes.byref(it)),
               'gpmi_sp_cg')
         self.last_cg_iterations = it.value
+        self._warn_unconverged('cg', maxiter)
         return X[:, 0] if B.ndim == 1 else X
 
     MS_MAXS = 16
@@ -549,5 +559,16 @@ class SparseOperator(object):
                                           maxiter, dptr(Gj), ctypes.byref(it)),
                   'gpmi_sp_msgram')
             G[j0:j0 + e.size] = Gj
+            self._warn_unconverged('msgram', maxiter)
         self.last_cg_iterations = it.value
         return G
+
+    def _warn_unconverged(self, what, maxiter):
+        """scipy's cg (the reference's sparse solve, _linear_solver.py:64,68)
+        returns an unconverged iterate silently; here it is a RuntimeWarning."""
+        ok = ctypes.c_int(1)
+        check(self.lib.gpmi_sp_last_status(self.h, ctypes.byref(ok)), 'gpmi_sp_last_status')
+        if not ok.value:
+            import warnings
+            warnings.warn('%s: CG stopped at maxiter=%d before reaching rtol' % (what, maxiter),
+                          RuntimeWarning, stacklevel=3)

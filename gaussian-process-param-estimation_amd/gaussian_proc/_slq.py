@@ -33,9 +33,28 @@ def nodes(alpha, beta):
     return out
 
 
-def quadrature(node_list, etas, fn):
+def min_ritz(node_list):
+    """Smallest Ritz value over the probes (inf for none)."""
+    return min((float(t.min()) for t, _ in node_list), default=numpy.inf)
+
+
+def check_shifts(theta_min, etas):
+    """Every K + eta I must be positive definite. Ritz values lie inside
+    [lambda_min, lambda_max] of K, so theta_min + eta <= 0 proves that
+    K + eta I is not (the tapered Matern is indefinite): raise
+    numpy.linalg.LinAlgError, as scipy's posv does on a dense non-SPD matrix."""
+    etas = numpy.atleast_1d(numpy.asarray(etas, dtype=float))
+    if etas.size and not theta_min + etas.min() > 0.0:
+        raise numpy.linalg.LinAlgError(
+            'K + eta I is not positive definite for eta = %r: a Lanczos Ritz value of K '
+            'is %r (choose eta > |lambda_min(K)|)' % (float(etas.min()), theta_min))
+
+
+def quadrature(node_list, etas, fn, check=True):
     """Per-probe sums sum_i tau_i^2 fn(theta_i + eta) -> [nprobe, neta]."""
     etas = numpy.atleast_1d(numpy.asarray(etas, dtype=float))
+    if check:
+        check_shifts(min_ritz(node_list), etas)
     q = numpy.empty((len(node_list), etas.size))
     for p, (theta, w) in enumerate(node_list):   # all eta of a probe in one array op
         q[p] = numpy.sum(w[None, :] * fn(theta[None, :] + etas[:, None]), axis=1)

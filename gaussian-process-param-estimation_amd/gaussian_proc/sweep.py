@@ -94,23 +94,33 @@ def slq_sweep(K_mixed, etas, group=None):
             dist = None
     lo, hi, per = shard(s, world, rank)
     names = ('logdet', 'traceinv', 'traceinv2')
-    local = numpy.zeros((per, len(names), etas.size))
+    # per probe row: the quadratures, then the smallest Ritz value (the SPD check
+    # runs after the all-gather, on every rank alike: no rank raises alone)
+    nq = len(names) * etas.size
+    local = numpy.zeros((per, nq + 1))
+    local[:, nq] = numpy.inf
     if hi > lo:
         a, b = K_mixed.sop.lanczos(hi - lo, K_mixed.lanczos_degree, K_mixed.seed,
                                    probe_offset=lo)
         nodes = _slq.nodes(a, b)
+        q = numpy.empty((hi - lo, len(names), etas.size))
         for f, name in enumerate(names):
-            local[:hi - lo, f] = _slq.quadrature(nodes, etas, _slq.FUNCS[name])
+            with numpy.errstate(invalid='ignore', divide='ignore'):
+                q[:, f] = _slq.quadrature(nodes, etas, _slq.FUNCS[name], check=False)
+        local[:hi - lo, :nq] = q.reshape(hi - lo, nq)
+        local[:hi - lo, nq] = [float(t.min()) for t, _ in nodes]
     if dist is not None and world > 1:
         import torch
         backend = dist.get_backend(group)
         dev = torch.device('cuda', torch.cuda.current_device()) if backend == 'nccl' \
             else torch.device('cpu')
-        t_local = torch.from_numpy(local.reshape(per, -1)).to(dev)
+        t_local = torch.from_numpy(local).to(dev)
         parts = [torch.empty_like(t_local) for _ in range(world)]
         dist.all_gather(parts, t_local, group=group)
-        allq = torch.cat(parts).cpu().numpy().reshape(world * per, len(names), etas.size)[:s]
+        allv = torch.cat(parts).cpu().numpy()[:s]
     else:
-        allq = local[:s]
+        allv = local[:s]
+    _slq.check_shifts(float(allv[:, nq].min()), etas)
+    allq = allv[:, :nq].reshape(s, len(names), etas.size)
     n = K_mixed.n
     return {name: n * allq[:, f].mean(axis=0) for f, name in enumerate(names)}

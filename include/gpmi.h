@@ -175,6 +175,13 @@ int gpmi_sp_cg(gpmi_sp* sp, double eta, const double* rhs, int64_t ld, int nrhs,
 int gpmi_sp_msgram(gpmi_sp* sp, const double* etas, int neta, const double* rhs, int64_t ld,
                    int nrhs, double rtol, int maxiter, double* G, int* iterations);
 
+/* Whether the last gpmi_sp_cg / gpmi_sp_msgram met rtol in every column before
+ * maxiter (1) or stopped at maxiter (0). scipy's cg, which the reference calls
+ * (_linear_solver.py:64,68), returns the unconverged iterate silently; the
+ * Python layer warns. (A non-positive p^T A p makes those calls return 1, "not
+ * positive definite".) */
+int gpmi_sp_last_status(const gpmi_sp* sp, int* converged);
+
 /* Device-resident SpMM timing: reps launches of Y = (K + eta I) X with an
  * [n][s] block already in HBM; average ms per launch (HIP events). */
 int gpmi_sp_bench_spmm(gpmi_sp* sp, int s, int reps, double eta, double* avg_ms);
@@ -230,6 +237,12 @@ int gpmi_band_loglik(gpmi_band* b, const double* etas, int neta, double* logdet,
  * dense solves per eta. Any output pointer may be NULL. */
 int gpmi_band_der_terms(gpmi_band* b, const double* etas, int neta, double* logdet,
                         double* g1, double* g2, double* g3, int* info);
+
+/* Reduction diagnostics: how many reductions of this band fell back to the
+ * per-column panel launches after a timed-out single-launch panel hand-off, and
+ * the largest panel grid (workgroups) run as one launch on this device
+ * (CU count x resident hh_panel workgroups per CU, at most 128). */
+int gpmi_band_stats(gpmi_band* b, int* panel_fallbacks, int* panel_maxg);
 
 /* Device ms of the last gpmi_band_der_terms call (HIP events). */
 int gpmi_band_der_ms(gpmi_band* b, double* der_ms);

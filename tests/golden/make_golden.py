@@ -16,6 +16,7 @@ Recipe:
 
 Outputs are data only (inputs and expected outputs). The reference never
 travels with the repo. Run:  python tests/golden/make_golden.py [--big]
+                             python tests/golden/make_golden.py --only <fixture>
 """
 
 import argparse
@@ -192,12 +193,28 @@ def config_case(R, name, num_points, dim, nu, scale=0.1, full_arrays=False,
         import io
         import contextlib
         buf = io.StringIO()
+        calls = []
+        der1 = PL.log_likelihood_der1_eta
+
+        def traced(z_, X_, K_, log_eta):
+            v = der1(z_, X_, K_, log_eta)
+            calls.append([f(log_eta), f(v)])
+            return v
         with contextlib.redirect_stdout(buf):
-            rd = R['Likelihood'](X, K, 'direct').maximize_log_likelihood(z)
-            rp = R['Likelihood'](X, K, 'profiled').maximize_log_likelihood(z)
-        out['maximize_direct'] = {k: f(v) for k, v in rd.items()}
+            if optimize != 'profiled':
+                rd = R['Likelihood'](X, K, 'direct').maximize_log_likelihood(z)
+                out['maximize_direct'] = {k: f(v) for k, v in rd.items()}
+            PL.log_likelihood_der1_eta = staticmethod(traced)
+            try:
+                rp = R['Likelihood'](X, K, 'profiled').maximize_log_likelihood(z)
+            finally:
+                PL.log_likelihood_der1_eta = staticmethod(der1)
         out['maximize_profiled'] = {k: (f(v) if not isinstance(v, bool) else v)
                                     for k, v in rp.items()}
+        # the (log10 eta, der1) sequence the reference driver evaluated:
+        # bracket search, then Chandrupatla (_profile_likelihood.py:244-350)
+        out['maximize_profiled_der1_calls'] = calls
+        out['maximize_profiled_bracket_found'] = 'Iter' in buf.getvalue()
     return out, arrays
 
 
@@ -249,17 +266,100 @@ def sparse_cases(R, big=False):
     return meta, arrays
 
 
-def big_case(R):
-    """N=16384 (2D 128x128 grid, nu=1.5): 'cholesky' imate method (3 dense
-    factorizations per lp) — the eigenvalue method needs a 227 s eigh."""
+class _SpluOperator(object):
+    """Exact sparse K + eta I for the reference's likelihood code: logdet from
+    scipy's SuperLU factor (sum log|U_ii|; K + eta I is SPD for the eta used),
+    solve by the same factor. Stands in for imate's sparse Cholesky (CHOLMOD,
+    absent here)."""
+
+    def __init__(self, K):
+        import scipy.sparse
+        self.K = K.tocsc()
+        self.n = K.shape[0]
+        self.I = scipy.sparse.eye(self.n, format='csc')
+        self._lu = {}
+
+    def _factor(self, eta):
+        import scipy.sparse.linalg
+        if eta not in self._lu:
+            self._lu = {eta: scipy.sparse.linalg.splu(self.K + eta * self.I,
+                                                      permc_spec='COLAMD')}
+        return self._lu[eta]
+
+    def get_matrix_size(self):
+        return self.n
+
+    def logdet(self, eta, exponent=1):
+        lu = self._factor(eta)
+        d = lu.U.diagonal()
+        assert numpy.all(d > 0) and numpy.all(lu.L.diagonal() == 1.0)
+        return exponent * float(numpy.sum(numpy.log(d)))
+
+    def solve(self, eta, Y):
+        return self._factor(eta).solve(numpy.asarray(Y, dtype=float))
+
+
+def sparse_big_case(R, name, npts, d, rho, nu, dens, etas_above, hypers=True):
+    """A BASELINE sparse config at full size: the reference generator (+ the 2
+    argument fixes) builds K; lambda_min by ARPACK; for eta above |lambda_min|
+    the exact logdet and Gram [X z]^T (K + eta I)^-1 [X z] by SuperLU, and the
+    reference DirectLikelihood.log_likelihood on that exact operator."""
+    import io
+    import contextlib
+    import time
+    import scipy.sparse.linalg
+    du = R['du']
+    pts = du.generate_points(npts, d, True)
+    z = du.generate_data(pts, 0.2)
+    X = du.generate_basis_functions(pts, 2)
+    t0 = time.time()
+    with contextlib.redirect_stdout(io.StringIO()):
+        K = R['gp'].generate_correlation(pts, rho, nu, True, sparse=True, density=dens)
+    K = K.tocsr()
+    K.sort_indices()
+    t_asm = time.time() - t0
+    n = K.shape[0]
+    out = dict(name=name, num_points=npts, dimension=d, correlation_scale=rho, nu=nu,
+               density=dens, n=n, m=X.shape[1], nnz=int(K.nnz),
+               data_sum=float(K.data.sum()), min_kept=float(K.data.min()),
+               diag_sum=float(K.diagonal().sum()), frob2=float(numpy.sum(K.data ** 2)),
+               reference_assembly_s=t_asm, note='reference + 2 arg fixes (SURVEY 0.4)')
+    ii = sample_idx(n)
+    out['sample_rows'] = ii.tolist()
+    out['row_sums_sample'] = numpy.asarray(K.sum(axis=1)).ravel()[ii].tolist()
+    out['row_nnz_sample'] = numpy.diff(K.indptr)[ii].tolist()
+    lam = scipy.sparse.linalg.eigsh(K, k=1, which='SA', tol=1e-8, return_eigenvectors=False)
+    out['lambda_min'] = float(lam[0])
+    if etas_above:
+        shift = abs(min(0.0, float(lam[0])))
+        etas = [shift + e for e in etas_above]
+        op = _SpluOperator(K)
+        Rm = numpy.column_stack([X, z])
+        out['etas'] = etas
+        out['logdet'] = []
+        out['gram'] = []
+        out['direct_lp'] = []
+        for e in etas:
+            out['logdet'].append(op.logdet(e))
+            out['gram'].append((Rm.T @ op.solve(e, Rm)).tolist())
+            # reference formula (_direct_likelihood.py:31-83) at sigma=1, sigma0=sqrt(eta)
+            out['direct_lp'].append(f(R['DL'].log_likelihood(z, X, op, False,
+                                                             [1.0, numpy.sqrt(e)])))
+    return out
+
+
+def big_case(R, nu=1.5):
+    """N=16384 (2D 128x128 grid; nu=1.5 the metric's kernel, nu=2.5 BASELINE
+    cfg3's): 'cholesky' imate method (3 dense factorizations per lp) — the
+    eigenvalue method needs a 227 s eigh."""
     du = R['du']
     pts = du.generate_points(128, 2, True)
     z = du.generate_data(pts, 0.2)
     X = du.generate_basis_functions(pts, 2)
-    K = R['gp'].generate_correlation(pts, 0.1, 1.5, True)
+    K = R['gp'].generate_correlation(pts, 0.1, nu, True)
     op = R['MC'](K, imate_method='cholesky')
     etas = [0.01, 1.0, 4.0]
-    out = dict(name='cfg3_n16384_nu1.5', n=16384, m=X.shape[1], nu=1.5,
+    out = dict(name='cfg3_n16384_nu%g' % nu, n=16384, m=X.shape[1], nu=nu,
                correlation_scale=0.1, K_sum=f(K.sum()),
                etas=etas, logdet=[f(op.logdet(e)) for e in etas],
                hypers=[[0.1, 0.2], [1.0, 0.1]])
@@ -273,7 +373,30 @@ def main():
     ap.add_argument('--big', action='store_true', help='also the N=16384 case (~5 min)')
     ap.add_argument('--sparse-only', action='store_true')
     ap.add_argument('--sparse-big', action='store_true', help='also config 4 (~5 min)')
+    ap.add_argument('--only', default=None,
+                    help='write only one fixture: cfg3_nu25 (~3 min), sparse_cfg4 (~10 min), '
+                         'sparse_cfg5 (~90 min), n1024 or cfg2_profiled')
     args = ap.parse_args()
+    if args.only:
+        R = import_reference()
+        if args.only == 'cfg3_nu25':
+            out = big_case(R, 2.5)
+        elif args.only == 'sparse_cfg4':
+            out = sparse_big_case(R, 'cfg4_n65536_2d', 256, 2, 0.005, 1.5, 1e-3,
+                                  [0.05, 0.5, 5.0])
+        elif args.only == 'sparse_cfg5':
+            out = sparse_big_case(R, 'cfg5_n262144_3d', 64, 3, 0.02, 1.5, 6e-4, [])
+        elif args.only == 'n1024':
+            out, _ = config_case(R, 'n1024_2d_nu2.5', 32, 2, 2.5, optimize=True)
+            args.only = 'n1024_nu25'
+        elif args.only == 'cfg2_profiled':
+            out, _ = config_case(R, 'cfg2_n4096_2d', 64, 2, 1.5, optimize='profiled')
+        else:
+            raise SystemExit('unknown fixture %r' % args.only)
+        with open(os.path.join(HERE, args.only + '.json'), 'w') as fh:
+            json.dump(out, fh, indent=1)
+        print('golden fixture written:', args.only)
+        return
     R = import_reference()
     smeta, sarr = sparse_cases(R, args.sparse_big)
     numpy.savez_compressed(os.path.join(HERE, 'sparse_small.npz'), **sarr)
@@ -293,12 +416,14 @@ def main():
     c2, _ = config_case(R, 'cfg2_n4096_2d', 64, 2, 1.5)
     with open(os.path.join(HERE, 'cfg2.json'), 'w') as fh:
         json.dump(c2, fh, indent=1)
-    c25, _ = config_case(R, 'n1024_2d_nu2.5', 32, 2, 2.5)
+    c25, _ = config_case(R, 'n1024_2d_nu2.5', 32, 2, 2.5, optimize=True)
     with open(os.path.join(HERE, 'n1024_nu25.json'), 'w') as fh:
         json.dump(c25, fh, indent=1)
     if args.big:
         with open(os.path.join(HERE, 'cfg3_big.json'), 'w') as fh:
             json.dump(big_case(R), fh, indent=1)
+        with open(os.path.join(HERE, 'cfg3_nu25.json'), 'w') as fh:
+            json.dump(big_case(R, 2.5), fh, indent=1)
     print('golden fixtures written to', HERE)
 
 

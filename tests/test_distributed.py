@@ -158,3 +158,45 @@ def test_eta_sweep_gloo_matches_single_process(world, neta):
     ref = MixedCorrelation(K, 'cholesky')
     for e, v in zip(etas, lp_ref):
         assert abs(v - olk.direct_lp(z, X, ref, [1.0, numpy.sqrt(e)])) <= 1e-10 * abs(v)
+
+
+def _slq_bad_worker(rank, world, port, etas, out_q):
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    from gaussian_proc.sweep import slq_sweep
+    K, _, _ = _problem()
+    try:
+        slq_sweep(_SparseMixed(K - 2.0 * numpy.eye(K.shape[0])), etas)
+        out_q.put((rank, 'returned'))
+    except numpy.linalg.LinAlgError:
+        out_q.put((rank, 'LinAlgError'))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_slq_sweep_rejects_eta_below_lambda_min_on_every_rank():
+    """K - 2I is indefinite (lambda_min(K) < 2): an eta grid reaching below
+    |lambda_min| must raise LinAlgError on every rank alike (the check runs after
+    the all-gather, so no rank is left waiting in a collective)."""
+    etas = numpy.array([0.5, 1.0, 4.0])
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_slq_bad_worker, args=(r, 2, port, etas, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert sorted(r for _, r in res) == ['LinAlgError', 'LinAlgError']
+
+
+def test_slq_quadrature_shift_check():
+    from gaussian_proc import _slq
+    nodes = [(numpy.array([-1.5, 0.2, 3.0]), numpy.array([0.2, 0.3, 0.5]))]
+    with pytest.raises(numpy.linalg.LinAlgError):
+        _slq.quadrature(nodes, [1.0, 2.0], _slq.FUNCS['logdet'])
+    q = _slq.quadrature(nodes, [1.6, 2.0], _slq.FUNCS['logdet'])
+    assert numpy.all(numpy.isfinite(q))

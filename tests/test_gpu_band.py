@@ -286,3 +286,26 @@ def test_band_refresh_with_rhs_matches_set_rhs(gp):
     op.refresh_band()
     ld2, G2 = op.loglik_terms(etas, X, z)
     numpy.testing.assert_array_equal(G0, G2)
+
+
+def test_panel_timeout_falls_back_to_per_column_launches(gp, monkeypatch):
+    """GPMI_HH_SPIN_LIMIT=0 turns the first unsuccessful hand-off poll of the
+    single-launch panel QR into a timeout (as when its workgroups cannot all be
+    resident): the reduction is redone with per-column launches, the result is
+    the same band form, and a later refresh starts clean (err flag reset)."""
+    K, X, z = _inputs(1000, 77)
+    ref = _mc(K)
+    ld_ref, G_ref = ref.loglik_terms([0.05, 2.0], X, z)
+    assert ref.band().stats()['panel_fallbacks'] == 0
+    assert ref.band().stats()['panel_maxg'] >= 8
+    monkeypatch.setenv('GPMI_HH_SPIN_LIMIT', '0')
+    op = _mc(K)
+    ld, G = op.loglik_terms([0.05, 2.0], X, z)
+    st = op.band().stats()
+    assert st['panel_fallbacks'] >= 1, st
+    assert rel(ld, ld_ref) < 1e-12
+    numpy.testing.assert_allclose(G, G_ref, rtol=1e-10, atol=1e-12)
+    op.refresh_band(X, z)
+    ld2, G2 = op.loglik_terms([0.05, 2.0], X, z)
+    assert rel(ld2, ld_ref) < 1e-12
+    assert op.band().stats()['panel_fallbacks'] >= 2
