@@ -2,15 +2,15 @@
 """Benchmark: log-likelihood evaluations / s on the N=16384 dense Matérn-3/2
 covariance (BASELINE.json metric), one process per GPU.
 
-A step = one block of ``--eta-per-rank`` (64) eta values per rank of the grid
-logspace(-3, 3, max(64, N * 64)) (at N=1 exactly the 64-point cfg3 curve; at
-N > 1 a finer grid over the same range, no eta repeated across ranks): one
-batched device call factorizes
-K + eta_b I (fp64 MFMA Cholesky, fused forward solve of [X | z], logdet and
-Gram), the host forms the direct log-likelihood (sigma = 1, sigma0 = sqrt(eta)),
-and ONE all-gather (RCCL over xGMI at N > 1) collects the [logdet, lp] curve.
-K is assembled on each GPU from the points before the timed region (inputs
-resident in HBM). Per-rank work is fixed: scaling "weak".
+A step = the cfg3 eta curve logspace(-3, 3, 64) (``--eta-total``), sharded over
+the ranks in contiguous blocks (64 / N eta per rank; strong scaling, BASELINE
+cfg3: "64-point eta sweep sharded over 8 x MI355X"): one batched device call per
+rank factorizes K + eta_b I (fp64 MFMA Cholesky, fused forward solve of [X | z],
+logdet and Gram), the host forms the direct log-likelihood (sigma = 1,
+sigma0 = sqrt(eta)), and ONE all-gather (RCCL over xGMI at N > 1) collects the
+[eta, logdet, lp] curve. K is assembled on each GPU from the points before the
+timed region (inputs resident in HBM). ``--scaling weak`` instead gives every
+rank ``--eta-per-rank`` eta of a finer grid (fixed per-rank work).
 
 Launch: python bench.py [--gpus 1 --steps K --warmup W]
         python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -42,9 +42,17 @@ def parse():
     ap.add_argument('--warmup', type=int, default=2)
     ap.add_argument('--grid', type=int, default=128, help='points per axis (n = grid^2)')
     ap.add_argument('--nu', type=float, default=1.5)
+    ap.add_argument('--scaling', default='strong', choices=['strong', 'weak'],
+                    help='strong: the --eta-total point curve split over the ranks (cfg3); '
+                         'weak: --eta-per-rank eta per rank of a finer grid')
+    ap.add_argument('--eta-total', type=int, default=64,
+                    help='strong scaling: eta values of the curve (cfg3: 64)')
     ap.add_argument('--eta-per-rank', type=int, default=64,
-                    help='eta values factorized together per device call (one step); at '
-                         'N=1 the default step is the whole 64-point eta curve')
+                    help='weak scaling: eta values factorized together per rank and step')
+    ap.add_argument('--cpu-samples', type=int, default=3,
+                    help='CPU baseline: timed evaluations per variant (after one warm-up)')
+    ap.add_argument('--cpu-budget-s', type=float, default=20.0,
+                    help='sparse CPU baseline: seconds of sampled CG work (extrapolated)')
     ap.add_argument('--outer', type=int, default=16, help='outer panel width / 128')
     ap.add_argument('--lookahead', type=int, default=0,
                     help='1: panel factorization on a second stream overlaps the bulk '
@@ -103,46 +111,181 @@ def pmc_traffic_sparse(config, kernel='gpmi::csr_spmm_kernel'):
     return (2.0 * pd['FETCH_SIZE'] + pd['WRITE_SIZE']) * 1024.0, os.path.relpath(files[-1], REPO)
 
 
-def cpu_baseline(points, z, X, nu, etas):
-    """The reference's CPU call pattern, timed on this host (rank 0, N=1):
-    Likelihood -> MixedCorrelation(imate_method='eigenvalue') -> per eval
-    2 x scipy.linalg.solve(K + eta I, ., assume_a='pos') + O(n) eigen logdet
-    (_direct_likelihood.py:59-71, mixed_correlation.py:239-299). Sample: ONE
-    evaluation at the full N (the one-time eigh setup is excluded and reported
-    separately as not timed). Uses the oracle restatement (kind 'port')."""
-    from oracle import matern
-    import scipy.linalg
-    try:
-        from threadpoolctl import threadpool_info
-        threads = max([i.get('num_threads', 1) for i in threadpool_info()
-                       if i.get('user_api') == 'blas'] or [os.cpu_count()])
-    except Exception:
-        threads = os.cpu_count()
-    K = matern.dense_correlation(points, 0.1, nu)
-    eta = float(etas[0])
-    n = K.shape[0]
-    t0 = time.perf_counter()
-    Kn = K.copy()
-    Kn[numpy.diag_indices(n)] += eta
-    Y = scipy.linalg.solve(Kn, X, assume_a='pos')          # solve(eta, X)  :62
-    Kn = K.copy()
-    Kn[numpy.diag_indices(n)] += eta
-    w = scipy.linalg.solve(Kn, z, assume_a='pos')          # solve(eta, z)  :332
-    _ = (X.T @ Y, w)
-    dt = time.perf_counter() - t0
-    cpu = platform.processor() or platform.machine()
+def host_info():
+    """The host the CPU baseline runs on: model, logical CPUs, physical cores,
+    and the CPUs this job may use (affinity, cgroup quota, OMP_NUM_THREADS: the
+    GPU box gives one GPU's job a share of the machine, 16 CPUs)."""
+    info = {'logical_cpus': os.cpu_count(), 'cpu_model': platform.processor() or
+            platform.machine()}
+    phys = set()
     try:
         with open('/proc/cpuinfo') as fh:
+            pid = cid = None
             for line in fh:
                 if line.startswith('model name'):
-                    cpu = line.split(':', 1)[1].strip()
-                    break
+                    info['cpu_model'] = line.split(':', 1)[1].strip()
+                elif line.startswith('physical id'):
+                    pid = line.split(':', 1)[1].strip()
+                elif line.startswith('core id'):
+                    cid = line.split(':', 1)[1].strip()
+                elif not line.strip() and cid is not None:
+                    phys.add((pid, cid))
+                    pid = cid = None
     except OSError:
         pass
-    return {'value': 1.0 / dt, 'unit': 'evals/s', 'cores': int(threads), 'kind': 'port',
-            'sample': 'one direct log-likelihood eval at N=%d (2 x scipy.linalg.solve '
-                      'assume_a=pos, eigen-logdet setup excluded), %.1f s; host %s, '
-                      'os.cpu_count()=%d' % (n, dt, cpu, os.cpu_count())}
+    info['physical_cores'] = len(phys) or None
+    try:
+        info['affinity_cpus'] = len(os.sched_getaffinity(0))
+    except AttributeError:
+        info['affinity_cpus'] = os.cpu_count()
+    quota = None
+    for path in ('/sys/fs/cgroup/cpu.max', '/sys/fs/cgroup/cpu/cpu.cfs_quota_us'):
+        try:
+            with open(path) as fh:
+                parts = fh.read().split()
+            if path.endswith('cpu.max') and parts[0] != 'max':
+                quota = int(parts[0]) / float(parts[1])
+            elif path.endswith('quota_us') and int(parts[0]) > 0:
+                with open('/sys/fs/cgroup/cpu/cpu.cfs_period_us') as fh:
+                    quota = int(parts[0]) / float(fh.read().split()[0])
+            break
+        except (OSError, ValueError, IndexError):
+            continue
+    info['cgroup_cpu_quota'] = quota
+    usable = info['affinity_cpus']
+    if quota:
+        usable = min(usable, max(1, int(quota)))
+    omp = os.environ.get('OMP_NUM_THREADS')
+    if omp and omp.isdigit() and int(omp) > 0:
+        usable = min(usable, int(omp))
+    info['job_cpus'] = usable
+    return info
+
+
+def log(msg):
+    """Progress on stderr (the JSON result is the only stdout line)."""
+    sys.stderr.write('[bench] %s\n' % msg)
+    sys.stderr.flush()
+
+
+def _timed(fn, reps, what=None):
+    out = []
+    for r in range(reps):
+        t0 = time.perf_counter()
+        v = fn()
+        out.append((time.perf_counter() - t0, v))
+        if what:
+            log('%s %d/%d: %.2f s' % (what, r + 1, reps, out[-1][0]))
+    return out
+
+
+def cpu_baseline(points, z, X, nu, eta, lam=None, samples=3):
+    """The reference's CPU call pattern, timed on this host (rank 0, N=1), by
+    the oracle restatement (kind 'port'; the reference itself never travels):
+    DirectLikelihood.log_likelihood (_direct_likelihood.py:31-83) at
+    (sigma, sigma0) = (1, sqrt(eta)) on
+      * the 'eigenvalue' operator Likelihood builds (likelihood.py:41):
+        O(n) eigen-logdet + 2 x scipy.linalg.solve(K + eta I, ., assume_a='pos')
+        (mixed_correlation.py:239-248,280-299); the one-time eigh(K) setup
+        (:76-79; 227 s at this N on 8 cores) is excluded. Its eigenvalues are
+        the device's (lam) when given, so the CPU lp is comparable;
+      * the 'cholesky' variant: a third factorization for logdet (:250-261).
+    BLAS threads = every CPU this job may use (host_info); one warm-up eval,
+    then the median of ``samples`` evals per variant."""
+    from oracle import matern
+    from oracle import likelihood as olk
+    from oracle.mixed_correlation import MixedCorrelation as OracleMC
+    from threadpoolctl import threadpool_limits, threadpool_info
+    info = host_info()
+    threads = info['job_cpus']
+    log('cpu baseline: host %s, %d job CPUs; assembling K' % (info['cpu_model'], threads))
+    K = matern.dense_correlation(points, 0.1, nu)
+    n = K.shape[0]
+    hp = [1.0, float(numpy.sqrt(eta))]
+    with threadpool_limits(limits=threads, user_api='blas'):
+        blas = [(i.get('internal_api'), i.get('num_threads')) for i in threadpool_info()
+                if i.get('user_api') == 'blas']
+        eig = OracleMC(K, 'cholesky')
+        eig.imate_method = 'eigenvalue'
+        eig.K_eigenvalues = numpy.asarray(lam, dtype=float) if lam is not None else numpy.ones(n)
+        chol = OracleMC(K, 'cholesky')
+        warm = _timed(lambda: olk.direct_lp(z, X, eig, hp), 1, 'cpu warm-up eval')
+        te = _timed(lambda: olk.direct_lp(z, X, eig, hp), samples, 'cpu eigenvalue-operator eval')
+        tc = _timed(lambda: olk.direct_lp(z, X, chol, hp), samples, 'cpu cholesky-variant eval')
+    med_e = float(numpy.median([t for t, _ in te]))
+    med_c = float(numpy.median([t for t, _ in tc]))
+    out = {'value': 1.0 / med_e, 'unit': 'evals/s', 'cores': int(threads), 'kind': 'port',
+           'sample': 'DirectLikelihood.log_likelihood at N=%d, eta=%g: median of %d evals after '
+                     '1 warm-up, eigenvalue operator (eigen-logdet + 2 x '
+                     'scipy.linalg.solve(assume_a=pos); one-time eigh excluded), BLAS threads=%d'
+                     % (n, eta, samples, threads),
+           'median_s': round(med_e, 3), 'samples_s': [round(t, 3) for t, _ in te],
+           'warmup_s': round(warm[0][0], 3),
+           'cholesky_variant': {'value': 1.0 / med_c, 'unit': 'evals/s', 'median_s':
+                                round(med_c, 3), 'samples_s': [round(t, 3) for t, _ in tc],
+                                'step': '3 factorizations per eval (logdet + 2 solves)'},
+           'threads': int(threads), 'blas': blas, 'host': info}
+    if info.get('physical_cores'):
+        # what every physical core of the host could do at perfect BLAS scaling
+        # (an upper bound for the CPU; the box gives this job job_cpus of them)
+        out['all_physical_cores_upper_bound'] = {
+            'cores': info['physical_cores'],
+            'value': out['value'] * info['physical_cores'] / float(threads),
+            'note': 'linear extrapolation from %d to %d cores (optimistic for the CPU)'
+                    % (threads, info['physical_cores'])}
+    if lam is not None:
+        out['lp_eigen'] = float(te[0][1])
+    out['lp_cholesky'] = float(tc[0][1])
+    return out
+
+
+def cpu_baseline_sparse(K, X, z, etas, nprobe, steps, seed, budget_s):
+    """Restated reference pattern for a sparse K on scipy (the shipped sparse
+    path cannot run: SURVEY 0.4): stochastic Lanczos quadrature with the SAME
+    counter-based probes as the device (oracle.sparse.slq: CSR SpMV Lanczos,
+    CGS2) for logdet at every eta, and per eta the reference's solves of X and
+    z column by column with scipy.sparse.linalg.cg, rtol 1e-6
+    (_linear_solver.py:57-68). Bounded sample: all probes' Lanczos, then CG
+    columns of spread eta until ``budget_s`` is spent, extrapolated to the whole
+    grid. scipy's CSR SpMV is single-threaded: cores = 1."""
+    import scipy.sparse
+    import scipy.sparse.linalg
+    from oracle import sparse as osp
+    n = K.shape[0]
+    t0 = time.perf_counter()
+    P = osp.rademacher_probes(n, nprobe, seed)
+    slq = osp.slq(K, etas, P, steps)
+    t_slq = time.perf_counter() - t0
+    log('cpu SLQ (%d probes): %.1f s' % (nprobe, t_slq))
+    R = numpy.column_stack([X, z])
+    order = numpy.argsort(numpy.arange(etas.size) % 4, kind='stable')   # spread etas
+    done, t_cg, its = 0, 0.0, []
+    eye = scipy.sparse.identity(n, format='csr')
+    for j in order:
+        A = (K + etas[j] * eye).tocsr()
+        for c in range(R.shape[1]):
+            cnt = [0]
+            t1 = time.perf_counter()
+            scipy.sparse.linalg.cg(A, R[:, c], rtol=1e-6, atol=0.0,
+                                   callback=lambda xk: cnt.__setitem__(0, cnt[0] + 1))
+            t_cg += time.perf_counter() - t1
+            its.append(cnt[0])
+            done += 1
+            log('cpu CG solve %d: %d iterations, %.1f s total' % (done, cnt[0], t_cg))
+            if t_cg > budget_s:
+                break
+        if t_cg > budget_s:
+            break
+    per_solve = t_cg / done
+    total = t_slq + per_solve * etas.size * R.shape[1]
+    return {'value': etas.size / total, 'unit': 'evals/s', 'cores': 1, 'kind': 'port',
+            'sample': 'SLQ of all %d probes x %d Lanczos steps (%.1f s, same probes as the '
+                      'device) + %d of %d CG solves (rtol 1e-6, %.1f s, mean %.0f iterations), '
+                      'extrapolated to the %d-eta grid' % (nprobe, steps, t_slq, done,
+                                                           etas.size * R.shape[1], t_cg,
+                                                           numpy.mean(its), etas.size),
+            'slq_s': round(t_slq, 3), 'cg_s_per_solve': round(per_solve, 4),
+            'est_s_per_step': round(total, 2), 'logdet': slq['logdet'].tolist()}
 
 
 SPARSE_CONFIGS = {
@@ -174,17 +317,21 @@ def run_sparse(args, world, rank, local, dist, torch):
     op = MixedCorrelation(D, imate_method='slq',
                           imate_options={'num_samples': nprobe, 'lanczos_degree': steps})
     # eta grid above |lambda_min| (the tapered matrix is indefinite): smallest Ritz
-    # value over the probes of a pilot Lanczos
-    a, b = op.sop.lanczos(4, steps, 99)
+    # value over the SLQ probes' own Lanczos (Ritz values converge to lambda_min
+    # from above: 10 % margin; the SLQ shift check and the CG curvature check
+    # raise LinAlgError if K + eta I is still not positive definite)
     from gaussian_proc import _slq
-    theta_min = min(float(t.min()) for t, _ in _slq.nodes(a, b))
+    theta_min = _slq.min_ritz(op.slq_nodes())
     shift = max(0.0, -1.1 * theta_min)
     etas = numpy.logspace(-2, 2, neta) + shift
     R = numpy.column_stack([X, z])
     lo, hi, per = shard(neta, world, rank)
 
+    holder = {}
+
     def step():
         curves = slq_sweep(op, etas)
+        holder['curves'] = curves
         rows = numpy.zeros((per, 3))
         if hi > lo:
             # all Gram blocks of the eta shard from one multi-shift CG (rtol 1e-6)
@@ -254,55 +401,135 @@ def run_sparse(args, world, rank, local, dist, torch):
             'lp_sample': [float(v) for v in last[0].tolist()],
             'cpu_baseline': None,
         }
+        ref = sparse_reference_check(op, args.config, X, z)
+        if ref:
+            res['reference_check'] = ref
+        if world == 1 and not args.no_cpu_baseline:
+            cb = cpu_baseline_sparse(op.sop.csr(), X, z, etas, nprobe, steps, op.seed,
+                                     args.cpu_budget_s)
+            dev = holder['curves']['logdet']
+            cb['slq_logdet_rel_diff_vs_device_same_probes'] = float(
+                numpy.max(numpy.abs(numpy.asarray(cb.pop('logdet')) - dev) / numpy.abs(dev)))
+            res['cpu_baseline'] = cb
+            res['speedup_vs_cpu'] = round(res['value'] / cb['value'], 1)
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
 
 
-def golden_logdet_err(op_logdet_fn, nu, n):
-    """max relative error of logdet(K + eta I) vs the reference's own values
-    (tests/golden/cfg3_big.json: eigh/Cholesky of the reference at N=16384,
-    nu=1.5, etas 0.01, 1, 4); None for other configurations."""
-    path = os.path.join(REPO, 'tests', 'golden', 'cfg3_big.json')
-    if n != 16384 or nu != 1.5 or not os.path.isfile(path):
+def sparse_reference_check(op, config, X, z):
+    """BASELINE cfg4 against the reference's own exact values
+    (tests/golden/sparse_cfg4.json: reference generator + the 2 argument fixes,
+    SuperLU logdet and Gram at three eta above |lambda_min|): the device CSR
+    (nnz, sum), the multi-shift CG Gram blocks (rtol 1e-10) and the SLQ logdet
+    with its Monte-Carlo standard error over the probes."""
+    from gaussian_proc import _slq
+    name = {'sparse4': 'sparse_cfg4.json', 'sparse5': 'sparse_cfg5.json'}[config]
+    path = os.path.join(REPO, 'tests', 'golden', name)
+    if not os.path.isfile(path):
         return None
     with open(path) as fh:
-        cfg = json.load(fh)
-    ld = numpy.asarray(op_logdet_fn(cfg['etas']))
-    ref = numpy.asarray(cfg['logdet'])
-    return float(numpy.max(numpy.abs(ld - ref) / numpy.abs(ref)))
+        g = json.load(fh)
+    out = {'fixture': name, 'nnz_equal': op.sop.nnz == g['nnz'],
+           'data_sum_rel_err': abs(float(op.sop.csr().data.sum()) - g['data_sum']) /
+           g['data_sum']}
+    if 'etas' in g:
+        R = numpy.column_stack([X, z])
+        G = op.sop.msgram(g['etas'], R, rtol=1e-10)
+        out['gram_rel_err'] = float(max(numpy.max(numpy.abs(Gj - numpy.asarray(Gr))) /
+                                        numpy.max(numpy.abs(Gr)) for Gj, Gr in zip(G, g['gram'])))
+        q = _slq.quadrature(op.slq_nodes(), g['etas'], _slq.FUNCS['logdet']) * op.n
+        est, se = q.mean(axis=0), q.std(axis=0, ddof=1) / numpy.sqrt(q.shape[0])
+        out['slq_logdet_err_in_std_errors'] = [round(float(v), 3) for v in
+                                               numpy.abs(est - g['logdet']) / se]
+    return out
+
+
+def golden_case(nu, n):
+    """The reference's own N=16384 values for this kernel (tests/golden:
+    cfg3_big.json nu=1.5, cfg3_nu25.json nu=2.5; 'cholesky' imate method, made
+    by tests/golden/make_golden.py), or None."""
+    name = {1.5: 'cfg3_big.json', 2.5: 'cfg3_nu25.json'}.get(nu)
+    path = os.path.join(REPO, 'tests', 'golden', name) if name else None
+    if n != 16384 or path is None or not os.path.isfile(path):
+        return None
+    with open(path) as fh:
+        return json.load(fh)
+
+
+def golden_errors(terms_fn, nu, n, m):
+    """max relative errors of logdet(K + eta I) at the golden etas and of the
+    direct log-likelihood at the golden (sigma, sigma0), vs the reference.
+    terms_fn(etas) -> (logdet[], G[]) of the operator under test."""
+    from gaussian_proc._likelihood._direct_likelihood import _lp_from_terms
+    cfg = golden_case(nu, n)
+    if cfg is None:
+        return None, None
+    ld = numpy.asarray(terms_fn(cfg['etas'])[0])
+    ld_err = float(numpy.max(numpy.abs(ld - cfg['logdet']) / numpy.abs(cfg['logdet'])))
+    lp_err = 0.0
+    for (sg, s0), ref in zip(cfg['hypers'], cfg['direct_lp']):
+        l, G = terms_fn([(s0 / sg) ** 2])
+        lp = _lp_from_terms(n, m, sg, l[0], G[0])
+        lp_err = max(lp_err, abs(lp - ref) / abs(ref))
+    return ld_err, float(lp_err)
+
+
+def eta_block(args, world, rank, s=0):
+    """This rank's eta of step s: strong scaling, the rank's contiguous block of
+    the --eta-total curve (gaussian_proc.sweep.shard, padded blocks repeat the
+    block's last eta so every rank factorizes the same batch size); weak
+    scaling, --eta-per-rank eta of logspace(-3, 3, N * eta_per_rank)."""
+    from gaussian_proc.sweep import shard
+    if args.scaling == 'strong':
+        grid = numpy.logspace(-3, 3, args.eta_total)
+        lo, hi, per = shard(grid.size, world, rank)
+        idx = list(range(lo, hi)) or [grid.size - 1]
+        idx += [idx[-1]] * (per - len(idx))
+        return grid[idx], hi - lo, per, grid.size
+    B = args.eta_per_rank
+    grid = numpy.logspace(-3, 3, max(64, world * B))
+    idx = [(s * world * B + rank * B + j) % grid.size for j in range(B)]
+    return grid[idx], B, B, grid.size
+
+
+def gather_rows(rows, world, dist, torch):
+    """ONE all-gather of the per-rank [eta, logdet, lp] rows (RCCL at N > 1)."""
+    t = torch.from_numpy(numpy.ascontiguousarray(rows)).cuda()
+    if world == 1:
+        return t
+    out = torch.empty((world * t.shape[0], t.shape[1]), dtype=torch.float64, device=t.device)
+    dist.all_gather_into_tensor(out, t)
+    return out
 
 
 def band_mode(args, D, X, z, world, rank, dist, torch, ld_ref=None):
     """The eigenvalue operator's path (MixedCorrelation imate_method='eigenvalue'):
     per step ONE device band reduction K = Q B Q^T of the resident K (redone every
-    step), Q^T [X z], and the banded-Cholesky terms of ``--band-etas`` eta values,
-    then the host lp and one all-gather. Same eta grid and lp as the dense line."""
+    step), Q^T [X z], and the banded-Cholesky terms of this rank's eta block, then
+    the host lp and one all-gather. Same eta blocks and lp as the dense line.
+    The reduction is the operator's one-time setup: every rank repeats it for
+    its own K (it does not shard); only the per-eta banded Cholesky does."""
     from gaussian_proc._mixed_correlation import MixedCorrelation
     from gaussian_proc._likelihood._direct_likelihood import _lp_from_terms
     n, m = X.shape
-    E = args.band_etas
-    grid = numpy.logspace(-3, 3, max(64, world * E))
     op = MixedCorrelation(D, imate_method='eigenvalue')
     b = op.band()
     acc = {'reduce_ms': 0.0, 'rhs_ms': 0.0, 'loglik_ms': 0.0}
 
     def step(s, record):
-        idx = [(s * world * E + rank * E + j) % grid.size for j in range(E)]
-        etas = grid[idx]
+        etas, own, per, _ = eta_block(args, world, rank, s)
+        if args.scaling == 'weak':
+            etas = etas[:args.band_etas]
         op.refresh_band(X, z)   # reduction of K with Q^T [X z] applied alongside
         ld, G = op.loglik_terms(etas, X, z)
         if record:
             for k, v in b.last_timing().items():
                 acc[k] += v
         lp = numpy.array([_lp_from_terms(n, m, 1.0, l, g) for l, g in zip(ld, G)])
-        res = torch.from_numpy(numpy.stack([etas, ld, lp], axis=1)).cuda()
-        if world > 1:
-            out = torch.empty((world * E, 3), dtype=torch.float64, device=res.device)
-            dist.all_gather_into_tensor(out, res)
-            return out
-        return res
+        return gather_rows(numpy.stack([etas, ld, lp], axis=1), world, dist, torch), own, \
+            etas.size
 
     for s in range(args.warmup):
         step(s, False)
@@ -310,8 +537,9 @@ def band_mode(args, D, X, z, world, rank, dist, torch, ld_ref=None):
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    own = E = 0
     for s in range(args.steps):
-        last = step(args.warmup + s, True)
+        last, own, E = step(args.warmup + s, True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -323,26 +551,30 @@ def band_mode(args, D, X, z, world, rank, dist, torch, ld_ref=None):
     K = args.steps
     red = acc['reduce_ms'] / K
     flops_red = 4.0 * n ** 3 / 3.0
+    total = args.eta_total if args.scaling == 'strong' else world * E
     out = {
-        'value': world * E * K / dt, 'unit': 'evals/s', 'ms_per_step': dt / K * 1e3,
+        'value': total * K / dt, 'unit': 'evals/s', 'ms_per_step': dt / K * 1e3,
         'eta_per_rank_per_step': E,
-        'step': 'band reduction of K (Q^T [X z] applied alongside) + %d banded Cholesky evals + '
-                'host lp' % E,
+        'step': 'band reduction of K (Q^T [X z] applied alongside; repeated on every rank, '
+                'the setup does not shard) + %d banded Cholesky evals per rank + host lp + '
+                'all-gather' % E,
         'reduce_ms': round(red, 3), 'rhs_ms': round(acc['rhs_ms'] / K, 3),
         'loglik_ms': round(acc['loglik_ms'] / K, 3),
         'marginal_evals_per_s_per_gpu': round(E / (acc['loglik_ms'] / K * 1e-3), 1),
         'reduction_tflops': round(flops_red / (red * 1e-3) / 1e12, 3),
         'reduction_mfma_frac': round(flops_red / (red * 1e-3) / 1e12 / FP64_MFMA_PEAK_TFLOPS, 4),
+        'panel': b.stats(),
         'lp_sample': [float(v) for v in last[0].tolist()],
-        'logdet_rel_err_vs_reference': golden_logdet_err(
-            lambda e: op.loglik_terms(e, X, z)[0], args.nu, n),
     }
+    ld_err, lp_err = golden_errors(lambda e: op.loglik_terms(e, X, z), args.nu, n, m)
+    out['logdet_rel_err_vs_reference'] = ld_err
+    out['lp_rel_err_vs_reference'] = lp_err
     if ld_ref is not None:
         out['logdet_rel_err_vs_cholesky'] = float(numpy.max(
             numpy.abs(op.loglik_terms(ld_ref[0], X, z)[0] - ld_ref[1]) / numpy.abs(ld_ref[1])))
     if not args.no_der:
         out['der1_sweep'] = der1_sweep(op, X, z, E, rank, torch)
-    return out
+    return out, op
 
 
 def der1_sweep(op, X, z, E, rank, torch):
@@ -364,6 +596,24 @@ def der1_sweep(op, X, z, E, rank, torch):
             'der1_evals_per_s_per_gpu': round(E / dt, 1),
             'eigenvalues_ms_once': round(eig_ms, 1),
             'der1_sample': [float(log_etas[0]), float(d1[0])]}
+
+
+def batch_efficiency(op, X, z, batches=(8, 16, 32)):
+    """Single-GPU evals/s of one device call at smaller eta batches: the
+    per-rank batch of the strong-scaled 64-eta curve at N = 8, 4, 2, hence the
+    expected time-to-curve there (one warm call, then the best of two)."""
+    out = {}
+    grid = numpy.logspace(-3, 3, 64)
+    for bsz in batches:
+        if bsz > op.op.max_batch:
+            continue
+        etas = grid[:bsz]
+        op.loglik_terms(etas, X, z)
+        best = min(t for t, _ in _timed(lambda: op.loglik_terms(etas, X, z), 2))
+        out[str(bsz)] = {'evals_per_s': round(bsz / best, 2), 'call_ms': round(best * 1e3, 2),
+                         'expected_time_to_64_curve_ms_at_N': {
+                             str(64 // bsz): round(best * 1e3, 2)}}
+    return out
 
 
 def main():
@@ -393,38 +643,24 @@ def main():
     z = _data.generate_data(points, 0.2)
     X = _data.generate_basis_functions(points, 2)
     n, m = X.shape
-    B = args.eta_per_rank
+    _, own, B, gsize = eta_block(args, world, rank)
+    max_batch = max(B, 64 if world == 1 else B)
     D = generate_correlation(points, 0.1, args.nu, device_resident=True, device=local,
-                             max_batch=B)
+                             max_batch=max_batch)
     op = MixedCorrelation(D)
     op.op.set_outer(args.outer)
     op.op.set_lookahead(args.lookahead)
     op.set_rhs(X, z)
-    # 64-point eta grid (cfg3); with more evaluations per step than points over all
-    # ranks, a finer grid over the same range, so every rank's eta values are distinct
-    grid = numpy.logspace(-3, 3, max(64, world * B))
-
-    def step_etas(s):
-        idx = [(s * world * B + rank * B + j) % grid.size for j in range(B)]
-        return grid[idx]
 
     def step(s, timing_acc=None):
-        etas = step_etas(s)
+        etas = eta_block(args, world, rank, s)[0]
         ld, G = op.loglik_terms(etas, X, z)
         if timing_acc is not None:
             t = op.op.last_timing()
-            timing_acc['syrk_ms'] += t['syrk_ms']
-            timing_acc['syrk_busy_ms'] += t['syrk_busy_ms']
-            timing_acc['syrk_flops'] += t['syrk_flops']
-            timing_acc['syrk_launches'] += t['syrk_launches']
-            timing_acc['total_ms'] += t['total_ms']
+            for k in ('syrk_ms', 'syrk_busy_ms', 'syrk_flops', 'syrk_launches', 'total_ms'):
+                timing_acc[k] += t[k]
         lp = numpy.array([_lp_from_terms(n, m, 1.0, l, g) for l, g in zip(ld, G)])
-        res = torch.from_numpy(numpy.stack([etas, ld, lp], axis=1)).cuda()
-        if world > 1:
-            out = torch.empty((world * B, 3), dtype=torch.float64, device=res.device)
-            dist.all_gather_into_tensor(out, res)
-            return out
-        return res
+        return gather_rows(numpy.stack([etas, ld, lp], axis=1), world, dist, torch)
 
     for s in range(args.warmup):
         step(s)
@@ -443,7 +679,10 @@ def main():
     if world > 1:
         dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
     dt = float(t_max.item())
-    evals = world * B * args.steps
+    log('dense: %d steps in %.2f s' % (args.steps, dt))
+    # evaluations the job completed: the whole curve per step (strong), or every
+    # rank's block (weak)
+    evals = (gsize if args.scaling == 'strong' else world * B) * args.steps
     flops_eval = n ** 3 / 3.0 + 2.0 * n ** 2 * (m + 1) + n ** 2
     result = None
     if rank == 0:
@@ -470,6 +709,12 @@ def main():
                     'per_launch_tflops': round(timing['syrk_flops'] / (timing['syrk_ms'] * 1e-3)
                                                / 1e12, 3)}
         whole = flops_eval * evals / world / dt / 1e12
+        if args.scaling == 'strong':
+            workload = ('cfg3: N=%d 2D grid Matern nu=%g rho=0.1, the %d-point eta curve '
+                        'logspace(-3,3,%d) per step, %d eta per rank' % (n, args.nu, gsize, gsize, B))
+        else:
+            workload = ('cfg3 grid, weak: N=%d 2D grid Matern nu=%g rho=0.1, %d eta per rank of '
+                        'logspace(-3,3,%d)' % (n, args.nu, B, gsize))
         result = {
             'metric': 'log-likelihood evals/sec (N=16384 dense Matern-3/2)',
             'value': evals / dt,
@@ -479,15 +724,15 @@ def main():
             'warmup': args.warmup,
             'ms_per_step': dt / args.steps * 1e3,
             'higher_is_better': True,
-            'scaling': 'weak',
+            'scaling': args.scaling,
             'vs_baseline': None,
             'dtype': 'f64',
             'data': 'synthetic (reference data_utilities: 2D grid, sin + 0.2 noise seed 31, '
                     'deg-2 basis)',
-            'config': {'workload': 'cfg3: N=%d 2D grid Matern nu=%g rho=0.1, eta grid '
-                                   'logspace(-3,3,%d), %d eta/rank/step' % (n, args.nu,
-                                                                          grid.size, B),
-                       'n': n, 'm': m, 'eta_per_rank_per_step': B,
+            'config': {'workload': workload, 'n': n, 'm': m, 'eta_per_rank_per_step': B,
+                       'operator': "imate_method='cholesky' (one dense fp64 MFMA Cholesky per "
+                                   "eta); band_mode below is the 'eigenvalue' operator "
+                                   "Likelihood uses",
                        'outer_panel': 128 * args.outer, 'lookahead': args.lookahead,
                        'parallelism': 'eta-shard x%d + all-gather' % world},
             'roofline': roof,
@@ -497,16 +742,31 @@ def main():
             'lp_sample': [float(v) for v in last[0].tolist()] if last is not None else None,
             'cpu_baseline': None,
         }
-    ld_err = golden_logdet_err(lambda e: op.loglik_terms(e, X, z)[0], args.nu, n)
+        if args.scaling == 'strong':
+            result['time_to_curve_ms'] = dt / args.steps * 1e3
+    ld_err, lp_err = golden_errors(lambda e: op.loglik_terms(e, X, z), args.nu, n, m)
     if rank == 0:
         result['logdet_rel_err_vs_reference'] = ld_err
+        result['lp_rel_err_vs_reference'] = lp_err
+        if world == 1 and args.scaling == 'strong':
+            result['batch_efficiency'] = batch_efficiency(op, X, z)
+    lam = None
     if not args.no_band:
-        ld_ref = (last[:, 0].cpu().numpy()[:B], last[:, 1].cpu().numpy()[:B])
-        bm = band_mode(args, D, X, z, world, rank, dist, torch, ld_ref)
+        ld_ref = (last[:own, 0].cpu().numpy(), last[:own, 1].cpu().numpy())
+        bm, bop = band_mode(args, D, X, z, world, rank, dist, torch, ld_ref)
+        log('band mode: %.1f evals/s' % bm['value'])
         if rank == 0:
             result['band_mode'] = bm
+        if bop._eig is not None:
+            lam = bop._eig
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result['cpu_baseline'] = cpu_baseline(points, z, X, args.nu, step_etas(0))
+        cb = cpu_baseline(points, z, X, args.nu, 1.0, lam, args.cpu_samples)
+        # the same evaluation on the device (eta = 1): CPU and GPU agree
+        ld1, G1 = op.loglik_terms([1.0], X, z)
+        lp_dev = _lp_from_terms(n, m, 1.0, ld1[0], G1[0])
+        cb['lp_rel_diff_vs_device'] = abs(cb['lp_cholesky'] - lp_dev) / abs(lp_dev)
+        result['cpu_baseline'] = cb
+        result['speedup_vs_cpu'] = round(result['value'] / cb['value'], 1)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

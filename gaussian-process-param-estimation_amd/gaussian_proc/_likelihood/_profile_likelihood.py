@@ -19,7 +19,8 @@ import numpy
 from scipy.optimize import minimize
 from functools import partial
 
-from ._root_finding import find_interval_with_sign_change, chandrupatla_method
+from ._root_finding import chandrupatla_method, BatchedFunction, \
+    find_interval_with_sign_change_batched
 
 __all__ = ['ProfileLikelihood']
 
@@ -146,10 +147,23 @@ class ProfileLikelihood(object):
 
     @staticmethod
     def find_log_likelihood_der1_zeros(z, X, K_mixed, interval_eta, tol=1e-6,
-                                       max_iterations=100, num_bracket_trials=3):  # :244-415
+                                       max_iterations=100, num_bracket_trials=3,
+                                       group=None):  # :244-415
+        """Root of d lp / d eta in log10(eta) (reference :244-415: bracket search,
+        then Chandrupatla, then the optimal sigma). The der1 evaluations are
+        batched: the bracket search requests every point it may need next in one
+        call (_root_finding.find_interval_with_sign_change_batched), sharded over
+        the ranks of a torch.distributed ``group`` when one is initialised
+        (sweep.der1_sweep: one all-gather per batch). Decisions and results are
+        those of the sequential reference driver."""
         n, m = X.shape
 
         def optimal_sigma(eta):
+            if hasattr(K_mixed, 'loglik_terms') and eta > 0:
+                _, G = K_mixed.loglik_terms([eta], X, z)
+                G = G[0]
+                zMz = G[m, m] - G[:m, m] @ numpy.linalg.solve(G[:m, :m], G[:m, m])
+                return numpy.sqrt(zMz / (n - m))
             Y, Binv, Mz = ProfileLikelihood._mz(z, X, K_mixed, eta)
             return numpy.sqrt(numpy.dot(z, Mz) / (n - m))
 
@@ -158,13 +172,14 @@ class ProfileLikelihood(object):
             v = X @ (Binv @ (X.T @ z))
             return numpy.sqrt(numpy.dot(z, z - v) / (n - m))
 
+        from ..sweep import der1_sweep
+        fb = BatchedFunction(lambda le: der1_sweep(K_mixed, X, z, le, group=group))
         print('Find root of log likelihood derivative ...')
-        der1 = partial(ProfileLikelihood.log_likelihood_der1_eta, z, X, K_mixed)
         bracket = [numpy.log10(interval_eta[0]), numpy.log10(interval_eta[1])]
-        found, bracket, values = find_interval_with_sign_change(
-            der1, bracket, num_bracket_trials, args=())
+        found, bracket, values = find_interval_with_sign_change_batched(
+            fb, bracket, num_bracket_trials)
         if found:
-            res = chandrupatla_method(der1, bracket, values, verbose=False, eps_m=tol,
+            res = chandrupatla_method(fb, bracket, values, verbose=False, eps_m=tol,
                                       eps_a=tol, maxiter=max_iterations)
             print('Iter: %d' % (res['iterations']))
             eta = 10 ** res['root']
@@ -191,4 +206,5 @@ class ProfileLikelihood(object):
             else:
                 raise ValueError('eta must be zero or inf at this point.')
             success = True
+        ProfileLikelihood.last_der1_calls = (fb.calls, fb.points, dict(fb.memo))
         return {'sigma': sigma, 'sigma0': sigma0, 'eta': eta, 'success': success}

@@ -5,11 +5,111 @@ Restates the reference's gaussian_proc/_likelihood/_root_finding.py:
   chandrupatla_method             :155-309 (IQI / bisection hybrid)
 The decision rules and return values match the reference for scalar f; the
 per-iteration diagnostic prints of the bracket search are kept.
+
+``BatchedFunction`` + ``find_interval_with_sign_change_batched`` evaluate the
+same bracket search with every point it may need next requested in ONE batched
+call (the device evaluates many eta per call at almost the cost of one): per
+trial the midpoint and the one outward probe the current |f0|, |f1| select, and
+up front also the first Chandrupatla point of the initial bracket. Function
+values do not depend on the batch they are computed in (one device workgroup
+per eta), so the decisions, the returned bracket and the root are identical to
+the sequential reference driver.
 """
 
 import numpy
 
-__all__ = ['find_interval_with_sign_change', 'chandrupatla_method']
+__all__ = ['find_interval_with_sign_change', 'chandrupatla_method', 'BatchedFunction',
+           'find_interval_with_sign_change_batched']
+
+
+class BatchedFunction(object):
+    """Scalar view f(x) of a batched function fb(xs) -> values, memoised by the
+    exact float x. ``request(xs)`` evaluates the missing points of xs in one
+    call of fb; ``f(x)`` returns a cached value or evaluates x alone.
+    ``calls`` counts the batched calls, ``points`` the evaluated points."""
+
+    def __init__(self, fb):
+        self.fb = fb
+        self.memo = {}
+        self.calls = 0
+        self.points = 0
+
+    def request(self, xs):
+        miss = []
+        for x in xs:
+            x = float(x)
+            if x not in self.memo and x not in miss:
+                miss.append(x)
+        if miss:
+            vals = self.fb(numpy.array(miss))
+            self.calls += 1
+            self.points += len(miss)
+            for x, v in zip(miss, vals):
+                self.memo[x] = float(v)
+
+    def __call__(self, x, *args):
+        x = float(x)
+        if x not in self.memo:
+            self.request([x])
+        return self.memo[x]
+
+
+def _mid(x0, x1):
+    return x0 * (1.0 - 0.5) + x1 * 0.5
+
+
+def _outward(x0, x1, f0, f1):
+    t = 1.5 if numpy.abs(f0) > numpy.abs(f1) else -0.5
+    return x0 * (1.0 - t) + x1 * t
+
+
+def find_interval_with_sign_change_batched(fb, bracket, num_bracket_trials):
+    """find_interval_with_sign_change (:21-148) with batched evaluations.
+    ``fb`` is a BatchedFunction. Call 1: x0, x1, the first trial's midpoint,
+    both of its possible outward probes, and the first Chandrupatla point
+    (:155-309, t = 0.5 from a = x1) of [x0, x1]; each later trial: its midpoint
+    and its outward probe together."""
+    x0, x1 = float(bracket[0]), float(bracket[1])
+    xm = _mid(x0, x1)
+    fb.request([x0, x1, xm, x0 * (1.0 - 1.5) + x1 * 1.5, x0 * (1.0 + 0.5) + x1 * -0.5,
+                x1 + 0.5 * (x0 - x1)])
+
+    def f(x):
+        return fb(x)
+    f0, f1 = f(x0), f(x1)
+    for it in range(1, num_bracket_trials + 1):
+        if numpy.sign(f0) != numpy.sign(f1):
+            return True, [x0, x1], [f0, f1]
+        xm = _mid(x0, x1)
+        fb.request([xm, _outward(x0, x1, f0, f1)])
+        print('bracket was not found. Search for bracket. Iteration: %d' % it)
+        print('x0: %0.2f, f0: %0.16f' % (x0, f0))
+        print('x1: %0.2f, f1: %0.16f' % (x1, f1))
+        fm = f(xm)
+        print('x_new: %0.2f, f_new: %0.16f' % (xm, fm))
+        left_smaller = numpy.abs(f0) < numpy.abs(f1)
+        if numpy.sign(f0) != numpy.sign(fm):
+            if left_smaller:
+                return True, [x0, xm], [f0, fm]
+            return True, [xm, x1], [fm, f1]
+        if numpy.abs(fm) < min(numpy.abs(f0), numpy.abs(f1)):
+            if left_smaller:
+                x1, f1 = xm, fm
+            else:
+                x0, f0 = xm, fm
+            continue
+        right = numpy.abs(f0) > numpy.abs(f1)
+        xo = _outward(x0, x1, f0, f1)
+        fo = f(xo)
+        if numpy.sign(f0) != numpy.sign(fo):
+            if right:
+                return True, [xo, x0], [fo, f0]
+            return True, [x1, xo], [f1, fo]
+        if right:
+            x0, f0, x1, f1 = x1, f1, xo, fo
+        else:
+            x1, f1, x0, f0 = x0, f0, xo, fo
+    return False, [x0, x1], [f0, f1]
 
 
 def find_interval_with_sign_change(f, bracket, num_bracket_trials, args=()):
@@ -21,7 +121,7 @@ def find_interval_with_sign_change(f, bracket, num_bracket_trials, args=()):
         print('bracket was not found. Search for bracket. Iteration: %d' % it)
         print('x0: %0.2f, f0: %0.16f' % (x0, f0))
         print('x1: %0.2f, f1: %0.16f' % (x1, f1))
-        xm = 0.5 * x0 + 0.5 * x1
+        xm = _mid(x0, x1)
         fm = f(xm, *args)
         print('x_new: %0.2f, f_new: %0.16f' % (xm, fm))
         left_smaller = numpy.abs(f0) < numpy.abs(f1)

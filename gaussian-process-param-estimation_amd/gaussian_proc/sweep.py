@@ -18,7 +18,7 @@ import numpy
 
 from ._likelihood._direct_likelihood import _lp_from_terms
 
-__all__ = ['shard', 'eta_sweep']
+__all__ = ['shard', 'eta_sweep', 'slq_sweep', 'der1_sweep']
 
 
 def shard(num, world, rank):
@@ -27,6 +27,55 @@ def shard(num, world, rank):
     lo = min(num, rank * per)
     hi = min(num, lo + per)
     return lo, hi, per
+
+
+def _group(group):
+    """(dist module or None, world, rank) of an initialised process group."""
+    if group is False:
+        return None, 1, 0
+    try:
+        import torch.distributed as dist_mod
+        if dist_mod.is_available() and dist_mod.is_initialized():
+            return dist_mod, dist_mod.get_world_size(group), dist_mod.get_rank(group)
+    except ImportError:
+        pass
+    return None, 1, 0
+
+
+def _all_gather_rows(dist, group, local, world):
+    """ONE all-gather of equally shaped float64 row blocks -> [world * rows, ...]."""
+    import torch
+    backend = dist.get_backend(group)
+    dev = torch.device('cuda', torch.cuda.current_device()) if backend == 'nccl' \
+        else torch.device('cpu')
+    t_local = torch.from_numpy(numpy.ascontiguousarray(local)).to(dev)
+    if backend == 'nccl':
+        t_all = torch.empty((world * local.shape[0],) + tuple(local.shape[1:]),
+                            dtype=torch.float64, device=dev)
+        dist.all_gather_into_tensor(t_all, t_local, group=group)
+    else:
+        parts = [torch.empty_like(t_local) for _ in range(world)]
+        dist.all_gather(parts, t_local, group=group)
+        t_all = torch.cat(parts)
+    return t_all.cpu().numpy()
+
+
+def der1_sweep(K_mixed, X, z, log_etas, group=None):
+    """ProfileLikelihood.log_likelihood_der1_eta (_profile_likelihood.py:91-132)
+    at many log10(eta): each rank evaluates its contiguous block in one batched
+    call (band Gram blocks on the eigenvalue operator), ONE all-gather collects
+    them. Returns der1[len(log_etas)] on every rank."""
+    from ._likelihood._profile_likelihood import ProfileLikelihood
+    log_etas = numpy.atleast_1d(numpy.asarray(log_etas, dtype=float))
+    dist, world, rank = _group(group)
+    lo, hi, per = shard(log_etas.size, world, rank)
+    local = numpy.zeros((per, 1))
+    if hi > lo:
+        local[:hi - lo, 0] = ProfileLikelihood.log_likelihood_der1_eta_batch(
+            z, X, K_mixed, log_etas[lo:hi])
+    if dist is None or world == 1:
+        return local[:log_etas.size, 0].copy()
+    return _all_gather_rows(dist, group, local, world)[:log_etas.size, 0].copy()
 
 
 def eta_sweep(K_mixed, X, z, etas, sigma=1.0, group=None):
