@@ -647,6 +647,9 @@ def main():
     max_batch = max(B, 64 if world == 1 else B)
     D = generate_correlation(points, 0.1, args.nu, device_resident=True, device=local,
                              max_batch=max_batch)
+    from gaussian_proc import _hip
+    asm_ms = _hip.last_assembly_ms()
+    asm_bytes = 8.0 * D.op.n_pad ** 2
     op = MixedCorrelation(D)
     op.op.set_outer(args.outer)
     op.op.set_lookahead(args.lookahead)
@@ -744,6 +747,12 @@ def main():
         }
         if args.scaling == 'strong':
             result['time_to_curve_ms'] = dt / args.steps * 1e3
+        # one-time dense assembly (HBM-write-bound, 8 n^2 bytes)
+        result['assembly'] = {'kernel': 'matern_dense_kernel (64x64 lower tiles, mirrored)',
+                              'ms': round(asm_ms, 4), 'bytes_written': asm_bytes,
+                              'gbs': round(asm_bytes / (asm_ms * 1e-3) / 1e9, 1),
+                              'hbm_frac': round(asm_bytes / (asm_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                                                4)}
     ld_err, lp_err = golden_errors(lambda e: op.loglik_terms(e, X, z), args.nu, n, m)
     if rank == 0:
         result['logdet_rel_err_vs_reference'] = ld_err

@@ -513,16 +513,26 @@ int gpmi_device_count(int* count) {
   return 0;
 }
 
+thread_local double g_assembly_ms = 0.0;   // last matern_dense_kernel launch (HIP events)
+
 static int matern_params(double nu, MaternParams* P) {
   if (!(nu > 0.0)) return set_err(-1002, "nu must be positive (got %g)", nu);
   P->nu = nu;
   P->sqrt2nu = std::sqrt(2.0 * nu);
-  P->prefactor = std::pow(2.0, 1.0 - nu) / std::tgamma(nu);
+  P->mu = nu < 2.0 ? nu : nu - std::floor(nu) + 1.0;
+  P->lp0 = (1.0 - P->mu) * std::log(2.0) - std::lgamma(P->mu);
+  P->lp1 = -P->mu * std::log(2.0) - std::lgamma(P->mu + 1.0);
   if (nu == 0.5) P->mode = MATERN_HALF;
   else if (nu == 1.5) P->mode = MATERN_3HALF;
   else if (nu == 2.5) P->mode = MATERN_5HALF;
   else if (nu < 100) P->mode = MATERN_GENERAL;
   else P->mode = MATERN_GAUSS;
+  return 0;
+}
+
+int gpmi_last_assembly_ms(double* ms) {
+  if (!ms) return set_err(-1004, "null output");
+  *ms = g_assembly_ms;
   return 0;
 }
 
@@ -559,11 +569,22 @@ static int assemble(int device, hipStream_t s, const double* points, int64_t n, 
   HIP_TRY(hipMalloc(&ds, sizeof(double) * d));
   HIP_TRY(hipMemcpyAsync(dp, points, sizeof(double) * n * d, hipMemcpyHostToDevice, s));
   HIP_TRY(hipMemcpyAsync(ds, scale, sizeof(double) * d, hipMemcpyHostToDevice, s));
-  dim3 grid((unsigned)((n_pad + 255) / 256), (unsigned)((n_pad + 15) / 16));
-  hipLaunchKernelGGL(matern_dense_kernel, grid, dim3(256), 0, s, dp, n, d, ds, P, Kdev, ldk,
-                     n_pad);
+  // lower-triangular 64 x 64 tiles, each mirrored (gpmi_matern.hip)
+  const int64_t T = (n_pad + 63) / 64;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  HIP_TRY(hipEventCreate(&e0));
+  HIP_TRY(hipEventCreate(&e1));
+  HIP_TRY(hipEventRecord(e0, s));
+  hipLaunchKernelGGL(matern_dense_kernel, dim3((unsigned)(T * (T + 1) / 2)), dim3(256), 0, s, dp,
+                     n, d, ds, P, Kdev, ldk, n_pad);
   LAUNCH_CHECK("matern_dense_kernel");
+  HIP_TRY(hipEventRecord(e1, s));
   HIP_TRY(hipStreamSynchronize(s));
+  float ms = 0.f;
+  HIP_TRY(hipEventElapsedTime(&ms, e0, e1));
+  g_assembly_ms = ms;
+  HIP_TRY(hipEventDestroy(e0));
+  HIP_TRY(hipEventDestroy(e1));
   HIP_TRY(hipFree(dp));
   HIP_TRY(hipFree(ds));
   return 0;

@@ -17,7 +17,8 @@ struct MaternParams {
   int mode;
   double nu;
   double sqrt2nu;     // sqrt(2 nu)
-  double prefactor;   // 2^(1-nu) / Gamma(nu)
+  double mu;          // general nu >= 2: starting order nu - floor(nu) + 1 in [1, 2)
+  double lp0, lp1;    // log(2^(1-a) / Gamma(a)) at a = mu, mu + 1 (a = nu when nu < 2)
 };
 
 __global__ void matern_dense_kernel(const double* points, int64_t n, int d,

@@ -54,6 +54,7 @@ SIGNATURES = {
                                            c_double_p, c_double_p]),
     'gpmi_op_set_lookahead': (ctypes.c_int, [c_op_p, ctypes.c_int]),
     'gpmi_op_set_outer': (ctypes.c_int, [c_op_p, ctypes.c_int]),
+    'gpmi_last_assembly_ms': (ctypes.c_int, [c_double_p]),
     'gpmi_matern_values': (ctypes.c_int, [ctypes.c_int, c_double_p, c_i64, ctypes.c_double,
                                           c_double_p]),
     'gpmi_sp_create_matern': (ctypes.c_int, [ctypes.c_int, c_double_p, c_i64, ctypes.c_int,
@@ -429,6 +430,13 @@ def matern_dense(points, scale, nu, device=None):
     check(lib.gpmi_matern_dense(device, dptr(points), n, d, dptr(scale), float(nu), dptr(K),
                                 n), 'gpmi_matern_dense')
     return K
+
+
+def last_assembly_ms():
+    """Device ms of this thread's last dense Matérn assembly kernel."""
+    v = ctypes.c_double()
+    check(load().gpmi_last_assembly_ms(ctypes.byref(v)), 'gpmi_last_assembly_ms')
+    return v.value
 
 
 def matern_values(x, nu, device=None):

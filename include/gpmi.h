@@ -48,6 +48,12 @@ int gpmi_device_count(int* count);
 int gpmi_matern_dense(int device, const double* points, int64_t n, int d,
                       const double* scale, double nu, double* K_out, int64_t ldk);
 
+/* Device ms of the calling thread's last dense Matérn assembly kernel
+ * (gpmi_matern_dense / gpmi_op_assemble_matern; HIP events around the launch):
+ * the lower-triangular tiles evaluated once and stored mirrored, 8 n_pad^2
+ * bytes written. */
+int gpmi_last_assembly_ms(double* ms);
+
 /* Create the device-resident K + eta I operator for an n x n correlation matrix,
  * with workspace for max_batch concurrent eta values.
  * Replaces MixedCorrelation.__init__  mixed_correlation.py:34-79. */

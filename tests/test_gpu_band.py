@@ -309,3 +309,27 @@ def test_panel_timeout_falls_back_to_per_column_launches(gp, monkeypatch):
     ld2, G2 = op.loglik_terms([0.05, 2.0], X, z)
     assert rel(ld2, ld_ref) < 1e-12
     assert op.band().stats()['panel_fallbacks'] >= 2
+
+
+@pytest.mark.slow
+def test_cfg3_nu25_n16384_dense_and_band_vs_reference(gp):
+    """BASELINE cfg3 as specified (N=16384 2D grid, nu=2.5) against the
+    reference's own values (tests/golden/cfg3_nu25.json, 'cholesky' imate
+    method): logdet <= 1e-9 and direct lp <= 1e-8 relative, on the dense
+    Cholesky operator and on the eigenvalue (band) operator."""
+    from oracle import data
+    from gaussian_proc._mixed_correlation import MixedCorrelation
+    from gaussian_proc._likelihood._direct_likelihood import DirectLikelihood
+    cfg = load_json('cfg3_nu25.json')
+    assert cfg['nu'] == 2.5 and cfg['n'] == 16384
+    pts = data.generate_points(128, 2, True)
+    z = data.generate_data(pts, 0.2)
+    X = data.generate_basis_functions(pts, 2)
+    D = gp.generate_correlation(pts, 0.1, 2.5, device_resident=True, max_batch=3)
+    dense = MixedCorrelation(D)
+    band = MixedCorrelation(D, imate_method='eigenvalue')
+    for op in (dense, band):
+        ld, _ = op.loglik_terms(cfg['etas'], X, z)
+        assert rel(ld, cfg['logdet']) < 1e-9, op.imate_method
+        lp = DirectLikelihood.log_likelihood_batch(z, X, op, cfg['hypers'])
+        assert rel(lp, cfg['direct_lp']) < 1e-8, op.imate_method

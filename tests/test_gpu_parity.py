@@ -40,13 +40,43 @@ def test_matern_dense_matches_reference_cython(gp):
         assert numpy.all(numpy.diag(K) == 1.0)
 
 
-@pytest.mark.parametrize('nu', [0.3, 0.5, 0.75, 1.0, 1.5, 2.0, 2.5, 3.2, 7.5, 40.0, 150.0])
-def test_matern_general_nu_vs_scipy(gp, nu):
+@pytest.mark.parametrize('nu', [0.3, 0.5, 0.75, 1.0, 1.5, 2.0, 2.5, 3.2, 7.5, 40.0, 99.5, 150.0])
+def test_matern_general_nu_vs_scipy_and_exact(gp, nu):
+    """General order: the device's integral + scaled-recurrence evaluation vs
+    the reference formula on scipy's kv (oracle.matern; its own error grows with
+    nu, ~1e-13 near nu = 100) and vs mpmath at 40 digits (<= 4e-15 absolute)."""
     rng = numpy.random.RandomState(5)
     pts = rng.rand(200, 2)
     K = gp.generate_correlation(pts, 0.15, nu, grid=False)
     K_ref = matern.dense_correlation(pts, 0.15, nu)
-    assert numpy.max(numpy.abs(K - K_ref)) <= 2e-14
+    tol = 2e-14 if nu <= 7.5 or nu >= 100 else 3e-13
+    assert numpy.max(numpy.abs(K - K_ref)) <= tol
+    if nu in (0.5, 1.5, 2.5) or nu >= 100:
+        return
+    mpmath = pytest.importorskip('mpmath')
+    mpmath.mp.dps = 40
+    ii = rng.randint(0, 200, 300)
+    jj = rng.randint(0, 200, 300)
+    d = numpy.sqrt(numpy.sum(((pts[ii] - pts[jj]) / 0.15) ** 2, axis=1))
+    v = mpmath.mpf(nu)
+    for a, b, x in zip(ii, jj, d):
+        if x == 0.0:
+            continue
+        t = mpmath.sqrt(2 * v) * mpmath.mpf(x)
+        ex = mpmath.power(2, 1 - v) / mpmath.gamma(v) * mpmath.power(t, v) * mpmath.besselk(v, t)
+        assert abs(K[a, b] - float(ex)) <= 4e-15, (nu, x)
+
+
+def test_matern_dense_symmetric_tiles_ragged(gp):
+    """Lower-triangular tiles mirrored: exact symmetry, unit diagonal and the
+    oracle's values at sizes around the 64-tile edge."""
+    rng = numpy.random.RandomState(9)
+    for n in (1, 63, 64, 65, 130, 257):
+        pts = rng.rand(n, 3)
+        K = gp.generate_correlation(pts, [0.2, 0.3, 0.1], 1.5, grid=False)
+        numpy.testing.assert_array_equal(K, K.T)
+        assert numpy.all(numpy.diag(K) == 1.0)
+        assert numpy.max(numpy.abs(K - matern.dense_correlation(pts, [0.2, 0.3, 0.1], 1.5))) <= 4e-16
 
 
 def test_device_resident_correlation_roundtrip(gp):
@@ -300,3 +330,30 @@ def test_bench_batch64_call_vs_single_and_oracle(gp):
         assert rel(ld[i], ref.logdet(etas[i])) < 1e-10, i
         Gref = R.T @ ref.solve(etas[i], R)
         assert numpy.max(numpy.abs(G[i] - Gref)) <= 1e-8 * numpy.max(numpy.abs(Gref)), i
+
+
+@pytest.mark.parametrize('fixture,nu', [('n1024_nu25.json', 2.5), ('cfg2_profiled.json', 1.5)])
+def test_profiled_maximize_bracket_found_matches_reference(gp, capsys, fixture, nu):
+    """Likelihood('profiled').maximize_log_likelihood on the device (band der1
+    terms, batched bracket search) where the reference finds a bracket and runs
+    Chandrupatla (_profile_likelihood.py:317-350): same optimum, and every der1
+    point the reference evaluated was evaluated here with the same value."""
+    from gaussian_proc._likelihood import Likelihood
+    from gaussian_proc._likelihood._profile_likelihood import ProfileLikelihood
+    cfg = load_json(fixture)
+    pts, z, X = config_inputs(cfg)
+    K = gp.generate_correlation(pts, cfg['correlation_scale'], nu)
+    res = Likelihood(X, K, 'profiled').maximize_log_likelihood(z)
+    ref = cfg['maximize_profiled']
+    assert cfg['maximize_profiled_bracket_found']
+    for k in ('sigma', 'sigma0', 'eta'):
+        assert abs(res[k] - ref[k]) <= 1e-8 * abs(ref[k]), (k, res[k], ref[k])
+    calls, points, memo = ProfileLikelihood.last_der1_calls
+    seq = cfg['maximize_profiled_der1_calls']
+    keys = numpy.array(sorted(memo))
+    scale = max(abs(v) for _, v in seq)
+    for le, v in seq:
+        k = keys[numpy.argmin(numpy.abs(keys - le))]
+        assert abs(k - le) <= 1e-9 * max(1.0, abs(le)), (le, k)
+        assert abs(memo[k] - v) <= 1e-9 * scale + 1e-6 * abs(v), (le, memo[k], v)
+    assert calls < len(seq)

@@ -1,0 +1,91 @@
+"""Host drivers of the profiled optimizer (CPU): the batched bracket search
+makes the reference's decisions (_root_finding.py:21-148) with fewer batched
+calls, and the whole batched profiled driver reproduces the reference's
+recorded optimum and evaluation sequence (tests/golden n1024: bracket found,
+Chandrupatla; cfg1: no bracket) with the oracle's exact operator standing in
+for the device one."""
+
+import contextlib
+import io
+
+import numpy
+import pytest
+
+from gaussian_proc._likelihood._root_finding import (
+    find_interval_with_sign_change, find_interval_with_sign_change_batched, BatchedFunction,
+    chandrupatla_method)
+from gaussian_proc._likelihood._profile_likelihood import ProfileLikelihood
+from oracle.mixed_correlation import MixedCorrelation as OracleMC
+from oracle import matern
+from _util import load_json, config_inputs
+
+FUNCS = [
+    lambda x: x - 0.3,                          # bracket at once
+    lambda x: (x - 0.25) * (x - 0.9) + 0.01,    # no sign change in [-4, 3]
+    lambda x: numpy.exp(-x) - 0.05,             # root near 3.0
+    lambda x: -(x + 3.7) * (x - 2.9),           # both ends negative, roots inside
+    lambda x: numpy.tanh(x - 4.2),              # root outside, found by an outward probe
+    lambda x: numpy.tanh(-x - 5.5),             # root outside on the left
+    lambda x: 1.0 + 0.0 * x,                    # never
+    lambda x: (x - 1.0) ** 2 - 1e-3,            # roots close together
+]
+
+
+@pytest.mark.parametrize('k', range(len(FUNCS)))
+@pytest.mark.parametrize('bracket', [(-4.0, 3.0), (-1.0, 1.0), (2.0, 5.0)])
+def test_batched_bracket_search_makes_the_reference_decisions(k, bracket):
+    f = FUNCS[k]
+    calls = []
+
+    def fs(x):
+        calls.append(x)
+        return float(f(x))
+    with contextlib.redirect_stdout(io.StringIO()) as out1:
+        ref = find_interval_with_sign_change(fs, list(bracket), 3)
+    fb = BatchedFunction(lambda xs: numpy.array([f(x) for x in xs]))
+    with contextlib.redirect_stdout(io.StringIO()) as out2:
+        got = find_interval_with_sign_change_batched(fb, list(bracket), 3)
+    assert got == ref
+    assert out1.getvalue() == out2.getvalue()          # same diagnostic prints
+    assert set(calls) <= set(fb.memo)                  # every point the reference used
+    assert fb.calls <= 1 + 3                            # one batch per trial at most
+    if ref[0]:
+        r1 = chandrupatla_method(fs, ref[1], ref[2], eps_m=1e-6, eps_a=1e-6, maxiter=100)
+        r2 = chandrupatla_method(fb, got[1], got[2], eps_m=1e-6, eps_a=1e-6, maxiter=100)
+        assert r1 == r2
+
+
+def _profiled(cfg_name, nu):
+    cfg = load_json(cfg_name)
+    pts, z, X = config_inputs(cfg)
+    K = matern.dense_correlation(pts, cfg['correlation_scale'], nu)
+    op = OracleMC(K, 'eigenvalue')
+    with contextlib.redirect_stdout(io.StringIO()):
+        res = ProfileLikelihood.find_log_likelihood_der1_zeros(z, X, op, [1e-4, 1e3])
+    return cfg, res
+
+
+def test_profiled_driver_bracket_found_matches_reference_n1024():
+    cfg, res = _profiled('n1024_nu25.json', 2.5)
+    ref = cfg['maximize_profiled']
+    assert cfg['maximize_profiled_bracket_found']
+    for k in ('sigma', 'sigma0', 'eta'):
+        assert abs(res[k] - ref[k]) <= 1e-8 * abs(ref[k]), (k, res[k], ref[k])
+    calls, points, memo = ProfileLikelihood.last_der1_calls
+    seq = cfg['maximize_profiled_der1_calls']
+    scale = max(abs(v) for _, v in seq)
+    keys = numpy.array(sorted(memo))
+    for le, v in seq:
+        # every reference evaluation point was evaluated here too (Chandrupatla's
+        # interpolation points agree to rounding: the der1 values do, to ~1e-12)
+        k = keys[numpy.argmin(numpy.abs(keys - le))]
+        assert abs(k - le) <= 1e-9 * max(1.0, abs(le)), (le, k)
+        assert abs(memo[k] - v) <= 1e-9 * scale + 1e-6 * abs(v), (le, memo[k], v)
+    assert calls < len(seq)                 # fewer (batched) calls than reference evals
+
+
+def test_profiled_driver_no_bracket_matches_reference_cfg1():
+    cfg, res = _profiled('cfg1.json', 1.5)
+    ref = cfg['maximize_profiled']
+    assert res['eta'] == numpy.inf and res['sigma'] == 0
+    assert abs(res['sigma0'] - ref['sigma0']) <= 1e-12 * ref['sigma0']
