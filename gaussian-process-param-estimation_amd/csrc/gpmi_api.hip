@@ -575,8 +575,7 @@ static int assemble(int device, hipStream_t s, const double* points, int64_t n, 
   HIP_TRY(hipEventCreate(&e0));
   HIP_TRY(hipEventCreate(&e1));
   HIP_TRY(hipEventRecord(e0, s));
-  hipLaunchKernelGGL(matern_dense_kernel, dim3((unsigned)(T * (T + 1) / 2)), dim3(256), 0, s, dp,
-                     n, d, ds, P, Kdev, ldk, n_pad);
+  launch_matern_dense(dim3((unsigned)(T * (T + 1) / 2)), s, dp, n, d, ds, P, Kdev, ldk, n_pad);
   LAUNCH_CHECK("matern_dense_kernel");
   HIP_TRY(hipEventRecord(e1, s));
   HIP_TRY(hipStreamSynchronize(s));

@@ -21,9 +21,11 @@ struct MaternParams {
   double lp0, lp1;    // log(2^(1-a) / Gamma(a)) at a = mu, mu + 1 (a = nu when nu < 2)
 };
 
-__global__ void matern_dense_kernel(const double* points, int64_t n, int d,
-                                    const double* scale_dev, MaternParams P,
-                                    double* K, int64_t ldk, int64_t n_pad);
+// Dense Matérn assembly: lower-triangular 64 x 64 tiles (grid = T (T + 1) / 2,
+// T = ceil(n_pad / 64)), each mirrored (gpmi_matern.hip).
+void launch_matern_dense(dim3 grid, hipStream_t s, const double* points, int64_t n, int d,
+                         const double* scale, const MaternParams& P, double* K, int64_t ldk,
+                         int64_t n_pad);
 
 // Batched factorization kernels (gpmi_chol.hip). All matrices are row-major
 // n_pad x n_pad with leading dimension lda; batch member b lives at base + b*stride.

@@ -20,6 +20,9 @@
 #ifndef GPMI_MATERN_NT
 #define GPMI_MATERN_NT 1
 #endif
+#ifndef GPMI_MATERN_PROBE
+#define GPMI_MATERN_PROBE 0   // development probes: 1 no kernel evaluation, 2 no stores
+#endif
 
 namespace gpmi {
 
@@ -73,11 +76,13 @@ __device__ double matern_general(double t, const MaternParams& P) {
   return m1;
 }
 
-// Matérn correlation of a scaled distance x (_kernels.pyx:73-93).
+// Matérn correlation of a scaled distance x (_kernels.pyx:73-93); MODE < 0:
+// the mode is read from P at run time, otherwise fixed at compile time.
+template <int MODE = -1>
 __device__ __forceinline__ double matern_value(double x, const MaternParams& P) {
 #pragma clang fp contract(off)
   if (x == 0.0) return 1.0;
-  switch (P.mode) {
+  switch (MODE < 0 ? P.mode : MODE) {
     case MATERN_HALF:
       return exp(-x);
     case MATERN_3HALF: {
@@ -95,18 +100,31 @@ __device__ __forceinline__ double matern_value(double x, const MaternParams& P) 
   }
 }
 
+// (p_i - p_j) / scale, correctly rounded as the reference's division, from the
+// correctly rounded reciprocal rs = RN(1 / scale): q0 = RN(a rs), the exact
+// remainder a - q0 scale (FMA), q = RN(q0 + rem rs) (Markstein's final step:
+// RN(a / scale) whenever rs is within half an ulp of 1 / scale and q0 within one
+// ulp of a / scale, no overflow / underflow; 2e8 random cases checked equal on
+// the host). One multiply and two FMAs instead of the ~10-instruction IEEE
+// division sequence.
+__device__ __forceinline__ double div_by_scale(double a, double sc, double rs) {
+  const double q0 = a * rs;
+  const double rem = fma(-q0, sc, a);
+  return fma(rem, rs, q0);
+}
+
 // Scaled Euclidean distance, summed in dimension order (_kernels.pyx:130-136).
 // Unrolled to GPMI_MAX_DIM so p_j stays in registers.
 __device__ __forceinline__ double scaled_distance(const double* __restrict__ pi,
                                                   const double (&pj)[GPMI_MAX_DIM],
                                                   const double* __restrict__ scale,
-                                                  int d) {
+                                                  const double* __restrict__ rscale, int d) {
 #pragma clang fp contract(off)
   double acc = 0.0;
 #pragma unroll
   for (int k = 0; k < GPMI_MAX_DIM; ++k) {
     if (k < d) {
-      const double v = (pi[k] - pj[k]) / scale[k];
+      const double v = div_by_scale(pi[k] - pj[k], scale[k], rscale[k]);
       acc += v * v;
     }
   }
@@ -132,13 +150,14 @@ __device__ __forceinline__ void store_nt(double* p, double v) {
 #endif
 }
 
-__global__ __launch_bounds__(256) void matern_dense_kernel(
+template <int MODE>
+__global__ __launch_bounds__(256) void matern_dense_kernel_t(
     const double* __restrict__ points, int64_t n, int d,
     const double* __restrict__ scale_dev, MaternParams P, double* __restrict__ K,
     int64_t ldk, int64_t n_pad) {
   __shared__ double tile[MT][MT + 1];
   __shared__ double srow[MT * GPMI_MAX_DIM];
-  __shared__ double sscale[GPMI_MAX_DIM];
+  __shared__ double sscale[GPMI_MAX_DIM], srs[GPMI_MAX_DIM];
   const int64_t b = blockIdx.x;
   int I = (int)((sqrt(8.0 * (double)b + 1.0) - 1.0) * 0.5);
   while ((int64_t)I * (I + 1) / 2 > b) --I;
@@ -146,7 +165,10 @@ __global__ __launch_bounds__(256) void matern_dense_kernel(
   const int J = (int)(b - (int64_t)I * (I + 1) / 2);
   const int t = threadIdx.x, c = t & (MT - 1), r0 = t >> 6;
   const int64_t i0 = (int64_t)I * MT, j0 = (int64_t)J * MT;
-  if (t < d) sscale[t] = scale_dev[t];
+  if (t < d) {
+    sscale[t] = scale_dev[t];
+    srs[t] = 1.0 / scale_dev[t];
+  }
   for (int e = t; e < MT * d; e += 256) {
     const int64_t i = i0 + e / d;
     srow[e] = (i < n) ? points[i * d + (e % d)] : 0.0;
@@ -161,13 +183,20 @@ __global__ __launch_bounds__(256) void matern_dense_kernel(
     const int64_t i = i0 + r;
     double v;
     if (i < n && j < n) {
-      v = matern_value(scaled_distance(&srow[r * d], pj, sscale, d), P);
+#if GPMI_MATERN_PROBE == 1
+      v = scaled_distance(&srow[r * d], pj, sscale, srs, d);   // probe: no kernel evaluation
+#else
+      v = matern_value<MODE>(scaled_distance(&srow[r * d], pj, sscale, srs, d), P);
+#endif
     } else {
       v = (i == j) ? 1.0 : 0.0;
     }
     tile[r][c] = v;
   }
   __syncthreads();
+#if GPMI_MATERN_PROBE == 2
+  if (tile[r0][c] != -1.0) return;   // probe: no stores
+#endif
   for (int q = 0; q < MT / 4; ++q) {
     const int r = r0 + 4 * q;
     if (i0 + r < n_pad && j0 + c < n_pad) store_nt(K + (i0 + r) * ldk + j0 + c, tile[r][c]);
@@ -176,6 +205,31 @@ __global__ __launch_bounds__(256) void matern_dense_kernel(
   for (int q = 0; q < MT / 4; ++q) {
     const int r = r0 + 4 * q;
     if (j0 + r < n_pad && i0 + c < n_pad) store_nt(K + (j0 + r) * ldk + i0 + c, tile[c][r]);
+  }
+}
+
+// One instantiation per closed form (lean register use), one for general nu
+// and the Gaussian limit.
+void launch_matern_dense(dim3 grid, hipStream_t s, const double* points, int64_t n, int d,
+                         const double* scale, const MaternParams& P, double* K, int64_t ldk,
+                         int64_t n_pad) {
+  switch (P.mode) {
+    case MATERN_HALF:
+      hipLaunchKernelGGL(matern_dense_kernel_t<MATERN_HALF>, grid, dim3(256), 0, s, points, n, d,
+                         scale, P, K, ldk, n_pad);
+      break;
+    case MATERN_3HALF:
+      hipLaunchKernelGGL(matern_dense_kernel_t<MATERN_3HALF>, grid, dim3(256), 0, s, points, n, d,
+                         scale, P, K, ldk, n_pad);
+      break;
+    case MATERN_5HALF:
+      hipLaunchKernelGGL(matern_dense_kernel_t<MATERN_5HALF>, grid, dim3(256), 0, s, points, n, d,
+                         scale, P, K, ldk, n_pad);
+      break;
+    default:
+      hipLaunchKernelGGL(matern_dense_kernel_t<-1>, grid, dim3(256), 0, s, points, n, d, scale, P,
+                         K, ldk, n_pad);
+      break;
   }
 }
 
@@ -193,6 +247,7 @@ __global__ __launch_bounds__(256) void matern_dense_kernel(
 // ---------------------------------------------------------------------------
 namespace gpmi {
 
+// scale: [scale | 1 / scale] (2 * GPMI_MAX_DIM doubles, see div_by_scale)
 __device__ __forceinline__ bool taper_keep(const double (&pi)[GPMI_MAX_DIM],
                                            const double* __restrict__ points, int64_t j,
                                            int d, const double* __restrict__ scale,
@@ -207,7 +262,7 @@ __device__ __forceinline__ bool taper_keep(const double (&pi)[GPMI_MAX_DIM],
 #pragma unroll
     for (int k = 0; k < GPMI_MAX_DIM; ++k) {
       if (k < d) {
-        const double v = (pi[k] - pj[k]) / scale[k];
+        const double v = div_by_scale(pi[k] - pj[k], scale[k], scale[GPMI_MAX_DIM + k]);
         acc += v * v;
       }
     }

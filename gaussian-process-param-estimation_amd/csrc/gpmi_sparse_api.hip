@@ -296,10 +296,15 @@ int gpmi_sp_create_matern(int device, const double* points, int64_t n, int d,
   double *dp = nullptr, *ds = nullptr;
   int* dcnt = nullptr;
   SP_TRY(hipMalloc(&dp, sizeof(double) * n * d));
-  SP_TRY(hipMalloc(&ds, sizeof(double) * d));
+  SP_TRY(hipMalloc(&ds, sizeof(double) * 2 * GPMI_MAX_DIM));   // [scale | 1 / scale]
   SP_TRY(hipMalloc(&dcnt, sizeof(int) * n));
   SP_TRY(hipMemcpyAsync(dp, points, sizeof(double) * n * d, hipMemcpyHostToDevice, st));
-  SP_TRY(hipMemcpyAsync(ds, scale, sizeof(double) * d, hipMemcpyHostToDevice, st));
+  std::vector<double> hsc(2 * GPMI_MAX_DIM, 1.0);
+  for (int k = 0; k < d; ++k) {
+    hsc[k] = scale[k];
+    hsc[GPMI_MAX_DIM + k] = 1.0 / scale[k];
+  }
+  SP_TRY(hipMemcpyAsync(ds, hsc.data(), sizeof(double) * hsc.size(), hipMemcpyHostToDevice, st));
   const unsigned grid = (unsigned)((n + 3) / 4);
   // Cell list (d <= 3): cells of width >= xcut * scale_k, so a kept pair is in the
   // same or an adjacent cell; coarsened while there are more cells than 4 n.

@@ -10,7 +10,7 @@ import pytest
 
 from oracle import matern, likelihood as olk
 from oracle.mixed_correlation import MixedCorrelation as OracleMC
-from _util import load_json, load_npz, config_inputs, rel
+from _util import check_der1_sequence, load_json, load_npz, config_inputs, rel
 
 pytestmark = pytest.mark.gpu
 
@@ -350,10 +350,5 @@ def test_profiled_maximize_bracket_found_matches_reference(gp, capsys, fixture, 
         assert abs(res[k] - ref[k]) <= 1e-8 * abs(ref[k]), (k, res[k], ref[k])
     calls, points, memo = ProfileLikelihood.last_der1_calls
     seq = cfg['maximize_profiled_der1_calls']
-    keys = numpy.array(sorted(memo))
-    scale = max(abs(v) for _, v in seq)
-    for le, v in seq:
-        k = keys[numpy.argmin(numpy.abs(keys - le))]
-        assert abs(k - le) <= 1e-9 * max(1.0, abs(le)), (le, k)
-        assert abs(memo[k] - v) <= 1e-9 * scale + 1e-6 * abs(v), (le, memo[k], v)
+    check_der1_sequence(memo, seq)
     assert calls < len(seq)

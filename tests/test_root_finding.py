@@ -17,7 +17,7 @@ from gaussian_proc._likelihood._root_finding import (
 from gaussian_proc._likelihood._profile_likelihood import ProfileLikelihood
 from oracle.mixed_correlation import MixedCorrelation as OracleMC
 from oracle import matern
-from _util import load_json, config_inputs
+from _util import check_der1_sequence, load_json, config_inputs
 
 FUNCS = [
     lambda x: x - 0.3,                          # bracket at once
@@ -74,13 +74,7 @@ def test_profiled_driver_bracket_found_matches_reference_n1024():
     calls, points, memo = ProfileLikelihood.last_der1_calls
     seq = cfg['maximize_profiled_der1_calls']
     scale = max(abs(v) for _, v in seq)
-    keys = numpy.array(sorted(memo))
-    for le, v in seq:
-        # every reference evaluation point was evaluated here too (Chandrupatla's
-        # interpolation points agree to rounding: the der1 values do, to ~1e-12)
-        k = keys[numpy.argmin(numpy.abs(keys - le))]
-        assert abs(k - le) <= 1e-9 * max(1.0, abs(le)), (le, k)
-        assert abs(memo[k] - v) <= 1e-9 * scale + 1e-6 * abs(v), (le, memo[k], v)
+    check_der1_sequence(memo, seq)
     assert calls < len(seq)                 # fewer (batched) calls than reference evals
 
 
