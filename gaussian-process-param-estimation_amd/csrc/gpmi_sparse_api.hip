@@ -638,7 +638,9 @@ int gpmi_sp_msgram(gpmi_sp* sp, const double* etas, int neta, const double* rhs,
     SP_TRY(hipMemcpyAsync(Pd, Bd, sizeof(double) * ns, hipMemcpyDeviceToDevice, str));
     SP_TRY(hipStreamSynchronize(str));
   }
-  const unsigned sthreads = (unsigned)((S * s + 63) / 64 * 64);
+  // scalar kernels: S * s threads for the per-shift recurrences (<= 1024), and
+  // 16 waves for their fixed-order partial reductions
+  const unsigned sthreads = 1024;
   launch_ms_dots(Bd, Rd, n, s, sp->partial, MS_NBLK, str);
   SP_LAUNCH("ms_dots_partial_kernel");
   hipLaunchKernelGGL(ms_init_kernel, dim3(1), dim3(sthreads), 0, str, st, sp->partial, MS_NBLK, S,

@@ -1,0 +1,39 @@
+"""Host-side breakdown of one sparse bench step (bench.py --config sparse4|5):
+device Lanczos, Ritz nodes + quadrature on the host, multi-shift CG Gram."""
+import os
+import sys
+import time
+
+import numpy
+
+REPO = os.path.join(os.path.dirname(os.path.abspath(__file__)), '..')
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, 'gaussian-process-param-estimation_amd'))
+import bench  # noqa: E402
+from gaussian_proc import generate_correlation, _data, _slq  # noqa: E402
+from gaussian_proc._mixed_correlation import MixedCorrelation  # noqa: E402
+
+cfg = sys.argv[1] if len(sys.argv) > 1 else 'sparse4'
+npts, dim, rho, nu, dens, nprobe, steps, neta = bench.SPARSE_CONFIGS[cfg]
+pts = _data.generate_points(npts, dim, True)
+z = _data.generate_data(pts, 0.2)
+X = _data.generate_basis_functions(pts, 2)
+D = generate_correlation(pts, rho, nu, sparse=True, density=dens, device_resident=True)
+op = MixedCorrelation(D, imate_method='slq',
+                      imate_options={'num_samples': nprobe, 'lanczos_degree': steps})
+shift = -1.1 * _slq.min_ritz(op.slq_nodes())
+etas = numpy.logspace(-2, 2, neta) + shift
+R = numpy.column_stack([X, z])
+for rep in range(4):
+    t0 = time.perf_counter()
+    a, b = op.sop.lanczos(nprobe, steps, 0)
+    t1 = time.perf_counter()
+    nodes = _slq.nodes(a, b)
+    t2 = time.perf_counter()
+    q = [_slq.quadrature(nodes, etas, _slq.FUNCS[f]) for f in ('logdet', 'traceinv', 'traceinv2')]
+    t3 = time.perf_counter()
+    G = op.sop.msgram(etas, R, rtol=1e-6)
+    t4 = time.perf_counter()
+    print('%s rep %d: lanczos %.2f ms, nodes %.2f ms, quadrature %.2f ms, msgram %.2f ms '
+          '(%d CG iterations)' % (cfg, rep, (t1 - t0) * 1e3, (t2 - t1) * 1e3, (t3 - t2) * 1e3,
+                                  (t4 - t3) * 1e3, op.sop.last_cg_iterations))
