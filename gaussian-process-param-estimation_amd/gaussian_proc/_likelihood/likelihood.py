@@ -2,10 +2,12 @@
 
 The reference builds ``MixedCorrelation(K, interpolate=False,
 imate_method='eigenvalue')`` (:40-49): a one-time dense eigh, then 2 dense
-solves per evaluation. Here the operator is device-resident and every
-evaluation is one fp64 MFMA Cholesky (exact, same values to rounding).
-``max_batch`` sets how many eta values one device call factorizes together
-(``log_likelihood_batch``).
+solves per evaluation. Here the same 'eigenvalue' operator is device-resident:
+its one-time setup is the band reduction K = Q B Q^T (bandwidth 128), after
+which every evaluation is one banded Cholesky of B + eta I (exact, same values
+to rounding); traceinv / trace use the device eigenvalues of B. ``max_batch``
+sizes the dense per-eta Cholesky workspace the operator's 'cholesky' calls
+(solve, hutchinson) use.
 """
 
 from .._mixed_correlation import MixedCorrelation

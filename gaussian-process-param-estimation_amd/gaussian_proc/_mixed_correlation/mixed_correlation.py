@@ -8,7 +8,10 @@ once per operator.
   :76-79, then cheap per-eta logdet, :239-248): the device reduces K once to
   band form K = Q B Q^T (bandwidth 128, csrc/gpmi_band.hip, on first use);
   logdet(eta) and the likelihood terms are then one banded Cholesky of
-  B + eta I per eta. traceinv uses the exact dense path below.
+  B + eta I per eta. traceinv / trace of any exponent are sums over the
+  eigenvalues of B (= those of K; device bulge chase + bisection, computed once
+  on first use, csrc/gpmi_chase.hip), as imate's 'eigenvalue' method (:172-181).
+  solve(eta, Y) uses the dense Cholesky below.
 * 'cholesky' (and 'hutchinson' for logdet, which the reference maps to
   Cholesky at :250-261): one fp64 MFMA Cholesky of K + eta I
   (csrc/gpmi_chol.hip), cached per eta so that logdet(eta) followed by
