@@ -21,6 +21,10 @@ once per operator.
   Cholesky (stochastic; parity unpinned against imate, which is absent).
 * sparse K: 'slq' / 'hutchinson' with device Lanczos and CG.
 
+``interpolate=True`` answers traceinv from an interpolant in eta built on the
+exact values at ``interpolant_points`` (_interpolate.py; the reference's
+imate.InterpolateTraceInv, :52-66,167-170; parity unpinned, imate is absent).
+
 Error conventions follow the reference: ``ValueError`` for an unknown method
 (:146,212,271) or a bad ``dot`` exponent (:323-326), ``TypeError`` for
 ``interpolate`` without points (:53-55), and ``numpy.linalg.LinAlgError`` when
@@ -53,7 +57,7 @@ class MixedCorrelation(object):
             if self.interpolant_points is None:
                 raise TypeError('When "interpolate" is set to "True", the '
                                 '"interpolant_points" cannot be None.')
-            raise NotImplementedError('traceinv interpolation is not implemented yet')
+        self.interpolate_traceinv = None
         self.sparse = False
         if isinstance(K, DeviceSparseCorrelation) or scipy.sparse.issparse(K):
             self._init_sparse(K, device)
@@ -79,6 +83,21 @@ class MixedCorrelation(object):
         self._band = None
         self._band_rhs = None
         self._eig = None
+        if self.interpolate:
+            self._build_interpolant()
+
+    def _build_interpolant(self):
+        """imate.InterpolateTraceInv of the reference (mixed_correlation.py:52-66),
+        restated in _interpolate.py (parity unpinned: imate is absent); its
+        nodes are the operator's exact traceinv at the interpolant points."""
+        from ._interpolate import InterpolateTraceInv
+        interp, self.interpolate = self.interpolate, False   # exact values for the nodes
+        try:
+            self.interpolate_traceinv = InterpolateTraceInv(
+                lambda t: self.traceinv(t, 1), self.n, self.trace(0.0, 1),
+                self.interpolant_points)
+        finally:
+            self.interpolate = interp
 
     # ---- 'eigenvalue': one-time band reduction -----------------------------
 
@@ -189,6 +208,8 @@ class MixedCorrelation(object):
         self.seed = int(opts.get('seed', 0))
         self.cg_rtol = float(opts.get('cg_rtol', 1e-6))
         self._nodes = None
+        if self.interpolate:
+            self._build_interpolant()
 
     def slq_nodes(self):
         """Ritz nodes of every probe (computed once; eta-independent)."""
@@ -249,6 +270,9 @@ class MixedCorrelation(object):
         raise ValueError('Existing methods are "exact", "eigenvalue", and "slq".')
 
     def traceinv(self, eta, exponent=1):                           # :155-215
+        if self.interpolate:
+            # :167-170: the interpolant of tr((K + eta I)^-1), whatever the exponent
+            return self.interpolate_traceinv.interpolate(eta)
         if self.sparse:
             self._sparse_method(('slq', 'hutchinson'))
             if self.imate_method == 'slq' and exponent in (1, 2):

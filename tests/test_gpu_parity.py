@@ -352,3 +352,21 @@ def test_profiled_maximize_bracket_found_matches_reference(gp, capsys, fixture, 
     seq = cfg['maximize_profiled_der1_calls']
     check_der1_sequence(memo, seq)
     assert calls < len(seq)
+
+
+def test_traceinv_interpolation_on_device_operators(gp):
+    """interpolate=True (imate.InterpolateTraceInv in the reference,
+    mixed_correlation.py:52-66,167-170; parity unpinned: imate is absent): the
+    interpolant reproduces the operator's exact traceinv at its points, and
+    stays within 2 % between them, on the eigenvalue and cholesky operators."""
+    from gaussian_proc._mixed_correlation import MixedCorrelation
+    rng = numpy.random.RandomState(21)
+    K = matern.dense_correlation(rng.rand(300, 2), 0.15, 1.5)
+    lam = numpy.linalg.eigvalsh(K)
+    pts = numpy.logspace(-3, 2, 11)
+    for meth in ('eigenvalue', 'cholesky'):
+        op = MixedCorrelation(K, interpolate=True, interpolant_points=pts, imate_method=meth)
+        for t in pts[::3]:
+            assert rel(op.traceinv(t), numpy.sum(1.0 / (lam + t))) < 1e-9, (meth, t)
+        for t in numpy.logspace(-3, 2, 37):
+            assert rel(op.traceinv(t), numpy.sum(1.0 / (lam + t))) < 2e-2, (meth, t)
