@@ -20,6 +20,9 @@
 #ifndef GPMI_MATERN_NT
 #define GPMI_MATERN_NT 1
 #endif
+#ifndef GPMI_MATERN_MINB
+#define GPMI_MATERN_MINB 5    // minimum resident workgroups per CU (register cap: 96 VGPRs)
+#endif
 #ifndef GPMI_MATERN_PROBE
 #define GPMI_MATERN_PROBE 0   // development probes: 1 no kernel evaluation, 2 no stores
 #endif
@@ -151,11 +154,11 @@ __device__ __forceinline__ void store_nt(double* p, double v) {
 }
 
 template <int MODE>
-__global__ __launch_bounds__(256) void matern_dense_kernel_t(
+__global__ __launch_bounds__(256, GPMI_MATERN_MINB) void matern_dense_kernel_t(
     const double* __restrict__ points, int64_t n, int d,
     const double* __restrict__ scale_dev, MaternParams P, double* __restrict__ K,
     int64_t ldk, int64_t n_pad) {
-  __shared__ double tile[MT][MT + 1];
+  __shared__ double half[MT / 2][MT + 1];   // transpose buffer: 32 rows of the tile
   __shared__ double srow[MT * GPMI_MAX_DIM];
   __shared__ double sscale[GPMI_MAX_DIM], srs[GPMI_MAX_DIM];
   const int64_t b = blockIdx.x;
@@ -178,33 +181,44 @@ __global__ __launch_bounds__(256) void matern_dense_kernel_t(
   double pj[GPMI_MAX_DIM];
 #pragma unroll
   for (int k = 0; k < GPMI_MAX_DIM; ++k) pj[k] = (k < d && j < n) ? points[j * d + k] : 0.0;
+  // thread (r0, c) evaluates rows r0 + 4 q of column c and stores them at once
+  double v[MT / 4];
+#pragma unroll
   for (int q = 0; q < MT / 4; ++q) {
     const int r = r0 + 4 * q;
     const int64_t i = i0 + r;
-    double v;
     if (i < n && j < n) {
 #if GPMI_MATERN_PROBE == 1
-      v = scaled_distance(&srow[r * d], pj, sscale, srs, d);   // probe: no kernel evaluation
+      v[q] = scaled_distance(&srow[r * d], pj, sscale, srs, d);   // probe: no kernel evaluation
 #else
-      v = matern_value<MODE>(scaled_distance(&srow[r * d], pj, sscale, srs, d), P);
+      v[q] = matern_value<MODE>(scaled_distance(&srow[r * d], pj, sscale, srs, d), P);
 #endif
     } else {
-      v = (i == j) ? 1.0 : 0.0;
+      v[q] = (i == j) ? 1.0 : 0.0;
     }
-    tile[r][c] = v;
-  }
-  __syncthreads();
-#if GPMI_MATERN_PROBE == 2
-  if (tile[r0][c] != -1.0) return;   // probe: no stores
+#if GPMI_MATERN_PROBE != 2
+    if (i < n_pad && j < n_pad) store_nt(K + i * ldk + j, v[q]);
 #endif
-  for (int q = 0; q < MT / 4; ++q) {
-    const int r = r0 + 4 * q;
-    if (i0 + r < n_pad && j0 + c < n_pad) store_nt(K + (i0 + r) * ldk + j0 + c, tile[r][c]);
   }
+#if GPMI_MATERN_PROBE == 2
+  if (v[0] != -1.0) return;   // probe: no stores
+#endif
   if (I == J) return;
-  for (int q = 0; q < MT / 4; ++q) {
-    const int r = r0 + 4 * q;
-    if (j0 + r < n_pad && i0 + c < n_pad) store_nt(K + (j0 + r) * ldk + i0 + c, tile[c][r]);
+  // the transpose, 32 tile rows per round through LDS: output row j0 + o holds
+  // tile column o; 32 lanes write its 32 entries i0 + 32 h .. + 32 (256 B)
+  const int oc = t & 31, orow = t >> 5;   // 8 output rows per pass
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+#pragma unroll
+    for (int q = 0; q < MT / 8; ++q) half[r0 + 4 * q][c] = v[q + (MT / 8) * h];
+    __syncthreads();
+#pragma unroll
+    for (int p = 0; p < MT / 8; ++p) {
+      const int o = orow + 8 * p;
+      const int64_t jr = j0 + o, ic = i0 + 32 * h + oc;
+      if (jr < n_pad && ic < n_pad) store_nt(K + jr * ldk + ic, half[oc][o]);
+    }
+    __syncthreads();
   }
 }
 
