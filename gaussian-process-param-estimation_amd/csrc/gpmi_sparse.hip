@@ -180,12 +180,16 @@ __global__ void lanczos_scalar_kernel(const double* __restrict__ H1k,
 
 // Normalised Rademacher probes: V[i][c] = +-1/sqrt(n), bit 63 of
 // splitmix64(seed * G + (c + c0) * H + i) (matches oracle/sparse.py).
+// perm (optional): device row r holds original point perm[r] (locality order of
+// gpmi_sp_create_matern); the probe entry follows the original index, so the
+// probe set is the same vectors whatever the storage order.
 __global__ __launch_bounds__(256) void rademacher_kernel(double* __restrict__ V, int64_t n, int s,
                                                          unsigned long long seed, int c0,
-                                                         double scale) {
+                                                         double scale,
+                                                         const int* __restrict__ perm) {
   const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (e >= n * s) return;
-  const int64_t i = e / s;
+  const int64_t i = perm ? (int64_t)perm[e / s] : e / s;
   const int c = (int)(e % s);
   unsigned long long x = seed * 0x9E3779B97F4A7C15ull +
                          (unsigned long long)(c + c0) * 0xD1B54A32D192ED03ull +
@@ -398,6 +402,23 @@ __global__ void ms_init_kernel(MsState st, const double* __restrict__ partial, i
     st.active[t] = br[s * s + t] > 0.0 ? 1 : 0;
   }
   if (t == 0) st.flags[0] = 0;
+}
+
+// Row r of the reordered CSR = row perm[r] of the original with every column j
+// renamed inv[j] (entries kept in their original order): one wave per row.
+__global__ __launch_bounds__(256) void csr_permute_kernel(
+    const int64_t* __restrict__ ip, const int* __restrict__ ix, const double* __restrict__ dv,
+    const int* __restrict__ perm, const int* __restrict__ inv, int64_t n,
+    const int64_t* __restrict__ ip2, int* __restrict__ ix2, double* __restrict__ dv2) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= n) return;
+  const int64_t i = perm[r];
+  const int64_t k0 = ip[i], cnt = ip[i + 1] - k0, o = ip2[r];
+  for (int64_t q = lane; q < cnt; q += 64) {
+    ix2[o + q] = inv[ix[k0 + q]];
+    dv2[o + q] = dv[k0 + q];
+  }
 }
 
 }  // namespace gpmi

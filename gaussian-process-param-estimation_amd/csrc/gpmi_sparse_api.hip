@@ -39,7 +39,10 @@ __global__ void col_gs_update_kernel(double*, const double*, int64_t, const doub
                                      int);
 __global__ void col_axpby_kernel(const double*, double*, const double*, const double*, int64_t,
                                  int);
-__global__ void rademacher_kernel(double*, int64_t, int, unsigned long long, int, double);
+__global__ void rademacher_kernel(double*, int64_t, int, unsigned long long, int, double,
+                                  const int*);
+__global__ void csr_permute_kernel(const int64_t*, const int*, const double*, const int*,
+                                   const int*, int64_t, const int64_t*, int*, double*);
 __global__ void lanczos_scalar_kernel(const double*, const double*, const double*, int, int, int,
                                       int*, double*, double*, double*, double*, double*,
                                       double*);
@@ -116,6 +119,12 @@ struct gpmi_sp {
   size_t lz_doubles = 0;
   size_t msbuf_doubles = 0;
   int last_converged = 1;      // last gpmi_sp_cg / gpmi_sp_msgram met rtol in every column
+  // Locality order (gpmi_sp_create_matern, d <= 3): device row r is original point
+  // perm[r] (cells in Morton order), so the rows a CU streams through have their X
+  // gathers in a compact window that stays in its XCD's L2. Host inputs and
+  // outputs of every call stay in the original order (permuted at the boundary).
+  std::vector<int> perm;       // empty: identity
+  int* perm_d = nullptr;
 };
 
 namespace {
@@ -161,6 +170,19 @@ int col_dots(gpmi_sp* sp, const double* A, int64_t strideA, int J, const double*
 }
 
 unsigned grid_ns(int64_t n, int s) { return (unsigned)((n * s + 255) / 256); }
+
+// device row r <- original row orig(r)
+inline int64_t orig_row(const gpmi_sp* sp, int64_t r) {
+  return sp->perm.empty() ? r : (int64_t)sp->perm[r];
+}
+
+// Morton (Z-order) key of a cell's integer coordinates (d <= 3, 21 bits each).
+uint64_t morton3(const int64_t (&q)[3], int d) {
+  uint64_t key = 0;
+  for (int b = 20; b >= 0; --b)
+    for (int k = 0; k < d; ++k) key = (key << 1) | (uint64_t)((q[k] >> b) & 1);
+  return key;
+}
 
 // Lanczos of K on s probe columns starting from V0 (already in V block 0).
 // alpha/beta: host [s][steps] (column-major by probe). CGS2 reorthogonalisation.
@@ -313,6 +335,7 @@ int gpmi_sp_create_matern(int device, const double* points, int64_t n, int d,
   bool cells = d <= 3 && n < (int64_t)1 << 28 && !(brute_env && std::atoi(brute_env) != 0);
   int* dcell = nullptr;   // [n] cell of each point, then gdim [d], cell_start, perm
   int *dgdim = nullptr, *dstart = nullptr, *dperm = nullptr;
+  std::vector<int> lorder;   // locality order of the rows (Morton order of the cells)
   if (cells) {
     double pmin[3], pmax[3], wid[3];
     int64_t G[3] = {1, 1, 1};
@@ -356,6 +379,25 @@ int gpmi_sp_create_matern(int device, const double* points, int64_t n, int d,
       for (int64_t c = 0; c < total; ++c) hstart[c + 1] += hstart[c];
       std::vector<int> fillp(hstart.begin(), hstart.end() - 1);
       for (int64_t i = 0; i < n; ++i) hperm[fillp[hcell[i]]++] = (int)i;   // ascending i per cell
+      // GPMI_SPARSE_REORDER=0 keeps the rows in the original order
+      const char* ro = std::getenv("GPMI_SPARSE_REORDER");
+      if (!(ro && std::atoi(ro) == 0) && n > 1) {
+        std::vector<std::pair<uint64_t, int64_t>> keys;
+        keys.reserve(total);
+        for (int64_t c = 0; c < total; ++c) {
+          if (hstart[c + 1] == hstart[c]) continue;
+          int64_t q[3] = {0, 0, 0}, cc = c;
+          for (int k = 0; k < d; ++k) {
+            q[k] = cc % G[k];
+            cc /= G[k];
+          }
+          keys.emplace_back(morton3(q, d), c);
+        }
+        std::sort(keys.begin(), keys.end());
+        lorder.reserve(n);
+        for (const auto& kc : keys)
+          for (int q = hstart[kc.second]; q < hstart[kc.second + 1]; ++q) lorder.push_back(hperm[q]);
+      }
       SP_TRY(hipMalloc(&dcell, sizeof(int) * (2 * n + d + total + 1)));
       dgdim = dcell + n;
       dstart = dgdim + d;
@@ -399,6 +441,37 @@ int gpmi_sp_create_matern(int device, const double* points, int64_t n, int d,
     SP_LAUNCH("csr_fill_kernel");
   }
   SP_TRY(hipStreamSynchronize(st));
+  if (cells && (int64_t)lorder.size() == n) {
+    // rows (and columns) renumbered in the locality order: K' = P K P^T
+    std::vector<int> inv(n);
+    for (int64_t r = 0; r < n; ++r) inv[lorder[r]] = (int)r;
+    std::vector<int64_t> ip2(n + 1, 0);
+    for (int64_t r = 0; r < n; ++r) ip2[r + 1] = ip2[r] + cnt[lorder[r]];
+    int* dpi = nullptr;
+    int64_t* dip2 = nullptr;
+    int* dix2 = nullptr;
+    double* ddv2 = nullptr;
+    SP_TRY(hipMalloc(&sp->perm_d, sizeof(int) * n));
+    SP_TRY(hipMalloc(&dpi, sizeof(int) * n));
+    SP_TRY(hipMalloc(&dip2, sizeof(int64_t) * (n + 1)));
+    SP_TRY(hipMalloc(&dix2, sizeof(int) * std::max<int64_t>(1, sp->nnz)));
+    SP_TRY(hipMalloc(&ddv2, sizeof(double) * std::max<int64_t>(1, sp->nnz)));
+    SP_TRY(hipMemcpyAsync(sp->perm_d, lorder.data(), sizeof(int) * n, hipMemcpyHostToDevice, st));
+    SP_TRY(hipMemcpyAsync(dpi, inv.data(), sizeof(int) * n, hipMemcpyHostToDevice, st));
+    SP_TRY(hipMemcpyAsync(dip2, ip2.data(), sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(csr_permute_kernel, dim3(grid), dim3(256), 0, st, sp->indptr, sp->indices,
+                       sp->data, sp->perm_d, dpi, n, dip2, dix2, ddv2);
+    SP_LAUNCH("csr_permute_kernel");
+    SP_TRY(hipStreamSynchronize(st));
+    SP_TRY(hipFree(sp->indptr));
+    SP_TRY(hipFree(sp->indices));
+    SP_TRY(hipFree(sp->data));
+    SP_TRY(hipFree(dpi));
+    sp->indptr = dip2;
+    sp->indices = dix2;
+    sp->data = ddv2;
+    sp->perm = std::move(lorder);
+  }
   if (dcell) SP_TRY(hipFree(dcell));
   SP_TRY(hipFree(dp));
   SP_TRY(hipFree(ds));
@@ -411,6 +484,7 @@ int gpmi_sp_destroy(gpmi_sp* sp) {
   if (!sp) return 0;
   Guard g(sp->device);
   if (sp->stream) (void)hipStreamSynchronize(sp->stream);
+  if (sp->perm_d) (void)hipFree(sp->perm_d);
   if (sp->indptr) (void)hipFree(sp->indptr);
   if (sp->indices) (void)hipFree(sp->indices);
   if (sp->data) (void)hipFree(sp->data);
@@ -434,9 +508,39 @@ int gpmi_sp_info(const gpmi_sp* sp, int64_t* n, int64_t* nnz) {
 int gpmi_sp_get_csr(gpmi_sp* sp, int64_t* indptr, int* indices, double* data) {
   if (!sp) return set_error(-1006, "null handle");
   Guard g(sp->device);
-  SP_TRY(hipMemcpy(indptr, sp->indptr, sizeof(int64_t) * (sp->n + 1), hipMemcpyDeviceToHost));
-  SP_TRY(hipMemcpy(indices, sp->indices, sizeof(int) * sp->nnz, hipMemcpyDeviceToHost));
-  SP_TRY(hipMemcpy(data, sp->data, sizeof(double) * sp->nnz, hipMemcpyDeviceToHost));
+  if (sp->perm.empty()) {
+    SP_TRY(hipMemcpy(indptr, sp->indptr, sizeof(int64_t) * (sp->n + 1), hipMemcpyDeviceToHost));
+    SP_TRY(hipMemcpy(indices, sp->indices, sizeof(int) * sp->nnz, hipMemcpyDeviceToHost));
+    SP_TRY(hipMemcpy(data, sp->data, sizeof(double) * sp->nnz, hipMemcpyDeviceToHost));
+    return 0;
+  }
+  // the original order: row i = device row inv[i], columns renamed back and sorted
+  const int64_t n = sp->n;
+  std::vector<int64_t> ip(n + 1);
+  std::vector<int> ix(sp->nnz);
+  std::vector<double> dv(sp->nnz);
+  SP_TRY(hipMemcpy(ip.data(), sp->indptr, sizeof(int64_t) * (n + 1), hipMemcpyDeviceToHost));
+  SP_TRY(hipMemcpy(ix.data(), sp->indices, sizeof(int) * sp->nnz, hipMemcpyDeviceToHost));
+  SP_TRY(hipMemcpy(dv.data(), sp->data, sizeof(double) * sp->nnz, hipMemcpyDeviceToHost));
+  std::vector<int> inv(n);
+  for (int64_t r = 0; r < n; ++r) inv[sp->perm[r]] = (int)r;
+  indptr[0] = 0;
+  std::vector<std::pair<int, double>> row;
+  for (int64_t i = 0; i < n; ++i) {
+    const int64_t r = inv[i];
+    row.clear();
+    for (int64_t q = ip[r]; q < ip[r + 1]; ++q) row.emplace_back(sp->perm[ix[q]], dv[q]);
+    std::sort(row.begin(), row.end(),
+              [](const std::pair<int, double>& a, const std::pair<int, double>& b) {
+                return a.first < b.first;
+              });
+    const int64_t o = indptr[i];
+    for (size_t q = 0; q < row.size(); ++q) {
+      indices[o + q] = row[q].first;
+      data[o + q] = row[q].second;
+    }
+    indptr[i + 1] = o + (int64_t)row.size();
+  }
   return 0;
 }
 
@@ -451,7 +555,7 @@ int gpmi_sp_spmm(gpmi_sp* sp, double eta, const double* X, int64_t ld, int ncol,
     if (rc) return rc;
     std::vector<double> h((size_t)n * s);
     for (int64_t i = 0; i < n; ++i)
-      for (int c = 0; c < s; ++c) h[(size_t)i * s + c] = X[i * ld + c0 + c];
+      for (int c = 0; c < s; ++c) h[(size_t)i * s + c] = X[orig_row(sp, i) * ld + c0 + c];
     SP_TRY(hipMemcpyAsync(sp->ws, h.data(), sizeof(double) * h.size(), hipMemcpyHostToDevice,
                           sp->stream));
     rc = spmm(sp, sp->ws, sp->ws + n * s, s, eta);
@@ -460,7 +564,7 @@ int gpmi_sp_spmm(gpmi_sp* sp, double eta, const double* X, int64_t ld, int ncol,
                           hipMemcpyDeviceToHost, sp->stream));
     SP_TRY(hipStreamSynchronize(sp->stream));
     for (int64_t i = 0; i < n; ++i)
-      for (int c = 0; c < s; ++c) Y[i * ldy + c0 + c] = h[(size_t)i * s + c];
+      for (int c = 0; c < s; ++c) Y[orig_row(sp, i) * ldy + c0 + c] = h[(size_t)i * s + c];
   }
   return 0;
 }
@@ -479,7 +583,8 @@ int gpmi_sp_lanczos(gpmi_sp* sp, int nprobe, int steps, uint64_t seed, int probe
     double* V = sp->ws;
     double* W = sp->ws + (size_t)(steps + 1) * n * s;
     hipLaunchKernelGGL(rademacher_kernel, dim3(grid_ns(n, s)), dim3(256), 0, sp->stream, V, n, s,
-                       (unsigned long long)seed, probe_offset + p0, 1.0 / std::sqrt((double)n));
+                       (unsigned long long)seed, probe_offset + p0, 1.0 / std::sqrt((double)n),
+                       (const int*)sp->perm_d);
     SP_LAUNCH("rademacher_kernel");
     rc = lanczos_block(sp, V, W, s, steps, alpha + (size_t)p0 * steps, beta + (size_t)p0 * steps);
     if (rc) return rc;
@@ -509,7 +614,7 @@ int gpmi_sp_cg(gpmi_sp* sp, double eta, const double* rhs, int64_t ld, int nrhs,
     double* cb = ca + MAXS;
     std::vector<double> h((size_t)ns);
     for (int64_t i = 0; i < n; ++i)
-      for (int c = 0; c < s; ++c) h[(size_t)i * s + c] = rhs[i * ld + c0 + c];
+      for (int c = 0; c < s; ++c) h[(size_t)i * s + c] = rhs[orig_row(sp, i) * ld + c0 + c];
     SP_TRY(hipMemcpyAsync(Rr, h.data(), sizeof(double) * ns, hipMemcpyHostToDevice, sp->stream));
     SP_TRY(hipMemcpyAsync(Pp, Rr, sizeof(double) * ns, hipMemcpyDeviceToDevice, sp->stream));
     SP_TRY(hipMemsetAsync(X, 0, sizeof(double) * ns, sp->stream));
@@ -574,7 +679,7 @@ int gpmi_sp_cg(gpmi_sp* sp, double eta, const double* rhs, int64_t ld, int nrhs,
     SP_TRY(hipMemcpyAsync(h.data(), X, sizeof(double) * ns, hipMemcpyDeviceToHost, sp->stream));
     SP_TRY(hipStreamSynchronize(sp->stream));
     for (int64_t i = 0; i < n; ++i)
-      for (int c = 0; c < s; ++c) sol[i * ldsol + c0 + c] = h[(size_t)i * s + c];
+      for (int c = 0; c < s; ++c) sol[orig_row(sp, i) * ldsol + c0 + c] = h[(size_t)i * s + c];
   }
   if (iterations) *iterations = max_it_used;
   sp->last_converged = converged ? 1 : 0;
@@ -629,7 +734,7 @@ int gpmi_sp_msgram(gpmi_sp* sp, const double* etas, int neta, const double* rhs,
   {
     std::vector<double> h((size_t)ns);
     for (int64_t i = 0; i < n; ++i)
-      for (int c = 0; c < s; ++c) h[(size_t)i * s + c] = rhs[i * ld + c];
+      for (int c = 0; c < s; ++c) h[(size_t)i * s + c] = rhs[orig_row(sp, i) * ld + c];
     SP_TRY(hipMemcpyAsync(Bd, h.data(), sizeof(double) * ns, hipMemcpyHostToDevice, str));
     std::vector<double> hd(S);
     for (int j = 0; j < S; ++j) hd[j] = etas[j] - eta0;
@@ -710,7 +815,7 @@ int gpmi_sp_bench_spmm(gpmi_sp* sp, int s, int reps, double eta, double* avg_ms)
   int rc = ensure_ws(sp, (size_t)2 * ns);
   if (rc) return rc;
   hipLaunchKernelGGL(rademacher_kernel, dim3(grid_ns(sp->n, s)), dim3(256), 0, sp->stream, sp->ws,
-                     sp->n, s, 12345ull, 0, 1.0);
+                     sp->n, s, 12345ull, 0, 1.0, (const int*)nullptr);
   SP_LAUNCH("rademacher_kernel");
   hipEvent_t e0, e1;
   SP_TRY(hipEventCreate(&e0));
