@@ -339,12 +339,7 @@ def run_sparse(args, world, rank, local, dist, torch):
             for i, e in enumerate(etas[lo:hi]):
                 rows[i] = [e, curves['logdet'][lo + i],
                            _lp_from_terms(n, m, 1.0, curves['logdet'][lo + i], Gs[i])]
-        t = torch.from_numpy(rows).cuda()
-        if world > 1:
-            out = torch.empty((world * per, 3), dtype=torch.float64, device=t.device)
-            dist.all_gather_into_tensor(out, t)
-            return out
-        return t
+        return gather_rows(rows, world, dist, torch)
 
     for _ in range(args.warmup):
         step()
@@ -495,13 +490,15 @@ def eta_block(args, world, rank, s=0):
 
 
 def gather_rows(rows, world, dist, torch):
-    """ONE all-gather of the per-rank [eta, logdet, lp] rows (RCCL at N > 1)."""
-    t = torch.from_numpy(numpy.ascontiguousarray(rows)).cuda()
+    """ONE all-gather of the per-rank [eta, logdet, lp] rows (RCCL over xGMI for
+    the nccl backend, gloo on CPU in the tests): gaussian_proc.sweep's
+    collective. Returns the [world * rows, 3] host array on every rank."""
+    rows = numpy.ascontiguousarray(rows)
     if world == 1:
-        return t
-    out = torch.empty((world * t.shape[0], t.shape[1]), dtype=torch.float64, device=t.device)
-    dist.all_gather_into_tensor(out, t)
-    return out
+        torch.cuda.synchronize()
+        return rows
+    from gaussian_proc.sweep import _all_gather_rows
+    return _all_gather_rows(dist, None, rows, world)
 
 
 def band_mode(args, D, X, z, world, rank, dist, torch, ld_ref=None):
@@ -764,7 +761,7 @@ def main():
             result['batch_efficiency'] = batch_efficiency(op, X, z)
     lam = None
     if not args.no_band:
-        ld_ref = (last[:own, 0].cpu().numpy(), last[:own, 1].cpu().numpy())
+        ld_ref = (last[:own, 0], last[:own, 1])
         bm, bop = band_mode(args, D, X, z, world, rank, dist, torch, ld_ref)
         log('band mode: %.1f evals/s' % bm['value'])
         if rank == 0:

@@ -200,3 +200,49 @@ def test_slq_quadrature_shift_check():
         _slq.quadrature(nodes, [1.0, 2.0], _slq.FUNCS['logdet'])
     q = _slq.quadrature(nodes, [1.6, 2.0], _slq.FUNCS['logdet'])
     assert numpy.all(numpy.isfinite(q))
+
+
+def _bench_worker(rank, world, port, out_q):
+    """bench.py's strong-scaled step plumbing on gloo: the rank's eta block of
+    the 64-point cfg3 curve and the one all-gather of the [eta, logdet, lp] rows
+    (the numbers here stand in for the device's)."""
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    import sys
+    import types
+    import torch
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import bench
+    args = types.SimpleNamespace(scaling='strong', eta_total=64, eta_per_rank=64)
+    etas, own, per, gsize = bench.eta_block(args, world, rank)
+    rows = numpy.stack([etas, numpy.log(etas), -etas], axis=1)
+    allrows = bench.gather_rows(rows, world, dist, torch)
+    out_q.put((rank, own, per, gsize, allrows))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('world', [2, 3])
+def test_bench_strong_scaling_blocks_and_all_gather_gloo(world):
+    """The 64-point curve split over N ranks (contiguous blocks, last block
+    padded by repeating its eta), gathered once: every rank ends with the whole
+    curve in order."""
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bench_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    grid = numpy.logspace(-3, 3, 64)
+    owns = [r[1] for r in res]
+    assert sum(owns) == 64
+    for rank, own, per, gsize, allrows in res:
+        assert gsize == 64 and allrows.shape == (world * per, 3)
+        got = numpy.concatenate([allrows[r * per:r * per + owns[r], 0] for r in range(world)])
+        numpy.testing.assert_array_equal(got, grid)
