@@ -288,6 +288,105 @@ void launch_ms_dots(const double* B, const double* R, int64_t n, int s, double* 
   }
 }
 
+// Fused r update + dots of one multi-shift CG iteration: every block first
+// reduces the p . q partials (fixed order, identical in every block) to the base
+// step a[c] = rr[c] / (p . q)[c] (0 once the column stopped; block (0, 0) stores a
+// and flags p^T A p <= 0), then r_new = r - a q from R (read only) into Rn
+// (written by the blockIdx.y == 0 blocks; the other column groups form the same
+// values in registers; R and Rn alternate between iterations) and the B^T r,
+// r . r partials as ms_dots_partial_kernel. Replaces the p . q reduce launch,
+// ms_r_update_kernel and one pass over r and q.
+template <int S>
+__global__ __launch_bounds__(256) void ms_rdots_partial_kernel(
+    const double* __restrict__ B, const double* __restrict__ R, double* __restrict__ Rn,
+    const double* __restrict__ Q, MsState st, const double* __restrict__ pqpart, int pq_nblk,
+    int64_t n, double* __restrict__ partial) {
+  constexpr int NE = S * S + S;
+  __shared__ double red[4][4 * S + S];
+  __shared__ double sa[S];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  for (int c = wv; c < S; c += 4) {
+    const double pq = wave_reduce_partials(pqpart, pq_nblk, S, c);
+    if (lane == 0) {
+      const int act = st.active[c];
+      const double a = act ? st.rr[c] / pq : 0.0;
+      sa[c] = a;
+      if (blockIdx.x == 0 && blockIdx.y == 0) {
+        st.a[c] = a;
+        if (act && !(pq > 0.0)) st.flags[0] = 1;
+      }
+    }
+  }
+  __syncthreads();
+  const int c0 = blockIdx.y * 4;
+  double acc[4][S], rr[S];
+#pragma unroll
+  for (int c = 0; c < S; ++c) {
+    rr[c] = 0.0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[q][c] = 0.0;
+  }
+  for (int64_t i = (int64_t)blockIdx.x * 256 + t; i < n; i += (int64_t)gridDim.x * 256) {
+    double r[S], b[4];
+#pragma unroll
+    for (int c = 0; c < S; ++c) r[c] = R[i * S + c] - sa[c] * Q[i * S + c];
+    if (blockIdx.y == 0) {
+#pragma unroll
+      for (int c = 0; c < S; ++c) Rn[i * S + c] = r[c];
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) b[q] = (c0 + q < S) ? B[i * S + c0 + q] : 0.0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int c = 0; c < S; ++c) acc[q][c] += b[q] * r[c];
+    if (blockIdx.y == 0) {
+#pragma unroll
+      for (int c = 0; c < S; ++c) rr[c] += r[c] * r[c];
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int c = 0; c < S; ++c) {
+      const double v = wave_sum(acc[q][c]);
+      if (lane == 0) red[wv][q * S + c] = v;
+    }
+#pragma unroll
+  for (int c = 0; c < S; ++c) {
+    const double v = wave_sum(rr[c]);
+    if (lane == 0) red[wv][4 * S + c] = v;
+  }
+  __syncthreads();
+  if (t < 5 * S) {
+    const double v = (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]);
+    if (t < 4 * S) {
+      const int q = t / S, c = t - q * S;
+      if (c0 + q < S) partial[(int64_t)blockIdx.x * NE + (c0 + q) * S + c] = v;
+    } else if (blockIdx.y == 0) {
+      partial[(int64_t)blockIdx.x * NE + S * S + (t - 4 * S)] = v;
+    }
+  }
+}
+
+void launch_ms_rdots(const double* B, const double* R, double* Rn, const double* Q,
+                     const MsState& st, const double* pqpart, int pq_nblk, int64_t n, int s,
+                     double* partial, int nblk, hipStream_t stream) {
+  const dim3 grid(nblk, (s + 3) / 4), blk(256);
+  switch (s) {
+#define MS_CASE(k)                                                                          \
+  case k:                                                                                   \
+    hipLaunchKernelGGL(ms_rdots_partial_kernel<k>, grid, blk, 0, stream, B, R, Rn, Q, st,     \
+                       pqpart, pq_nblk, n, partial);                                        \
+    break;
+    MS_CASE(1) MS_CASE(2) MS_CASE(3) MS_CASE(4) MS_CASE(5) MS_CASE(6) MS_CASE(7) MS_CASE(8)
+    MS_CASE(9) MS_CASE(10) MS_CASE(11) MS_CASE(12) MS_CASE(13) MS_CASE(14) MS_CASE(15)
+    MS_CASE(16)
+#undef MS_CASE
+    default: break;
+  }
+}
+
 // r[i][c] -= a[c] q[i][c] with the base step a[c] = rr[c] / (p . q)[c] (0 once the
 // column stopped) formed per element; the first workgroup also stores a for the
 // scalar kernel (the separate alpha launch folded in).

@@ -49,6 +49,9 @@ __global__ void lanczos_scalar_kernel(const double*, const double*, const double
 void launch_ms_dots(const double* B, const double* R, int64_t n, int s, double* partial, int nblk,
                     hipStream_t st);
 __global__ void ms_r_update_kernel(double*, const double*, MsState, const double*, int64_t, int);
+void launch_ms_rdots(const double* B, const double* R, double* Rn, const double* Q,
+                     const MsState& st, const double* pqpart, int pq_nblk, int64_t n, int s,
+                     double* partial, int nblk, hipStream_t stream);
 __global__ void ms_scalar_kernel(MsState, const double*, int, const double*, int, int, double,
                                  double*);
 __global__ void ms_p_update_kernel(double*, const double*, const double*, const int*, int64_t,
@@ -696,11 +699,13 @@ int gpmi_sp_msgram(gpmi_sp* sp, const double* etas, int neta, const double* rhs,
   const int s = nrhs, S = neta;
   const int64_t ns = n * s;
   const double eta0 = *std::min_element(etas, etas + neta);
-  int rc = ensure_ws(sp, (size_t)4 * ns);
+  int rc = ensure_ws(sp, (size_t)5 * ns);
   if (rc) return rc;
   const int ne = s * s + s;
-  rc = ensure_partial(sp, (size_t)NBLK * std::max(ne, s));
+  // [MS_NBLK][ne] dot partials, then [NBLK][s] p . q partials
+  rc = ensure_partial(sp, (size_t)MS_NBLK * ne + (size_t)NBLK * s);
   if (rc) return rc;
+  double* pqpart = sp->partial + (size_t)MS_NBLK * ne;
   const size_t need = (size_t)6 * s + 2 * (size_t)S * s + 2 * (size_t)S * s * s + S + s + s + 1;
   if (sp->msbuf_doubles < need) {
     if (sp->msbuf) SP_TRY(hipFree(sp->msbuf));
@@ -715,7 +720,7 @@ int gpmi_sp_msgram(gpmi_sp* sp, const double* etas, int neta, const double* rhs,
   st.a_prev = q; q += s;
   st.beta = q; q += s;
   st.bn2 = q; q += s;
-  double* pq = q; q += s;
+  double* pqd = q; q += s;   // p . q (unfused r update)
   st.z = q; q += (size_t)S * s;
   st.z_prev = q; q += (size_t)S * s;
   st.bp = q; q += (size_t)S * s * s;
@@ -730,6 +735,12 @@ int gpmi_sp_msgram(gpmi_sp* sp, const double* etas, int neta, const double* rhs,
   double* Rd = Bd + ns;
   double* Pd = Rd + ns;
   double* Qd = Pd + ns;
+  double* Rd2 = Qd + ns;   // the residual alternates between Rd and Rd2
+  // fused p . q reduction + r update + dots for <= 2 column groups of 4 (the
+  // fused kernel re-reads q once per group)
+  const bool fused_r = (s + 3) / 4 <= 2;
+  double* Rcur = Rd;     // the live residual
+  double* Rnext = Rd2;
   hipStream_t str = sp->stream;
   {
     std::vector<double> h((size_t)ns);
@@ -773,18 +784,33 @@ int gpmi_sp_msgram(gpmi_sp* sp, const double* etas, int neta, const double* rhs,
     }
     rc = spmm(sp, Pd, Qd, s, eta0);
     if (rc) return rc;
-    rc = col_dots(sp, Pd, 0, 1, Qd, s, pq);
-    if (rc) return rc;
-    hipLaunchKernelGGL(ms_r_update_kernel, dim3(grid_ns(n, s)), dim3(256), 0, str, Rd, Qd, st,
-                       pq, n, s);
-    SP_LAUNCH("ms_r_update_kernel");
-    launch_ms_dots(Bd, Rd, n, s, sp->partial, MS_NBLK, str);
-    SP_LAUNCH("ms_dots_partial_kernel");
+    double* Rout = Rcur;
+    if (fused_r) {
+      // p . q partials; the reduction, r update and dots in one launch (r_new to the
+      // other buffer)
+      hipLaunchKernelGGL(col_dot_partial_kernel, dim3(NBLK, 1), dim3(256), 0, str, Pd,
+                         (int64_t)0, Qd, n, s, pqpart);
+      SP_LAUNCH("col_dot_partial_kernel");
+      Rout = Rnext;
+      launch_ms_rdots(Bd, Rcur, Rout, Qd, st, pqpart, NBLK, n, s, sp->partial, MS_NBLK, str);
+      SP_LAUNCH("ms_rdots_partial_kernel");
+      std::swap(Rcur, Rnext);
+    } else {
+      // more than two 4-column groups would re-read q per group in the fused form:
+      // the r update in place, then the dots
+      rc = col_dots(sp, Pd, 0, 1, Qd, s, pqd);
+      if (rc) return rc;
+      hipLaunchKernelGGL(ms_r_update_kernel, dim3(grid_ns(n, s)), dim3(256), 0, str, Rcur, Qd, st,
+                         pqd, n, s);
+      SP_LAUNCH("ms_r_update_kernel");
+      launch_ms_dots(Bd, Rcur, n, s, sp->partial, MS_NBLK, str);
+      SP_LAUNCH("ms_dots_partial_kernel");
+    }
     hipLaunchKernelGGL(ms_scalar_kernel, dim3(1), dim3(sthreads), 0, str, st, sp->partial, MS_NBLK,
                        dshift, S, s, rtol * rtol, beta_out);
     SP_LAUNCH("ms_scalar_kernel");
-    hipLaunchKernelGGL(ms_p_update_kernel, dim3(grid_ns(n, s)), dim3(256), 0, str, Pd, Rd, st.beta,
-                       st.active, n, s);
+    hipLaunchKernelGGL(ms_p_update_kernel, dim3(grid_ns(n, s)), dim3(256), 0, str, Pd, Rout,
+                       st.beta, st.active, n, s);
     SP_LAUNCH("ms_p_update_kernel");
   }
   {
