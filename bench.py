@@ -353,10 +353,7 @@ def run_sparse(args, world, rank, local, dist, torch):
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    t_max = torch.tensor([dt], dtype=torch.float64, device='cuda')
-    if world > 1:
-        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
-    dt = float(t_max.item())
+    dt = max_over_ranks(dt, world, dist, torch)
     # SpMM roofline on a device-resident probe block (HIP events)
     s_blk = max(1, min(32, nprobe // world))
     ms = op.sop.bench_spmm(s_blk, 50)
@@ -489,6 +486,17 @@ def eta_block(args, world, rank, s=0):
     return grid[idx], B, B, grid.size
 
 
+def max_over_ranks(dt, world, dist, torch):
+    """Wall time of the slowest rank (all-reduce MAX; a device tensor on RCCL,
+    a host tensor on gloo)."""
+    if world == 1:
+        return dt
+    dev = 'cuda' if dist.get_backend() == 'nccl' else 'cpu'
+    t_max = torch.tensor([dt], dtype=torch.float64, device=dev)
+    dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+    return float(t_max.item())
+
+
 def gather_rows(rows, world, dist, torch):
     """ONE all-gather of the per-rank [eta, logdet, lp] rows (RCCL over xGMI for
     the nccl backend, gloo on CPU in the tests): gaussian_proc.sweep's
@@ -541,10 +549,7 @@ def band_mode(args, D, X, z, world, rank, dist, torch, ld_ref=None):
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    t_max = torch.tensor([dt], dtype=torch.float64, device='cuda')
-    if world > 1:
-        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
-    dt = float(t_max.item())
+    dt = max_over_ranks(dt, world, dist, torch)
     K = args.steps
     red = acc['reduce_ms'] / K
     flops_red = 4.0 * n ** 3 / 3.0
@@ -620,9 +625,18 @@ def main():
     local = int(os.environ.get('LOCAL_RANK', '0'))
     import torch
     import torch.distributed as dist
+    # one process per GPU over RCCL; GPMI_BENCH_BACKEND=gloo with
+    # GPMI_BENCH_SHARE_DEVICE=1 rehearses the N>1 flow with every rank on
+    # device 0 (the one-GPU box), host-side collectives
+    backend = os.environ.get('GPMI_BENCH_BACKEND', 'nccl')
+    if os.environ.get('GPMI_BENCH_SHARE_DEVICE') == '1':
+        local = 0
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        if backend == 'nccl':
+            dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        else:
+            dist.init_process_group(backend)
 
     if args.config != 'dense':
         return run_sparse(args, world, rank, local, dist, torch)
@@ -677,10 +691,7 @@ def main():
     barrier()
     dt = time.perf_counter() - t0
     op.op.set_timing(False)
-    t_max = torch.tensor([dt], dtype=torch.float64, device='cuda')
-    if world > 1:
-        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
-    dt = float(t_max.item())
+    dt = max_over_ranks(dt, world, dist, torch)
     log('dense: %d steps in %.2f s' % (args.steps, dt))
     # evaluations the job completed: the whole curve per step (strong), or every
     # rank's block (weak)
