@@ -435,6 +435,26 @@ def sparse_reference_check(op, config, X, z):
         est, se = q.mean(axis=0), q.std(axis=0, ddof=1) / numpy.sqrt(q.shape[0])
         out['slq_logdet_err_in_std_errors'] = [round(float(v), 3) for v in
                                                numpy.abs(est - g['logdet']) / se]
+        if op.n <= 65536:
+            # the exact 'cholesky' method on this sparse K (dense device copy,
+            # fp64 MFMA Cholesky per eta) against the same SuperLU values
+            from gaussian_proc._mixed_correlation import MixedCorrelation
+            ex = MixedCorrelation(op.K, imate_method='cholesky')
+            t0 = time.perf_counter()
+            ex._dense()
+            t_copy = time.perf_counter() - t0
+            t0 = time.perf_counter()
+            ld, Ge = ex.loglik_terms(g['etas'], X, z)
+            t_eval = (time.perf_counter() - t0) / len(g['etas'])
+            out['exact_cholesky'] = {
+                'dense_copy_s': round(t_copy, 3), 'per_eta_s': round(t_eval, 3),
+                'logdet_rel_err': float(numpy.max(numpy.abs(ld - g['logdet']) /
+                                                  numpy.abs(g['logdet']))),
+                'gram_rel_err': float(max(numpy.max(numpy.abs(Gj - numpy.asarray(Gr))) /
+                                          numpy.max(numpy.abs(Gr))
+                                          for Gj, Gr in zip(Ge, g['gram'])))}
+            ex.op.close()
+            del ex
     return out
 
 

@@ -497,6 +497,14 @@ int op_view(const gpmi_op* op, OpView* v) {
 }
 }  // namespace gpmi
 
+namespace {
+// K[i][i] = 1 for the pad rows n <= i < n_pad (at most 127 of them).
+__global__ void pad_identity_kernel(double* K, int64_t ldk, int64_t n) {
+  const int64_t i = n + threadIdx.x;
+  if (i < ldk) K[i * ldk + i] = 1.0;
+}
+}  // namespace
+
 extern "C" {
 
 int gpmi_version(void) { return 100; }
@@ -712,6 +720,26 @@ int gpmi_op_load_matrix(gpmi_op* op, const double* K_host, int64_t ldk) {
     for (int64_t i = n; i < np; ++i)
       HIP_TRY(hipMemcpyAsync(op->K + i * np + i, one.data(), sizeof(double),
                              hipMemcpyHostToDevice, op->stream));
+  }
+  HIP_TRY(hipStreamSynchronize(op->stream));
+  op->has_K = true;
+  op->cache_valid = false;
+  return 0;
+}
+
+int gpmi_op_load_sparse(gpmi_op* op, const gpmi_sp* sp) {
+  if (!op || !sp) return set_err(-1006, "null handle");
+  int64_t n_sp = 0;
+  if (int rc = gpmi_sp_info(sp, &n_sp, nullptr)) return rc;
+  if (n_sp != op->n) return set_err(-1005, "sparse operator has n = %lld, dense has %lld",
+                                    (long long)n_sp, (long long)op->n);
+  DeviceGuard g(op->device);
+  const int64_t np = op->n_pad;
+  HIP_TRY(hipMemsetAsync(op->K, 0, sizeof(double) * np * np, op->stream));
+  if (int rc = gpmi::sp_scatter_dense(sp, op->device, op->K, np, op->stream)) return rc;
+  if (np > op->n) {
+    hipLaunchKernelGGL(pad_identity_kernel, dim3(1), dim3(128), 0, op->stream, op->K, np, op->n);
+    HIP_TRY(hipGetLastError());
   }
   HIP_TRY(hipStreamSynchronize(op->stream));
   op->has_K = true;

@@ -8,6 +8,8 @@
 #define GPMI_TS 128        // tile / diagonal-block size of the blocked Cholesky
 #define GPMI_RHS_LD 16     // leading dimension (max columns) of a resident RHS block
 
+struct gpmi_sp;   // include/gpmi.h
+
 namespace gpmi {
 
 enum MaternMode { MATERN_HALF = 0, MATERN_3HALF = 1, MATERN_5HALF = 2,
@@ -78,5 +80,10 @@ struct MsState {
   double* g;       // [S][s'][s] accumulated G_j[c'][c]
   int* flags;      // [1]   set when an active column meets p^T (K + eta_0 I) p <= 0
 };
+
+// Scatter a sparse operator's CSR (original point order) into a zeroed dense
+// [n][ldk] matrix on the same device (gpmi_sparse_api.hip).
+int sp_scatter_dense(const ::gpmi_sp* sp, int device, double* K, int64_t ldk,
+                     hipStream_t st);
 
 }  // namespace gpmi

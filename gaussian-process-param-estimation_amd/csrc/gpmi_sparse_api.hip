@@ -547,6 +547,45 @@ int gpmi_sp_get_csr(gpmi_sp* sp, int64_t* indptr, int* indices, double* data) {
   return 0;
 }
 
+}  // extern "C"
+
+namespace gpmi {
+
+// K[perm[r]][perm[c]] = a_rc: one wavefront per device row (the dense copy is in
+// the original point order).
+__global__ void __launch_bounds__(256) csr_scatter_dense_kernel(
+    const int64_t* __restrict__ indptr, const int* __restrict__ indices,
+    const double* __restrict__ data, const int* __restrict__ perm, int64_t n,
+    double* __restrict__ K, int64_t ldk) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= n) return;
+  const int lane = threadIdx.x & 63;
+  const int64_t i = perm ? perm[r] : r;
+  double* Ki = K + i * ldk;
+  for (int64_t q = indptr[r] + lane; q < indptr[r + 1]; q += 64) {
+    const int c = indices[q];
+    Ki[perm ? perm[c] : c] = data[q];
+  }
+}
+
+// Scatter the operator's CSR into a zeroed dense [n][ldk] device matrix on the
+// device `device` (stream st); the dense operator's exact methods on a sparse K.
+int sp_scatter_dense(const gpmi_sp* sp, int device, double* K, int64_t ldk, hipStream_t st) {
+  if (sp->device != device)
+    return set_error(-1011, "sparse and dense operators live on different devices");
+  SP_TRY(hipStreamSynchronize(sp->stream));
+  const unsigned grid = (unsigned)((sp->n + 3) / 4);
+  hipLaunchKernelGGL(csr_scatter_dense_kernel, dim3(grid), dim3(256), 0, st, sp->indptr,
+                     sp->indices, sp->data, sp->perm.empty() ? nullptr : sp->perm_d, sp->n, K,
+                     ldk);
+  SP_LAUNCH("csr_scatter_dense_kernel");
+  return 0;
+}
+
+}  // namespace gpmi
+
+extern "C" {
+
 int gpmi_sp_spmm(gpmi_sp* sp, double eta, const double* X, int64_t ld, int ncol, double* Y,
                  int64_t ldy) {
   if (!sp) return set_error(-1006, "null handle");

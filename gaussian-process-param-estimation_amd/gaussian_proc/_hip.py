@@ -36,6 +36,7 @@ SIGNATURES = {
     'gpmi_op_destroy': (ctypes.c_int, [c_op_p]),
     'gpmi_op_size': (ctypes.c_int, [c_op_p, ctypes.POINTER(c_i64), ctypes.POINTER(c_i64)]),
     'gpmi_op_load_matrix': (ctypes.c_int, [c_op_p, c_double_p, c_i64]),
+    'gpmi_op_load_sparse': (ctypes.c_int, [c_op_p, c_op_p]),
     'gpmi_op_assemble_matern': (ctypes.c_int, [c_op_p, c_double_p, ctypes.c_int, c_double_p,
                                                ctypes.c_double]),
     'gpmi_op_get_matrix': (ctypes.c_int, [c_op_p, c_double_p, c_i64]),
@@ -202,6 +203,13 @@ class Operator(object):
         if K.shape != (self.n, self.n):
             raise ValueError('K must be %d x %d' % (self.n, self.n))
         check(self.lib.gpmi_op_load_matrix(self.h, dptr(K), self.n), 'gpmi_op_load_matrix')
+
+    def load_sparse(self, sop):
+        """K from a SparseOperator on the same device (device-side scatter of its
+        CSR): the exact methods on a sparse K."""
+        if sop.n != self.n:
+            raise ValueError('sparse operator has n = %d, expected %d' % (sop.n, self.n))
+        check(self.lib.gpmi_op_load_sparse(self.h, sop.h), 'gpmi_op_load_sparse')
 
     def assemble_matern(self, points, scale, nu):
         points = as_c(points)

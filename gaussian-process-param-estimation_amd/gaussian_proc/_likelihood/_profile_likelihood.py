@@ -27,7 +27,7 @@ __all__ = ['ProfileLikelihood']
 
 def _use_band(K_mixed):
     return hasattr(K_mixed, 'der_terms') and getattr(K_mixed, 'imate_method', None) == \
-        'eigenvalue' and not getattr(K_mixed, 'sparse', False)
+        'eigenvalue'
 
 
 def _der_from_terms(n, m, G1, G2, G3, tr1, tr2=None):

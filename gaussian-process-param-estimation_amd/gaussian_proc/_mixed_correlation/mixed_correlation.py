@@ -19,7 +19,14 @@ once per operator.
   inverse.
 * 'hutchinson' traceinv (:193-203): Rademacher probes solved with the device
   Cholesky (stochastic; parity unpinned against imate, which is absent).
-* sparse K: 'slq' / 'hutchinson' with device Lanczos and CG.
+* sparse K: 'slq' (logdet / traceinv by device Lanczos quadrature) and
+  'hutchinson' traceinv (CG solves); solve by device CG as the reference's
+  linear_solver (_linear_solver.py:57-68). The exact methods ('cholesky', and
+  'hutchinson' logdet, which the reference hands to imate's sparse Cholesky
+  via CHOLMOD, :250-261; 'eigenvalue', whose eigh of a sparse K raises in the
+  reference, :76-79) run the dense device paths above on a copy of K scattered
+  from the CSR on the device (8 n_pad^2 bytes per copy: N = 65536 takes 34 GB
+  of the 288 GB HBM).
 
 ``interpolate=True`` answers traceinv from an interpolant in eta built on the
 exact values at ``interpolant_points`` (_interpolate.py; the reference's
@@ -60,7 +67,7 @@ class MixedCorrelation(object):
         self.interpolate_traceinv = None
         self.sparse = False
         if isinstance(K, DeviceSparseCorrelation) or scipy.sparse.issparse(K):
-            self._init_sparse(K, device)
+            self._init_sparse(K, device, max_batch)
             return
         if isinstance(K, DeviceCorrelation):
             if max_batch is not None and max_batch > K.op.max_batch:
@@ -116,7 +123,7 @@ class MixedCorrelation(object):
         Afterwards logdet(eta) and the likelihood terms cost one banded Cholesky
         of B + eta I per eta (csrc/gpmi_band.hip)."""
         if self._band is None:
-            self._band = _hip.Band(self.op)
+            self._band = _hip.Band(self._dense())
         return self._band
 
     def refresh_band(self, X=None, z=None):
@@ -170,8 +177,8 @@ class MixedCorrelation(object):
         (csrc/gpmi_band.hip band_der_kernel). They replace the 2-5 dense solves
         per eta of ProfileLikelihood.log_likelihood_der1_eta / der2_eta
         (_profile_likelihood.py:91-192). Returns (logdet, G1, G2, G3)."""
-        if self.sparse or self.imate_method != 'eigenvalue':
-            raise NotImplementedError('der_terms needs the dense eigenvalue operator')
+        if self.imate_method != 'eigenvalue':
+            raise NotImplementedError('der_terms needs the eigenvalue operator')
         etas = numpy.atleast_1d(numpy.asarray(etas, dtype=float))
         b = self._band_rhs_set(X, z)
         c = getattr(self, '_der_cache', None)
@@ -186,7 +193,7 @@ class MixedCorrelation(object):
 
     # ---- sparse K (tapered Matérn, CSR on the device) -------------------------
 
-    def _init_sparse(self, K, device):
+    def _init_sparse(self, K, device, max_batch):
         """Sparse K: logdet / traceinv by stochastic Lanczos quadrature
         ('slq'; one device Lanczos run per probe, cached, serves every eta) or
         Hutchinson ('hutchinson' traceinv, CG solves); solve by blocked CG with
@@ -199,9 +206,13 @@ class MixedCorrelation(object):
             self.K = K.tocsr()
             self.sop = _hip.SparseOperator.from_csr(self.K, device=device)
         self.n = self.sop.n
-        self.op = None
+        self.op = None            # dense copy of K for the exact methods (_dense)
+        self._max_batch = max_batch
         self._trace_cache = None
         self._rhs_cache = None
+        self._band = None
+        self._band_rhs = None
+        self._eig = None
         opts = dict(self.imate_options or {})
         self.num_samples = int(opts.get('num_samples', opts.get('max_num_samples', 20)))
         self.lanczos_degree = int(opts.get('lanczos_degree', 30))
@@ -228,14 +239,17 @@ class MixedCorrelation(object):
             self._trace_cache = (float(Kc.diagonal().sum()), float(numpy.sum(Kc.data ** 2)))
         return self._trace_cache
 
-    def _sparse_method(self, allowed):
-        if self.imate_method not in allowed:
-            if self.imate_method in _METHODS:
-                raise NotImplementedError(
-                    'imate_method %r on a sparse K needs a sparse direct factorization '
-                    '(not implemented); use "slq"' % self.imate_method)
-            raise ValueError('Existing methods are "eigenvalue", "cholesky", '
-                             '"hutchinson", and "slq".')
+    def _dense(self):
+        """The dense device operator the exact methods run on: K itself, or
+        for a sparse K a dense copy scattered from its CSR on the device (created
+        on first use). imate factorizes a sparse K with CHOLMOD (absent here);
+        the dense fp64 MFMA Cholesky gives the same exact values."""
+        if self.op is None:
+            op = _hip.Operator(self.n, device=self.sop.device,
+                               max_batch=self._max_batch or 1)
+            op.load_sparse(self.sop)
+            self.op = op
+        return self.op
 
     # ---- reference duck type -------------------------------------------------
 
@@ -262,7 +276,7 @@ class MixedCorrelation(object):
             if eta == 0:
                 return tk2
             return tk2 + 2.0 * eta * tk + eta ** 2 * self.n
-        if self.imate_method == 'eigenvalue' and not self.sparse:
+        if self.imate_method == 'eigenvalue':
             # sum over the eigenvalues (imate 'eigenvalue', :127-133)
             return float(numpy.sum((self.eigenvalues() + eta) ** float(exponent)))
         if self.imate_method == 'slq':
@@ -273,8 +287,7 @@ class MixedCorrelation(object):
         if self.interpolate:
             # :167-170: the interpolant of tr((K + eta I)^-1), whatever the exponent
             return self.interpolate_traceinv.interpolate(eta)
-        if self.sparse:
-            self._sparse_method(('slq', 'hutchinson'))
+        if self.sparse and self.imate_method in ('slq', 'hutchinson'):
             if self.imate_method == 'slq' and exponent in (1, 2):
                 return self._slq(eta, 'traceinv' if exponent == 1 else 'traceinv2')
             if self.imate_method == 'hutchinson' and exponent in (1, 2):
@@ -307,14 +320,13 @@ class MixedCorrelation(object):
             return float(numpy.sum((self.eigenvalues() + eta) ** (-float(exponent))))
         if exponent in (1, 2):
             # exact, from the device triangular inverse of the cached factor
-            return self.op.traceinv(eta, exponent)
+            return self._dense().traceinv(eta, exponent)
         # higher powers (not used by the likelihoods): columns of A^-1 solved on the device
-        Ainv = self.op.solve(eta, numpy.eye(self.n))
+        Ainv = self._dense().solve(eta, numpy.eye(self.n))
         return float(numpy.trace(numpy.linalg.matrix_power(Ainv, exponent)))
 
     def logdet(self, eta, exponent=1):                             # :221-274
-        if self.sparse:
-            self._sparse_method(('slq',))
+        if self.sparse and self.imate_method == 'slq':
             return exponent * self._slq(eta, 'logdet')
         if self.imate_method not in ('eigenvalue', 'cholesky', 'hutchinson'):
             if self.imate_method == 'slq':
@@ -323,7 +335,7 @@ class MixedCorrelation(object):
                              ' and "slq".')
         if self.imate_method == 'eigenvalue':
             return exponent * float(self._band_terms([eta])[0][0])
-        return exponent * self.op.logdet(eta)
+        return exponent * self._dense().logdet(eta)
 
     def solve(self, eta, Y):                                       # :280-299
         if self.sparse:
@@ -365,7 +377,7 @@ class MixedCorrelation(object):
         from ONE Cholesky per eta, batched over up to ``max_batch`` etas per
         device call. Returns (logdet[neta], G[neta, m+1, m+1])."""
         etas = numpy.atleast_1d(numpy.asarray(etas, dtype=float))
-        if self.sparse:
+        if self.sparse and self.imate_method == 'slq':
             # SLQ logdet per eta (cached Ritz nodes) and all Gram blocks from one
             # multi-shift CG on K + min(eta) I (tolerance as _linear_solver.py:24)
             R = numpy.column_stack([numpy.asarray(X, dtype=float), numpy.asarray(z, dtype=float)])
@@ -373,6 +385,7 @@ class MixedCorrelation(object):
             return lds, self.sop.msgram(etas, R, rtol=self.cg_rtol)
         if self.imate_method == 'eigenvalue':
             return self._band_terms(etas, X, z)
+        self._dense()
         self.set_rhs(X, z)
         lds, gs = [], []
         mb = self.op.max_batch

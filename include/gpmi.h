@@ -28,6 +28,7 @@ extern "C" {
 #endif
 
 typedef struct gpmi_op gpmi_op;
+typedef struct gpmi_sp gpmi_sp;   /* sparse operator (below) */
 
 #define GPMI_MAX_RHS 16   /* columns of the resident RHS block (m + 1 <= 16) */
 
@@ -64,6 +65,12 @@ int gpmi_op_size(const gpmi_op* op, int64_t* n, int64_t* n_pad);
 
 /* Fill K from a host matrix [n][ldk] (symmetric; the lower triangle is used). */
 int gpmi_op_load_matrix(gpmi_op* op, const double* K_host, int64_t ldk);
+/* Fill K from a sparse operator on the same device (device-side scatter of its
+ * CSR, original point order): the exact ('cholesky' / 'eigenvalue') methods on a
+ * sparse K. Replaces imate's sparse Cholesky (CHOLMOD) call at
+ * mixed_correlation.py:250-261 and the eigh of a sparse K (:76-79, which raises
+ * in the reference) with the dense device paths; needs 8 n_pad^2 bytes per copy. */
+int gpmi_op_load_sparse(gpmi_op* op, const gpmi_sp* sp);
 /* Assemble K on the device from points (no host round trip):
  * generate_correlation(points, scale, nu) fused into the operator. */
 int gpmi_op_assemble_matern(gpmi_op* op, const double* points, int d,
@@ -139,7 +146,6 @@ int gpmi_op_set_outer(gpmi_op* op, int s);
  *     (mixed_correlation.py:138-143,204-209,263-268)
  *   linear_solver for sparse A: scipy.sparse.linalg.cg (_linear_solver.py:57-68).
  */
-typedef struct gpmi_sp gpmi_sp;
 
 /* matern(x_i) for m scaled distances (the device kernel the assembly uses). */
 int gpmi_matern_values(int device, const double* x, int64_t m, double nu, double* out);

@@ -142,8 +142,6 @@ def test_sparse_operator_slq_vs_exact(gp):
     hop = MixedCorrelation(K, imate_method='hutchinson', imate_options={'num_samples': 64})
     exi = numpy.trace(numpy.linalg.inv(Kd + 5.0 * numpy.eye(n)))
     assert abs(hop.traceinv(5.0) - exi) < 0.05 * exi
-    with pytest.raises(NotImplementedError):
-        MixedCorrelation(K, imate_method='cholesky').logdet(5.0)
     # trace / dot use the CSR exactly
     assert rel(op.trace(0.5, 2), numpy.trace((Kd + 0.5 * numpy.eye(n)) @
                                             (Kd + 0.5 * numpy.eye(n)))) < 1e-12
@@ -167,6 +165,54 @@ def test_sparse_likelihood_vs_oracle(gp):
         lp = DirectLikelihood.log_likelihood(z, X, op, False, hp)
         lp_ref = olk.direct_lp(z, X, ref, hp)
         assert abs(lp - lp_ref) < 0.01 * abs(lp_ref) + 1.0
+
+
+def test_sparse_exact_methods_vs_dense(gp):
+    """The exact methods on a sparse K (the reference hands 'cholesky' to imate's
+    CHOLMOD, mixed_correlation.py:250-261; its eigh of a sparse K raises,
+    :76-79): the dense device copy scattered from the Morton-ordered CSR equals
+    K exactly (pad included), and logdet / traceinv / eigenvalues / the
+    likelihood terms match numpy on K.toarray() (<= 1e-11 relative)."""
+    from gaussian_proc._mixed_correlation import MixedCorrelation
+    from gaussian_proc._likelihood._direct_likelihood import DirectLikelihood
+    from oracle.mixed_correlation import MixedCorrelation as OracleMC
+    pts = data.generate_points(24, 2, True)          # n = 576: n_pad = 640
+    D = gp.generate_correlation(pts, 0.08, 1.5, sparse=True, density=0.03,
+                                device_resident=True)
+    K = D.tocsr()
+    n = K.shape[0]
+    Kd = K.toarray()
+    op = MixedCorrelation(D, imate_method='cholesky')
+    assert op.sparse
+    numpy.testing.assert_array_equal(op._dense().get_matrix(), Kd)
+    lam = numpy.linalg.eigvalsh(Kd)
+    eta = abs(lam[0]) + 0.5
+    A = Kd + eta * numpy.eye(n)
+    Ainv = numpy.linalg.inv(A)
+    assert rel(op.logdet(eta), numpy.linalg.slogdet(A)[1]) < 1e-11
+    assert rel(op.traceinv(eta, 1), numpy.trace(Ainv)) < 1e-11
+    assert rel(op.traceinv(eta, 2), numpy.sum(Ainv * Ainv)) < 1e-11
+    z = data.generate_data(pts, 0.2)
+    X = data.generate_basis_functions(pts, 2)
+    R = numpy.column_stack([X, z])
+    ld, G = op.loglik_terms([eta, eta + 1.0], X, z)
+    assert _nrel(G[0], R.T @ numpy.linalg.solve(A, R)) < 1e-11
+    assert rel(ld[1], numpy.linalg.slogdet(A + numpy.eye(n))[1]) < 1e-11
+    ref = OracleMC(Kd, 'cholesky')
+    hp = [1.0, numpy.sqrt(eta)]
+    assert rel(DirectLikelihood.log_likelihood(z, X, op, False, hp),
+               olk.direct_lp(z, X, ref, hp)) < 1e-10
+    # 'hutchinson' logdet is Cholesky (reference :250-261)
+    assert rel(MixedCorrelation(D, imate_method='hutchinson').logdet(eta),
+               numpy.linalg.slogdet(A)[1]) < 1e-11
+    eop = MixedCorrelation(D, imate_method='eigenvalue')
+    assert numpy.max(numpy.abs(eop.eigenvalues() - lam)) < 1e-12 * numpy.max(numpy.abs(lam))
+    assert rel(eop.traceinv(eta, 1), numpy.trace(Ainv)) < 1e-11
+    assert rel(eop.logdet(eta), numpy.linalg.slogdet(A)[1]) < 1e-11
+    with pytest.raises(numpy.linalg.LinAlgError):
+        op.logdet(0.5 * abs(lam[0]))
+    with pytest.raises(ValueError):
+        MixedCorrelation(D, imate_method='exact').logdet(eta)
 
 
 @pytest.mark.parametrize('dim,npts,rho,dens', [(1, 3000, 0.01, 1e-2), (2, 2500, 0.02, 5e-3),
@@ -251,6 +297,26 @@ def test_config4_full_size_vs_reference(gp):
     for e, ld_se, lp_ref in zip(etas, se, meta['direct_lp']):
         lp = DirectLikelihood.log_likelihood(z, X, op, False, [1.0, numpy.sqrt(e)])
         assert abs(lp - lp_ref) <= 0.5 * 3.0 * ld_se + 1e-6 * abs(lp_ref), (e, lp, lp_ref)
+
+
+def test_config4_exact_cholesky_vs_splu(gp):
+    """cfg4 (N=65536) under imate_method='cholesky': the dense device copy of the
+    sparse K (34 GB) and its fp64 MFMA Cholesky against the fixture's SuperLU
+    logdet and exact Gram blocks (<= 1e-10) and the reference-formula lp."""
+    from gaussian_proc._mixed_correlation import MixedCorrelation
+    from gaussian_proc._likelihood._direct_likelihood import DirectLikelihood
+    meta, pts, D = _cfg_sparse(gp, 'sparse_cfg4.json', 256, 2, 0.005, 1e-3)
+    op = MixedCorrelation(D, imate_method='cholesky')
+    z = data.generate_data(pts, 0.2)
+    X = data.generate_basis_functions(pts, 2)
+    etas = meta['etas']
+    ld, G = op.loglik_terms(etas, X, z)
+    for j in range(len(etas)):
+        assert rel(ld[j], meta['logdet'][j]) < 1e-10, etas[j]
+        assert _nrel(G[j], numpy.asarray(meta['gram'][j])) < 1e-10, etas[j]
+    e = etas[0]
+    lp = DirectLikelihood.log_likelihood(z, X, op, False, [1.0, numpy.sqrt(e)])
+    assert rel(lp, meta['direct_lp'][0]) < 1e-10
 
 
 def test_config4_eta_below_lambda_min_raises(gp):
