@@ -60,6 +60,11 @@ __global__ void band_chol_kernel(const double* B, int64_t lda, int nt, int64_t n
 __global__ void band_der_kernel(const double* fac, int nt, double* ysol, double* der);
 
 __global__ void chase_copy_kernel(const double* Ab, double* A, int64_t lda, int n);
+constexpr int CHASE_MSG = 136;   // = CMSG (gpmi_chase.hip): values per hand-off slot
+constexpr int CHASE_THREADS = 512;   // = SCT (gpmi_chase.hip): systolic chase workgroup
+__global__ void chase_systolic_kernel(const double* Ab, int64_t lda, int n,
+                                      unsigned long long* msg_r, unsigned long long* msg_c,
+                                      int* err, unsigned spin_limit, double* dout, double* e2out);
 __global__ void chase_task_kernel(double* A, int64_t lda, int n, int t, int s_hi);
 __global__ void chase_reflect_kernel(double* A, int64_t lda, int n, int s, double* sl);
 __global__ void chase_apply_kernel(double* A, int64_t lda, int n, int t, int s_hi,

@@ -295,16 +295,6 @@ __global__ __launch_bounds__(HH_THREADS) void hh_col_kernel(double* __restrict__
 // redoes the reduction with the per-column launches (hh_col_kernel).
 // counter[0..127] must be zero at launch (the host memsets it per panel).
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void st_sc1(double* p, double v) {
-  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p),
-                     (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ double ld_sc1(const double* p) {
-  return __longlong_as_double((long long)__hip_atomic_load(
-      reinterpret_cast<const unsigned long long*>(p), __ATOMIC_RELAXED,
-      __HIP_MEMORY_SCOPE_AGENT));
-}
 
 __global__ __launch_bounds__(HH_THREADS) void hh_panel_kernel(double* __restrict__ P,
                                                               int64_t lda, int m,

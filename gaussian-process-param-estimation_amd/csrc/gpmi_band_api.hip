@@ -9,6 +9,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #include "gpmi_internal.h"
@@ -119,6 +120,14 @@ struct gpmi_band {
   double* Ac = nullptr;      // [n_pad][n_pad] chase copy of the band (lower)
   double* td = nullptr;      // [n] diagonal, then [n] squared subdiagonal, then [n] eigenvalues
   double eig_ms = 0.0;
+  // systolic chase (chase_systolic_kernel): one workgroup per position, all
+  // co-resident; used when chase_maxg (CU count x resident workgroups per CU)
+  // covers the positions, else (and after a timed-out hand-off) the launch form
+  unsigned long long* cmsg = nullptr;  // reflector, column slots [2][K + 1][2][2 CHASE_MSG], err
+  int chase_maxg = 0;
+  unsigned chase_spin = 1u << 24;
+  int chase_systolic = 0;    // the last eigenvalues() took the systolic form
+  int chase_fallbacks = 0;   // systolic attempts that timed out and reran the launch form
 };
 
 namespace {
@@ -132,6 +141,7 @@ int band_free(gpmi_band* b) {
   if (b->info) (void)hipFree(b->info);
   if (b->ctr) (void)hipFree(b->ctr);
   if (b->err) (void)hipFree(b->err);
+  if (b->cmsg) (void)hipFree(b->cmsg);
   if (b->ev0) (void)hipEventDestroy(b->ev0);
   if (b->ev1) (void)hipEventDestroy(b->ev1);
   if (b->stream) (void)hipStreamDestroy(b->stream);
@@ -145,6 +155,28 @@ int band_free(gpmi_band* b) {
   if (b->ev_t) (void)hipEventDestroy(b->ev_t);
   delete b;
   return 0;
+}
+
+// The systolic chase (one launch): d, e2 of the tridiagonal. Returns 0 when done,
+// 1 when the positions cannot all be co-resident, 2 after a timed-out hand-off.
+int chase_systolic_run(gpmi_band* b, hipStream_t s, double* d, double* e2) {
+  const int n = (int)b->n;
+  const int K = (n - 1 + TS - 1) / TS;
+  if (K > b->chase_maxg) return 1;
+  // per message slot: CHASE_MSG values as two tagged 8-byte granules each
+  const size_t slots = (size_t)(K + 1) * 2 * 2 * CHASE_MSG;
+  if (!b->cmsg) {
+    BD_TRY(hipMalloc(&b->cmsg, sizeof(unsigned long long) * 2 * slots + 64));
+  }
+  int* err = reinterpret_cast<int*>(b->cmsg + 2 * slots);
+  BD_TRY(hipMemsetAsync(b->cmsg, 0, sizeof(unsigned long long) * 2 * slots + 64, s));
+  hipLaunchKernelGGL(chase_systolic_kernel, dim3(K), dim3(CHASE_THREADS), 0, s, b->Ab,
+                     (int64_t)b->n_pad, n, b->cmsg, b->cmsg + slots, err, b->chase_spin, d, e2);
+  BD_LAUNCH("chase_systolic_kernel");
+  int herr = 0;
+  BD_TRY(hipMemcpyAsync(&herr, err, sizeof(int), hipMemcpyDeviceToHost, s));
+  BD_TRY(hipStreamSynchronize(s));
+  return herr ? 2 : 0;
 }
 
 // Y <- Q_j^T Y for panel j (Y = b->Y, rows from 128 (j + 1)) on stream st.
@@ -437,6 +469,17 @@ int gpmi_band_create(gpmi_op* op, gpmi_band** out) {
       return fail(e, "hh_panel occupancy");
     b->panel_maxg = std::min(HH_PANEL_MAXG, std::max(0, per_cu) * b->ncu);
   }
+  {
+    int per_cu = 0;
+    if ((e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+             &per_cu, reinterpret_cast<const void*>(&chase_systolic_kernel), CHASE_THREADS, 0)) !=
+        hipSuccess)
+      return fail(e, "chase occupancy");
+    b->chase_maxg = std::max(0, per_cu) * b->ncu;
+  }
+  // test hook: GPMI_CHASE_SPIN_LIMIT=0 times the systolic chase out at its first wait
+  if (const char* sl = std::getenv("GPMI_CHASE_SPIN_LIMIT"))
+    b->chase_spin = (unsigned)std::strtoul(sl, nullptr, 10);
   // test hook: GPMI_HH_SPIN_LIMIT=0 makes the first unsuccessful poll a timeout
   if (const char* sl = std::getenv("GPMI_HH_SPIN_LIMIT"))
     b->spin_limit = (unsigned)std::strtoul(sl, nullptr, 10);
@@ -613,21 +656,34 @@ int gpmi_band_eigenvalues(gpmi_band* b, double* lam) {
   hipStream_t s = b->stream;
   const int64_t np = b->n_pad;
   const int n = (int)b->n;
-  if (!b->Ac) {
-    BD_TRY(hipMalloc(&b->Ac, sizeof(double) * np * np));
-    // td: [n] diagonal, [n] squared subdiagonal, [n] eigenvalues, then the chase's
-    // reflector slots (two wavefront parities x ((n - 2) / 128 + 3) slots of 130)
+  if (!b->td) {
+    // td: [n] diagonal, [n] squared subdiagonal, [n] eigenvalues, then the launch
+    // form's reflector slots (two wavefront parities x ((n - 2) / 128 + 3) slots of 130)
     BD_TRY(hipMalloc(&b->td, sizeof(double) * (3 * np + 2 * ((np - 2) / TS + 3) * (TS + 2))));
   }
+  double* d = b->td;
+  double* e2 = b->td + np;
+  double* dl = b->td + 2 * np;
   BD_TRY(hipEventRecord(b->ev0, s));
+  // GPMI_CHASE_MODE: systolic (default; one launch), split (reflector + per-block
+  // launches per wavefront t = 3 s + k), task (one workgroup per task per wavefront)
+  const char* mode_env = std::getenv("GPMI_CHASE_MODE");
+  const int chase_mode = !mode_env ? 0 : std::strcmp(mode_env, "split") == 0 ? 1
+                                     : std::strcmp(mode_env, "task") == 0    ? 2 : 0;
+  bool done = false;
+  b->chase_systolic = 0;
+  if (chase_mode == 0 && n > 2) {
+    const int rc = chase_systolic_run(b, s, d, e2);
+    if (rc < 0) return rc;
+    if (rc == 2) ++b->chase_fallbacks;
+    done = rc == 0;
+    b->chase_systolic = done;
+  }
+  if (!done) {
+  if (!b->Ac) BD_TRY(hipMalloc(&b->Ac, sizeof(double) * np * np));
   hipLaunchKernelGGL(chase_copy_kernel, dim3(n), dim3(256), 0, s, b->Ab, b->Ac, np, n);
   BD_LAUNCH("chase_copy_kernel");
-  // wavefront t = 3 s + k: tasks s in [s_lo, s_hi]. GPMI_CHASE_SPLIT=0: one
-  // workgroup per task (chase_task_kernel) instead of reflector + per-block launches
-  static const bool chase_split = [] {
-    const char* v = std::getenv("GPMI_CHASE_SPLIT");
-    return !(v && std::atoi(v) == 0);
-  }();
+  const bool chase_split = chase_mode != 2;
   const int kmax = (n - 2) / TS + 1;
   const int tmax = 3 * std::max(0, n - 3) + kmax;
   for (int t = 0; t <= tmax && n > 2; ++t) {
@@ -657,12 +713,10 @@ int gpmi_band_eigenvalues(gpmi_band* b, double* lam) {
       BD_LAUNCH("chase_task_kernel");
     }
   }
-  double* d = b->td;
-  double* e2 = b->td + np;
-  double* dl = b->td + 2 * np;
   hipLaunchKernelGGL(tridiag_extract_kernel, dim3((n + 255) / 256), dim3(256), 0, s, b->Ac, np, n,
                      d, e2);
   BD_LAUNCH("tridiag_extract_kernel");
+  }
   std::vector<double> hd(n), he2(n);
   BD_TRY(hipMemcpyAsync(hd.data(), d, sizeof(double) * n, hipMemcpyDeviceToHost, s));
   BD_TRY(hipMemcpyAsync(he2.data(), e2, sizeof(double) * n, hipMemcpyDeviceToHost, s));
@@ -714,6 +768,14 @@ int gpmi_band_last_timing(gpmi_band* b, double* reduce_ms, double* rhs_ms, doubl
   if (reduce_ms) *reduce_ms = b->reduce_ms;
   if (rhs_ms) *rhs_ms = b->rhs_ms;
   if (loglik_ms) *loglik_ms = b->loglik_ms;
+  return 0;
+}
+
+int gpmi_band_chase_info(gpmi_band* b, int* systolic, int* fallbacks, int* maxg) {
+  if (!b) return set_error(-1006, "null handle");
+  if (systolic) *systolic = b->chase_systolic;
+  if (fallbacks) *fallbacks = b->chase_fallbacks;
+  if (maxg) *maxg = b->chase_maxg;
   return 0;
 }
 

@@ -475,6 +475,346 @@ __global__ __launch_bounds__(CT) void chase_apply_kernel(double* __restrict__ A,
   }
 }
 
+// ---------------------------------------------------------------------------
+// Systolic form (default): ONE launch, one workgroup per chase position k (the
+// row block J_k(s) = [s + 1 + k b, s + 1 + (k + 1) b) of every sweep s), all
+// co-resident. Workgroup k keeps its two blocks in registers for the whole chase:
+//   D = A[J_k, J_k] (full, exactly symmetric) and E = A[J_{k+1}, J_k],
+// so the matrix never goes back to HBM. Per sweep s it
+//   1. receives the reflector of task (s, k) from workgroup k - 1 (k = 0 forms it
+//      from column s, which it holds);
+//   2. applies it: D <- H D H, E <- E H (row sums in one pass over both blocks);
+//   3. forms the reflector of task (s, k + 1) from E's first column and posts it
+//      to workgroup k + 1, then applies that reflector from the left to E (the
+//      bulge block F of task (s, k + 1) is this E, so its owner updates it);
+//   4. posts D's first column and E[0][0] to workgroup k - 1: exactly the row and
+//      column that workgroup appends when its window slides by one (workgroup 0
+//      keeps them: the finished diagonal d[s + 1] and the column of sweep s + 1);
+//   5. slides its own window: drops logical row/column 0, appends the message of
+//      workgroup k + 1. Indices are circular (physical = (logical + s) mod b), so
+//      sliding moves no data.
+// Tasks (s, k) run at about (2 s + k) hand-off steps instead of the 3 s + k
+// wavefront launches of chase_apply_kernel. Same Householder arithmetic (LAPACK
+// dlarfg, H D H in the symmetric rank-2 form); sums are taken in another order, so
+// the tridiagonal agrees with the launch form to rounding, not bit for bit.
+// Hand-offs (the guide's handoff-1to1 row: data-tagged granules, no flag): every
+// double goes as two naturally aligned 8-byte granules {32 data bits, 32-bit tag
+// = sweep + 1}, each written by ONE sc1 store; a consumer thread polls its value's
+// two granules with sc1 loads until both carry the tag (bounded; a timeout sets
+// *err, every workgroup leaves and the host reruns the launch form), then the
+// workgroup barrier. Slots are double-buffered by sweep parity: a producer
+// reusing slot s & 1 at sweep s + 2 has received data its consumer sent after
+// reading sweep s's slot, and the tag tells a fresh slot from a stale one.
+// ---------------------------------------------------------------------------
+constexpr int CMSG = 136;   // message stride in values: 128 + 1 scalar (padded)
+
+__device__ __forceinline__ void put_granules(unsigned long long* p, double v, unsigned tag) {
+  const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+  const unsigned long long t = (unsigned long long)tag << 32;
+  __hip_atomic_store(p, t | (b & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(p + 1, t | (b >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ bool get_granules(const unsigned long long* p, unsigned tag, int* err,
+                                             unsigned spin_limit, double& v) {
+  unsigned spins = 0;
+  for (;;) {
+    const unsigned long long a =
+        __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long b =
+        __hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((unsigned)(a >> 32) == tag && (unsigned)(b >> 32) == tag) {
+      v = __longlong_as_double((long long)(((b & 0xffffffffull) << 32) | (a & 0xffffffffull)));
+      return true;
+    }
+    __builtin_amdgcn_s_sleep(1);
+    if (++spins > spin_limit ||
+        ((spins & 1023u) == 0 &&
+         __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)) {
+      __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+  }
+}
+
+// LAPACK dlarfg on x (x0 first, nb2 = sum of the other squares)
+__device__ __forceinline__ void chase_dlarfg(double x0, double nb2, double& tau, double& beta,
+                                             double& scale) {
+  tau = 0.0;
+  beta = x0;
+  scale = 0.0;
+  if (nb2 > 0.0) {
+    const double nrm = sqrt(x0 * x0 + nb2);
+    beta = x0 >= 0.0 ? -nrm : nrm;
+    tau = (beta - x0) / beta;
+    scale = 1.0 / (x0 - beta);
+  }
+}
+
+// w_i = p_i - (tau / 2)(v.p) v_i, every operation rounded on its own: the row and
+// the column side of D's update see bitwise the same w_i (D stays symmetric)
+__device__ __forceinline__ double chase_w(double tau, double sp, double hvp, double v) {
+#pragma clang fp contract(off)
+  return tau * sp - hvp * v;
+}
+
+constexpr int SCT = CHASE_THREADS;        // systolic chase workgroup (gpmi_band.h)
+constexpr int SNW = SCT / 64;             // waves
+constexpr int SRW = CB / SNW;             // rows per thread
+
+static_assert(SRW % 8 == 0, "row sums go through 8-row butterflies");
+
+// fixed-order sum of one value per wave
+__device__ __forceinline__ double wave_sum_n(const double* r) {
+  double a = 0.0;
+#pragma unroll
+  for (int q = 0; q < SNW; ++q) a += r[q];
+  return a;
+}
+
+__device__ __forceinline__ double block_sum_n(double v, double* red) {
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  __syncthreads();
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  return wave_sum_n(red);
+}
+
+__global__ __launch_bounds__(SCT) void chase_systolic_kernel(
+    const double* __restrict__ Ab, int64_t lda, int n, unsigned long long* __restrict__ msg_r,
+    unsigned long long* __restrict__ msg_c, int* __restrict__ err, unsigned spin_limit,
+    double* __restrict__ dout, double* __restrict__ e2out) {
+  __shared__ double sv[CB], sv2[CB], sp[CB], sq[CB], sx[CB], scol[CB], serow[CB], snew[CB];
+  __shared__ double xk0[CB];
+  __shared__ double cpart[SNW][CB];
+  __shared__ double red[SNW], redp[SNW], rednb[SNW];
+  __shared__ double sscal[4];
+  __shared__ int s_bail;
+  constexpr int M = CB - 1;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int c0 = 2 * lane;
+  const int k = blockIdx.x;
+  const int rb = 1 + k * CB;                      // first row of J_k(0)
+  const int s_end = min(n - 3, n - 2 - k * CB);   // last sweep this position works in
+  // thread: physical rows SNW u + w (u < SRW), physical columns c0, c0 + 1
+  d2 D[SRW], E[SRW];
+#pragma unroll
+  for (int u = 0; u < SRW; ++u) {
+    const int i = SNW * u + w;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int r = rb + i, c = rb + c0 + j;
+      D[u][j] = (r < n && c < n) ? Ab[(int64_t)max(r, c) * lda + min(r, c)] : 0.0;
+      const int re = r + CB;   // E = A[J_{k+1}, J_k]: band part only (re - c <= b)
+      E[u][j] = (re < n && c < n && re - c <= CB) ? Ab[(int64_t)re * lda + c] : 0.0;
+    }
+  }
+  if (k == 0) {
+    if (tid < CB) xk0[tid] = (1 + tid < n) ? Ab[(int64_t)(1 + tid) * lda] : 0.0;
+    if (tid == 0) dout[0] = Ab[0];
+  }
+  if (tid == 0) s_bail = 0;
+  __syncthreads();
+  for (int s = 0; s <= s_end; ++s) {
+    const int off = s & M;
+    const int uo = off / SNW, wo = off % SNW, lo = off >> 1, jo = off & 1;
+    const bool nxt = s + 1 + (k + 1) * CB < n;   // position k + 1 works in sweep s
+    // ---- 1. reflector of task (s, k) into sv (physical order)
+    double tau = 0.0;
+    if (k == 0) {
+      const double xi = (tid < CB) ? xk0[tid] : 0.0;
+      const double x0 = xk0[0];
+      const double nb2 = block_sum_n((tid > 0 && tid < CB) ? xi * xi : 0.0, red);
+      double beta, scale;
+      chase_dlarfg(x0, nb2, tau, beta, scale);
+      if (tid < CB) sv[(tid + off) & M] = (tid == 0) ? 1.0 : xi * scale;
+      if (tid == 0) e2out[s] = beta * beta;
+    } else {
+      if (tid <= CB) {
+        const unsigned long long* m = msg_r + ((int64_t)k * 2 + (s & 1)) * (2 * CMSG);
+        double v = 0.0;
+        if (!get_granules(m + 2 * tid, (unsigned)(s + 1), err, spin_limit, v)) s_bail = 1;
+        if (tid < CB) sv[(tid + off) & M] = v;
+        else sscal[0] = v;
+      }
+    }
+    __syncthreads();
+    if (s_bail) return;
+    if (k != 0) tau = sscal[0];
+    // ---- 2. D <- H D H, E <- E H: the row sums D v, E v in one pass, v.(D v) per
+    //      wave, one barrier
+    if (tau != 0.0) {
+      const double vc0 = sv[c0], vc1 = sv[c0 + 1];
+      constexpr int NH = SRW / 8;   // 8-row halves per thread
+      double prow[NH], qrow[NH];
+#pragma unroll
+      for (int h = 0; h < NH; ++h) {
+        double rowv[8];
+#pragma unroll
+        for (int uu = 0; uu < 8; ++uu)
+          rowv[uu] = D[8 * h + uu][0] * vc0 + D[8 * h + uu][1] * vc1;
+        prow[h] = butterfly8(rowv);
+#pragma unroll
+        for (int uu = 0; uu < 8; ++uu)
+          rowv[uu] = E[8 * h + uu][0] * vc0 + E[8 * h + uu][1] * vc1;
+        qrow[h] = butterfly8(rowv);
+      }
+      double vpw = 0.0;
+#pragma unroll
+      for (int h = 0; h < NH; ++h) {
+        // the row this lane's sums of half h belong to
+        const int rr = SNW * (8 * h + ((lane >> 3) & 7)) + w;
+        if ((lane & 7) == 0) {
+          vpw += prow[h] * sv[rr];
+          sp[rr] = prow[h];
+          sq[rr] = qrow[h];
+        }
+      }
+      vpw += __shfl_xor(vpw, 8);
+      vpw += __shfl_xor(vpw, 16);
+      vpw += __shfl_xor(vpw, 32);
+      if (lane == 0) redp[w] = vpw;
+      __syncthreads();
+      const double vp = tau * wave_sum_n(redp);
+      const double hvp = 0.5 * tau * vp;
+      const double wc0 = chase_w(tau, sp[c0], hvp, vc0), wc1 = chase_w(tau, sp[c0 + 1], hvp, vc1);
+#pragma unroll
+      for (int u = 0; u < SRW; ++u) {
+        const int r = SNW * u + w;
+        const double vr = sv[r], wr = chase_w(tau, sp[r], hvp, vr), qr = tau * sq[r];
+        {
+          // both products rounded, then summed (commutative): D stays exactly symmetric
+#pragma clang fp contract(off)
+          D[u][0] = D[u][0] - (vr * wc0 + wr * vc0);
+          D[u][1] = D[u][1] - (vr * wc1 + wr * vc1);
+        }
+        E[u][0] = E[u][0] - qr * vc0;
+        E[u][1] = E[u][1] - qr * vc1;
+      }
+    }
+    // ---- 3. E's first column and D's first column (lane lo of every wave holds
+    //      them) into LDS; the reflector of task (s, k + 1); post it, and D's first
+    //      column + E[0][0] for position k - 1
+    if (lane == lo) {
+      double part = 0.0;
+#pragma unroll
+      for (int u = 0; u < SRW; ++u) {
+        const int r = SNW * u + w;
+        const double x = jo ? E[u][1] : E[u][0];
+        sx[r] = x;
+        scol[r] = jo ? D[u][1] : D[u][0];
+        if (r != off) part += x * x;
+      }
+      rednb[w] = part;
+    }
+    __syncthreads();
+    double taun = 0.0, betan = 0.0, scn = 0.0;
+    if (nxt) {
+      chase_dlarfg(sx[off], wave_sum_n(rednb), taun, betan, scn);
+      if (tid < CB) sv2[tid] = (tid == off) ? 1.0 : sx[tid] * scn;
+      unsigned long long* m = msg_r + ((int64_t)(k + 1) * 2 + (s & 1)) * (2 * CMSG);
+      if (tid < CB) put_granules(m + 2 * tid, (tid == 0) ? 1.0 : sx[(tid + off) & M] * scn,
+                                 (unsigned)(s + 1));
+      else if (tid == CB) put_granules(m + 2 * CB, taun, (unsigned)(s + 1));
+    }
+    const double e00 = nxt ? betan : 0.0;   // E[0][0] after the left update of step 4
+    if (k >= 1) {
+      const int t2 = tid - 256;
+      unsigned long long* m = msg_c + ((int64_t)k * 2 + (s & 1)) * (2 * CMSG);
+      if (t2 >= 0 && t2 < CB) put_granules(m + 2 * t2, scol[(t2 + off) & M], (unsigned)(s + 1));
+      else if (t2 == CB) put_granules(m + 2 * CB, e00, (unsigned)(s + 1));
+    } else {
+      // position 0 keeps them: the finished diagonal and the column of sweep s + 1
+      if (tid < CB) {
+        if (tid == off) dout[s + 1] = scol[tid];
+        else xk0[(tid - off - 1) & M] = scol[tid];
+      } else if (tid == CB) {
+        xk0[M] = e00;
+      }
+      if (s == n - 3) {   // last sweep: the trailing 2 x 2 block is final
+        const int o1 = (off + 1) & M;
+        if (tid == 0) {
+          e2out[n - 2] = scol[o1] * scol[o1];
+          e2out[n - 1] = 0.0;
+        }
+        if (w == (o1 % SNW) && lane == (o1 >> 1)) {
+#pragma unroll
+          for (int u = 0; u < SRW; ++u)
+            if (u == o1 / SNW) dout[n - 1] = (o1 & 1) ? D[u][1] : D[u][0];
+        }
+      }
+    }
+    __syncthreads();   // sv2 for step 4
+    // ---- 4. E <- H' E (the bulge block of task (s, k + 1)); column off -> (beta', 0...)
+    if (nxt && taun != 0.0) {
+      double cp0 = 0.0, cp1 = 0.0;
+#pragma unroll
+      for (int u = 0; u < SRW; ++u) {
+        const int r = SNW * u + w;
+        const double vr = sv2[r];
+        cp0 += E[u][0] * vr;
+        cp1 += E[u][1] * vr;
+      }
+      cpart[w][c0] = cp0;
+      cpart[w][c0 + 1] = cp1;
+      __syncthreads();
+      double r0s = 0.0, r1s = 0.0;
+#pragma unroll
+      for (int q = 0; q < SNW; ++q) {
+        r0s += cpart[q][c0];
+        r1s += cpart[q][c0 + 1];
+      }
+      r0s *= taun;
+      r1s *= taun;
+#pragma unroll
+      for (int u = 0; u < SRW; ++u) {
+        const int r = SNW * u + w;
+        const double vr = sv2[r];
+        E[u][0] = (c0 == off) ? (r == off ? betan : 0.0) : E[u][0] - vr * r0s;
+        E[u][1] = (c0 + 1 == off) ? (r == off ? betan : 0.0) : E[u][1] - vr * r1s;
+      }
+    }
+    // ---- 5. slide the window: physical row / column off becomes logical b - 1
+    if (w == wo) {
+#pragma unroll
+      for (int u = 0; u < SRW; ++u)
+        if (u == uo) {
+          serow[c0] = E[u][0];
+          serow[c0 + 1] = E[u][1];
+        }
+    }
+    if (tid <= CB) {
+      double v = 0.0;
+      if (nxt) {
+        const unsigned long long* m = msg_c + ((int64_t)(k + 1) * 2 + (s & 1)) * (2 * CMSG);
+        if (!get_granules(m + 2 * tid, (unsigned)(s + 1), err, spin_limit, v)) s_bail = 1;
+      }
+      if (tid < CB) snew[tid] = v;
+      else sscal[3] = v;
+    }
+    __syncthreads();
+    if (s_bail) return;
+    const double d00 = snew[0], ne00 = sscal[3];
+#pragma unroll
+    for (int u = 0; u < SRW; ++u) {
+      const int r = SNW * u + w;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int c = c0 + j;
+        if (r == off) {
+          D[u][j] = (c == off) ? d00 : serow[c];
+          E[u][j] = (c == off) ? ne00 : 0.0;
+        } else if (c == off) {
+          D[u][j] = serow[r];
+          E[u][j] = snew[((r - off - 1) & M) + 1];
+        }
+      }
+    }
+  }
+}
+
 // Copy of the band for the chase: B's lower band (0 <= i - j <= 128) of the
 // reduced matrix, zero for 128 < i - j <= 2 * 128 + 1 (the bulge envelope; the
 // reduced matrix keeps Householder vectors there). Row i per workgroup.

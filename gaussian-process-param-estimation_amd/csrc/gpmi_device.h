@@ -26,6 +26,19 @@ __device__ __forceinline__ int slab_off(int row, int k) {
 }
 constexpr int RLD = GPMI_RHS_LD; // 16
 
+// Hand-off words between co-resident workgroups: agent-scope relaxed atomic
+// stores / loads (write-through to L2, loads that bypass the non-coherent caches).
+__device__ __forceinline__ void st_sc1(double* p, double v) {
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p),
+                     (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_sc1(const double* p) {
+  return __longlong_as_double((long long)__hip_atomic_load(
+      reinterpret_cast<const unsigned long long*>(p), __ATOMIC_RELAXED,
+      __HIP_MEMORY_SCOPE_AGENT));
+}
+
 __device__ __forceinline__ d4 mfma64(double a, double b, d4 c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }

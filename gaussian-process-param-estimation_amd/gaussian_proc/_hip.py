@@ -90,6 +90,7 @@ SIGNATURES = {
                                            c_double_p, c_double_p, c_double_p, c_int_p]),
     'gpmi_band_der_ms': (ctypes.c_int, [c_op_p, c_double_p]),
     'gpmi_band_stats': (ctypes.c_int, [c_op_p, c_int_p, c_int_p]),
+    'gpmi_band_chase_info': (ctypes.c_int, [c_op_p, c_int_p, c_int_p, c_int_p]),
     'gpmi_sp_last_status': (ctypes.c_int, [c_op_p, c_int_p]),
     'gpmi_band_last_timing': (ctypes.c_int, [c_op_p, c_double_p, c_double_p, c_double_p]),
 }
@@ -401,6 +402,14 @@ class Band(object):
         check(self.lib.gpmi_band_stats(self.h, ctypes.byref(fb), ctypes.byref(mg)),
               'gpmi_band_stats')
         return dict(panel_fallbacks=fb.value, panel_maxg=mg.value)
+
+    def chase_info(self):
+        """-> dict(systolic, fallbacks, maxg) of the last eigenvalues() (see
+        gpmi_band_chase_info)."""
+        sy, fb, mg = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        check(self.lib.gpmi_band_chase_info(self.h, ctypes.byref(sy), ctypes.byref(fb),
+                                            ctypes.byref(mg)), 'gpmi_band_chase_info')
+        return dict(systolic=bool(sy.value), fallbacks=fb.value, maxg=mg.value)
 
     def der_ms(self):
         v = ctypes.c_double()

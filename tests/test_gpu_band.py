@@ -151,6 +151,39 @@ def test_eigenvalues_vs_numpy(gp, n):
     assert numpy.max(numpy.abs(lam - ref)) <= 1e-12 * numpy.abs(ref).max()
 
 
+@pytest.mark.parametrize('n', [3, 130, 1000, 2177])
+def test_systolic_chase_matches_launch_form(gp, n, monkeypatch):
+    """The one-launch systolic chase (default) and the per-wavefront launch form
+    give the same tridiagonal up to rounding (sums in another order): the
+    spectra agree to 1e-13 ||K|| and both match numpy to 1e-12 ||K||."""
+    K, _, _ = _inputs(n, n + 3)
+    op = _mc(K)
+    lam = op.eigenvalues()
+    info = op.band().chase_info()
+    assert info['systolic'] and info['fallbacks'] == 0, info
+    monkeypatch.setenv('GPMI_CHASE_MODE', 'split')
+    lam_s = _mc(K).band().eigenvalues()
+    ref = numpy.linalg.eigvalsh(K)
+    scale = numpy.abs(ref).max()
+    assert numpy.max(numpy.abs(lam - lam_s)) <= 1e-13 * scale
+    assert numpy.max(numpy.abs(lam - ref)) <= 1e-12 * scale
+
+
+def test_systolic_chase_timeout_falls_back(gp, monkeypatch):
+    """GPMI_CHASE_SPIN_LIMIT=0 makes the first hand-off wait of the systolic
+    chase a timeout (as when its workgroups cannot all be resident): every
+    workgroup leaves, the launch form reruns the chase, the spectrum is right
+    and the fallback is counted."""
+    K, _, _ = _inputs(1000, 5)
+    monkeypatch.setenv('GPMI_CHASE_SPIN_LIMIT', '0')
+    op = _mc(K)
+    lam = op.eigenvalues()
+    info = op.band().chase_info()
+    assert not info['systolic'] and info['fallbacks'] == 1, info
+    ref = numpy.linalg.eigvalsh(K)
+    assert numpy.max(numpy.abs(lam - ref)) <= 1e-12 * numpy.abs(ref).max()
+
+
 def test_eigenvalue_operator_traces(gp):
     """'eigenvalue' traceinv (exponent 1, 2, 3) and trace (exponent 3) as sums over
     the device eigenvalues vs explicit matrix functions (rel <= 1e-9)."""
