@@ -166,16 +166,30 @@ int chase_systolic_run(gpmi_band* b, hipStream_t s, double* d, double* e2) {
   // per message slot: CHASE_MSG values as two tagged 8-byte granules each
   const size_t slots = (size_t)(K + 1) * 2 * 2 * CHASE_MSG;
   if (!b->cmsg) {
-    BD_TRY(hipMalloc(&b->cmsg, sizeof(unsigned long long) * 2 * slots + 64));
+    BD_TRY(hipMalloc(&b->cmsg, sizeof(unsigned long long) * 2 * slots + 64 + 8192));
   }
   int* err = reinterpret_cast<int*>(b->cmsg + 2 * slots);
-  BD_TRY(hipMemsetAsync(b->cmsg, 0, sizeof(unsigned long long) * 2 * slots + 64, s));
+  BD_TRY(hipMemsetAsync(b->cmsg, 0, sizeof(unsigned long long) * 2 * slots + 64 + 8192, s));
   hipLaunchKernelGGL(chase_systolic_kernel, dim3(K), dim3(CHASE_THREADS), 0, s, b->Ab,
                      (int64_t)b->n_pad, n, b->cmsg, b->cmsg + slots, err, b->chase_spin, d, e2);
   BD_LAUNCH("chase_systolic_kernel");
   int herr = 0;
   BD_TRY(hipMemcpyAsync(&herr, err, sizeof(int), hipMemcpyDeviceToHost, s));
   BD_TRY(hipStreamSynchronize(s));
+#ifdef GPMI_CHASE_PROF
+  {
+    std::vector<long long> st(4 * 16 * 8);
+    BD_TRY(hipMemcpy(st.data(), err + 16, sizeof(long long) * st.size(), hipMemcpyDeviceToHost));
+    for (int q = 0; q < 4; ++q)
+      for (int i = 0; i < 16; ++i) {
+        const long long* t = st.data() + (q * 16 + i) * 8;
+        const long long* tn = (i + 1 < 16) ? t + 8 : nullptr;
+        fprintf(stderr, "[chase prof] k=%d s=%d dt(10ns): recvR %lld prod %lld post %lld upd %lld "
+                "F %lld recvC %lld shift %lld\n", q + 1, 1000 + i, t[1] - t[0], t[2] - t[1],
+                t[3] - t[2], t[4] - t[3], t[5] - t[4], t[6] - t[5], tn ? tn[0] - t[6] : 0LL);
+      }
+  }
+#endif
   return herr ? 2 : 0;
 }
 

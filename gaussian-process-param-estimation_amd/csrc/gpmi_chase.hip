@@ -558,6 +558,12 @@ __device__ __forceinline__ double chase_w(double tau, double sp, double hvp, dou
   return tau * sp - hvp * v;
 }
 
+// d - (a b + c e), every operation rounded on its own
+__device__ __forceinline__ double chase_dsub(double d, double a, double b, double c, double e) {
+#pragma clang fp contract(off)
+  return d - (a * b + c * e);
+}
+
 constexpr int SCT = CHASE_THREADS;        // systolic chase workgroup (gpmi_band.h)
 constexpr int SNW = SCT / 64;             // waves
 constexpr int SRW = CB / SNW;             // rows per thread
@@ -582,14 +588,91 @@ __device__ __forceinline__ double block_sum_n(double v, double* red) {
   return wave_sum_n(red);
 }
 
+// GPMI_CHASE_PROF builds: workgroups 1-4 stamp the wall clock (100 MHz) at 8
+// points of sweeps 1000-1015 into the words after *err (tools/eig_timing.py)
+#ifdef GPMI_CHASE_PROF
+#define CHASE_STAMP(p)                                                                   \
+  if (tid == 0 && k >= 1 && k <= 4 && s >= 1000 && s < 1016)                          \
+    reinterpret_cast<long long*>(err + 16)[((k - 1) * 16 + (s - 1000)) * 8 + (p)] =      \
+        wall_clock64();
+#else
+#define CHASE_STAMP(p)
+#endif
+
+// Cross-lane steps of the systolic kernel on the VALU (DPP, permlane swaps)
+// instead of LDS permutes: the row sums sit on the hand-off path.
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xf, 0xf, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+constexpr int DPP_QUAD_XOR1 = 0xB1;    // quad_perm [1, 0, 3, 2]
+constexpr int DPP_QUAD_MIRROR = 0x1B;  // quad_perm [3, 2, 1, 0]
+constexpr int DPP_ROW_MIRROR = 0x140;
+constexpr int DPP_ROW_HALF_MIRROR = 0x141;
+constexpr int DPP_ROW_ROR8 = 0x128;
+
+// v_permlane{32,16}_swap on both halves of a double pair: afterwards a + b holds, in
+// the lanes with that lane bit clear, the pair sums of a, and where it is set, of b
+template <int W>
+__device__ __forceinline__ double swap_add(double a, double b) {
+  const long long A = __double_as_longlong(a), B = __double_as_longlong(b);
+  unsigned lo0, lo1, hi0, hi1;
+  if constexpr (W == 32) {
+    const auto l = __builtin_amdgcn_permlane32_swap((unsigned)A, (unsigned)B, false, false);
+    const auto h =
+        __builtin_amdgcn_permlane32_swap((unsigned)(A >> 32), (unsigned)(B >> 32), false, false);
+    lo0 = l[0]; lo1 = l[1]; hi0 = h[0]; hi1 = h[1];
+  } else {
+    const auto l = __builtin_amdgcn_permlane16_swap((unsigned)A, (unsigned)B, false, false);
+    const auto h =
+        __builtin_amdgcn_permlane16_swap((unsigned)(A >> 32), (unsigned)(B >> 32), false, false);
+    lo0 = l[0]; lo1 = l[1]; hi0 = h[0]; hi1 = h[1];
+  }
+  const double x = __longlong_as_double((long long)(((unsigned long long)hi0 << 32) | lo0));
+  const double y = __longlong_as_double((long long)(((unsigned long long)hi1 << 32) | lo1));
+  return x + y;
+}
+
+// butterfly8 on the VALU: every lane gets the 64-lane sum of value (lane >> 3) & 7
+__device__ __forceinline__ double butterfly8_valu(double (&v)[8]) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) v[q] = swap_add<32>(v[q], v[q + 4]);
+#pragma unroll
+  for (int q = 0; q < 2; ++q) v[q] = swap_add<16>(v[q], v[q + 2]);
+  const bool up = (lane & 8) != 0;
+  double r = (up ? v[1] : v[0]) + dpp_d<DPP_ROW_MIRROR>(up ? v[0] : v[1]);
+  r += dpp_d<DPP_ROW_HALF_MIRROR>(r);
+  r += dpp_d<DPP_QUAD_MIRROR>(r);
+  r += dpp_d<DPP_QUAD_XOR1>(r);
+  return r;
+}
+
+// sum over the lanes (lane & 7) == 0 (others hold 0), in lane 0 (and every lane)
+__device__ __forceinline__ double group_lead_sum(double t) {
+  t = swap_add<32>(t, t);
+  t = swap_add<16>(t, t);
+  return t + dpp_d<DPP_ROW_ROR8>(t);
+}
+
+__device__ __forceinline__ double readlane_dbl(double v, int l) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)b, l);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
 __global__ __launch_bounds__(SCT) void chase_systolic_kernel(
     const double* __restrict__ Ab, int64_t lda, int n, unsigned long long* __restrict__ msg_r,
     unsigned long long* __restrict__ msg_c, int* __restrict__ err, unsigned spin_limit,
     double* __restrict__ dout, double* __restrict__ e2out) {
-  __shared__ double sv[CB], sv2[CB], sp[CB], sq[CB], sx[CB], scol[CB], serow[CB], snew[CB];
+  __shared__ double sv[CB], sv2[CB], sp[CB], sx[CB], scol[CB], serow[CB], snew[CB + 1];
   __shared__ double xk0[CB];
   __shared__ double cpart[SNW][CB];
-  __shared__ double red[SNW], redp[SNW], rednb[SNW];
+  __shared__ double red[SNW], redp[SNW], rednb[SNW], redx[SNW];
   __shared__ double sscal[4];
   __shared__ int s_bail;
   constexpr int M = CB - 1;
@@ -611,27 +694,30 @@ __global__ __launch_bounds__(SCT) void chase_systolic_kernel(
       E[u][j] = (re < n && c < n && re - c <= CB) ? Ab[(int64_t)re * lda + c] : 0.0;
     }
   }
-  if (k == 0) {
-    if (tid < CB) xk0[tid] = (1 + tid < n) ? Ab[(int64_t)(1 + tid) * lda] : 0.0;
-    if (tid == 0) dout[0] = Ab[0];
-  }
   if (tid == 0) s_bail = 0;
+  if (k == 0) {
+    // the reflector of sweep 0 from column 0; later sweeps' are formed one sweep
+    // ahead (step 4), off the hand-off path
+    const double xi = (tid < CB && 1 + tid < n) ? Ab[(int64_t)(1 + tid) * lda] : 0.0;
+    if (tid == 0) sscal[1] = xi;
+    const double nb2 = block_sum_n((tid > 0 && tid < CB) ? xi * xi : 0.0, red);
+    double tau0, beta0, sc0;
+    chase_dlarfg(sscal[1], nb2, tau0, beta0, sc0);
+    if (tid < CB) sv[tid] = (tid == 0) ? 1.0 : xi * sc0;
+    if (tid == 0) {
+      sscal[0] = tau0;
+      dout[0] = Ab[0];
+      e2out[0] = beta0 * beta0;
+    }
+  }
   __syncthreads();
   for (int s = 0; s <= s_end; ++s) {
     const int off = s & M;
     const int uo = off / SNW, wo = off % SNW, lo = off >> 1, jo = off & 1;
     const bool nxt = s + 1 + (k + 1) * CB < n;   // position k + 1 works in sweep s
-    // ---- 1. reflector of task (s, k) into sv (physical order)
-    double tau = 0.0;
-    if (k == 0) {
-      const double xi = (tid < CB) ? xk0[tid] : 0.0;
-      const double x0 = xk0[0];
-      const double nb2 = block_sum_n((tid > 0 && tid < CB) ? xi * xi : 0.0, red);
-      double beta, scale;
-      chase_dlarfg(x0, nb2, tau, beta, scale);
-      if (tid < CB) sv[(tid + off) & M] = (tid == 0) ? 1.0 : xi * scale;
-      if (tid == 0) e2out[s] = beta * beta;
-    } else {
+    // ---- 1. the reflector of task (s, k) (physical order in sv, tau in sscal[0])
+    CHASE_STAMP(0)
+    if (k != 0) {
       if (tid <= CB) {
         const unsigned long long* m = msg_r + ((int64_t)k * 2 + (s & 1)) * (2 * CMSG);
         double v = 0.0;
@@ -639,121 +725,160 @@ __global__ __launch_bounds__(SCT) void chase_systolic_kernel(
         if (tid < CB) sv[(tid + off) & M] = v;
         else sscal[0] = v;
       }
+      __syncthreads();
+      if (s_bail) return;
     }
-    __syncthreads();
-    if (s_bail) return;
-    if (k != 0) tau = sscal[0];
-    // ---- 2. D <- H D H, E <- E H: the row sums D v, E v in one pass, v.(D v) per
-    //      wave, one barrier
-    if (tau != 0.0) {
-      const double vc0 = sv[c0], vc1 = sv[c0 + 1];
-      constexpr int NH = SRW / 8;   // 8-row halves per thread
-      double prow[NH], qrow[NH];
+    CHASE_STAMP(1)
+    const double tau = sscal[0];
+    const double vc0 = sv[c0], vc1 = sv[c0 + 1];
+    // ---- 2. row sums D v, E v (one pass); v.(D v) per wave; lane lo of every
+    //      wave forms E's updated first column x' = E[:, 0] - tau (E v) and keeps
+    //      D's first column; one barrier
+    constexpr int NH = SRW / 8;   // 8-row halves per thread
+    double qrow[NH];
+    {
+      double prow[NH];
 #pragma unroll
       for (int h = 0; h < NH; ++h) {
         double rowv[8];
 #pragma unroll
         for (int uu = 0; uu < 8; ++uu)
           rowv[uu] = D[8 * h + uu][0] * vc0 + D[8 * h + uu][1] * vc1;
-        prow[h] = butterfly8(rowv);
+        prow[h] = butterfly8_valu(rowv);
 #pragma unroll
         for (int uu = 0; uu < 8; ++uu)
           rowv[uu] = E[8 * h + uu][0] * vc0 + E[8 * h + uu][1] * vc1;
-        qrow[h] = butterfly8(rowv);
+        qrow[h] = butterfly8_valu(rowv);
       }
       double vpw = 0.0;
 #pragma unroll
       for (int h = 0; h < NH; ++h) {
-        // the row this lane's sums of half h belong to
-        const int rr = SNW * (8 * h + ((lane >> 3) & 7)) + w;
+        const int rr = SNW * (8 * h + ((lane >> 3) & 7)) + w;   // row of this lane's sums
         if ((lane & 7) == 0) {
           vpw += prow[h] * sv[rr];
           sp[rr] = prow[h];
-          sq[rr] = qrow[h];
         }
       }
-      vpw += __shfl_xor(vpw, 8);
-      vpw += __shfl_xor(vpw, 16);
-      vpw += __shfl_xor(vpw, 32);
+      vpw = group_lead_sum(vpw);
       if (lane == 0) redp[w] = vpw;
-      __syncthreads();
-      const double vp = tau * wave_sum_n(redp);
-      const double hvp = 0.5 * tau * vp;
-      const double wc0 = chase_w(tau, sp[c0], hvp, vc0), wc1 = chase_w(tau, sp[c0 + 1], hvp, vc1);
+    }
+    // E <- E H = E - (tau E v) v^T here (the row sums are wave-uniform by readlane):
+    // E's first column is then the x' of the next reflector
+    if (tau != 0.0) {
 #pragma unroll
       for (int u = 0; u < SRW; ++u) {
-        const int r = SNW * u + w;
-        const double vr = sv[r], wr = chase_w(tau, sp[r], hvp, vr), qr = tau * sq[r];
-        {
-          // both products rounded, then summed (commutative): D stays exactly symmetric
-#pragma clang fp contract(off)
-          D[u][0] = D[u][0] - (vr * wc0 + wr * vc0);
-          D[u][1] = D[u][1] - (vr * wc1 + wr * vc1);
-        }
+        const double qr = tau * readlane_dbl(qrow[u >> 3], 8 * (u & 7));
         E[u][0] = E[u][0] - qr * vc0;
         E[u][1] = E[u][1] - qr * vc1;
       }
     }
-    // ---- 3. E's first column and D's first column (lane lo of every wave holds
-    //      them) into LDS; the reflector of task (s, k + 1); post it, and D's first
-    //      column + E[0][0] for position k - 1
     if (lane == lo) {
       double part = 0.0;
+      if (jo) {
 #pragma unroll
-      for (int u = 0; u < SRW; ++u) {
-        const int r = SNW * u + w;
-        const double x = jo ? E[u][1] : E[u][0];
-        sx[r] = x;
-        scol[r] = jo ? D[u][1] : D[u][0];
-        if (r != off) part += x * x;
+        for (int u = 0; u < SRW; ++u) {
+          const int r = SNW * u + w;
+          sx[r] = E[u][1];
+          scol[r] = D[u][1];
+          part += (r != off) ? E[u][1] * E[u][1] : 0.0;
+        }
+      } else {
+#pragma unroll
+        for (int u = 0; u < SRW; ++u) {
+          const int r = SNW * u + w;
+          sx[r] = E[u][0];
+          scol[r] = D[u][0];
+          part += (r != off) ? E[u][0] * E[u][0] : 0.0;
+        }
       }
       rednb[w] = part;
     }
     __syncthreads();
+    CHASE_STAMP(2)
+    // ---- 3. post: the reflector of task (s, k + 1) to position k + 1, D's first
+    //      column (after H D H) and E[0][0] to position k - 1 (position 0 keeps
+    //      them: the finished diagonal and the column of sweep s + 1)
+    const double hvp = 0.5 * tau * (tau * wave_sum_n(redp));
     double taun = 0.0, betan = 0.0, scn = 0.0;
     if (nxt) {
       chase_dlarfg(sx[off], wave_sum_n(rednb), taun, betan, scn);
-      if (tid < CB) sv2[tid] = (tid == off) ? 1.0 : sx[tid] * scn;
       unsigned long long* m = msg_r + ((int64_t)(k + 1) * 2 + (s & 1)) * (2 * CMSG);
       if (tid < CB) put_granules(m + 2 * tid, (tid == 0) ? 1.0 : sx[(tid + off) & M] * scn,
                                  (unsigned)(s + 1));
       else if (tid == CB) put_granules(m + 2 * CB, taun, (unsigned)(s + 1));
     }
     const double e00 = nxt ? betan : 0.0;   // E[0][0] after the left update of step 4
+    // D[r][0] after H D H (physical column off); the value the update below gives
+    auto dcol = [&](int r) {
+      if (tau == 0.0) return scol[r];
+      const double vr = sv[r], wr = chase_w(tau, sp[r], hvp, vr);
+      const double wo_ = chase_w(tau, sp[off], hvp, sv[off]);
+      return chase_dsub(scol[r], vr, wo_, wr, sv[off]);
+    };
+    double xn = 0.0;   // k = 0: this thread's entry of the next sweep's column
     if (k >= 1) {
       const int t2 = tid - 256;
       unsigned long long* m = msg_c + ((int64_t)k * 2 + (s & 1)) * (2 * CMSG);
-      if (t2 >= 0 && t2 < CB) put_granules(m + 2 * t2, scol[(t2 + off) & M], (unsigned)(s + 1));
+      if (t2 >= 0 && t2 < CB) put_granules(m + 2 * t2, dcol((t2 + off) & M), (unsigned)(s + 1));
       else if (t2 == CB) put_granules(m + 2 * CB, e00, (unsigned)(s + 1));
     } else {
-      // position 0 keeps them: the finished diagonal and the column of sweep s + 1
       if (tid < CB) {
-        if (tid == off) dout[s + 1] = scol[tid];
-        else xk0[(tid - off - 1) & M] = scol[tid];
-      } else if (tid == CB) {
-        xk0[M] = e00;
-      }
-      if (s == n - 3) {   // last sweep: the trailing 2 x 2 block is final
-        const int o1 = (off + 1) & M;
-        if (tid == 0) {
-          e2out[n - 2] = scol[o1] * scol[o1];
+        const double dv = dcol(tid);
+        if (tid == off) {
+          dout[s + 1] = dv;
+        } else {
+          xk0[(tid - off - 1) & M] = dv;
+          xn = dv;
+        }
+        if (s == n - 3 && tid == ((off + 1) & M)) {   // last sweep: trailing 2 x 2 block
+          e2out[n - 2] = dv * dv;
           e2out[n - 1] = 0.0;
         }
+      } else if (tid == CB) {
+        xk0[M] = e00;
+        xn = e00;
+      }
+    }
+    if (nxt && tid < CB) sv2[tid] = (tid == off) ? 1.0 : sx[tid] * scn;
+    CHASE_STAMP(3)
+    // ---- 4. D <- H D H, E <- E H (registers), then E <- H' E
+    if (tau != 0.0) {
+      const double wc0 = chase_w(tau, sp[c0], hvp, vc0), wc1 = chase_w(tau, sp[c0 + 1], hvp, vc1);
+#pragma unroll
+      for (int u = 0; u < SRW; ++u) {
+        const int r = SNW * u + w;
+        const double vr = sv[r], wr = chase_w(tau, sp[r], hvp, vr);
+        {
+          // both products rounded, then summed (commutative): D stays exactly symmetric
+#pragma clang fp contract(off)
+          D[u][0] = D[u][0] - (vr * wc0 + wr * vc0);
+          D[u][1] = D[u][1] - (vr * wc1 + wr * vc1);
+        }
+      }
+    }
+    if (k == 0) {
+      if (s == n - 3) {
+        const int o1 = (off + 1) & M;
         if (w == (o1 % SNW) && lane == (o1 >> 1)) {
 #pragma unroll
           for (int u = 0; u < SRW; ++u)
             if (u == o1 / SNW) dout[n - 1] = (o1 & 1) ? D[u][1] : D[u][0];
         }
       }
+      // sum of squares of the next column below its first entry
+      const int idx = (tid < CB) ? ((tid - off - 1) & M) : M;
+      double x2 = (tid <= CB && tid != off && idx >= 1) ? xn * xn : 0.0;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) x2 += __shfl_xor(x2, o);
+      if (lane == 0) redx[w] = x2;
     }
-    __syncthreads();   // sv2 for step 4
-    // ---- 4. E <- H' E (the bulge block of task (s, k + 1)); column off -> (beta', 0...)
+    __syncthreads();   // sv2, xk0 / redx
+    CHASE_STAMP(4)
     if (nxt && taun != 0.0) {
       double cp0 = 0.0, cp1 = 0.0;
 #pragma unroll
       for (int u = 0; u < SRW; ++u) {
-        const int r = SNW * u + w;
-        const double vr = sv2[r];
+        const double vr = sv2[SNW * u + w];
         cp0 += E[u][0] * vr;
         cp1 += E[u][1] * vr;
       }
@@ -776,7 +901,18 @@ __global__ __launch_bounds__(SCT) void chase_systolic_kernel(
         E[u][1] = (c0 + 1 == off) ? (r == off ? betan : 0.0) : E[u][1] - vr * r1s;
       }
     }
+    if (k == 0 && s < s_end) {
+      // the reflector of sweep s + 1 (its column is final now), into sv / sscal[0]
+      double tn, bn, scl;
+      chase_dlarfg(xk0[0], wave_sum_n(redx), tn, bn, scl);
+      if (tid < CB) sv[(tid + off + 1) & M] = (tid == 0) ? 1.0 : xk0[tid] * scl;
+      if (tid == 0) {
+        sscal[0] = tn;
+        e2out[s + 1] = bn * bn;
+      }
+    }
     // ---- 5. slide the window: physical row / column off becomes logical b - 1
+    CHASE_STAMP(5)
     if (w == wo) {
 #pragma unroll
       for (int u = 0; u < SRW; ++u)
@@ -796,19 +932,31 @@ __global__ __launch_bounds__(SCT) void chase_systolic_kernel(
     }
     __syncthreads();
     if (s_bail) return;
+    CHASE_STAMP(6)
     const double d00 = snew[0], ne00 = sscal[3];
+    if (w == wo) {   // row off: D's from E's old first row, E's (0 ... 0, ne00)
 #pragma unroll
-    for (int u = 0; u < SRW; ++u) {
-      const int r = SNW * u + w;
+      for (int u = 0; u < SRW; ++u)
+        if (u == uo) {
+          D[u][0] = (c0 == off) ? d00 : serow[c0];
+          D[u][1] = (c0 + 1 == off) ? d00 : serow[c0 + 1];
+          E[u][0] = (c0 == off) ? ne00 : 0.0;
+          E[u][1] = (c0 + 1 == off) ? ne00 : 0.0;
+        }
+    }
+    if (lane == lo) {   // column off below / above row off
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int c = c0 + j;
-        if (r == off) {
-          D[u][j] = (c == off) ? d00 : serow[c];
-          E[u][j] = (c == off) ? ne00 : 0.0;
-        } else if (c == off) {
-          D[u][j] = serow[r];
-          E[u][j] = snew[((r - off - 1) & M) + 1];
+      for (int u = 0; u < SRW; ++u) {
+        const int r = SNW * u + w;
+        if (r != off) {
+          const double dn = serow[r], en = snew[((r - off - 1) & M) + 1];
+          if (jo) {
+            D[u][1] = dn;
+            E[u][1] = en;
+          } else {
+            D[u][0] = dn;
+            E[u][0] = en;
+          }
         }
       }
     }
