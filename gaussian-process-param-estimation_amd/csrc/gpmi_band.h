@@ -72,6 +72,9 @@ __global__ void chase_apply_kernel(double* A, int64_t lda, int n, int t, int s_h
 __global__ void tridiag_extract_kernel(const double* A, int64_t lda, int n, double* d, double* e2);
 __global__ void bisect_kernel(const double* d, const double* e2, int n, double lo0, double hi0,
                               double pivmin, double* lam);
+__global__ void bisect_multi_kernel(const double* d, const double* e2, int n, double lo0,
+                                    double hi0, double pivmin, double* lam);
+constexpr int BISECT_LANES = 16;   // = BG (gpmi_chase.hip)
 
 // Read-only view of an operator for the band path (gpmi_api.hip).
 struct OpView {

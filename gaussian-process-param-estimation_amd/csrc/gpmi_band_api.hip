@@ -748,9 +748,18 @@ int gpmi_band_eigenvalues(gpmi_band* b, double* lam) {
   lo -= span;
   hi += span;
   const double pivmin = 2.2250738585072014e-308 * std::max(1.0, emax);
-  hipLaunchKernelGGL(bisect_kernel, dim3((n + 255) / 256), dim3(256), 0, s, d, e2, n, lo, hi,
-                     pivmin, dl);
-  BD_LAUNCH("bisect_kernel");
+  // GPMI_BISECT=1: one thread per eigenvalue (plain bisection) instead of multisection
+  const char* bis = std::getenv("GPMI_BISECT");
+  if (bis && std::atoi(bis) == 1) {
+    hipLaunchKernelGGL(bisect_kernel, dim3((n + 255) / 256), dim3(256), 0, s, d, e2, n, lo, hi,
+                       pivmin, dl);
+    BD_LAUNCH("bisect_kernel");
+  } else {
+    const int64_t lanes = (int64_t)n * BISECT_LANES;
+    hipLaunchKernelGGL(bisect_multi_kernel, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, s,
+                       d, e2, n, lo, hi, pivmin, dl);
+    BD_LAUNCH("bisect_multi_kernel");
+  }
   BD_TRY(hipMemcpyAsync(lam, dl, sizeof(double) * n, hipMemcpyDeviceToHost, s));
   BD_TRY(hipEventRecord(b->ev1, s));
   BD_TRY(hipStreamSynchronize(s));

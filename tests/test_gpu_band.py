@@ -169,6 +169,18 @@ def test_systolic_chase_matches_launch_form(gp, n, monkeypatch):
     assert numpy.max(numpy.abs(lam - ref)) <= 1e-12 * scale
 
 
+def test_multisection_matches_bisection(gp, monkeypatch):
+    """Multisection (16 Sturm counts per round, default) and one-thread bisection
+    find every eigenvalue to the same 2-ulp interval: they agree to 4 ulp of
+    max |lambda|."""
+    K, _, _ = _inputs(1500, 8)
+    lam = _mc(K).eigenvalues()
+    monkeypatch.setenv('GPMI_BISECT', '1')
+    lam_b = _mc(K).eigenvalues()
+    scale = numpy.abs(lam_b).max()
+    assert numpy.max(numpy.abs(lam - lam_b)) <= 8.9e-16 * scale
+
+
 def test_systolic_chase_timeout_falls_back(gp, monkeypatch):
     """GPMI_CHASE_SPIN_LIMIT=0 makes the first hand-off wait of the systolic
     chase a timeout (as when its workgroups cannot all be resident): every
