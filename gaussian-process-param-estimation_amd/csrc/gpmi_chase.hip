@@ -762,33 +762,29 @@ __global__ __launch_bounds__(SCT) void chase_systolic_kernel(
       vpw = group_lead_sum(vpw);
       if (lane == 0) redp[w] = vpw;
     }
-    // E <- E H = E - (tau E v) v^T here (the row sums are wave-uniform by readlane):
-    // E's first column is then the x' of the next reflector
-    if (tau != 0.0) {
-#pragma unroll
-      for (int u = 0; u < SRW; ++u) {
-        const double qr = tau * readlane_dbl(qrow[u >> 3], 8 * (u & 7));
-        E[u][0] = E[u][0] - qr * vc0;
-        E[u][1] = E[u][1] - qr * vc1;
-      }
-    }
+    // E's updated first column x' = E[:, 0] - tau (E v) (v_0 = 1; the row sums are
+    // wave-uniform by readlane) and D's first column, from lane lo of every wave;
+    // the sum of squares over all rows (row off's square is taken out after the
+    // barrier)
     if (lane == lo) {
       double part = 0.0;
       if (jo) {
 #pragma unroll
         for (int u = 0; u < SRW; ++u) {
           const int r = SNW * u + w;
-          sx[r] = E[u][1];
+          const double x = E[u][1] - (tau * readlane_dbl(qrow[u >> 3], 8 * (u & 7))) * vc1;
+          sx[r] = x;
           scol[r] = D[u][1];
-          part += (r != off) ? E[u][1] * E[u][1] : 0.0;
+          part += x * x;
         }
       } else {
 #pragma unroll
         for (int u = 0; u < SRW; ++u) {
           const int r = SNW * u + w;
-          sx[r] = E[u][0];
+          const double x = E[u][0] - (tau * readlane_dbl(qrow[u >> 3], 8 * (u & 7))) * vc0;
+          sx[r] = x;
           scol[r] = D[u][0];
-          part += (r != off) ? E[u][0] * E[u][0] : 0.0;
+          part += x * x;
         }
       }
       rednb[w] = part;
@@ -801,7 +797,8 @@ __global__ __launch_bounds__(SCT) void chase_systolic_kernel(
     const double hvp = 0.5 * tau * (tau * wave_sum_n(redp));
     double taun = 0.0, betan = 0.0, scn = 0.0;
     if (nxt) {
-      chase_dlarfg(sx[off], wave_sum_n(rednb), taun, betan, scn);
+      const double x0 = sx[off];
+      chase_dlarfg(x0, fmax(wave_sum_n(rednb) - x0 * x0, 0.0), taun, betan, scn);
       unsigned long long* m = msg_r + ((int64_t)(k + 1) * 2 + (s & 1)) * (2 * CMSG);
       if (tid < CB) put_granules(m + 2 * tid, (tid == 0) ? 1.0 : sx[(tid + off) & M] * scn,
                                  (unsigned)(s + 1));
@@ -854,6 +851,9 @@ __global__ __launch_bounds__(SCT) void chase_systolic_kernel(
           D[u][0] = D[u][0] - (vr * wc0 + wr * vc0);
           D[u][1] = D[u][1] - (vr * wc1 + wr * vc1);
         }
+        const double qr = tau * readlane_dbl(qrow[u >> 3], 8 * (u & 7));
+        E[u][0] = E[u][0] - qr * vc0;
+        E[u][1] = E[u][1] - qr * vc1;
       }
     }
     if (k == 0) {
