@@ -74,7 +74,10 @@ __global__ void bisect_kernel(const double* d, const double* e2, int n, double l
                               double pivmin, double* lam);
 __global__ void bisect_multi_kernel(const double* d, const double* e2, int n, double lo0,
                                     double hi0, double pivmin, double* lam);
-constexpr int BISECT_LANES = 16;   // = BG (gpmi_chase.hip)
+#ifndef GPMI_BISECT_LANES
+#define GPMI_BISECT_LANES 16
+#endif
+constexpr int BISECT_LANES = GPMI_BISECT_LANES;   // lanes per eigenvalue (multisection)
 
 // Read-only view of an operator for the band path (gpmi_api.hip).
 struct OpView {

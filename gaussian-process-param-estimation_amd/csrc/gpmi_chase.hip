@@ -1027,7 +1027,7 @@ __global__ __launch_bounds__(256) void bisect_kernel(const double* __restrict__ 
 // 16 x n lanes keep the SIMDs busy where n threads left most of them idle.
 // The count streams d and e2 in blocks of 8 loaded ahead of the dependent
 // pivot chain.
-constexpr int BG = 16;
+constexpr int BG = BISECT_LANES;
 
 __device__ __forceinline__ int sturm_count_blk(const double* __restrict__ d,
                                                const double* __restrict__ e2, int n, double x,
@@ -1046,7 +1046,16 @@ __device__ __forceinline__ int sturm_count_blk(const double* __restrict__ d,
     }
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
+#ifdef GPMI_BISECT_FASTDIV
+      // e2 / q as e2 * (1 / q): v_rcp_f64 and two Newton steps (a few ulp; the
+      // count is the number of negative pivots, insensitive at that level)
+      double r = __builtin_amdgcn_rcp(q);
+      r = fma(fma(-q, r, 1.0), r, r);
+      r = fma(fma(-q, r, 1.0), r, r);
+      q = dd[t] - x - ee[t] * r;
+#else
       q = dd[t] - x - ee[t] / q;
+#endif
       if (fabs(q) < pivmin) q = -pivmin;
       cnt += q < 0.0;
     }
@@ -1074,8 +1083,8 @@ __global__ __launch_bounds__(256) void bisect_multi_kernel(const double* __restr
     const double x = lo + wdt * (double)(j + 1) / (double)(BG + 1);
     const int cnt = sturm_count_blk(d, e2, n, x, pivmin);
     const unsigned long long m = __ballot(cnt > i);
-    const unsigned gm = (unsigned)(m >> (lane & ~(BG - 1))) & ((1u << BG) - 1u);
-    const int js = gm ? __builtin_ctz(gm) : BG;   // first point whose count exceeds i
+    const unsigned long long gm = (m >> (lane & ~(BG - 1))) & ((2ull << (BG - 1)) - 1ull);
+    const int js = gm ? __builtin_ctzll(gm) : BG;   // first point whose count exceeds i
     const double nlo = (js == 0) ? lo : lo + wdt * (double)js / (double)(BG + 1);
     const double nhi = (js == BG) ? hi : lo + wdt * (double)(js + 1) / (double)(BG + 1);
     lo = nlo;
