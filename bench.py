@@ -360,7 +360,12 @@ def run_sparse(args, world, rank, local, dist, torch):
     nnz = op.sop.nnz
     alg_bytes = 12.0 * nnz + 8.0 * (n + 1) + 16.0 * n * s_blk
     gbs = alg_bytes / (ms * 1e-3) / 1e9
-    sp_traffic, sp_tsrc = pmc_traffic_sparse(args.config) if s_blk == 20 else (None, None)
+    info = op.sop.spmm_info()
+    sp_kernel = 'csr_spmm_win_kernel' if info['windowed'] else 'csr_spmm_kernel'
+    gather_bytes = (8.0 * s_blk * info['mean_window'] * ((n + 63) // 64) if info['windowed']
+                    else 8.0 * nnz * s_blk)
+    sp_traffic, sp_tsrc = (pmc_traffic_sparse(args.config, 'gpmi::' + sp_kernel)
+                           if s_blk == 20 else (None, None))
     if rank == 0:
         res = {
             'metric': 'log-likelihood evals/sec (%s, sparse tapered Matern, SLQ + CG)'
@@ -382,13 +387,15 @@ def run_sparse(args, world, rank, local, dist, torch):
                          'traffic': None if sp_traffic is None else round(sp_traffic),
                          'traffic_unit': 'bytes per launch (HBM side, PMC)',
                          'traffic_source': sp_tsrc,
-                         'kernel': 'csr_spmm_kernel (s=%d columns)' % s_blk,
+                         'kernel': '%s (s=%d columns)' % (sp_kernel, s_blk),
                          'avg_launch_ms': round(ms, 4),
-                         # every nonzero gathers s contiguous doubles of X: cache-side bytes
-                         'gather_bytes': 8.0 * nnz * s_blk,
-                         'gather_gbs': round(8.0 * nnz * s_blk / (ms * 1e-3) / 1e9, 1),
+                         # cache-side X bytes: every nonzero gathers s contiguous doubles
+                         # (gather kernel), or every 64-row block stages its window
+                         'gather_bytes': gather_bytes,
+                         'gather_gbs': round(gather_bytes / (ms * 1e-3) / 1e9, 1),
+                         'spmm_window': info,
                          'note': 'working set %.1f MB: Infinity-Cache resident when < 256 MB; '
-                                 'the X gathers (gather_bytes) are served by L2 / MALL'
+                                 'the X reads (gather_bytes) are served by L2 / MALL'
                                  % (alg_bytes / 1e6)},
             'lp_sample': [float(v) for v in last[0].tolist()],
             'cpu_baseline': None,

@@ -32,6 +32,14 @@ __global__ void csr_cell_fill_kernel(const double*, int64_t, int, const double*,
 constexpr int CELL_CAP_HOST = 512;   // = CELL_CAP (gpmi_matern.hip)
 __global__ void csr_spmm_kernel(const int64_t*, const int*, const double*, int64_t, const double*,
                                 int64_t, double*, int64_t, int, int, double);
+__global__ void spmm_window_build_kernel(const int64_t*, const int*, int64_t, int*, int*,
+                                         unsigned short*);
+__global__ void csr_spmm_win_kernel(const int64_t*, const int*, const unsigned short*,
+                                    const double*, int64_t, const int*, const int*, const double*,
+                                    int64_t, double*, int64_t, int, double);
+constexpr int WIN_ROWS_HOST = 64;    // = WIN_ROWS (gpmi_sparse.hip)
+constexpr int WIN_MAXU_HOST = 1024;  // = WIN_MAXU
+constexpr int WIN_CS_HOST = 8;       // = WIN_CS
 __global__ void col_dot_partial_kernel(const double*, int64_t, const double*, int64_t, int,
                                        double*);
 __global__ void col_dot_reduce_kernel(const double*, int, int, int, double*);
@@ -128,6 +136,15 @@ struct gpmi_sp {
   // outputs of every call stay in the original order (permuted at the boundary).
   std::vector<int> perm;       // empty: identity
   int* perm_d = nullptr;
+  // X windows of the default SpMM (csr_spmm_win_kernel), built on first use
+  int* win_cols = nullptr;             // [nblk][WIN_MAXU] sorted window columns
+  int* win_u = nullptr;                // [nblk] window sizes (0: block gathers from X)
+  unsigned short* win_lidx = nullptr;  // [nnz] window position of every nonzero
+  int win_maxu = -1;                   // -1: not built
+  int win_maxm = 0;                    // most nonzeros in a windowed block
+  double win_mean = 0.0;               // mean window columns per block
+  bool win_use = false;                // the windowed kernel is the faster one here
+  int64_t win_nblk = 0;
 };
 
 namespace {
@@ -150,7 +167,78 @@ int ensure_partial(gpmi_sp* sp, size_t doubles) {
   return 0;
 }
 
+int ensure_window(gpmi_sp* sp) {
+  if (sp->win_maxu >= 0) return 0;
+  const int64_t nblk = (sp->n + WIN_ROWS_HOST - 1) / WIN_ROWS_HOST;
+  SP_TRY(hipMalloc(&sp->win_cols, sizeof(int) * (size_t)nblk * WIN_MAXU_HOST));
+  SP_TRY(hipMalloc(&sp->win_u, sizeof(int) * (size_t)nblk));
+  SP_TRY(hipMalloc(&sp->win_lidx, sizeof(unsigned short) * (size_t)std::max<int64_t>(1, sp->nnz)));
+  hipLaunchKernelGGL(spmm_window_build_kernel, dim3((unsigned)nblk), dim3(256), 0, sp->stream,
+                     sp->indptr, sp->indices, sp->n, sp->win_cols, sp->win_u, sp->win_lidx);
+  SP_LAUNCH("spmm_window_build_kernel");
+  std::vector<int> hu((size_t)nblk);
+  SP_TRY(hipMemcpyAsync(hu.data(), sp->win_u, sizeof(int) * nblk, hipMemcpyDeviceToHost,
+                        sp->stream));
+  SP_TRY(hipStreamSynchronize(sp->stream));
+  int mu = 0;
+  for (int v : hu) mu = std::max(mu, v);
+  {
+    double su = 0.0;
+    for (int v : hu) su += v;
+    sp->win_mean = su / (double)nblk;
+  }
+  std::vector<int64_t> hp((size_t)sp->n + 1);
+  SP_TRY(hipMemcpy(hp.data(), sp->indptr, sizeof(int64_t) * (sp->n + 1), hipMemcpyDeviceToHost));
+  int mm = 0;
+  for (int64_t b = 0; b < nblk; ++b)
+    if (hu[(size_t)b] > 0) {
+      const int64_t r0 = b * WIN_ROWS_HOST, r1 = std::min<int64_t>(r0 + WIN_ROWS_HOST, sp->n);
+      mm = std::max<int>(mm, (int)(hp[(size_t)r1] - hp[(size_t)r0]));
+    }
+  sp->win_maxm = mm;
+  if (std::getenv("GPMI_SPMM_TRACE")) {
+    double su = 0.0;
+    int nz = 0;
+    for (int v : hu) {
+      su += v;
+      nz += v == 0;
+    }
+    fprintf(stderr, "[gpmi spmm] %lld blocks of %d rows: window mean %.1f max %d, %d unwindowed, "
+            "max block nnz %d\n", (long long)nblk, WIN_ROWS_HOST, su / (double)nblk, mu, nz, mm);
+  }
+  const size_t lds = (size_t)std::max(1, mu) * WIN_CS_HOST * 8 + 10 * (size_t)mm + 4 +
+                     4 * (WIN_ROWS_HOST + 1);
+  // the windowed kernel pays off while several workgroups fit a CU (2D tapered
+  // Matern: windows of ~160 columns, 24 KB, 6 per CU: 1.2x); with 3D windows
+  // (~350 columns, 49 KB, 3 per CU) it is slower than gathering from X
+  sp->win_use = lds <= 32 * 1024;
+  if (lds > 160 * 1024) return set_error(-1104, "spmm window exceeds LDS");
+  if (lds > 64 * 1024)
+    SP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&csr_spmm_win_kernel),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  sp->win_nblk = nblk;
+  sp->win_maxu = mu;
+  return 0;
+}
+
 int spmm(gpmi_sp* sp, const double* X, double* Y, int s, double eta) {
+  // GPMI_SPMM_WINDOW: 0 the gather-from-X kernel, 2 the windowed kernel, unset or 1
+  // the faster one for this matrix (win_use)
+  const char* wenv = std::getenv("GPMI_SPMM_WINDOW");
+  const int wmode = wenv ? std::atoi(wenv) : 1;
+  if (wmode != 0 && sp->win_maxu < 0)
+    if (int rc = ensure_window(sp)) return rc;
+  if (wmode == 2 || (wmode != 0 && sp->win_use)) {
+    // window + the largest windowed block's values, positions and row starts
+    const size_t lds = sizeof(double) * WIN_CS_HOST * (size_t)std::max(1, sp->win_maxu) +
+                       10 * (size_t)sp->win_maxm + 4 + sizeof(int) * (WIN_ROWS_HOST + 1);
+    hipLaunchKernelGGL(csr_spmm_win_kernel,
+                       dim3((unsigned)sp->win_nblk),
+                       dim3(256), lds, sp->stream, sp->indptr, sp->indices, sp->win_lidx, sp->data,
+                       sp->n, sp->win_cols, sp->win_u, X, (int64_t)s, Y, (int64_t)s, s, eta);
+    SP_LAUNCH("csr_spmm_win_kernel");
+    return 0;
+  }
   hipLaunchKernelGGL(csr_spmm_kernel, dim3((unsigned)((sp->n + 3) / 4)), dim3(256), 0,
                      sp->stream, sp->indptr, sp->indices, sp->data, sp->n, X, (int64_t)s, Y,
                      (int64_t)s, s, 64 / s, eta);
@@ -496,6 +584,9 @@ int gpmi_sp_destroy(gpmi_sp* sp) {
   if (sp->small) (void)hipFree(sp->small);
   if (sp->msbuf) (void)hipFree(sp->msbuf);
   if (sp->lz) (void)hipFree(sp->lz);
+  if (sp->win_cols) (void)hipFree(sp->win_cols);
+  if (sp->win_u) (void)hipFree(sp->win_u);
+  if (sp->win_lidx) (void)hipFree(sp->win_lidx);
   if (sp->stream) (void)hipStreamDestroy(sp->stream);
   delete sp;
   return 0;
@@ -863,6 +954,19 @@ int gpmi_sp_msgram(gpmi_sp* sp, const double* etas, int neta, const double* rhs,
   SP_TRY(hipStreamSynchronize(str));
   std::copy(hg.begin(), hg.end(), G);
   if (iterations) *iterations = it;
+  return 0;
+}
+
+int gpmi_sp_spmm_info(gpmi_sp* sp, int* windowed, double* mean_window, int* max_window) {
+  if (!sp) return set_error(-1006, "null handle");
+  Guard g(sp->device);
+  if (sp->win_maxu < 0)
+    if (int rc = ensure_window(sp)) return rc;
+  const char* wenv = std::getenv("GPMI_SPMM_WINDOW");
+  const int wmode = wenv ? std::atoi(wenv) : 1;
+  if (windowed) *windowed = wmode == 2 || (wmode != 0 && sp->win_use);
+  if (mean_window) *mean_window = sp->win_mean;
+  if (max_window) *max_window = sp->win_maxu;
   return 0;
 }
 

@@ -92,6 +92,7 @@ SIGNATURES = {
     'gpmi_band_stats': (ctypes.c_int, [c_op_p, c_int_p, c_int_p]),
     'gpmi_band_chase_info': (ctypes.c_int, [c_op_p, c_int_p, c_int_p, c_int_p]),
     'gpmi_sp_last_status': (ctypes.c_int, [c_op_p, c_int_p]),
+    'gpmi_sp_spmm_info': (ctypes.c_int, [c_op_p, c_int_p, c_double_p, c_int_p]),
     'gpmi_band_last_timing': (ctypes.c_int, [c_op_p, c_double_p, c_double_p, c_double_p]),
 }
 
@@ -536,6 +537,13 @@ class SparseOperator(object):
         check(self.lib.gpmi_sp_spmm(self.h, float(eta), dptr(X2), X2.shape[1], X2.shape[1],
                                     dptr(Y), Y.shape[1]), 'gpmi_sp_spmm')
         return Y[:, 0] if X.ndim == 1 else Y
+
+    def spmm_info(self):
+        """-> dict(windowed, mean_window, max_window) (see gpmi_sp_spmm_info)."""
+        w, mw, xw = ctypes.c_int(), ctypes.c_double(), ctypes.c_int()
+        check(self.lib.gpmi_sp_spmm_info(self.h, ctypes.byref(w), ctypes.byref(mw),
+                                         ctypes.byref(xw)), 'gpmi_sp_spmm_info')
+        return dict(windowed=bool(w.value), mean_window=mw.value, max_window=xw.value)
 
     def lanczos(self, nprobe, steps, seed=0, probe_offset=0):
         """-> alpha[nprobe, steps], beta[nprobe, steps] (beta = 0 ends a tridiagonal)."""

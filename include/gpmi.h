@@ -187,6 +187,10 @@ int gpmi_sp_cg(gpmi_sp* sp, double eta, const double* rhs, int64_t ld, int nrhs,
 int gpmi_sp_msgram(gpmi_sp* sp, const double* etas, int neta, const double* rhs, int64_t ld,
                    int nrhs, double rtol, int maxiter, double* G, int* iterations);
 
+/* The SpMM kernel this operator uses (1: X-window staged in LDS, 64-row blocks;
+ * 0: gathers from X, one wave per row) and its window sizes (columns per block:
+ * mean, max). */
+int gpmi_sp_spmm_info(gpmi_sp* sp, int* windowed, double* mean_window, int* max_window);
 /* Whether the last gpmi_sp_cg / gpmi_sp_msgram met rtol in every column before
  * maxiter (1) or stopped at maxiter (0). scipy's cg, which the reference calls
  * (_linear_solver.py:64,68), returns the unconverged iterate silently; the

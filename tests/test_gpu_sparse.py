@@ -76,6 +76,44 @@ def test_spmm_and_cg(gp):
     numpy.testing.assert_allclose(Y, scipy.sparse.linalg.spsolve(A, X), rtol=1e-8, atol=1e-9)
 
 
+def test_window_spmm_equals_gather_spmm(gp, monkeypatch):
+    """The X-window SpMM (64-row blocks, window rows staged in LDS; the default
+    where its blocks fit 32 KB of LDS, e.g. 2D tapered Matern) against the
+    one-wave-per-row gather kernel and scipy, for s = 1 .. 32
+    columns, on a matrix whose first blocks overflow the window limits (more
+    than 4096 nonzeros, more than 1024 distinct columns) and so take the
+    gather path inside the same launch."""
+    from gaussian_proc import _hip
+    rng = numpy.random.RandomState(4)
+    n = 3000
+    rows, cols = [], []
+    for i in range(n):
+        if i < 64:
+            k = 100                                  # 6400 nonzeros in block 0
+            c = rng.choice(n, k, replace=False)
+        elif i < 128:
+            c = rng.choice(n, 40, replace=False)     # ~2000 distinct columns in block 1
+        else:
+            c = numpy.clip(i + rng.randint(-30, 31, 12), 0, n - 1)
+        rows.extend([i] * len(c))
+        cols.extend(c)
+    A = scipy.sparse.csr_matrix((rng.randn(len(rows)), (rows, cols)), shape=(n, n))
+    A = (A + A.T).tocsr()
+    A.sum_duplicates()
+    A.sort_indices()
+    sop = _hip.SparseOperator.from_csr(A)
+    for s in (1, 7, 8, 11, 20, 32):
+        X = rng.randn(n, s)
+        monkeypatch.setenv('GPMI_SPMM_WINDOW', '2')
+        Yw = sop.spmm(0.3, X)
+        monkeypatch.setenv('GPMI_SPMM_WINDOW', '0')
+        Yg = sop.spmm(0.3, X)
+        monkeypatch.delenv('GPMI_SPMM_WINDOW')
+        ref = A @ X + 0.3 * X
+        assert _nrel(Yw, ref) < 1e-13, s
+        assert _nrel(Yw, Yg) < 1e-13, s
+
+
 def _nrel(a, b):
     return float(numpy.max(numpy.abs(a - b)) / numpy.max(numpy.abs(b)))
 
