@@ -398,8 +398,10 @@ __global__ __launch_bounds__(HH_THREADS) void hh_panel_kernel(double* __restrict
       rn[u] = 0.0;
       if (q < G) {
         const uint32_t roff = slot_off + (uint32_t)(q * HH_PART_LD * 8);
-        rv[u] = __builtin_bit_cast(
-            d2, __builtin_amdgcn_raw_buffer_load_b128(prs, roff + 16 * lane, 0, 16));
+        // only the columns right of c enter the update: lanes left of it skip the load
+        if (2 * lane + 1 > c)
+          rv[u] = __builtin_bit_cast(
+              d2, __builtin_amdgcn_raw_buffer_load_b128(prs, roff + 16 * lane, 0, 16));
         if (lane == 0) rn[u] = ld_sc1(part + (roff >> 3) + 128);
       }
     }

@@ -37,3 +37,11 @@ if grid == 128:
     cfg = json.load(open(os.path.join(REPO, 'tests', 'golden', 'cfg3_big.json')))
     ld3, _ = op.loglik_terms(cfg['etas'], X, z)
     print('cfg3 logdet rel err', numpy.abs(ld3 - cfg['logdet']) / numpy.abs(cfg['logdet']))
+# the reduction alone vs with Q^T [X z] applied alongside (bench band_mode's form)
+for rhs in (False, True, False, True):
+    if rhs:
+        op.refresh_band(X, z)
+    else:
+        op.refresh_band()
+    print('refresh%s: reduce %.1f ms' % (' with Q^T[X z]' if rhs else '', b.last_timing()['reduce_ms']),
+          flush=True)
