@@ -125,8 +125,9 @@ struct gpmi_band {
   // covers the positions, else (and after a timed-out hand-off) the launch form
   unsigned long long* cmsg = nullptr;  // reflector, column slots [2][K + 1][2][2 CHASE_MSG], err
   int chase_maxg = 0;
+  int split_maxg = 0;        // the same for chase_split_kernel (2K workgroups)
   unsigned chase_spin = 1u << 24;
-  int chase_systolic = 0;    // the last eigenvalues() took the systolic form
+  int chase_systolic = 0;    // the last eigenvalues(): 2 split, 1 one-per-position, 0 launches
   int chase_fallbacks = 0;   // systolic attempts that timed out and reran the launch form
 };
 
@@ -159,20 +160,27 @@ int band_free(gpmi_band* b) {
 
 // The systolic chase (one launch): d, e2 of the tridiagonal. Returns 0 when done,
 // 1 when the positions cannot all be co-resident, 2 after a timed-out hand-off.
-int chase_systolic_run(gpmi_band* b, hipStream_t s, double* d, double* e2) {
+int chase_systolic_run(gpmi_band* b, hipStream_t s, double* d, double* e2, bool split) {
   const int n = (int)b->n;
   const int K = (n - 1 + TS - 1) / TS;
-  if (K > b->chase_maxg) return 1;
+  if (split ? 2 * K > b->split_maxg : K > b->chase_maxg) return 1;
   // per message slot: CHASE_MSG values as two tagged 8-byte granules each
+  // four message kinds (the one-per-position kernel uses two) x (K + 1) positions
   const size_t slots = (size_t)(K + 1) * 2 * 2 * CHASE_MSG;
   if (!b->cmsg) {
-    BD_TRY(hipMalloc(&b->cmsg, sizeof(unsigned long long) * 2 * slots + 64 + 8192));
+    BD_TRY(hipMalloc(&b->cmsg, sizeof(unsigned long long) * 4 * slots + 64 + 8192));
   }
-  int* err = reinterpret_cast<int*>(b->cmsg + 2 * slots);
-  BD_TRY(hipMemsetAsync(b->cmsg, 0, sizeof(unsigned long long) * 2 * slots + 64 + 8192, s));
-  hipLaunchKernelGGL(chase_systolic_kernel, dim3(K), dim3(CHASE_THREADS), 0, s, b->Ab,
-                     (int64_t)b->n_pad, n, b->cmsg, b->cmsg + slots, err, b->chase_spin, d, e2);
-  BD_LAUNCH("chase_systolic_kernel");
+  int* err = reinterpret_cast<int*>(b->cmsg + 4 * slots);
+  BD_TRY(hipMemsetAsync(b->cmsg, 0, sizeof(unsigned long long) * 4 * slots + 64 + 8192, s));
+  if (split) {
+    hipLaunchKernelGGL(chase_split_kernel, dim3(2 * K), dim3(CHASE_THREADS), 0, s, b->Ab,
+                       (int64_t)b->n_pad, n, b->cmsg, K, err, b->chase_spin, d, e2);
+    BD_LAUNCH("chase_split_kernel");
+  } else {
+    hipLaunchKernelGGL(chase_systolic_kernel, dim3(K), dim3(CHASE_THREADS), 0, s, b->Ab,
+                       (int64_t)b->n_pad, n, b->cmsg, b->cmsg + slots, err, b->chase_spin, d, e2);
+    BD_LAUNCH("chase_systolic_kernel");
+  }
   int herr = 0;
   BD_TRY(hipMemcpyAsync(&herr, err, sizeof(int), hipMemcpyDeviceToHost, s));
   BD_TRY(hipStreamSynchronize(s));
@@ -490,6 +498,11 @@ int gpmi_band_create(gpmi_op* op, gpmi_band** out) {
         hipSuccess)
       return fail(e, "chase occupancy");
     b->chase_maxg = std::max(0, per_cu) * b->ncu;
+    if ((e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+             &per_cu, reinterpret_cast<const void*>(&chase_split_kernel), CHASE_THREADS, 0)) !=
+        hipSuccess)
+      return fail(e, "chase split occupancy");
+    b->split_maxg = std::max(0, per_cu) * b->ncu;
   }
   // test hook: GPMI_CHASE_SPIN_LIMIT=0 times the systolic chase out at its first wait
   if (const char* sl = std::getenv("GPMI_CHASE_SPIN_LIMIT"))
@@ -681,17 +694,31 @@ int gpmi_band_eigenvalues(gpmi_band* b, double* lam) {
   BD_TRY(hipEventRecord(b->ev0, s));
   // GPMI_CHASE_MODE: systolic (default; one launch), split (reflector + per-block
   // launches per wavefront t = 3 s + k), task (one workgroup per task per wavefront)
+  // GPMI_CHASE_MODE: unset = the systolic chase with a D and an E workgroup per
+  // position if its 2K workgroups fit, else one workgroup per position (K), else the
+  // launch form; "systolic" = one workgroup per position; "split" / "task" = the
+  // launch forms
   const char* mode_env = std::getenv("GPMI_CHASE_MODE");
   const int chase_mode = !mode_env ? 0 : std::strcmp(mode_env, "split") == 0 ? 1
-                                     : std::strcmp(mode_env, "task") == 0    ? 2 : 0;
+                                     : std::strcmp(mode_env, "task") == 0    ? 2
+                                     : std::strcmp(mode_env, "systolic") == 0 ? 3 : 0;
   bool done = false;
   b->chase_systolic = 0;
-  if (chase_mode == 0 && n > 2) {
-    const int rc = chase_systolic_run(b, s, d, e2);
-    if (rc < 0) return rc;
-    if (rc == 2) ++b->chase_fallbacks;
+  if ((chase_mode == 0 || chase_mode == 3) && n > 2) {
+    int rc = 1;
+    if (chase_mode == 0) {
+      rc = chase_systolic_run(b, s, d, e2, true);
+      if (rc < 0) return rc;
+      if (rc == 2) ++b->chase_fallbacks;
+      if (rc == 0) b->chase_systolic = 2;
+    }
+    if (rc != 0) {
+      rc = chase_systolic_run(b, s, d, e2, false);
+      if (rc < 0) return rc;
+      if (rc == 2) ++b->chase_fallbacks;
+      if (rc == 0) b->chase_systolic = 1;
+    }
     done = rc == 0;
-    b->chase_systolic = done;
   }
   if (!done) {
   if (!b->Ac) BD_TRY(hipMalloc(&b->Ac, sizeof(double) * np * np));

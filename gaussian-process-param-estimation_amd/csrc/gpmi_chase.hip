@@ -963,6 +963,318 @@ __global__ __launch_bounds__(SCT) void chase_systolic_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// Split systolic chase (default where 2K workgroups fit): every chase position
+// has a D workgroup (D_k) and an E workgroup (E_k), so each sweep's products
+// pass (D v, E v) runs on two CUs at once and the per-sweep loop
+// E(k) -> D(k+1) / E(k+1) -> E(k) carries one block's products per hop instead
+// of two. Messages (tagged granules, slots by sweep parity):
+//   R[k]    reflector (s, k) + tau: from E(k-1), for k = 0 from D(0); read by E(k), D(k)
+//   Dcol[k] D(k)'s first column after H D H: read by E(k-1) (its new last column)
+//           and D(k-1) (entry 0: its new diagonal entry)
+//   Erow[k] E(k)'s first row after both updates (physical order): read by D(k)
+//   E00[k]  E(k)[0][0] = beta': read by E(k-1), for k = 0 by D(0) (the last entry
+//           of the next sweep's column)
+// (host prototype of the protocol: tools/chase_systolic_proto.py, chase_split)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(SCT) void chase_split_kernel(
+    const double* __restrict__ Ab, int64_t lda, int n, unsigned long long* __restrict__ msg,
+    int K, int* __restrict__ err, unsigned spin_limit, double* __restrict__ dout,
+    double* __restrict__ e2out) {
+  __shared__ double sv[CB], sv2[CB], sp[CB], sx[CB], serow[CB], snew[CB + 1];
+  __shared__ double xk0[CB];
+  __shared__ double cpart[SNW][CB];
+  __shared__ double red[SNW], redp[SNW], rednb[SNW];
+  __shared__ double sscal[4];
+  __shared__ int s_bail;
+  constexpr int M = CB - 1;
+  constexpr size_t SLOTS = 2 * (size_t)(2 * CMSG);   // per position: 2 parities x granules
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int c0 = 2 * lane;
+  const bool isD = blockIdx.x >= (unsigned)K;
+  const int k = isD ? (int)blockIdx.x - K : (int)blockIdx.x;
+  unsigned long long* mR = msg;                                  // [K + 1] positions
+  unsigned long long* mDcol = mR + (size_t)(K + 1) * SLOTS;
+  unsigned long long* mErow = mDcol + (size_t)(K + 1) * SLOTS;
+  unsigned long long* mE00 = mErow + (size_t)(K + 1) * SLOTS;
+  auto slot = [&](unsigned long long* base, int pos, int s) {
+    return base + (size_t)pos * SLOTS + (size_t)(s & 1) * (2 * CMSG);
+  };
+  const int rb = 1 + k * CB;
+  const int s_end = min(n - 3, n - 2 - k * CB);
+  d2 Bk[SRW];   // this workgroup's block: D_k or E_k
+#pragma unroll
+  for (int u = 0; u < SRW; ++u) {
+    const int i = SNW * u + w;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int r = rb + i, c = rb + c0 + j;
+      if (isD) {
+        Bk[u][j] = (r < n && c < n) ? Ab[(int64_t)max(r, c) * lda + min(r, c)] : 0.0;
+      } else {
+        const int re = r + CB;
+        Bk[u][j] = (re < n && c < n && re - c <= CB) ? Ab[(int64_t)re * lda + c] : 0.0;
+      }
+    }
+  }
+  if (tid == 0) s_bail = 0;
+  if (isD && k == 0) {
+    if (tid < CB) xk0[tid] = (1 + tid < n) ? Ab[(int64_t)(1 + tid) * lda] : 0.0;
+    if (tid == 0) dout[0] = Ab[0];
+  }
+  __syncthreads();
+  for (int s = 0; s <= s_end; ++s) {
+    const int off = s & M;
+    const int uo = off / SNW, wo = off % SNW, lo = off >> 1, jo = off & 1;
+    const bool nxt = s + 1 + (k + 1) * CB < n;
+    const unsigned tag = (unsigned)(s + 1);
+    // ---- 1. the reflector of task (s, k) into sv, tau into sscal[0]
+    if (isD && k == 0) {
+      const double xi = (tid < CB) ? xk0[tid] : 0.0;
+      const double x0 = xk0[0];
+      const double nb2 = block_sum_n((tid > 0 && tid < CB) ? xi * xi : 0.0, red);
+      double tau0, beta0, sc0;
+      chase_dlarfg(x0, nb2, tau0, beta0, sc0);
+      const double vi = (tid == 0) ? 1.0 : xi * sc0;
+      if (tid < CB) {
+        sv[(tid + off) & M] = vi;
+        put_granules(slot(mR, 0, s) + 2 * tid, vi, tag);
+      } else if (tid == CB) {
+        put_granules(slot(mR, 0, s) + 2 * CB, tau0, tag);
+        sscal[0] = tau0;
+      }
+      if (tid == 0) e2out[s] = beta0 * beta0;
+    } else {
+      if (tid <= CB) {
+        double v = 0.0;
+        if (!get_granules(slot(mR, k, s) + 2 * tid, tag, err, spin_limit, v)) s_bail = 1;
+        if (tid < CB) sv[(tid + off) & M] = v;
+        else sscal[0] = v;
+      }
+    }
+    __syncthreads();
+    if (s_bail) return;
+    const double tau = sscal[0];
+    const double vc0 = sv[c0], vc1 = sv[c0 + 1];
+    // ---- 2. row sums B v (one block) and, for D, v.(D v) per wave
+    constexpr int NH = SRW / 8;
+    double qrow[NH];
+    {
+      double vpw = 0.0;
+#pragma unroll
+      for (int h = 0; h < NH; ++h) {
+        double rowv[8];
+#pragma unroll
+        for (int uu = 0; uu < 8; ++uu)
+          rowv[uu] = Bk[8 * h + uu][0] * vc0 + Bk[8 * h + uu][1] * vc1;
+        qrow[h] = butterfly8_valu(rowv);
+        const int rr = SNW * (8 * h + ((lane >> 3) & 7)) + w;
+        if ((lane & 7) == 0) {
+          vpw += qrow[h] * sv[rr];
+          sp[rr] = qrow[h];
+        }
+      }
+      if (isD) {
+        vpw = group_lead_sum(vpw);
+        if (lane == 0) redp[w] = vpw;
+      }
+    }
+    if (!isD && lane == lo) {   // E's updated first column x' and its sum of squares
+      double part = 0.0;
+      if (jo) {
+#pragma unroll
+        for (int u = 0; u < SRW; ++u) {
+          const double x = Bk[u][1] - (tau * readlane_dbl(qrow[u >> 3], 8 * (u & 7))) * vc1;
+          sx[SNW * u + w] = x;
+          part += x * x;
+        }
+      } else {
+#pragma unroll
+        for (int u = 0; u < SRW; ++u) {
+          const double x = Bk[u][0] - (tau * readlane_dbl(qrow[u >> 3], 8 * (u & 7))) * vc0;
+          sx[SNW * u + w] = x;
+          part += x * x;
+        }
+      }
+      rednb[w] = part;
+    }
+    if (isD && lane == lo) {    // D's first column before the update
+#pragma unroll
+      for (int u = 0; u < SRW; ++u) sx[SNW * u + w] = jo ? Bk[u][1] : Bk[u][0];
+    }
+    __syncthreads();
+    if (isD) {
+      // ---- 3D. post D's first column after H D H; position 0 keeps it
+      const double hvp = 0.5 * tau * (tau * wave_sum_n(redp));
+      auto dcol = [&](int r) {
+        if (tau == 0.0) return sx[r];
+        const double vr = sv[r], wr = chase_w(tau, sp[r], hvp, vr);
+        const double wo_ = chase_w(tau, sp[off], hvp, sv[off]);
+        return chase_dsub(sx[r], vr, wo_, wr, sv[off]);
+      };
+      if (k >= 1) {
+        if (tid < CB) put_granules(slot(mDcol, k, s) + 2 * tid, dcol((tid + off) & M), tag);
+      } else if (tid < CB) {
+        const double dv = dcol(tid);
+        if (tid == off) dout[s + 1] = dv;
+        else xk0[(tid - off - 1) & M] = dv;
+        if (s == n - 3 && tid == ((off + 1) & M)) {
+          e2out[n - 2] = dv * dv;
+          e2out[n - 1] = 0.0;
+        }
+      }
+      // ---- 4D. D <- H D H
+      if (tau != 0.0) {
+        const double wc0 = chase_w(tau, sp[c0], hvp, vc0), wc1 = chase_w(tau, sp[c0 + 1], hvp, vc1);
+#pragma unroll
+        for (int u = 0; u < SRW; ++u) {
+          const int r = SNW * u + w;
+          const double vr = sv[r], wr = chase_w(tau, sp[r], hvp, vr);
+          Bk[u][0] = chase_dsub(Bk[u][0], vr, wc0, wr, vc0);
+          Bk[u][1] = chase_dsub(Bk[u][1], vr, wc1, wr, vc1);
+        }
+      }
+      if (k == 0 && s == n - 3) {
+        const int o1 = (off + 1) & M;
+        if (w == (o1 % SNW) && lane == (o1 >> 1)) {
+#pragma unroll
+          for (int u = 0; u < SRW; ++u)
+            if (u == o1 / SNW) dout[n - 1] = (o1 & 1) ? Bk[u][1] : Bk[u][0];
+        }
+      }
+      // ---- 5D. slide: E(k)'s first row (and for position 0 the next column's
+      //      last entry), D(k+1)'s diagonal entry
+      if (tid < CB) {
+        double v = 0.0;
+        if (!get_granules(slot(mErow, k, s) + 2 * tid, tag, err, spin_limit, v)) s_bail = 1;
+        serow[tid] = v;
+      } else if (tid == CB) {
+        double v = 0.0;
+        if (nxt && !get_granules(slot(mDcol, k + 1, s), tag, err, spin_limit, v)) s_bail = 1;
+        sscal[3] = v;
+      } else if (tid == CB + 1 && k == 0) {
+        double v = 0.0;
+        if (!get_granules(slot(mE00, 0, s), tag, err, spin_limit, v)) s_bail = 1;
+        xk0[M] = v;
+      }
+      __syncthreads();
+      if (s_bail) return;
+      const double d00 = sscal[3];
+      if (lane == lo) {
+#pragma unroll
+        for (int u = 0; u < SRW; ++u) {
+          const int r = SNW * u + w;
+          if (r != off) {
+            if (jo) Bk[u][1] = serow[r];
+            else Bk[u][0] = serow[r];
+          }
+        }
+      }
+      if (w == wo) {
+#pragma unroll
+        for (int u = 0; u < SRW; ++u)
+          if (u == uo) {
+            Bk[u][0] = (c0 == off) ? d00 : serow[c0];
+            Bk[u][1] = (c0 + 1 == off) ? d00 : serow[c0 + 1];
+          }
+      }
+    } else {
+      // ---- 3E. the reflector of task (s, k + 1): post it and beta' (E00)
+      double taun = 0.0, betan = 0.0, scn = 0.0;
+      if (nxt) {
+        const double x0 = sx[off];
+        chase_dlarfg(x0, fmax(wave_sum_n(rednb) - x0 * x0, 0.0), taun, betan, scn);
+        if (tid < CB) {
+          sv2[tid] = (tid == off) ? 1.0 : sx[tid] * scn;
+          put_granules(slot(mR, k + 1, s) + 2 * tid,
+                       (tid == 0) ? 1.0 : sx[(tid + off) & M] * scn, tag);
+        } else if (tid == CB) {
+          put_granules(slot(mR, k + 1, s) + 2 * CB, taun, tag);
+        }
+      }
+      if (tid == 256) put_granules(slot(mE00, k, s), nxt ? betan : 0.0, tag);
+      // ---- 4E. E <- E H, then E <- H' E (column off -> (beta', 0 ...))
+      if (tau != 0.0) {
+#pragma unroll
+        for (int u = 0; u < SRW; ++u) {
+          const double qr = tau * readlane_dbl(qrow[u >> 3], 8 * (u & 7));
+          Bk[u][0] = Bk[u][0] - qr * vc0;
+          Bk[u][1] = Bk[u][1] - qr * vc1;
+        }
+      }
+      __syncthreads();   // sv2
+      if (nxt && taun != 0.0) {
+        double cp0 = 0.0, cp1 = 0.0;
+#pragma unroll
+        for (int u = 0; u < SRW; ++u) {
+          const double vr = sv2[SNW * u + w];
+          cp0 += Bk[u][0] * vr;
+          cp1 += Bk[u][1] * vr;
+        }
+        cpart[w][c0] = cp0;
+        cpart[w][c0 + 1] = cp1;
+        __syncthreads();
+        double r0s = 0.0, r1s = 0.0;
+#pragma unroll
+        for (int q = 0; q < SNW; ++q) {
+          r0s += cpart[q][c0];
+          r1s += cpart[q][c0 + 1];
+        }
+        r0s *= taun;
+        r1s *= taun;
+#pragma unroll
+        for (int u = 0; u < SRW; ++u) {
+          const int r = SNW * u + w;
+          const double vr = sv2[r];
+          Bk[u][0] = (c0 == off) ? (r == off ? betan : 0.0) : Bk[u][0] - vr * r0s;
+          Bk[u][1] = (c0 + 1 == off) ? (r == off ? betan : 0.0) : Bk[u][1] - vr * r1s;
+        }
+      }
+      // ---- 5E. post the first row (physical order) to D(k); slide with D(k+1)'s
+      //      first column and E(k+1)'s beta'
+      if (w == wo) {
+#pragma unroll
+        for (int u = 0; u < SRW; ++u)
+          if (u == uo) {
+            put_granules(slot(mErow, k, s) + 2 * c0, Bk[u][0], tag);
+            put_granules(slot(mErow, k, s) + 2 * (c0 + 1), Bk[u][1], tag);
+          }
+      }
+      if (tid <= CB) {
+        double v = 0.0;
+        if (nxt) {
+          unsigned long long* src = tid < CB ? slot(mDcol, k + 1, s) + 2 * tid
+                                             : slot(mE00, k + 1, s);
+          if (!get_granules(src, tag, err, spin_limit, v)) s_bail = 1;
+        }
+        if (tid < CB) snew[tid] = v;
+        else sscal[3] = v;
+      }
+      __syncthreads();
+      if (s_bail) return;
+      const double ne00 = sscal[3];
+      if (lane == lo) {
+#pragma unroll
+        for (int u = 0; u < SRW; ++u) {
+          const int r = SNW * u + w;
+          if (r != off) {
+            if (jo) Bk[u][1] = snew[((r - off - 1) & M) + 1];
+            else Bk[u][0] = snew[((r - off - 1) & M) + 1];
+          }
+        }
+      }
+      if (w == wo) {
+#pragma unroll
+        for (int u = 0; u < SRW; ++u)
+          if (u == uo) {
+            Bk[u][0] = (c0 == off) ? ne00 : 0.0;
+            Bk[u][1] = (c0 + 1 == off) ? ne00 : 0.0;
+          }
+      }
+    }
+  }
+}
+
 // Copy of the band for the chase: B's lower band (0 <= i - j <= 128) of the
 // reduced matrix, zero for 128 < i - j <= 2 * 128 + 1 (the bulge envelope; the
 // reduced matrix keeps Householder vectors there). Row i per workgroup.

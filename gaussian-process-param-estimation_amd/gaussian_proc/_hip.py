@@ -405,12 +405,12 @@ class Band(object):
         return dict(panel_fallbacks=fb.value, panel_maxg=mg.value)
 
     def chase_info(self):
-        """-> dict(systolic, fallbacks, maxg) of the last eigenvalues() (see
-        gpmi_band_chase_info)."""
+        """-> dict(systolic (2 split, 1 one-per-position, 0 launches), fallbacks,
+        maxg) of the last eigenvalues() (see gpmi_band_chase_info)."""
         sy, fb, mg = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
         check(self.lib.gpmi_band_chase_info(self.h, ctypes.byref(sy), ctypes.byref(fb),
                                             ctypes.byref(mg)), 'gpmi_band_chase_info')
-        return dict(systolic=bool(sy.value), fallbacks=fb.value, maxg=mg.value)
+        return dict(systolic=sy.value, fallbacks=fb.value, maxg=mg.value)
 
     def der_ms(self):
         v = ctypes.c_double()

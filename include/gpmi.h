@@ -259,9 +259,11 @@ int gpmi_band_der_terms(gpmi_band* b, const double* etas, int neta, double* logd
  * the largest panel grid (workgroups) run as one launch on this device
  * (CU count x resident hh_panel workgroups per CU, at most 128). */
 int gpmi_band_stats(gpmi_band* b, int* panel_fallbacks, int* panel_maxg);
-/* Which form the last gpmi_band_eigenvalues took (1: the one-launch systolic
- * chase, 0: the per-wavefront launches), how many systolic attempts timed out and
- * were redone by launches, and how many positions can be co-resident. */
+/* Which form the last gpmi_band_eigenvalues took (2: the one-launch systolic chase
+ * with a D and an E workgroup per position, 1: one workgroup per position, 0: the
+ * per-wavefront launches), how many systolic attempts timed out and were redone by
+ * another form, and how many workgroups of the one-per-position form can be
+ * co-resident. */
 int gpmi_band_chase_info(gpmi_band* b, int* systolic, int* fallbacks, int* maxg);
 
 /* Device ms of the last gpmi_band_der_terms call (HIP events). */

@@ -153,19 +153,25 @@ def test_eigenvalues_vs_numpy(gp, n):
 
 @pytest.mark.parametrize('n', [3, 130, 1000, 2177])
 def test_systolic_chase_matches_launch_form(gp, n, monkeypatch):
-    """The one-launch systolic chase (default) and the per-wavefront launch form
+    """The one-launch systolic chase (default: a D and an E workgroup per chase
+    position; also one workgroup per position) and the per-wavefront launch form
     give the same tridiagonal up to rounding (sums in another order): the
-    spectra agree to 1e-13 ||K|| and both match numpy to 1e-12 ||K||."""
+    spectra agree to 1e-13 ||K|| and match numpy to 1e-12 ||K||."""
     K, _, _ = _inputs(n, n + 3)
     op = _mc(K)
     lam = op.eigenvalues()
     info = op.band().chase_info()
-    assert info['systolic'] and info['fallbacks'] == 0, info
-    monkeypatch.setenv('GPMI_CHASE_MODE', 'split')
+    assert info['systolic'] == 2 and info['fallbacks'] == 0, info   # D / E workgroups
+    monkeypatch.setenv('GPMI_CHASE_MODE', 'systolic')                # one per position
+    b1 = _mc(K).band()
+    lam_1 = b1.eigenvalues()
+    assert b1.chase_info()['systolic'] == 1
+    monkeypatch.setenv('GPMI_CHASE_MODE', 'split')                   # launch form
     lam_s = _mc(K).band().eigenvalues()
     ref = numpy.linalg.eigvalsh(K)
     scale = numpy.abs(ref).max()
     assert numpy.max(numpy.abs(lam - lam_s)) <= 1e-13 * scale
+    assert numpy.max(numpy.abs(lam_1 - lam_s)) <= 1e-13 * scale
     assert numpy.max(numpy.abs(lam - ref)) <= 1e-12 * scale
 
 
@@ -191,7 +197,7 @@ def test_systolic_chase_timeout_falls_back(gp, monkeypatch):
     op = _mc(K)
     lam = op.eigenvalues()
     info = op.band().chase_info()
-    assert not info['systolic'] and info['fallbacks'] == 1, info
+    assert info['systolic'] == 0 and info['fallbacks'] == 2, info   # split, then one per position
     ref = numpy.linalg.eigvalsh(K)
     assert numpy.max(numpy.abs(lam - ref)) <= 1e-12 * numpy.abs(ref).max()
 
