@@ -992,6 +992,15 @@ __global__ __launch_bounds__(SCT) void chase_split_kernel(
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int c0 = 2 * lane;
   const bool isD = blockIdx.x >= (unsigned)K;
+#ifdef GPMI_CHASE_PROF
+  // positions 2 and 3, both roles: rows q = 2 (k - 2) + isD of the stamp table
+#define SPLIT_STAMP(p)                                                                   \
+  if (tid == 0 && (k == 2 || k == 3) && s >= 1000 && s < 1016)                          \
+    reinterpret_cast<long long*>(err + 16)[((2 * (k - 2) + (isD ? 1 : 0)) * 16 + (s - 1000)) * 8 + \
+                                          (p)] = wall_clock64();
+#else
+#define SPLIT_STAMP(p)
+#endif
   const int k = isD ? (int)blockIdx.x - K : (int)blockIdx.x;
   unsigned long long* mR = msg;                                  // [K + 1] positions
   unsigned long long* mDcol = mR + (size_t)(K + 1) * SLOTS;
@@ -1028,6 +1037,7 @@ __global__ __launch_bounds__(SCT) void chase_split_kernel(
     const int uo = off / SNW, wo = off % SNW, lo = off >> 1, jo = off & 1;
     const bool nxt = s + 1 + (k + 1) * CB < n;
     const unsigned tag = (unsigned)(s + 1);
+    SPLIT_STAMP(0)
     // ---- 1. the reflector of task (s, k) into sv, tau into sscal[0]
     if (isD && k == 0) {
       const double xi = (tid < CB) ? xk0[tid] : 0.0;
@@ -1054,6 +1064,7 @@ __global__ __launch_bounds__(SCT) void chase_split_kernel(
     }
     __syncthreads();
     if (s_bail) return;
+    SPLIT_STAMP(1)
     const double tau = sscal[0];
     const double vc0 = sv[c0], vc1 = sv[c0 + 1];
     // ---- 2. row sums B v (one block) and, for D, v.(D v) per wave
@@ -1103,6 +1114,7 @@ __global__ __launch_bounds__(SCT) void chase_split_kernel(
       for (int u = 0; u < SRW; ++u) sx[SNW * u + w] = jo ? Bk[u][1] : Bk[u][0];
     }
     __syncthreads();
+    SPLIT_STAMP(2)
     if (isD) {
       // ---- 3D. post D's first column after H D H; position 0 keeps it
       const double hvp = 0.5 * tau * (tau * wave_sum_n(redp));
@@ -1123,6 +1135,7 @@ __global__ __launch_bounds__(SCT) void chase_split_kernel(
           e2out[n - 1] = 0.0;
         }
       }
+      SPLIT_STAMP(3)
       // ---- 4D. D <- H D H
       if (tau != 0.0) {
         const double wc0 = chase_w(tau, sp[c0], hvp, vc0), wc1 = chase_w(tau, sp[c0 + 1], hvp, vc1);
@@ -1142,6 +1155,8 @@ __global__ __launch_bounds__(SCT) void chase_split_kernel(
             if (u == o1 / SNW) dout[n - 1] = (o1 & 1) ? Bk[u][1] : Bk[u][0];
         }
       }
+      SPLIT_STAMP(4)
+      SPLIT_STAMP(5)
       // ---- 5D. slide: E(k)'s first row (and for position 0 the next column's
       //      last entry), D(k+1)'s diagonal entry
       if (tid < CB) {
@@ -1159,15 +1174,15 @@ __global__ __launch_bounds__(SCT) void chase_split_kernel(
       }
       __syncthreads();
       if (s_bail) return;
+      SPLIT_STAMP(6)
       const double d00 = sscal[3];
-      if (lane == lo) {
+      if (lane == lo) {   // column off (every row; (off, off) is rewritten below)
+        if (jo) {
 #pragma unroll
-        for (int u = 0; u < SRW; ++u) {
-          const int r = SNW * u + w;
-          if (r != off) {
-            if (jo) Bk[u][1] = serow[r];
-            else Bk[u][0] = serow[r];
-          }
+          for (int u = 0; u < SRW; ++u) Bk[u][1] = serow[SNW * u + w];
+        } else {
+#pragma unroll
+          for (int u = 0; u < SRW; ++u) Bk[u][0] = serow[SNW * u + w];
         }
       }
       if (w == wo) {
@@ -1193,6 +1208,7 @@ __global__ __launch_bounds__(SCT) void chase_split_kernel(
         }
       }
       if (tid == 256) put_granules(slot(mE00, k, s), nxt ? betan : 0.0, tag);
+      SPLIT_STAMP(3)
       // ---- 4E. E <- E H, then E <- H' E (column off -> (beta', 0 ...))
       if (tau != 0.0) {
 #pragma unroll
@@ -1203,6 +1219,7 @@ __global__ __launch_bounds__(SCT) void chase_split_kernel(
         }
       }
       __syncthreads();   // sv2
+      SPLIT_STAMP(4)
       if (nxt && taun != 0.0) {
         double cp0 = 0.0, cp1 = 0.0;
 #pragma unroll
@@ -1228,11 +1245,12 @@ __global__ __launch_bounds__(SCT) void chase_split_kernel(
           const double vr = sv2[r];
           Bk[u][0] = (c0 == off) ? (r == off ? betan : 0.0) : Bk[u][0] - vr * r0s;
           Bk[u][1] = (c0 + 1 == off) ? (r == off ? betan : 0.0) : Bk[u][1] - vr * r1s;
+          if (u == uo && w == wo) {   // row off is final: D(k) may slide
+            put_granules(slot(mErow, k, s) + 2 * c0, Bk[u][0], tag);
+            put_granules(slot(mErow, k, s) + 2 * (c0 + 1), Bk[u][1], tag);
+          }
         }
-      }
-      // ---- 5E. post the first row (physical order) to D(k); slide with D(k+1)'s
-      //      first column and E(k+1)'s beta'
-      if (w == wo) {
+      } else if (w == wo) {
 #pragma unroll
         for (int u = 0; u < SRW; ++u)
           if (u == uo) {
@@ -1240,6 +1258,9 @@ __global__ __launch_bounds__(SCT) void chase_split_kernel(
             put_granules(slot(mErow, k, s) + 2 * (c0 + 1), Bk[u][1], tag);
           }
       }
+      SPLIT_STAMP(5)
+      // ---- 5E. slide with D(k+1)'s first column (stored by physical row: entry
+      //      i >= 1 becomes row (i + off) mod b of column off) and E(k+1)'s beta'
       if (tid <= CB) {
         double v = 0.0;
         if (nxt) {
@@ -1247,20 +1268,21 @@ __global__ __launch_bounds__(SCT) void chase_split_kernel(
                                              : slot(mE00, k + 1, s);
           if (!get_granules(src, tag, err, spin_limit, v)) s_bail = 1;
         }
-        if (tid < CB) snew[tid] = v;
-        else sscal[3] = v;
+        if (tid == CB) sscal[3] = v;
+        else if (tid > 0) snew[(tid + off) & M] = v;
       }
       __syncthreads();
       if (s_bail) return;
+      SPLIT_STAMP(6)
       const double ne00 = sscal[3];
+      // column off (every row; (off, off) is rewritten by the row below), then row off
       if (lane == lo) {
+        if (jo) {
 #pragma unroll
-        for (int u = 0; u < SRW; ++u) {
-          const int r = SNW * u + w;
-          if (r != off) {
-            if (jo) Bk[u][1] = snew[((r - off - 1) & M) + 1];
-            else Bk[u][0] = snew[((r - off - 1) & M) + 1];
-          }
+          for (int u = 0; u < SRW; ++u) Bk[u][1] = snew[SNW * u + w];
+        } else {
+#pragma unroll
+          for (int u = 0; u < SRW; ++u) Bk[u][0] = snew[SNW * u + w];
         }
       }
       if (w == wo) {
