@@ -624,6 +624,9 @@ def der1_sweep(op, X, z, E, rank, torch):
     return {'etas': E, 'wall_ms': round(dt * 1e3, 3), 'device_ms': round(op.band().der_ms(), 3),
             'der1_evals_per_s_per_gpu': round(E / dt, 1),
             'eigenvalues_ms_once': round(eig_ms, 1),
+            'eigenvalues_chase': {2: 'chase_split_kernel (D and E workgroup per position)',
+                                  1: 'chase_systolic_kernel (one workgroup per position)',
+                                  0: 'per-wavefront launches'}[op.band().chase_info()['systolic']],
             'der1_sample': [float(log_etas[0]), float(d1[0])]}
 
 

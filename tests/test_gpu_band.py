@@ -187,6 +187,24 @@ def test_multisection_matches_bisection(gp, monkeypatch):
     assert numpy.max(numpy.abs(lam - lam_b)) <= 8.9e-16 * scale
 
 
+def test_chase_over_split_capacity_uses_one_workgroup_per_position(gp, monkeypatch):
+    """N = 129^2 = 16641 needs 2 x 130 split-chase workgroups, more than 256 CUs
+    hold: the one-workgroup-per-position systolic kernel takes over (no timeout)
+    and agrees with the launch form to 1e-13 max |lambda|."""
+    from oracle import data
+    pts = data.generate_points(129, 2, True)
+    D = gp.generate_correlation(pts, 0.1, 1.5, device_resident=True)
+    b = _mc(D).band()
+    lam = b.eigenvalues()
+    info = b.chase_info()
+    if 2 * 130 <= info['maxg']:
+        pytest.skip('this device holds the split chase at N = 16641')
+    assert info['systolic'] == 1 and info['fallbacks'] == 0, info
+    monkeypatch.setenv('GPMI_CHASE_MODE', 'split')
+    lam_s = _mc(D).band().eigenvalues()
+    assert numpy.max(numpy.abs(lam - lam_s)) <= 1e-13 * numpy.abs(lam_s).max()
+
+
 def test_systolic_chase_timeout_falls_back(gp, monkeypatch):
     """GPMI_CHASE_SPIN_LIMIT=0 makes the first hand-off wait of the systolic
     chase a timeout (as when its workgroups cannot all be resident): every
