@@ -293,17 +293,45 @@ __global__ __launch_bounds__(256) void col_dot_reduce_kernel(const double* __res
 }
 
 // W[i][c] = alpha * W[i][c] - sum_{j<J} A_j[i][c] * H[j][c]   (H on the device)
+// W -= sum_j A_j diag(H_j): two consecutive elements per thread (16-byte loads when
+// the vector stride is even), the J vector loads issued four at a time (the same
+// per-element order of subtraction as one element per thread)
 __global__ __launch_bounds__(256) void col_gs_update_kernel(double* __restrict__ W,
                                                             const double* __restrict__ A,
                                                             int64_t strideA,
                                                             const double* __restrict__ H, int J,
                                                             int64_t n, int s) {
-  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (e >= n * s) return;
-  const int c = (int)(e % s);
-  double w = W[e];
-  for (int j = 0; j < J; ++j) w -= A[j * strideA + e] * H[j * s + c];
-  W[e] = w;
+  const int64_t ns = n * s;
+  const int64_t e = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 2;
+  if (e >= ns) return;
+  if (e + 1 < ns && (strideA & 1) == 0) {
+    const int c0 = (int)(e % s), c1 = (c0 + 1 == s) ? 0 : c0 + 1;
+    d2 w = *reinterpret_cast<const d2*>(W + e);
+    int j = 0;
+    for (; j + 4 <= J; j += 4) {
+      d2 a[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) a[q] = *reinterpret_cast<const d2*>(A + (j + q) * strideA + e);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        w[0] -= a[q][0] * H[(j + q) * s + c0];
+        w[1] -= a[q][1] * H[(j + q) * s + c1];
+      }
+    }
+    for (; j < J; ++j) {
+      const d2 a = *reinterpret_cast<const d2*>(A + j * strideA + e);
+      w[0] -= a[0] * H[j * s + c0];
+      w[1] -= a[1] * H[j * s + c1];
+    }
+    *reinterpret_cast<d2*>(W + e) = w;
+  } else {
+    for (int64_t f = e; f < e + 2 && f < ns; ++f) {
+      const int c = (int)(f % s);
+      double w = W[f];
+      for (int j = 0; j < J; ++j) w -= A[j * strideA + f] * H[j * s + c];
+      W[f] = w;
+    }
+  }
 }
 
 // Y[i][c] = a[c] * X[i][c] + b[c] * Y[i][c]  (per-column coefficients, device)

@@ -313,8 +313,8 @@ int lanczos_block(gpmi_sp* sp, double* V, double* W, int s, int steps, double* h
       double* H = pass == 0 ? H1 : H2;
       rc = col_dots(sp, V, ns, k + 1, W, s, H);
       if (rc) return rc;
-      hipLaunchKernelGGL(col_gs_update_kernel, dim3(grid_ns(sp->n, s)), dim3(256), 0, sp->stream,
-                         W, V, ns, H, k + 1, sp->n, s);
+      hipLaunchKernelGGL(col_gs_update_kernel, dim3((unsigned)((ns + 511) / 512)), dim3(256), 0,
+                         sp->stream, W, V, ns, H, k + 1, sp->n, s);
       SP_LAUNCH("col_gs_update_kernel");
     }
     rc = col_dots(sp, W, 0, 1, W, s, nrm);
