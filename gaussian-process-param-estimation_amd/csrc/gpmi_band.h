@@ -62,6 +62,10 @@ __global__ void band_der_kernel(const double* fac, int nt, double* ysol, double*
 __global__ void chase_copy_kernel(const double* Ab, double* A, int64_t lda, int n);
 constexpr int CHASE_MSG = 136;   // = CMSG (gpmi_chase.hip): values per hand-off slot
 constexpr int CHASE_THREADS = 512;   // = SCT (gpmi_chase.hip): systolic chase workgroup
+#ifndef GPMI_CHASE_SPLIT_THREADS
+#define GPMI_CHASE_SPLIT_THREADS 512
+#endif
+constexpr int CHASE_SPLIT_THREADS = GPMI_CHASE_SPLIT_THREADS;   // split chase workgroup
 __global__ void chase_split_kernel(const double* Ab, int64_t lda, int n, unsigned long long* msg,
                                    int K, int* err, unsigned spin_limit, double* dout,
                                    double* e2out);

@@ -173,7 +173,7 @@ int chase_systolic_run(gpmi_band* b, hipStream_t s, double* d, double* e2, bool 
   int* err = reinterpret_cast<int*>(b->cmsg + 4 * slots);
   BD_TRY(hipMemsetAsync(b->cmsg, 0, sizeof(unsigned long long) * 4 * slots + 64 + 8192, s));
   if (split) {
-    hipLaunchKernelGGL(chase_split_kernel, dim3(2 * K), dim3(CHASE_THREADS), 0, s, b->Ab,
+    hipLaunchKernelGGL(chase_split_kernel, dim3(2 * K), dim3(CHASE_SPLIT_THREADS), 0, s, b->Ab,
                        (int64_t)b->n_pad, n, b->cmsg, K, err, b->chase_spin, d, e2);
     BD_LAUNCH("chase_split_kernel");
   } else {
@@ -499,7 +499,8 @@ int gpmi_band_create(gpmi_op* op, gpmi_band** out) {
       return fail(e, "chase occupancy");
     b->chase_maxg = std::max(0, per_cu) * b->ncu;
     if ((e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-             &per_cu, reinterpret_cast<const void*>(&chase_split_kernel), CHASE_THREADS, 0)) !=
+             &per_cu, reinterpret_cast<const void*>(&chase_split_kernel), CHASE_SPLIT_THREADS,
+             0)) !=
         hipSuccess)
       return fail(e, "chase split occupancy");
     b->split_maxg = std::max(0, per_cu) * b->ncu;

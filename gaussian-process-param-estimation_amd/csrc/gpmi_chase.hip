@@ -977,14 +977,36 @@ __global__ __launch_bounds__(SCT) void chase_systolic_kernel(
 //           of the next sweep's column)
 // (host prototype of the protocol: tools/chase_systolic_proto.py, chase_split)
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(SCT) void chase_split_kernel(
+// fixed-order sums over the NW waves of a workgroup (templated on NW)
+template <int NW>
+__device__ __forceinline__ double wave_sum_t(const double* r) {
+  double a = 0.0;
+#pragma unroll
+  for (int q = 0; q < NW; ++q) a += r[q];
+  return a;
+}
+template <int NW>
+__device__ __forceinline__ double block_sum_t(double v, double* red) {
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  __syncthreads();
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  return wave_sum_t<NW>(red);
+}
+
+template <int T>
+__device__ __forceinline__ void chase_split_body(
     const double* __restrict__ Ab, int64_t lda, int n, unsigned long long* __restrict__ msg,
     int K, int* __restrict__ err, unsigned spin_limit, double* __restrict__ dout,
     double* __restrict__ e2out) {
+  constexpr int NW = T / 64, RW = CB / NW;
+  static_assert(RW % 8 == 0, "row sums go through 8-row butterflies");
   __shared__ double sv[CB], sv2[CB], sp[CB], sx[CB], serow[CB], snew[CB + 1];
   __shared__ double xk0[CB];
-  __shared__ double cpart[SNW][CB];
-  __shared__ double red[SNW], redp[SNW], rednb[SNW];
+  __shared__ double cpart[NW][CB];
+  __shared__ double red[NW], redp[NW], rednb[NW];
   __shared__ double sscal[4];
   __shared__ int s_bail;
   constexpr int M = CB - 1;
@@ -1011,10 +1033,10 @@ __global__ __launch_bounds__(SCT) void chase_split_kernel(
   };
   const int rb = 1 + k * CB;
   const int s_end = min(n - 3, n - 2 - k * CB);
-  d2 Bk[SRW];   // this workgroup's block: D_k or E_k
+  d2 Bk[RW];   // this workgroup's block: D_k or E_k
 #pragma unroll
-  for (int u = 0; u < SRW; ++u) {
-    const int i = SNW * u + w;
+  for (int u = 0; u < RW; ++u) {
+    const int i = NW * u + w;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int r = rb + i, c = rb + c0 + j;
@@ -1034,7 +1056,7 @@ __global__ __launch_bounds__(SCT) void chase_split_kernel(
   __syncthreads();
   for (int s = 0; s <= s_end; ++s) {
     const int off = s & M;
-    const int uo = off / SNW, wo = off % SNW, lo = off >> 1, jo = off & 1;
+    const int uo = off / NW, wo = off % NW, lo = off >> 1, jo = off & 1;
     const bool nxt = s + 1 + (k + 1) * CB < n;
     const unsigned tag = (unsigned)(s + 1);
     SPLIT_STAMP(0)
@@ -1042,7 +1064,7 @@ __global__ __launch_bounds__(SCT) void chase_split_kernel(
     if (isD && k == 0) {
       const double xi = (tid < CB) ? xk0[tid] : 0.0;
       const double x0 = xk0[0];
-      const double nb2 = block_sum_n((tid > 0 && tid < CB) ? xi * xi : 0.0, red);
+      const double nb2 = block_sum_t<NW>((tid > 0 && tid < CB) ? xi * xi : 0.0, red);
       double tau0, beta0, sc0;
       chase_dlarfg(x0, nb2, tau0, beta0, sc0);
       const double vi = (tid == 0) ? 1.0 : xi * sc0;
@@ -1068,7 +1090,7 @@ __global__ __launch_bounds__(SCT) void chase_split_kernel(
     const double tau = sscal[0];
     const double vc0 = sv[c0], vc1 = sv[c0 + 1];
     // ---- 2. row sums B v (one block) and, for D, v.(D v) per wave
-    constexpr int NH = SRW / 8;
+    constexpr int NH = RW / 8;
     double qrow[NH];
     {
       double vpw = 0.0;
@@ -1079,7 +1101,7 @@ __global__ __launch_bounds__(SCT) void chase_split_kernel(
         for (int uu = 0; uu < 8; ++uu)
           rowv[uu] = Bk[8 * h + uu][0] * vc0 + Bk[8 * h + uu][1] * vc1;
         qrow[h] = butterfly8_valu(rowv);
-        const int rr = SNW * (8 * h + ((lane >> 3) & 7)) + w;
+        const int rr = NW * (8 * h + ((lane >> 3) & 7)) + w;
         if ((lane & 7) == 0) {
           vpw += qrow[h] * sv[rr];
           sp[rr] = qrow[h];
@@ -1094,16 +1116,16 @@ __global__ __launch_bounds__(SCT) void chase_split_kernel(
       double part = 0.0;
       if (jo) {
 #pragma unroll
-        for (int u = 0; u < SRW; ++u) {
+        for (int u = 0; u < RW; ++u) {
           const double x = Bk[u][1] - (tau * readlane_dbl(qrow[u >> 3], 8 * (u & 7))) * vc1;
-          sx[SNW * u + w] = x;
+          sx[NW * u + w] = x;
           part += x * x;
         }
       } else {
 #pragma unroll
-        for (int u = 0; u < SRW; ++u) {
+        for (int u = 0; u < RW; ++u) {
           const double x = Bk[u][0] - (tau * readlane_dbl(qrow[u >> 3], 8 * (u & 7))) * vc0;
-          sx[SNW * u + w] = x;
+          sx[NW * u + w] = x;
           part += x * x;
         }
       }
@@ -1111,13 +1133,13 @@ __global__ __launch_bounds__(SCT) void chase_split_kernel(
     }
     if (isD && lane == lo) {    // D's first column before the update
 #pragma unroll
-      for (int u = 0; u < SRW; ++u) sx[SNW * u + w] = jo ? Bk[u][1] : Bk[u][0];
+      for (int u = 0; u < RW; ++u) sx[NW * u + w] = jo ? Bk[u][1] : Bk[u][0];
     }
     __syncthreads();
     SPLIT_STAMP(2)
     if (isD) {
       // ---- 3D. post D's first column after H D H; position 0 keeps it
-      const double hvp = 0.5 * tau * (tau * wave_sum_n(redp));
+      const double hvp = 0.5 * tau * (tau * wave_sum_t<NW>(redp));
       auto dcol = [&](int r) {
         if (tau == 0.0) return sx[r];
         const double vr = sv[r], wr = chase_w(tau, sp[r], hvp, vr);
@@ -1140,8 +1162,8 @@ __global__ __launch_bounds__(SCT) void chase_split_kernel(
       if (tau != 0.0) {
         const double wc0 = chase_w(tau, sp[c0], hvp, vc0), wc1 = chase_w(tau, sp[c0 + 1], hvp, vc1);
 #pragma unroll
-        for (int u = 0; u < SRW; ++u) {
-          const int r = SNW * u + w;
+        for (int u = 0; u < RW; ++u) {
+          const int r = NW * u + w;
           const double vr = sv[r], wr = chase_w(tau, sp[r], hvp, vr);
           Bk[u][0] = chase_dsub(Bk[u][0], vr, wc0, wr, vc0);
           Bk[u][1] = chase_dsub(Bk[u][1], vr, wc1, wr, vc1);
@@ -1149,10 +1171,10 @@ __global__ __launch_bounds__(SCT) void chase_split_kernel(
       }
       if (k == 0 && s == n - 3) {
         const int o1 = (off + 1) & M;
-        if (w == (o1 % SNW) && lane == (o1 >> 1)) {
+        if (w == (o1 % NW) && lane == (o1 >> 1)) {
 #pragma unroll
-          for (int u = 0; u < SRW; ++u)
-            if (u == o1 / SNW) dout[n - 1] = (o1 & 1) ? Bk[u][1] : Bk[u][0];
+          for (int u = 0; u < RW; ++u)
+            if (u == o1 / NW) dout[n - 1] = (o1 & 1) ? Bk[u][1] : Bk[u][0];
         }
       }
       SPLIT_STAMP(4)
@@ -1179,15 +1201,15 @@ __global__ __launch_bounds__(SCT) void chase_split_kernel(
       if (lane == lo) {   // column off (every row; (off, off) is rewritten below)
         if (jo) {
 #pragma unroll
-          for (int u = 0; u < SRW; ++u) Bk[u][1] = serow[SNW * u + w];
+          for (int u = 0; u < RW; ++u) Bk[u][1] = serow[NW * u + w];
         } else {
 #pragma unroll
-          for (int u = 0; u < SRW; ++u) Bk[u][0] = serow[SNW * u + w];
+          for (int u = 0; u < RW; ++u) Bk[u][0] = serow[NW * u + w];
         }
       }
       if (w == wo) {
 #pragma unroll
-        for (int u = 0; u < SRW; ++u)
+        for (int u = 0; u < RW; ++u)
           if (u == uo) {
             Bk[u][0] = (c0 == off) ? d00 : serow[c0];
             Bk[u][1] = (c0 + 1 == off) ? d00 : serow[c0 + 1];
@@ -1198,7 +1220,7 @@ __global__ __launch_bounds__(SCT) void chase_split_kernel(
       double taun = 0.0, betan = 0.0, scn = 0.0;
       if (nxt) {
         const double x0 = sx[off];
-        chase_dlarfg(x0, fmax(wave_sum_n(rednb) - x0 * x0, 0.0), taun, betan, scn);
+        chase_dlarfg(x0, fmax(wave_sum_t<NW>(rednb) - x0 * x0, 0.0), taun, betan, scn);
         if (tid < CB) {
           sv2[tid] = (tid == off) ? 1.0 : sx[tid] * scn;
           put_granules(slot(mR, k + 1, s) + 2 * tid,
@@ -1212,7 +1234,7 @@ __global__ __launch_bounds__(SCT) void chase_split_kernel(
       // ---- 4E. E <- E H, then E <- H' E (column off -> (beta', 0 ...))
       if (tau != 0.0) {
 #pragma unroll
-        for (int u = 0; u < SRW; ++u) {
+        for (int u = 0; u < RW; ++u) {
           const double qr = tau * readlane_dbl(qrow[u >> 3], 8 * (u & 7));
           Bk[u][0] = Bk[u][0] - qr * vc0;
           Bk[u][1] = Bk[u][1] - qr * vc1;
@@ -1223,8 +1245,8 @@ __global__ __launch_bounds__(SCT) void chase_split_kernel(
       if (nxt && taun != 0.0) {
         double cp0 = 0.0, cp1 = 0.0;
 #pragma unroll
-        for (int u = 0; u < SRW; ++u) {
-          const double vr = sv2[SNW * u + w];
+        for (int u = 0; u < RW; ++u) {
+          const double vr = sv2[NW * u + w];
           cp0 += Bk[u][0] * vr;
           cp1 += Bk[u][1] * vr;
         }
@@ -1233,15 +1255,15 @@ __global__ __launch_bounds__(SCT) void chase_split_kernel(
         __syncthreads();
         double r0s = 0.0, r1s = 0.0;
 #pragma unroll
-        for (int q = 0; q < SNW; ++q) {
+        for (int q = 0; q < NW; ++q) {
           r0s += cpart[q][c0];
           r1s += cpart[q][c0 + 1];
         }
         r0s *= taun;
         r1s *= taun;
 #pragma unroll
-        for (int u = 0; u < SRW; ++u) {
-          const int r = SNW * u + w;
+        for (int u = 0; u < RW; ++u) {
+          const int r = NW * u + w;
           const double vr = sv2[r];
           Bk[u][0] = (c0 == off) ? (r == off ? betan : 0.0) : Bk[u][0] - vr * r0s;
           Bk[u][1] = (c0 + 1 == off) ? (r == off ? betan : 0.0) : Bk[u][1] - vr * r1s;
@@ -1252,7 +1274,7 @@ __global__ __launch_bounds__(SCT) void chase_split_kernel(
         }
       } else if (w == wo) {
 #pragma unroll
-        for (int u = 0; u < SRW; ++u)
+        for (int u = 0; u < RW; ++u)
           if (u == uo) {
             put_granules(slot(mErow, k, s) + 2 * c0, Bk[u][0], tag);
             put_granules(slot(mErow, k, s) + 2 * (c0 + 1), Bk[u][1], tag);
@@ -1279,15 +1301,15 @@ __global__ __launch_bounds__(SCT) void chase_split_kernel(
       if (lane == lo) {
         if (jo) {
 #pragma unroll
-          for (int u = 0; u < SRW; ++u) Bk[u][1] = snew[SNW * u + w];
+          for (int u = 0; u < RW; ++u) Bk[u][1] = snew[NW * u + w];
         } else {
 #pragma unroll
-          for (int u = 0; u < SRW; ++u) Bk[u][0] = snew[SNW * u + w];
+          for (int u = 0; u < RW; ++u) Bk[u][0] = snew[NW * u + w];
         }
       }
       if (w == wo) {
 #pragma unroll
-        for (int u = 0; u < SRW; ++u)
+        for (int u = 0; u < RW; ++u)
           if (u == uo) {
             Bk[u][0] = (c0 == off) ? ne00 : 0.0;
             Bk[u][1] = (c0 + 1 == off) ? ne00 : 0.0;
@@ -1295,6 +1317,14 @@ __global__ __launch_bounds__(SCT) void chase_split_kernel(
       }
     }
   }
+}
+
+
+__global__ __launch_bounds__(CHASE_SPLIT_THREADS) void chase_split_kernel(
+    const double* __restrict__ Ab, int64_t lda, int n, unsigned long long* __restrict__ msg,
+    int K, int* __restrict__ err, unsigned spin_limit, double* __restrict__ dout,
+    double* __restrict__ e2out) {
+  chase_split_body<CHASE_SPLIT_THREADS>(Ab, lda, n, msg, K, err, spin_limit, dout, e2out);
 }
 
 // Copy of the band for the chase: B's lower band (0 <= i - j <= 128) of the
