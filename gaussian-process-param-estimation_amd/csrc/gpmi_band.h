@@ -33,7 +33,8 @@ constexpr int BAND_MAX_NPAD = HH_MAXG * HH_ROWS;
 __global__ void hh_col_kernel(double* P, int64_t lda, int m, int c, double* part, double* pivrow,
                               double* tau);
 __global__ void hh_panel_kernel(double* P, int64_t lda, int m, double* part, double* pivrow,
-                                unsigned* counter, double* tau, int* err, unsigned spin_limit);
+                                unsigned* counter, double* tau, int* err, unsigned spin_limit,
+                                const int* guard);
 __global__ void vcopy_kernel(const double* P, int64_t lda, int m, double* U, int64_t ldu);
 __global__ void tn_partial_kernel(const double* P1, int64_t ld1, const double* P2, int64_t ld2,
                                   int m, double* part);
@@ -57,6 +58,19 @@ __global__ void qt_apply_kernel(const double* P, int64_t lda, int m, double* Y, 
 __global__ void band_chol_kernel(const double* B, int64_t lda, int nt, int64_t n, const double* Y,
                                  const double* etas, double* out, int out_ld, int* info,
                                  double* fac, double* ysol);
+__global__ void cq_chol_kernel(const double* G, int pass, double coef, double tau_fo, double* Lout,
+                               double* Linv, int* fo, int* fail, unsigned* ctr);
+__global__ void cq_gram_kernel(const double* Src, int64_t lds, double* part);
+__global__ void cq_reduce_kernel(const double* part, int np, double* G);
+constexpr int CQ_GPK = 36 * 256;   // doubles per packed CholeskyQR Gram partial
+__global__ void cq_apply_kernel(const double* Src, int64_t lds, double* Dst, int64_t ldd,
+                                const double* M, double* part, const int* skip);
+__global__ void cq_recon_kernel(const double* Q2, const double* G3, double tau_fo, double* P,
+                                int64_t lda, double* S, double* tau, double* Lx3, double* Linv3,
+                                double* C, int* fo, int* fail);
+constexpr int CQ_DYN_LDS = 64 * (GPMI_TS + 4) * 8;   // cq_gram / cq_apply dynamic LDS (bytes)
+__global__ void cq_top_kernel(double* Lx, const double* Linv, const int* flags, const double* S,
+                              double* scr, double* Ab, int64_t lda);
 __global__ void band_der_kernel(const double* fac, int nt, double* ysol, double* der);
 
 __global__ void chase_copy_kernel(const double* Ab, double* A, int64_t lda, int n);

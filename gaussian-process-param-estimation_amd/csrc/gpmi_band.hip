@@ -35,130 +35,13 @@
 #include "gpmi_device.h"
 #include "gpmi_lds_chol.h"
 #include "gpmi_band.h"
+#include "gpmi_tile.h"
 
 #ifndef GPMI_BAND_STAMPS
 #define GPMI_BAND_STAMPS 0   // probe builds: phase stamps of band_chol_kernel (printf)
 #endif
 
 namespace gpmi {
-
-// ---------------------------------------------------------------------------
-// Generic 128 x 128 tile product on fp64 MFMA with either operand layout:
-//   KFAST: op(P)[r][k] = P[r * ld + k]   (staged as the swizzled [row][16] slab)
-//   KSLOW: op(P)[r][k] = P[k * ld + r]   (staged as [16][SLD], k-major; the
-//          fragment reads of lanes 0-15 and 16-31 land 32 banks apart)
-// acc (wave tile 64 x 64 at (wr, wc)) (+|-)= op(P1)[0:128, 0:kdim] op(P2)[0:128, 0:kdim]^T.
-// Ends with a workgroup barrier (back-to-back calls may reuse smem).
-// ---------------------------------------------------------------------------
-constexpr int SLD = 144;
-constexpr int GSTAGE = 16 * SLD;   // doubles per staged operand (>= STAGE)
-
-template <int L>
-__device__ __forceinline__ void gl_op(const double* __restrict__ base, int64_t ld, int k0,
-                                      d2 (&r)[4]) {
-  if (L == KFAST) {
-    gload_slab(base, ld, k0, r);
-    return;
-  }
-  const int t = threadIdx.x, kk = t >> 4, c0 = (t & 15) * 8;
-  const double* p = base + (int64_t)(k0 + kk) * ld + c0;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) r[q] = *reinterpret_cast<const d2*>(p + 2 * q);
-}
-
-template <int L>
-__device__ __forceinline__ void st_op(double* s, const d2 (&r)[4]) {
-  if (L == KFAST) {
-    sstore_slab(s, r);
-    return;
-  }
-  const int t = threadIdx.x, kk = t >> 4, c0 = (t & 15) * 8;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) *reinterpret_cast<d2*>(s + kk * SLD + c0 + 2 * q) = r[q];
-}
-
-template <int L>
-__device__ __forceinline__ double fr_op(const double* s, int row, int k) {
-  return L == KFAST ? s[slab_off(row, k)] : s[k * SLD + row];
-}
-
-template <int AL, int BL, bool NEG>
-__device__ __forceinline__ void gemm_tile(const double* __restrict__ P1, int64_t ld1,
-                                          const double* __restrict__ P2, int64_t ld2, int kdim,
-                                          double* smem, d4 (&acc)[4][4]) {
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int wr = w >> 1, wc = w & 1, fr = lane & 15, fk = lane >> 4;
-  double* sA = smem;
-  double* sB = smem + 2 * GSTAGE;
-  d2 ra[4], rb[4];
-  gl_op<AL>(P1, ld1, 0, ra);
-  gl_op<BL>(P2, ld2, 0, rb);
-  st_op<AL>(sA, ra);
-  st_op<BL>(sB, rb);
-  __syncthreads();
-  const int nsteps = kdim / BK;
-  for (int s = 0; s < nsteps; ++s) {
-    const int cur = s & 1;
-    const double* cA = sA + cur * GSTAGE;
-    const double* cB = sB + cur * GSTAGE;
-    if (s + 1 < nsteps) {
-      gl_op<AL>(P1, ld1, (s + 1) * BK, ra);
-      gl_op<BL>(P2, ld2, (s + 1) * BK, rb);
-    }
-#pragma unroll
-    for (int kk = 0; kk < BK / 4; ++kk) {
-      double a[4], b[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) a[i] = fr_op<AL>(cA, wr * 64 + i * 16 + fr, kk * 4 + fk);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) b[j] = fr_op<BL>(cB, wc * 64 + j * 16 + fr, kk * 4 + fk);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[i][j] = NEG ? mfma64_neg(a[i], b[j], acc[i][j]) : mfma64(a[i], b[j], acc[i][j]);
-    }
-    if (s + 1 < nsteps) {
-      st_op<AL>(sA + (cur ^ 1) * GSTAGE, ra);
-      st_op<BL>(sB + (cur ^ 1) * GSTAGE, rb);
-    }
-    __syncthreads();
-  }
-}
-
-__device__ __forceinline__ void zero_tile(d4 (&acc)[4][4]) {
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = d4{0.0, 0.0, 0.0, 0.0};
-}
-
-// C/D map of v_mfma_f64_16x16x4f64: row = (lane>>4) + 4 r, col = lane & 15.
-__device__ __forceinline__ void load_tile(const double* C, int64_t ldc, d4 (&acc)[4][4]) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int wr = w >> 1, wc = w & 1, fr = lane & 15, fk = lane >> 4;
-#pragma unroll
-  for (int a = 0; a < 4; ++a)
-#pragma unroll
-    for (int c = 0; c < 4; ++c)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        acc[a][c][r] = C[(int64_t)(wr * 64 + a * 16 + fk + 4 * r) * ldc + wc * 64 + c * 16 + fr];
-}
-
-__device__ __forceinline__ void store_tile(double* C, int64_t ldc, const d4 (&acc)[4][4],
-                                           double scale) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int wr = w >> 1, wc = w & 1, fr = lane & 15, fk = lane >> 4;
-#pragma unroll
-  for (int a = 0; a < 4; ++a)
-#pragma unroll
-    for (int c = 0; c < 4; ++c)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        C[(int64_t)(wr * 64 + a * 16 + fk + 4 * r) * ldc + wc * 64 + c * 16 + fr] =
-            scale * acc[a][c][r];
-}
 
 // ---------------------------------------------------------------------------
 // Householder QR of the m x 128 panel P (row-major, ld lda), column c.
@@ -303,7 +186,10 @@ __global__ __launch_bounds__(HH_THREADS) void hh_panel_kernel(double* __restrict
                                                               unsigned* __restrict__ counter,
                                                               double* __restrict__ tau,
                                                               int* __restrict__ err,
-                                                              unsigned spin_limit) {
+                                                              unsigned spin_limit,
+                                                              const int* __restrict__ guard) {
+  // guarded form (after a CholeskyQR panel): run only if that panel failed
+  if (guard && !__hip_atomic_load(guard, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
   extern __shared__ double dyn_lds[];   // sized by the host to keep one workgroup per CU
   double(*sacc)[HH_PART_LD] = reinterpret_cast<double(*)[HH_PART_LD]>(dyn_lds);
   __shared__ int s_bail;
@@ -513,7 +399,7 @@ __global__ __launch_bounds__(256) void tbuild_kernel(const double* __restrict__ 
   __shared__ double Ls[TS * DL];
   __shared__ double Aux[TS * RLD];
   __shared__ double stau[TS];
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int t = threadIdx.x;
   if (t < TS) stau[t] = tau[t];
   __syncthreads();
   for (int e = t; e < TS * TS; e += 256) {
@@ -525,32 +411,7 @@ __global__ __launch_bounds__(256) void tbuild_kernel(const double* __restrict__ 
   }
   __syncthreads();
   // inverses of the eight 16 x 16 diagonal blocks (wave w: blocks w and w + 4)
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int j0 = (w + 4 * h) * DB;
-    const int r = lane >> 2, g = lane & 3;
-    double lrow[DB];
-#pragma unroll
-    for (int p = 0; p < DB; ++p) lrow[p] = Ls[(j0 + r) * DL + j0 + p];
-    const double rinv = 1.0 / Ls[(j0 + r) * DL + j0 + r];
-    double s[4] = {0.0, 0.0, 0.0, 0.0}, x[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-    for (int p = 0; p < DB; ++p) {
-      if (r == p) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) x[k] = (((4 * g + k) == p ? 1.0 : 0.0) - s[k]) * rinv;
-      }
-      double xp[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) xp[k] = __shfl(x[k], (p << 2) | g);
-      if (r > p) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) s[k] += lrow[p] * xp[k];
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) Aux[(j0 / DB) * 256 + r * 16 + 4 * g + k] = x[k];
-  }
+  lds_diag_inv_lower(Ls, Aux);
   __syncthreads();
   lds_inv_block(Ls, Aux);
   __syncthreads();

@@ -107,6 +107,25 @@ struct gpmi_band {
   int panel_maxg = HH_PANEL_MAXG;
   unsigned spin_limit = 1u << 24;
   int panel_fallbacks = 0;
+  // CholeskyQR panel (gpmi_cholqr.hip; default, GPMI_BAND_PANEL=hh selects the
+  // Householder panel): Q [n_pad][128], Gram partials, the three Cholesky factors
+  // and inverses, the reconstruction's U^-T, V1, signs, scratch, failure flag
+  int panel_mode = 0;        // 0 CholeskyQR, 1 Householder (single launch)
+  int cq_fallbacks = 0;      // reductions redone with Householder panels
+  int cq_la_grid = 0;        // SYR2K grid cap beside a CholeskyQR panel (0: none)
+  double* Qb = nullptr;
+  double* cqpart = nullptr;
+  double* cqG = nullptr;
+  // per panel (cq_top_kernel forms every panel's R after the reduction):
+  double* cqL = nullptr;     // [nt][3][128][128] exact factors (first-order passes: by top)
+  double* cqLinv = nullptr;  // [nt][3][128][128] applied inverses
+  double* cqS = nullptr;     // [nt][128] reconstruction signs
+  double* cqscr = nullptr;   // [nt][128][128]
+  int* cqflag = nullptr;     // [nt][8]: [0..2] first-order flag per pass, [3] CholeskyQR
+                             // succeeded, [4] failed (the guarded Householder panel ran)
+  int cq_panel_fallbacks = 0;   // panels factored by the guarded Householder panel
+  double* cqMinv = nullptr;  // C = U^-T M3 of the current panel
+  double cq_fo[3] = {0.0, 1e-4, 3e-8};   // first-order thresholds on ||G - I||_F
   int cap = 0;
   int nrhs = 0;
   double reduce_ms = 0.0, rhs_ms = 0.0, loglik_ms = 0.0, der_ms = 0.0;
@@ -136,7 +155,9 @@ namespace {
 int band_free(gpmi_band* b) {
   double* bufs[] = {b->Ab, b->U, b->X, b->Xp, b->part, b->pivrow, b->tau, b->Tm, b->tnp, b->tnp2,
                     b->VtV, b->M, b->Zh, b->Y, b->qtp, b->qa, b->qb, b->etas, b->out, b->Ac, b->td,
-                    b->fac, b->ysol, b->der};
+                    b->fac, b->ysol, b->der, b->Qb, b->cqpart, b->cqG, b->cqL, b->cqLinv,
+                    b->cqMinv, b->cqS, b->cqscr};
+  if (b->cqflag) (void)hipFree(b->cqflag);
   for (double* p : bufs)
     if (p) (void)hipFree(p);
   if (b->info) (void)hipFree(b->info);
@@ -221,20 +242,85 @@ int qt_panel(gpmi_band* b, int j, hipStream_t st) {
   return 0;
 }
 
-// Householder QR of panel j (columns [128 j, +128), rows from 128 (j + 1)) on st;
-// single = false forces the per-column launches.
-int panel_qr(gpmi_band* b, int j, hipStream_t st, bool single) {
+// CholeskyQR panel j (gpmi_cholqr.hip): shifted CholeskyQR3 of the m x 128 panel,
+// then Householder reconstruction into V (the panel below its top block), tau and
+// S R (the top block). A failure sets the panel's flag [4] before anything is written
+// to the panel, and the guarded Householder panel factors it instead.
+int cq_panel(gpmi_band* b, int j, hipStream_t st) {
   const int64_t np = b->n_pad;
   const int64_t r0 = (int64_t)(j + 1) * TS, c0 = (int64_t)j * TS;
+  const int m = (int)(np - r0);
+  const int mt = m / TS;
+  double* P = b->Ab + r0 * np + c0;
+  const double coef = 11.0 * ((double)m * TS + (double)TS * (TS + 1)) * 1.1102230246251565e-16;
+  const int64_t pt = (int64_t)j * 3 * TS * TS;   // this panel's factor slots
+  int* fl = b->cqflag + 8 * j;
+  // Gram partials of P (64-row tiles), then per pass: reduce -> factor -> apply
+  // (+ the next Gram)
+  const int rt = m / 64;
+  hipLaunchKernelGGL(cq_gram_kernel, dim3(rt), dim3(256), CQ_DYN_LDS, st, P, np, b->cqpart);
+  BD_LAUNCH("cq_gram_kernel");
+  for (int pass = 0; pass < 2; ++pass) {
+    hipLaunchKernelGGL(cq_reduce_kernel, dim3(CQ_GPK / 256), dim3(256), 0, st, b->cqpart, rt,
+                       b->cqG);
+    BD_LAUNCH("cq_reduce_kernel");
+    double* L = b->cqL + pt + (int64_t)pass * TS * TS;
+    double* Li = b->cqLinv + pt + (int64_t)pass * TS * TS;
+    hipLaunchKernelGGL(cq_chol_kernel, dim3(1), dim3(256), 0, st, b->cqG, pass, coef,
+                       b->cq_fo[pass], L, Li, fl, fl + 4, b->ctr);
+    BD_LAUNCH("cq_chol_kernel");
+    const double* src = pass == 0 ? P : b->Qb;
+    hipLaunchKernelGGL(cq_apply_kernel, dim3(rt), dim3(256), CQ_DYN_LDS, st, src,
+                       pass == 0 ? np : (int64_t)TS, b->Qb, (int64_t)TS, Li, b->cqpart,
+                       nullptr);
+    BD_LAUNCH("cq_apply_kernel");
+  }
+  hipLaunchKernelGGL(cq_reduce_kernel, dim3(CQ_GPK / 256), dim3(256), 0, st, b->cqpart, rt,
+                     b->cqG);
+  BD_LAUNCH("cq_reduce_kernel");
+  // third factor, reconstruction: V1 into P, tau, S, C = U^-T M3
+  hipLaunchKernelGGL(cq_recon_kernel, dim3(1), dim3(256), 0, st, b->Qb, b->cqG, b->cq_fo[2], P,
+                     np, b->cqS + (int64_t)j * TS, b->tau + (int64_t)j * TS,
+                     b->cqL + pt + 2 * TS * TS, b->cqLinv + pt + 2 * TS * TS, b->cqMinv, fl,
+                     fl + 4);
+  BD_LAUNCH("cq_recon_kernel");
+  // V2 = Q2 C^T below the top block
+  if (mt > 1) {
+    hipLaunchKernelGGL(cq_apply_kernel, dim3(rt - 2), dim3(256), CQ_DYN_LDS, st, b->Qb + TS * TS,
+                       (int64_t)TS, P + TS * np, np, b->cqMinv, nullptr, fl + 4);
+    BD_LAUNCH("cq_apply_kernel");
+  }
+  // a failed panel (flag fl[4], P untouched) by the Householder panel in one launch;
+  // past its size the host redoes the reduction (band_reduce_pass)
+  const int G = (m + HH_ROWS - 1) / HH_ROWS;
+  if (G <= b->panel_maxg) {
+    hipLaunchKernelGGL(hh_panel_kernel, dim3(G), dim3(HH_THREADS), HH_PANEL_LDS, st, P, np, m,
+                       b->part, b->pivrow, b->ctr, b->tau + (int64_t)j * TS, b->err,
+                       b->spin_limit, fl + 4);
+    BD_LAUNCH("hh_panel_kernel");
+  }
+  return 0;
+}
+
+// Panel j (columns [128 j, +128), rows from 128 (j + 1)) on st. mode 0: CholeskyQR;
+// 1: Householder, one launch per panel where its workgroups fit; 2: Householder,
+// one launch per column.
+int panel_qr(gpmi_band* b, int j, hipStream_t st, int mode) {
+  const int64_t np = b->n_pad;
+  const int64_t r0 = (int64_t)(j + 1) * TS, c0 = (int64_t)j * TS;
+  // a last panel with fewer than 128 real rows (ragged n: the rest is the zero
+  // pad) has rank < 128, which CholeskyQR cannot orthonormalise: Householder
+  if (mode == 0 && b->n - r0 >= TS) return cq_panel(b, j, st);
+  if (mode == 0) mode = 1;
   const int m = (int)(np - r0);
   const int G = (m + HH_ROWS - 1) / HH_ROWS;
   double* P = b->Ab + r0 * np + c0;
   double* tau = b->tau + (int64_t)j * TS;
-  if (single && G <= b->panel_maxg) {
+  if (mode == 1 && G <= b->panel_maxg) {
     // one launch per panel (rows in registers, in-launch reductions)
     BD_TRY(hipMemsetAsync(b->ctr, 0, 512, st));
     hipLaunchKernelGGL(hh_panel_kernel, dim3(G), dim3(HH_THREADS), HH_PANEL_LDS, st, P, np, m,
-                       b->part, b->pivrow, b->ctr, tau, b->err, b->spin_limit);
+                       b->part, b->pivrow, b->ctr, tau, b->err, b->spin_limit, nullptr);
     BD_LAUNCH("hh_panel_kernel");
   } else {
     for (int c = -1; c < TS; ++c) {
@@ -257,19 +343,20 @@ std::vector<double> pack_rhs(const gpmi_band* b, const double* rhs, int64_t ld, 
 // Dense -> band: panels j = 0 .. nt-2 of 128 columns (see gpmi_band.hip).
 // With yh (the packed RHS), Y = Q^T R is applied panel by panel on the qs
 // stream as soon as each panel's T exists, beside the rest of the reduction.
-// single = false: every panel by per-column launches, no look-ahead.
-int band_reduce_pass(gpmi_band* b, const double* K, const std::vector<double>* yh, bool single) {
+// mode: the panel algorithm (panel_qr); mode 2 runs without look-ahead.
+int band_reduce_pass(gpmi_band* b, const double* K, const std::vector<double>* yh, int mode) {
   hipStream_t s = b->stream;
   const int64_t np = b->n_pad;
   const int nt = b->nt;
   BD_TRY(hipMemsetAsync(b->err, 0, 16, s));
+  if (mode == 0) BD_TRY(hipMemsetAsync(b->cqflag, 0, sizeof(int) * 8 * nt, s));
   BD_TRY(hipEventRecord(b->ev0, s));
   if (yh) {
     BD_TRY(hipMemcpyAsync(b->Y, yh->data(), sizeof(double) * yh->size(), hipMemcpyHostToDevice,
                           b->qs));
   }
   BD_TRY(hipMemcpyAsync(b->Ab, K, sizeof(double) * np * np, hipMemcpyDeviceToDevice, s));
-  const bool la = single && b->lookahead && b->s_pan;
+  const bool la = mode != 2 && b->lookahead && b->s_pan;
   bool ahead = false;   // panel j already factored by the previous look-ahead
   for (int j = 0; j + 1 < nt; ++j) {
     const int64_t r0 = (int64_t)(j + 1) * TS, c0 = (int64_t)j * TS;
@@ -278,7 +365,7 @@ int band_reduce_pass(gpmi_band* b, const double* K, const std::vector<double>* y
     double* tau = b->tau + (int64_t)j * TS;
     double* T = b->Tm + (int64_t)j * TS * TS;
     if (!ahead) {
-      int rc = panel_qr(b, j, s, single);
+      int rc = panel_qr(b, j, s, mode);
       if (rc) return rc;
     }
     ahead = false;
@@ -325,7 +412,7 @@ int band_reduce_pass(gpmi_band* b, const double* K, const std::vector<double>* y
     hipLaunchKernelGGL(w_kernel, dim3(mt), dim3(256), 0, s, b->X, Ur, (int64_t)BAND_ULD, b->Zh);
     BD_LAUNCH("w_kernel");
     const int next_g = (int)((np - r0 - TS + HH_ROWS - 1) / HH_ROWS);   // panel j + 1's grid
-    if (la && j + 2 < nt && next_g <= b->panel_maxg) {
+    if (la && j + 2 < nt && (mode == 0 || next_g <= b->panel_maxg)) {
       // tile column 0 of the update (panel j + 1's columns) first; then that
       // panel's QR beside the rest of the update on a grid capped to la_grid
       // workgroups, so that the panel's workgroups find free CUs
@@ -334,13 +421,15 @@ int band_reduce_pass(gpmi_band* b, const double* K, const std::vector<double>* y
       BD_LAUNCH("syr2k_kernel");
       BD_TRY(hipEventRecord(b->ev_col, s));
       BD_TRY(hipStreamWaitEvent(b->s_pan, b->ev_col, 0));
-      int rc = panel_qr(b, j + 1, b->s_pan, single);
+      int rc = panel_qr(b, j + 1, b->s_pan, mode);
       if (rc) return rc;
       BD_TRY(hipEventRecord(b->ev_pan, b->s_pan));
       const int rest = (mt - 1) * mt / 2;
       // la_grid 0: leave exactly the panel's workgroup count of CUs free (measured:
-      // slower than a fixed 128-workgroup cap at N = 16384, 302 vs 262 ms)
-      const int cap = b->la_grid > 0 ? b->la_grid : std::max(64, b->ncu - next_g);
+      // slower than a fixed 128-workgroup cap at N = 16384, 302 vs 262 ms); the
+      // CholeskyQR panel needs no co-resident workgroups (cq_la_grid, 0: no cap)
+      const int cap = mode == 0 ? (b->cq_la_grid > 0 ? b->cq_la_grid : rest)
+                      : b->la_grid > 0 ? b->la_grid : std::max(64, b->ncu - next_g);
       hipLaunchKernelGGL(syr2k_rest_kernel, dim3(std::min(rest, cap)), dim3(256), 0, s, b->Ab,
                          np, b->U, (int64_t)BAND_ULD, j + 1, mt);
       BD_LAUNCH("syr2k_rest_kernel");
@@ -357,12 +446,32 @@ int band_reduce_pass(gpmi_band* b, const double* K, const std::vector<double>* y
     BD_TRY(hipEventRecord(b->ev_q, b->qs));
     BD_TRY(hipStreamWaitEvent(s, b->ev_q, 0));
   }
+  if (mode == 0 && nt > 1) {
+    // R (the band's subdiagonal blocks) of every CholeskyQR panel
+    hipLaunchKernelGGL(cq_top_kernel, dim3(nt - 1), dim3(256), 0, s, b->cqL, b->cqLinv, b->cqflag,
+                       b->cqS, b->cqscr, b->Ab, np);
+    BD_LAUNCH("cq_top_kernel");
+  }
   BD_TRY(hipEventRecord(b->ev1, s));
   int herr = 0;
+  std::vector<int> hflag(mode == 0 ? 8 * nt : 0);
   BD_TRY(hipMemcpyAsync(&herr, b->err, sizeof(int), hipMemcpyDeviceToHost, s));
+  if (mode == 0)
+    BD_TRY(hipMemcpyAsync(hflag.data(), b->cqflag, sizeof(int) * hflag.size(),
+                          hipMemcpyDeviceToHost, s));
   BD_TRY(hipEventSynchronize(b->ev1));
   BD_TRY(hipStreamSynchronize(s));
   if (herr) return set_error(-1201, "band reduction: panel hand-off timed out (workgroups not co-resident?)");
+  if (mode == 0) {
+    // failed CholeskyQR panels: refactored by the guarded Householder panel, or (past
+    // its single-launch size) the reduction is redone with Householder panels
+    for (int j = 0; j + 1 < nt; ++j) {
+      if (!hflag[8 * j + 4]) continue;
+      const int G = (int)((np - (int64_t)(j + 1) * TS + HH_ROWS - 1) / HH_ROWS);
+      if (G > b->panel_maxg) return -1204;
+      ++b->cq_panel_fallbacks;
+    }
+  }
   float ms = 0.f;
   BD_TRY(hipEventElapsedTime(&ms, b->ev0, b->ev1));
   b->reduce_ms = ms;
@@ -372,11 +481,20 @@ int band_reduce_pass(gpmi_band* b, const double* K, const std::vector<double>* y
 // The reduction with the single-launch panel QR; if a hand-off times out (its
 // workgroups were not all resident, e.g. the GPU is shared or partitioned), the
 // whole reduction is redone from K with the per-column panel launches.
+// CholeskyQR panels first (unless GPMI_BAND_PANEL=hh); if one of them reports a
+// breakdown (a numerically rank-deficient panel) the reduction is redone with
+// Householder panels.
 int band_reduce(gpmi_band* b, const double* K, const std::vector<double>* yh = nullptr) {
-  int rc = band_reduce_pass(b, K, yh, true);
+  int rc = -1204;
+  if (b->panel_mode == 0) {
+    rc = band_reduce_pass(b, K, yh, 0);
+    if (rc != -1204) return rc;
+    ++b->cq_fallbacks;
+  }
+  rc = band_reduce_pass(b, K, yh, 1);
   if (rc != -1201) return rc;
   ++b->panel_fallbacks;
-  return band_reduce_pass(b, K, yh, false);
+  return band_reduce_pass(b, K, yh, 2);
 }
 
 int ensure_cap(gpmi_band* b, int neta) {
@@ -437,6 +555,13 @@ int gpmi_band_create(gpmi_op* op, gpmi_band** out) {
     return fail(e, "rhs stream");
   if (const char* la = std::getenv("GPMI_BAND_LA")) b->lookahead = std::atoi(la);
   if (const char* lg = std::getenv("GPMI_BAND_LA_GRID")) b->la_grid = std::max(0, std::atoi(lg));
+  if (const char* lg = std::getenv("GPMI_BAND_CQ_LA_GRID"))
+    b->cq_la_grid = std::max(0, std::atoi(lg));
+  if (const char* pm = std::getenv("GPMI_BAND_PANEL")) b->panel_mode = std::strcmp(pm, "hh") == 0;
+  // GPMI_CQ_FO=0: every CholeskyQR pass by an exact Cholesky (no first-order passes)
+  if (const char* fo = std::getenv("GPMI_CQ_FO"))
+    if (std::atoi(fo) == 0) b->cq_fo[1] = b->cq_fo[2] = 0.0;
+
   if ((e = hipDeviceGetAttribute(&b->ncu, hipDeviceAttributeMultiprocessorCount, v.device)) !=
       hipSuccess)
     return fail(e, "CU count");
@@ -474,10 +599,24 @@ int gpmi_band_create(gpmi_op* op, gpmi_band** out) {
   BALLOC(qtp, (size_t)(np / QT_ROWS + 1) * TS * RLD);
   BALLOC(qa, TS * RLD);
   BALLOC(qb, TS * RLD);
+  BALLOC(Qb, np * TS);
+  BALLOC(cqpart, (size_t)(np / 64) * CQ_GPK);
+  BALLOC(cqG, TS * TS);
+  BALLOC(cqL, (size_t)nt * 3 * TS * TS);
+  BALLOC(cqLinv, (size_t)nt * 3 * TS * TS);
+  BALLOC(cqMinv, TS * TS);
+  BALLOC(cqS, (size_t)nt * TS);
+  BALLOC(cqscr, (size_t)nt * TS * TS);
 #undef BALLOC
+  if ((e = hipMalloc(&b->cqflag, sizeof(int) * 8 * nt)) != hipSuccess) return fail(e, "cqflag");
   if ((e = hipMalloc(&b->ctr, 512)) != hipSuccess) return fail(e, "ctr");
   if ((e = hipMalloc(&b->err, 16)) != hipSuccess) return fail(e, "err");
   if ((e = hipMemsetAsync(b->err, 0, 16, b->stream)) != hipSuccess) return fail(e, "err memset");
+  for (const void* f : {reinterpret_cast<const void*>(&cq_gram_kernel),
+                        reinterpret_cast<const void*>(&cq_apply_kernel)})
+    if ((e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, CQ_DYN_LDS)) !=
+        hipSuccess)
+      return fail(e, "CholeskyQR LDS attribute");
   // per device (this one is current): cheap, so set on every create
   if ((e = hipFuncSetAttribute(reinterpret_cast<const void*>(&hh_panel_kernel),
                                hipFuncAttributeMaxDynamicSharedMemorySize, HH_PANEL_LDS)) !=
@@ -827,6 +966,15 @@ int gpmi_band_chase_info(gpmi_band* b, int* systolic, int* fallbacks, int* maxg)
   if (systolic) *systolic = b->chase_systolic;
   if (fallbacks) *fallbacks = b->chase_fallbacks;
   if (maxg) *maxg = b->chase_maxg;
+  return 0;
+}
+
+int gpmi_band_cq_stats(gpmi_band* b, int* panel_mode, int* cq_fallbacks,
+                       int* cq_panel_fallbacks) {
+  if (!b) return set_error(-1006, "null handle");
+  if (panel_mode) *panel_mode = b->panel_mode;
+  if (cq_fallbacks) *cq_fallbacks = b->cq_fallbacks;
+  if (cq_panel_fallbacks) *cq_panel_fallbacks = b->cq_panel_fallbacks;
   return 0;
 }
 

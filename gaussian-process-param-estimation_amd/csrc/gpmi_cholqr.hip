@@ -1,0 +1,624 @@
+// CholeskyQR panel of the band reduction (the default panel; gpmi_band_api.hip
+// falls back to the Householder panel of gpmi_band.hip when it reports failure).
+//
+// The Householder panel QR needs one grid-wide reduction per column (128 per
+// panel, ~7.6 us each across CUs). This panel needs three: shifted CholeskyQR3
+// (Fukaya, Kannan, Nakatsukasa, Yamamoto, Yanagisawa, SIAM J. Sci. Comput. 42
+// (2020) A477) orthonormalises the m x 128 panel P = Q R with three Gram /
+// Cholesky / triangular-solve passes, the first with the shift
+// s = 11 (m b + b (b + 1)) u ||P||_F^2 so that it cannot break down for
+// cond(P) < 1/u; then Householder reconstruction (Ballard, Demmel, Grigori,
+// Jacquelin, Knight, Nguyen, IPDPS 2014) turns Q into the compact-WY form the
+// rest of the reduction consumes: LU without pivoting of Q - [S; 0], with
+// S_ii = -sign of the running pivot (|pivot| >= 1), gives Q - [S; 0] = V U with V
+// unit lower trapezoidal (the Householder vectors), tau_i = -U_ii S_ii, and
+// (I - V T V^T)^T P = [S R; 0]. Only the 128 x 128 top block of Q needs the
+// sequential LU; the rows below are V_2 = Q_2 U^-1, one MFMA tile product each.
+//
+// Kernels (one panel; host sequence in gpmi_band_api.hip: cq_panel):
+//   cq_gram_kernel     (m/64 tiles)     Gram partials of P's row tiles (packed lower)
+//   cq_reduce_kernel                    G = sum of the partials
+//   cq_chol_kernel     (1 workgroup)    L = chol(G [+ s I]), L^-1; failure flag
+//   cq_apply_kernel    (m/64 tiles)     Q = Src L^-T and the Gram partials of Q
+//   (passes 0 and 1; then reduce)
+//   cq_recon_kernel    (1 workgroup)    third factor, Q3's top block, its LU with
+//                                       signs, U^-1, tau, C = U^-T M3
+//   cq_apply_kernel    (m/64 - 2)       V2 = Q2 C^T below the top block
+//   cq_top_kernel      (after the       top block of every panel above the diagonal:
+//                       reduction)      S R, R = L3^T L2^T L1^T, one workgroup each
+// Failure (a non-positive pivot in any pass, or a third-pass factor farther than
+// CQ_TOL from I, i.e. a second-pass Q that is not yet nearly orthonormal) sets the
+// panel's failure flag before anything is written to the panel; the guarded
+// Householder panel (hh_panel_kernel with that flag) then factors the untouched
+// panel on the device (or, past its single-launch size, the host redoes the
+// reduction with Householder panels). Numerics
+// checked on Matern matrices first in numpy (tools/cholqr_proto.py).
+
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "gpmi_internal.h"
+#include "gpmi_device.h"
+#include "gpmi_lds_chol.h"
+#include "gpmi_band.h"
+#include "gpmi_tile.h"
+
+namespace gpmi {
+
+constexpr double CQ_TOL = 1e-2;   // third pass: max |L3 - I| accepted
+
+// A 128 x 128 row-major matrix in registers: thread t holds the pairs
+// e = it * 256 + t (row e >> 6, columns 2 (e & 63) and +1), every load in flight.
+__device__ __forceinline__ void load_regs(const double* __restrict__ G, d2 (&v)[32]) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int it = 0; it < 32; ++it) v[it] = *reinterpret_cast<const d2*>(G + 2 * (it * 256 + t));
+}
+
+// ||G - I||_F^2 over the workgroup (every thread gets the sum); sred: 4 doubles.
+__device__ __forceinline__ double frob_dev2(const d2 (&v)[32], double* sred) {
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  double s = 0.0;
+#pragma unroll
+  for (int it = 0; it < 32; ++it) {
+    const int e = it * 256 + t, r = e >> 6, c = (e & 63) * 2;
+    const double d0 = v[it][0] - (r == c ? 1.0 : 0.0);
+    const double d1 = v[it][1] - (r == c + 1 ? 1.0 : 0.0);
+    s += d0 * d0 + d1 * d1;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+  if (lane == 0) sred[w] = s;
+  __syncthreads();
+  const double tot = ((sred[0] + sred[1]) + sred[2]) + sred[3];
+  __syncthreads();
+  return tot;
+}
+
+// First-order inverse Cholesky factor of G = I + E: I - E_l, E_l = stril(E) + diag(E)/2.
+__device__ __forceinline__ double fo_entry(double g, int r, int c) {
+  return r > c ? -g : (r == c ? 1.0 - 0.5 * (g - 1.0) : 0.0);
+}
+
+// L = chol(G + shift I) (lower), L^-1 (lower), both row-major 128 x 128 with
+// zeros above the diagonal. pass 0 adds the shift coef * trace(G); pass 2
+// checks L against I.
+// First-order pass (pass > 0, ||G - I||_F <= tau_fo): G = I + E with E tiny, so
+// L = I + E_l + O(E^2), E_l = stril(E) + diag(E) / 2, and the applied factor is
+// Linv = I - E_l: the new Q's orthogonality error is O(||E||^2) (the next pass,
+// or none for the last at tau_fo <= 3e-8, removes it). fo[pass] records the
+// choice; cq_top_kernel then forms L = Linv^-1 (LDS triangular inverse), so
+// P = Q (L1 L2 L3)^T stays exact to rounding. Lout is not written then.
+__global__ __launch_bounds__(256) void cq_chol_kernel(const double* __restrict__ G, int pass,
+                                                      double coef, double tau_fo,
+                                                      double* __restrict__ Lout,
+                                                      double* __restrict__ Linv,
+                                                      int* __restrict__ fo,
+                                                      int* __restrict__ fail,
+                                                      unsigned* __restrict__ ctr) {
+  __shared__ double Ls[TS * DL];
+  __shared__ double Aux[TS * RLD];
+  __shared__ double sdiag[TS];
+  __shared__ double sred[4];
+  __shared__ int s_fail;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  if (t == 0) s_fail = 0;
+  if (pass == 0 && t < 128) ctr[t] = 0u;   // the guarded Householder panel's counter
+  d2 v[32];
+  load_regs(G, v);
+  double shift = 0.0;
+  if (pass == 0) {
+    double d = t < TS ? G[t * TS + t] : 0.0;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) d += __shfl_xor(d, off);
+    if (lane == 0) sred[w] = d;
+    __syncthreads();
+    shift = coef * (((sred[0] + sred[1]) + sred[2]) + sred[3]);
+  } else if (tau_fo > 0.0) {
+    // NaN takes the exact path (and fails there)
+    if (frob_dev2(v, sred) <= tau_fo * tau_fo) {
+#pragma unroll
+      for (int it = 0; it < 32; ++it) {
+        const int e = it * 256 + t, r = e >> 6, c = (e & 63) * 2;
+        *reinterpret_cast<d2*>(Linv + 2 * e) =
+            d2{fo_entry(v[it][0], r, c), fo_entry(v[it][1], r, c + 1)};
+      }
+      if (t == 0) fo[pass] = 1;
+      return;
+    }
+  }
+  if (t == 0) fo[pass] = 0;
+#pragma unroll
+  for (int it = 0; it < 32; ++it) {
+    const int e = it * 256 + t, r = e >> 6, c = (e & 63) * 2;
+    Ls[r * DL + c] = (c <= r) ? v[it][0] + (c == r ? shift : 0.0) : 0.0;
+    Ls[r * DL + c + 1] = (c + 1 <= r) ? v[it][1] + (c + 1 == r ? shift : 0.0) : 0.0;
+  }
+  __syncthreads();
+  lds_chol_block(Ls, Aux, sdiag, &s_fail);
+  __syncthreads();
+  int bad = s_fail;
+  double dev = 0.0;
+  for (int e = t; e < TS * TS; e += 256) {
+    const int r = e >> 7, c = e & 127;
+    const double v = (c <= r) ? Ls[r * DL + c] : 0.0;
+    Lout[e] = v;
+    if (pass == 2) dev = fmax(dev, fabs(v - (c == r ? 1.0 : 0.0)));
+  }
+  if (pass == 2) {
+    // a NaN fails the test too (!(dev <= tol))
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) dev = fmax(dev, __shfl_xor(dev, off));
+    if (!(dev <= CQ_TOL)) bad = 1;
+  }
+  if (bad && lane == 0) __hip_atomic_store(fail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();   // every thread is done reading L before the inverse overwrites it
+  lds_inv_block(Ls, Aux);
+  __syncthreads();
+  for (int e = t; e < TS * TS; e += 256) {
+    const int r = e >> 7, c = e & 127;
+    Linv[e] = (c <= r) ? Ls[r * DL + c] : 0.0;
+  }
+}
+
+// Row tiles of 64: m / 64 workgroups of two per CU (67.6 KB of LDS each), so the
+// fp64 MFMA work (~307 GFLOP/s per CU) spreads over the whole chip. Gram partials
+// are packed: the 36 lower 16 x 16 tiles (ti >= tj) of the symmetric 128 x 128
+// block, tile q = ti (ti + 1) / 2 + tj, 256 doubles each.
+constexpr int RT = 64;           // rows per tile
+constexpr int T_LD = TS + 4;     // LDS row stride of a staged 64 x 128 tile
+constexpr int GPK = 36 * 256;    // doubles per packed Gram partial
+
+__device__ __forceinline__ void tri_tile(int q, int* ti, int* tj) {
+  int i = 0;
+  while ((i + 1) * (i + 2) / 2 <= q) ++i;
+  *ti = i;
+  *tj = q - i * (i + 1) / 2;
+}
+
+// Stage the 64 x 128 row tile S0 (stride lds) into LDS (stride T_LD).
+__device__ __forceinline__ void stage_rows(const double* __restrict__ S0, int64_t lds,
+                                           double* T) {
+  const int t = threadIdx.x;
+  d2 v[16];
+#pragma unroll
+  for (int it = 0; it < 16; ++it) {
+    const int e = it * 256 + t;
+    v[it] = *reinterpret_cast<const d2*>(S0 + (int64_t)(e >> 6) * lds + (e & 63) * 2);
+  }
+#pragma unroll
+  for (int it = 0; it < 16; ++it) {
+    const int e = it * 256 + t;
+    *reinterpret_cast<d2*>(T + (e >> 6) * T_LD + (e & 63) * 2) = v[it];
+  }
+}
+
+// Packed lower Gram partial T^T T of the staged 64 x 128 tile; wave w forms the
+// 16 x 16 tiles q = w, w + 4, .. (9 each), 16 k-steps over the 64 rows.
+__device__ __forceinline__ void lds_tile_gram(const double* T, double* __restrict__ part) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int fr = lane & 15, fk = lane >> 4;
+  for (int q = w; q < 36; q += 4) {
+    int ti, tj;
+    tri_tile(q, &ti, &tj);
+    d4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int kk = 0; kk < RT / 4; ++kk) {
+      const double* row = T + (kk * 4 + fk) * T_LD;
+      acc = mfma64(row[ti * 16 + fr], row[tj * 16 + fr], acc);
+    }
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) part[q * 256 + (fk + 4 * rr) * 16 + fr] = acc[rr];
+  }
+}
+
+// part[tile] = packed lower Gram of Src's 64-row tile blockIdx.x.
+__global__ __launch_bounds__(256, 2) void cq_gram_kernel(const double* __restrict__ Src,
+                                                         int64_t lds,
+                                                         double* __restrict__ part) {
+  extern __shared__ double cq_dyn[];
+  stage_rows(Src + (int64_t)blockIdx.x * RT * lds, lds, cq_dyn);
+  __syncthreads();
+  lds_tile_gram(cq_dyn, part + (int64_t)blockIdx.x * GPK);
+}
+
+// G (128 x 128, symmetric, row-major) = sum over the np packed partials, fixed
+// order; each packed element is written to both mirror positions.
+__global__ __launch_bounds__(256) void cq_reduce_kernel(const double* __restrict__ part, int np,
+                                                        double* __restrict__ G) {
+  const int e = blockIdx.x * 256 + threadIdx.x;   // < GPK
+  double s0 = 0.0, s1 = 0.0;
+  int p = 0;
+  for (; p + 1 < np; p += 2) {
+    s0 += part[(int64_t)p * GPK + e];
+    s1 += part[(int64_t)(p + 1) * GPK + e];
+  }
+  if (p < np) s0 += part[(int64_t)p * GPK + e];
+  const double v = s0 + s1;
+  int ti, tj;
+  tri_tile(e >> 8, &ti, &tj);
+  const int r = ti * 16 + ((e >> 4) & 15), c = tj * 16 + (e & 15);
+  G[r * TS + c] = v;
+  G[c * TS + r] = v;
+}
+
+// Dst[tile] = Src[tile] M^T for the 64-row tile blockIdx.x (M lower, row-major):
+// with M = L^-1 this is Src L^-T = Src R^-1; with M = U^-T M3 it is the final
+// V2 = Q2 M3^T U^-1. Wave w forms the output column blocks w and 7 - w (k-steps
+// 4 (cb + 1) each: M is lower) for all four 16-row blocks; its M fragments are
+// loaded from global (L2) once, all in flight, and the tile from LDS. With
+// part, also the packed Gram partial of Dst[tile] (the next pass's Gram).
+// Src may equal Dst (in place): each workgroup reads its rows before storing them.
+__global__ __launch_bounds__(256, 2) void cq_apply_kernel(const double* Src, int64_t lds,
+                                                          double* Dst, int64_t ldd,
+                                                          const double* __restrict__ M,
+                                                          double* __restrict__ part,
+                                                          const int* __restrict__ skip) {
+  extern __shared__ double cq_dyn[];
+  if (skip && __hip_atomic_load(skip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int fr = lane & 15, fk = lane >> 4;
+  const int64_t r0 = (int64_t)blockIdx.x * RT;
+  const int cb0 = w, cb1 = 7 - w;
+  // M fragments of both column blocks: b0[kk] = M[cb0*16 + fr][4 kk + fk]
+  double b0[16], b1[32];
+#pragma unroll
+  for (int kk = 0; kk < 16; ++kk)
+    b0[kk] = kk < 4 * (cb0 + 1) ? M[(cb0 * 16 + fr) * TS + kk * 4 + fk] : 0.0;
+#pragma unroll
+  for (int kk = 0; kk < 32; ++kk)
+    b1[kk] = kk < 4 * (cb1 + 1) ? M[(cb1 * 16 + fr) * TS + kk * 4 + fk] : 0.0;
+  stage_rows(Src + r0 * lds, lds, cq_dyn);
+  __syncthreads();
+  d4 acc0[4], acc1[4];
+#pragma unroll
+  for (int rb = 0; rb < 4; ++rb) {
+    acc0[rb] = d4{0.0, 0.0, 0.0, 0.0};
+    acc1[rb] = d4{0.0, 0.0, 0.0, 0.0};
+  }
+  // column block cb0 <= 3: k-steps < 16; cb1 >= 4: k-steps < 32
+#pragma unroll
+  for (int kk = 0; kk < 16; ++kk) {
+    if (kk < 4 * (cb0 + 1)) {
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb)
+        acc0[rb] = mfma64(cq_dyn[(rb * 16 + fr) * T_LD + kk * 4 + fk], b0[kk], acc0[rb]);
+    }
+  }
+#pragma unroll
+  for (int kk = 0; kk < 32; ++kk) {
+    if (kk < 4 * (cb1 + 1)) {
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb)
+        acc1[rb] = mfma64(cq_dyn[(rb * 16 + fr) * T_LD + kk * 4 + fk], b1[kk], acc1[rb]);
+    }
+  }
+  double* D0 = Dst + r0 * ldd;
+#pragma unroll
+  for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int row = rb * 16 + fk + 4 * rr;
+      D0[(int64_t)row * ldd + cb0 * 16 + fr] = acc0[rb][rr];
+      D0[(int64_t)row * ldd + cb1 * 16 + fr] = acc1[rb][rr];
+    }
+  if (!part) return;
+  __syncthreads();   // every wave is done reading the source tile
+#pragma unroll
+  for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int row = rb * 16 + fk + 4 * rr;
+      cq_dyn[row * T_LD + cb0 * 16 + fr] = acc0[rb][rr];
+      cq_dyn[row * T_LD + cb1 * 16 + fr] = acc1[rb][rr];
+    }
+  __syncthreads();
+  lds_tile_gram(cq_dyn, part + (int64_t)blockIdx.x * GPK);
+}
+
+// Third pass + reconstruction (one workgroup). From G3 = Q2^T Q2 (Q2 the second
+// pass's Q) the third factor M3 = L3^-1 (exact LDS Cholesky, or first order when
+// ||G3 - I||_F <= tau_fo), then Q3's top block Q3t = Q2t M3^T, then the LU without
+// pivoting of Q3t - S, S_ii = -sign of the running pivot, blocked by 16 in LDS:
+//   per column block: the tall panel (rows j0.., 16 columns) on wave 0 with the
+//   rows in registers (pivot row by readlane), U12 = L11^-1 A12 by forward
+//   substitution (one thread per column), then A22 -= L21 U12 on fp64 MFMA.
+// Outputs: V1 (strictly lower: the Householder vectors' top rows, into the top
+// block of the panel P), S, tau = -diag(U) S, L3 / M3 (Lx3 / Linv3, for
+// cq_top_kernel), and C = U^-T M3 (lower), so that the rows below the top block
+// are V2 = Q2 M3^T U^-1 = Q2 C^T in one cq_apply_kernel pass (Q3 itself is never
+// formed below the top block).
+__global__ __launch_bounds__(256) void cq_recon_kernel(const double* __restrict__ Q2,
+                                                       const double* __restrict__ G3,
+                                                       double tau_fo,
+                                                       double* __restrict__ P, int64_t lda,
+                                                       double* __restrict__ S,
+                                                       double* __restrict__ tau,
+                                                       double* __restrict__ Lx3,
+                                                       double* __restrict__ Linv3,
+                                                       double* __restrict__ C,
+                                                       int* __restrict__ fo,
+                                                       int* __restrict__ fail) {
+  __shared__ double A[TS * DL];
+  __shared__ double Aux[TS * RLD];
+  __shared__ double sS[TS];
+  __shared__ double sdiag[TS];
+  __shared__ double sred[4];
+  __shared__ int s_fail;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int fr = lane & 15, fk = lane >> 4;
+  const int wr = w >> 1, wc = w & 1;
+  // an earlier pass failed: leave the panel untouched for the Householder panel
+  if (__hip_atomic_load(fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+  if (t == 0) s_fail = 0;
+  // ---- M3 = L3^-1 into A (lower) and Linv3
+  d2 v[32];
+  load_regs(G3, v);
+  const bool first_order = frob_dev2(v, sred) <= tau_fo * tau_fo;
+  if (first_order) {
+#pragma unroll
+    for (int it = 0; it < 32; ++it) {
+      const int e = it * 256 + t, r = e >> 6, c = (e & 63) * 2;
+      A[r * DL + c] = fo_entry(v[it][0], r, c);
+      A[r * DL + c + 1] = fo_entry(v[it][1], r, c + 1);
+    }
+    if (t == 0) fo[2] = 1;
+  } else {
+#pragma unroll
+    for (int it = 0; it < 32; ++it) {
+      const int e = it * 256 + t, r = e >> 6, c = (e & 63) * 2;
+      A[r * DL + c] = (c <= r) ? v[it][0] : 0.0;
+      A[r * DL + c + 1] = (c + 1 <= r) ? v[it][1] : 0.0;
+    }
+    __syncthreads();
+    lds_chol_block(A, Aux, sdiag, &s_fail);
+    __syncthreads();
+    int bad = s_fail;
+    double dev = 0.0;
+    for (int e = t; e < TS * TS; e += 256) {
+      const int r = e >> 7, c = e & 127;
+      const double v = (c <= r) ? A[r * DL + c] : 0.0;
+      Lx3[e] = v;
+      dev = fmax(dev, fabs(v - (c == r ? 1.0 : 0.0)));
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) dev = fmax(dev, __shfl_xor(dev, off));
+    if (!(dev <= CQ_TOL)) bad = 1;   // NaN included
+    __syncthreads();
+    if (bad && lane == 0) s_fail = 1;
+    __syncthreads();
+    if (s_fail) {
+      if (t == 0) __hip_atomic_store(fail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+    lds_inv_block(A, Aux);
+    if (t == 0) fo[2] = 0;
+  }
+  __syncthreads();
+  for (int e = t; e < TS * TS; e += 256) {
+    const int r = e >> 7, c = e & 127;
+    Linv3[e] = (c <= r) ? A[r * DL + c] : 0.0;
+  }
+  // ---- Q3t = Q2t M3^T: wave (wr, wc) forms rows wr*64.., columns wc*64..; the
+  // A operand straight from global (L2), M3 from LDS (lower: k <= column)
+  {
+    d4 acc[4][4];
+    zero_tile(acc);
+    const int kmax = wc * 64 + 64;
+    for (int k0 = 0; k0 < kmax; k0 += 32) {
+      // the chunk's Q2t operands (8 k-steps) in flight together
+      double a[8][4];
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a[q][i] = Q2[(wr * 64 + i * 16 + fr) * TS + k0 + 4 * q + fk];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int k = k0 + 4 * q + fk;
+        double b[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) b[j] = A[(wc * 64 + j * 16 + fr) * DL + k];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = mfma64(a[q][i], b[j], acc[i][j]);
+      }
+    }
+    __syncthreads();   // every wave is done reading M3 from A
+    store_tile(A, DL, acc, 1.0);
+  }
+  __syncthreads();
+  for (int jb = 0; jb < NDB; ++jb) {
+    const int j0 = jb * DB;
+    // ---- tall panel: rows j0 + lane and j0 + 64 + lane, columns j0 .. j0 + 15
+    if (w == 0) {
+      const int ra = j0 + lane, rb = j0 + 64 + lane;
+      double pa[DB], pb[DB];
+#pragma unroll
+      for (int k = 0; k < DB; ++k) {
+        pa[k] = ra < TS ? A[ra * DL + j0 + k] : 0.0;
+        pb[k] = rb < TS ? A[rb * DL + j0 + k] : 0.0;
+      }
+#pragma unroll
+      for (int j = 0; j < DB; ++j) {
+        double prow[DB];
+#pragma unroll
+        for (int k = j; k < DB; ++k) prow[k] = readlane_d(pa[k], j);
+        const double s = prow[j] >= 0.0 ? -1.0 : 1.0;
+        const double u = prow[j] - s;   // |u| = |pivot| + 1
+        const double rinv = 1.0 / u;
+        if (lane == j) pa[j] = u;
+        if (lane > j) {
+          const double l = pa[j] * rinv;
+          pa[j] = l;
+#pragma unroll
+          for (int k = j + 1; k < DB; ++k) pa[k] -= l * prow[k];
+        }
+        {
+          const double l = pb[j] * rinv;
+          pb[j] = l;
+#pragma unroll
+          for (int k = j + 1; k < DB; ++k) pb[k] -= l * prow[k];
+        }
+        if (lane == 0) sS[j0 + j] = s;
+      }
+#pragma unroll
+      for (int k = 0; k < DB; ++k) {
+        if (ra < TS) A[ra * DL + j0 + k] = pa[k];
+        if (rb < TS) A[rb * DL + j0 + k] = pb[k];
+      }
+    }
+    __syncthreads();
+    if (jb + 1 == NDB) break;
+    // ---- U12 = L11^-1 A12: one thread per column right of the block
+    {
+      const int c = j0 + DB + t;
+      if (c < TS) {
+        double x[DB];
+#pragma unroll
+        for (int r = 0; r < DB; ++r) x[r] = A[(j0 + r) * DL + c];
+#pragma unroll
+        for (int r = 1; r < DB; ++r) {
+          double s = x[r];
+#pragma unroll
+          for (int p = 0; p < r; ++p) s -= A[(j0 + r) * DL + j0 + p] * x[p];
+          x[r] = s;
+        }
+#pragma unroll
+        for (int r = 1; r < DB; ++r) A[(j0 + r) * DL + c] = x[r];
+      }
+    }
+    __syncthreads();
+    // ---- A22 -= L21 U12 over the (7 - jb)^2 trailing 16 x 16 tiles
+    {
+      const int nt = NDB - 1 - jb;
+      for (int q = w; q < nt * nt; q += 4) {
+        const int r0 = (jb + 1 + q / nt) * DB, c0 = (jb + 1 + q % nt) * DB;
+        d4 acc;
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) acc[rr] = A[(r0 + fk + 4 * rr) * DL + c0 + fr];
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+          const double av = A[(r0 + fr) * DL + j0 + 4 * kk + fk];
+          const double bv = A[(j0 + 4 * kk + fk) * DL + c0 + fr];
+          acc = mfma64_neg(av, bv, acc);
+        }
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) A[(r0 + fk + 4 * rr) * DL + c0 + fr] = acc[rr];
+      }
+    }
+    __syncthreads();
+  }
+  // V1 (strictly lower, into the panel's top block) and the signs / tau out
+  for (int e = t; e < TS * TS; e += 256) {
+    const int r = e >> 7, c = e & 127;
+    if (c < r) P[(int64_t)r * lda + c] = A[r * DL + c];
+  }
+  if (t < TS) {
+    S[t] = sS[t];
+    tau[t] = -A[t * DL + t] * sS[t];
+  }
+  if (t == 0) fo[3] = 1;   // this panel's R is formed by cq_top_kernel
+  __syncthreads();
+  // U^T into the lower triangle (each lower slot is written by the one thread
+  // that reads its mirror), then U^-T by the LDS triangular inverse
+  for (int e = t; e < TS * TS; e += 256) {
+    const int r = e >> 7, c = e & 127;
+    if (r > c) A[r * DL + c] = A[c * DL + r];
+  }
+  __syncthreads();
+  lds_diag_inv_lower(A, Aux);
+  __syncthreads();
+  lds_inv_block(A, Aux);
+  __syncthreads();
+  // ---- C = U^-T M3 (lower x lower): A operand from LDS, M3 from global (Linv3,
+  // written above by this workgroup)
+  {
+    d4 acc[4][4];
+    zero_tile(acc);
+    const int kmax = wr * 64 + 64;   // U^-T rows wr*64.. have k <= row
+    for (int k0 = 0; k0 < kmax; k0 += 32) {
+      double b[8][4];   // the chunk's M3 operands in flight together
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) b[q][j] = Linv3[(k0 + 4 * q + fk) * TS + wc * 64 + j * 16 + fr];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int k = k0 + 4 * q + fk;
+        double a[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = wr * 64 + i * 16 + fr;   // above the diagonal A still holds U
+          a[i] = k <= row ? A[row * DL + k] : 0.0;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = mfma64(a[i], b[q][j], acc[i][j]);
+      }
+    }
+    store_tile(C, TS, acc, 1.0);
+  }
+}
+
+// The top 128 x 128 block above the diagonal of every CholeskyQR panel, one
+// workgroup per panel after the whole reduction: R = (L1 L2 L3)^T, then
+// P[r][c] = S_r R[r][c] (c >= r) (the vectors below the diagonal are written by
+// cq_recon_kernel). A first-order pass's L is the exact inverse of its applied
+// factor Linv (LDS triangular inverse). Per panel p: Lx / Linv at p * 3 * 128^2,
+// S at p * 128, flags at p * 8 (flag[3] = 1: the panel's CholeskyQR succeeded), the
+// panel at Ab + (p + 1) * 128 * lda + p * 128; scr: 128^2 per panel.
+__global__ __launch_bounds__(256) void cq_top_kernel(double* __restrict__ Lx,
+                                                     const double* __restrict__ Linv,
+                                                     const int* __restrict__ flags,
+                                                     const double* __restrict__ S,
+                                                     double* __restrict__ scr,
+                                                     double* __restrict__ Ab, int64_t lda) {
+  __shared__ double pool[TS * DL + TS * RLD];   // LDS inverse, or the gemm_tile stages
+  __shared__ double sS[TS];
+  const int t = threadIdx.x, p = blockIdx.x;
+  const int* fl = flags + 8 * p;
+  if (!fl[3]) return;
+  double* L = Lx + (int64_t)p * 3 * TS * TS;
+  const double* Li = Linv + (int64_t)p * 3 * TS * TS;
+  double* sc = scr + (int64_t)p * TS * TS;
+  if (t < TS) sS[t] = S[p * TS + t];
+  for (int k = 1; k < 3; ++k) {
+    if (!fl[k]) continue;
+    double* Ls = pool;
+    double* Aux = pool + TS * DL;
+    for (int e = t; e < TS * TS; e += 256) {
+      const int r = e >> 7, c = e & 127;
+      Ls[r * DL + c] = (c <= r) ? Li[k * TS * TS + e] : 0.0;
+    }
+    __syncthreads();
+    lds_diag_inv_lower(Ls, Aux);
+    __syncthreads();
+    lds_inv_block(Ls, Aux);
+    __syncthreads();
+    for (int e = t; e < TS * TS; e += 256) {
+      const int r = e >> 7, c = e & 127;
+      L[k * TS * TS + e] = (c <= r) ? Ls[r * DL + c] : 0.0;
+    }
+    __syncthreads();
+  }
+  d4 acc[4][4];
+  zero_tile(acc);
+  // acc[r][c] = sum_k L1[r][k] L2[k][c]
+  gemm_tile<KFAST, KSLOW, false>(L, TS, L + TS * TS, TS, TS, pool, acc);
+  store_tile(sc, TS, acc, 1.0);
+  __syncthreads();
+  zero_tile(acc);
+  gemm_tile<KFAST, KSLOW, false>(sc, TS, L + 2 * TS * TS, TS, TS, pool, acc);
+  store_tile(sc, TS, acc, 1.0);   // M = L1 L2 L3 (lower); R = M^T
+  __syncthreads();
+  double* P = Ab + (int64_t)(p + 1) * TS * lda + (int64_t)p * TS;
+  for (int e = t; e < TS * TS; e += 256) {
+    const int r = e >> 7, c = e & 127;
+    if (c >= r) P[(int64_t)r * lda + c] = sS[r] * sc[c * TS + r];
+  }
+}
+
+}  // namespace gpmi

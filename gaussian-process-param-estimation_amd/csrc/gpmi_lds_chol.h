@@ -272,6 +272,39 @@ __device__ __forceinline__ void lds_chol_block(double* Ls, double* Aux, double* 
 #endif
 }
 
+// Aux[8][16][16] <- inverses of the eight 16 x 16 diagonal blocks of the lower
+// triangular Ls (non-unit diagonal), by forward substitution; wave w inverts
+// blocks w and w + 4. Lane (r, g) holds row r, columns 4g..4g+3 of the inverse.
+__device__ __forceinline__ void lds_diag_inv_lower(const double* Ls, double* Aux) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int j0 = (w + 4 * h) * DB;
+    const int r = lane >> 2, g = lane & 3;
+    double lrow[DB];
+#pragma unroll
+    for (int p = 0; p < DB; ++p) lrow[p] = Ls[(j0 + r) * DL + j0 + p];
+    const double rinv = 1.0 / Ls[(j0 + r) * DL + j0 + r];
+    double s[4] = {0.0, 0.0, 0.0, 0.0}, x[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int p = 0; p < DB; ++p) {
+      if (r == p) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) x[k] = (((4 * g + k) == p ? 1.0 : 0.0) - s[k]) * rinv;
+      }
+      double xp[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) xp[k] = __shfl(x[k], (p << 2) | g);
+      if (r > p) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) s[k] += lrow[p] * xp[k];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) Aux[(j0 / DB) * 256 + r * 16 + 4 * g + k] = x[k];
+  }
+}
+
 __device__ __forceinline__ void lds_inv_block(double* Ls, const double* Aux) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int fr = lane & 15, fk = lane >> 4;

@@ -90,6 +90,7 @@ SIGNATURES = {
                                            c_double_p, c_double_p, c_double_p, c_int_p]),
     'gpmi_band_der_ms': (ctypes.c_int, [c_op_p, c_double_p]),
     'gpmi_band_stats': (ctypes.c_int, [c_op_p, c_int_p, c_int_p]),
+    'gpmi_band_cq_stats': (ctypes.c_int, [c_op_p, c_int_p, c_int_p, c_int_p]),
     'gpmi_band_chase_info': (ctypes.c_int, [c_op_p, c_int_p, c_int_p, c_int_p]),
     'gpmi_sp_last_status': (ctypes.c_int, [c_op_p, c_int_p]),
     'gpmi_sp_spmm_info': (ctypes.c_int, [c_op_p, c_int_p, c_double_p, c_int_p]),
@@ -398,11 +399,17 @@ class Band(object):
         return ld, g[0], g[1], g[2], info
 
     def stats(self):
-        """-> dict(panel_fallbacks, panel_maxg) (see gpmi_band_stats)."""
+        """-> dict(panel_fallbacks, panel_maxg, panel, cholqr_fallbacks,
+        cholqr_panel_fallbacks) (see gpmi_band_stats, gpmi_band_cq_stats)."""
         fb, mg = ctypes.c_int(), ctypes.c_int()
         check(self.lib.gpmi_band_stats(self.h, ctypes.byref(fb), ctypes.byref(mg)),
               'gpmi_band_stats')
-        return dict(panel_fallbacks=fb.value, panel_maxg=mg.value)
+        pm, cf, cp = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        check(self.lib.gpmi_band_cq_stats(self.h, ctypes.byref(pm), ctypes.byref(cf),
+                                          ctypes.byref(cp)), 'gpmi_band_cq_stats')
+        return dict(panel_fallbacks=fb.value, panel_maxg=mg.value,
+                    panel='cholqr' if pm.value == 0 else 'householder',
+                    cholqr_fallbacks=cf.value, cholqr_panel_fallbacks=cp.value)
 
     def chase_info(self):
         """-> dict(systolic (2 split, 1 one-per-position, 0 launches), fallbacks,

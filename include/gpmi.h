@@ -259,6 +259,16 @@ int gpmi_band_der_terms(gpmi_band* b, const double* etas, int neta, double* logd
  * the largest panel grid (workgroups) run as one launch on this device
  * (CU count x resident hh_panel workgroups per CU, at most 128). */
 int gpmi_band_stats(gpmi_band* b, int* panel_fallbacks, int* panel_maxg);
+/* The panel algorithm of this band's reductions (0: CholeskyQR panels, shifted
+ * CholeskyQR3 + Householder reconstruction, the default; 1: Householder panels,
+ * GPMI_BAND_PANEL=hh), how many reductions were redone with Householder panels
+ * (a CholeskyQR panel broke down past the single-launch Householder panel's
+ * size) and how many panels broke down (numerically rank-deficient) and were
+ * factored on the device by the Householder panel instead. Replaces nothing in
+ * the reference: the panel QR is inside its one-time eigh
+ * (mixed_correlation.py:76-79). */
+int gpmi_band_cq_stats(gpmi_band* b, int* panel_mode, int* cq_fallbacks,
+                       int* cq_panel_fallbacks);
 /* Which form the last gpmi_band_eigenvalues took (2: the one-launch systolic chase
  * with a D and an E workgroup per position, 1: one workgroup per position, 0: the
  * per-wavefront launches), how many systolic attempts timed out and were redone by

@@ -323,9 +323,10 @@ def test_band_direct_jac_hess_vs_oracle(gp):
 
 
 @pytest.mark.slow
-def test_band_past_single_launch_panel_limit(gp):
-    """n = 16640: the first panel has 129 row blocks, past the single-launch panel
-    QR (<= 128 workgroups), so it runs the per-column hh_col path; logdet and the
+def test_band_past_single_launch_panel_limit(gp, monkeypatch):
+    """n = 16640: the first panel has 129 row blocks, past the single-launch
+    Householder panel QR (<= 128 workgroups): the CholeskyQR panel (default)
+    and, with GPMI_BAND_PANEL=hh, the per-column hh_col path; logdet and the
     Gram block vs the dense device Cholesky (an independent factorization)."""
     from gaussian_proc._mixed_correlation import MixedCorrelation
     n = 16640
@@ -335,10 +336,17 @@ def test_band_past_single_launch_panel_limit(gp):
     X = numpy.column_stack([numpy.ones(n), pts])
     z = numpy.cos(4 * pts[:, 1]) + 0.1 * rng.randn(n)
     etas = [0.05, 2.0]
-    ld_b, G_b = MixedCorrelation(D, imate_method='eigenvalue').loglik_terms(etas, X, z)
     ld_c, G_c = MixedCorrelation(D, imate_method='cholesky').loglik_terms(etas, X, z)
-    assert rel(ld_b, ld_c) < 1e-10
-    numpy.testing.assert_allclose(G_b, G_c, rtol=1e-8, atol=1e-10 * numpy.abs(G_c).max())
+    for panel in ('cholqr', 'hh'):
+        if panel == 'hh':
+            monkeypatch.setenv('GPMI_BAND_PANEL', 'hh')
+        op = MixedCorrelation(D, imate_method='eigenvalue')
+        ld_b, G_b = op.loglik_terms(etas, X, z)
+        # scattered points: a numerically rank-deficient panel may send this size
+        # (past the single-launch Householder panel) back to Householder panels
+        print(panel, op.band().stats())
+        assert rel(ld_b, ld_c) < 1e-10, panel
+        numpy.testing.assert_allclose(G_b, G_c, rtol=1e-8, atol=1e-10 * numpy.abs(G_c).max())
 
 
 def test_band_refresh_with_rhs_matches_set_rhs(gp):
@@ -358,13 +366,15 @@ def test_band_refresh_with_rhs_matches_set_rhs(gp):
 
 
 def test_panel_timeout_falls_back_to_per_column_launches(gp, monkeypatch):
-    """GPMI_HH_SPIN_LIMIT=0 turns the first unsuccessful hand-off poll of the
-    single-launch panel QR into a timeout (as when its workgroups cannot all be
+    """With Householder panels (GPMI_BAND_PANEL=hh), GPMI_HH_SPIN_LIMIT=0 turns the
+    first unsuccessful hand-off poll of the single-launch panel QR into a timeout (as when its workgroups cannot all be
     resident): the reduction is redone with per-column launches, the result is
     the same band form, and a later refresh starts clean (err flag reset)."""
+    monkeypatch.setenv('GPMI_BAND_PANEL', 'hh')   # the Householder panel
     K, X, z = _inputs(1000, 77)
     ref = _mc(K)
     ld_ref, G_ref = ref.loglik_terms([0.05, 2.0], X, z)
+    assert ref.band().stats()['panel'] == 'householder'
     assert ref.band().stats()['panel_fallbacks'] == 0
     assert ref.band().stats()['panel_maxg'] >= 8
     monkeypatch.setenv('GPMI_HH_SPIN_LIMIT', '0')
@@ -402,3 +412,63 @@ def test_cfg3_nu25_n16384_dense_and_band_vs_reference(gp):
         assert rel(ld, cfg['logdet']) < 1e-9, op.imate_method
         lp = DirectLikelihood.log_likelihood_batch(z, X, op, cfg['hypers'])
         assert rel(lp, cfg['direct_lp']) < 1e-8, op.imate_method
+
+
+@pytest.mark.parametrize('n', [129, 300, 1000, 2304])
+def test_cholqr_panel_matches_householder_panel(gp, n, monkeypatch):
+    """The CholeskyQR panel (shifted CholeskyQR3 + Householder reconstruction,
+    gpmi_cholqr.hip; the default) and the Householder panel give the same band
+    reduction up to rounding: logdet, the Gram blocks and the spectrum."""
+    K, X, z = _inputs(n, 3 * n, nu=2.5)
+    etas = [1e-3, 0.05, 2.0]
+    op = _mc(K)
+    ld, G = op.loglik_terms(etas, X, z)
+    st = op.band().stats()
+    assert st['panel'] == 'cholqr' and st['cholqr_fallbacks'] == 0, st
+    assert st['cholqr_panel_fallbacks'] == 0, st
+    monkeypatch.setenv('GPMI_BAND_PANEL', 'hh')
+    oh = _mc(K)
+    ld_h, G_h = oh.loglik_terms(etas, X, z)
+    assert oh.band().stats()['panel'] == 'householder'
+    assert rel(ld, ld_h) < 1e-12
+    numpy.testing.assert_allclose(G, G_h, rtol=1e-9, atol=1e-11 * numpy.abs(G_h).max())
+    lam = numpy.linalg.eigvalsh(op.band().band())
+    lam_h = numpy.linalg.eigvalsh(oh.band().band())
+    assert numpy.max(numpy.abs(lam - lam_h)) <= 1e-12 * numpy.abs(lam_h).max()
+
+
+def test_cholqr_breakdown_falls_back_to_householder(gp):
+    """A rank-deficient panel (K = I + a rank-one block: the first panel has rank
+    one) breaks the CholeskyQR passes down before anything is written to it; the
+    guarded Householder panel factors it on the device (no second reduction) and
+    the values stay exact."""
+    n = 700
+    rng = numpy.random.RandomState(5)
+    u = numpy.zeros(n)
+    u[:200] = rng.rand(200)
+    K = numpy.eye(n) + numpy.outer(u, u)
+    R = numpy.column_stack([numpy.ones(n), rng.randn(n)])
+    op = _mc(K)
+    etas = [0.1, 1.0]
+    ld, G = op.loglik_terms(etas, R[:, :1], R[:, 1])
+    st = op.band().stats()
+    assert st['cholqr_panel_fallbacks'] >= 1 and st['cholqr_fallbacks'] == 0, st
+    for e, l, g in zip(etas, ld, G):
+        M = K + e * numpy.eye(n)
+        assert rel(l, numpy.linalg.slogdet(M)[1]) < 1e-12
+        numpy.testing.assert_allclose(g, R.T @ numpy.linalg.solve(M, R), rtol=1e-10)
+
+
+@pytest.mark.parametrize('nu', [0.5, 100.0])
+def test_band_rough_and_gaussian_kernels(gp, nu):
+    """Matern 1/2 (rough) and the Gaussian limit (nu >= 100: smooth, numerically
+    low-rank panels, where CholeskyQR may fall back): logdet and Gram vs the
+    oracle whichever panel ran."""
+    K, X, z = _inputs(1000, 11, nu=nu)
+    op = _mc(K)
+    ref = OracleMC(K, 'cholesky')
+    R = numpy.column_stack([X, z])
+    for e in (0.05, 1.0):
+        ld, G = op.loglik_terms([e], X, z)
+        assert rel(ld[0], ref.logdet(e)) < 1e-10, (nu, e)
+        numpy.testing.assert_allclose(G[0], R.T @ ref.solve(e, R), rtol=1e-7, atol=1e-9)
