@@ -112,7 +112,8 @@ struct gpmi_band {
   // and inverses, the reconstruction's U^-T, V1, signs, scratch, failure flag
   int panel_mode = 0;        // 0 CholeskyQR, 1 Householder (single launch)
   int cq_fallbacks = 0;      // reductions redone with Householder panels
-  int cq_la_grid = 0;        // SYR2K grid cap beside a CholeskyQR panel (0: none)
+  int cq_la_grid = 448;      // SYR2K grid cap beside a CholeskyQR panel (0: none; measured
+                             // at N = 16384: 448 161-163 ms, none 165-168, no look-ahead 164-166)
   double* Qb = nullptr;
   double* cqpart = nullptr;
   double* cqG = nullptr;

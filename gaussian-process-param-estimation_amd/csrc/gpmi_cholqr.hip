@@ -44,7 +44,19 @@
 #include "gpmi_band.h"
 #include "gpmi_tile.h"
 
+#ifndef GPMI_CQ_STAMPS
+#define GPMI_CQ_STAMPS 0   // probe builds: phase stamps of one cq_recon_kernel call (printf)
+#endif
+
 namespace gpmi {
+
+#if GPMI_CQ_STAMPS
+__device__ int g_cq_calls;
+#define CQST(i) \
+  if (cst) cs[i] = wall_clock64()
+#else
+#define CQST(i)
+#endif
 
 constexpr double CQ_TOL = 1e-2;   // third pass: max |L3 - I| accepted
 
@@ -228,14 +240,18 @@ __global__ __launch_bounds__(256, 2) void cq_gram_kernel(const double* __restric
 __global__ __launch_bounds__(256) void cq_reduce_kernel(const double* __restrict__ part, int np,
                                                         double* __restrict__ G) {
   const int e = blockIdx.x * 256 + threadIdx.x;   // < GPK
-  double s0 = 0.0, s1 = 0.0;
+  // eight partial sums (p mod 8), their loads in flight together; fixed order
+  double acc[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
   int p = 0;
-  for (; p + 1 < np; p += 2) {
-    s0 += part[(int64_t)p * GPK + e];
-    s1 += part[(int64_t)(p + 1) * GPK + e];
+  for (; p + 8 <= np; p += 8) {
+    double x[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) x[q] = part[(int64_t)(p + q) * GPK + e];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc[q] += x[q];
   }
-  if (p < np) s0 += part[(int64_t)p * GPK + e];
-  const double v = s0 + s1;
+  for (int q = 0; p + q < np; ++q) acc[q] += part[(int64_t)(p + q) * GPK + e];
+  const double v = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
   int ti, tj;
   tri_tile(e >> 8, &ti, &tj);
   const int r = ti * 16 + ((e >> 4) & 15), c = tj * 16 + (e & 15);
@@ -321,8 +337,8 @@ __global__ __launch_bounds__(256, 2) void cq_apply_kernel(const double* Src, int
 // pass's Q) the third factor M3 = L3^-1 (exact LDS Cholesky, or first order when
 // ||G3 - I||_F <= tau_fo), then Q3's top block Q3t = Q2t M3^T, then the LU without
 // pivoting of Q3t - S, S_ii = -sign of the running pivot, blocked by 16 in LDS:
-//   per column block: the tall panel (rows j0.., 16 columns) on wave 0 with the
-//   rows in registers (pivot row by readlane), U12 = L11^-1 A12 by forward
+//   per column block: the tall panel (rows j0.., 16 columns) with the rows in
+//   registers over the four waves (pivot rows by readlane), U12 = L11^-1 A12 by forward
 //   substitution (one thread per column), then A22 -= L21 U12 on fp64 MFMA.
 // Outputs: V1 (strictly lower: the Householder vectors' top rows, into the top
 // block of the panel P), S, tau = -diag(U) S, L3 / M3 (Lx3 / Linv3, for
@@ -351,6 +367,12 @@ __global__ __launch_bounds__(256) void cq_recon_kernel(const double* __restrict_
   const int wr = w >> 1, wc = w & 1;
   // an earlier pass failed: leave the panel untouched for the Householder panel
   if (__hip_atomic_load(fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+#if GPMI_CQ_STAMPS
+  unsigned long long cs[10] = {0};
+  bool cst = false;
+  if (t == 0) cst = atomicAdd(&g_cq_calls, 1) == 20;
+#endif
+  CQST(0);
   if (t == 0) s_fail = 0;
   // ---- M3 = L3^-1 into A (lower) and Linv3
   d2 v[32];
@@ -396,10 +418,12 @@ __global__ __launch_bounds__(256) void cq_recon_kernel(const double* __restrict_
     if (t == 0) fo[2] = 0;
   }
   __syncthreads();
+  CQST(1);
   for (int e = t; e < TS * TS; e += 256) {
     const int r = e >> 7, c = e & 127;
     Linv3[e] = (c <= r) ? A[r * DL + c] : 0.0;
   }
+  CQST(2);
   // ---- Q3t = Q2t M3^T: wave (wr, wc) forms rows wr*64.., columns wc*64..; the
   // A operand straight from global (L2), M3 from LDS (lower: k <= column)
   {
@@ -429,17 +453,19 @@ __global__ __launch_bounds__(256) void cq_recon_kernel(const double* __restrict_
     store_tile(A, DL, acc, 1.0);
   }
   __syncthreads();
+  CQST(3);
   for (int jb = 0; jb < NDB; ++jb) {
     const int j0 = jb * DB;
-    // ---- tall panel: rows j0 + lane and j0 + 64 + lane, columns j0 .. j0 + 15
-    if (w == 0) {
-      const int ra = j0 + lane, rb = j0 + 64 + lane;
-      double pa[DB], pb[DB];
+    // ---- tall panel (columns j0 .. j0 + 15) on all four waves: lanes 0-15 of every
+    // wave hold the diagonal block's rows (each wave factors them redundantly, so
+    // the pivot rows come by readlane, no exchange), lanes 16-63 hold rows
+    // j0 + 16 + 4 (lane - 16) + w below it
+    {
+      const int row = lane < DB ? j0 + lane : j0 + DB + 4 * (lane - DB) + w;
+      const bool live = row < TS;
+      double pa[DB];
 #pragma unroll
-      for (int k = 0; k < DB; ++k) {
-        pa[k] = ra < TS ? A[ra * DL + j0 + k] : 0.0;
-        pb[k] = rb < TS ? A[rb * DL + j0 + k] : 0.0;
-      }
+      for (int k = 0; k < DB; ++k) pa[k] = live ? A[row * DL + j0 + k] : 0.0;
 #pragma unroll
       for (int j = 0; j < DB; ++j) {
         double prow[DB];
@@ -455,34 +481,34 @@ __global__ __launch_bounds__(256) void cq_recon_kernel(const double* __restrict_
 #pragma unroll
           for (int k = j + 1; k < DB; ++k) pa[k] -= l * prow[k];
         }
-        {
-          const double l = pb[j] * rinv;
-          pb[j] = l;
-#pragma unroll
-          for (int k = j + 1; k < DB; ++k) pb[k] -= l * prow[k];
-        }
-        if (lane == 0) sS[j0 + j] = s;
+        if (w == 0 && lane == 0) sS[j0 + j] = s;
       }
+      __syncthreads();   // every wave read its rows before any wave writes back
+      if (live && (lane >= DB || w == 0)) {
 #pragma unroll
-      for (int k = 0; k < DB; ++k) {
-        if (ra < TS) A[ra * DL + j0 + k] = pa[k];
-        if (rb < TS) A[rb * DL + j0 + k] = pb[k];
+        for (int k = 0; k < DB; ++k) A[row * DL + j0 + k] = pa[k];
       }
     }
     __syncthreads();
     if (jb + 1 == NDB) break;
-    // ---- U12 = L11^-1 A12: one thread per column right of the block
+    // ---- U12 = L11^-1 A12: one thread per column right of the block; L11 (120
+    // values, the same for every thread) read from LDS up front, not inside the
+    // dependent substitution chain
     {
       const int c = j0 + DB + t;
       if (c < TS) {
-        double x[DB];
+        double x[DB], l11[DB * (DB - 1) / 2];
 #pragma unroll
         for (int r = 0; r < DB; ++r) x[r] = A[(j0 + r) * DL + c];
+#pragma unroll
+        for (int r = 1; r < DB; ++r)
+#pragma unroll
+          for (int p = 0; p < r; ++p) l11[r * (r - 1) / 2 + p] = A[(j0 + r) * DL + j0 + p];
 #pragma unroll
         for (int r = 1; r < DB; ++r) {
           double s = x[r];
 #pragma unroll
-          for (int p = 0; p < r; ++p) s -= A[(j0 + r) * DL + j0 + p] * x[p];
+          for (int p = 0; p < r; ++p) s -= l11[r * (r - 1) / 2 + p] * x[p];
           x[r] = s;
         }
 #pragma unroll
@@ -510,6 +536,7 @@ __global__ __launch_bounds__(256) void cq_recon_kernel(const double* __restrict_
     }
     __syncthreads();
   }
+  CQST(4);
   // V1 (strictly lower, into the panel's top block) and the signs / tau out
   for (int e = t; e < TS * TS; e += 256) {
     const int r = e >> 7, c = e & 127;
@@ -528,10 +555,12 @@ __global__ __launch_bounds__(256) void cq_recon_kernel(const double* __restrict_
     if (r > c) A[r * DL + c] = A[c * DL + r];
   }
   __syncthreads();
+  CQST(5);
   lds_diag_inv_lower(A, Aux);
   __syncthreads();
   lds_inv_block(A, Aux);
   __syncthreads();
+  CQST(6);
   // ---- C = U^-T M3 (lower x lower): A operand from LDS, M3 from global (Linv3,
   // written above by this workgroup)
   {
@@ -561,6 +590,13 @@ __global__ __launch_bounds__(256) void cq_recon_kernel(const double* __restrict_
     }
     store_tile(C, TS, acc, 1.0);
   }
+#if GPMI_CQ_STAMPS
+  CQST(7);
+  if (cst)
+    printf("cq_recon (10ns): M3 %llu  Linv3 %llu  Q3t %llu  LU %llu  V1/U^T %llu  inv %llu  C %llu\n",
+           cs[1] - cs[0], cs[2] - cs[1], cs[3] - cs[2], cs[4] - cs[3], cs[5] - cs[4],
+           cs[6] - cs[5], cs[7] - cs[6]);
+#endif
 }
 
 // The top 128 x 128 block above the diagonal of every CholeskyQR panel, one
