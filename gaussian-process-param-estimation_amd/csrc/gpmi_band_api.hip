@@ -354,7 +354,7 @@ int band_reduce_pass(gpmi_band* b, const double* K, const std::vector<double>* y
   BD_TRY(hipEventRecord(b->ev0, s));
   if (yh) {
     BD_TRY(hipMemcpyAsync(b->Y, yh->data(), sizeof(double) * yh->size(), hipMemcpyHostToDevice,
-                          b->qs));
+                          b->qs ? b->qs : b->side));
   }
   BD_TRY(hipMemcpyAsync(b->Ab, K, sizeof(double) * np * np, hipMemcpyDeviceToDevice, s));
   const bool la = mode != 2 && b->lookahead && b->s_pan;
@@ -388,8 +388,11 @@ int band_reduce_pass(gpmi_band* b, const double* K, const std::vector<double>* y
     BD_LAUNCH("tbuild_kernel");
     BD_TRY(hipEventRecord(b->ev_t, b->side));
     if (yh) {
-      BD_TRY(hipStreamWaitEvent(b->qs, b->ev_t, 0));
-      int rc = qt_panel(b, j, b->qs);
+      // Q_j^T on the side stream right after T_j (default), or on a stream of its
+      // own (GPMI_BAND_QS=1)
+      hipStream_t qst = b->qs ? b->qs : b->side;
+      if (b->qs) BD_TRY(hipStreamWaitEvent(b->qs, b->ev_t, 0));
+      int rc = qt_panel(b, j, qst);
       if (rc) return rc;
     }
     const int chunk = symm_chunk(mt);
@@ -444,7 +447,7 @@ int band_reduce_pass(gpmi_band* b, const double* K, const std::vector<double>* y
     }
   }
   if (yh) {
-    BD_TRY(hipEventRecord(b->ev_q, b->qs));
+    BD_TRY(hipEventRecord(b->ev_q, b->qs ? b->qs : b->side));
     BD_TRY(hipStreamWaitEvent(s, b->ev_q, 0));
   }
   if (mode == 0 && nt > 1) {
@@ -552,7 +555,8 @@ int gpmi_band_create(gpmi_op* op, gpmi_band** out) {
   if ((e = hipEventCreate(&b->ev1)) != hipSuccess) return fail(e, "event");
   if ((e = hipStreamCreateWithFlags(&b->side, hipStreamNonBlocking)) != hipSuccess)
     return fail(e, "side stream");
-  if ((e = hipStreamCreateWithFlags(&b->qs, hipStreamNonBlocking)) != hipSuccess)
+  if (std::getenv("GPMI_BAND_QS") && std::atoi(std::getenv("GPMI_BAND_QS")) &&
+      (e = hipStreamCreateWithFlags(&b->qs, hipStreamNonBlocking)) != hipSuccess)
     return fail(e, "rhs stream");
   if (const char* la = std::getenv("GPMI_BAND_LA")) b->lookahead = std::atoi(la);
   if (const char* lg = std::getenv("GPMI_BAND_LA_GRID")) b->la_grid = std::max(0, std::atoi(lg));
