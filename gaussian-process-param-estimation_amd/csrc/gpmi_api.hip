@@ -640,12 +640,10 @@ int gpmi_op_create(int device, int64_t n, int max_batch, gpmi_op** out) {
   hipError_t e;
   if ((e = hipStreamCreateWithFlags(&op->stream, hipStreamNonBlocking)) != hipSuccess)
     return fail(e, "stream");
-  {
-    int lo = 0, hi = 0;
-    if ((e = hipDeviceGetStreamPriorityRange(&lo, &hi)) != hipSuccess) return fail(e, "priority");
-    if ((e = hipStreamCreateWithPriority(&op->stream2, hipStreamNonBlocking, hi)) != hipSuccess)
-      return fail(e, "stream2");
-  }
+  // op->stream2 (look-ahead) is created by gpmi_op_set_lookahead(op, 1) only: HIP
+  // streams beyond the process's hardware queues (GPU_MAX_HW_QUEUES = 4) share
+  // queues and slow other objects' multi-stream work (a band reduction beside a dense
+  // operator holding three streams: 161 -> 181 ms)
   if ((e = hipEventCreateWithFlags(&op->ev_fork, hipEventDisableTiming)) != hipSuccess)
     return fail(e, "event");
   if ((e = hipEventCreateWithFlags(&op->ev_join, hipEventDisableTiming)) != hipSuccess)
@@ -795,6 +793,13 @@ int gpmi_op_loglik_batch(gpmi_op* op, const double* etas, int neta, double* logd
   HIP_TRY(hipMemcpyAsync(hinfo.data(), op->info, sizeof(int) * neta, hipMemcpyDeviceToHost,
                          op->stream));
   HIP_TRY(hipStreamSynchronize(op->stream));
+  // the batch-halves stream is joined and idle: release it, so that it does not hold
+  // one of the process's hardware queues while other objects run (a band reduction
+  // after a batch-8 call here: 181 ms with it alive, 162 ms without)
+  if (op->stream3) {
+    HIP_TRY(hipStreamDestroy(op->stream3));
+    op->stream3 = nullptr;
+  }
   rc = collect_timing(op);
   if (rc) return rc;
   const int m = op->nrhs;
@@ -1033,6 +1038,14 @@ int gpmi_op_last_timing(gpmi_op* op, double* syrk_ms, int* syrk_launches, double
 
 int gpmi_op_set_lookahead(gpmi_op* op, int enable) {
   if (!op) return set_err(-1006, "null handle");
+  if (enable && !op->stream2) {
+    DeviceGuard g(op->device);
+    int lo = 0, hi = 0;
+    hipError_t e;
+    if ((e = hipDeviceGetStreamPriorityRange(&lo, &hi)) != hipSuccess ||
+        (e = hipStreamCreateWithPriority(&op->stream2, hipStreamNonBlocking, hi)) != hipSuccess)
+      return set_err(-(int)e, "look-ahead stream: %s", hipGetErrorString(e));
+  }
   op->lookahead = enable != 0;
   return 0;
 }

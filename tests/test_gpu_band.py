@@ -472,3 +472,28 @@ def test_band_rough_and_gaussian_kernels(gp, nu):
         ld, G = op.loglik_terms([e], X, z)
         assert rel(ld[0], ref.logdet(e)) < 1e-10, (nu, e)
         numpy.testing.assert_allclose(G[0], R.T @ ref.solve(e, R), rtol=1e-7, atol=1e-9)
+
+
+@pytest.mark.slow
+def test_cholqr_breakdown_past_single_launch_panel_redoes_reduction(gp):
+    """n = 16640 (the first panel has 129 row blocks, past the guarded single-launch
+    Householder panel) with a rank-one first panel: the CholeskyQR breakdown makes
+    the host redo the whole reduction with Householder panels (per-column launches
+    there), and the values stay exact (K = I + u u^T: logdet = log(1 + eta + |u|^2)
+    + (n - 1) log(1 + eta))."""
+    from gaussian_proc._mixed_correlation import MixedCorrelation
+    n = 16640
+    rng = numpy.random.RandomState(9)
+    u = numpy.zeros(n)
+    u[:300] = rng.rand(300)
+    K = numpy.eye(n) + numpy.outer(u, u)
+    op = MixedCorrelation(K, imate_method='eigenvalue')
+    etas = [0.1, 2.0]
+    X = numpy.ones((n, 1))
+    z = rng.randn(n)
+    ld, _ = op.loglik_terms(etas, X, z)
+    st = op.band().stats()
+    assert st['cholqr_fallbacks'] == 1, st
+    uu = u @ u
+    for e, l in zip(etas, ld):
+        assert rel(l, numpy.log(1 + e + uu) + (n - 1) * numpy.log(1 + e)) < 1e-12

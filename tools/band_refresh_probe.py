@@ -9,6 +9,10 @@ sys.path[:0] = [REPO, os.path.join(REPO, 'gaussian-process-param-estimation_amd'
 from gaussian_proc import generate_correlation, _data  # noqa: E402
 from gaussian_proc._mixed_correlation import MixedCorrelation  # noqa: E402
 
+if os.environ.get('PROBE_TORCH') == '1':   # a torch HIP context beside ours (as bench.py)
+    import torch
+    torch.cuda.set_device(0)
+    torch.cuda.synchronize()
 grid = int(sys.argv[1]) if len(sys.argv) > 1 else 128
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 2
 pts = _data.generate_points(grid, 2, True)
