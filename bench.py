@@ -85,7 +85,10 @@ def pmc_traffic(outer, batch, kernel='gpmi::syrk_kernel'):
     if not files:
         return None, None
     with open(files[-1]) as fh:
-        k = json.load(fh)['kernels'].get(kernel)
+        kernels = json.load(fh)['kernels']
+    # template instances appear as 'void gpmi::name<20>'
+    k = kernels.get(kernel) or next((v for key, v in kernels.items()
+                                     if key.replace('void ', '').split('<')[0] == kernel), None)
     if not k:
         return None, None
     # per_dispatch_first: only the timed call's launches (the run's later
@@ -104,7 +107,10 @@ def pmc_traffic_sparse(config, kernel='gpmi::csr_spmm_kernel'):
     if not files:
         return None, None
     with open(files[-1]) as fh:
-        k = json.load(fh)['kernels'].get(kernel)
+        kernels = json.load(fh)['kernels']
+    # template instances appear as 'void gpmi::name<20>'
+    k = kernels.get(kernel) or next((v for key, v in kernels.items()
+                                     if key.replace('void ', '').split('<')[0] == kernel), None)
     if not k or 'per_dispatch_last' not in k:
         return None, None
     pd = k['per_dispatch_last']
@@ -361,7 +367,7 @@ def run_sparse(args, world, rank, local, dist, torch):
     alg_bytes = 12.0 * nnz + 8.0 * (n + 1) + 16.0 * n * s_blk
     gbs = alg_bytes / (ms * 1e-3) / 1e9
     info = op.sop.spmm_info()
-    sp_kernel = 'csr_spmm_win_kernel' if info['windowed'] else 'csr_spmm_kernel'
+    sp_kernel = op.sop.spmm_kernel(s_blk)
     gather_bytes = (8.0 * s_blk * info['mean_window'] * ((n + 63) // 64) if info['windowed']
                     else 8.0 * nnz * s_blk)
     sp_traffic, sp_tsrc = (pmc_traffic_sparse(args.config, 'gpmi::' + sp_kernel)

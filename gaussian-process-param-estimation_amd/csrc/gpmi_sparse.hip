@@ -241,6 +241,88 @@ __global__ __launch_bounds__(256) void csr_spmm_win_kernel(
   }
 }
 
+// The windowed SpMM in ONE pass over all S columns (S a compile-time width: the
+// Lanczos probe block s = 20; at the multi-shift CG width 11 the 8-column chunks
+// measured faster): the block's window rows
+// of X staged at full width (u x S doubles), then thread (row r = t / 4, column
+// group g = t % 4) sums its row for ceil(S / 4) columns, reading each nonzero's
+// value and window position once for all of them (the 8-column chunks of
+// csr_spmm_win_kernel re-read them per column and stage three times).
+template <int S>
+__global__ __launch_bounds__(256) void csr_spmm_winf_kernel(
+    const int64_t* __restrict__ indptr, const int* __restrict__ indices,
+    const unsigned short* __restrict__ lidx, const double* __restrict__ data, int64_t n,
+    const int* __restrict__ wcols, const int* __restrict__ ucount,
+    const double* __restrict__ X, double* __restrict__ Y, double eta) {
+  extern __shared__ double smem[];
+  constexpr int CG = (S + 3) / 4;
+  const int t = threadIdx.x;
+  const int64_t b = xcd_remap(blockIdx.x, gridDim.x);
+  const int64_t r0 = b * WIN_ROWS, r1 = min(r0 + WIN_ROWS, n);
+  const int nr = (int)(r1 - r0);
+  const int u = ucount[b];
+  const int r = t >> 2, g = t & 3, c0 = g * CG;
+  if (u == 0) {
+    // window over its limits: gather straight from X
+    if (r < nr) {
+      const int64_t row = r0 + r;
+      double acc[CG];
+#pragma unroll
+      for (int j = 0; j < CG; ++j) acc[j] = 0.0;
+      for (int64_t k = indptr[row]; k < indptr[row + 1]; ++k) {
+        const double v = data[k];
+        const double* xr = X + (int64_t)indices[k] * S;
+#pragma unroll
+        for (int j = 0; j < CG; ++j)
+          if (c0 + j < S) acc[j] += v * xr[c0 + j];
+      }
+#pragma unroll
+      for (int j = 0; j < CG; ++j)
+        if (c0 + j < S) Y[row * S + c0 + j] = acc[j] + eta * X[row * S + c0 + j];
+    }
+    return;
+  }
+  const int64_t k0 = indptr[r0];
+  const int m = (int)(indptr[r1] - k0);
+  double* win = smem;                                    // [u][S]
+  double* sval = win + (size_t)u * S;                    // [m]
+  unsigned short* slix = reinterpret_cast<unsigned short*>(sval + m);   // [m]
+  int* srow = reinterpret_cast<int*>(slix + ((m + 1) & ~1));            // [WIN_ROWS + 1]
+  for (int i = t; i < m; i += 256) {
+    sval[i] = data[k0 + i];
+    slix[i] = lidx[k0 + i];
+  }
+  if (t <= nr) srow[t] = (int)(indptr[r0 + t] - k0);
+  const int* wc = wcols + b * WIN_MAXU;
+  for (int i = t; i < u * S; i += 256) {
+    const int e = i / S, cj = i - e * S;
+    win[i] = X[(int64_t)wc[e] * S + cj];
+  }
+  __syncthreads();
+  if (r < nr) {
+    const int ka = srow[r], kb = srow[r + 1];
+    double acc[CG];
+#pragma unroll
+    for (int j = 0; j < CG; ++j) acc[j] = 0.0;
+    for (int k = ka; k < kb; ++k) {
+      const double v = sval[k];
+      const double* wr = win + slix[k] * S + c0;
+#pragma unroll
+      for (int j = 0; j < CG; ++j)
+        if (c0 + j < S) acc[j] += v * wr[j];
+    }
+    const int64_t row = r0 + r;
+#pragma unroll
+    for (int j = 0; j < CG; ++j)
+      if (c0 + j < S) Y[row * S + c0 + j] = acc[j] + eta * X[row * S + c0 + j];
+  }
+}
+
+template __global__ void csr_spmm_winf_kernel<20>(const int64_t*, const int*,
+                                                  const unsigned short*, const double*, int64_t,
+                                                  const int*, const int*, const double*, double*,
+                                                  double);
+
 // partial[b][j][c] = sum over this block's rows of A_j[i][c] * B[i][c],
 // A_j = A + j * strideA, j = blockIdx.y; grid-stride over rows.
 __global__ __launch_bounds__(256) void col_dot_partial_kernel(const double* __restrict__ A,

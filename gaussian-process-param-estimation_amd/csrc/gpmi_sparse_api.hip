@@ -37,6 +37,10 @@ __global__ void spmm_window_build_kernel(const int64_t*, const int*, int64_t, in
 __global__ void csr_spmm_win_kernel(const int64_t*, const int*, const unsigned short*,
                                     const double*, int64_t, const int*, const int*, const double*,
                                     int64_t, double*, int64_t, int, double);
+template <int S>
+__global__ void csr_spmm_winf_kernel(const int64_t*, const int*, const unsigned short*,
+                                     const double*, int64_t, const int*, const int*,
+                                     const double*, double*, double);
 constexpr int WIN_ROWS_HOST = 64;    // = WIN_ROWS (gpmi_sparse.hip)
 constexpr int WIN_MAXU_HOST = 1024;  // = WIN_MAXU
 constexpr int WIN_CS_HOST = 8;       // = WIN_CS
@@ -221,14 +225,40 @@ int ensure_window(gpmi_sp* sp) {
   return 0;
 }
 
-int spmm(gpmi_sp* sp, const double* X, double* Y, int s, double eta) {
-  // GPMI_SPMM_WINDOW: 0 the gather-from-X kernel, 2 the windowed kernel, unset or 1
-  // the faster one for this matrix (win_use)
+// The SpMM kernel for an s-column block (0 gather, 1 windowed chunks, 2 windowed
+// full width). GPMI_SPMM_WINDOW: 0 the gather-from-X kernel, 2 the windowed kernel,
+// unset or 1 the faster one for this matrix (win_use); GPMI_SPMM_FULL=0 keeps the
+// 8-column chunks at s = 20.
+int spmm_kind(gpmi_sp* sp, int s, int* kind) {
   const char* wenv = std::getenv("GPMI_SPMM_WINDOW");
   const int wmode = wenv ? std::atoi(wenv) : 1;
   if (wmode != 0 && sp->win_maxu < 0)
     if (int rc = ensure_window(sp)) return rc;
+  *kind = 0;
   if (wmode == 2 || (wmode != 0 && sp->win_use)) {
+    *kind = 1;
+    const char* fenv = std::getenv("GPMI_SPMM_FULL");
+    const size_t lds = sizeof(double) * (size_t)s * (size_t)std::max(1, sp->win_maxu) +
+                       10 * (size_t)sp->win_maxm + 4 + sizeof(int) * (WIN_ROWS_HOST + 1);
+    if (s == 20 && !(fenv && std::atoi(fenv) == 0) && lds <= 64 * 1024) *kind = 2;
+  }
+  return 0;
+}
+
+int spmm(gpmi_sp* sp, const double* X, double* Y, int s, double eta) {
+  int kind = 0;
+  if (int rc = spmm_kind(sp, s, &kind)) return rc;
+  if (kind == 2) {
+    // the one-pass full-width window (csr_spmm_winf_kernel) at the Lanczos width
+    const size_t lds = sizeof(double) * (size_t)s * (size_t)std::max(1, sp->win_maxu) +
+                       10 * (size_t)sp->win_maxm + 4 + sizeof(int) * (WIN_ROWS_HOST + 1);
+    hipLaunchKernelGGL(csr_spmm_winf_kernel<20>, dim3((unsigned)sp->win_nblk), dim3(256), lds,
+                       sp->stream, sp->indptr, sp->indices, sp->win_lidx, sp->data, sp->n,
+                       sp->win_cols, sp->win_u, X, Y, eta);
+    SP_LAUNCH("csr_spmm_winf_kernel");
+    return 0;
+  }
+  if (kind == 1) {
     // window + the largest windowed block's values, positions and row starts
     const size_t lds = sizeof(double) * WIN_CS_HOST * (size_t)std::max(1, sp->win_maxu) +
                        10 * (size_t)sp->win_maxm + 4 + sizeof(int) * (WIN_ROWS_HOST + 1);
@@ -968,6 +998,12 @@ int gpmi_sp_spmm_info(gpmi_sp* sp, int* windowed, double* mean_window, int* max_
   if (mean_window) *mean_window = sp->win_mean;
   if (max_window) *max_window = sp->win_maxu;
   return 0;
+}
+
+int gpmi_sp_spmm_kernel(gpmi_sp* sp, int s, int* kind) {
+  if (!sp || !kind) return set_error(-1006, "null handle");
+  Guard g(sp->device);
+  return spmm_kind(sp, s, kind);
 }
 
 int gpmi_sp_last_status(const gpmi_sp* sp, int* converged) {

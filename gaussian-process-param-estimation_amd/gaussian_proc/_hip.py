@@ -94,6 +94,7 @@ SIGNATURES = {
     'gpmi_band_chase_info': (ctypes.c_int, [c_op_p, c_int_p, c_int_p, c_int_p]),
     'gpmi_sp_last_status': (ctypes.c_int, [c_op_p, c_int_p]),
     'gpmi_sp_spmm_info': (ctypes.c_int, [c_op_p, c_int_p, c_double_p, c_int_p]),
+    'gpmi_sp_spmm_kernel': (ctypes.c_int, [c_op_p, ctypes.c_int, c_int_p]),
     'gpmi_band_last_timing': (ctypes.c_int, [c_op_p, c_double_p, c_double_p, c_double_p]),
 }
 
@@ -551,6 +552,15 @@ class SparseOperator(object):
         check(self.lib.gpmi_sp_spmm_info(self.h, ctypes.byref(w), ctypes.byref(mw),
                                          ctypes.byref(xw)), 'gpmi_sp_spmm_info')
         return dict(windowed=bool(w.value), mean_window=mw.value, max_window=xw.value)
+
+    def spmm_kernel(self, s):
+        """-> the SpMM kernel an s-column block runs: 'csr_spmm_kernel' (gather),
+        'csr_spmm_win_kernel' (window, 8-column chunks) or 'csr_spmm_winf_kernel'
+        (window, one full-width pass) (see gpmi_sp_spmm_kernel)."""
+        k = ctypes.c_int()
+        check(self.lib.gpmi_sp_spmm_kernel(self.h, int(s), ctypes.byref(k)),
+              'gpmi_sp_spmm_kernel')
+        return ('csr_spmm_kernel', 'csr_spmm_win_kernel', 'csr_spmm_winf_kernel')[k.value]
 
     def lanczos(self, nprobe, steps, seed=0, probe_offset=0):
         """-> alpha[nprobe, steps], beta[nprobe, steps] (beta = 0 ends a tridiagonal)."""

@@ -191,6 +191,11 @@ int gpmi_sp_msgram(gpmi_sp* sp, const double* etas, int neta, const double* rhs,
  * 0: gathers from X, one wave per row) and its window sizes (columns per block:
  * mean, max). */
 int gpmi_sp_spmm_info(gpmi_sp* sp, int* windowed, double* mean_window, int* max_window);
+/* The SpMM kernel gpmi_sp_spmm runs for an s-column block on this operator:
+ * 0 gather from X (csr_spmm_kernel), 1 X-window in 8-column chunks
+ * (csr_spmm_win_kernel), 2 X-window in one full-width pass (csr_spmm_winf_kernel,
+ * s = 20). Diagnostic; no reference counterpart. */
+int gpmi_sp_spmm_kernel(gpmi_sp* sp, int s, int* kind);
 /* Whether the last gpmi_sp_cg / gpmi_sp_msgram met rtol in every column before
  * maxiter (1) or stopped at maxiter (0). scipy's cg, which the reference calls
  * (_linear_solver.py:64,68), returns the unconverged iterate silently; the
