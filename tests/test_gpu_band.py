@@ -497,3 +497,22 @@ def test_cholqr_breakdown_past_single_launch_panel_redoes_reduction(gp):
     uu = u @ u
     for e, l in zip(etas, ld):
         assert rel(l, numpy.log(1 + e + uu) + (n - 1) * numpy.log(1 + e)) < 1e-12
+
+
+def test_band_reduction_variants_agree(gp, monkeypatch):
+    """The default reduction (CholeskyQR panels with first-order passes, look-ahead
+    with the capped SYR2K grid) equals the one without look-ahead bit for bit (same
+    kernels, same summation orders; only the overlap differs) and the one with an
+    exact Cholesky in every pass (GPMI_CQ_FO=0) to rounding."""
+    K, X, z = _inputs(2304, 41, nu=1.5, scale=0.1)
+    etas = [1e-3, 0.1, 10.0]
+    ld0, G0 = _mc(K).loglik_terms(etas, X, z)
+    monkeypatch.setenv('GPMI_BAND_LA', '0')
+    ld1, G1 = _mc(K).loglik_terms(etas, X, z)
+    numpy.testing.assert_array_equal(ld0, ld1)
+    numpy.testing.assert_array_equal(G0, G1)
+    monkeypatch.delenv('GPMI_BAND_LA')
+    monkeypatch.setenv('GPMI_CQ_FO', '0')
+    ld2, G2 = _mc(K).loglik_terms(etas, X, z)
+    assert rel(ld0, ld2) < 1e-12
+    numpy.testing.assert_allclose(G0, G2, rtol=1e-9, atol=1e-11 * numpy.abs(G2).max())
