@@ -262,7 +262,7 @@ int cq_panel(gpmi_band* b, int j, hipStream_t st) {
   hipLaunchKernelGGL(cq_gram_kernel, dim3(rt), dim3(256), CQ_DYN_LDS, st, P, np, b->cqpart);
   BD_LAUNCH("cq_gram_kernel");
   for (int pass = 0; pass < 2; ++pass) {
-    hipLaunchKernelGGL(cq_reduce_kernel, dim3(CQ_GPK / 256), dim3(256), 0, st, b->cqpart, rt,
+    hipLaunchKernelGGL(cq_reduce_kernel, dim3(CQ_GPK / 64), dim3(256), 0, st, b->cqpart, rt,
                        b->cqG);
     BD_LAUNCH("cq_reduce_kernel");
     double* L = b->cqL + pt + (int64_t)pass * TS * TS;
@@ -276,7 +276,7 @@ int cq_panel(gpmi_band* b, int j, hipStream_t st) {
                        nullptr);
     BD_LAUNCH("cq_apply_kernel");
   }
-  hipLaunchKernelGGL(cq_reduce_kernel, dim3(CQ_GPK / 256), dim3(256), 0, st, b->cqpart, rt,
+  hipLaunchKernelGGL(cq_reduce_kernel, dim3(CQ_GPK / 64), dim3(256), 0, st, b->cqpart, rt,
                      b->cqG);
   BD_LAUNCH("cq_reduce_kernel");
   // third factor, reconstruction: V1 into P, tau, S, C = U^-T M3

@@ -236,27 +236,34 @@ __global__ __launch_bounds__(256, 2) void cq_gram_kernel(const double* __restric
 }
 
 // G (128 x 128, symmetric, row-major) = sum over the np packed partials, fixed
-// order; each packed element is written to both mirror positions.
+// order; 64 packed elements per workgroup, each summed by its four waves over the
+// partials p = w (mod 4) (eight loads in flight per lane), the four sums combined in
+// a fixed order; each element is written to both mirror positions.
 __global__ __launch_bounds__(256) void cq_reduce_kernel(const double* __restrict__ part, int np,
                                                         double* __restrict__ G) {
-  const int e = blockIdx.x * 256 + threadIdx.x;   // < GPK
-  // eight partial sums (p mod 8), their loads in flight together; fixed order
+  __shared__ double red[4][64];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int e = blockIdx.x * 64 + lane;   // < GPK
   double acc[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-  int p = 0;
-  for (; p + 8 <= np; p += 8) {
+  int p = w;
+  for (; p + 28 < np; p += 32) {
     double x[8];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) x[q] = part[(int64_t)(p + q) * GPK + e];
+    for (int q = 0; q < 8; ++q) x[q] = part[(int64_t)(p + 4 * q) * GPK + e];
 #pragma unroll
     for (int q = 0; q < 8; ++q) acc[q] += x[q];
   }
-  for (int q = 0; p + q < np; ++q) acc[q] += part[(int64_t)(p + q) * GPK + e];
-  const double v = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
-  int ti, tj;
-  tri_tile(e >> 8, &ti, &tj);
-  const int r = ti * 16 + ((e >> 4) & 15), c = tj * 16 + (e & 15);
-  G[r * TS + c] = v;
-  G[c * TS + r] = v;
+  for (int q = 0; p < np; p += 4, ++q) acc[q] += part[(int64_t)p * GPK + e];
+  red[w][lane] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+  __syncthreads();
+  if (w == 0) {
+    const double v = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+    int ti, tj;
+    tri_tile(e >> 8, &ti, &tj);
+    const int r = ti * 16 + ((e >> 4) & 15), c = tj * 16 + (e & 15);
+    G[r * TS + c] = v;
+    G[c * TS + r] = v;
+  }
 }
 
 // Dst[tile] = Src[tile] M^T for the 64-row tile blockIdx.x (M lower, row-major):
