@@ -377,14 +377,27 @@ __global__ __launch_bounds__(256, 2) void tn_partial_kernel(const double* __rest
   store_tile(part + (int64_t)ch * TS * TS, TS, acc, 1.0);
 }
 
-// out = scale * sum_ch part[ch] (128 x 128), fixed order.
+// out = scale * sum_ch part[ch] (128 x 128), fixed order: 64 elements per
+// workgroup, each summed by its four waves over ch = w (mod 4) (eight loads in
+// flight per lane), the four sums combined in a fixed order.
 __global__ __launch_bounds__(256) void tn_reduce_kernel(const double* __restrict__ part, int nch,
                                                         double* __restrict__ out, double scale) {
-  const int e = blockIdx.x * 256 + threadIdx.x;
-  double s = 0.0;
-#pragma unroll 8
-  for (int c = 0; c < nch; ++c) s += part[(int64_t)c * TS * TS + e];
-  out[e] = scale * s;
+  __shared__ double red[4][64];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int e = blockIdx.x * 64 + lane;
+  double acc[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  int c = w;
+  for (; c + 28 < nch; c += 32) {
+    double x[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) x[q] = part[(int64_t)(c + 4 * q) * TS * TS + e];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc[q] += x[q];
+  }
+  for (int q = 0; c < nch; c += 4, ++q) acc[q] += part[(int64_t)c * TS * TS + e];
+  red[w][lane] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+  __syncthreads();
+  if (w == 0) out[e] = scale * ((red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]));
 }
 
 // Compact-WY T (upper) of the panel's 128 reflectors, one workgroup:
@@ -455,8 +468,19 @@ __global__ __launch_bounds__(256) void psum_kernel(const double* __restrict__ Xp
   const int il = blockIdx.y;
   const int e = (blockIdx.x * 256 + threadIdx.x) * 2;
   d2 s = {0.0, 0.0};
-  for (int c = 0; c < nch; ++c)
-    s += *reinterpret_cast<const d2*>(Xp + ((int64_t)il * nch + c) * TS * TS + e);
+  // the split-K partials' loads in flight eight at a time, summed in order (the
+  // same sums as one load at a time)
+  for (int c0 = 0; c0 < nch; c0 += 8) {
+    d2 x[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      x[q] = c0 + q < nch
+                 ? *reinterpret_cast<const d2*>(Xp + ((int64_t)il * nch + c0 + q) * TS * TS + e)
+                 : d2{0.0, 0.0};
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      if (c0 + q < nch) s += x[q];
+  }
   *reinterpret_cast<d2*>(X + (int64_t)il * TS * TS + e) = s;
 }
 

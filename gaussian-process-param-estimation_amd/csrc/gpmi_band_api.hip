@@ -381,7 +381,7 @@ int band_reduce_pass(gpmi_band* b, const double* K, const std::vector<double>* y
     hipLaunchKernelGGL(tn_partial_kernel, dim3(nch), dim3(256), 0, b->side, Ur + TS,
                        (int64_t)BAND_ULD, Ur + TS, (int64_t)BAND_ULD, m, b->tnp2);
     BD_LAUNCH("tn_partial_kernel");
-    hipLaunchKernelGGL(tn_reduce_kernel, dim3(TS * TS / 256), dim3(256), 0, b->side, b->tnp2,
+    hipLaunchKernelGGL(tn_reduce_kernel, dim3(TS * TS / 64), dim3(256), 0, b->side, b->tnp2,
                        nch, b->VtV, 1.0);
     BD_LAUNCH("tn_reduce_kernel");
     hipLaunchKernelGGL(tbuild_kernel, dim3(1), dim3(256), 0, b->side, b->VtV, tau, T);
@@ -408,7 +408,7 @@ int band_reduce_pass(gpmi_band* b, const double* K, const std::vector<double>* y
     hipLaunchKernelGGL(tn_partial_kernel, dim3(nch), dim3(256), 0, s, Ur + TS,
                        (int64_t)BAND_ULD, b->X, (int64_t)TS, m, b->tnp);
     BD_LAUNCH("tn_partial_kernel");
-    hipLaunchKernelGGL(tn_reduce_kernel, dim3(TS * TS / 256), dim3(256), 0, s, b->tnp, nch, b->M,
+    hipLaunchKernelGGL(tn_reduce_kernel, dim3(TS * TS / 64), dim3(256), 0, s, b->tnp, nch, b->M,
                        1.0);
     BD_LAUNCH("tn_reduce_kernel");
     hipLaunchKernelGGL(z_kernel, dim3(1), dim3(256), 0, s, T, b->M, b->Zh);
