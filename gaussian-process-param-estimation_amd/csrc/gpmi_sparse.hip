@@ -25,22 +25,32 @@ namespace gpmi {
 // slots are summed with shuffles in a fixed order. (Runs of rows per wave with
 // the next row prefetched measured 1.5x slower: fewer waves in flight.) The gathers (nnz * s doubles) come from
 // L2 / MALL; HBM sees the CSR arrays once.
+// The SPMM_UNR gathers of a lane are issued before any of their products (the
+// predicate on the load only): cfg 5 172 -> 140 us per s = 20 launch; eight in flight
+// measured slower (194 us).
+#ifndef GPMI_SPMM_UNR
+#define GPMI_SPMM_UNR 4   // gathers in flight per lane
+#endif
+constexpr int SPMM_UNR = GPMI_SPMM_UNR;
 __device__ __forceinline__ void spmm_chunk(const int myidx, const double myval, int cnt,
                                            const double* __restrict__ X, int64_t ldx, int slots,
                                            int slot, int c, bool on, double (&acc)[4]) {
   // wave-uniform trip count: every lane takes part in every ds_bpermute
-  for (int jb = 0; jb < cnt; jb += 4 * slots) {
-    int ix[4];
-    double vx[4];
+  for (int jb = 0; jb < cnt; jb += SPMM_UNR * slots) {
+    int ix[SPMM_UNR];
+    double vx[SPMM_UNR], g[SPMM_UNR];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < SPMM_UNR; ++u) {
       const int j = (jb + u * slots + slot) & 63;
       ix[u] = __shfl(myidx, j);
       vx[u] = __shfl(myval, j);
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
-      if (on && jb + u * slots + slot < cnt) acc[u] += vx[u] * X[(int64_t)ix[u] * ldx + c];
+    for (int u = 0; u < SPMM_UNR; ++u)
+      g[u] = (on && jb + u * slots + slot < cnt) ? X[(int64_t)ix[u] * ldx + c] : 0.0;
+#pragma unroll
+    for (int u = 0; u < SPMM_UNR; ++u)
+      if (on && jb + u * slots + slot < cnt) acc[u & 3] += vx[u] * g[u];
   }
 }
 
