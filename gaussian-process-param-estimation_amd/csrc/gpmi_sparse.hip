@@ -314,7 +314,25 @@ __global__ __launch_bounds__(256) void csr_spmm_winf_kernel(
     double acc[CG];
 #pragma unroll
     for (int j = 0; j < CG; ++j) acc[j] = 0.0;
-    for (int k = ka; k < kb; ++k) {
+    // four nonzeros' values, positions and window entries loaded before their products
+    // (22.7 vs 24.0 us per cfg 4 launch)
+    int k = ka;
+    for (; k + 4 <= kb; k += 4) {
+      double v[4], x[4][CG];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        v[q] = sval[k + q];
+        const double* wr = win + slix[k + q] * S + c0;
+#pragma unroll
+        for (int j = 0; j < CG; ++j) x[q][j] = (c0 + j < S) ? wr[j] : 0.0;
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int j = 0; j < CG; ++j)
+          if (c0 + j < S) acc[j] += v[q] * x[q][j];
+    }
+    for (; k < kb; ++k) {
       const double v = sval[k];
       const double* wr = win + slix[k] * S + c0;
 #pragma unroll
