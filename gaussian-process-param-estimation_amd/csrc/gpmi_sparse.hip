@@ -81,6 +81,65 @@ __global__ __launch_bounds__(256) void csr_spmm_kernel(const int64_t* __restrict
   if (slot == 0) Y[row * ldy + c] = tot + eta * X[row * ldx + c];
 }
 
+// The gather kernel with a lane reading a column pair (16-byte loads): h = s/2 lanes
+// per nonzero, slots = 64 / h nonzeros at a time, so a wave instruction covers twice
+// the nonzeros of csr_spmm_kernel. Needs s even and X, Y 16-byte aligned with ld = s
+// (the host checks); same per-column summation order as csr_spmm_kernel.
+__global__ __launch_bounds__(256) void csr_spmm_pair_kernel(const int64_t* __restrict__ indptr,
+                                                            const int* __restrict__ indices,
+                                                            const double* __restrict__ data,
+                                                            int64_t n, const double* __restrict__ X,
+                                                            double* __restrict__ Y, int s,
+                                                            int slots, double eta) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t row = (int64_t)xcd_remap(blockIdx.x, gridDim.x) * 4 + wv;
+  if (row >= n) return;
+  const int h = s >> 1;
+  const int slot = lane / h;
+  const int c = lane - slot * h;
+  const bool on = slot < slots;
+  const double2* __restrict__ X2 = reinterpret_cast<const double2*>(X);
+  const int64_t k0 = indptr[row], k1 = indptr[row + 1];
+  double ax[4] = {0.0, 0.0, 0.0, 0.0}, ay[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int64_t kb = k0; kb < k1; kb += 64) {
+    const int cnt = (int)((k1 - kb) < 64 ? (k1 - kb) : 64);
+    const int myidx = lane < cnt ? indices[kb + lane] : 0;
+    const double myval = lane < cnt ? data[kb + lane] : 0.0;
+    for (int jb = 0; jb < cnt; jb += SPMM_UNR * slots) {
+      int ix[SPMM_UNR];
+      double vx[SPMM_UNR];
+      double2 g[SPMM_UNR];
+#pragma unroll
+      for (int u = 0; u < SPMM_UNR; ++u) {
+        const int j = (jb + u * slots + slot) & 63;
+        ix[u] = __shfl(myidx, j);
+        vx[u] = __shfl(myval, j);
+      }
+#pragma unroll
+      for (int u = 0; u < SPMM_UNR; ++u)
+        g[u] = (on && jb + u * slots + slot < cnt) ? X2[(int64_t)ix[u] * h + c]
+                                                    : make_double2(0.0, 0.0);
+#pragma unroll
+      for (int u = 0; u < SPMM_UNR; ++u)
+        if (on && jb + u * slots + slot < cnt) {
+          ax[u & 3] += vx[u] * g[u].x;
+          ay[u & 3] += vx[u] * g[u].y;
+        }
+    }
+  }
+  const double px = (ax[0] + ax[1]) + (ax[2] + ax[3]);
+  const double py = (ay[0] + ay[1]) + (ay[2] + ay[3]);
+  double tx = 0.0, ty = 0.0;
+  for (int u = 0; u < slots; ++u) {
+    tx += __shfl(px, (c + u * h) & 63);
+    ty += __shfl(py, (c + u * h) & 63);
+  }
+  if (slot == 0) {
+    const double2 xr = X2[row * h + c];
+    reinterpret_cast<double2*>(Y)[row * h + c] = make_double2(tx + eta * xr.x, ty + eta * xr.y);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // X-window SpMM (default). Rows in blocks of WIN_ROWS (64, consecutive in the
 // locality order); a block's nonzeros reference a compact set of columns (its

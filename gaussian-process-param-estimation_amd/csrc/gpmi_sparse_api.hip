@@ -32,6 +32,8 @@ __global__ void csr_cell_fill_kernel(const double*, int64_t, int, const double*,
 constexpr int CELL_CAP_HOST = 512;   // = CELL_CAP (gpmi_matern.hip)
 __global__ void csr_spmm_kernel(const int64_t*, const int*, const double*, int64_t, const double*,
                                 int64_t, double*, int64_t, int, int, double);
+__global__ void csr_spmm_pair_kernel(const int64_t*, const int*, const double*, int64_t,
+                                     const double*, double*, int, int, double);
 __global__ void spmm_window_build_kernel(const int64_t*, const int*, int64_t, int*, int*,
                                          unsigned short*);
 __global__ void csr_spmm_win_kernel(const int64_t*, const int*, const unsigned short*,
@@ -226,9 +228,11 @@ int ensure_window(gpmi_sp* sp) {
 }
 
 // The SpMM kernel for an s-column block (0 gather, 1 windowed chunks, 2 windowed
-// full width). GPMI_SPMM_WINDOW: 0 the gather-from-X kernel, 2 the windowed kernel,
-// unset or 1 the faster one for this matrix (win_use); GPMI_SPMM_FULL=0 keeps the
-// 8-column chunks at s = 20.
+// full width, 3 gather by column pairs). GPMI_SPMM_WINDOW: 0 the gather-from-X
+// kernel, 2 the windowed kernel, unset or 1 the faster one for this matrix
+// (win_use); GPMI_SPMM_FULL=0 keeps the 8-column chunks at s = 20; GPMI_SPMM_PAIR=0
+// keeps the one-column gather for even s (the pair kernel also needs 16-byte
+// aligned blocks, else the one-column gather runs).
 int spmm_kind(gpmi_sp* sp, int s, int* kind) {
   const char* wenv = std::getenv("GPMI_SPMM_WINDOW");
   const int wmode = wenv ? std::atoi(wenv) : 1;
@@ -242,6 +246,8 @@ int spmm_kind(gpmi_sp* sp, int s, int* kind) {
                        10 * (size_t)sp->win_maxm + 4 + sizeof(int) * (WIN_ROWS_HOST + 1);
     if (s == 20 && !(fenv && std::atoi(fenv) == 0) && lds <= 64 * 1024) *kind = 2;
   }
+  const char* penv = std::getenv("GPMI_SPMM_PAIR");
+  if (*kind == 0 && s % 2 == 0 && s <= 64 && !(penv && std::atoi(penv) == 0)) *kind = 3;
   return 0;
 }
 
@@ -267,6 +273,14 @@ int spmm(gpmi_sp* sp, const double* X, double* Y, int s, double eta) {
                        dim3(256), lds, sp->stream, sp->indptr, sp->indices, sp->win_lidx, sp->data,
                        sp->n, sp->win_cols, sp->win_u, X, (int64_t)s, Y, (int64_t)s, s, eta);
     SP_LAUNCH("csr_spmm_win_kernel");
+    return 0;
+  }
+  if (kind == 3 && (reinterpret_cast<uintptr_t>(X) & 15) == 0 &&
+      (reinterpret_cast<uintptr_t>(Y) & 15) == 0) {
+    hipLaunchKernelGGL(csr_spmm_pair_kernel, dim3((unsigned)((sp->n + 3) / 4)), dim3(256), 0,
+                       sp->stream, sp->indptr, sp->indices, sp->data, sp->n, X, Y, s,
+                       64 / (s / 2), eta);
+    SP_LAUNCH("csr_spmm_pair_kernel");
     return 0;
   }
   hipLaunchKernelGGL(csr_spmm_kernel, dim3((unsigned)((sp->n + 3) / 4)), dim3(256), 0,

@@ -555,12 +555,14 @@ class SparseOperator(object):
 
     def spmm_kernel(self, s):
         """-> the SpMM kernel an s-column block runs: 'csr_spmm_kernel' (gather),
-        'csr_spmm_win_kernel' (window, 8-column chunks) or 'csr_spmm_winf_kernel'
-        (window, one full-width pass) (see gpmi_sp_spmm_kernel)."""
+        'csr_spmm_win_kernel' (window, 8-column chunks), 'csr_spmm_winf_kernel'
+        (window, one full-width pass) or 'csr_spmm_pair_kernel' (gather by column
+        pairs) (see gpmi_sp_spmm_kernel)."""
         k = ctypes.c_int()
         check(self.lib.gpmi_sp_spmm_kernel(self.h, int(s), ctypes.byref(k)),
               'gpmi_sp_spmm_kernel')
-        return ('csr_spmm_kernel', 'csr_spmm_win_kernel', 'csr_spmm_winf_kernel')[k.value]
+        return ('csr_spmm_kernel', 'csr_spmm_win_kernel', 'csr_spmm_winf_kernel',
+                'csr_spmm_pair_kernel')[k.value]
 
     def lanczos(self, nprobe, steps, seed=0, probe_offset=0):
         """-> alpha[nprobe, steps], beta[nprobe, steps] (beta = 0 ends a tridiagonal)."""

@@ -194,7 +194,9 @@ int gpmi_sp_spmm_info(gpmi_sp* sp, int* windowed, double* mean_window, int* max_
 /* The SpMM kernel gpmi_sp_spmm runs for an s-column block on this operator:
  * 0 gather from X (csr_spmm_kernel), 1 X-window in 8-column chunks
  * (csr_spmm_win_kernel), 2 X-window in one full-width pass (csr_spmm_winf_kernel,
- * s = 20). Diagnostic; no reference counterpart. */
+ * s = 20), 3 gather from X by column pairs (csr_spmm_pair_kernel, even s; a block
+ * that is not 16-byte aligned runs csr_spmm_kernel). Diagnostic; no reference
+ * counterpart. */
 int gpmi_sp_spmm_kernel(gpmi_sp* sp, int s, int* kind);
 /* Whether the last gpmi_sp_cg / gpmi_sp_msgram met rtol in every column before
  * maxiter (1) or stopped at maxiter (0). scipy's cg, which the reference calls

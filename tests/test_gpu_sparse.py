@@ -82,7 +82,8 @@ def test_window_spmm_equals_gather_spmm(gp, monkeypatch):
     one-wave-per-row gather kernel and scipy, for s = 1 .. 32
     columns, on a matrix whose first blocks overflow the window limits (more
     than 4096 nonzeros, more than 1024 distinct columns) and so take the
-    gather path inside the same launch."""
+    gather path inside the same launch. For even s the gather is the column-pair
+    kernel; GPMI_SPMM_PAIR=0 gives the one-column gather to compare with."""
     from gaussian_proc import _hip
     rng = numpy.random.RandomState(4)
     n = 3000
@@ -108,10 +109,16 @@ def test_window_spmm_equals_gather_spmm(gp, monkeypatch):
         Yw = sop.spmm(0.3, X)
         monkeypatch.setenv('GPMI_SPMM_WINDOW', '0')
         Yg = sop.spmm(0.3, X)
+        monkeypatch.setenv('GPMI_SPMM_PAIR', '0')
+        Y1 = sop.spmm(0.3, X)
+        assert sop.spmm_kernel(s) == 'csr_spmm_kernel'
+        monkeypatch.delenv('GPMI_SPMM_PAIR')
+        assert sop.spmm_kernel(s) == ('csr_spmm_pair_kernel' if s % 2 == 0 else 'csr_spmm_kernel')
         monkeypatch.delenv('GPMI_SPMM_WINDOW')
         ref = A @ X + 0.3 * X
         assert _nrel(Yw, ref) < 1e-13, s
         assert _nrel(Yw, Yg) < 1e-13, s
+        assert _nrel(Y1, Yg) < 1e-13, s
 
 
 def _nrel(a, b):
