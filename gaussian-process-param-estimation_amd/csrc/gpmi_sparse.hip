@@ -84,7 +84,8 @@ __global__ __launch_bounds__(256) void csr_spmm_kernel(const int64_t* __restrict
 // The gather kernel with a lane reading a column pair (16-byte loads): h = s/2 lanes
 // per nonzero, slots = 64 / h nonzeros at a time, so a wave instruction covers twice
 // the nonzeros of csr_spmm_kernel. Needs s even and X, Y 16-byte aligned with ld = s
-// (the host checks); same per-column summation order as csr_spmm_kernel.
+// (the host checks). Fixed summation order (not csr_spmm_kernel's: the slots differ).
+template <int U>
 __global__ __launch_bounds__(256) void csr_spmm_pair_kernel(const int64_t* __restrict__ indptr,
                                                             const int* __restrict__ indices,
                                                             const double* __restrict__ data,
@@ -105,22 +106,22 @@ __global__ __launch_bounds__(256) void csr_spmm_pair_kernel(const int64_t* __res
     const int cnt = (int)((k1 - kb) < 64 ? (k1 - kb) : 64);
     const int myidx = lane < cnt ? indices[kb + lane] : 0;
     const double myval = lane < cnt ? data[kb + lane] : 0.0;
-    for (int jb = 0; jb < cnt; jb += SPMM_UNR * slots) {
-      int ix[SPMM_UNR];
-      double vx[SPMM_UNR];
-      double2 g[SPMM_UNR];
+    for (int jb = 0; jb < cnt; jb += U * slots) {
+      int ix[U];
+      double vx[U];
+      double2 g[U];
 #pragma unroll
-      for (int u = 0; u < SPMM_UNR; ++u) {
+      for (int u = 0; u < U; ++u) {
         const int j = (jb + u * slots + slot) & 63;
         ix[u] = __shfl(myidx, j);
         vx[u] = __shfl(myval, j);
       }
 #pragma unroll
-      for (int u = 0; u < SPMM_UNR; ++u)
+      for (int u = 0; u < U; ++u)
         g[u] = (on && jb + u * slots + slot < cnt) ? X2[(int64_t)ix[u] * h + c]
                                                     : make_double2(0.0, 0.0);
 #pragma unroll
-      for (int u = 0; u < SPMM_UNR; ++u)
+      for (int u = 0; u < U; ++u)
         if (on && jb + u * slots + slot < cnt) {
           ax[u & 3] += vx[u] * g[u].x;
           ay[u & 3] += vx[u] * g[u].y;
@@ -139,6 +140,13 @@ __global__ __launch_bounds__(256) void csr_spmm_pair_kernel(const int64_t* __res
     reinterpret_cast<double2*>(Y)[row * h + c] = make_double2(tx + eta * xr.x, ty + eta * xr.y);
   }
 }
+
+template __global__ void csr_spmm_pair_kernel<2>(const int64_t*, const int*, const double*, int64_t,
+                                                const double*, double*, int, int, double);
+template __global__ void csr_spmm_pair_kernel<3>(const int64_t*, const int*, const double*, int64_t,
+                                                const double*, double*, int, int, double);
+template __global__ void csr_spmm_pair_kernel<4>(const int64_t*, const int*, const double*, int64_t,
+                                                const double*, double*, int, int, double);
 
 // ---------------------------------------------------------------------------
 // X-window SpMM (default). Rows in blocks of WIN_ROWS (64, consecutive in the

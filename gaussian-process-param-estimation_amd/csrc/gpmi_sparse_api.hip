@@ -32,6 +32,7 @@ __global__ void csr_cell_fill_kernel(const double*, int64_t, int, const double*,
 constexpr int CELL_CAP_HOST = 512;   // = CELL_CAP (gpmi_matern.hip)
 __global__ void csr_spmm_kernel(const int64_t*, const int*, const double*, int64_t, const double*,
                                 int64_t, double*, int64_t, int, int, double);
+template <int U>
 __global__ void csr_spmm_pair_kernel(const int64_t*, const int*, const double*, int64_t,
                                      const double*, double*, int, int, double);
 __global__ void spmm_window_build_kernel(const int64_t*, const int*, int64_t, int*, int*,
@@ -277,9 +278,13 @@ int spmm(gpmi_sp* sp, const double* X, double* Y, int s, double eta) {
   }
   if (kind == 3 && (reinterpret_cast<uintptr_t>(X) & 15) == 0 &&
       (reinterpret_cast<uintptr_t>(Y) & 15) == 0) {
-    hipLaunchKernelGGL(csr_spmm_pair_kernel, dim3((unsigned)((sp->n + 3) / 4)), dim3(256), 0,
-                       sp->stream, sp->indptr, sp->indices, sp->data, sp->n, X, Y, s,
-                       64 / (s / 2), eta);
+    // gathers in flight per lane (GPMI_SPMM_PUNR: 2, 3 or 4)
+    const char* uenv = std::getenv("GPMI_SPMM_PUNR");
+    const int u = uenv ? std::atoi(uenv) : 4;
+    auto kfn = u == 2 ? csr_spmm_pair_kernel<2> : u == 3 ? csr_spmm_pair_kernel<3>
+                                                           : csr_spmm_pair_kernel<4>;
+    hipLaunchKernelGGL(kfn, dim3((unsigned)((sp->n + 3) / 4)), dim3(256), 0, sp->stream,
+                       sp->indptr, sp->indices, sp->data, sp->n, X, Y, s, 64 / (s / 2), eta);
     SP_LAUNCH("csr_spmm_pair_kernel");
     return 0;
   }
