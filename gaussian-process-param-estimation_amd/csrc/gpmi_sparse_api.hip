@@ -278,9 +278,9 @@ int spmm(gpmi_sp* sp, const double* X, double* Y, int s, double eta) {
   }
   if (kind == 3 && (reinterpret_cast<uintptr_t>(X) & 15) == 0 &&
       (reinterpret_cast<uintptr_t>(Y) & 15) == 0) {
-    // gathers in flight per lane (GPMI_SPMM_PUNR: 2, 3 or 4)
+    // gathers in flight per lane (GPMI_SPMM_PUNR: 2, 3 or 4; 3 measured fastest at cfg 5)
     const char* uenv = std::getenv("GPMI_SPMM_PUNR");
-    const int u = uenv ? std::atoi(uenv) : 4;
+    const int u = uenv ? std::atoi(uenv) : 3;
     auto kfn = u == 2 ? csr_spmm_pair_kernel<2> : u == 3 ? csr_spmm_pair_kernel<3>
                                                            : csr_spmm_pair_kernel<4>;
     hipLaunchKernelGGL(kfn, dim3((unsigned)((sp->n + 3) / 4)), dim3(256), 0, sp->stream,
