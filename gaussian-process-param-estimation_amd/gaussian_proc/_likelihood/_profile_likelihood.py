@@ -148,14 +148,20 @@ class ProfileLikelihood(object):
     @staticmethod
     def find_log_likelihood_der1_zeros(z, X, K_mixed, interval_eta, tol=1e-6,
                                        max_iterations=100, num_bracket_trials=3,
-                                       group=None):  # :244-415
+                                       group=False, speculative=None):  # :244-415
         """Root of d lp / d eta in log10(eta) (reference :244-415: bracket search,
         then Chandrupatla, then the optimal sigma). The der1 evaluations are
         batched: the bracket search requests every point it may need next in one
         call (_root_finding.find_interval_with_sign_change_batched), sharded over
-        the ranks of a torch.distributed ``group`` when one is initialised
-        (sweep.der1_sweep: one all-gather per batch). Decisions and results are
-        those of the sequential reference driver."""
+        the ranks of a torch.distributed ``group`` when the caller passes one
+        (sweep.der1_sweep: one all-gather per batch; every rank must hold the
+        same K, X, z, so sharding is opt-in: the default False keeps the search
+        on the local device). Chandrupatla's iterations are speculative: each
+        device call also evaluates up to ``speculative`` points the next
+        iterations may need (_root_finding._chandrupatla_candidates; default 64
+        on the band operator, where a batch of eta costs one banded Cholesky's
+        latency, else 0). Decisions and results are those of the sequential
+        reference driver."""
         n, m = X.shape
 
         def optimal_sigma(eta):
@@ -173,11 +179,14 @@ class ProfileLikelihood(object):
             return numpy.sqrt(numpy.dot(z, z - v) / (n - m))
 
         from ..sweep import der1_sweep
-        fb = BatchedFunction(lambda le: der1_sweep(K_mixed, X, z, le, group=group))
+        if speculative is None:
+            speculative = 64 if _use_band(K_mixed) else 0
+        fb = BatchedFunction(lambda le: der1_sweep(K_mixed, X, z, le, group=group),
+                             spec_budget=speculative)
         print('Find root of log likelihood derivative ...')
         bracket = [numpy.log10(interval_eta[0]), numpy.log10(interval_eta[1])]
         found, bracket, values = find_interval_with_sign_change_batched(
-            fb, bracket, num_bracket_trials)
+            fb, bracket, num_bracket_trials, tol=tol)
         if found:
             res = chandrupatla_method(fb, bracket, values, verbose=False, eps_m=tol,
                                       eps_a=tol, maxiter=max_iterations)

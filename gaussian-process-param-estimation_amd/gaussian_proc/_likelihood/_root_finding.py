@@ -24,28 +24,65 @@ __all__ = ['find_interval_with_sign_change', 'chandrupatla_method', 'BatchedFunc
 
 class BatchedFunction(object):
     """Scalar view f(x) of a batched function fb(xs) -> values, memoised by the
-    exact float x. ``request(xs)`` evaluates the missing points of xs in one
-    call of fb; ``f(x)`` returns a cached value or evaluates x alone.
-    ``calls`` counts the batched calls, ``points`` the evaluated points."""
+    exact float x. ``request(xs, speculative)`` evaluates the missing points of
+    xs, plus the missing speculative points, in one call of fb (at most
+    ``spec_budget`` of them per call; 0 turns speculation off); ``f(x)``
+    returns a cached value or evaluates x alone. ``calls`` counts the batched
+    calls, ``points`` the evaluated points.
 
-    def __init__(self, fb):
+    Speculative points are ones the sequential reference may never evaluate
+    (an outward bracket probe, a candidate of the next Chandrupatla step). A
+    speculative point must not change what the caller sees: when the combined
+    call raises (``LinAlgError``: K + eta I not positive definite at one of the
+    speculative eta) the required points are evaluated again on their own, and
+    a non-finite speculative value is not memoised (a later request evaluates
+    it as a required point, so any error it causes surfaces where the
+    reference's would)."""
+
+    def __init__(self, fb, spec_budget=64):
         self.fb = fb
+        self.spec_budget = spec_budget
         self.memo = {}
         self.calls = 0
         self.points = 0
+        self.spec_failures = 0
 
-    def request(self, xs):
+    def _missing(self, xs, skip=()):
         miss = []
         for x in xs:
             x = float(x)
-            if x not in self.memo and x not in miss:
+            if x not in self.memo and x not in miss and x not in skip:
                 miss.append(x)
-        if miss:
-            vals = self.fb(numpy.array(miss))
-            self.calls += 1
-            self.points += len(miss)
-            for x, v in zip(miss, vals):
-                self.memo[x] = float(v)
+        return miss
+
+    def _eval(self, miss):
+        vals = self.fb(numpy.array(miss))
+        self.calls += 1
+        self.points += len(miss)
+        return [float(v) for v in vals]
+
+    def request(self, xs, speculative=()):
+        miss = self._missing(xs)
+        spec = self._missing(speculative, skip=miss)[:self.spec_budget]
+        if not miss:
+            # nothing is needed yet: prefetching alone would be a call the
+            # reference does not make
+            return
+        if spec:
+            try:
+                vals = self._eval(miss + spec)
+            except numpy.linalg.LinAlgError:
+                self.spec_failures += 1
+                vals = None
+            if vals is not None:
+                for x, v in zip(miss, vals[:len(miss)]):
+                    self.memo[x] = v
+                for x, v in zip(spec, vals[len(miss):]):
+                    if numpy.isfinite(v):
+                        self.memo[x] = v
+                return
+        for x, v in zip(miss, self._eval(miss)):
+            self.memo[x] = v
 
     def __call__(self, x, *args):
         x = float(x)
@@ -63,16 +100,23 @@ def _outward(x0, x1, f0, f1):
     return x0 * (1.0 - t) + x1 * t
 
 
-def find_interval_with_sign_change_batched(fb, bracket, num_bracket_trials):
+def find_interval_with_sign_change_batched(fb, bracket, num_bracket_trials, tol=None):
     """find_interval_with_sign_change (:21-148) with batched evaluations.
-    ``fb`` is a BatchedFunction. Call 1: x0, x1, the first trial's midpoint,
-    both of its possible outward probes, and the first Chandrupatla point
-    (:155-309, t = 0.5 from a = x1) of [x0, x1]; each later trial: its midpoint
-    and its outward probe together."""
+    ``fb`` is a BatchedFunction. Call 1: x0, x1, and speculatively the first
+    trial's midpoint, both of its possible outward probes and the first
+    Chandrupatla point (:155-309, t = 0.5 from a = x1) of [x0, x1] (with
+    ``tol``, the Chandrupatla eps_m = eps_a, also the candidate tree that
+    follows it, _chandrupatla_candidates); each later
+    trial: its midpoint, and its outward probe speculatively."""
     x0, x1 = float(bracket[0]), float(bracket[1])
     xm = _mid(x0, x1)
-    fb.request([x0, x1, xm, x0 * (1.0 - 1.5) + x1 * 1.5, x0 * (1.0 + 0.5) + x1 * -0.5,
-                x1 + 0.5 * (x0 - x1)])
+    spec = [xm, x0 * (1.0 - 1.5) + x1 * 1.5, x0 * (1.0 + 0.5) + x1 * -0.5]
+    xt = x1 + 0.5 * (x0 - x1)
+    spec.append(xt)
+    if tol is not None:
+        spec += _chandrupatla_candidates(x1, x0, x1, xt, tol, tol,
+                                         max(0, fb.spec_budget - len(spec)))
+    fb.request([x0, x1], speculative=spec)
 
     def f(x):
         return fb(x)
@@ -81,7 +125,7 @@ def find_interval_with_sign_change_batched(fb, bracket, num_bracket_trials):
         if numpy.sign(f0) != numpy.sign(f1):
             return True, [x0, x1], [f0, f1]
         xm = _mid(x0, x1)
-        fb.request([xm, _outward(x0, x1, f0, f1)])
+        fb.request([xm], speculative=[_outward(x0, x1, f0, f1)])
         print('bracket was not found. Search for bracket. Iteration: %d' % it)
         print('x0: %0.2f, f0: %0.16f' % (x0, f0))
         print('x1: %0.2f, f1: %0.16f' % (x1, f1))
@@ -152,6 +196,40 @@ def find_interval_with_sign_change(f, bracket, num_bracket_trials, args=()):
     return False, [x0, x1], [f0, f1]
 
 
+def _chandrupatla_candidates(a, b, c, xt, eps_m, eps_a, budget):
+    """Points later iterations of chandrupatla_method can evaluate whatever
+    f(xt) turns out to be, except interior inverse-quadratic ones, breadth
+    first (at most ``budget``). For either sign of f(xt) (which fixes the new
+    b, c) and either of the new a = xt, b as the smaller-|f| end xm (which
+    fixes tlim): the bisection point t = 0.5 and the two clamped steps
+    t = tlim, 1 - tlim, each formed by the same float expression as the
+    iteration itself (a + t (b - a)); then the same from each of those points.
+    The bracketing chain of the first iterations is bisections, and near the
+    root every step is clamped, so these cover most non-IQI iterations."""
+    out, seen = [], set()
+    level = [(a, b, c, xt)]
+    while level and len(out) < budget:
+        nxt = []
+        for a0, b0, c0, x0 in level:
+            for same in (True, False):
+                bn, cn = (b0, a0) if same else (a0, b0)
+                for xm in (x0, bn):
+                    tol = 2 * eps_m * numpy.abs(xm) + eps_a
+                    tlim = tol / numpy.abs(bn - cn)
+                    if not tlim <= 0.5:
+                        continue
+                    for t in (0.5, tlim, 1 - tlim):
+                        t = min(1 - tlim, max(tlim, t))
+                        xn = x0 + t * (bn - x0)
+                        if float(xn) in seen:
+                            continue
+                        seen.add(float(xn))
+                        out.append(xn)
+                        nxt.append((x0, bn, cn, xn))
+        level = nxt
+    return out[:budget]
+
+
 def chandrupatla_method(f, bracket, bracket_values, verbose=False, eps_m=None, eps_a=None,
                         maxiter=50, args=()):
     b, a = float(bracket[0]), float(bracket[1])
@@ -167,9 +245,14 @@ def chandrupatla_method(f, bracket, bracket_values, verbose=False, eps_m=None, e
     t = 0.5
     iterations = 0
     xm = b
+    budget = getattr(f, 'spec_budget', 0) if isinstance(f, BatchedFunction) and not args \
+        else 0
     while maxiter > 0:
         maxiter -= 1
         xt = a + t * (b - a)
+        if budget > 0 and float(xt) not in f.memo:
+            f.request([xt], speculative=_chandrupatla_candidates(a, b, c, xt, eps_m, eps_a,
+                                                                 budget))
         ft = f(xt, *args)
         if numpy.sign(ft) == numpy.sign(fa):
             c, fc = a, fa

@@ -60,22 +60,41 @@ def _all_gather_rows(dist, group, local, world):
     return t_all.cpu().numpy()
 
 
-def der1_sweep(K_mixed, X, z, log_etas, group=None):
+def der1_sweep(K_mixed, X, z, log_etas, group=False):
     """ProfileLikelihood.log_likelihood_der1_eta (_profile_likelihood.py:91-132)
     at many log10(eta): each rank evaluates its contiguous block in one batched
     call (band Gram blocks on the eigenvalue operator), ONE all-gather collects
-    them. Returns der1[len(log_etas)] on every rank."""
+    them. Returns der1[len(log_etas)] on every rank.
+
+    Sharding is opt-in (``group`` None = the default process group, or a
+    group): every rank of it must hold the same K, X, z and call this with the
+    same log_etas. A rank whose block raises ``LinAlgError`` (K + eta I not
+    positive definite there) still joins the all-gather with an error flag in
+    its rows, and then every rank raises together."""
     from ._likelihood._profile_likelihood import ProfileLikelihood
     log_etas = numpy.atleast_1d(numpy.asarray(log_etas, dtype=float))
     dist, world, rank = _group(group)
     lo, hi, per = shard(log_etas.size, world, rank)
-    local = numpy.zeros((per, 1))
+    local = numpy.zeros((per, 2))
+    err = None
     if hi > lo:
-        local[:hi - lo, 0] = ProfileLikelihood.log_likelihood_der1_eta_batch(
-            z, X, K_mixed, log_etas[lo:hi])
+        try:
+            local[:hi - lo, 0] = ProfileLikelihood.log_likelihood_der1_eta_batch(
+                z, X, K_mixed, log_etas[lo:hi])
+        except numpy.linalg.LinAlgError as e:
+            if dist is None or world == 1:
+                raise
+            err = e
+            local[:, 1] = 1.0
     if dist is None or world == 1:
         return local[:log_etas.size, 0].copy()
-    return _all_gather_rows(dist, group, local, world)[:log_etas.size, 0].copy()
+    allv = _all_gather_rows(dist, group, local, world)
+    if err is not None:
+        raise err
+    if allv[:, 1].any():
+        raise numpy.linalg.LinAlgError(
+            'K + eta I is not positive definite at an eta of another rank\'s block')
+    return allv[:log_etas.size, 0].copy()
 
 
 def eta_sweep(K_mixed, X, z, etas, sigma=1.0, group=None):
@@ -84,17 +103,7 @@ def eta_sweep(K_mixed, X, z, etas, sigma=1.0, group=None):
     Returns (logdet[neta], lp[neta]) on every rank."""
     etas = numpy.asarray(etas, dtype=float)
     n, m = X.shape
-    world, rank = 1, 0
-    dist = None
-    if group is not False:
-        try:
-            import torch.distributed as dist_mod
-            if dist_mod.is_available() and dist_mod.is_initialized():
-                dist = dist_mod
-                world = dist.get_world_size(group)
-                rank = dist.get_rank(group)
-        except ImportError:
-            dist = None
+    dist, world, rank = _group(group)
     lo, hi, per = shard(etas.size, world, rank)
     local = numpy.zeros((per, 2))
     if hi > lo:
@@ -103,19 +112,7 @@ def eta_sweep(K_mixed, X, z, etas, sigma=1.0, group=None):
         local[:hi - lo, 1] = [_lp_from_terms(n, m, sigma, l, g) for l, g in zip(ld, G)]
     if dist is None or world == 1:
         return local[:etas.size, 0].copy(), local[:etas.size, 1].copy()
-    import torch
-    backend = dist.get_backend(group)
-    dev = torch.device('cuda', torch.cuda.current_device()) if backend == 'nccl' \
-        else torch.device('cpu')
-    t_local = torch.from_numpy(local).to(dev)
-    t_all = torch.empty((world * per, 2), dtype=torch.float64, device=dev)
-    if backend == 'nccl':
-        dist.all_gather_into_tensor(t_all, t_local, group=group)
-    else:
-        parts = list(t_all.chunk(world))
-        dist.all_gather(parts, t_local, group=group)
-        t_all = torch.cat(parts)
-    allv = t_all.cpu().numpy()[:etas.size]
+    allv = _all_gather_rows(dist, group, local, world)[:etas.size]
     return allv[:, 0].copy(), allv[:, 1].copy()
 
 
@@ -131,16 +128,7 @@ def slq_sweep(K_mixed, etas, group=None):
     from . import _slq
     etas = numpy.atleast_1d(numpy.asarray(etas, dtype=float))
     s = K_mixed.num_samples
-    world, rank, dist = 1, 0, None
-    if group is not False:
-        try:
-            import torch.distributed as dist_mod
-            if dist_mod.is_available() and dist_mod.is_initialized():
-                dist = dist_mod
-                world = dist.get_world_size(group)
-                rank = dist.get_rank(group)
-        except ImportError:
-            dist = None
+    dist, world, rank = _group(group)
     lo, hi, per = shard(s, world, rank)
     names = ('logdet', 'traceinv', 'traceinv2')
     # per probe row: the quadratures, then the smallest Ritz value (the SPD check
@@ -159,14 +147,7 @@ def slq_sweep(K_mixed, etas, group=None):
         local[:hi - lo, :nq] = q.reshape(hi - lo, nq)
         local[:hi - lo, nq] = [float(t.min()) for t, _ in nodes]
     if dist is not None and world > 1:
-        import torch
-        backend = dist.get_backend(group)
-        dev = torch.device('cuda', torch.cuda.current_device()) if backend == 'nccl' \
-            else torch.device('cpu')
-        t_local = torch.from_numpy(local).to(dev)
-        parts = [torch.empty_like(t_local) for _ in range(world)]
-        dist.all_gather(parts, t_local, group=group)
-        allv = torch.cat(parts).cpu().numpy()[:s]
+        allv = _all_gather_rows(dist, group, local, world)[:s]
     else:
         allv = local[:s]
     _slq.check_shifts(float(allv[:, nq].min()), etas)

@@ -246,3 +246,58 @@ def test_bench_strong_scaling_blocks_and_all_gather_gloo(world):
         assert gsize == 64 and allrows.shape == (world * per, 3)
         got = numpy.concatenate([allrows[r * per:r * per + owns[r], 0] for r in range(world)])
         numpy.testing.assert_array_equal(got, grid)
+
+
+class _Der1Operator(object):
+    """Stand-in whose batched der1 raises LinAlgError for eta < 1e-3 (as a
+    device operator raises for K + eta I not positive definite)."""
+    imate_method = 'cholesky'
+
+
+def _der1_worker(rank, world, port, log_etas, out_q):
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    from gaussian_proc import sweep
+    from gaussian_proc._likelihood._profile_likelihood import ProfileLikelihood
+
+    def fake(z, X, K_mixed, les):
+        les = numpy.asarray(les, dtype=float)
+        if numpy.any(les < -3.0):
+            raise numpy.linalg.LinAlgError('not positive definite')
+        return numpy.tanh(les - 0.7)
+    ProfileLikelihood.log_likelihood_der1_eta_batch = staticmethod(fake)
+    outs = []
+    for le in log_etas:
+        try:
+            outs.append(sweep.der1_sweep(_Der1Operator(), None, None, le, group=None))
+        except numpy.linalg.LinAlgError:
+            outs.append('LinAlgError')
+    # the default is local (group=False): no collective, runs on one rank alone
+    outs.append(sweep.der1_sweep(_Der1Operator(), None, None, [0.0, 1.0]))
+    out_q.put((rank, outs))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_der1_sweep_error_raises_on_every_rank_gloo():
+    """A LinAlgError in one rank's shard raises on every rank after the
+    all-gather (no rank is left blocked in it); a clean batch is gathered in
+    order; without an explicit group der1_sweep stays local."""
+    good = numpy.linspace(-1.0, 2.0, 5)
+    bad = numpy.array([0.0, 0.5, 1.0, -4.0])       # the last eta lands on rank 1
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_der1_worker, args=(r, 2, port, [good, bad], q))
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for _, outs in res:
+        numpy.testing.assert_array_equal(outs[0], numpy.tanh(good - 0.7))
+        assert outs[1] == 'LinAlgError'
+        numpy.testing.assert_array_equal(outs[2], numpy.tanh(numpy.array([0.0, 1.0]) - 0.7))

@@ -351,7 +351,7 @@ def test_profiled_maximize_bracket_found_matches_reference(gp, capsys, fixture, 
     calls, points, memo = ProfileLikelihood.last_der1_calls
     seq = cfg['maximize_profiled_der1_calls']
     check_der1_sequence(memo, seq)
-    assert calls < len(seq)
+    assert 2 * calls <= len(seq), (calls, len(seq))   # speculative Chandrupatla
 
 
 def test_traceinv_interpolation_on_device_operators(gp):

@@ -83,3 +83,89 @@ def test_profiled_driver_no_bracket_matches_reference_cfg1():
     ref = cfg['maximize_profiled']
     assert res['eta'] == numpy.inf and res['sigma'] == 0
     assert abs(res['sigma0'] - ref['sigma0']) <= 1e-12 * ref['sigma0']
+
+
+def _raising(f, lo, hi, log):
+    """f on [lo, hi]; LinAlgError outside (K + eta I indefinite there)."""
+    def fb(xs):
+        xs = numpy.asarray(xs, dtype=float)
+        log.append(xs.size)
+        if numpy.any((xs < lo) | (xs > hi)):
+            raise numpy.linalg.LinAlgError('not positive definite')
+        return numpy.array([f(x) for x in xs])
+    return fb
+
+
+@pytest.mark.parametrize('k', [0, 2, 3])
+def test_speculative_points_outside_the_domain_do_not_fail_the_search(k):
+    """The outward probes and Chandrupatla candidates are speculative: a
+    function that raises outside [x0, x1] (where the reference never looks
+    when the bracket is found inside) gives the reference's result."""
+    f = FUNCS[k]
+    bracket = (-4.0, 3.0)
+    with contextlib.redirect_stdout(io.StringIO()):
+        ref = find_interval_with_sign_change(lambda x: float(f(x)), list(bracket), 3)
+    assert ref[0]
+    log = []
+    fb = BatchedFunction(_raising(f, -4.0, 3.0, log), spec_budget=32)
+    with contextlib.redirect_stdout(io.StringIO()):
+        got = find_interval_with_sign_change_batched(fb, list(bracket), 3, tol=1e-6)
+    assert got == ref
+    assert fb.spec_failures >= 1                      # the outward probes raised
+    r1 = chandrupatla_method(lambda x: float(f(x)), ref[1], ref[2], eps_m=1e-6, eps_a=1e-6,
+                             maxiter=100)
+    r2 = chandrupatla_method(fb, got[1], got[2], eps_m=1e-6, eps_a=1e-6, maxiter=100)
+    assert r1 == r2
+
+
+@pytest.mark.parametrize('k', [0, 2, 4, 5])
+def test_speculative_chandrupatla_same_root_fewer_calls(k):
+    """Chandrupatla on a BatchedFunction prefetches the bisection / clamped
+    candidates of the next iterations: the same root and iteration count as
+    the sequential method, every point it evaluated among the prefetched ones,
+    and fewer batched calls than its evaluations."""
+    f = FUNCS[k]
+    with contextlib.redirect_stdout(io.StringIO()):
+        found, br, vals = find_interval_with_sign_change(lambda x: float(f(x)), [-4.0, 3.0], 3)
+    assert found
+    seq = []
+
+    def fs(x):
+        seq.append(x)
+        return float(f(x))
+    r1 = chandrupatla_method(fs, br, vals, eps_m=1e-6, eps_a=1e-6, maxiter=100)
+    fb = BatchedFunction(lambda xs: numpy.array([f(x) for x in xs]), spec_budget=64)
+    r2 = chandrupatla_method(fb, br, vals, eps_m=1e-6, eps_a=1e-6, maxiter=100)
+    assert r1 == r2
+    assert set(seq) <= set(fb.memo)
+    assert fb.calls < len(seq), (fb.calls, len(seq))
+
+
+def test_profiled_driver_speculative_n1024():
+    """The profiled driver with speculation on (the band operator's default,
+    forced here on the oracle operator): the reference's optimum, its recorded
+    evaluation sequence among the evaluated points, at most 2/3 of its
+    evaluations as batched calls."""
+    cfg = load_json('n1024_nu25.json')
+    pts, z, X = config_inputs(cfg)
+    K = matern.dense_correlation(pts, cfg['correlation_scale'], 2.5)
+
+    class _Batched(OracleMC):
+        cache = {}
+
+        def traceinv(self, eta, exponent=1):
+            key = (float(eta), exponent)
+            if key not in self.cache:
+                self.cache[key] = OracleMC.traceinv(self, eta, exponent)
+            return self.cache[key]
+    op = _Batched(K, 'eigenvalue')
+    with contextlib.redirect_stdout(io.StringIO()):
+        res = ProfileLikelihood.find_log_likelihood_der1_zeros(z, X, op, [1e-4, 1e3],
+                                                               speculative=24)
+    ref = cfg['maximize_profiled']
+    for k in ('sigma', 'sigma0', 'eta'):
+        assert abs(res[k] - ref[k]) <= 1e-8 * abs(ref[k]), (k, res[k], ref[k])
+    calls, points, memo = ProfileLikelihood.last_der1_calls
+    seq = cfg['maximize_profiled_der1_calls']
+    check_der1_sequence(memo, seq)
+    assert 3 * calls <= 2 * len(seq), (calls, len(seq))
