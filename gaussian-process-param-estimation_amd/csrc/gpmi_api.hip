@@ -384,7 +384,10 @@ int run_factor(gpmi_op* op, const double* etas_host, int nb, const double* rhs_d
   const int groups = op->groups ? op->groups : (nb <= 32 ? 2 : 1);
   if (groups == 2 && nb >= 2 && !op->lookahead) {
     // two independent halves of the batch on two streams: one half's
-    // latency-bound diagonal-block / panel kernels run beside the other's SYRK
+    // latency-bound diagonal-block / panel kernels run beside the other's SYRK.
+    // Only batched callers (nb >= 2) get here, and the one batched caller,
+    // gpmi_op_loglik_batch, releases stream3 after its synchronisation
+    // (the single-eta factor calls never create it)
     const int h = nb / 2;
     if (!op->stream3) {
       HIP_TRY(hipStreamCreateWithFlags(&op->stream3, hipStreamNonBlocking));

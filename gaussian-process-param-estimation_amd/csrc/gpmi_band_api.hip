@@ -124,7 +124,9 @@ struct gpmi_band {
   double* cqscr = nullptr;   // [nt][128][128]
   int* cqflag = nullptr;     // [nt][8]: [0..2] first-order flag per pass, [3] CholeskyQR
                              // succeeded, [4] failed (the guarded Householder panel ran)
-  int cq_panel_fallbacks = 0;   // panels factored by the guarded Householder panel
+  int cq_panel_fallbacks = 0;   // panels factored by the guarded Householder panel, or
+                                // (past its single-launch size) by per-column launches
+  int cq_host_checks = 0;       // panels past the single-launch size whose flag the host read
   double* cqMinv = nullptr;  // C = U^-T M3 of the current panel
   double cq_fo[3] = {0.0, 1e-4, 3e-8};   // first-order thresholds on ||G - I||_F
   int cap = 0;
@@ -291,14 +293,30 @@ int cq_panel(gpmi_band* b, int j, hipStream_t st) {
                        (int64_t)TS, P + TS * np, np, b->cqMinv, nullptr, fl + 4);
     BD_LAUNCH("cq_apply_kernel");
   }
-  // a failed panel (flag fl[4], P untouched) by the Householder panel in one launch;
-  // past its size the host redoes the reduction (band_reduce_pass)
+  // a failed panel (flag fl[4], P untouched) by the Householder panel in one launch,
+  // guarded on the device (it exits at once when the flag is clear); past that
+  // launch's size (G > panel_maxg workgroups cannot all be co-resident) the host
+  // reads the flag after the chain and, only for a failed panel, runs the
+  // per-column Householder launches on the same stream: that panel alone falls
+  // back, the reduction goes on (one host round trip per such panel)
   const int G = (m + HH_ROWS - 1) / HH_ROWS;
   if (G <= b->panel_maxg) {
     hipLaunchKernelGGL(hh_panel_kernel, dim3(G), dim3(HH_THREADS), HH_PANEL_LDS, st, P, np, m,
                        b->part, b->pivrow, b->ctr, b->tau + (int64_t)j * TS, b->err,
                        b->spin_limit, fl + 4);
     BD_LAUNCH("hh_panel_kernel");
+  } else {
+    int failed = 0;
+    BD_TRY(hipMemcpyAsync(&failed, fl + 4, sizeof(int), hipMemcpyDeviceToHost, st));
+    BD_TRY(hipStreamSynchronize(st));
+    ++b->cq_host_checks;
+    if (failed) {
+      for (int c = -1; c < TS; ++c) {
+        hipLaunchKernelGGL(hh_col_kernel, dim3(G), dim3(HH_THREADS), 0, st, P, np, m, c, b->part,
+                           b->pivrow, b->tau + (int64_t)j * TS);
+        BD_LAUNCH("hh_col_kernel");
+      }
+    }
   }
   return 0;
 }
@@ -467,14 +485,9 @@ int band_reduce_pass(gpmi_band* b, const double* K, const std::vector<double>* y
   BD_TRY(hipStreamSynchronize(s));
   if (herr) return set_error(-1201, "band reduction: panel hand-off timed out (workgroups not co-resident?)");
   if (mode == 0) {
-    // failed CholeskyQR panels: refactored by the guarded Householder panel, or (past
-    // its single-launch size) the reduction is redone with Householder panels
-    for (int j = 0; j + 1 < nt; ++j) {
-      if (!hflag[8 * j + 4]) continue;
-      const int G = (int)((np - (int64_t)(j + 1) * TS + HH_ROWS - 1) / HH_ROWS);
-      if (G > b->panel_maxg) return -1204;
-      ++b->cq_panel_fallbacks;
-    }
+    // failed CholeskyQR panels, each refactored in place during the pass (cq_panel)
+    for (int j = 0; j + 1 < nt; ++j)
+      if (hflag[8 * j + 4]) ++b->cq_panel_fallbacks;
   }
   float ms = 0.f;
   BD_TRY(hipEventElapsedTime(&ms, b->ev0, b->ev1));
@@ -489,11 +502,16 @@ int band_reduce_pass(gpmi_band* b, const double* K, const std::vector<double>* y
 // breakdown (a numerically rank-deficient panel) the reduction is redone with
 // Householder panels.
 int band_reduce(gpmi_band* b, const double* K, const std::vector<double>* yh = nullptr) {
-  int rc = -1204;
+  int rc;
   if (b->panel_mode == 0) {
+    // a failed CholeskyQR panel is refactored in place (cq_panel); only a timed-out
+    // guarded Householder panel (its workgroups not co-resident on a shared GPU)
+    // sends the reduction back, straight to the per-column launches
     rc = band_reduce_pass(b, K, yh, 0);
-    if (rc != -1204) return rc;
+    if (rc != -1201) return rc;
     ++b->cq_fallbacks;
+    ++b->panel_fallbacks;
+    return band_reduce_pass(b, K, yh, 2);
   }
   rc = band_reduce_pass(b, K, yh, 1);
   if (rc != -1201) return rc;

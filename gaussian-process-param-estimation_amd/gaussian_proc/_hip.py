@@ -557,7 +557,10 @@ class SparseOperator(object):
         """-> the SpMM kernel an s-column block runs: 'csr_spmm_kernel' (gather),
         'csr_spmm_win_kernel' (window, 8-column chunks), 'csr_spmm_winf_kernel'
         (window, one full-width pass) or 'csr_spmm_pair_kernel' (gather by column
-        pairs) (see gpmi_sp_spmm_kernel)."""
+        pairs) (see gpmi_sp_spmm_kernel). It names the kernel for a 16-byte
+        aligned block, which every block the library forms is (host inputs are
+        copied into hipMalloc'd workspaces; even-s offsets keep the alignment);
+        an unaligned device block handed in directly runs csr_spmm_kernel."""
         k = ctypes.c_int()
         check(self.lib.gpmi_sp_spmm_kernel(self.h, int(s), ctypes.byref(k)),
               'gpmi_sp_spmm_kernel')
