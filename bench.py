@@ -69,6 +69,8 @@ def parse():
                     help='band mode: eta values per rank per step (one reduction per step)')
     ap.add_argument('--no-timing', action='store_true',
                     help='skip the per-kernel HIP-event roofline timing')
+    ap.add_argument('--no-sparse', action='store_true',
+                    help='dense run: skip the sparse_modes block (configs 4 and 5, N=1 only)')
     return ap.parse_args()
 
 
@@ -245,53 +247,94 @@ def cpu_baseline(points, z, X, nu, eta, lam=None, samples=3):
     return out
 
 
-def cpu_baseline_sparse(K, X, z, etas, nprobe, steps, seed, budget_s):
+def cpu_baseline_sparse(K, X, z, etas, nprobe, steps, seed, budget_s, workers=None):
     """Restated reference pattern for a sparse K on scipy (the shipped sparse
     path cannot run: SURVEY 0.4): stochastic Lanczos quadrature with the SAME
-    counter-based probes as the device (oracle.sparse.slq: CSR SpMV Lanczos,
-    CGS2) for logdet at every eta, and per eta the reference's solves of X and
-    z column by column with scipy.sparse.linalg.cg, rtol 1e-6
-    (_linear_solver.py:57-68). Bounded sample: all probes' Lanczos, then CG
-    columns of spread eta until ``budget_s`` is spent, extrapolated to the whole
-    grid. scipy's CSR SpMV is single-threaded: cores = 1."""
+    counter-based probes as the device (oracle.sparse: CSR SpMV Lanczos, CGS2)
+    for logdet at every eta, and per eta the reference's solves of X and z
+    column by column with scipy.sparse.linalg.cg, rtol 1e-6
+    (_linear_solver.py:57-68). The probes and the (eta, column) solves are
+    independent, so they run on a thread pool over every CPU this job may use
+    (host_info; scipy's CSR SpMV and numpy's vector kernels release the GIL,
+    BLAS pinned to one thread per worker). Bounded sample: all probes' Lanczos,
+    then CG solves of spread eta until ``budget_s`` of wall time is spent,
+    extrapolated to the whole grid at the measured pool throughput."""
     import scipy.sparse
     import scipy.sparse.linalg
+    from concurrent.futures import ThreadPoolExecutor
+    from threadpoolctl import threadpool_limits
     from oracle import sparse as osp
     n = K.shape[0]
-    t0 = time.perf_counter()
+    info = host_info()
+    workers = int(workers or info['job_cpus'])
+    K = K.tocsr()
     P = osp.rademacher_probes(n, nprobe, seed)
-    slq = osp.slq(K, etas, P, steps)
-    t_slq = time.perf_counter() - t0
-    log('cpu SLQ (%d probes): %.1f s' % (nprobe, t_slq))
     R = numpy.column_stack([X, z])
-    order = numpy.argsort(numpy.arange(etas.size) % 4, kind='stable')   # spread etas
-    done, t_cg, its = 0, 0.0, []
     eye = scipy.sparse.identity(n, format='csr')
-    for j in order:
-        A = (K + etas[j] * eye).tocsr()
-        for c in range(R.shape[1]):
-            cnt = [0]
-            t1 = time.perf_counter()
-            scipy.sparse.linalg.cg(A, R[:, c], rtol=1e-6, atol=0.0,
-                                   callback=lambda xk: cnt.__setitem__(0, cnt[0] + 1))
-            t_cg += time.perf_counter() - t1
-            its.append(cnt[0])
-            done += 1
-            log('cpu CG solve %d: %d iterations, %.1f s total' % (done, cnt[0], t_cg))
-            if t_cg > budget_s:
-                break
-        if t_cg > budget_s:
-            break
-    per_solve = t_cg / done
-    total = t_slq + per_solve * etas.size * R.shape[1]
-    return {'value': etas.size / total, 'unit': 'evals/s', 'cores': 1, 'kind': 'port',
+    # (eta, column) tasks with the etas spread over the grid
+    order = numpy.argsort(numpy.arange(etas.size) % 4, kind='stable')
+    tasks = [(j, c) for j in order for c in range(R.shape[1])]
+    mats = {}
+
+    def lanczos(p):
+        return osp.lanczos(K, P[:, p], steps)
+
+    def solve(task):
+        j, c = task
+        cnt = [0]
+        scipy.sparse.linalg.cg(mats[j], R[:, c], rtol=1e-6, atol=0.0,
+                               callback=lambda xk: cnt.__setitem__(0, cnt[0] + 1))
+        return cnt[0]
+    with threadpool_limits(limits=1, user_api='blas'), ThreadPoolExecutor(workers) as ex:
+        t0 = time.perf_counter()
+        ab = list(ex.map(lanczos, range(nprobe)))
+        t_slq = time.perf_counter() - t0
+        log('cpu SLQ (%d probes, %d threads): %.1f s' % (nprobe, workers, t_slq))
+        for j in order:
+            mats[j] = (K + etas[j] * eye).tocsr()
+        t0 = time.perf_counter()
+        futs, its, k = [], [], 0
+        # keep the pool full; stop issuing once the budget is spent
+        while k < len(tasks) and (k < workers or time.perf_counter() - t0 < budget_s):
+            futs.append(ex.submit(solve, tasks[k]))
+            k += 1
+            if len(futs) >= workers:
+                its.append(futs.pop(0).result())
+        its += [f.result() for f in futs]
+        t_cg = time.perf_counter() - t0
+    done = len(its)
+    log('cpu CG: %d solves in %.1f s on %d threads' % (done, t_cg, workers))
+    total = t_slq + t_cg * (etas.size * R.shape[1]) / float(done)
+    theta = [osp.slq_nodes(a, b) for a, b in ab]
+    logdet = numpy.array([n * numpy.mean([numpy.sum(w * numpy.log(t + e)) for t, w in theta])
+                          for e in etas])
+    return {'value': etas.size / total, 'unit': 'evals/s', 'cores': workers, 'kind': 'port',
             'sample': 'SLQ of all %d probes x %d Lanczos steps (%.1f s, same probes as the '
                       'device) + %d of %d CG solves (rtol 1e-6, %.1f s, mean %.0f iterations), '
-                      'extrapolated to the %d-eta grid' % (nprobe, steps, t_slq, done,
-                                                           etas.size * R.shape[1], t_cg,
-                                                           numpy.mean(its), etas.size),
-            'slq_s': round(t_slq, 3), 'cg_s_per_solve': round(per_solve, 4),
-            'est_s_per_step': round(total, 2), 'logdet': slq['logdet'].tolist()}
+                      'on a %d-thread pool, extrapolated to the %d-eta grid'
+                      % (nprobe, steps, t_slq, done, etas.size * R.shape[1], t_cg,
+                         numpy.mean(its), workers, etas.size),
+            'slq_s': round(t_slq, 3), 'cg_s_per_solve_wall': round(t_cg / done, 4),
+            'est_s_per_step': round(total, 2), 'threads': workers, 'host': info,
+            'logdet': logdet.tolist()}
+
+
+def sparse_step_bytes(n, nnz, s_lanczos, steps, s_cg, cg_iters):
+    """Algorithmic bytes of one sparse step as implemented (each vector block
+    read or written once per pass): per Lanczos step k (block b_L = 8 n s_L)
+    the SpMM (12 nnz + 8(n+1) + 2 b_L), W -= beta V_{k-1} (3 b_L), two CGS2
+    passes of dots (k+1 basis blocks + W) and update (k+1 basis blocks + W read
+    and write), the norm (b_L) and V_{k+1} = W / beta (2 b_L); per multi-shift CG
+    iteration (b_C = 8 n s_C) the SpMM, p . q (2 b_C), the fused r update + dots
+    (B, r, q read, r written: 4 b_C) and p = r + beta p (3 b_C)."""
+    csr = 12.0 * nnz + 8.0 * (n + 1)
+    bl, bc = 8.0 * n * s_lanczos, 8.0 * n * s_cg
+    lanczos = sum(csr + 2 * bl + (3 * bl if k else 0) + 2 * ((k + 2) * bl + (k + 3) * bl) +
+                  bl + 2 * bl for k in range(steps))
+    basis = sum(4.0 * (k + 1) * bl for k in range(steps))
+    cg = cg_iters * (csr + 2 * bc + 9 * bc)
+    return {'lanczos': lanczos, 'lanczos_basis_reads': basis, 'cg': cg,
+            'total': lanczos + cg}
 
 
 SPARSE_CONFIGS = {
@@ -302,16 +345,29 @@ SPARSE_CONFIGS = {
 
 
 def run_sparse(args, world, rank, local, dist, torch):
+    """``--config sparse4|sparse5``: the sparse line alone (sparse_measure)."""
+    res = sparse_measure(args, args.config, world, rank, local, dist, torch,
+                         cpu=world == 1 and not args.no_cpu_baseline, exact=True)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def sparse_measure(args, config, world, rank, local, dist, torch, cpu, exact):
     """BASELINE configs 4 / 5: tapered Matern in CSR on the device; per step the
     rank runs the Lanczos of its probe shard (SLQ logdet / traceinv for the
     whole eta grid, one all-gather of per-probe quadratures) and the blocked-CG
     solves of [X | z] for its eta shard (direct lp), then one all-gather of the
-    [eta, logdet, lp] rows. The global problem is fixed: scaling "strong"."""
+    [eta, logdet, lp] rows. The global problem is fixed: scaling "strong".
+    Returns the line (rank 0; None elsewhere). ``exact``: the reference check
+    also runs the exact 'cholesky' method on a dense copy (cfg 4: 34 GB)."""
     from gaussian_proc import generate_correlation, _data
     from gaussian_proc._mixed_correlation import MixedCorrelation
     from gaussian_proc._likelihood._direct_likelihood import _lp_from_terms
     from gaussian_proc.sweep import slq_sweep, shard
-    npts, dim, rho, nu, dens, nprobe, steps, neta = SPARSE_CONFIGS[args.config]
+    npts, dim, rho, nu, dens, nprobe, steps, neta = SPARSE_CONFIGS[config]
     points = _data.generate_points(npts, dim, True)
     z = _data.generate_data(points, 0.2)
     X = _data.generate_basis_functions(points, 2)
@@ -333,7 +389,7 @@ def run_sparse(args, world, rank, local, dist, torch):
     R = numpy.column_stack([X, z])
     lo, hi, per = shard(neta, world, rank)
 
-    holder = {}
+    holder = {'cg_iters': 0}
 
     def step():
         curves = slq_sweep(op, etas)
@@ -342,6 +398,7 @@ def run_sparse(args, world, rank, local, dist, torch):
         if hi > lo:
             # all Gram blocks of the eta shard from one multi-shift CG (rtol 1e-6)
             Gs = op.sop.msgram(etas[lo:hi], R, rtol=1e-6)
+            holder['cg_iters'] = op.sop.last_cg_iterations
             for i, e in enumerate(etas[lo:hi]):
                 rows[i] = [e, curves['logdet'][lo + i],
                            _lp_from_terms(n, m, 1.0, curves['logdet'][lo + i], Gs[i])]
@@ -370,19 +427,24 @@ def run_sparse(args, world, rank, local, dist, torch):
     sp_kernel = op.sop.spmm_kernel(s_blk)
     gather_bytes = (8.0 * s_blk * info['mean_window'] * ((n + 63) // 64) if info['windowed']
                     else 8.0 * nnz * s_blk)
-    sp_traffic, sp_tsrc = (pmc_traffic_sparse(args.config, 'gpmi::' + sp_kernel)
+    sp_traffic, sp_tsrc = (pmc_traffic_sparse(config, 'gpmi::' + sp_kernel)
                            if s_blk == 20 else (None, None))
+    my_probes = shard(nprobe, world, rank)
+    sb = sparse_step_bytes(n, nnz, my_probes[1] - my_probes[0], steps, R.shape[1],
+                           holder['cg_iters'])
+    step_s = dt / args.steps
+    res = None
     if rank == 0:
         res = {
             'metric': 'log-likelihood evals/sec (%s, sparse tapered Matern, SLQ + CG)'
-                      % args.config,
+                      % config,
             'value': neta * args.steps / dt, 'unit': 'evals/s', 'n_gpus': world,
             'steps': args.steps, 'warmup': args.warmup,
             'ms_per_step': dt / args.steps * 1e3, 'higher_is_better': True,
             'scaling': 'strong', 'vs_baseline': None, 'dtype': 'f64',
             'data': 'synthetic (reference data_utilities grid, sin + 0.2 noise seed 31)',
             'config': {'workload': '%s: N=%d %dD grid, nu=%g rho=%g density=%g, %d probes x '
-                                   '%d Lanczos steps, %d etas' % (args.config, n, dim, nu, rho,
+                                   '%d Lanczos steps, %d etas' % (config, n, dim, nu, rho,
                                                                  dens, nprobe, steps, neta),
                        'n': n, 'nnz': nnz, 'nnz_per_row': nnz / float(n), 'tau': D.tau,
                        'lambda_min_ritz': theta_min, 'eta_shift': shift,
@@ -403,13 +465,25 @@ def run_sparse(args, world, rank, local, dist, torch):
                          'note': 'working set %.1f MB: Infinity-Cache resident when < 256 MB; '
                                  'the X reads (gather_bytes) are served by L2 / MALL'
                                  % (alg_bytes / 1e6)},
+            # the whole step against HBM: algorithmic bytes of every pass of the
+            # step (sparse_step_bytes) / ms_per_step, rank 0's shard
+            'step_roofline': {
+                'bound': 'hbm', 'bytes_per_step': sb['total'],
+                'achieved': round(sb['total'] / step_s / 1e9, 1), 'peak': HBM_PEAK_GBS,
+                'unit': 'GB/s', 'frac': round(sb['total'] / step_s / 1e9 / HBM_PEAK_GBS, 4),
+                'lanczos_bytes': sb['lanczos'], 'lanczos_basis_read_bytes':
+                    sb['lanczos_basis_reads'], 'cg_bytes': sb['cg'],
+                'cg_iterations': holder['cg_iters'],
+                'lanczos_probes': my_probes[1] - my_probes[0], 'lanczos_steps': steps,
+                'cg_columns': R.shape[1],
+                'model': 'bench.sparse_step_bytes (each vector block once per pass)'},
             'lp_sample': [float(v) for v in last[0].tolist()],
             'cpu_baseline': None,
         }
-        ref = sparse_reference_check(op, args.config, X, z)
+        ref = sparse_reference_check(op, config, X, z, exact)
         if ref:
             res['reference_check'] = ref
-        if world == 1 and not args.no_cpu_baseline:
+        if cpu:
             cb = cpu_baseline_sparse(op.sop.csr(), X, z, etas, nprobe, steps, op.seed,
                                      args.cpu_budget_s)
             dev = holder['curves']['logdet']
@@ -417,13 +491,32 @@ def run_sparse(args, world, rank, local, dist, torch):
                 numpy.max(numpy.abs(numpy.asarray(cb.pop('logdet')) - dev) / numpy.abs(dev)))
             res['cpu_baseline'] = cb
             res['speedup_vs_cpu'] = round(res['value'] / cb['value'], 1)
-        print(json.dumps(res), flush=True)
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
+    op.sop.close()
+    return res
 
 
-def sparse_reference_check(op, config, X, z):
+def sparse_modes(args, local, dist, torch):
+    """The sparse configs 4 and 5 in the default (dense) line at N=1, each with
+    its own value, step time, SpMM and whole-step rooflines, reference check and
+    thread-pool CPU baseline (sparse_measure; the exact-Cholesky leg of the
+    reference check is left to --config sparse4)."""
+    out = {}
+    for cfg in ('sparse4', 'sparse5'):
+        r = sparse_measure(args, cfg, 1, 0, local, dist, torch,
+                           cpu=not args.no_cpu_baseline, exact=False)
+        log('%s: %.1f evals/s' % (cfg, r['value']))
+        out[cfg] = {k: r[k] for k in ('metric', 'value', 'unit', 'ms_per_step', 'steps',
+                                      'warmup', 'roofline', 'step_roofline', 'cpu_baseline',
+                                      'lp_sample') if k in r}
+        out[cfg]['workload'] = r['config']['workload']
+        out[cfg]['assembly_s'] = r['config']['assembly_s']
+        for k in ('reference_check', 'speedup_vs_cpu'):
+            if k in r:
+                out[cfg][k] = r[k]
+    return out
+
+
+def sparse_reference_check(op, config, X, z, exact=True):
     """BASELINE cfg4 against the reference's own exact values
     (tests/golden/sparse_cfg4.json: reference generator + the 2 argument fixes,
     SuperLU logdet and Gram at three eta above |lambda_min|): the device CSR
@@ -448,7 +541,7 @@ def sparse_reference_check(op, config, X, z):
         est, se = q.mean(axis=0), q.std(axis=0, ddof=1) / numpy.sqrt(q.shape[0])
         out['slq_logdet_err_in_std_errors'] = [round(float(v), 3) for v in
                                                numpy.abs(est - g['logdet']) / se]
-        if op.n <= 65536:
+        if exact and op.n <= 65536:
             # the exact 'cholesky' method on this sparse K (dense device copy,
             # fp64 MFMA Cholesky per eta) against the same SuperLU values
             from gaussian_proc._mixed_correlation import MixedCorrelation
@@ -827,6 +920,13 @@ def main():
         cb['lp_rel_diff_vs_device'] = abs(cb['lp_cholesky'] - lp_dev) / abs(lp_dev)
         result['cpu_baseline'] = cb
         result['speedup_vs_cpu'] = round(result['value'] / cb['value'], 1)
+    if world == 1 and not args.no_sparse:
+        # release the dense and band operators (their streams count against the
+        # process's hardware queues) before the sparse configs run
+        if not args.no_band:
+            bop.band().close()
+        op.op.close()
+        result['sparse_modes'] = sparse_modes(args, local, dist, torch)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

@@ -375,7 +375,7 @@ def main():
     ap.add_argument('--sparse-big', action='store_true', help='also config 4 (~5 min)')
     ap.add_argument('--only', default=None,
                     help='write only one fixture: cfg3_nu25 (~3 min), sparse_cfg4 (~10 min), '
-                         'sparse_cfg5 (~90 min), n1024 or cfg2_profiled')
+                         'sparse_cfg5 (~90 min), sparse_3d32, n1024 or cfg2_profiled')
     args = ap.parse_args()
     if args.only:
         R = import_reference()
@@ -386,6 +386,12 @@ def main():
                                   [0.05, 0.5, 5.0])
         elif args.only == 'sparse_cfg5':
             out = sparse_big_case(R, 'cfg5_n262144_3d', 64, 3, 0.02, 1.5, 6e-4, [])
+        elif args.only == 'sparse_3d32':
+            # cfg5's 3-D stencil on a 32^3 grid (half the points per axis: rho and
+            # density scaled so that a row keeps the same neighbours, nnz/row ~ 32),
+            # small enough for SuperLU's exact logdet and Gram
+            out = sparse_big_case(R, 'sparse3d_n32768', 32, 3, 0.04, 1.5, 4.8e-3,
+                                  [0.05, 0.5, 5.0])
         elif args.only == 'n1024':
             out, _ = config_case(R, 'n1024_2d_nu2.5', 32, 2, 2.5, optimize=True)
             args.only = 'n1024_nu25'

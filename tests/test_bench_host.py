@@ -1,0 +1,49 @@
+"""Host-side pieces of bench.py (CPU): the thread-pool sparse CPU baseline
+reproduces the oracle's SLQ logdet with the device's probes, and the sparse
+step byte model counts what its docstring says."""
+
+import os
+import sys
+
+import numpy
+import scipy.sparse
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+from oracle import sparse as osp  # noqa: E402
+
+
+def _spd(n, seed=0):
+    rng = numpy.random.RandomState(seed)
+    r = numpy.repeat(numpy.arange(n), 6)
+    c = (r + rng.randint(-20, 21, r.size)) % n
+    A = scipy.sparse.csr_matrix((rng.rand(r.size) * 0.1, (r, c)), shape=(n, n))
+    return (A + A.T + scipy.sparse.identity(n)).tocsr()
+
+
+def test_cpu_baseline_sparse_thread_pool():
+    n = 3000
+    K = _spd(n)
+    rng = numpy.random.RandomState(1)
+    X = numpy.column_stack([numpy.ones(n), rng.rand(n)])
+    z = rng.randn(n)
+    etas = numpy.array([0.1, 0.5, 1.0, 2.0])
+    cb = bench.cpu_baseline_sparse(K, X, z, etas, 4, 12, 5, 0.2, workers=3)
+    assert cb['value'] > 0 and cb['cores'] == 3 and cb['threads'] == 3
+    P = osp.rademacher_probes(n, 4, 5)
+    ref = osp.slq(K, etas, P, 12)['logdet']
+    numpy.testing.assert_allclose(cb['logdet'], ref, rtol=1e-12)
+
+
+def test_sparse_step_bytes_model():
+    n, nnz = 1000, 20000
+    b = bench.sparse_step_bytes(n, nnz, 4, 3, 2, 10)
+    csr = 12.0 * nnz + 8.0 * (n + 1)
+    bl, bc = 8.0 * n * 4, 8.0 * n * 2
+    lz = 0.0
+    for k in range(3):
+        lz += csr + 2 * bl + (3 * bl if k else 0) + 2 * ((k + 2) + (k + 3)) * bl + 3 * bl
+    assert b['lanczos'] == lz
+    assert b['lanczos_basis_reads'] == sum(4 * (k + 1) * bl for k in range(3))
+    assert b['cg'] == 10 * (csr + 11 * bc)
+    assert b['total'] == b['lanczos'] + b['cg']

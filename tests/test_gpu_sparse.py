@@ -414,8 +414,11 @@ def test_config5_full_size_vs_reference(gp):
     6e-4) against tests/golden/sparse_cfg5.json (reference generator + the 2
     argument fixes): CSR, and the device Lanczos vs the oracle with identical
     probes (<= 1e-9). Exact logdet at this size is out of reach of the host
-    sparse LU (3D fill-in); the SLQ estimate is checked for consistency: the
-    64-probe mean lies within 3 standard errors of the 20-probe one."""
+    sparse LU (3D fill-in; test_sparse_3d_exact_logdet_vs_reference pins the same
+    stencil at 32^3 against exact values); the SLQ estimate is checked for
+    consistency: the 64-probe mean lies within 3 standard errors of the 20-probe
+    one. The multi-shift Gram is checked against host CG (<= 1e-9), and the direct
+    lp against the oracle's formula on a host operator with the same probes."""
     from gaussian_proc._mixed_correlation import MixedCorrelation
     from gaussian_proc import _slq
     meta, pts, D = _cfg_sparse(gp, 'sparse_cfg5.json', 64, 3, 0.02, 6e-4)
@@ -427,3 +430,97 @@ def test_config5_full_size_vs_reference(gp):
     q = _slq.quadrature(op.slq_nodes(), [eta], _slq.FUNCS['logdet'])[:, 0] * op.n
     se = q.std(ddof=1) / numpy.sqrt(q.size)
     assert abs(q[:20].mean() - q.mean()) <= 3.0 * se * numpy.sqrt(64 / 20.0)
+    # beyond the CSR: the multi-shift CG Gram at two eta above |lambda_min| against
+    # host CG (the oracle's solve, rtol 1e-12, thread pool over the columns), and
+    # the direct lp (_direct_likelihood.py:31-83) on the device operator (8-probe
+    # SLQ logdet + CG Gram) against the oracle formula on the host operator with
+    # the same 8 probes (oracle.sparse.slq) and the host CG solves
+    z = data.generate_data(pts, 0.2)
+    X = data.generate_basis_functions(pts, 2)
+    R = numpy.column_stack([X, z])
+    etas = [eta, eta + 1.0]
+    G = op.sop.msgram(etas, R, rtol=1e-10)
+    host = _HostSparseOperator(K, 8, 30, 0)
+    for e, Gj in zip(etas, G):
+        assert _nrel(Gj, R.T @ host.solve(e, R)) < 1e-9, e
+    op8 = MixedCorrelation(D, imate_method='slq',
+                           imate_options={'num_samples': 8, 'lanczos_degree': 30})
+    from gaussian_proc._likelihood._direct_likelihood import DirectLikelihood
+    from oracle import likelihood as olk
+    assert rel(op8.logdet(eta), host.logdet(eta)) < 1e-9
+    for hp in ([1.0, numpy.sqrt(eta)], [0.5, 0.5 * numpy.sqrt(eta + 1.0)]):
+        lp = DirectLikelihood.log_likelihood(z, X, op8, False, hp)
+        assert rel(lp, olk.direct_lp(z, X, host, hp)) < 1e-8, hp
+
+
+class _HostSparseOperator(object):
+    """Host operator for the oracle's likelihood formulas on a sparse K: SLQ
+    logdet with the device's counter-based probes (oracle.sparse.slq) and solves
+    by scipy CG at rtol 1e-12, probes and columns on a thread pool."""
+
+    def __init__(self, K, nprobe, steps, seed):
+        self.K = K.tocsr()
+        self.n = K.shape[0]
+        self.P = osp.rademacher_probes(self.n, nprobe, seed)
+        self.steps = steps
+        self._nodes = None
+
+    def logdet(self, eta):
+        from concurrent.futures import ThreadPoolExecutor
+        if self._nodes is None:
+            with ThreadPoolExecutor(16) as ex:
+                ab = list(ex.map(lambda p: osp.lanczos(self.K, self.P[:, p], self.steps),
+                                 range(self.P.shape[1])))
+            self._nodes = [osp.slq_nodes(a, b) for a, b in ab]
+        return self.n * numpy.mean([numpy.sum(w * numpy.log(t + eta)) for t, w in self._nodes])
+
+    def solve(self, eta, Y):
+        import scipy.sparse
+        import scipy.sparse.linalg
+        from concurrent.futures import ThreadPoolExecutor
+        A = (self.K + eta * scipy.sparse.identity(self.n, format='csr')).tocsr()
+        Y2 = numpy.asarray(Y, dtype=float)
+        cols = Y2[:, None] if Y2.ndim == 1 else Y2
+
+        def one(c):
+            x, info = scipy.sparse.linalg.cg(A, cols[:, c], rtol=1e-12, atol=0.0,
+                                             maxiter=20 * self.n)
+            assert info == 0
+            return x
+        with ThreadPoolExecutor(16) as ex:
+            out = numpy.column_stack(list(ex.map(one, range(cols.shape[1]))))
+        return out[:, 0] if Y2.ndim == 1 else out
+
+
+def test_sparse_3d_exact_logdet_vs_reference(gp):
+    """cfg5's 3-D stencil on a 32^3 grid (N=32768, rho and density scaled so a row
+    keeps cfg5's neighbours) against tests/golden/sparse_3d32.json, made by the
+    reference generator (+ the 2 argument fixes) with SuperLU exact values at
+    three eta above |lambda_min|: CSR; multi-shift CG Gram <= 1e-9 at rtol 1e-10
+    (<= 1e-6 at the reference's rtol 1e-6); the 64-probe SLQ logdet within 3
+    Monte-Carlo standard errors of the exact logdet; the direct lp within that
+    error of the reference's lp on the exact operator."""
+    from gaussian_proc._mixed_correlation import MixedCorrelation
+    from gaussian_proc._likelihood._direct_likelihood import DirectLikelihood
+    from gaussian_proc import _slq
+    meta, pts, D = _cfg_sparse(gp, 'sparse_3d32.json', 32, 3, 0.04, 4.8e-3)
+    K = _check_csr(D, meta)
+    op = MixedCorrelation(D, imate_method='slq',
+                          imate_options={'num_samples': 64, 'lanczos_degree': 30})
+    _lanczos_same_probes(op.sop, K, 3, 30, 0)
+    z = data.generate_data(pts, 0.2)
+    X = data.generate_basis_functions(pts, 2)
+    R = numpy.column_stack([X, z])
+    etas = meta['etas']
+    for rtol, tol in ((1e-6, 1e-6), (1e-10, 1e-9)):
+        G = op.sop.msgram(etas, R, rtol=rtol)
+        for Gj, Gr in zip(G, meta['gram']):
+            assert _nrel(Gj, numpy.asarray(Gr)) < tol, rtol
+    q = _slq.quadrature(op.slq_nodes(), etas, _slq.FUNCS['logdet']) * op.n
+    est = q.mean(axis=0)
+    se = q.std(axis=0, ddof=1) / numpy.sqrt(q.shape[0])
+    err = numpy.abs(est - meta['logdet'])
+    assert numpy.all(err <= 3.0 * se), (err / se)
+    for e, ld_se, lp_ref in zip(etas, se, meta['direct_lp']):
+        lp = DirectLikelihood.log_likelihood(z, X, op, False, [1.0, numpy.sqrt(e)])
+        assert abs(lp - lp_ref) <= 0.5 * 3.0 * ld_se + 1e-6 * abs(lp_ref), (e, lp, lp_ref)
