@@ -321,18 +321,20 @@ def cpu_baseline_sparse(K, X, z, etas, nprobe, steps, seed, budget_s, workers=No
 
 def sparse_step_bytes(n, nnz, s_lanczos, steps, s_cg, cg_iters):
     """Algorithmic bytes of one sparse step as implemented (each vector block
-    read or written once per pass): per Lanczos step k (block b_L = 8 n s_L)
-    the SpMM (12 nnz + 8(n+1) + 2 b_L), W -= beta V_{k-1} (3 b_L), two CGS2
-    passes of dots (k+1 basis blocks + W) and update (k+1 basis blocks + W read
-    and write), the norm (b_L) and V_{k+1} = W / beta (2 b_L); per multi-shift CG
-    iteration (b_C = 8 n s_C) the SpMM, p . q (2 b_C), the fused r update + dots
-    (B, r, q read, r written: 4 b_C) and p = r + beta p (3 b_C)."""
+    read or written once per pass). Lanczos (block b_L = 8 n s_L), DCGS2
+    (gpmi_sparse.hip lz_*): per step k the SpMM (12 nnz + 8(n+1) + 2 b_L), the
+    dot pass over the k basis blocks, u and y ((k + 2) b_L) and the update pass
+    (k basis blocks, u, y read; v_k, u written: (k + 4) b_L), then one final dot
+    pass over the basis and u ((steps + 1) b_L). Multi-shift CG (b_C = 8 n s_C,
+    s_C the device width: an odd width that would run the one-column gather is
+    padded by one zero column) per iteration: the SpMM, p . q (2 b_C), the r
+    update (3 b_C), the B^T r / r . r dots (2 b_C) and p = r + beta p (3 b_C)."""
     csr = 12.0 * nnz + 8.0 * (n + 1)
     bl, bc = 8.0 * n * s_lanczos, 8.0 * n * s_cg
-    lanczos = sum(csr + 2 * bl + (3 * bl if k else 0) + 2 * ((k + 2) * bl + (k + 3) * bl) +
-                  bl + 2 * bl for k in range(steps))
-    basis = sum(4.0 * (k + 1) * bl for k in range(steps))
-    cg = cg_iters * (csr + 2 * bc + 9 * bc)
+    lanczos = sum(csr + 2 * bl + (k + 2) * bl + (k + 4) * bl for k in range(steps)) + \
+        (steps + 1) * bl
+    basis = sum(2.0 * k * bl for k in range(steps)) + steps * bl
+    cg = cg_iters * (csr + 2 * bc + 10 * bc)
     return {'lanczos': lanczos, 'lanczos_basis_reads': basis, 'cg': cg,
             'total': lanczos + cg}
 
@@ -430,7 +432,9 @@ def sparse_measure(args, config, world, rank, local, dist, torch, cpu, exact):
     sp_traffic, sp_tsrc = (pmc_traffic_sparse(config, 'gpmi::' + sp_kernel)
                            if s_blk == 20 else (None, None))
     my_probes = shard(nprobe, world, rank)
-    sb = sparse_step_bytes(n, nnz, my_probes[1] - my_probes[0], steps, R.shape[1],
+    s_cg = R.shape[1] + (1 if (R.shape[1] % 2 and op.sop.spmm_kernel(R.shape[1]) ==
+                               'csr_spmm_kernel' and R.shape[1] < 16) else 0)
+    sb = sparse_step_bytes(n, nnz, my_probes[1] - my_probes[0], steps, s_cg,
                            holder['cg_iters'])
     step_s = dt / args.steps
     res = None
@@ -475,7 +479,7 @@ def sparse_measure(args, config, world, rank, local, dist, torch, cpu, exact):
                     sb['lanczos_basis_reads'], 'cg_bytes': sb['cg'],
                 'cg_iterations': holder['cg_iters'],
                 'lanczos_probes': my_probes[1] - my_probes[0], 'lanczos_steps': steps,
-                'cg_columns': R.shape[1],
+                'cg_columns': R.shape[1], 'cg_device_width': s_cg,
                 'model': 'bench.sparse_step_bytes (each vector block once per pass)'},
             'lp_sample': [float(v) for v in last[0].tolist()],
             'cpu_baseline': None,
@@ -700,9 +704,35 @@ def band_mode(args, D, X, z, world, rank, dist, torch, ld_ref=None):
     if ld_ref is not None:
         out['logdet_rel_err_vs_cholesky'] = float(numpy.max(
             numpy.abs(op.loglik_terms(ld_ref[0], X, z)[0] - ld_ref[1]) / numpy.abs(ld_ref[1])))
+    if world == 1 and args.scaling == 'strong':
+        out['batch_efficiency'] = band_batch_efficiency(op, X, z)
     if not args.no_der:
         out['der1_sweep'] = der1_sweep(op, X, z, E, rank, torch)
     return out, op
+
+
+def band_batch_efficiency(op, X, z, batches=(8, 16, 32, 64)):
+    """The band operator's per-rank eta batches of the strong-scaled curve at
+    N = 8 / 4 / 2 / 1: device time of the banded-Cholesky call for that batch
+    (one workgroup per eta, so 8 eta leave most CUs idle) and the expected
+    time-to-curve with the reduction (repeated on every rank, it does not shard)."""
+    b = op.band()
+    red = b.last_timing()['reduce_ms']
+    grid = numpy.logspace(-3, 3, 64)
+    out = {}
+    for bsz in batches:
+        etas = grid[:bsz]
+        op.loglik_terms(etas, X, z)
+        times = []
+        for _ in range(2):
+            op.loglik_terms(etas, X, z)
+            times.append(b.last_timing()['loglik_ms'])
+        best = min(times)
+        out[str(bsz)] = {'loglik_ms': round(best, 3),
+                         'evals_per_s_after_reduction': round(bsz / (best * 1e-3), 1),
+                         'expected_time_to_64_curve_ms_at_N': {
+                             str(64 // bsz): round(red + best, 2)}}
+    return out
 
 
 def der1_sweep(op, X, z, E, rank, torch):

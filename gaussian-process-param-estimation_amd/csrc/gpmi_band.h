@@ -50,6 +50,16 @@ __global__ void syr2k_kernel(double* A, int64_t lda, const double* U, int64_t ld
                              int mt, int sub);
 __global__ void syr2k_rest_kernel(double* A, int64_t lda, const double* U, int64_t ldu, int tr0,
                                   int mt);
+__global__ void syr2k_g_kernel(double* A, int64_t lda, const double* PA, const double* PB,
+                               int64_t ldu, int kdim, int tr0, int mt, int sub);
+__global__ void syr2k_g_rest_kernel(double* A, int64_t lda, const double* PA, const double* PB,
+                                    int64_t ldu, int kdim, int tr0, int mt);
+__global__ void slot_copy_kernel(const double* U, int64_t ldu, int m, double* Va, double* Vb,
+                                 double* Wa, double* Wb, int64_t ldg);
+__global__ void zc_partial_kernel(const double* PB, int64_t ldb, const double* V, int64_t ldv,
+                                  int m, double* part);
+__global__ void zc_reduce_kernel(const double* part, int nch, double* Z);
+__global__ void xcorr_kernel(double* X, const double* PA, int64_t lda, const double* Z, int kdim);
 __global__ void qt_partial_kernel(const double* P, int64_t lda, int m, const double* Y,
                                   double* part);
 __global__ void qt_reduce_kernel(const double* part, int G, double* a);

@@ -127,6 +127,13 @@ struct gpmi_band {
   int cq_panel_fallbacks = 0;   // panels factored by the guarded Householder panel, or
                                 // (past its single-launch size) by per-column launches
   int cq_host_checks = 0;       // panels past the single-launch size whose flag the host read
+  // delayed trailing update (CholeskyQR panels): one SYR2K per `delay` panels
+  // (band_reduce_pass_delayed; GPMI_BAND_DELAY, 1 = one SYR2K per panel)
+  int delay = 1;              // measured at N = 16384: 1 159 ms, 2 167, 4 181, 8 202
+  double* UA = nullptr;      // [n_pad][256 delay] = [W_{p-1} .. W_0 | V_0 .. V_{p-1}]
+  double* UB = nullptr;      // [n_pad][256 delay] = [V_{p-1} .. V_0 | W_0 .. W_{p-1}]
+  double* zpart = nullptr;   // [2 delay][nt][128][128] partials of UB^T V
+  double* Zc = nullptr;      // [2 delay][128][128]
   double* cqMinv = nullptr;  // C = U^-T M3 of the current panel
   double cq_fo[3] = {0.0, 1e-4, 3e-8};   // first-order thresholds on ||G - I||_F
   int cap = 0;
@@ -159,7 +166,7 @@ int band_free(gpmi_band* b) {
   double* bufs[] = {b->Ab, b->U, b->X, b->Xp, b->part, b->pivrow, b->tau, b->Tm, b->tnp, b->tnp2,
                     b->VtV, b->M, b->Zh, b->Y, b->qtp, b->qa, b->qb, b->etas, b->out, b->Ac, b->td,
                     b->fac, b->ysol, b->der, b->Qb, b->cqpart, b->cqG, b->cqL, b->cqLinv,
-                    b->cqMinv, b->cqS, b->cqscr};
+                    b->cqMinv, b->cqS, b->cqscr, b->UA, b->UB, b->zpart, b->Zc};
   if (b->cqflag) (void)hipFree(b->cqflag);
   for (double* p : bufs)
     if (p) (void)hipFree(p);
@@ -495,6 +502,174 @@ int band_reduce_pass(gpmi_band* b, const double* K, const std::vector<double>* y
   return 0;
 }
 
+// The reduction with CholeskyQR panels and the trailing update delayed over groups
+// of p = b->delay panels (gpmi_band.hip, "Delayed trailing update"): inside a
+// group each panel's tile column gets the pending pairs' update just before its
+// QR, X = A22 V is corrected by the pending pairs, and the group ends with ONE
+// rank-256p SYR2K of the trailing block (the look-ahead runs the next panel's QR
+// beside it, as in band_reduce_pass).
+int band_reduce_pass_delayed(gpmi_band* b, const double* K, const std::vector<double>* yh) {
+  const int mode = 0;
+  hipStream_t s = b->stream;
+  const int64_t np = b->n_pad;
+  const int nt = b->nt;
+  const int p = b->delay;
+  const int64_t ldg = (int64_t)2 * TS * p;
+  if (!b->UA) {
+    BD_TRY(hipMalloc(&b->UA, sizeof(double) * np * ldg));
+    BD_TRY(hipMalloc(&b->UB, sizeof(double) * np * ldg));
+    BD_TRY(hipMalloc(&b->zpart, sizeof(double) * 2 * p * (size_t)nt * TS * TS));
+    BD_TRY(hipMalloc(&b->Zc, sizeof(double) * 2 * p * TS * TS));
+  }
+  BD_TRY(hipMemsetAsync(b->err, 0, 16, s));
+  BD_TRY(hipMemsetAsync(b->cqflag, 0, sizeof(int) * 8 * nt, s));
+  BD_TRY(hipEventRecord(b->ev0, s));
+  if (yh) {
+    BD_TRY(hipMemcpyAsync(b->Y, yh->data(), sizeof(double) * yh->size(), hipMemcpyHostToDevice,
+                          b->qs ? b->qs : b->side));
+  }
+  BD_TRY(hipMemcpyAsync(b->Ab, K, sizeof(double) * np * np, hipMemcpyDeviceToDevice, s));
+  const bool la = b->lookahead && b->s_pan;
+  bool ahead = false;
+  int Q = 0;   // pending pairs of the current group
+  for (int j = 0; j + 1 < nt; ++j) {
+    const int64_t r0 = (int64_t)(j + 1) * TS;
+    const int m = (int)(np - r0), mt = nt - j - 1;
+    double* tau = b->tau + (int64_t)j * TS;
+    double* T = b->Tm + (int64_t)j * TS * TS;
+    const double* PA = b->UA + (int64_t)(p - Q) * TS;
+    const double* PB = b->UB + (int64_t)(p - Q) * TS;
+    if (!ahead) {
+      if (Q > 0) {
+        // the panel's tile column (tiles j .. nt-1) with the pending pairs
+        hipLaunchKernelGGL(syr2k_g_kernel, dim3(nt - j), dim3(256), 0, s, b->Ab, np, PA, PB, ldg,
+                           2 * TS * Q, j, nt - j, 1);
+        BD_LAUNCH("syr2k_g_kernel");
+      }
+      int rc = panel_qr(b, j, s, mode);
+      if (rc) return rc;
+    }
+    ahead = false;
+    double* P = b->Ab + r0 * np + (int64_t)j * TS;
+    double* Ur = b->U + r0 * BAND_ULD;
+    hipLaunchKernelGGL(vcopy_kernel, dim3((unsigned)((int64_t)m * TS / 256)), dim3(256), 0, s, P,
+                       np, m, Ur, (int64_t)BAND_ULD);
+    BD_LAUNCH("vcopy_kernel");
+    const int nch = (m + TN_CH - 1) / TN_CH;
+    // side stream, beside the SYMM: T from V^T V, and Z = UB_pend^T V
+    BD_TRY(hipEventRecord(b->ev_v, s));
+    BD_TRY(hipStreamWaitEvent(b->side, b->ev_v, 0));
+    hipLaunchKernelGGL(tn_partial_kernel, dim3(nch), dim3(256), 0, b->side, Ur + TS,
+                       (int64_t)BAND_ULD, Ur + TS, (int64_t)BAND_ULD, m, b->tnp2);
+    BD_LAUNCH("tn_partial_kernel");
+    hipLaunchKernelGGL(tn_reduce_kernel, dim3(TS * TS / 64), dim3(256), 0, b->side, b->tnp2, nch,
+                       b->VtV, 1.0);
+    BD_LAUNCH("tn_reduce_kernel");
+    hipLaunchKernelGGL(tbuild_kernel, dim3(1), dim3(256), 0, b->side, b->VtV, tau, T);
+    BD_LAUNCH("tbuild_kernel");
+    if (Q > 0) {
+      hipLaunchKernelGGL(zc_partial_kernel, dim3(nch, 2 * Q), dim3(256), 0, b->side,
+                         PB + r0 * ldg, ldg, Ur + TS, (int64_t)BAND_ULD, m, b->zpart);
+      BD_LAUNCH("zc_partial_kernel");
+      hipLaunchKernelGGL(zc_reduce_kernel, dim3(TS * TS / 64, 2 * Q), dim3(256), 0, b->side,
+                         b->zpart, nch, b->Zc);
+      BD_LAUNCH("zc_reduce_kernel");
+    }
+    BD_TRY(hipEventRecord(b->ev_t, b->side));
+    if (yh) {
+      hipStream_t qst = b->qs ? b->qs : b->side;
+      if (b->qs) BD_TRY(hipStreamWaitEvent(b->qs, b->ev_t, 0));
+      int rc = qt_panel(b, j, qst);
+      if (rc) return rc;
+    }
+    const int chunk = symm_chunk(mt);
+    const int sch = (mt + chunk - 1) / chunk;
+    hipLaunchKernelGGL(symm_kernel, dim3(mt, sch), dim3(256), 0, s, b->Ab, np, b->U,
+                       (int64_t)BAND_ULD, j + 1, mt, chunk, b->Xp);
+    BD_LAUNCH("symm_kernel");
+    hipLaunchKernelGGL(psum_kernel, dim3(TS * TS / 512, mt), dim3(256), 0, s, b->Xp, sch, b->X);
+    BD_LAUNCH("psum_kernel");
+    BD_TRY(hipStreamWaitEvent(s, b->ev_t, 0));
+    if (Q > 0) {
+      hipLaunchKernelGGL(xcorr_kernel, dim3(mt), dim3(256), 0, s, b->X, PA + r0 * ldg, ldg, b->Zc,
+                         2 * TS * Q);
+      BD_LAUNCH("xcorr_kernel");
+    }
+    hipLaunchKernelGGL(xt_kernel, dim3(mt), dim3(256), 0, s, b->X, T);
+    BD_LAUNCH("xt_kernel");
+    hipLaunchKernelGGL(tn_partial_kernel, dim3(nch), dim3(256), 0, s, Ur + TS,
+                       (int64_t)BAND_ULD, b->X, (int64_t)TS, m, b->tnp);
+    BD_LAUNCH("tn_partial_kernel");
+    hipLaunchKernelGGL(tn_reduce_kernel, dim3(TS * TS / 64), dim3(256), 0, s, b->tnp, nch, b->M,
+                       1.0);
+    BD_LAUNCH("tn_reduce_kernel");
+    hipLaunchKernelGGL(z_kernel, dim3(1), dim3(256), 0, s, T, b->M, b->Zh);
+    BD_LAUNCH("z_kernel");
+    hipLaunchKernelGGL(w_kernel, dim3(mt), dim3(256), 0, s, b->X, Ur, (int64_t)BAND_ULD, b->Zh);
+    BD_LAUNCH("w_kernel");
+    // the pair into pending slot Q
+    hipLaunchKernelGGL(slot_copy_kernel, dim3((unsigned)((int64_t)m * TS / 512)), dim3(256), 0, s,
+                       Ur, (int64_t)BAND_ULD, m, b->UA + r0 * ldg + (int64_t)(p + Q) * TS,
+                       b->UB + r0 * ldg + (int64_t)(p - 1 - Q) * TS,
+                       b->UA + r0 * ldg + (int64_t)(p - 1 - Q) * TS,
+                       b->UB + r0 * ldg + (int64_t)(p + Q) * TS, ldg);
+    BD_LAUNCH("slot_copy_kernel");
+    ++Q;
+    if (Q < p && j + 2 < nt) continue;
+    // group end: ONE rank-256Q SYR2K of the trailing block
+    const double* GA = b->UA + (int64_t)(p - Q) * TS;
+    const double* GB = b->UB + (int64_t)(p - Q) * TS;
+    const int kd = 2 * TS * Q;
+    if (la && j + 2 < nt) {
+      hipLaunchKernelGGL(syr2k_g_kernel, dim3(mt), dim3(256), 0, s, b->Ab, np, GA, GB, ldg, kd,
+                         j + 1, mt, 1);
+      BD_LAUNCH("syr2k_g_kernel");
+      BD_TRY(hipEventRecord(b->ev_col, s));
+      BD_TRY(hipStreamWaitEvent(b->s_pan, b->ev_col, 0));
+      int rc = panel_qr(b, j + 1, b->s_pan, mode);
+      if (rc) return rc;
+      BD_TRY(hipEventRecord(b->ev_pan, b->s_pan));
+      const int rest = (mt - 1) * mt / 2;
+      const int cap = b->cq_la_grid > 0 ? b->cq_la_grid : rest;
+      hipLaunchKernelGGL(syr2k_g_rest_kernel, dim3(std::min(rest, cap)), dim3(256), 0, s, b->Ab,
+                         np, GA, GB, ldg, kd, j + 1, mt);
+      BD_LAUNCH("syr2k_g_rest_kernel");
+      BD_TRY(hipStreamWaitEvent(s, b->ev_pan, 0));
+      ahead = true;
+    } else {
+      const int tiles = mt * (mt + 1) / 2;
+      hipLaunchKernelGGL(syr2k_g_kernel, dim3(tiles), dim3(256), 0, s, b->Ab, np, GA, GB, ldg, kd,
+                         j + 1, mt, 0);
+      BD_LAUNCH("syr2k_g_kernel");
+    }
+    Q = 0;
+  }
+  if (yh) {
+    BD_TRY(hipEventRecord(b->ev_q, b->qs ? b->qs : b->side));
+    BD_TRY(hipStreamWaitEvent(s, b->ev_q, 0));
+  }
+  if (nt > 1) {
+    hipLaunchKernelGGL(cq_top_kernel, dim3(nt - 1), dim3(256), 0, s, b->cqL, b->cqLinv, b->cqflag,
+                       b->cqS, b->cqscr, b->Ab, np);
+    BD_LAUNCH("cq_top_kernel");
+  }
+  BD_TRY(hipEventRecord(b->ev1, s));
+  int herr = 0;
+  std::vector<int> hflag(8 * nt);
+  BD_TRY(hipMemcpyAsync(&herr, b->err, sizeof(int), hipMemcpyDeviceToHost, s));
+  BD_TRY(hipMemcpyAsync(hflag.data(), b->cqflag, sizeof(int) * hflag.size(),
+                        hipMemcpyDeviceToHost, s));
+  BD_TRY(hipEventSynchronize(b->ev1));
+  BD_TRY(hipStreamSynchronize(s));
+  if (herr) return set_error(-1201, "band reduction: panel hand-off timed out (workgroups not co-resident?)");
+  for (int j = 0; j + 1 < nt; ++j)
+    if (hflag[8 * j + 4]) ++b->cq_panel_fallbacks;
+  float ms = 0.f;
+  BD_TRY(hipEventElapsedTime(&ms, b->ev0, b->ev1));
+  b->reduce_ms = ms;
+  return 0;
+}
+
 // The reduction with the single-launch panel QR; if a hand-off times out (its
 // workgroups were not all resident, e.g. the GPU is shared or partitioned), the
 // whole reduction is redone from K with the per-column panel launches.
@@ -507,7 +682,7 @@ int band_reduce(gpmi_band* b, const double* K, const std::vector<double>* yh = n
     // a failed CholeskyQR panel is refactored in place (cq_panel); only a timed-out
     // guarded Householder panel (its workgroups not co-resident on a shared GPU)
     // sends the reduction back, straight to the per-column launches
-    rc = band_reduce_pass(b, K, yh, 0);
+    rc = b->delay > 1 ? band_reduce_pass_delayed(b, K, yh) : band_reduce_pass(b, K, yh, 0);
     if (rc != -1201) return rc;
     ++b->cq_fallbacks;
     ++b->panel_fallbacks;
@@ -581,6 +756,7 @@ int gpmi_band_create(gpmi_op* op, gpmi_band** out) {
   if (const char* lg = std::getenv("GPMI_BAND_CQ_LA_GRID"))
     b->cq_la_grid = std::max(0, std::atoi(lg));
   if (const char* pm = std::getenv("GPMI_BAND_PANEL")) b->panel_mode = std::strcmp(pm, "hh") == 0;
+  if (const char* dl = std::getenv("GPMI_BAND_DELAY")) b->delay = std::max(1, std::min(8, std::atoi(dl)));
   // GPMI_CQ_FO=0: every CholeskyQR pass by an exact Cholesky (no first-order passes)
   if (const char* fo = std::getenv("GPMI_CQ_FO"))
     if (std::atoi(fo) == 0) b->cq_fo[1] = b->cq_fo[2] = 0.0;

@@ -553,6 +553,227 @@ __global__ void lanczos_scalar_kernel(const double* __restrict__ H1k,
   nb[c] = 1.0;
 }
 
+// ---------------------------------------------------------------------------
+// Lanczos with delayed classical Gram-Schmidt reorthogonalisation (DCGS2:
+// Bielich, Langou, Thomas, Swirydowicz, Yamazaki, Boman, Parallel Computing 112
+// (2022) 102940; numpy prototype tools/dcgs2_proto.py). CGS2 reads the basis four
+// times per step (two dot passes, two update passes); here step k reads it twice:
+//   y = (K) u_k                                  (SpMM of the once-projected u_k)
+//   dots:   s = V^T u_k, t = V^T y, sigma = u.u, tau = u.y   (ONE pass, lz_dots)
+//   scalar: rho = sqrt(sigma - s.s) = beta_{k-1}, H[:, k-1] += s (alpha_{k-1}
+//           final), Hs = H s (K V s = V_{k+1} H s), h = V_{k+1}^T K v_k from
+//           (t, tau, Hs)                                 (lz_scalar)
+//   update: v_k = (u - V s) / rho, u_{k+1} = y / rho - V_{k+1} (Hs / rho + h)
+//           (ONE pass, both vectors, lz_update)
+// Per probe column c; every reduction has a fixed order (deterministic).
+
+// partial[b][v][c] over this block's rows: v = j0 + q: V_{j0+q} . u; v = J + j0 + q:
+// V_{j0+q} . y (Y given); with j0 == 0 also v = 2J: u . u and 2J + 1: u . y.
+// Vectors [j0, j0 + LZ_JC) of the J per launch; rows grid-strided, one column per
+// thread (256 / s rows per block iteration).
+__global__ __launch_bounds__(256) void lz_dots_kernel(const double* __restrict__ V, int64_t ns,
+                                                      int J, int j0,
+                                                      const double* __restrict__ U,
+                                                      const double* __restrict__ Y, int64_t n,
+                                                      int s, int nv,
+                                                      double* __restrict__ partial) {
+  __shared__ double red[256];
+  const int t = threadIdx.x;
+  const int rows_per = 256 / s;
+  const int c = t % s, r = t / s;
+  const int jc = min(LZ_JC, J - j0);
+  double as[LZ_JC], at[LZ_JC];
+#pragma unroll
+  for (int q = 0; q < LZ_JC; ++q) as[q] = at[q] = 0.0;
+  double uu = 0.0, uy = 0.0;
+  if (r < rows_per)
+    for (int64_t i = (int64_t)blockIdx.x * rows_per + r; i < n;
+         i += (int64_t)gridDim.x * rows_per) {
+      const int64_t e = i * s + c;
+      const double u = U[e];
+      const double y = Y ? Y[e] : 0.0;
+      double v[LZ_JC];
+#pragma unroll
+      for (int q = 0; q < LZ_JC; ++q) v[q] = q < jc ? V[(int64_t)(j0 + q) * ns + e] : 0.0;
+      uu += u * u;
+      uy += u * y;
+#pragma unroll
+      for (int q = 0; q < LZ_JC; ++q) {
+        as[q] += v[q] * u;
+        at[q] += v[q] * y;
+      }
+    }
+  // per column: the rows_per threads of column c summed in row order
+  auto put = [&](double val, int vi) {
+    red[t] = val;
+    __syncthreads();
+    if (t < s) {
+      double acc = 0.0;
+      for (int q = 0; q < rows_per; ++q) acc += red[q * s + t];
+      partial[((int64_t)blockIdx.x * nv + vi) * s + t] = acc;
+    }
+    __syncthreads();
+  };
+  for (int q = 0; q < jc; ++q) {
+    put(as[q], j0 + q);
+    if (Y) put(at[q], J + j0 + q);
+  }
+  if (j0 == 0) {
+    put(uu, 2 * J);
+    put(uy, 2 * J + 1);
+  }
+}
+
+// Step k's scalars (one workgroup; d = reduced dots [(2k + 2)][s]; per column c:
+// H [c][(steps + 2) x (steps + 1)] row-major (H[i][j]: coefficient of v_i in K v_j),
+// the update coefficients cv [k][s] (of V_j in v_k, times -1), cu [k + 1][s] (of V_j
+// in u_{k+1}, times -1), ir[s] = 1 / rho; alpha / beta [c][steps] as lanczos_scalar;
+// inexact[c]: sigma - s.s lost more than six digits to cancellation (rho then
+// unreliable; the host reruns the block with CGS2).
+__global__ void lz_scalar_kernel(const double* __restrict__ d, int k, int steps, int s,
+                                 double* __restrict__ H, double* __restrict__ cv,
+                                 double* __restrict__ cu, double* __restrict__ ir,
+                                 double* __restrict__ rho_s, int* __restrict__ dead,
+                                 int* __restrict__ inexact, double* __restrict__ alpha,
+                                 double* __restrict__ beta) {
+  const int ld = steps + 1;
+  const size_t hsz = (size_t)(steps + 2) * ld;
+  const int J = k;
+  const int t = threadIdx.x;
+  if (t < s) {
+    const int c = t;
+    if (k == 0) {
+      dead[c] = 0;
+      inexact[c] = 0;
+    }
+    double* Hc = H + c * hsz;
+    double rho = 1.0;
+    if (k > 0) {
+      double ss = 0.0;
+      for (int j = 0; j < J; ++j) {
+        const double sj = d[j * s + c];
+        ss += sj * sj;
+        Hc[j * ld + (k - 1)] += sj;
+      }
+      const double sig = d[2 * J * s + c];
+      const double dd = sig - ss;
+      rho = sqrt(fmax(dd, 0.0));
+      const double a = dead[c] ? 0.0 : Hc[(k - 1) * ld + (k - 1)];
+      double b = dead[c] ? 0.0 : rho;
+      if (!dead[c] && !(b > 1e-13 * fmax(1.0, fabs(a)))) {
+        dead[c] = 1;
+        b = 0.0;
+      } else if (!dead[c] && !(dd >= 1e-6 * sig)) {
+        inexact[c] = 1;
+      }
+      alpha[(int64_t)c * steps + (k - 1)] = a;
+      beta[(int64_t)c * steps + (k - 1)] = b;
+      if (!dead[c] && k < steps) Hc[k * ld + (k - 1)] = rho;
+    }
+    rho_s[c] = dead[c] ? 0.0 : rho;
+  }
+  if (k == steps) return;
+  __syncthreads();
+  // Hs_i = sum_{j >= i - 1} H[i][j] s_j (H upper Hessenberg), thread per (c, i); into cu
+  for (int task = t; task < s * (k + 1); task += blockDim.x) {
+    const int c = task % s, i = task / s;
+    const double* Hc = H + c * hsz;
+    double acc = 0.0;
+    for (int j = i > 0 ? i - 1 : 0; j < J; ++j) acc += Hc[i * ld + j] * d[j * s + c];
+    cu[i * s + c] = acc;
+  }
+  __syncthreads();
+  if (t < s) {
+    const int c = t;
+    double* Hc = H + c * hsz;
+    const double rho = rho_s[c];
+    if (rho == 0.0) {
+      for (int j = 0; j < J; ++j) cv[j * s + c] = 0.0;
+      for (int i = 0; i <= k; ++i) cu[i * s + c] = 0.0;
+      ir[c] = 0.0;
+    } else {
+      const double inv = 1.0 / rho;
+      double st = 0.0;
+      for (int j = 0; j < J; ++j) st += d[j * s + c] * d[(J + j) * s + c];
+      const double tau = d[(2 * J + 1) * s + c];
+      for (int i = 0; i < k; ++i) {
+        const double hs = cu[i * s + c];
+        const double h = (d[(J + i) * s + c] - hs) * inv;
+        Hc[i * ld + k] = h;
+        cu[i * s + c] = hs * inv + h;
+        cv[i * s + c] = d[i * s + c] * inv;
+      }
+      const double hsk = cu[k * s + c];
+      const double hk = (tau - st) * inv * inv - hsk * inv;
+      Hc[k * ld + k] = hk;
+      cu[k * s + c] = hsk * inv + hk;
+      ir[c] = inv;
+    }
+  }
+}
+
+// v_k = u / rho - sum_{j<k} V_j cv_j;  u <- y / rho - sum_{j<k} V_j cu_j - v_k cu_k;
+// V_k = v_k. Two consecutive elements per thread (16-byte loads), the basis loads
+// four vectors at a time.
+__global__ __launch_bounds__(256) void lz_update_kernel(double* __restrict__ V, int64_t ns, int k,
+                                                        double* __restrict__ U,
+                                                        const double* __restrict__ Y,
+                                                        const double* __restrict__ cv,
+                                                        const double* __restrict__ cu,
+                                                        const double* __restrict__ ir, int s) {
+  const int64_t e = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 2;
+  if (e >= ns) return;
+  const int c0 = (int)(e % s), c1 = (c0 + 1 == s) ? 0 : c0 + 1;
+  if (e + 1 < ns && (ns & 1) == 0) {
+    const d2 u = *reinterpret_cast<const d2*>(U + e);
+    const d2 y = *reinterpret_cast<const d2*>(Y + e);
+    double v0 = u[0] * ir[c0], v1 = u[1] * ir[c1];
+    double w0 = y[0] * ir[c0], w1 = y[1] * ir[c1];
+    int j = 0;
+    for (; j + 4 <= k; j += 4) {
+      d2 a[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) a[q] = *reinterpret_cast<const d2*>(V + (j + q) * ns + e);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        v0 -= a[q][0] * cv[(j + q) * s + c0];
+        v1 -= a[q][1] * cv[(j + q) * s + c1];
+        w0 -= a[q][0] * cu[(j + q) * s + c0];
+        w1 -= a[q][1] * cu[(j + q) * s + c1];
+      }
+    }
+    for (; j < k; ++j) {
+      const d2 a = *reinterpret_cast<const d2*>(V + j * ns + e);
+      v0 -= a[0] * cv[j * s + c0];
+      v1 -= a[1] * cv[j * s + c1];
+      w0 -= a[0] * cu[j * s + c0];
+      w1 -= a[1] * cu[j * s + c1];
+    }
+    w0 -= v0 * cu[k * s + c0];
+    w1 -= v1 * cu[k * s + c1];
+    d2 vo, wo;
+    vo[0] = v0;
+    vo[1] = v1;
+    wo[0] = w0;
+    wo[1] = w1;
+    *reinterpret_cast<d2*>(V + k * ns + e) = vo;
+    *reinterpret_cast<d2*>(U + e) = wo;
+  } else {
+    for (int64_t f = e; f < e + 2 && f < ns; ++f) {
+      const int c = (int)(f % s);
+      double v = U[f] * ir[c], w = Y[f] * ir[c];
+      for (int j = 0; j < k; ++j) {
+        const double a = V[j * ns + f];
+        v -= a * cv[j * s + c];
+        w -= a * cu[j * s + c];
+      }
+      w -= v * cu[k * s + c];
+      V[k * ns + f] = v;
+      U[f] = w;
+    }
+  }
+}
+
 // Normalised Rademacher probes: V[i][c] = +-1/sqrt(n), bit 63 of
 // splitmix64(seed * G + (c + c0) * H + i) (matches oracle/sparse.py).
 // perm (optional): device row r holds original point perm[r] (locality order of

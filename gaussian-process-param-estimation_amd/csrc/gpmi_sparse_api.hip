@@ -54,6 +54,12 @@ __global__ void col_gs_update_kernel(double*, const double*, int64_t, const doub
                                      int);
 __global__ void col_axpby_kernel(const double*, double*, const double*, const double*, int64_t,
                                  int);
+__global__ void lz_dots_kernel(const double*, int64_t, int, int, const double*, const double*,
+                               int64_t, int, int, double*);
+__global__ void lz_scalar_kernel(const double*, int, int, int, double*, double*, double*, double*,
+                                 double*, int*, int*, double*, double*);
+__global__ void lz_update_kernel(double*, int64_t, int, double*, const double*, const double*,
+                                 const double*, const double*, int);
 __global__ void rademacher_kernel(double*, int64_t, int, unsigned long long, int, double,
                                   const int*);
 __global__ void csr_permute_kernel(const int64_t*, const int*, const double*, const int*,
@@ -135,6 +141,9 @@ struct gpmi_sp {
   double* msbuf = nullptr;     // multi-shift CG scalar state
   double* lz = nullptr;        // Lanczos scalars (lanczos_block)
   size_t lz_doubles = 0;
+  double* lzd = nullptr;       // DCGS2 Lanczos scalars (lanczos_block_dcgs2)
+  size_t lzd_doubles = 0;
+  int lanczos_cgs2_reruns = 0; // DCGS2 blocks rerun with CGS2 (cancellation in rho)
   size_t msbuf_doubles = 0;
   int last_converged = 1;      // last gpmi_sp_cg / gpmi_sp_msgram met rtol in every column
   // Locality order (gpmi_sp_create_matern, d <= 3): device row r is original point
@@ -389,6 +398,76 @@ int lanczos_block(gpmi_sp* sp, double* V, double* W, int s, int steps, double* h
   return 0;
 }
 
+constexpr int LZ_NB = 512;   // row blocks of the DCGS2 dot partials (fixed: deterministic)
+
+// Lanczos of K on s probe columns from V block 0 (normalised probes) with DCGS2
+// reorthogonalisation (lz_*_kernel in gpmi_sparse.hip): per step one SpMM, one dot
+// pass and one update pass over the basis. V: steps blocks [n][s]; U, Y: one block
+// each. alpha / beta: host [s][steps]. *inexact: a column lost more than six digits
+// of rho to cancellation (the caller reruns the block with CGS2).
+int lanczos_block_dcgs2(gpmi_sp* sp, double* V, double* U, double* Y, int s, int steps,
+                        double* h_alpha, double* h_beta, bool* inexact) {
+  const int64_t n = sp->n, ns = n * s;
+  const size_t hsz = (size_t)(steps + 2) * (steps + 1);
+  const size_t need = (size_t)s * hsz + (size_t)(2 * steps + 2) * s + (size_t)steps * s +
+                      (size_t)(steps + 1) * s + 2 * (size_t)s + 2 * (size_t)s * steps + 2 * s;
+  if (sp->lzd_doubles < need) {
+    if (sp->lzd) SP_TRY(hipFree(sp->lzd));
+    sp->lzd = nullptr;
+    SP_TRY(hipMalloc(&sp->lzd, sizeof(double) * need));
+    sp->lzd_doubles = need;
+  }
+  double* H = sp->lzd;
+  double* d = H + (size_t)s * hsz;
+  double* cv = d + (size_t)(2 * steps + 2) * s;
+  double* cu = cv + (size_t)steps * s;
+  double* ir = cu + (size_t)(steps + 1) * s;
+  double* rho = ir + s;
+  double* dal = rho + s;
+  double* dbe = dal + (size_t)s * steps;
+  int* dead = reinterpret_cast<int*>(dbe + (size_t)s * steps);
+  int* inex = dead + s;
+  int rc = ensure_partial(sp, (size_t)LZ_NB * (2 * steps + 2) * s);
+  if (rc) return rc;
+  SP_TRY(hipMemsetAsync(H, 0, sizeof(double) * s * hsz, sp->stream));
+  SP_TRY(hipMemsetAsync(dal, 0, sizeof(double) * 2 * s * steps, sp->stream));
+  SP_TRY(hipMemcpyAsync(U, V, sizeof(double) * ns, hipMemcpyDeviceToDevice, sp->stream));
+  for (int k = 0; k <= steps; ++k) {
+    const bool last = k == steps;
+    if (!last) {
+      rc = spmm(sp, U, Y, s, 0.0);
+      if (rc) return rc;
+    }
+    const int nv = 2 * k + 2;
+    for (int j0 = 0; j0 == 0 || j0 < k; j0 += LZ_JC) {
+      hipLaunchKernelGGL(lz_dots_kernel, dim3(LZ_NB), dim3(256), 0, sp->stream, V, ns, k, j0, U,
+                         last ? (const double*)nullptr : Y, n, s, nv, sp->partial);
+      SP_LAUNCH("lz_dots_kernel");
+    }
+    hipLaunchKernelGGL(col_dot_reduce_kernel, dim3((nv * s + 3) / 4), dim3(256), 0, sp->stream,
+                       sp->partial, LZ_NB, nv, s, d);
+    SP_LAUNCH("col_dot_reduce_kernel");
+    hipLaunchKernelGGL(lz_scalar_kernel, dim3(1), dim3(1024), 0, sp->stream, d, k, steps, s, H, cv,
+                       cu, ir, rho, dead, inex, dal, dbe);
+    SP_LAUNCH("lz_scalar_kernel");
+    if (!last) {
+      hipLaunchKernelGGL(lz_update_kernel, dim3((unsigned)((ns + 511) / 512)), dim3(256), 0,
+                         sp->stream, V, ns, k, U, Y, cv, cu, ir, s);
+      SP_LAUNCH("lz_update_kernel");
+    }
+  }
+  std::vector<int> hin(s);
+  SP_TRY(hipMemcpyAsync(h_alpha, dal, sizeof(double) * s * steps, hipMemcpyDeviceToHost,
+                        sp->stream));
+  SP_TRY(hipMemcpyAsync(h_beta, dbe, sizeof(double) * s * steps, hipMemcpyDeviceToHost,
+                        sp->stream));
+  SP_TRY(hipMemcpyAsync(hin.data(), inex, sizeof(int) * s, hipMemcpyDeviceToHost, sp->stream));
+  SP_TRY(hipStreamSynchronize(sp->stream));
+  *inexact = false;
+  for (int c = 0; c < s; ++c) *inexact = *inexact || hin[c];
+  return 0;
+}
+
 }  // namespace
 
 extern "C" {
@@ -633,6 +712,7 @@ int gpmi_sp_destroy(gpmi_sp* sp) {
   if (sp->small) (void)hipFree(sp->small);
   if (sp->msbuf) (void)hipFree(sp->msbuf);
   if (sp->lz) (void)hipFree(sp->lz);
+  if (sp->lzd) (void)hipFree(sp->lzd);
   if (sp->win_cols) (void)hipFree(sp->win_cols);
   if (sp->win_u) (void)hipFree(sp->win_u);
   if (sp->win_lidx) (void)hipFree(sp->win_lidx);
@@ -764,12 +844,34 @@ int gpmi_sp_lanczos(gpmi_sp* sp, int nprobe, int steps, uint64_t seed, int probe
     if (rc) return rc;
     double* V = sp->ws;
     double* W = sp->ws + (size_t)(steps + 1) * n * s;
-    hipLaunchKernelGGL(rademacher_kernel, dim3(grid_ns(n, s)), dim3(256), 0, sp->stream, V, n, s,
-                       (unsigned long long)seed, probe_offset + p0, 1.0 / std::sqrt((double)n),
-                       (const int*)sp->perm_d);
-    SP_LAUNCH("rademacher_kernel");
-    rc = lanczos_block(sp, V, W, s, steps, alpha + (size_t)p0 * steps, beta + (size_t)p0 * steps);
-    if (rc) return rc;
+    auto probes = [&]() -> int {
+      hipLaunchKernelGGL(rademacher_kernel, dim3(grid_ns(n, s)), dim3(256), 0, sp->stream, V, n,
+                         s, (unsigned long long)seed, probe_offset + p0,
+                         1.0 / std::sqrt((double)n), (const int*)sp->perm_d);
+      SP_LAUNCH("rademacher_kernel");
+      return 0;
+    };
+    if ((rc = probes())) return rc;
+    // DCGS2 (default; GPMI_LANCZOS=cgs2 selects CGS2). A block whose rho lost
+    // precision to cancellation (near an invariant subspace) is redone with CGS2.
+    const char* lenv = std::getenv("GPMI_LANCZOS");
+    bool cgs2 = lenv && std::strcmp(lenv, "cgs2") == 0;
+    if (!cgs2) {
+      bool inexact = false;
+      rc = lanczos_block_dcgs2(sp, V, sp->ws + (size_t)steps * n * s, W, s, steps,
+                               alpha + (size_t)p0 * steps, beta + (size_t)p0 * steps, &inexact);
+      if (rc) return rc;
+      if (inexact) {
+        ++sp->lanczos_cgs2_reruns;
+        cgs2 = true;
+        if ((rc = probes())) return rc;
+      }
+    }
+    if (cgs2) {
+      rc = lanczos_block(sp, V, W, s, steps, alpha + (size_t)p0 * steps,
+                         beta + (size_t)p0 * steps);
+      if (rc) return rc;
+    }
   }
   return 0;
 }
@@ -875,7 +977,20 @@ int gpmi_sp_msgram(gpmi_sp* sp, const double* etas, int neta, const double* rhs,
     return set_error(-1104, "msgram: need 1 <= nrhs <= 16 and neta * nrhs <= 1024");
   Guard g(sp->device);
   const int64_t n = sp->n;
-  const int s = nrhs, S = neta;
+  const int S = neta;
+  // an odd block that would run the one-column gather SpMM gets a zero column (an
+  // inactive CG column from the start: ||b|| = 0) so that the column-pair gather
+  // runs (cfg 5, s = 11 -> 12); the Gram of the real columns is unchanged
+  int s = nrhs;
+  {
+    int kind = 0;
+    int rc0 = spmm_kind(sp, s, &kind);
+    if (rc0) return rc0;
+    const char* penv = std::getenv("GPMI_MSGRAM_PAD");
+    if (kind == 0 && (s & 1) && s + 1 <= MS_MAXS && S * (s + 1) <= 1024 &&
+        !(penv && std::atoi(penv) == 0))
+      ++s;
+  }
   const int64_t ns = n * s;
   const double eta0 = *std::min_element(etas, etas + neta);
   int rc = ensure_ws(sp, (size_t)5 * ns);
@@ -922,9 +1037,9 @@ int gpmi_sp_msgram(gpmi_sp* sp, const double* etas, int neta, const double* rhs,
   double* Rnext = Rd2;
   hipStream_t str = sp->stream;
   {
-    std::vector<double> h((size_t)ns);
+    std::vector<double> h((size_t)ns, 0.0);
     for (int64_t i = 0; i < n; ++i)
-      for (int c = 0; c < s; ++c) h[(size_t)i * s + c] = rhs[orig_row(sp, i) * ld + c];
+      for (int c = 0; c < nrhs; ++c) h[(size_t)i * s + c] = rhs[orig_row(sp, i) * ld + c];
     SP_TRY(hipMemcpyAsync(Bd, h.data(), sizeof(double) * ns, hipMemcpyHostToDevice, str));
     std::vector<double> hd(S);
     for (int j = 0; j < S; ++j) hd[j] = etas[j] - eta0;
@@ -1001,7 +1116,10 @@ int gpmi_sp_msgram(gpmi_sp* sp, const double* etas, int neta, const double* rhs,
   std::vector<double> hg((size_t)S * s * s);
   SP_TRY(hipMemcpyAsync(hg.data(), st.g, sizeof(double) * hg.size(), hipMemcpyDeviceToHost, str));
   SP_TRY(hipStreamSynchronize(str));
-  std::copy(hg.begin(), hg.end(), G);
+  for (int j = 0; j < S; ++j)
+    for (int a = 0; a < nrhs; ++a)
+      for (int c = 0; c < nrhs; ++c)
+        G[((size_t)j * nrhs + a) * nrhs + c] = hg[((size_t)j * s + a) * s + c];
   if (iterations) *iterations = it;
   return 0;
 }

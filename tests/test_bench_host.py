@@ -42,8 +42,9 @@ def test_sparse_step_bytes_model():
     bl, bc = 8.0 * n * 4, 8.0 * n * 2
     lz = 0.0
     for k in range(3):
-        lz += csr + 2 * bl + (3 * bl if k else 0) + 2 * ((k + 2) + (k + 3)) * bl + 3 * bl
+        lz += csr + 2 * bl + (k + 2) * bl + (k + 4) * bl
+    lz += 4 * bl
     assert b['lanczos'] == lz
-    assert b['lanczos_basis_reads'] == sum(4 * (k + 1) * bl for k in range(3))
-    assert b['cg'] == 10 * (csr + 11 * bc)
+    assert b['lanczos_basis_reads'] == sum(2 * k * bl for k in range(3)) + 3 * bl
+    assert b['cg'] == 10 * (csr + 12 * bc)
     assert b['total'] == b['lanczos'] + b['cg']

@@ -1,0 +1,19 @@
+# Sparse iteration: the sparse GPU tests, then sparse5 / sparse4 bench lines
+# (no CPU baseline), and sparse5 with CGS2 Lanczos for comparison. Logs under
+# gpurun_out/$1/.
+set -o pipefail
+export TMPDIR=/tmp
+D=gpurun_out/${1:-sp}
+mkdir -p $D
+timeout -k 10 600 python -u -m pytest tests/test_gpu_sparse.py -m gpu -v --timeout 300 --timeout-method thread > $D/tests.log 2>&1 || { tail -40 $D/tests.log; exit 1; }
+tail -1 $D/tests.log
+for cfg in sparse5 sparse4; do
+  timeout -k 10 200 python -u bench.py --config $cfg --no-cpu-baseline > $D/bench_$cfg.json 2> $D/bench_$cfg.err || { tail -5 $D/bench_$cfg.err; exit 1; }
+done
+GPMI_LANCZOS=cgs2 timeout -k 10 200 python -u bench.py --config sparse5 --no-cpu-baseline > $D/bench_sparse5_cgs2.json 2> $D/bench_sparse5_cgs2.err || exit 1
+python - $D <<'PY'
+import json, sys
+for f in ('bench_sparse5', 'bench_sparse4', 'bench_sparse5_cgs2'):
+    d = json.load(open('%s/%s.json' % (sys.argv[1], f)))
+    print(f, round(d['value'], 1), 'evals/s', round(d['ms_per_step'], 2), 'ms', 'step frac', d['step_roofline']['frac'], 'spmm frac', d['roofline']['frac'], 'cg it', d['step_roofline']['cg_iterations'])
+PY
