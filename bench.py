@@ -368,7 +368,7 @@ def sparse_measure(args, config, world, rank, local, dist, torch, cpu, exact):
     from gaussian_proc import generate_correlation, _data
     from gaussian_proc._mixed_correlation import MixedCorrelation
     from gaussian_proc._likelihood._direct_likelihood import _lp_from_terms
-    from gaussian_proc.sweep import slq_sweep, shard
+    from gaussian_proc.sweep import slq_gram_sweep, shard
     npts, dim, rho, nu, dens, nprobe, steps, neta = SPARSE_CONFIGS[config]
     points = _data.generate_points(npts, dim, True)
     z = _data.generate_data(points, 0.2)
@@ -394,12 +394,12 @@ def sparse_measure(args, config, world, rank, local, dist, torch, cpu, exact):
     holder = {'cg_iters': 0}
 
     def step():
-        curves = slq_sweep(op, etas)
+        # the SLQ Lanczos of the probe shard and the multi-shift CG Gram blocks of
+        # the eta shard (rtol 1e-6) run together on two streams (sweep.slq_gram_sweep)
+        curves, _, Gs = slq_gram_sweep(op, etas, R, rtol=1e-6)
         holder['curves'] = curves
         rows = numpy.zeros((per, 3))
         if hi > lo:
-            # all Gram blocks of the eta shard from one multi-shift CG (rtol 1e-6)
-            Gs = op.sop.msgram(etas[lo:hi], R, rtol=1e-6)
             holder['cg_iters'] = op.sop.last_cg_iterations
             for i, e in enumerate(etas[lo:hi]):
                 rows[i] = [e, curves['logdet'][lo + i],
@@ -711,6 +711,26 @@ def band_mode(args, D, X, z, world, rank, dist, torch, ld_ref=None):
     return out, op
 
 
+def band_nu25_check(D, points, X, z):
+    """BASELINE cfg3 as specified (nu = 2.5, smoother, so more nearly rank-deficient
+    panels): one band reduction of that K, its panel statistics (CholeskyQR
+    panels that fell back to Householder, reductions redone) and the band logdet /
+    lp against the reference's N = 16384 nu = 2.5 values (cfg3_nu25.json). The
+    resident K is reassembled at nu = 2.5 (the dense measurements are done)."""
+    from gaussian_proc._mixed_correlation import MixedCorrelation
+    n, m = X.shape
+    D.op.assemble_matern(points, numpy.full(2, 0.1), 2.5)
+    op = MixedCorrelation(D, imate_method='eigenvalue')
+    b = op.band()
+    op.refresh_band(X, z)
+    red = b.last_timing()['reduce_ms']
+    ld_err, lp_err = golden_errors(lambda e: op.loglik_terms(e, X, z), 2.5, n, m)
+    out = {'reduce_ms': round(red, 3), 'panel': b.stats(),
+           'logdet_rel_err_vs_reference': ld_err, 'lp_rel_err_vs_reference': lp_err}
+    b.close()
+    return out
+
+
 def band_batch_efficiency(op, X, z, batches=(8, 16, 32, 64)):
     """The band operator's per-rank eta batches of the strong-scaled curve at
     N = 8 / 4 / 2 / 1: device time of the banded-Cholesky call for that batch
@@ -950,6 +970,8 @@ def main():
         cb['lp_rel_diff_vs_device'] = abs(cb['lp_cholesky'] - lp_dev) / abs(lp_dev)
         result['cpu_baseline'] = cb
         result['speedup_vs_cpu'] = round(result['value'] / cb['value'], 1)
+    if rank == 0 and world == 1 and not args.no_band and args.nu == 1.5:
+        result['band_mode']['nu25_check'] = band_nu25_check(D, points, X, z)
     if world == 1 and not args.no_sparse:
         # release the dense and band operators (their streams count against the
         # process's hardware queues) before the sparse configs run

@@ -60,6 +60,21 @@ __global__ void zc_partial_kernel(const double* PB, int64_t ldb, const double* V
                                   int m, double* part);
 __global__ void zc_reduce_kernel(const double* part, int nch, double* Z);
 __global__ void xcorr_kernel(double* X, const double* PA, int64_t lda, const double* Z, int kdim);
+__global__ void bcr_f0_kernel(const double* Ab, int64_t lda, double* F0);
+__global__ void bcr_chol_kernel(const double* Ab, int64_t lda, const double* etas, int lvl,
+                                int first, const double* Din, int64_t sD, const double* Yin,
+                                int64_t sY, double* Lout, int64_t sL, int lout, double* Zall,
+                                int64_t sZ, double* logd, double* gpart, int* failv, int nt,
+                                int64_t n);
+__global__ void bcr_w_kernel(const double* Lin, int64_t sL, const double* Fin, int64_t sF,
+                             double* W, int64_t sW, int m);
+__global__ void bcr_upd_kernel(const double* Ab, int64_t lda, const double* etas, int lvl,
+                               const double* Din, int64_t sD, const double* Yin, int64_t sY,
+                               const double* W, int64_t sW, const double* Zall, int64_t sZ,
+                               double* Dout, double* Fout, double* Yout, int64_t sO, int64_t sOY,
+                               int m);
+__global__ void bcr_final_kernel(const double* logd, const double* gpart, const int* failv, int nt,
+                                 double* out, int out_ld, int* info);
 __global__ void qt_partial_kernel(const double* P, int64_t lda, int m, const double* Y,
                                   double* part);
 __global__ void qt_reduce_kernel(const double* part, int G, double* a);

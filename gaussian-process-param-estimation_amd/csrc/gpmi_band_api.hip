@@ -112,6 +112,9 @@ struct gpmi_band {
   // and inverses, the reconstruction's U^-T, V1, signs, scratch, failure flag
   int panel_mode = 0;        // 0 CholeskyQR, 1 Householder (single launch)
   int cq_fallbacks = 0;      // reductions redone with Householder panels
+  int la_lds = 0;            // dynamic LDS padding of the look-ahead SYR2K (bytes): with
+                             // > 6 KB only one of its workgroups fits a CU, so a grid cap
+                             // below the CU count leaves whole CUs to the panel chain
   int cq_la_grid = 448;      // SYR2K grid cap beside a CholeskyQR panel (0: none; measured
                              // at N = 16384: 448 161-163 ms, none 165-168, no look-ahead 164-166)
   double* Qb = nullptr;
@@ -134,6 +137,20 @@ struct gpmi_band {
   double* UB = nullptr;      // [n_pad][256 delay] = [V_{p-1} .. V_0 | W_0 .. W_{p-1}]
   double* zpart = nullptr;   // [2 delay][nt][128][128] partials of UB^T V
   double* Zc = nullptr;      // [2 delay][128][128]
+  // block cyclic reduction of B + eta I (gpmi_bcr.hip; GPMI_BAND_BCR): per eta
+  // capacity bcap, half = ceil(nt / 2) blocks per level
+  int bcr_mode = 0;          // 0 sequential band_chol_kernel, 1 cyclic reduction
+  int bcap = 0;
+  double* bcrD[2] = {nullptr, nullptr};   // [bcap][half][128][128]
+  double* bcrF[2] = {nullptr, nullptr};
+  double* bcrY[2] = {nullptr, nullptr};   // [bcap][half][128][16]
+  double* bcrL = nullptr;    // [bcap][half][128][128]
+  double* bcrW = nullptr;    // [bcap][half][2][128][128]
+  double* bcrZ = nullptr;    // [bcap][nt][128][16]
+  double* bcrG = nullptr;    // [bcap][nt][16][16]
+  double* bcrLd = nullptr;   // [bcap][nt]
+  int* bcrFail = nullptr;    // [bcap][nt]
+  double* bcrF0 = nullptr;   // [nt - 1][128][128]
   double* cqMinv = nullptr;  // C = U^-T M3 of the current panel
   double cq_fo[3] = {0.0, 1e-4, 3e-8};   // first-order thresholds on ||G - I||_F
   int cap = 0;
@@ -166,7 +183,10 @@ int band_free(gpmi_band* b) {
   double* bufs[] = {b->Ab, b->U, b->X, b->Xp, b->part, b->pivrow, b->tau, b->Tm, b->tnp, b->tnp2,
                     b->VtV, b->M, b->Zh, b->Y, b->qtp, b->qa, b->qb, b->etas, b->out, b->Ac, b->td,
                     b->fac, b->ysol, b->der, b->Qb, b->cqpart, b->cqG, b->cqL, b->cqLinv,
-                    b->cqMinv, b->cqS, b->cqscr, b->UA, b->UB, b->zpart, b->Zc};
+                    b->cqMinv, b->cqS, b->cqscr, b->UA, b->UB, b->zpart, b->Zc,
+                    b->bcrD[0], b->bcrD[1], b->bcrF[0], b->bcrF[1], b->bcrY[0], b->bcrY[1],
+                    b->bcrL, b->bcrW, b->bcrZ, b->bcrG, b->bcrLd, b->bcrF0};
+  if (b->bcrFail) (void)hipFree(b->bcrFail);
   if (b->cqflag) (void)hipFree(b->cqflag);
   for (double* p : bufs)
     if (p) (void)hipFree(p);
@@ -459,8 +479,9 @@ int band_reduce_pass(gpmi_band* b, const double* K, const std::vector<double>* y
       // CholeskyQR panel needs no co-resident workgroups (cq_la_grid, 0: no cap)
       const int cap = mode == 0 ? (b->cq_la_grid > 0 ? b->cq_la_grid : rest)
                       : b->la_grid > 0 ? b->la_grid : std::max(64, b->ncu - next_g);
-      hipLaunchKernelGGL(syr2k_rest_kernel, dim3(std::min(rest, cap)), dim3(256), 0, s, b->Ab,
-                         np, b->U, (int64_t)BAND_ULD, j + 1, mt);
+      hipLaunchKernelGGL(syr2k_rest_kernel, dim3(std::min(rest, cap)), dim3(256),
+                         mode == 0 ? b->la_lds : 0, s, b->Ab, np, b->U, (int64_t)BAND_ULD, j + 1,
+                         mt);
       BD_LAUNCH("syr2k_rest_kernel");
       BD_TRY(hipStreamWaitEvent(s, b->ev_pan, 0));
       ahead = true;
@@ -753,10 +774,12 @@ int gpmi_band_create(gpmi_op* op, gpmi_band** out) {
     return fail(e, "rhs stream");
   if (const char* la = std::getenv("GPMI_BAND_LA")) b->lookahead = std::atoi(la);
   if (const char* lg = std::getenv("GPMI_BAND_LA_GRID")) b->la_grid = std::max(0, std::atoi(lg));
+  if (const char* ll = std::getenv("GPMI_BAND_LA_LDS")) b->la_lds = std::max(0, std::atoi(ll));
   if (const char* lg = std::getenv("GPMI_BAND_CQ_LA_GRID"))
     b->cq_la_grid = std::max(0, std::atoi(lg));
   if (const char* pm = std::getenv("GPMI_BAND_PANEL")) b->panel_mode = std::strcmp(pm, "hh") == 0;
   if (const char* dl = std::getenv("GPMI_BAND_DELAY")) b->delay = std::max(1, std::min(8, std::atoi(dl)));
+  if (const char* bm = std::getenv("GPMI_BAND_BCR")) b->bcr_mode = std::atoi(bm) == 1 ? 1 : 0;
   // GPMI_CQ_FO=0: every CholeskyQR pass by an exact Cholesky (no first-order passes)
   if (const char* fo = std::getenv("GPMI_CQ_FO"))
     if (std::atoi(fo) == 0) b->cq_fo[1] = b->cq_fo[2] = 0.0;
@@ -924,6 +947,82 @@ int gpmi_band_set_rhs(gpmi_band* b, const double* rhs, int64_t ld, int nrhs) {
   return 0;
 }
 
+// The likelihood terms of neta eta (b->etas on the device) by block cyclic
+// reduction (gpmi_bcr.hip) into b->out / b->info, on stream s.
+int band_loglik_bcr(gpmi_band* b, int neta, hipStream_t s) {
+  const int nt = b->nt;
+  const int64_t np = b->n_pad;
+  const int half = (nt + 1) / 2;
+  if (b->bcap < neta) {
+    double** bufs[] = {&b->bcrD[0], &b->bcrD[1], &b->bcrF[0], &b->bcrF[1], &b->bcrY[0],
+                       &b->bcrY[1], &b->bcrL, &b->bcrW, &b->bcrZ, &b->bcrG, &b->bcrLd};
+    for (double** q : bufs)
+      if (*q) {
+        BD_TRY(hipFree(*q));
+        *q = nullptr;
+      }
+    if (b->bcrFail) BD_TRY(hipFree(b->bcrFail));
+    b->bcrFail = nullptr;
+    b->bcap = 0;
+    const size_t blk = (size_t)TS * TS, yb = (size_t)TS * RLD;
+    for (int q = 0; q < 2; ++q) {
+      BD_TRY(hipMalloc(&b->bcrD[q], sizeof(double) * neta * half * blk));
+      BD_TRY(hipMalloc(&b->bcrF[q], sizeof(double) * neta * half * blk));
+      BD_TRY(hipMalloc(&b->bcrY[q], sizeof(double) * neta * half * yb));
+    }
+    BD_TRY(hipMalloc(&b->bcrL, sizeof(double) * neta * half * blk));
+    BD_TRY(hipMalloc(&b->bcrW, sizeof(double) * neta * half * 2 * blk));
+    BD_TRY(hipMalloc(&b->bcrZ, sizeof(double) * neta * nt * yb));
+    BD_TRY(hipMalloc(&b->bcrG, sizeof(double) * neta * nt * RLD * RLD));
+    BD_TRY(hipMalloc(&b->bcrLd, sizeof(double) * neta * nt));
+    BD_TRY(hipMalloc(&b->bcrFail, sizeof(int) * neta * nt));
+    b->bcap = neta;
+  }
+  if (!b->bcrF0 && nt > 1) BD_TRY(hipMalloc(&b->bcrF0, sizeof(double) * (nt - 1) * TS * TS));
+  const int64_t sH = (int64_t)half * TS * TS, sHY = (int64_t)half * TS * RLD;
+  const int64_t sZ = (int64_t)nt * TS * RLD, sW = 2 * sH;
+  if (nt > 1) {
+    hipLaunchKernelGGL(bcr_f0_kernel, dim3(nt - 1), dim3(256), 0, s, b->Ab, np, b->bcrF0);
+    BD_LAUNCH("bcr_f0_kernel");
+  }
+  const double* Din = nullptr;
+  const double* Yin = b->Y;
+  const double* Fin = b->bcrF0;
+  int64_t sD = 0, sY = 0, sF = 0;
+  int m = nt, lvl = 0, cur = 0;
+  while (m > 1) {
+    const int nodd = m / 2, neven = (m + 1) / 2;
+    hipLaunchKernelGGL(bcr_chol_kernel, dim3(nodd, neta), dim3(256), 0, s, b->Ab, np, b->etas,
+                       lvl, 1, Din, sD, Yin, sY, b->bcrL, sH, 1, b->bcrZ, sZ, b->bcrLd, b->bcrG,
+                       b->bcrFail, nt, b->n);
+    BD_LAUNCH("bcr_chol_kernel");
+    hipLaunchKernelGGL(bcr_w_kernel, dim3(2 * nodd, neta), dim3(256), 0, s, b->bcrL, sH, Fin, sF,
+                       b->bcrW, sW, m);
+    BD_LAUNCH("bcr_w_kernel");
+    hipLaunchKernelGGL(bcr_upd_kernel, dim3(2 * neven, neta), dim3(256), 0, s, b->Ab, np, b->etas,
+                       lvl, Din, sD, Yin, sY, b->bcrW, sW, b->bcrZ, sZ, b->bcrD[cur], b->bcrF[cur],
+                       b->bcrY[cur], sH, sHY, m);
+    BD_LAUNCH("bcr_upd_kernel");
+    Din = b->bcrD[cur];
+    Yin = b->bcrY[cur];
+    Fin = b->bcrF[cur];
+    sD = sH;
+    sY = sHY;
+    sF = sH;
+    cur ^= 1;
+    m = neven;
+    ++lvl;
+  }
+  hipLaunchKernelGGL(bcr_chol_kernel, dim3(1, neta), dim3(256), 0, s, b->Ab, np, b->etas, lvl, 0,
+                     Din, sD, Yin, sY, b->bcrL, sH, 0, b->bcrZ, sZ, b->bcrLd, b->bcrG, b->bcrFail,
+                     nt, b->n);
+  BD_LAUNCH("bcr_chol_kernel");
+  hipLaunchKernelGGL(bcr_final_kernel, dim3(neta), dim3(256), 0, s, b->bcrLd, b->bcrG, b->bcrFail,
+                     nt, b->out, OUT_LD, b->info);
+  BD_LAUNCH("bcr_final_kernel");
+  return 0;
+}
+
 int gpmi_band_loglik(gpmi_band* b, const double* etas, int neta, double* logdet, double* gram,
                      int* info) {
   if (!b) return set_error(-1006, "null handle");
@@ -934,9 +1033,14 @@ int gpmi_band_loglik(gpmi_band* b, const double* etas, int neta, double* logdet,
   hipStream_t s = b->stream;
   BD_TRY(hipMemcpyAsync(b->etas, etas, sizeof(double) * neta, hipMemcpyHostToDevice, s));
   BD_TRY(hipEventRecord(b->ev0, s));
-  hipLaunchKernelGGL(band_chol_kernel, dim3(neta), dim3(256), 0, s, b->Ab, b->n_pad, b->nt, b->n,
-                     b->Y, b->etas, b->out, OUT_LD, b->info, nullptr, nullptr);
-  BD_LAUNCH("band_chol_kernel");
+  if (b->bcr_mode == 1) {
+    rc = band_loglik_bcr(b, neta, s);
+    if (rc) return rc;
+  } else {
+    hipLaunchKernelGGL(band_chol_kernel, dim3(neta), dim3(256), 0, s, b->Ab, b->n_pad, b->nt,
+                       b->n, b->Y, b->etas, b->out, OUT_LD, b->info, nullptr, nullptr);
+    BD_LAUNCH("band_chol_kernel");
+  }
   BD_TRY(hipEventRecord(b->ev1, s));
   std::vector<double> hout((size_t)neta * OUT_LD);
   std::vector<int> hinfo(neta);

@@ -1,0 +1,301 @@
+// Banded Cholesky of B + eta I by block cyclic reduction (odd-even elimination):
+// the likelihood terms of the band path with every CU busy even for one eta.
+//
+// band_chol_kernel (gpmi_band.hip) walks the nt = n_pad / 128 block steps in
+// sequence, one workgroup per eta: 128 steps of a 128 x 128 LDS Cholesky chain
+// (~9.6 ms at N = 16384 whatever the eta count), so a call with few eta (the
+// optimizer's one (sigma, eta) at a time, the per-rank block of a strong-scaled
+// curve) leaves most CUs idle. Here each level of the reduction eliminates every
+// odd block of the current block-tridiagonal matrix independently and forms the
+// Schur complement on the even blocks (numpy prototype tools/bcr_proto.py):
+//   odd i:   L_i = chol(D_i), Linv_i, Z_i = Linv_i Y_i,            bcr_chol_kernel
+//            logdet += 2 sum log diag L_i, G += Z_i^T Z_i
+//            W_l = Linv_i F_{i-1},  W_r = Linv_i F_i^T              bcr_w_kernel
+//   even j:  D_j' = D_j - W_r(j-1)^T W_r(j-1) - W_l(j+1)^T W_l(j+1)  bcr_upd_kernel
+//            Y_j' = Y_j - W_r(j-1)^T Z_{j-1} - W_l(j+1)^T Z_{j+1}
+//            F_{j/2}' = -W_r(j+1)^T W_l(j+1)
+// (F_i = B_{i+1,i}: upper triangular at level 0, full after). ceil(log2 nt)
+// levels of three launches, each with (blocks x eta) workgroups; it is a block
+// Cholesky factorization of the odd-even permuted matrix, so logdet and
+// Y^T (B + eta I)^-1 Y are exact to rounding (not bit-identical to the sequential
+// order). Every sum has a fixed order: per-block partials (logdet, Z^T Z,
+// failure) are reduced by bcr_final_kernel in original block order.
+//
+// Replaces, like band_chol_kernel, the per-eta logdet + 2 solves of the
+// reference's 'eigenvalue' operator (mixed_correlation.py:239-248,
+// _direct_likelihood.py:59,62,332).
+
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "gpmi_internal.h"
+#include "gpmi_device.h"
+#include "gpmi_lds_chol.h"
+#include "gpmi_band.h"
+#include "gpmi_tile.h"
+
+namespace gpmi {
+
+// Level-0 couplings F_i = triu(B_{i+1,i}) (the lower part of the stored tile holds
+// Householder vectors), shared by every eta. grid (nt - 1).
+__global__ __launch_bounds__(256) void bcr_f0_kernel(const double* __restrict__ Ab, int64_t lda,
+                                                     double* __restrict__ F0) {
+  const int i = blockIdx.x;
+  const double* src = Ab + (int64_t)(i + 1) * TS * lda + (int64_t)i * TS;
+  double* dst = F0 + (int64_t)i * TS * TS;
+  for (int e = threadIdx.x; e < TS * TS; e += 256) {
+    const int r = e >> 7, c = e & 127;
+    dst[e] = c >= r ? src[(int64_t)r * lda + c] : 0.0;
+  }
+}
+
+// Eliminate block p = first + 2 blockIdx.x of level `lvl` for eta blockIdx.y:
+// D_p (level 0: the stored diagonal tile + eta I; else Din) -> L, Linv (to Lout
+// when lout), Z = Linv Y_p (to Zall at the block's original index o = p << lvl),
+// the block's logdet, Z^T Z and failure partials (original index o).
+__global__ __launch_bounds__(256) void bcr_chol_kernel(
+    const double* __restrict__ Ab, int64_t lda, const double* __restrict__ etas, int lvl, int first,
+    const double* __restrict__ Din, int64_t sD, const double* __restrict__ Yin, int64_t sY,
+    double* __restrict__ Lout, int64_t sL, int lout, double* __restrict__ Zall, int64_t sZ,
+    double* __restrict__ logd, double* __restrict__ gpart, int* __restrict__ failv, int nt,
+    int64_t n) {
+  __shared__ double Ls[TS * DL];
+  __shared__ double Aux[TS * RLD];
+  __shared__ double sdiag[TS];
+  __shared__ double sred[2];
+  __shared__ int s_fail;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int fr = lane & 15, fk = lane >> 4;
+  const int e = blockIdx.y;
+  const int p = first + 2 * blockIdx.x;
+  const int o = p << lvl;   // original block index
+  if (lvl == 0) {
+    const double eta = etas[e];
+    const double* src = Ab + (int64_t)p * TS * lda + (int64_t)p * TS;
+    for (int q = t; q < TS * TS; q += 256) {
+      const int r = q >> 7, c = q & 127;
+      Ls[r * DL + c] = (c <= r) ? src[(int64_t)r * lda + c] + (r == c ? eta : 0.0) : 0.0;
+    }
+  } else {
+    const double* src = Din + e * sD + (int64_t)p * TS * TS;
+    for (int q = t; q < TS * TS; q += 256) {
+      const int r = q >> 7, c = q & 127;
+      Ls[r * DL + c] = (c <= r) ? src[q] : 0.0;
+    }
+  }
+  // Y_p -> Aux (k-major [128][16])
+  const double* ysrc = Yin + e * sY + (int64_t)p * TS * RLD;
+  for (int q = t; q < TS * RLD; q += 256) Aux[q] = ysrc[q];
+  if (t == 0) s_fail = 0;
+  __syncthreads();
+  // keep Y in registers: lds_chol_block uses Aux as scratch
+  d4 Rr[2];
+#pragma unroll
+  for (int slot = 0; slot < 2; ++slot) {
+    const int ti = slot == 0 ? w : NDB - 1 - w;
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) Rr[slot][rr] = Aux[(ti * DB + fk + 4 * rr) * RLD + fr];
+  }
+  __syncthreads();
+  lds_chol_block(Ls, Aux, sdiag, &s_fail);
+  if (w < 2) {
+    double v = ((int64_t)o * TS + t < n) ? log(sdiag[t]) : 0.0;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    if (lane == 0) sred[w] = v;
+  }
+  __syncthreads();
+  if (t == 0) {
+    logd[(int64_t)e * nt + o] = 2.0 * (sred[0] + sred[1]);
+    failv[(int64_t)e * nt + o] = s_fail ? o * TS + s_fail : 0;
+  }
+  lds_inv_block(Ls, Aux);
+  __syncthreads();
+  if (lout) {
+    double* dst = Lout + e * sL + (int64_t)(p >> 1) * TS * TS;
+    for (int q = t; q < TS * TS; q += 256) {
+      const int r = q >> 7, c = q & 127;
+      dst[q] = (c <= r) ? Ls[r * DL + c] : 0.0;
+    }
+  }
+  // Y back to Aux, then Z = Linv Y (the lower-triangular k-tiles only)
+#pragma unroll
+  for (int slot = 0; slot < 2; ++slot) {
+    const int ti = slot == 0 ? w : NDB - 1 - w;
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) Aux[(ti * DB + fk + 4 * rr) * RLD + fr] = Rr[slot][rr];
+  }
+  __syncthreads();
+  d4 Zv[2];
+#pragma unroll
+  for (int slot = 0; slot < 2; ++slot) {
+    const int ti = slot == 0 ? w : NDB - 1 - w;
+    d4 a0 = {0.0, 0.0, 0.0, 0.0}, a1 = {0.0, 0.0, 0.0, 0.0};
+    for (int kt = 0; kt <= ti; ++kt) {
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const double av = Ls[(ti * DB + fr) * DL + kt * DB + 4 * kk + fk];
+        const double bv = Aux[(kt * DB + 4 * kk + fk) * RLD + fr];
+        if (kk & 1) a1 = mfma64(av, bv, a1);
+        else a0 = mfma64(av, bv, a0);
+      }
+    }
+    Zv[slot] = a0 + a1;
+  }
+  __syncthreads();
+  double* zdst = Zall + e * sZ + (int64_t)o * TS * RLD;
+#pragma unroll
+  for (int slot = 0; slot < 2; ++slot) {
+    const int ti = slot == 0 ? w : NDB - 1 - w;
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int r = ti * DB + fk + 4 * rr;
+      Aux[r * RLD + fr] = Zv[slot][rr];
+      zdst[r * RLD + fr] = Zv[slot][rr];
+    }
+  }
+  __syncthreads();
+  // Z^T Z over this wave's two 16-row slices, the waves summed in order
+  d4 G = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int kt = 2 * w + h;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const double v = Aux[(kt * DB + 4 * kk + fk) * RLD + fr];
+      G = mfma64(v, v, G);
+    }
+  }
+  d4* sg = reinterpret_cast<d4*>(Ls);
+  __syncthreads();
+  sg[w * 64 + lane] = G;
+  __syncthreads();
+  if (w == 0) {
+    const d4 Gs = ((sg[lane] + sg[64 + lane]) + sg[128 + lane]) + sg[192 + lane];
+    double* gd = gpart + ((int64_t)e * nt + o) * RLD * RLD;
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) gd[(fk + 4 * rr) * RLD + fr] = Gs[rr];
+  }
+}
+
+// W of odd block p = 1 + 2 (blockIdx.x >> 1): which = blockIdx.x & 1:
+//   0: W_l = Linv_p F_{p-1};  1: W_r = Linv_p F_p^T (only when p + 1 < m).
+// F: level 0 the shared F0 (sF = 0), else Fin.
+__global__ __launch_bounds__(256, 2) void bcr_w_kernel(const double* __restrict__ Lin, int64_t sL,
+                                                       const double* __restrict__ Fin, int64_t sF,
+                                                       double* __restrict__ W, int64_t sW,
+                                                       int m) {
+  __shared__ double smem[4 * GSTAGE];
+  const int e = blockIdx.y;
+  const int h = blockIdx.x >> 1, which = blockIdx.x & 1;
+  const int p = 1 + 2 * h;
+  if (which == 1 && p + 1 >= m) return;
+  const double* L = Lin + e * sL + (int64_t)h * TS * TS;
+  d4 acc[4][4];
+  zero_tile(acc);
+  if (which == 0)
+    gemm_tile<KFAST, KSLOW, false>(L, TS, Fin + e * sF + (int64_t)(p - 1) * TS * TS, TS, TS, smem,
+                                   acc);
+  else
+    gemm_tile<KFAST, KFAST, false>(L, TS, Fin + e * sF + (int64_t)p * TS * TS, TS, TS, smem, acc);
+  store_tile(W + e * sW + ((int64_t)h * 2 + which) * TS * TS, TS, acc, 1.0);
+}
+
+// Even block j = 2 (blockIdx.x >> 1) of an m-block level: which = blockIdx.x & 1:
+//   0: D_j' (and Y_j'),  1: F_{j/2}' = -W_r(j+1)^T W_l(j+1)  (only when j + 2 < m).
+// W pairs of odd block i at W[(i >> 1) * 2 + {0: l, 1: r}]; Z of odd block i at its
+// original index (i << lvl) in Zall.
+__global__ __launch_bounds__(256, 2) void bcr_upd_kernel(
+    const double* __restrict__ Ab, int64_t lda, const double* __restrict__ etas, int lvl,
+    const double* __restrict__ Din, int64_t sD, const double* __restrict__ Yin, int64_t sY,
+    const double* __restrict__ W, int64_t sW, const double* __restrict__ Zall, int64_t sZ,
+    double* __restrict__ Dout, double* __restrict__ Fout, double* __restrict__ Yout, int64_t sO,
+    int64_t sOY, int m) {
+  __shared__ double smem[4 * GSTAGE];
+  const int e = blockIdx.y;
+  const int h = blockIdx.x >> 1, which = blockIdx.x & 1;
+  const int j = 2 * h;
+  const double* We = W + e * sW;
+  d4 acc[4][4];
+  if (which == 1) {
+    if (j + 2 >= m) return;
+    const double* Wl = We + ((int64_t)((j + 1) >> 1) * 2 + 0) * TS * TS;
+    const double* Wr = We + ((int64_t)((j + 1) >> 1) * 2 + 1) * TS * TS;
+    zero_tile(acc);
+    gemm_tile<KSLOW, KSLOW, true>(Wr, TS, Wl, TS, TS, smem, acc);
+    store_tile(Fout + e * sO + (int64_t)h * TS * TS, TS, acc, 1.0);
+    return;
+  }
+  if (lvl == 0) {
+    load_tile(Ab + (int64_t)j * TS * lda + (int64_t)j * TS, lda, acc);
+    const double eta = etas[e];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int wr = w >> 1, wc = w & 1, fr = lane & 15, fk = lane >> 4;
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (wr * 64 + a * 16 + fk + 4 * r == wc * 64 + c * 16 + fr) acc[a][c][r] += eta;
+  } else {
+    load_tile(Din + e * sD + (int64_t)j * TS * TS, TS, acc);
+  }
+  const bool left = j >= 1, right = j + 1 < m;
+  if (left) {
+    const double* Wr = We + ((int64_t)((j - 1) >> 1) * 2 + 1) * TS * TS;
+    gemm_tile<KSLOW, KSLOW, true>(Wr, TS, Wr, TS, TS, smem, acc);
+  }
+  if (right) {
+    const double* Wl = We + ((int64_t)((j + 1) >> 1) * 2 + 0) * TS * TS;
+    gemm_tile<KSLOW, KSLOW, true>(Wl, TS, Wl, TS, TS, smem, acc);
+  }
+  store_tile(Dout + e * sO + (int64_t)h * TS * TS, TS, acc, 1.0);
+  // Y_j' = Y_j - W_r(j-1)^T Z_{j-1} - W_l(j+1)^T Z_{j+1}: thread (row r, 8 columns)
+  const int t = threadIdx.x, r = t >> 1, c0 = (t & 1) * 8;
+  const double* ysrc = Yin + e * sY + (int64_t)j * TS * RLD;
+  double y[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) y[q] = ysrc[r * RLD + c0 + q];
+  for (int side = 0; side < 2; ++side) {
+    if (side == 0 && !left) continue;
+    if (side == 1 && !right) continue;
+    const int i = side == 0 ? j - 1 : j + 1;
+    const double* Wm = We + ((int64_t)(i >> 1) * 2 + (side == 0 ? 1 : 0)) * TS * TS;
+    const double* Z = Zall + e * sZ + (int64_t)(i << lvl) * TS * RLD;
+    for (int k = 0; k < TS; ++k) {
+      const double wv = Wm[k * TS + r];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) y[q] -= wv * Z[k * RLD + c0 + q];
+    }
+  }
+  double* ydst = Yout + e * sOY + (int64_t)h * TS * RLD;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) ydst[r * RLD + c0 + q] = y[q];
+}
+
+// out[e][0] = logdet (original block order), out[e][1 + a * 16 + c] = sum of the
+// blocks' Z^T Z, info[e] = the first failing block's pivot code. grid (neta).
+__global__ __launch_bounds__(256) void bcr_final_kernel(const double* __restrict__ logd,
+                                                        const double* __restrict__ gpart,
+                                                        const int* __restrict__ failv, int nt,
+                                                        double* __restrict__ out, int out_ld,
+                                                        int* __restrict__ info) {
+  const int e = blockIdx.x, t = threadIdx.x;
+  double g = 0.0;
+  for (int o = 0; o < nt; ++o) g += gpart[((int64_t)e * nt + o) * RLD * RLD + t];
+  out[(int64_t)e * out_ld + 1 + t] = g;
+  if (t == 0) {
+    double s = 0.0;
+    int f = 0;
+    for (int o = 0; o < nt; ++o) {
+      s += logd[(int64_t)e * nt + o];
+      if (!f) f = failv[(int64_t)e * nt + o];
+    }
+    out[(int64_t)e * out_ld] = s;
+    info[e] = f;
+  }
+}
+
+}  // namespace gpmi

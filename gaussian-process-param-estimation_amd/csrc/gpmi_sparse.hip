@@ -983,6 +983,85 @@ void launch_ms_rdots(const double* B, const double* R, double* Rn, const double*
   }
 }
 
+// Fused r update + dots of one multi-shift CG iteration for s <= 16 columns on fp64
+// MFMA: every block first reduces the p . q partials (fixed order, identical in
+// every block) to a[c] = rr[c] / (p . q)[c] (0 once the column stopped; block 0
+// stores a and flags p^T A p <= 0), then, four rows per wave instruction, lane
+// (row = r0 + lane / 16, column c = lane % 16) reads b, r and q of its element,
+// writes r_new = r - a q in place, and feeds b as the A operand and r_new as the
+// B operand of v_mfma_f64_16x16x4f64: the wave's 16 x 16 accumulator is B^T r_new
+// over its rows (columns >= s padded with zeros); r_new . r_new accumulates per
+// lane. Partials [block][s * s + s] as ms_dots_partial_kernel (waves summed in a
+// fixed order). One pass over b, r, q (ms_r_update + ms_dots_partial read r and
+// q, then b and r once per four-column group).
+__global__ __launch_bounds__(256) void ms_rmfma_kernel(const double* __restrict__ B,
+                                                       double* __restrict__ R,
+                                                       const double* __restrict__ Q, MsState st,
+                                                       const double* __restrict__ pqpart,
+                                                       int pq_nblk, int64_t n, int s,
+                                                       double* __restrict__ partial) {
+  __shared__ double sa[16];
+  __shared__ double red[4][16 * 16 + 16];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  for (int c = wv; c < s; c += 4) {
+    const double pq = wave_reduce_partials(pqpart, pq_nblk, s, c);
+    if (lane == 0) {
+      const int act = st.active[c];
+      const double a = act ? st.rr[c] / pq : 0.0;
+      sa[c] = a;
+      if (blockIdx.x == 0) {
+        st.a[c] = a;
+        if (act && !(pq > 0.0)) st.flags[0] = 1;
+      }
+    }
+  }
+  __syncthreads();
+  const int c = lane & 15, rq = lane >> 4;
+  const bool on = c < s;
+  const double a = on ? sa[c] : 0.0;
+  d4 acc = {0.0, 0.0, 0.0, 0.0};
+  double rr = 0.0;
+  // rows in groups of 16 per block iteration (4 waves x 4 rows), two groups per
+  // trip so that six loads per lane are in flight
+  // (the trip condition is wave-uniform: every lane issues every MFMA)
+  const int64_t stride = (int64_t)gridDim.x * 16;
+  for (int64_t base = (int64_t)blockIdx.x * 16 + wv * 4; base < n; base += 2 * stride) {
+    const int64_t i0 = base + rq, i1 = base + stride + rq;
+    const bool v0 = on && i0 < n, v1 = on && i1 < n;
+    const int64_t e0 = i0 * s + c, e1 = i1 * s + c;
+    const double b0 = v0 ? B[e0] : 0.0, r0 = v0 ? R[e0] : 0.0, q0 = v0 ? Q[e0] : 0.0;
+    const double b1 = v1 ? B[e1] : 0.0, r1 = v1 ? R[e1] : 0.0, q1 = v1 ? Q[e1] : 0.0;
+    const double n0 = r0 - a * q0, n1 = r1 - a * q1;
+    if (v0) R[e0] = n0;
+    if (v1) R[e1] = n1;
+    rr += n0 * n0;
+    rr += n1 * n1;
+    acc = mfma64(b0, n0, acc);
+    acc = mfma64(b1, n1, acc);
+  }
+  // C map: row (c') = rq + 4 k, column (c) = lane & 15
+#pragma unroll
+  for (int k = 0; k < 4; ++k) red[wv][(rq + 4 * k) * 16 + c] = acc[k];
+  // r . r: the four lanes of column c (rq = 0..3), in order
+  double rs = rr;
+  rs += __shfl_down(rs, 16);
+  rs += __shfl_down(rs, 32);
+  if (rq == 0) red[wv][256 + c] = rs;
+  __syncthreads();
+  const int ne = s * s + s;
+  for (int e = t; e < ne; e += 256) {
+    int idx;
+    if (e < s * s) {
+      const int cp = e / s, cc = e - cp * s;
+      idx = cp * 16 + cc;
+    } else {
+      idx = 256 + (e - s * s);
+    }
+    partial[(int64_t)blockIdx.x * ne + e] =
+        (red[0][idx] + red[1][idx]) + (red[2][idx] + red[3][idx]);
+  }
+}
+
 // r[i][c] -= a[c] q[i][c] with the base step a[c] = rr[c] / (p . q)[c] (0 once the
 // column stopped) formed per element; the first workgroup also stores a for the
 // scalar kernel (the separate alpha launch folded in).

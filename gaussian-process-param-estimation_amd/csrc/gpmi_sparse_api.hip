@@ -10,6 +10,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <vector>
 
 #include "gpmi_internal.h"
@@ -69,6 +70,8 @@ __global__ void lanczos_scalar_kernel(const double*, const double*, const double
                                       double*);
 void launch_ms_dots(const double* B, const double* R, int64_t n, int s, double* partial, int nblk,
                     hipStream_t st);
+__global__ void ms_rmfma_kernel(const double*, double*, const double*, MsState, const double*, int,
+                                int64_t, int, double*);
 __global__ void ms_r_update_kernel(double*, const double*, MsState, const double*, int64_t, int);
 void launch_ms_rdots(const double* B, const double* R, double* Rn, const double* Q,
                      const MsState& st, const double* pqpart, int pq_nblk, int64_t n, int s,
@@ -107,6 +110,7 @@ namespace {
 constexpr int NBLK = 256;   // fixed reduction grid (deterministic sums)
 constexpr int MAXS = 32;    // vector-block width per device pass
 constexpr int MS_NBLK = 128; // row blocks of the multi-shift dot partials
+constexpr int MS_RB = 512;   // row blocks of ms_rmfma_kernel (its loads in flight)
 
 struct Guard {
   int prev = -1;
@@ -144,6 +148,15 @@ struct gpmi_sp {
   double* lzd = nullptr;       // DCGS2 Lanczos scalars (lanczos_block_dcgs2)
   size_t lzd_doubles = 0;
   int lanczos_cgs2_reruns = 0; // DCGS2 blocks rerun with CGS2 (cancellation in rho)
+  // the multi-shift CG (gpmi_sp_msgram) has a stream and workspaces of its own, so
+  // that it may run from another host thread beside a Lanczos on `stream` (the
+  // sparse step's two independent halves overlap on the device)
+  hipStream_t ms_stream = nullptr;
+  double* ms_ws = nullptr;
+  size_t ms_ws_doubles = 0;
+  double* ms_partial = nullptr;
+  size_t ms_partial_doubles = 0;
+  std::mutex win_mu;           // the lazy X-window build (ensure_window)
   size_t msbuf_doubles = 0;
   int last_converged = 1;      // last gpmi_sp_cg / gpmi_sp_msgram met rtol in every column
   // Locality order (gpmi_sp_create_matern, d <= 3): device row r is original point
@@ -184,6 +197,7 @@ int ensure_partial(gpmi_sp* sp, size_t doubles) {
 }
 
 int ensure_window(gpmi_sp* sp) {
+  std::lock_guard<std::mutex> lock(sp->win_mu);
   if (sp->win_maxu >= 0) return 0;
   const int64_t nblk = (sp->n + WIN_ROWS_HOST - 1) / WIN_ROWS_HOST;
   SP_TRY(hipMalloc(&sp->win_cols, sizeof(int) * (size_t)nblk * WIN_MAXU_HOST));
@@ -261,7 +275,8 @@ int spmm_kind(gpmi_sp* sp, int s, int* kind) {
   return 0;
 }
 
-int spmm(gpmi_sp* sp, const double* X, double* Y, int s, double eta) {
+int spmm(gpmi_sp* sp, const double* X, double* Y, int s, double eta, hipStream_t st = nullptr) {
+  if (!st) st = sp->stream;
   int kind = 0;
   if (int rc = spmm_kind(sp, s, &kind)) return rc;
   if (kind == 2) {
@@ -269,7 +284,7 @@ int spmm(gpmi_sp* sp, const double* X, double* Y, int s, double eta) {
     const size_t lds = sizeof(double) * (size_t)s * (size_t)std::max(1, sp->win_maxu) +
                        10 * (size_t)sp->win_maxm + 4 + sizeof(int) * (WIN_ROWS_HOST + 1);
     hipLaunchKernelGGL(csr_spmm_winf_kernel<20>, dim3((unsigned)sp->win_nblk), dim3(256), lds,
-                       sp->stream, sp->indptr, sp->indices, sp->win_lidx, sp->data, sp->n,
+                       st, sp->indptr, sp->indices, sp->win_lidx, sp->data, sp->n,
                        sp->win_cols, sp->win_u, X, Y, eta);
     SP_LAUNCH("csr_spmm_winf_kernel");
     return 0;
@@ -280,7 +295,7 @@ int spmm(gpmi_sp* sp, const double* X, double* Y, int s, double eta) {
                        10 * (size_t)sp->win_maxm + 4 + sizeof(int) * (WIN_ROWS_HOST + 1);
     hipLaunchKernelGGL(csr_spmm_win_kernel,
                        dim3((unsigned)sp->win_nblk),
-                       dim3(256), lds, sp->stream, sp->indptr, sp->indices, sp->win_lidx, sp->data,
+                       dim3(256), lds, st, sp->indptr, sp->indices, sp->win_lidx, sp->data,
                        sp->n, sp->win_cols, sp->win_u, X, (int64_t)s, Y, (int64_t)s, s, eta);
     SP_LAUNCH("csr_spmm_win_kernel");
     return 0;
@@ -292,13 +307,13 @@ int spmm(gpmi_sp* sp, const double* X, double* Y, int s, double eta) {
     const int u = uenv ? std::atoi(uenv) : 3;
     auto kfn = u == 2 ? csr_spmm_pair_kernel<2> : u == 3 ? csr_spmm_pair_kernel<3>
                                                            : csr_spmm_pair_kernel<4>;
-    hipLaunchKernelGGL(kfn, dim3((unsigned)((sp->n + 3) / 4)), dim3(256), 0, sp->stream,
+    hipLaunchKernelGGL(kfn, dim3((unsigned)((sp->n + 3) / 4)), dim3(256), 0, st,
                        sp->indptr, sp->indices, sp->data, sp->n, X, Y, s, 64 / (s / 2), eta);
     SP_LAUNCH("csr_spmm_pair_kernel");
     return 0;
   }
   hipLaunchKernelGGL(csr_spmm_kernel, dim3((unsigned)((sp->n + 3) / 4)), dim3(256), 0,
-                     sp->stream, sp->indptr, sp->indices, sp->data, sp->n, X, (int64_t)s, Y,
+                     st, sp->indptr, sp->indices, sp->data, sp->n, X, (int64_t)s, Y,
                      (int64_t)s, s, 64 / s, eta);
   SP_LAUNCH("csr_spmm_kernel");
   return 0;
@@ -306,14 +321,18 @@ int spmm(gpmi_sp* sp, const double* X, double* Y, int s, double eta) {
 
 // out[j][c] = sum_i A_j[i][c] B[i][c], j < J  (device out)
 int col_dots(gpmi_sp* sp, const double* A, int64_t strideA, int J, const double* B, int s,
-             double* out) {
-  int rc = ensure_partial(sp, (size_t)NBLK * J * s);
-  if (rc) return rc;
-  hipLaunchKernelGGL(col_dot_partial_kernel, dim3(NBLK, J), dim3(256), 0, sp->stream, A, strideA,
-                     B, sp->n, s, sp->partial);
+             double* out, double* partial = nullptr, hipStream_t st = nullptr) {
+  if (!partial) {
+    int rc = ensure_partial(sp, (size_t)NBLK * J * s);
+    if (rc) return rc;
+    partial = sp->partial;
+  }
+  if (!st) st = sp->stream;
+  hipLaunchKernelGGL(col_dot_partial_kernel, dim3(NBLK, J), dim3(256), 0, st, A, strideA,
+                     B, sp->n, s, partial);
   SP_LAUNCH("col_dot_partial_kernel");
-  hipLaunchKernelGGL(col_dot_reduce_kernel, dim3((J * s + 3) / 4), dim3(256), 0, sp->stream,
-                     sp->partial, NBLK, J, s, out);
+  hipLaunchKernelGGL(col_dot_reduce_kernel, dim3((J * s + 3) / 4), dim3(256), 0, st,
+                     partial, NBLK, J, s, out);
   SP_LAUNCH("col_dot_reduce_kernel");
   return 0;
 }
@@ -713,6 +732,9 @@ int gpmi_sp_destroy(gpmi_sp* sp) {
   if (sp->msbuf) (void)hipFree(sp->msbuf);
   if (sp->lz) (void)hipFree(sp->lz);
   if (sp->lzd) (void)hipFree(sp->lzd);
+  if (sp->ms_ws) (void)hipFree(sp->ms_ws);
+  if (sp->ms_partial) (void)hipFree(sp->ms_partial);
+  if (sp->ms_stream) (void)hipStreamDestroy(sp->ms_stream);
   if (sp->win_cols) (void)hipFree(sp->win_cols);
   if (sp->win_u) (void)hipFree(sp->win_u);
   if (sp->win_lidx) (void)hipFree(sp->win_lidx);
@@ -981,25 +1003,41 @@ int gpmi_sp_msgram(gpmi_sp* sp, const double* etas, int neta, const double* rhs,
   // an odd block that would run the one-column gather SpMM gets a zero column (an
   // inactive CG column from the start: ||b|| = 0) so that the column-pair gather
   // runs (cfg 5, s = 11 -> 12); the Gram of the real columns is unchanged
+  // GPMI_MSGRAM_PAD=1: an odd block that would run the one-column gather SpMM gets a
+  // zero column (an inactive CG column from the start: ||b|| = 0) so that the
+  // column-pair gather runs; measured slower at cfg 5 (s = 11 gather 119 us, s = 12
+  // pair 161 us per launch), so off by default
   int s = nrhs;
   {
     int kind = 0;
     int rc0 = spmm_kind(sp, s, &kind);
     if (rc0) return rc0;
     const char* penv = std::getenv("GPMI_MSGRAM_PAD");
-    if (kind == 0 && (s & 1) && s + 1 <= MS_MAXS && S * (s + 1) <= 1024 &&
-        !(penv && std::atoi(penv) == 0))
+    if (kind == 0 && (s & 1) && s + 1 <= MS_MAXS && S * (s + 1) <= 1024 && penv &&
+        std::atoi(penv) == 1)
       ++s;
   }
+  if (!sp->ms_stream) SP_TRY(hipStreamCreateWithFlags(&sp->ms_stream, hipStreamNonBlocking));
   const int64_t ns = n * s;
   const double eta0 = *std::min_element(etas, etas + neta);
-  int rc = ensure_ws(sp, (size_t)5 * ns);
-  if (rc) return rc;
+  int rc = 0;
+  if (sp->ms_ws_doubles < (size_t)5 * ns) {
+    if (sp->ms_ws) SP_TRY(hipFree(sp->ms_ws));
+    sp->ms_ws = nullptr;
+    SP_TRY(hipMalloc(&sp->ms_ws, sizeof(double) * 5 * ns));
+    sp->ms_ws_doubles = (size_t)5 * ns;
+  }
   const int ne = s * s + s;
   // [MS_NBLK][ne] dot partials, then [NBLK][s] p . q partials
-  rc = ensure_partial(sp, (size_t)MS_NBLK * ne + (size_t)NBLK * s);
-  if (rc) return rc;
-  double* pqpart = sp->partial + (size_t)MS_NBLK * ne;
+  const size_t pneed = (size_t)MS_RB * ne + (size_t)NBLK * s;
+  if (sp->ms_partial_doubles < pneed) {
+    if (sp->ms_partial) SP_TRY(hipFree(sp->ms_partial));
+    sp->ms_partial = nullptr;
+    SP_TRY(hipMalloc(&sp->ms_partial, sizeof(double) * pneed));
+    sp->ms_partial_doubles = pneed;
+  }
+  double* partial = sp->ms_partial;
+  double* pqpart = partial + (size_t)MS_RB * ne;
   const size_t need = (size_t)6 * s + 2 * (size_t)S * s + 2 * (size_t)S * s * s + S + s + s + 1;
   if (sp->msbuf_doubles < need) {
     if (sp->msbuf) SP_TRY(hipFree(sp->msbuf));
@@ -1025,7 +1063,7 @@ int gpmi_sp_msgram(gpmi_sp* sp, const double* etas, int neta, const double* rhs,
   q += s;
   st.flags = reinterpret_cast<int*>(q);    // 1 int in 1 double
   sp->last_converged = 0;
-  double* Bd = sp->ws;
+  double* Bd = sp->ms_ws;
   double* Rd = Bd + ns;
   double* Pd = Rd + ns;
   double* Qd = Pd + ns;
@@ -1033,9 +1071,12 @@ int gpmi_sp_msgram(gpmi_sp* sp, const double* etas, int neta, const double* rhs,
   // fused p . q reduction + r update + dots for <= 2 column groups of 4 (the
   // fused kernel re-reads q once per group)
   const bool fused_r = (s + 3) / 4 <= 2;
+  // wider blocks: the MFMA form (GPMI_MS_MFMA=0 keeps the separate update and dots)
+  const char* menv = std::getenv("GPMI_MS_MFMA");
+  const bool mfma_r = !fused_r && s <= 16 && !(menv && std::atoi(menv) == 0);
   double* Rcur = Rd;     // the live residual
   double* Rnext = Rd2;
-  hipStream_t str = sp->stream;
+  hipStream_t str = sp->ms_stream;
   {
     std::vector<double> h((size_t)ns, 0.0);
     for (int64_t i = 0; i < n; ++i)
@@ -1051,9 +1092,9 @@ int gpmi_sp_msgram(gpmi_sp* sp, const double* etas, int neta, const double* rhs,
   // scalar kernels: S * s threads for the per-shift recurrences (<= 1024), and
   // 16 waves for their fixed-order partial reductions
   const unsigned sthreads = 1024;
-  launch_ms_dots(Bd, Rd, n, s, sp->partial, MS_NBLK, str);
+  launch_ms_dots(Bd, Rd, n, s, partial, MS_NBLK, str);
   SP_LAUNCH("ms_dots_partial_kernel");
-  hipLaunchKernelGGL(ms_init_kernel, dim3(1), dim3(sthreads), 0, str, st, sp->partial, MS_NBLK, S,
+  hipLaunchKernelGGL(ms_init_kernel, dim3(1), dim3(sthreads), 0, str, st, partial, MS_NBLK, S,
                      s);
   SP_LAUNCH("ms_init_kernel");
   int it = 0;
@@ -1076,7 +1117,7 @@ int gpmi_sp_msgram(gpmi_sp* sp, const double* etas, int neta, const double* rhs,
       if (rc) return rc;
       if (!any) break;
     }
-    rc = spmm(sp, Pd, Qd, s, eta0);
+    rc = spmm(sp, Pd, Qd, s, eta0, str);
     if (rc) return rc;
     double* Rout = Rcur;
     if (fused_r) {
@@ -1086,22 +1127,31 @@ int gpmi_sp_msgram(gpmi_sp* sp, const double* etas, int neta, const double* rhs,
                          (int64_t)0, Qd, n, s, pqpart);
       SP_LAUNCH("col_dot_partial_kernel");
       Rout = Rnext;
-      launch_ms_rdots(Bd, Rcur, Rout, Qd, st, pqpart, NBLK, n, s, sp->partial, MS_NBLK, str);
+      launch_ms_rdots(Bd, Rcur, Rout, Qd, st, pqpart, NBLK, n, s, partial, MS_NBLK, str);
       SP_LAUNCH("ms_rdots_partial_kernel");
       std::swap(Rcur, Rnext);
+    } else if (mfma_r) {
+      // p . q partials, then the reduction, the r update (in place) and B^T r, r . r
+      // on MFMA in one pass over b, r, q (ms_rmfma_kernel)
+      hipLaunchKernelGGL(col_dot_partial_kernel, dim3(NBLK, 1), dim3(256), 0, str, Pd,
+                         (int64_t)0, Qd, n, s, pqpart);
+      SP_LAUNCH("col_dot_partial_kernel");
+      hipLaunchKernelGGL(ms_rmfma_kernel, dim3(MS_RB), dim3(256), 0, str, Bd, Rcur, Qd, st,
+                         pqpart, NBLK, n, s, partial);
+      SP_LAUNCH("ms_rmfma_kernel");
     } else {
       // more than two 4-column groups would re-read q per group in the fused form:
       // the r update in place, then the dots
-      rc = col_dots(sp, Pd, 0, 1, Qd, s, pqd);
+      rc = col_dots(sp, Pd, 0, 1, Qd, s, pqd, pqpart, str);
       if (rc) return rc;
       hipLaunchKernelGGL(ms_r_update_kernel, dim3(grid_ns(n, s)), dim3(256), 0, str, Rcur, Qd, st,
                          pqd, n, s);
       SP_LAUNCH("ms_r_update_kernel");
-      launch_ms_dots(Bd, Rcur, n, s, sp->partial, MS_NBLK, str);
+      launch_ms_dots(Bd, Rcur, n, s, partial, MS_NBLK, str);
       SP_LAUNCH("ms_dots_partial_kernel");
     }
-    hipLaunchKernelGGL(ms_scalar_kernel, dim3(1), dim3(sthreads), 0, str, st, sp->partial, MS_NBLK,
-                       dshift, S, s, rtol * rtol, beta_out);
+    hipLaunchKernelGGL(ms_scalar_kernel, dim3(1), dim3(sthreads), 0, str, st, partial,
+                       mfma_r ? MS_RB : MS_NBLK, dshift, S, s, rtol * rtol, beta_out);
     SP_LAUNCH("ms_scalar_kernel");
     hipLaunchKernelGGL(ms_p_update_kernel, dim3(grid_ns(n, s)), dim3(256), 0, str, Pd, Rout,
                        st.beta, st.active, n, s);

@@ -63,6 +63,11 @@ __device__ __forceinline__ void gemm_tile(const double* __restrict__ P1, int64_t
   st_op<AL>(sA, ra);
   st_op<BL>(sB, rb);
   __syncthreads();
+  // Drain every global load issued before the loop (a caller's accumulator preload,
+  // load_tile) once, here: otherwise the waitcnt pass puts vmcnt waits on the first
+  // accumulator uses INSIDE the loop, which (vmcnt counts in order) also drain the
+  // next stage's prefetch every iteration (the dense tile_mma does the same).
+  __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0) expcnt(7) lgkmcnt(15)
   const int nsteps = kdim / BK;
   for (int s = 0; s < nsteps; ++s) {
     const int cur = s & 1;

@@ -18,7 +18,7 @@ import numpy
 
 from ._likelihood._direct_likelihood import _lp_from_terms
 
-__all__ = ['shard', 'eta_sweep', 'slq_sweep', 'der1_sweep']
+__all__ = ['shard', 'eta_sweep', 'slq_sweep', 'der1_sweep', 'slq_gram_sweep']
 
 
 def shard(num, world, rank):
@@ -154,3 +154,28 @@ def slq_sweep(K_mixed, etas, group=None):
     allq = allv[:, :nq].reshape(s, len(names), etas.size)
     n = K_mixed.n
     return {name: n * allq[:, f].mean(axis=0) for f, name in enumerate(names)}
+
+
+def slq_gram_sweep(K_mixed, etas, R, rtol=1e-6, group=None):
+    """One sparse likelihood sweep: slq_sweep (the Lanczos of this rank's probe
+    shard, all-gathered quadratures) and the multi-shift CG Gram blocks
+    R^T (K + eta I)^-1 R of this rank's contiguous eta block
+    (_linear_solver.py:57-68 at ``rtol``), run TOGETHER: the Gram on a second host
+    thread, whose device calls go to the multi-shift CG's own stream
+    (gpmi_sp_msgram), beside the Lanczos on the operator's stream. The two are
+    independent (the same K, different vectors), and each alone leaves the device
+    partly idle (latency-bound scalar and reduction launches).
+
+    Returns (curves, (lo, hi), G[hi - lo, s, s]): slq_sweep's curves on every
+    rank, and this rank's eta block with its Gram blocks."""
+    from concurrent.futures import ThreadPoolExecutor
+    etas = numpy.atleast_1d(numpy.asarray(etas, dtype=float))
+    dist, world, rank = _group(group)
+    lo, hi, _ = shard(etas.size, world, rank)
+    with ThreadPoolExecutor(1) as ex:
+        fut = ex.submit(K_mixed.sop.msgram, etas[lo:hi], R, rtol) if hi > lo else None
+        try:
+            curves = slq_sweep(K_mixed, etas, group=group)
+        finally:
+            G = fut.result() if fut is not None else None
+    return curves, (lo, hi), G

@@ -301,3 +301,57 @@ def test_der1_sweep_error_raises_on_every_rank_gloo():
         numpy.testing.assert_array_equal(outs[0], numpy.tanh(good - 0.7))
         assert outs[1] == 'LinAlgError'
         numpy.testing.assert_array_equal(outs[2], numpy.tanh(numpy.array([0.0, 1.0]) - 0.7))
+
+
+class _FakeSparseGram(_FakeSparse):
+    def msgram(self, etas, R, rtol=1e-6):
+        n = self.K.shape[0]
+        return numpy.array([R.T @ numpy.linalg.solve(self.K + e * numpy.eye(n), R)
+                            for e in etas])
+
+
+class _SparseMixedGram(_SparseMixed):
+    def __init__(self, K):
+        _SparseMixed.__init__(self, K)
+        self.sop = _FakeSparseGram(K, 12)
+
+
+def _slq_gram_worker(rank, world, port, etas, out_q):
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    from gaussian_proc.sweep import slq_gram_sweep
+    K, X, z = _problem()
+    R = numpy.column_stack([X, z])
+    out_q.put((rank, slq_gram_sweep(_SparseMixedGram(K + 0.5 * numpy.eye(K.shape[0])), etas, R)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_slq_gram_sweep_gloo():
+    """slq_gram_sweep: the probe-sharded SLQ curves (all-gathered, equal on every
+    rank) and each rank's eta block of multi-shift Gram blocks, computed together
+    (second host thread); the union of the blocks is the single-process result."""
+    from gaussian_proc.sweep import slq_gram_sweep
+    etas = numpy.array([0.5, 1.0, 2.0, 4.0, 8.0])
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_slq_gram_worker, args=(r, 2, port, etas, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(2)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    K, X, z = _problem()
+    R = numpy.column_stack([X, z])
+    op = _SparseMixedGram(K + 0.5 * numpy.eye(K.shape[0]))
+    curves, (lo, hi), G = slq_gram_sweep(op, etas, R, group=False)
+    assert (lo, hi) == (0, etas.size)
+    blocks = []
+    for _, (c, (l, h), g) in res:
+        for k in ('logdet', 'traceinv', 'traceinv2'):
+            numpy.testing.assert_allclose(c[k], curves[k], rtol=1e-12)
+        blocks.append(g)
+    numpy.testing.assert_allclose(numpy.concatenate(blocks), G, rtol=1e-12)
