@@ -248,7 +248,7 @@ def test_eigenvalue_operator_cfg2_golden(gp):
 
 
 @pytest.mark.parametrize('n', [5, 128, 129, 300, 1000])
-def test_band_der_terms_vs_numpy(gp, n):
+def test_band_der_terms_vs_numpy(gp, n, monkeypatch):
     """G_p = [X z]^T (K + eta I)^-p [X z], p = 1, 2, 3, from the banded factor
     (forward, backward, forward sweeps) vs numpy, ragged n, rtol 1e-9."""
     K, X, z = _inputs(n, n + 5)
@@ -263,10 +263,18 @@ def test_band_der_terms_vs_numpy(gp, n):
         for G, P in ((G1, Si), (G2, Si @ Si), (G3, Si @ Si @ Si)):
             Gr = R.T @ P @ R
             numpy.testing.assert_allclose(G[i], Gr, rtol=1e-9, atol=1e-11 * numpy.abs(Gr).max())
-    # same logdet / G1 as the likelihood call
+    # the likelihood call's logdet / G1: the same sequential factorization with
+    # GPMI_BAND_BCR=0 (bit for bit), by default (cyclic reduction) to rounding
     ld_l, G_l = op.loglik_terms(etas, X, z)
-    numpy.testing.assert_array_equal(ld, ld_l)
-    numpy.testing.assert_array_equal(G1, G_l)
+    assert rel(ld_l, ld) < 1e-12
+    numpy.testing.assert_allclose(G_l, G1, rtol=1e-10, atol=1e-12 * numpy.abs(G1).max())
+    monkeypatch.setenv('GPMI_BAND_BCR', '0')
+    op0 = _mc(K)
+    op0.der_terms(etas, X, z)
+    ld_0, G_0 = op0.loglik_terms(etas, X, z)
+    ld_d, G1_d = op0.der_terms(etas, X, z)[:2]
+    numpy.testing.assert_array_equal(ld_d, ld_0)
+    numpy.testing.assert_array_equal(G1_d, G_0)
 
 
 def test_band_der1_der2_vs_oracle(gp):
@@ -551,3 +559,34 @@ def test_band_delayed_update_matches_per_panel_update(gp, monkeypatch, n, delay)
     ld2, G2 = _mc(K).loglik_terms(etas, X, z)
     numpy.testing.assert_array_equal(ld1, ld2)
     numpy.testing.assert_array_equal(G1, G2)
+
+
+@pytest.mark.parametrize('n', [1, 5, 127, 128, 129, 300, 1000, 2304, 4224])
+def test_band_cyclic_reduction_matches_sequential(gp, monkeypatch, n):
+    """The banded Cholesky by block cyclic reduction (gpmi_bcr.hip, the default up
+    to 64 eta per call: odd blocks eliminated independently per level) against the
+    sequential band_chol_kernel (GPMI_BAND_BCR=0) on the same band: logdet and Gram blocks to
+    rounding, for 1, 3 and 8 eta per call (levels with odd and even block counts)."""
+    K, X, z = _inputs(n, 17 * n + 3, nu=1.5, scale=0.1)
+    etas = [1e-3, 0.1, 2.0, 5.0, 0.02, 30.0, 0.5, 1e-2]
+    monkeypatch.setenv('GPMI_BAND_BCR', '0')
+    op0 = _mc(K)
+    ld0, G0 = op0.loglik_terms(etas, X, z)
+    monkeypatch.setenv('GPMI_BAND_BCR', '1')
+    op1 = _mc(K)
+    for sel in ([1], [0, 3, 5], list(range(8))):
+        ld1, G1 = op1.loglik_terms([etas[i] for i in sel], X, z)
+        assert rel(ld1, ld0[sel]) < 1e-12, (n, sel)
+        numpy.testing.assert_allclose(G1, G0[sel], rtol=1e-9,
+                                      atol=1e-11 * numpy.abs(G0).max())
+
+
+def test_band_cyclic_reduction_not_spd(gp, monkeypatch):
+    """An eta that leaves B + eta I indefinite raises LinAlgError through the
+    cyclic reduction as through the sequential path."""
+    K, X, z = _inputs(700, 5, nu=1.5, scale=0.2)
+    lam = numpy.linalg.eigvalsh(K)
+    monkeypatch.setenv('GPMI_BAND_BCR', '1')
+    op = _mc(K)
+    with pytest.raises(numpy.linalg.LinAlgError):
+        op.loglik_terms([0.1, -lam[0] - 0.5 * (lam[1] - lam[0]) - 1e-3], X, z)
