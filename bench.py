@@ -711,6 +711,45 @@ def band_mode(args, D, X, z, world, rank, dist, torch, ld_ref=None):
     return out, op
 
 
+def optimizer_timing(D, X, z):
+    """The reference's end-to-end task at this N: Likelihood(X, K, method)
+    .maximize_log_likelihood(z) (likelihood.py:67-102) for 'direct' (trust-exact
+    on lp, jacobian, hessian; _direct_likelihood.py:346-405) and 'profiled'
+    (bracket search + Chandrupatla on der1; _profile_likelihood.py:244-415),
+    from the resident K: the operator's band reduction, its eigenvalues (traceinv)
+    and every evaluation included. Wall time and the optimum."""
+    import contextlib
+    import io
+    from gaussian_proc._likelihood import Likelihood
+    from gaussian_proc._likelihood._profile_likelihood import ProfileLikelihood
+    out = {}
+    for method in ('direct', 'profiled'):
+        torch_sync()
+        t0 = time.perf_counter()
+        lik = Likelihood(X, D, method)
+        with contextlib.redirect_stdout(io.StringIO()) as buf:
+            res = lik.maximize_log_likelihood(z)
+        dt = time.perf_counter() - t0
+        entry = {'wall_s': round(dt, 3),
+                 'result': {k: (float(v) if not isinstance(v, bool) else v)
+                            for k, v in res.items()}}
+        if method == 'profiled':
+            calls, points, _ = ProfileLikelihood.last_der1_calls
+            entry['der1_device_calls'] = calls
+            entry['der1_points'] = points
+        else:
+            txt = buf.getvalue()
+            entry['optimizer'] = [l for l in txt.splitlines() if l.startswith('Iter')][-1:]
+        lik.K_mixed.band().close()
+        out[method] = entry
+    return out
+
+
+def torch_sync():
+    import torch
+    torch.cuda.synchronize()
+
+
 def band_nu25_check(D, points, X, z):
     """BASELINE cfg3 as specified (nu = 2.5, smoother, so more nearly rank-deficient
     panels): one band reduction of that K, its panel statistics (CholeskyQR
@@ -970,6 +1009,8 @@ def main():
         cb['lp_rel_diff_vs_device'] = abs(cb['lp_cholesky'] - lp_dev) / abs(lp_dev)
         result['cpu_baseline'] = cb
         result['speedup_vs_cpu'] = round(result['value'] / cb['value'], 1)
+    if rank == 0 and world == 1 and not args.no_band:
+        result['band_mode']['optimizer'] = optimizer_timing(D, X, z)
     if rank == 0 and world == 1 and not args.no_band and args.nu == 1.5:
         result['band_mode']['nu25_check'] = band_nu25_check(D, points, X, z)
     if world == 1 and not args.no_sparse:

@@ -67,7 +67,18 @@ __global__ void bcr_chol_kernel(const double* Ab, int64_t lda, const double* eta
                                 int64_t sZ, double* logd, double* gpart, int* failv, int nt,
                                 int64_t n);
 __global__ void bcr_w_kernel(const double* Lin, int64_t sL, const double* Fin, int64_t sF,
-                             double* W, int64_t sW, int m);
+                             double* W, int64_t sW, int m, int lvl);
+__global__ void bcr_back_kernel(const double* L, int64_t sL, const double* W, int64_t sW,
+                                const double* Zall, int64_t sZ, double* Xall, double* g2part,
+                                int nt, int lvl, int first, int m);
+__global__ void bcr_rhs_odd_kernel(const double* L, int64_t sL, const double* Yin, int64_t sY,
+                                   double* Zp, int64_t sZ, double* g3part, int nt, int lvl,
+                                   int first);
+__global__ void bcr_rhs_even_kernel(const double* W, int64_t sW, const double* Zp, int64_t sZ,
+                                    const double* Yin, int64_t sY, double* Yout, int64_t sOY,
+                                    int lvl, int m);
+__global__ void bcr_der_final_kernel(const double* g2part, const double* g3part, int nt,
+                                     double* der);
 __global__ void bcr_upd_kernel(const double* Ab, int64_t lda, const double* etas, int lvl,
                                const double* Din, int64_t sD, const double* Yin, int64_t sY,
                                const double* W, int64_t sW, const double* Zall, int64_t sZ,

@@ -139,14 +139,21 @@ struct gpmi_band {
   double* Zc = nullptr;      // [2 delay][128][128]
   // block cyclic reduction of B + eta I (gpmi_bcr.hip; GPMI_BAND_BCR): per eta
   // capacity bcap, half = ceil(nt / 2) blocks per level
-  int bcr_mode = 0;          // 0 sequential band_chol_kernel, 1 cyclic reduction
+  int bcr_mode = 2;          // 0 sequential band_chol_kernel, 1 cyclic reduction, 2 auto:
+                             // cyclic reduction up to 64 eta per call (measured at N = 16384:
+                             // 1 eta 9.97 -> 1.30 ms, 8 eta 10.05 -> 1.85, 64 eta 9.9 -> 8.8;
+                             // the sequential kernel's time is flat up to the CU count)
   int bcap = 0;
   double* bcrD[2] = {nullptr, nullptr};   // [bcap][half][128][128]
   double* bcrF[2] = {nullptr, nullptr};
   double* bcrY[2] = {nullptr, nullptr};   // [bcap][half][128][16]
-  double* bcrL = nullptr;    // [bcap][half][128][128]
-  double* bcrW = nullptr;    // [bcap][half][2][128][128]
+  double* bcrL = nullptr;    // [bcap][nt][128][128]     every level's Linv, by original block
+  double* bcrW = nullptr;    // [bcap][nt][2][128][128]  every level's W_l, W_r, likewise
   double* bcrZ = nullptr;    // [bcap][nt][128][16]
+  double* bcrX = nullptr;    // [bcap][nt][128][16]      derivative terms: X, then Z'
+  double* bcrZp = nullptr;
+  double* bcrG2 = nullptr;   // [bcap][nt][16][16]
+  double* bcrG3 = nullptr;
   double* bcrG = nullptr;    // [bcap][nt][16][16]
   double* bcrLd = nullptr;   // [bcap][nt]
   int* bcrFail = nullptr;    // [bcap][nt]
@@ -185,7 +192,8 @@ int band_free(gpmi_band* b) {
                     b->fac, b->ysol, b->der, b->Qb, b->cqpart, b->cqG, b->cqL, b->cqLinv,
                     b->cqMinv, b->cqS, b->cqscr, b->UA, b->UB, b->zpart, b->Zc,
                     b->bcrD[0], b->bcrD[1], b->bcrF[0], b->bcrF[1], b->bcrY[0], b->bcrY[1],
-                    b->bcrL, b->bcrW, b->bcrZ, b->bcrG, b->bcrLd, b->bcrF0};
+                    b->bcrL, b->bcrW, b->bcrZ, b->bcrG, b->bcrLd, b->bcrF0, b->bcrX,
+                    b->bcrZp, b->bcrG2, b->bcrG3};
   if (b->bcrFail) (void)hipFree(b->bcrFail);
   if (b->cqflag) (void)hipFree(b->cqflag);
   for (double* p : bufs)
@@ -779,7 +787,7 @@ int gpmi_band_create(gpmi_op* op, gpmi_band** out) {
     b->cq_la_grid = std::max(0, std::atoi(lg));
   if (const char* pm = std::getenv("GPMI_BAND_PANEL")) b->panel_mode = std::strcmp(pm, "hh") == 0;
   if (const char* dl = std::getenv("GPMI_BAND_DELAY")) b->delay = std::max(1, std::min(8, std::atoi(dl)));
-  if (const char* bm = std::getenv("GPMI_BAND_BCR")) b->bcr_mode = std::atoi(bm) == 1 ? 1 : 0;
+  if (const char* bm = std::getenv("GPMI_BAND_BCR")) b->bcr_mode = std::max(0, std::min(2, std::atoi(bm)));
   // GPMI_CQ_FO=0: every CholeskyQR pass by an exact Cholesky (no first-order passes)
   if (const char* fo = std::getenv("GPMI_CQ_FO"))
     if (std::atoi(fo) == 0) b->cq_fo[1] = b->cq_fo[2] = 0.0;
@@ -955,7 +963,8 @@ int band_loglik_bcr(gpmi_band* b, int neta, hipStream_t s) {
   const int half = (nt + 1) / 2;
   if (b->bcap < neta) {
     double** bufs[] = {&b->bcrD[0], &b->bcrD[1], &b->bcrF[0], &b->bcrF[1], &b->bcrY[0],
-                       &b->bcrY[1], &b->bcrL, &b->bcrW, &b->bcrZ, &b->bcrG, &b->bcrLd};
+                       &b->bcrY[1], &b->bcrL, &b->bcrW, &b->bcrZ, &b->bcrG, &b->bcrLd,
+                       &b->bcrX, &b->bcrZp, &b->bcrG2, &b->bcrG3};
     for (double** q : bufs)
       if (*q) {
         BD_TRY(hipFree(*q));
@@ -970,17 +979,21 @@ int band_loglik_bcr(gpmi_band* b, int neta, hipStream_t s) {
       BD_TRY(hipMalloc(&b->bcrF[q], sizeof(double) * neta * half * blk));
       BD_TRY(hipMalloc(&b->bcrY[q], sizeof(double) * neta * half * yb));
     }
-    BD_TRY(hipMalloc(&b->bcrL, sizeof(double) * neta * half * blk));
-    BD_TRY(hipMalloc(&b->bcrW, sizeof(double) * neta * half * 2 * blk));
+    BD_TRY(hipMalloc(&b->bcrL, sizeof(double) * neta * nt * blk));
+    BD_TRY(hipMalloc(&b->bcrW, sizeof(double) * neta * nt * 2 * blk));
     BD_TRY(hipMalloc(&b->bcrZ, sizeof(double) * neta * nt * yb));
+    BD_TRY(hipMalloc(&b->bcrX, sizeof(double) * neta * nt * yb));
+    BD_TRY(hipMalloc(&b->bcrZp, sizeof(double) * neta * nt * yb));
     BD_TRY(hipMalloc(&b->bcrG, sizeof(double) * neta * nt * RLD * RLD));
+    BD_TRY(hipMalloc(&b->bcrG2, sizeof(double) * neta * nt * RLD * RLD));
+    BD_TRY(hipMalloc(&b->bcrG3, sizeof(double) * neta * nt * RLD * RLD));
     BD_TRY(hipMalloc(&b->bcrLd, sizeof(double) * neta * nt));
     BD_TRY(hipMalloc(&b->bcrFail, sizeof(int) * neta * nt));
     b->bcap = neta;
   }
   if (!b->bcrF0 && nt > 1) BD_TRY(hipMalloc(&b->bcrF0, sizeof(double) * (nt - 1) * TS * TS));
   const int64_t sH = (int64_t)half * TS * TS, sHY = (int64_t)half * TS * RLD;
-  const int64_t sZ = (int64_t)nt * TS * RLD, sW = 2 * sH;
+  const int64_t sZ = (int64_t)nt * TS * RLD, sL = (int64_t)nt * TS * TS, sW = 2 * sL;
   if (nt > 1) {
     hipLaunchKernelGGL(bcr_f0_kernel, dim3(nt - 1), dim3(256), 0, s, b->Ab, np, b->bcrF0);
     BD_LAUNCH("bcr_f0_kernel");
@@ -993,11 +1006,11 @@ int band_loglik_bcr(gpmi_band* b, int neta, hipStream_t s) {
   while (m > 1) {
     const int nodd = m / 2, neven = (m + 1) / 2;
     hipLaunchKernelGGL(bcr_chol_kernel, dim3(nodd, neta), dim3(256), 0, s, b->Ab, np, b->etas,
-                       lvl, 1, Din, sD, Yin, sY, b->bcrL, sH, 1, b->bcrZ, sZ, b->bcrLd, b->bcrG,
+                       lvl, 1, Din, sD, Yin, sY, b->bcrL, sL, 1, b->bcrZ, sZ, b->bcrLd, b->bcrG,
                        b->bcrFail, nt, b->n);
     BD_LAUNCH("bcr_chol_kernel");
-    hipLaunchKernelGGL(bcr_w_kernel, dim3(2 * nodd, neta), dim3(256), 0, s, b->bcrL, sH, Fin, sF,
-                       b->bcrW, sW, m);
+    hipLaunchKernelGGL(bcr_w_kernel, dim3(2 * nodd, neta), dim3(256), 0, s, b->bcrL, sL, Fin, sF,
+                       b->bcrW, sW, m, lvl);
     BD_LAUNCH("bcr_w_kernel");
     hipLaunchKernelGGL(bcr_upd_kernel, dim3(2 * neven, neta), dim3(256), 0, s, b->Ab, np, b->etas,
                        lvl, Din, sD, Yin, sY, b->bcrW, sW, b->bcrZ, sZ, b->bcrD[cur], b->bcrF[cur],
@@ -1014,12 +1027,56 @@ int band_loglik_bcr(gpmi_band* b, int neta, hipStream_t s) {
     ++lvl;
   }
   hipLaunchKernelGGL(bcr_chol_kernel, dim3(1, neta), dim3(256), 0, s, b->Ab, np, b->etas, lvl, 0,
-                     Din, sD, Yin, sY, b->bcrL, sH, 0, b->bcrZ, sZ, b->bcrLd, b->bcrG, b->bcrFail,
+                     Din, sD, Yin, sY, b->bcrL, sL, 1, b->bcrZ, sZ, b->bcrLd, b->bcrG, b->bcrFail,
                      nt, b->n);
   BD_LAUNCH("bcr_chol_kernel");
   hipLaunchKernelGGL(bcr_final_kernel, dim3(neta), dim3(256), 0, s, b->bcrLd, b->bcrG, b->bcrFail,
                      nt, b->out, OUT_LD, b->info);
   BD_LAUNCH("bcr_final_kernel");
+  return 0;
+}
+
+// Derivative terms by cyclic reduction (after band_loglik_bcr, whose levels stay
+// stored): X = (B + eta I)^-1 Y by back substitution from the last level down, then
+// the forward elimination of X; G2, G3 into b->der (gpmi_bcr.hip).
+int band_der_bcr(gpmi_band* b, int neta, hipStream_t s) {
+  int rc = band_loglik_bcr(b, neta, s);
+  if (rc) return rc;
+  const int nt = b->nt;
+  const int half = (nt + 1) / 2;
+  const int64_t sHY = (int64_t)half * TS * RLD;
+  const int64_t sZ = (int64_t)nt * TS * RLD, sL = (int64_t)nt * TS * TS, sW = 2 * sL;
+  std::vector<int> ms;   // blocks per level, the last level has one
+  for (int m = nt; m > 1; m = (m + 1) / 2) ms.push_back(m);
+  const int L = (int)ms.size();
+  hipLaunchKernelGGL(bcr_back_kernel, dim3(1, neta), dim3(256), 0, s, b->bcrL, sL, b->bcrW, sW,
+                     b->bcrZ, sZ, b->bcrX, b->bcrG2, nt, L, 0, 1);
+  BD_LAUNCH("bcr_back_kernel");
+  for (int l = L - 1; l >= 0; --l) {
+    hipLaunchKernelGGL(bcr_back_kernel, dim3(ms[l] / 2, neta), dim3(256), 0, s, b->bcrL, sL,
+                       b->bcrW, sW, b->bcrZ, sZ, b->bcrX, b->bcrG2, nt, l, 1, ms[l]);
+    BD_LAUNCH("bcr_back_kernel");
+  }
+  const double* Yin = b->bcrX;
+  int64_t sY = sZ;
+  int cur = 0;
+  for (int l = 0; l < L; ++l) {
+    hipLaunchKernelGGL(bcr_rhs_odd_kernel, dim3(ms[l] / 2, neta), dim3(256), 0, s, b->bcrL, sL,
+                       Yin, sY, b->bcrZp, sZ, b->bcrG3, nt, l, 1);
+    BD_LAUNCH("bcr_rhs_odd_kernel");
+    hipLaunchKernelGGL(bcr_rhs_even_kernel, dim3((ms[l] + 1) / 2, neta), dim3(256), 0, s, b->bcrW,
+                       sW, b->bcrZp, sZ, Yin, sY, b->bcrY[cur], sHY, l, ms[l]);
+    BD_LAUNCH("bcr_rhs_even_kernel");
+    Yin = b->bcrY[cur];
+    sY = sHY;
+    cur ^= 1;
+  }
+  hipLaunchKernelGGL(bcr_rhs_odd_kernel, dim3(1, neta), dim3(256), 0, s, b->bcrL, sL, Yin, sY,
+                     b->bcrZp, sZ, b->bcrG3, nt, L, 0);
+  BD_LAUNCH("bcr_rhs_odd_kernel");
+  hipLaunchKernelGGL(bcr_der_final_kernel, dim3(neta), dim3(256), 0, s, b->bcrG2, b->bcrG3, nt,
+                     b->der);
+  BD_LAUNCH("bcr_der_final_kernel");
   return 0;
 }
 
@@ -1033,7 +1090,7 @@ int gpmi_band_loglik(gpmi_band* b, const double* etas, int neta, double* logdet,
   hipStream_t s = b->stream;
   BD_TRY(hipMemcpyAsync(b->etas, etas, sizeof(double) * neta, hipMemcpyHostToDevice, s));
   BD_TRY(hipEventRecord(b->ev0, s));
-  if (b->bcr_mode == 1) {
+  if (b->bcr_mode == 1 || (b->bcr_mode == 2 && neta <= 64)) {
     rc = band_loglik_bcr(b, neta, s);
     if (rc) return rc;
   } else {
@@ -1088,11 +1145,17 @@ int gpmi_band_der_terms(gpmi_band* b, const double* etas, int neta, double* logd
   hipStream_t s = b->stream;
   BD_TRY(hipMemcpyAsync(b->etas, etas, sizeof(double) * neta, hipMemcpyHostToDevice, s));
   BD_TRY(hipEventRecord(b->ev0, s));
-  hipLaunchKernelGGL(band_chol_kernel, dim3(neta), dim3(256), 0, s, b->Ab, np, nt, b->n, b->Y,
-                     b->etas, b->out, OUT_LD, b->info, b->fac, b->ysol);
-  BD_LAUNCH("band_chol_kernel");
-  hipLaunchKernelGGL(band_der_kernel, dim3(neta), dim3(256), 0, s, b->fac, nt, b->ysol, b->der);
-  BD_LAUNCH("band_der_kernel");
+  if (b->bcr_mode == 1 || (b->bcr_mode == 2 && neta <= 64)) {
+    rc = band_der_bcr(b, neta, s);
+    if (rc) return rc;
+  } else {
+    hipLaunchKernelGGL(band_chol_kernel, dim3(neta), dim3(256), 0, s, b->Ab, np, nt, b->n, b->Y,
+                       b->etas, b->out, OUT_LD, b->info, b->fac, b->ysol);
+    BD_LAUNCH("band_chol_kernel");
+    hipLaunchKernelGGL(band_der_kernel, dim3(neta), dim3(256), 0, s, b->fac, nt, b->ysol,
+                       b->der);
+    BD_LAUNCH("band_der_kernel");
+  }
   BD_TRY(hipEventRecord(b->ev1, s));
   std::vector<double> hout((size_t)neta * OUT_LD), hder((size_t)neta * 2 * RLD * RLD);
   std::vector<int> hinfo(neta);

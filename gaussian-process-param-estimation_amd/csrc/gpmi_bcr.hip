@@ -113,7 +113,7 @@ __global__ __launch_bounds__(256) void bcr_chol_kernel(
   lds_inv_block(Ls, Aux);
   __syncthreads();
   if (lout) {
-    double* dst = Lout + e * sL + (int64_t)(p >> 1) * TS * TS;
+    double* dst = Lout + e * sL + (int64_t)o * TS * TS;
     for (int q = t; q < TS * TS; q += 256) {
       const int r = q >> 7, c = q & 127;
       dst[q] = (c <= r) ? Ls[r * DL + c] : 0.0;
@@ -181,17 +181,20 @@ __global__ __launch_bounds__(256) void bcr_chol_kernel(
 
 // W of odd block p = 1 + 2 (blockIdx.x >> 1): which = blockIdx.x & 1:
 //   0: W_l = Linv_p F_{p-1};  1: W_r = Linv_p F_p^T (only when p + 1 < m).
-// F: level 0 the shared F0 (sF = 0), else Fin.
+// F: level 0 the shared F0 (sF = 0), else Fin. Linv and W are stored by the block's
+// original index (p << lvl): every level's factor survives for the solves of
+// bcr_back_kernel / bcr_rhs_*.
 __global__ __launch_bounds__(256, 2) void bcr_w_kernel(const double* __restrict__ Lin, int64_t sL,
                                                        const double* __restrict__ Fin, int64_t sF,
                                                        double* __restrict__ W, int64_t sW,
-                                                       int m) {
+                                                       int m, int lvl) {
   __shared__ double smem[4 * GSTAGE];
   const int e = blockIdx.y;
   const int h = blockIdx.x >> 1, which = blockIdx.x & 1;
   const int p = 1 + 2 * h;
+  const int o = p << lvl;
   if (which == 1 && p + 1 >= m) return;
-  const double* L = Lin + e * sL + (int64_t)h * TS * TS;
+  const double* L = Lin + e * sL + (int64_t)o * TS * TS;
   d4 acc[4][4];
   zero_tile(acc);
   if (which == 0)
@@ -199,13 +202,13 @@ __global__ __launch_bounds__(256, 2) void bcr_w_kernel(const double* __restrict_
                                    acc);
   else
     gemm_tile<KFAST, KFAST, false>(L, TS, Fin + e * sF + (int64_t)p * TS * TS, TS, TS, smem, acc);
-  store_tile(W + e * sW + ((int64_t)h * 2 + which) * TS * TS, TS, acc, 1.0);
+  store_tile(W + e * sW + ((int64_t)o * 2 + which) * TS * TS, TS, acc, 1.0);
 }
 
 // Even block j = 2 (blockIdx.x >> 1) of an m-block level: which = blockIdx.x & 1:
 //   0: D_j' (and Y_j'),  1: F_{j/2}' = -W_r(j+1)^T W_l(j+1)  (only when j + 2 < m).
-// W pairs of odd block i at W[(i >> 1) * 2 + {0: l, 1: r}]; Z of odd block i at its
-// original index (i << lvl) in Zall.
+// W pairs of odd block i at W[(i << lvl) * 2 + {0: l, 1: r}]; Z of odd block i at
+// its original index (i << lvl) in Zall.
 __global__ __launch_bounds__(256, 2) void bcr_upd_kernel(
     const double* __restrict__ Ab, int64_t lda, const double* __restrict__ etas, int lvl,
     const double* __restrict__ Din, int64_t sD, const double* __restrict__ Yin, int64_t sY,
@@ -220,8 +223,8 @@ __global__ __launch_bounds__(256, 2) void bcr_upd_kernel(
   d4 acc[4][4];
   if (which == 1) {
     if (j + 2 >= m) return;
-    const double* Wl = We + ((int64_t)((j + 1) >> 1) * 2 + 0) * TS * TS;
-    const double* Wr = We + ((int64_t)((j + 1) >> 1) * 2 + 1) * TS * TS;
+    const double* Wl = We + ((int64_t)((j + 1) << lvl) * 2 + 0) * TS * TS;
+    const double* Wr = We + ((int64_t)((j + 1) << lvl) * 2 + 1) * TS * TS;
     zero_tile(acc);
     gemm_tile<KSLOW, KSLOW, true>(Wr, TS, Wl, TS, TS, smem, acc);
     store_tile(Fout + e * sO + (int64_t)h * TS * TS, TS, acc, 1.0);
@@ -244,11 +247,11 @@ __global__ __launch_bounds__(256, 2) void bcr_upd_kernel(
   }
   const bool left = j >= 1, right = j + 1 < m;
   if (left) {
-    const double* Wr = We + ((int64_t)((j - 1) >> 1) * 2 + 1) * TS * TS;
+    const double* Wr = We + ((int64_t)((j - 1) << lvl) * 2 + 1) * TS * TS;
     gemm_tile<KSLOW, KSLOW, true>(Wr, TS, Wr, TS, TS, smem, acc);
   }
   if (right) {
-    const double* Wl = We + ((int64_t)((j + 1) >> 1) * 2 + 0) * TS * TS;
+    const double* Wl = We + ((int64_t)((j + 1) << lvl) * 2 + 0) * TS * TS;
     gemm_tile<KSLOW, KSLOW, true>(Wl, TS, Wl, TS, TS, smem, acc);
   }
   store_tile(Dout + e * sO + (int64_t)h * TS * TS, TS, acc, 1.0);
@@ -262,7 +265,7 @@ __global__ __launch_bounds__(256, 2) void bcr_upd_kernel(
     if (side == 0 && !left) continue;
     if (side == 1 && !right) continue;
     const int i = side == 0 ? j - 1 : j + 1;
-    const double* Wm = We + ((int64_t)(i >> 1) * 2 + (side == 0 ? 1 : 0)) * TS * TS;
+    const double* Wm = We + ((int64_t)(i << lvl) * 2 + (side == 0 ? 1 : 0)) * TS * TS;
     const double* Z = Zall + e * sZ + (int64_t)(i << lvl) * TS * RLD;
     for (int k = 0; k < TS; ++k) {
       const double wv = Wm[k * TS + r];
@@ -296,6 +299,160 @@ __global__ __launch_bounds__(256) void bcr_final_kernel(const double* __restrict
     out[(int64_t)e * out_ld] = s;
     info[e] = f;
   }
+}
+
+// ---------------------------------------------------------------------------
+// Derivative terms (ProfileLikelihood der1 / der2, _profile_likelihood.py:91-192:
+// G2 = Y^T (B + eta I)^-2 Y, G3 = Y^T (B + eta I)^-3 Y) from the stored levels:
+// back substitution X = (B + eta I)^-1 Y from the last level down,
+//   x_i = Linv_i^T (Z_i - W_l(i) x_{i-1} - W_r(i) x_{i+1}),   G2 = sum X_o^T X_o,
+// then the forward elimination again with X as the right-hand side,
+//   Z'_i = Linv_i Y'_i,  Y'_j -= W_r(j-1)^T Z'_{j-1} + W_l(j+1)^T Z'_{j+1},
+//   G3 = sum Z'^T Z' (= X^T (B + eta I)^-1 X).
+// Blocks by original index; 128 x 16 products as plain FMAs (thread = row, 8 columns).
+// ---------------------------------------------------------------------------
+
+// Z^T Z of a 128 x 16 block in LDS (row stride RLD) into g[256], fixed order.
+__device__ __forceinline__ void block_gram(const double* Zs, double* g) {
+  const int t = threadIdx.x, a = t >> 4, c = t & 15;
+  double acc = 0.0;
+  for (int k = 0; k < TS; ++k) acc += Zs[k * RLD + a] * Zs[k * RLD + c];
+  g[t] = acc;
+}
+
+// Odd blocks p = first + 2 blockIdx.x of level lvl (first 0: the last level's single
+// block): x_p -> Xall[o], X_o^T X_o -> g2part[o].
+__global__ __launch_bounds__(256) void bcr_back_kernel(
+    const double* __restrict__ L, int64_t sL, const double* __restrict__ W, int64_t sW,
+    const double* __restrict__ Zall, int64_t sZ, double* __restrict__ Xall,
+    double* __restrict__ g2part, int nt, int lvl, int first, int m) {
+  __shared__ double xs[2][TS * RLD];
+  __shared__ double vs[TS * RLD];
+  const int t = threadIdx.x, r = t >> 1, c0 = (t & 1) * 8;
+  const int e = blockIdx.y;
+  const int p = first + 2 * blockIdx.x;
+  const int o = p << lvl;
+  const double* Z = Zall + e * sZ + (int64_t)o * TS * RLD;
+  const bool left = first == 1, right = first == 1 && p + 1 < m;
+  const double* Xe = Xall + e * sZ;
+  for (int q = t; q < TS * RLD; q += 256) {
+    xs[0][q] = left ? Xe[(int64_t)((p - 1) << lvl) * TS * RLD + q] : 0.0;
+    xs[1][q] = right ? Xe[(int64_t)((p + 1) << lvl) * TS * RLD + q] : 0.0;
+  }
+  __syncthreads();
+  double v[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) v[q] = Z[r * RLD + c0 + q];
+  for (int side = 0; side < 2; ++side) {
+    if ((side == 0 && !left) || (side == 1 && !right)) continue;
+    const double* Wm = W + e * sW + ((int64_t)o * 2 + side) * TS * TS + (int64_t)r * TS;
+    const double* x = xs[side];
+    for (int k = 0; k < TS; ++k) {
+      const double wv = Wm[k];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] -= wv * x[k * RLD + c0 + q];
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 8; ++q) vs[r * RLD + c0 + q] = v[q];
+  __syncthreads();
+  // x = Linv^T v (Linv lower: rows k >= r of column r)
+  const double* Lm = L + e * sL + (int64_t)o * TS * TS;
+  double x[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) x[q] = 0.0;
+  for (int k = r; k < TS; ++k) {
+    const double lv = Lm[k * TS + r];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) x[q] += lv * vs[k * RLD + c0 + q];
+  }
+  __syncthreads();
+  double* Xo = Xall + e * sZ + (int64_t)o * TS * RLD;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    Xo[r * RLD + c0 + q] = x[q];
+    vs[r * RLD + c0 + q] = x[q];
+  }
+  __syncthreads();
+  block_gram(vs, g2part + ((int64_t)e * nt + o) * RLD * RLD);
+}
+
+// Forward elimination of a right-hand side, odd blocks p = first + 2 blockIdx.x:
+// Z'_o = Linv_o Y'_p -> Zp[o], Z'^T Z' -> g3part[o]. Yin: the level's blocks (level 0:
+// Xall, blocks by original index = level index).
+__global__ __launch_bounds__(256) void bcr_rhs_odd_kernel(
+    const double* __restrict__ L, int64_t sL, const double* __restrict__ Yin, int64_t sY,
+    double* __restrict__ Zp, int64_t sZ, double* __restrict__ g3part, int nt, int lvl,
+    int first) {
+  __shared__ double ys[TS * RLD];
+  const int t = threadIdx.x, r = t >> 1, c0 = (t & 1) * 8;
+  const int e = blockIdx.y;
+  const int p = first + 2 * blockIdx.x;
+  const int o = p << lvl;
+  const double* Y = Yin + e * sY + (int64_t)p * TS * RLD;
+  for (int q = t; q < TS * RLD; q += 256) ys[q] = Y[q];
+  __syncthreads();
+  const double* Lm = L + e * sL + (int64_t)o * TS * TS + (int64_t)r * TS;
+  double z[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) z[q] = 0.0;
+  for (int k = 0; k <= r; ++k) {
+    const double lv = Lm[k];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) z[q] += lv * ys[k * RLD + c0 + q];
+  }
+  __syncthreads();
+  double* Zo = Zp + e * sZ + (int64_t)o * TS * RLD;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    Zo[r * RLD + c0 + q] = z[q];
+    ys[r * RLD + c0 + q] = z[q];
+  }
+  __syncthreads();
+  block_gram(ys, g3part + ((int64_t)e * nt + o) * RLD * RLD);
+}
+
+// Even blocks j = 2 blockIdx.x of an m-block level: Y'_j - W_r(j-1)^T Z'_{j-1}
+// - W_l(j+1)^T Z'_{j+1} -> Yout[j / 2].
+__global__ __launch_bounds__(256) void bcr_rhs_even_kernel(
+    const double* __restrict__ W, int64_t sW, const double* __restrict__ Zp, int64_t sZ,
+    const double* __restrict__ Yin, int64_t sY, double* __restrict__ Yout, int64_t sOY, int lvl,
+    int m) {
+  const int t = threadIdx.x, r = t >> 1, c0 = (t & 1) * 8;
+  const int e = blockIdx.y;
+  const int j = 2 * blockIdx.x;
+  const double* Y = Yin + e * sY + (int64_t)j * TS * RLD;
+  double y[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) y[q] = Y[r * RLD + c0 + q];
+  for (int side = 0; side < 2; ++side) {
+    if ((side == 0 && j < 1) || (side == 1 && j + 1 >= m)) continue;
+    const int i = side == 0 ? j - 1 : j + 1;
+    const double* Wm = W + e * sW + ((int64_t)(i << lvl) * 2 + (side == 0 ? 1 : 0)) * TS * TS;
+    const double* Z = Zp + e * sZ + (int64_t)(i << lvl) * TS * RLD;
+    for (int k = 0; k < TS; ++k) {
+      const double wv = Wm[k * TS + r];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) y[q] -= wv * Z[k * RLD + c0 + q];
+    }
+  }
+  double* yd = Yout + e * sOY + (int64_t)blockIdx.x * TS * RLD;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) yd[r * RLD + c0 + q] = y[q];
+}
+
+// der[e][0:256] = sum_o g2part, der[e][256:512] = sum_o g3part (original block order).
+__global__ __launch_bounds__(256) void bcr_der_final_kernel(const double* __restrict__ g2part,
+                                                            const double* __restrict__ g3part,
+                                                            int nt, double* __restrict__ der) {
+  const int e = blockIdx.x, t = threadIdx.x;
+  double a = 0.0, b = 0.0;
+  for (int o = 0; o < nt; ++o) {
+    a += g2part[((int64_t)e * nt + o) * RLD * RLD + t];
+    b += g3part[((int64_t)e * nt + o) * RLD * RLD + t];
+  }
+  der[(int64_t)e * 2 * RLD * RLD + t] = a;
+  der[(int64_t)e * 2 * RLD * RLD + RLD * RLD + t] = b;
 }
 
 }  // namespace gpmi

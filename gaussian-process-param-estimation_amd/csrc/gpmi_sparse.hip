@@ -453,9 +453,19 @@ __device__ __forceinline__ double wave_sum(double v) {
 // sum_b partial[b * stride + e], b < nblk, by one wave (nblk strided over lanes).
 __device__ __forceinline__ double wave_reduce_partials(const double* __restrict__ partial,
                                                        int nblk, int64_t stride, int e) {
+  // a lane's partials (b = lane, lane + 64, ...) summed in ascending b, their loads
+  // issued eight at a time (the same additions, in the same order, as one at a time)
   const int lane = threadIdx.x & 63;
   double v = 0.0;
-  for (int b = lane; b < nblk; b += 64) v += partial[(int64_t)b * stride + e];
+  int b = lane;
+  for (; b + 7 * 64 < nblk; b += 8 * 64) {
+    double x[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) x[q] = partial[(int64_t)(b + q * 64) * stride + e];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v += x[q];
+  }
+  for (; b < nblk; b += 64) v += partial[(int64_t)b * stride + e];
   return wave_sum(v);
 }
 
@@ -1176,6 +1186,21 @@ __global__ void ms_init_kernel(MsState st, const double* __restrict__ partial, i
     st.active[t] = br[s * s + t] > 0.0 ? 1 : 0;
   }
   if (t == 0) st.flags[0] = 0;
+}
+
+// dst[i][c] = src[perm[i]][c] for c < ns_src, 0 for the padding columns up to s
+// (perm null: identity): a host block in the caller's row order into the device's
+// locality order, on the device.
+__global__ __launch_bounds__(256) void rows_gather_kernel(const double* __restrict__ src,
+                                                          int ns_src, const int* __restrict__ perm,
+                                                          int64_t n, int s,
+                                                          double* __restrict__ dst) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= n * s) return;
+  const int64_t i = e / s;
+  const int c = (int)(e - i * s);
+  const int64_t r = perm ? (int64_t)perm[i] : i;
+  dst[e] = c < ns_src ? src[r * ns_src + c] : 0.0;
 }
 
 // Row r of the reordered CSR = row perm[r] of the original with every column j

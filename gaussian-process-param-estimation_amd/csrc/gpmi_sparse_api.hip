@@ -70,6 +70,7 @@ __global__ void lanczos_scalar_kernel(const double*, const double*, const double
                                       double*);
 void launch_ms_dots(const double* B, const double* R, int64_t n, int s, double* partial, int nblk,
                     hipStream_t st);
+__global__ void rows_gather_kernel(const double*, int, const int*, int64_t, int, double*);
 __global__ void ms_rmfma_kernel(const double*, double*, const double*, MsState, const double*, int,
                                 int64_t, int, double*);
 __global__ void ms_r_update_kernel(double*, const double*, MsState, const double*, int64_t, int);
@@ -1078,10 +1079,21 @@ int gpmi_sp_msgram(gpmi_sp* sp, const double* etas, int neta, const double* rhs,
   double* Rnext = Rd2;
   hipStream_t str = sp->ms_stream;
   {
-    std::vector<double> h((size_t)ns, 0.0);
-    for (int64_t i = 0; i < n; ++i)
-      for (int c = 0; c < nrhs; ++c) h[(size_t)i * s + c] = rhs[orig_row(sp, i) * ld + c];
-    SP_TRY(hipMemcpyAsync(Bd, h.data(), sizeof(double) * ns, hipMemcpyHostToDevice, str));
+    // the RHS block as the caller holds it (rows in the original order) into the
+    // staging Qd, then into the locality order (and zero padding columns) on the
+    // device: no host-side permutation pass over n x s doubles
+    if (ld == nrhs) {
+      SP_TRY(hipMemcpyAsync(Qd, rhs, sizeof(double) * n * nrhs, hipMemcpyHostToDevice, str));
+    } else {
+      std::vector<double> h((size_t)n * nrhs);
+      for (int64_t i = 0; i < n; ++i)
+        for (int c = 0; c < nrhs; ++c) h[(size_t)i * nrhs + c] = rhs[i * ld + c];
+      SP_TRY(hipMemcpyAsync(Qd, h.data(), sizeof(double) * h.size(), hipMemcpyHostToDevice, str));
+      SP_TRY(hipStreamSynchronize(str));
+    }
+    hipLaunchKernelGGL(rows_gather_kernel, dim3(grid_ns(n, s)), dim3(256), 0, str, Qd, nrhs,
+                       (const int*)sp->perm_d, n, s, Bd);
+    SP_LAUNCH("rows_gather_kernel");
     std::vector<double> hd(S);
     for (int j = 0; j < S; ++j) hd[j] = etas[j] - eta0;
     SP_TRY(hipMemcpyAsync(dshift, hd.data(), sizeof(double) * S, hipMemcpyHostToDevice, str));
