@@ -49,7 +49,7 @@ __global__ void w_kernel(const double* X, double* U, int64_t ldu, const double* 
 __global__ void syr2k_kernel(double* A, int64_t lda, const double* U, int64_t ldu, int tr0,
                              int mt, int sub);
 __global__ void syr2k_rest_kernel(double* A, int64_t lda, const double* U, int64_t ldu, int tr0,
-                                  int mt);
+                                  int mt, const uint32_t* order);
 __global__ void syr2k_g_kernel(double* A, int64_t lda, const double* PA, const double* PB,
                                int64_t ldu, int kdim, int tr0, int mt, int sub);
 __global__ void syr2k_g_rest_kernel(double* A, int64_t lda, const double* PA, const double* PB,

@@ -544,12 +544,28 @@ __global__ __launch_bounds__(256, 2) void syr2k_kernel(double* __restrict__ A, i
 }
 
 // Look-ahead: the lower tiles right of tile column 0, looped over by a capped
-// grid so that CUs stay free for the next panel's QR.
+// grid so that CUs stay free for the next panel's QR. With `order` (the
+// (mt - 1)-triangle in row groups, column-major inside a group, packed
+// (i << 16) | j): XCD x (workgroups b = x mod 8) takes the x-th contiguous eighth
+// of the list, its workgroups striding through it together, so the tiles in
+// flight on one XCD share a few W / V row slabs in its L2 (without: consecutive
+// tiles of the triangle land on different XCDs and every XCD streams all of U).
 __global__ __launch_bounds__(256, 2) void syr2k_rest_kernel(double* __restrict__ A, int64_t lda,
                                                             const double* __restrict__ U,
-                                                            int64_t ldu, int tr0, int mt) {
+                                                            int64_t ldu, int tr0, int mt,
+                                                            const uint32_t* __restrict__ order) {
   __shared__ double smem[4 * GSTAGE];
   const int ntiles = (mt - 1) * mt / 2;
+  if (order && gridDim.x >= 8) {   // (every XCD needs a workgroup for its eighth)
+    const int nwg = gridDim.x, x = blockIdx.x & 7, l = blockIdx.x >> 3;
+    const int nx = (nwg >> 3) + (x < (nwg & 7) ? 1 : 0);   // workgroups on XCD x
+    const int c0 = (int)((int64_t)ntiles * x / 8), c1 = (int)((int64_t)ntiles * (x + 1) / 8);
+    for (int q = c0 + l; q < c1; q += nx) {
+      const uint32_t o = order[q];
+      syr2k_tile(A, lda, U, ldu, tr0 + 1 + (int)(o >> 16), tr0 + 1 + (int)(o & 0xffffu), smem);
+    }
+    return;
+  }
   for (int q = blockIdx.x; q < ntiles; q += gridDim.x) {
     int i, j;
     tri_decode(q, mt - 1, &i, &j);

@@ -137,6 +137,11 @@ struct gpmi_band {
   double* UB = nullptr;      // [n_pad][256 delay] = [V_{p-1} .. V_0 | W_0 .. W_{p-1}]
   double* zpart = nullptr;   // [2 delay][nt][128][128] partials of UB^T V
   double* Zc = nullptr;      // [2 delay][128][128]
+  // grouped tile orders of the look-ahead SYR2K, one per (w x w)-triangle, w < nt
+  // (GPMI_BAND_RGROUP rows per group, 0: plain triangle order)
+  uint32_t* rorder = nullptr;
+  std::vector<int64_t> rorder_off;
+  int rgroup = 8;
   // block cyclic reduction of B + eta I (gpmi_bcr.hip; GPMI_BAND_BCR): per eta
   // capacity bcap, half = ceil(nt / 2) blocks per level
   int bcr_mode = 2;          // 0 sequential band_chol_kernel, 1 cyclic reduction, 2 auto:
@@ -196,6 +201,7 @@ int band_free(gpmi_band* b) {
                     b->bcrZp, b->bcrG2, b->bcrG3};
   if (b->bcrFail) (void)hipFree(b->bcrFail);
   if (b->cqflag) (void)hipFree(b->cqflag);
+  if (b->rorder) (void)hipFree(b->rorder);
   for (double* p : bufs)
     if (p) (void)hipFree(p);
   if (b->info) (void)hipFree(b->info);
@@ -489,7 +495,7 @@ int band_reduce_pass(gpmi_band* b, const double* K, const std::vector<double>* y
                       : b->la_grid > 0 ? b->la_grid : std::max(64, b->ncu - next_g);
       hipLaunchKernelGGL(syr2k_rest_kernel, dim3(std::min(rest, cap)), dim3(256),
                          mode == 0 ? b->la_lds : 0, s, b->Ab, np, b->U, (int64_t)BAND_ULD, j + 1,
-                         mt);
+                         mt, b->rorder ? b->rorder + b->rorder_off[mt - 1] : nullptr);
       BD_LAUNCH("syr2k_rest_kernel");
       BD_TRY(hipStreamWaitEvent(s, b->ev_pan, 0));
       ahead = true;
@@ -787,6 +793,7 @@ int gpmi_band_create(gpmi_op* op, gpmi_band** out) {
     b->cq_la_grid = std::max(0, std::atoi(lg));
   if (const char* pm = std::getenv("GPMI_BAND_PANEL")) b->panel_mode = std::strcmp(pm, "hh") == 0;
   if (const char* dl = std::getenv("GPMI_BAND_DELAY")) b->delay = std::max(1, std::min(8, std::atoi(dl)));
+  if (const char* rg = std::getenv("GPMI_BAND_RGROUP")) b->rgroup = std::max(0, std::atoi(rg));
   if (const char* bm = std::getenv("GPMI_BAND_BCR")) b->bcr_mode = std::max(0, std::min(2, std::atoi(bm)));
   // GPMI_CQ_FO=0: every CholeskyQR pass by an exact Cholesky (no first-order passes)
   if (const char* fo = std::getenv("GPMI_CQ_FO"))
@@ -839,6 +846,24 @@ int gpmi_band_create(gpmi_op* op, gpmi_band** out) {
   BALLOC(cqscr, (size_t)nt * TS * TS);
 #undef BALLOC
   if ((e = hipMalloc(&b->cqflag, sizeof(int) * 8 * nt)) != hipSuccess) return fail(e, "cqflag");
+  if (b->rgroup > 0 && nt > 2) {
+    // row groups of rgroup tile rows, column-major inside a group (packed (i << 16) | j)
+    std::vector<uint32_t> h;
+    b->rorder_off.assign(nt, 0);
+    for (int w = 1; w < nt; ++w) {
+      b->rorder_off[w] = (int64_t)h.size();
+      for (int r0 = 0; r0 < w; r0 += b->rgroup) {
+        const int r1 = std::min(w, r0 + b->rgroup);
+        for (int j = 0; j < r1; ++j)
+          for (int i = std::max(r0, j); i < r1; ++i) h.push_back(((uint32_t)i << 16) | (uint32_t)j);
+      }
+    }
+    if ((e = hipMalloc(&b->rorder, sizeof(uint32_t) * h.size())) != hipSuccess)
+      return fail(e, "rorder");
+    if ((e = hipMemcpy(b->rorder, h.data(), sizeof(uint32_t) * h.size(), hipMemcpyHostToDevice)) !=
+        hipSuccess)
+      return fail(e, "rorder copy");
+  }
   if ((e = hipMalloc(&b->ctr, 512)) != hipSuccess) return fail(e, "ctr");
   if ((e = hipMalloc(&b->err, 16)) != hipSuccess) return fail(e, "err");
   if ((e = hipMemsetAsync(b->err, 0, 16, b->stream)) != hipSuccess) return fail(e, "err memset");

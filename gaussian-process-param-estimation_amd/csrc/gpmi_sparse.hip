@@ -1220,4 +1220,80 @@ __global__ __launch_bounds__(256) void csr_permute_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// Dense operator of the Krylov methods (gpmi_sp_create_dense: 'slq' on a dense K):
+// Yp[y] = K[rows, k-split y] X for s <= 16 * CT columns, fp64 MFMA 16x16x4.
+// A workgroup owns 64 rows (wave w: rows 16 w .. 16 w + 15) and the k range of
+// split y = blockIdx.y (kcs chunks of 64 columns). Per chunk each lane reads 16
+// consecutive doubles of its row, K[r0 + (l & 15)][k0 + 16 (l >> 4) + m] (128 B
+// per lane, the whole 16 x 64 block per wave), and MFMA m takes k = k0 +
+// 16 (l >> 4) + m: a fixed permutation of the k order inside the chunk. The X
+// chunk (64 x 16 CT, zero past n and s) is staged in LDS for the four waves.
+// K must have ceil(n / 64) * 64 readable rows and columns (the dense operator's
+// n_pad); the partials are summed by dense_mm_reduce_kernel in split order.
+// HBM-bound: 8 n^2 bytes of K per launch.
+// ---------------------------------------------------------------------------
+template <int CT>
+__global__ __launch_bounds__(256) void dense_mm_kernel(const double* __restrict__ K, int64_t ldk,
+                                                       int64_t n, const double* __restrict__ X,
+                                                       int s, int kcs,
+                                                       double* __restrict__ Yp) {
+  constexpr int XC = 16 * CT;
+  __shared__ double sx[64][XC + 1];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int64_t r0 = (int64_t)blockIdx.x * 64 + w * 16;
+  const int kq = lane >> 4, fr = lane & 15;
+  const double* Kr = K + (r0 + fr) * ldk + 16 * kq;
+  const int64_t nch = (n + 63) / 64;
+  const int64_t c0 = (int64_t)blockIdx.y * kcs, c1 = c0 + kcs < nch ? c0 + kcs : nch;
+  d4 acc[CT];
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct) acc[ct] = d4{0.0, 0.0, 0.0, 0.0};
+  for (int64_t c = c0; c < c1; ++c) {
+    const int64_t k0 = c * 64;
+    d2 kv[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) kv[q] = *reinterpret_cast<const d2*>(Kr + k0 + 2 * q);
+#pragma unroll
+    for (int u = 0; u < XC / 4; ++u) {
+      const int e = u * 256 + t, kr = e / XC, col = e % XC;
+      const int64_t k = k0 + kr;
+      sx[kr][col] = (k < n && col < s) ? X[k * s + col] : 0.0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+      const double a = kv[m >> 1][m & 1];
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) acc[ct] = mfma64(a, sx[16 * kq + m][16 * ct + fr], acc[ct]);
+    }
+    __syncthreads();
+  }
+  double* out = Yp + (int64_t)blockIdx.y * n * s;
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t row = r0 + kq + 4 * r;
+      const int col = 16 * ct + fr;
+      if (row < n && col < s) out[row * s + col] = acc[ct][r];
+    }
+}
+template __global__ void dense_mm_kernel<1>(const double*, int64_t, int64_t, const double*, int,
+                                            int, double*);
+template __global__ void dense_mm_kernel<2>(const double*, int64_t, int64_t, const double*, int,
+                                            int, double*);
+
+// Y = sum_y Yp[y] (split order) + eta X, elementwise over [n][s].
+__global__ __launch_bounds__(256) void dense_mm_reduce_kernel(const double* __restrict__ Yp,
+                                                              int nsplit, int64_t ns,
+                                                              const double* __restrict__ X,
+                                                              double eta, double* __restrict__ Y) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= ns) return;
+  double v = 0.0;
+  for (int y = 0; y < nsplit; ++y) v += Yp[(int64_t)y * ns + e];
+  Y[e] = v + eta * X[e];
+}
+
 }  // namespace gpmi

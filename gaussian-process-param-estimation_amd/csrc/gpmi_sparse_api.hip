@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "gpmi_internal.h"
+#include "gpmi_band.h"
 #include "../../include/gpmi.h"
 
 using namespace gpmi;
@@ -82,6 +83,10 @@ __global__ void ms_scalar_kernel(MsState, const double*, int, const double*, int
 __global__ void ms_p_update_kernel(double*, const double*, const double*, const int*, int64_t,
                                    int);
 __global__ void ms_init_kernel(MsState, const double*, int, int, int);
+template <int CT>
+__global__ void dense_mm_kernel(const double*, int64_t, int64_t, const double*, int, int, double*);
+__global__ void dense_mm_reduce_kernel(const double*, int, int64_t, const double*, double, double*);
+int op_view(const gpmi_op* op, OpView* v);            // gpmi_api.hip
 int matern_params_host(double nu, MaternParams* P);   // gpmi_api.hip
 int set_error(int code, const char* msg);             // gpmi_api.hip
 }  // namespace gpmi
@@ -175,6 +180,12 @@ struct gpmi_sp {
   double win_mean = 0.0;               // mean window columns per block
   bool win_use = false;                // the windowed kernel is the faster one here
   int64_t win_nblk = 0;
+  // dense mode (gpmi_sp_create_dense): K borrowed from a gpmi_op, no CSR
+  const double* dK = nullptr;
+  int64_t dld = 0;
+  int dsplit = 1, dkcs = 1;            // k splits of dense_mm_kernel, 64-column chunks each
+  double* dYp = nullptr;               // split partials [dsplit][n][MAXS] of `stream`
+  double* dYp_ms = nullptr;            // ... of ms_stream (the CG beside the Lanczos)
 };
 
 namespace {
@@ -259,6 +270,10 @@ int ensure_window(gpmi_sp* sp) {
 // keeps the one-column gather for even s (the pair kernel also needs 16-byte
 // aligned blocks, else the one-column gather runs).
 int spmm_kind(gpmi_sp* sp, int s, int* kind) {
+  if (sp->dK) {
+    *kind = 4;
+    return 0;
+  }
   const char* wenv = std::getenv("GPMI_SPMM_WINDOW");
   const int wmode = wenv ? std::atoi(wenv) : 1;
   if (wmode != 0 && sp->win_maxu < 0)
@@ -278,6 +293,23 @@ int spmm_kind(gpmi_sp* sp, int s, int* kind) {
 
 int spmm(gpmi_sp* sp, const double* X, double* Y, int s, double eta, hipStream_t st = nullptr) {
   if (!st) st = sp->stream;
+  if (sp->dK) {
+    // dense: split partials of K X on fp64 MFMA, summed in split order (+ eta X)
+    double* Yp = st == sp->ms_stream ? sp->dYp_ms : sp->dYp;
+    const dim3 grid((unsigned)((sp->n + 63) / 64), (unsigned)sp->dsplit);
+    if (s <= 16)
+      hipLaunchKernelGGL(dense_mm_kernel<1>, grid, dim3(256), 0, st, sp->dK, sp->dld, sp->n, X, s,
+                         sp->dkcs, Yp);
+    else
+      hipLaunchKernelGGL(dense_mm_kernel<2>, grid, dim3(256), 0, st, sp->dK, sp->dld, sp->n, X, s,
+                         sp->dkcs, Yp);
+    SP_LAUNCH("dense_mm_kernel");
+    const int64_t ns = sp->n * s;
+    hipLaunchKernelGGL(dense_mm_reduce_kernel, dim3((unsigned)((ns + 255) / 256)), dim3(256), 0, st,
+                       Yp, sp->dsplit, ns, X, eta, Y);
+    SP_LAUNCH("dense_mm_reduce_kernel");
+    return 0;
+  }
   int kind = 0;
   if (int rc = spmm_kind(sp, s, &kind)) return rc;
   if (kind == 2) {
@@ -719,10 +751,48 @@ int gpmi_sp_create_matern(int device, const double* points, int64_t n, int d,
   return 0;
 }
 
+int gpmi_sp_create_dense(gpmi_op* op, gpmi_sp** out) {
+  if (!out) return set_error(-1004, "null output handle");
+  OpView v;
+  int rc = op_view(op, &v);
+  if (rc) return rc;
+  if (!v.has_K) return set_error(-1000, "operator has no matrix (load or assemble first)");
+  Guard g(v.device);
+  gpmi_sp* sp = new gpmi_sp();
+  sp->device = v.device;
+  sp->n = v.n;
+  sp->nnz = v.n * v.n;
+  sp->dK = v.K;
+  sp->dld = v.n_pad;
+  // k splits: about 1024 workgroups (row blocks x splits) keep the HBM stream busy
+  const int64_t nch = (v.n + 63) / 64;
+  int split = (int)std::min<int64_t>(16, std::max<int64_t>(1, (1024 + nch - 1) / nch));
+  split = (int)std::min<int64_t>(split, nch);
+  sp->dkcs = (int)((nch + split - 1) / split);
+  sp->dsplit = (int)((nch + sp->dkcs - 1) / sp->dkcs);
+  auto fail = [&](hipError_t e, const char* what) {
+    char b[300];
+    snprintf(b, sizeof(b), "%s failed: %s", what, hipGetErrorString(e));
+    gpmi_sp_destroy(sp);
+    return set_error(-(int)e, b);
+  };
+  hipError_t e;
+  if ((e = hipStreamCreateWithFlags(&sp->stream, hipStreamNonBlocking)) != hipSuccess)
+    return fail(e, "stream");
+  const size_t part = sizeof(double) * (size_t)sp->dsplit * (size_t)sp->n * MAXS;
+  if ((e = hipMalloc(&sp->small, sizeof(double) * 16384)) != hipSuccess) return fail(e, "small");
+  if ((e = hipMalloc(&sp->dYp, part)) != hipSuccess) return fail(e, "dense partials");
+  if ((e = hipMalloc(&sp->dYp_ms, part)) != hipSuccess) return fail(e, "dense partials");
+  *out = sp;
+  return 0;
+}
+
 int gpmi_sp_destroy(gpmi_sp* sp) {
   if (!sp) return 0;
   Guard g(sp->device);
   if (sp->stream) (void)hipStreamSynchronize(sp->stream);
+  if (sp->dYp) (void)hipFree(sp->dYp);
+  if (sp->dYp_ms) (void)hipFree(sp->dYp_ms);
   if (sp->perm_d) (void)hipFree(sp->perm_d);
   if (sp->indptr) (void)hipFree(sp->indptr);
   if (sp->indices) (void)hipFree(sp->indices);
@@ -753,6 +823,7 @@ int gpmi_sp_info(const gpmi_sp* sp, int64_t* n, int64_t* nnz) {
 
 int gpmi_sp_get_csr(gpmi_sp* sp, int64_t* indptr, int* indices, double* data) {
   if (!sp) return set_error(-1006, "null handle");
+  if (sp->dK) return set_error(-1105, "a dense operator has no CSR");
   Guard g(sp->device);
   if (sp->perm.empty()) {
     SP_TRY(hipMemcpy(indptr, sp->indptr, sizeof(int64_t) * (sp->n + 1), hipMemcpyDeviceToHost));
@@ -816,6 +887,7 @@ __global__ void __launch_bounds__(256) csr_scatter_dense_kernel(
 int sp_scatter_dense(const gpmi_sp* sp, int device, double* K, int64_t ldk, hipStream_t st) {
   if (sp->device != device)
     return set_error(-1011, "sparse and dense operators live on different devices");
+  if (sp->dK) return set_error(-1105, "a dense operator has no CSR");
   SP_TRY(hipStreamSynchronize(sp->stream));
   const unsigned grid = (unsigned)((sp->n + 3) / 4);
   hipLaunchKernelGGL(csr_scatter_dense_kernel, dim3(grid), dim3(256), 0, st, sp->indptr,
@@ -1189,6 +1261,12 @@ int gpmi_sp_msgram(gpmi_sp* sp, const double* etas, int neta, const double* rhs,
 int gpmi_sp_spmm_info(gpmi_sp* sp, int* windowed, double* mean_window, int* max_window) {
   if (!sp) return set_error(-1006, "null handle");
   Guard g(sp->device);
+  if (sp->dK) {   // dense: no window
+    if (windowed) *windowed = 0;
+    if (mean_window) *mean_window = 0.0;
+    if (max_window) *max_window = 0;
+    return 0;
+  }
   if (sp->win_maxu < 0)
     if (int rc = ensure_window(sp)) return rc;
   const char* wenv = std::getenv("GPMI_SPMM_WINDOW");

@@ -63,6 +63,7 @@ SIGNATURES = {
                                              ctypes.POINTER(c_op_p)]),
     'gpmi_sp_create_csr': (ctypes.c_int, [ctypes.c_int, c_i64, ctypes.POINTER(c_i64),
                                           c_int_p, c_double_p, ctypes.POINTER(c_op_p)]),
+    'gpmi_sp_create_dense': (ctypes.c_int, [c_op_p, ctypes.POINTER(c_op_p)]),
     'gpmi_sp_destroy': (ctypes.c_int, [c_op_p]),
     'gpmi_sp_info': (ctypes.c_int, [c_op_p, ctypes.POINTER(c_i64), ctypes.POINTER(c_i64)]),
     'gpmi_sp_get_csr': (ctypes.c_int, [c_op_p, ctypes.POINTER(c_i64), c_int_p, c_double_p]),
@@ -518,6 +519,17 @@ class SparseOperator(object):
               'gpmi_sp_create_csr')
         return cls(h, device)
 
+    @classmethod
+    def from_dense(cls, op):
+        """The Krylov primitives (spmm, lanczos, cg, msgram) on a dense
+        ``Operator``'s device K (fp64 MFMA products, dense_mm_kernel): imate's
+        'slq' on a dense K. Borrows op's matrix; keeps op alive."""
+        h = c_op_p()
+        check(op.lib.gpmi_sp_create_dense(op.h, ctypes.byref(h)), 'gpmi_sp_create_dense')
+        out = cls(h, op.device)
+        out.dense_op = op
+        return out
+
     def close(self):
         if getattr(self, 'h', None) is not None and self.h.value:
             self.lib.gpmi_sp_destroy(self.h)
@@ -565,7 +577,7 @@ class SparseOperator(object):
         check(self.lib.gpmi_sp_spmm_kernel(self.h, int(s), ctypes.byref(k)),
               'gpmi_sp_spmm_kernel')
         return ('csr_spmm_kernel', 'csr_spmm_win_kernel', 'csr_spmm_winf_kernel',
-                'csr_spmm_pair_kernel')[k.value]
+                'csr_spmm_pair_kernel', 'dense_mm_kernel')[k.value]
 
     def lanczos(self, nprobe, steps, seed=0, probe_offset=0):
         """-> alpha[nprobe, steps], beta[nprobe, steps] (beta = 0 ends a tridiagonal)."""

@@ -19,6 +19,13 @@ once per operator.
   inverse.
 * 'hutchinson' traceinv (:193-203): Rademacher probes solved with the device
   Cholesky (stochastic; parity unpinned against imate, which is absent).
+* 'slq' on a dense K: the same device Lanczos quadrature as on a sparse K,
+  its products K X on fp64 MFMA over the resident dense K
+  (_hip.SparseOperator.from_dense, dense_mm_kernel). The reference's branch
+  passes the misspelt ``self.K_afm`` to imate (:141,207,266) and raises
+  AttributeError; this is the estimator that branch names (parity unpinned:
+  no reference value exists; tests check it against the exact logdet within
+  the probes' standard error).
 * sparse K: 'slq' (logdet / traceinv by device Lanczos quadrature) and
   'hutchinson' traceinv (CG solves); solve by device CG as the reference's
   linear_solver (_linear_solver.py:57-68). The exact methods ('cholesky', and
@@ -69,6 +76,7 @@ class MixedCorrelation(object):
         if isinstance(K, DeviceSparseCorrelation) or scipy.sparse.issparse(K):
             self._init_sparse(K, device, max_batch)
             return
+        self.sop = None
         if isinstance(K, DeviceCorrelation):
             if max_batch is not None and max_batch > K.op.max_batch:
                 raise ValueError('DeviceCorrelation was created with max_batch=%d'
@@ -90,8 +98,20 @@ class MixedCorrelation(object):
         self._band = None
         self._band_rhs = None
         self._eig = None
+        if self.imate_method == 'slq':
+            # Krylov primitives over the resident dense K (dense_mm_kernel)
+            self.sop = _hip.SparseOperator.from_dense(self.op)
+            self._slq_options()
         if self.interpolate:
             self._build_interpolant()
+
+    def _slq_options(self):
+        opts = dict(self.imate_options or {})
+        self.num_samples = int(opts.get('num_samples', opts.get('max_num_samples', 20)))
+        self.lanczos_degree = int(opts.get('lanczos_degree', 30))
+        self.seed = int(opts.get('seed', 0))
+        self.cg_rtol = float(opts.get('cg_rtol', 1e-6))
+        self._nodes = None
 
     def _build_interpolant(self):
         """imate.InterpolateTraceInv of the reference (mixed_correlation.py:52-66),
@@ -213,12 +233,7 @@ class MixedCorrelation(object):
         self._band = None
         self._band_rhs = None
         self._eig = None
-        opts = dict(self.imate_options or {})
-        self.num_samples = int(opts.get('num_samples', opts.get('max_num_samples', 20)))
-        self.lanczos_degree = int(opts.get('lanczos_degree', 30))
-        self.seed = int(opts.get('seed', 0))
-        self.cg_rtol = float(opts.get('cg_rtol', 1e-6))
-        self._nodes = None
+        self._slq_options()
         if self.interpolate:
             self._build_interpolant()
 
@@ -230,7 +245,8 @@ class MixedCorrelation(object):
         return self._nodes
 
     def _slq(self, eta, what):
-        q = _slq.quadrature(self.slq_nodes(), [eta], _slq.FUNCS[what])
+        fn = _slq.FUNCS[what] if isinstance(what, str) else what
+        q = _slq.quadrature(self.slq_nodes(), [eta], fn)
         return float(self.n * q[:, 0].mean())
 
     def _sparse_traces(self):
@@ -280,17 +296,24 @@ class MixedCorrelation(object):
             # sum over the eigenvalues (imate 'eigenvalue', :127-133)
             return float(numpy.sum((self.eigenvalues() + eta) ** float(exponent)))
         if self.imate_method == 'slq':
-            raise NotImplementedError('trace with exponent %r on the slq operator' % exponent)
+            # tr (K + eta I)^p ~ n E[e1^T f(T) e1], f(x) = x^p (imate.trace, 'slq')
+            p = float(exponent)
+            return self._slq(eta, lambda x: x ** p)
         raise ValueError('Existing methods are "exact", "eigenvalue", and "slq".')
 
     def traceinv(self, eta, exponent=1):                           # :155-215
         if self.interpolate:
             # :167-170: the interpolant of tr((K + eta I)^-1), whatever the exponent
             return self.interpolate_traceinv.interpolate(eta)
-        if self.sparse and self.imate_method in ('slq', 'hutchinson'):
-            if self.imate_method == 'slq' and exponent in (1, 2):
+        if self.imate_method == 'slq' and self.sop is not None:
+            if exponent == 0:
+                return float(self.n)
+            if exponent in (1, 2):
                 return self._slq(eta, 'traceinv' if exponent == 1 else 'traceinv2')
-            if self.imate_method == 'hutchinson' and exponent in (1, 2):
+            p = float(exponent)
+            return self._slq(eta, lambda x: x ** -p)
+        if self.sparse and self.imate_method == 'hutchinson':
+            if exponent in (1, 2):
                 V = _slq.rademacher(self.n, self.num_samples, self.seed)
                 W = self.sop.cg(eta, V, rtol=self.cg_rtol)
                 if exponent == 1:
@@ -326,11 +349,9 @@ class MixedCorrelation(object):
         return float(numpy.trace(numpy.linalg.matrix_power(Ainv, exponent)))
 
     def logdet(self, eta, exponent=1):                             # :221-274
-        if self.sparse and self.imate_method == 'slq':
+        if self.imate_method == 'slq' and self.sop is not None:
             return exponent * self._slq(eta, 'logdet')
         if self.imate_method not in ('eigenvalue', 'cholesky', 'hutchinson'):
-            if self.imate_method == 'slq':
-                raise NotImplementedError('slq logdet is not implemented yet')
             raise ValueError('Existing methods are "eigenvalue", "cholesky",'
                              ' and "slq".')
         if self.imate_method == 'eigenvalue':
@@ -387,6 +408,14 @@ class MixedCorrelation(object):
             return self._band_terms(etas, X, z)
         self._dense()
         self.set_rhs(X, z)
+        if self.imate_method == 'slq':
+            # dense K: SLQ logdet (imate 'slq') and the exact Gram blocks of the
+            # dense solve the reference pairs it with (_linear_solver.py:71)
+            lds = numpy.array([self.logdet(e) for e in etas])
+            return lds, self._exact_terms(etas)[1]
+        return self._exact_terms(etas)
+
+    def _exact_terms(self, etas):
         lds, gs = [], []
         mb = self.op.max_batch
         for i in range(0, etas.size, mb):

@@ -157,6 +157,15 @@ int gpmi_sp_create_matern(int device, const double* points, int64_t n, int d,
 /* From a host CSR (indptr[n+1] int64, indices int32, data fp64). */
 int gpmi_sp_create_csr(int device, int64_t n, const int64_t* indptr, const int* indices,
                        const double* data, gpmi_sp** out);
+/* The Krylov primitives below (spmm, lanczos, cg, msgram) on a DENSE operator's
+ * K: a handle that borrows op's device matrix (op must outlive it, and its K must
+ * not change while the handle is used). Products run on fp64 MFMA
+ * (dense_mm_kernel); nnz reports n * n; gpmi_sp_get_csr is refused (-1105).
+ * Replaces imate 'slq' on a dense K (mixed_correlation.py:138-143,204-209,263-268:
+ * the reference's branch passes the misspelt self.K_afm and raises
+ * AttributeError, so there is no reference value; the estimator is the same as
+ * on a sparse K). */
+int gpmi_sp_create_dense(gpmi_op* op, gpmi_sp** out);
 int gpmi_sp_destroy(gpmi_sp* sp);
 int gpmi_sp_info(const gpmi_sp* sp, int64_t* n, int64_t* nnz);
 int gpmi_sp_get_csr(gpmi_sp* sp, int64_t* indptr, int* indices, double* data);
@@ -195,7 +204,8 @@ int gpmi_sp_spmm_info(gpmi_sp* sp, int* windowed, double* mean_window, int* max_
  * 0 gather from X (csr_spmm_kernel), 1 X-window in 8-column chunks
  * (csr_spmm_win_kernel), 2 X-window in one full-width pass (csr_spmm_winf_kernel,
  * s = 20), 3 gather from X by column pairs (csr_spmm_pair_kernel, even s; a block
- * that is not 16-byte aligned runs csr_spmm_kernel). Diagnostic; no reference
+ * that is not 16-byte aligned runs csr_spmm_kernel), 4 dense (dense_mm_kernel,
+ * gpmi_sp_create_dense). Diagnostic; no reference
  * counterpart. */
 int gpmi_sp_spmm_kernel(gpmi_sp* sp, int s, int* kind);
 /* Whether the last gpmi_sp_cg / gpmi_sp_msgram met rtol in every column before

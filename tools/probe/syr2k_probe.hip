@@ -1,0 +1,216 @@
+// Dev probe (not shipped): the band reduction's trailing SYR2K tile loop in
+// isolation, timed per grid size and k depth, to find where the look-ahead
+// SYR2K loses MFMA time. build: hipcc --offload-arch=gfx950 -O3 -std=c++17
+//   -I../../gaussian-process-param-estimation_amd/csrc syr2k_probe.hip -o syr2k_probe
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <vector>
+#include "gpmi_tile.h"
+
+using namespace gpmi;
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e_), __LINE__); exit(1);} } while (0)
+
+// the shipped tile (gpmi_band.hip syr2k_tile) with the k depth as a parameter
+__device__ __forceinline__ void tile_k(double* A, int64_t lda, const double* U, int64_t ldu, int I,
+                                       int J, int kdim, double* smem) {
+  double* C = A + (int64_t)I * TS * lda + (int64_t)J * TS;
+  d4 acc[4][4];
+  load_tile(C, lda, acc);
+  gemm_tile<KFAST, KFAST, true>(U + (int64_t)I * TS * ldu, ldu, U + (int64_t)J * TS * ldu + kdim / 2,
+                                ldu, kdim, smem, acc);
+  store_tile(C, lda, acc, 1.0);
+}
+
+__global__ __launch_bounds__(256, 2) void rest_base(double* A, int64_t lda, const double* U,
+                                                     int64_t ldu, int mt, int kdim) {
+  __shared__ double smem[4 * GSTAGE];
+  const int ntiles = (mt - 1) * mt / 2;
+  for (int q = blockIdx.x; q < ntiles; q += gridDim.x) {
+    int i, j;
+    tri_decode(q, mt - 1, &i, &j);
+    tile_k(A, lda, U, ldu, i + 1, j + 1, kdim, smem);
+  }
+}
+
+// no C traffic: the same MFMA work with zero accumulators, result not stored
+// unless it is NaN (keeps the compiler from dropping it)
+__global__ __launch_bounds__(256, 2) void rest_noc(double* A, int64_t lda, const double* U,
+                                                    int64_t ldu, int mt, int kdim) {
+  __shared__ double smem[4 * GSTAGE];
+  const int ntiles = (mt - 1) * mt / 2;
+  for (int q = blockIdx.x; q < ntiles; q += gridDim.x) {
+    int i, j;
+    tri_decode(q, mt - 1, &i, &j);
+    d4 acc[4][4];
+    zero_tile(acc);
+    gemm_tile<KFAST, KFAST, true>(U + (int64_t)(i + 1) * TS * ldu, ldu,
+                                  U + (int64_t)(j + 1) * TS * ldu + kdim / 2, ldu, kdim, smem, acc);
+    if (acc[0][0][0] != acc[0][0][0]) A[0] = acc[1][1][1];
+  }
+}
+
+
+// Software-pipelined persistent tile loop, one wave per SIMD (all 512 registers):
+// while tile q runs its 16 k-steps, 4 of the 64 per-lane C values of tile q + grid
+// are loaded and 4 of tile q - grid's results are stored per step, and step 15
+// stages tile q + grid's first operand slab, so the C traffic is spread over the
+// MFMA loop instead of a load and a store phase per tile that every workgroup
+// of the launch runs at the same time.
+template <int KD>
+__global__ __launch_bounds__(256, 1) void rest_pipe(double* __restrict__ A, int64_t lda,
+                                                    const double* __restrict__ U, int64_t ldu,
+                                                    int mt) {
+  __shared__ double smem[4 * GSTAGE];
+  constexpr int NS = KD / BK;
+  constexpr int PER = (64 + NS - 1) / NS;   // C values per lane per step
+  const int ntiles = (mt - 1) * mt / 2;
+  int q = blockIdx.x;
+  if (q >= ntiles) return;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int wr = w >> 1, wc = w & 1, fr = lane & 15, fk = lane >> 4;
+  double* sA = smem;
+  double* sB = smem + 2 * GSTAGE;
+  auto tile_ptrs = [&](int qq, double** C, const double** P1, const double** P2) {
+    int i, j;
+    tri_decode(qq, mt - 1, &i, &j);
+    *C = A + (int64_t)(i + 1) * TS * lda + (int64_t)(j + 1) * TS;
+    *P1 = U + (int64_t)(i + 1) * TS * ldu;
+    *P2 = U + (int64_t)(j + 1) * TS * ldu + KD / 2;
+  };
+  const int64_t coff = (int64_t)(wr * 64 + fk) * lda + wc * 64 + fr;
+  auto cidx = [&](int e) -> int64_t {   // e = a * 16 + c * 4 + r
+    return (int64_t)((e >> 4) * 16 + 4 * (e & 3)) * lda + ((e >> 2) & 3) * 16;
+  };
+  d4 acc[4][4], cn[4][4], po[4][4];
+  double* Cq;
+  const double *P1, *P2;
+  tile_ptrs(q, &Cq, &P1, &P2);
+  load_tile(Cq, lda, acc);
+  d2 ra[4], rb[4];
+  gl_op<KFAST>(P1, ldu, 0, ra);
+  gl_op<KFAST>(P2, ldu, 0, rb);
+  st_op<KFAST>(sA, ra);
+  st_op<KFAST>(sB, rb);
+  __syncthreads();
+  double* Cp = nullptr;
+  bool has_p = false;
+  while (true) {
+    const int qn = q + gridDim.x;
+    const bool has_n = qn < ntiles;
+    double* Cn = nullptr;
+    const double *N1 = nullptr, *N2 = nullptr;
+    if (has_n) tile_ptrs(qn, &Cn, &N1, &N2);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const int cur = s & 1;
+      const double* cA = sA + cur * GSTAGE;
+      const double* cB = sB + cur * GSTAGE;
+      const bool ld = s + 1 < NS || has_n;
+      if (s + 1 < NS) {
+        gl_op<KFAST>(P1, ldu, (s + 1) * BK, ra);
+        gl_op<KFAST>(P2, ldu, (s + 1) * BK, rb);
+      } else if (has_n) {
+        gl_op<KFAST>(N1, ldu, 0, ra);
+        gl_op<KFAST>(N2, ldu, 0, rb);
+      }
+      if (has_n) {
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+          const int e = s * PER + u;
+          if (e < 64) cn[e >> 4][(e >> 2) & 3][e & 3] = Cn[coff + cidx(e)];
+        }
+      }
+      if (has_p) {
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+          const int e = s * PER + u;
+          if (e < 64) Cp[coff + cidx(e)] = po[e >> 4][(e >> 2) & 3][e & 3];
+        }
+      }
+#pragma unroll
+      for (int kk = 0; kk < BK / 4; ++kk) {
+        double a[4], b[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a[i] = fr_op<KFAST>(cA, wr * 64 + i * 16 + fr, kk * 4 + fk);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) b[j] = fr_op<KFAST>(cB, wc * 64 + j * 16 + fr, kk * 4 + fk);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = mfma64_neg(a[i], b[j], acc[i][j]);
+      }
+      if (ld) {
+        st_op<KFAST>(sA + (cur ^ 1) * GSTAGE, ra);
+        st_op<KFAST>(sB + (cur ^ 1) * GSTAGE, rb);
+      }
+      __syncthreads();
+    }
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        po[a][c] = acc[a][c];
+        acc[a][c] = cn[a][c];
+      }
+    Cp = Cq;
+    has_p = true;
+    if (!has_n) break;
+    q = qn;
+    Cq = Cn;
+    P1 = N1;
+    P2 = N2;
+  }
+#pragma unroll
+  for (int e = 0; e < 64; ++e) Cp[coff + cidx(e)] = po[e >> 4][(e >> 2) & 3][e & 3];
+}
+
+int main(int argc, char** argv) {
+  const int n = argc > 1 ? atoi(argv[1]) : 16384;
+  const int nt = n / TS;
+  const int64_t ldu = 1024 + 128;
+  double *A, *U;
+  CK(hipMalloc(&A, sizeof(double) * (size_t)n * n));
+  CK(hipMalloc(&U, sizeof(double) * (size_t)n * ldu));
+  {
+    std::vector<double> h((size_t)n * ldu);
+    for (size_t i = 0; i < h.size(); ++i) h[i] = 1e-3 * ((i * 2654435761u) % 1000) / 1000.0;
+    CK(hipMemcpy(U, h.data(), sizeof(double) * h.size(), hipMemcpyHostToDevice));
+    CK(hipMemset(A, 0, sizeof(double) * (size_t)n * n));
+  }
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  const int mts[] = {nt - 1, nt / 2};
+  const int grids[] = {256, 448, 512, 100000};
+  (void)0;
+  const int kds[] = {128, 256, 512, 1024};
+  for (int kern = 0; kern < 3; ++kern)
+    for (int mt : mts)
+      for (int kd : kds)
+        for (int g0 : grids) {
+          if (kern == 2 && kd != 256) continue;
+          const int ntiles = (mt - 1) * mt / 2;
+          const int g = g0 < ntiles ? g0 : ntiles;
+          auto launch = [&]() {
+            if (kern == 0) hipLaunchKernelGGL(rest_base, dim3(g), dim3(256), 0, 0, A, (int64_t)n, U, ldu, mt, kd);
+            else if (kern == 2) hipLaunchKernelGGL(rest_pipe<256>, dim3(g), dim3(256), 0, 0, A, (int64_t)n, U, ldu, mt);
+            else hipLaunchKernelGGL(rest_noc, dim3(g), dim3(256), 0, 0, A, (int64_t)n, U, ldu, mt, kd);
+          };
+          launch();
+          CK(hipDeviceSynchronize());
+          const int reps = 5;
+          CK(hipEventRecord(e0, 0));
+          for (int r = 0; r < reps; ++r) launch();
+          CK(hipEventRecord(e1, 0));
+          CK(hipEventSynchronize(e1));
+          float ms = 0;
+          CK(hipEventElapsedTime(&ms, e0, e1));
+          ms /= reps;
+          const double fl = 2.0 * TS * TS * (double)kd * ntiles;
+          printf("%s mt=%3d kdim=%4d grid=%6d tiles=%6d  %8.3f ms  %6.1f TF  %.3f of 78.6\n",
+                 kern == 2 ? "pipe" : kern ? "noC " : "base", mt, kd, g, ntiles, ms, fl / ms * 1e-9, fl / ms * 1e-9 / 78.6);
+        }
+  return 0;
+}
