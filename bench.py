@@ -750,6 +750,46 @@ def torch_sync():
     torch.cuda.synchronize()
 
 
+def dense_slq_mode(D, etas, ld_exact, nprobe=20, steps=30, reps=3):
+    """imate 'slq' on the resident dense K (gpmi_sp_create_dense): the logdet
+    curve over the same eta grid from ONE device Lanczos of nprobe probes x
+    steps (K X on fp64 MFMA, dense_mm_kernel: 8 n^2 bytes of K per product,
+    HBM-bound), against the dense Cholesky logdets of the headline line (in
+    standard errors of the probe mean). A logdet-curve leg, not an lp: the
+    likelihood's Gram blocks still take the exact solves (_linear_solver.py:71)."""
+    from gaussian_proc import _slq
+    from gaussian_proc._mixed_correlation import MixedCorrelation
+    op = MixedCorrelation(D, imate_method='slq',
+                          imate_options={'num_samples': nprobe, 'lanczos_degree': steps})
+    n = op.n
+    times = []
+    for r in range(reps + 1):
+        op._nodes = None
+        t0 = time.perf_counter()
+        nodes = op.slq_nodes()
+        per = n * _slq.quadrature(nodes, etas, numpy.log)
+        times.append(time.perf_counter() - t0)
+    t = float(numpy.median(times[1:]))
+    est = per.mean(axis=0)
+    se = per.std(axis=0, ddof=1) / numpy.sqrt(nprobe)
+    mm_ms = op.sop.bench_spmm(nprobe, 10)
+    kbytes = 8.0 * n * n
+    out = {'value': round(len(etas) / t, 1), 'unit': 'logdet evals/s',
+           'curve_ms': round(t * 1e3, 3), 'etas': len(etas), 'probes': nprobe, 'steps': steps,
+           'kernel': op.sop.spmm_kernel(nprobe),
+           'dense_mm': {'avg_launch_ms': round(mm_ms, 4), 'bytes': kbytes,
+                        'gbs': round(kbytes / (mm_ms * 1e-3) / 1e9, 1),
+                        'hbm_frac': round(kbytes / (mm_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
+           }
+    if ld_exact is not None:
+        z = (est - ld_exact) / se
+        out['logdet_err_in_std_errors'] = {'max_abs': round(float(numpy.max(numpy.abs(z))), 3),
+                                           'mean': round(float(numpy.mean(z)), 3)}
+        out['logdet_rel_err_max'] = float(numpy.max(numpy.abs(est - ld_exact) / numpy.abs(ld_exact)))
+    op.sop.close()
+    return out
+
+
 def band_nu25_check(D, points, X, z):
     """BASELINE cfg3 as specified (nu = 2.5, smoother, so more nearly rank-deficient
     panels): one band reduction of that K, its panel statistics (CholeskyQR
@@ -1013,6 +1053,9 @@ def main():
         result['band_mode']['optimizer'] = optimizer_timing(D, X, z)
     if rank == 0 and world == 1 and not args.no_band and args.nu == 1.5:
         result['band_mode']['nu25_check'] = band_nu25_check(D, points, X, z)
+    if rank == 0 and world == 1 and args.scaling == 'strong' and last is not None:
+        result['dense_slq_mode'] = dense_slq_mode(D, last[:, 0], last[:, 1])
+        log('dense slq: %s' % result['dense_slq_mode'])
     if world == 1 and not args.no_sparse:
         # release the dense and band operators (their streams count against the
         # process's hardware queues) before the sparse configs run
