@@ -772,20 +772,27 @@ def dense_slq_mode(D, etas, ld_exact, nprobe=20, steps=30, reps=3):
     t = float(numpy.median(times[1:]))
     est = per.mean(axis=0)
     se = per.std(axis=0, ddof=1) / numpy.sqrt(nprobe)
-    mm_ms = op.sop.bench_spmm(nprobe, 10)
+    mm = {w: op.sop.bench_spmm(w, 10) for w in sorted({16, nprobe, 32})}
+    mm_ms = mm[nprobe]
     kbytes = 8.0 * n * n
     out = {'value': round(len(etas) / t, 1), 'unit': 'logdet evals/s',
            'curve_ms': round(t * 1e3, 3), 'etas': len(etas), 'probes': nprobe, 'steps': steps,
            'kernel': op.sop.spmm_kernel(nprobe),
            'dense_mm': {'avg_launch_ms': round(mm_ms, 4), 'bytes': kbytes,
                         'gbs': round(kbytes / (mm_ms * 1e-3) / 1e9, 1),
-                        'hbm_frac': round(kbytes / (mm_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
-           }
+                        'hbm_frac': round(kbytes / (mm_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                        'ms_by_columns': {str(w): round(v, 4) for w, v in mm.items()}}}
     if ld_exact is not None:
-        z = (est - ld_exact) / se
-        out['logdet_err_in_std_errors'] = {'max_abs': round(float(numpy.max(numpy.abs(z))), 3),
-                                           'mean': round(float(numpy.mean(z)), 3)}
-        out['logdet_rel_err_max'] = float(numpy.max(numpy.abs(est - ld_exact) / numpy.abs(ld_exact)))
+        # SLQ with 30 Lanczos steps does not resolve the smallest eigenvalues of the
+        # smooth nu = 1.5 K at small eta (cond ~1e5 at eta = 1e-3): a bias of the
+        # estimator there, not of the kernel; at eta >= 1 it is within the probe error
+        zs = (est - ld_exact) / se
+        pick = [0, int(numpy.argmin(numpy.abs(numpy.log(etas)))), len(etas) - 1]
+        out['logdet_check'] = {
+            'eta': [float(etas[i]) for i in pick],
+            'rel_err': [float(abs(est[i] - ld_exact[i]) / abs(ld_exact[i])) for i in pick],
+            'err_in_std_errors': [round(float(zs[i]), 3) for i in pick],
+            'max_abs_std_errors_eta_ge_1': round(float(numpy.max(numpy.abs(zs[etas >= 1.0]))), 3)}
     op.sop.close()
     return out
 

@@ -1228,7 +1228,8 @@ __global__ __launch_bounds__(256) void csr_permute_kernel(
 // consecutive doubles of its row, K[r0 + (l & 15)][k0 + 16 (l >> 4) + m] (128 B
 // per lane, the whole 16 x 64 block per wave), and MFMA m takes k = k0 +
 // 16 (l >> 4) + m: a fixed permutation of the k order inside the chunk. The X
-// chunk (64 x 16 CT, zero past n and s) is staged in LDS for the four waves.
+// chunk (64 x 16 CT, zero past n and s) is staged in LDS for the four waves,
+// double-buffered, with the next chunk's K and X in registers.
 // K must have ceil(n / 64) * 64 readable rows and columns (the dense operator's
 // n_pad); the partials are summed by dense_mm_reduce_kernel in split order.
 // HBM-bound: 8 n^2 bytes of K per launch.
@@ -1239,7 +1240,8 @@ __global__ __launch_bounds__(256) void dense_mm_kernel(const double* __restrict_
                                                        int s, int kcs,
                                                        double* __restrict__ Yp) {
   constexpr int XC = 16 * CT;
-  __shared__ double sx[64][XC + 1];
+  constexpr int XU = XC / 4;   // X values per thread per chunk
+  __shared__ double sx[2][64][XC + 1];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int64_t r0 = (int64_t)blockIdx.x * 64 + w * 16;
   const int kq = lane >> 4, fr = lane & 15;
@@ -1249,25 +1251,43 @@ __global__ __launch_bounds__(256) void dense_mm_kernel(const double* __restrict_
   d4 acc[CT];
 #pragma unroll
   for (int ct = 0; ct < CT; ++ct) acc[ct] = d4{0.0, 0.0, 0.0, 0.0};
-  for (int64_t c = c0; c < c1; ++c) {
+  // chunk c + 1's K and X are loaded into registers while chunk c computes (the
+  // loads' latency, not the MFMA, bounds a chunk otherwise); X goes to the LDS
+  // buffer of its parity, one barrier per chunk
+  d2 kn[8];
+  double xn[XU];
+  auto load = [&](int64_t c) {
     const int64_t k0 = c * 64;
-    d2 kv[8];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) kv[q] = *reinterpret_cast<const d2*>(Kr + k0 + 2 * q);
+    for (int q = 0; q < 8; ++q) kn[q] = *reinterpret_cast<const d2*>(Kr + k0 + 2 * q);
 #pragma unroll
-    for (int u = 0; u < XC / 4; ++u) {
+    for (int u = 0; u < XU; ++u) {
       const int e = u * 256 + t, kr = e / XC, col = e % XC;
       const int64_t k = k0 + kr;
-      sx[kr][col] = (k < n && col < s) ? X[k * s + col] : 0.0;
+      xn[u] = (k < n && col < s) ? X[k * s + col] : 0.0;
+    }
+  };
+  if (c0 < c1) load(c0);
+  int buf = 0;
+  for (int64_t c = c0; c < c1; ++c) {
+    d2 kv[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) kv[q] = kn[q];
+#pragma unroll
+    for (int u = 0; u < XU; ++u) {
+      const int e = u * 256 + t;
+      sx[buf][e / XC][e % XC] = xn[u];
     }
     __syncthreads();
+    if (c + 1 < c1) load(c + 1);
 #pragma unroll
     for (int m = 0; m < 16; ++m) {
       const double a = kv[m >> 1][m & 1];
 #pragma unroll
-      for (int ct = 0; ct < CT; ++ct) acc[ct] = mfma64(a, sx[16 * kq + m][16 * ct + fr], acc[ct]);
+      for (int ct = 0; ct < CT; ++ct)
+        acc[ct] = mfma64(a, sx[buf][16 * kq + m][16 * ct + fr], acc[ct]);
     }
-    __syncthreads();
+    buf ^= 1;
   }
   double* out = Yp + (int64_t)blockIdx.y * n * s;
 #pragma unroll

@@ -166,6 +166,105 @@ __global__ __launch_bounds__(256, 1) void rest_pipe(double* __restrict__ A, int6
   for (int e = 0; e < 64; ++e) Cp[coff + cidx(e)] = po[e >> 4][(e >> 2) & 3][e & 3];
 }
 
+// SYMM as shipped (gpmi_band.hip symm_kernel), and a timing-only variant that
+// reads every tile in the row-major (KFAST) layout: how much the transposed
+// (KSLOW, J > I) tiles cost.
+template <bool ALLFAST>
+__global__ __launch_bounds__(256, 2) void symm_probe(const double* __restrict__ A, int64_t lda,
+                                                     const double* __restrict__ U, int64_t ldu,
+                                                     int tr0, int mt, int chunk,
+                                                     double* __restrict__ Xp) {
+  __shared__ double smem[4 * GSTAGE];
+  const int il = blockIdx.x, ch = blockIdx.y, nch = gridDim.y;
+  const int I = tr0 + il;
+  const int jl0 = ch * chunk, jl1 = min(mt, (ch + 1) * chunk);
+  const int jsplit = ALLFAST ? jl1 : min(jl1, max(jl0, il + 1));
+  d4 acc[4][4];
+  zero_tile(acc);
+  for (int jl = jl0; jl < jsplit; ++jl) {
+    const int J = tr0 + jl;
+    gemm_tile<KFAST, KSLOW, false>(A + (int64_t)I * TS * lda + (int64_t)J * TS, lda,
+                                   U + (int64_t)J * TS * ldu + TS, ldu, TS, smem, acc);
+  }
+  for (int jl = jsplit; jl < jl1; ++jl) {
+    const int J = tr0 + jl;
+    gemm_tile<KSLOW, KSLOW, false>(A + (int64_t)J * TS * lda + (int64_t)I * TS, lda,
+                                   U + (int64_t)J * TS * ldu + TS, ldu, TS, smem, acc);
+  }
+  store_tile(Xp + ((int64_t)il * nch + ch) * TS * TS, TS, acc, 1.0);
+}
+
+// KFAST-only tile loop with 8-deep k stages (LDS 32 KB per workgroup: three
+// workgroups fit a CU, with <= 168 VGPRs three waves per SIMD), row-group swizzled
+// slabs: s[row * 8 + (k ^ 2 ((row >> 2) & 3))].
+__device__ __forceinline__ int s8(int row, int k) { return row * 8 + (k ^ (2 * ((row >> 2) & 3))); }
+__device__ __forceinline__ void gl8(const double* __restrict__ P, int64_t ld, int k0, d2 (&r)[2]) {
+  const int t = threadIdx.x, row = t >> 1, h = (t & 1) * 4;
+  const double* p = P + (int64_t)row * ld + k0 + h;
+  r[0] = *reinterpret_cast<const d2*>(p);
+  r[1] = *reinterpret_cast<const d2*>(p + 2);
+}
+__device__ __forceinline__ void st8(double* s, const d2 (&r)[2]) {
+  const int t = threadIdx.x, row = t >> 1, h = (t & 1) * 4;
+  *reinterpret_cast<d2*>(s + s8(row, h)) = r[0];
+  *reinterpret_cast<d2*>(s + s8(row, h + 2)) = r[1];
+}
+template <int OCC>
+__global__ __launch_bounds__(256, OCC) void rest_b8(double* __restrict__ A, int64_t lda,
+                                                    const double* __restrict__ U, int64_t ldu,
+                                                    int mt, int kdim) {
+  __shared__ double smem[4 * 1024];
+  const int ntiles = (mt - 1) * mt / 2;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int wr = w >> 1, wc = w & 1, fr = lane & 15, fk = lane >> 4;
+  double* sA = smem;
+  double* sB = smem + 2048;
+  for (int q = blockIdx.x; q < ntiles; q += gridDim.x) {
+    int i, j;
+    tri_decode(q, mt - 1, &i, &j);
+    double* C = A + (int64_t)(i + 1) * TS * lda + (int64_t)(j + 1) * TS;
+    const double* P1 = U + (int64_t)(i + 1) * TS * ldu;
+    const double* P2 = U + (int64_t)(j + 1) * TS * ldu + kdim / 2;
+    d4 acc[4][4];
+    load_tile(C, lda, acc);
+    d2 ra[2], rb[2];
+    gl8(P1, ldu, 0, ra);
+    gl8(P2, ldu, 0, rb);
+    st8(sA, ra);
+    st8(sB, rb);
+    __syncthreads();
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    const int nsteps = kdim / 8;
+    for (int s = 0; s < nsteps; ++s) {
+      const int cur = s & 1;
+      const double* cA = sA + cur * 1024;
+      const double* cB = sB + cur * 1024;
+      if (s + 1 < nsteps) {
+        gl8(P1, ldu, (s + 1) * 8, ra);
+        gl8(P2, ldu, (s + 1) * 8, rb);
+      }
+#pragma unroll 1
+      for (int kk = 0; kk < 2; ++kk) {
+        double a[4], b[4];
+#pragma unroll
+        for (int x = 0; x < 4; ++x) a[x] = cA[s8(wr * 64 + x * 16 + fr, kk * 4 + fk)];
+#pragma unroll
+        for (int y = 0; y < 4; ++y) b[y] = cB[s8(wc * 64 + y * 16 + fr, kk * 4 + fk)];
+#pragma unroll
+        for (int x = 0; x < 4; ++x)
+#pragma unroll
+          for (int y = 0; y < 4; ++y) acc[x][y] = mfma64_neg(a[x], b[y], acc[x][y]);
+      }
+      if (s + 1 < nsteps) {
+        st8(sA + (cur ^ 1) * 1024, ra);
+        st8(sB + (cur ^ 1) * 1024, rb);
+      }
+      __syncthreads();
+    }
+    store_tile(C, lda, acc, 1.0);
+  }
+}
+
 int main(int argc, char** argv) {
   const int n = argc > 1 ? atoi(argv[1]) : 16384;
   const int nt = n / TS;
@@ -183,18 +282,22 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   const int mts[] = {nt - 1, nt / 2};
-  const int grids[] = {256, 448, 512, 100000};
+  const int grids[] = {448, 512, 768, 1024, 100000};
   (void)0;
-  const int kds[] = {128, 256, 512, 1024};
-  for (int kern = 0; kern < 3; ++kern)
+  const int kds[] = {256, 512};
+  for (int kern : {0, 3, 4, 5})
     for (int mt : mts)
       for (int kd : kds)
         for (int g0 : grids) {
           if (kern == 2 && kd != 256) continue;
+          if (kern == 0 && g0 > 512 && g0 < 100000) continue;
           const int ntiles = (mt - 1) * mt / 2;
           const int g = g0 < ntiles ? g0 : ntiles;
           auto launch = [&]() {
-            if (kern == 0) hipLaunchKernelGGL(rest_base, dim3(g), dim3(256), 0, 0, A, (int64_t)n, U, ldu, mt, kd);
+            if (kern == 3) hipLaunchKernelGGL(rest_b8<2>, dim3(g), dim3(256), 0, 0, A, (int64_t)n, U, ldu, mt, kd);
+            else if (kern == 4) hipLaunchKernelGGL(rest_b8<3>, dim3(g), dim3(256), 0, 0, A, (int64_t)n, U, ldu, mt, kd);
+            else if (kern == 5) hipLaunchKernelGGL(rest_b8<4>, dim3(g), dim3(256), 0, 0, A, (int64_t)n, U, ldu, mt, kd);
+            else if (kern == 0) hipLaunchKernelGGL(rest_base, dim3(g), dim3(256), 0, 0, A, (int64_t)n, U, ldu, mt, kd);
             else if (kern == 2) hipLaunchKernelGGL(rest_pipe<256>, dim3(g), dim3(256), 0, 0, A, (int64_t)n, U, ldu, mt);
             else hipLaunchKernelGGL(rest_noc, dim3(g), dim3(256), 0, 0, A, (int64_t)n, U, ldu, mt, kd);
           };
@@ -210,7 +313,33 @@ int main(int argc, char** argv) {
           ms /= reps;
           const double fl = 2.0 * TS * TS * (double)kd * ntiles;
           printf("%s mt=%3d kdim=%4d grid=%6d tiles=%6d  %8.3f ms  %6.1f TF  %.3f of 78.6\n",
-                 kern == 2 ? "pipe" : kern ? "noC " : "base", mt, kd, g, ntiles, ms, fl / ms * 1e-9, fl / ms * 1e-9 / 78.6);
+                 kern == 3 ? "b8o2" : kern == 4 ? "b8o3" : kern == 5 ? "b8o4" : kern == 2 ? "pipe" : kern ? "noC " : "base", mt, kd, g, ntiles, ms, fl / ms * 1e-9, fl / ms * 1e-9 / 78.6);
         }
+  {
+    double* Xp;
+    CK(hipMalloc(&Xp, sizeof(double) * (size_t)nt * 16 * TS * TS));
+    for (int mt : {nt - 1, nt / 2})
+      for (int chunk : {4, 8, 16, 32})
+        for (int af = 0; af < 2; ++af) {
+          const int sch = (mt + chunk - 1) / chunk;
+          if (sch > 16) continue;
+          auto launch = [&]() {
+            if (af) hipLaunchKernelGGL(symm_probe<true>, dim3(mt, sch), dim3(256), 0, 0, A, (int64_t)n, U, ldu, 1, mt, chunk, Xp);
+            else hipLaunchKernelGGL(symm_probe<false>, dim3(mt, sch), dim3(256), 0, 0, A, (int64_t)n, U, ldu, 1, mt, chunk, Xp);
+          };
+          launch();
+          CK(hipDeviceSynchronize());
+          CK(hipEventRecord(e0, 0));
+          for (int r = 0; r < 5; ++r) launch();
+          CK(hipEventRecord(e1, 0));
+          CK(hipEventSynchronize(e1));
+          float ms = 0;
+          CK(hipEventElapsedTime(&ms, e0, e1));
+          ms /= 5;
+          const double fl = 2.0 * (double)mt * TS * mt * TS * TS;
+          printf("symm%s mt=%3d chunk=%2d wgs=%5d  %8.3f ms  %6.1f TF  %.3f\n", af ? "(allfast)" : "         ",
+                 mt, chunk, mt * sch, ms, fl / ms * 1e-9, fl / ms * 1e-9 / 78.6);
+        }
+  }
   return 0;
 }
