@@ -1094,19 +1094,23 @@ __global__ __launch_bounds__(256) void ms_r_update_kernel(double* __restrict__ R
 }
 
 // Scalar step 2 (thread (j, c), j < S shifts): with BR = B^T r_new and rr_new
-// reduced from the partials (fixed order), advance zeta, accumulate G, update
+// reduced from the partials (fixed order; nblk == 0: reduced beforehand), advance zeta, accumulate G, update
 // b^T p and the base beta; a column stops when sqrt(rr) <= rtol ||b||.
 __global__ void ms_scalar_kernel(MsState st, const double* __restrict__ partial, int nblk,
                                  const double* __restrict__ dshift, int S, int s, double rtol2,
                                  double* __restrict__ beta_out) {
   __shared__ double br[MS_MAXS * MS_MAXS + MS_MAXS];
   const int ne = s * s + s;
-  {
+  if (nblk > 0) {
     const int nw = blockDim.x >> 6, wv = threadIdx.x >> 6;
     for (int e = wv; e < ne; e += nw) {
       const double v = wave_reduce_partials(partial, nblk, ne, e);
       if ((threadIdx.x & 63) == 0) br[e] = v;
     }
+  } else {
+    // nblk == 0: `partial` holds the reduced values (col_dot_reduce_kernel, one wave
+    // per element over the whole chip: the same sums as above)
+    for (int e = threadIdx.x; e < ne; e += blockDim.x) br[e] = partial[e];
   }
   __syncthreads();
   const int t = threadIdx.x;

@@ -1111,7 +1111,8 @@ int gpmi_sp_msgram(gpmi_sp* sp, const double* etas, int neta, const double* rhs,
   }
   double* partial = sp->ms_partial;
   double* pqpart = partial + (size_t)MS_RB * ne;
-  const size_t need = (size_t)6 * s + 2 * (size_t)S * s + 2 * (size_t)S * s * s + S + s + s + 1;
+  const size_t need = (size_t)6 * s + 2 * (size_t)S * s + 2 * (size_t)S * s * s + S + s + s + 1 +
+                      (size_t)ne;
   if (sp->msbuf_doubles < need) {
     if (sp->msbuf) SP_TRY(hipFree(sp->msbuf));
     sp->msbuf = nullptr;
@@ -1135,6 +1136,8 @@ int gpmi_sp_msgram(gpmi_sp* sp, const double* etas, int neta, const double* rhs,
   st.active = reinterpret_cast<int*>(q);   // s ints in s doubles
   q += s;
   st.flags = reinterpret_cast<int*>(q);    // 1 int in 1 double
+  q += 1;
+  double* brd = q;                         // [ne] reduced B^T r, r . r
   sp->last_converged = 0;
   double* Bd = sp->ms_ws;
   double* Rd = Bd + ns;
@@ -1147,6 +1150,11 @@ int gpmi_sp_msgram(gpmi_sp* sp, const double* etas, int neta, const double* rhs,
   // wider blocks: the MFMA form (GPMI_MS_MFMA=0 keeps the separate update and dots)
   const char* menv = std::getenv("GPMI_MS_MFMA");
   const bool mfma_r = !fused_r && s <= 16 && !(menv && std::atoi(menv) == 0);
+  // chip-wide partial reduction for the MFMA form's 512 partial rows (cfg 5: step
+  // 33.6 -> 32.0 ms); the fused form's 128 stay in the scalar kernel (cfg 4: the
+  // extra launch costs more than it saves). GPMI_MS_RED=0 / 1 forces either.
+  const char* renv = std::getenv("GPMI_MS_RED");
+  const bool chip_red = renv ? std::atoi(renv) != 0 : mfma_r;
   double* Rcur = Rd;     // the live residual
   double* Rnext = Rd2;
   hipStream_t str = sp->ms_stream;
@@ -1234,8 +1242,17 @@ int gpmi_sp_msgram(gpmi_sp* sp, const double* etas, int neta, const double* rhs,
       launch_ms_dots(Bd, Rcur, n, s, partial, MS_NBLK, str);
       SP_LAUNCH("ms_dots_partial_kernel");
     }
-    hipLaunchKernelGGL(ms_scalar_kernel, dim3(1), dim3(sthreads), 0, str, st, partial,
-                       mfma_r ? MS_RB : MS_NBLK, dshift, S, s, rtol * rtol, beta_out);
+    // the ne = s^2 + s partial sums reduced one wave per element across the chip
+    // (GPMI_MS_RED=0: inside the one-workgroup scalar kernel, 16 waves)
+    const int pnb = mfma_r ? MS_RB : MS_NBLK;
+    if (chip_red) {
+      hipLaunchKernelGGL(col_dot_reduce_kernel, dim3((ne + 3) / 4), dim3(256), 0, str, partial,
+                         pnb, 1, ne, brd);
+      SP_LAUNCH("col_dot_reduce_kernel");
+    }
+    hipLaunchKernelGGL(ms_scalar_kernel, dim3(1), dim3(sthreads), 0, str, st,
+                       chip_red ? (const double*)brd : partial, chip_red ? 0 : pnb, dshift, S, s,
+                       rtol * rtol, beta_out);
     SP_LAUNCH("ms_scalar_kernel");
     hipLaunchKernelGGL(ms_p_update_kernel, dim3(grid_ns(n, s)), dim3(256), 0, str, Pd, Rout,
                        st.beta, st.active, n, s);
