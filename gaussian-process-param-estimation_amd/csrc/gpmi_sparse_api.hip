@@ -46,6 +46,11 @@ template <int S>
 __global__ void csr_spmm_winf_kernel(const int64_t*, const int*, const unsigned short*,
                                      const double*, int64_t, const int*, const int*,
                                      const double*, double*, double);
+template <int S, int U>
+__global__ void csr_spmm_wing_kernel(const int64_t*, const int*, const unsigned short*,
+                                     const double*, int64_t, const int*, const int*,
+                                     const double*, double*, double);
+constexpr int WING_MAX_LDS = 80 * 1024;   // two workgroups per CU
 constexpr int WIN_ROWS_HOST = 64;    // = WIN_ROWS (gpmi_sparse.hip)
 constexpr int WIN_MAXU_HOST = 1024;  // = WIN_MAXU
 constexpr int WIN_CS_HOST = 8;       // = WIN_CS
@@ -258,6 +263,16 @@ int ensure_window(gpmi_sp* sp) {
   if (lds > 64 * 1024)
     SP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&csr_spmm_win_kernel),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  for (const void* f : {reinterpret_cast<const void*>(&csr_spmm_wing_kernel<20, 4>),
+                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<20, 8>),
+                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<20, 16>),
+                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<11, 4>),
+                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<11, 8>),
+                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<11, 16>),
+                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<7, 4>),
+                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<7, 8>),
+                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<7, 16>)})
+    SP_TRY(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, WING_MAX_LDS));
   sp->win_nblk = nblk;
   sp->win_maxu = mu;
   return 0;
@@ -279,6 +294,15 @@ int spmm_kind(gpmi_sp* sp, int s, int* kind) {
   if (wmode != 0 && sp->win_maxu < 0)
     if (int rc = ensure_window(sp)) return rc;
   *kind = 0;
+  // the window with latency-hidden staging (csr_spmm_wing_kernel) at the Lanczos
+  // and multi-shift CG widths while the widest window fits two workgroups per CU
+  // (GPMI_SPMM_WING=0: off)
+  const char* genv = std::getenv("GPMI_SPMM_WING");
+  if (wmode != 0 && !(genv && std::atoi(genv) == 0) && (s == 20 || s == 11 || s == 7) &&
+      sp->win_maxu > 0 && sizeof(double) * (size_t)sp->win_maxu * s <= (size_t)WING_MAX_LDS) {
+    *kind = 5;
+    return 0;
+  }
   if (wmode == 2 || (wmode != 0 && sp->win_use)) {
     *kind = 1;
     const char* fenv = std::getenv("GPMI_SPMM_FULL");
@@ -312,6 +336,25 @@ int spmm(gpmi_sp* sp, const double* X, double* Y, int s, double eta, hipStream_t
   }
   int kind = 0;
   if (int rc = spmm_kind(sp, s, &kind)) return rc;
+  if (kind == 5) {
+    const size_t lds = sizeof(double) * (size_t)s * (size_t)sp->win_maxu;
+    // nonzeros in flight per thread (GPMI_SPMM_WUNR 4, 8 or 16; 8 measured best at
+    // cfg 5, within 0.3 us of 4 at cfg 4)
+    const char* uenv = std::getenv("GPMI_SPMM_WUNR");
+    const int un = uenv ? std::atoi(uenv) : 8;
+    auto pick = [un](auto k4, auto k8, auto k16) { return un == 4 ? k4 : un == 8 ? k8 : k16; };
+    auto kfn = s == 20 ? pick(csr_spmm_wing_kernel<20, 4>, csr_spmm_wing_kernel<20, 8>,
+                              csr_spmm_wing_kernel<20, 16>)
+               : s == 11 ? pick(csr_spmm_wing_kernel<11, 4>, csr_spmm_wing_kernel<11, 8>,
+                                csr_spmm_wing_kernel<11, 16>)
+                         : pick(csr_spmm_wing_kernel<7, 4>, csr_spmm_wing_kernel<7, 8>,
+                                csr_spmm_wing_kernel<7, 16>);
+    hipLaunchKernelGGL(kfn, dim3((unsigned)sp->win_nblk), dim3(256), lds, st, sp->indptr,
+                       sp->indices, sp->win_lidx, sp->data, sp->n, sp->win_cols, sp->win_u, X, Y,
+                       eta);
+    SP_LAUNCH("csr_spmm_wing_kernel");
+    return 0;
+  }
   if (kind == 2) {
     // the one-pass full-width window (csr_spmm_winf_kernel) at the Lanczos width
     const size_t lds = sizeof(double) * (size_t)s * (size_t)std::max(1, sp->win_maxu) +

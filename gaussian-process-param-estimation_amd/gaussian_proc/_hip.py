@@ -577,7 +577,7 @@ class SparseOperator(object):
         check(self.lib.gpmi_sp_spmm_kernel(self.h, int(s), ctypes.byref(k)),
               'gpmi_sp_spmm_kernel')
         return ('csr_spmm_kernel', 'csr_spmm_win_kernel', 'csr_spmm_winf_kernel',
-                'csr_spmm_pair_kernel', 'dense_mm_kernel')[k.value]
+                'csr_spmm_pair_kernel', 'dense_mm_kernel', 'csr_spmm_wing_kernel')[k.value]
 
     def lanczos(self, nprobe, steps, seed=0, probe_offset=0):
         """-> alpha[nprobe, steps], beta[nprobe, steps] (beta = 0 ends a tridiagonal)."""

@@ -83,7 +83,9 @@ def test_window_spmm_equals_gather_spmm(gp, monkeypatch):
     columns, on a matrix whose first blocks overflow the window limits (more
     than 4096 nonzeros, more than 1024 distinct columns) and so take the
     gather path inside the same launch. For even s the gather is the column-pair
-    kernel; GPMI_SPMM_PAIR=0 gives the one-column gather to compare with."""
+    kernel; GPMI_SPMM_PAIR=0 gives the one-column gather to compare with. At
+    s = 7, 11, 20 the default is the window with latency-hidden staging
+    (csr_spmm_wing_kernel); GPMI_SPMM_WING=0 gives the chunked window kernel."""
     from gaussian_proc import _hip
     rng = numpy.random.RandomState(4)
     n = 3000
@@ -105,6 +107,11 @@ def test_window_spmm_equals_gather_spmm(gp, monkeypatch):
     sop = _hip.SparseOperator.from_csr(A)
     for s in (1, 7, 8, 11, 20, 32):
         X = rng.randn(n, s)
+        # the window with latency-hidden staging (default at s = 7, 11, 20)
+        Ywg = sop.spmm(0.3, X)
+        if s in (7, 11, 20):
+            assert sop.spmm_kernel(s) == 'csr_spmm_wing_kernel'
+        monkeypatch.setenv('GPMI_SPMM_WING', '0')
         monkeypatch.setenv('GPMI_SPMM_WINDOW', '2')
         Yw = sop.spmm(0.3, X)
         monkeypatch.setenv('GPMI_SPMM_WINDOW', '0')
@@ -115,7 +122,9 @@ def test_window_spmm_equals_gather_spmm(gp, monkeypatch):
         monkeypatch.delenv('GPMI_SPMM_PAIR')
         assert sop.spmm_kernel(s) == ('csr_spmm_pair_kernel' if s % 2 == 0 else 'csr_spmm_kernel')
         monkeypatch.delenv('GPMI_SPMM_WINDOW')
+        monkeypatch.delenv('GPMI_SPMM_WING')
         ref = A @ X + 0.3 * X
+        assert _nrel(Ywg, ref) < 1e-13, s
         assert _nrel(Yw, ref) < 1e-13, s
         assert _nrel(Yw, Yg) < 1e-13, s
         assert _nrel(Y1, Yg) < 1e-13, s
