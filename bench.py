@@ -427,7 +427,8 @@ def sparse_measure(args, config, world, rank, local, dist, torch, cpu, exact):
     gbs = alg_bytes / (ms * 1e-3) / 1e9
     info = op.sop.spmm_info()
     sp_kernel = op.sop.spmm_kernel(s_blk)
-    gather_bytes = (8.0 * s_blk * info['mean_window'] * ((n + 63) // 64) if info['windowed']
+    windowed = info['windowed'] or sp_kernel == 'csr_spmm_wing_kernel'
+    gather_bytes = (8.0 * s_blk * info['mean_window'] * ((n + 63) // 64) if windowed
                     else 8.0 * nnz * s_blk)
     sp_traffic, sp_tsrc = (pmc_traffic_sparse(config, 'gpmi::' + sp_kernel)
                            if s_blk == 20 else (None, None))

@@ -205,7 +205,8 @@ int gpmi_sp_spmm_info(gpmi_sp* sp, int* windowed, double* mean_window, int* max_
  * (csr_spmm_win_kernel), 2 X-window in one full-width pass (csr_spmm_winf_kernel,
  * s = 20), 3 gather from X by column pairs (csr_spmm_pair_kernel, even s; a block
  * that is not 16-byte aligned runs csr_spmm_kernel), 4 dense (dense_mm_kernel,
- * gpmi_sp_create_dense). Diagnostic; no reference
+ * gpmi_sp_create_dense), 5 window with latency-hidden staging (csr_spmm_wing_kernel,
+ * s = 7, 11, 20 while the widest window fits 80 KB of LDS). Diagnostic; no reference
  * counterpart. */
 int gpmi_sp_spmm_kernel(gpmi_sp* sp, int s, int* kind);
 /* Whether the last gpmi_sp_cg / gpmi_sp_msgram met rtol in every column before
