@@ -868,66 +868,105 @@ __global__ void lz_scalar_kernel(const double* __restrict__ d, int k, int steps,
 }
 
 // v_k = u / rho - sum_{j<k} V_j cv_j;  u <- y / rho - sum_{j<k} V_j cu_j - v_k cu_k;
-// V_k = v_k. Two consecutive elements per thread (16-byte loads), the basis loads
-// four vectors at a time.
+// V_k = v_k. Two consecutive elements per thread (16-byte loads) in each of NR
+// row chunks P pairs apart (P = the grid's thread count, 2 P a multiple of s, so the
+// chunks share the thread's two columns and their coefficient loads), the basis
+// loads four vectors at a time; the same per-element order of subtraction as one
+// element per thread.
+template <int NR>
 __global__ __launch_bounds__(256) void lz_update_kernel(double* __restrict__ V, int64_t ns, int k,
                                                         double* __restrict__ U,
                                                         const double* __restrict__ Y,
                                                         const double* __restrict__ cv,
                                                         const double* __restrict__ cu,
                                                         const double* __restrict__ ir, int s) {
-  const int64_t e = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 2;
-  if (e >= ns) return;
-  const int c0 = (int)(e % s), c1 = (c0 + 1 == s) ? 0 : c0 + 1;
-  if (e + 1 < ns && (ns & 1) == 0) {
-    const d2 u = *reinterpret_cast<const d2*>(U + e);
-    const d2 y = *reinterpret_cast<const d2*>(Y + e);
-    double v0 = u[0] * ir[c0], v1 = u[1] * ir[c1];
-    double w0 = y[0] * ir[c0], w1 = y[1] * ir[c1];
+  const int64_t P = (int64_t)gridDim.x * 256;
+  const int64_t e0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 2;
+  if (e0 >= ns) return;
+  const int c0 = (int)(e0 % s), c1 = (c0 + 1 == s) ? 0 : c0 + 1;
+  if ((ns & 1) == 0) {
+    double v0[NR], v1[NR], w0[NR], w1[NR];
+    bool on[NR];
+    const double i0 = ir[c0], i1 = ir[c1];
+#pragma unroll
+    for (int m = 0; m < NR; ++m) {
+      const int64_t e = e0 + 2 * P * m;
+      on[m] = e < ns;
+      const d2 u = on[m] ? *reinterpret_cast<const d2*>(U + e) : d2{0.0, 0.0};
+      const d2 y = on[m] ? *reinterpret_cast<const d2*>(Y + e) : d2{0.0, 0.0};
+      v0[m] = u[0] * i0;
+      v1[m] = u[1] * i1;
+      w0[m] = y[0] * i0;
+      w1[m] = y[1] * i1;
+    }
     int j = 0;
     for (; j + 4 <= k; j += 4) {
-      d2 a[4];
+      d2 a[4][NR];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) a[q] = *reinterpret_cast<const d2*>(V + (j + q) * ns + e);
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int m = 0; m < NR; ++m)
+          a[q][m] = on[m] ? *reinterpret_cast<const d2*>(V + (j + q) * ns + e0 + 2 * P * m)
+                          : d2{0.0, 0.0};
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        v0 -= a[q][0] * cv[(j + q) * s + c0];
-        v1 -= a[q][1] * cv[(j + q) * s + c1];
-        w0 -= a[q][0] * cu[(j + q) * s + c0];
-        w1 -= a[q][1] * cu[(j + q) * s + c1];
+        const double cv0 = cv[(j + q) * s + c0], cv1 = cv[(j + q) * s + c1];
+        const double cu0 = cu[(j + q) * s + c0], cu1 = cu[(j + q) * s + c1];
+#pragma unroll
+        for (int m = 0; m < NR; ++m) {
+          v0[m] -= a[q][m][0] * cv0;
+          v1[m] -= a[q][m][1] * cv1;
+          w0[m] -= a[q][m][0] * cu0;
+          w1[m] -= a[q][m][1] * cu1;
+        }
       }
     }
     for (; j < k; ++j) {
-      const d2 a = *reinterpret_cast<const d2*>(V + j * ns + e);
-      v0 -= a[0] * cv[j * s + c0];
-      v1 -= a[1] * cv[j * s + c1];
-      w0 -= a[0] * cu[j * s + c0];
-      w1 -= a[1] * cu[j * s + c1];
-    }
-    w0 -= v0 * cu[k * s + c0];
-    w1 -= v1 * cu[k * s + c1];
-    d2 vo, wo;
-    vo[0] = v0;
-    vo[1] = v1;
-    wo[0] = w0;
-    wo[1] = w1;
-    *reinterpret_cast<d2*>(V + k * ns + e) = vo;
-    *reinterpret_cast<d2*>(U + e) = wo;
-  } else {
-    for (int64_t f = e; f < e + 2 && f < ns; ++f) {
-      const int c = (int)(f % s);
-      double v = U[f] * ir[c], w = Y[f] * ir[c];
-      for (int j = 0; j < k; ++j) {
-        const double a = V[j * ns + f];
-        v -= a * cv[j * s + c];
-        w -= a * cu[j * s + c];
+      const double cv0 = cv[j * s + c0], cv1 = cv[j * s + c1];
+      const double cu0 = cu[j * s + c0], cu1 = cu[j * s + c1];
+#pragma unroll
+      for (int m = 0; m < NR; ++m) {
+        const d2 a = on[m] ? *reinterpret_cast<const d2*>(V + j * ns + e0 + 2 * P * m)
+                           : d2{0.0, 0.0};
+        v0[m] -= a[0] * cv0;
+        v1[m] -= a[1] * cv1;
+        w0[m] -= a[0] * cu0;
+        w1[m] -= a[1] * cu1;
       }
-      w -= v * cu[k * s + c];
-      V[k * ns + f] = v;
-      U[f] = w;
     }
+    const double ck0 = cu[k * s + c0], ck1 = cu[k * s + c1];
+#pragma unroll
+    for (int m = 0; m < NR; ++m) {
+      if (!on[m]) continue;
+      const int64_t e = e0 + 2 * P * m;
+      d2 vo, wo;
+      vo[0] = v0[m];
+      vo[1] = v1[m];
+      wo[0] = w0[m] - v0[m] * ck0;
+      wo[1] = w1[m] - v1[m] * ck1;
+      *reinterpret_cast<d2*>(V + k * ns + e) = vo;
+      *reinterpret_cast<d2*>(U + e) = wo;
+    }
+  } else {
+    for (int m = 0; m < NR; ++m)
+      for (int64_t f = e0 + 2 * P * m; f < e0 + 2 * P * m + 2 && f < ns; ++f) {
+        const int c = (int)(f % s);
+        double v = U[f] * ir[c], w = Y[f] * ir[c];
+        for (int jj = 0; jj < k; ++jj) {
+          const double a = V[jj * ns + f];
+          v -= a * cv[jj * s + c];
+          w -= a * cu[jj * s + c];
+        }
+        w -= v * cu[k * s + c];
+        V[k * ns + f] = v;
+        U[f] = w;
+      }
   }
 }
+template __global__ void lz_update_kernel<1>(double*, int64_t, int, double*, const double*,
+                                             const double*, const double*, const double*, int);
+template __global__ void lz_update_kernel<4>(double*, int64_t, int, double*, const double*,
+                                             const double*, const double*, const double*, int);
 
 // Normalised Rademacher probes: V[i][c] = +-1/sqrt(n), bit 63 of
 // splitmix64(seed * G + (c + c0) * H + i) (matches oracle/sparse.py).

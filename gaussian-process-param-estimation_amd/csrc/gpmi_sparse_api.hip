@@ -65,6 +65,7 @@ __global__ void lz_dots_kernel(const double*, int64_t, int, int, const double*, 
                                int64_t, int, int, double*);
 __global__ void lz_scalar_kernel(const double*, int, int, int, double*, double*, double*, double*,
                                  double*, int*, int*, double*, double*);
+template <int NR>
 __global__ void lz_update_kernel(double*, int64_t, int, double*, const double*, const double*,
                                  const double*, const double*, int);
 __global__ void rademacher_kernel(double*, int64_t, int, unsigned long long, int, double,
@@ -527,6 +528,9 @@ int lanczos_block_dcgs2(gpmi_sp* sp, double* V, double* U, double* Y, int s, int
   SP_TRY(hipMemsetAsync(H, 0, sizeof(double) * s * hsz, sp->stream));
   SP_TRY(hipMemsetAsync(dal, 0, sizeof(double) * 2 * s * steps, sp->stream));
   SP_TRY(hipMemcpyAsync(U, V, sizeof(double) * ns, hipMemcpyDeviceToDevice, sp->stream));
+  // GPMI_LZ_NR: row chunks per thread of the update pass (1 or 4)
+  const char* nenv = std::getenv("GPMI_LZ_NR");
+  const int lz_nr = nenv ? std::atoi(nenv) : 4;
   for (int k = 0; k <= steps; ++k) {
     const bool last = k == steps;
     if (!last) {
@@ -535,6 +539,8 @@ int lanczos_block_dcgs2(gpmi_sp* sp, double* V, double* U, double* Y, int s, int
     }
     const int nv = 2 * k + 2;
     for (int j0 = 0; j0 == 0 || j0 < k; j0 += LZ_JC) {
+      // (column pairs with 16-byte loads measured slower: 15.9 against 13.1 ms per
+      // cfg 5 Lanczos, at half the occupancy for the doubled accumulators)
       hipLaunchKernelGGL(lz_dots_kernel, dim3(LZ_NB), dim3(256), 0, sp->stream, V, ns, k, j0, U,
                          last ? (const double*)nullptr : Y, n, s, nv, sp->partial);
       SP_LAUNCH("lz_dots_kernel");
@@ -546,8 +552,18 @@ int lanczos_block_dcgs2(gpmi_sp* sp, double* V, double* U, double* Y, int s, int
                        cu, ir, rho, dead, inex, dal, dbe);
     SP_LAUNCH("lz_scalar_kernel");
     if (!last) {
-      hipLaunchKernelGGL(lz_update_kernel, dim3((unsigned)((ns + 511) / 512)), dim3(256), 0,
-                         sp->stream, V, ns, k, U, Y, cv, cu, ir, s);
+      if (lz_nr == 4) {
+        // four row chunks per thread sharing its two columns' coefficients: the grid's
+        // thread-pair count P with 2 P a multiple of s
+        const int64_t q = s / std::__gcd(512, s);
+        int64_t g = (ns / 2 + 1023) / 1024;
+        g = (g + q - 1) / q * q;
+        hipLaunchKernelGGL(lz_update_kernel<4>, dim3((unsigned)g), dim3(256), 0, sp->stream, V,
+                           ns, k, U, Y, cv, cu, ir, s);
+      } else {
+        hipLaunchKernelGGL(lz_update_kernel<1>, dim3((unsigned)((ns + 511) / 512)), dim3(256), 0,
+                           sp->stream, V, ns, k, U, Y, cv, cu, ir, s);
+      }
       SP_LAUNCH("lz_update_kernel");
     }
   }
