@@ -523,7 +523,10 @@ int lanczos_block_dcgs2(gpmi_sp* sp, double* V, double* U, double* Y, int s, int
   double* dbe = dal + (size_t)s * steps;
   int* dead = reinterpret_cast<int*>(dbe + (size_t)s * steps);
   int* inex = dead + s;
-  int rc = ensure_partial(sp, (size_t)LZ_NB * (2 * steps + 2) * s);
+  // row blocks of the dot partials (GPMI_LZ_NB; fixed per call: deterministic)
+  const char* benv = std::getenv("GPMI_LZ_NB");
+  const int lz_nb = benv ? std::max(64, std::min(4096, std::atoi(benv))) : LZ_NB;
+  int rc = ensure_partial(sp, (size_t)lz_nb * (2 * steps + 2) * s);
   if (rc) return rc;
   SP_TRY(hipMemsetAsync(H, 0, sizeof(double) * s * hsz, sp->stream));
   SP_TRY(hipMemsetAsync(dal, 0, sizeof(double) * 2 * s * steps, sp->stream));
@@ -541,12 +544,12 @@ int lanczos_block_dcgs2(gpmi_sp* sp, double* V, double* U, double* Y, int s, int
     for (int j0 = 0; j0 == 0 || j0 < k; j0 += LZ_JC) {
       // (column pairs with 16-byte loads measured slower: 15.9 against 13.1 ms per
       // cfg 5 Lanczos, at half the occupancy for the doubled accumulators)
-      hipLaunchKernelGGL(lz_dots_kernel, dim3(LZ_NB), dim3(256), 0, sp->stream, V, ns, k, j0, U,
+      hipLaunchKernelGGL(lz_dots_kernel, dim3(lz_nb), dim3(256), 0, sp->stream, V, ns, k, j0, U,
                          last ? (const double*)nullptr : Y, n, s, nv, sp->partial);
       SP_LAUNCH("lz_dots_kernel");
     }
     hipLaunchKernelGGL(col_dot_reduce_kernel, dim3((nv * s + 3) / 4), dim3(256), 0, sp->stream,
-                       sp->partial, LZ_NB, nv, s, d);
+                       sp->partial, lz_nb, nv, s, d);
     SP_LAUNCH("col_dot_reduce_kernel");
     hipLaunchKernelGGL(lz_scalar_kernel, dim3(1), dim3(1024), 0, sp->stream, d, k, steps, s, H, cv,
                        cu, ir, rho, dead, inex, dal, dbe);
