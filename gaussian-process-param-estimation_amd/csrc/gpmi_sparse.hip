@@ -431,7 +431,8 @@ __global__ __launch_bounds__(256) void csr_spmm_wing_kernel(
     const int64_t* __restrict__ indptr, const int* __restrict__ indices,
     const unsigned short* __restrict__ lidx, const double* __restrict__ data, int64_t n,
     const int* __restrict__ wcols, const int* __restrict__ ucount,
-    const double* __restrict__ X, double* __restrict__ Y, double eta) {
+    const double* __restrict__ X, double* __restrict__ Y, double eta,
+    double* __restrict__ pqp) {
   extern __shared__ double smem[];
   constexpr int CG = (S + 3) / 4;
   constexpr int NB = 16;
@@ -441,13 +442,13 @@ __global__ __launch_bounds__(256) void csr_spmm_wing_kernel(
   const int nr = (int)(r1 - r0);
   const int u = ucount[b];
   const int r = t >> 2, g = t & 3, c0 = g * CG;
+  double acc[CG];
+#pragma unroll
+  for (int j = 0; j < CG; ++j) acc[j] = 0.0;
   if (u == 0) {
     // window over its limits: gather straight from X
     if (r < nr) {
       const int64_t row = r0 + r;
-      double acc[CG];
-#pragma unroll
-      for (int j = 0; j < CG; ++j) acc[j] = 0.0;
       for (int64_t k = indptr[row]; k < indptr[row + 1]; ++k) {
         const double v = data[k];
         const double* xr = X + (int64_t)indices[k] * S;
@@ -455,113 +456,133 @@ __global__ __launch_bounds__(256) void csr_spmm_wing_kernel(
         for (int j = 0; j < CG; ++j)
           if (c0 + j < S) acc[j] += v * xr[c0 + j];
       }
-#pragma unroll
-      for (int j = 0; j < CG; ++j)
-        if (c0 + j < S) Y[row * S + c0 + j] = acc[j] + eta * X[row * S + c0 + j];
-    }
-    return;
-  }
-  double* win = smem;   // [u][S]
-  const int* wc = wcols + b * WIN_MAXU;
-  if (S % 2 == 0) {
-    constexpr int H = S / 2;   // 16-byte pairs per row
-    const int E2 = u * H;
-    for (int base = 0; base < E2; base += 256 * NB) {
-      d2 v[NB];
-#pragma unroll
-      for (int q = 0; q < NB; ++q) {
-        const int i = base + q * 256 + t;
-        v[q] = i < E2 ? *reinterpret_cast<const d2*>(X + (int64_t)wc[i / H] * S + 2 * (i % H))
-                      : d2{0.0, 0.0};
-      }
-#pragma unroll
-      for (int q = 0; q < NB; ++q) {
-        const int i = base + q * 256 + t;
-        if (i < E2) *reinterpret_cast<d2*>(win + 2 * i) = v[q];
-      }
     }
   } else {
-    const int E = u * S;
-    for (int base = 0; base < E; base += 256 * NB) {
-      double v[NB];
+    double* win = smem;   // [u][S]
+    const int* wc = wcols + b * WIN_MAXU;
+    if (S % 2 == 0) {
+      constexpr int H = S / 2;   // 16-byte pairs per row
+      const int E2 = u * H;
+      for (int base = 0; base < E2; base += 256 * NB) {
+        d2 v[NB];
 #pragma unroll
-      for (int q = 0; q < NB; ++q) {
-        const int i = base + q * 256 + t;
-        v[q] = i < E ? X[(int64_t)wc[i / S] * S + i % S] : 0.0;
+        for (int q = 0; q < NB; ++q) {
+          const int i = base + q * 256 + t;
+          v[q] = i < E2 ? *reinterpret_cast<const d2*>(X + (int64_t)wc[i / H] * S + 2 * (i % H))
+                        : d2{0.0, 0.0};
+        }
+#pragma unroll
+        for (int q = 0; q < NB; ++q) {
+          const int i = base + q * 256 + t;
+          if (i < E2) *reinterpret_cast<d2*>(win + 2 * i) = v[q];
+        }
       }
+    } else {
+      const int E = u * S;
+      for (int base = 0; base < E; base += 256 * NB) {
+        double v[NB];
 #pragma unroll
-      for (int q = 0; q < NB; ++q) {
-        const int i = base + q * 256 + t;
-        if (i < E) win[i] = v[q];
+        for (int q = 0; q < NB; ++q) {
+          const int i = base + q * 256 + t;
+          v[q] = i < E ? X[(int64_t)wc[i / S] * S + i % S] : 0.0;
+        }
+#pragma unroll
+        for (int q = 0; q < NB; ++q) {
+          const int i = base + q * 256 + t;
+          if (i < E) win[i] = v[q];
+        }
+      }
+    }
+    __syncthreads();
+    if (r < nr) {
+      const int64_t row = r0 + r;
+      const int64_t ka = indptr[row], kb = indptr[row + 1];
+      // U nonzeros' values and window positions loaded (global, in flight together)
+      // before their window reads and products
+      int64_t k = ka;
+      for (; k + U <= kb; k += U) {
+        double v[U];
+        int p[U];
+#pragma unroll
+        for (int q = 0; q < U; ++q) {
+          v[q] = data[k + q];
+          p[q] = (int)lidx[k + q];
+        }
+#pragma unroll
+        for (int q = 0; q < U; ++q) {
+          const double* wr = win + p[q] * S + c0;
+#pragma unroll
+          for (int j = 0; j < CG; ++j)
+            if (c0 + j < S) acc[j] += v[q] * wr[j];
+        }
+      }
+      for (; k < kb; ++k) {
+        const double v = data[k];
+        const double* wr = win + (int)lidx[k] * S + c0;
+#pragma unroll
+        for (int j = 0; j < CG; ++j)
+          if (c0 + j < S) acc[j] += v * wr[j];
       }
     }
   }
-  __syncthreads();
+  double xy[CG];
+#pragma unroll
+  for (int j = 0; j < CG; ++j) xy[j] = 0.0;
   if (r < nr) {
     const int64_t row = r0 + r;
-    const int64_t ka = indptr[row], kb = indptr[row + 1];
-    double acc[CG];
-#pragma unroll
-    for (int j = 0; j < CG; ++j) acc[j] = 0.0;
-    // U nonzeros' values and window positions loaded (global, in flight together)
-    // before their window reads and products
-    int64_t k = ka;
-    for (; k + U <= kb; k += U) {
-      double v[U];
-      int p[U];
-#pragma unroll
-      for (int q = 0; q < U; ++q) {
-        v[q] = data[k + q];
-        p[q] = (int)lidx[k + q];
-      }
-#pragma unroll
-      for (int q = 0; q < U; ++q) {
-        const double* wr = win + p[q] * S + c0;
-#pragma unroll
-        for (int j = 0; j < CG; ++j)
-          if (c0 + j < S) acc[j] += v[q] * wr[j];
-      }
-    }
-    for (; k < kb; ++k) {
-      const double v = data[k];
-      const double* wr = win + (int)lidx[k] * S + c0;
-#pragma unroll
-      for (int j = 0; j < CG; ++j)
-        if (c0 + j < S) acc[j] += v * wr[j];
-    }
 #pragma unroll
     for (int j = 0; j < CG; ++j)
-      if (c0 + j < S) Y[row * S + c0 + j] = acc[j] + eta * X[row * S + c0 + j];
+      if (c0 + j < S) {
+        const double x = X[row * S + c0 + j];
+        const double y = acc[j] + eta * x;
+        Y[row * S + c0 + j] = y;
+        xy[j] = x * y;
+      }
+  }
+  if (pqp) {
+    // the block's x . y per column (the multi-shift CG's p . q), rows summed in order:
+    // pqp[b][c]; the window's LDS is free once every thread is past its products
+    __syncthreads();
+    double* red = smem;   // [64][S]
+#pragma unroll
+    for (int j = 0; j < CG; ++j)
+      if (c0 + j < S) red[r * S + c0 + j] = xy[j];
+    __syncthreads();
+    if (t < S) {
+      double sum = 0.0;
+      for (int q = 0; q < nr; ++q) sum += red[q * S + t];
+      pqp[b * S + t] = sum;
+    }
   }
 }
 
 template __global__ void csr_spmm_wing_kernel<20, 4>(const int64_t*, const int*,
     const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
-    double*, double);
+    double*, double, double*);
 template __global__ void csr_spmm_wing_kernel<20, 8>(const int64_t*, const int*,
     const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
-    double*, double);
+    double*, double, double*);
 template __global__ void csr_spmm_wing_kernel<20, 16>(const int64_t*, const int*,
     const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
-    double*, double);
+    double*, double, double*);
 template __global__ void csr_spmm_wing_kernel<11, 4>(const int64_t*, const int*,
     const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
-    double*, double);
+    double*, double, double*);
 template __global__ void csr_spmm_wing_kernel<11, 8>(const int64_t*, const int*,
     const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
-    double*, double);
+    double*, double, double*);
 template __global__ void csr_spmm_wing_kernel<11, 16>(const int64_t*, const int*,
     const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
-    double*, double);
+    double*, double, double*);
 template __global__ void csr_spmm_wing_kernel<7, 4>(const int64_t*, const int*,
     const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
-    double*, double);
+    double*, double, double*);
 template __global__ void csr_spmm_wing_kernel<7, 8>(const int64_t*, const int*,
     const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
-    double*, double);
+    double*, double, double*);
 template __global__ void csr_spmm_wing_kernel<7, 16>(const int64_t*, const int*,
     const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
-    double*, double);
+    double*, double, double*);
 
 // partial[b][j][c] = sum over this block's rows of A_j[i][c] * B[i][c],
 // A_j = A + j * strideA, j = blockIdx.y; grid-stride over rows.

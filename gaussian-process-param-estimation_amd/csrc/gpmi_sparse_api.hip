@@ -49,7 +49,7 @@ __global__ void csr_spmm_winf_kernel(const int64_t*, const int*, const unsigned 
 template <int S, int U>
 __global__ void csr_spmm_wing_kernel(const int64_t*, const int*, const unsigned short*,
                                      const double*, int64_t, const int*, const int*,
-                                     const double*, double*, double);
+                                     const double*, double*, double, double*);
 constexpr int WING_MAX_LDS = 80 * 1024;   // two workgroups per CU
 constexpr int WIN_ROWS_HOST = 64;    // = WIN_ROWS (gpmi_sparse.hip)
 constexpr int WIN_MAXU_HOST = 1024;  // = WIN_MAXU
@@ -300,7 +300,8 @@ int spmm_kind(gpmi_sp* sp, int s, int* kind) {
   // (GPMI_SPMM_WING=0: off)
   const char* genv = std::getenv("GPMI_SPMM_WING");
   if (wmode != 0 && !(genv && std::atoi(genv) == 0) && (s == 20 || s == 11 || s == 7) &&
-      sp->win_maxu > 0 && sizeof(double) * (size_t)sp->win_maxu * s <= (size_t)WING_MAX_LDS) {
+      sp->win_maxu > 0 &&
+      sizeof(double) * (size_t)std::max(sp->win_maxu, WIN_ROWS_HOST) * s <= (size_t)WING_MAX_LDS) {
     *kind = 5;
     return 0;
   }
@@ -316,8 +317,13 @@ int spmm_kind(gpmi_sp* sp, int s, int* kind) {
   return 0;
 }
 
-int spmm(gpmi_sp* sp, const double* X, double* Y, int s, double eta, hipStream_t st = nullptr) {
+// Y = (K + eta I) X. With pqp, a kernel that can also writes the per-block partials
+// X . Y per column (pqp[block][s], the multi-shift CG's p . q) and sets *pq_blocks to
+// their count; otherwise *pq_blocks = 0 and the caller forms them.
+int spmm(gpmi_sp* sp, const double* X, double* Y, int s, double eta, hipStream_t st = nullptr,
+         double* pqp = nullptr, int* pq_blocks = nullptr) {
   if (!st) st = sp->stream;
+  if (pq_blocks) *pq_blocks = 0;
   if (sp->dK) {
     // dense: split partials of K X on fp64 MFMA, summed in split order (+ eta X)
     double* Yp = st == sp->ms_stream ? sp->dYp_ms : sp->dYp;
@@ -338,7 +344,8 @@ int spmm(gpmi_sp* sp, const double* X, double* Y, int s, double eta, hipStream_t
   int kind = 0;
   if (int rc = spmm_kind(sp, s, &kind)) return rc;
   if (kind == 5) {
-    const size_t lds = sizeof(double) * (size_t)s * (size_t)sp->win_maxu;
+    // the window, and the epilogue's [64][s] row partials of X . Y (pqp)
+    const size_t lds = sizeof(double) * (size_t)s * (size_t)std::max(sp->win_maxu, WIN_ROWS_HOST);
     // nonzeros in flight per thread (GPMI_SPMM_WUNR 4, 8 or 16; 8 measured best at
     // cfg 5, within 0.3 us of 4 at cfg 4)
     const char* uenv = std::getenv("GPMI_SPMM_WUNR");
@@ -352,8 +359,9 @@ int spmm(gpmi_sp* sp, const double* X, double* Y, int s, double eta, hipStream_t
                                 csr_spmm_wing_kernel<7, 16>);
     hipLaunchKernelGGL(kfn, dim3((unsigned)sp->win_nblk), dim3(256), lds, st, sp->indptr,
                        sp->indices, sp->win_lidx, sp->data, sp->n, sp->win_cols, sp->win_u, X, Y,
-                       eta);
+                       eta, pqp);
     SP_LAUNCH("csr_spmm_wing_kernel");
+    if (pqp && pq_blocks) *pq_blocks = (int)sp->win_nblk;
     return 0;
   }
   if (kind == 2) {
@@ -1163,8 +1171,16 @@ int gpmi_sp_msgram(gpmi_sp* sp, const double* etas, int neta, const double* rhs,
     sp->ms_ws_doubles = (size_t)5 * ns;
   }
   const int ne = s * s + s;
-  // [MS_NBLK][ne] dot partials, then [NBLK][s] p . q partials
-  const size_t pneed = (size_t)MS_RB * ne + (size_t)NBLK * s;
+  {
+    // the SpMM kernel choice builds the window (and so win_nblk) before the p . q
+    // partial rows are sized from it
+    int kind = 0;
+    if ((rc = spmm_kind(sp, s, &kind))) return rc;
+  }
+  // [MS_NBLK][ne] dot partials, then the p . q partials: [NBLK][s] (col_dot_partial)
+  // or [win_nblk][s] from the window SpMM's epilogue, and their [s] sums
+  const size_t pq_rows = std::max<size_t>(NBLK, (size_t)std::max<int64_t>(0, sp->win_nblk));
+  const size_t pneed = (size_t)MS_RB * ne + pq_rows * s + s;
   if (sp->ms_partial_doubles < pneed) {
     if (sp->ms_partial) SP_TRY(hipFree(sp->ms_partial));
     sp->ms_partial = nullptr;
@@ -1173,6 +1189,7 @@ int gpmi_sp_msgram(gpmi_sp* sp, const double* etas, int neta, const double* rhs,
   }
   double* partial = sp->ms_partial;
   double* pqpart = partial + (size_t)MS_RB * ne;
+  double* pqsum = pqpart + pq_rows * s;
   const size_t need = (size_t)6 * s + 2 * (size_t)S * s + 2 * (size_t)S * s * s + S + s + s + 1 +
                       (size_t)ne;
   if (sp->msbuf_doubles < need) {
@@ -1217,6 +1234,9 @@ int gpmi_sp_msgram(gpmi_sp* sp, const double* etas, int neta, const double* rhs,
   // extra launch costs more than it saves). GPMI_MS_RED=0 / 1 forces either.
   const char* renv = std::getenv("GPMI_MS_RED");
   const bool chip_red = renv ? std::atoi(renv) != 0 : mfma_r;
+  // p . q from the window SpMM's epilogue (GPMI_MS_PQEPI=0: col_dot_partial_kernel)
+  const char* qenv = std::getenv("GPMI_MS_PQEPI");
+  const bool pq_epi = (fused_r || mfma_r) && !(qenv && std::atoi(qenv) == 0);
   double* Rcur = Rd;     // the live residual
   double* Rnext = Rd2;
   hipStream_t str = sp->ms_stream;
@@ -1271,27 +1291,43 @@ int gpmi_sp_msgram(gpmi_sp* sp, const double* etas, int neta, const double* rhs,
       if (rc) return rc;
       if (!any) break;
     }
-    rc = spmm(sp, Pd, Qd, s, eta0, str);
+    // the window SpMM also forms the p . q block partials in its epilogue (summed
+    // across the chip below); other kernels leave them to col_dot_partial_kernel
+    int pqb = 0;
+    rc = spmm(sp, Pd, Qd, s, eta0, str, pq_epi ? pqpart : nullptr, &pqb);
     if (rc) return rc;
+    const double* pqin = pqpart;
+    int pqn = NBLK;
+    if (pqb > 0) {
+      hipLaunchKernelGGL(col_dot_reduce_kernel, dim3((s + 3) / 4), dim3(256), 0, str, pqpart, pqb,
+                         1, s, pqsum);
+      SP_LAUNCH("col_dot_reduce_kernel");
+      pqin = pqsum;
+      pqn = 1;
+    }
     double* Rout = Rcur;
     if (fused_r) {
       // p . q partials; the reduction, r update and dots in one launch (r_new to the
       // other buffer)
-      hipLaunchKernelGGL(col_dot_partial_kernel, dim3(NBLK, 1), dim3(256), 0, str, Pd,
-                         (int64_t)0, Qd, n, s, pqpart);
-      SP_LAUNCH("col_dot_partial_kernel");
+      if (pqb == 0) {
+        hipLaunchKernelGGL(col_dot_partial_kernel, dim3(NBLK, 1), dim3(256), 0, str, Pd,
+                           (int64_t)0, Qd, n, s, pqpart);
+        SP_LAUNCH("col_dot_partial_kernel");
+      }
       Rout = Rnext;
-      launch_ms_rdots(Bd, Rcur, Rout, Qd, st, pqpart, NBLK, n, s, partial, MS_NBLK, str);
+      launch_ms_rdots(Bd, Rcur, Rout, Qd, st, pqin, pqn, n, s, partial, MS_NBLK, str);
       SP_LAUNCH("ms_rdots_partial_kernel");
       std::swap(Rcur, Rnext);
     } else if (mfma_r) {
       // p . q partials, then the reduction, the r update (in place) and B^T r, r . r
       // on MFMA in one pass over b, r, q (ms_rmfma_kernel)
-      hipLaunchKernelGGL(col_dot_partial_kernel, dim3(NBLK, 1), dim3(256), 0, str, Pd,
-                         (int64_t)0, Qd, n, s, pqpart);
-      SP_LAUNCH("col_dot_partial_kernel");
+      if (pqb == 0) {
+        hipLaunchKernelGGL(col_dot_partial_kernel, dim3(NBLK, 1), dim3(256), 0, str, Pd,
+                           (int64_t)0, Qd, n, s, pqpart);
+        SP_LAUNCH("col_dot_partial_kernel");
+      }
       hipLaunchKernelGGL(ms_rmfma_kernel, dim3(MS_RB), dim3(256), 0, str, Bd, Rcur, Qd, st,
-                         pqpart, NBLK, n, s, partial);
+                         pqin, pqn, n, s, partial);
       SP_LAUNCH("ms_rmfma_kernel");
     } else {
       // more than two 4-column groups would re-read q per group in the fused form:
