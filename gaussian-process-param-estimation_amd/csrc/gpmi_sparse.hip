@@ -1329,11 +1329,21 @@ __global__ void ms_scalar_kernel(MsState st, const double* __restrict__ partial,
     const double rrn = br[s * s + c];
     const double bnew = rrn / st.rr[c];
     const double bs = bnew * (zn / z) * (zn / z);
-    for (int cp = 0; cp < s; ++cp) {
+    // every b^T p and G entry of (j, c) loaded before any store (the state arrays
+    // may alias for the compiler: one at a time, each iteration waited for its loads)
+    double bpv[MS_MAXS], gv[MS_MAXS];
+#pragma unroll
+    for (int cp = 0; cp < MS_MAXS; ++cp) {
       const int e = (j * s + cp) * s + c;
-      const double bpv = st.bp[e];
-      st.g[e] += as * bpv;
-      st.bp[e] = zn * br[cp * s + c] + bs * bpv;
+      bpv[cp] = cp < s ? st.bp[e] : 0.0;
+      gv[cp] = cp < s ? st.g[e] : 0.0;
+    }
+#pragma unroll
+    for (int cp = 0; cp < MS_MAXS; ++cp) {
+      if (cp >= s) break;
+      const int e = (j * s + cp) * s + c;
+      st.g[e] = gv[cp] + as * bpv[cp];
+      st.bp[e] = zn * br[cp * s + c] + bs * bpv[cp];
     }
     st.z_prev[j * s + c] = z;
     st.z[j * s + c] = zn;
