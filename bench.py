@@ -1040,6 +1040,10 @@ def main():
         result['lp_rel_err_vs_reference'] = lp_err
         if world == 1 and args.scaling == 'strong':
             result['batch_efficiency'] = batch_efficiency(op, X, z)
+            # (before band_nu25_check reassembles the resident K at nu = 2.5)
+            if last is not None:
+                result['dense_slq_mode'] = dense_slq_mode(D, last[:, 0], last[:, 1])
+                log('dense slq: %s' % result['dense_slq_mode'])
     lam = None
     if not args.no_band:
         ld_ref = (last[:own, 0], last[:own, 1])
@@ -1061,9 +1065,6 @@ def main():
         result['band_mode']['optimizer'] = optimizer_timing(D, X, z)
     if rank == 0 and world == 1 and not args.no_band and args.nu == 1.5:
         result['band_mode']['nu25_check'] = band_nu25_check(D, points, X, z)
-    if rank == 0 and world == 1 and args.scaling == 'strong' and last is not None:
-        result['dense_slq_mode'] = dense_slq_mode(D, last[:, 0], last[:, 1])
-        log('dense slq: %s' % result['dense_slq_mode'])
     if world == 1 and not args.no_sparse:
         # release the dense and band operators (their streams count against the
         # process's hardware queues) before the sparse configs run
