@@ -67,7 +67,10 @@ __global__ void matern_eval_kernel(const double* x, int64_t m, MaternParams P, d
 
 // Multi-shift CG Gram state (gpmi_sparse.hip, gpmi_sparse_api.hip); device pointers.
 constexpr int MS_MAXS = 16;   // RHS columns per multi-shift block
-constexpr int LZ_JC = 16;     // basis vectors per lz_dots_kernel launch (DCGS2 Lanczos)
+#ifndef GPMI_LZ_JC
+#define GPMI_LZ_JC 16
+#endif
+constexpr int LZ_JC = GPMI_LZ_JC;   // basis vectors per lz_dots_kernel launch (DCGS2 Lanczos)
 struct MsState {
   double* rr;      // [s]   r_c . r_c
   double* a;       // [s]   alpha_c of this iteration (0 once converged)
