@@ -426,22 +426,24 @@ template __global__ void csr_spmm_winf_kernel<20>(const int64_t*, const int*,
 // are read from global memory (the four threads of a row share each; U of them in
 // flight per thread), so LDS holds only the window: u S doubles, two workgroups per
 // CU up to 80 KB.
-template <int S, int U>
-__global__ __launch_bounds__(256) void csr_spmm_wing_kernel(
+template <int S, int U, int TPR>
+__global__ __launch_bounds__(64 * TPR) void csr_spmm_wing_kernel(
     const int64_t* __restrict__ indptr, const int* __restrict__ indices,
     const unsigned short* __restrict__ lidx, const double* __restrict__ data, int64_t n,
     const int* __restrict__ wcols, const int* __restrict__ ucount,
     const double* __restrict__ X, double* __restrict__ Y, double eta,
     double* __restrict__ pqp) {
   extern __shared__ double smem[];
-  constexpr int CG = (S + 3) / 4;
-  constexpr int NB = 16;
+  // TPR threads per row (4: 256-thread blocks, 8: 512), CG columns each
+  constexpr int NT = 64 * TPR;
+  constexpr int CG = (S + TPR - 1) / TPR;
+  constexpr int NB = 4096 / NT;   // loads in flight per thread while staging
   const int t = threadIdx.x;
   const int64_t b = xcd_remap(blockIdx.x, gridDim.x);
   const int64_t r0 = b * WIN_ROWS, r1 = min(r0 + WIN_ROWS, n);
   const int nr = (int)(r1 - r0);
   const int u = ucount[b];
-  const int r = t >> 2, g = t & 3, c0 = g * CG;
+  const int r = t / TPR, g = t % TPR, c0 = g * CG;
   double acc[CG];
 #pragma unroll
   for (int j = 0; j < CG; ++j) acc[j] = 0.0;
@@ -463,32 +465,32 @@ __global__ __launch_bounds__(256) void csr_spmm_wing_kernel(
     if (S % 2 == 0) {
       constexpr int H = S / 2;   // 16-byte pairs per row
       const int E2 = u * H;
-      for (int base = 0; base < E2; base += 256 * NB) {
+      for (int base = 0; base < E2; base += NT * NB) {
         d2 v[NB];
 #pragma unroll
         for (int q = 0; q < NB; ++q) {
-          const int i = base + q * 256 + t;
+          const int i = base + q * NT + t;
           v[q] = i < E2 ? *reinterpret_cast<const d2*>(X + (int64_t)wc[i / H] * S + 2 * (i % H))
                         : d2{0.0, 0.0};
         }
 #pragma unroll
         for (int q = 0; q < NB; ++q) {
-          const int i = base + q * 256 + t;
+          const int i = base + q * NT + t;
           if (i < E2) *reinterpret_cast<d2*>(win + 2 * i) = v[q];
         }
       }
     } else {
       const int E = u * S;
-      for (int base = 0; base < E; base += 256 * NB) {
+      for (int base = 0; base < E; base += NT * NB) {
         double v[NB];
 #pragma unroll
         for (int q = 0; q < NB; ++q) {
-          const int i = base + q * 256 + t;
+          const int i = base + q * NT + t;
           v[q] = i < E ? X[(int64_t)wc[i / S] * S + i % S] : 0.0;
         }
 #pragma unroll
         for (int q = 0; q < NB; ++q) {
-          const int i = base + q * 256 + t;
+          const int i = base + q * NT + t;
           if (i < E) win[i] = v[q];
         }
       }
@@ -556,31 +558,58 @@ __global__ __launch_bounds__(256) void csr_spmm_wing_kernel(
   }
 }
 
-template __global__ void csr_spmm_wing_kernel<20, 4>(const int64_t*, const int*,
+template __global__ void csr_spmm_wing_kernel<20, 4, 4>(const int64_t*, const int*,
     const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
     double*, double, double*);
-template __global__ void csr_spmm_wing_kernel<20, 8>(const int64_t*, const int*,
+template __global__ void csr_spmm_wing_kernel<20, 4, 8>(const int64_t*, const int*,
     const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
     double*, double, double*);
-template __global__ void csr_spmm_wing_kernel<20, 16>(const int64_t*, const int*,
+template __global__ void csr_spmm_wing_kernel<20, 8, 4>(const int64_t*, const int*,
     const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
     double*, double, double*);
-template __global__ void csr_spmm_wing_kernel<11, 4>(const int64_t*, const int*,
+template __global__ void csr_spmm_wing_kernel<20, 8, 8>(const int64_t*, const int*,
     const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
     double*, double, double*);
-template __global__ void csr_spmm_wing_kernel<11, 8>(const int64_t*, const int*,
+template __global__ void csr_spmm_wing_kernel<20, 16, 4>(const int64_t*, const int*,
     const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
     double*, double, double*);
-template __global__ void csr_spmm_wing_kernel<11, 16>(const int64_t*, const int*,
+template __global__ void csr_spmm_wing_kernel<20, 16, 8>(const int64_t*, const int*,
     const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
     double*, double, double*);
-template __global__ void csr_spmm_wing_kernel<7, 4>(const int64_t*, const int*,
+template __global__ void csr_spmm_wing_kernel<11, 4, 4>(const int64_t*, const int*,
     const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
     double*, double, double*);
-template __global__ void csr_spmm_wing_kernel<7, 8>(const int64_t*, const int*,
+template __global__ void csr_spmm_wing_kernel<11, 4, 8>(const int64_t*, const int*,
     const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
     double*, double, double*);
-template __global__ void csr_spmm_wing_kernel<7, 16>(const int64_t*, const int*,
+template __global__ void csr_spmm_wing_kernel<11, 8, 4>(const int64_t*, const int*,
+    const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
+    double*, double, double*);
+template __global__ void csr_spmm_wing_kernel<11, 8, 8>(const int64_t*, const int*,
+    const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
+    double*, double, double*);
+template __global__ void csr_spmm_wing_kernel<11, 16, 4>(const int64_t*, const int*,
+    const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
+    double*, double, double*);
+template __global__ void csr_spmm_wing_kernel<11, 16, 8>(const int64_t*, const int*,
+    const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
+    double*, double, double*);
+template __global__ void csr_spmm_wing_kernel<7, 4, 4>(const int64_t*, const int*,
+    const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
+    double*, double, double*);
+template __global__ void csr_spmm_wing_kernel<7, 4, 8>(const int64_t*, const int*,
+    const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
+    double*, double, double*);
+template __global__ void csr_spmm_wing_kernel<7, 8, 4>(const int64_t*, const int*,
+    const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
+    double*, double, double*);
+template __global__ void csr_spmm_wing_kernel<7, 8, 8>(const int64_t*, const int*,
+    const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
+    double*, double, double*);
+template __global__ void csr_spmm_wing_kernel<7, 16, 4>(const int64_t*, const int*,
+    const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
+    double*, double, double*);
+template __global__ void csr_spmm_wing_kernel<7, 16, 8>(const int64_t*, const int*,
     const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
     double*, double, double*);
 

@@ -46,7 +46,7 @@ template <int S>
 __global__ void csr_spmm_winf_kernel(const int64_t*, const int*, const unsigned short*,
                                      const double*, int64_t, const int*, const int*,
                                      const double*, double*, double);
-template <int S, int U>
+template <int S, int U, int TPR>
 __global__ void csr_spmm_wing_kernel(const int64_t*, const int*, const unsigned short*,
                                      const double*, int64_t, const int*, const int*,
                                      const double*, double*, double, double*);
@@ -264,15 +264,24 @@ int ensure_window(gpmi_sp* sp) {
   if (lds > 64 * 1024)
     SP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&csr_spmm_win_kernel),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  for (const void* f : {reinterpret_cast<const void*>(&csr_spmm_wing_kernel<20, 4>),
-                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<20, 8>),
-                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<20, 16>),
-                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<11, 4>),
-                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<11, 8>),
-                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<11, 16>),
-                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<7, 4>),
-                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<7, 8>),
-                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<7, 16>)})
+  for (const void* f : {reinterpret_cast<const void*>(&csr_spmm_wing_kernel<20, 4, 4>),
+                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<20, 4, 8>),
+                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<20, 8, 4>),
+                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<20, 8, 8>),
+                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<20, 16, 4>),
+                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<20, 16, 8>),
+                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<11, 4, 4>),
+                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<11, 4, 8>),
+                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<11, 8, 4>),
+                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<11, 8, 8>),
+                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<11, 16, 4>),
+                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<11, 16, 8>),
+                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<7, 4, 4>),
+                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<7, 4, 8>),
+                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<7, 8, 4>),
+                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<7, 8, 8>),
+                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<7, 16, 4>),
+                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<7, 16, 8>)})
     SP_TRY(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, WING_MAX_LDS));
   sp->win_nblk = nblk;
   sp->win_maxu = mu;
@@ -347,17 +356,26 @@ int spmm(gpmi_sp* sp, const double* X, double* Y, int s, double eta, hipStream_t
     // the window, and the epilogue's [64][s] row partials of X . Y (pqp)
     const size_t lds = sizeof(double) * (size_t)s * (size_t)std::max(sp->win_maxu, WIN_ROWS_HOST);
     // nonzeros in flight per thread (GPMI_SPMM_WUNR 4, 8 or 16; 8 measured best at
-    // cfg 5, within 0.3 us of 4 at cfg 4)
+    // cfg 5, within 0.3 us of 4 at cfg 4) and threads per row (GPMI_SPMM_WTPR 4 or 8)
     const char* uenv = std::getenv("GPMI_SPMM_WUNR");
     const int un = uenv ? std::atoi(uenv) : 8;
+    const char* tenv = std::getenv("GPMI_SPMM_WTPR");
+    const int tpr = tenv && std::atoi(tenv) == 8 ? 8 : 4;
     auto pick = [un](auto k4, auto k8, auto k16) { return un == 4 ? k4 : un == 8 ? k8 : k16; };
-    auto kfn = s == 20 ? pick(csr_spmm_wing_kernel<20, 4>, csr_spmm_wing_kernel<20, 8>,
-                              csr_spmm_wing_kernel<20, 16>)
-               : s == 11 ? pick(csr_spmm_wing_kernel<11, 4>, csr_spmm_wing_kernel<11, 8>,
-                                csr_spmm_wing_kernel<11, 16>)
-                         : pick(csr_spmm_wing_kernel<7, 4>, csr_spmm_wing_kernel<7, 8>,
-                                csr_spmm_wing_kernel<7, 16>);
-    hipLaunchKernelGGL(kfn, dim3((unsigned)sp->win_nblk), dim3(256), lds, st, sp->indptr,
+    auto kfn = tpr == 4
+        ? (s == 20 ? pick(csr_spmm_wing_kernel<20, 4, 4>, csr_spmm_wing_kernel<20, 8, 4>,
+                          csr_spmm_wing_kernel<20, 16, 4>)
+           : s == 11 ? pick(csr_spmm_wing_kernel<11, 4, 4>, csr_spmm_wing_kernel<11, 8, 4>,
+                            csr_spmm_wing_kernel<11, 16, 4>)
+                     : pick(csr_spmm_wing_kernel<7, 4, 4>, csr_spmm_wing_kernel<7, 8, 4>,
+                            csr_spmm_wing_kernel<7, 16, 4>))
+        : (s == 20 ? pick(csr_spmm_wing_kernel<20, 4, 8>, csr_spmm_wing_kernel<20, 8, 8>,
+                          csr_spmm_wing_kernel<20, 16, 8>)
+           : s == 11 ? pick(csr_spmm_wing_kernel<11, 4, 8>, csr_spmm_wing_kernel<11, 8, 8>,
+                            csr_spmm_wing_kernel<11, 16, 8>)
+                     : pick(csr_spmm_wing_kernel<7, 4, 8>, csr_spmm_wing_kernel<7, 8, 8>,
+                            csr_spmm_wing_kernel<7, 16, 8>));
+    hipLaunchKernelGGL(kfn, dim3((unsigned)sp->win_nblk), dim3(64 * tpr), lds, st, sp->indptr,
                        sp->indices, sp->win_lidx, sp->data, sp->n, sp->win_cols, sp->win_u, X, Y,
                        eta, pqp);
     SP_LAUNCH("csr_spmm_wing_kernel");
