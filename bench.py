@@ -419,6 +419,29 @@ def sparse_measure(args, config, world, rank, local, dist, torch, cpu, exact):
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     dt = max_over_ranks(dt, world, dist, torch)
+    # imate's `orthogonalize` option: this rank's probe block by the plain three-term
+    # recurrence (0, imate's default) against the full reorthogonalisation the step
+    # uses (-1), Lanczos alone, and the two logdet curves in probe standard errors
+    lz = None
+    if rank == 0:
+        plo, phi, _ = shard(nprobe, world, rank)
+        lzt = {}
+        curves = {}
+        for orth in (-1, 0):
+            op.sop.lanczos(phi - plo, steps, op.seed, probe_offset=plo, orthogonalize=orth)
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            a_, b_ = op.sop.lanczos(phi - plo, steps, op.seed, probe_offset=plo,
+                                    orthogonalize=orth)
+            lzt[orth] = (time.perf_counter() - t1) * 1e3
+            curves[orth] = n * _slq.quadrature(_slq.nodes(a_, b_), etas, numpy.log)
+        se = curves[-1].std(axis=0, ddof=1) / numpy.sqrt(curves[-1].shape[0])
+        dz = (curves[0].mean(axis=0) - curves[-1].mean(axis=0)) / se
+        lz = {'probes': phi - plo, 'steps': steps, 'full_reorth_ms': round(lzt[-1], 3),
+              'orthogonalize_0_ms': round(lzt[0], 3),
+              'logdet_diff_in_std_errors_max': round(float(numpy.max(numpy.abs(dz))), 3),
+              'note': "imate's default orthogonalize=0 (plain three-term recurrence); the "
+                      "measured step uses full reorthogonalisation (DCGS2)"}
     # SpMM roofline on a device-resident probe block (HIP events)
     s_blk = max(1, min(32, nprobe // world))
     ms = op.sop.bench_spmm(s_blk, 50)
@@ -472,6 +495,7 @@ def sparse_measure(args, config, world, rank, local, dist, torch, cpu, exact):
                                  % (alg_bytes / 1e6)},
             # the whole step against HBM: algorithmic bytes of every pass of the
             # step (sparse_step_bytes) / ms_per_step, rank 0's shard
+            'lanczos_orthogonalize': lz,
             'step_roofline': {
                 'bound': 'hbm', 'bytes_per_step': sb['total'],
                 'achieved': round(sb['total'] / step_s / 1e9, 1), 'peak': HBM_PEAK_GBS,
@@ -512,7 +536,7 @@ def sparse_modes(args, local, dist, torch):
         log('%s: %.1f evals/s' % (cfg, r['value']))
         out[cfg] = {k: r[k] for k in ('metric', 'value', 'unit', 'ms_per_step', 'steps',
                                       'warmup', 'roofline', 'step_roofline', 'cpu_baseline',
-                                      'lp_sample') if k in r}
+                                      'lp_sample', 'lanczos_orthogonalize') if k in r}
         out[cfg]['workload'] = r['config']['workload']
         out[cfg]['assembly_s'] = r['config']['assembly_s']
         for k in ('reference_check', 'speedup_vs_cpu'):

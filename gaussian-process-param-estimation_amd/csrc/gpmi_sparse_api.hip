@@ -456,9 +456,12 @@ uint64_t morton3(const int64_t (&q)[3], int d) {
 }
 
 // Lanczos of K on s probe columns starting from V0 (already in V block 0).
-// alpha/beta: host [s][steps] (column-major by probe). CGS2 reorthogonalisation.
+// alpha/beta: host [s][steps] (column-major by probe). orth < 0: CGS2 against every
+// previous vector (full reorthogonalisation); orth = 0: the plain three-term
+// recurrence (one projection on v_k after subtracting beta v_{k-1}: imate's
+// orthogonalize=0); orth > 0: CGS2 against the last orth vectors and v_k.
 int lanczos_block(gpmi_sp* sp, double* V, double* W, int s, int steps, double* h_alpha,
-                  double* h_beta) {
+                  double* h_beta, int orth = -1) {
   const int64_t ns = sp->n * s;
   // device scalars: H1, H2 [(steps+1)][MAXS] (the two CGS2 passes), norms, the
   // alpha/beta tables [s][steps], two axpby coefficient pairs and the dead flags
@@ -480,8 +483,12 @@ int lanczos_block(gpmi_sp* sp, double* V, double* W, int s, int steps, double* h
   double* na = cb + MAXS;
   double* nb = na + MAXS;
   int* dead = reinterpret_cast<int*>(nb + MAXS);
+  // one pass (orth = 0): the second pass's coefficients stay zero
+  if (orth == 0) SP_TRY(hipMemsetAsync(H2, 0, sizeof(double) * MAXS, sp->stream));
   for (int k = 0; k < steps; ++k) {
     double* Vk = V + (int64_t)k * ns;
+    const int jlo = orth < 0 ? 0 : std::max(0, k - orth);   // projection window [jlo, k]
+    const int J = k + 1 - jlo;
     int rc = spmm(sp, Vk, W, s, 0.0);
     if (rc) return rc;
     if (k > 0) {   // W -= beta_{k-1} V_{k-1}
@@ -489,19 +496,19 @@ int lanczos_block(gpmi_sp* sp, double* V, double* W, int s, int steps, double* h
                          V + (int64_t)(k - 1) * ns, W, na, nb, sp->n, s);
       SP_LAUNCH("col_axpby_kernel");
     }
-    for (int pass = 0; pass < 2; ++pass) {   // CGS2 against V_0 .. V_k
+    for (int pass = 0; pass < (orth == 0 ? 1 : 2); ++pass) {   // CGS(2) against V_jlo .. V_k
       double* H = pass == 0 ? H1 : H2;
-      rc = col_dots(sp, V, ns, k + 1, W, s, H);
+      rc = col_dots(sp, V + (int64_t)jlo * ns, ns, J, W, s, H);
       if (rc) return rc;
       hipLaunchKernelGGL(col_gs_update_kernel, dim3((unsigned)((ns + 511) / 512)), dim3(256), 0,
-                         sp->stream, W, V, ns, H, k + 1, sp->n, s);
+                         sp->stream, W, V + (int64_t)jlo * ns, ns, H, J, sp->n, s);
       SP_LAUNCH("col_gs_update_kernel");
     }
     rc = col_dots(sp, W, 0, 1, W, s, nrm);
     if (rc) return rc;
     hipLaunchKernelGGL(lanczos_scalar_kernel, dim3(1), dim3(64), 0, sp->stream,
-                       H1 + (size_t)k * s, H2 + (size_t)k * s, nrm, s, k, steps, dead, dalpha,
-                       dbeta, ca, cb, na, nb);
+                       H1 + (size_t)(k - jlo) * s, orth == 0 ? H2 : H2 + (size_t)(k - jlo) * s,
+                       nrm, s, k, steps, dead, dalpha, dbeta, ca, cb, na, nb);
     SP_LAUNCH("lanczos_scalar_kernel");
     if (k + 1 < steps) {
       // V_{k+1} = W / beta  (b = 0 -> X * 0 + 0 * Y; Y is zero-initialised below)
@@ -1016,6 +1023,11 @@ int gpmi_sp_spmm(gpmi_sp* sp, double eta, const double* X, int64_t ld, int ncol,
 
 int gpmi_sp_lanczos(gpmi_sp* sp, int nprobe, int steps, uint64_t seed, int probe_offset,
                     double* alpha, double* beta) {
+  return gpmi_sp_lanczos_ex(sp, nprobe, steps, seed, probe_offset, -1, alpha, beta);
+}
+
+int gpmi_sp_lanczos_ex(gpmi_sp* sp, int nprobe, int steps, uint64_t seed, int probe_offset,
+                       int orthogonalize, double* alpha, double* beta) {
   if (!sp) return set_error(-1006, "null handle");
   if (steps < 1 || steps > 256 || nprobe < 1)
     return set_error(-1102, "steps must be in [1, 256] and nprobe >= 1");
@@ -1035,6 +1047,13 @@ int gpmi_sp_lanczos(gpmi_sp* sp, int nprobe, int steps, uint64_t seed, int probe
       return 0;
     };
     if ((rc = probes())) return rc;
+    if (orthogonalize >= 0) {
+      // no or windowed reorthogonalisation (imate's orthogonalize = 0 / k)
+      rc = lanczos_block(sp, V, W, s, steps, alpha + (size_t)p0 * steps,
+                         beta + (size_t)p0 * steps, orthogonalize);
+      if (rc) return rc;
+      continue;
+    }
     // DCGS2 (default; GPMI_LANCZOS=cgs2 selects CGS2). A block whose rho lost
     // precision to cancellation (near an invariant subspace) is redone with CGS2.
     const char* lenv = std::getenv("GPMI_LANCZOS");

@@ -71,6 +71,8 @@ SIGNATURES = {
                                     c_double_p, c_i64]),
     'gpmi_sp_lanczos': (ctypes.c_int, [c_op_p, ctypes.c_int, ctypes.c_int, ctypes.c_uint64,
                                        ctypes.c_int, c_double_p, c_double_p]),
+    'gpmi_sp_lanczos_ex': (ctypes.c_int, [c_op_p, ctypes.c_int, ctypes.c_int, ctypes.c_uint64,
+                                          ctypes.c_int, ctypes.c_int, c_double_p, c_double_p]),
     'gpmi_sp_bench_spmm': (ctypes.c_int, [c_op_p, ctypes.c_int, ctypes.c_int, ctypes.c_double,
                                           c_double_p]),
     'gpmi_sp_cg': (ctypes.c_int, [c_op_p, ctypes.c_double, c_double_p, c_i64, ctypes.c_int,
@@ -579,12 +581,15 @@ class SparseOperator(object):
         return ('csr_spmm_kernel', 'csr_spmm_win_kernel', 'csr_spmm_winf_kernel',
                 'csr_spmm_pair_kernel', 'dense_mm_kernel', 'csr_spmm_wing_kernel')[k.value]
 
-    def lanczos(self, nprobe, steps, seed=0, probe_offset=0):
-        """-> alpha[nprobe, steps], beta[nprobe, steps] (beta = 0 ends a tridiagonal)."""
+    def lanczos(self, nprobe, steps, seed=0, probe_offset=0, orthogonalize=-1):
+        """-> alpha[nprobe, steps], beta[nprobe, steps] (beta = 0 ends a tridiagonal).
+        orthogonalize: imate's option: -1 full reorthogonalisation (DCGS2), 0 the
+        plain three-term recurrence, k > 0 against the last k vectors."""
         a = numpy.zeros((nprobe, steps))
         b = numpy.zeros((nprobe, steps))
-        check(self.lib.gpmi_sp_lanczos(self.h, int(nprobe), int(steps), int(seed),
-                                       int(probe_offset), dptr(a), dptr(b)), 'gpmi_sp_lanczos')
+        check(self.lib.gpmi_sp_lanczos_ex(self.h, int(nprobe), int(steps), int(seed),
+                                          int(probe_offset), int(orthogonalize), dptr(a),
+                                          dptr(b)), 'gpmi_sp_lanczos_ex')
         return a, b
 
     def bench_spmm(self, s, reps, eta=0.0):

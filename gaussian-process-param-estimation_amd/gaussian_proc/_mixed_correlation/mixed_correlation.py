@@ -111,6 +111,9 @@ class MixedCorrelation(object):
         self.lanczos_degree = int(opts.get('lanczos_degree', 30))
         self.seed = int(opts.get('seed', 0))
         self.cg_rtol = float(opts.get('cg_rtol', 1e-6))
+        # imate's Lanczos option (-1 full reorthogonalisation, this build's default;
+        # 0 the plain three-term recurrence, imate's default; k > 0 the last k vectors)
+        self.orthogonalize = int(opts.get('orthogonalize', -1))
         self._nodes = None
 
     def _build_interpolant(self):
@@ -240,7 +243,8 @@ class MixedCorrelation(object):
     def slq_nodes(self):
         """Ritz nodes of every probe (computed once; eta-independent)."""
         if self._nodes is None:
-            a, b = self.sop.lanczos(self.num_samples, self.lanczos_degree, self.seed)
+            a, b = self.sop.lanczos(self.num_samples, self.lanczos_degree, self.seed,
+                                    orthogonalize=self.orthogonalize)
             self._nodes = _slq.nodes(a, b)
         return self._nodes
 

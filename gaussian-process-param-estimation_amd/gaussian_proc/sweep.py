@@ -138,7 +138,8 @@ def slq_sweep(K_mixed, etas, group=None):
     local[:, nq] = numpy.inf
     if hi > lo:
         a, b = K_mixed.sop.lanczos(hi - lo, K_mixed.lanczos_degree, K_mixed.seed,
-                                   probe_offset=lo)
+                                   probe_offset=lo,
+                                   orthogonalize=getattr(K_mixed, 'orthogonalize', -1))
         nodes = _slq.nodes(a, b)
         q = numpy.empty((hi - lo, len(names), etas.size))
         for f, name in enumerate(names):

@@ -180,6 +180,13 @@ int gpmi_sp_spmm(gpmi_sp* sp, double eta, const double* X, int64_t ld, int ncol,
  * padded with zeros (beta = 0 marks the end of its tridiagonal). */
 int gpmi_sp_lanczos(gpmi_sp* sp, int nprobe, int steps, uint64_t seed, int probe_offset,
                     double* alpha, double* beta);
+/* The same with imate's `orthogonalize` option: -1 full reorthogonalisation (as
+ * gpmi_sp_lanczos), 0 the plain three-term recurrence (imate's default), k > 0
+ * CGS2 against the last k vectors. Replaces the Lanczos inside imate.logdet /
+ * traceinv(method='slq', orthogonalize=...) (mixed_correlation.py:138-143,
+ * 204-209,263-268 pass imate_options through). */
+int gpmi_sp_lanczos_ex(gpmi_sp* sp, int nprobe, int steps, uint64_t seed, int probe_offset,
+                       int orthogonalize, double* alpha, double* beta);
 
 /* Blocked CG for (K + eta I) X = RHS, per-column stop ||r|| <= rtol ||b||. */
 int gpmi_sp_cg(gpmi_sp* sp, double eta, const double* rhs, int64_t ld, int nrhs, double rtol,

@@ -61,13 +61,13 @@ class _FakeSparse(object):
         self.K = K
         self.steps = steps
 
-    def lanczos(self, nprobe, steps, seed=0, probe_offset=0):
+    def lanczos(self, nprobe, steps, seed=0, probe_offset=0, orthogonalize=-1):
         from oracle import sparse as osp
         P = osp.rademacher_probes(self.K.shape[0], probe_offset + nprobe, seed)[:, probe_offset:]
         a = numpy.zeros((nprobe, steps))
         b = numpy.zeros((nprobe, steps))
         for p in range(nprobe):
-            ao, bo = osp.lanczos(self.K, P[:, p], steps)
+            ao, bo = osp.lanczos(self.K, P[:, p], steps, reorth=orthogonalize != 0)
             a[p, :ao.size] = ao
             b[p, :bo.size] = bo
         return a, b

@@ -181,6 +181,43 @@ def test_lanczos_and_slq_match_oracle_same_probes(gp):
         assert rel(est, ref[what]) < 1e-9, what
 
 
+def test_lanczos_without_reorthogonalisation_matches_oracle(gp):
+    """imate's orthogonalize option: 0 (imate's default) is the plain three-term
+    recurrence, against the oracle's (oracle.sparse.lanczos reorth=False) with the
+    same probes: alpha / beta <= 1e-9 over 12 steps (before the recurrence loses
+    orthogonality the two agree to rounding; later steps amplify the rounding
+    differences, so the SLQ sums are compared at 1e-6); a window of 3 previous
+    vectors lies between the two; -1 is the full DCGS2 path."""
+    from gaussian_proc import _hip, _slq
+    from gaussian_proc._mixed_correlation import MixedCorrelation
+    _, K = _small_sparse()
+    n = K.shape[0]
+    sop = _hip.SparseOperator.from_csr(K)
+    nprobe, seed = 6, 11
+    P = osp.rademacher_probes(n, nprobe, seed)
+    a, b = sop.lanczos(nprobe, 12, seed, orthogonalize=0)
+    for p in range(nprobe):
+        ao, bo = osp.lanczos(K, P[:, p], 12, reorth=False)
+        k = ao.size
+        assert rel(a[p, :k], ao) < 1e-9
+        assert rel(b[p, :k - 1], bo) < 1e-9
+    steps = 25
+    a0, b0 = sop.lanczos(nprobe, steps, seed, orthogonalize=0)
+    ref = osp.slq(K, [2.5, 10.0], P, steps, reorth=False)
+    est = n * _slq.quadrature(_slq.nodes(a0, b0), [2.5, 10.0], numpy.log).mean(axis=0)
+    assert rel(est, ref['logdet']) < 1e-6
+    af, bf = sop.lanczos(nprobe, steps, seed)
+    aw, bw = sop.lanczos(nprobe, steps, seed, orthogonalize=3)
+    full = n * _slq.quadrature(_slq.nodes(af, bf), [2.5, 10.0], numpy.log).mean(axis=0)
+    win = n * _slq.quadrature(_slq.nodes(aw, bw), [2.5, 10.0], numpy.log).mean(axis=0)
+    # every variant estimates the same logdet (Monte-Carlo error of 6 probes >> these)
+    assert rel(win, full) < 1e-3 and rel(est, full) < 1e-3
+    op = MixedCorrelation(K, imate_method='slq',
+                          imate_options={'num_samples': nprobe, 'lanczos_degree': steps,
+                                         'seed': seed, 'orthogonalize': 0})
+    assert op.logdet(2.5) == pytest.approx(est[0], rel=1e-12)
+
+
 def test_sparse_operator_slq_vs_exact(gp):
     from gaussian_proc._mixed_correlation import MixedCorrelation
     _, K = _small_sparse()
