@@ -114,6 +114,22 @@ class MixedCorrelation(object):
         # imate's Lanczos option (-1 full reorthogonalisation, this build's default;
         # 0 the plain three-term recurrence, imate's default; k > 0 the last k vectors)
         self.orthogonalize = int(opts.get('orthogonalize', -1))
+        # imate's adaptive sample count (opt-in: any of its error options without
+        # 'num_samples'): probes are added until the confidence-interval half width
+        # z sigma / sqrt(k) of the estimate meets max(error_atol, error_rtol |mean|),
+        # between min_num_samples and max_num_samples (imate's defaults 10, 50, 1e-2,
+        # 0.95). Counter-based probes: the adaptive set is a prefix of the fixed one.
+        self._adaptive = 'num_samples' not in opts and any(
+            k in opts for k in ('min_num_samples', 'error_rtol', 'error_atol',
+                                'confidence_level'))
+        if self._adaptive:
+            self.min_num_samples = int(opts.get('min_num_samples', 10))
+            self.max_num_samples = max(self.min_num_samples,
+                                       int(opts.get('max_num_samples', 50)))
+            self.error_rtol = float(opts.get('error_rtol', 1e-2) or 0.0)
+            self.error_atol = float(opts.get('error_atol', 0.0) or 0.0)
+            self.confidence_level = float(opts.get('confidence_level', 0.95))
+            self.num_samples = self.min_num_samples
         self._nodes = None
 
     def _build_interpolant(self):
@@ -250,8 +266,25 @@ class MixedCorrelation(object):
 
     def _slq(self, eta, what):
         fn = _slq.FUNCS[what] if isinstance(what, str) else what
-        q = _slq.quadrature(self.slq_nodes(), [eta], fn)
-        return float(self.n * q[:, 0].mean())
+        nodes = self.slq_nodes()
+        q = self.n * _slq.quadrature(nodes, [eta], fn)[:, 0]
+        if self._adaptive:
+            import scipy.stats
+            zc = float(scipy.stats.norm.ppf(0.5 * (1.0 + self.confidence_level)))
+            while True:
+                k = q.size
+                err = zc * q.std(ddof=1) / numpy.sqrt(k) if k > 1 else numpy.inf
+                if err <= max(self.error_atol, self.error_rtol * abs(q.mean())) or \
+                        k >= self.max_num_samples:
+                    break
+                extra = min(self.max_num_samples - k, max(1, self.min_num_samples))
+                a, b = self.sop.lanczos(extra, self.lanczos_degree, self.seed, probe_offset=k,
+                                        orthogonalize=self.orthogonalize)
+                more = _slq.nodes(a, b)
+                nodes.extend(more)
+                self.num_samples = len(nodes)
+                q = numpy.concatenate([q, self.n * _slq.quadrature(more, [eta], fn)[:, 0]])
+        return float(q.mean())
 
     def _sparse_traces(self):
         if self._trace_cache is None:

@@ -218,6 +218,34 @@ def test_lanczos_without_reorthogonalisation_matches_oracle(gp):
     assert op.logdet(2.5) == pytest.approx(est[0], rel=1e-12)
 
 
+def test_slq_adaptive_sample_count(gp):
+    """imate's adaptive sampling (min_num_samples / max_num_samples / error_rtol /
+    confidence_level): probes are added until the confidence half width meets the
+    tolerance; the estimate equals the fixed-count one at the count it stopped at
+    (counter-based probes: a prefix of the same probe set)."""
+    import scipy.stats
+    from gaussian_proc._mixed_correlation import MixedCorrelation
+    _, K = _small_sparse()
+    opts = {'min_num_samples': 4, 'max_num_samples': 40, 'error_rtol': 2e-3,
+            'lanczos_degree': 25, 'seed': 5}
+    op = MixedCorrelation(K, imate_method='slq', imate_options=opts)
+    v = op.logdet(2.5)
+    k = op.num_samples
+    assert 4 <= k <= 40
+    fixed = MixedCorrelation(K, imate_method='slq',
+                             imate_options={'num_samples': k, 'lanczos_degree': 25, 'seed': 5})
+    assert v == pytest.approx(fixed.logdet(2.5), rel=1e-12)
+    q = numpy.array([K.shape[0] * numpy.sum(w * numpy.log(t + 2.5)) for t, w in op.slq_nodes()])
+    half = scipy.stats.norm.ppf(0.975) * q.std(ddof=1) / numpy.sqrt(q.size)
+    assert k == 40 or half <= 2e-3 * abs(q.mean())
+    # a looser tolerance stops at the minimum
+    op2 = MixedCorrelation(K, imate_method='slq',
+                           imate_options={'min_num_samples': 4, 'error_rtol': 0.5,
+                                          'lanczos_degree': 25})
+    op2.logdet(2.5)
+    assert op2.num_samples == 4
+
+
 def test_sparse_operator_slq_vs_exact(gp):
     from gaussian_proc._mixed_correlation import MixedCorrelation
     _, K = _small_sparse()
