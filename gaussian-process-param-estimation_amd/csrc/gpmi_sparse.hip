@@ -1053,7 +1053,9 @@ __global__ __launch_bounds__(256) void rademacher_kernel(double* __restrict__ V,
 //
 // Scalar state (device, double): see MsState below; one column c per CG.
 // ---------------------------------------------------------------------------
-// partial[blk][e]: e = c' * S + c < S*S -> sum_i B[i][c'] R[i][c]; e = S*S + c -> R_c . R_c.
+// partial[blk][e]: e = c' * S + c < SA*S -> sum_i B[i][c'] R[i][c]; e = SA*S + c -> R_c . R_c
+// (B: [n][SA], the dot columns; R: [n][S], the right-hand sides: SA >= S when the
+// RHS columns are a shard of B's).
 // One thread per row (grid-stride), the row's S values of R in registers;
 // blockIdx.y selects four B columns c' (group 0 also forms R.R), so a thread
 // holds at most 4*S + S accumulators. Block sums: wave butterflies, then the
@@ -1061,9 +1063,9 @@ __global__ __launch_bounds__(256) void rademacher_kernel(double* __restrict__ V,
 template <int S>
 __global__ __launch_bounds__(256) void ms_dots_partial_kernel(const double* __restrict__ B,
                                                               const double* __restrict__ R,
-                                                              int64_t n,
+                                                              int64_t n, int SA,
                                                               double* __restrict__ partial) {
-  constexpr int NE = S * S + S;
+  const int NE = SA * S + S;
   __shared__ double red[4][4 * S + S];
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int c0 = blockIdx.y * 4;
@@ -1079,7 +1081,7 @@ __global__ __launch_bounds__(256) void ms_dots_partial_kernel(const double* __re
 #pragma unroll
     for (int c = 0; c < S; ++c) r[c] = R[i * S + c];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) b[q] = (c0 + q < S) ? B[i * S + c0 + q] : 0.0;
+    for (int q = 0; q < 4; ++q) b[q] = (c0 + q < SA) ? B[i * SA + c0 + q] : 0.0;
 #pragma unroll
     for (int q = 0; q < 4; ++q)
 #pragma unroll
@@ -1106,20 +1108,23 @@ __global__ __launch_bounds__(256) void ms_dots_partial_kernel(const double* __re
     const double v = (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]);
     if (t < 4 * S) {
       const int q = t / S, c = t - q * S;
-      if (c0 + q < S) partial[(int64_t)blockIdx.x * NE + (c0 + q) * S + c] = v;
+      if (c0 + q < SA) partial[(int64_t)blockIdx.x * NE + (c0 + q) * S + c] = v;
     } else if (blockIdx.y == 0) {
-      partial[(int64_t)blockIdx.x * NE + S * S + (t - 4 * S)] = v;
+      partial[(int64_t)blockIdx.x * NE + SA * S + (t - 4 * S)] = v;
     }
   }
 }
 
 // Host-side dispatch over the instantiated widths.
 void launch_ms_dots(const double* B, const double* R, int64_t n, int s, double* partial,
-                    int nblk, hipStream_t st) {
-  const dim3 grid(nblk, (s + 3) / 4), blk(256);
+                    int nblk, hipStream_t st, int sa) {
+  if (sa <= 0) sa = s;
+  const dim3 grid(nblk, (sa + 3) / 4), blk(256);
   switch (s) {
 #define MS_CASE(k) \
-  case k: hipLaunchKernelGGL(ms_dots_partial_kernel<k>, grid, blk, 0, st, B, R, n, partial); break;
+  case k:                                                                                   \
+    hipLaunchKernelGGL(ms_dots_partial_kernel<k>, grid, blk, 0, st, B, R, n, sa, partial);    \
+    break;
     MS_CASE(1) MS_CASE(2) MS_CASE(3) MS_CASE(4) MS_CASE(5) MS_CASE(6) MS_CASE(7) MS_CASE(8)
     MS_CASE(9) MS_CASE(10) MS_CASE(11) MS_CASE(12) MS_CASE(13) MS_CASE(14) MS_CASE(15)
     MS_CASE(16)
@@ -1140,8 +1145,8 @@ template <int S>
 __global__ __launch_bounds__(256) void ms_rdots_partial_kernel(
     const double* __restrict__ B, const double* __restrict__ R, double* __restrict__ Rn,
     const double* __restrict__ Q, MsState st, const double* __restrict__ pqpart, int pq_nblk,
-    int64_t n, double* __restrict__ partial) {
-  constexpr int NE = S * S + S;
+    int64_t n, int SA, double* __restrict__ partial) {
+  const int NE = SA * S + S;
   __shared__ double red[4][4 * S + S];
   __shared__ double sa[S];
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
@@ -1175,7 +1180,7 @@ __global__ __launch_bounds__(256) void ms_rdots_partial_kernel(
       for (int c = 0; c < S; ++c) Rn[i * S + c] = r[c];
     }
 #pragma unroll
-    for (int q = 0; q < 4; ++q) b[q] = (c0 + q < S) ? B[i * S + c0 + q] : 0.0;
+    for (int q = 0; q < 4; ++q) b[q] = (c0 + q < SA) ? B[i * SA + c0 + q] : 0.0;
 #pragma unroll
     for (int q = 0; q < 4; ++q)
 #pragma unroll
@@ -1202,22 +1207,23 @@ __global__ __launch_bounds__(256) void ms_rdots_partial_kernel(
     const double v = (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]);
     if (t < 4 * S) {
       const int q = t / S, c = t - q * S;
-      if (c0 + q < S) partial[(int64_t)blockIdx.x * NE + (c0 + q) * S + c] = v;
+      if (c0 + q < SA) partial[(int64_t)blockIdx.x * NE + (c0 + q) * S + c] = v;
     } else if (blockIdx.y == 0) {
-      partial[(int64_t)blockIdx.x * NE + S * S + (t - 4 * S)] = v;
+      partial[(int64_t)blockIdx.x * NE + SA * S + (t - 4 * S)] = v;
     }
   }
 }
 
 void launch_ms_rdots(const double* B, const double* R, double* Rn, const double* Q,
                      const MsState& st, const double* pqpart, int pq_nblk, int64_t n, int s,
-                     double* partial, int nblk, hipStream_t stream) {
-  const dim3 grid(nblk, (s + 3) / 4), blk(256);
+                     double* partial, int nblk, hipStream_t stream, int sa) {
+  if (sa <= 0) sa = s;
+  const dim3 grid(nblk, (sa + 3) / 4), blk(256);
   switch (s) {
 #define MS_CASE(k)                                                                          \
   case k:                                                                                   \
     hipLaunchKernelGGL(ms_rdots_partial_kernel<k>, grid, blk, 0, stream, B, R, Rn, Q, st,     \
-                       pqpart, pq_nblk, n, partial);                                        \
+                       pqpart, pq_nblk, n, sa, partial);                                    \
     break;
     MS_CASE(1) MS_CASE(2) MS_CASE(3) MS_CASE(4) MS_CASE(5) MS_CASE(6) MS_CASE(7) MS_CASE(8)
     MS_CASE(9) MS_CASE(10) MS_CASE(11) MS_CASE(12) MS_CASE(13) MS_CASE(14) MS_CASE(15)
@@ -1243,7 +1249,8 @@ __global__ __launch_bounds__(256) void ms_rmfma_kernel(const double* __restrict_
                                                        const double* __restrict__ Q, MsState st,
                                                        const double* __restrict__ pqpart,
                                                        int pq_nblk, int64_t n, int s,
-                                                       double* __restrict__ partial) {
+                                                       int nb, double* __restrict__ partial) {
+  // B: [n][nb] (nb >= s: the RHS columns R may be a shard of B's), R, Q: [n][s]
   __shared__ double sa[16];
   __shared__ double red[4][16 * 16 + 16];
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
@@ -1261,7 +1268,7 @@ __global__ __launch_bounds__(256) void ms_rmfma_kernel(const double* __restrict_
   }
   __syncthreads();
   const int c = lane & 15, rq = lane >> 4;
-  const bool on = c < s;
+  const bool on = c < s, onb = c < nb;
   const double a = on ? sa[c] : 0.0;
   d4 acc = {0.0, 0.0, 0.0, 0.0};
   double rr = 0.0;
@@ -1272,9 +1279,10 @@ __global__ __launch_bounds__(256) void ms_rmfma_kernel(const double* __restrict_
   for (int64_t base = (int64_t)blockIdx.x * 16 + wv * 4; base < n; base += 2 * stride) {
     const int64_t i0 = base + rq, i1 = base + stride + rq;
     const bool v0 = on && i0 < n, v1 = on && i1 < n;
+    const bool w0 = onb && i0 < n, w1 = onb && i1 < n;
     const int64_t e0 = i0 * s + c, e1 = i1 * s + c;
-    const double b0 = v0 ? B[e0] : 0.0, r0 = v0 ? R[e0] : 0.0, q0 = v0 ? Q[e0] : 0.0;
-    const double b1 = v1 ? B[e1] : 0.0, r1 = v1 ? R[e1] : 0.0, q1 = v1 ? Q[e1] : 0.0;
+    const double b0 = w0 ? B[i0 * nb + c] : 0.0, r0 = v0 ? R[e0] : 0.0, q0 = v0 ? Q[e0] : 0.0;
+    const double b1 = w1 ? B[i1 * nb + c] : 0.0, r1 = v1 ? R[e1] : 0.0, q1 = v1 ? Q[e1] : 0.0;
     const double n0 = r0 - a * q0, n1 = r1 - a * q1;
     if (v0) R[e0] = n0;
     if (v1) R[e1] = n1;
@@ -1292,14 +1300,14 @@ __global__ __launch_bounds__(256) void ms_rmfma_kernel(const double* __restrict_
   rs += __shfl_down(rs, 32);
   if (rq == 0) red[wv][256 + c] = rs;
   __syncthreads();
-  const int ne = s * s + s;
+  const int ne = nb * s + s;
   for (int e = t; e < ne; e += 256) {
     int idx;
-    if (e < s * s) {
+    if (e < nb * s) {
       const int cp = e / s, cc = e - cp * s;
       idx = cp * 16 + cc;
     } else {
-      idx = 256 + (e - s * s);
+      idx = 256 + (e - nb * s);
     }
     partial[(int64_t)blockIdx.x * ne + e] =
         (red[0][idx] + red[1][idx]) + (red[2][idx] + red[3][idx]);
@@ -1331,10 +1339,11 @@ __global__ __launch_bounds__(256) void ms_r_update_kernel(double* __restrict__ R
 // reduced from the partials (fixed order; nblk == 0: reduced beforehand), advance zeta, accumulate G, update
 // b^T p and the base beta; a column stops when sqrt(rr) <= rtol ||b||.
 __global__ void ms_scalar_kernel(MsState st, const double* __restrict__ partial, int nblk,
-                                 const double* __restrict__ dshift, int S, int s, double rtol2,
-                                 double* __restrict__ beta_out) {
+                                 const double* __restrict__ dshift, int S, int s, int nb,
+                                 double rtol2, double* __restrict__ beta_out) {
+  // nb: the dot columns of B (the bp / G rows c' < nb; nb >= s, the RHS columns)
   __shared__ double br[MS_MAXS * MS_MAXS + MS_MAXS];
-  const int ne = s * s + s;
+  const int ne = nb * s + s;
   if (nblk > 0) {
     const int nw = blockDim.x >> 6, wv = threadIdx.x >> 6;
     for (int e = wv; e < ne; e += nw) {
@@ -1355,7 +1364,7 @@ __global__ void ms_scalar_kernel(MsState st, const double* __restrict__ partial,
     const double d = dshift[j];
     const double zn = z * zp * ap / (a * bo * (zp - z) + zp * ap * (1.0 + d * a));
     const double as = a * zn / z;
-    const double rrn = br[s * s + c];
+    const double rrn = br[nb * s + c];
     const double bnew = rrn / st.rr[c];
     const double bs = bnew * (zn / z) * (zn / z);
     // every b^T p and G entry of (j, c) loaded before any store (the state arrays
@@ -1363,14 +1372,14 @@ __global__ void ms_scalar_kernel(MsState st, const double* __restrict__ partial,
     double bpv[MS_MAXS], gv[MS_MAXS];
 #pragma unroll
     for (int cp = 0; cp < MS_MAXS; ++cp) {
-      const int e = (j * s + cp) * s + c;
-      bpv[cp] = cp < s ? st.bp[e] : 0.0;
-      gv[cp] = cp < s ? st.g[e] : 0.0;
+      const int e = (j * nb + cp) * s + c;
+      bpv[cp] = cp < nb ? st.bp[e] : 0.0;
+      gv[cp] = cp < nb ? st.g[e] : 0.0;
     }
 #pragma unroll
     for (int cp = 0; cp < MS_MAXS; ++cp) {
-      if (cp >= s) break;
-      const int e = (j * s + cp) * s + c;
+      if (cp >= nb) break;
+      const int e = (j * nb + cp) * s + c;
       st.g[e] = gv[cp] + as * bpv[cp];
       st.bp[e] = zn * br[cp * s + c] + bs * bpv[cp];
     }
@@ -1379,7 +1388,7 @@ __global__ void ms_scalar_kernel(MsState st, const double* __restrict__ partial,
   }
   __syncthreads();
   if (t < s && st.active[t]) {
-    const double rrn = br[s * s + t];
+    const double rrn = br[nb * s + t];
     const double bnew = rrn / st.rr[t];
     st.a_prev[t] = st.a[t];
     st.beta[t] = bnew;
@@ -1403,9 +1412,9 @@ __global__ __launch_bounds__(256) void ms_p_update_kernel(double* __restrict__ P
 
 // Initial scalar state from BR0 = B^T b (= b . p_0 for every shift) and ||b||^2.
 __global__ void ms_init_kernel(MsState st, const double* __restrict__ partial, int nblk, int S,
-                               int s) {
+                               int s, int nb) {
   __shared__ double br[MS_MAXS * MS_MAXS + MS_MAXS];
-  const int ne = s * s + s;
+  const int ne = nb * s + s;
   {
     const int nw = blockDim.x >> 6, wv = threadIdx.x >> 6;
     for (int e = wv; e < ne; e += nw) {
@@ -1419,19 +1428,19 @@ __global__ void ms_init_kernel(MsState st, const double* __restrict__ partial, i
   if (j < S) {
     st.z[j * s + c] = 1.0;
     st.z_prev[j * s + c] = 1.0;
-    for (int cp = 0; cp < s; ++cp) {
-      const int e = (j * s + cp) * s + c;
+    for (int cp = 0; cp < nb; ++cp) {
+      const int e = (j * nb + cp) * s + c;
       st.bp[e] = br[cp * s + c];
       st.g[e] = 0.0;
     }
   }
   if (t < s) {
-    st.rr[t] = br[s * s + t];
-    st.bn2[t] = br[s * s + t];
+    st.rr[t] = br[nb * s + t];
+    st.bn2[t] = br[nb * s + t];
     st.a[t] = 0.0;
     st.a_prev[t] = 1.0;
     st.beta[t] = 0.0;
-    st.active[t] = br[s * s + t] > 0.0 ? 1 : 0;
+    st.active[t] = br[nb * s + t] > 0.0 ? 1 : 0;
   }
   if (t == 0) st.flags[0] = 0;
 }

@@ -76,19 +76,19 @@ __global__ void lanczos_scalar_kernel(const double*, const double*, const double
                                       int*, double*, double*, double*, double*, double*,
                                       double*);
 void launch_ms_dots(const double* B, const double* R, int64_t n, int s, double* partial, int nblk,
-                    hipStream_t st);
+                    hipStream_t st, int sa);
 __global__ void rows_gather_kernel(const double*, int, const int*, int64_t, int, double*);
 __global__ void ms_rmfma_kernel(const double*, double*, const double*, MsState, const double*, int,
-                                int64_t, int, double*);
+                                int64_t, int, int, double*);
 __global__ void ms_r_update_kernel(double*, const double*, MsState, const double*, int64_t, int);
 void launch_ms_rdots(const double* B, const double* R, double* Rn, const double* Q,
                      const MsState& st, const double* pqpart, int pq_nblk, int64_t n, int s,
-                     double* partial, int nblk, hipStream_t stream);
-__global__ void ms_scalar_kernel(MsState, const double*, int, const double*, int, int, double,
-                                 double*);
+                     double* partial, int nblk, hipStream_t stream, int sa);
+__global__ void ms_scalar_kernel(MsState, const double*, int, const double*, int, int, int,
+                                 double, double*);
 __global__ void ms_p_update_kernel(double*, const double*, const double*, const int*, int64_t,
                                    int);
-__global__ void ms_init_kernel(MsState, const double*, int, int, int);
+__global__ void ms_init_kernel(MsState, const double*, int, int, int, int);
 template <int CT>
 __global__ void dense_mm_kernel(const double*, int64_t, int64_t, const double*, int, int, double*);
 __global__ void dense_mm_reduce_kernel(const double*, int, int64_t, const double*, double, double*);
@@ -1172,11 +1172,19 @@ int gpmi_sp_cg(gpmi_sp* sp, double eta, const double* rhs, int64_t ld, int nrhs,
   return 0;
 }
 
-int gpmi_sp_msgram(gpmi_sp* sp, const double* etas, int neta, const double* rhs, int64_t ld,
-                   int nrhs, double rtol, int maxiter, double* G, int* iterations) {
+// Multi-shift CG Gram blocks for the right-hand sides B[:, c_lo:c_hi] of the nb-column
+// host block B (every eta): G[j][a][c] = b_a^T (K + eta_j I)^-1 b_{c_lo + c}, a < nb
+// (the dots run over all of B, so a shard of columns gives complete G columns).
+static int msgram_impl(gpmi_sp* sp, const double* etas, int neta, const double* rhs,
+                       int64_t ld, int nrhs, int c_lo, int c_hi, double rtol, int maxiter,
+                       double* G, int* iterations) {
   if (!sp) return set_error(-1006, "null handle");
-  if (neta < 1 || nrhs < 1 || nrhs > MS_MAXS || neta * nrhs > 1024)
-    return set_error(-1104, "msgram: need 1 <= nrhs <= 16 and neta * nrhs <= 1024");
+  if (neta < 1 || nrhs < 1 || nrhs > MS_MAXS || c_lo < 0 || c_hi > nrhs || c_lo >= c_hi ||
+      neta * (c_hi - c_lo) > 1024)
+    return set_error(-1104, "msgram: need 1 <= nrhs <= 16, 0 <= c_lo < c_hi <= nrhs and "
+                            "neta * (c_hi - c_lo) <= 1024");
+  const int nsub = c_hi - c_lo;
+  const bool full = nsub == nrhs;
   Guard g(sp->device);
   const int64_t n = sp->n;
   const int S = neta;
@@ -1187,27 +1195,32 @@ int gpmi_sp_msgram(gpmi_sp* sp, const double* etas, int neta, const double* rhs,
   // zero column (an inactive CG column from the start: ||b|| = 0) so that the
   // column-pair gather runs; measured slower at cfg 5 (s = 11 gather 119 us, s = 12
   // pair 161 us per launch), so off by default
-  int s = nrhs;
+  int s = nsub;
   {
     int kind = 0;
     int rc0 = spmm_kind(sp, s, &kind);
     if (rc0) return rc0;
     const char* penv = std::getenv("GPMI_MSGRAM_PAD");
-    if (kind == 0 && (s & 1) && s + 1 <= MS_MAXS && S * (s + 1) <= 1024 && penv &&
+    if (full && kind == 0 && (s & 1) && s + 1 <= MS_MAXS && S * (s + 1) <= 1024 && penv &&
         std::atoi(penv) == 1)
       ++s;
   }
+  // the dot columns: all of B (with the padding column when the full block is padded)
+  const int nbd = full ? s : nrhs;
+  const int64_t nsb = n * nbd;
   if (!sp->ms_stream) SP_TRY(hipStreamCreateWithFlags(&sp->ms_stream, hipStreamNonBlocking));
   const int64_t ns = n * s;
   const double eta0 = *std::min_element(etas, etas + neta);
   int rc = 0;
-  if (sp->ms_ws_doubles < (size_t)5 * ns) {
+  // B [n][nbd], its host staging [n][nrhs], and R, P, Q, R' [n][s]
+  const size_t wsn = (size_t)nsb + (size_t)n * nrhs + (size_t)4 * ns;
+  if (sp->ms_ws_doubles < wsn) {
     if (sp->ms_ws) SP_TRY(hipFree(sp->ms_ws));
     sp->ms_ws = nullptr;
-    SP_TRY(hipMalloc(&sp->ms_ws, sizeof(double) * 5 * ns));
-    sp->ms_ws_doubles = (size_t)5 * ns;
+    SP_TRY(hipMalloc(&sp->ms_ws, sizeof(double) * wsn));
+    sp->ms_ws_doubles = wsn;
   }
-  const int ne = s * s + s;
+  const int ne = nbd * s + s;
   {
     // the SpMM kernel choice builds the window (and so win_nblk) before the p . q
     // partial rows are sized from it
@@ -1227,8 +1240,8 @@ int gpmi_sp_msgram(gpmi_sp* sp, const double* etas, int neta, const double* rhs,
   double* partial = sp->ms_partial;
   double* pqpart = partial + (size_t)MS_RB * ne;
   double* pqsum = pqpart + pq_rows * s;
-  const size_t need = (size_t)6 * s + 2 * (size_t)S * s + 2 * (size_t)S * s * s + S + s + s + 1 +
-                      (size_t)ne;
+  const size_t need = (size_t)6 * s + 2 * (size_t)S * s + 2 * (size_t)S * nbd * s + S + s + s +
+                      1 + (size_t)ne;
   if (sp->msbuf_doubles < need) {
     if (sp->msbuf) SP_TRY(hipFree(sp->msbuf));
     sp->msbuf = nullptr;
@@ -1245,8 +1258,8 @@ int gpmi_sp_msgram(gpmi_sp* sp, const double* etas, int neta, const double* rhs,
   double* pqd = q; q += s;   // p . q (unfused r update)
   st.z = q; q += (size_t)S * s;
   st.z_prev = q; q += (size_t)S * s;
-  st.bp = q; q += (size_t)S * s * s;
-  st.g = q; q += (size_t)S * s * s;
+  st.bp = q; q += (size_t)S * nbd * s;
+  st.g = q; q += (size_t)S * nbd * s;
   double* dshift = q; q += S;
   double* beta_out = q; q += s;
   st.active = reinterpret_cast<int*>(q);   // s ints in s doubles
@@ -1256,13 +1269,14 @@ int gpmi_sp_msgram(gpmi_sp* sp, const double* etas, int neta, const double* rhs,
   double* brd = q;                         // [ne] reduced B^T r, r . r
   sp->last_converged = 0;
   double* Bd = sp->ms_ws;
-  double* Rd = Bd + ns;
+  double* Hs = Bd + nsb;   // the host block as given (original row order)
+  double* Rd = Hs + n * nrhs;
   double* Pd = Rd + ns;
   double* Qd = Pd + ns;
   double* Rd2 = Qd + ns;   // the residual alternates between Rd and Rd2
-  // fused p . q reduction + r update + dots for <= 2 column groups of 4 (the
+  // fused p . q reduction + r update + dots for <= 2 column groups of 4 of B (the
   // fused kernel re-reads q once per group)
-  const bool fused_r = (s + 3) / 4 <= 2;
+  const bool fused_r = (nbd + 3) / 4 <= 2;
   // wider blocks: the MFMA form (GPMI_MS_MFMA=0 keeps the separate update and dots)
   const char* menv = std::getenv("GPMI_MS_MFMA");
   const bool mfma_r = !fused_r && s <= 16 && !(menv && std::atoi(menv) == 0);
@@ -1282,31 +1296,38 @@ int gpmi_sp_msgram(gpmi_sp* sp, const double* etas, int neta, const double* rhs,
     // staging Qd, then into the locality order (and zero padding columns) on the
     // device: no host-side permutation pass over n x s doubles
     if (ld == nrhs) {
-      SP_TRY(hipMemcpyAsync(Qd, rhs, sizeof(double) * n * nrhs, hipMemcpyHostToDevice, str));
+      SP_TRY(hipMemcpyAsync(Hs, rhs, sizeof(double) * n * nrhs, hipMemcpyHostToDevice, str));
     } else {
       std::vector<double> h((size_t)n * nrhs);
       for (int64_t i = 0; i < n; ++i)
         for (int c = 0; c < nrhs; ++c) h[(size_t)i * nrhs + c] = rhs[i * ld + c];
-      SP_TRY(hipMemcpyAsync(Qd, h.data(), sizeof(double) * h.size(), hipMemcpyHostToDevice, str));
+      SP_TRY(hipMemcpyAsync(Hs, h.data(), sizeof(double) * h.size(), hipMemcpyHostToDevice, str));
       SP_TRY(hipStreamSynchronize(str));
     }
-    hipLaunchKernelGGL(rows_gather_kernel, dim3(grid_ns(n, s)), dim3(256), 0, str, Qd, nrhs,
-                       (const int*)sp->perm_d, n, s, Bd);
+    hipLaunchKernelGGL(rows_gather_kernel, dim3(grid_ns(n, nbd)), dim3(256), 0, str, Hs, nrhs,
+                       (const int*)sp->perm_d, n, nbd, Bd);
     SP_LAUNCH("rows_gather_kernel");
     std::vector<double> hd(S);
     for (int j = 0; j < S; ++j) hd[j] = etas[j] - eta0;
     SP_TRY(hipMemcpyAsync(dshift, hd.data(), sizeof(double) * S, hipMemcpyHostToDevice, str));
-    SP_TRY(hipMemcpyAsync(Rd, Bd, sizeof(double) * ns, hipMemcpyDeviceToDevice, str));
-    SP_TRY(hipMemcpyAsync(Pd, Bd, sizeof(double) * ns, hipMemcpyDeviceToDevice, str));
+    if (full) {
+      SP_TRY(hipMemcpyAsync(Rd, Bd, sizeof(double) * ns, hipMemcpyDeviceToDevice, str));
+    } else {
+      // the shard's columns of B (already in the device row order)
+      hipLaunchKernelGGL(rows_gather_kernel, dim3(grid_ns(n, s)), dim3(256), 0, str, Bd + c_lo,
+                         nbd, (const int*)nullptr, n, s, Rd);
+      SP_LAUNCH("rows_gather_kernel");
+    }
+    SP_TRY(hipMemcpyAsync(Pd, Rd, sizeof(double) * ns, hipMemcpyDeviceToDevice, str));
     SP_TRY(hipStreamSynchronize(str));
   }
   // scalar kernels: S * s threads for the per-shift recurrences (<= 1024), and
   // 16 waves for their fixed-order partial reductions
   const unsigned sthreads = 1024;
-  launch_ms_dots(Bd, Rd, n, s, partial, MS_NBLK, str);
+  launch_ms_dots(Bd, Rd, n, s, partial, MS_NBLK, str, nbd);
   SP_LAUNCH("ms_dots_partial_kernel");
   hipLaunchKernelGGL(ms_init_kernel, dim3(1), dim3(sthreads), 0, str, st, partial, MS_NBLK, S,
-                     s);
+                     s, nbd);
   SP_LAUNCH("ms_init_kernel");
   int it = 0;
   std::vector<int> hact(2 * s + 2);
@@ -1352,7 +1373,7 @@ int gpmi_sp_msgram(gpmi_sp* sp, const double* etas, int neta, const double* rhs,
         SP_LAUNCH("col_dot_partial_kernel");
       }
       Rout = Rnext;
-      launch_ms_rdots(Bd, Rcur, Rout, Qd, st, pqin, pqn, n, s, partial, MS_NBLK, str);
+      launch_ms_rdots(Bd, Rcur, Rout, Qd, st, pqin, pqn, n, s, partial, MS_NBLK, str, nbd);
       SP_LAUNCH("ms_rdots_partial_kernel");
       std::swap(Rcur, Rnext);
     } else if (mfma_r) {
@@ -1364,7 +1385,7 @@ int gpmi_sp_msgram(gpmi_sp* sp, const double* etas, int neta, const double* rhs,
         SP_LAUNCH("col_dot_partial_kernel");
       }
       hipLaunchKernelGGL(ms_rmfma_kernel, dim3(MS_RB), dim3(256), 0, str, Bd, Rcur, Qd, st,
-                         pqin, pqn, n, s, partial);
+                         pqin, pqn, n, s, nbd, partial);
       SP_LAUNCH("ms_rmfma_kernel");
     } else {
       // more than two 4-column groups would re-read q per group in the fused form:
@@ -1374,7 +1395,7 @@ int gpmi_sp_msgram(gpmi_sp* sp, const double* etas, int neta, const double* rhs,
       hipLaunchKernelGGL(ms_r_update_kernel, dim3(grid_ns(n, s)), dim3(256), 0, str, Rcur, Qd, st,
                          pqd, n, s);
       SP_LAUNCH("ms_r_update_kernel");
-      launch_ms_dots(Bd, Rcur, n, s, partial, MS_NBLK, str);
+      launch_ms_dots(Bd, Rcur, n, s, partial, MS_NBLK, str, nbd);
       SP_LAUNCH("ms_dots_partial_kernel");
     }
     // the ne = s^2 + s partial sums reduced one wave per element across the chip
@@ -1387,7 +1408,7 @@ int gpmi_sp_msgram(gpmi_sp* sp, const double* etas, int neta, const double* rhs,
     }
     hipLaunchKernelGGL(ms_scalar_kernel, dim3(1), dim3(sthreads), 0, str, st,
                        chip_red ? (const double*)brd : partial, chip_red ? 0 : pnb, dshift, S, s,
-                       rtol * rtol, beta_out);
+                       nbd, rtol * rtol, beta_out);
     SP_LAUNCH("ms_scalar_kernel");
     hipLaunchKernelGGL(ms_p_update_kernel, dim3(grid_ns(n, s)), dim3(256), 0, str, Pd, Rout,
                        st.beta, st.active, n, s);
@@ -1399,15 +1420,26 @@ int gpmi_sp_msgram(gpmi_sp* sp, const double* etas, int neta, const double* rhs,
     if (rc) return rc;
     sp->last_converged = any ? 0 : 1;
   }
-  std::vector<double> hg((size_t)S * s * s);
+  std::vector<double> hg((size_t)S * nbd * s);
   SP_TRY(hipMemcpyAsync(hg.data(), st.g, sizeof(double) * hg.size(), hipMemcpyDeviceToHost, str));
   SP_TRY(hipStreamSynchronize(str));
   for (int j = 0; j < S; ++j)
     for (int a = 0; a < nrhs; ++a)
-      for (int c = 0; c < nrhs; ++c)
-        G[((size_t)j * nrhs + a) * nrhs + c] = hg[((size_t)j * s + a) * s + c];
+      for (int c = 0; c < nsub; ++c)
+        G[((size_t)j * nrhs + a) * nsub + c] = hg[((size_t)j * nbd + a) * s + c];
   if (iterations) *iterations = it;
   return 0;
+}
+
+int gpmi_sp_msgram(gpmi_sp* sp, const double* etas, int neta, const double* rhs, int64_t ld,
+                   int nrhs, double rtol, int maxiter, double* G, int* iterations) {
+  return msgram_impl(sp, etas, neta, rhs, ld, nrhs, 0, nrhs, rtol, maxiter, G, iterations);
+}
+
+int gpmi_sp_msgram_cols(gpmi_sp* sp, const double* etas, int neta, const double* rhs, int64_t ld,
+                        int nrhs, int c_lo, int c_hi, double rtol, int maxiter, double* G,
+                        int* iterations) {
+  return msgram_impl(sp, etas, neta, rhs, ld, nrhs, c_lo, c_hi, rtol, maxiter, G, iterations);
 }
 
 int gpmi_sp_spmm_info(gpmi_sp* sp, int* windowed, double* mean_window, int* max_window) {

@@ -80,6 +80,9 @@ SIGNATURES = {
     'gpmi_sp_msgram': (ctypes.c_int, [c_op_p, c_double_p, ctypes.c_int, c_double_p, c_i64,
                                       ctypes.c_int, ctypes.c_double, ctypes.c_int, c_double_p,
                                       c_int_p]),
+    'gpmi_sp_msgram_cols': (ctypes.c_int, [c_op_p, c_double_p, ctypes.c_int, c_double_p, c_i64,
+                                           ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                           ctypes.c_double, ctypes.c_int, c_double_p, c_int_p]),
     'gpmi_band_create': (ctypes.c_int, [c_op_p, ctypes.POINTER(c_op_p)]),
     'gpmi_band_destroy': (ctypes.c_int, [c_op_p]),
     'gpmi_band_refresh': (ctypes.c_int, [c_op_p, c_op_p]),
@@ -613,23 +616,33 @@ class SparseOperator(object):
 
     MS_MAXS = 16
 
-    def msgram(self, etas, B, rtol=1e-6, maxiter=None):
+    def msgram(self, etas, B, rtol=1e-6, maxiter=None, cols=None):
         """G[j] = B^T (K + etas[j] I)^-1 B for all etas from one multi-shift CG
-        (B: [n, s], s <= 16). Returns G [neta, s, s]."""
+        (B: [n, s], s <= 16). Returns G [neta, s, s]; with cols = (c_lo, c_hi) only
+        those right-hand sides are solved (dotted with all of B): G [neta, s,
+        c_hi - c_lo], the columns of the full G (gpmi_sp_msgram_cols)."""
         B = as_c(B)
         B2 = B[:, None] if B.ndim == 1 else B
         etas = as_c(numpy.atleast_1d(etas))
         s = B2.shape[1]
-        G = numpy.empty((etas.size, s, s))
+        c_lo, c_hi = (0, s) if cols is None else (int(cols[0]), int(cols[1]))
+        w = c_hi - c_lo
+        G = numpy.empty((etas.size, s, w))
         it = ctypes.c_int(0)
         maxiter = 10 * self.n if maxiter is None else int(maxiter)
-        step = max(1, 1024 // s)
+        step = max(1, 1024 // max(1, w))
         for j0 in range(0, etas.size, step):
             e = as_c(etas[j0:j0 + step])
-            Gj = numpy.empty((e.size, s, s))
-            check(self.lib.gpmi_sp_msgram(self.h, dptr(e), e.size, dptr(B2), s, s, float(rtol),
-                                          maxiter, dptr(Gj), ctypes.byref(it)),
-                  'gpmi_sp_msgram')
+            Gj = numpy.empty((e.size, s, w))
+            if cols is None:
+                check(self.lib.gpmi_sp_msgram(self.h, dptr(e), e.size, dptr(B2), s, s,
+                                              float(rtol), maxiter, dptr(Gj), ctypes.byref(it)),
+                      'gpmi_sp_msgram')
+            else:
+                check(self.lib.gpmi_sp_msgram_cols(self.h, dptr(e), e.size, dptr(B2), s, s, c_lo,
+                                                   c_hi, float(rtol), maxiter, dptr(Gj),
+                                                   ctypes.byref(it)),
+                      'gpmi_sp_msgram_cols')
             G[j0:j0 + e.size] = Gj
             self._warn_unconverged('msgram', maxiter)
         self.last_cg_iterations = it.value

@@ -157,26 +157,56 @@ def slq_sweep(K_mixed, etas, group=None):
     return {name: n * allq[:, f].mean(axis=0) for f, name in enumerate(names)}
 
 
-def slq_gram_sweep(K_mixed, etas, R, rtol=1e-6, group=None):
+def slq_gram_sweep(K_mixed, etas, R, rtol=1e-6, group=None, split='columns'):
     """One sparse likelihood sweep: slq_sweep (the Lanczos of this rank's probe
     shard, all-gathered quadratures) and the multi-shift CG Gram blocks
-    R^T (K + eta I)^-1 R of this rank's contiguous eta block
-    (_linear_solver.py:57-68 at ``rtol``), run TOGETHER: the Gram on a second host
-    thread, whose device calls go to the multi-shift CG's own stream
-    (gpmi_sp_msgram), beside the Lanczos on the operator's stream. The two are
-    independent (the same K, different vectors), and each alone leaves the device
-    partly idle (latency-bound scalar and reduction launches).
+    R^T (K + eta I)^-1 R (_linear_solver.py:57-68 at ``rtol``), run TOGETHER: the
+    Gram on a second host thread, whose device calls go to the multi-shift CG's own
+    stream (gpmi_sp_msgram), beside the Lanczos on the operator's stream. The two
+    are independent (the same K, different vectors), and each alone leaves the
+    device partly idle (latency-bound scalar and reduction launches).
+
+    On several ranks the Gram is split by right-hand-side columns (``split=
+    'columns'``, default): rank r solves its column shard of R for EVERY eta
+    (gpmi_sp_msgram_cols, dotted with all of R) and one all-gather after the
+    Lanczos's collects the columns, so each rank runs a fraction of the CG's SpMMs.
+    ``split='eta'`` gives each rank the full CG for its eta block (the per-shift
+    scalars only divide).
 
     Returns (curves, (lo, hi), G[hi - lo, s, s]): slq_sweep's curves on every
-    rank, and this rank's eta block with its Gram blocks."""
+    rank, and this rank's contiguous eta block with its Gram blocks."""
     from concurrent.futures import ThreadPoolExecutor
     etas = numpy.atleast_1d(numpy.asarray(etas, dtype=float))
+    R = numpy.asarray(R, dtype=float)
+    R2 = R[:, None] if R.ndim == 1 else R
+    s = R2.shape[1]
     dist, world, rank = _group(group)
     lo, hi, _ = shard(etas.size, world, rank)
+    by_cols = world > 1 and split == 'columns'
+    clo, chi, cper = shard(s, world, rank)
     with ThreadPoolExecutor(1) as ex:
-        fut = ex.submit(K_mixed.sop.msgram, etas[lo:hi], R, rtol) if hi > lo else None
+        if by_cols:
+            fut = (ex.submit(K_mixed.sop.msgram, etas, R2, rtol, None, (clo, chi))
+                   if chi > clo else None)
+        else:
+            fut = ex.submit(K_mixed.sop.msgram, etas[lo:hi], R2, rtol) if hi > lo else None
         try:
             curves = slq_sweep(K_mixed, etas, group=group)
         finally:
             G = fut.result() if fut is not None else None
+    if by_cols:
+        # one row per column c (its G[:, :, c] flattened), cper rows per rank; the
+        # all-gather runs after the Lanczos's (collectives in the same order on
+        # every rank, from the main thread)
+        local = numpy.zeros((cper, etas.size * s))
+        if G is not None:
+            local[:chi - clo] = G.transpose(2, 0, 1).reshape(chi - clo, -1)
+        allv = _all_gather_rows(dist, group, local, world)
+        Gf = numpy.empty((etas.size, s, s))
+        for r in range(world):
+            a, b, _ = shard(s, world, r)
+            if b > a:
+                blk = allv[r * cper:r * cper + (b - a)].reshape(b - a, etas.size, s)
+                Gf[:, :, a:b] = blk.transpose(1, 2, 0)
+        G = Gf[lo:hi] if hi > lo else None
     return curves, (lo, hi), G

@@ -202,6 +202,15 @@ int gpmi_sp_cg(gpmi_sp* sp, double eta, const double* rhs, int64_t ld, int nrhs,
  * -> _linear_solver.py:57-68 (scipy.sparse.linalg.cg, tol 1e-6). */
 int gpmi_sp_msgram(gpmi_sp* sp, const double* etas, int neta, const double* rhs, int64_t ld,
                    int nrhs, double rtol, int maxiter, double* G, int* iterations);
+/* The same for a shard of the right-hand sides: the columns [c_lo, c_hi) of the
+ * nrhs-column block solved (every eta), dotted with all nrhs columns:
+ * G[neta][nrhs][c_hi - c_lo], G[j][a][c] = b_a^T (K + eta_j I)^-1 b_{c_lo + c}. Ranks
+ * holding different column shards together form the whole Gram with a fraction of
+ * the multi-shift CG's SpMMs each (the eta shard alone divides only its per-shift
+ * scalars). */
+int gpmi_sp_msgram_cols(gpmi_sp* sp, const double* etas, int neta, const double* rhs, int64_t ld,
+                        int nrhs, int c_lo, int c_hi, double rtol, int maxiter, double* G,
+                        int* iterations);
 
 /* The SpMM kernel this operator uses (1: X-window staged in LDS, 64-row blocks;
  * 0: gathers from X, one wave per row) and its window sizes (columns per block:

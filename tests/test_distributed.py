@@ -304,10 +304,11 @@ def test_der1_sweep_error_raises_on_every_rank_gloo():
 
 
 class _FakeSparseGram(_FakeSparse):
-    def msgram(self, etas, R, rtol=1e-6):
+    def msgram(self, etas, R, rtol=1e-6, maxiter=None, cols=None):
         n = self.K.shape[0]
-        return numpy.array([R.T @ numpy.linalg.solve(self.K + e * numpy.eye(n), R)
-                            for e in etas])
+        G = numpy.array([R.T @ numpy.linalg.solve(self.K + e * numpy.eye(n), R)
+                         for e in etas])
+        return G if cols is None else G[:, :, cols[0]:cols[1]]
 
 
 class _SparseMixedGram(_SparseMixed):
@@ -330,8 +331,10 @@ def _slq_gram_worker(rank, world, port, etas, out_q):
 
 def test_slq_gram_sweep_gloo():
     """slq_gram_sweep: the probe-sharded SLQ curves (all-gathered, equal on every
-    rank) and each rank's eta block of multi-shift Gram blocks, computed together
-    (second host thread); the union of the blocks is the single-process result."""
+    rank) and the multi-shift Gram blocks computed together (second host thread),
+    the Gram split by right-hand-side columns over the ranks and all-gathered after
+    the Lanczos; each rank's eta block of the result, whose union is the
+    single-process result."""
     from gaussian_proc.sweep import slq_gram_sweep
     etas = numpy.array([0.5, 1.0, 2.0, 4.0, 8.0])
     ctx = mp.get_context('spawn')

@@ -160,6 +160,29 @@ def test_multishift_gram_vs_exact(gp):
     assert g1.shape == (2, 1, 1)
 
 
+def test_msgram_column_shards_equal_full(gp):
+    """gpmi_sp_msgram_cols: shards of the right-hand-side columns, each solved for
+    every eta and dotted with all of B, give the columns of the full multi-shift
+    Gram (the per-column CG recurrences do not depend on the other columns; the
+    shards run other kernel forms, so equal to 1e-9, not bit for bit), and vs
+    the exact solve."""
+    from gaussian_proc import _hip
+    _, K = _small_sparse()
+    n = K.shape[0]
+    sop = _hip.SparseOperator.from_csr(K)
+    rng = numpy.random.RandomState(7)
+    B = rng.randn(n, 11)
+    etas = numpy.array([2.5, 4.0, 10.0, 100.0])
+    G = sop.msgram(etas, B, rtol=1e-10)
+    for lo, hi in ((0, 2), (2, 3), (3, 9), (9, 11), (0, 11)):
+        Gc = sop.msgram(etas, B, rtol=1e-10, cols=(lo, hi))
+        assert Gc.shape == (etas.size, 11, hi - lo)
+        assert _nrel(Gc, G[:, :, lo:hi]) < 1e-9, (lo, hi)
+    for e, g in zip(etas, G):
+        ex = B.T @ scipy.sparse.linalg.spsolve((K + e * scipy.sparse.eye(n)).tocsc(), B)
+        assert _nrel(g, ex) < 1e-9
+
+
 def test_lanczos_and_slq_match_oracle_same_probes(gp):
     from gaussian_proc import _hip, _slq
     _, K = _small_sparse()
