@@ -772,10 +772,27 @@ __global__ void lanczos_scalar_kernel(const double* __restrict__ H1k,
 //           (ONE pass, both vectors, lz_update)
 // Per probe column c; every reduction has a fixed order (deterministic).
 
+// Basis reads of the DCGS2 passes as non-temporal loads when NT (chosen by the host
+// for a basis larger than twice the Infinity Cache): the basis (1.26 GB at cfg 5)
+// then streams through each pass without evicting the CSR and window rows the SpMMs
+// (the Lanczos's own and the multi-shift CG's beside it) reread (cfg 5 Lanczos
+// 13.0 -> 11.2 ms); a basis that fits (cfg 4: 0.3 GB) is faster cached.
+template <bool NT>
+__device__ __forceinline__ double ld_basis(const double* p) {
+  if (NT) return __builtin_nontemporal_load(p);
+  return *p;
+}
+template <bool NT>
+__device__ __forceinline__ d2 ld_basis2(const double* p) {
+  if (NT) return __builtin_nontemporal_load(reinterpret_cast<const d2*>(p));
+  return *reinterpret_cast<const d2*>(p);
+}
+
 // partial[b][v][c] over this block's rows: v = j0 + q: V_{j0+q} . u; v = J + j0 + q:
 // V_{j0+q} . y (Y given); with j0 == 0 also v = 2J: u . u and 2J + 1: u . y.
 // Vectors [j0, j0 + LZ_JC) of the J per launch; rows grid-strided, one column per
 // thread (256 / s rows per block iteration).
+template <bool NT>
 __global__ __launch_bounds__(256) void lz_dots_kernel(const double* __restrict__ V, int64_t ns,
                                                       int J, int j0,
                                                       const double* __restrict__ U,
@@ -799,7 +816,8 @@ __global__ __launch_bounds__(256) void lz_dots_kernel(const double* __restrict__
       const double y = Y ? Y[e] : 0.0;
       double v[LZ_JC];
 #pragma unroll
-      for (int q = 0; q < LZ_JC; ++q) v[q] = q < jc ? V[(int64_t)(j0 + q) * ns + e] : 0.0;
+      for (int q = 0; q < LZ_JC; ++q)
+        v[q] = q < jc ? ld_basis<NT>(V + (int64_t)(j0 + q) * ns + e) : 0.0;
       uu += u * u;
       uy += u * y;
 #pragma unroll
@@ -828,6 +846,10 @@ __global__ __launch_bounds__(256) void lz_dots_kernel(const double* __restrict__
     put(uy, 2 * J + 1);
   }
 }
+template __global__ void lz_dots_kernel<false>(const double*, int64_t, int, int, const double*,
+                                               const double*, int64_t, int, int, double*);
+template __global__ void lz_dots_kernel<true>(const double*, int64_t, int, int, const double*,
+                                              const double*, int64_t, int, int, double*);
 
 // Step k's scalars (one workgroup; d = reduced dots [(2k + 2)][s]; per column c:
 // H [c][(steps + 2) x (steps + 1)] row-major (H[i][j]: coefficient of v_i in K v_j),
@@ -923,7 +945,7 @@ __global__ void lz_scalar_kernel(const double* __restrict__ d, int k, int steps,
 // chunks share the thread's two columns and their coefficient loads), the basis
 // loads four vectors at a time; the same per-element order of subtraction as one
 // element per thread.
-template <int NR>
+template <int NR, bool NT>
 __global__ __launch_bounds__(256) void lz_update_kernel(double* __restrict__ V, int64_t ns, int k,
                                                         double* __restrict__ U,
                                                         const double* __restrict__ Y,
@@ -956,7 +978,7 @@ __global__ __launch_bounds__(256) void lz_update_kernel(double* __restrict__ V, 
       for (int q = 0; q < 4; ++q)
 #pragma unroll
         for (int m = 0; m < NR; ++m)
-          a[q][m] = on[m] ? *reinterpret_cast<const d2*>(V + (j + q) * ns + e0 + 2 * P * m)
+          a[q][m] = on[m] ? ld_basis2<NT>(V + (j + q) * ns + e0 + 2 * P * m)
                           : d2{0.0, 0.0};
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -976,7 +998,7 @@ __global__ __launch_bounds__(256) void lz_update_kernel(double* __restrict__ V, 
       const double cu0 = cu[j * s + c0], cu1 = cu[j * s + c1];
 #pragma unroll
       for (int m = 0; m < NR; ++m) {
-        const d2 a = on[m] ? *reinterpret_cast<const d2*>(V + j * ns + e0 + 2 * P * m)
+        const d2 a = on[m] ? ld_basis2<NT>(V + j * ns + e0 + 2 * P * m)
                            : d2{0.0, 0.0};
         v0[m] -= a[0] * cv0;
         v1[m] -= a[1] * cv1;
@@ -1013,10 +1035,18 @@ __global__ __launch_bounds__(256) void lz_update_kernel(double* __restrict__ V, 
       }
   }
 }
-template __global__ void lz_update_kernel<1>(double*, int64_t, int, double*, const double*,
-                                             const double*, const double*, const double*, int);
-template __global__ void lz_update_kernel<4>(double*, int64_t, int, double*, const double*,
-                                             const double*, const double*, const double*, int);
+template __global__ void lz_update_kernel<1, false>(double*, int64_t, int, double*, const double*,
+                                                    const double*, const double*, const double*,
+                                                    int);
+template __global__ void lz_update_kernel<4, false>(double*, int64_t, int, double*, const double*,
+                                                    const double*, const double*, const double*,
+                                                    int);
+template __global__ void lz_update_kernel<1, true>(double*, int64_t, int, double*, const double*,
+                                                   const double*, const double*, const double*,
+                                                   int);
+template __global__ void lz_update_kernel<4, true>(double*, int64_t, int, double*, const double*,
+                                                   const double*, const double*, const double*,
+                                                   int);
 
 // Normalised Rademacher probes: V[i][c] = +-1/sqrt(n), bit 63 of
 // splitmix64(seed * G + (c + c0) * H + i) (matches oracle/sparse.py).

@@ -61,11 +61,12 @@ __global__ void col_gs_update_kernel(double*, const double*, int64_t, const doub
                                      int);
 __global__ void col_axpby_kernel(const double*, double*, const double*, const double*, int64_t,
                                  int);
+template <bool NT>
 __global__ void lz_dots_kernel(const double*, int64_t, int, int, const double*, const double*,
                                int64_t, int, int, double*);
 __global__ void lz_scalar_kernel(const double*, int, int, int, double*, double*, double*, double*,
                                  double*, int*, int*, double*, double*);
-template <int NR>
+template <int NR, bool NT>
 __global__ void lz_update_kernel(double*, int64_t, int, double*, const double*, const double*,
                                  const double*, const double*, int);
 __global__ void rademacher_kernel(double*, int64_t, int, unsigned long long, int, double,
@@ -567,6 +568,11 @@ int lanczos_block_dcgs2(gpmi_sp* sp, double* V, double* U, double* Y, int s, int
   // GPMI_LZ_NR: row chunks per thread of the update pass (1 or 4)
   const char* nenv = std::getenv("GPMI_LZ_NR");
   const int lz_nr = nenv ? std::atoi(nenv) : 4;
+  // non-temporal basis reads for a basis over twice the 256 MB Infinity Cache
+  // (GPMI_LZ_NT=0 / 1 forces either)
+  const char* tenv = std::getenv("GPMI_LZ_NT");
+  const bool lz_nt = tenv ? std::atoi(tenv) != 0
+                          : sizeof(double) * (double)ns * (steps + 1) > 512.0 * 1024 * 1024;
   for (int k = 0; k <= steps; ++k) {
     const bool last = k == steps;
     if (!last) {
@@ -577,7 +583,8 @@ int lanczos_block_dcgs2(gpmi_sp* sp, double* V, double* U, double* Y, int s, int
     for (int j0 = 0; j0 == 0 || j0 < k; j0 += LZ_JC) {
       // (column pairs with 16-byte loads measured slower: 15.9 against 13.1 ms per
       // cfg 5 Lanczos, at half the occupancy for the doubled accumulators)
-      hipLaunchKernelGGL(lz_dots_kernel, dim3(lz_nb), dim3(256), 0, sp->stream, V, ns, k, j0, U,
+      hipLaunchKernelGGL(lz_nt ? lz_dots_kernel<true> : lz_dots_kernel<false>, dim3(lz_nb),
+                         dim3(256), 0, sp->stream, V, ns, k, j0, U,
                          last ? (const double*)nullptr : Y, n, s, nv, sp->partial);
       SP_LAUNCH("lz_dots_kernel");
     }
@@ -594,11 +601,13 @@ int lanczos_block_dcgs2(gpmi_sp* sp, double* V, double* U, double* Y, int s, int
         const int64_t q = s / std::__gcd(512, s);
         int64_t g = (ns / 2 + 1023) / 1024;
         g = (g + q - 1) / q * q;
-        hipLaunchKernelGGL(lz_update_kernel<4>, dim3((unsigned)g), dim3(256), 0, sp->stream, V,
-                           ns, k, U, Y, cv, cu, ir, s);
+        auto kfn = lz_nt ? lz_update_kernel<4, true> : lz_update_kernel<4, false>;
+        hipLaunchKernelGGL(kfn, dim3((unsigned)g), dim3(256), 0, sp->stream, V, ns, k, U, Y, cv,
+                           cu, ir, s);
       } else {
-        hipLaunchKernelGGL(lz_update_kernel<1>, dim3((unsigned)((ns + 511) / 512)), dim3(256), 0,
-                           sp->stream, V, ns, k, U, Y, cv, cu, ir, s);
+        auto kfn = lz_nt ? lz_update_kernel<1, true> : lz_update_kernel<1, false>;
+        hipLaunchKernelGGL(kfn, dim3((unsigned)((ns + 511) / 512)), dim3(256), 0, sp->stream, V,
+                           ns, k, U, Y, cv, cu, ir, s);
       }
       SP_LAUNCH("lz_update_kernel");
     }
