@@ -1419,7 +1419,8 @@ static int msgram_impl(gpmi_sp* sp, const double* etas, int neta, const double* 
                        chip_red ? (const double*)brd : partial, chip_red ? 0 : pnb, dshift, S, s,
                        nbd, rtol * rtol, beta_out);
     SP_LAUNCH("ms_scalar_kernel");
-    hipLaunchKernelGGL(ms_p_update_kernel, dim3(grid_ns(n, s)), dim3(256), 0, str, Pd, Rout,
+    hipLaunchKernelGGL(ms_p_update_kernel, dim3((unsigned)((ns + 1023) / 1024)), dim3(256), 0,
+                       str, Pd, Rout,
                        st.beta, st.active, n, s);
     SP_LAUNCH("ms_p_update_kernel");
   }

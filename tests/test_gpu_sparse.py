@@ -183,6 +183,43 @@ def test_msgram_column_shards_equal_full(gp):
         assert _nrel(g, ex) < 1e-9
 
 
+def test_msgram_stopped_column_and_overflowing_windows(gp):
+    """The multi-shift CG on the window SpMM (csr_spmm_wing_kernel at s = 7 and 11)
+    over a matrix whose first blocks overflow the window (the gather branch), with a
+    zero right-hand side (a column stopped from the start: its p and x stay zero):
+    the Gram matches the exact solve, the zero column's row and column exactly 0."""
+    from gaussian_proc import _hip
+    rng = numpy.random.RandomState(5)
+    n = 3000
+    rows, cols = [], []
+    for i in range(n):
+        if i < 64:
+            c = rng.choice(n, 100, replace=False)
+        elif i < 128:
+            c = rng.choice(n, 40, replace=False)
+        else:
+            c = numpy.clip(i + rng.randint(-30, 31, 12), 0, n - 1)
+        rows.extend([i] * len(c))
+        cols.extend(c)
+    A = scipy.sparse.csr_matrix((numpy.abs(rng.randn(len(rows))), (rows, cols)), shape=(n, n))
+    A = (A + A.T).tocsr()
+    A.sum_duplicates()
+    # symmetric, diagonally dominant: positive definite
+    A = (A + scipy.sparse.diags(numpy.asarray(A.sum(axis=1)).ravel() + 0.1)).tocsr()
+    A.sort_indices()
+    sop = _hip.SparseOperator.from_csr(A)
+    etas = numpy.array([0.5, 2.0, 30.0])
+    for s in (7, 11):
+        assert sop.spmm_kernel(s) == 'csr_spmm_wing_kernel'
+        B = rng.randn(n, s)
+        B[:, 3] = 0.0
+        G = sop.msgram(etas, B, rtol=1e-11, maxiter=2000)
+        assert not G[:, 3, :].any() and not G[:, :, 3].any()
+        for e, g in zip(etas, G):
+            ex = B.T @ scipy.sparse.linalg.spsolve((A + e * scipy.sparse.eye(n)).tocsc(), B)
+            assert _nrel(g, ex) < 1e-9, (s, e)
+
+
 def test_lanczos_and_slq_match_oracle_same_probes(gp):
     from gaussian_proc import _hip, _slq
     _, K = _small_sparse()
