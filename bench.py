@@ -282,9 +282,10 @@ def cpu_baseline_sparse(K, X, z, etas, nprobe, steps, seed, budget_s, workers=No
     def solve(task):
         j, c = task
         cnt = [0]
-        scipy.sparse.linalg.cg(mats[j], R[:, c], rtol=1e-6, atol=0.0,
-                               callback=lambda xk: cnt.__setitem__(0, cnt[0] + 1))
-        return cnt[0]
+        x, _ = scipy.sparse.linalg.cg(mats[j], R[:, c], rtol=1e-6, atol=0.0,
+                                      callback=lambda xk: cnt.__setitem__(0, cnt[0] + 1))
+        # the Gram column R^T x (checked against the device's multi-shift CG)
+        return cnt[0], (j, c, R.T @ x)
     with threadpool_limits(limits=1, user_api='blas'), ThreadPoolExecutor(workers) as ex:
         t0 = time.perf_counter()
         ab = list(ex.map(lanczos, range(nprobe)))
@@ -302,6 +303,8 @@ def cpu_baseline_sparse(K, X, z, etas, nprobe, steps, seed, budget_s, workers=No
                 its.append(futs.pop(0).result())
         its += [f.result() for f in futs]
         t_cg = time.perf_counter() - t0
+    cols = [g for _, g in its]
+    its = [i for i, _ in its]
     done = len(its)
     log('cpu CG: %d solves in %.1f s on %d threads' % (done, t_cg, workers))
     total = t_slq + t_cg * (etas.size * R.shape[1]) / float(done)
@@ -316,7 +319,7 @@ def cpu_baseline_sparse(K, X, z, etas, nprobe, steps, seed, budget_s, workers=No
                          numpy.mean(its), workers, etas.size),
             'slq_s': round(t_slq, 3), 'cg_s_per_solve_wall': round(t_cg / done, 4),
             'est_s_per_step': round(total, 2), 'threads': workers, 'host': info,
-            'logdet': logdet.tolist()}
+            'logdet': logdet.tolist(), 'gram_columns': cols}
 
 
 def sparse_step_bytes(n, nnz, s_lanczos, steps, s_cg, cg_iters):
@@ -398,6 +401,7 @@ def sparse_measure(args, config, world, rank, local, dist, torch, cpu, exact):
         # the eta shard (rtol 1e-6) run together on two streams (sweep.slq_gram_sweep)
         curves, _, Gs = slq_gram_sweep(op, etas, R, rtol=1e-6)
         holder['curves'] = curves
+        holder['grams'] = Gs
         rows = numpy.zeros((per, 3))
         if hi > lo:
             holder['cg_iters'] = op.sop.last_cg_iterations
@@ -518,6 +522,13 @@ def sparse_measure(args, config, world, rank, local, dist, torch, cpu, exact):
             dev = holder['curves']['logdet']
             cb['slq_logdet_rel_diff_vs_device_same_probes'] = float(
                 numpy.max(numpy.abs(numpy.asarray(cb.pop('logdet')) - dev) / numpy.abs(dev)))
+            # the Gram columns the host CG solved (both at rtol 1e-6) against the device's
+            # multi-shift CG blocks of the last timed step (rank 0 holds every eta at N=1)
+            Gd = holder['grams']
+            cb['cg_gram_column_rel_diff_vs_device_max'] = float(max(
+                numpy.max(numpy.abs(numpy.asarray(Gd[j])[:, c] - g)) /
+                numpy.max(numpy.abs(numpy.asarray(Gd[j])[:, c]))
+                for j, c, g in cb.pop('gram_columns')))
             res['cpu_baseline'] = cb
             res['speedup_vs_cpu'] = round(res['value'] / cb['value'], 1)
     op.sop.close()

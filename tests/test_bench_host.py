@@ -7,6 +7,7 @@ import sys
 
 import numpy
 import scipy.sparse
+import scipy.sparse.linalg
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import bench  # noqa: E402
@@ -33,6 +34,13 @@ def test_cpu_baseline_sparse_thread_pool():
     P = osp.rademacher_probes(n, 4, 5)
     ref = osp.slq(K, etas, P, 12)['logdet']
     numpy.testing.assert_allclose(cb['logdet'], ref, rtol=1e-12)
+    # the solved Gram columns R^T (K + eta I)^-1 r_c (rtol 1e-6) against a direct solve
+    R = numpy.column_stack([X, z])
+    assert cb['gram_columns']
+    for j, c, g in cb['gram_columns']:
+        ex = R.T @ scipy.sparse.linalg.spsolve((K + etas[j] * scipy.sparse.identity(n)).tocsc(),
+                                               R[:, c])
+        assert numpy.max(numpy.abs(g - ex)) <= 1e-5 * numpy.max(numpy.abs(ex))
 
 
 def test_sparse_step_bytes_model():
