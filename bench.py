@@ -329,8 +329,8 @@ def sparse_step_bytes(n, nnz, s_lanczos, steps, s_cg, cg_iters):
     dot pass over the k basis blocks, u and y ((k + 2) b_L) and the update pass
     (k basis blocks, u, y read; v_k, u written: (k + 4) b_L), then one final dot
     pass over the basis and u ((steps + 1) b_L). Multi-shift CG (b_C = 8 n s_C,
-    s_C the device width: an odd width that would run the one-column gather is
-    padded by one zero column) per iteration: the SpMM, p . q (2 b_C), the r
+    s_C the device width: a full 11-column block on the window SpMM is padded
+    by one zero column) per iteration: the SpMM, p . q (2 b_C), the r
     update (3 b_C), the B^T r / r . r dots (2 b_C) and p = r + beta p (3 b_C)."""
     csr = 12.0 * nnz + 8.0 * (n + 1)
     bl, bc = 8.0 * n * s_lanczos, 8.0 * n * s_cg
@@ -460,8 +460,10 @@ def sparse_measure(args, config, world, rank, local, dist, torch, cpu, exact):
     sp_traffic, sp_tsrc = (pmc_traffic_sparse(config, 'gpmi::' + sp_kernel)
                            if s_blk == 20 else (None, None))
     my_probes = shard(nprobe, world, rank)
-    s_cg = R.shape[1] + (1 if (R.shape[1] % 2 and op.sop.spmm_kernel(R.shape[1]) ==
-                               'csr_spmm_kernel' and R.shape[1] < 16) else 0)
+    # the library pads a full 11-column block on the window SpMM to 12 (msgram_impl);
+    # a column shard (N > 1) runs unpadded
+    s_cg = R.shape[1] + (1 if (world == 1 and R.shape[1] == 11 and
+                               op.sop.spmm_kernel(11) == 'csr_spmm_wing_kernel') else 0)
     sb = sparse_step_bytes(n, nnz, my_probes[1] - my_probes[0], steps, s_cg,
                            holder['cg_iters'])
     step_s = dt / args.steps

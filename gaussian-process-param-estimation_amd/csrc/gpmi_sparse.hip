@@ -594,6 +594,42 @@ template __global__ void csr_spmm_wing_kernel<11, 16, 4>(const int64_t*, const i
 template __global__ void csr_spmm_wing_kernel<11, 16, 8>(const int64_t*, const int*,
     const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
     double*, double, double*);
+template __global__ void csr_spmm_wing_kernel<12, 4, 4>(const int64_t*, const int*,
+    const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
+    double*, double, double*);
+template __global__ void csr_spmm_wing_kernel<12, 4, 8>(const int64_t*, const int*,
+    const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
+    double*, double, double*);
+template __global__ void csr_spmm_wing_kernel<12, 8, 4>(const int64_t*, const int*,
+    const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
+    double*, double, double*);
+template __global__ void csr_spmm_wing_kernel<12, 8, 8>(const int64_t*, const int*,
+    const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
+    double*, double, double*);
+template __global__ void csr_spmm_wing_kernel<12, 16, 4>(const int64_t*, const int*,
+    const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
+    double*, double, double*);
+template __global__ void csr_spmm_wing_kernel<12, 16, 8>(const int64_t*, const int*,
+    const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
+    double*, double, double*);
+template __global__ void csr_spmm_wing_kernel<8, 4, 4>(const int64_t*, const int*,
+    const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
+    double*, double, double*);
+template __global__ void csr_spmm_wing_kernel<8, 4, 8>(const int64_t*, const int*,
+    const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
+    double*, double, double*);
+template __global__ void csr_spmm_wing_kernel<8, 8, 4>(const int64_t*, const int*,
+    const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
+    double*, double, double*);
+template __global__ void csr_spmm_wing_kernel<8, 8, 8>(const int64_t*, const int*,
+    const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
+    double*, double, double*);
+template __global__ void csr_spmm_wing_kernel<8, 16, 4>(const int64_t*, const int*,
+    const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
+    double*, double, double*);
+template __global__ void csr_spmm_wing_kernel<8, 16, 8>(const int64_t*, const int*,
+    const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
+    double*, double, double*);
 template __global__ void csr_spmm_wing_kernel<7, 4, 4>(const int64_t*, const int*,
     const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
     double*, double, double*);

@@ -282,7 +282,19 @@ int ensure_window(gpmi_sp* sp) {
                         reinterpret_cast<const void*>(&csr_spmm_wing_kernel<7, 8, 4>),
                         reinterpret_cast<const void*>(&csr_spmm_wing_kernel<7, 8, 8>),
                         reinterpret_cast<const void*>(&csr_spmm_wing_kernel<7, 16, 4>),
-                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<7, 16, 8>)})
+                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<7, 16, 8>),
+                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<12, 4, 4>),
+                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<12, 4, 8>),
+                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<12, 8, 4>),
+                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<12, 8, 8>),
+                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<12, 16, 4>),
+                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<12, 16, 8>),
+                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<8, 4, 4>),
+                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<8, 4, 8>),
+                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<8, 8, 4>),
+                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<8, 8, 8>),
+                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<8, 16, 4>),
+                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<8, 16, 8>)})
     SP_TRY(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, WING_MAX_LDS));
   sp->win_nblk = nblk;
   sp->win_maxu = mu;
@@ -309,7 +321,7 @@ int spmm_kind(gpmi_sp* sp, int s, int* kind) {
   // and multi-shift CG widths while the widest window fits two workgroups per CU
   // (GPMI_SPMM_WING=0: off)
   const char* genv = std::getenv("GPMI_SPMM_WING");
-  if (wmode != 0 && !(genv && std::atoi(genv) == 0) && (s == 20 || s == 11 || s == 7) &&
+  if (wmode != 0 && !(genv && std::atoi(genv) == 0) && (s == 20 || s == 12 || s == 11 || s == 8 || s == 7) &&
       sp->win_maxu > 0 &&
       sizeof(double) * (size_t)std::max(sp->win_maxu, WIN_ROWS_HOST) * s <= (size_t)WING_MAX_LDS) {
     *kind = 5;
@@ -366,14 +378,22 @@ int spmm(gpmi_sp* sp, const double* X, double* Y, int s, double eta, hipStream_t
     auto kfn = tpr == 4
         ? (s == 20 ? pick(csr_spmm_wing_kernel<20, 4, 4>, csr_spmm_wing_kernel<20, 8, 4>,
                           csr_spmm_wing_kernel<20, 16, 4>)
+           : s == 12 ? pick(csr_spmm_wing_kernel<12, 4, 4>, csr_spmm_wing_kernel<12, 8, 4>,
+                            csr_spmm_wing_kernel<12, 16, 4>)
            : s == 11 ? pick(csr_spmm_wing_kernel<11, 4, 4>, csr_spmm_wing_kernel<11, 8, 4>,
                             csr_spmm_wing_kernel<11, 16, 4>)
+           : s == 8 ? pick(csr_spmm_wing_kernel<8, 4, 4>, csr_spmm_wing_kernel<8, 8, 4>,
+                           csr_spmm_wing_kernel<8, 16, 4>)
                      : pick(csr_spmm_wing_kernel<7, 4, 4>, csr_spmm_wing_kernel<7, 8, 4>,
                             csr_spmm_wing_kernel<7, 16, 4>))
         : (s == 20 ? pick(csr_spmm_wing_kernel<20, 4, 8>, csr_spmm_wing_kernel<20, 8, 8>,
                           csr_spmm_wing_kernel<20, 16, 8>)
+           : s == 12 ? pick(csr_spmm_wing_kernel<12, 4, 8>, csr_spmm_wing_kernel<12, 8, 8>,
+                            csr_spmm_wing_kernel<12, 16, 8>)
            : s == 11 ? pick(csr_spmm_wing_kernel<11, 4, 8>, csr_spmm_wing_kernel<11, 8, 8>,
                             csr_spmm_wing_kernel<11, 16, 8>)
+           : s == 8 ? pick(csr_spmm_wing_kernel<8, 4, 8>, csr_spmm_wing_kernel<8, 8, 8>,
+                           csr_spmm_wing_kernel<8, 16, 8>)
                      : pick(csr_spmm_wing_kernel<7, 4, 8>, csr_spmm_wing_kernel<7, 8, 8>,
                             csr_spmm_wing_kernel<7, 16, 8>));
     hipLaunchKernelGGL(kfn, dim3((unsigned)sp->win_nblk), dim3(64 * tpr), lds, st, sp->indptr,
@@ -1197,10 +1217,8 @@ static int msgram_impl(gpmi_sp* sp, const double* etas, int neta, const double* 
   Guard g(sp->device);
   const int64_t n = sp->n;
   const int S = neta;
-  // an odd block that would run the one-column gather SpMM gets a zero column (an
-  // inactive CG column from the start: ||b|| = 0) so that the column-pair gather
-  // runs (cfg 5, s = 11 -> 12); the Gram of the real columns is unchanged
-  // GPMI_MSGRAM_PAD=1: an odd block that would run the one-column gather SpMM gets a
+  // Padding (the Gram of the real columns is unchanged by a zero column, inactive
+  // from the start: ||b|| = 0). GPMI_MSGRAM_PAD=1: an odd block that would run the one-column gather SpMM gets a
   // zero column (an inactive CG column from the start: ||b|| = 0) so that the
   // column-pair gather runs; measured slower at cfg 5 (s = 11 gather 119 us, s = 12
   // pair 161 us per launch), so off by default
@@ -1212,6 +1230,14 @@ static int msgram_impl(gpmi_sp* sp, const double* etas, int neta, const double* 
     const char* penv = std::getenv("GPMI_MSGRAM_PAD");
     if (full && kind == 0 && (s & 1) && s + 1 <= MS_MAXS && S * (s + 1) <= 1024 && penv &&
         std::atoi(penv) == 1)
+      ++s;
+    // the window SpMM at s = 11 stages 12-column rows with 16-byte loads (a zero
+    // column, stopped from the start): cfg 5 s = 11 88 -> 73 us per launch, step 21.7 ->
+    // 20.9 ms; s = 7 -> 8 measured neutral at cfg 4, only with GPMI_MSGRAM_PAD=2
+    // (GPMI_MSGRAM_PAD=0: no padding)
+    const int pmode = penv ? std::atoi(penv) : -1;
+    if (full && kind == 5 && (s == 11 || (s == 7 && pmode == 2)) && S * (s + 1) <= 1024 &&
+        pmode != 0 && pmode != 1)
       ++s;
   }
   // the dot columns: all of B (with the padding column when the full block is padded)
