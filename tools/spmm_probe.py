@@ -22,7 +22,7 @@ for name in sys.argv[1:] or ['sparse5', 'sparse4']:
     D = generate_correlation(pts, rho, 1.5, sparse=True, density=dens, device_resident=True)
     sop = D.op
     n, nnz = sop.n, sop.nnz
-    for s in (20, 11, 7):
+    for s in (20, 12, 11):
         alg = 12.0 * nnz + 4.0 * (n + 1) + 16.0 * n * s
         for label, env in SETTINGS:
             keep = {k: os.environ.get(k) for k in ('GPMI_SPMM_WING', 'GPMI_SPMM_WINDOW',
