@@ -330,14 +330,15 @@ def sparse_step_bytes(n, nnz, s_lanczos, steps, s_cg, cg_iters):
     (k basis blocks, u, y read; v_k, u written: (k + 4) b_L), then one final dot
     pass over the basis and u ((steps + 1) b_L). Multi-shift CG (b_C = 8 n s_C,
     s_C the device width: a full 11-column block on the window SpMM is padded
-    by one zero column) per iteration: the SpMM, p . q (2 b_C), the r
-    update (3 b_C), the B^T r / r . r dots (2 b_C) and p = r + beta p (3 b_C)."""
+    by one zero column) per iteration: the SpMM (p . q in its epilogue), the
+    r update with B^T r / r . r on MFMA (b, r, q read, r written: 4 b_C) and
+    p = r + beta p (3 b_C)."""
     csr = 12.0 * nnz + 8.0 * (n + 1)
     bl, bc = 8.0 * n * s_lanczos, 8.0 * n * s_cg
     lanczos = sum(csr + 2 * bl + (k + 2) * bl + (k + 4) * bl for k in range(steps)) + \
         (steps + 1) * bl
     basis = sum(2.0 * k * bl for k in range(steps)) + steps * bl
-    cg = cg_iters * (csr + 2 * bc + 10 * bc)
+    cg = cg_iters * (csr + 2 * bc + 7 * bc)
     return {'lanczos': lanczos, 'lanczos_basis_reads': basis, 'cg': cg,
             'total': lanczos + cg}
 

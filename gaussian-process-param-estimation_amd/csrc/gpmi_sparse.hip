@@ -893,16 +893,24 @@ template __global__ void lz_dots_kernel<true>(const double*, int64_t, int, int, 
 // in u_{k+1}, times -1), ir[s] = 1 / rho; alpha / beta [c][steps] as lanczos_scalar;
 // inexact[c]: sigma - s.s lost more than six digits to cancellation (rho then
 // unreliable; the host reruns the block with CGS2).
-__global__ void lz_scalar_kernel(const double* __restrict__ d, int k, int steps, int s,
+// stage: the host gave (2k + 2) s doubles of dynamic LDS, and d is read from there
+// (the phases' per-column loops over the dots then wait on LDS, not L2).
+__global__ void lz_scalar_kernel(const double* __restrict__ dg, int k, int steps, int s,
                                  double* __restrict__ H, double* __restrict__ cv,
                                  double* __restrict__ cu, double* __restrict__ ir,
                                  double* __restrict__ rho_s, int* __restrict__ dead,
                                  int* __restrict__ inexact, double* __restrict__ alpha,
-                                 double* __restrict__ beta) {
+                                 double* __restrict__ beta, int stage) {
+  extern __shared__ double sdots[];
   const int ld = steps + 1;
   const size_t hsz = (size_t)(steps + 2) * ld;
   const int J = k;
   const int t = threadIdx.x;
+  if (stage) {
+    for (int i = t; i < (2 * J + 2) * s; i += blockDim.x) sdots[i] = dg[i];
+    __syncthreads();
+  }
+  const double* d = stage ? sdots : dg;
   if (t < s) {
     const int c = t;
     if (k == 0) {

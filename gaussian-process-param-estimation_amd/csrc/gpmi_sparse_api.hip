@@ -65,7 +65,7 @@ template <bool NT>
 __global__ void lz_dots_kernel(const double*, int64_t, int, int, const double*, const double*,
                                int64_t, int, int, double*);
 __global__ void lz_scalar_kernel(const double*, int, int, int, double*, double*, double*, double*,
-                                 double*, int*, int*, double*, double*);
+                                 double*, int*, int*, double*, double*, int);
 template <int NR, bool NT>
 __global__ void lz_update_kernel(double*, int64_t, int, double*, const double*, const double*,
                                  const double*, const double*, int);
@@ -611,8 +611,10 @@ int lanczos_block_dcgs2(gpmi_sp* sp, double* V, double* U, double* Y, int s, int
     hipLaunchKernelGGL(col_dot_reduce_kernel, dim3((nv * s + 3) / 4), dim3(256), 0, sp->stream,
                        sp->partial, lz_nb, nv, s, d);
     SP_LAUNCH("col_dot_reduce_kernel");
-    hipLaunchKernelGGL(lz_scalar_kernel, dim3(1), dim3(1024), 0, sp->stream, d, k, steps, s, H, cv,
-                       cu, ir, rho, dead, inex, dal, dbe);
+    const size_t sdb = sizeof(double) * (size_t)(2 * k + 2) * s;   // the dots in LDS
+    const int stage = sdb <= 64 * 1024 ? 1 : 0;
+    hipLaunchKernelGGL(lz_scalar_kernel, dim3(1), dim3(1024), stage ? sdb : 0, sp->stream, d, k,
+                       steps, s, H, cv, cu, ir, rho, dead, inex, dal, dbe, stage);
     SP_LAUNCH("lz_scalar_kernel");
     if (!last) {
       if (lz_nr == 4) {
@@ -1309,12 +1311,14 @@ static int msgram_impl(gpmi_sp* sp, const double* etas, int neta, const double* 
   double* Pd = Rd + ns;
   double* Qd = Pd + ns;
   double* Rd2 = Qd + ns;   // the residual alternates between Rd and Rd2
-  // fused p . q reduction + r update + dots for <= 2 column groups of 4 of B (the
-  // fused kernel re-reads q once per group)
-  const bool fused_r = (nbd + 3) / 4 <= 2;
-  // wider blocks: the MFMA form (GPMI_MS_MFMA=0 keeps the separate update and dots)
+  // The r update and B^T r, r . r on MFMA in one pass (ms_rmfma_kernel, s <= 16: every
+  // block the library forms). GPMI_MS_MFMA=0: the fused scalar form for <= 2 column groups
+  // of 4 of B (ms_rdots_partial_kernel, which re-reads q once per group; the default
+  // before: cfg 4 6.9-7.3 ms per step against 6.3 with the MFMA form), else the separate
+  // update and dots
   const char* menv = std::getenv("GPMI_MS_MFMA");
-  const bool mfma_r = !fused_r && s <= 16 && !(menv && std::atoi(menv) == 0);
+  const bool mfma_r = s <= 16 && !(menv && std::atoi(menv) == 0);
+  const bool fused_r = !mfma_r && (nbd + 3) / 4 <= 2;
   // chip-wide partial reduction for the MFMA form's 512 partial rows (cfg 5: step
   // 33.6 -> 32.0 ms); the fused form's 128 stay in the scalar kernel (cfg 4: the
   // extra launch costs more than it saves). GPMI_MS_RED=0 / 1 forces either.

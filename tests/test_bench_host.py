@@ -54,5 +54,5 @@ def test_sparse_step_bytes_model():
     lz += 4 * bl
     assert b['lanczos'] == lz
     assert b['lanczos_basis_reads'] == sum(2 * k * bl for k in range(3)) + 3 * bl
-    assert b['cg'] == 10 * (csr + 12 * bc)
+    assert b['cg'] == 10 * (csr + 9 * bc)
     assert b['total'] == b['lanczos'] + b['cg']

@@ -183,6 +183,33 @@ def test_msgram_column_shards_equal_full(gp):
         assert _nrel(g, ex) < 1e-9
 
 
+def test_msgram_iteration_forms_agree(gp, monkeypatch):
+    """The multi-shift CG's r update + dots: the MFMA form (default, ms_rmfma_kernel;
+    its partials summed across the chip or, GPMI_MS_RED=0, in the scalar kernel) and
+    GPMI_MS_MFMA=0's scalar forms (fused ms_rdots_partial_kernel for <= 8 columns,
+    the separate update and dots above) give the same Gram to rounding, and the
+    exact solve's."""
+    from gaussian_proc import _hip
+    _, K = _small_sparse()
+    n = K.shape[0]
+    sop = _hip.SparseOperator.from_csr(K)
+    rng = numpy.random.RandomState(3)
+    etas = numpy.array([2.5, 7.0, 40.0])
+    for s in (3, 7, 11):
+        B = rng.randn(n, s)
+        G = sop.msgram(etas, B, rtol=1e-10)
+        for env in ({'GPMI_MS_RED': '0'}, {'GPMI_MS_MFMA': '0'}):
+            for k, v in env.items():
+                monkeypatch.setenv(k, v)
+            Gf = sop.msgram(etas, B, rtol=1e-10)
+            for k in env:
+                monkeypatch.delenv(k)
+            assert _nrel(Gf, G) < 1e-11, (s, env)
+        for e, g in zip(etas, G):
+            ex = B.T @ scipy.sparse.linalg.spsolve((K + e * scipy.sparse.eye(n)).tocsc(), B)
+            assert _nrel(g, ex) < 1e-9, (s, e)
+
+
 def test_msgram_stopped_column_and_overflowing_windows(gp):
     """The multi-shift CG on the window SpMM (csr_spmm_wing_kernel at s = 7 and 11)
     over a matrix whose first blocks overflow the window (the gather branch), with a
