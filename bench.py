@@ -13,7 +13,11 @@ timed region (inputs resident in HBM). ``--scaling weak`` instead gives every
 rank ``--eta-per-rank`` eta of a finer grid (fixed per-rank work).
 
 Launch: python bench.py [--gpus 1 --steps K --warmup W]
+        python bench.py --gpus N ...      (starts the N ranks itself: launch_ranks)
         python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+The world size must equal --gpus; each rank uses device LOCAL_RANK and the line
+lists them (``devices``). At N > 1 the line holds the dense curve, the band mode
+and the sparse configs 4 and 5 (probe and right-hand-side column shards).
 """
 
 import argparse
@@ -69,6 +73,12 @@ def parse():
                     help='band mode: eta values per rank per step (one reduction per step)')
     ap.add_argument('--no-timing', action='store_true',
                     help='skip the per-kernel HIP-event roofline timing')
+    ap.add_argument('--out-json', default=None,
+                    help='also write the JSON line (rank 0) to this file')
+    ap.add_argument('--launch-check', action='store_true',
+                    help='check the N-rank launch only (no device): world size against '
+                         '--gpus, the eta blocks and the all-gather / max-time collectives '
+                         'over gloo; prints one JSON line')
     ap.add_argument('--no-sparse', action='store_true',
                     help='dense run: skip the sparse_modes block (configs 4 and 5, N=1 only)')
     return ap.parse_args()
@@ -174,6 +184,15 @@ def log(msg):
     """Progress on stderr (the JSON result is the only stdout line)."""
     sys.stderr.write('[bench] %s\n' % msg)
     sys.stderr.flush()
+
+
+def emit(args, line):
+    """The ONE stdout JSON line (rank 0); with --out-json also into that file."""
+    txt = json.dumps(line)
+    print(txt, flush=True)
+    if getattr(args, 'out_json', None):
+        with open(args.out_json, 'w') as fh:
+            fh.write(txt + '\n')
 
 
 def _timed(fn, reps, what=None):
@@ -350,13 +369,14 @@ SPARSE_CONFIGS = {
 }
 
 
-def run_sparse(args, world, rank, local, dist, torch):
+def run_sparse(args, world, rank, local, dist, torch, devices=None):
     """``--config sparse4|sparse5``: the sparse line alone (sparse_measure)."""
     res = sparse_measure(args, args.config, world, rank, local, dist, torch,
                          cpu=world == 1 and not args.no_cpu_baseline, exact=True)
     if rank == 0:
-        print(json.dumps(res), flush=True)
-    if world > 1:
+        res['devices'] = devices
+        emit(args, res)
+    if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
 
@@ -413,13 +433,13 @@ def sparse_measure(args, config, world, rank, local, dist, torch, cpu, exact, de
 
     for _ in range(args.warmup):
         step()
-    if world > 1:
+    if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         last = step()
-    if world > 1:
+    if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
@@ -462,9 +482,10 @@ def sparse_measure(args, config, world, rank, local, dist, torch, cpu, exact, de
                            if s_blk == 20 else (None, None))
     my_probes = shard(nprobe, world, rank)
     # the library pads a full 11-column block on the window SpMM to 12 (msgram_impl);
-    # a column shard (N > 1) runs unpadded
-    s_cg = R.shape[1] + (1 if (world == 1 and R.shape[1] == 11 and
-                               op.sop.spmm_kernel(11) == 'csr_spmm_wing_kernel') else 0)
+    # a column shard (N > 1) runs unpadded: rank 0's shard width
+    clo0, chi0, _ = shard(R.shape[1], world, 0)
+    s_cg = (chi0 - clo0) + (1 if (world == 1 and R.shape[1] == 11 and
+                                  op.sop.spmm_kernel(11) == 'csr_spmm_wing_kernel') else 0)
     sb = sparse_step_bytes(n, nnz, my_probes[1] - my_probes[0], steps, s_cg,
                            holder['cg_iters'])
     step_s = dt / args.steps
@@ -484,7 +505,8 @@ def sparse_measure(args, config, world, rank, local, dist, torch, cpu, exact, de
                        'n': n, 'nnz': nnz, 'nnz_per_row': nnz / float(n), 'tau': D.tau,
                        'lambda_min_ritz': theta_min, 'eta_shift': shift,
                        'assembly_s': t_asm,
-                       'parallelism': 'probe + eta shards x%d + all-gather' % world},
+                       'parallelism': ('probe shards + right-hand-side column shards x%d, '
+                                       'all-gathers' % world) if world > 1 else 'one GPU'},
             'roofline': {'bound': 'hbm', 'achieved': round(gbs, 1), 'peak': HBM_PEAK_GBS,
                          'unit': 'GB/s', 'frac': round(gbs / HBM_PEAK_GBS, 4),
                          'traffic': None if sp_traffic is None else round(sp_traffic),
@@ -554,16 +576,22 @@ def cpu_baseline_leg(res, holder, csr, X, z, etas, nprobe, steps, seed, budget_s
     res['speedup_vs_cpu'] = round(res['value'] / cb['value'], 1)
 
 
-def sparse_modes(args, local, dist, torch):
-    """The sparse configs 4 and 5 in the default (dense) line at N=1, each with
-    its own value, step time, SpMM and whole-step rooflines, reference check and
+def sparse_modes(args, world, rank, local, dist, torch):
+    """The sparse configs 4 and 5 in the default (dense) line, each with its own
+    value, step time, SpMM and whole-step rooflines, reference check and (N=1)
     thread-pool CPU baseline (sparse_measure; the exact-Cholesky leg of the
-    reference check is left to --config sparse4)."""
+    reference check is left to --config sparse4). At N > 1 every rank runs its
+    probe shard and right-hand-side column shard (BASELINE cfg5: "sharded over
+    8 x MI355X with RCCL all-gather"); rank 0 returns the lines, the others None."""
     out, res = {}, {}
     for cfg in ('sparse4', 'sparse5'):
-        res[cfg] = sparse_measure(args, cfg, 1, 0, local, dist, torch,
-                                  cpu=not args.no_cpu_baseline, exact=False, defer_cpu=True)
-        log('%s: %.1f evals/s' % (cfg, res[cfg]['value']))
+        res[cfg] = sparse_measure(args, cfg, world, rank, local, dist, torch,
+                                  cpu=world == 1 and not args.no_cpu_baseline, exact=False,
+                                  defer_cpu=True)
+        if rank == 0:
+            log('%s: %.1f evals/s' % (cfg, res[cfg]['value']))
+    if rank != 0:
+        return None
     # the CPU baselines after both device measurements
     for cfg in ('sparse4', 'sparse5'):
         leg = res[cfg].pop('_cpu_leg', None)
@@ -571,9 +599,11 @@ def sparse_modes(args, local, dist, torch):
             leg()
     for cfg in ('sparse4', 'sparse5'):
         r = res[cfg]
-        out[cfg] = {k: r[k] for k in ('metric', 'value', 'unit', 'ms_per_step', 'steps',
-                                      'warmup', 'roofline', 'step_roofline', 'cpu_baseline',
-                                      'lp_sample', 'lanczos_orthogonalize') if k in r}
+        out[cfg] = {k: r[k] for k in ('metric', 'value', 'unit', 'n_gpus', 'ms_per_step',
+                                      'steps', 'warmup', 'scaling', 'roofline',
+                                      'step_roofline', 'cpu_baseline', 'lp_sample',
+                                      'lanczos_orthogonalize') if k in r}
+        out[cfg]['parallelism'] = r['config']['parallelism']
         out[cfg]['workload'] = r['config']['workload']
         out[cfg]['assembly_s'] = r['config']['assembly_s']
         for k in ('reference_check', 'speedup_vs_cpu'):
@@ -680,8 +710,8 @@ def eta_block(args, world, rank, s=0):
 
 def max_over_ranks(dt, world, dist, torch):
     """Wall time of the slowest rank (all-reduce MAX; a device tensor on RCCL,
-    a host tensor on gloo)."""
-    if world == 1:
+    a host tensor on gloo). ``dist`` None: no process group."""
+    if dist is None:
         return dt
     dev = 'cuda' if dist.get_backend() == 'nccl' else 'cpu'
     t_max = torch.tensor([dt], dtype=torch.float64, device=dev)
@@ -694,7 +724,7 @@ def gather_rows(rows, world, dist, torch):
     the nccl backend, gloo on CPU in the tests): gaussian_proc.sweep's
     collective. Returns the [world * rows, 3] host array on every rank."""
     rows = numpy.ascontiguousarray(rows)
-    if world == 1:
+    if dist is None:
         torch.cuda.synchronize()
         return rows
     from gaussian_proc.sweep import _all_gather_rows
@@ -730,14 +760,14 @@ def band_mode(args, D, X, z, world, rank, dist, torch, ld_ref=None):
 
     for s in range(args.warmup):
         step(s, False)
-    if world > 1:
+    if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     own = E = 0
     for s in range(args.steps):
         last, own, E = step(args.warmup + s, True)
-    if world > 1:
+    if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
@@ -945,31 +975,140 @@ def batch_efficiency(op, X, z, batches=(8, 16, 32)):
     return out
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args, argv=None):
+    """``--gpus N`` (N > 1) started as a plain ``python bench.py --gpus N``: run
+    the N ranks, one process per GPU, under ``torch.distributed.run`` as a CHILD
+    process (rendezvous on 127.0.0.1), forward its output and return its exit
+    code. This process never touches a device (no HIP call before the ranks
+    exist, none after), so the launch is the same one the driver makes itself."""
+    import subprocess
+    argv = sys.argv[1:] if argv is None else list(argv)
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1',
+           '--nproc-per-node', str(args.gpus), '--master-addr', '127.0.0.1',
+           '--master-port', str(_free_port()), os.path.abspath(__file__)] + argv
+    log('launching %d ranks: %s' % (args.gpus, ' '.join(cmd[1:])))
+    return subprocess.call(cmd)
+
+
+def rank_devices(args, world, rank, local, dist, torch):
+    """Check the launch against ``--gpus`` and name the device every rank uses.
+    Fails loudly (SystemExit) when the job's world size is not ``--gpus`` or
+    fewer devices are visible than ranks need. Returns the per-rank list
+    (gathered at N > 1) for the line's ``devices``."""
+    share = os.environ.get('GPMI_BENCH_SHARE_DEVICE') == '1'
+    if world != args.gpus:
+        raise SystemExit('bench: --gpus %d but the job has %d ranks (WORLD_SIZE)'
+                         % (args.gpus, world))
+    visible = torch.cuda.device_count()
+    need = 1 if share else max(world, local + 1)
+    if visible < need:
+        raise SystemExit('bench: %d ranks need %d visible devices, %d visible'
+                         % (world, need, visible))
+    props = torch.cuda.get_device_properties(local)
+    me = {'rank': rank, 'local_rank': int(os.environ.get('LOCAL_RANK', '0')), 'device': local,
+          'name': props.name, 'pci_bus_id': getattr(props, 'pci_bus_id', None),
+          'uuid': str(getattr(props, 'uuid', '')), 'host': platform.node(),
+          'shared_device': share}
+    if dist is None:
+        return [me]
+    out = [None] * world
+    dist.all_gather_object(out, me)
+    if not share and world > 1:
+        ids = {(d['host'], d['uuid'] or d['device']) for d in out}
+        if len(ids) != world:
+            raise SystemExit('bench: ranks share a device: %s' % out)
+    return out
+
+
+def launch_check(args, world, rank, torch):
+    """``--launch-check``: the multi-rank plumbing of the line without a device
+    (CPU box, gloo): the world size against --gpus, each rank's eta block of the
+    strong-scaled curve, the ONE all-gather of the rows and the max-over-ranks
+    time. Rank 0 prints {n_gpus, ranks, curve_etas, ...}."""
+    dist = None
+    if world > 1:
+        dist = torch.distributed
+        dist.init_process_group('gloo')
+    if world != args.gpus or (dist is not None and dist.get_world_size() != args.gpus):
+        raise SystemExit('bench: --gpus %d but the job has %d ranks' % (args.gpus, world))
+    from gaussian_proc.sweep import shard
+    t0 = time.perf_counter()
+    etas, own, per, gsize = eta_block(args, world, rank)
+    rows = numpy.stack([etas, numpy.full(per, float(rank)), numpy.arange(per, dtype=float)],
+                       axis=1)
+    if dist is None:
+        allrows = rows
+    else:
+        from gaussian_proc.sweep import _all_gather_rows
+        allrows = _all_gather_rows(dist, None, rows, world)
+    dt = max_over_ranks(time.perf_counter() - t0, world, dist, torch)
+    owns = [shard(gsize, world, r)[1] - shard(gsize, world, r)[0] for r in range(world)] \
+        if args.scaling == 'strong' else [per] * world
+    curve = numpy.concatenate([allrows[r * per:r * per + owns[r], 0] for r in range(world)])
+    if rank == 0:
+        print(json.dumps({'launch_check': True, 'n_gpus': world, 'gpus_arg': args.gpus,
+                          'ranks': sorted({int(v) for v in allrows[:, 1]}),
+                          'eta_per_rank': per, 'curve_etas': curve.tolist(),
+                          'max_rank_s': dt}), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    if args.gpus < 1:
+        raise SystemExit('bench: --gpus must be >= 1')
+    if args.gpus > 1 and 'WORLD_SIZE' not in os.environ:
+        # plain `python bench.py --gpus N`: start the N ranks (child process)
+        sys.exit(launch_ranks(args))
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
     import torch
-    import torch.distributed as dist
+    import torch.distributed
+    if args.launch_check:
+        return launch_check(args, world, rank, torch)
     # one process per GPU over RCCL; GPMI_BENCH_BACKEND=gloo with
     # GPMI_BENCH_SHARE_DEVICE=1 rehearses the N>1 flow with every rank on
-    # device 0 (the one-GPU box), host-side collectives
+    # device 0 (the one-GPU box), host-side collectives. GPMI_BENCH_PG=1 creates
+    # the process group (and its collectives) at N = 1 too: the RCCL
+    # communicator's streams beside the measured kernels, on one GPU
     backend = os.environ.get('GPMI_BENCH_BACKEND', 'nccl')
     if os.environ.get('GPMI_BENCH_SHARE_DEVICE') == '1':
         local = 0
     torch.cuda.set_device(local)
-    if world > 1:
+    dist = None
+    if world > 1 or os.environ.get('GPMI_BENCH_PG') == '1':
+        dist = torch.distributed
+        if world == 1:
+            # a one-rank group of a plain `python bench.py` (env:// rendezvous)
+            for k, v in (('RANK', '0'), ('WORLD_SIZE', '1'), ('MASTER_ADDR', '127.0.0.1'),
+                         ('MASTER_PORT', str(_free_port()))):
+                os.environ.setdefault(k, v)
         if backend == 'nccl':
             dist.init_process_group('nccl', device_id=torch.device('cuda', local))
         else:
             dist.init_process_group(backend)
+        if dist.get_world_size() != world:
+            raise SystemExit('bench: process group has %d ranks, WORLD_SIZE %d'
+                             % (dist.get_world_size(), world))
+    devices = rank_devices(args, world, rank, local, dist, torch)
 
     if args.config != 'dense':
-        return run_sparse(args, world, rank, local, dist, torch)
+        return run_sparse(args, world, rank, local, dist, torch, devices)
 
     def barrier():
-        if world > 1:
+        if dist is not None:
             dist.barrier()
         torch.cuda.synchronize()
 
@@ -1085,6 +1224,7 @@ def main():
             'flops_per_eval': flops_eval,
             'lp_sample': [float(v) for v in last[0].tolist()] if last is not None else None,
             'cpu_baseline': None,
+            'devices': devices,
         }
         if args.scaling == 'strong':
             result['time_to_curve_ms'] = dt / args.steps * 1e3
@@ -1123,13 +1263,15 @@ def main():
         result['band_mode']['optimizer'] = optimizer_timing(D, X, z)
     if rank == 0 and world == 1 and not args.no_band and args.nu == 1.5:
         result['band_mode']['nu25_check'] = band_nu25_check(D, points, X, z)
-    if world == 1 and not args.no_sparse:
+    if not args.no_sparse:
         # release the dense and band operators (their streams count against the
         # process's hardware queues) before the sparse configs run
         if not args.no_band:
             bop.band().close()
         op.op.close()
-        result['sparse_modes'] = sparse_modes(args, local, dist, torch)
+        sm = sparse_modes(args, world, rank, local, dist, torch)
+        if rank == 0:
+            result['sparse_modes'] = sm
     if lp_dev is not None:
         # after every device measurement (its thread pool's leftovers slow the launch-bound
         # sparse steps); CPU and GPU agree on the same evaluation
@@ -1138,8 +1280,8 @@ def main():
         result['cpu_baseline'] = cb
         result['speedup_vs_cpu'] = round(result['value'] / cb['value'], 1)
     if rank == 0:
-        print(json.dumps(result), flush=True)
-    if world > 1:
+        emit(args, result)
+    if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
 

@@ -174,16 +174,23 @@ def slq_gram_sweep(K_mixed, etas, R, rtol=1e-6, group=None, split='columns'):
     scalars only divide).
 
     Returns (curves, (lo, hi), G[hi - lo, s, s]): slq_sweep's curves on every
-    rank, and this rank's contiguous eta block with its Gram blocks."""
+    rank, and this rank's contiguous eta block with its Gram blocks.
+
+    The multi-shift CG's negative-curvature check (``LinAlgError``) depends on
+    the right-hand sides, so on several ranks it can fire on one rank only: that
+    rank still joins the collectives with an error flag, and every rank raises
+    after them (as der1_sweep)."""
     from concurrent.futures import ThreadPoolExecutor
     etas = numpy.atleast_1d(numpy.asarray(etas, dtype=float))
     R = numpy.asarray(R, dtype=float)
     R2 = R[:, None] if R.ndim == 1 else R
     s = R2.shape[1]
     dist, world, rank = _group(group)
+    multi = dist is not None and world > 1
     lo, hi, _ = shard(etas.size, world, rank)
-    by_cols = world > 1 and split == 'columns'
+    by_cols = multi and split == 'columns'
     clo, chi, cper = shard(s, world, rank)
+    err = None
     with ThreadPoolExecutor(1) as ex:
         if by_cols:
             fut = (ex.submit(K_mixed.sop.msgram, etas, R2, rtol, None, (clo, chi))
@@ -193,15 +200,35 @@ def slq_gram_sweep(K_mixed, etas, R, rtol=1e-6, group=None, split='columns'):
         try:
             curves = slq_sweep(K_mixed, etas, group=group)
         finally:
-            G = fut.result() if fut is not None else None
+            try:
+                G = fut.result() if fut is not None else None
+            except numpy.linalg.LinAlgError as e:
+                if not multi:
+                    raise
+                err, G = e, None
     if by_cols:
-        # one row per column c (its G[:, :, c] flattened), cper rows per rank; the
-        # all-gather runs after the Lanczos's (collectives in the same order on
-        # every rank, from the main thread)
-        local = numpy.zeros((cper, etas.size * s))
+        # one row per column c (its G[:, :, c] flattened) plus an error flag, cper
+        # rows per rank; the all-gather runs after the Lanczos's (collectives in the
+        # same order on every rank, from the main thread)
+        local = numpy.zeros((cper, etas.size * s + 1))
         if G is not None:
-            local[:chi - clo] = G.transpose(2, 0, 1).reshape(chi - clo, -1)
+            local[:chi - clo, :-1] = G.transpose(2, 0, 1).reshape(chi - clo, -1)
+        if err is not None:
+            local[:, -1] = 1.0
         allv = _all_gather_rows(dist, group, local, world)
+        flags = allv[:, -1]
+        allv = allv[:, :-1]
+    elif multi:
+        # the eta split has no collective of its own: one flag per rank
+        flags = _all_gather_rows(dist, group, numpy.array([[1.0 if err else 0.0]]), world)
+    if multi:
+        if err is not None:
+            raise err
+        if flags.any():
+            raise numpy.linalg.LinAlgError(
+                'K + eta I is not positive definite: negative curvature in another '
+                'rank\'s multi-shift CG')
+    if by_cols:
         Gf = numpy.empty((etas.size, s, s))
         for r in range(world):
             a, b, _ = shard(s, world, r)

@@ -1,16 +1,19 @@
 """Host-side pieces of bench.py (CPU): the thread-pool sparse CPU baseline
-reproduces the oracle's SLQ logdet with the device's probes, and the sparse
-step byte model counts what its docstring says."""
+reproduces the oracle's SLQ logdet with the device's probes, the sparse step
+byte model counts what its docstring says, and ``--gpus N`` starts and checks
+N ranks."""
 
 import os
 import sys
 
 import numpy
+import pytest
 import scipy.sparse
 import scipy.sparse.linalg
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import bench  # noqa: E402
+BENCH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'bench.py')
 from oracle import sparse as osp  # noqa: E402
 
 
@@ -56,3 +59,40 @@ def test_sparse_step_bytes_model():
     assert b['lanczos_basis_reads'] == sum(2 * k * bl for k in range(3)) + 3 * bl
     assert b['cg'] == 10 * (csr + 9 * bc)
     assert b['total'] == b['lanczos'] + b['cg']
+
+
+def _json_line(out):
+    lines = [l for l in out.splitlines() if l.startswith('{')]
+    assert lines, out
+    import json
+    return json.loads(lines[-1])
+
+
+@pytest.mark.parametrize('world', [2, 3])
+def test_bench_gpus_n_launches_n_ranks(world):
+    """`python bench.py --gpus N` (no torch.distributed environment) starts N
+    ranks itself (launch_ranks: torch.distributed.run as a child process), every
+    rank checks the world size against --gpus, and the gathered eta blocks cover
+    the 64-point curve once, in order (--launch-check: no device, gloo)."""
+    import subprocess
+    env = dict(os.environ)
+    for k in ('WORLD_SIZE', 'RANK', 'LOCAL_RANK', 'MASTER_ADDR', 'MASTER_PORT'):
+        env.pop(k, None)
+    out = subprocess.run([sys.executable, BENCH, '--gpus', str(world), '--launch-check'],
+                         env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    d = _json_line(out.stdout)
+    assert d['n_gpus'] == world and d['gpus_arg'] == world
+    assert d['ranks'] == list(range(world))
+    numpy.testing.assert_array_equal(d['curve_etas'], numpy.logspace(-3, 3, 64))
+
+
+def test_bench_rejects_world_size_other_than_gpus():
+    """A job whose world size is not --gpus fails loudly instead of reporting
+    the wrong n_gpus."""
+    import subprocess
+    env = dict(os.environ, WORLD_SIZE='1', RANK='0', LOCAL_RANK='0')
+    out = subprocess.run([sys.executable, BENCH, '--gpus', '2', '--launch-check'],
+                         env=env, capture_output=True, text=True, timeout=120)
+    assert out.returncode != 0
+    assert '--gpus 2 but the job has 1 ranks' in out.stderr

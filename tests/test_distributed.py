@@ -358,3 +358,59 @@ def test_slq_gram_sweep_gloo():
             numpy.testing.assert_allclose(c[k], curves[k], rtol=1e-12)
         blocks.append(g)
     numpy.testing.assert_allclose(numpy.concatenate(blocks), G, rtol=1e-12)
+
+
+class _FakeSparseGramCurv(_FakeSparseGram):
+    """msgram that meets negative curvature on the last right-hand-side column
+    (the device check depends on the columns a rank solves)."""
+
+    def msgram(self, etas, R, rtol=1e-6, maxiter=None, cols=None):
+        c_hi = R.shape[1] if cols is None else cols[1]
+        if c_hi == R.shape[1]:
+            raise numpy.linalg.LinAlgError('negative curvature p^T (K + eta I) p <= 0')
+        return _FakeSparseGram.msgram(self, etas, R, rtol, maxiter, cols)
+
+
+def _slq_gram_curv_worker(rank, world, port, etas, split, out_q):
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    from gaussian_proc.sweep import slq_gram_sweep
+    K, X, z = _problem()
+    R = numpy.column_stack([X, z])
+    op = _SparseMixed(K + 0.5 * numpy.eye(K.shape[0]))
+    op.sop = _FakeSparseGramCurv(op.sop.K, 12)
+    outs = []
+    try:
+        slq_gram_sweep(op, etas, R, split=split)
+        outs.append('ok')
+    except numpy.linalg.LinAlgError:
+        outs.append('LinAlgError')
+    # the group is still usable afterwards: a clean all-gather in step
+    from gaussian_proc.sweep import _all_gather_rows
+    outs.append(_all_gather_rows(dist, None, numpy.array([[float(rank)]]), world).ravel().tolist())
+    out_q.put((rank, outs))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('split', ['columns', 'eta'])
+def test_slq_gram_sweep_curvature_on_one_rank_raises_everywhere_gloo(split):
+    """Negative curvature in ONE rank's multi-shift CG (its column shard holds the
+    offending right-hand side, or only its eta block runs the full CG): every rank
+    raises LinAlgError after the collectives, none is left blocked in one."""
+    etas = numpy.array([0.5, 1.0, 2.0, 4.0])
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_slq_gram_curv_worker, args=(r, 2, port, etas, split, q))
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for _, outs in res:
+        assert outs[0] == 'LinAlgError'
+        assert outs[1] == [0.0, 1.0]

@@ -1,13 +1,59 @@
 """Summarise a rocprofv3 --kernel-trace CSV (kernel_trace.csv): per-kernel
 count / total / average device time over the last `window` of the trace (a
 time window ending at the last dispatch, default: everything), and the union of
-busy intervals (GPU-busy fraction) in that window."""
+busy intervals (GPU-busy fraction) in that window.
+
+``--timed-syrk <trace dir> <bench json>``: the headline kernel's launches of the
+bench's timed region from a trace of ``bench.py --no-band --no-sparse``: the
+batch-B ``syrk_kernel`` dispatches (Grid_Size_Y = B, the eta batch) are
+(warmup + steps) x launches-per-step; the last steps x launches-per-step of them
+are the timed ones. Prints count / average / total against the bench line's
+HIP-event ``roofline.avg_launch_ms`` (JSON).
+"""
 import csv
+import glob
+import json
+import os
 import sys
 from collections import defaultdict
 
 
+def timed_syrk(trace_dir, bench_json):
+    with open(bench_json) as fh:
+        line = json.loads([l for l in fh if l.startswith('{')][-1])
+    roof = line['roofline']
+    B = line['config']['eta_per_rank_per_step']
+    steps, warm = line['steps'], line['warmup']
+    files = glob.glob(os.path.join(trace_dir, '**', '*kernel_trace.csv'), recursive=True)
+    rows = []
+    for f in files:
+        with open(f) as fh:
+            for r in csv.DictReader(fh):
+                if 'syrk_kernel' in r['Kernel_Name'] and 'band' not in r['Kernel_Name'] and \
+                        int(r['Grid_Size_Y']) == B:
+                    rows.append((int(r['Start_Timestamp']), int(r['End_Timestamp'])))
+    rows.sort()
+    per_step = roof['launches'] // steps
+    assert len(rows) == (warm + steps) * per_step, (len(rows), warm, steps, per_step)
+    timed = rows[warm * per_step:]
+    durs = [(e - s) / 1e6 for s, e in timed]
+    avg = sum(durs) / len(durs)
+    flops = roof['algorithmic_flops_per_launch']
+    out = {'trace_files': [os.path.relpath(f) for f in files], 'batch': B,
+           'launches_per_step': per_step, 'timed_launches': len(timed),
+           'trace_avg_launch_ms': round(avg, 4), 'trace_total_ms': round(sum(durs), 3),
+           'bench_avg_launch_ms': roof['avg_launch_ms'],
+           'rel_diff_vs_bench': round(avg / roof['avg_launch_ms'] - 1.0, 5),
+           'algorithmic_flops_per_launch': flops,
+           'trace_tflops': round(flops / (avg * 1e-3) / 1e12, 3),
+           'trace_frac_of_peak': round(flops / (avg * 1e-3) / 1e12 / roof['peak'], 4),
+           'bench_frac': roof['frac']}
+    print(json.dumps(out, indent=1))
+
+
 def main():
+    if sys.argv[1] == '--timed-syrk':
+        return timed_syrk(sys.argv[2], sys.argv[3])
     path = sys.argv[1]
     window_ms = float(sys.argv[2]) if len(sys.argv) > 2 else 0.0
     rows = []
