@@ -842,49 +842,66 @@ def torch_sync():
     torch.cuda.synchronize()
 
 
-def dense_slq_mode(D, etas, ld_exact, nprobe=20, steps=30, reps=3):
+def dense_slq_mode(D, etas, ld_exact, nprobe=20, steps=30, tol=1e-3, reps=3):
     """imate 'slq' on the resident dense K (gpmi_sp_create_dense): the logdet
-    curve over the same eta grid from ONE device Lanczos of nprobe probes x
-    steps (K X on fp64 MFMA, dense_mm_kernel: 8 n^2 bytes of K per product,
-    HBM-bound), against the dense Cholesky logdets of the headline line (in
-    standard errors of the probe mean). A logdet-curve leg, not an lp: the
-    likelihood's Gram blocks still take the exact solves (_linear_solver.py:71)."""
+    curve over the same eta grid from ONE device Lanczos of nprobe probes (K X on
+    fp64 MFMA, dense_mm_kernel: 8 n^2 bytes of K per product, HBM-bound), with
+    imate's ``lanczos_tol`` = tol: the degree doubles from ``steps`` until the
+    Gauss / Gauss-Radau gap of the probe-mean logdet quadrature at min(eta) is
+    within tol (MixedCorrelation.slq_converge; at N = 16384, nu = 1.5 the smooth
+    K needs ~240 steps at eta = 1e-3, where 30 steps left a 22 % bias). Checked
+    against the dense Cholesky logdets of the headline line in standard errors of
+    the probe mean. ``value``: the curve at the converged degree, degree search
+    included (``search_ms``) and alone at that degree (``curve_ms``). A
+    logdet-curve leg, not an lp: the likelihood's Gram blocks still take the
+    exact solves (_linear_solver.py:71)."""
     from gaussian_proc import _slq
     from gaussian_proc._mixed_correlation import MixedCorrelation
     op = MixedCorrelation(D, imate_method='slq',
-                          imate_options={'num_samples': nprobe, 'lanczos_degree': steps})
+                          imate_options={'num_samples': nprobe, 'lanczos_degree': steps,
+                                         'lanczos_tol': tol})
     n = op.n
+    torch_sync()
+    t0 = time.perf_counter()
+    conv = op.slq_converge(etas)
+    per = n * _slq.quadrature(op.slq_nodes(), etas, numpy.log)
+    t_search = time.perf_counter() - t0
+    deg = conv['degree']
+    fixed = MixedCorrelation(D, imate_method='slq',
+                             imate_options={'num_samples': nprobe, 'lanczos_degree': deg})
     times = []
-    for r in range(reps + 1):
-        op._nodes = None
+    for r in range(reps):
+        fixed._lz = None
         t0 = time.perf_counter()
-        nodes = op.slq_nodes()
-        per = n * _slq.quadrature(nodes, etas, numpy.log)
+        per_f = n * _slq.quadrature(fixed.slq_nodes(), etas, numpy.log)
         times.append(time.perf_counter() - t0)
-    t = float(numpy.median(times[1:]))
+    t = float(numpy.median(times))
     est = per.mean(axis=0)
     se = per.std(axis=0, ddof=1) / numpy.sqrt(nprobe)
     mm = {w: op.sop.bench_spmm(w, 10) for w in sorted({16, nprobe, 32})}
     mm_ms = mm[nprobe]
     kbytes = 8.0 * n * n
-    out = {'value': round(len(etas) / t, 1), 'unit': 'logdet evals/s',
-           'curve_ms': round(t * 1e3, 3), 'etas': len(etas), 'probes': nprobe, 'steps': steps,
+    out = {'value': round(len(etas) / t_search, 1), 'unit': 'logdet evals/s',
+           'value_at_fixed_degree': round(len(etas) / t, 1),
+           'search_ms': round(t_search * 1e3, 3), 'curve_ms': round(t * 1e3, 3),
+           'etas': len(etas), 'probes': nprobe, 'lanczos_degree_start': steps,
+           'lanczos_tol': tol, 'convergence': conv,
+           'fixed_degree_curve_equal': bool(numpy.array_equal(per_f, per)),
            'kernel': op.sop.spmm_kernel(nprobe),
            'dense_mm': {'avg_launch_ms': round(mm_ms, 4), 'bytes': kbytes,
                         'gbs': round(kbytes / (mm_ms * 1e-3) / 1e9, 1),
                         'hbm_frac': round(kbytes / (mm_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                         'ms_by_columns': {str(w): round(v, 4) for w, v in mm.items()}}}
     if ld_exact is not None:
-        # SLQ with 30 Lanczos steps does not resolve the smallest eigenvalues of the
-        # smooth nu = 1.5 K at small eta (cond ~1e5 at eta = 1e-3): a bias of the
-        # estimator there, not of the kernel; at eta >= 1 it is within the probe error
         zs = (est - ld_exact) / se
         pick = [0, int(numpy.argmin(numpy.abs(numpy.log(etas)))), len(etas) - 1]
         out['logdet_check'] = {
             'eta': [float(etas[i]) for i in pick],
             'rel_err': [float(abs(est[i] - ld_exact[i]) / abs(ld_exact[i])) for i in pick],
             'err_in_std_errors': [round(float(zs[i]), 3) for i in pick],
-            'max_abs_std_errors_eta_ge_1': round(float(numpy.max(numpy.abs(zs[etas >= 1.0]))), 3)}
+            'max_abs_std_errors_all_eta': round(float(numpy.max(numpy.abs(zs))), 3),
+            'etas_within_3_std_errors': int(numpy.sum(numpy.abs(zs) <= 3.0))}
+    fixed.sop.close()
     op.sop.close()
     return out
 

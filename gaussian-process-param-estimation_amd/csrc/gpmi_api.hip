@@ -633,7 +633,6 @@ int gpmi_op_create(int device, int64_t n, int max_batch, gpmi_op** out) {
   op->n_pad = (n + TS - 1) / TS * TS;
   op->nt = (int)(op->n_pad / TS);
   op->max_batch = max_batch;
-  if (const char* g = std::getenv("GPMI_SYRK_GROUP")) op->group = std::atoi(g);
   if (const char* g = std::getenv("GPMI_GROUPS")) op->groups = std::atoi(g);
   const int64_t np = op->n_pad;
   auto fail = [&](hipError_t e, const char* what) {

@@ -50,16 +50,6 @@ __global__ void syr2k_kernel(double* A, int64_t lda, const double* U, int64_t ld
                              int mt, int sub);
 __global__ void syr2k_rest_kernel(double* A, int64_t lda, const double* U, int64_t ldu, int tr0,
                                   int mt, const uint32_t* order);
-__global__ void syr2k_g_kernel(double* A, int64_t lda, const double* PA, const double* PB,
-                               int64_t ldu, int kdim, int tr0, int mt, int sub);
-__global__ void syr2k_g_rest_kernel(double* A, int64_t lda, const double* PA, const double* PB,
-                                    int64_t ldu, int kdim, int tr0, int mt);
-__global__ void slot_copy_kernel(const double* U, int64_t ldu, int m, double* Va, double* Vb,
-                                 double* Wa, double* Wb, int64_t ldg);
-__global__ void zc_partial_kernel(const double* PB, int64_t ldb, const double* V, int64_t ldv,
-                                  int m, double* part);
-__global__ void zc_reduce_kernel(const double* part, int nch, double* Z);
-__global__ void xcorr_kernel(double* X, const double* PA, int64_t lda, const double* Z, int kdim);
 __global__ void bcr_f0_kernel(const double* Ab, int64_t lda, double* F0);
 __global__ void bcr_chol_kernel(const double* Ab, int64_t lda, const double* etas, int lvl,
                                 int first, const double* Din, int64_t sD, const double* Yin,

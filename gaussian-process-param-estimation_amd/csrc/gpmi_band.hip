@@ -574,130 +574,6 @@ __global__ __launch_bounds__(256, 2) void syr2k_rest_kernel(double* __restrict__
 }
 
 // ---------------------------------------------------------------------------
-// Delayed trailing update (band_reduce_pass, delay > 1): the SYR2K of up to p
-// panels is applied once per group of p panels as one rank-256p product, and
-// until then every panel of the group works on the stored (not yet updated)
-// trailing matrix with the pending pairs' corrections (LAPACK dlatrd-style):
-//   the panel's tile column:  A[:, J] -= [W V]_pend [V W]_pend,J^T  (syr2k_g, sub 1)
-//   X = A22 V - UA_pend (UB_pend^T V)                 (zc_partial/reduce, xcorr)
-// Pending pairs live in UA = [W_{p-1} .. W_0 | V_0 .. V_{p-1}] and
-// UB = [V_{p-1} .. V_0 | W_0 .. W_{p-1}] (n_pad x 256 p each): the Q pairs of a
-// group are the 256 Q columns from (p - Q) * 128 of both, and UA UB^T over them is
-// sum_q (W_q V_q^T + V_q W_q^T).
-// ---------------------------------------------------------------------------
-// A_IJ -= PA_I PB_J^T over kdim columns (lower tiles of the trailing block, tiles
-// from tr0): sub 0 every lower tile (XCD-aware), sub 1 tile column 0 only.
-__device__ __forceinline__ void syr2k_g_tile(double* __restrict__ A, int64_t lda,
-                                             const double* __restrict__ PA,
-                                             const double* __restrict__ PB, int64_t ldu,
-                                             int kdim, int I, int J, double* smem) {
-  double* C = A + (int64_t)I * TS * lda + (int64_t)J * TS;
-  d4 acc[4][4];
-  load_tile(C, lda, acc);
-  gemm_tile<KFAST, KFAST, true>(PA + (int64_t)I * TS * ldu, ldu, PB + (int64_t)J * TS * ldu, ldu,
-                                kdim, smem, acc);
-  store_tile(C, lda, acc, 1.0);
-}
-
-__global__ __launch_bounds__(256, 2) void syr2k_g_kernel(double* __restrict__ A, int64_t lda,
-                                                         const double* __restrict__ PA,
-                                                         const double* __restrict__ PB,
-                                                         int64_t ldu, int kdim, int tr0, int mt,
-                                                         int sub) {
-  __shared__ double smem[4 * GSTAGE];
-  int i = blockIdx.x, j = 0;
-  if (sub == 0) tri_decode(xcd_remap(blockIdx.x, gridDim.x), mt, &i, &j);
-  syr2k_g_tile(A, lda, PA, PB, ldu, kdim, tr0 + i, tr0 + j, smem);
-}
-
-// the lower tiles right of tile column 0, on a capped grid (look-ahead)
-__global__ __launch_bounds__(256, 2) void syr2k_g_rest_kernel(double* __restrict__ A, int64_t lda,
-                                                              const double* __restrict__ PA,
-                                                              const double* __restrict__ PB,
-                                                              int64_t ldu, int kdim, int tr0,
-                                                              int mt) {
-  __shared__ double smem[4 * GSTAGE];
-  const int ntiles = (mt - 1) * mt / 2;
-  for (int q = blockIdx.x; q < ntiles; q += gridDim.x) {
-    int i, j;
-    tri_decode(q, mt - 1, &i, &j);
-    syr2k_g_tile(A, lda, PA, PB, ldu, kdim, tr0 + i + 1, tr0 + j + 1, smem);
-  }
-}
-
-// the panel's V (U[:, 128:256]) and W (U[:, 0:128]) rows [0, m) into a pending slot:
-// V -> Va, Vb; W -> Wa, Wb (pointers at the slot's first row and column)
-__global__ __launch_bounds__(256) void slot_copy_kernel(const double* __restrict__ U, int64_t ldu,
-                                                        int m, double* __restrict__ Va,
-                                                        double* __restrict__ Vb,
-                                                        double* __restrict__ Wa,
-                                                        double* __restrict__ Wb, int64_t ldg) {
-  const int64_t e = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 2;
-  const int64_t i = e >> 7;
-  const int q = (int)(e & 127);
-  if (i >= m) return;
-  const d2 v = *reinterpret_cast<const d2*>(U + i * ldu + TS + q);
-  const d2 w = *reinterpret_cast<const d2*>(U + i * ldu + q);
-  *reinterpret_cast<d2*>(Va + i * ldg + q) = v;
-  *reinterpret_cast<d2*>(Vb + i * ldg + q) = v;
-  *reinterpret_cast<d2*>(Wa + i * ldg + q) = w;
-  *reinterpret_cast<d2*>(Wb + i * ldg + q) = w;
-}
-
-// part[y][ch] = PB[rows, y-th 128 columns]^T V[rows] over TN_CH-row chunks of m
-__global__ __launch_bounds__(256, 2) void zc_partial_kernel(const double* __restrict__ PB,
-                                                            int64_t ldb,
-                                                            const double* __restrict__ V,
-                                                            int64_t ldv, int m,
-                                                            double* __restrict__ part) {
-  __shared__ double smem[4 * GSTAGE];
-  const int ch = blockIdx.x, y = blockIdx.y, nch = gridDim.x;
-  const int i0 = ch * TN_CH, kd = min(TN_CH, m - i0);
-  d4 acc[4][4];
-  zero_tile(acc);
-  gemm_tile<KSLOW, KSLOW, false>(PB + (int64_t)i0 * ldb + (int64_t)y * TS, ldb,
-                                 V + (int64_t)i0 * ldv, ldv, kd, smem, acc);
-  store_tile(part + ((int64_t)y * nch + ch) * TS * TS, TS, acc, 1.0);
-}
-
-// Z[y] = sum_ch part[y][ch] (fixed order, as tn_reduce_kernel)
-__global__ __launch_bounds__(256) void zc_reduce_kernel(const double* __restrict__ part, int nch,
-                                                        double* __restrict__ Z) {
-  __shared__ double red[4][64];
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int e = blockIdx.x * 64 + lane;
-  const double* py = part + (int64_t)blockIdx.y * nch * TS * TS;
-  double acc[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-  int c = w;
-  for (; c + 28 < nch; c += 32) {
-    double x[8];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) x[q] = py[(int64_t)(c + 4 * q) * TS * TS + e];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) acc[q] += x[q];
-  }
-  for (int q = 0; c < nch; c += 4, ++q) acc[q] += py[(int64_t)c * TS * TS + e];
-  red[w][lane] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
-  __syncthreads();
-  if (w == 0)
-    Z[(int64_t)blockIdx.y * TS * TS + e] =
-        (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
-}
-
-// X_I -= PA_I Z (kdim rows of Z: the pending pairs' correction of X = A22 V)
-__global__ __launch_bounds__(256, 2) void xcorr_kernel(double* __restrict__ X,
-                                                       const double* __restrict__ PA, int64_t lda,
-                                                       const double* __restrict__ Z, int kdim) {
-  __shared__ double smem[4 * GSTAGE];
-  const int il = blockIdx.x;
-  double* Xi = X + (int64_t)il * TS * TS;
-  d4 acc[4][4];
-  load_tile(Xi, TS, acc);
-  gemm_tile<KFAST, KSLOW, true>(PA + (int64_t)il * TS * lda, lda, Z, TS, kdim, smem, acc);
-  store_tile(Xi, TS, acc, 1.0);
-}
-
-// ---------------------------------------------------------------------------
 // Y <- Q_j^T Y for one panel (Y rows r0.., 16 columns): Y -= V (T^T (V^T Y)).
 // V is read from the reduced matrix (unit lower trapezoidal below the band).
 //   qt_partial : workgroup g: part[g] = V[rows]^T Y[rows] over QT_ROWS rows

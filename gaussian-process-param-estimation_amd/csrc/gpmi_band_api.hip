@@ -64,6 +64,8 @@ struct Guard {
 
 }  // namespace
 
+constexpr int RGROUP = 8;   // tile rows per group of the look-ahead SYR2K's tile order
+
 struct gpmi_band {
   int device = 0;
   int64_t n = 0, n_pad = 0;
@@ -82,7 +84,6 @@ struct gpmi_band {
   double* tnp = nullptr;     // tn partials [nch][128][128]
   double* tnp2 = nullptr;    // tn partials of V^T V (side stream) [nch][128][128]
   hipStream_t side = nullptr;          // V^T V and T of a panel, beside its SYMM
-  hipStream_t qs = nullptr;            // Q^T R during the reduction (gpmi_band_refresh_rhs)
   // look-ahead: the next panel's QR (high-priority stream) beside the rest of the
   // SYR2K on a capped grid
   int lookahead = 1, la_grid = 128, ncu = 256;
@@ -112,9 +113,6 @@ struct gpmi_band {
   // and inverses, the reconstruction's U^-T, V1, signs, scratch, failure flag
   int panel_mode = 0;        // 0 CholeskyQR, 1 Householder (single launch)
   int cq_fallbacks = 0;      // reductions redone with Householder panels
-  int la_lds = 0;            // dynamic LDS padding of the look-ahead SYR2K (bytes): with
-                             // > 6 KB only one of its workgroups fits a CU, so a grid cap
-                             // below the CU count leaves whole CUs to the panel chain
   int cq_la_grid = 448;      // SYR2K grid cap beside a CholeskyQR panel (0: none; measured
                              // at N = 16384: 448 161-163 ms, none 165-168, no look-ahead 164-166)
   double* Qb = nullptr;
@@ -130,18 +128,10 @@ struct gpmi_band {
   int cq_panel_fallbacks = 0;   // panels factored by the guarded Householder panel, or
                                 // (past its single-launch size) by per-column launches
   int cq_host_checks = 0;       // panels past the single-launch size whose flag the host read
-  // delayed trailing update (CholeskyQR panels): one SYR2K per `delay` panels
-  // (band_reduce_pass_delayed; GPMI_BAND_DELAY, 1 = one SYR2K per panel)
-  int delay = 1;              // measured at N = 16384: 1 159 ms, 2 167, 4 181, 8 202
-  double* UA = nullptr;      // [n_pad][256 delay] = [W_{p-1} .. W_0 | V_0 .. V_{p-1}]
-  double* UB = nullptr;      // [n_pad][256 delay] = [V_{p-1} .. V_0 | W_0 .. W_{p-1}]
-  double* zpart = nullptr;   // [2 delay][nt][128][128] partials of UB^T V
-  double* Zc = nullptr;      // [2 delay][128][128]
   // grouped tile orders of the look-ahead SYR2K, one per (w x w)-triangle, w < nt
-  // (GPMI_BAND_RGROUP rows per group, 0: plain triangle order)
+  // (RGROUP tile rows per group; measured within +-0.5 % of the plain triangle order)
   uint32_t* rorder = nullptr;
   std::vector<int64_t> rorder_off;
-  int rgroup = 8;
   // block cyclic reduction of B + eta I (gpmi_bcr.hip; GPMI_BAND_BCR): per eta
   // capacity bcap, half = ceil(nt / 2) blocks per level
   int bcr_mode = 2;          // 0 sequential band_chol_kernel, 1 cyclic reduction, 2 auto:
@@ -195,7 +185,7 @@ int band_free(gpmi_band* b) {
   double* bufs[] = {b->Ab, b->U, b->X, b->Xp, b->part, b->pivrow, b->tau, b->Tm, b->tnp, b->tnp2,
                     b->VtV, b->M, b->Zh, b->Y, b->qtp, b->qa, b->qb, b->etas, b->out, b->Ac, b->td,
                     b->fac, b->ysol, b->der, b->Qb, b->cqpart, b->cqG, b->cqL, b->cqLinv,
-                    b->cqMinv, b->cqS, b->cqscr, b->UA, b->UB, b->zpart, b->Zc,
+                    b->cqMinv, b->cqS, b->cqscr,
                     b->bcrD[0], b->bcrD[1], b->bcrF[0], b->bcrF[1], b->bcrY[0], b->bcrY[1],
                     b->bcrL, b->bcrW, b->bcrZ, b->bcrG, b->bcrLd, b->bcrF0, b->bcrX,
                     b->bcrZp, b->bcrG2, b->bcrG3};
@@ -212,7 +202,6 @@ int band_free(gpmi_band* b) {
   if (b->ev1) (void)hipEventDestroy(b->ev1);
   if (b->stream) (void)hipStreamDestroy(b->stream);
   if (b->side) (void)hipStreamDestroy(b->side);
-  if (b->qs) (void)hipStreamDestroy(b->qs);
   if (b->s_pan) (void)hipStreamDestroy(b->s_pan);
   for (hipEvent_t e : {b->ev_col, b->ev_pan})
     if (e) (void)hipEventDestroy(e);
@@ -401,7 +390,7 @@ std::vector<double> pack_rhs(const gpmi_band* b, const double* rhs, int64_t ld, 
 }
 
 // Dense -> band: panels j = 0 .. nt-2 of 128 columns (see gpmi_band.hip).
-// With yh (the packed RHS), Y = Q^T R is applied panel by panel on the qs
+// With yh (the packed RHS), Y = Q^T R is applied panel by panel on the side
 // stream as soon as each panel's T exists, beside the rest of the reduction.
 // mode: the panel algorithm (panel_qr); mode 2 runs without look-ahead.
 int band_reduce_pass(gpmi_band* b, const double* K, const std::vector<double>* yh, int mode) {
@@ -413,7 +402,7 @@ int band_reduce_pass(gpmi_band* b, const double* K, const std::vector<double>* y
   BD_TRY(hipEventRecord(b->ev0, s));
   if (yh) {
     BD_TRY(hipMemcpyAsync(b->Y, yh->data(), sizeof(double) * yh->size(), hipMemcpyHostToDevice,
-                          b->qs ? b->qs : b->side));
+                          b->side));
   }
   BD_TRY(hipMemcpyAsync(b->Ab, K, sizeof(double) * np * np, hipMemcpyDeviceToDevice, s));
   const bool la = mode != 2 && b->lookahead && b->s_pan;
@@ -447,11 +436,9 @@ int band_reduce_pass(gpmi_band* b, const double* K, const std::vector<double>* y
     BD_LAUNCH("tbuild_kernel");
     BD_TRY(hipEventRecord(b->ev_t, b->side));
     if (yh) {
-      // Q_j^T on the side stream right after T_j (default), or on a stream of its
-      // own (GPMI_BAND_QS=1)
-      hipStream_t qst = b->qs ? b->qs : b->side;
-      if (b->qs) BD_TRY(hipStreamWaitEvent(b->qs, b->ev_t, 0));
-      int rc = qt_panel(b, j, qst);
+      // Q_j^T on the side stream right after T_j (a stream of its own measured the
+      // same, and a fourth stream of the reduction costs more elsewhere: DESIGN 5)
+      int rc = qt_panel(b, j, b->side);
       if (rc) return rc;
     }
     const int chunk = symm_chunk(mt);
@@ -493,8 +480,8 @@ int band_reduce_pass(gpmi_band* b, const double* K, const std::vector<double>* y
       // CholeskyQR panel needs no co-resident workgroups (cq_la_grid, 0: no cap)
       const int cap = mode == 0 ? (b->cq_la_grid > 0 ? b->cq_la_grid : rest)
                       : b->la_grid > 0 ? b->la_grid : std::max(64, b->ncu - next_g);
-      hipLaunchKernelGGL(syr2k_rest_kernel, dim3(std::min(rest, cap)), dim3(256),
-                         mode == 0 ? b->la_lds : 0, s, b->Ab, np, b->U, (int64_t)BAND_ULD, j + 1,
+      hipLaunchKernelGGL(syr2k_rest_kernel, dim3(std::min(rest, cap)), dim3(256), 0, s, b->Ab,
+                         np, b->U, (int64_t)BAND_ULD, j + 1,
                          mt, b->rorder ? b->rorder + b->rorder_off[mt - 1] : nullptr);
       BD_LAUNCH("syr2k_rest_kernel");
       BD_TRY(hipStreamWaitEvent(s, b->ev_pan, 0));
@@ -507,7 +494,7 @@ int band_reduce_pass(gpmi_band* b, const double* K, const std::vector<double>* y
     }
   }
   if (yh) {
-    BD_TRY(hipEventRecord(b->ev_q, b->qs ? b->qs : b->side));
+    BD_TRY(hipEventRecord(b->ev_q, b->side));
     BD_TRY(hipStreamWaitEvent(s, b->ev_q, 0));
   }
   if (mode == 0 && nt > 1) {
@@ -537,174 +524,6 @@ int band_reduce_pass(gpmi_band* b, const double* K, const std::vector<double>* y
   return 0;
 }
 
-// The reduction with CholeskyQR panels and the trailing update delayed over groups
-// of p = b->delay panels (gpmi_band.hip, "Delayed trailing update"): inside a
-// group each panel's tile column gets the pending pairs' update just before its
-// QR, X = A22 V is corrected by the pending pairs, and the group ends with ONE
-// rank-256p SYR2K of the trailing block (the look-ahead runs the next panel's QR
-// beside it, as in band_reduce_pass).
-int band_reduce_pass_delayed(gpmi_band* b, const double* K, const std::vector<double>* yh) {
-  const int mode = 0;
-  hipStream_t s = b->stream;
-  const int64_t np = b->n_pad;
-  const int nt = b->nt;
-  const int p = b->delay;
-  const int64_t ldg = (int64_t)2 * TS * p;
-  if (!b->UA) {
-    BD_TRY(hipMalloc(&b->UA, sizeof(double) * np * ldg));
-    BD_TRY(hipMalloc(&b->UB, sizeof(double) * np * ldg));
-    BD_TRY(hipMalloc(&b->zpart, sizeof(double) * 2 * p * (size_t)nt * TS * TS));
-    BD_TRY(hipMalloc(&b->Zc, sizeof(double) * 2 * p * TS * TS));
-  }
-  BD_TRY(hipMemsetAsync(b->err, 0, 16, s));
-  BD_TRY(hipMemsetAsync(b->cqflag, 0, sizeof(int) * 8 * nt, s));
-  BD_TRY(hipEventRecord(b->ev0, s));
-  if (yh) {
-    BD_TRY(hipMemcpyAsync(b->Y, yh->data(), sizeof(double) * yh->size(), hipMemcpyHostToDevice,
-                          b->qs ? b->qs : b->side));
-  }
-  BD_TRY(hipMemcpyAsync(b->Ab, K, sizeof(double) * np * np, hipMemcpyDeviceToDevice, s));
-  const bool la = b->lookahead && b->s_pan;
-  bool ahead = false;
-  int Q = 0;   // pending pairs of the current group
-  for (int j = 0; j + 1 < nt; ++j) {
-    const int64_t r0 = (int64_t)(j + 1) * TS;
-    const int m = (int)(np - r0), mt = nt - j - 1;
-    double* tau = b->tau + (int64_t)j * TS;
-    double* T = b->Tm + (int64_t)j * TS * TS;
-    const double* PA = b->UA + (int64_t)(p - Q) * TS;
-    const double* PB = b->UB + (int64_t)(p - Q) * TS;
-    if (!ahead) {
-      if (Q > 0) {
-        // the panel's tile column (tiles j .. nt-1) with the pending pairs
-        hipLaunchKernelGGL(syr2k_g_kernel, dim3(nt - j), dim3(256), 0, s, b->Ab, np, PA, PB, ldg,
-                           2 * TS * Q, j, nt - j, 1);
-        BD_LAUNCH("syr2k_g_kernel");
-      }
-      int rc = panel_qr(b, j, s, mode);
-      if (rc) return rc;
-    }
-    ahead = false;
-    double* P = b->Ab + r0 * np + (int64_t)j * TS;
-    double* Ur = b->U + r0 * BAND_ULD;
-    hipLaunchKernelGGL(vcopy_kernel, dim3((unsigned)((int64_t)m * TS / 256)), dim3(256), 0, s, P,
-                       np, m, Ur, (int64_t)BAND_ULD);
-    BD_LAUNCH("vcopy_kernel");
-    const int nch = (m + TN_CH - 1) / TN_CH;
-    // side stream, beside the SYMM: T from V^T V, and Z = UB_pend^T V
-    BD_TRY(hipEventRecord(b->ev_v, s));
-    BD_TRY(hipStreamWaitEvent(b->side, b->ev_v, 0));
-    hipLaunchKernelGGL(tn_partial_kernel, dim3(nch), dim3(256), 0, b->side, Ur + TS,
-                       (int64_t)BAND_ULD, Ur + TS, (int64_t)BAND_ULD, m, b->tnp2);
-    BD_LAUNCH("tn_partial_kernel");
-    hipLaunchKernelGGL(tn_reduce_kernel, dim3(TS * TS / 64), dim3(256), 0, b->side, b->tnp2, nch,
-                       b->VtV, 1.0);
-    BD_LAUNCH("tn_reduce_kernel");
-    hipLaunchKernelGGL(tbuild_kernel, dim3(1), dim3(256), 0, b->side, b->VtV, tau, T);
-    BD_LAUNCH("tbuild_kernel");
-    if (Q > 0) {
-      hipLaunchKernelGGL(zc_partial_kernel, dim3(nch, 2 * Q), dim3(256), 0, b->side,
-                         PB + r0 * ldg, ldg, Ur + TS, (int64_t)BAND_ULD, m, b->zpart);
-      BD_LAUNCH("zc_partial_kernel");
-      hipLaunchKernelGGL(zc_reduce_kernel, dim3(TS * TS / 64, 2 * Q), dim3(256), 0, b->side,
-                         b->zpart, nch, b->Zc);
-      BD_LAUNCH("zc_reduce_kernel");
-    }
-    BD_TRY(hipEventRecord(b->ev_t, b->side));
-    if (yh) {
-      hipStream_t qst = b->qs ? b->qs : b->side;
-      if (b->qs) BD_TRY(hipStreamWaitEvent(b->qs, b->ev_t, 0));
-      int rc = qt_panel(b, j, qst);
-      if (rc) return rc;
-    }
-    const int chunk = symm_chunk(mt);
-    const int sch = (mt + chunk - 1) / chunk;
-    hipLaunchKernelGGL(symm_kernel, dim3(mt, sch), dim3(256), 0, s, b->Ab, np, b->U,
-                       (int64_t)BAND_ULD, j + 1, mt, chunk, b->Xp);
-    BD_LAUNCH("symm_kernel");
-    hipLaunchKernelGGL(psum_kernel, dim3(TS * TS / 512, mt), dim3(256), 0, s, b->Xp, sch, b->X);
-    BD_LAUNCH("psum_kernel");
-    BD_TRY(hipStreamWaitEvent(s, b->ev_t, 0));
-    if (Q > 0) {
-      hipLaunchKernelGGL(xcorr_kernel, dim3(mt), dim3(256), 0, s, b->X, PA + r0 * ldg, ldg, b->Zc,
-                         2 * TS * Q);
-      BD_LAUNCH("xcorr_kernel");
-    }
-    hipLaunchKernelGGL(xt_kernel, dim3(mt), dim3(256), 0, s, b->X, T);
-    BD_LAUNCH("xt_kernel");
-    hipLaunchKernelGGL(tn_partial_kernel, dim3(nch), dim3(256), 0, s, Ur + TS,
-                       (int64_t)BAND_ULD, b->X, (int64_t)TS, m, b->tnp);
-    BD_LAUNCH("tn_partial_kernel");
-    hipLaunchKernelGGL(tn_reduce_kernel, dim3(TS * TS / 64), dim3(256), 0, s, b->tnp, nch, b->M,
-                       1.0);
-    BD_LAUNCH("tn_reduce_kernel");
-    hipLaunchKernelGGL(z_kernel, dim3(1), dim3(256), 0, s, T, b->M, b->Zh);
-    BD_LAUNCH("z_kernel");
-    hipLaunchKernelGGL(w_kernel, dim3(mt), dim3(256), 0, s, b->X, Ur, (int64_t)BAND_ULD, b->Zh);
-    BD_LAUNCH("w_kernel");
-    // the pair into pending slot Q
-    hipLaunchKernelGGL(slot_copy_kernel, dim3((unsigned)((int64_t)m * TS / 512)), dim3(256), 0, s,
-                       Ur, (int64_t)BAND_ULD, m, b->UA + r0 * ldg + (int64_t)(p + Q) * TS,
-                       b->UB + r0 * ldg + (int64_t)(p - 1 - Q) * TS,
-                       b->UA + r0 * ldg + (int64_t)(p - 1 - Q) * TS,
-                       b->UB + r0 * ldg + (int64_t)(p + Q) * TS, ldg);
-    BD_LAUNCH("slot_copy_kernel");
-    ++Q;
-    if (Q < p && j + 2 < nt) continue;
-    // group end: ONE rank-256Q SYR2K of the trailing block
-    const double* GA = b->UA + (int64_t)(p - Q) * TS;
-    const double* GB = b->UB + (int64_t)(p - Q) * TS;
-    const int kd = 2 * TS * Q;
-    if (la && j + 2 < nt) {
-      hipLaunchKernelGGL(syr2k_g_kernel, dim3(mt), dim3(256), 0, s, b->Ab, np, GA, GB, ldg, kd,
-                         j + 1, mt, 1);
-      BD_LAUNCH("syr2k_g_kernel");
-      BD_TRY(hipEventRecord(b->ev_col, s));
-      BD_TRY(hipStreamWaitEvent(b->s_pan, b->ev_col, 0));
-      int rc = panel_qr(b, j + 1, b->s_pan, mode);
-      if (rc) return rc;
-      BD_TRY(hipEventRecord(b->ev_pan, b->s_pan));
-      const int rest = (mt - 1) * mt / 2;
-      const int cap = b->cq_la_grid > 0 ? b->cq_la_grid : rest;
-      hipLaunchKernelGGL(syr2k_g_rest_kernel, dim3(std::min(rest, cap)), dim3(256), 0, s, b->Ab,
-                         np, GA, GB, ldg, kd, j + 1, mt);
-      BD_LAUNCH("syr2k_g_rest_kernel");
-      BD_TRY(hipStreamWaitEvent(s, b->ev_pan, 0));
-      ahead = true;
-    } else {
-      const int tiles = mt * (mt + 1) / 2;
-      hipLaunchKernelGGL(syr2k_g_kernel, dim3(tiles), dim3(256), 0, s, b->Ab, np, GA, GB, ldg, kd,
-                         j + 1, mt, 0);
-      BD_LAUNCH("syr2k_g_kernel");
-    }
-    Q = 0;
-  }
-  if (yh) {
-    BD_TRY(hipEventRecord(b->ev_q, b->qs ? b->qs : b->side));
-    BD_TRY(hipStreamWaitEvent(s, b->ev_q, 0));
-  }
-  if (nt > 1) {
-    hipLaunchKernelGGL(cq_top_kernel, dim3(nt - 1), dim3(256), 0, s, b->cqL, b->cqLinv, b->cqflag,
-                       b->cqS, b->cqscr, b->Ab, np);
-    BD_LAUNCH("cq_top_kernel");
-  }
-  BD_TRY(hipEventRecord(b->ev1, s));
-  int herr = 0;
-  std::vector<int> hflag(8 * nt);
-  BD_TRY(hipMemcpyAsync(&herr, b->err, sizeof(int), hipMemcpyDeviceToHost, s));
-  BD_TRY(hipMemcpyAsync(hflag.data(), b->cqflag, sizeof(int) * hflag.size(),
-                        hipMemcpyDeviceToHost, s));
-  BD_TRY(hipEventSynchronize(b->ev1));
-  BD_TRY(hipStreamSynchronize(s));
-  if (herr) return set_error(-1201, "band reduction: panel hand-off timed out (workgroups not co-resident?)");
-  for (int j = 0; j + 1 < nt; ++j)
-    if (hflag[8 * j + 4]) ++b->cq_panel_fallbacks;
-  float ms = 0.f;
-  BD_TRY(hipEventElapsedTime(&ms, b->ev0, b->ev1));
-  b->reduce_ms = ms;
-  return 0;
-}
-
 // The reduction with the single-launch panel QR; if a hand-off times out (its
 // workgroups were not all resident, e.g. the GPU is shared or partitioned), the
 // whole reduction is redone from K with the per-column panel launches.
@@ -717,7 +536,7 @@ int band_reduce(gpmi_band* b, const double* K, const std::vector<double>* yh = n
     // a failed CholeskyQR panel is refactored in place (cq_panel); only a timed-out
     // guarded Householder panel (its workgroups not co-resident on a shared GPU)
     // sends the reduction back, straight to the per-column launches
-    rc = b->delay > 1 ? band_reduce_pass_delayed(b, K, yh) : band_reduce_pass(b, K, yh, 0);
+    rc = band_reduce_pass(b, K, yh, 0);
     if (rc != -1201) return rc;
     ++b->cq_fallbacks;
     ++b->panel_fallbacks;
@@ -783,17 +602,8 @@ int gpmi_band_create(gpmi_op* op, gpmi_band** out) {
   if ((e = hipEventCreate(&b->ev1)) != hipSuccess) return fail(e, "event");
   if ((e = hipStreamCreateWithFlags(&b->side, hipStreamNonBlocking)) != hipSuccess)
     return fail(e, "side stream");
-  if (std::getenv("GPMI_BAND_QS") && std::atoi(std::getenv("GPMI_BAND_QS")) &&
-      (e = hipStreamCreateWithFlags(&b->qs, hipStreamNonBlocking)) != hipSuccess)
-    return fail(e, "rhs stream");
   if (const char* la = std::getenv("GPMI_BAND_LA")) b->lookahead = std::atoi(la);
-  if (const char* lg = std::getenv("GPMI_BAND_LA_GRID")) b->la_grid = std::max(0, std::atoi(lg));
-  if (const char* ll = std::getenv("GPMI_BAND_LA_LDS")) b->la_lds = std::max(0, std::atoi(ll));
-  if (const char* lg = std::getenv("GPMI_BAND_CQ_LA_GRID"))
-    b->cq_la_grid = std::max(0, std::atoi(lg));
   if (const char* pm = std::getenv("GPMI_BAND_PANEL")) b->panel_mode = std::strcmp(pm, "hh") == 0;
-  if (const char* dl = std::getenv("GPMI_BAND_DELAY")) b->delay = std::max(1, std::min(8, std::atoi(dl)));
-  if (const char* rg = std::getenv("GPMI_BAND_RGROUP")) b->rgroup = std::max(0, std::atoi(rg));
   if (const char* bm = std::getenv("GPMI_BAND_BCR")) b->bcr_mode = std::max(0, std::min(2, std::atoi(bm)));
   // GPMI_CQ_FO=0: every CholeskyQR pass by an exact Cholesky (no first-order passes)
   if (const char* fo = std::getenv("GPMI_CQ_FO"))
@@ -846,14 +656,14 @@ int gpmi_band_create(gpmi_op* op, gpmi_band** out) {
   BALLOC(cqscr, (size_t)nt * TS * TS);
 #undef BALLOC
   if ((e = hipMalloc(&b->cqflag, sizeof(int) * 8 * nt)) != hipSuccess) return fail(e, "cqflag");
-  if (b->rgroup > 0 && nt > 2) {
-    // row groups of rgroup tile rows, column-major inside a group (packed (i << 16) | j)
+  if (nt > 2) {
+    // row groups of RGROUP tile rows, column-major inside a group (packed (i << 16) | j)
     std::vector<uint32_t> h;
     b->rorder_off.assign(nt, 0);
     for (int w = 1; w < nt; ++w) {
       b->rorder_off[w] = (int64_t)h.size();
-      for (int r0 = 0; r0 < w; r0 += b->rgroup) {
-        const int r1 = std::min(w, r0 + b->rgroup);
+      for (int r0 = 0; r0 < w; r0 += RGROUP) {
+        const int r1 = std::min(w, r0 + RGROUP);
         for (int j = 0; j < r1; ++j)
           for (int i = std::max(r0, j); i < r1; ++i) h.push_back(((uint32_t)i << 16) | (uint32_t)j);
       }

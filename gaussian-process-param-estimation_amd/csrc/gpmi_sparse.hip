@@ -141,11 +141,7 @@ __global__ __launch_bounds__(256) void csr_spmm_pair_kernel(const int64_t* __res
   }
 }
 
-template __global__ void csr_spmm_pair_kernel<2>(const int64_t*, const int*, const double*, int64_t,
-                                                const double*, double*, int, int, double);
 template __global__ void csr_spmm_pair_kernel<3>(const int64_t*, const int*, const double*, int64_t,
-                                                const double*, double*, int, int, double);
-template __global__ void csr_spmm_pair_kernel<4>(const int64_t*, const int*, const double*, int64_t,
                                                 const double*, double*, int, int, double);
 
 // ---------------------------------------------------------------------------
@@ -318,110 +314,10 @@ __global__ __launch_bounds__(256) void csr_spmm_win_kernel(
   }
 }
 
-// The windowed SpMM in ONE pass over all S columns (S a compile-time width: the
-// Lanczos probe block s = 20; at the multi-shift CG width 11 the 8-column chunks
-// measured faster): the block's window rows
-// of X staged at full width (u x S doubles), then thread (row r = t / 4, column
-// group g = t % 4) sums its row for ceil(S / 4) columns, reading each nonzero's
-// value and window position once for all of them (the 8-column chunks of
-// csr_spmm_win_kernel re-read them per column and stage three times).
-template <int S>
-__global__ __launch_bounds__(256) void csr_spmm_winf_kernel(
-    const int64_t* __restrict__ indptr, const int* __restrict__ indices,
-    const unsigned short* __restrict__ lidx, const double* __restrict__ data, int64_t n,
-    const int* __restrict__ wcols, const int* __restrict__ ucount,
-    const double* __restrict__ X, double* __restrict__ Y, double eta) {
-  extern __shared__ double smem[];
-  constexpr int CG = (S + 3) / 4;
-  const int t = threadIdx.x;
-  const int64_t b = xcd_remap(blockIdx.x, gridDim.x);
-  const int64_t r0 = b * WIN_ROWS, r1 = min(r0 + WIN_ROWS, n);
-  const int nr = (int)(r1 - r0);
-  const int u = ucount[b];
-  const int r = t >> 2, g = t & 3, c0 = g * CG;
-  if (u == 0) {
-    // window over its limits: gather straight from X
-    if (r < nr) {
-      const int64_t row = r0 + r;
-      double acc[CG];
-#pragma unroll
-      for (int j = 0; j < CG; ++j) acc[j] = 0.0;
-      for (int64_t k = indptr[row]; k < indptr[row + 1]; ++k) {
-        const double v = data[k];
-        const double* xr = X + (int64_t)indices[k] * S;
-#pragma unroll
-        for (int j = 0; j < CG; ++j)
-          if (c0 + j < S) acc[j] += v * xr[c0 + j];
-      }
-#pragma unroll
-      for (int j = 0; j < CG; ++j)
-        if (c0 + j < S) Y[row * S + c0 + j] = acc[j] + eta * X[row * S + c0 + j];
-    }
-    return;
-  }
-  const int64_t k0 = indptr[r0];
-  const int m = (int)(indptr[r1] - k0);
-  double* win = smem;                                    // [u][S]
-  double* sval = win + (size_t)u * S;                    // [m]
-  unsigned short* slix = reinterpret_cast<unsigned short*>(sval + m);   // [m]
-  int* srow = reinterpret_cast<int*>(slix + ((m + 1) & ~1));            // [WIN_ROWS + 1]
-  for (int i = t; i < m; i += 256) {
-    sval[i] = data[k0 + i];
-    slix[i] = lidx[k0 + i];
-  }
-  if (t <= nr) srow[t] = (int)(indptr[r0 + t] - k0);
-  const int* wc = wcols + b * WIN_MAXU;
-  for (int i = t; i < u * S; i += 256) {
-    const int e = i / S, cj = i - e * S;
-    win[i] = X[(int64_t)wc[e] * S + cj];
-  }
-  __syncthreads();
-  if (r < nr) {
-    const int ka = srow[r], kb = srow[r + 1];
-    double acc[CG];
-#pragma unroll
-    for (int j = 0; j < CG; ++j) acc[j] = 0.0;
-    // four nonzeros' values, positions and window entries loaded before their products
-    // (22.7 vs 24.0 us per cfg 4 launch)
-    int k = ka;
-    for (; k + 4 <= kb; k += 4) {
-      double v[4], x[4][CG];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        v[q] = sval[k + q];
-        const double* wr = win + slix[k + q] * S + c0;
-#pragma unroll
-        for (int j = 0; j < CG; ++j) x[q][j] = (c0 + j < S) ? wr[j] : 0.0;
-      }
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int j = 0; j < CG; ++j)
-          if (c0 + j < S) acc[j] += v[q] * x[q][j];
-    }
-    for (; k < kb; ++k) {
-      const double v = sval[k];
-      const double* wr = win + slix[k] * S + c0;
-#pragma unroll
-      for (int j = 0; j < CG; ++j)
-        if (c0 + j < S) acc[j] += v * wr[j];
-    }
-    const int64_t row = r0 + r;
-#pragma unroll
-    for (int j = 0; j < CG; ++j)
-      if (c0 + j < S) Y[row * S + c0 + j] = acc[j] + eta * X[row * S + c0 + j];
-  }
-}
-
-template __global__ void csr_spmm_winf_kernel<20>(const int64_t*, const int*,
-                                                  const unsigned short*, const double*, int64_t,
-                                                  const int*, const int*, const double*, double*,
-                                                  double);
-
 // The one-pass window with its staging latency hidden (round 3): the window rows of
 // X are gathered with NB loads in flight per thread (16-byte loads for even S; a
-// batch covers 8192 doubles, ~410 rows at S = 20), where csr_spmm_winf_kernel waits
-// for each 8-byte load before the next (its 3D windows of ~350 rows then took 27
+// batch covers 8192 doubles, ~410 rows at S = 20), where the round-2 one-pass window
+// kernel waited for each 8-byte load before the next (its 3D windows of ~350 rows then took 27
 // serialised L2 round trips per thread); the nonzeros' values and window positions
 // are read from global memory (the four threads of a row share each; U of them in
 // flight per thread), so LDS holds only the window: u S doubles, two workgroups per
@@ -558,94 +454,19 @@ __global__ __launch_bounds__(64 * TPR) void csr_spmm_wing_kernel(
   }
 }
 
-template __global__ void csr_spmm_wing_kernel<20, 4, 4>(const int64_t*, const int*,
-    const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
-    double*, double, double*);
-template __global__ void csr_spmm_wing_kernel<20, 4, 8>(const int64_t*, const int*,
-    const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
-    double*, double, double*);
 template __global__ void csr_spmm_wing_kernel<20, 8, 4>(const int64_t*, const int*,
-    const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
-    double*, double, double*);
-template __global__ void csr_spmm_wing_kernel<20, 8, 8>(const int64_t*, const int*,
-    const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
-    double*, double, double*);
-template __global__ void csr_spmm_wing_kernel<20, 16, 4>(const int64_t*, const int*,
-    const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
-    double*, double, double*);
-template __global__ void csr_spmm_wing_kernel<20, 16, 8>(const int64_t*, const int*,
-    const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
-    double*, double, double*);
-template __global__ void csr_spmm_wing_kernel<11, 4, 4>(const int64_t*, const int*,
-    const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
-    double*, double, double*);
-template __global__ void csr_spmm_wing_kernel<11, 4, 8>(const int64_t*, const int*,
     const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
     double*, double, double*);
 template __global__ void csr_spmm_wing_kernel<11, 8, 4>(const int64_t*, const int*,
     const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
     double*, double, double*);
-template __global__ void csr_spmm_wing_kernel<11, 8, 8>(const int64_t*, const int*,
-    const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
-    double*, double, double*);
-template __global__ void csr_spmm_wing_kernel<11, 16, 4>(const int64_t*, const int*,
-    const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
-    double*, double, double*);
-template __global__ void csr_spmm_wing_kernel<11, 16, 8>(const int64_t*, const int*,
-    const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
-    double*, double, double*);
-template __global__ void csr_spmm_wing_kernel<12, 4, 4>(const int64_t*, const int*,
-    const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
-    double*, double, double*);
-template __global__ void csr_spmm_wing_kernel<12, 4, 8>(const int64_t*, const int*,
-    const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
-    double*, double, double*);
 template __global__ void csr_spmm_wing_kernel<12, 8, 4>(const int64_t*, const int*,
-    const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
-    double*, double, double*);
-template __global__ void csr_spmm_wing_kernel<12, 8, 8>(const int64_t*, const int*,
-    const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
-    double*, double, double*);
-template __global__ void csr_spmm_wing_kernel<12, 16, 4>(const int64_t*, const int*,
-    const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
-    double*, double, double*);
-template __global__ void csr_spmm_wing_kernel<12, 16, 8>(const int64_t*, const int*,
-    const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
-    double*, double, double*);
-template __global__ void csr_spmm_wing_kernel<8, 4, 4>(const int64_t*, const int*,
-    const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
-    double*, double, double*);
-template __global__ void csr_spmm_wing_kernel<8, 4, 8>(const int64_t*, const int*,
     const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
     double*, double, double*);
 template __global__ void csr_spmm_wing_kernel<8, 8, 4>(const int64_t*, const int*,
     const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
     double*, double, double*);
-template __global__ void csr_spmm_wing_kernel<8, 8, 8>(const int64_t*, const int*,
-    const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
-    double*, double, double*);
-template __global__ void csr_spmm_wing_kernel<8, 16, 4>(const int64_t*, const int*,
-    const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
-    double*, double, double*);
-template __global__ void csr_spmm_wing_kernel<8, 16, 8>(const int64_t*, const int*,
-    const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
-    double*, double, double*);
-template __global__ void csr_spmm_wing_kernel<7, 4, 4>(const int64_t*, const int*,
-    const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
-    double*, double, double*);
-template __global__ void csr_spmm_wing_kernel<7, 4, 8>(const int64_t*, const int*,
-    const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
-    double*, double, double*);
 template __global__ void csr_spmm_wing_kernel<7, 8, 4>(const int64_t*, const int*,
-    const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
-    double*, double, double*);
-template __global__ void csr_spmm_wing_kernel<7, 8, 8>(const int64_t*, const int*,
-    const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
-    double*, double, double*);
-template __global__ void csr_spmm_wing_kernel<7, 16, 4>(const int64_t*, const int*,
-    const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
-    double*, double, double*);
-template __global__ void csr_spmm_wing_kernel<7, 16, 8>(const int64_t*, const int*,
     const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
     double*, double, double*);
 
@@ -1079,15 +900,9 @@ __global__ __launch_bounds__(256) void lz_update_kernel(double* __restrict__ V, 
       }
   }
 }
-template __global__ void lz_update_kernel<1, false>(double*, int64_t, int, double*, const double*,
-                                                    const double*, const double*, const double*,
-                                                    int);
 template __global__ void lz_update_kernel<4, false>(double*, int64_t, int, double*, const double*,
                                                     const double*, const double*, const double*,
                                                     int);
-template __global__ void lz_update_kernel<1, true>(double*, int64_t, int, double*, const double*,
-                                                   const double*, const double*, const double*,
-                                                   int);
 template __global__ void lz_update_kernel<4, true>(double*, int64_t, int, double*, const double*,
                                                    const double*, const double*, const double*,
                                                    int);
@@ -1207,106 +1022,6 @@ void launch_ms_dots(const double* B, const double* R, int64_t n, int s, double* 
   }
 }
 
-// Fused r update + dots of one multi-shift CG iteration: every block first
-// reduces the p . q partials (fixed order, identical in every block) to the base
-// step a[c] = rr[c] / (p . q)[c] (0 once the column stopped; block (0, 0) stores a
-// and flags p^T A p <= 0), then r_new = r - a q from R (read only) into Rn
-// (written by the blockIdx.y == 0 blocks; the other column groups form the same
-// values in registers; R and Rn alternate between iterations) and the B^T r,
-// r . r partials as ms_dots_partial_kernel. Replaces the p . q reduce launch,
-// ms_r_update_kernel and one pass over r and q.
-template <int S>
-__global__ __launch_bounds__(256) void ms_rdots_partial_kernel(
-    const double* __restrict__ B, const double* __restrict__ R, double* __restrict__ Rn,
-    const double* __restrict__ Q, MsState st, const double* __restrict__ pqpart, int pq_nblk,
-    int64_t n, int SA, double* __restrict__ partial) {
-  const int NE = SA * S + S;
-  __shared__ double red[4][4 * S + S];
-  __shared__ double sa[S];
-  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  for (int c = wv; c < S; c += 4) {
-    const double pq = wave_reduce_partials(pqpart, pq_nblk, S, c);
-    if (lane == 0) {
-      const int act = st.active[c];
-      const double a = act ? st.rr[c] / pq : 0.0;
-      sa[c] = a;
-      if (blockIdx.x == 0 && blockIdx.y == 0) {
-        st.a[c] = a;
-        if (act && !(pq > 0.0)) st.flags[0] = 1;
-      }
-    }
-  }
-  __syncthreads();
-  const int c0 = blockIdx.y * 4;
-  double acc[4][S], rr[S];
-#pragma unroll
-  for (int c = 0; c < S; ++c) {
-    rr[c] = 0.0;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) acc[q][c] = 0.0;
-  }
-  for (int64_t i = (int64_t)blockIdx.x * 256 + t; i < n; i += (int64_t)gridDim.x * 256) {
-    double r[S], b[4];
-#pragma unroll
-    for (int c = 0; c < S; ++c) r[c] = R[i * S + c] - sa[c] * Q[i * S + c];
-    if (blockIdx.y == 0) {
-#pragma unroll
-      for (int c = 0; c < S; ++c) Rn[i * S + c] = r[c];
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) b[q] = (c0 + q < SA) ? B[i * SA + c0 + q] : 0.0;
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-      for (int c = 0; c < S; ++c) acc[q][c] += b[q] * r[c];
-    if (blockIdx.y == 0) {
-#pragma unroll
-      for (int c = 0; c < S; ++c) rr[c] += r[c] * r[c];
-    }
-  }
-#pragma unroll
-  for (int q = 0; q < 4; ++q)
-#pragma unroll
-    for (int c = 0; c < S; ++c) {
-      const double v = wave_sum(acc[q][c]);
-      if (lane == 0) red[wv][q * S + c] = v;
-    }
-#pragma unroll
-  for (int c = 0; c < S; ++c) {
-    const double v = wave_sum(rr[c]);
-    if (lane == 0) red[wv][4 * S + c] = v;
-  }
-  __syncthreads();
-  if (t < 5 * S) {
-    const double v = (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]);
-    if (t < 4 * S) {
-      const int q = t / S, c = t - q * S;
-      if (c0 + q < SA) partial[(int64_t)blockIdx.x * NE + (c0 + q) * S + c] = v;
-    } else if (blockIdx.y == 0) {
-      partial[(int64_t)blockIdx.x * NE + SA * S + (t - 4 * S)] = v;
-    }
-  }
-}
-
-void launch_ms_rdots(const double* B, const double* R, double* Rn, const double* Q,
-                     const MsState& st, const double* pqpart, int pq_nblk, int64_t n, int s,
-                     double* partial, int nblk, hipStream_t stream, int sa) {
-  if (sa <= 0) sa = s;
-  const dim3 grid(nblk, (sa + 3) / 4), blk(256);
-  switch (s) {
-#define MS_CASE(k)                                                                          \
-  case k:                                                                                   \
-    hipLaunchKernelGGL(ms_rdots_partial_kernel<k>, grid, blk, 0, stream, B, R, Rn, Q, st,     \
-                       pqpart, pq_nblk, n, sa, partial);                                    \
-    break;
-    MS_CASE(1) MS_CASE(2) MS_CASE(3) MS_CASE(4) MS_CASE(5) MS_CASE(6) MS_CASE(7) MS_CASE(8)
-    MS_CASE(9) MS_CASE(10) MS_CASE(11) MS_CASE(12) MS_CASE(13) MS_CASE(14) MS_CASE(15)
-    MS_CASE(16)
-#undef MS_CASE
-    default: break;
-  }
-}
-
 // Fused r update + dots of one multi-shift CG iteration for s <= 16 columns on fp64
 // MFMA: every block first reduces the p . q partials (fixed order, identical in
 // every block) to a[c] = rr[c] / (p . q)[c] (0 once the column stopped; block 0
@@ -1386,27 +1101,6 @@ __global__ __launch_bounds__(256) void ms_rmfma_kernel(const double* __restrict_
     partial[(int64_t)blockIdx.x * ne + e] =
         (red[0][idx] + red[1][idx]) + (red[2][idx] + red[3][idx]);
   }
-}
-
-// r[i][c] -= a[c] q[i][c] with the base step a[c] = rr[c] / (p . q)[c] (0 once the
-// column stopped) formed per element; the first workgroup also stores a for the
-// scalar kernel (the separate alpha launch folded in).
-__global__ __launch_bounds__(256) void ms_r_update_kernel(double* __restrict__ R,
-                                                          const double* __restrict__ Q,
-                                                          MsState st,
-                                                          const double* __restrict__ pq,
-                                                          int64_t n, int s) {
-  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (blockIdx.x == 0 && threadIdx.x < s) {
-    const int c = threadIdx.x;
-    st.a[c] = st.active[c] ? st.rr[c] / pq[c] : 0.0;
-    // negative curvature: K + eta_0 I is not positive definite
-    if (st.active[c] && !(pq[c] > 0.0)) st.flags[0] = 1;
-  }
-  if (e >= n * s) return;
-  const int c = (int)(e % s);
-  const double a = st.active[c] ? st.rr[c] / pq[c] : 0.0;
-  R[e] -= a * Q[e];
 }
 
 // Scalar step 2 (thread (j, c), j < S shifts): with BR = B^T r_new and rr_new

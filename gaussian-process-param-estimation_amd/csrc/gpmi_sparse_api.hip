@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -42,15 +43,15 @@ __global__ void spmm_window_build_kernel(const int64_t*, const int*, int64_t, in
 __global__ void csr_spmm_win_kernel(const int64_t*, const int*, const unsigned short*,
                                     const double*, int64_t, const int*, const int*, const double*,
                                     int64_t, double*, int64_t, int, double);
-template <int S>
-__global__ void csr_spmm_winf_kernel(const int64_t*, const int*, const unsigned short*,
-                                     const double*, int64_t, const int*, const int*,
-                                     const double*, double*, double);
 template <int S, int U, int TPR>
 __global__ void csr_spmm_wing_kernel(const int64_t*, const int*, const unsigned short*,
                                      const double*, int64_t, const int*, const int*,
                                      const double*, double*, double, double*);
 constexpr int WING_MAX_LDS = 80 * 1024;   // two workgroups per CU
+// nonzeros in flight per thread and threads per row of csr_spmm_wing_kernel (measured:
+// 8 in flight best at cfg 5, within 0.3 us of 4 at cfg 4; 8 threads per row in
+// 512-thread blocks faster only at cfg 5 s = 11, 55 against 59 us, slower elsewhere)
+constexpr int WING_U = 8, WING_TPR = 4;
 constexpr int WIN_ROWS_HOST = 64;    // = WIN_ROWS (gpmi_sparse.hip)
 constexpr int WIN_MAXU_HOST = 1024;  // = WIN_MAXU
 constexpr int WIN_CS_HOST = 8;       // = WIN_CS
@@ -81,10 +82,6 @@ void launch_ms_dots(const double* B, const double* R, int64_t n, int s, double* 
 __global__ void rows_gather_kernel(const double*, int, const int*, int64_t, int, double*);
 __global__ void ms_rmfma_kernel(const double*, double*, const double*, MsState, const double*, int,
                                 int64_t, int, int, double*);
-__global__ void ms_r_update_kernel(double*, const double*, MsState, const double*, int64_t, int);
-void launch_ms_rdots(const double* B, const double* R, double* Rn, const double* Q,
-                     const MsState& st, const double* pqpart, int pq_nblk, int64_t n, int s,
-                     double* partial, int nblk, hipStream_t stream, int sa);
 __global__ void ms_scalar_kernel(MsState, const double*, int, const double*, int, int, int,
                                  double, double*);
 __global__ void ms_p_update_kernel(double*, const double*, const double*, const int*, int64_t,
@@ -182,7 +179,10 @@ struct gpmi_sp {
   int* win_cols = nullptr;             // [nblk][WIN_MAXU] sorted window columns
   int* win_u = nullptr;                // [nblk] window sizes (0: block gathers from X)
   unsigned short* win_lidx = nullptr;  // [nnz] window position of every nonzero
-  int win_maxu = -1;                   // -1: not built
+  // -1: not built. Published (release) after every other window field, so a reader
+  // that sees it >= 0 (acquire; the Lanczos and the multi-shift CG may run on two
+  // host threads) sees the whole window
+  std::atomic<int> win_maxu{-1};
   int win_maxm = 0;                    // most nonzeros in a windowed block
   double win_mean = 0.0;               // mean window columns per block
   bool win_use = false;                // the windowed kernel is the faster one here
@@ -215,9 +215,27 @@ int ensure_partial(gpmi_sp* sp, size_t doubles) {
   return 0;
 }
 
+int build_window(gpmi_sp* sp);
+
+// The X windows of the window SpMMs, built once (under win_mu); a failed build
+// frees its buffers, so a retry allocates afresh.
 int ensure_window(gpmi_sp* sp) {
+  if (sp->win_maxu.load(std::memory_order_acquire) >= 0) return 0;
   std::lock_guard<std::mutex> lock(sp->win_mu);
-  if (sp->win_maxu >= 0) return 0;
+  if (sp->win_maxu.load(std::memory_order_acquire) >= 0) return 0;
+  const int rc = build_window(sp);
+  if (rc) {
+    if (sp->win_cols) (void)hipFree(sp->win_cols);
+    if (sp->win_u) (void)hipFree(sp->win_u);
+    if (sp->win_lidx) (void)hipFree(sp->win_lidx);
+    sp->win_cols = nullptr;
+    sp->win_u = nullptr;
+    sp->win_lidx = nullptr;
+  }
+  return rc;
+}
+
+int build_window(gpmi_sp* sp) {
   const int64_t nblk = (sp->n + WIN_ROWS_HOST - 1) / WIN_ROWS_HOST;
   SP_TRY(hipMalloc(&sp->win_cols, sizeof(int) * (size_t)nblk * WIN_MAXU_HOST));
   SP_TRY(hipMalloc(&sp->win_u, sizeof(int) * (size_t)nblk));
@@ -265,46 +283,22 @@ int ensure_window(gpmi_sp* sp) {
   if (lds > 64 * 1024)
     SP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&csr_spmm_win_kernel),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  for (const void* f : {reinterpret_cast<const void*>(&csr_spmm_wing_kernel<20, 4, 4>),
-                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<20, 4, 8>),
-                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<20, 8, 4>),
-                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<20, 8, 8>),
-                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<20, 16, 4>),
-                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<20, 16, 8>),
-                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<11, 4, 4>),
-                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<11, 4, 8>),
-                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<11, 8, 4>),
-                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<11, 8, 8>),
-                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<11, 16, 4>),
-                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<11, 16, 8>),
-                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<7, 4, 4>),
-                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<7, 4, 8>),
-                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<7, 8, 4>),
-                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<7, 8, 8>),
-                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<7, 16, 4>),
-                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<7, 16, 8>),
-                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<12, 4, 4>),
-                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<12, 4, 8>),
-                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<12, 8, 4>),
-                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<12, 8, 8>),
-                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<12, 16, 4>),
-                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<12, 16, 8>),
-                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<8, 4, 4>),
-                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<8, 4, 8>),
-                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<8, 8, 4>),
-                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<8, 8, 8>),
-                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<8, 16, 4>),
-                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<8, 16, 8>)})
+  for (const void* f : {reinterpret_cast<const void*>(&csr_spmm_wing_kernel<20, WING_U, WING_TPR>),
+                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<12, WING_U, WING_TPR>),
+                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<11, WING_U, WING_TPR>),
+                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<8, WING_U, WING_TPR>),
+                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<7, WING_U, WING_TPR>)})
     SP_TRY(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, WING_MAX_LDS));
   sp->win_nblk = nblk;
-  sp->win_maxu = mu;
+  sp->win_maxu.store(mu, std::memory_order_release);
   return 0;
 }
 
-// The SpMM kernel for an s-column block (0 gather, 1 windowed chunks, 2 windowed
-// full width, 3 gather by column pairs). GPMI_SPMM_WINDOW: 0 the gather-from-X
+// The SpMM kernel for an s-column block (0 gather, 1 windowed chunks, 3 gather by
+// column pairs, 5 window with latency-hidden staging; 2, the round-2 one-pass
+// window, is superseded by 5). GPMI_SPMM_WINDOW: 0 the gather-from-X
 // kernel, 2 the windowed kernel, unset or 1 the faster one for this matrix
-// (win_use); GPMI_SPMM_FULL=0 keeps the 8-column chunks at s = 20; GPMI_SPMM_PAIR=0
+// (win_use); GPMI_SPMM_PAIR=0
 // keeps the one-column gather for even s (the pair kernel also needs 16-byte
 // aligned blocks, else the one-column gather runs).
 int spmm_kind(gpmi_sp* sp, int s, int* kind) {
@@ -314,7 +308,7 @@ int spmm_kind(gpmi_sp* sp, int s, int* kind) {
   }
   const char* wenv = std::getenv("GPMI_SPMM_WINDOW");
   const int wmode = wenv ? std::atoi(wenv) : 1;
-  if (wmode != 0 && sp->win_maxu < 0)
+  if (wmode != 0)
     if (int rc = ensure_window(sp)) return rc;
   *kind = 0;
   // the window with latency-hidden staging (csr_spmm_wing_kernel) at the Lanczos
@@ -322,18 +316,13 @@ int spmm_kind(gpmi_sp* sp, int s, int* kind) {
   // (GPMI_SPMM_WING=0: off)
   const char* genv = std::getenv("GPMI_SPMM_WING");
   if (wmode != 0 && !(genv && std::atoi(genv) == 0) && (s == 20 || s == 12 || s == 11 || s == 8 || s == 7) &&
-      sp->win_maxu > 0 &&
-      sizeof(double) * (size_t)std::max(sp->win_maxu, WIN_ROWS_HOST) * s <= (size_t)WING_MAX_LDS) {
+      sp->win_maxu.load(std::memory_order_acquire) > 0 &&
+      sizeof(double) * (size_t)std::max(sp->win_maxu.load(std::memory_order_acquire),
+                                        WIN_ROWS_HOST) * s <= (size_t)WING_MAX_LDS) {
     *kind = 5;
     return 0;
   }
-  if (wmode == 2 || (wmode != 0 && sp->win_use)) {
-    *kind = 1;
-    const char* fenv = std::getenv("GPMI_SPMM_FULL");
-    const size_t lds = sizeof(double) * (size_t)s * (size_t)std::max(1, sp->win_maxu) +
-                       10 * (size_t)sp->win_maxm + 4 + sizeof(int) * (WIN_ROWS_HOST + 1);
-    if (s == 20 && !(fenv && std::atoi(fenv) == 0) && lds <= 64 * 1024) *kind = 2;
-  }
+  if (wmode == 2 || (wmode != 0 && sp->win_use)) *kind = 1;
   const char* penv = std::getenv("GPMI_SPMM_PAIR");
   if (*kind == 0 && s % 2 == 0 && s <= 64 && !(penv && std::atoi(penv) == 0)) *kind = 3;
   return 0;
@@ -365,37 +354,21 @@ int spmm(gpmi_sp* sp, const double* X, double* Y, int s, double eta, hipStream_t
   }
   int kind = 0;
   if (int rc = spmm_kind(sp, s, &kind)) return rc;
+  // the window kernel stages even-width rows of X with 16-byte loads: an 8-byte
+  // aligned block handed in directly takes the one-column gather instead
+  if (kind == 5 && s % 2 == 0 &&
+      ((reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(Y)) & 15) != 0)
+    kind = 0;
   if (kind == 5) {
     // the window, and the epilogue's [64][s] row partials of X . Y (pqp)
-    const size_t lds = sizeof(double) * (size_t)s * (size_t)std::max(sp->win_maxu, WIN_ROWS_HOST);
-    // nonzeros in flight per thread (GPMI_SPMM_WUNR 4, 8 or 16; 8 measured best at
-    // cfg 5, within 0.3 us of 4 at cfg 4) and threads per row (GPMI_SPMM_WTPR 4 or 8)
-    const char* uenv = std::getenv("GPMI_SPMM_WUNR");
-    const int un = uenv ? std::atoi(uenv) : 8;
-    const char* tenv = std::getenv("GPMI_SPMM_WTPR");
-    const int tpr = tenv && std::atoi(tenv) == 8 ? 8 : 4;
-    auto pick = [un](auto k4, auto k8, auto k16) { return un == 4 ? k4 : un == 8 ? k8 : k16; };
-    auto kfn = tpr == 4
-        ? (s == 20 ? pick(csr_spmm_wing_kernel<20, 4, 4>, csr_spmm_wing_kernel<20, 8, 4>,
-                          csr_spmm_wing_kernel<20, 16, 4>)
-           : s == 12 ? pick(csr_spmm_wing_kernel<12, 4, 4>, csr_spmm_wing_kernel<12, 8, 4>,
-                            csr_spmm_wing_kernel<12, 16, 4>)
-           : s == 11 ? pick(csr_spmm_wing_kernel<11, 4, 4>, csr_spmm_wing_kernel<11, 8, 4>,
-                            csr_spmm_wing_kernel<11, 16, 4>)
-           : s == 8 ? pick(csr_spmm_wing_kernel<8, 4, 4>, csr_spmm_wing_kernel<8, 8, 4>,
-                           csr_spmm_wing_kernel<8, 16, 4>)
-                     : pick(csr_spmm_wing_kernel<7, 4, 4>, csr_spmm_wing_kernel<7, 8, 4>,
-                            csr_spmm_wing_kernel<7, 16, 4>))
-        : (s == 20 ? pick(csr_spmm_wing_kernel<20, 4, 8>, csr_spmm_wing_kernel<20, 8, 8>,
-                          csr_spmm_wing_kernel<20, 16, 8>)
-           : s == 12 ? pick(csr_spmm_wing_kernel<12, 4, 8>, csr_spmm_wing_kernel<12, 8, 8>,
-                            csr_spmm_wing_kernel<12, 16, 8>)
-           : s == 11 ? pick(csr_spmm_wing_kernel<11, 4, 8>, csr_spmm_wing_kernel<11, 8, 8>,
-                            csr_spmm_wing_kernel<11, 16, 8>)
-           : s == 8 ? pick(csr_spmm_wing_kernel<8, 4, 8>, csr_spmm_wing_kernel<8, 8, 8>,
-                           csr_spmm_wing_kernel<8, 16, 8>)
-                     : pick(csr_spmm_wing_kernel<7, 4, 8>, csr_spmm_wing_kernel<7, 8, 8>,
-                            csr_spmm_wing_kernel<7, 16, 8>));
+    const size_t lds = sizeof(double) * (size_t)s *
+                       (size_t)std::max(sp->win_maxu.load(std::memory_order_acquire), WIN_ROWS_HOST);
+    auto kfn = s == 20   ? csr_spmm_wing_kernel<20, WING_U, WING_TPR>
+               : s == 12 ? csr_spmm_wing_kernel<12, WING_U, WING_TPR>
+               : s == 11 ? csr_spmm_wing_kernel<11, WING_U, WING_TPR>
+               : s == 8  ? csr_spmm_wing_kernel<8, WING_U, WING_TPR>
+                         : csr_spmm_wing_kernel<7, WING_U, WING_TPR>;
+    const int tpr = WING_TPR;
     hipLaunchKernelGGL(kfn, dim3((unsigned)sp->win_nblk), dim3(64 * tpr), lds, st, sp->indptr,
                        sp->indices, sp->win_lidx, sp->data, sp->n, sp->win_cols, sp->win_u, X, Y,
                        eta, pqp);
@@ -403,19 +376,10 @@ int spmm(gpmi_sp* sp, const double* X, double* Y, int s, double eta, hipStream_t
     if (pqp && pq_blocks) *pq_blocks = (int)sp->win_nblk;
     return 0;
   }
-  if (kind == 2) {
-    // the one-pass full-width window (csr_spmm_winf_kernel) at the Lanczos width
-    const size_t lds = sizeof(double) * (size_t)s * (size_t)std::max(1, sp->win_maxu) +
-                       10 * (size_t)sp->win_maxm + 4 + sizeof(int) * (WIN_ROWS_HOST + 1);
-    hipLaunchKernelGGL(csr_spmm_winf_kernel<20>, dim3((unsigned)sp->win_nblk), dim3(256), lds,
-                       st, sp->indptr, sp->indices, sp->win_lidx, sp->data, sp->n,
-                       sp->win_cols, sp->win_u, X, Y, eta);
-    SP_LAUNCH("csr_spmm_winf_kernel");
-    return 0;
-  }
   if (kind == 1) {
     // window + the largest windowed block's values, positions and row starts
-    const size_t lds = sizeof(double) * WIN_CS_HOST * (size_t)std::max(1, sp->win_maxu) +
+    const size_t lds = sizeof(double) * WIN_CS_HOST *
+                           (size_t)std::max(1, sp->win_maxu.load(std::memory_order_acquire)) +
                        10 * (size_t)sp->win_maxm + 4 + sizeof(int) * (WIN_ROWS_HOST + 1);
     hipLaunchKernelGGL(csr_spmm_win_kernel,
                        dim3((unsigned)sp->win_nblk),
@@ -426,12 +390,9 @@ int spmm(gpmi_sp* sp, const double* X, double* Y, int s, double eta, hipStream_t
   }
   if (kind == 3 && (reinterpret_cast<uintptr_t>(X) & 15) == 0 &&
       (reinterpret_cast<uintptr_t>(Y) & 15) == 0) {
-    // gathers in flight per lane (GPMI_SPMM_PUNR: 2, 3 or 4; 3 measured fastest at cfg 5)
-    const char* uenv = std::getenv("GPMI_SPMM_PUNR");
-    const int u = uenv ? std::atoi(uenv) : 3;
-    auto kfn = u == 2 ? csr_spmm_pair_kernel<2> : u == 3 ? csr_spmm_pair_kernel<3>
-                                                           : csr_spmm_pair_kernel<4>;
-    hipLaunchKernelGGL(kfn, dim3((unsigned)((sp->n + 3) / 4)), dim3(256), 0, st,
+    // three gathers in flight per lane (measured at cfg 5: two 126.4, three 125.9, four
+    // 132.5 us per s = 20 launch)
+    hipLaunchKernelGGL(csr_spmm_pair_kernel<3>, dim3((unsigned)((sp->n + 3) / 4)), dim3(256), 0, st,
                        sp->indptr, sp->indices, sp->data, sp->n, X, Y, s, 64 / (s / 2), eta);
     SP_LAUNCH("csr_spmm_pair_kernel");
     return 0;
@@ -577,22 +538,17 @@ int lanczos_block_dcgs2(gpmi_sp* sp, double* V, double* U, double* Y, int s, int
   double* dbe = dal + (size_t)s * steps;
   int* dead = reinterpret_cast<int*>(dbe + (size_t)s * steps);
   int* inex = dead + s;
-  // row blocks of the dot partials (GPMI_LZ_NB; fixed per call: deterministic)
-  const char* benv = std::getenv("GPMI_LZ_NB");
-  const int lz_nb = benv ? std::max(64, std::min(4096, std::atoi(benv))) : LZ_NB;
+  // row blocks of the dot partials (fixed: deterministic; 256 / 1024 / 2048 measured
+  // 2-5 % slower at cfg 5)
+  const int lz_nb = LZ_NB;
   int rc = ensure_partial(sp, (size_t)lz_nb * (2 * steps + 2) * s);
   if (rc) return rc;
   SP_TRY(hipMemsetAsync(H, 0, sizeof(double) * s * hsz, sp->stream));
   SP_TRY(hipMemsetAsync(dal, 0, sizeof(double) * 2 * s * steps, sp->stream));
   SP_TRY(hipMemcpyAsync(U, V, sizeof(double) * ns, hipMemcpyDeviceToDevice, sp->stream));
-  // GPMI_LZ_NR: row chunks per thread of the update pass (1 or 4)
-  const char* nenv = std::getenv("GPMI_LZ_NR");
-  const int lz_nr = nenv ? std::atoi(nenv) : 4;
-  // non-temporal basis reads for a basis over twice the 256 MB Infinity Cache
-  // (GPMI_LZ_NT=0 / 1 forces either)
-  const char* tenv = std::getenv("GPMI_LZ_NT");
-  const bool lz_nt = tenv ? std::atoi(tenv) != 0
-                          : sizeof(double) * (double)ns * (steps + 1) > 512.0 * 1024 * 1024;
+  // non-temporal basis reads for a basis over twice the 256 MB Infinity Cache (cfg 5
+  // Lanczos 13.0 -> 11.2 ms; at cfg 4's 0.3 GB they measured slower, 6.8 -> 7.0 ms)
+  const bool lz_nt = sizeof(double) * (double)ns * (steps + 1) > 512.0 * 1024 * 1024;
   for (int k = 0; k <= steps; ++k) {
     const bool last = k == steps;
     if (!last) {
@@ -617,20 +573,15 @@ int lanczos_block_dcgs2(gpmi_sp* sp, double* V, double* U, double* Y, int s, int
                        steps, s, H, cv, cu, ir, rho, dead, inex, dal, dbe, stage);
     SP_LAUNCH("lz_scalar_kernel");
     if (!last) {
-      if (lz_nr == 4) {
-        // four row chunks per thread sharing its two columns' coefficients: the grid's
-        // thread-pair count P with 2 P a multiple of s
-        const int64_t q = s / std::__gcd(512, s);
-        int64_t g = (ns / 2 + 1023) / 1024;
-        g = (g + q - 1) / q * q;
-        auto kfn = lz_nt ? lz_update_kernel<4, true> : lz_update_kernel<4, false>;
-        hipLaunchKernelGGL(kfn, dim3((unsigned)g), dim3(256), 0, sp->stream, V, ns, k, U, Y, cv,
-                           cu, ir, s);
-      } else {
-        auto kfn = lz_nt ? lz_update_kernel<1, true> : lz_update_kernel<1, false>;
-        hipLaunchKernelGGL(kfn, dim3((unsigned)((ns + 511) / 512)), dim3(256), 0, sp->stream, V,
-                           ns, k, U, Y, cv, cu, ir, s);
-      }
+      // four row chunks per thread sharing its two columns' coefficients (cfg 5 Lanczos
+      // 13.7 -> 12.65 ms against one): the grid's thread-pair count P with 2 P a
+      // multiple of s
+      const int64_t q = s / std::__gcd(512, s);
+      int64_t g = (ns / 2 + 1023) / 1024;
+      g = (g + q - 1) / q * q;
+      auto kfn = lz_nt ? lz_update_kernel<4, true> : lz_update_kernel<4, false>;
+      hipLaunchKernelGGL(kfn, dim3((unsigned)g), dim3(256), 0, sp->stream, V, ns, k, U, Y, cv, cu,
+                         ir, s);
       SP_LAUNCH("lz_update_kernel");
     }
   }
@@ -1220,27 +1171,16 @@ static int msgram_impl(gpmi_sp* sp, const double* etas, int neta, const double* 
   const int64_t n = sp->n;
   const int S = neta;
   // Padding (the Gram of the real columns is unchanged by a zero column, inactive
-  // from the start: ||b|| = 0). GPMI_MSGRAM_PAD=1: an odd block that would run the one-column gather SpMM gets a
-  // zero column (an inactive CG column from the start: ||b|| = 0) so that the
-  // column-pair gather runs; measured slower at cfg 5 (s = 11 gather 119 us, s = 12
-  // pair 161 us per launch), so off by default
+  // from the start: ||b|| = 0): the window SpMM at s = 11 stages 12-column rows with
+  // 16-byte loads: cfg 5 s = 11 88 -> 73 us per launch, step 21.7 -> 20.9 ms (s = 7 ->
+  // 8 measured neutral at cfg 4; an odd block padded for the column-pair gather
+  // measured slower at cfg 5, 161 against 119 us)
   int s = nsub;
   {
     int kind = 0;
     int rc0 = spmm_kind(sp, s, &kind);
     if (rc0) return rc0;
-    const char* penv = std::getenv("GPMI_MSGRAM_PAD");
-    if (full && kind == 0 && (s & 1) && s + 1 <= MS_MAXS && S * (s + 1) <= 1024 && penv &&
-        std::atoi(penv) == 1)
-      ++s;
-    // the window SpMM at s = 11 stages 12-column rows with 16-byte loads (a zero
-    // column, stopped from the start): cfg 5 s = 11 88 -> 73 us per launch, step 21.7 ->
-    // 20.9 ms; s = 7 -> 8 measured neutral at cfg 4, only with GPMI_MSGRAM_PAD=2
-    // (GPMI_MSGRAM_PAD=0: no padding)
-    const int pmode = penv ? std::atoi(penv) : -1;
-    if (full && kind == 5 && (s == 11 || (s == 7 && pmode == 2)) && S * (s + 1) <= 1024 &&
-        pmode != 0 && pmode != 1)
-      ++s;
+    if (full && kind == 5 && s == 11 && S * (s + 1) <= 1024) ++s;
   }
   // the dot columns: all of B (with the padding column when the full block is padded)
   const int nbd = full ? s : nrhs;
@@ -1249,8 +1189,11 @@ static int msgram_impl(gpmi_sp* sp, const double* etas, int neta, const double* 
   const int64_t ns = n * s;
   const double eta0 = *std::min_element(etas, etas + neta);
   int rc = 0;
-  // B [n][nbd], its host staging [n][nrhs], and R, P, Q, R' [n][s]
-  const size_t wsn = (size_t)nsb + (size_t)n * nrhs + (size_t)4 * ns;
+  // B [n][nbd], its host staging [n][nrhs], and R, P, Q [n][s], each segment an even
+  // number of doubles so that every block starts 16-byte aligned (the window and
+  // pair SpMMs read X with 16-byte loads; an odd n would misalign them)
+  auto even = [](size_t d) { return (d + 1) & ~(size_t)1; };
+  const size_t wsn = even((size_t)nsb) + even((size_t)n * nrhs) + 3 * even((size_t)ns);
   if (sp->ms_ws_doubles < wsn) {
     if (sp->ms_ws) SP_TRY(hipFree(sp->ms_ws));
     sp->ms_ws = nullptr;
@@ -1292,7 +1235,6 @@ static int msgram_impl(gpmi_sp* sp, const double* etas, int neta, const double* 
   st.a_prev = q; q += s;
   st.beta = q; q += s;
   st.bn2 = q; q += s;
-  double* pqd = q; q += s;   // p . q (unfused r update)
   st.z = q; q += (size_t)S * s;
   st.z_prev = q; q += (size_t)S * s;
   st.bp = q; q += (size_t)S * nbd * s;
@@ -1306,29 +1248,17 @@ static int msgram_impl(gpmi_sp* sp, const double* etas, int neta, const double* 
   double* brd = q;                         // [ne] reduced B^T r, r . r
   sp->last_converged = 0;
   double* Bd = sp->ms_ws;
-  double* Hs = Bd + nsb;   // the host block as given (original row order)
-  double* Rd = Hs + n * nrhs;
-  double* Pd = Rd + ns;
-  double* Qd = Pd + ns;
-  double* Rd2 = Qd + ns;   // the residual alternates between Rd and Rd2
-  // The r update and B^T r, r . r on MFMA in one pass (ms_rmfma_kernel, s <= 16: every
-  // block the library forms). GPMI_MS_MFMA=0: the fused scalar form for <= 2 column groups
-  // of 4 of B (ms_rdots_partial_kernel, which re-reads q once per group; the default
-  // before: cfg 4 6.9-7.3 ms per step against 6.3 with the MFMA form), else the separate
-  // update and dots
-  const char* menv = std::getenv("GPMI_MS_MFMA");
-  const bool mfma_r = s <= 16 && !(menv && std::atoi(menv) == 0);
-  const bool fused_r = !mfma_r && (nbd + 3) / 4 <= 2;
-  // chip-wide partial reduction for the MFMA form's 512 partial rows (cfg 5: step
-  // 33.6 -> 32.0 ms); the fused form's 128 stay in the scalar kernel (cfg 4: the
-  // extra launch costs more than it saves). GPMI_MS_RED=0 / 1 forces either.
-  const char* renv = std::getenv("GPMI_MS_RED");
-  const bool chip_red = renv ? std::atoi(renv) != 0 : mfma_r;
-  // p . q from the window SpMM's epilogue (GPMI_MS_PQEPI=0: col_dot_partial_kernel)
-  const char* qenv = std::getenv("GPMI_MS_PQEPI");
-  const bool pq_epi = (fused_r || mfma_r) && !(qenv && std::atoi(qenv) == 0);
+  double* Hs = Bd + even((size_t)nsb);   // the host block as given (original row order)
+  double* Rd = Hs + even((size_t)n * nrhs);
+  double* Pd = Rd + even((size_t)ns);
+  double* Qd = Pd + even((size_t)ns);
+  // Per iteration: the SpMM (p . q partials from the window kernel's epilogue, else
+  // col_dot_partial_kernel), then the r update and B^T r, r . r on MFMA in one pass over
+  // b, r, q (ms_rmfma_kernel, s <= 16: every block the library forms; cfg 4 6.9-7.3 ->
+  // 6.3 ms per step against the scalar forms it replaced), its 512 partial rows summed
+  // one wave per element across the chip (cfg 5 33.6 -> 32.0 ms against the
+  // one-workgroup sum), the per-shift scalars, and p = r + beta p.
   double* Rcur = Rd;     // the live residual
-  double* Rnext = Rd2;
   hipStream_t str = sp->ms_stream;
   {
     // the RHS block as the caller holds it (rows in the original order) into the
@@ -1391,7 +1321,7 @@ static int msgram_impl(gpmi_sp* sp, const double* etas, int neta, const double* 
     // the window SpMM also forms the p . q block partials in its epilogue (summed
     // across the chip below); other kernels leave them to col_dot_partial_kernel
     int pqb = 0;
-    rc = spmm(sp, Pd, Qd, s, eta0, str, pq_epi ? pqpart : nullptr, &pqb);
+    rc = spmm(sp, Pd, Qd, s, eta0, str, pqpart, &pqb);
     if (rc) return rc;
     const double* pqin = pqpart;
     int pqn = NBLK;
@@ -1402,56 +1332,22 @@ static int msgram_impl(gpmi_sp* sp, const double* etas, int neta, const double* 
       pqin = pqsum;
       pqn = 1;
     }
-    double* Rout = Rcur;
-    if (fused_r) {
-      // p . q partials; the reduction, r update and dots in one launch (r_new to the
-      // other buffer)
-      if (pqb == 0) {
-        hipLaunchKernelGGL(col_dot_partial_kernel, dim3(NBLK, 1), dim3(256), 0, str, Pd,
-                           (int64_t)0, Qd, n, s, pqpart);
-        SP_LAUNCH("col_dot_partial_kernel");
-      }
-      Rout = Rnext;
-      launch_ms_rdots(Bd, Rcur, Rout, Qd, st, pqin, pqn, n, s, partial, MS_NBLK, str, nbd);
-      SP_LAUNCH("ms_rdots_partial_kernel");
-      std::swap(Rcur, Rnext);
-    } else if (mfma_r) {
-      // p . q partials, then the reduction, the r update (in place) and B^T r, r . r
-      // on MFMA in one pass over b, r, q (ms_rmfma_kernel)
-      if (pqb == 0) {
-        hipLaunchKernelGGL(col_dot_partial_kernel, dim3(NBLK, 1), dim3(256), 0, str, Pd,
-                           (int64_t)0, Qd, n, s, pqpart);
-        SP_LAUNCH("col_dot_partial_kernel");
-      }
-      hipLaunchKernelGGL(ms_rmfma_kernel, dim3(MS_RB), dim3(256), 0, str, Bd, Rcur, Qd, st,
-                         pqin, pqn, n, s, nbd, partial);
-      SP_LAUNCH("ms_rmfma_kernel");
-    } else {
-      // more than two 4-column groups would re-read q per group in the fused form:
-      // the r update in place, then the dots
-      rc = col_dots(sp, Pd, 0, 1, Qd, s, pqd, pqpart, str);
-      if (rc) return rc;
-      hipLaunchKernelGGL(ms_r_update_kernel, dim3(grid_ns(n, s)), dim3(256), 0, str, Rcur, Qd, st,
-                         pqd, n, s);
-      SP_LAUNCH("ms_r_update_kernel");
-      launch_ms_dots(Bd, Rcur, n, s, partial, MS_NBLK, str, nbd);
-      SP_LAUNCH("ms_dots_partial_kernel");
+    if (pqb == 0) {
+      hipLaunchKernelGGL(col_dot_partial_kernel, dim3(NBLK, 1), dim3(256), 0, str, Pd, (int64_t)0,
+                         Qd, n, s, pqpart);
+      SP_LAUNCH("col_dot_partial_kernel");
     }
-    // the ne = s^2 + s partial sums reduced one wave per element across the chip
-    // (GPMI_MS_RED=0: inside the one-workgroup scalar kernel, 16 waves)
-    const int pnb = mfma_r ? MS_RB : MS_NBLK;
-    if (chip_red) {
-      hipLaunchKernelGGL(col_dot_reduce_kernel, dim3((ne + 3) / 4), dim3(256), 0, str, partial,
-                         pnb, 1, ne, brd);
-      SP_LAUNCH("col_dot_reduce_kernel");
-    }
-    hipLaunchKernelGGL(ms_scalar_kernel, dim3(1), dim3(sthreads), 0, str, st,
-                       chip_red ? (const double*)brd : partial, chip_red ? 0 : pnb, dshift, S, s,
-                       nbd, rtol * rtol, beta_out);
+    hipLaunchKernelGGL(ms_rmfma_kernel, dim3(MS_RB), dim3(256), 0, str, Bd, Rcur, Qd, st, pqin,
+                       pqn, n, s, nbd, partial);
+    SP_LAUNCH("ms_rmfma_kernel");
+    hipLaunchKernelGGL(col_dot_reduce_kernel, dim3((ne + 3) / 4), dim3(256), 0, str, partial, MS_RB,
+                       1, ne, brd);
+    SP_LAUNCH("col_dot_reduce_kernel");
+    hipLaunchKernelGGL(ms_scalar_kernel, dim3(1), dim3(sthreads), 0, str, st, (const double*)brd,
+                       0, dshift, S, s, nbd, rtol * rtol, beta_out);
     SP_LAUNCH("ms_scalar_kernel");
     hipLaunchKernelGGL(ms_p_update_kernel, dim3((unsigned)((ns + 1023) / 1024)), dim3(256), 0,
-                       str, Pd, Rout,
-                       st.beta, st.active, n, s);
+                       str, Pd, Rcur, st.beta, st.active, n, s);
     SP_LAUNCH("ms_p_update_kernel");
   }
   {
@@ -1491,13 +1387,12 @@ int gpmi_sp_spmm_info(gpmi_sp* sp, int* windowed, double* mean_window, int* max_
     if (max_window) *max_window = 0;
     return 0;
   }
-  if (sp->win_maxu < 0)
-    if (int rc = ensure_window(sp)) return rc;
+  if (int rc = ensure_window(sp)) return rc;
   const char* wenv = std::getenv("GPMI_SPMM_WINDOW");
   const int wmode = wenv ? std::atoi(wenv) : 1;
   if (windowed) *windowed = wmode == 2 || (wmode != 0 && sp->win_use);
   if (mean_window) *mean_window = sp->win_mean;
-  if (max_window) *max_window = sp->win_maxu;
+  if (max_window) *max_window = sp->win_maxu.load(std::memory_order_acquire);
   return 0;
 }
 

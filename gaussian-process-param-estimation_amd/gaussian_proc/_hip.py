@@ -196,6 +196,8 @@ class Operator(object):
         check(self.lib.gpmi_op_size(self.h, None, ctypes.byref(npad)), 'gpmi_op_size')
         self.n_pad = npad.value
         self.nrhs = 0
+        # bumped whenever K changes: caches over K (e.g. SLQ Ritz nodes) compare it
+        self.generation = 0
 
     def close(self):
         if getattr(self, 'h', None) is not None and self.h.value:
@@ -213,6 +215,7 @@ class Operator(object):
         if K.shape != (self.n, self.n):
             raise ValueError('K must be %d x %d' % (self.n, self.n))
         check(self.lib.gpmi_op_load_matrix(self.h, dptr(K), self.n), 'gpmi_op_load_matrix')
+        self.generation += 1
 
     def load_sparse(self, sop):
         """K from a SparseOperator on the same device (device-side scatter of its
@@ -220,6 +223,7 @@ class Operator(object):
         if sop.n != self.n:
             raise ValueError('sparse operator has n = %d, expected %d' % (sop.n, self.n))
         check(self.lib.gpmi_op_load_sparse(self.h, sop.h), 'gpmi_op_load_sparse')
+        self.generation += 1
 
     def assemble_matern(self, points, scale, nu):
         points = as_c(points)
@@ -227,6 +231,7 @@ class Operator(object):
         check(self.lib.gpmi_op_assemble_matern(self.h, dptr(points), points.shape[1],
                                                dptr(scale), float(nu)),
               'gpmi_op_assemble_matern')
+        self.generation += 1
 
     def get_matrix(self):
         K = numpy.empty((self.n, self.n))
@@ -572,15 +577,17 @@ class SparseOperator(object):
 
     def spmm_kernel(self, s):
         """-> the SpMM kernel an s-column block runs: 'csr_spmm_kernel' (gather),
-        'csr_spmm_win_kernel' (window, 8-column chunks), 'csr_spmm_winf_kernel'
-        (window, one full-width pass) or 'csr_spmm_pair_kernel' (gather by column
-        pairs) (see gpmi_sp_spmm_kernel). It names the kernel for a 16-byte
-        aligned block, which every block the library forms is (host inputs are
-        copied into hipMalloc'd workspaces; even-s offsets keep the alignment);
-        an unaligned device block handed in directly runs csr_spmm_kernel."""
+        'csr_spmm_win_kernel' (window, 8-column chunks), 'csr_spmm_pair_kernel'
+        (gather by column pairs), 'dense_mm_kernel' (a dense K) or
+        'csr_spmm_wing_kernel' (window with latency-hidden staging) (see
+        gpmi_sp_spmm_kernel). It names the kernel for a 16-byte aligned block,
+        which every block the library forms is (host inputs are copied into
+        hipMalloc'd workspaces whose segments are even numbers of doubles); an
+        unaligned device block handed in directly runs csr_spmm_kernel."""
         k = ctypes.c_int()
         check(self.lib.gpmi_sp_spmm_kernel(self.h, int(s), ctypes.byref(k)),
               'gpmi_sp_spmm_kernel')
+        # index 2 was the round-2 one-pass window (superseded by the wing kernel)
         return ('csr_spmm_kernel', 'csr_spmm_win_kernel', 'csr_spmm_winf_kernel',
                 'csr_spmm_pair_kernel', 'dense_mm_kernel', 'csr_spmm_wing_kernel')[k.value]
 

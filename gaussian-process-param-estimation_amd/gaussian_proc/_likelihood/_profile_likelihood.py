@@ -216,4 +216,7 @@ class ProfileLikelihood(object):
                 raise ValueError('eta must be zero or inf at this point.')
             success = True
         ProfileLikelihood.last_der1_calls = (fb.calls, fb.points, dict(fb.memo))
+        # the largest eta batch of one device call (<= 64: the band operator's
+        # cyclic-reduction path, gpmi_band_der_terms)
+        ProfileLikelihood.last_der1_max_batch = fb.max_points
         return {'sigma': sigma, 'sigma0': sigma0, 'eta': eta, 'success': success}

@@ -25,8 +25,10 @@ __all__ = ['find_interval_with_sign_change', 'chandrupatla_method', 'BatchedFunc
 class BatchedFunction(object):
     """Scalar view f(x) of a batched function fb(xs) -> values, memoised by the
     exact float x. ``request(xs, speculative)`` evaluates the missing points of
-    xs, plus the missing speculative points, in one call of fb (at most
-    ``spec_budget`` of them per call; 0 turns speculation off); ``f(x)``
+    xs, plus the missing speculative points, in one call of fb (speculative
+    points only up to ``spec_budget`` points per call, required ones included:
+    the band operator's default 64 keeps every call on its cyclic-reduction
+    path, gpmi_band_der_terms' limit; 0 turns speculation off); ``f(x)``
     returns a cached value or evaluates x alone. ``calls`` counts the batched
     calls, ``points`` the evaluated points.
 
@@ -45,6 +47,7 @@ class BatchedFunction(object):
         self.memo = {}
         self.calls = 0
         self.points = 0
+        self.max_points = 0
         self.spec_failures = 0
 
     def _missing(self, xs, skip=()):
@@ -59,11 +62,12 @@ class BatchedFunction(object):
         vals = self.fb(numpy.array(miss))
         self.calls += 1
         self.points += len(miss)
+        self.max_points = max(self.max_points, len(miss))
         return [float(v) for v in vals]
 
     def request(self, xs, speculative=()):
         miss = self._missing(xs)
-        spec = self._missing(speculative, skip=miss)[:self.spec_budget]
+        spec = self._missing(speculative, skip=miss)[:max(0, self.spec_budget - len(miss))]
         if not miss:
             # nothing is needed yet: prefetching alone would be a call the
             # reference does not make
@@ -115,7 +119,7 @@ def find_interval_with_sign_change_batched(fb, bracket, num_bracket_trials, tol=
     spec.append(xt)
     if tol is not None:
         spec += _chandrupatla_candidates(x1, x0, x1, xt, tol, tol,
-                                         max(0, fb.spec_budget - len(spec)))
+                                         max(0, fb.spec_budget - len(spec) - 2))
     fb.request([x0, x1], speculative=spec)
 
     def f(x):
@@ -245,7 +249,8 @@ def chandrupatla_method(f, bracket, bracket_values, verbose=False, eps_m=None, e
     t = 0.5
     iterations = 0
     xm = b
-    budget = getattr(f, 'spec_budget', 0) if isinstance(f, BatchedFunction) and not args \
+    # speculative candidates beside the one required point xt per call
+    budget = getattr(f, 'spec_budget', 0) - 1 if isinstance(f, BatchedFunction) and not args \
         else 0
     while maxiter > 0:
         maxiter -= 1

@@ -57,6 +57,40 @@ __all__ = ['MixedCorrelation']
 
 _METHODS = ('eigenvalue', 'cholesky', 'hutchinson', 'slq')
 
+# The imate keyword options the reference forwards as **imate_options
+# (mixed_correlation.py:133-143,183-209,241-268) to imate's trace / traceinv /
+# logdet functions of each method; those functions take no other keywords, so
+# any other key is a TypeError there (and here, at construction). The keys the
+# reference passes itself (exponent, symmetric, eigenvalues, assume_matrix,
+# parameters) are duplicates, a TypeError as well.
+_IMATE_OPTIONS = {
+    'eigenvalue': {'non_zero_ratio', 'tol'},
+    'cholesky': {'cholmod', 'invert_cholesky'},
+    'hutchinson': {'min_num_samples', 'max_num_samples', 'error_atol', 'error_rtol',
+                   'confidence_level', 'outlier_significance_level', 'solver_tol',
+                   'orthogonalize', 'num_threads', 'verbose', 'plot', 'seed'},
+    'slq': {'min_num_samples', 'max_num_samples', 'error_atol', 'error_rtol',
+            'confidence_level', 'outlier_significance_level', 'lanczos_degree', 'lanczos_tol',
+            'orthogonalize', 'num_threads', 'num_gpu_devices', 'gpu', 'verbose', 'plot', 'seed'},
+}
+# this build's extensions ("imate options"): a fixed probe count,
+# the CG tolerance of the sparse solves, and the bounds of the lanczos_tol control
+_EXTENSIONS = {
+    'hutchinson': {'num_samples', 'cg_rtol'},
+    'slq': {'num_samples', 'cg_rtol', 'max_lanczos_degree', 'spectrum_lower_bound'},
+}
+
+
+def _check_options(method, options):
+    """TypeError for a key imate's functions of ``method`` would not accept."""
+    if method not in _IMATE_OPTIONS:
+        return
+    allowed = _IMATE_OPTIONS[method] | _EXTENSIONS.get(method, set())
+    bad = sorted(k for k in (options or {}) if k not in allowed)
+    if bad:
+        raise TypeError("imate_options for imate_method='%s': unexpected keyword argument%s %s"
+                        % (method, 's' if len(bad) > 1 else '', ', '.join(map(repr, bad))))
+
 
 class MixedCorrelation(object):
     """K + eta I without forming sigma^2 K + sigma0^2 I."""
@@ -67,6 +101,7 @@ class MixedCorrelation(object):
         self.interpolant_points = interpolant_points
         self.imate_method = imate_method
         self.imate_options = imate_options
+        _check_options(imate_method, imate_options)
         if self.interpolate:
             if self.interpolant_points is None:
                 raise TypeError('When "interpolate" is set to "True", the '
@@ -98,27 +133,48 @@ class MixedCorrelation(object):
         self._band = None
         self._band_rhs = None
         self._eig = None
+        self._slq_options()
         if self.imate_method == 'slq':
             # Krylov primitives over the resident dense K (dense_mm_kernel)
             self.sop = _hip.SparseOperator.from_dense(self.op)
-            self._slq_options()
         if self.interpolate:
             self._build_interpolant()
 
     def _slq_options(self):
+        """The stochastic estimators' options ('slq', 'hutchinson'; INTEGRATION.md
+        lists where the defaults differ from imate's)."""
         opts = dict(self.imate_options or {})
         self.num_samples = int(opts.get('num_samples', opts.get('max_num_samples', 20)))
         self.lanczos_degree = int(opts.get('lanczos_degree', 30))
-        self.seed = int(opts.get('seed', 0))
-        self.cg_rtol = float(opts.get('cg_rtol', 1e-6))
+        self.seed = int(opts.get('seed', 0) or 0)
+        self.cg_rtol = float(opts.get('cg_rtol', opts.get('solver_tol', 1e-6)))
         # imate's Lanczos option (-1 full reorthogonalisation, this build's default;
         # 0 the plain three-term recurrence, imate's default; k > 0 the last k vectors)
         self.orthogonalize = int(opts.get('orthogonalize', -1))
+        if self.imate_method == 'hutchinson':
+            # imate's Hutchinson option: orthogonalised probes (its default True)
+            self.orthogonalize = bool(opts.get('orthogonalize', True))
+        # imate's lanczos_tol: the Lanczos runs until the quadrature has converged
+        # to this relative tolerance at the eta asked (the gap of the Gauss and
+        # Gauss-Radau rules, _slq.bracket), its degree doubling from lanczos_degree
+        # up to max_lanczos_degree (extension; 256, the device's limit). None: the
+        # fixed lanczos_degree, as imate.
+        tol = opts.get('lanczos_tol')
+        self.lanczos_tol = None if tol is None else float(tol)
+        self.max_lanczos_degree = max(self.lanczos_degree,
+                                      min(256, int(opts.get('max_lanczos_degree', 256))))
+        # the Gauss-Radau node: a lower bound of the spectrum of K (a dense
+        # correlation matrix is positive semi-definite: 0; a sparse tapered K is
+        # indefinite: its Gershgorin bound unless given)
+        lb = opts.get('spectrum_lower_bound')
+        self.spectrum_lower_bound = None if lb is None else float(lb)
         # imate's adaptive sample count (opt-in: any of its error options without
         # 'num_samples'): probes are added until the confidence-interval half width
         # z sigma / sqrt(k) of the estimate meets max(error_atol, error_rtol |mean|),
         # between min_num_samples and max_num_samples (imate's defaults 10, 50, 1e-2,
         # 0.95). Counter-based probes: the adaptive set is a prefix of the fixed one.
+        # The probes it adds are kept apart from the fixed set (num_samples and
+        # slq_nodes() do not change with earlier adaptive calls).
         self._adaptive = 'num_samples' not in opts and any(
             k in opts for k in ('min_num_samples', 'error_rtol', 'error_atol',
                                 'confidence_level'))
@@ -131,6 +187,9 @@ class MixedCorrelation(object):
             self.confidence_level = float(opts.get('confidence_level', 0.95))
             self.num_samples = self.min_num_samples
         self._nodes = None
+        self._lz = None            # (generation, degree, alpha, beta) of the fixed set
+        self._extra = []           # adaptive probes beyond the fixed set: (alpha, beta)
+        self.lanczos_degree_used = self.lanczos_degree
 
     def _build_interpolant(self):
         """imate.InterpolateTraceInv of the reference (mixed_correlation.py:52-66),
@@ -256,34 +315,149 @@ class MixedCorrelation(object):
         if self.interpolate:
             self._build_interpolant()
 
-    def slq_nodes(self):
-        """Ritz nodes of every probe (computed once; eta-independent)."""
+    def _generation(self):
+        return getattr(self.op, 'generation', 0) if not self.sparse else 0
+
+    def _lower_bound(self):
+        if self.spectrum_lower_bound is not None:
+            return self.spectrum_lower_bound
+        if not self.sparse:
+            return 0.0
+        Kc = self.sop.csr()
+        off = numpy.asarray(abs(Kc).sum(axis=1)).ravel() - numpy.abs(Kc.diagonal())
+        return float(numpy.min(Kc.diagonal() - off))
+
+    def _lanczos(self, nprobe, degree, offset=0):
+        return self.sop.lanczos(nprobe, degree, self.seed, probe_offset=offset,
+                                orthogonalize=self.orthogonalize)
+
+    def _fixed_lanczos(self, degree):
+        """alpha / beta of the fixed probe set at ``degree`` (cached per K)."""
+        c = self._lz
+        if c is None or c[0] != self._generation() or c[1] != degree:
+            a, b = self._lanczos(self.num_samples, degree)
+            self._lz = (self._generation(), degree, a, b)
+            self._nodes = None
+            self._extra = []
+        return self._lz[2], self._lz[3]
+
+    def slq_nodes(self, etas=None, funcs=('logdet',)):
+        """Ritz nodes of every probe of the fixed set (eta-independent; cached
+        until K changes). With ``lanczos_tol`` set and ``etas`` given, the
+        Lanczos degree is first raised (doubling, up to max_lanczos_degree) until
+        the Gauss / Gauss-Radau gap of the probe-mean quadrature of each of
+        ``funcs`` at min(etas) is within lanczos_tol (slq_converge)."""
+        if etas is not None and self.lanczos_tol is not None:
+            self.slq_converge(etas, funcs)
+        a, b = self._fixed_lanczos(self.lanczos_degree_used)
         if self._nodes is None:
-            a, b = self.sop.lanczos(self.num_samples, self.lanczos_degree, self.seed,
-                                    orthogonalize=self.orthogonalize)
             self._nodes = _slq.nodes(a, b)
         return self._nodes
 
+    def slq_converge(self, etas, funcs=('logdet',)):
+        """imate's lanczos_tol on this operator: the Lanczos degree of the fixed
+        probe set at which the quadrature of ``funcs`` (names of _slq.FUNCS or
+        callables) has converged at min(etas) to lanczos_tol, relative (or the
+        max_lanczos_degree cap). Returns dict(degree, bracket, converged)."""
+        etas = numpy.atleast_1d(numpy.asarray(etas, dtype=float))
+        e = [float(etas.min())]
+        fns = [_slq.FUNCS[f] if isinstance(f, str) else f for f in funcs]
+        lo = self._lower_bound()
+        deg = self.lanczos_degree_used
+        while True:
+            a, b = self._fixed_lanczos(deg)
+            g = _slq.nodes(a, b)
+            _slq.check_shifts(_slq.min_ritz(g), e)
+            r = _slq.radau_nodes(a, b, min(lo, _slq.min_ritz(g) - 1e-12 * abs(_slq.min_ritz(g))))
+            gap = max(float(_slq.bracket(g, r, e, f)[0]) for f in fns)
+            ok = gap <= self.lanczos_tol
+            if ok or deg >= self.max_lanczos_degree:
+                break
+            deg = min(self.max_lanczos_degree, 2 * deg)
+        self.lanczos_degree_used = deg
+        self._nodes = g
+        self.last_slq_convergence = {'degree': deg, 'bracket': gap, 'converged': ok,
+                                     'eta': e[0]}
+        return self.last_slq_convergence
+
     def _slq(self, eta, what):
         fn = _slq.FUNCS[what] if isinstance(what, str) else what
-        nodes = self.slq_nodes()
+        nodes = self.slq_nodes([eta], (fn,))
         q = self.n * _slq.quadrature(nodes, [eta], fn)[:, 0]
         if self._adaptive:
             import scipy.stats
             zc = float(scipy.stats.norm.ppf(0.5 * (1.0 + self.confidence_level)))
+            deg = self.lanczos_degree_used
+            extra = [x for x in self._extra if x[0] == deg]
+            for _, a, b in extra:
+                q = numpy.concatenate([q, self.n * _slq.quadrature(_slq.nodes(a, b), [eta],
+                                                                   fn)[:, 0]])
             while True:
                 k = q.size
                 err = zc * q.std(ddof=1) / numpy.sqrt(k) if k > 1 else numpy.inf
                 if err <= max(self.error_atol, self.error_rtol * abs(q.mean())) or \
                         k >= self.max_num_samples:
                     break
-                extra = min(self.max_num_samples - k, max(1, self.min_num_samples))
-                a, b = self.sop.lanczos(extra, self.lanczos_degree, self.seed, probe_offset=k,
-                                        orthogonalize=self.orthogonalize)
-                more = _slq.nodes(a, b)
-                nodes.extend(more)
-                self.num_samples = len(nodes)
-                q = numpy.concatenate([q, self.n * _slq.quadrature(more, [eta], fn)[:, 0]])
+                more = min(self.max_num_samples - k, max(1, self.min_num_samples))
+                a, b = self._lanczos(more, deg, offset=k)
+                self._extra.append((deg, a, b))
+                q = numpy.concatenate([q, self.n * _slq.quadrature(_slq.nodes(a, b), [eta],
+                                                                   fn)[:, 0]])
+        self.last_num_samples = int(q.size)
+        return float(q.mean())
+
+    def _probes(self, k, offset=0):
+        """Hutchinson probes [n, k]: the counter-based Rademacher set, with imate's
+        ``orthogonalize`` (default True) orthonormalised and scaled by sqrt(n)
+        (Householder QR: the first columns do not depend on later ones, so a
+        larger set extends a smaller one)."""
+        V = _slq.rademacher(self.n, offset + k, self.seed)
+        if self.orthogonalize and offset + k <= self.n:
+            Q, _ = numpy.linalg.qr(V)
+            V = Q * numpy.sqrt(self.n)
+        return V[:, offset:]
+
+    def _hutchinson_traceinv(self, eta, exponent):
+        """imate 'hutchinson' traceinv (:193-203): tr (K + eta I)^-p ~ mean_v
+        v^T (K + eta I)^-p v, with u = (K + eta I)^-q v, q = floor(p / 2):
+        |u|^2 for even p, u^T (K + eta I)^-1 u for odd p, so ceil(p / 2) solves
+        per probe (device Cholesky solves with the factor cached per eta, or CG on
+        a sparse K); a negative p takes products instead."""
+        if float(exponent) != int(exponent):
+            raise ValueError('"exponent" should be an integer.')
+        p = int(exponent)
+        if p == 0:
+            return float(self.n)
+
+        def solve(W):
+            return self.sop.cg(eta, W, rtol=self.cg_rtol) if self.sparse else \
+                self.op.solve(eta, W)
+
+        def apply(W):
+            KW = self.sop.spmm(0.0, W) if self.sparse else self.op.matvec(W)
+            return KW + eta * W
+
+        def estimates(V):
+            step = solve if p > 0 else apply
+            U = V
+            for _ in range(abs(p) // 2):
+                U = step(U)
+            W = step(U) if abs(p) % 2 else U
+            return numpy.sum(U * W, axis=0)
+
+        if not self._adaptive:
+            self.last_num_samples = self.num_samples
+            return float(numpy.mean(estimates(self._probes(self.num_samples))))
+        import scipy.stats
+        zc = float(scipy.stats.norm.ppf(0.5 * (1.0 + self.confidence_level)))
+        q = estimates(self._probes(self.min_num_samples))
+        while q.size < self.max_num_samples:
+            err = zc * q.std(ddof=1) / numpy.sqrt(q.size) if q.size > 1 else numpy.inf
+            if err <= max(self.error_atol, self.error_rtol * abs(q.mean())):
+                break
+            more = min(self.max_num_samples - q.size, max(1, self.min_num_samples))
+            q = numpy.concatenate([q, estimates(self._probes(more, q.size))])
+        self.last_num_samples = int(q.size)
         return float(q.mean())
 
     def _sparse_traces(self):
@@ -349,28 +523,10 @@ class MixedCorrelation(object):
                 return self._slq(eta, 'traceinv' if exponent == 1 else 'traceinv2')
             p = float(exponent)
             return self._slq(eta, lambda x: x ** -p)
-        if self.sparse and self.imate_method == 'hutchinson':
-            if exponent in (1, 2):
-                V = _slq.rademacher(self.n, self.num_samples, self.seed)
-                W = self.sop.cg(eta, V, rtol=self.cg_rtol)
-                if exponent == 1:
-                    return float(numpy.sum(V * W) / self.num_samples)
-                return float(numpy.sum(W * W) / self.num_samples)
-            raise NotImplementedError('sparse traceinv with exponent %r' % exponent)
-        if self.imate_method == 'hutchinson' and exponent in (1, 2):
-            # Hutchinson estimator (imate 'hutchinson', assume_matrix='sym_pos'):
-            # tr(A^-1) ~ mean v^T A^-1 v, tr(A^-2) ~ mean |A^-1 v|^2, Rademacher v
-            opts = dict(self.imate_options or {})
-            s = int(opts.get('num_samples', opts.get('max_num_samples', 20)))
-            V = _slq.rademacher(self.n, s, int(opts.get('seed', 0)))
-            W = self.op.solve(eta, V)
-            if exponent == 1:
-                return float(numpy.sum(V * W) / s)
-            return float(numpy.sum(W * W) / s)
+        if self.imate_method == 'hutchinson':
+            # Hutchinson estimator (imate 'hutchinson', assume_matrix='sym_pos')
+            return self._hutchinson_traceinv(eta, exponent)
         if self.imate_method not in ('eigenvalue', 'cholesky'):
-            if self.imate_method in _METHODS:
-                raise NotImplementedError('stochastic traceinv (%s) is not implemented yet'
-                                          % self.imate_method)
             raise ValueError('Existing methods are "eigenvalue", "cholesky,"'
                              '"hutchinson", and "slq".')
         if exponent == 0:

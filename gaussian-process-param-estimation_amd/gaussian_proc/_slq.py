@@ -15,22 +15,73 @@ identical to the single-GPU one.
 """
 
 import numpy
+import scipy.linalg
+
+
+def _length(b):
+    """Order of a probe's tridiagonal: up to its first zero beta (breakdown:
+    the Krylov space is invariant and the Gauss rule exact) or all steps."""
+    z = numpy.flatnonzero(b == 0.0)
+    return int(z[0]) + 1 if z.size else len(b)
+
+
+def _rule(d, e):
+    """Nodes and squared first eigenvector components of the symmetric
+    tridiagonal (diagonal d, off-diagonal e): LAPACK stemr through scipy."""
+    if d.size == 1:
+        return d.copy(), numpy.ones(1)
+    theta, U = scipy.linalg.eigh_tridiagonal(d, e)
+    return theta, U[0] ** 2
 
 
 def nodes(alpha, beta):
-    """Ritz values and squared first components for each probe.
+    """Ritz values and squared first components for each probe (the Gauss
+    quadrature rule of the probe's spectral measure).
     alpha, beta: [nprobe, steps]; beta[p, k] = 0 ends probe p's tridiagonal
-    after step k."""
+    after step k; beta[p, steps - 1] is the coupling beta_m of the last Lanczos
+    vector to the next one (used by radau_nodes only)."""
     out = []
     for a, b in zip(alpha, beta):
-        k = len(a)
-        z = numpy.flatnonzero(b == 0.0)
-        if z.size:
-            k = int(z[0]) + 1
-        T = numpy.diag(a[:k]) + numpy.diag(b[:k - 1], 1) + numpy.diag(b[:k - 1], -1)
-        theta, U = numpy.linalg.eigh(T)
-        out.append((theta, U[0] ** 2))
+        k = _length(b)
+        out.append(_rule(numpy.asarray(a[:k], dtype=float), numpy.asarray(b[:k - 1], dtype=float)))
     return out
+
+
+def radau_nodes(alpha, beta, lower):
+    """Gauss-Radau rules with one node fixed at ``lower`` <= lambda_min(K)
+    (Golub and Meurant, "Matrices, Moments and Quadrature with Applications",
+    2010, ch. 6): the tridiagonal T_m extended by beta_m and the diagonal entry
+    a~ = lower + beta_m^2 / d_m, d_m the last pivot of (T_m - lower I) = L D L^T.
+    For f with f^(2m) of constant sign on the spectrum (log(x + eta),
+    (x + eta)^-p) the Gauss and Gauss-Radau values bracket the exact quadratic
+    form, so their gap bounds the Lanczos quadrature error of each probe. A
+    probe whose tridiagonal broke down (exact rule) gets its Gauss rule."""
+    out = []
+    for a, b in zip(alpha, beta):
+        a = numpy.asarray(a, dtype=float)
+        b = numpy.asarray(b, dtype=float)
+        k = _length(b)
+        if k < len(b) or b[k - 1] == 0.0:
+            out.append(_rule(a[:k], b[:k - 1]))
+            continue
+        d = a[0] - lower
+        for i in range(1, k):
+            d = (a[i] - lower) - b[i - 1] ** 2 / d
+        if not d > 0.0:
+            raise ValueError('Gauss-Radau node %r is not below the Ritz values' % lower)
+        dd = numpy.append(a[:k], lower + b[k - 1] ** 2 / d)
+        out.append(_rule(dd, b[:k]))
+    return out
+
+
+def bracket(gauss, radau, etas, fn):
+    """Relative gap |mean_p G_p - mean_p R_p| / |mean_p G_p| of the probe-mean
+    Gauss and Gauss-Radau quadratures at each eta: a bound on the Lanczos
+    (quadrature) part of the SLQ error, as opposed to its Monte-Carlo part."""
+    g = quadrature(gauss, etas, fn, check=False).mean(axis=0)
+    r = quadrature(radau, etas, fn, check=False).mean(axis=0)
+    with numpy.errstate(divide='ignore', invalid='ignore'):
+        return numpy.where(g != 0.0, numpy.abs(g - r) / numpy.abs(g), numpy.abs(g - r))
 
 
 def min_ritz(node_list):

@@ -116,7 +116,7 @@ def eta_sweep(K_mixed, X, z, etas, sigma=1.0, group=None):
     return allv[:, 0].copy(), allv[:, 1].copy()
 
 
-def slq_sweep(K_mixed, etas, group=None):
+def slq_sweep(K_mixed, etas, group=None, converge=('logdet',)):
     """Stochastic-Lanczos-quadrature curves over an eta grid for a sparse
     ``MixedCorrelation`` (imate_method 'slq'), probes sharded over the ranks.
 
@@ -124,34 +124,69 @@ def slq_sweep(K_mixed, etas, group=None):
     probe set (counter-based probes: the union over ranks is exactly the
     single-GPU probe set), evaluates its per-probe quadrature for every eta, and
     ONE all-gather collects the [probe, eta] blocks. Returns
-    dict(logdet, traceinv, traceinv2), each [neta], identical on every rank."""
+    dict(logdet, traceinv, traceinv2), each [neta], identical on every rank.
+
+    With the operator's ``lanczos_tol`` set, each probe row also carries its Gauss
+    and Gauss-Radau quadratures of ``converge`` at min(etas); while their
+    probe-mean gap (_slq.bracket) exceeds lanczos_tol, every rank redoes its
+    shard at twice the degree (up to max_lanczos_degree) and gathers again. The
+    decision is taken from the gathered rows, so all ranks agree."""
     from . import _slq
     etas = numpy.atleast_1d(numpy.asarray(etas, dtype=float))
     s = K_mixed.num_samples
     dist, world, rank = _group(group)
     lo, hi, per = shard(s, world, rank)
     names = ('logdet', 'traceinv', 'traceinv2')
-    # per probe row: the quadratures, then the smallest Ritz value (the SPD check
-    # runs after the all-gather, on every rank alike: no rank raises alone)
+    tol = getattr(K_mixed, 'lanczos_tol', None)
+    conv = [_slq.FUNCS[f] if isinstance(f, str) else f for f in converge] if tol else []
+    lower = K_mixed._lower_bound() if tol else None
+    deg = getattr(K_mixed, 'lanczos_degree_used', K_mixed.lanczos_degree)
+    # per probe row: the quadratures, the smallest Ritz value (the SPD check runs
+    # after the all-gather, on every rank alike: no rank raises alone), then the
+    # Gauss / Gauss-Radau pair of each converge function at min(etas)
     nq = len(names) * etas.size
-    local = numpy.zeros((per, nq + 1))
-    local[:, nq] = numpy.inf
-    if hi > lo:
-        a, b = K_mixed.sop.lanczos(hi - lo, K_mixed.lanczos_degree, K_mixed.seed,
-                                   probe_offset=lo,
-                                   orthogonalize=getattr(K_mixed, 'orthogonalize', -1))
-        nodes = _slq.nodes(a, b)
-        q = numpy.empty((hi - lo, len(names), etas.size))
-        for f, name in enumerate(names):
-            with numpy.errstate(invalid='ignore', divide='ignore'):
-                q[:, f] = _slq.quadrature(nodes, etas, _slq.FUNCS[name], check=False)
-        local[:hi - lo, :nq] = q.reshape(hi - lo, nq)
-        local[:hi - lo, nq] = [float(t.min()) for t, _ in nodes]
-    if dist is not None and world > 1:
-        allv = _all_gather_rows(dist, group, local, world)[:s]
-    else:
-        allv = local[:s]
-    _slq.check_shifts(float(allv[:, nq].min()), etas)
+    while True:
+        local = numpy.zeros((per, nq + 1 + 2 * len(conv)))
+        local[:, nq] = numpy.inf
+        if hi > lo:
+            a, b = K_mixed.sop.lanczos(hi - lo, deg, K_mixed.seed, probe_offset=lo,
+                                       orthogonalize=getattr(K_mixed, 'orthogonalize', -1))
+            nodes = _slq.nodes(a, b)
+            q = numpy.empty((hi - lo, len(names), etas.size))
+            for f, name in enumerate(names):
+                with numpy.errstate(invalid='ignore', divide='ignore'):
+                    q[:, f] = _slq.quadrature(nodes, etas, _slq.FUNCS[name], check=False)
+            local[:hi - lo, :nq] = q.reshape(hi - lo, nq)
+            local[:hi - lo, nq] = [float(t.min()) for t, _ in nodes]
+            if conv:
+                tmin = _slq.min_ritz(nodes)
+                radau = _slq.radau_nodes(a, b, min(lower, tmin - 1e-12 * abs(tmin)))
+                e = [float(etas.min())]
+                for i, fn in enumerate(conv):
+                    with numpy.errstate(invalid='ignore', divide='ignore'):
+                        local[:hi - lo, nq + 1 + 2 * i] = _slq.quadrature(nodes, e, fn,
+                                                                          check=False)[:, 0]
+                        local[:hi - lo, nq + 2 + 2 * i] = _slq.quadrature(radau, e, fn,
+                                                                          check=False)[:, 0]
+        if dist is not None and world > 1:
+            allv = _all_gather_rows(dist, group, local, world)[:s]
+        else:
+            allv = local[:s]
+        _slq.check_shifts(float(allv[:, nq].min()), etas)
+        if not conv:
+            break
+        gap = 0.0
+        for i in range(len(conv)):
+            g = allv[:, nq + 1 + 2 * i].mean()
+            r = allv[:, nq + 2 + 2 * i].mean()
+            gap = max(gap, abs(g - r) / abs(g) if g != 0.0 else abs(g - r))
+        if gap <= tol or deg >= K_mixed.max_lanczos_degree:
+            break
+        deg = min(K_mixed.max_lanczos_degree, 2 * deg)
+    if conv:
+        K_mixed.lanczos_degree_used = deg
+        K_mixed.last_slq_convergence = {'degree': deg, 'bracket': gap, 'converged': gap <= tol,
+                                        'eta': float(etas.min())}
     allq = allv[:, :nq].reshape(s, len(names), etas.size)
     n = K_mixed.n
     return {name: n * allq[:, f].mean(axis=0) for f, name in enumerate(names)}

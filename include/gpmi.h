@@ -218,12 +218,12 @@ int gpmi_sp_msgram_cols(gpmi_sp* sp, const double* etas, int neta, const double*
 int gpmi_sp_spmm_info(gpmi_sp* sp, int* windowed, double* mean_window, int* max_window);
 /* The SpMM kernel gpmi_sp_spmm runs for an s-column block on this operator:
  * 0 gather from X (csr_spmm_kernel), 1 X-window in 8-column chunks
- * (csr_spmm_win_kernel), 2 X-window in one full-width pass (csr_spmm_winf_kernel,
- * s = 20), 3 gather from X by column pairs (csr_spmm_pair_kernel, even s; a block
- * that is not 16-byte aligned runs csr_spmm_kernel), 4 dense (dense_mm_kernel,
- * gpmi_sp_create_dense), 5 window with latency-hidden staging (csr_spmm_wing_kernel,
- * s = 7, 11, 20 while the widest window fits 80 KB of LDS). Diagnostic; no reference
- * counterpart. */
+ * (csr_spmm_win_kernel), 3 gather from X by column pairs (csr_spmm_pair_kernel,
+ * even s), 4 dense (dense_mm_kernel, gpmi_sp_create_dense), 5 window with
+ * latency-hidden staging (csr_spmm_wing_kernel, s = 7, 8, 11, 12, 20 while the
+ * widest window fits 80 KB of LDS); a 16-byte-wide kernel handed a block that is
+ * not 16-byte aligned runs csr_spmm_kernel. (2, the round-2 one-pass window, is no
+ * longer returned.) Diagnostic; no reference counterpart. */
 int gpmi_sp_spmm_kernel(gpmi_sp* sp, int s, int* kind);
 /* Whether the last gpmi_sp_cg / gpmi_sp_msgram met rtol in every column before
  * maxiter (1) or stopped at maxiter (0). scipy's cg, which the reference calls

@@ -140,6 +140,28 @@ def test_dense_hutchinson_traceinv_within_mc_error(gp):
                                                rel=1e-10)
 
 
+@pytest.mark.parametrize('orth', [True, False])
+def test_dense_hutchinson_traceinv_exponent_3_and_4(gp, orth):
+    """'hutchinson' traceinv of exponent 3 (two chained device solves per probe:
+    u = A^-1 v, u^T A^-1 u) and 4 (|A^-2 v|^2) within 4 standard errors of the
+    eigenvalue sum; imate's orthogonalize option on and off."""
+    from gaussian_proc._mixed_correlation import MixedCorrelation
+    K, _, _ = _inputs(400, 9)
+    s = 200
+    op = MixedCorrelation(K, imate_method='hutchinson',
+                          imate_options={'num_samples': s, 'orthogonalize': orth})
+    lam = numpy.linalg.eigvalsh(K)
+    for p in (3, 4):
+        for eta in (0.5, 2.0):
+            B = numpy.linalg.matrix_power(numpy.linalg.inv(K + eta * numpy.eye(400)), p)
+            se = numpy.sqrt(2.0 * (numpy.sum(B ** 2) - numpy.sum(numpy.diag(B) ** 2)) / s)
+            exact = numpy.sum((lam + eta) ** -float(p))
+            assert abs(op.traceinv(eta, p) - exact) < 4 * se + 1e-12 * exact, (p, eta)
+    assert op.traceinv(1.0, 0) == 400
+    with pytest.raises(ValueError):
+        op.traceinv(1.0, 1.5)
+
+
 @pytest.mark.parametrize('n', [2, 5, 129, 300, 1000])
 def test_eigenvalues_vs_numpy(gp, n):
     """Device bulge chase + bisection: the spectrum of K to 1e-12 ||K||."""
@@ -532,33 +554,6 @@ def test_band_reduction_variants_agree(gp, monkeypatch):
     ld2, G2 = _mc(K).loglik_terms(etas, X, z)
     assert rel(ld0, ld2) < 1e-12
     numpy.testing.assert_allclose(G0, G2, rtol=1e-9, atol=1e-11 * numpy.abs(G2).max())
-
-
-@pytest.mark.parametrize('delay', ['2', '3', '4', '8'])
-@pytest.mark.parametrize('n', [1000, 2304])
-def test_band_delayed_update_matches_per_panel_update(gp, monkeypatch, n, delay):
-    """The delayed trailing update (one rank-256p SYR2K per group of p panels,
-    the group's panels on the stored matrix with the pending pairs' corrections;
-    GPMI_BAND_DELAY=p) against the per-panel update (the default, p = 1) and
-    several group sizes, incl. groups cut by the last panel: logdet and Gram to
-    rounding, B orthogonally similar to K (its spectrum), and the look-ahead
-    off bit for bit equal."""
-    K, X, z = _inputs(n, 5 * n + int(delay), nu=1.5, scale=0.1)
-    etas = [1e-3, 0.1, 10.0]
-    op0 = _mc(K)
-    ld0, G0 = op0.loglik_terms(etas, X, z)
-    monkeypatch.setenv('GPMI_BAND_DELAY', delay)
-    op1 = _mc(K)
-    ld1, G1 = op1.loglik_terms(etas, X, z)
-    assert rel(ld0, ld1) < 1e-12
-    numpy.testing.assert_allclose(G0, G1, rtol=1e-9, atol=1e-11 * numpy.abs(G0).max())
-    lam = numpy.linalg.eigvalsh(K)
-    lam1 = numpy.linalg.eigvalsh(op1.band().band())
-    assert numpy.max(numpy.abs(lam1 - lam)) <= 1e-12 * numpy.abs(lam).max()
-    monkeypatch.setenv('GPMI_BAND_LA', '0')
-    ld2, G2 = _mc(K).loglik_terms(etas, X, z)
-    numpy.testing.assert_array_equal(ld1, ld2)
-    numpy.testing.assert_array_equal(G1, G2)
 
 
 @pytest.mark.parametrize('n', [1, 5, 127, 128, 129, 300, 1000, 2304, 4224])

@@ -183,12 +183,10 @@ def test_msgram_column_shards_equal_full(gp):
         assert _nrel(g, ex) < 1e-9
 
 
-def test_msgram_iteration_forms_agree(gp, monkeypatch):
-    """The multi-shift CG's r update + dots: the MFMA form (default, ms_rmfma_kernel;
-    its partials summed across the chip or, GPMI_MS_RED=0, in the scalar kernel) and
-    GPMI_MS_MFMA=0's scalar forms (fused ms_rdots_partial_kernel for <= 8 columns,
-    the separate update and dots above) give the same Gram to rounding, and the
-    exact solve's."""
+def test_msgram_widths_vs_exact_solve(gp):
+    """The multi-shift CG (r update and B^T r, r . r on MFMA, ms_rmfma_kernel; partial
+    sums across the chip) at 3, 7 and 11 columns (11 padded to 12 on the window SpMM)
+    against the exact solve's Gram."""
     from gaussian_proc import _hip
     _, K = _small_sparse()
     n = K.shape[0]
@@ -198,13 +196,6 @@ def test_msgram_iteration_forms_agree(gp, monkeypatch):
     for s in (3, 7, 11):
         B = rng.randn(n, s)
         G = sop.msgram(etas, B, rtol=1e-10)
-        for env in ({'GPMI_MS_RED': '0'}, {'GPMI_MS_MFMA': '0'}):
-            for k, v in env.items():
-                monkeypatch.setenv(k, v)
-            Gf = sop.msgram(etas, B, rtol=1e-10)
-            for k in env:
-                monkeypatch.delenv(k)
-            assert _nrel(Gf, G) < 1e-11, (s, env)
         for e, g in zip(etas, G):
             ex = B.T @ scipy.sparse.linalg.spsolve((K + e * scipy.sparse.eye(n)).tocsc(), B)
             assert _nrel(g, ex) < 1e-9, (s, e)
@@ -317,12 +308,17 @@ def test_slq_adaptive_sample_count(gp):
             'lanczos_degree': 25, 'seed': 5}
     op = MixedCorrelation(K, imate_method='slq', imate_options=opts)
     v = op.logdet(2.5)
-    k = op.num_samples
+    k = op.last_num_samples
     assert 4 <= k <= 40
+    # the adaptive probes are kept apart: the fixed set (num_samples, slq_nodes)
+    # does not grow with earlier calls, and a repeat call gives the same value
+    assert op.num_samples == 4 and len(op.slq_nodes()) == 4
+    assert op.logdet(2.5) == v and op.last_num_samples == k
     fixed = MixedCorrelation(K, imate_method='slq',
                              imate_options={'num_samples': k, 'lanczos_degree': 25, 'seed': 5})
     assert v == pytest.approx(fixed.logdet(2.5), rel=1e-12)
-    q = numpy.array([K.shape[0] * numpy.sum(w * numpy.log(t + 2.5)) for t, w in op.slq_nodes()])
+    q = numpy.array([K.shape[0] * numpy.sum(w * numpy.log(t + 2.5))
+                     for t, w in fixed.slq_nodes()])
     half = scipy.stats.norm.ppf(0.975) * q.std(ddof=1) / numpy.sqrt(q.size)
     assert k == 40 or half <= 2e-3 * abs(q.mean())
     # a looser tolerance stops at the minimum
@@ -330,7 +326,7 @@ def test_slq_adaptive_sample_count(gp):
                            imate_options={'min_num_samples': 4, 'error_rtol': 0.5,
                                           'lanczos_degree': 25})
     op2.logdet(2.5)
-    assert op2.num_samples == 4
+    assert op2.last_num_samples == 4
 
 
 def test_sparse_operator_slq_vs_exact(gp):
@@ -353,6 +349,24 @@ def test_sparse_operator_slq_vs_exact(gp):
                                             (Kd + 0.5 * numpy.eye(n)))) < 1e-12
     x = numpy.arange(n, dtype=float)
     numpy.testing.assert_allclose(op.dot(0.5, x, 2), 2 * (Kd @ x + 0.5 * x), rtol=1e-13)
+
+
+def test_sparse_hutchinson_traceinv_exponent_3(gp):
+    """Sparse 'hutchinson' traceinv of exponent 3: two chained device CG solves
+    per probe (rtol 1e-10 here), within 4 standard errors of the eigenvalue sum."""
+    from gaussian_proc._mixed_correlation import MixedCorrelation
+    _, K = _small_sparse()
+    n = K.shape[0]
+    Kd = K.toarray()
+    lam = numpy.linalg.eigvalsh(Kd)
+    s = 64
+    hop = MixedCorrelation(K, imate_method='hutchinson',
+                           imate_options={'num_samples': s, 'cg_rtol': 1e-10})
+    for eta in (5.0, 10.0):
+        B = numpy.linalg.matrix_power(numpy.linalg.inv(Kd + eta * numpy.eye(n)), 3)
+        se = numpy.sqrt(2.0 * (numpy.sum(B ** 2) - numpy.sum(numpy.diag(B) ** 2)) / s)
+        exact = numpy.sum((lam + eta) ** -3.0)
+        assert abs(hop.traceinv(eta, 3) - exact) < 4 * se + 1e-9 * exact
 
 
 def test_sparse_likelihood_vs_oracle(gp):

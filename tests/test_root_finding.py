@@ -173,3 +173,28 @@ def test_profiled_driver_speculative_n1024():
     seq = cfg['maximize_profiled_der1_calls']
     check_der1_sequence(memo, seq)
     assert 3 * calls <= 2 * len(seq), (calls, len(seq))
+    # speculation never makes a call larger than its budget (24 here)
+    assert ProfileLikelihood.last_der1_max_batch <= 24
+
+
+def test_speculative_batches_stay_within_the_budget():
+    """Required plus speculative points of every call stay within spec_budget
+    (the band operator's 64 is gpmi_band_der_terms' cyclic-reduction limit):
+    the bracket search's first call (x0, x1 + 4 probes + Chandrupatla tree)
+    and every Chandrupatla step (xt + its candidate tree)."""
+    from gaussian_proc._likelihood._root_finding import (BatchedFunction, chandrupatla_method,
+                                                         find_interval_with_sign_change_batched)
+    sizes = []
+
+    def fbatch(xs):
+        sizes.append(len(xs))
+        return numpy.tanh(numpy.asarray(xs) - 0.3123)
+    for budget in (8, 64):
+        sizes.clear()
+        fb = BatchedFunction(fbatch, spec_budget=budget)
+        found, bracket, values = find_interval_with_sign_change_batched(fb, [-2.0, 3.0], 8,
+                                                                        tol=1e-9)
+        assert found
+        res = chandrupatla_method(fb, bracket, values, eps_m=1e-9, eps_a=1e-9)
+        assert abs(res['root'] - 0.3123) < 1e-8
+        assert max(sizes) <= budget and fb.max_points == max(sizes), (budget, sizes)

@@ -15,6 +15,12 @@
 #   trace-dense  the same for the dense line only (--no-band --no-sparse): the
 #                headline syrk_kernel launches, summarised by tools/trace_summary.py
 #   pmc-dense    FETCH_SIZE / WRITE_SIZE passes over the dense line (batch 64)
+#   pmc-mfma     MFMA busy / fp64 MOPS / CU busy / GPU clock pass over the dense line
+#   pmc-band     the same MFMA pass and FETCH / WRITE passes over two band reductions
+#                (tools/band_refresh_probe.py 128 1)
+#   pmc-sparse4 / pmc-sparse5   FETCH / WRITE passes over one sparse step
+#   trace-sparse4 / trace-sparse5   kernel-trace stats of bench --config sparseN
+#   host         the box's CPU / cgroup facts (host.txt)
 #   py:<file>    python -u <file> (a probe under tools/)
 set -o pipefail
 export TMPDIR=/tmp
@@ -72,6 +78,24 @@ for task in "$@"; do
       for c in FETCH_SIZE WRITE_SIZE; do
         run 300 $D/pmc_$c.log rocprofv3 --pmc $c --kernel-trace -d $D/pmc_dense_$c -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-band --no-sparse --no-timing
       done ;;
+    pmc-mfma)
+      run 300 $D/pmc_mfma.log rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F64 GRBM_GUI_ACTIVE --kernel-trace -d $D/pmc_mfma -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-timing --no-band --no-sparse ;;
+    pmc-band)
+      run 200 $D/pmc_band_mfma.log rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F64 GRBM_GUI_ACTIVE --kernel-trace -d $D/pmc_band_mfma -o run --output-format csv -- python3 tools/band_refresh_probe.py 128 1
+      for c in FETCH_SIZE WRITE_SIZE; do
+        run 200 $D/pmc_band_$c.log rocprofv3 --pmc $c --kernel-trace -d $D/pmc_band_$c -o run --output-format csv -- python3 tools/band_refresh_probe.py 128 1
+      done ;;
+    pmc-sparse4|pmc-sparse5)
+      cfg=${task#pmc-}
+      for c in FETCH_SIZE WRITE_SIZE; do
+        run 200 $D/pmc_${cfg}_$c.log rocprofv3 --pmc $c --kernel-trace -d $D/pmc_${cfg}_$c -o run --output-format csv -- python3 bench.py --config $cfg --steps 1 --warmup 0 --no-cpu-baseline
+      done ;;
+    trace-sparse4|trace-sparse5)
+      cfg=${task#trace-}
+      run 400 $D/trace_$cfg.err rocprofv3 --kernel-trace --stats -d $D/prof_$cfg -o run --output-format csv -- python3 bench.py --config $cfg --steps 3 --warmup 1 --no-cpu-baseline --out-json $D/bench_under_rocprof_$cfg.json
+      python tools/bench_summary.py $D/bench_under_rocprof_$cfg.json ;;
+    host)
+      (nproc; cat /sys/fs/cgroup/cpu.max 2>/dev/null; python -c "import os; print('aff', len(os.sched_getaffinity(0)), 'omp', os.environ.get('OMP_NUM_THREADS'))"; lscpu | head -20) > $D/host.txt 2>&1 ;;
     py:*)
       f=${task#py:}
       run 900 $D/$(basename $f .py).log python -u $f

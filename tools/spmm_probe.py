@@ -11,11 +11,7 @@ from gaussian_proc import generate_correlation, _data  # noqa: E402
 CFG = {'sparse4': (256, 2, 0.005, 1e-3), 'sparse5': (64, 3, 0.02, 6e-4)}
 SETTINGS = [('pair/gather', {'GPMI_SPMM_WING': '0', 'GPMI_SPMM_WINDOW': '0'}),
             ('window (old)', {'GPMI_SPMM_WING': '0'}),
-            ('wing U4', {'GPMI_SPMM_WUNR': '4'}),
-            ('wing U8', {'GPMI_SPMM_WUNR': '8'}),
-            ('wing U16', {'GPMI_SPMM_WUNR': '16'}),
-            ('wing U4 T8', {'GPMI_SPMM_WUNR': '4', 'GPMI_SPMM_WTPR': '8'}),
-            ('wing U8 T8', {'GPMI_SPMM_WUNR': '8', 'GPMI_SPMM_WTPR': '8'})]
+            ('wing', {})]
 for name in sys.argv[1:] or ['sparse5', 'sparse4']:
     g, d, rho, dens = CFG[name]
     pts = _data.generate_points(g, d, True)
@@ -25,8 +21,7 @@ for name in sys.argv[1:] or ['sparse5', 'sparse4']:
     for s in (20, 12, 11):
         alg = 12.0 * nnz + 4.0 * (n + 1) + 16.0 * n * s
         for label, env in SETTINGS:
-            keep = {k: os.environ.get(k) for k in ('GPMI_SPMM_WING', 'GPMI_SPMM_WINDOW',
-                                                   'GPMI_SPMM_WUNR', 'GPMI_SPMM_WTPR')}
+            keep = {k: os.environ.get(k) for k in ('GPMI_SPMM_WING', 'GPMI_SPMM_WINDOW')}
             os.environ.update(env)
             ms = sop.bench_spmm(s, 20)
             kern = sop.spmm_kernel(s)
