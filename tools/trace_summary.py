@@ -24,7 +24,7 @@ def timed_syrk(trace_dir, bench_json):
     roof = line['roofline']
     B = line['config']['eta_per_rank_per_step']
     steps, warm = line['steps'], line['warmup']
-    files = glob.glob(os.path.join(trace_dir, '**', '*kernel_trace.csv'), recursive=True)
+    files = glob.glob(os.path.join(trace_dir, '**', '*kernel_trace*.csv'), recursive=True)
     rows = []
     for f in files:
         with open(f) as fh:
