@@ -81,6 +81,23 @@ _EXTENSIONS = {
 }
 
 
+def _next_degree(seen, tol):
+    """The next Lanczos degree of the lanczos_tol search from the (degree, gap)
+    pairs so far: twice the last degree, or, with two decreasing gaps, the degree
+    where the line through their logarithms reaches tol (+10 %; the quadrature
+    error decays at least geometrically in the degree, faster once the extreme
+    Ritz values settle, so the line overshoots), at least 8 more steps."""
+    m2, g2 = seen[-1]
+    nxt = 2 * m2
+    if len(seen) >= 2:
+        m1, g1 = seen[-2]
+        if 0.0 < g2 < g1 and m2 > m1:
+            rate = (numpy.log(g1) - numpy.log(g2)) / float(m2 - m1)
+            want = m2 + (numpy.log(g2) - numpy.log(tol)) / rate
+            nxt = int(min(1e6, numpy.ceil(1.1 * want / 8.0) * 8))
+    return max(m2 + 8, nxt)
+
+
 def _check_options(method, options):
     """TypeError for a key imate's functions of ``method`` would not accept."""
     if method not in _IMATE_OPTIONS:
@@ -156,9 +173,9 @@ class MixedCorrelation(object):
             self.orthogonalize = bool(opts.get('orthogonalize', True))
         # imate's lanczos_tol: the Lanczos runs until the quadrature has converged
         # to this relative tolerance at the eta asked (the gap of the Gauss and
-        # Gauss-Radau rules, _slq.bracket), its degree doubling from lanczos_degree
-        # up to max_lanczos_degree (extension; 256, the device's limit). None: the
-        # fixed lanczos_degree, as imate.
+        # Gauss-Radau rules, _slq.bracket), its degree growing from lanczos_degree
+        # (_next_degree) up to max_lanczos_degree (extension; 256, the device's
+        # limit). None: the fixed lanczos_degree, as imate.
         tol = opts.get('lanczos_tol')
         self.lanczos_tol = None if tol is None else float(tol)
         self.max_lanczos_degree = max(self.lanczos_degree,
@@ -344,7 +361,7 @@ class MixedCorrelation(object):
     def slq_nodes(self, etas=None, funcs=('logdet',)):
         """Ritz nodes of every probe of the fixed set (eta-independent; cached
         until K changes). With ``lanczos_tol`` set and ``etas`` given, the
-        Lanczos degree is first raised (doubling, up to max_lanczos_degree) until
+        Lanczos degree is first raised (_next_degree, up to max_lanczos_degree) until
         the Gauss / Gauss-Radau gap of the probe-mean quadrature of each of
         ``funcs`` at min(etas) is within lanczos_tol (slq_converge)."""
         if etas is not None and self.lanczos_tol is not None:
@@ -364,6 +381,7 @@ class MixedCorrelation(object):
         fns = [_slq.FUNCS[f] if isinstance(f, str) else f for f in funcs]
         lo = self._lower_bound()
         deg = self.lanczos_degree_used
+        seen = []
         while True:
             a, b = self._fixed_lanczos(deg)
             g = _slq.nodes(a, b)
@@ -373,7 +391,8 @@ class MixedCorrelation(object):
             ok = gap <= self.lanczos_tol
             if ok or deg >= self.max_lanczos_degree:
                 break
-            deg = min(self.max_lanczos_degree, 2 * deg)
+            seen.append((deg, gap))
+            deg = min(self.max_lanczos_degree, _next_degree(seen, self.lanczos_tol))
         self.lanczos_degree_used = deg
         self._nodes = g
         self.last_slq_convergence = {'degree': deg, 'bracket': gap, 'converged': ok,

@@ -129,9 +129,11 @@ def slq_sweep(K_mixed, etas, group=None, converge=('logdet',)):
     With the operator's ``lanczos_tol`` set, each probe row also carries its Gauss
     and Gauss-Radau quadratures of ``converge`` at min(etas); while their
     probe-mean gap (_slq.bracket) exceeds lanczos_tol, every rank redoes its
-    shard at twice the degree (up to max_lanczos_degree) and gathers again. The
+    shard at a higher degree (_next_degree, up to max_lanczos_degree) and gathers
+    again. The
     decision is taken from the gathered rows, so all ranks agree."""
     from . import _slq
+    from ._mixed_correlation.mixed_correlation import _next_degree
     etas = numpy.atleast_1d(numpy.asarray(etas, dtype=float))
     s = K_mixed.num_samples
     dist, world, rank = _group(group)
@@ -145,6 +147,7 @@ def slq_sweep(K_mixed, etas, group=None, converge=('logdet',)):
     # after the all-gather, on every rank alike: no rank raises alone), then the
     # Gauss / Gauss-Radau pair of each converge function at min(etas)
     nq = len(names) * etas.size
+    seen = []
     while True:
         local = numpy.zeros((per, nq + 1 + 2 * len(conv)))
         local[:, nq] = numpy.inf
@@ -182,7 +185,8 @@ def slq_sweep(K_mixed, etas, group=None, converge=('logdet',)):
             gap = max(gap, abs(g - r) / abs(g) if g != 0.0 else abs(g - r))
         if gap <= tol or deg >= K_mixed.max_lanczos_degree:
             break
-        deg = min(K_mixed.max_lanczos_degree, 2 * deg)
+        seen.append((deg, gap))
+        deg = min(K_mixed.max_lanczos_degree, _next_degree(seen, tol))
     if conv:
         K_mixed.lanczos_degree_used = deg
         K_mixed.last_slq_convergence = {'degree': deg, 'bracket': gap, 'converged': gap <= tol,

@@ -1,0 +1,110 @@
+"""Host side of the stochastic estimators (CPU): the Gauss-Radau rules of
+_slq bracket the exact quadratic form, so their gap bounds the Lanczos part of
+the SLQ error (imate's lanczos_tol control), and imate_options are checked
+against the keywords imate's functions accept (TypeError otherwise)."""
+
+import numpy
+import pytest
+
+from gaussian_proc import _slq
+
+
+def _lanczos_with_last_beta(K, v, m):
+    """Lanczos (CGS2) returning alpha[m] and beta[m], beta[m - 1] the coupling
+    to the next vector (the device's convention)."""
+    n = K.shape[0]
+    V = numpy.zeros((m + 1, n))
+    V[0] = v / numpy.linalg.norm(v)
+    a, b = [], []
+    bp, vp = 0.0, numpy.zeros(n)
+    for k in range(m):
+        w = K @ V[k] - bp * vp
+        for _ in range(2):
+            h = V[:k + 1] @ w
+            w -= V[:k + 1].T @ h
+        a.append(V[k] @ K @ V[k])
+        bb = numpy.linalg.norm(w)
+        b.append(bb)
+        vp, bp = V[k], bb
+        V[k + 1] = w / bb
+    return numpy.array(a), numpy.array(b)
+
+
+@pytest.mark.parametrize('m', [5, 12, 25])
+def test_gauss_and_radau_bracket_the_quadratic_form(m):
+    rng = numpy.random.RandomState(m)
+    lam = numpy.sort(rng.gamma(0.3, 2.0, 400)) + 1e-4      # clustered near 0, like a smooth K
+    K = numpy.diag(lam)
+    P = _slq.rademacher(lam.size, 6, 2)
+    ab = [_lanczos_with_last_beta(K, P[:, p], m) for p in range(6)]
+    A = numpy.array([a for a, _ in ab])
+    B = numpy.array([b for _, b in ab])
+    g = _slq.nodes(A, B)
+    r = _slq.radau_nodes(A, B, 0.0)
+    for fn in (numpy.log, lambda x: 1.0 / x, lambda x: x ** -2.0):
+        for eta in (1e-3, 0.1, 2.0):
+            exact = numpy.mean([numpy.sum(P[:, p] ** 2 * fn(lam + eta)) / lam.size
+                                for p in range(6)])
+            G = _slq.quadrature(g, [eta], fn).mean()
+            R = _slq.quadrature(r, [eta], fn).mean()
+            lo, hi = min(G, R), max(G, R)
+            assert lo - 1e-12 * abs(exact) <= exact <= hi + 1e-12 * abs(exact)
+            assert abs(G - exact) <= _slq.bracket(g, r, [eta], fn)[0] * abs(G) * (1 + 1e-9) + \
+                1e-14 * abs(exact)
+
+
+def test_radau_of_a_broken_down_probe_is_its_gauss_rule():
+    a = numpy.array([[2.0, 1.0, 3.0]])
+    b = numpy.array([[0.5, 0.0, 0.0]])      # invariant after two steps: exact rule
+    g = _slq.nodes(a, b)
+    r = _slq.radau_nodes(a, b, 0.0)
+    numpy.testing.assert_array_equal(g[0][0], r[0][0])
+    assert _slq.bracket(g, r, [0.1], numpy.log)[0] == 0.0
+
+
+def test_radau_node_above_the_ritz_values_is_refused():
+    a = numpy.array([[2.0, 2.0]])
+    b = numpy.array([[1.0, 0.5]])
+    with pytest.raises(ValueError):
+        _slq.radau_nodes(a, b, 5.0)
+
+
+@pytest.mark.parametrize('method,options', [
+    ('slq', {'lanczos_degree': 10, 'bogus': 1}),
+    ('slq', {'exponent': 2}),                 # the reference passes it itself
+    ('hutchinson', {'lanczos_degree': 20}),
+    ('cholesky', {'num_samples': 5}),
+    ('eigenvalue', {'eigenvalues': None}),
+])
+def test_unknown_imate_options_raise_type_error(method, options):
+    """imate's keyword functions take no other keys than their own: a key that
+    no imate function of the method accepts is a TypeError at construction
+    (before any device work)."""
+    from gaussian_proc._mixed_correlation import MixedCorrelation
+    with pytest.raises(TypeError, match='unexpected keyword'):
+        MixedCorrelation(numpy.eye(4), imate_method=method, imate_options=options)
+
+
+def test_known_imate_options_pass_the_check():
+    from gaussian_proc._mixed_correlation.mixed_correlation import _check_options
+    _check_options('slq', {'min_num_samples': 5, 'max_num_samples': 9, 'error_rtol': 1e-2,
+                           'lanczos_degree': 20, 'lanczos_tol': 1e-6, 'orthogonalize': 0,
+                           'num_samples': 8, 'max_lanczos_degree': 64})
+    _check_options('hutchinson', {'solver_tol': 1e-8, 'orthogonalize': False, 'seed': 3})
+    _check_options('cholesky', {'cholmod': None, 'invert_cholesky': True})
+    _check_options('eigenvalue', {'non_zero_ratio': 0.9, 'tol': 1e-3})
+
+
+def test_next_lanczos_degree_extrapolates_the_gap():
+    """The lanczos_tol search: the first retry doubles the degree; with two gaps
+    the next degree is where the line through their logarithms reaches the
+    tolerance (+10 %, a multiple of 8), never fewer than 8 more steps."""
+    from gaussian_proc._mixed_correlation.mixed_correlation import _next_degree
+    assert _next_degree([(30, 0.46)], 1e-3) == 60
+    m = _next_degree([(30, 0.46), (60, 0.195)], 1e-3)
+    rate = numpy.log(0.46 / 0.195) / 30.0
+    want = 60 + numpy.log(0.195 / 1e-3) / rate
+    assert m % 8 == 0 and 1.1 * want <= m < 1.1 * want + 8
+    assert _next_degree([(40, 1e-3), (48, 2e-3)], 1e-6) == 96      # gap grew: double
+    assert _next_degree([(40, 1e-5), (80, 1.01e-6)], 1e-6) == 96   # 1.1 x 80.2, rounded up
+    assert _next_degree([(40, 1e-5), (41, 1e-12)], 1e-6) == 49     # at least 8 more
