@@ -266,10 +266,12 @@ def cpu_baseline(points, z, X, nu, eta, lam=None, samples=3):
     return out
 
 
-def cpu_baseline_sparse(K, X, z, etas, nprobe, steps, seed, budget_s, workers=None):
+def cpu_baseline_sparse(K, X, z, etas, nprobe, steps, seed, budget_s, workers=None,
+                        reorth=False):
     """Restated reference pattern for a sparse K on scipy (the shipped sparse
     path cannot run: SURVEY 0.4): stochastic Lanczos quadrature with the SAME
-    counter-based probes as the device (oracle.sparse: CSR SpMV Lanczos, CGS2)
+    counter-based probes and the same recurrence as the device (oracle.sparse: CSR
+    SpMV Lanczos, plain three-term for imate's orthogonalize = 0, else CGS2)
     for logdet at every eta, and per eta the reference's solves of X and z
     column by column with scipy.sparse.linalg.cg, rtol 1e-6
     (_linear_solver.py:57-68). The probes and the (eta, column) solves are
@@ -296,7 +298,7 @@ def cpu_baseline_sparse(K, X, z, etas, nprobe, steps, seed, budget_s, workers=No
     mats = {}
 
     def lanczos(p):
-        return osp.lanczos(K, P[:, p], steps)
+        return osp.lanczos(K, P[:, p], steps, reorth=reorth)
 
     def solve(task):
         j, c = task
@@ -341,22 +343,28 @@ def cpu_baseline_sparse(K, X, z, etas, nprobe, steps, seed, budget_s, workers=No
             'logdet': logdet.tolist(), 'gram_columns': cols}
 
 
-def sparse_step_bytes(n, nnz, s_lanczos, steps, s_cg, cg_iters):
+def sparse_step_bytes(n, nnz, s_lanczos, steps, s_cg, cg_iters, orthogonalize=0):
     """Algorithmic bytes of one sparse step as implemented (each vector block
-    read or written once per pass). Lanczos (block b_L = 8 n s_L), DCGS2
-    (gpmi_sparse.hip lz_*): per step k the SpMM (12 nnz + 8(n+1) + 2 b_L), the
-    dot pass over the k basis blocks, u and y ((k + 2) b_L) and the update pass
-    (k basis blocks, u, y read; v_k, u written: (k + 4) b_L), then one final dot
-    pass over the basis and u ((steps + 1) b_L). Multi-shift CG (b_C = 8 n s_C,
-    s_C the device width: a full 11-column block on the window SpMM is padded
-    by one zero column) per iteration: the SpMM (p . q in its epilogue), the
-    r update with B^T r / r . r on MFMA (b, r, q read, r written: 4 b_C) and
-    p = r + beta p (3 b_C)."""
+    read or written once per pass). Lanczos (block b_L = 8 n s_L): with
+    orthogonalize = 0 (imate's default, the plain recurrence, gpmi_sparse.hip
+    lz0_*) per step the SpMM (12 nnz + 8(n+1) + 2 b_L, u . Ku in its epilogue) and
+    the update pass (y, u_{k-1}, u_k read, u_{k+1} written: 4 b_L); with -1, DCGS2
+    (lz_*): per step k the SpMM, the dot pass over the k basis blocks, u and y
+    ((k + 2) b_L) and the update pass (k basis blocks, u, y read; v_k, u written:
+    (k + 4) b_L), then one final dot pass over the basis and u ((steps + 1) b_L).
+    Multi-shift CG (b_C = 8 n s_C, s_C the device width: a full 11-column block on
+    the window SpMM is padded by one zero column) per iteration: the SpMM (p . q in
+    its epilogue), the r update with B^T r / r . r on MFMA (b, r, q read, r
+    written: 4 b_C) and p = r + beta p (3 b_C)."""
     csr = 12.0 * nnz + 8.0 * (n + 1)
     bl, bc = 8.0 * n * s_lanczos, 8.0 * n * s_cg
-    lanczos = sum(csr + 2 * bl + (k + 2) * bl + (k + 4) * bl for k in range(steps)) + \
-        (steps + 1) * bl
-    basis = sum(2.0 * k * bl for k in range(steps)) + steps * bl
+    if orthogonalize == 0:
+        lanczos = steps * (csr + 2 * bl + 4 * bl)
+        basis = 0.0
+    else:
+        lanczos = sum(csr + 2 * bl + (k + 2) * bl + (k + 4) * bl for k in range(steps)) + \
+            (steps + 1) * bl
+        basis = sum(2.0 * k * bl for k in range(steps)) + steps * bl
     cg = cg_iters * (csr + 2 * bc + 7 * bc)
     return {'lanczos': lanczos, 'lanczos_basis_reads': basis, 'cg': cg,
             'total': lanczos + cg}
@@ -402,6 +410,7 @@ def sparse_measure(args, config, world, rank, local, dist, torch, cpu, exact, de
     D = generate_correlation(points, rho, nu, sparse=True, density=dens, device=local,
                              device_resident=True)
     t_asm = time.perf_counter() - t_asm
+    # imate's defaults otherwise: orthogonalize=0, the plain three-term recurrence
     op = MixedCorrelation(D, imate_method='slq',
                           imate_options={'num_samples': nprobe, 'lanczos_degree': steps})
     # eta grid above |lambda_min| (the tapered matrix is indefinite): smallest Ritz
@@ -445,8 +454,9 @@ def sparse_measure(args, config, world, rank, local, dist, torch, cpu, exact, de
     dt = time.perf_counter() - t0
     dt = max_over_ranks(dt, world, dist, torch)
     # imate's `orthogonalize` option: this rank's probe block by the plain three-term
-    # recurrence (0, imate's default) against the full reorthogonalisation the step
-    # uses (-1), Lanczos alone, and the two logdet curves in probe standard errors
+    # recurrence (0, imate's default, what the step uses) against full
+    # reorthogonalisation (-1, DCGS2), Lanczos alone, and the two logdet curves in
+    # probe standard errors
     lz = None
     if rank == 0:
         plo, phi, _ = shard(nprobe, world, rank)
@@ -465,8 +475,8 @@ def sparse_measure(args, config, world, rank, local, dist, torch, cpu, exact, de
         lz = {'probes': phi - plo, 'steps': steps, 'full_reorth_ms': round(lzt[-1], 3),
               'orthogonalize_0_ms': round(lzt[0], 3),
               'logdet_diff_in_std_errors_max': round(float(numpy.max(numpy.abs(dz))), 3),
-              'note': "imate's default orthogonalize=0 (plain three-term recurrence); the "
-                      "measured step uses full reorthogonalisation (DCGS2)"}
+              'note': "the measured step uses imate's default orthogonalize=0 (plain "
+                      "three-term recurrence); -1 is full reorthogonalisation (DCGS2)"}
     # SpMM roofline on a device-resident probe block (HIP events)
     s_blk = max(1, min(32, nprobe // world))
     ms = op.sop.bench_spmm(s_blk, 50)
@@ -487,7 +497,7 @@ def sparse_measure(args, config, world, rank, local, dist, torch, cpu, exact, de
     s_cg = (chi0 - clo0) + (1 if (world == 1 and R.shape[1] == 11 and
                                   op.sop.spmm_kernel(11) == 'csr_spmm_wing_kernel') else 0)
     sb = sparse_step_bytes(n, nnz, my_probes[1] - my_probes[0], steps, s_cg,
-                           holder['cg_iters'])
+                           holder['cg_iters'], op.orthogonalize)
     step_s = dt / args.steps
     res = None
     if rank == 0:
@@ -500,8 +510,9 @@ def sparse_measure(args, config, world, rank, local, dist, torch, cpu, exact, de
             'scaling': 'strong', 'vs_baseline': None, 'dtype': 'f64',
             'data': 'synthetic (reference data_utilities grid, sin + 0.2 noise seed 31)',
             'config': {'workload': '%s: N=%d %dD grid, nu=%g rho=%g density=%g, %d probes x '
-                                   '%d Lanczos steps, %d etas' % (config, n, dim, nu, rho,
-                                                                 dens, nprobe, steps, neta),
+                                   '%d Lanczos steps (orthogonalize=%d), %d etas'
+                                   % (config, n, dim, nu, rho, dens, nprobe, steps,
+                                      op.orthogonalize, neta),
                        'n': n, 'nnz': nnz, 'nnz_per_row': nnz / float(n), 'tau': D.tau,
                        'lambda_min_ritz': theta_min, 'eta_shift': shift,
                        'assembly_s': t_asm,
@@ -534,6 +545,7 @@ def sparse_measure(args, config, world, rank, local, dist, torch, cpu, exact, de
                 'cg_iterations': holder['cg_iters'],
                 'lanczos_probes': my_probes[1] - my_probes[0], 'lanczos_steps': steps,
                 'cg_columns': R.shape[1], 'cg_device_width': s_cg,
+                'lanczos_orthogonalize': op.orthogonalize,
                 'model': 'bench.sparse_step_bytes (each vector block once per pass)'},
             'lp_sample': [float(v) for v in last[0].tolist()],
             'cpu_baseline': None,
@@ -546,7 +558,7 @@ def sparse_measure(args, config, world, rank, local, dist, torch, cpu, exact, de
 
             def cpu_leg():
                 cpu_baseline_leg(res, holder, csr, X, z, etas, nprobe, steps, seed,
-                                 args.cpu_budget_s)
+                                 args.cpu_budget_s, reorth=op.orthogonalize != 0)
             if defer_cpu:
                 # run by the caller after every device measurement (host-side leftovers of
                 # the CPU baseline's thread pool slowed the launch-bound sparse steps that
@@ -558,10 +570,11 @@ def sparse_measure(args, config, world, rank, local, dist, torch, cpu, exact, de
     return res
 
 
-def cpu_baseline_leg(res, holder, csr, X, z, etas, nprobe, steps, seed, budget_s):
+def cpu_baseline_leg(res, holder, csr, X, z, etas, nprobe, steps, seed, budget_s,
+                     reorth=False):
     """The sparse line's CPU baseline (cpu_baseline_sparse) and its checks against the
     device results of the timed steps (holder), into res."""
-    cb = cpu_baseline_sparse(csr, X, z, etas, nprobe, steps, seed, budget_s)
+    cb = cpu_baseline_sparse(csr, X, z, etas, nprobe, steps, seed, budget_s, reorth=reorth)
     dev = holder['curves']['logdet']
     cb['slq_logdet_rel_diff_vs_device_same_probes'] = float(
         numpy.max(numpy.abs(numpy.asarray(cb.pop('logdet')) - dev) / numpy.abs(dev)))
@@ -857,9 +870,12 @@ def dense_slq_mode(D, etas, ld_exact, nprobe=20, steps=30, tol=1e-3, reps=3):
     exact solves (_linear_solver.py:71)."""
     from gaussian_proc import _slq
     from gaussian_proc._mixed_correlation import MixedCorrelation
+    # full reorthogonalisation: the plain recurrence (imate's default) had not converged
+    # at 256 steps at eta = 1e-3 on this smooth K (Gauss / Gauss-Radau gap 1.6e-2,
+    # 7.3 standard errors off)
     op = MixedCorrelation(D, imate_method='slq',
                           imate_options={'num_samples': nprobe, 'lanczos_degree': steps,
-                                         'lanczos_tol': tol})
+                                         'lanczos_tol': tol, 'orthogonalize': -1})
     n = op.n
     torch_sync()
     t0 = time.perf_counter()
@@ -868,7 +884,8 @@ def dense_slq_mode(D, etas, ld_exact, nprobe=20, steps=30, tol=1e-3, reps=3):
     t_search = time.perf_counter() - t0
     deg = conv['degree']
     fixed = MixedCorrelation(D, imate_method='slq',
-                             imate_options={'num_samples': nprobe, 'lanczos_degree': deg})
+                             imate_options={'num_samples': nprobe, 'lanczos_degree': deg,
+                                            'orthogonalize': -1})
     times = []
     for r in range(reps):
         fixed._lz = None

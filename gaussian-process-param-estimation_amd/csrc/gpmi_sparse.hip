@@ -616,6 +616,122 @@ __global__ void lanczos_scalar_kernel(const double* __restrict__ H1k,
 }
 
 // ---------------------------------------------------------------------------
+// Lanczos by the plain three-term recurrence (imate's orthogonalize = 0, its
+// default) in three launches per step and one pass over three vectors. The
+// vectors are stored unnormalised, u_k = gamma_k v_k (gamma_0 = 1: the probes are
+// normalised, gamma_k = beta_{k-1} after). Step k, in the order of
+// oracle/sparse.py lanczos(reorth=False) (w = K v_k - beta v_{k-1}; h = v_k . w;
+// w -= h v_k):
+//   SpMM    y = K u_k, with the 64-row block partials of u_k . y (the window
+//           kernel's epilogue, or lz0_dot64_kernel)
+//   alpha   per column (one wave each): gamma_k = ||u_k|| from the previous
+//           update's partials (= beta_{k-1}, with lanczos_scalar_kernel's breakdown
+//           test), alpha_k = h = (u_k . y) / gamma_k^2 - (u_k . u_{k-1}) / gamma_{k-1},
+//           and the update's coefficients
+//   update  u_{k+1} = y / gamma_k - (gamma_k / gamma_{k-1}) u_{k-1} - (h / gamma_k) u_k,
+//           with the 64-row block partials of ||u_{k+1}||^2 and u_{k+1} . u_k
+// A last alpha launch (k = steps) forms beta_{steps-1}. Every reduction has a fixed
+// order (deterministic). st: [0, s) gamma_k, [s, 2s) gamma_{k-1}; coef [3][s].
+
+// out[b][c] = sum over the 64 rows of block b of X[i][c] Y[i][c] (fixed order).
+__global__ __launch_bounds__(256) void lz0_dot64_kernel(const double* __restrict__ X,
+                                                        const double* __restrict__ Y, int64_t n,
+                                                        int s, double* __restrict__ out) {
+  __shared__ double sp[64 * 32];
+  const int t = threadIdx.x;
+  const int64_t r0 = (int64_t)blockIdx.x * 64;
+  const int rows = (int)min((int64_t)64, n - r0);
+  for (int e = t; e < 64 * s; e += 256) {
+    const int i = e / s;
+    sp[e] = i < rows ? X[r0 * s + e] * Y[r0 * s + e] : 0.0;
+  }
+  __syncthreads();
+  if (t < s) {
+    double a = 0.0;
+    for (int i = 0; i < 64; ++i) a += sp[i * s + t];
+    out[(int64_t)blockIdx.x * s + t] = a;
+  }
+}
+
+__global__ __launch_bounds__(256) void lz0_alpha_kernel(const double* __restrict__ pq,
+                                                        const double* __restrict__ pv, int nb,
+                                                        int s, int k, int steps,
+                                                        double* __restrict__ st,
+                                                        int* __restrict__ dead,
+                                                        double* __restrict__ alpha,
+                                                        double* __restrict__ beta,
+                                                        double* __restrict__ coef) {
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (c >= s) return;
+  const double d1 = k < steps ? wave_reduce_partials(pq, nb, s, c) : 0.0;
+  const double nrm2 = k > 0 ? wave_reduce_partials(pv, nb, 2 * s, c) : 1.0;
+  const double d2 = k > 0 ? wave_reduce_partials(pv, nb, 2 * s, s + c) : 0.0;
+  if ((threadIdx.x & 63) != 0) return;
+  double gam = 1.0, gamp = 1.0;
+  if (k == 0) {
+    dead[c] = 0;
+  } else {
+    gamp = st[c];
+    double b = dead[c] ? 0.0 : sqrt(fmax(nrm2, 0.0));
+    if (!dead[c] && !(b > 1e-13 * fmax(1.0, fabs(alpha[(int64_t)c * steps + k - 1])))) {
+      dead[c] = 1;
+      b = 0.0;
+    }
+    beta[(int64_t)c * steps + k - 1] = b;
+    gam = b;
+  }
+  if (k == steps) return;
+  st[c] = gam;
+  st[s + c] = gamp;
+  if (dead[c]) {
+    alpha[(int64_t)c * steps + k] = 0.0;
+    coef[c] = coef[s + c] = coef[2 * s + c] = 0.0;
+    return;
+  }
+  const double h = d1 / (gam * gam) - (k > 0 ? d2 / gamp : 0.0);
+  alpha[(int64_t)c * steps + k] = h;
+  coef[c] = 1.0 / gam;
+  coef[s + c] = k > 0 ? gam / gamp : 0.0;
+  coef[2 * s + c] = h / gam;
+}
+
+// u_{k+1} = c1 y - c2 u_{k-1} - c3 u_k per column, and per 64-row block b the partials
+// pv[b][0][c] = ||u_{k+1}||^2, pv[b][1][c] = u_{k+1} . u_k (fixed order).
+__global__ __launch_bounds__(256) void lz0_update_kernel(const double* __restrict__ Y,
+                                                         const double* __restrict__ Up,
+                                                         const double* __restrict__ Uc,
+                                                         double* __restrict__ Un,
+                                                         const double* __restrict__ coef,
+                                                         int64_t n, int s,
+                                                         double* __restrict__ pv) {
+  __shared__ double sq[64 * 32];
+  __shared__ double sx[64 * 32];
+  const int t = threadIdx.x;
+  const int64_t r0 = (int64_t)blockIdx.x * 64;
+  const int rows = (int)min((int64_t)64, n - r0);
+  for (int e = t; e < 64 * s; e += 256) {
+    const int i = e / s, c = e - i * s;
+    double w = 0.0, uc = 0.0;
+    if (i < rows) {
+      const int64_t g = r0 * s + e;
+      uc = Uc[g];
+      w = coef[c] * Y[g] - coef[s + c] * Up[g] - coef[2 * s + c] * uc;
+      Un[g] = w;
+    }
+    sq[e] = w * w;
+    sx[e] = w * uc;
+  }
+  __syncthreads();
+  if (t < 2 * s) {
+    const double* src = t < s ? sq : sx;
+    const int c = t < s ? t : t - s;
+    double a = 0.0;
+    for (int i = 0; i < 64; ++i) a += src[i * s + c];
+    pv[(int64_t)blockIdx.x * 2 * s + t] = a;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Lanczos with delayed classical Gram-Schmidt reorthogonalisation (DCGS2:
 // Bielich, Langou, Thomas, Swirydowicz, Yamazaki, Boman, Parallel Computing 112
 // (2022) 102940; numpy prototype tools/dcgs2_proto.py). CGS2 reads the basis four
@@ -1103,98 +1219,100 @@ __global__ __launch_bounds__(256) void ms_rmfma_kernel(const double* __restrict_
   }
 }
 
-// Scalar step 2 (thread (j, c), j < S shifts): with BR = B^T r_new and rr_new
-// reduced from the partials (fixed order; nblk == 0: reduced beforehand), advance zeta, accumulate G, update
-// b^T p and the base beta; a column stops when sqrt(rr) <= rtol ||b||.
-__global__ void ms_scalar_kernel(MsState st, const double* __restrict__ partial, int nblk,
-                                 const double* __restrict__ dshift, int S, int s, int nb,
-                                 double rtol2, double* __restrict__ beta_out) {
-  // nb: the dot columns of B (the bp / G rows c' < nb; nb >= s, the RHS columns)
+// The tail of one multi-shift CG iteration in ONE launch (replaces ms_scalar_kernel
+// + ms_p_update_kernel): every block forms p = r + beta p for its elements, with
+// beta = rr_new / rr and the stop test of each column computed from the reduced
+// r . r (br) and the CURRENT state `cur` (the values ms_scalar_kernel would have
+// written), and block 0 also advances the per-shift scalars as ms_scalar_kernel
+// and writes rr / active of the NEXT state `nxt` (double-buffered: the other blocks
+// read cur's during this launch). Four consecutive elements per thread as
+// ms_p_update_kernel.
+__global__ __launch_bounds__(256) void ms_tail_kernel(MsState cur, MsState nxt,
+                                                      const double* __restrict__ br_in,
+                                                      const double* __restrict__ dshift, int S,
+                                                      int s, int nb, double rtol2,
+                                                      double* __restrict__ P,
+                                                      const double* __restrict__ R, int64_t n) {
   __shared__ double br[MS_MAXS * MS_MAXS + MS_MAXS];
+  __shared__ double sbeta[MS_MAXS];
+  __shared__ int supd[MS_MAXS];
+  const int t = threadIdx.x;
   const int ne = nb * s + s;
-  if (nblk > 0) {
-    const int nw = blockDim.x >> 6, wv = threadIdx.x >> 6;
-    for (int e = wv; e < ne; e += nw) {
-      const double v = wave_reduce_partials(partial, nblk, ne, e);
-      if ((threadIdx.x & 63) == 0) br[e] = v;
-    }
-  } else {
-    // nblk == 0: `partial` holds the reduced values (col_dot_reduce_kernel, one wave
-    // per element over the whole chip: the same sums as above)
-    for (int e = threadIdx.x; e < ne; e += blockDim.x) br[e] = partial[e];
+  for (int e = t; e < ne; e += blockDim.x) br[e] = br_in[e];
+  __syncthreads();
+  if (t < s) {
+    const double rrn = br[nb * s + t];
+    const int act = cur.active[t];
+    const bool upd = act && !(rrn <= rtol2 * cur.bn2[t]);
+    sbeta[t] = act ? rrn / cur.rr[t] : 0.0;
+    supd[t] = upd ? 1 : 0;
   }
   __syncthreads();
-  const int t = threadIdx.x;
-  const int j = t / s, c = t % s;
-  if (j < S && st.active[c]) {
-    const double a = st.a[c], ap = st.a_prev[c], bo = st.beta[c];
-    const double z = st.z[j * s + c], zp = st.z_prev[j * s + c];
+  // p = r + beta p for the columns still active after this iteration
+  {
+    const int64_t ns = n * s;
+    const int64_t e = ((int64_t)blockIdx.x * 256 + t) * 4;
+    if (e < ns) {
+      int c = (int)(e % s);
+      if (((ns | (int64_t)(((uintptr_t)P | (uintptr_t)R) >> 3)) & 1) == 0 && e + 3 < ns) {
+        d2 p[2] = {*reinterpret_cast<const d2*>(P + e), *reinterpret_cast<const d2*>(P + e + 2)};
+        const d2 r[2] = {*reinterpret_cast<const d2*>(R + e),
+                         *reinterpret_cast<const d2*>(R + e + 2)};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (supd[c]) p[k >> 1][k & 1] = r[k >> 1][k & 1] + sbeta[c] * p[k >> 1][k & 1];
+          c = c + 1 == s ? 0 : c + 1;
+        }
+        *reinterpret_cast<d2*>(P + e) = p[0];
+        *reinterpret_cast<d2*>(P + e + 2) = p[1];
+      } else {
+        for (int k = 0; k < 4 && e + k < ns; ++k) {
+          if (supd[c]) P[e + k] = R[e + k] + sbeta[c] * P[e + k];
+          c = c + 1 == s ? 0 : c + 1;
+        }
+      }
+    }
+  }
+  if (blockIdx.x != 0) return;
+  // block 0: the per-shift scalars (thread (j, c) tasks in rounds of the block)
+  for (int task = t; task < S * s; task += blockDim.x) {
+    const int j = task / s, c = task % s;
+    if (!cur.active[c]) continue;
+    const double a = cur.a[c], ap = cur.a_prev[c], bo = cur.beta[c];
+    const double z = cur.z[j * s + c], zp = cur.z_prev[j * s + c];
     const double d = dshift[j];
     const double zn = z * zp * ap / (a * bo * (zp - z) + zp * ap * (1.0 + d * a));
     const double as = a * zn / z;
-    const double rrn = br[nb * s + c];
-    const double bnew = rrn / st.rr[c];
+    const double bnew = sbeta[c];
     const double bs = bnew * (zn / z) * (zn / z);
-    // every b^T p and G entry of (j, c) loaded before any store (the state arrays
-    // may alias for the compiler: one at a time, each iteration waited for its loads)
     double bpv[MS_MAXS], gv[MS_MAXS];
 #pragma unroll
     for (int cp = 0; cp < MS_MAXS; ++cp) {
       const int e = (j * nb + cp) * s + c;
-      bpv[cp] = cp < nb ? st.bp[e] : 0.0;
-      gv[cp] = cp < nb ? st.g[e] : 0.0;
+      bpv[cp] = cp < nb ? cur.bp[e] : 0.0;
+      gv[cp] = cp < nb ? cur.g[e] : 0.0;
     }
 #pragma unroll
     for (int cp = 0; cp < MS_MAXS; ++cp) {
       if (cp >= nb) break;
       const int e = (j * nb + cp) * s + c;
-      st.g[e] = gv[cp] + as * bpv[cp];
-      st.bp[e] = zn * br[cp * s + c] + bs * bpv[cp];
+      cur.g[e] = gv[cp] + as * bpv[cp];
+      cur.bp[e] = zn * br[cp * s + c] + bs * bpv[cp];
     }
-    st.z_prev[j * s + c] = z;
-    st.z[j * s + c] = zn;
+    cur.z_prev[j * s + c] = z;
+    cur.z[j * s + c] = zn;
   }
   __syncthreads();
-  if (t < s && st.active[t]) {
-    const double rrn = br[nb * s + t];
-    const double bnew = rrn / st.rr[t];
-    st.a_prev[t] = st.a[t];
-    st.beta[t] = bnew;
-    beta_out[t] = bnew;
-    st.rr[t] = rrn;
-    if (rrn <= rtol2 * st.bn2[t]) st.active[t] = 0;
-  }
-}
-
-// p[i][c] = r[i][c] + beta[c] p[i][c] for active columns
-// Four consecutive elements per thread, 16-byte loads and stores when n s is even and
-// both buffers are 16-byte aligned; grid: ceil(n s / 1024) workgroups. (Forming p
-// inside the next SpMM's window staging instead measured slower: the gathered
-// residual doubles the staging, 88 -> 174 us per cfg 5 launch against 21 us here.)
-__global__ __launch_bounds__(256) void ms_p_update_kernel(double* __restrict__ P,
-                                                          const double* __restrict__ R,
-                                                          const double* __restrict__ beta,
-                                                          const int* __restrict__ active,
-                                                          int64_t n, int s) {
-  const int64_t ns = n * s;
-  const int64_t e = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
-  if (e >= ns) return;
-  int c = (int)(e % s);
-  if (((ns | (int64_t)(((uintptr_t)P | (uintptr_t)R) >> 3)) & 1) == 0 && e + 3 < ns) {
-    d2 p[2] = {*reinterpret_cast<const d2*>(P + e), *reinterpret_cast<const d2*>(P + e + 2)};
-    const d2 r[2] = {*reinterpret_cast<const d2*>(R + e), *reinterpret_cast<const d2*>(R + e + 2)};
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      if (active[c]) p[k >> 1][k & 1] = r[k >> 1][k & 1] + beta[c] * p[k >> 1][k & 1];
-      c = c + 1 == s ? 0 : c + 1;
+  if (t < s) {
+    if (cur.active[t]) {
+      cur.a_prev[t] = cur.a[t];
+      cur.beta[t] = sbeta[t];
+      nxt.rr[t] = br[nb * s + t];
+      nxt.active[t] = supd[t];
+    } else {
+      nxt.rr[t] = cur.rr[t];
+      nxt.active[t] = 0;
     }
-    *reinterpret_cast<d2*>(P + e) = p[0];
-    *reinterpret_cast<d2*>(P + e + 2) = p[1];
-    return;
-  }
-  for (int k = 0; k < 4 && e + k < ns; ++k) {
-    if (active[c]) P[e + k] = R[e + k] + beta[c] * P[e + k];
-    c = c + 1 == s ? 0 : c + 1;
   }
 }
 

@@ -74,6 +74,11 @@ __global__ void rademacher_kernel(double*, int64_t, int, unsigned long long, int
                                   const int*);
 __global__ void csr_permute_kernel(const int64_t*, const int*, const double*, const int*,
                                    const int*, int64_t, const int64_t*, int*, double*);
+__global__ void lz0_dot64_kernel(const double*, const double*, int64_t, int, double*);
+__global__ void lz0_alpha_kernel(const double*, const double*, int, int, int, int, double*, int*,
+                                 double*, double*, double*);
+__global__ void lz0_update_kernel(const double*, const double*, const double*, double*,
+                                  const double*, int64_t, int, double*);
 __global__ void lanczos_scalar_kernel(const double*, const double*, const double*, int, int, int,
                                       int*, double*, double*, double*, double*, double*,
                                       double*);
@@ -82,10 +87,8 @@ void launch_ms_dots(const double* B, const double* R, int64_t n, int s, double* 
 __global__ void rows_gather_kernel(const double*, int, const int*, int64_t, int, double*);
 __global__ void ms_rmfma_kernel(const double*, double*, const double*, MsState, const double*, int,
                                 int64_t, int, int, double*);
-__global__ void ms_scalar_kernel(MsState, const double*, int, const double*, int, int, int,
-                                 double, double*);
-__global__ void ms_p_update_kernel(double*, const double*, const double*, const int*, int64_t,
-                                   int);
+__global__ void ms_tail_kernel(MsState, MsState, const double*, const double*, int, int, int, double,
+                               double*, const double*, int64_t);
 __global__ void ms_init_kernel(MsState, const double*, int, int, int, int);
 template <int CT>
 __global__ void dense_mm_kernel(const double*, int64_t, int64_t, const double*, int, int, double*);
@@ -137,6 +140,8 @@ struct Guard {
 
 
 }  // namespace
+
+constexpr int MS_BATCH = 8;   // multi-shift CG iterations between host polls
 
 struct gpmi_sp {
   int device = 0;
@@ -504,6 +509,66 @@ int lanczos_block(gpmi_sp* sp, double* V, double* W, int s, int steps, double* h
   SP_TRY(hipMemcpyAsync(h_alpha, dalpha, sizeof(double) * s * steps, hipMemcpyDeviceToHost,
                         sp->stream));
   SP_TRY(hipMemcpyAsync(h_beta, dbeta, sizeof(double) * s * steps, hipMemcpyDeviceToHost,
+                        sp->stream));
+  SP_TRY(hipStreamSynchronize(sp->stream));
+  return 0;
+}
+
+// Lanczos of K on s probe columns by the plain three-term recurrence (imate's
+// orthogonalize = 0; lz0_*_kernel in gpmi_sparse.hip): three launches per step (the
+// SpMM with u . Ku in its epilogue, the per-column scalars, one update pass over three
+// vectors with the next norm and overlap partials), the vectors unnormalised. U:
+// three rotating blocks [n][s] (U[0] = the normalised probes), Y one block.
+// alpha / beta: host [s][steps].
+int lanczos_block_plain(gpmi_sp* sp, double* U, double* Y, int s, int steps, double* h_alpha,
+                        double* h_beta) {
+  const int64_t n = sp->n, ns = n * s;
+  const int nb = (int)((n + 63) / 64);
+  const size_t need = 5 * (size_t)s + 2 * (size_t)s * steps + s;
+  if (sp->lz_doubles < need) {
+    if (sp->lz) SP_TRY(hipFree(sp->lz));
+    sp->lz = nullptr;
+    SP_TRY(hipMalloc(&sp->lz, sizeof(double) * need));
+    sp->lz_doubles = need;
+  }
+  double* st = sp->lz;
+  double* coef = st + 2 * s;
+  double* dal = coef + 3 * s;
+  double* dbe = dal + (size_t)s * steps;
+  int* dead = reinterpret_cast<int*>(dbe + (size_t)s * steps);
+  int rc = ensure_partial(sp, (size_t)nb * 3 * s);
+  if (rc) return rc;
+  double* pq = sp->partial;                 // [nb][s]: u_k . y
+  double* pv = pq + (size_t)nb * s;         // [nb][2][s]: ||u_{k+1}||^2, u_{k+1} . u_k
+  SP_TRY(hipMemsetAsync(dbe, 0, sizeof(double) * s * steps, sp->stream));
+  // u_{-1}: zero (its coefficient is 0 at k = 0; 0 * garbage could be NaN)
+  SP_TRY(hipMemsetAsync(U + 2 * ns, 0, sizeof(double) * ns, sp->stream));
+  const unsigned sgrid = (unsigned)((s + 3) / 4);
+  for (int k = 0; k < steps; ++k) {
+    double* Uc = U + (int64_t)(k % 3) * ns;
+    double* Un = U + (int64_t)((k + 1) % 3) * ns;
+    double* Up = U + (int64_t)((k + 2) % 3) * ns;
+    int pqb = 0;
+    rc = spmm(sp, Uc, Y, s, 0.0, sp->stream, pq, &pqb);
+    if (rc) return rc;
+    if (pqb != nb) {
+      hipLaunchKernelGGL(lz0_dot64_kernel, dim3((unsigned)nb), dim3(256), 0, sp->stream, Uc, Y, n,
+                         s, pq);
+      SP_LAUNCH("lz0_dot64_kernel");
+    }
+    hipLaunchKernelGGL(lz0_alpha_kernel, dim3(sgrid), dim3(256), 0, sp->stream, pq, pv, nb, s, k,
+                       steps, st, dead, dal, dbe, coef);
+    SP_LAUNCH("lz0_alpha_kernel");
+    hipLaunchKernelGGL(lz0_update_kernel, dim3((unsigned)nb), dim3(256), 0, sp->stream, Y, Up, Uc,
+                       Un, coef, n, s, pv);
+    SP_LAUNCH("lz0_update_kernel");
+  }
+  hipLaunchKernelGGL(lz0_alpha_kernel, dim3(sgrid), dim3(256), 0, sp->stream, pq, pv, nb, s, steps,
+                     steps, st, dead, dal, dbe, coef);
+  SP_LAUNCH("lz0_alpha_kernel");
+  SP_TRY(hipMemcpyAsync(h_alpha, dal, sizeof(double) * s * steps, hipMemcpyDeviceToHost,
+                        sp->stream));
+  SP_TRY(hipMemcpyAsync(h_beta, dbe, sizeof(double) * s * steps, hipMemcpyDeviceToHost,
                         sp->stream));
   SP_TRY(hipStreamSynchronize(sp->stream));
   return 0;
@@ -1017,7 +1082,8 @@ int gpmi_sp_lanczos_ex(gpmi_sp* sp, int nprobe, int steps, uint64_t seed, int pr
   const int64_t n = sp->n;
   for (int p0 = 0; p0 < nprobe; p0 += MAXS) {
     const int s = std::min(MAXS, nprobe - p0);
-    int rc = ensure_ws(sp, (size_t)(steps + 2) * n * s);
+    // the basis and a work block (the plain recurrence: three rotating blocks + one)
+    int rc = ensure_ws(sp, (size_t)std::max(steps + 2, 4) * n * s);
     if (rc) return rc;
     double* V = sp->ws;
     double* W = sp->ws + (size_t)(steps + 1) * n * s;
@@ -1029,8 +1095,15 @@ int gpmi_sp_lanczos_ex(gpmi_sp* sp, int nprobe, int steps, uint64_t seed, int pr
       return 0;
     };
     if ((rc = probes())) return rc;
-    if (orthogonalize >= 0) {
-      // no or windowed reorthogonalisation (imate's orthogonalize = 0 / k)
+    if (orthogonalize == 0) {
+      // the plain three-term recurrence (imate's default)
+      rc = lanczos_block_plain(sp, V, sp->ws + 3 * (size_t)n * s, s, steps,
+                               alpha + (size_t)p0 * steps, beta + (size_t)p0 * steps);
+      if (rc) return rc;
+      continue;
+    }
+    if (orthogonalize > 0) {
+      // windowed reorthogonalisation (imate's orthogonalize = k)
       rc = lanczos_block(sp, V, W, s, steps, alpha + (size_t)p0 * steps,
                          beta + (size_t)p0 * steps, orthogonalize);
       if (rc) return rc;
@@ -1221,7 +1294,7 @@ static int msgram_impl(gpmi_sp* sp, const double* etas, int neta, const double* 
   double* pqpart = partial + (size_t)MS_RB * ne;
   double* pqsum = pqpart + pq_rows * s;
   const size_t need = (size_t)6 * s + 2 * (size_t)S * s + 2 * (size_t)S * nbd * s + S + s + s +
-                      1 + (size_t)ne;
+                      1 + (size_t)ne + 2 * (size_t)s;
   if (sp->msbuf_doubles < need) {
     if (sp->msbuf) SP_TRY(hipFree(sp->msbuf));
     sp->msbuf = nullptr;
@@ -1240,12 +1313,19 @@ static int msgram_impl(gpmi_sp* sp, const double* etas, int neta, const double* 
   st.bp = q; q += (size_t)S * nbd * s;
   st.g = q; q += (size_t)S * nbd * s;
   double* dshift = q; q += S;
-  double* beta_out = q; q += s;
+  q += s;   // (spare slot)
   st.active = reinterpret_cast<int*>(q);   // s ints in s doubles
   q += s;
   st.flags = reinterpret_cast<int*>(q);    // 1 int in 1 double
   q += 1;
   double* brd = q;                         // [ne] reduced B^T r, r . r
+  q += ne;
+  // the second rr / active buffers (ms_tail_kernel reads one state's and writes the
+  // other's; iteration it's current state is st2[it & 1])
+  MsState st2[2] = {st, st};
+  st2[1].rr = q; q += s;
+  st2[1].active = reinterpret_cast<int*>(q);
+  q += s;
   sp->last_converged = 0;
   double* Bd = sp->ms_ws;
   double* Hs = Bd + even((size_t)nsb);   // the host block as given (original row order)
@@ -1301,9 +1381,10 @@ static int msgram_impl(gpmi_sp* sp, const double* etas, int neta, const double* 
   int it = 0;
   std::vector<int> hact(2 * s + 2);
   auto poll = [&](bool* any) -> int {
-    // active[0..s) and flags[0] (2 doubles after active's s) in one copy
-    SP_TRY(hipMemcpyAsync(hact.data(), st.active, sizeof(int) * (2 * s + 2), hipMemcpyDeviceToHost,
+    // the current state's active[0..s) and flags[0]
+    SP_TRY(hipMemcpyAsync(hact.data(), st2[it & 1].active, sizeof(int) * s, hipMemcpyDeviceToHost,
                           str));
+    SP_TRY(hipMemcpyAsync(hact.data() + 2 * s, st.flags, sizeof(int), hipMemcpyDeviceToHost, str));
     SP_TRY(hipStreamSynchronize(str));
     *any = false;
     for (int c = 0; c < s; ++c) *any = *any || hact[c];
@@ -1311,18 +1392,13 @@ static int msgram_impl(gpmi_sp* sp, const double* etas, int neta, const double* 
                                       "definite)")
                        : 0;
   };
-  for (; it < maxiter; ++it) {
-    if (it % 8 == 0) {
-      bool any = false;
-      rc = poll(&any);
-      if (rc) return rc;
-      if (!any) break;
-    }
+  // one iteration's launches on str (parity it & 1 picks the state double buffer)
+  auto iterate = [&](int itx) -> int {
     // the window SpMM also forms the p . q block partials in its epilogue (summed
     // across the chip below); other kernels leave them to col_dot_partial_kernel
     int pqb = 0;
-    rc = spmm(sp, Pd, Qd, s, eta0, str, pqpart, &pqb);
-    if (rc) return rc;
+    int rc1 = spmm(sp, Pd, Qd, s, eta0, str, pqpart, &pqb);
+    if (rc1) return rc1;
     const double* pqin = pqpart;
     int pqn = NBLK;
     if (pqb > 0) {
@@ -1331,24 +1407,35 @@ static int msgram_impl(gpmi_sp* sp, const double* etas, int neta, const double* 
       SP_LAUNCH("col_dot_reduce_kernel");
       pqin = pqsum;
       pqn = 1;
-    }
-    if (pqb == 0) {
+    } else {
       hipLaunchKernelGGL(col_dot_partial_kernel, dim3(NBLK, 1), dim3(256), 0, str, Pd, (int64_t)0,
                          Qd, n, s, pqpart);
       SP_LAUNCH("col_dot_partial_kernel");
     }
-    hipLaunchKernelGGL(ms_rmfma_kernel, dim3(MS_RB), dim3(256), 0, str, Bd, Rcur, Qd, st, pqin,
-                       pqn, n, s, nbd, partial);
+    hipLaunchKernelGGL(ms_rmfma_kernel, dim3(MS_RB), dim3(256), 0, str, Bd, Rcur, Qd, st2[itx & 1],
+                       pqin, pqn, n, s, nbd, partial);
     SP_LAUNCH("ms_rmfma_kernel");
     hipLaunchKernelGGL(col_dot_reduce_kernel, dim3((ne + 3) / 4), dim3(256), 0, str, partial, MS_RB,
                        1, ne, brd);
     SP_LAUNCH("col_dot_reduce_kernel");
-    hipLaunchKernelGGL(ms_scalar_kernel, dim3(1), dim3(sthreads), 0, str, st, (const double*)brd,
-                       0, dshift, S, s, nbd, rtol * rtol, beta_out);
-    SP_LAUNCH("ms_scalar_kernel");
-    hipLaunchKernelGGL(ms_p_update_kernel, dim3((unsigned)((ns + 1023) / 1024)), dim3(256), 0,
-                       str, Pd, Rcur, st.beta, st.active, n, s);
-    SP_LAUNCH("ms_p_update_kernel");
+    // the per-shift scalars and p = r + beta p in one launch (ms_tail_kernel)
+    hipLaunchKernelGGL(ms_tail_kernel, dim3((unsigned)((ns + 1023) / 1024)), dim3(256), 0, str,
+                       st2[itx & 1], st2[(itx + 1) & 1], (const double*)brd, dshift, S, s, nbd,
+                       rtol * rtol, Pd, (const double*)Rcur, n);
+    SP_LAUNCH("ms_tail_kernel");
+    return 0;
+  };
+  // Iterations run in batches of MS_BATCH between the host polls of the stop flags.
+  // (A batch captured once as a HIP graph and relaunched measured the same: the
+  // per-kernel cost is on the device, not in the host launches.)
+  for (; it < maxiter;) {
+    bool any = false;
+    rc = poll(&any);
+    if (rc) return rc;
+    if (!any) break;
+    const int nb = std::min(MS_BATCH, maxiter - it);
+    for (int q = 0; q < nb; ++q, ++it)
+      if ((rc = iterate(it))) return rc;
   }
   {
     bool any = false;

@@ -27,10 +27,15 @@ def _length(b):
 
 def _rule(d, e):
     """Nodes and squared first eigenvector components of the symmetric
-    tridiagonal (diagonal d, off-diagonal e): LAPACK stemr through scipy."""
+    tridiagonal (diagonal d, off-diagonal e): LAPACK stemr through scipy; the
+    dense symmetric solver where stemr does not converge (tight clusters: the
+    duplicated Ritz values of a recurrence without reorthogonalisation)."""
     if d.size == 1:
         return d.copy(), numpy.ones(1)
-    theta, U = scipy.linalg.eigh_tridiagonal(d, e)
+    try:
+        theta, U = scipy.linalg.eigh_tridiagonal(d, e)
+    except numpy.linalg.LinAlgError:
+        theta, U = numpy.linalg.eigh(numpy.diag(d) + numpy.diag(e, 1) + numpy.diag(e, -1))
     return theta, U[0] ** 2
 
 

@@ -153,7 +153,7 @@ def slq_sweep(K_mixed, etas, group=None, converge=('logdet',)):
         local[:, nq] = numpy.inf
         if hi > lo:
             a, b = K_mixed.sop.lanczos(hi - lo, deg, K_mixed.seed, probe_offset=lo,
-                                       orthogonalize=getattr(K_mixed, 'orthogonalize', -1))
+                                       orthogonalize=getattr(K_mixed, 'orthogonalize', 0))
             nodes = _slq.nodes(a, b)
             q = numpy.empty((hi - lo, len(names), etas.size))
             for f, name in enumerate(names):

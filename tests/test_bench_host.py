@@ -35,7 +35,7 @@ def test_cpu_baseline_sparse_thread_pool():
     cb = bench.cpu_baseline_sparse(K, X, z, etas, 4, 12, 5, 0.2, workers=3)
     assert cb['value'] > 0 and cb['cores'] == 3 and cb['threads'] == 3
     P = osp.rademacher_probes(n, 4, 5)
-    ref = osp.slq(K, etas, P, 12)['logdet']
+    ref = osp.slq(K, etas, P, 12, reorth=False)['logdet']
     numpy.testing.assert_allclose(cb['logdet'], ref, rtol=1e-12)
     # the solved Gram columns R^T (K + eta I)^-1 r_c (rtol 1e-6) against a direct solve
     R = numpy.column_stack([X, z])
@@ -48,7 +48,11 @@ def test_cpu_baseline_sparse_thread_pool():
 
 def test_sparse_step_bytes_model():
     n, nnz = 1000, 20000
-    b = bench.sparse_step_bytes(n, nnz, 4, 3, 2, 10)
+    p = bench.sparse_step_bytes(n, nnz, 4, 3, 2, 10)     # imate's default orthogonalize = 0
+    csr = 12.0 * nnz + 8.0 * (n + 1)
+    assert p['lanczos'] == 3 * (csr + 6 * 8.0 * n * 4) and p['lanczos_basis_reads'] == 0.0
+    assert p['cg'] == 10 * (csr + 9 * 8.0 * n * 2)
+    b = bench.sparse_step_bytes(n, nnz, 4, 3, 2, 10, orthogonalize=-1)
     csr = 12.0 * nnz + 8.0 * (n + 1)
     bl, bc = 8.0 * n * 4, 8.0 * n * 2
     lz = 0.0

@@ -83,13 +83,15 @@ def test_dense_lanczos_matches_oracle_same_probes(gp):
         assert rel(est, ref[what]) < 1e-9, what
 
 
-def test_dense_slq_operator_vs_exact(gp):
+@pytest.mark.parametrize('orth', [0, -1])
+def test_dense_slq_operator_vs_exact(gp, orth):
     """MixedCorrelation(K, imate_method='slq') on a dense K with imate's
     lanczos_tol: every SLQ quantity within 4 standard errors of its exact value,
     two-sided, down to eta = 0.01 (the Lanczos degree grows from 40 until the
     Gauss / Gauss-Radau gap at the eta asked is within the tolerance; at a fixed
     30 steps traceinv at eta = 0.01 was 14 standard errors low on this smooth
-    kernel, at 40 steps 3.8; the tolerance takes it to 160 steps)."""
+    kernel, at 40 steps 3.8; the tolerance takes it to ~110 steps). imate's default
+    plain three-term recurrence (orthogonalize=0) and full reorthogonalisation (-1)."""
     from gaussian_proc import _slq
     from gaussian_proc._mixed_correlation import MixedCorrelation
     K = _dense_K(32)
@@ -97,7 +99,7 @@ def test_dense_slq_operator_vs_exact(gp):
     ns = 64
     op = MixedCorrelation(K, imate_method='slq',
                           imate_options={'num_samples': ns, 'lanczos_degree': 40,
-                                         'lanczos_tol': 1e-6})
+                                         'lanczos_tol': 1e-6, 'orthogonalize': orth})
     lam = numpy.linalg.eigvalsh(K)
     cases = (('logdet', numpy.log, lambda e: op.logdet(e), (0.01, 0.3, 5.0)),
              ('traceinv', lambda x: 1.0 / x, lambda e: op.traceinv(e), (0.01, 0.3, 5.0)),
