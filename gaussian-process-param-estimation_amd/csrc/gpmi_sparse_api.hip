@@ -171,6 +171,8 @@ struct gpmi_sp {
   size_t ms_ws_doubles = 0;
   double* ms_partial = nullptr;
   size_t ms_partial_doubles = 0;
+  void* ms_pin = nullptr;                  // pinned flags / r.r of two CG batches
+  hipEvent_t ms_ev[2] = {nullptr, nullptr};
   std::mutex win_mu;           // the lazy X-window build (ensure_window)
   size_t msbuf_doubles = 0;
   int last_converged = 1;      // last gpmi_sp_cg / gpmi_sp_msgram met rtol in every column
@@ -947,6 +949,9 @@ int gpmi_sp_destroy(gpmi_sp* sp) {
   if (sp->lzd) (void)hipFree(sp->lzd);
   if (sp->ms_ws) (void)hipFree(sp->ms_ws);
   if (sp->ms_partial) (void)hipFree(sp->ms_partial);
+  if (sp->ms_pin) (void)hipHostFree(sp->ms_pin);
+  for (hipEvent_t e : sp->ms_ev)
+    if (e) (void)hipEventDestroy(e);
   if (sp->ms_stream) (void)hipStreamDestroy(sp->ms_stream);
   if (sp->win_cols) (void)hipFree(sp->win_cols);
   if (sp->win_u) (void)hipFree(sp->win_u);
@@ -1425,17 +1430,100 @@ static int msgram_impl(gpmi_sp* sp, const double* etas, int neta, const double* 
     SP_LAUNCH("ms_tail_kernel");
     return 0;
   };
-  // Iterations run in batches of MS_BATCH between the host polls of the stop flags.
-  // (A batch captured once as a HIP graph and relaunched measured the same: the
-  // per-kernel cost is on the device, not in the host launches.)
-  for (; it < maxiter;) {
+  // Iterations run in batches between host reads of the stop flags. Each batch's end
+  // state (active flags, the negative-curvature flag, r . r) is copied into pinned
+  // memory behind it and read while the NEXT batch is already queued, so the device
+  // does not wait for the host between batches (a synchronous poll every 8
+  // iterations drained the queue). The next batch's size comes from the residuals'
+  // decay: the iterations the slowest active column still needs to reach rtol at its
+  // rate since the previous read, beyond what is queued (at most MS_BATCH); when the
+  // queued iterations should suffice, the host waits for them instead of queueing
+  // more. Iterations past a column's convergence leave it unchanged (zero steps).
+  // (A batch captured as a HIP graph and relaunched measured the same as launching
+  // it: the per-kernel cost is on the device.)
+  struct PinSlot {
+    int act[MS_MAXS];
+    int flag;
+    int pad;
+    double rr[MS_MAXS];
+  };
+  if (!sp->ms_pin) {
+    SP_TRY(hipHostMalloc(reinterpret_cast<void**>(&sp->ms_pin), 2 * sizeof(PinSlot),
+                         hipHostMallocDefault));
+    for (hipEvent_t* e : {&sp->ms_ev[0], &sp->ms_ev[1]})
+      SP_TRY(hipEventCreateWithFlags(e, hipEventDisableTiming));
+  }
+  PinSlot* pin = reinterpret_cast<PinSlot*>(sp->ms_pin);
+  std::vector<double> hbn2(s);
+  {
     bool any = false;
+    SP_TRY(hipMemcpyAsync(hbn2.data(), st.bn2, sizeof(double) * s, hipMemcpyDeviceToHost, str));
     rc = poll(&any);
     if (rc) return rc;
-    if (!any) break;
-    const int nb = std::min(MS_BATCH, maxiter - it);
+    if (!any) maxiter = 0;
+  }
+  int slot_it[2] = {0, 0};
+  int it_done = -1;   // the iterations after which every column had stopped
+  std::vector<double> rr_seen(s, -1.0);
+  int it_seen = 0;
+  bool prev = false;   // a previous batch's slot awaits reading
+  int nb = MS_BATCH;
+  int k = 0;
+  // read slot q: 0 = columns remain, 1 = all stopped, < 0 / > 0 an error code
+  auto read_slot = [&](int q, int* remaining_after) -> int {
+    SP_TRY(hipEventSynchronize(sp->ms_ev[q]));
+    if (pin[q].flag) {
+      SP_TRY(hipStreamSynchronize(str));
+      return set_error(1, "multi-shift CG: p^T (K + min(eta) I) p <= 0 (not positive definite)");
+    }
+    bool any = false;
+    double need = 0.0;
+    const int at = slot_it[q];
+    for (int c = 0; c < s; ++c) {
+      if (!pin[q].act[c]) continue;
+      any = true;
+      const double r1 = pin[q].rr[c], r0 = rr_seen[c], target = rtol * rtol * hbn2[c];
+      double m = (double)MS_BATCH;
+      if (r0 > 0.0 && r1 > 0.0 && r1 < r0 && at > it_seen && target > 0.0)
+        m = std::log(target / r1) / (std::log(r1 / r0) / (double)(at - it_seen));
+      need = std::max(need, m);
+      rr_seen[c] = r1;
+    }
+    it_seen = at;
+    *remaining_after = (int)std::ceil(at + need) - it;   // beyond the queued iterations
+    if (!any) it_done = at;
+    return any ? 0 : 2;
+  };
+  while (it < maxiter) {
+    nb = std::max(1, std::min(nb, maxiter - it));
     for (int q = 0; q < nb; ++q, ++it)
       if ((rc = iterate(it))) return rc;
+    const int q = k & 1;
+    SP_TRY(hipMemcpyAsync(pin[q].act, st2[it & 1].active, sizeof(int) * s, hipMemcpyDeviceToHost,
+                          str));
+    SP_TRY(hipMemcpyAsync(&pin[q].flag, st.flags, sizeof(int), hipMemcpyDeviceToHost, str));
+    SP_TRY(hipMemcpyAsync(pin[q].rr, st2[it & 1].rr, sizeof(double) * s, hipMemcpyDeviceToHost,
+                          str));
+    SP_TRY(hipEventRecord(sp->ms_ev[q], str));
+    slot_it[q] = it;
+    ++k;
+    int rem = MS_BATCH;
+    if (prev) {
+      const int r = read_slot(q ^ 1, &rem);
+      if (r == 2) break;   // stopped before the queued batch (which then ran as zero steps)
+      if (r) return r;
+    }
+    prev = true;
+    if (rem <= 0) {
+      // the queued iterations should reach rtol: wait for them rather than queue more
+      int rem2 = 0;
+      const int r = read_slot(q, &rem2);
+      if (r == 2) break;
+      if (r) return r;
+      prev = false;
+      rem = rem2;
+    }
+    nb = std::max(1, std::min(MS_BATCH, rem));
   }
   {
     bool any = false;
@@ -1450,7 +1538,7 @@ static int msgram_impl(gpmi_sp* sp, const double* etas, int neta, const double* 
     for (int a = 0; a < nrhs; ++a)
       for (int c = 0; c < nsub; ++c)
         G[((size_t)j * nrhs + a) * nsub + c] = hg[((size_t)j * nbd + a) * s + c];
-  if (iterations) *iterations = it;
+  if (iterations) *iterations = it_done >= 0 ? it_done : it;
   return 0;
 }
 
