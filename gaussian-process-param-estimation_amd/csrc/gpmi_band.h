@@ -50,6 +50,8 @@ __global__ void syr2k_kernel(double* A, int64_t lda, const double* U, int64_t ld
                              int mt, int sub);
 __global__ void syr2k_rest_kernel(double* A, int64_t lda, const double* U, int64_t ldu, int tr0,
                                   int mt, const uint32_t* order);
+__global__ void syr2k_pipe_kernel(double* A, int64_t lda, const double* U, int64_t ldu, int tr0,
+                                  int mt);
 __global__ void bcr_f0_kernel(const double* Ab, int64_t lda, double* F0);
 __global__ void bcr_chol_kernel(const double* Ab, int64_t lda, const double* etas, int lvl,
                                 int first, const double* Din, int64_t sD, const double* Yin,

@@ -573,6 +573,126 @@ __global__ __launch_bounds__(256, 2) void syr2k_rest_kernel(double* __restrict__
   }
 }
 
+// Look-ahead SYR2K that leaves whole CUs to the next panel's chain: a persistent
+// tile loop of ONE workgroup per CU (launch_bounds (256, 1): every wave owns a
+// SIMD's 512 registers), so a grid of NCU - F workgroups leaves F CUs with nothing
+// of it and the chain's single-workgroup kernels (cq_chol, cq_recon: 280-400
+// registers, 150 KB of LDS) run there at once instead of after the SYR2K drains.
+// One workgroup per CU keeps the two-per-CU throughput by software pipelining
+// (tools/probe/syr2k_probe.hip rest_pipe: 0.716 of the fp64 peak at k = 256, as two
+// plain workgroups per CU): while tile q runs its 16 k-steps, 4 of the 64 per-lane C
+// values of tile q + grid are loaded and 4 of tile q - grid's results are stored per
+// step, and the last step stages tile q + grid's first operand slab. Tiles as
+// syr2k_rest_kernel (the triangle right of tile column 0, from tile row tr0 + 1).
+__global__ __launch_bounds__(256, 1) void syr2k_pipe_kernel(double* __restrict__ A, int64_t lda,
+                                                            const double* __restrict__ U,
+                                                            int64_t ldu, int tr0, int mt) {
+  __shared__ double smem[4 * GSTAGE];
+  constexpr int KD = 2 * TS;
+  constexpr int NS = KD / BK;
+  constexpr int PER = (64 + NS - 1) / NS;   // C values per lane per step
+  const int ntiles = (mt - 1) * mt / 2;
+  int q = blockIdx.x;
+  if (q >= ntiles) return;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int wr = w >> 1, wc = w & 1, fr = lane & 15, fk = lane >> 4;
+  double* sA = smem;
+  double* sB = smem + 2 * GSTAGE;
+  auto tile_ptrs = [&](int qq, double** C, const double** P1, const double** P2) {
+    int i, j;
+    tri_decode(qq, mt - 1, &i, &j);
+    const int I = tr0 + 1 + i, J = tr0 + 1 + j;
+    *C = A + (int64_t)I * TS * lda + (int64_t)J * TS;
+    *P1 = U + (int64_t)I * TS * ldu;
+    *P2 = U + (int64_t)J * TS * ldu + TS;
+  };
+  const int64_t coff = (int64_t)(wr * 64 + fk) * lda + wc * 64 + fr;
+  auto cidx = [&](int e) -> int64_t {   // e = a * 16 + c * 4 + r
+    return (int64_t)((e >> 4) * 16 + 4 * (e & 3)) * lda + ((e >> 2) & 3) * 16;
+  };
+  d4 acc[4][4], cn[4][4], po[4][4];
+  double* Cq;
+  const double *P1, *P2;
+  tile_ptrs(q, &Cq, &P1, &P2);
+  load_tile(Cq, lda, acc);
+  d2 ra[4], rb[4];
+  gl_op<KFAST>(P1, ldu, 0, ra);
+  gl_op<KFAST>(P2, ldu, 0, rb);
+  st_op<KFAST>(sA, ra);
+  st_op<KFAST>(sB, rb);
+  __syncthreads();
+  double* Cp = nullptr;
+  bool has_p = false;
+  while (true) {
+    const int qn = q + gridDim.x;
+    const bool has_n = qn < ntiles;
+    double* Cn = nullptr;
+    const double *N1 = nullptr, *N2 = nullptr;
+    if (has_n) tile_ptrs(qn, &Cn, &N1, &N2);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const int cur = s & 1;
+      const double* cA = sA + cur * GSTAGE;
+      const double* cB = sB + cur * GSTAGE;
+      const bool ld = s + 1 < NS || has_n;
+      if (s + 1 < NS) {
+        gl_op<KFAST>(P1, ldu, (s + 1) * BK, ra);
+        gl_op<KFAST>(P2, ldu, (s + 1) * BK, rb);
+      } else if (has_n) {
+        gl_op<KFAST>(N1, ldu, 0, ra);
+        gl_op<KFAST>(N2, ldu, 0, rb);
+      }
+      if (has_n) {
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+          const int e = s * PER + u;
+          if (e < 64) cn[e >> 4][(e >> 2) & 3][e & 3] = Cn[coff + cidx(e)];
+        }
+      }
+      if (has_p) {
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+          const int e = s * PER + u;
+          if (e < 64) Cp[coff + cidx(e)] = po[e >> 4][(e >> 2) & 3][e & 3];
+        }
+      }
+#pragma unroll
+      for (int kk = 0; kk < BK / 4; ++kk) {
+        double a[4], b[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a[i] = fr_op<KFAST>(cA, wr * 64 + i * 16 + fr, kk * 4 + fk);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) b[j] = fr_op<KFAST>(cB, wc * 64 + j * 16 + fr, kk * 4 + fk);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = mfma64_neg(a[i], b[j], acc[i][j]);
+      }
+      if (ld) {
+        st_op<KFAST>(sA + (cur ^ 1) * GSTAGE, ra);
+        st_op<KFAST>(sB + (cur ^ 1) * GSTAGE, rb);
+      }
+      __syncthreads();
+    }
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        po[a][c] = acc[a][c];
+        acc[a][c] = cn[a][c];
+      }
+    Cp = Cq;
+    has_p = true;
+    if (!has_n) break;
+    q = qn;
+    Cq = Cn;
+    P1 = N1;
+    P2 = N2;
+  }
+#pragma unroll
+  for (int e = 0; e < 64; ++e) Cp[coff + cidx(e)] = po[e >> 4][(e >> 2) & 3][e & 3];
+}
+
 // ---------------------------------------------------------------------------
 // Y <- Q_j^T Y for one panel (Y rows r0.., 16 columns): Y -= V (T^T (V^T Y)).
 // V is read from the reduced matrix (unit lower trapezoidal below the band).

@@ -113,6 +113,8 @@ struct gpmi_band {
   // and inverses, the reconstruction's U^-T, V1, signs, scratch, failure flag
   int panel_mode = 0;        // 0 CholeskyQR, 1 Householder (single launch)
   int cq_fallbacks = 0;      // reductions redone with Householder panels
+  int la_free = 32;          // CUs the pipelined look-ahead SYR2K leaves to the chain
+                             // (GPMI_BAND_LA_FREE; < 0: the capped two-per-CU SYR2K below)
   int cq_la_grid = 448;      // SYR2K grid cap beside a CholeskyQR panel (0: none; measured
                              // at N = 16384: 448 161-163 ms, none 165-168, no look-ahead 164-166)
   double* Qb = nullptr;
@@ -279,7 +281,11 @@ int qt_panel(gpmi_band* b, int j, hipStream_t st) {
 // then Householder reconstruction into V (the panel below its top block), tau and
 // S R (the top block). A failure sets the panel's flag [4] before anything is written
 // to the panel, and the guarded Householder panel factors it instead.
-int cq_panel(gpmi_band* b, int j, hipStream_t st) {
+int cq_guard(gpmi_band* b, int j, hipStream_t st);
+
+// guard: launch the guarded Householder panel right behind the chain (false: the
+// caller launches it, cq_guard, where every CU is free again)
+int cq_panel(gpmi_band* b, int j, hipStream_t st, bool guard = true) {
   const int64_t np = b->n_pad;
   const int64_t r0 = (int64_t)(j + 1) * TS, c0 = (int64_t)j * TS;
   const int m = (int)(np - r0);
@@ -323,12 +329,22 @@ int cq_panel(gpmi_band* b, int j, hipStream_t st) {
                        (int64_t)TS, P + TS * np, np, b->cqMinv, nullptr, fl + 4);
     BD_LAUNCH("cq_apply_kernel");
   }
-  // a failed panel (flag fl[4], P untouched) by the Householder panel in one launch,
-  // guarded on the device (it exits at once when the flag is clear); past that
-  // launch's size (G > panel_maxg workgroups cannot all be co-resident) the host
-  // reads the flag after the chain and, only for a failed panel, runs the
-  // per-column Householder launches on the same stream: that panel alone falls
-  // back, the reduction goes on (one host round trip per such panel)
+  return guard ? cq_guard(b, j, st) : 0;
+}
+
+// A failed CholeskyQR panel j (flag fl[4], P untouched) by the Householder panel in
+// one launch, guarded on the device (it exits at once when the flag is clear); past
+// that launch's size (G > panel_maxg workgroups cannot all be co-resident) the host
+// reads the flag after the chain and, only for a failed panel, runs the per-column
+// Householder launches on the same stream: that panel alone falls back, the
+// reduction goes on (one host round trip per such panel). The guarded launch needs
+// its G workgroups co-resident, so it runs where no SYR2K holds CUs.
+int cq_guard(gpmi_band* b, int j, hipStream_t st) {
+  const int64_t np = b->n_pad;
+  const int64_t r0 = (int64_t)(j + 1) * TS, c0 = (int64_t)j * TS;
+  const int m = (int)(np - r0);
+  double* P = b->Ab + r0 * np + c0;
+  int* fl = b->cqflag + 8 * j;
   const int G = (m + HH_ROWS - 1) / HH_ROWS;
   if (G <= b->panel_maxg) {
     hipLaunchKernelGGL(hh_panel_kernel, dim3(G), dim3(HH_THREADS), HH_PANEL_LDS, st, P, np, m,
@@ -354,12 +370,16 @@ int cq_panel(gpmi_band* b, int j, hipStream_t st) {
 // Panel j (columns [128 j, +128), rows from 128 (j + 1)) on st. mode 0: CholeskyQR;
 // 1: Householder, one launch per panel where its workgroups fit; 2: Householder,
 // one launch per column.
-int panel_qr(gpmi_band* b, int j, hipStream_t st, int mode) {
+int panel_qr(gpmi_band* b, int j, hipStream_t st, int mode, bool* guard_deferred = nullptr) {
   const int64_t np = b->n_pad;
   const int64_t r0 = (int64_t)(j + 1) * TS, c0 = (int64_t)j * TS;
+  if (guard_deferred) *guard_deferred = false;
   // a last panel with fewer than 128 real rows (ragged n: the rest is the zero
   // pad) has rank < 128, which CholeskyQR cannot orthonormalise: Householder
-  if (mode == 0 && b->n - r0 >= TS) return cq_panel(b, j, st);
+  if (mode == 0 && b->n - r0 >= TS) {
+    if (guard_deferred) *guard_deferred = true;
+    return cq_panel(b, j, st, guard_deferred == nullptr);
+  }
   if (mode == 0) mode = 1;
   const int m = (int)(np - r0);
   const int G = (m + HH_ROWS - 1) / HH_ROWS;
@@ -471,20 +491,36 @@ int band_reduce_pass(gpmi_band* b, const double* K, const std::vector<double>* y
       BD_LAUNCH("syr2k_kernel");
       BD_TRY(hipEventRecord(b->ev_col, s));
       BD_TRY(hipStreamWaitEvent(b->s_pan, b->ev_col, 0));
-      int rc = panel_qr(b, j + 1, b->s_pan, mode);
+      const bool pipe = mode == 0 && b->la_free >= 0;
+      bool guard = false;
+      int rc = panel_qr(b, j + 1, b->s_pan, mode, pipe ? &guard : nullptr);
       if (rc) return rc;
       BD_TRY(hipEventRecord(b->ev_pan, b->s_pan));
       const int rest = (mt - 1) * mt / 2;
-      // la_grid 0: leave exactly the panel's workgroup count of CUs free (measured:
-      // slower than a fixed 128-workgroup cap at N = 16384, 302 vs 262 ms); the
-      // CholeskyQR panel needs no co-resident workgroups (cq_la_grid, 0: no cap)
-      const int cap = mode == 0 ? (b->cq_la_grid > 0 ? b->cq_la_grid : rest)
-                      : b->la_grid > 0 ? b->la_grid : std::max(64, b->ncu - next_g);
-      hipLaunchKernelGGL(syr2k_rest_kernel, dim3(std::min(rest, cap)), dim3(256), 0, s, b->Ab,
-                         np, b->U, (int64_t)BAND_ULD, j + 1,
-                         mt, b->rorder ? b->rorder + b->rorder_off[mt - 1] : nullptr);
-      BD_LAUNCH("syr2k_rest_kernel");
+      if (pipe) {
+        // one SYR2K workgroup per CU on all but la_free CUs, which the chain (its
+        // single-workgroup kernels need a whole CU) has to itself
+        hipLaunchKernelGGL(syr2k_pipe_kernel, dim3(std::min(rest, std::max(1, b->ncu - b->la_free))),
+                           dim3(256), 0, s, b->Ab, np, b->U, (int64_t)BAND_ULD, j + 1, mt);
+        BD_LAUNCH("syr2k_pipe_kernel");
+      } else {
+        // la_grid 0: leave exactly the panel's workgroup count of CUs free (measured:
+        // slower than a fixed 128-workgroup cap at N = 16384, 302 vs 262 ms); the
+        // CholeskyQR panel needs no co-resident workgroups (cq_la_grid, 0: no cap)
+        const int cap = mode == 0 ? (b->cq_la_grid > 0 ? b->cq_la_grid : rest)
+                        : b->la_grid > 0 ? b->la_grid : std::max(64, b->ncu - next_g);
+        hipLaunchKernelGGL(syr2k_rest_kernel, dim3(std::min(rest, cap)), dim3(256), 0, s, b->Ab,
+                           np, b->U, (int64_t)BAND_ULD, j + 1,
+                           mt, b->rorder ? b->rorder + b->rorder_off[mt - 1] : nullptr);
+        BD_LAUNCH("syr2k_rest_kernel");
+      }
       BD_TRY(hipStreamWaitEvent(s, b->ev_pan, 0));
+      if (guard) {
+        // the guarded Householder panel behind the SYR2K (its workgroups must be
+        // co-resident: every CU is free again here)
+        rc = cq_guard(b, j + 1, s);
+        if (rc) return rc;
+      }
       ahead = true;
     } else {
       const int tiles = mt * (mt + 1) / 2;
@@ -603,6 +639,7 @@ int gpmi_band_create(gpmi_op* op, gpmi_band** out) {
   if ((e = hipStreamCreateWithFlags(&b->side, hipStreamNonBlocking)) != hipSuccess)
     return fail(e, "side stream");
   if (const char* la = std::getenv("GPMI_BAND_LA")) b->lookahead = std::atoi(la);
+  if (const char* lf = std::getenv("GPMI_BAND_LA_FREE")) b->la_free = std::atoi(lf);
   if (const char* pm = std::getenv("GPMI_BAND_PANEL")) b->panel_mode = std::strcmp(pm, "hh") == 0;
   if (const char* bm = std::getenv("GPMI_BAND_BCR")) b->bcr_mode = std::max(0, std::min(2, std::atoi(bm)));
   // GPMI_CQ_FO=0: every CholeskyQR pass by an exact Cholesky (no first-order passes)

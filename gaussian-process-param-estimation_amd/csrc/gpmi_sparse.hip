@@ -585,6 +585,71 @@ __global__ __launch_bounds__(256) void col_axpby_kernel(const double* __restrict
   Y[e] = a[c] * X[e] + b[c] * Y[e];
 }
 
+// gpmi_sp_cg with its scalars on the device (no host round trip per iteration).
+// Step 1: an active column c (act[c]) takes a = rr[c] / pq[c]; x += a p, r -= a q.
+// Block 0 flags a non-positive p.q of an active column (the host reads err when it polls).
+__global__ __launch_bounds__(256) void cg_xr_kernel(const double* __restrict__ P,
+                                                    const double* __restrict__ Q,
+                                                    double* __restrict__ X, double* __restrict__ R,
+                                                    const double* __restrict__ rr,
+                                                    const double* __restrict__ pq,
+                                                    const int* __restrict__ act, int64_t n, int s,
+                                                    int* __restrict__ err) {
+  if (blockIdx.x == 0 && threadIdx.x < (unsigned)s) {
+    const int c = threadIdx.x;
+    if (act[c] && !(pq[c] > 0.0)) err[0] = 1;
+  }
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= n * s) return;
+  const int c = (int)(e % s);
+  if (!act[c]) return;
+  const double a = rr[c] / pq[c];
+  X[e] += a * P[e];
+  R[e] -= a * Q[e];
+}
+
+// Step 2: p = r + (rrn[c] / rr[c]) p on the active columns. Block 0 writes the next
+// iteration's flags (active while sqrt(rrn) > rtol ||b||, the host loop's test) and,
+// when any column ran this iteration, the iteration count it + 1.
+__global__ __launch_bounds__(256) void cg_p_kernel(const double* __restrict__ R,
+                                                   double* __restrict__ P,
+                                                   const double* __restrict__ rr,
+                                                   const double* __restrict__ rrn,
+                                                   const int* __restrict__ act,
+                                                   int* __restrict__ act_next,
+                                                   const double* __restrict__ thr, int it,
+                                                   int* __restrict__ iters, int64_t n, int s) {
+  if (blockIdx.x == 0 && threadIdx.x < (unsigned)s) {
+    const int c = threadIdx.x;
+    act_next[c] = act[c] && (std::sqrt(rrn[c]) > thr[c]);
+    if (c == 0) {
+      int any = 0;
+      for (int k = 0; k < s; ++k) any |= act[k];
+      if (any) iters[0] = it + 1;
+    }
+  }
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= n * s) return;
+  const int c = (int)(e % s);
+  if (!act[c]) return;
+  P[e] = R[e] + (rrn[c] / rr[c]) * P[e];
+}
+
+// First flags: thr = rtol sqrt(rr0), act = sqrt(rr0) > thr.
+__global__ void cg_init_kernel(const double* __restrict__ rr, double rtol, int s,
+                               double* __restrict__ thr, int* __restrict__ act,
+                               int* __restrict__ err, int* __restrict__ iters) {
+  const int c = threadIdx.x;
+  if (c == 0) {
+    err[0] = 0;
+    iters[0] = 0;
+  }
+  if (c >= s) return;
+  const double bn = std::sqrt(rr[c]);
+  thr[c] = rtol * bn;
+  act[c] = bn > rtol * bn;
+}
+
 // Lanczos step k scalars on the device (no host round trip): alpha = the two
 // CGS2 passes' projections on V_k, beta = ||W||, a column whose beta falls below
 // 1e-13 max(1, |alpha|) is dead (invariant subspace: padding from then on).
@@ -661,12 +726,52 @@ __global__ __launch_bounds__(256) void lz0_alpha_kernel(const double* __restrict
                                                         double* __restrict__ alpha,
                                                         double* __restrict__ beta,
                                                         double* __restrict__ coef) {
-  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (c >= s) return;
-  const double d1 = k < steps ? wave_reduce_partials(pq, nb, s, c) : 0.0;
-  const double nrm2 = k > 0 ? wave_reduce_partials(pv, nb, 2 * s, c) : 1.0;
-  const double d2 = k > 0 ? wave_reduce_partials(pv, nb, 2 * s, s + c) : 0.0;
-  if ((threadIdx.x & 63) != 0) return;
+  // one workgroup per column c: thread t sums blocks b = t, t + 256, ... of the three
+  // partial arrays (their loads in flight together, eight blocks at a time), then the
+  // four waves' sums combine in a fixed order (the round-3 form, one wave per column
+  // and one array after the other, took ~44 us at 4096 blocks)
+  const int c = blockIdx.x, t = threadIdx.x;
+  __shared__ double red[3][4];
+  const bool has1 = k < steps, has2 = k > 0;
+  double a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  int b = t;
+  for (; b + 7 * 256 < nb; b += 8 * 256) {
+    double x1[8], x2[8], x3[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int64_t bq = b + q * 256;
+      x1[q] = has1 ? pq[bq * s + c] : 0.0;
+      x2[q] = has2 ? pv[bq * 2 * s + c] : 0.0;
+      x3[q] = has2 ? pv[bq * 2 * s + s + c] : 0.0;
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      a1 += x1[q];
+      a2 += x2[q];
+      a3 += x3[q];
+    }
+  }
+  for (; b < nb; b += 256) {
+    if (has1) a1 += pq[(int64_t)b * s + c];
+    if (has2) {
+      a2 += pv[(int64_t)b * 2 * s + c];
+      a3 += pv[(int64_t)b * 2 * s + s + c];
+    }
+  }
+  a1 = wave_sum(a1);
+  a2 = wave_sum(a2);
+  a3 = wave_sum(a3);
+  const int w = t >> 6;
+  if ((t & 63) == 0) {
+    red[0][w] = a1;
+    red[1][w] = a2;
+    red[2][w] = a3;
+  }
+  __syncthreads();
+  if (t != 0) return;
+  const double d1 = has1 ? (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]) : 0.0;
+  const double nrm2 = has2 ? (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]) : 1.0;
+  const double d2 = has2 ? (red[2][0] + red[2][1]) + (red[2][2] + red[2][3]) : 0.0;
   double gam = 1.0, gamp = 1.0;
   if (k == 0) {
     dead[c] = 0;
@@ -1177,24 +1282,29 @@ __global__ __launch_bounds__(256) void ms_rmfma_kernel(const double* __restrict_
   const double a = on ? sa[c] : 0.0;
   d4 acc = {0.0, 0.0, 0.0, 0.0};
   double rr = 0.0;
-  // rows in groups of 16 per block iteration (4 waves x 4 rows), two groups per
-  // trip so that six loads per lane are in flight
+  // rows in groups of 16 per block iteration (4 waves x 4 rows), RG groups per trip
+  // so that 3 RG loads per lane are in flight (two groups, six loads: cfg 4 8.0 us)
   // (the trip condition is wave-uniform: every lane issues every MFMA)
+  constexpr int RG = 4;
   const int64_t stride = (int64_t)gridDim.x * 16;
-  for (int64_t base = (int64_t)blockIdx.x * 16 + wv * 4; base < n; base += 2 * stride) {
-    const int64_t i0 = base + rq, i1 = base + stride + rq;
-    const bool v0 = on && i0 < n, v1 = on && i1 < n;
-    const bool w0 = onb && i0 < n, w1 = onb && i1 < n;
-    const int64_t e0 = i0 * s + c, e1 = i1 * s + c;
-    const double b0 = w0 ? B[i0 * nb + c] : 0.0, r0 = v0 ? R[e0] : 0.0, q0 = v0 ? Q[e0] : 0.0;
-    const double b1 = w1 ? B[i1 * nb + c] : 0.0, r1 = v1 ? R[e1] : 0.0, q1 = v1 ? Q[e1] : 0.0;
-    const double n0 = r0 - a * q0, n1 = r1 - a * q1;
-    if (v0) R[e0] = n0;
-    if (v1) R[e1] = n1;
-    rr += n0 * n0;
-    rr += n1 * n1;
-    acc = mfma64(b0, n0, acc);
-    acc = mfma64(b1, n1, acc);
+  for (int64_t base = (int64_t)blockIdx.x * 16 + wv * 4; base < n; base += RG * stride) {
+    double bv[RG], rv[RG], qv[RG];
+#pragma unroll
+    for (int u = 0; u < RG; ++u) {
+      const int64_t i = base + u * stride + rq;
+      const bool v = on && i < n, w = onb && i < n;
+      bv[u] = w ? B[i * nb + c] : 0.0;
+      rv[u] = v ? R[i * s + c] : 0.0;
+      qv[u] = v ? Q[i * s + c] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < RG; ++u) {
+      const int64_t i = base + u * stride + rq;
+      const double nr = rv[u] - a * qv[u];
+      if (on && i < n) R[i * s + c] = nr;
+      rr += nr * nr;
+      acc = mfma64(bv[u], nr, acc);
+    }
   }
   // C map: row (c') = rq + 4 k, column (c) = lane & 15
 #pragma unroll

@@ -62,6 +62,11 @@ __global__ void col_gs_update_kernel(double*, const double*, int64_t, const doub
                                      int);
 __global__ void col_axpby_kernel(const double*, double*, const double*, const double*, int64_t,
                                  int);
+__global__ void cg_xr_kernel(const double*, const double*, double*, double*, const double*,
+                             const double*, const int*, int64_t, int, int*);
+__global__ void cg_p_kernel(const double*, double*, const double*, const double*, const int*, int*,
+                            const double*, int, int*, int64_t, int);
+__global__ void cg_init_kernel(const double*, double, int, double*, int*, int*, int*);
 template <bool NT>
 __global__ void lz_dots_kernel(const double*, int64_t, int, int, const double*, const double*,
                                int64_t, int, int, double*);
@@ -545,7 +550,7 @@ int lanczos_block_plain(gpmi_sp* sp, double* U, double* Y, int s, int steps, dou
   SP_TRY(hipMemsetAsync(dbe, 0, sizeof(double) * s * steps, sp->stream));
   // u_{-1}: zero (its coefficient is 0 at k = 0; 0 * garbage could be NaN)
   SP_TRY(hipMemsetAsync(U + 2 * ns, 0, sizeof(double) * ns, sp->stream));
-  const unsigned sgrid = (unsigned)((s + 3) / 4);
+  const unsigned sgrid = (unsigned)s;   // lz0_alpha_kernel: one workgroup per column
   for (int k = 0; k < steps; ++k) {
     double* Uc = U + (int64_t)(k % 3) * ns;
     double* Un = U + (int64_t)((k + 1) % 3) * ns;
@@ -1155,73 +1160,74 @@ int gpmi_sp_cg(gpmi_sp* sp, double eta, const double* rhs, int64_t ld, int nrhs,
     double* Rr = X + ns;
     double* Pp = Rr + ns;
     double* Q = Pp + ns;
-    double* dots = sp->small;
-    double* ca = sp->small + 2 * MAXS;
-    double* cb = ca + MAXS;
+    // device scalars: pq, rr (double-buffered by iteration parity), thr = rtol ||b||,
+    // the active flags (double-buffered), the error flag and the iteration count
+    double* pq = sp->small;
+    double* rrb[2] = {sp->small + MAXS, sp->small + 2 * MAXS};
+    double* thr = sp->small + 3 * MAXS;
+    int* actb[2] = {reinterpret_cast<int*>(sp->small + 4 * MAXS),
+                    reinterpret_cast<int*>(sp->small + 5 * MAXS)};
+    int* err = reinterpret_cast<int*>(sp->small + 6 * MAXS);
+    int* iters = err + 1;
     std::vector<double> h((size_t)ns);
     for (int64_t i = 0; i < n; ++i)
       for (int c = 0; c < s; ++c) h[(size_t)i * s + c] = rhs[orig_row(sp, i) * ld + c0 + c];
     SP_TRY(hipMemcpyAsync(Rr, h.data(), sizeof(double) * ns, hipMemcpyHostToDevice, sp->stream));
     SP_TRY(hipMemcpyAsync(Pp, Rr, sizeof(double) * ns, hipMemcpyDeviceToDevice, sp->stream));
     SP_TRY(hipMemsetAsync(X, 0, sizeof(double) * ns, sp->stream));
-    std::vector<double> rr(s), bn(s), pq(s), rrn(s), ha(s), hb(s);
-    rc = col_dots(sp, Rr, 0, 1, Rr, s, dots);
+    rc = col_dots(sp, Rr, 0, 1, Rr, s, rrb[0]);
     if (rc) return rc;
-    SP_TRY(hipMemcpyAsync(rr.data(), dots, sizeof(double) * s, hipMemcpyDeviceToHost, sp->stream));
-    SP_TRY(hipStreamSynchronize(sp->stream));
-    for (int c = 0; c < s; ++c) bn[c] = std::sqrt(rr[c]);
-    std::vector<int> done(s, 0);
-    int it = 0;
-    for (; it < maxiter; ++it) {
-      bool all = true;
-      for (int c = 0; c < s; ++c) {
-        if (!(std::sqrt(rr[c]) > rtol * bn[c])) done[c] = 1;
-        all = all && done[c];
-      }
-      if (all) break;
+    hipLaunchKernelGGL(cg_init_kernel, dim3(1), dim3(64), 0, sp->stream, rrb[0], rtol, s, thr,
+                       actb[0], err, iters);
+    SP_LAUNCH("cg_init_kernel");
+    // The host reads the flags every CG_POLL iterations (one round trip each, not two per
+    // iteration): iterations queued after the last column stopped do no vector work.
+    constexpr int CG_POLL = 8;
+    std::vector<int> flags(MAXS + 2);
+    const unsigned grid = grid_ns(n, s);
+    for (int it = 0; it < maxiter; ++it) {
+      const int cur = it & 1;
       rc = spmm(sp, Pp, Q, s, eta);
       if (rc) return rc;
-      rc = col_dots(sp, Pp, 0, 1, Q, s, dots);
+      rc = col_dots(sp, Pp, 0, 1, Q, s, pq);
       if (rc) return rc;
-      SP_TRY(hipMemcpyAsync(pq.data(), dots, sizeof(double) * s, hipMemcpyDeviceToHost,
-                            sp->stream));
-      SP_TRY(hipStreamSynchronize(sp->stream));
-      for (int c = 0; c < s; ++c) {
-        if (!done[c] && !(pq[c] > 0.0))
+      hipLaunchKernelGGL(cg_xr_kernel, dim3(grid), dim3(256), 0, sp->stream, Pp, Q, X, Rr,
+                         rrb[cur], pq, actb[cur], n, s, err);   // x += a p, r -= a q
+      SP_LAUNCH("cg_xr_kernel");
+      rc = col_dots(sp, Rr, 0, 1, Rr, s, rrb[cur ^ 1]);
+      if (rc) return rc;
+      hipLaunchKernelGGL(cg_p_kernel, dim3(grid), dim3(256), 0, sp->stream, Rr, Pp, rrb[cur],
+                         rrb[cur ^ 1], actb[cur], actb[cur ^ 1], thr, it, iters, n, s);
+      SP_LAUNCH("cg_p_kernel");   // p = r + b p
+      if ((it + 1) % CG_POLL == 0 || it + 1 == maxiter) {
+        SP_TRY(hipMemcpyAsync(flags.data(), actb[cur ^ 1], sizeof(int) * s, hipMemcpyDeviceToHost,
+                              sp->stream));
+        SP_TRY(hipMemcpyAsync(flags.data() + MAXS, err, sizeof(int), hipMemcpyDeviceToHost,
+                              sp->stream));
+        SP_TRY(hipStreamSynchronize(sp->stream));
+        if (flags[MAXS])
           return set_error(1, "CG: p^T (K + eta I) p <= 0 (K + eta I is not positive definite)");
-        const double a = done[c] ? 0.0 : rr[c] / pq[c];
-        ha[c] = a;
-        hb[c] = 1.0;
+        bool any = false;
+        for (int c = 0; c < s; ++c) any = any || flags[c];
+        if (!any) break;
       }
-      SP_TRY(hipMemcpyAsync(ca, ha.data(), sizeof(double) * s, hipMemcpyHostToDevice, sp->stream));
-      SP_TRY(hipMemcpyAsync(cb, hb.data(), sizeof(double) * s, hipMemcpyHostToDevice, sp->stream));
-      hipLaunchKernelGGL(col_axpby_kernel, dim3(grid_ns(n, s)), dim3(256), 0, sp->stream, Pp, X, ca,
-                         cb, n, s);   // x += a p
-      SP_LAUNCH("col_axpby_kernel");
-      for (int c = 0; c < s; ++c) ha[c] = -ha[c];
-      SP_TRY(hipMemcpyAsync(ca, ha.data(), sizeof(double) * s, hipMemcpyHostToDevice, sp->stream));
-      hipLaunchKernelGGL(col_axpby_kernel, dim3(grid_ns(n, s)), dim3(256), 0, sp->stream, Q, Rr, ca,
-                         cb, n, s);   // r -= a q
-      SP_LAUNCH("col_axpby_kernel");
-      rc = col_dots(sp, Rr, 0, 1, Rr, s, dots);
-      if (rc) return rc;
-      SP_TRY(hipMemcpyAsync(rrn.data(), dots, sizeof(double) * s, hipMemcpyDeviceToHost,
-                            sp->stream));
-      SP_TRY(hipStreamSynchronize(sp->stream));
-      for (int c = 0; c < s; ++c) {
-        ha[c] = 1.0;
-        hb[c] = done[c] ? 1.0 : rrn[c] / rr[c];
-        if (!done[c]) rr[c] = rrn[c];
-      }
-      SP_TRY(hipMemcpyAsync(ca, ha.data(), sizeof(double) * s, hipMemcpyHostToDevice, sp->stream));
-      SP_TRY(hipMemcpyAsync(cb, hb.data(), sizeof(double) * s, hipMemcpyHostToDevice, sp->stream));
-      hipLaunchKernelGGL(col_axpby_kernel, dim3(grid_ns(n, s)), dim3(256), 0, sp->stream, Rr, Pp, ca,
-                         cb, n, s);   // p = r + b p
-      SP_LAUNCH("col_axpby_kernel");
     }
-    max_it_used = std::max(max_it_used, it);
+    // the residual norms after the last iteration that ran sit in rrb[it_used & 1] (rrb[0]
+    // when none ran); the no-op iterations queued after it rewrite the same values
+    std::vector<double> rr(s), bnt(s);
+    SP_TRY(hipMemcpyAsync(flags.data() + MAXS, err, sizeof(int) * 2, hipMemcpyDeviceToHost,
+                          sp->stream));
+    SP_TRY(hipStreamSynchronize(sp->stream));
+    if (flags[MAXS])
+      return set_error(1, "CG: p^T (K + eta I) p <= 0 (K + eta I is not positive definite)");
+    const int it_used = flags[MAXS + 1];
+    max_it_used = std::max(max_it_used, it_used);
+    SP_TRY(hipMemcpyAsync(bnt.data(), thr, sizeof(double) * s, hipMemcpyDeviceToHost, sp->stream));
+    SP_TRY(hipMemcpyAsync(rr.data(), rrb[it_used & 1], sizeof(double) * s, hipMemcpyDeviceToHost,
+                          sp->stream));
+    SP_TRY(hipStreamSynchronize(sp->stream));
     for (int c = 0; c < s; ++c)
-      if (!(std::sqrt(rr[c]) <= rtol * bn[c])) converged = false;
+      if (!(std::sqrt(rr[c]) <= bnt[c])) converged = false;
     SP_TRY(hipMemcpyAsync(h.data(), X, sizeof(double) * ns, hipMemcpyDeviceToHost, sp->stream));
     SP_TRY(hipStreamSynchronize(sp->stream));
     for (int64_t i = 0; i < n; ++i)

@@ -76,6 +76,53 @@ def test_spmm_and_cg(gp):
     numpy.testing.assert_allclose(Y, scipy.sparse.linalg.spsolve(A, X), rtol=1e-8, atol=1e-9)
 
 
+def _host_cg_iterations(A, B, rtol):
+    """Iterations of the per-column CG gpmi_sp_cg runs (a column stops once
+    ||r|| <= rtol ||b||; the count is the last iteration any column ran)."""
+    its = 0
+    for c in range(B.shape[1]):
+        b = B[:, c]
+        x = numpy.zeros_like(b)
+        r = b.copy()
+        p = r.copy()
+        rr = r @ r
+        k = 0
+        while numpy.sqrt(rr) > rtol * numpy.linalg.norm(b):
+            q = A @ p
+            a = rr / (p @ q)
+            x += a * p
+            r -= a * q
+            rrn = r @ r
+            p = r + (rrn / rr) * p
+            rr = rrn
+            k += 1
+        its = max(its, k)
+    return its
+
+
+def test_cg_device_scalars(gp):
+    """gpmi_sp_cg keeps its scalars on the device (the host polls every 8
+    iterations): the iteration count equals a host CG's (+-1 for rounding at the
+    threshold), a zero right-hand side stays zero without stopping the others,
+    and a run that stops between polls returns the converged iterate."""
+    from gaussian_proc import _hip
+    _, K = _small_sparse()
+    sop = _hip.SparseOperator.from_csr(K)
+    n = K.shape[0]
+    eta = 3.0
+    A = (K + eta * scipy.sparse.eye(n)).tocsr()
+    B = numpy.random.RandomState(5).randn(n, 4)
+    B[:, 2] = 0.0
+    for rtol in (1e-4, 1e-10):
+        Y = sop.cg(eta, B, rtol=rtol)
+        ex = scipy.sparse.linalg.spsolve(A.tocsc(), B)
+        assert numpy.all(Y[:, 2] == 0.0)
+        assert _nrel(Y, ex) < 50 * rtol
+        assert abs(sop.last_cg_iterations - _host_cg_iterations(A, B, rtol)) <= 1
+    Y = sop.cg(eta, B[:, 2], rtol=1e-8)
+    assert numpy.all(Y == 0.0) and sop.last_cg_iterations == 0
+
+
 def test_window_spmm_equals_gather_spmm(gp, monkeypatch):
     """The X-window SpMM (64-row blocks, window rows staged in LDS; the default
     where its blocks fit 32 KB of LDS, e.g. 2D tapered Matern) against the
@@ -706,3 +753,35 @@ def test_sparse_3d_exact_logdet_vs_reference(gp):
     for e, ld_se, lp_ref in zip(etas, se, meta['direct_lp']):
         lp = DirectLikelihood.log_likelihood(z, X, op, False, [1.0, numpy.sqrt(e)])
         assert abs(lp - lp_ref) <= 0.5 * 3.0 * ld_se + 1e-6 * abs(lp_ref), (e, lp, lp_ref)
+
+
+@pytest.mark.parametrize('world', [2, 4, 8])
+def test_rank_shards_equal_one_device(gp, world):
+    """The bench's sparse shards at N ranks, run one after another on one device:
+    every rank's probe block of the Lanczos (counter-based probes at its offset,
+    imate's plain recurrence and DCGS2) and right-hand-side column block of the
+    multi-shift CG (gpmi_sp_msgram_cols; 1-3 columns at N = 8) together equal the
+    single-device results to 1e-9 (other block widths take other SpMM kernels)."""
+    from gaussian_proc import _hip
+    from gaussian_proc.sweep import shard
+    _, K = _small_sparse()
+    n = K.shape[0]
+    sop = _hip.SparseOperator.from_csr(K)
+    nprobe, steps, seed = 20, 12, 3
+    for orth in (0, -1):
+        a, b = sop.lanczos(nprobe, steps, seed, orthogonalize=orth)
+        for r in range(world):
+            lo, hi, _ = shard(nprobe, world, r)
+            if hi > lo:
+                ar, br = sop.lanczos(hi - lo, steps, seed, probe_offset=lo, orthogonalize=orth)
+                # (other block widths run other SpMM kernels: rounding-level differences)
+                assert rel(ar, a[lo:hi]) < 1e-9 and rel(br, b[lo:hi]) < 1e-9, (world, r, orth)
+    rng = numpy.random.RandomState(world)
+    B = rng.randn(n, 7)
+    etas = numpy.array([2.5, 4.0, 10.0])
+    G = sop.msgram(etas, B, rtol=1e-10)
+    for r in range(world):
+        lo, hi, _ = shard(7, world, r)
+        if hi > lo:
+            Gc = sop.msgram(etas, B, rtol=1e-10, cols=(lo, hi))
+            assert _nrel(Gc, G[:, :, lo:hi]) < 1e-9, (world, r)
