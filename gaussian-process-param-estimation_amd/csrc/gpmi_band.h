@@ -17,15 +17,25 @@ constexpr int HH_PANEL_LDS = 96 * 1024;  // dynamic LDS: one hh_panel workgroup 
 constexpr int HH_PART_LD = 136;    // partial record: S_j (j < 128), sum x^2 at [128]
 constexpr int QT_ROWS = 64;        // rows per qt_partial / qt_apply workgroup
 constexpr int TN_CH = 128;         // rows per tn_partial chunk
-#ifndef GPMI_SYMM_DIV
-#define GPMI_SYMM_DIV 1024
-#endif
 constexpr int SY_CH = 16;          // tile columns per symm split-K chunk (at most)
-// symm split-K chunk for an mt-tile trailing block: SY_CH tile columns, fewer
-// when mt is small so that mt x chunks still gives ~2 workgroups per CU
-inline int symm_chunk(int mt) {
-  int ch = mt * mt / GPMI_SYMM_DIV;
-  return ch < 1 ? 1 : (ch > SY_CH ? SY_CH : ch);
+// symm split-K chunk for an mt-tile trailing block on `slots` resident workgroups (two
+// per CU): the mt x ceil(mt / chunk) workgroups run in ceil(W / slots) rounds of chunk
+// 128^3 products each, so the chunk minimising rounds x chunk (+ the partial sums'
+// reads, ~1/620 of a product each) ends the grid in full rounds: at mt = 117, chunk 9
+// (1521 workgroups, 2.97 rounds of 512) instead of mt^2 / 1024 = 13 (1053, 2.06 rounds
+// run as 3: the third nearly empty, 1.06 ms against ~0.73).
+inline int symm_chunk(int mt, int slots) {
+  int best = 1;
+  long long bc = -1;
+  for (int ch = 1; ch <= SY_CH; ++ch) {
+    const long long w = (long long)mt * ((mt + ch - 1) / ch);
+    const long long c = (w + slots - 1) / slots * ch * 620 + w;
+    if (bc < 0 || c <= bc) {
+      bc = c;
+      best = ch;
+    }
+  }
+  return best;
 }
 constexpr int BAND_ULD = 384;      // U = [W | V | W]
 constexpr int BAND_MAX_NPAD = HH_MAXG * HH_ROWS;
@@ -37,9 +47,10 @@ __global__ void hh_panel_kernel(double* P, int64_t lda, int m, double* part, dou
                                 const int* guard);
 __global__ void vcopy_kernel(const double* P, int64_t lda, int m, double* U, int64_t ldu);
 __global__ void tn_partial_kernel(const double* P1, int64_t ld1, const double* P2, int64_t ld2,
-                                  int m, double* part);
-__global__ void tn_reduce_kernel(const double* part, int nch, double* out, double scale);
-__global__ void tbuild_kernel(const double* VtV, const double* tau, double* T);
+                                  int m, double* part, const int* only_if);
+__global__ void tn_reduce_kernel(const double* part, int nch, double* out, double scale,
+                                 const int* only_if);
+__global__ void tbuild_kernel(const double* VtV, const double* tau, double* T, const int* only_if);
 __global__ void symm_kernel(const double* A, int64_t lda, const double* U, int64_t ldu, int tr0,
                             int mt, int chunk, double* Xp);
 __global__ void psum_kernel(const double* Xp, int nch, double* X);
@@ -95,7 +106,9 @@ __global__ void cq_apply_kernel(const double* Src, int64_t lds, double* Dst, int
                                 const double* M, double* part, const int* skip);
 __global__ void cq_recon_kernel(const double* Q2, const double* G3, double tau_fo, double* P,
                                 int64_t lda, double* S, double* tau, double* Lx3, double* Linv3,
-                                double* C, int* fo, int* fail);
+                                double* C, int* fo, int* fail, double* US);
+__global__ void cq_t_kernel(const double* P, int64_t lda, const double* US, double* W, double* T,
+                            const int* fail);
 constexpr int CQ_DYN_LDS = 64 * (GPMI_TS + 4) * 8;   // cq_gram / cq_apply dynamic LDS (bytes)
 __global__ void cq_top_kernel(double* Lx, const double* Linv, const int* flags, const double* S,
                               double* scr, double* Ab, int64_t lda);

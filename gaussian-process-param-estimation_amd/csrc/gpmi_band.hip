@@ -366,8 +366,10 @@ __global__ __launch_bounds__(256, 2) void tn_partial_kernel(const double* __rest
                                                             int64_t ld1,
                                                             const double* __restrict__ P2,
                                                             int64_t ld2, int m,
-                                                            double* __restrict__ part) {
+                                                            double* __restrict__ part,
+                                                            const int* __restrict__ only_if) {
   __shared__ double smem[4 * GSTAGE];
+  if (only_if && *only_if == 0) return;
   const int ch = blockIdx.x;
   const int i0 = ch * TN_CH, kd = min(TN_CH, m - i0);
   d4 acc[4][4];
@@ -381,8 +383,10 @@ __global__ __launch_bounds__(256, 2) void tn_partial_kernel(const double* __rest
 // workgroup, each summed by its four waves over ch = w (mod 4) (eight loads in
 // flight per lane), the four sums combined in a fixed order.
 __global__ __launch_bounds__(256) void tn_reduce_kernel(const double* __restrict__ part, int nch,
-                                                        double* __restrict__ out, double scale) {
+                                                        double* __restrict__ out, double scale,
+                                                        const int* __restrict__ only_if) {
   __shared__ double red[4][64];
+  if (only_if && *only_if == 0) return;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int e = blockIdx.x * 64 + lane;
   double acc[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
@@ -408,10 +412,12 @@ __global__ __launch_bounds__(256) void tn_reduce_kernel(const double* __restrict
 // (tau_c = 0) is decoupled: unit diagonal, no coupling, and T_cc = 0.
 __global__ __launch_bounds__(256) void tbuild_kernel(const double* __restrict__ VtV,
                                                      const double* __restrict__ tau,
-                                                     double* __restrict__ T) {
+                                                     double* __restrict__ T,
+                                                     const int* __restrict__ only_if) {
   __shared__ double Ls[TS * DL];
   __shared__ double Aux[TS * RLD];
   __shared__ double stau[TS];
+  if (only_if && *only_if == 0) return;
   const int t = threadIdx.x;
   if (t < TS) stau[t] = tau[t];
   __syncthreads();

@@ -115,6 +115,7 @@ struct gpmi_band {
   int cq_fallbacks = 0;      // reductions redone with Householder panels
   int la_free = 32;          // CUs the pipelined look-ahead SYR2K leaves to the chain
                              // (GPMI_BAND_LA_FREE; < 0: the capped two-per-CU SYR2K below)
+  bool cq_t = true;          // T of CholeskyQR panels by cq_t_kernel (GPMI_BAND_CQT=0: tbuild)
   int cq_la_grid = 448;      // SYR2K grid cap beside a CholeskyQR panel (0: none; measured
                              // at N = 16384: 448 161-163 ms, none 165-168, no look-ahead 164-166)
   double* Qb = nullptr;
@@ -156,6 +157,14 @@ struct gpmi_band {
   int* bcrFail = nullptr;    // [bcap][nt]
   double* bcrF0 = nullptr;   // [nt - 1][128][128]
   double* cqMinv = nullptr;  // C = U^-T M3 of the current panel
+  // T of a CholeskyQR panel from its reconstruction (cq_t_kernel) on a stream of its
+  // own: U S and V1^-1 per panel; t_from_q[j]: panel j's T comes from there (the
+  // side stream's V^T V / tbuild_kernel then run only if the panel fell back)
+  double* cqUS = nullptr;    // [nt][128][128]
+  double* cqW = nullptr;     // [nt][128][128]
+  hipStream_t s_t = nullptr;
+  hipEvent_t ev_rc = nullptr, ev_t2 = nullptr;
+  std::vector<char> t_from_q;
   double cq_fo[3] = {0.0, 1e-4, 3e-8};   // first-order thresholds on ||G - I||_F
   int cap = 0;
   int nrhs = 0;
@@ -187,7 +196,7 @@ int band_free(gpmi_band* b) {
   double* bufs[] = {b->Ab, b->U, b->X, b->Xp, b->part, b->pivrow, b->tau, b->Tm, b->tnp, b->tnp2,
                     b->VtV, b->M, b->Zh, b->Y, b->qtp, b->qa, b->qb, b->etas, b->out, b->Ac, b->td,
                     b->fac, b->ysol, b->der, b->Qb, b->cqpart, b->cqG, b->cqL, b->cqLinv,
-                    b->cqMinv, b->cqS, b->cqscr,
+                    b->cqMinv, b->cqS, b->cqscr, b->cqUS, b->cqW,
                     b->bcrD[0], b->bcrD[1], b->bcrF[0], b->bcrF[1], b->bcrY[0], b->bcrY[1],
                     b->bcrL, b->bcrW, b->bcrZ, b->bcrG, b->bcrLd, b->bcrF0, b->bcrX,
                     b->bcrZp, b->bcrG2, b->bcrG3};
@@ -205,7 +214,8 @@ int band_free(gpmi_band* b) {
   if (b->stream) (void)hipStreamDestroy(b->stream);
   if (b->side) (void)hipStreamDestroy(b->side);
   if (b->s_pan) (void)hipStreamDestroy(b->s_pan);
-  for (hipEvent_t e : {b->ev_col, b->ev_pan})
+  if (b->s_t) (void)hipStreamDestroy(b->s_t);
+  for (hipEvent_t e : {b->ev_col, b->ev_pan, b->ev_rc, b->ev_t2})
     if (e) (void)hipEventDestroy(e);
   if (b->ev_q) (void)hipEventDestroy(b->ev_q);
   if (b->ev_v) (void)hipEventDestroy(b->ev_v);
@@ -321,8 +331,19 @@ int cq_panel(gpmi_band* b, int j, hipStream_t st, bool guard = true) {
   hipLaunchKernelGGL(cq_recon_kernel, dim3(1), dim3(256), 0, st, b->Qb, b->cqG, b->cq_fo[2], P,
                      np, b->cqS + (int64_t)j * TS, b->tau + (int64_t)j * TS,
                      b->cqL + pt + 2 * TS * TS, b->cqLinv + pt + 2 * TS * TS, b->cqMinv, fl,
-                     fl + 4);
+                     fl + 4, b->s_t ? b->cqUS + (int64_t)j * TS * TS : nullptr);
   BD_LAUNCH("cq_recon_kernel");
+  if (b->s_t) {
+    // T = -U S V1^-T beside the rest of the chain (exits when the panel failed)
+    BD_TRY(hipEventRecord(b->ev_rc, st));
+    BD_TRY(hipStreamWaitEvent(b->s_t, b->ev_rc, 0));
+    hipLaunchKernelGGL(cq_t_kernel, dim3(1), dim3(256), 0, b->s_t, P, np,
+                       b->cqUS + (int64_t)j * TS * TS, b->cqW + (int64_t)j * TS * TS,
+                       b->Tm + (int64_t)j * TS * TS, fl + 4);
+    BD_LAUNCH("cq_t_kernel");
+    BD_TRY(hipEventRecord(b->ev_t2, b->s_t));
+    b->t_from_q[j] = 1;
+  }
   // V2 = Q2 C^T below the top block
   if (mt > 1) {
     hipLaunchKernelGGL(cq_apply_kernel, dim3(rt - 2), dim3(256), CQ_DYN_LDS, st, b->Qb + TS * TS,
@@ -425,6 +446,7 @@ int band_reduce_pass(gpmi_band* b, const double* K, const std::vector<double>* y
                           b->side));
   }
   BD_TRY(hipMemcpyAsync(b->Ab, K, sizeof(double) * np * np, hipMemcpyDeviceToDevice, s));
+  std::fill(b->t_from_q.begin(), b->t_from_q.end(), 0);
   const bool la = mode != 2 && b->lookahead && b->s_pan;
   bool ahead = false;   // panel j already factored by the previous look-ahead
   for (int j = 0; j + 1 < nt; ++j) {
@@ -446,14 +468,18 @@ int band_reduce_pass(gpmi_band* b, const double* K, const std::vector<double>* y
     // T from V^T V on the side stream, beside the SYMM (which needs only V)
     BD_TRY(hipEventRecord(b->ev_v, s));
     BD_TRY(hipStreamWaitEvent(b->side, b->ev_v, 0));
+    // (a CholeskyQR panel's T comes from cq_t_kernel: these run only if it fell back)
+    const int* only_if = b->t_from_q[j] ? b->cqflag + 8 * j + 4 : nullptr;
     hipLaunchKernelGGL(tn_partial_kernel, dim3(nch), dim3(256), 0, b->side, Ur + TS,
-                       (int64_t)BAND_ULD, Ur + TS, (int64_t)BAND_ULD, m, b->tnp2);
+                       (int64_t)BAND_ULD, Ur + TS, (int64_t)BAND_ULD, m, b->tnp2, only_if);
     BD_LAUNCH("tn_partial_kernel");
     hipLaunchKernelGGL(tn_reduce_kernel, dim3(TS * TS / 64), dim3(256), 0, b->side, b->tnp2,
-                       nch, b->VtV, 1.0);
+                       nch, b->VtV, 1.0, only_if);
     BD_LAUNCH("tn_reduce_kernel");
-    hipLaunchKernelGGL(tbuild_kernel, dim3(1), dim3(256), 0, b->side, b->VtV, tau, T);
+    hipLaunchKernelGGL(tbuild_kernel, dim3(1), dim3(256), 0, b->side, b->VtV, tau, T, only_if);
     BD_LAUNCH("tbuild_kernel");
+    if (b->t_from_q[j]) BD_TRY(hipStreamWaitEvent(b->side, b->ev_t2, 0));
+    b->t_from_q[j] = 0;
     BD_TRY(hipEventRecord(b->ev_t, b->side));
     if (yh) {
       // Q_j^T on the side stream right after T_j (a stream of its own measured the
@@ -461,7 +487,7 @@ int band_reduce_pass(gpmi_band* b, const double* K, const std::vector<double>* y
       int rc = qt_panel(b, j, b->side);
       if (rc) return rc;
     }
-    const int chunk = symm_chunk(mt);
+    const int chunk = symm_chunk(mt, 2 * b->ncu);
     const int sch = (mt + chunk - 1) / chunk;
     hipLaunchKernelGGL(symm_kernel, dim3(mt, sch), dim3(256), 0, s, b->Ab, np, b->U,
                        (int64_t)BAND_ULD, j + 1, mt, chunk, b->Xp);
@@ -472,10 +498,10 @@ int band_reduce_pass(gpmi_band* b, const double* K, const std::vector<double>* y
     hipLaunchKernelGGL(xt_kernel, dim3(mt), dim3(256), 0, s, b->X, T);
     BD_LAUNCH("xt_kernel");
     hipLaunchKernelGGL(tn_partial_kernel, dim3(nch), dim3(256), 0, s, Ur + TS,
-                       (int64_t)BAND_ULD, b->X, (int64_t)TS, m, b->tnp);
+                       (int64_t)BAND_ULD, b->X, (int64_t)TS, m, b->tnp, nullptr);
     BD_LAUNCH("tn_partial_kernel");
     hipLaunchKernelGGL(tn_reduce_kernel, dim3(TS * TS / 64), dim3(256), 0, s, b->tnp, nch, b->M,
-                       1.0);
+                       1.0, nullptr);
     BD_LAUNCH("tn_reduce_kernel");
     hipLaunchKernelGGL(z_kernel, dim3(1), dim3(256), 0, s, T, b->M, b->Zh);
     BD_LAUNCH("z_kernel");
@@ -619,9 +645,13 @@ int gpmi_band_create(gpmi_op* op, gpmi_band** out) {
   b->nt = (int)(v.n_pad / TS);
   const int64_t np = b->n_pad;
   const int nt = b->nt;
+  int ncu_alloc = 0;   // (b->ncu is read below; the Xp size needs it here)
+  if (hipDeviceGetAttribute(&ncu_alloc, hipDeviceAttributeMultiprocessorCount, v.device) !=
+      hipSuccess)
+    ncu_alloc = 256;
   int64_t xp_tiles = 1;   // the largest mt x split-K chunks over the panels
   for (int mt = 1; mt < nt; ++mt) {
-    const int ch = symm_chunk(mt);
+    const int ch = symm_chunk(mt, 2 * ncu_alloc);
     xp_tiles = std::max<int64_t>(xp_tiles, (int64_t)mt * ((mt + ch - 1) / ch));
   }
   const int nch = (int)std::max<int64_t>(1, (np + TN_CH - 1) / TN_CH);
@@ -640,6 +670,7 @@ int gpmi_band_create(gpmi_op* op, gpmi_band** out) {
     return fail(e, "side stream");
   if (const char* la = std::getenv("GPMI_BAND_LA")) b->lookahead = std::atoi(la);
   if (const char* lf = std::getenv("GPMI_BAND_LA_FREE")) b->la_free = std::atoi(lf);
+  if (const char* ct = std::getenv("GPMI_BAND_CQT")) b->cq_t = std::atoi(ct) != 0;
   if (const char* pm = std::getenv("GPMI_BAND_PANEL")) b->panel_mode = std::strcmp(pm, "hh") == 0;
   if (const char* bm = std::getenv("GPMI_BAND_BCR")) b->bcr_mode = std::max(0, std::min(2, std::atoi(bm)));
   // GPMI_CQ_FO=0: every CholeskyQR pass by an exact Cholesky (no first-order passes)
@@ -689,6 +720,18 @@ int gpmi_band_create(gpmi_op* op, gpmi_band** out) {
   BALLOC(cqL, (size_t)nt * 3 * TS * TS);
   BALLOC(cqLinv, (size_t)nt * 3 * TS * TS);
   BALLOC(cqMinv, TS * TS);
+  if (b->cq_t) {
+    BALLOC(cqUS, (int64_t)nt * TS * TS);
+    BALLOC(cqW, (int64_t)nt * TS * TS);
+    int lo = 0, hi = 0;
+    if ((e = hipDeviceGetStreamPriorityRange(&lo, &hi)) != hipSuccess) return fail(e, "prio");
+    if ((e = hipStreamCreateWithPriority(&b->s_t, hipStreamNonBlocking, hi)) != hipSuccess)
+      return fail(e, "T stream");
+    for (hipEvent_t* ev : {&b->ev_rc, &b->ev_t2})
+      if ((e = hipEventCreateWithFlags(ev, hipEventDisableTiming)) != hipSuccess)
+        return fail(e, "event");
+  }
+  b->t_from_q.assign((size_t)nt, 0);
   BALLOC(cqS, (size_t)nt * TS);
   BALLOC(cqscr, (size_t)nt * TS * TS);
 #undef BALLOC

@@ -362,7 +362,8 @@ __global__ __launch_bounds__(256) void cq_recon_kernel(const double* __restrict_
                                                        double* __restrict__ Linv3,
                                                        double* __restrict__ C,
                                                        int* __restrict__ fo,
-                                                       int* __restrict__ fail) {
+                                                       int* __restrict__ fail,
+                                                       double* __restrict__ US) {
   __shared__ double A[TS * DL];
   __shared__ double Aux[TS * RLD];
   __shared__ double sS[TS];
@@ -548,6 +549,7 @@ __global__ __launch_bounds__(256) void cq_recon_kernel(const double* __restrict_
   for (int e = t; e < TS * TS; e += 256) {
     const int r = e >> 7, c = e & 127;
     if (c < r) P[(int64_t)r * lda + c] = A[r * DL + c];
+    if (US) US[e] = c >= r ? A[r * DL + c] * sS[c] : 0.0;   // U S, for cq_t_kernel
   }
   if (t < TS) {
     S[t] = sS[t];
@@ -604,6 +606,46 @@ __global__ __launch_bounds__(256) void cq_recon_kernel(const double* __restrict_
            cs[1] - cs[0], cs[2] - cs[1], cs[3] - cs[2], cs[4] - cs[3], cs[5] - cs[4],
            cs[6] - cs[5], cs[7] - cs[6]);
 #endif
+}
+
+// The panel's compact-WY T straight from the reconstruction (one workgroup, on a
+// stream of its own beside the rest of the chain): from (I - V T V^T) [S; 0] = Q and
+// Q - [S; 0] = V U, U = -T V1^T S, so T = -U S V1^-T (V1 the unit lower top block of
+// V, S = diag(+-1)). It replaces the V^T V pass and the inverse of tbuild_kernel,
+// which had to wait for the whole V (vcopy) and, for the last panels, delayed the
+// X T product. A failed panel (the Householder fallback owns it) is left to
+// tbuild_kernel. V1^-1 by the LDS triangular inverse, written to W; then
+// T = -(U S) (V1^-1)^T as one 128^3 MFMA tile product (upper x upper: the zeros
+// below the diagonal come out exactly).
+__global__ __launch_bounds__(256) void cq_t_kernel(const double* __restrict__ P, int64_t lda,
+                                                   const double* __restrict__ US,
+                                                   double* __restrict__ W,
+                                                   double* __restrict__ T,
+                                                   const int* __restrict__ fail) {
+  __shared__ double buf[TS * DL + TS * RLD];
+  double* Ls = buf;
+  double* Aux = buf + TS * DL;
+  const int t = threadIdx.x;
+  if (__hip_atomic_load(fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+  for (int e = t; e < TS * TS; e += 256) {
+    const int r = e >> 7, c = e & 127;
+    Ls[r * DL + c] = c < r ? P[(int64_t)r * lda + c] : (c == r ? 1.0 : 0.0);
+  }
+  __syncthreads();
+  lds_diag_inv_lower(Ls, Aux);
+  __syncthreads();
+  lds_inv_block(Ls, Aux);
+  __syncthreads();
+  for (int e = t; e < TS * TS; e += 256) {
+    const int r = e >> 7, c = e & 127;
+    W[e] = c <= r ? Ls[r * DL + c] : 0.0;
+  }
+  __threadfence();
+  __syncthreads();   // W complete (the product reads it from L2); Ls free for the stages
+  d4 acc[4][4];
+  zero_tile(acc);
+  gemm_tile<KFAST, KFAST, true>(US, TS, W, TS, TS, buf, acc);
+  store_tile(T, TS, acc, 1.0);
 }
 
 // The top 128 x 128 block above the diagonal of every CholeskyQR panel, one

@@ -20,6 +20,8 @@
 #                (tools/band_refresh_probe.py 128 1)
 #   pmc-sparse4 / pmc-sparse5   FETCH / WRITE passes over one sparse step
 #   trace-sparse4 / trace-sparse5   kernel-trace stats of bench --config sparseN
+#   trace-band   kernel trace of two band reductions + the per-panel timeline
+#                (tools/band_timeline.py)
 #   host         the box's CPU / cgroup facts (host.txt)
 #   py:<file>    python -u <file> (a probe under tools/)
 set -o pipefail
@@ -90,6 +92,10 @@ for task in "$@"; do
       for c in FETCH_SIZE WRITE_SIZE; do
         run 200 $D/pmc_${cfg}_$c.log rocprofv3 --pmc $c --kernel-trace -d $D/pmc_${cfg}_$c -o run --output-format csv -- python3 bench.py --config $cfg --steps 1 --warmup 0 --no-cpu-baseline
       done ;;
+    trace-band)
+      run 300 $D/trace_band.err rocprofv3 --kernel-trace --stats -d $D/prof_band -o run --output-format csv -- python3 tools/band_refresh_probe.py 128 1
+      python tools/band_timeline.py $D/prof_band 10 60 110 > $D/band_timeline.txt
+      head -12 $D/band_timeline.txt ;;
     trace-sparse4|trace-sparse5)
       cfg=${task#trace-}
       run 400 $D/trace_$cfg.err rocprofv3 --kernel-trace --stats -d $D/prof_$cfg -o run --output-format csv -- python3 bench.py --config $cfg --steps 3 --warmup 1 --no-cpu-baseline --out-json $D/bench_under_rocprof_$cfg.json

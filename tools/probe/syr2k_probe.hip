@@ -6,6 +6,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <vector>
+#include <string>
 #include "gpmi_tile.h"
 
 using namespace gpmi;
@@ -285,6 +286,8 @@ int main(int argc, char** argv) {
   const int grids[] = {448, 512, 768, 1024, 100000};
   (void)0;
   const int kds[] = {256, 512};
+  const bool symm_only = argc > 2 && std::string(argv[2]) == "symm";
+  if (!symm_only)
   for (int kern : {0, 3, 4, 5})
     for (int mt : mts)
       for (int kd : kds)
@@ -317,12 +320,16 @@ int main(int argc, char** argv) {
         }
   {
     double* Xp;
-    CK(hipMalloc(&Xp, sizeof(double) * (size_t)nt * 16 * TS * TS));
-    for (int mt : {nt - 1, nt / 2})
-      for (int chunk : {4, 8, 16, 32})
+    CK(hipMalloc(&Xp, sizeof(double) * (size_t)nt * nt * TS * TS));
+    // "symm": the split-K chunk sweep at the band's mt values (the shipped kernel only)
+    std::vector<int> mtv = symm_only ? std::vector<int>{117, 97, 77, 57} : std::vector<int>{nt - 1, nt / 2};
+    std::vector<int> chv = symm_only ? std::vector<int>{4, 6, 8, 9, 10, 12, 13, 16} : std::vector<int>{4, 8, 16, 32};
+    for (int mt : mtv)
+      for (int chunk : chv)
         for (int af = 0; af < 2; ++af) {
           const int sch = (mt + chunk - 1) / chunk;
-          if (sch > 16) continue;
+          if (!symm_only && sch > 16) continue;
+          if (symm_only && af) continue;
           auto launch = [&]() {
             if (af) hipLaunchKernelGGL(symm_probe<true>, dim3(mt, sch), dim3(256), 0, 0, A, (int64_t)n, U, ldu, 1, mt, chunk, Xp);
             else hipLaunchKernelGGL(symm_probe<false>, dim3(mt, sch), dim3(256), 0, 0, A, (int64_t)n, U, ldu, 1, mt, chunk, Xp);
