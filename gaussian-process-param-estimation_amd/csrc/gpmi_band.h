@@ -38,6 +38,11 @@ inline int symm_chunk(int mt, int slots) {
   return best;
 }
 constexpr int BAND_ULD = 384;      // U = [W | V | W]
+// CUs the pipelined look-ahead SYR2K (one workgroup per CU) leaves to the next panel's
+// CholeskyQR chain, whose single-workgroup kernels need a whole CU (N = 16384:
+// 16 171 ms, 24-28 172-173, 32 153, 36 153, 40 154, 48 155, 64 158; the capped
+// two-per-CU SYR2K 160)
+constexpr int LA_FREE = 32;
 constexpr int BAND_MAX_NPAD = HH_MAXG * HH_ROWS;
 
 __global__ void hh_col_kernel(double* P, int64_t lda, int m, int c, double* part, double* pivrow,
@@ -54,11 +59,14 @@ __global__ void tbuild_kernel(const double* VtV, const double* tau, double* T, c
 __global__ void symm_kernel(const double* A, int64_t lda, const double* U, int64_t ldu, int tr0,
                             int mt, int chunk, double* Xp);
 __global__ void psum_kernel(const double* Xp, int nch, double* X);
-__global__ void xt_kernel(double* X, const double* T);
-__global__ void z_kernel(const double* T, const double* M, double* Zh);
-__global__ void w_kernel(const double* X, double* U, int64_t ldu, const double* Zh);
+__global__ void xt_q_kernel(const double* X, const double* T, double* X2);
+__global__ void tn_partial_q_kernel(const double* P1, int64_t ld1, const double* P2, int64_t ld2,
+                                    int m, double* part);
+__global__ void z_q_kernel(const double* T, const double* M, double* Zh);
+__global__ void w_q_kernel(const double* X, double* U, int64_t ldu, const double* Zh);
+__global__ void syr2k_col_q_kernel(double* A, int64_t lda, const double* U, int64_t ldu, int tr0);
 __global__ void syr2k_kernel(double* A, int64_t lda, const double* U, int64_t ldu, int tr0,
-                             int mt, int sub);
+                             int mt);
 __global__ void syr2k_rest_kernel(double* A, int64_t lda, const double* U, int64_t ldu, int tr0,
                                   int mt, const uint32_t* order);
 __global__ void syr2k_pipe_kernel(double* A, int64_t lda, const double* U, int64_t ldu, int tr0,

@@ -490,40 +490,78 @@ __global__ __launch_bounds__(256) void psum_kernel(const double* __restrict__ Xp
   *reinterpret_cast<d2*>(X + (int64_t)il * TS * TS + e) = s;
 }
 
-// X_I <- X_I T (in place; one tile row per workgroup).
-__global__ __launch_bounds__(256, 2) void xt_kernel(double* __restrict__ X,
-                                                    const double* __restrict__ T) {
+// The serial steps between the SYMM and the look-ahead on quadrant workgroups
+// (blockIdx.y = the 64 x 64 quadrant, gemm_quad): each is one 128^3 product per output
+// tile, whose MFMA chain bounds one workgroup (~14 us at the CU's fp64 rate plus the
+// staging); four workgroups per tile run a quarter of it each.
+// X2_I = X_I T (out of place: the quadrants of a row read all of X_I).
+__global__ __launch_bounds__(256, 2) void xt_q_kernel(const double* __restrict__ X,
+                                                      const double* __restrict__ T,
+                                                      double* __restrict__ X2) {
   __shared__ double smem[4 * GSTAGE];
-  double* Xi = X + (int64_t)blockIdx.x * TS * TS;
-  d4 acc[4][4];
-  zero_tile(acc);
-  gemm_tile<KFAST, KSLOW, false>(Xi, TS, T, TS, TS, smem, acc);
-  store_tile(Xi, TS, acc, 1.0);
+  const int q = blockIdx.y;
+  const int64_t off = (int64_t)blockIdx.x * TS * TS;
+  d4 acc[2][2];
+  zero_quad(acc);
+  gemm_quad<KFAST, KSLOW, false>(X + off, TS, T, TS, TS, smem, acc, q >> 1, q & 1);
+  store_quad(X2 + off, TS, acc, 1.0, q >> 1, q & 1);
 }
 
-// Zh = 1/2 T^T M (one workgroup).
-__global__ __launch_bounds__(256) void z_kernel(const double* __restrict__ T,
-                                                const double* __restrict__ M,
-                                                double* __restrict__ Zh) {
+// part[ch] = P1[rows]^T P2[rows] as tn_partial_kernel, one quadrant per workgroup.
+__global__ __launch_bounds__(256, 2) void tn_partial_q_kernel(const double* __restrict__ P1,
+                                                              int64_t ld1,
+                                                              const double* __restrict__ P2,
+                                                              int64_t ld2, int m,
+                                                              double* __restrict__ part) {
   __shared__ double smem[4 * GSTAGE];
-  d4 acc[4][4];
-  zero_tile(acc);
-  gemm_tile<KSLOW, KSLOW, false>(T, TS, M, TS, TS, smem, acc);
-  store_tile(Zh, TS, acc, 0.5);
+  const int ch = blockIdx.x, q = blockIdx.y;
+  const int i0 = ch * TN_CH, kd = min(TN_CH, m - i0);
+  d4 acc[2][2];
+  zero_quad(acc);
+  gemm_quad<KSLOW, KSLOW, false>(P1 + (int64_t)i0 * ld1, ld1, P2 + (int64_t)i0 * ld2, ld2, kd,
+                                 smem, acc, q >> 1, q & 1);
+  store_quad(part + (int64_t)ch * TS * TS, TS, acc, 1.0, q >> 1, q & 1);
 }
 
-// W_I = X_I - V_I Zh  ->  U[rows I][0:128] and U[rows I][256:384].
-__global__ __launch_bounds__(256, 2) void w_kernel(const double* __restrict__ X,
-                                                   double* __restrict__ U, int64_t ldu,
-                                                   const double* __restrict__ Zh) {
+// Zh = 1/2 T^T M (four workgroups).
+__global__ __launch_bounds__(256) void z_q_kernel(const double* __restrict__ T,
+                                                  const double* __restrict__ M,
+                                                  double* __restrict__ Zh) {
   __shared__ double smem[4 * GSTAGE];
-  const int il = blockIdx.x;
+  const int q = blockIdx.x;
+  d4 acc[2][2];
+  zero_quad(acc);
+  gemm_quad<KSLOW, KSLOW, false>(T, TS, M, TS, TS, smem, acc, q >> 1, q & 1);
+  store_quad(Zh, TS, acc, 0.5, q >> 1, q & 1);
+}
+
+// W_I = X_I - V_I Zh -> U[rows I][0:128] and U[rows I][256:384].
+__global__ __launch_bounds__(256, 2) void w_q_kernel(const double* __restrict__ X,
+                                                     double* __restrict__ U, int64_t ldu,
+                                                     const double* __restrict__ Zh) {
+  __shared__ double smem[4 * GSTAGE];
+  const int il = blockIdx.x, q = blockIdx.y;
   double* Ui = U + (int64_t)il * TS * ldu;
-  d4 acc[4][4];
-  load_tile(X + (int64_t)il * TS * TS, TS, acc);
-  gemm_tile<KFAST, KSLOW, true>(Ui + TS, ldu, Zh, TS, TS, smem, acc);
-  store_tile(Ui, ldu, acc, 1.0);
-  store_tile(Ui + 2 * TS, ldu, acc, 1.0);
+  d4 acc[2][2];
+  load_quad(X + (int64_t)il * TS * TS, TS, acc, q >> 1, q & 1);
+  gemm_quad<KFAST, KSLOW, true>(Ui + TS, ldu, Zh, TS, TS, smem, acc, q >> 1, q & 1);
+  store_quad(Ui, ldu, acc, 1.0, q >> 1, q & 1);
+  store_quad(Ui + 2 * TS, ldu, acc, 1.0, q >> 1, q & 1);
+}
+
+// Tile column 0 of the trailing update (the next panel's columns, look-ahead):
+// A_I0 -= [W_I V_I] [V_0 W_0]^T, one quadrant per workgroup.
+__global__ __launch_bounds__(256, 2) void syr2k_col_q_kernel(double* __restrict__ A, int64_t lda,
+                                                             const double* __restrict__ U,
+                                                             int64_t ldu, int tr0) {
+  __shared__ double smem[4 * GSTAGE];
+  const int I = tr0 + blockIdx.x, q = blockIdx.y;
+  double* C = A + (int64_t)I * TS * lda + (int64_t)tr0 * TS;
+  d4 acc[2][2];
+  load_quad(C, lda, acc, q >> 1, q & 1);
+  gemm_quad<KFAST, KFAST, true>(U + (int64_t)I * TS * ldu, ldu, U + (int64_t)tr0 * TS * ldu + TS,
+                                ldu, 2 * TS, smem, acc, q >> 1, q & 1);
+  store_quad(C, lda, acc, 1.0, q >> 1, q & 1);
 }
 
 // A_IJ -= [W_I V_I] [V_J W_J]^T on the lower tiles of the trailing mt x mt tiles.
@@ -538,14 +576,13 @@ __device__ __forceinline__ void syr2k_tile(double* __restrict__ A, int64_t lda,
   store_tile(C, lda, acc, 1.0);
 }
 
-// sub 0: every lower tile of the trailing mt x mt block (XCD-aware order);
-// sub 1: tile column 0 only (the next panel's columns, look-ahead).
+// Every lower tile of the trailing mt x mt block (XCD-aware order; no look-ahead).
 __global__ __launch_bounds__(256, 2) void syr2k_kernel(double* __restrict__ A, int64_t lda,
                                                        const double* __restrict__ U,
-                                                       int64_t ldu, int tr0, int mt, int sub) {
+                                                       int64_t ldu, int tr0, int mt) {
   __shared__ double smem[4 * GSTAGE];
-  int i = blockIdx.x, j = 0;
-  if (sub == 0) tri_decode(xcd_remap(blockIdx.x, gridDim.x), mt, &i, &j);
+  int i, j;
+  tri_decode(xcd_remap(blockIdx.x, gridDim.x), mt, &i, &j);
   syr2k_tile(A, lda, U, ldu, tr0 + i, tr0 + j, smem);
 }
 

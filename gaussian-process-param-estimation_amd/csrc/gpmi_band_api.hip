@@ -76,6 +76,7 @@ struct gpmi_band {
                              // tiles) + Householder vectors below the band
   double* U = nullptr;       // [n_pad][384] = [W | V | W] of the current panel
   double* X = nullptr;       // [n_pad][128] (rows relative to the panel's trailing block)
+  double* X2 = nullptr;      // [n_pad][128] X T (quadrant steps: out of place)
   double* Xp = nullptr;      // symm split-K partials
   double* part = nullptr;    // [2][HH_MAXG][HH_PART_LD] column partials
   double* pivrow = nullptr;  // [2][128]
@@ -85,7 +86,8 @@ struct gpmi_band {
   double* tnp2 = nullptr;    // tn partials of V^T V (side stream) [nch][128][128]
   hipStream_t side = nullptr;          // V^T V and T of a panel, beside its SYMM
   // look-ahead: the next panel's QR (high-priority stream) beside the rest of the
-  // SYR2K on a capped grid
+  // SYR2K: a CholeskyQR panel beside syr2k_pipe_kernel on all but LA_FREE CUs, a
+  // Householder panel beside syr2k_rest_kernel on la_grid workgroups
   int lookahead = 1, la_grid = 128, ncu = 256;
   hipStream_t s_pan = nullptr;
   hipEvent_t ev_col = nullptr, ev_pan = nullptr;
@@ -113,11 +115,6 @@ struct gpmi_band {
   // and inverses, the reconstruction's U^-T, V1, signs, scratch, failure flag
   int panel_mode = 0;        // 0 CholeskyQR, 1 Householder (single launch)
   int cq_fallbacks = 0;      // reductions redone with Householder panels
-  int la_free = 32;          // CUs the pipelined look-ahead SYR2K leaves to the chain
-                             // (GPMI_BAND_LA_FREE; < 0: the capped two-per-CU SYR2K below)
-  bool cq_t = true;          // T of CholeskyQR panels by cq_t_kernel (GPMI_BAND_CQT=0: tbuild)
-  int cq_la_grid = 448;      // SYR2K grid cap beside a CholeskyQR panel (0: none; measured
-                             // at N = 16384: 448 161-163 ms, none 165-168, no look-ahead 164-166)
   double* Qb = nullptr;
   double* cqpart = nullptr;
   double* cqG = nullptr;
@@ -193,7 +190,7 @@ struct gpmi_band {
 namespace {
 
 int band_free(gpmi_band* b) {
-  double* bufs[] = {b->Ab, b->U, b->X, b->Xp, b->part, b->pivrow, b->tau, b->Tm, b->tnp, b->tnp2,
+  double* bufs[] = {b->Ab, b->U, b->X, b->X2, b->Xp, b->part, b->pivrow, b->tau, b->Tm, b->tnp, b->tnp2,
                     b->VtV, b->M, b->Zh, b->Y, b->qtp, b->qa, b->qb, b->etas, b->out, b->Ac, b->td,
                     b->fac, b->ysol, b->der, b->Qb, b->cqpart, b->cqG, b->cqL, b->cqLinv,
                     b->cqMinv, b->cqS, b->cqscr, b->cqUS, b->cqW,
@@ -495,29 +492,31 @@ int band_reduce_pass(gpmi_band* b, const double* K, const std::vector<double>* y
     hipLaunchKernelGGL(psum_kernel, dim3(TS * TS / 512, mt), dim3(256), 0, s, b->Xp, sch, b->X);
     BD_LAUNCH("psum_kernel");
     BD_TRY(hipStreamWaitEvent(s, b->ev_t, 0));
-    hipLaunchKernelGGL(xt_kernel, dim3(mt), dim3(256), 0, s, b->X, T);
-    BD_LAUNCH("xt_kernel");
-    hipLaunchKernelGGL(tn_partial_kernel, dim3(nch), dim3(256), 0, s, Ur + TS,
-                       (int64_t)BAND_ULD, b->X, (int64_t)TS, m, b->tnp, nullptr);
-    BD_LAUNCH("tn_partial_kernel");
+    // the serial 128^3 steps on quadrant workgroups (gemm_quad, gpmi_tile.h)
+    hipLaunchKernelGGL(xt_q_kernel, dim3(mt, 4), dim3(256), 0, s, b->X, T, b->X2);
+    BD_LAUNCH("xt_q_kernel");
+    hipLaunchKernelGGL(tn_partial_q_kernel, dim3(nch, 4), dim3(256), 0, s, Ur + TS,
+                       (int64_t)BAND_ULD, b->X2, (int64_t)TS, m, b->tnp);
+    BD_LAUNCH("tn_partial_q_kernel");
     hipLaunchKernelGGL(tn_reduce_kernel, dim3(TS * TS / 64), dim3(256), 0, s, b->tnp, nch, b->M,
                        1.0, nullptr);
     BD_LAUNCH("tn_reduce_kernel");
-    hipLaunchKernelGGL(z_kernel, dim3(1), dim3(256), 0, s, T, b->M, b->Zh);
-    BD_LAUNCH("z_kernel");
-    hipLaunchKernelGGL(w_kernel, dim3(mt), dim3(256), 0, s, b->X, Ur, (int64_t)BAND_ULD, b->Zh);
-    BD_LAUNCH("w_kernel");
+    hipLaunchKernelGGL(z_q_kernel, dim3(4), dim3(256), 0, s, T, b->M, b->Zh);
+    BD_LAUNCH("z_q_kernel");
+    hipLaunchKernelGGL(w_q_kernel, dim3(mt, 4), dim3(256), 0, s, b->X2, Ur, (int64_t)BAND_ULD,
+                       b->Zh);
+    BD_LAUNCH("w_q_kernel");
     const int next_g = (int)((np - r0 - TS + HH_ROWS - 1) / HH_ROWS);   // panel j + 1's grid
     if (la && j + 2 < nt && (mode == 0 || next_g <= b->panel_maxg)) {
       // tile column 0 of the update (panel j + 1's columns) first; then that
       // panel's QR beside the rest of the update on a grid capped to la_grid
       // workgroups, so that the panel's workgroups find free CUs
-      hipLaunchKernelGGL(syr2k_kernel, dim3(mt), dim3(256), 0, s, b->Ab, np, b->U,
-                         (int64_t)BAND_ULD, j + 1, mt, 1);
-      BD_LAUNCH("syr2k_kernel");
+      hipLaunchKernelGGL(syr2k_col_q_kernel, dim3(mt, 4), dim3(256), 0, s, b->Ab, np, b->U,
+                         (int64_t)BAND_ULD, j + 1);
+      BD_LAUNCH("syr2k_col_q_kernel");
       BD_TRY(hipEventRecord(b->ev_col, s));
       BD_TRY(hipStreamWaitEvent(b->s_pan, b->ev_col, 0));
-      const bool pipe = mode == 0 && b->la_free >= 0;
+      const bool pipe = mode == 0;
       bool guard = false;
       int rc = panel_qr(b, j + 1, b->s_pan, mode, pipe ? &guard : nullptr);
       if (rc) return rc;
@@ -526,15 +525,14 @@ int band_reduce_pass(gpmi_band* b, const double* K, const std::vector<double>* y
       if (pipe) {
         // one SYR2K workgroup per CU on all but la_free CUs, which the chain (its
         // single-workgroup kernels need a whole CU) has to itself
-        hipLaunchKernelGGL(syr2k_pipe_kernel, dim3(std::min(rest, std::max(1, b->ncu - b->la_free))),
+        hipLaunchKernelGGL(syr2k_pipe_kernel, dim3(std::min(rest, std::max(1, b->ncu - LA_FREE))),
                            dim3(256), 0, s, b->Ab, np, b->U, (int64_t)BAND_ULD, j + 1, mt);
         BD_LAUNCH("syr2k_pipe_kernel");
       } else {
-        // la_grid 0: leave exactly the panel's workgroup count of CUs free (measured:
-        // slower than a fixed 128-workgroup cap at N = 16384, 302 vs 262 ms); the
-        // CholeskyQR panel needs no co-resident workgroups (cq_la_grid, 0: no cap)
-        const int cap = mode == 0 ? (b->cq_la_grid > 0 ? b->cq_la_grid : rest)
-                        : b->la_grid > 0 ? b->la_grid : std::max(64, b->ncu - next_g);
+        // the Householder panel (its workgroups must be co-resident) beside a capped
+        // grid; la_grid 0: leave exactly the panel's workgroup count of CUs free
+        // (measured: slower than a fixed 128-workgroup cap at N = 16384, 302 vs 262 ms)
+        const int cap = b->la_grid > 0 ? b->la_grid : std::max(64, b->ncu - next_g);
         hipLaunchKernelGGL(syr2k_rest_kernel, dim3(std::min(rest, cap)), dim3(256), 0, s, b->Ab,
                            np, b->U, (int64_t)BAND_ULD, j + 1,
                            mt, b->rorder ? b->rorder + b->rorder_off[mt - 1] : nullptr);
@@ -551,7 +549,7 @@ int band_reduce_pass(gpmi_band* b, const double* K, const std::vector<double>* y
     } else {
       const int tiles = mt * (mt + 1) / 2;
       hipLaunchKernelGGL(syr2k_kernel, dim3(tiles), dim3(256), 0, s, b->Ab, np, b->U,
-                         (int64_t)BAND_ULD, j + 1, mt, 0);
+                         (int64_t)BAND_ULD, j + 1, mt);
       BD_LAUNCH("syr2k_kernel");
     }
   }
@@ -669,8 +667,6 @@ int gpmi_band_create(gpmi_op* op, gpmi_band** out) {
   if ((e = hipStreamCreateWithFlags(&b->side, hipStreamNonBlocking)) != hipSuccess)
     return fail(e, "side stream");
   if (const char* la = std::getenv("GPMI_BAND_LA")) b->lookahead = std::atoi(la);
-  if (const char* lf = std::getenv("GPMI_BAND_LA_FREE")) b->la_free = std::atoi(lf);
-  if (const char* ct = std::getenv("GPMI_BAND_CQT")) b->cq_t = std::atoi(ct) != 0;
   if (const char* pm = std::getenv("GPMI_BAND_PANEL")) b->panel_mode = std::strcmp(pm, "hh") == 0;
   if (const char* bm = std::getenv("GPMI_BAND_BCR")) b->bcr_mode = std::max(0, std::min(2, std::atoi(bm)));
   // GPMI_CQ_FO=0: every CholeskyQR pass by an exact Cholesky (no first-order passes)
@@ -700,6 +696,7 @@ int gpmi_band_create(gpmi_op* op, gpmi_band** out) {
   BALLOC(Ab, np * np);
   BALLOC(U, np * BAND_ULD);
   BALLOC(X, np * TS);
+  BALLOC(X2, np * TS);
   BALLOC(Xp, (size_t)xp_tiles * TS * TS);
   BALLOC(part, 2 * HH_MAXG * HH_PART_LD);
   BALLOC(pivrow, 2 * TS);
@@ -720,7 +717,7 @@ int gpmi_band_create(gpmi_op* op, gpmi_band** out) {
   BALLOC(cqL, (size_t)nt * 3 * TS * TS);
   BALLOC(cqLinv, (size_t)nt * 3 * TS * TS);
   BALLOC(cqMinv, TS * TS);
-  if (b->cq_t) {
+  {
     BALLOC(cqUS, (int64_t)nt * TS * TS);
     BALLOC(cqW, (int64_t)nt * TS * TS);
     int lo = 0, hi = 0;

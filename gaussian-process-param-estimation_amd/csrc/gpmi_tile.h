@@ -98,6 +98,94 @@ __device__ __forceinline__ void gemm_tile(const double* __restrict__ P1, int64_t
   }
 }
 
+// One 64 x 64 quadrant (qr, qc) of the 128 x 128 product above: the same staging
+// (both 128-row slabs, so the operand layouts and swizzles are shared), each wave a
+// 32 x 32 piece (wave w: rows qr*64 + (w>>1)*32, columns qc*64 + (w&1)*32). Four
+// workgroups then cover one output tile with a quarter of the MFMA chain each: the
+// band's serial 128^3 steps (X T, V^T X, T^T M, X - V Zh, the tile-column update)
+// are latency-bound single products per tile, ~4x shorter this way.
+template <int AL, int BL, bool NEG>
+__device__ __forceinline__ void gemm_quad(const double* __restrict__ P1, int64_t ld1,
+                                          const double* __restrict__ P2, int64_t ld2, int kdim,
+                                          double* smem, d4 (&acc)[2][2], int qr, int qc) {
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int r0 = qr * 64 + (w >> 1) * 32, c0 = qc * 64 + (w & 1) * 32;
+  const int fr = lane & 15, fk = lane >> 4;
+  double* sA = smem;
+  double* sB = smem + 2 * GSTAGE;
+  d2 ra[4], rb[4];
+  gl_op<AL>(P1, ld1, 0, ra);
+  gl_op<BL>(P2, ld2, 0, rb);
+  st_op<AL>(sA, ra);
+  st_op<BL>(sB, rb);
+  __syncthreads();
+  __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): as gemm_tile
+  const int nsteps = kdim / BK;
+  for (int s = 0; s < nsteps; ++s) {
+    const int cur = s & 1;
+    const double* cA = sA + cur * GSTAGE;
+    const double* cB = sB + cur * GSTAGE;
+    if (s + 1 < nsteps) {
+      gl_op<AL>(P1, ld1, (s + 1) * BK, ra);
+      gl_op<BL>(P2, ld2, (s + 1) * BK, rb);
+    }
+#pragma unroll
+    for (int kk = 0; kk < BK / 4; ++kk) {
+      double a[2], b[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) a[i] = fr_op<AL>(cA, r0 + i * 16 + fr, kk * 4 + fk);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) b[j] = fr_op<BL>(cB, c0 + j * 16 + fr, kk * 4 + fk);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = NEG ? mfma64_neg(a[i], b[j], acc[i][j]) : mfma64(a[i], b[j], acc[i][j]);
+    }
+    if (s + 1 < nsteps) {
+      st_op<AL>(sA + (cur ^ 1) * GSTAGE, ra);
+      st_op<BL>(sB + (cur ^ 1) * GSTAGE, rb);
+    }
+    __syncthreads();
+  }
+}
+
+__device__ __forceinline__ void zero_quad(d4 (&acc)[2][2]) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = d4{0.0, 0.0, 0.0, 0.0};
+}
+
+// C points at the 128 x 128 tile; the quadrant's wave pieces as in gemm_quad.
+__device__ __forceinline__ void load_quad(const double* C, int64_t ldc, d4 (&acc)[2][2], int qr,
+                                          int qc) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r0 = qr * 64 + (w >> 1) * 32, c0 = qc * 64 + (w & 1) * 32;
+  const int fr = lane & 15, fk = lane >> 4;
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        acc[a][c][r] = C[(int64_t)(r0 + a * 16 + fk + 4 * r) * ldc + c0 + c * 16 + fr];
+}
+
+__device__ __forceinline__ void store_quad(double* C, int64_t ldc, const d4 (&acc)[2][2],
+                                           double scale, int qr, int qc) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r0 = qr * 64 + (w >> 1) * 32, c0 = qc * 64 + (w & 1) * 32;
+  const int fr = lane & 15, fk = lane >> 4;
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        C[(int64_t)(r0 + a * 16 + fk + 4 * r) * ldc + c0 + c * 16 + fr] = scale * acc[a][c][r];
+}
+
 __device__ __forceinline__ void zero_tile(d4 (&acc)[4][4]) {
 #pragma unroll
   for (int i = 0; i < 4; ++i)
