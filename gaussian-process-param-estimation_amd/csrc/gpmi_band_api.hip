@@ -154,13 +154,14 @@ struct gpmi_band {
   int* bcrFail = nullptr;    // [bcap][nt]
   double* bcrF0 = nullptr;   // [nt - 1][128][128]
   double* cqMinv = nullptr;  // C = U^-T M3 of the current panel
-  // T of a CholeskyQR panel from its reconstruction (cq_t_kernel) on a stream of its
-  // own: U S and V1^-1 per panel; t_from_q[j]: panel j's T comes from there (the
-  // side stream's V^T V / tbuild_kernel then run only if the panel fell back)
+  // T of a CholeskyQR panel from its reconstruction (cq_t_kernel) on the side stream
+  // (not a stream of its own: the process's streams share GPU_MAX_HW_QUEUES hardware
+  // queues, and two streams on one queue serialise): U S and V1^-1 per panel;
+  // t_from_q[j]: panel j's T comes from there (the side stream's V^T V / tbuild_kernel
+  // then run only if the panel fell back)
   double* cqUS = nullptr;    // [nt][128][128]
   double* cqW = nullptr;     // [nt][128][128]
-  hipStream_t s_t = nullptr;
-  hipEvent_t ev_rc = nullptr, ev_t2 = nullptr;
+  hipEvent_t ev_rc = nullptr;
   std::vector<char> t_from_q;
   double cq_fo[3] = {0.0, 1e-4, 3e-8};   // first-order thresholds on ||G - I||_F
   int cap = 0;
@@ -211,8 +212,7 @@ int band_free(gpmi_band* b) {
   if (b->stream) (void)hipStreamDestroy(b->stream);
   if (b->side) (void)hipStreamDestroy(b->side);
   if (b->s_pan) (void)hipStreamDestroy(b->s_pan);
-  if (b->s_t) (void)hipStreamDestroy(b->s_t);
-  for (hipEvent_t e : {b->ev_col, b->ev_pan, b->ev_rc, b->ev_t2})
+  for (hipEvent_t e : {b->ev_col, b->ev_pan, b->ev_rc})
     if (e) (void)hipEventDestroy(e);
   if (b->ev_q) (void)hipEventDestroy(b->ev_q);
   if (b->ev_v) (void)hipEventDestroy(b->ev_v);
@@ -328,19 +328,17 @@ int cq_panel(gpmi_band* b, int j, hipStream_t st, bool guard = true) {
   hipLaunchKernelGGL(cq_recon_kernel, dim3(1), dim3(256), 0, st, b->Qb, b->cqG, b->cq_fo[2], P,
                      np, b->cqS + (int64_t)j * TS, b->tau + (int64_t)j * TS,
                      b->cqL + pt + 2 * TS * TS, b->cqLinv + pt + 2 * TS * TS, b->cqMinv, fl,
-                     fl + 4, b->s_t ? b->cqUS + (int64_t)j * TS * TS : nullptr);
+                     fl + 4, b->cqUS + (int64_t)j * TS * TS);
   BD_LAUNCH("cq_recon_kernel");
-  if (b->s_t) {
-    // T = -U S V1^-T beside the rest of the chain (exits when the panel failed)
-    BD_TRY(hipEventRecord(b->ev_rc, st));
-    BD_TRY(hipStreamWaitEvent(b->s_t, b->ev_rc, 0));
-    hipLaunchKernelGGL(cq_t_kernel, dim3(1), dim3(256), 0, b->s_t, P, np,
-                       b->cqUS + (int64_t)j * TS * TS, b->cqW + (int64_t)j * TS * TS,
-                       b->Tm + (int64_t)j * TS * TS, fl + 4);
-    BD_LAUNCH("cq_t_kernel");
-    BD_TRY(hipEventRecord(b->ev_t2, b->s_t));
-    b->t_from_q[j] = 1;
-  }
+  // T = -U S V1^-T on the side stream beside the rest of the chain (exits when the
+  // panel failed); the side stream's later work for this panel is behind it
+  BD_TRY(hipEventRecord(b->ev_rc, st));
+  BD_TRY(hipStreamWaitEvent(b->side, b->ev_rc, 0));
+  hipLaunchKernelGGL(cq_t_kernel, dim3(1), dim3(256), 0, b->side, P, np,
+                     b->cqUS + (int64_t)j * TS * TS, b->cqW + (int64_t)j * TS * TS,
+                     b->Tm + (int64_t)j * TS * TS, fl + 4);
+  BD_LAUNCH("cq_t_kernel");
+  b->t_from_q[j] = 1;
   // V2 = Q2 C^T below the top block
   if (mt > 1) {
     hipLaunchKernelGGL(cq_apply_kernel, dim3(rt - 2), dim3(256), CQ_DYN_LDS, st, b->Qb + TS * TS,
@@ -475,7 +473,6 @@ int band_reduce_pass(gpmi_band* b, const double* K, const std::vector<double>* y
     BD_LAUNCH("tn_reduce_kernel");
     hipLaunchKernelGGL(tbuild_kernel, dim3(1), dim3(256), 0, b->side, b->VtV, tau, T, only_if);
     BD_LAUNCH("tbuild_kernel");
-    if (b->t_from_q[j]) BD_TRY(hipStreamWaitEvent(b->side, b->ev_t2, 0));
     b->t_from_q[j] = 0;
     BD_TRY(hipEventRecord(b->ev_t, b->side));
     if (yh) {
@@ -717,17 +714,10 @@ int gpmi_band_create(gpmi_op* op, gpmi_band** out) {
   BALLOC(cqL, (size_t)nt * 3 * TS * TS);
   BALLOC(cqLinv, (size_t)nt * 3 * TS * TS);
   BALLOC(cqMinv, TS * TS);
-  {
-    BALLOC(cqUS, (int64_t)nt * TS * TS);
-    BALLOC(cqW, (int64_t)nt * TS * TS);
-    int lo = 0, hi = 0;
-    if ((e = hipDeviceGetStreamPriorityRange(&lo, &hi)) != hipSuccess) return fail(e, "prio");
-    if ((e = hipStreamCreateWithPriority(&b->s_t, hipStreamNonBlocking, hi)) != hipSuccess)
-      return fail(e, "T stream");
-    for (hipEvent_t* ev : {&b->ev_rc, &b->ev_t2})
-      if ((e = hipEventCreateWithFlags(ev, hipEventDisableTiming)) != hipSuccess)
-        return fail(e, "event");
-  }
+  BALLOC(cqUS, (int64_t)nt * TS * TS);
+  BALLOC(cqW, (int64_t)nt * TS * TS);
+  if ((e = hipEventCreateWithFlags(&b->ev_rc, hipEventDisableTiming)) != hipSuccess)
+    return fail(e, "event");
   b->t_from_q.assign((size_t)nt, 0);
   BALLOC(cqS, (size_t)nt * TS);
   BALLOC(cqscr, (size_t)nt * TS * TS);
