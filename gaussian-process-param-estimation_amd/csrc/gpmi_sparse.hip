@@ -1342,7 +1342,8 @@ __global__ __launch_bounds__(256) void ms_tail_kernel(MsState cur, MsState nxt,
                                                       const double* __restrict__ dshift, int S,
                                                       int s, int nb, double rtol2,
                                                       double* __restrict__ P,
-                                                      const double* __restrict__ R, int64_t n) {
+                                                      const double* __restrict__ R, int64_t n,
+                                                      MsPin* __restrict__ pin) {
   __shared__ double br[MS_MAXS * MS_MAXS + MS_MAXS];
   __shared__ double sbeta[MS_MAXS];
   __shared__ int supd[MS_MAXS];
@@ -1414,14 +1415,23 @@ __global__ __launch_bounds__(256) void ms_tail_kernel(MsState cur, MsState nxt,
   }
   __syncthreads();
   if (t < s) {
+    double rr_n;
+    int act_n;
     if (cur.active[t]) {
       cur.a_prev[t] = cur.a[t];
       cur.beta[t] = sbeta[t];
-      nxt.rr[t] = br[nb * s + t];
-      nxt.active[t] = supd[t];
+      rr_n = br[nb * s + t];
+      act_n = supd[t];
     } else {
-      nxt.rr[t] = cur.rr[t];
-      nxt.active[t] = 0;
+      rr_n = cur.rr[t];
+      act_n = 0;
+    }
+    nxt.rr[t] = rr_n;
+    nxt.active[t] = act_n;
+    if (pin) {   // the batch's end state for the host (pinned, device-mapped)
+      pin->rr[t] = rr_n;
+      pin->act[t] = act_n;
+      if (t == 0) pin->flag = cur.flags[0];   // set by ms_rmfma_kernel, before this launch
     }
   }
 }

@@ -93,7 +93,7 @@ __global__ void rows_gather_kernel(const double*, int, const int*, int64_t, int,
 __global__ void ms_rmfma_kernel(const double*, double*, const double*, MsState, const double*, int,
                                 int64_t, int, int, double*);
 __global__ void ms_tail_kernel(MsState, MsState, const double*, const double*, int, int, int, double,
-                               double*, const double*, int64_t);
+                               double*, const double*, int64_t, MsPin*);
 __global__ void ms_init_kernel(MsState, const double*, int, int, int, int);
 template <int CT>
 __global__ void dense_mm_kernel(const double*, int64_t, int64_t, const double*, int, int, double*);
@@ -173,6 +173,8 @@ struct gpmi_sp {
   // sparse step's two independent halves overlap on the device)
   hipStream_t ms_stream = nullptr;
   double* ms_ws = nullptr;
+  double* rhs_dev = nullptr;               // resident RHS block [n][rhs_nrhs] (gpmi_sp_set_rhs)
+  int rhs_nrhs = 0;
   size_t ms_ws_doubles = 0;
   double* ms_partial = nullptr;
   size_t ms_partial_doubles = 0;
@@ -953,6 +955,7 @@ int gpmi_sp_destroy(gpmi_sp* sp) {
   if (sp->lz) (void)hipFree(sp->lz);
   if (sp->lzd) (void)hipFree(sp->lzd);
   if (sp->ms_ws) (void)hipFree(sp->ms_ws);
+  if (sp->rhs_dev) (void)hipFree(sp->rhs_dev);
   if (sp->ms_partial) (void)hipFree(sp->ms_partial);
   if (sp->ms_pin) (void)hipHostFree(sp->ms_pin);
   for (hipEvent_t e : sp->ms_ev)
@@ -1245,6 +1248,10 @@ static int msgram_impl(gpmi_sp* sp, const double* etas, int neta, const double* 
                        int64_t ld, int nrhs, int c_lo, int c_hi, double rtol, int maxiter,
                        double* G, int* iterations) {
   if (!sp) return set_error(-1006, "null handle");
+  // rhs == NULL: the resident block of gpmi_sp_set_rhs (already in HBM: no upload)
+  if (!rhs && (!sp->rhs_dev || nrhs != sp->rhs_nrhs))
+    return set_error(-1105, "msgram: rhs NULL needs a resident block of nrhs columns "
+                            "(gpmi_sp_set_rhs)");
   if (neta < 1 || nrhs < 1 || nrhs > MS_MAXS || c_lo < 0 || c_hi > nrhs || c_lo >= c_hi ||
       neta * (c_hi - c_lo) > 1024)
     return set_error(-1104, "msgram: need 1 <= nrhs <= 16, 0 <= c_lo < c_hi <= nrhs and "
@@ -1355,7 +1362,10 @@ static int msgram_impl(gpmi_sp* sp, const double* etas, int neta, const double* 
     // the RHS block as the caller holds it (rows in the original order) into the
     // staging Qd, then into the locality order (and zero padding columns) on the
     // device: no host-side permutation pass over n x s doubles
-    if (ld == nrhs) {
+    const double* Hsrc = Hs;
+    if (!rhs) {
+      Hsrc = sp->rhs_dev;
+    } else if (ld == nrhs) {
       SP_TRY(hipMemcpyAsync(Hs, rhs, sizeof(double) * n * nrhs, hipMemcpyHostToDevice, str));
     } else {
       std::vector<double> h((size_t)n * nrhs);
@@ -1364,7 +1374,7 @@ static int msgram_impl(gpmi_sp* sp, const double* etas, int neta, const double* 
       SP_TRY(hipMemcpyAsync(Hs, h.data(), sizeof(double) * h.size(), hipMemcpyHostToDevice, str));
       SP_TRY(hipStreamSynchronize(str));
     }
-    hipLaunchKernelGGL(rows_gather_kernel, dim3(grid_ns(n, nbd)), dim3(256), 0, str, Hs, nrhs,
+    hipLaunchKernelGGL(rows_gather_kernel, dim3(grid_ns(n, nbd)), dim3(256), 0, str, Hsrc, nrhs,
                        (const int*)sp->perm_d, n, nbd, Bd);
     SP_LAUNCH("rows_gather_kernel");
     std::vector<double> hd(S);
@@ -1404,7 +1414,7 @@ static int msgram_impl(gpmi_sp* sp, const double* etas, int neta, const double* 
                        : 0;
   };
   // one iteration's launches on str (parity it & 1 picks the state double buffer)
-  auto iterate = [&](int itx) -> int {
+  auto iterate = [&](int itx, MsPin* pin_out) -> int {
     // the window SpMM also forms the p . q block partials in its epilogue (summed
     // across the chip below); other kernels leave them to col_dot_partial_kernel
     int pqb = 0;
@@ -1432,7 +1442,7 @@ static int msgram_impl(gpmi_sp* sp, const double* etas, int neta, const double* 
     // the per-shift scalars and p = r + beta p in one launch (ms_tail_kernel)
     hipLaunchKernelGGL(ms_tail_kernel, dim3((unsigned)((ns + 1023) / 1024)), dim3(256), 0, str,
                        st2[itx & 1], st2[(itx + 1) & 1], (const double*)brd, dshift, S, s, nbd,
-                       rtol * rtol, Pd, (const double*)Rcur, n);
+                       rtol * rtol, Pd, (const double*)Rcur, n, pin_out);
     SP_LAUNCH("ms_tail_kernel");
     return 0;
   };
@@ -1447,19 +1457,17 @@ static int msgram_impl(gpmi_sp* sp, const double* etas, int neta, const double* 
   // more. Iterations past a column's convergence leave it unchanged (zero steps).
   // (A batch captured as a HIP graph and relaunched measured the same as launching
   // it: the per-kernel cost is on the device.)
-  struct PinSlot {
-    int act[MS_MAXS];
-    int flag;
-    int pad;
-    double rr[MS_MAXS];
-  };
+  using PinSlot = MsPin;
   if (!sp->ms_pin) {
+    // coherent: the batch's last ms_tail_kernel stores the end state into it directly
     SP_TRY(hipHostMalloc(reinterpret_cast<void**>(&sp->ms_pin), 2 * sizeof(PinSlot),
-                         hipHostMallocDefault));
+                         hipHostMallocCoherent | hipHostMallocMapped));
     for (hipEvent_t* e : {&sp->ms_ev[0], &sp->ms_ev[1]})
       SP_TRY(hipEventCreateWithFlags(e, hipEventDisableTiming));
   }
   PinSlot* pin = reinterpret_cast<PinSlot*>(sp->ms_pin);
+  PinSlot* pin_dev = nullptr;
+  SP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&pin_dev), sp->ms_pin, 0));
   std::vector<double> hbn2(s);
   {
     bool any = false;
@@ -1502,14 +1510,9 @@ static int msgram_impl(gpmi_sp* sp, const double* etas, int neta, const double* 
   };
   while (it < maxiter) {
     nb = std::max(1, std::min(nb, maxiter - it));
-    for (int q = 0; q < nb; ++q, ++it)
-      if ((rc = iterate(it))) return rc;
     const int q = k & 1;
-    SP_TRY(hipMemcpyAsync(pin[q].act, st2[it & 1].active, sizeof(int) * s, hipMemcpyDeviceToHost,
-                          str));
-    SP_TRY(hipMemcpyAsync(&pin[q].flag, st.flags, sizeof(int), hipMemcpyDeviceToHost, str));
-    SP_TRY(hipMemcpyAsync(pin[q].rr, st2[it & 1].rr, sizeof(double) * s, hipMemcpyDeviceToHost,
-                          str));
+    for (int i = 0; i < nb; ++i, ++it)
+      if ((rc = iterate(it, i + 1 == nb ? pin_dev + q : nullptr))) return rc;
     SP_TRY(hipEventRecord(sp->ms_ev[q], str));
     slot_it[q] = it;
     ++k;
@@ -1557,6 +1560,29 @@ int gpmi_sp_msgram_cols(gpmi_sp* sp, const double* etas, int neta, const double*
                         int nrhs, int c_lo, int c_hi, double rtol, int maxiter, double* G,
                         int* iterations) {
   return msgram_impl(sp, etas, neta, rhs, ld, nrhs, c_lo, c_hi, rtol, maxiter, G, iterations);
+}
+
+int gpmi_sp_set_rhs(gpmi_sp* sp, const double* rhs, int64_t ld, int nrhs) {
+  if (!sp) return set_error(-1006, "null handle");
+  if (!rhs || nrhs < 1 || nrhs > MS_MAXS || ld < nrhs)
+    return set_error(-1104, "set_rhs: need 1 <= nrhs <= 16 and ld >= nrhs");
+  Guard g(sp->device);
+  const int64_t n = sp->n;
+  if (sp->rhs_dev && sp->rhs_nrhs != nrhs) {
+    SP_TRY(hipFree(sp->rhs_dev));
+    sp->rhs_dev = nullptr;
+  }
+  if (!sp->rhs_dev) SP_TRY(hipMalloc(&sp->rhs_dev, sizeof(double) * (size_t)n * nrhs));
+  sp->rhs_nrhs = nrhs;
+  if (ld == nrhs) {
+    SP_TRY(hipMemcpy(sp->rhs_dev, rhs, sizeof(double) * (size_t)n * nrhs, hipMemcpyHostToDevice));
+  } else {
+    std::vector<double> h((size_t)n * nrhs);
+    for (int64_t i = 0; i < n; ++i)
+      for (int c = 0; c < nrhs; ++c) h[(size_t)i * nrhs + c] = rhs[i * ld + c];
+    SP_TRY(hipMemcpy(sp->rhs_dev, h.data(), sizeof(double) * h.size(), hipMemcpyHostToDevice));
+  }
+  return 0;
 }
 
 int gpmi_sp_spmm_info(gpmi_sp* sp, int* windowed, double* mean_window, int* max_window) {

@@ -83,6 +83,7 @@ SIGNATURES = {
     'gpmi_sp_msgram_cols': (ctypes.c_int, [c_op_p, c_double_p, ctypes.c_int, c_double_p, c_i64,
                                            ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                            ctypes.c_double, ctypes.c_int, c_double_p, c_int_p]),
+    'gpmi_sp_set_rhs': (ctypes.c_int, [c_op_p, c_double_p, c_i64, ctypes.c_int]),
     'gpmi_band_create': (ctypes.c_int, [c_op_p, ctypes.POINTER(c_op_p)]),
     'gpmi_band_destroy': (ctypes.c_int, [c_op_p]),
     'gpmi_band_refresh': (ctypes.c_int, [c_op_p, c_op_p]),
@@ -623,15 +624,34 @@ class SparseOperator(object):
 
     MS_MAXS = 16
 
-    def msgram(self, etas, B, rtol=1e-6, maxiter=None, cols=None):
-        """G[j] = B^T (K + etas[j] I)^-1 B for all etas from one multi-shift CG
-        (B: [n, s], s <= 16). Returns G [neta, s, s]; with cols = (c_lo, c_hi) only
-        those right-hand sides are solved (dotted with all of B): G [neta, s,
-        c_hi - c_lo], the columns of the full G (gpmi_sp_msgram_cols)."""
+    def set_rhs(self, B):
+        """Keep the [n, s] block B resident in HBM (gpmi_sp_set_rhs): msgram(etas,
+        None) then reads it there instead of uploading B per call."""
         B = as_c(B)
         B2 = B[:, None] if B.ndim == 1 else B
+        if B2.shape[0] != self.n:
+            raise ValueError('set_rhs: %d rows, the operator has %d' % (B2.shape[0], self.n))
+        check(self.lib.gpmi_sp_set_rhs(self.h, dptr(B2), B2.shape[1], B2.shape[1]),
+              'gpmi_sp_set_rhs')
+        self.rhs_cols = B2.shape[1]
+
+    rhs_cols = 0
+
+    def msgram(self, etas, B, rtol=1e-6, maxiter=None, cols=None):
+        """G[j] = B^T (K + etas[j] I)^-1 B for all etas from one multi-shift CG
+        (B: [n, s], s <= 16; None: the block of set_rhs, resident in HBM). Returns
+        G [neta, s, s]; with cols = (c_lo, c_hi) only those right-hand sides are
+        solved (dotted with all of B): G [neta, s, c_hi - c_lo], the columns of the
+        full G (gpmi_sp_msgram_cols)."""
+        if B is None:
+            if not self.rhs_cols:
+                raise ValueError('msgram: no resident right-hand sides (set_rhs)')
+            B2, s, ld = None, self.rhs_cols, self.rhs_cols
+        else:
+            B = as_c(B)
+            B2 = B[:, None] if B.ndim == 1 else B
+            s = ld = B2.shape[1]
         etas = as_c(numpy.atleast_1d(etas))
-        s = B2.shape[1]
         c_lo, c_hi = (0, s) if cols is None else (int(cols[0]), int(cols[1]))
         w = c_hi - c_lo
         G = numpy.empty((etas.size, s, w))
@@ -642,12 +662,14 @@ class SparseOperator(object):
             e = as_c(etas[j0:j0 + step])
             Gj = numpy.empty((e.size, s, w))
             if cols is None:
-                check(self.lib.gpmi_sp_msgram(self.h, dptr(e), e.size, dptr(B2), s, s,
+                check(self.lib.gpmi_sp_msgram(self.h, dptr(e), e.size,
+                                              None if B2 is None else dptr(B2), ld, s,
                                               float(rtol), maxiter, dptr(Gj), ctypes.byref(it)),
                       'gpmi_sp_msgram')
             else:
-                check(self.lib.gpmi_sp_msgram_cols(self.h, dptr(e), e.size, dptr(B2), s, s, c_lo,
-                                                   c_hi, float(rtol), maxiter, dptr(Gj),
+                check(self.lib.gpmi_sp_msgram_cols(self.h, dptr(e), e.size,
+                                                   None if B2 is None else dptr(B2), ld, s,
+                                                   c_lo, c_hi, float(rtol), maxiter, dptr(Gj),
                                                    ctypes.byref(it)),
                       'gpmi_sp_msgram_cols')
             G[j0:j0 + e.size] = Gj

@@ -212,6 +212,8 @@ def slq_gram_sweep(K_mixed, etas, R, rtol=1e-6, group=None, split='columns'):
     ``split='eta'`` gives each rank the full CG for its eta block (the per-shift
     scalars only divide).
 
+    ``R = None``: the right-hand sides K_mixed.sop.set_rhs made resident in HBM.
+
     Returns (curves, (lo, hi), G[hi - lo, s, s]): slq_sweep's curves on every
     rank, and this rank's contiguous eta block with its Gram blocks.
 
@@ -221,9 +223,15 @@ def slq_gram_sweep(K_mixed, etas, R, rtol=1e-6, group=None, split='columns'):
     after them (as der1_sweep)."""
     from concurrent.futures import ThreadPoolExecutor
     etas = numpy.atleast_1d(numpy.asarray(etas, dtype=float))
-    R = numpy.asarray(R, dtype=float)
-    R2 = R[:, None] if R.ndim == 1 else R
-    s = R2.shape[1]
+    if R is None:
+        # the block K_mixed.sop.set_rhs made resident in HBM (no upload per sweep)
+        R2, s = None, K_mixed.sop.rhs_cols
+        if not s:
+            raise ValueError('slq_gram_sweep: R is None but no resident block (sop.set_rhs)')
+    else:
+        R = numpy.asarray(R, dtype=float)
+        R2 = R[:, None] if R.ndim == 1 else R
+        s = R2.shape[1]
     dist, world, rank = _group(group)
     multi = dist is not None and world > 1
     lo, hi, _ = shard(etas.size, world, rank)

@@ -202,6 +202,7 @@ int gpmi_sp_cg(gpmi_sp* sp, double eta, const double* rhs, int64_t ld, int nrhs,
  * -> _linear_solver.py:57-68 (scipy.sparse.linalg.cg, tol 1e-6). */
 int gpmi_sp_msgram(gpmi_sp* sp, const double* etas, int neta, const double* rhs, int64_t ld,
                    int nrhs, double rtol, int maxiter, double* G, int* iterations);
+/* (rhs == NULL: the block made resident by gpmi_sp_set_rhs.) */
 /* The same for a shard of the right-hand sides: the columns [c_lo, c_hi) of the
  * nrhs-column block solved (every eta), dotted with all nrhs columns:
  * G[neta][nrhs][c_hi - c_lo], G[j][a][c] = b_a^T (K + eta_j I)^-1 b_{c_lo + c}. Ranks
@@ -211,6 +212,13 @@ int gpmi_sp_msgram(gpmi_sp* sp, const double* etas, int neta, const double* rhs,
 int gpmi_sp_msgram_cols(gpmi_sp* sp, const double* etas, int neta, const double* rhs, int64_t ld,
                         int nrhs, int c_lo, int c_hi, double rtol, int maxiter, double* G,
                         int* iterations);
+/* Keep the nrhs-column block [n][ld] (host, original row order) resident in HBM:
+ * gpmi_sp_msgram / gpmi_sp_msgram_cols with rhs == NULL (ld ignored, nrhs equal to
+ * this block's) then read it there instead of uploading the host block per call (the
+ * likelihood's [X z] is fixed across evaluations; at cfg 5, 262144 x 11 doubles,
+ * the per-call upload from pageable memory took ~1.9 ms of a ~14 ms step). Replaces
+ * nothing in the reference (its CG reads the numpy arrays in place). */
+int gpmi_sp_set_rhs(gpmi_sp* sp, const double* rhs, int64_t ld, int nrhs);
 
 /* The SpMM kernel this operator uses (1: X-window staged in LDS, 64-row blocks;
  * 0: gathers from X, one wave per row) and its window sizes (columns per block:

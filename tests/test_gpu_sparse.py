@@ -230,6 +230,28 @@ def test_msgram_column_shards_equal_full(gp):
         assert _nrel(g, ex) < 1e-9
 
 
+def test_msgram_resident_rhs(gp):
+    """gpmi_sp_set_rhs: the right-hand sides kept in HBM give the same Gram as the
+    host block, bit for bit (the same kernels on the same values), for the full
+    block and a column shard; a block of another width replaces it; without one,
+    msgram(etas, None) raises."""
+    from gaussian_proc import _hip
+    _, K = _small_sparse()
+    n = K.shape[0]
+    sop = _hip.SparseOperator.from_csr(K)
+    etas = numpy.array([3.0, 6.0, 50.0])
+    with pytest.raises(ValueError):
+        sop.msgram(etas, None)
+    rng = numpy.random.RandomState(11)
+    for s in (11, 4):
+        B = rng.randn(n, s)
+        G = sop.msgram(etas, B, rtol=1e-10)
+        sop.set_rhs(B)
+        assert numpy.array_equal(sop.msgram(etas, None, rtol=1e-10), G)
+        assert numpy.array_equal(sop.msgram(etas, None, rtol=1e-10, cols=(1, 3)),
+                                 sop.msgram(etas, B, rtol=1e-10, cols=(1, 3)))
+
+
 def test_msgram_widths_vs_exact_solve(gp):
     """The multi-shift CG (r update and B^T r, r . r on MFMA, ms_rmfma_kernel; partial
     sums across the chip) at 3, 7 and 11 columns (11 padded to 12 on the window SpMM)
