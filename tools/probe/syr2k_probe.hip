@@ -167,6 +167,102 @@ __global__ __launch_bounds__(256, 1) void rest_pipe(double* __restrict__ A, int6
   for (int e = 0; e < 64; ++e) Cp[coff + cidx(e)] = po[e >> 4][(e >> 2) & 3][e & 3];
 }
 
+// The same persistent tile loop with the operand slabs staged by LDS-DMA
+// (global_load_lds, 16 B per lane) into a ring of NBUF stages, NBUF - 1 of them in
+// flight across the raw barriers (counted vmcnt, never 0 inside a tile): no VGPRs
+// for staging, so the C tile's next values can be prefetched into registers. The
+// LDS image is lane-linear (row r = 8 chunk + lane / 8, 16-B slot lane % 8); the
+// slab swizzle moves to the source address (pair (slot ^ (r >> 1) & 7)), so the
+// fragment reads (slab_off) are unchanged.
+template <int KD, int NBUF>
+__global__ __launch_bounds__(256, 1) void rest_glds(double* __restrict__ A, int64_t lda,
+                                                    const double* __restrict__ U, int64_t ldu,
+                                                    int mt) {
+  __shared__ double lds[NBUF * 2 * STAGE];
+  constexpr int NS = KD / BK;
+  const int ntiles = (mt - 1) * mt / 2;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int wr = w >> 1, wc = w & 1, fr = lane & 15, fk = lane >> 4;
+  const int nmine = blockIdx.x < ntiles ? (ntiles - 1 - blockIdx.x) / gridDim.x + 1 : 0;
+  if (nmine == 0) return;
+  const int total = nmine * NS;
+  auto tile_of = [&](int it, int* I, int* J) {
+    int i, j;
+    tri_decode(blockIdx.x + it * gridDim.x, mt - 1, &i, &j);
+    *I = i + 1;
+    *J = j + 1;
+  };
+  // stage g -> its tile's operands at k0 = (g % NS) * BK into ring slot g % NBUF
+  auto issue = [&](int g) {
+    int I, J;
+    tile_of(g / NS, &I, &J);
+    const int k0 = (g % NS) * BK;
+    double* dA = lds + (g % NBUF) * 2 * STAGE;
+    double* dB = dA + STAGE;
+    const double* P1 = U + (int64_t)I * TS * ldu + k0;
+    const double* P2 = U + (int64_t)J * TS * ldu + KD / 2 + k0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int chunk = w + 4 * c;
+      const int r = 8 * chunk + (lane >> 3), slot = lane & 7;
+      const int pair = slot ^ ((r >> 1) & 7);
+      __builtin_amdgcn_global_load_lds(P1 + (int64_t)r * ldu + 2 * pair, dA + chunk * 128, 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(P2 + (int64_t)r * ldu + 2 * pair, dB + chunk * 128, 16, 0, 0);
+    }
+  };
+  const int64_t coff = (int64_t)(wr * 64 + fk) * lda + wc * 64 + fr;
+  d4 acc[4][4];
+  zero_tile(acc);
+  for (int g = 0; g < NBUF - 1 && g < total; ++g) issue(g);
+  for (int g = 0; g < total; ++g) {
+    // stage g landed: at most min(NBUF - 2, total - 1 - g) later stages (8 DMAs each) in flight
+    const int later = min(NBUF - 2, total - 1 - g);
+    if (later >= 2) __builtin_amdgcn_s_waitcnt(0x4F70);        // vmcnt(16)
+    else if (later == 1) __builtin_amdgcn_s_waitcnt(0x0F78);   // vmcnt(8)
+    else __builtin_amdgcn_s_waitcnt(0x0F70);                   // vmcnt(0)
+    __builtin_amdgcn_s_waitcnt(0xC07F);                        // lgkmcnt(0): stage g - 1 read
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (g + NBUF - 1 < total) issue(g + NBUF - 1);
+    const double* cA = lds + (g % NBUF) * 2 * STAGE;
+    const double* cB = cA + STAGE;
+#pragma unroll
+    for (int kk = 0; kk < BK / 4; ++kk) {
+      double a[4], b[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = cA[slab_off(wr * 64 + i * 16 + fr, kk * 4 + fk)];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = cB[slab_off(wc * 64 + j * 16 + fr, kk * 4 + fk)];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma64_neg(a[i], b[j], acc[i][j]);
+    }
+    if (g % NS == NS - 1) {
+      // the tile's epilogue: C += acc (read-modify-write), acc = 0
+      int I, J;
+      tile_of(g / NS, &I, &J);
+      double* C = A + (int64_t)I * TS * lda + (int64_t)J * TS + coff;
+      d4 cv[4][4];
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) cv[a][c][r] = C[(int64_t)(a * 16 + 4 * r) * lda + c * 16];
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            C[(int64_t)(a * 16 + 4 * r) * lda + c * 16] = cv[a][c][r] + acc[a][c][r];
+      zero_tile(acc);
+    }
+  }
+}
+
 // SYMM as shipped (gpmi_band.hip symm_kernel), and a timing-only variant that
 // reads every tile in the row-major (KFAST) layout: how much the transposed
 // (KSLOW, J > I) tiles cost.
@@ -287,6 +383,58 @@ int main(int argc, char** argv) {
   (void)0;
   const int kds[] = {256, 512};
   const bool symm_only = argc > 2 && std::string(argv[2]) == "symm";
+  if (argc > 2 && std::string(argv[2]) == "glds") {
+    // LDS-DMA ring against the register-staged pipeline (k = 256): equal results on
+    // the same C, then the rate at the look-ahead grid (224 = 256 - 32 free CUs) and 256
+    double *A1, *A2;
+    CK(hipMalloc(&A1, sizeof(double) * (size_t)n * n));
+    CK(hipMalloc(&A2, sizeof(double) * (size_t)n * n));
+    {
+      std::vector<double> h((size_t)n * n);
+      for (size_t i = 0; i < h.size(); ++i) h[i] = 1e-2 * ((i * 40503u) % 997) / 997.0;
+      CK(hipMemcpy(A1, h.data(), sizeof(double) * h.size(), hipMemcpyHostToDevice));
+      CK(hipMemcpy(A2, h.data(), sizeof(double) * h.size(), hipMemcpyHostToDevice));
+    }
+    const int mt = nt - 1;
+    hipLaunchKernelGGL(rest_pipe<256>, dim3(224), dim3(256), 0, 0, A1, (int64_t)n, U, ldu, mt);
+    hipLaunchKernelGGL((rest_glds<256, 4>), dim3(224), dim3(256), 0, 0, A2, (int64_t)n, U, ldu, mt);
+    CK(hipDeviceSynchronize());
+    {
+      std::vector<double> h1((size_t)n * n), h2((size_t)n * n);
+      CK(hipMemcpy(h1.data(), A1, sizeof(double) * h1.size(), hipMemcpyDeviceToHost));
+      CK(hipMemcpy(h2.data(), A2, sizeof(double) * h2.size(), hipMemcpyDeviceToHost));
+      double md = 0.0, mx = 0.0;
+      for (size_t i = 0; i < h1.size(); ++i) {
+        md = fmax(md, fabs(h1[i] - h2[i]));
+        mx = fmax(mx, fabs(h1[i]));
+      }
+      printf("glds vs pipe: max |diff| %.3e (max |C| %.3e)\n", md, mx);
+    }
+    const int ntiles = (mt - 1) * mt / 2;
+    const double fl = 2.0 * TS * TS * 256.0 * ntiles;
+    for (int g : {224, 256}) {
+      for (int kern = 0; kern < 3; ++kern) {
+        auto launch = [&]() {
+          if (kern == 0) hipLaunchKernelGGL(rest_pipe<256>, dim3(g), dim3(256), 0, 0, A1, (int64_t)n, U, ldu, mt);
+          else if (kern == 1) hipLaunchKernelGGL((rest_glds<256, 4>), dim3(g), dim3(256), 0, 0, A1, (int64_t)n, U, ldu, mt);
+          else hipLaunchKernelGGL((rest_glds<256, 3>), dim3(g), dim3(256), 0, 0, A1, (int64_t)n, U, ldu, mt);
+        };
+        launch();
+        CK(hipDeviceSynchronize());
+        CK(hipEventRecord(e0, 0));
+        for (int r = 0; r < 5; ++r) launch();
+        CK(hipEventRecord(e1, 0));
+        CK(hipEventSynchronize(e1));
+        float ms = 0;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        ms /= 5;
+        printf("%s grid=%d  %8.3f ms  %6.1f TF  %.3f of 78.6 (%.3f per busy CU)\n",
+               kern == 0 ? "pipe   " : kern == 1 ? "glds4  " : "glds3  ", g, ms, fl / ms * 1e-9,
+               fl / ms * 1e-9 / 78.6, fl / ms * 1e-9 / 78.6 * 256.0 / g);
+      }
+    }
+    return 0;
+  }
   if (!symm_only)
   for (int kern : {0, 3, 4, 5})
     for (int mt : mts)
