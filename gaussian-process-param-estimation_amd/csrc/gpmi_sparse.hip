@@ -531,6 +531,31 @@ __global__ __launch_bounds__(256) void col_dot_reduce_kernel(const double* __res
   if ((threadIdx.x & 63) == 0) out[e] = v;
 }
 
+// The same sums by one workgroup per output element, for many partial rows (the
+// window SpMM's p . q partials: one row per 64-row block, 4096 at cfg 5): thread t
+// sums rows t, t + 256, ... (eight loads in flight), then the four waves' sums in a
+// fixed order. (One wave per element took ~9.6 us there: 64 dependent-ish loads a lane.)
+__global__ __launch_bounds__(256) void col_dot_reduce_wg_kernel(const double* __restrict__ partial,
+                                                                int nblk, int ne,
+                                                                double* __restrict__ out) {
+  __shared__ double red[4];
+  const int e = blockIdx.x, t = threadIdx.x;
+  double a = 0.0;
+  int b = t;
+  for (; b + 7 * 256 < nblk; b += 8 * 256) {
+    double x[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) x[q] = partial[(int64_t)(b + q * 256) * ne + e];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) a += x[q];
+  }
+  for (; b < nblk; b += 256) a += partial[(int64_t)b * ne + e];
+  a = wave_sum(a);
+  if ((t & 63) == 0) red[t >> 6] = a;
+  __syncthreads();
+  if (t == 0) out[e] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
 // W[i][c] = alpha * W[i][c] - sum_{j<J} A_j[i][c] * H[j][c]   (H on the device)
 // W -= sum_j A_j diag(H_j): two consecutive elements per thread (16-byte loads when
 // the vector stride is even), the J vector loads issued four at a time (the same

@@ -58,6 +58,7 @@ constexpr int WIN_CS_HOST = 8;       // = WIN_CS
 __global__ void col_dot_partial_kernel(const double*, int64_t, const double*, int64_t, int,
                                        double*);
 __global__ void col_dot_reduce_kernel(const double*, int, int, int, double*);
+__global__ void col_dot_reduce_wg_kernel(const double*, int, int, double*);
 __global__ void col_gs_update_kernel(double*, const double*, int64_t, const double*, int, int64_t,
                                      int);
 __global__ void col_axpby_kernel(const double*, double*, const double*, const double*, int64_t,
@@ -1422,7 +1423,13 @@ static int msgram_impl(gpmi_sp* sp, const double* etas, int neta, const double* 
     if (rc1) return rc1;
     const double* pqin = pqpart;
     int pqn = NBLK;
-    if (pqb > 0) {
+    if (pqb >= 1024) {
+      hipLaunchKernelGGL(col_dot_reduce_wg_kernel, dim3(s), dim3(256), 0, str, pqpart, pqb, s,
+                         pqsum);
+      SP_LAUNCH("col_dot_reduce_wg_kernel");
+      pqin = pqsum;
+      pqn = 1;
+    } else if (pqb > 0) {
       hipLaunchKernelGGL(col_dot_reduce_kernel, dim3((s + 3) / 4), dim3(256), 0, str, pqpart, pqb,
                          1, s, pqsum);
       SP_LAUNCH("col_dot_reduce_kernel");
