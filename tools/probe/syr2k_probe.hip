@@ -167,6 +167,107 @@ __global__ __launch_bounds__(256, 1) void rest_pipe(double* __restrict__ A, int6
   for (int e = 0; e < 64; ++e) Cp[coff + cidx(e)] = po[e >> 4][(e >> 2) & 3][e & 3];
 }
 
+// rest_pipe with the operand loads issued TWO k-steps ahead (two register sets;
+// the LDS double buffer unchanged), paid for by storing each tile's results in one
+// burst at its end instead of spreading them over the next tile (no `po` registers).
+template <int KD>
+__global__ __launch_bounds__(256, 1) void rest_pipe2(double* __restrict__ A, int64_t lda,
+                                                     const double* __restrict__ U, int64_t ldu,
+                                                     int mt) {
+  __shared__ double smem[4 * GSTAGE];
+  constexpr int NS = KD / BK;
+  static_assert(NS % 2 == 0 && NS >= 2, "stage parity");
+  constexpr int PER = (64 + NS - 1) / NS;
+  const int ntiles = (mt - 1) * mt / 2;
+  int q = blockIdx.x;
+  if (q >= ntiles) return;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int wr = w >> 1, wc = w & 1, fr = lane & 15, fk = lane >> 4;
+  double* sA = smem;
+  double* sB = smem + 2 * GSTAGE;
+  auto tile_ptrs = [&](int qq, double** C, const double** P1, const double** P2) {
+    int i, j;
+    tri_decode(qq, mt - 1, &i, &j);
+    *C = A + (int64_t)(i + 1) * TS * lda + (int64_t)(j + 1) * TS;
+    *P1 = U + (int64_t)(i + 1) * TS * ldu;
+    *P2 = U + (int64_t)(j + 1) * TS * ldu + KD / 2;
+  };
+  const int64_t coff = (int64_t)(wr * 64 + fk) * lda + wc * 64 + fr;
+  auto cidx = [&](int e) -> int64_t {
+    return (int64_t)((e >> 4) * 16 + 4 * (e & 3)) * lda + ((e >> 2) & 3) * 16;
+  };
+  d4 acc[4][4], cn[4][4];
+  double* Cq;
+  const double *P1, *P2;
+  tile_ptrs(q, &Cq, &P1, &P2);
+  load_tile(Cq, lda, acc);
+  d2 ra[2][4], rb[2][4];   // register sets by stage parity
+  gl_op<KFAST>(P1, ldu, 0, ra[0]);
+  gl_op<KFAST>(P2, ldu, 0, rb[0]);
+  gl_op<KFAST>(P1, ldu, BK, ra[1]);
+  gl_op<KFAST>(P2, ldu, BK, rb[1]);
+  st_op<KFAST>(sA, ra[0]);
+  st_op<KFAST>(sB, rb[0]);
+  __syncthreads();
+  while (true) {
+    const int qn = q + gridDim.x;
+    const bool has_n = qn < ntiles;
+    double* Cn = nullptr;
+    const double *N1 = nullptr, *N2 = nullptr;
+    if (has_n) tile_ptrs(qn, &Cn, &N1, &N2);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const int cur = s & 1;
+      const double* cA = sA + cur * GSTAGE;
+      const double* cB = sB + cur * GSTAGE;
+      // stage s + 2 into the set stage s used (already in LDS)
+      if (s + 2 < NS) {
+        gl_op<KFAST>(P1, ldu, (s + 2) * BK, ra[cur]);
+        gl_op<KFAST>(P2, ldu, (s + 2) * BK, rb[cur]);
+      } else if (has_n) {
+        gl_op<KFAST>(N1, ldu, (s + 2 - NS) * BK, ra[cur]);
+        gl_op<KFAST>(N2, ldu, (s + 2 - NS) * BK, rb[cur]);
+      }
+      if (has_n) {
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+          const int e = s * PER + u;
+          if (e < 64) cn[e >> 4][(e >> 2) & 3][e & 3] = Cn[coff + cidx(e)];
+        }
+      }
+#pragma unroll
+      for (int kk = 0; kk < BK / 4; ++kk) {
+        double a[4], b[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a[i] = fr_op<KFAST>(cA, wr * 64 + i * 16 + fr, kk * 4 + fk);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) b[j] = fr_op<KFAST>(cB, wc * 64 + j * 16 + fr, kk * 4 + fk);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = mfma64_neg(a[i], b[j], acc[i][j]);
+      }
+      // stage s + 1 (loaded a step ago) into the other LDS buffer
+      if (s + 1 < NS || has_n) {
+        st_op<KFAST>(sA + (cur ^ 1) * GSTAGE, ra[cur ^ 1]);
+        st_op<KFAST>(sB + (cur ^ 1) * GSTAGE, rb[cur ^ 1]);
+      }
+      __syncthreads();
+    }
+#pragma unroll
+    for (int e = 0; e < 64; ++e) Cq[coff + cidx(e)] = acc[e >> 4][(e >> 2) & 3][e & 3];
+    if (!has_n) break;
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[a][c] = cn[a][c];
+    q = qn;
+    Cq = Cn;
+    P1 = N1;
+    P2 = N2;
+  }
+}
+
 // The same persistent tile loop with the operand slabs staged by LDS-DMA
 // (global_load_lds, 16 B per lane) into a ring of NBUF stages, NBUF - 1 of them in
 // flight across the raw barriers (counted vmcnt, never 0 inside a tile): no VGPRs
@@ -383,6 +484,29 @@ int main(int argc, char** argv) {
   (void)0;
   const int kds[] = {256, 512};
   const bool symm_only = argc > 2 && std::string(argv[2]) == "symm";
+  if (argc > 2 && std::string(argv[2]) == "noc") {
+    // the tile loop with and without its C tile traffic (k per tile 128 .. 1024)
+    const int mt = nt - 1, ntiles = (mt - 1) * mt / 2;
+    for (int kd : {128, 256, 512, 1024})
+      for (int kern = 0; kern < 2; ++kern) {
+        auto launch = [&]() {
+          if (kern) hipLaunchKernelGGL(rest_noc, dim3(512), dim3(256), 0, 0, A, (int64_t)n, U, ldu, mt, kd);
+          else hipLaunchKernelGGL(rest_base, dim3(512), dim3(256), 0, 0, A, (int64_t)n, U, ldu, mt, kd);
+        };
+        launch();
+        CK(hipDeviceSynchronize());
+        CK(hipEventRecord(e0, 0));
+        for (int r = 0; r < 5; ++r) launch();
+        CK(hipEventRecord(e1, 0));
+        CK(hipEventSynchronize(e1));
+        float ms = 0;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        ms /= 5;
+        const double fl = 2.0 * TS * TS * (double)kd * ntiles;
+        printf("%s k=%4d  %8.3f ms  %.3f of 78.6\n", kern ? "noC " : "base", kd, ms, fl / ms * 1e-9 / 78.6);
+      }
+    return 0;
+  }
   if (argc > 2 && std::string(argv[2]) == "glds") {
     // LDS-DMA ring against the register-staged pipeline (k = 256): equal results on
     // the same C, then the rate at the look-ahead grid (224 = 256 - 32 free CUs) and 256
@@ -397,7 +521,10 @@ int main(int argc, char** argv) {
     }
     const int mt = nt - 1;
     hipLaunchKernelGGL(rest_pipe<256>, dim3(224), dim3(256), 0, 0, A1, (int64_t)n, U, ldu, mt);
-    hipLaunchKernelGGL((rest_glds<256, 4>), dim3(224), dim3(256), 0, 0, A2, (int64_t)n, U, ldu, mt);
+    if (argc > 3 && std::string(argv[3]) == "pipe2")
+      hipLaunchKernelGGL(rest_pipe2<256>, dim3(224), dim3(256), 0, 0, A2, (int64_t)n, U, ldu, mt);
+    else
+      hipLaunchKernelGGL((rest_glds<256, 4>), dim3(224), dim3(256), 0, 0, A2, (int64_t)n, U, ldu, mt);
     CK(hipDeviceSynchronize());
     {
       std::vector<double> h1((size_t)n * n), h2((size_t)n * n);
@@ -408,14 +535,15 @@ int main(int argc, char** argv) {
         md = fmax(md, fabs(h1[i] - h2[i]));
         mx = fmax(mx, fabs(h1[i]));
       }
-      printf("glds vs pipe: max |diff| %.3e (max |C| %.3e)\n", md, mx);
+      printf("variant vs pipe: max |diff| %.3e (max |C| %.3e)\n", md, mx);
     }
     const int ntiles = (mt - 1) * mt / 2;
     const double fl = 2.0 * TS * TS * 256.0 * ntiles;
     for (int g : {224, 256}) {
-      for (int kern = 0; kern < 3; ++kern) {
+      for (int kern = 0; kern < 4; ++kern) {
         auto launch = [&]() {
-          if (kern == 0) hipLaunchKernelGGL(rest_pipe<256>, dim3(g), dim3(256), 0, 0, A1, (int64_t)n, U, ldu, mt);
+          if (kern == 3) hipLaunchKernelGGL(rest_pipe2<256>, dim3(g), dim3(256), 0, 0, A1, (int64_t)n, U, ldu, mt);
+          else if (kern == 0) hipLaunchKernelGGL(rest_pipe<256>, dim3(g), dim3(256), 0, 0, A1, (int64_t)n, U, ldu, mt);
           else if (kern == 1) hipLaunchKernelGGL((rest_glds<256, 4>), dim3(g), dim3(256), 0, 0, A1, (int64_t)n, U, ldu, mt);
           else hipLaunchKernelGGL((rest_glds<256, 3>), dim3(g), dim3(256), 0, 0, A1, (int64_t)n, U, ldu, mt);
         };
@@ -429,7 +557,7 @@ int main(int argc, char** argv) {
         CK(hipEventElapsedTime(&ms, e0, e1));
         ms /= 5;
         printf("%s grid=%d  %8.3f ms  %6.1f TF  %.3f of 78.6 (%.3f per busy CU)\n",
-               kern == 0 ? "pipe   " : kern == 1 ? "glds4  " : "glds3  ", g, ms, fl / ms * 1e-9,
+               kern == 0 ? "pipe   " : kern == 1 ? "glds4  " : kern == 2 ? "glds3  " : "pipe2  ", g, ms, fl / ms * 1e-9,
                fl / ms * 1e-9 / 78.6, fl / ms * 1e-9 / 78.6 * 256.0 / g);
       }
     }
