@@ -35,6 +35,22 @@ __global__ __launch_bounds__(256, 2) void rest_base(double* A, int64_t lda, cons
   }
 }
 
+// rest_base with the second workgroup of each CU (blockIdx >= 256) starting late by
+// ~half a tile (s_sleep), so that the two workgroups' tile prologues / epilogues
+// (C in and out, first stage) stop coinciding
+__global__ __launch_bounds__(256, 2) void rest_stagger(double* A, int64_t lda, const double* U,
+                                                       int64_t ldu, int mt, int kdim, int nap) {
+  __shared__ double smem[4 * GSTAGE];
+  if (blockIdx.x >= 256)
+    for (int i = 0; i < nap; ++i) __builtin_amdgcn_s_sleep(127);
+  const int ntiles = (mt - 1) * mt / 2;
+  for (int q = blockIdx.x; q < ntiles; q += gridDim.x) {
+    int i, j;
+    tri_decode(q, mt - 1, &i, &j);
+    tile_k(A, lda, U, ldu, i + 1, j + 1, kdim, smem);
+  }
+}
+
 // no C traffic: the same MFMA work with zero accumulators, result not stored
 // unless it is NaN (keeps the compiler from dropping it)
 __global__ __launch_bounds__(256, 2) void rest_noc(double* A, int64_t lda, const double* U,
@@ -484,6 +500,27 @@ int main(int argc, char** argv) {
   (void)0;
   const int kds[] = {256, 512};
   const bool symm_only = argc > 2 && std::string(argv[2]) == "symm";
+  if (argc > 2 && std::string(argv[2]) == "stagger") {
+    const int mt = nt - 1, ntiles = (mt - 1) * mt / 2;
+    for (int nap : {0, 4, 8, 16, 24, 32})
+      for (int kd : {256}) {
+        auto launch = [&]() {
+          hipLaunchKernelGGL(rest_stagger, dim3(512), dim3(256), 0, 0, A, (int64_t)n, U, ldu, mt, kd, nap);
+        };
+        launch();
+        CK(hipDeviceSynchronize());
+        CK(hipEventRecord(e0, 0));
+        for (int r = 0; r < 5; ++r) launch();
+        CK(hipEventRecord(e1, 0));
+        CK(hipEventSynchronize(e1));
+        float ms = 0;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        ms /= 5;
+        const double fl = 2.0 * TS * TS * (double)kd * ntiles;
+        printf("stagger nap=%2d (x 127 x 64 clk) k=%4d  %8.3f ms  %.3f of 78.6\n", nap, kd, ms, fl / ms * 1e-9 / 78.6);
+      }
+    return 0;
+  }
   if (argc > 2 && std::string(argv[2]) == "noc") {
     // the tile loop with and without its C tile traffic (k per tile 128 .. 1024)
     const int mt = nt - 1, ntiles = (mt - 1) * mt / 2;
