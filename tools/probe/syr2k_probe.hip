@@ -75,7 +75,15 @@ __global__ __launch_bounds__(256, 2) void rest_noc(double* A, int64_t lda, const
 // stages tile q + grid's first operand slab, so the C traffic is spread over the
 // MFMA loop instead of a load and a store phase per tile that every workgroup
 // of the launch runs at the same time.
-template <int KD>
+// the previous tile's result values stored by an inline-asm global_store (hipcc
+// does not count it, so the wait for this step's operand loads before their LDS
+// store is not made conservative by a store pending in the same counter); issued
+// BEFORE the step's loads, so vmcnt(N later loads) stays exact
+__device__ __forceinline__ void st_asm(double* p, double v) {
+  asm volatile("global_store_dwordx2 %0, %1, off\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+}
+
+template <int KD, bool SB = false, bool ASM = false>
 __global__ __launch_bounds__(256, 1) void rest_pipe(double* __restrict__ A, int64_t lda,
                                                     const double* __restrict__ U, int64_t ldu,
                                                     int mt) {
@@ -125,6 +133,13 @@ __global__ __launch_bounds__(256, 1) void rest_pipe(double* __restrict__ A, int6
       const double* cA = sA + cur * GSTAGE;
       const double* cB = sB + cur * GSTAGE;
       const bool ld = s + 1 < NS || has_n;
+      if (ASM && has_p) {
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+          const int e = s * PER + u;
+          if (e < 64) st_asm(Cp + coff + cidx(e), po[e >> 4][(e >> 2) & 3][e & 3]);
+        }
+      }
       if (s + 1 < NS) {
         gl_op<KFAST>(P1, ldu, (s + 1) * BK, ra);
         gl_op<KFAST>(P2, ldu, (s + 1) * BK, rb);
@@ -132,6 +147,9 @@ __global__ __launch_bounds__(256, 1) void rest_pipe(double* __restrict__ A, int6
         gl_op<KFAST>(N1, ldu, 0, ra);
         gl_op<KFAST>(N2, ldu, 0, rb);
       }
+      // SB: keep the C traffic after the operand loads in the instruction stream, so
+      // the wait for the operands (before their LDS store) does not also wait for it
+      if (SB) __builtin_amdgcn_sched_barrier(0);
       if (has_n) {
 #pragma unroll
         for (int u = 0; u < PER; ++u) {
@@ -139,7 +157,8 @@ __global__ __launch_bounds__(256, 1) void rest_pipe(double* __restrict__ A, int6
           if (e < 64) cn[e >> 4][(e >> 2) & 3][e & 3] = Cn[coff + cidx(e)];
         }
       }
-      if (has_p) {
+      if (SB) __builtin_amdgcn_sched_barrier(0);
+      if (!ASM && has_p) {
 #pragma unroll
         for (int u = 0; u < PER; ++u) {
           const int e = s * PER + u;
@@ -181,6 +200,82 @@ __global__ __launch_bounds__(256, 1) void rest_pipe(double* __restrict__ A, int6
   }
 #pragma unroll
   for (int e = 0; e < 64; ++e) Cp[coff + cidx(e)] = po[e >> 4][(e >> 2) & 3][e & 3];
+}
+
+// rest_pipe without any C traffic: the accumulators run on across all of a
+// workgroup's tiles (no per-tile load / store) and are stored once at the end; the
+// operand staging and the k-loop exactly as rest_pipe
+template <int KD>
+__global__ __launch_bounds__(256, 1) void rest_pipe_noc(double* __restrict__ A, int64_t lda,
+                                                        const double* __restrict__ U, int64_t ldu,
+                                                        int mt) {
+  __shared__ double smem[4 * GSTAGE];
+  constexpr int NS = KD / BK;
+  const int ntiles = (mt - 1) * mt / 2;
+  int q = blockIdx.x;
+  if (q >= ntiles) return;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int wr = w >> 1, wc = w & 1, fr = lane & 15, fk = lane >> 4;
+  double* sA = smem;
+  double* sB = smem + 2 * GSTAGE;
+  auto tile_ptrs = [&](int qq, const double** P1, const double** P2) {
+    int i, j;
+    tri_decode(qq, mt - 1, &i, &j);
+    *P1 = U + (int64_t)(i + 1) * TS * ldu;
+    *P2 = U + (int64_t)(j + 1) * TS * ldu + KD / 2;
+  };
+  d4 acc[4][4];
+  zero_tile(acc);
+  const double *P1, *P2;
+  tile_ptrs(q, &P1, &P2);
+  d2 ra[4], rb[4];
+  gl_op<KFAST>(P1, ldu, 0, ra);
+  gl_op<KFAST>(P2, ldu, 0, rb);
+  st_op<KFAST>(sA, ra);
+  st_op<KFAST>(sB, rb);
+  __syncthreads();
+  while (true) {
+    const int qn = q + gridDim.x;
+    const bool has_n = qn < ntiles;
+    const double *N1 = nullptr, *N2 = nullptr;
+    if (has_n) tile_ptrs(qn, &N1, &N2);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const int cur = s & 1;
+      const double* cA = sA + cur * GSTAGE;
+      const double* cB = sB + cur * GSTAGE;
+      const bool ld = s + 1 < NS || has_n;
+      if (s + 1 < NS) {
+        gl_op<KFAST>(P1, ldu, (s + 1) * BK, ra);
+        gl_op<KFAST>(P2, ldu, (s + 1) * BK, rb);
+      } else if (has_n) {
+        gl_op<KFAST>(N1, ldu, 0, ra);
+        gl_op<KFAST>(N2, ldu, 0, rb);
+      }
+#pragma unroll
+      for (int kk = 0; kk < BK / 4; ++kk) {
+        double a[4], b[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a[i] = fr_op<KFAST>(cA, wr * 64 + i * 16 + fr, kk * 4 + fk);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) b[j] = fr_op<KFAST>(cB, wc * 64 + j * 16 + fr, kk * 4 + fk);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = mfma64_neg(a[i], b[j], acc[i][j]);
+      }
+      if (ld) {
+        st_op<KFAST>(sA + (cur ^ 1) * GSTAGE, ra);
+        st_op<KFAST>(sB + (cur ^ 1) * GSTAGE, rb);
+      }
+      __syncthreads();
+    }
+    if (!has_n) break;
+    q = qn;
+    P1 = N1;
+    P2 = N2;
+  }
+  store_tile(A + (int64_t)blockIdx.x * TS, lda, acc, 1.0);
 }
 
 // rest_pipe with the operand loads issued TWO k-steps ahead (two register sets;
@@ -558,7 +653,9 @@ int main(int argc, char** argv) {
     }
     const int mt = nt - 1;
     hipLaunchKernelGGL(rest_pipe<256>, dim3(224), dim3(256), 0, 0, A1, (int64_t)n, U, ldu, mt);
-    if (argc > 3 && std::string(argv[3]) == "pipe2")
+    if (argc > 3 && std::string(argv[3]) == "asm")
+      hipLaunchKernelGGL((rest_pipe<256, false, true>), dim3(224), dim3(256), 0, 0, A2, (int64_t)n, U, ldu, mt);
+    else if (argc > 3 && std::string(argv[3]) == "pipe2")
       hipLaunchKernelGGL(rest_pipe2<256>, dim3(224), dim3(256), 0, 0, A2, (int64_t)n, U, ldu, mt);
     else
       hipLaunchKernelGGL((rest_glds<256, 4>), dim3(224), dim3(256), 0, 0, A2, (int64_t)n, U, ldu, mt);
@@ -577,9 +674,12 @@ int main(int argc, char** argv) {
     const int ntiles = (mt - 1) * mt / 2;
     const double fl = 2.0 * TS * TS * 256.0 * ntiles;
     for (int g : {224, 256}) {
-      for (int kern = 0; kern < 4; ++kern) {
+      for (int kern = 0; kern < 7; ++kern) {
         auto launch = [&]() {
-          if (kern == 3) hipLaunchKernelGGL(rest_pipe2<256>, dim3(g), dim3(256), 0, 0, A1, (int64_t)n, U, ldu, mt);
+          if (kern == 4) hipLaunchKernelGGL(rest_pipe_noc<256>, dim3(g), dim3(256), 0, 0, A1, (int64_t)n, U, ldu, mt);
+          else if (kern == 5) hipLaunchKernelGGL((rest_pipe<256, true>), dim3(g), dim3(256), 0, 0, A1, (int64_t)n, U, ldu, mt);
+          else if (kern == 6) hipLaunchKernelGGL((rest_pipe<256, false, true>), dim3(g), dim3(256), 0, 0, A1, (int64_t)n, U, ldu, mt);
+          else if (kern == 3) hipLaunchKernelGGL(rest_pipe2<256>, dim3(g), dim3(256), 0, 0, A1, (int64_t)n, U, ldu, mt);
           else if (kern == 0) hipLaunchKernelGGL(rest_pipe<256>, dim3(g), dim3(256), 0, 0, A1, (int64_t)n, U, ldu, mt);
           else if (kern == 1) hipLaunchKernelGGL((rest_glds<256, 4>), dim3(g), dim3(256), 0, 0, A1, (int64_t)n, U, ldu, mt);
           else hipLaunchKernelGGL((rest_glds<256, 3>), dim3(g), dim3(256), 0, 0, A1, (int64_t)n, U, ldu, mt);
@@ -594,7 +694,7 @@ int main(int argc, char** argv) {
         CK(hipEventElapsedTime(&ms, e0, e1));
         ms /= 5;
         printf("%s grid=%d  %8.3f ms  %6.1f TF  %.3f of 78.6 (%.3f per busy CU)\n",
-               kern == 0 ? "pipe   " : kern == 1 ? "glds4  " : kern == 2 ? "glds3  " : "pipe2  ", g, ms, fl / ms * 1e-9,
+               kern == 0 ? "pipe   " : kern == 1 ? "glds4  " : kern == 2 ? "glds3  " : kern == 3 ? "pipe2  " : kern == 4 ? "pipenoC" : kern == 5 ? "pipeSB " : "pipeASM", g, ms, fl / ms * 1e-9,
                fl / ms * 1e-9 / 78.6, fl / ms * 1e-9 / 78.6 * 256.0 / g);
       }
     }
