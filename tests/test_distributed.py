@@ -304,7 +304,15 @@ def test_der1_sweep_error_raises_on_every_rank_gloo():
 
 
 class _FakeSparseGram(_FakeSparse):
+    rhs_cols = 0
+
+    def set_rhs(self, B):   # the resident block (gpmi_sp_set_rhs) stand-in
+        self._rhs = numpy.array(B, dtype=float)
+        self.rhs_cols = self._rhs.shape[1]
+
     def msgram(self, etas, R, rtol=1e-6, maxiter=None, cols=None):
+        if R is None:
+            R = self._rhs
         n = self.K.shape[0]
         G = numpy.array([R.T @ numpy.linalg.solve(self.K + e * numpy.eye(n), R)
                          for e in etas])
@@ -317,30 +325,37 @@ class _SparseMixedGram(_SparseMixed):
         self.sop = _FakeSparseGram(K, 12)
 
 
-def _slq_gram_worker(rank, world, port, etas, out_q):
+def _slq_gram_worker(rank, world, port, etas, out_q, resident=False):
     os.environ['MASTER_ADDR'] = '127.0.0.1'
     os.environ['MASTER_PORT'] = str(port)
     dist.init_process_group('gloo', rank=rank, world_size=world)
     from gaussian_proc.sweep import slq_gram_sweep
     K, X, z = _problem()
     R = numpy.column_stack([X, z])
-    out_q.put((rank, slq_gram_sweep(_SparseMixedGram(K + 0.5 * numpy.eye(K.shape[0])), etas, R)))
+    op = _SparseMixedGram(K + 0.5 * numpy.eye(K.shape[0]))
+    if resident:
+        op.sop.set_rhs(R)   # the bench's form: [X z] resident, the sweep given R = None
+        R = None
+    out_q.put((rank, slq_gram_sweep(op, etas, R)))
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_slq_gram_sweep_gloo():
+@pytest.mark.parametrize('resident', [False, True])
+def test_slq_gram_sweep_gloo(resident):
     """slq_gram_sweep: the probe-sharded SLQ curves (all-gathered, equal on every
     rank) and the multi-shift Gram blocks computed together (second host thread),
     the Gram split by right-hand-side columns over the ranks and all-gathered after
     the Lanczos; each rank's eta block of the result, whose union is the
-    single-process result."""
+    single-process result. ``resident``: the right-hand sides made resident first
+    (sop.set_rhs) and the sweep given R = None, as the bench runs it."""
     from gaussian_proc.sweep import slq_gram_sweep
     etas = numpy.array([0.5, 1.0, 2.0, 4.0, 8.0])
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_slq_gram_worker, args=(r, 2, port, etas, q)) for r in range(2)]
+    procs = [ctx.Process(target=_slq_gram_worker, args=(r, 2, port, etas, q, resident))
+             for r in range(2)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=120) for _ in range(2)], key=lambda r: r[0])
