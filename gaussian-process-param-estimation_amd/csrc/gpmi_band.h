@@ -41,7 +41,8 @@ constexpr int BAND_ULD = 384;      // U = [W | V | W]
 // CUs the pipelined look-ahead SYR2K (one workgroup per CU) leaves to the next panel's
 // CholeskyQR chain, whose single-workgroup kernels need a whole CU (N = 16384:
 // 16 171 ms, 24-28 172-173, 32 153, 36 153, 40 154, 48 155, 64 158; the capped
-// two-per-CU SYR2K 160)
+// two-per-CU SYR2K 160). A filler launch gives them back to the update once the
+// chain ends; with it: 24 164, 32 139.2-139.6, 40 140.4, 48 140.4, 64 140.1 ms.
 constexpr int LA_FREE = 32;
 constexpr int BAND_MAX_NPAD = HH_MAXG * HH_ROWS;
 
@@ -49,7 +50,7 @@ __global__ void hh_col_kernel(double* P, int64_t lda, int m, int c, double* part
                               double* tau);
 __global__ void hh_panel_kernel(double* P, int64_t lda, int m, double* part, double* pivrow,
                                 unsigned* counter, double* tau, int* err, unsigned spin_limit,
-                                const int* guard);
+                                const int* guard, double* Uv, int64_t ldu);
 __global__ void vcopy_kernel(const double* P, int64_t lda, int m, double* U, int64_t ldu);
 __global__ void tn_partial_kernel(const double* P1, int64_t ld1, const double* P2, int64_t ld2,
                                   int m, double* part, const int* only_if);
@@ -70,7 +71,7 @@ __global__ void syr2k_kernel(double* A, int64_t lda, const double* U, int64_t ld
 __global__ void syr2k_rest_kernel(double* A, int64_t lda, const double* U, int64_t ldu, int tr0,
                                   int mt, const uint32_t* order);
 __global__ void syr2k_pipe_kernel(double* A, int64_t lda, const double* U, int64_t ldu, int tr0,
-                                  int mt);
+                                  int mt, int* cnt, int nmain, int filler);
 __global__ void bcr_f0_kernel(const double* Ab, int64_t lda, double* F0);
 __global__ void bcr_chol_kernel(const double* Ab, int64_t lda, const double* etas, int lvl,
                                 int first, const double* Din, int64_t sD, const double* Yin,

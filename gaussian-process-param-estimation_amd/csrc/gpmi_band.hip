@@ -187,15 +187,42 @@ __global__ __launch_bounds__(HH_THREADS) void hh_panel_kernel(double* __restrict
                                                               double* __restrict__ tau,
                                                               int* __restrict__ err,
                                                               unsigned spin_limit,
-                                                              const int* __restrict__ guard) {
-  // guarded form (after a CholeskyQR panel): run only if that panel failed
-  if (guard && !__hip_atomic_load(guard, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
-  extern __shared__ double dyn_lds[];   // sized by the host to keep one workgroup per CU
-  double(*sacc)[HH_PART_LD] = reinterpret_cast<double(*)[HH_PART_LD]>(dyn_lds);
-  __shared__ int s_bail;
+                                                              const int* __restrict__ guard,
+                                                              double* __restrict__ Uv,
+                                                              int64_t ldu) {
   const int G = gridDim.x, g = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int j0 = lane, j1 = lane + 64;
   const int rbase = g * HH_ROWS + w * HH_RPW;
+  // the panel's reflectors into U[.][128:256] (vcopy_kernel's layout), from P's rows
+  // (a CholeskyQR panel) or from the registers (this kernel's own)
+  auto copy_v = [&](const double* p0, const double* p1) {
+#pragma unroll
+    for (int q = 0; q < HH_RPW; ++q) {
+      const int i = rbase + q;
+      if (i < m) {
+        double* u = Uv + (int64_t)i * ldu + TS;
+        u[j0] = i > j0 ? p0[q] : (i == j0 ? 1.0 : 0.0);
+        u[j1] = i > j1 ? p1[q] : (i == j1 ? 1.0 : 0.0);
+      }
+    }
+  };
+  // guarded form (after a CholeskyQR panel): run only if that panel failed
+  if (guard && !__hip_atomic_load(guard, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+    if (Uv) {
+      double v0[HH_RPW], v1[HH_RPW];
+#pragma unroll
+      for (int q = 0; q < HH_RPW; ++q) {
+        const int i = rbase + q;
+        v0[q] = i < m ? P[(int64_t)i * lda + j0] : 0.0;
+        v1[q] = i < m ? P[(int64_t)i * lda + j1] : 0.0;
+      }
+      copy_v(v0, v1);
+    }
+    return;
+  }
+  extern __shared__ double dyn_lds[];   // sized by the host to keep one workgroup per CU
+  double(*sacc)[HH_PART_LD] = reinterpret_cast<double(*)[HH_PART_LD]>(dyn_lds);
+  __shared__ int s_bail;
   double p0[HH_RPW], p1[HH_RPW];
 #pragma unroll
   for (int q = 0; q < HH_RPW; ++q) {
@@ -348,6 +375,7 @@ __global__ __launch_bounds__(HH_THREADS) void hh_panel_kernel(double* __restrict
       row[j1] = p1[q];
     }
   }
+  if (Uv) copy_v(p0, p1);
 }
 
 // U[r0 + i][128 + q] = V[i][q] (unit lower trapezoidal), i < m.
@@ -491,19 +519,20 @@ __global__ __launch_bounds__(256) void psum_kernel(const double* __restrict__ Xp
 }
 
 // The serial steps between the SYMM and the look-ahead on quadrant workgroups
-// (blockIdx.y = the 64 x 64 quadrant, gemm_quad): each is one 128^3 product per output
+// (blockIdx.y = the 64 x 64 quadrant, gemm_quad2): each is one 128^3 product per output
 // tile, whose MFMA chain bounds one workgroup (~14 us at the CU's fp64 rate plus the
-// staging); four workgroups per tile run a quarter of it each.
+// staging); four workgroups per tile run a quarter of it each, all operand loads in
+// flight at once.
 // X2_I = X_I T (out of place: the quadrants of a row read all of X_I).
 __global__ __launch_bounds__(256, 2) void xt_q_kernel(const double* __restrict__ X,
                                                       const double* __restrict__ T,
                                                       double* __restrict__ X2) {
-  __shared__ double smem[4 * GSTAGE];
+  __shared__ double smem[Q2_SMEM];
   const int q = blockIdx.y;
   const int64_t off = (int64_t)blockIdx.x * TS * TS;
   d4 acc[2][2];
   zero_quad(acc);
-  gemm_quad<KFAST, KSLOW, false>(X + off, TS, T, TS, TS, smem, acc, q >> 1, q & 1);
+  gemm_quad2<KFAST, KSLOW, false, TS>(X + off, TS, T, TS, smem, acc, q >> 1, q & 1);
   store_quad(X2 + off, TS, acc, 1.0, q >> 1, q & 1);
 }
 
@@ -513,13 +542,13 @@ __global__ __launch_bounds__(256, 2) void tn_partial_q_kernel(const double* __re
                                                               const double* __restrict__ P2,
                                                               int64_t ld2, int m,
                                                               double* __restrict__ part) {
-  __shared__ double smem[4 * GSTAGE];
+  __shared__ double smem[Q2_SMEM];
   const int ch = blockIdx.x, q = blockIdx.y;
-  const int i0 = ch * TN_CH, kd = min(TN_CH, m - i0);
+  const int i0 = ch * TN_CH;   // (m is a multiple of TN_CH = 128)
   d4 acc[2][2];
   zero_quad(acc);
-  gemm_quad<KSLOW, KSLOW, false>(P1 + (int64_t)i0 * ld1, ld1, P2 + (int64_t)i0 * ld2, ld2, kd,
-                                 smem, acc, q >> 1, q & 1);
+  gemm_quad2<KSLOW, KSLOW, false, TN_CH>(P1 + (int64_t)i0 * ld1, ld1, P2 + (int64_t)i0 * ld2,
+                                         ld2, smem, acc, q >> 1, q & 1);
   store_quad(part + (int64_t)ch * TS * TS, TS, acc, 1.0, q >> 1, q & 1);
 }
 
@@ -527,11 +556,11 @@ __global__ __launch_bounds__(256, 2) void tn_partial_q_kernel(const double* __re
 __global__ __launch_bounds__(256) void z_q_kernel(const double* __restrict__ T,
                                                   const double* __restrict__ M,
                                                   double* __restrict__ Zh) {
-  __shared__ double smem[4 * GSTAGE];
+  __shared__ double smem[Q2_SMEM];
   const int q = blockIdx.x;
   d4 acc[2][2];
   zero_quad(acc);
-  gemm_quad<KSLOW, KSLOW, false>(T, TS, M, TS, TS, smem, acc, q >> 1, q & 1);
+  gemm_quad2<KSLOW, KSLOW, false, TS>(T, TS, M, TS, smem, acc, q >> 1, q & 1);
   store_quad(Zh, TS, acc, 0.5, q >> 1, q & 1);
 }
 
@@ -539,12 +568,12 @@ __global__ __launch_bounds__(256) void z_q_kernel(const double* __restrict__ T,
 __global__ __launch_bounds__(256, 2) void w_q_kernel(const double* __restrict__ X,
                                                      double* __restrict__ U, int64_t ldu,
                                                      const double* __restrict__ Zh) {
-  __shared__ double smem[4 * GSTAGE];
+  __shared__ double smem[Q2_SMEM];
   const int il = blockIdx.x, q = blockIdx.y;
   double* Ui = U + (int64_t)il * TS * ldu;
   d4 acc[2][2];
   load_quad(X + (int64_t)il * TS * TS, TS, acc, q >> 1, q & 1);
-  gemm_quad<KFAST, KSLOW, true>(Ui + TS, ldu, Zh, TS, TS, smem, acc, q >> 1, q & 1);
+  gemm_quad2<KFAST, KSLOW, true, TS>(Ui + TS, ldu, Zh, TS, smem, acc, q >> 1, q & 1);
   store_quad(Ui, ldu, acc, 1.0, q >> 1, q & 1);
   store_quad(Ui + 2 * TS, ldu, acc, 1.0, q >> 1, q & 1);
 }
@@ -554,13 +583,14 @@ __global__ __launch_bounds__(256, 2) void w_q_kernel(const double* __restrict__ 
 __global__ __launch_bounds__(256, 2) void syr2k_col_q_kernel(double* __restrict__ A, int64_t lda,
                                                              const double* __restrict__ U,
                                                              int64_t ldu, int tr0) {
-  __shared__ double smem[4 * GSTAGE];
+  __shared__ double smem[Q2_SMEM];
   const int I = tr0 + blockIdx.x, q = blockIdx.y;
   double* C = A + (int64_t)I * TS * lda + (int64_t)tr0 * TS;
   d4 acc[2][2];
   load_quad(C, lda, acc, q >> 1, q & 1);
-  gemm_quad<KFAST, KFAST, true>(U + (int64_t)I * TS * ldu, ldu, U + (int64_t)tr0 * TS * ldu + TS,
-                                ldu, 2 * TS, smem, acc, q >> 1, q & 1);
+  gemm_quad2<KFAST, KFAST, true, 2 * TS>(U + (int64_t)I * TS * ldu, ldu,
+                                         U + (int64_t)tr0 * TS * ldu + TS, ldu, smem, acc,
+                                         q >> 1, q & 1);
   store_quad(C, lda, acc, 1.0, q >> 1, q & 1);
 }
 
@@ -627,17 +657,38 @@ __global__ __launch_bounds__(256, 2) void syr2k_rest_kernel(double* __restrict__
 // values of tile q + grid are loaded and 4 of tile q - grid's results are stored per
 // step, and the last step stages tile q + grid's first operand slab. Tiles as
 // syr2k_rest_kernel (the triangle right of tile column 0, from tile row tr0 + 1).
+//
+// With cnt (dynamic tiles): the launch's workgroup b starts on tile b (filler = 0)
+// and every further tile is nmain + a ticket of *cnt, drawn by thread 0 half-way
+// through the tile before the one it is for and passed on through LDS, so the
+// atomic's latency stays off the loop. A filler launch (filler = 1, on the chain's
+// stream after the chain) draws every tile from *cnt: the CUs the chain had to
+// itself join the update once it ends. *cnt is zeroed before the launch.
 __global__ __launch_bounds__(256, 1) void syr2k_pipe_kernel(double* __restrict__ A, int64_t lda,
                                                             const double* __restrict__ U,
-                                                            int64_t ldu, int tr0, int mt) {
-  __shared__ double smem[4 * GSTAGE];
+                                                            int64_t ldu, int tr0, int mt,
+                                                            int* __restrict__ cnt, int nmain,
+                                                            int filler) {
+  __shared__ double smem[4 * GSTAGE + 2];
+  int* stk = reinterpret_cast<int*>(smem + 4 * GSTAGE);   // [0] next ticket, [1] first
   constexpr int KD = 2 * TS;
   constexpr int NS = KD / BK;
   constexpr int PER = (64 + NS - 1) / NS;   // C values per lane per step
   const int ntiles = (mt - 1) * mt / 2;
-  int q = blockIdx.x;
-  if (q >= ntiles) return;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  int q = blockIdx.x, qn = q + gridDim.x;
+  if (cnt) {
+    if (t == 0) {
+      const int a = filler ? nmain + atomicAdd(cnt, 1) : q;
+      stk[1] = a;
+      stk[0] = a < ntiles ? nmain + atomicAdd(cnt, 1) : ntiles;
+    }
+    __syncthreads();
+    q = stk[1];
+    qn = stk[0];
+    __syncthreads();
+  }
+  if (q >= ntiles) return;
   const int wr = w >> 1, wc = w & 1, fr = lane & 15, fk = lane >> 4;
   double* sA = smem;
   double* sB = smem + 2 * GSTAGE;
@@ -666,8 +717,8 @@ __global__ __launch_bounds__(256, 1) void syr2k_pipe_kernel(double* __restrict__
   __syncthreads();
   double* Cp = nullptr;
   bool has_p = false;
+  int tk = 0;
   while (true) {
-    const int qn = q + gridDim.x;
     const bool has_n = qn < ntiles;
     double* Cn = nullptr;
     const double *N1 = nullptr, *N2 = nullptr;
@@ -678,6 +729,12 @@ __global__ __launch_bounds__(256, 1) void syr2k_pipe_kernel(double* __restrict__
       const double* cA = sA + cur * GSTAGE;
       const double* cB = sB + cur * GSTAGE;
       const bool ld = s + 1 < NS || has_n;
+      // the ticket before this step's loads (its return is waited for at once: the
+      // value goes to an AGPR; ~1 us of wave 0 per tile)
+      if (cnt && t == 0 && has_n) {
+        if (s == NS / 2) tk = atomicAdd(cnt, 1);
+        if (s == NS - 1) stk[0] = nmain + tk;
+      }
       if (s + 1 < NS) {
         gl_op<KFAST>(P1, ldu, (s + 1) * BK, ra);
         gl_op<KFAST>(P2, ldu, (s + 1) * BK, rb);
@@ -728,6 +785,7 @@ __global__ __launch_bounds__(256, 1) void syr2k_pipe_kernel(double* __restrict__
     has_p = true;
     if (!has_n) break;
     q = qn;
+    qn = cnt ? stk[0] : q + gridDim.x;   // (written before the last step's barrier)
     Cq = Cn;
     P1 = N1;
     P2 = N2;

@@ -124,7 +124,8 @@ struct gpmi_band {
   double* cqS = nullptr;     // [nt][128] reconstruction signs
   double* cqscr = nullptr;   // [nt][128][128]
   int* cqflag = nullptr;     // [nt][8]: [0..2] first-order flag per pass, [3] CholeskyQR
-                             // succeeded, [4] failed (the guarded Householder panel ran)
+                             // succeeded, [4] failed (the guarded Householder panel ran),
+                             // [6] the look-ahead SYR2K's tile tickets
   int cq_panel_fallbacks = 0;   // panels factored by the guarded Householder panel, or
                                 // (past its single-launch size) by per-column launches
   int cq_host_checks = 0;       // panels past the single-launch size whose flag the host read
@@ -163,6 +164,7 @@ struct gpmi_band {
   double* cqW = nullptr;     // [nt][128][128]
   hipEvent_t ev_rc = nullptr;
   std::vector<char> t_from_q;
+  std::vector<char> v_in_u;   // v_in_u[j]: panel j's reflectors are in U already
   double cq_fo[3] = {0.0, 1e-4, 3e-8};   // first-order thresholds on ||G - I||_F
   int cap = 0;
   int nrhs = 0;
@@ -363,10 +365,12 @@ int cq_guard(gpmi_band* b, int j, hipStream_t st) {
   int* fl = b->cqflag + 8 * j;
   const int G = (m + HH_ROWS - 1) / HH_ROWS;
   if (G <= b->panel_maxg) {
+    // (it also copies the panel's reflectors into U, vcopy_kernel's work)
     hipLaunchKernelGGL(hh_panel_kernel, dim3(G), dim3(HH_THREADS), HH_PANEL_LDS, st, P, np, m,
                        b->part, b->pivrow, b->ctr, b->tau + (int64_t)j * TS, b->err,
-                       b->spin_limit, fl + 4);
+                       b->spin_limit, fl + 4, b->U + r0 * BAND_ULD, (int64_t)BAND_ULD);
     BD_LAUNCH("hh_panel_kernel");
+    b->v_in_u[j] = 1;
   } else {
     int failed = 0;
     BD_TRY(hipMemcpyAsync(&failed, fl + 4, sizeof(int), hipMemcpyDeviceToHost, st));
@@ -405,7 +409,8 @@ int panel_qr(gpmi_band* b, int j, hipStream_t st, int mode, bool* guard_deferred
     // one launch per panel (rows in registers, in-launch reductions)
     BD_TRY(hipMemsetAsync(b->ctr, 0, 512, st));
     hipLaunchKernelGGL(hh_panel_kernel, dim3(G), dim3(HH_THREADS), HH_PANEL_LDS, st, P, np, m,
-                       b->part, b->pivrow, b->ctr, tau, b->err, b->spin_limit, nullptr);
+                       b->part, b->pivrow, b->ctr, tau, b->err, b->spin_limit, nullptr, nullptr,
+                       (int64_t)0);
     BD_LAUNCH("hh_panel_kernel");
   } else {
     for (int c = -1; c < TS; ++c) {
@@ -442,6 +447,7 @@ int band_reduce_pass(gpmi_band* b, const double* K, const std::vector<double>* y
   }
   BD_TRY(hipMemcpyAsync(b->Ab, K, sizeof(double) * np * np, hipMemcpyDeviceToDevice, s));
   std::fill(b->t_from_q.begin(), b->t_from_q.end(), 0);
+  std::fill(b->v_in_u.begin(), b->v_in_u.end(), 0);
   const bool la = mode != 2 && b->lookahead && b->s_pan;
   bool ahead = false;   // panel j already factored by the previous look-ahead
   for (int j = 0; j + 1 < nt; ++j) {
@@ -456,9 +462,11 @@ int band_reduce_pass(gpmi_band* b, const double* K, const std::vector<double>* y
     }
     ahead = false;
     double* Ur = b->U + r0 * BAND_ULD;
-    hipLaunchKernelGGL(vcopy_kernel, dim3((unsigned)((int64_t)m * TS / 256)), dim3(256), 0, s, P,
-                       np, m, Ur, (int64_t)BAND_ULD);
-    BD_LAUNCH("vcopy_kernel");
+    if (!b->v_in_u[j]) {   // (the guarded Householder panel copied them already)
+      hipLaunchKernelGGL(vcopy_kernel, dim3((unsigned)((int64_t)m * TS / 256)), dim3(256), 0, s,
+                         P, np, m, Ur, (int64_t)BAND_ULD);
+      BD_LAUNCH("vcopy_kernel");
+    }
     const int nch = (m + TN_CH - 1) / TN_CH;
     // T from V^T V on the side stream, beside the SYMM (which needs only V)
     BD_TRY(hipEventRecord(b->ev_v, s));
@@ -489,7 +497,10 @@ int band_reduce_pass(gpmi_band* b, const double* K, const std::vector<double>* y
     hipLaunchKernelGGL(psum_kernel, dim3(TS * TS / 512, mt), dim3(256), 0, s, b->Xp, sch, b->X);
     BD_LAUNCH("psum_kernel");
     BD_TRY(hipStreamWaitEvent(s, b->ev_t, 0));
-    // the serial 128^3 steps on quadrant workgroups (gemm_quad, gpmi_tile.h)
+    // the serial 128^3 steps on quadrant workgroups (gemm_quad2, gpmi_tile.h; one
+    // launch summing the split-K partials and forming X T per half tile instead:
+    // slower, 139.0 against 138.2 ms, its 34-234 workgroups each read 1/2 of a row
+    // tile's partials)
     hipLaunchKernelGGL(xt_q_kernel, dim3(mt, 4), dim3(256), 0, s, b->X, T, b->X2);
     BD_LAUNCH("xt_q_kernel");
     hipLaunchKernelGGL(tn_partial_q_kernel, dim3(nch, 4), dim3(256), 0, s, Ur + TS,
@@ -517,13 +528,24 @@ int band_reduce_pass(gpmi_band* b, const double* K, const std::vector<double>* y
       bool guard = false;
       int rc = panel_qr(b, j + 1, b->s_pan, mode, pipe ? &guard : nullptr);
       if (rc) return rc;
-      BD_TRY(hipEventRecord(b->ev_pan, b->s_pan));
       const int rest = (mt - 1) * mt / 2;
+      const int nmain = std::min(rest, std::max(1, b->ncu - LA_FREE));
+      int* tcnt = pipe ? b->cqflag + 8 * j + 6 : nullptr;
+      if (tcnt && rest > nmain) {
+        // the chain's CUs join the update once the chain ends (tickets of tcnt;
+        // 139.2 against 141.0 ms at N = 16384; launched only from panels whose
+        // update outlasts the chain: no difference)
+        hipLaunchKernelGGL(syr2k_pipe_kernel, dim3(std::min(LA_FREE, rest - nmain)), dim3(256),
+                           0, b->s_pan, b->Ab, np, b->U, (int64_t)BAND_ULD, j + 1, mt, tcnt,
+                           nmain, 1);
+        BD_LAUNCH("syr2k_pipe_kernel");
+      }
+      BD_TRY(hipEventRecord(b->ev_pan, b->s_pan));
       if (pipe) {
         // one SYR2K workgroup per CU on all but la_free CUs, which the chain (its
         // single-workgroup kernels need a whole CU) has to itself
-        hipLaunchKernelGGL(syr2k_pipe_kernel, dim3(std::min(rest, std::max(1, b->ncu - LA_FREE))),
-                           dim3(256), 0, s, b->Ab, np, b->U, (int64_t)BAND_ULD, j + 1, mt);
+        hipLaunchKernelGGL(syr2k_pipe_kernel, dim3(nmain), dim3(256), 0, s, b->Ab, np, b->U,
+                           (int64_t)BAND_ULD, j + 1, mt, tcnt, nmain, 0);
         BD_LAUNCH("syr2k_pipe_kernel");
       } else {
         // the Householder panel (its workgroups must be co-resident) beside a capped
@@ -719,6 +741,7 @@ int gpmi_band_create(gpmi_op* op, gpmi_band** out) {
   if ((e = hipEventCreateWithFlags(&b->ev_rc, hipEventDisableTiming)) != hipSuccess)
     return fail(e, "event");
   b->t_from_q.assign((size_t)nt, 0);
+  b->v_in_u.assign((size_t)nt, 0);
   BALLOC(cqS, (size_t)nt * TS);
   BALLOC(cqscr, (size_t)nt * TS * TS);
 #undef BALLOC

@@ -98,56 +98,96 @@ __device__ __forceinline__ void gemm_tile(const double* __restrict__ P1, int64_t
   }
 }
 
-// One 64 x 64 quadrant (qr, qc) of the 128 x 128 product above: the same staging
-// (both 128-row slabs, so the operand layouts and swizzles are shared), each wave a
-// 32 x 32 piece (wave w: rows qr*64 + (w>>1)*32, columns qc*64 + (w&1)*32). Four
-// workgroups then cover one output tile with a quarter of the MFMA chain each: the
-// band's serial 128^3 steps (X T, V^T X, T^T M, X - V Zh, the tile-column update)
-// are latency-bound single products per tile, ~4x shorter this way.
-template <int AL, int BL, bool NEG>
-__device__ __forceinline__ void gemm_quad(const double* __restrict__ P1, int64_t ld1,
-                                          const double* __restrict__ P2, int64_t ld2, int kdim,
-                                          double* smem, d4 (&acc)[2][2], int qr, int qc) {
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int r0 = qr * 64 + (w >> 1) * 32, c0 = qc * 64 + (w & 1) * 32;
+// One 64 x 64 quadrant (qr, qc) of the 128 x 128 product above, each wave a 32 x 32
+// piece (wave w: rows qr*64 + (w>>1)*32, columns qc*64 + (w&1)*32). Four workgroups
+// then cover one output tile with a quarter of the MFMA chain each: the band's serial
+// 128^3 steps (X T, V^T X, T^T M, X - V Zh, the tile-column update) are latency-bound
+// single products per tile. Every operand load is in flight from the start (only the
+// quadrant's 64 rows of each operand, in k-chunks of Q2_CK, up to Q2_NR chunks in
+// registers at once: all of them at kdim 128), staged k-major ([k][Q2_LP]) into two
+// LDS buffers. Against a one-slab-ahead prefetch (the 128 x 128 gemm_tile's staging):
+// 140.3 against 141.0 ms for the N = 16384 reduction. The MFMA sequence per output
+// element is gemm_tile's (k ascending, 4 per instruction): the same results.
+constexpr int Q2_CK = 32;                      // k per chunk
+constexpr int Q2_LP = 80;                      // LDS pitch (== 16 mod 32 doubles: the
+                                               // fk = 0 / 1 fragment rows 32 banks apart)
+constexpr int Q2_NR = 4;                       // chunks in registers at once
+constexpr int Q2_SMEM = 2 * 2 * Q2_CK * Q2_LP;   // doubles (80 KB: two per CU)
+
+// chunk c of op(P)'s rows [r0, r0 + 64): 4 d2 per thread
+template <int L>
+__device__ __forceinline__ void q2_load(const double* __restrict__ P, int64_t ld, int r0, int k0,
+                                        d2 (&r)[4]) {
+  const int t = threadIdx.x;
+  if (L == KSLOW) {   // op(P)[r][k] = P[k * ld + r]: rows contiguous
+    const double* p = P + (int64_t)(k0 + (t >> 3)) * ld + r0 + (t & 7) * 8;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) r[q] = *reinterpret_cast<const d2*>(p + 2 * q);
+  } else {            // op(P)[r][k] = P[r * ld + k]: k contiguous
+    const double* p = P + (int64_t)(r0 + (t >> 2)) * ld + k0 + (t & 3) * 8;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) r[q] = *reinterpret_cast<const d2*>(p + 2 * q);
+  }
+}
+
+template <int L>
+__device__ __forceinline__ void q2_store(double* s, const d2 (&r)[4]) {
+  const int t = threadIdx.x;
+  if (L == KSLOW) {
+    double* d = s + (t >> 3) * Q2_LP + (t & 7) * 8;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) *reinterpret_cast<d2*>(d + 2 * q) = r[q];
+  } else {
+    double* d = s + ((t & 3) * 8) * Q2_LP + (t >> 2);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      d[(2 * q) * Q2_LP] = r[q][0];
+      d[(2 * q + 1) * Q2_LP] = r[q][1];
+    }
+  }
+}
+
+template <int AL, int BL, bool NEG, int KDIM>
+__device__ __forceinline__ void gemm_quad2(const double* __restrict__ P1, int64_t ld1,
+                                           const double* __restrict__ P2, int64_t ld2,
+                                           double* smem, d4 (&acc)[2][2], int qr, int qc) {
+  constexpr int NC = KDIM / Q2_CK;
+  constexpr int NR = NC < Q2_NR ? NC : Q2_NR;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int ra0 = (w >> 1) * 32, rb0 = (w & 1) * 32;   // the wave's rows in the halves
   const int fr = lane & 15, fk = lane >> 4;
-  double* sA = smem;
-  double* sB = smem + 2 * GSTAGE;
-  d2 ra[4], rb[4];
-  gl_op<AL>(P1, ld1, 0, ra);
-  gl_op<BL>(P2, ld2, 0, rb);
-  st_op<AL>(sA, ra);
-  st_op<BL>(sB, rb);
-  __syncthreads();
-  __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): as gemm_tile
-  const int nsteps = kdim / BK;
-  for (int s = 0; s < nsteps; ++s) {
-    const int cur = s & 1;
-    const double* cA = sA + cur * GSTAGE;
-    const double* cB = sB + cur * GSTAGE;
-    if (s + 1 < nsteps) {
-      gl_op<AL>(P1, ld1, (s + 1) * BK, ra);
-      gl_op<BL>(P2, ld2, (s + 1) * BK, rb);
+  d2 ra[NR][4], rb[NR][4];
+#pragma unroll
+  for (int c = 0; c < NR; ++c) {
+    q2_load<AL>(P1, ld1, qr * 64, c * Q2_CK, ra[c]);
+    q2_load<BL>(P2, ld2, qc * 64, c * Q2_CK, rb[c]);
+  }
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    double* sA = smem + (c & 1) * (2 * Q2_CK * Q2_LP);
+    double* sB = sA + Q2_CK * Q2_LP;
+    q2_store<AL>(sA, ra[c % NR]);
+    q2_store<BL>(sB, rb[c % NR]);
+    __syncthreads();
+    if (c + NR < NC) {
+      q2_load<AL>(P1, ld1, qr * 64, (c + NR) * Q2_CK, ra[c % NR]);
+      q2_load<BL>(P2, ld2, qc * 64, (c + NR) * Q2_CK, rb[c % NR]);
     }
 #pragma unroll
-    for (int kk = 0; kk < BK / 4; ++kk) {
+    for (int kk = 0; kk < Q2_CK / 4; ++kk) {
       double a[2], b[2];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) a[i] = fr_op<AL>(cA, r0 + i * 16 + fr, kk * 4 + fk);
+      for (int i = 0; i < 2; ++i) a[i] = sA[(kk * 4 + fk) * Q2_LP + ra0 + i * 16 + fr];
 #pragma unroll
-      for (int j = 0; j < 2; ++j) b[j] = fr_op<BL>(cB, c0 + j * 16 + fr, kk * 4 + fk);
+      for (int j = 0; j < 2; ++j) b[j] = sB[(kk * 4 + fk) * Q2_LP + rb0 + j * 16 + fr];
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
           acc[i][j] = NEG ? mfma64_neg(a[i], b[j], acc[i][j]) : mfma64(a[i], b[j], acc[i][j]);
     }
-    if (s + 1 < nsteps) {
-      st_op<AL>(sA + (cur ^ 1) * GSTAGE, ra);
-      st_op<BL>(sB + (cur ^ 1) * GSTAGE, rb);
-    }
-    __syncthreads();
   }
+  __syncthreads();   // (the caller may reuse smem)
 }
 
 __device__ __forceinline__ void zero_quad(d4 (&acc)[2][2]) {
@@ -157,7 +197,7 @@ __device__ __forceinline__ void zero_quad(d4 (&acc)[2][2]) {
     for (int j = 0; j < 2; ++j) acc[i][j] = d4{0.0, 0.0, 0.0, 0.0};
 }
 
-// C points at the 128 x 128 tile; the quadrant's wave pieces as in gemm_quad.
+// C points at the 128 x 128 tile; the quadrant's wave pieces as in gemm_quad2.
 __device__ __forceinline__ void load_quad(const double* C, int64_t ldc, d4 (&acc)[2][2], int qr,
                                           int qc) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
