@@ -372,7 +372,6 @@ __global__ __launch_bounds__(256) void cq_recon_kernel(const double* __restrict_
   __shared__ int s_fail;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int fr = lane & 15, fk = lane >> 4;
-  const int wr = w >> 1, wc = w & 1;
   // an earlier pass failed: leave the panel untouched for the Householder panel
   if (__hip_atomic_load(fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
 #if GPMI_CQ_STAMPS
@@ -435,33 +434,57 @@ __global__ __launch_bounds__(256) void cq_recon_kernel(const double* __restrict_
     Linv3[e] = (c <= r) ? A[r * DL + c] : 0.0;
   }
   CQST(2);
-  // ---- Q3t = Q2t M3^T: wave (wr, wc) forms rows wr*64.., columns wc*64..; the
-  // A operand straight from global (L2), M3 from LDS (lower: k <= column)
+  // ---- Q3t = Q2t M3^T (M3 lower: output column block cb needs k < 16 (cb + 1)): wave
+  // w forms the column blocks w and 7 - w of all eight row blocks, 9 of the 36 units
+  // of work each (a split by quadrants gives two waves 2/3 of it). Q2t's loads are
+  // issued first (all in flight), M3's fragments of the wave's two column blocks go
+  // to registers, then Q2t replaces M3 in LDS and the products read it from there.
+  // The same MFMA sequence per output element (k ascending).
   {
-    d4 acc[4][4];
-    zero_tile(acc);
-    const int kmax = wc * 64 + 64;
-    for (int k0 = 0; k0 < kmax; k0 += 32) {
-      // the chunk's Q2t operands (8 k-steps) in flight together
-      double a[8][4];
+    d2 q2[32];
 #pragma unroll
-      for (int q = 0; q < 8; ++q)
+    for (int it = 0; it < 32; ++it) q2[it] = *reinterpret_cast<const d2*>(Q2 + 2 * (it * 256 + t));
+    const int cb0 = w, cb1 = 7 - w;
+    double b0[16], b1[32];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) a[q][i] = Q2[(wr * 64 + i * 16 + fr) * TS + k0 + 4 * q + fk];
+    for (int kk = 0; kk < 16; ++kk)
+      b0[kk] = kk < 4 * (cb0 + 1) ? A[(cb0 * 16 + fr) * DL + kk * 4 + fk] : 0.0;
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const int k = k0 + 4 * q + fk;
-        double b[4];
+    for (int kk = 0; kk < 32; ++kk)
+      b1[kk] = kk < 4 * (cb1 + 1) ? A[(cb1 * 16 + fr) * DL + kk * 4 + fk] : 0.0;
+    __syncthreads();   // every wave has its M3 fragments
 #pragma unroll
-        for (int j = 0; j < 4; ++j) b[j] = A[(wc * 64 + j * 16 + fr) * DL + k];
+    for (int it = 0; it < 32; ++it) {
+      const int e = it * 256 + t, r = e >> 6, c = (e & 63) * 2;
+      A[r * DL + c] = q2[it][0];
+      A[r * DL + c + 1] = q2[it][1];
+    }
+    __syncthreads();
+    d4 acc0[8], acc1[8];
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+    for (int rb = 0; rb < 8; ++rb) {
+      acc0[rb] = d4{0.0, 0.0, 0.0, 0.0};
+      acc1[rb] = d4{0.0, 0.0, 0.0, 0.0};
+    }
 #pragma unroll
-          for (int j = 0; j < 4; ++j) acc[i][j] = mfma64(a[q][i], b[j], acc[i][j]);
+    for (int kk = 0; kk < 32; ++kk) {
+      if (kk < 4 * (cb1 + 1)) {
+#pragma unroll
+        for (int rb = 0; rb < 8; ++rb) {
+          const double a = A[(rb * 16 + fr) * DL + kk * 4 + fk];
+          if (kk < 4 * (cb0 + 1)) acc0[rb] = mfma64(a, b0[kk < 16 ? kk : 0], acc0[rb]);
+          acc1[rb] = mfma64(a, b1[kk], acc1[rb]);
+        }
       }
     }
-    __syncthreads();   // every wave is done reading M3 from A
-    store_tile(A, DL, acc, 1.0);
+    __syncthreads();   // every wave is done reading Q2t from A
+#pragma unroll
+    for (int rb = 0; rb < 8; ++rb)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        A[(rb * 16 + fk + 4 * rr) * DL + cb0 * 16 + fr] = acc0[rb][rr];
+        A[(rb * 16 + fk + 4 * rr) * DL + cb1 * 16 + fr] = acc1[rb][rr];
+      }
   }
   __syncthreads();
   CQST(3);
@@ -578,6 +601,7 @@ __global__ __launch_bounds__(256) void cq_recon_kernel(const double* __restrict_
   {
     d4 acc[4][4];
     zero_tile(acc);
+    const int wr = w >> 1, wc = w & 1;
     const int kmax = wr * 64 + 64;   // U^-T rows wr*64.. have k <= row
     for (int k0 = 0; k0 < kmax; k0 += 32) {
       double b[8][4];   // the chunk's M3 operands in flight together
