@@ -556,6 +556,22 @@ def test_band_reduction_variants_agree(gp, monkeypatch):
     numpy.testing.assert_allclose(G0, G2, rtol=1e-9, atol=1e-11 * numpy.abs(G2).max())
 
 
+@pytest.mark.parametrize('n', [4224, 6016])
+def test_band_filler_tiles_bit_identical(gp, monkeypatch, n):
+    """Sizes whose first panels' look-ahead SYR2K has more tiles than its main launch
+    has workgroups (mt (mt - 1) / 2 > CUs - 32), so the tiles after the first go out
+    by ticket and the filler launch after the chain takes its share: the reduction
+    must still equal the one without look-ahead bit for bit (every tile updated
+    exactly once, by the same product)."""
+    K, X, z = _inputs(n, 7 * n + 1, nu=1.5, scale=0.1)
+    etas = [1e-2, 1.0]
+    ld0, G0 = _mc(K).loglik_terms(etas, X, z)
+    monkeypatch.setenv('GPMI_BAND_LA', '0')
+    ld1, G1 = _mc(K).loglik_terms(etas, X, z)
+    numpy.testing.assert_array_equal(ld0, ld1)
+    numpy.testing.assert_array_equal(G0, G1)
+
+
 @pytest.mark.parametrize('n', [1, 5, 127, 128, 129, 300, 1000, 2304, 4224])
 def test_band_cyclic_reduction_matches_sequential(gp, monkeypatch, n):
     """The banded Cholesky by block cyclic reduction (gpmi_bcr.hip, the default up
