@@ -44,6 +44,13 @@ constexpr int BAND_ULD = 384;      // U = [W | V | W]
 // two-per-CU SYR2K 160). A filler launch gives them back to the update once the
 // chain ends; with it: 24 164, 32 139.2-139.6, 40 140.4, 48 140.4, 64 140.1 ms.
 constexpr int LA_FREE = 32;
+// The last panels (trailing tile count mt < LA_LATE_MT) are chain-bound: their SYR2K
+// is short and the chain's many-workgroup kernels (cq_gram / cq_apply, m / 64
+// workgroups) finish sooner on more CUs. Free CUs for mt < T (32 above; N = 16384,
+// one box): 64 for T = 60 137.0 ms, 96 137.7, 128 137.6; 64 for T = 40 138.1, T = 80
+// 137.3; against 138.7-139.0 with 32 throughout (and 64 for mt >= 50: 140.0).
+constexpr int LA_FREE_LATE = 64;
+constexpr int LA_LATE_MT = 60;
 constexpr int BAND_MAX_NPAD = HH_MAXG * HH_ROWS;
 
 __global__ void hh_col_kernel(double* P, int64_t lda, int m, int c, double* part, double* pivrow,

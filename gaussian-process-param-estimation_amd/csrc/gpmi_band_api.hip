@@ -529,13 +529,14 @@ int band_reduce_pass(gpmi_band* b, const double* K, const std::vector<double>* y
       int rc = panel_qr(b, j + 1, b->s_pan, mode, pipe ? &guard : nullptr);
       if (rc) return rc;
       const int rest = (mt - 1) * mt / 2;
-      const int nmain = std::min(rest, std::max(1, b->ncu - LA_FREE));
+      const int la_free = mt < LA_LATE_MT ? LA_FREE_LATE : LA_FREE;
+      const int nmain = std::min(rest, std::max(1, b->ncu - la_free));
       int* tcnt = pipe ? b->cqflag + 8 * j + 6 : nullptr;
       if (tcnt && rest > nmain) {
         // the chain's CUs join the update once the chain ends (tickets of tcnt;
         // 139.2 against 141.0 ms at N = 16384; launched only from panels whose
         // update outlasts the chain: no difference)
-        hipLaunchKernelGGL(syr2k_pipe_kernel, dim3(std::min(LA_FREE, rest - nmain)), dim3(256),
+        hipLaunchKernelGGL(syr2k_pipe_kernel, dim3(std::min(la_free, rest - nmain)), dim3(256),
                            0, b->s_pan, b->Ab, np, b->U, (int64_t)BAND_ULD, j + 1, mt, tcnt,
                            nmain, 1);
         BD_LAUNCH("syr2k_pipe_kernel");
