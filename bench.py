@@ -22,6 +22,7 @@ and the sparse configs 4 and 5 (probe and right-hand-side column shards).
 
 import argparse
 import json
+import re
 import os
 import platform
 import sys
@@ -109,24 +110,34 @@ def pmc_traffic(outer, batch, kernel='gpmi::syrk_kernel'):
     return (2.0 * pd['FETCH_SIZE'] + pd['WRITE_SIZE']) * 1024.0, os.path.relpath(files[-1], REPO)
 
 
-def pmc_traffic_sparse(config, kernel='gpmi::csr_spmm_kernel'):
-    """HBM-side bytes per timed SpMM launch from the committed PMC summary of this
-    sparse config (profiles/r*/pmc_traffic_{config}.json, per_dispatch_last = the
-    bench's timed s=20 launches; FETCH_SIZE doubled as in pmc_traffic)."""
+def pmc_traffic_sparse(config, kernel='gpmi::csr_spmm_kernel', width=None):
+    """HBM-side bytes per SpMM launch of `kernel` (at block width `width`: template
+    instances appear as 'void gpmi::name<12, 8, 4>') from the newest committed PMC
+    summary of this sparse config that holds it (profiles/r*/pmc_traffic_{config}.json,
+    FETCH_SIZE / WRITE_SIZE passes over `bench.py --config <config> --steps 1`;
+    FETCH_SIZE doubled as in pmc_traffic). Per launch: 'per_dispatch_last' where the
+    summary has it (the last K dispatches), else the mean over every dispatch of
+    that instance (the step's launches of that width and the reference check's)."""
     import glob
     files = sorted(glob.glob(os.path.join(REPO, 'profiles', 'r*',
-                                          'pmc_traffic_%s.json' % config)))
-    if not files:
-        return None, None
-    with open(files[-1]) as fh:
-        kernels = json.load(fh)['kernels']
-    # template instances appear as 'void gpmi::name<20>'
-    k = kernels.get(kernel) or next((v for key, v in kernels.items()
-                                     if key.replace('void ', '').split('<')[0] == kernel), None)
-    if not k or 'per_dispatch_last' not in k:
-        return None, None
-    pd = k['per_dispatch_last']
-    return (2.0 * pd['FETCH_SIZE'] + pd['WRITE_SIZE']) * 1024.0, os.path.relpath(files[-1], REPO)
+                                          'pmc_traffic_%s.json' % config)),
+                   key=lambda f: (int(re.search(r'profiles/r(\d+)', f).group(1)), f))
+    for f in reversed(files):
+        with open(f) as fh:
+            kernels = json.load(fh)['kernels']
+
+        def match(key):
+            base = key.replace('void ', '')
+            if base.split('<')[0] != kernel:
+                return False
+            return width is None or base.startswith('%s<%d,' % (kernel, width)) or \
+                base == '%s<%d>' % (kernel, width)
+        k = next((v for key, v in kernels.items() if match(key)), None)
+        if not k:
+            continue
+        pd = k.get('per_dispatch_last', k['per_dispatch'])
+        return (2.0 * pd['FETCH_SIZE'] + pd['WRITE_SIZE']) * 1024.0, os.path.relpath(f, REPO)
+    return None, None
 
 
 def host_info():
@@ -448,6 +459,9 @@ def sparse_measure(args, config, world, rank, local, dist, torch, cpu, exact, de
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
+    # in-step SpMM timing: a HIP event pair around every SpMM launch of the timed
+    # steps, on the stream it runs on (the Lanczos's and the multi-shift CG's)
+    op.sop.set_timing(True)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         last = step()
@@ -455,6 +469,8 @@ def sparse_measure(args, config, world, rank, local, dist, torch, cpu, exact, de
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    spmm_in_step = op.sop.spmm_timing()
+    op.sop.set_timing(False)
     dt = max_over_ranks(dt, world, dist, torch)
     # imate's `orthogonalize` option: this rank's probe block by the plain three-term
     # recurrence (0, imate's default, what the step uses) against full
@@ -480,10 +496,15 @@ def sparse_measure(args, config, world, rank, local, dist, torch, cpu, exact, de
               'logdet_diff_in_std_errors_max': round(float(numpy.max(numpy.abs(dz))), 3),
               'note': "the measured step uses imate's default orthogonalize=0 (plain "
                       "three-term recurrence); -1 is full reorthogonalisation (DCGS2)"}
-    # SpMM roofline on a device-resident probe block (HIP events)
-    s_blk = max(1, min(32, nprobe // world))
-    ms = op.sop.bench_spmm(s_blk, 50)
+    # SpMM roofline from the timed steps: the width whose SpMM launches took the most
+    # device time (the multi-shift CG's s = 12, or the Lanczos's s = 20), its average
+    # in-step HIP-event launch time; the same kernel isolated (50 back-to-back
+    # launches on a resident block) is reported beside it as isolated_ms
     nnz = op.sop.nnz
+    s_blk = max(spmm_in_step, key=lambda w: spmm_in_step[w][1])
+    n_launch, tot_ms = spmm_in_step[s_blk]
+    ms = tot_ms / n_launch
+    ms_iso = op.sop.bench_spmm(s_blk, 50)
     alg_bytes = 12.0 * nnz + 8.0 * (n + 1) + 16.0 * n * s_blk
     gbs = alg_bytes / (ms * 1e-3) / 1e9
     info = op.sop.spmm_info()
@@ -491,8 +512,12 @@ def sparse_measure(args, config, world, rank, local, dist, torch, cpu, exact, de
     windowed = info['windowed'] or sp_kernel == 'csr_spmm_wing_kernel'
     gather_bytes = (8.0 * s_blk * info['mean_window'] * ((n + 63) // 64) if windowed
                     else 8.0 * nnz * s_blk)
-    sp_traffic, sp_tsrc = (pmc_traffic_sparse(config, 'gpmi::' + sp_kernel)
-                           if s_blk == 20 else (None, None))
+    sp_traffic, sp_tsrc = pmc_traffic_sparse(config, 'gpmi::' + sp_kernel, s_blk)
+    by_width = {str(w): {'launches': c, 'total_ms': round(t, 3),
+                         'avg_launch_ms': round(t / c, 4),
+                         'frac': round((12.0 * nnz + 8.0 * (n + 1) + 16.0 * n * w) /
+                                       (t / c * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+                for w, (c, t) in sorted(spmm_in_step.items())}
     my_probes = shard(nprobe, world, rank)
     # the library pads a full 11-column block on the window SpMM to 12 (msgram_impl);
     # a column shard (N > 1) runs unpadded: rank 0's shard width
@@ -528,6 +553,12 @@ def sparse_measure(args, config, world, rank, local, dist, torch, cpu, exact, de
                          'traffic_source': sp_tsrc,
                          'kernel': '%s (s=%d columns)' % (sp_kernel, s_blk),
                          'avg_launch_ms': round(ms, 4),
+                         'avg_launch_ms_source': 'HIP events around each SpMM launch of the '
+                                                 'timed steps (%d launches at s=%d)'
+                                                 % (n_launch, s_blk),
+                         'isolated_ms': round(ms_iso, 4),
+                         'algorithmic_bytes_per_launch': alg_bytes,
+                         'in_step_by_width': by_width,
                          # cache-side X bytes: every nonzero gathers s contiguous doubles
                          # (gather kernel), or every 64-row block stages its window
                          'gather_bytes': gather_bytes,

@@ -12,6 +12,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <map>
 #include <vector>
 
 #include "gpmi_internal.h"
@@ -208,6 +209,18 @@ struct gpmi_sp {
   int dsplit = 1, dkcs = 1;            // k splits of dense_mm_kernel, 64-column chunks each
   double* dYp = nullptr;               // split partials [dsplit][n][MAXS] of `stream`
   double* dYp_ms = nullptr;            // ... of ms_stream (the CG beside the Lanczos)
+  // In-step SpMM timing (gpmi_sp_set_timing): a HIP event pair around every SpMM
+  // launch on the stream it runs on (the Lanczos's and the CG's), logged with its
+  // width; gpmi_sp_spmm_timing sums the pairs per width. The two host threads of a
+  // sweep both launch SpMMs: the log is under timing_mu.
+  std::mutex timing_mu;
+  bool timing = false;
+  std::vector<hipEvent_t> ev_pool;     // free events
+  struct SpmmRec {
+    hipEvent_t e0, e1;
+    int s;
+  };
+  std::vector<SpmmRec> spmm_log;
 };
 
 namespace {
@@ -346,9 +359,8 @@ int spmm_kind(gpmi_sp* sp, int s, int* kind) {
 // Y = (K + eta I) X. With pqp, a kernel that can also writes the per-block partials
 // X . Y per column (pqp[block][s], the multi-shift CG's p . q) and sets *pq_blocks to
 // their count; otherwise *pq_blocks = 0 and the caller forms them.
-int spmm(gpmi_sp* sp, const double* X, double* Y, int s, double eta, hipStream_t st = nullptr,
-         double* pqp = nullptr, int* pq_blocks = nullptr) {
-  if (!st) st = sp->stream;
+int spmm_launch(gpmi_sp* sp, const double* X, double* Y, int s, double eta, hipStream_t st,
+                double* pqp, int* pq_blocks) {
   if (pq_blocks) *pq_blocks = 0;
   if (sp->dK) {
     // dense: split partials of K X on fp64 MFMA, summed in split order (+ eta X)
@@ -416,6 +428,36 @@ int spmm(gpmi_sp* sp, const double* X, double* Y, int s, double eta, hipStream_t
                      st, sp->indptr, sp->indices, sp->data, sp->n, X, (int64_t)s, Y,
                      (int64_t)s, s, 64 / s, eta);
   SP_LAUNCH("csr_spmm_kernel");
+  return 0;
+}
+
+int take_event(gpmi_sp* sp, hipEvent_t* e) {
+  if (!sp->ev_pool.empty()) {
+    *e = sp->ev_pool.back();
+    sp->ev_pool.pop_back();
+    return 0;
+  }
+  SP_TRY(hipEventCreate(e));
+  return 0;
+}
+
+// Y = (K + eta I) X (spmm_launch), bracketed by a HIP event pair on its stream when
+// in-step timing is on (gpmi_sp_set_timing).
+int spmm(gpmi_sp* sp, const double* X, double* Y, int s, double eta, hipStream_t st = nullptr,
+         double* pqp = nullptr, int* pq_blocks = nullptr) {
+  if (!st) st = sp->stream;
+  if (!sp->timing) return spmm_launch(sp, X, Y, s, eta, st, pqp, pq_blocks);
+  gpmi_sp::SpmmRec rec{nullptr, nullptr, s};
+  {
+    std::lock_guard<std::mutex> lock(sp->timing_mu);
+    if (int rc = take_event(sp, &rec.e0)) return rc;
+    if (int rc = take_event(sp, &rec.e1)) return rc;
+  }
+  SP_TRY(hipEventRecord(rec.e0, st));
+  if (int rc = spmm_launch(sp, X, Y, s, eta, st, pqp, pq_blocks)) return rc;
+  SP_TRY(hipEventRecord(rec.e1, st));
+  std::lock_guard<std::mutex> lock(sp->timing_mu);
+  sp->spmm_log.push_back(rec);
   return 0;
 }
 
@@ -959,6 +1001,11 @@ int gpmi_sp_destroy(gpmi_sp* sp) {
   if (sp->rhs_dev) (void)hipFree(sp->rhs_dev);
   if (sp->ms_partial) (void)hipFree(sp->ms_partial);
   if (sp->ms_pin) (void)hipHostFree(sp->ms_pin);
+  for (hipEvent_t e : sp->ev_pool) (void)hipEventDestroy(e);
+  for (auto& r : sp->spmm_log) {
+    (void)hipEventDestroy(r.e0);
+    (void)hipEventDestroy(r.e1);
+  }
   for (hipEvent_t e : sp->ms_ev)
     if (e) (void)hipEventDestroy(e);
   if (sp->ms_stream) (void)hipStreamDestroy(sp->ms_stream);
@@ -1619,6 +1666,61 @@ int gpmi_sp_spmm_kernel(gpmi_sp* sp, int s, int* kind) {
 int gpmi_sp_last_status(const gpmi_sp* sp, int* converged) {
   if (!sp) return set_error(-1006, "null handle");
   if (converged) *converged = sp->last_converged;
+  return 0;
+}
+
+}  // extern "C"
+
+namespace gpmi {
+// An empty launch that marks the start / end of a timing window in a rocprofv3
+// kernel trace (tools/trace_summary.py --timed-spmm takes the SpMM launches
+// between two marks as the timed ones).
+__global__ void timing_mark_kernel(int on) { (void)on; }
+}  // namespace gpmi
+
+extern "C" {
+
+int gpmi_sp_set_timing(gpmi_sp* sp, int enable) {
+  if (!sp) return set_error(-1006, "null handle");
+  Guard g(sp->device);
+  hipLaunchKernelGGL(gpmi::timing_mark_kernel, dim3(1), dim3(64), 0, sp->stream, enable);
+  SP_LAUNCH("timing_mark_kernel");
+  std::lock_guard<std::mutex> lock(sp->timing_mu);
+  // the pairs of an earlier window go back to the pool (their streams are idle
+  // once the caller synchronised; wait for them anyway)
+  for (auto& r : sp->spmm_log) {
+    SP_TRY(hipEventSynchronize(r.e1));
+    sp->ev_pool.push_back(r.e0);
+    sp->ev_pool.push_back(r.e1);
+  }
+  sp->spmm_log.clear();
+  sp->timing = enable != 0;
+  return 0;
+}
+
+int gpmi_sp_spmm_timing(gpmi_sp* sp, int max_widths, int* n_widths, int* widths, int* launches,
+                        double* total_ms) {
+  if (!sp || !n_widths) return set_error(-1006, "null handle");
+  Guard g(sp->device);
+  std::lock_guard<std::mutex> lock(sp->timing_mu);
+  std::map<int, std::pair<int, double>> acc;
+  for (auto& r : sp->spmm_log) {
+    SP_TRY(hipEventSynchronize(r.e1));
+    float ms = 0.f;
+    SP_TRY(hipEventElapsedTime(&ms, r.e0, r.e1));
+    auto& a = acc[r.s];
+    a.first += 1;
+    a.second += ms;
+  }
+  *n_widths = (int)acc.size();
+  int k = 0;
+  for (auto& kv : acc) {
+    if (k >= max_widths) break;
+    if (widths) widths[k] = kv.first;
+    if (launches) launches[k] = kv.second.first;
+    if (total_ms) total_ms[k] = kv.second.second;
+    ++k;
+  }
   return 0;
 }
 

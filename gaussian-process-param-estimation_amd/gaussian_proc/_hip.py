@@ -75,6 +75,9 @@ SIGNATURES = {
                                           ctypes.c_int, ctypes.c_int, c_double_p, c_double_p]),
     'gpmi_sp_bench_spmm': (ctypes.c_int, [c_op_p, ctypes.c_int, ctypes.c_int, ctypes.c_double,
                                           c_double_p]),
+    'gpmi_sp_set_timing': (ctypes.c_int, [c_op_p, ctypes.c_int]),
+    'gpmi_sp_spmm_timing': (ctypes.c_int, [c_op_p, ctypes.c_int, c_int_p, c_int_p, c_int_p,
+                                           c_double_p]),
     'gpmi_sp_cg': (ctypes.c_int, [c_op_p, ctypes.c_double, c_double_p, c_i64, ctypes.c_int,
                                   ctypes.c_double, ctypes.c_int, c_double_p, c_i64, c_int_p]),
     'gpmi_sp_msgram': (ctypes.c_int, [c_op_p, c_double_p, ctypes.c_int, c_double_p, c_i64,
@@ -602,6 +605,22 @@ class SparseOperator(object):
                                           int(probe_offset), int(orthogonalize), dptr(a),
                                           dptr(b)), 'gpmi_sp_lanczos_ex')
         return a, b
+
+    def set_timing(self, on):
+        """In-step SpMM timing: HIP event pairs around every SpMM launch of this
+        operator while on (the log is cleared on every call)."""
+        check(self.lib.gpmi_sp_set_timing(self.h, int(bool(on))), 'gpmi_sp_set_timing')
+
+    def spmm_timing(self):
+        """{width s: (launches, total_ms)} of the SpMM launches logged since
+        set_timing(True)."""
+        nw = ctypes.c_int(0)
+        w = (ctypes.c_int * 64)()
+        c = (ctypes.c_int * 64)()
+        t = (ctypes.c_double * 64)()
+        check(self.lib.gpmi_sp_spmm_timing(self.h, 64, ctypes.byref(nw), w, c, t),
+              'gpmi_sp_spmm_timing')
+        return {int(w[k]): (int(c[k]), float(t[k])) for k in range(min(64, nw.value))}
 
     def bench_spmm(self, s, reps, eta=0.0):
         ms = ctypes.c_double()

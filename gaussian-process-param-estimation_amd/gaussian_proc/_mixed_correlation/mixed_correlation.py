@@ -389,7 +389,8 @@ class MixedCorrelation(object):
             a, b = self._fixed_lanczos(deg)
             g = _slq.nodes(a, b)
             _slq.check_shifts(_slq.min_ritz(g), e)
-            r = _slq.radau_nodes(a, b, min(lo, _slq.min_ritz(g) - 1e-12 * abs(_slq.min_ritz(g))))
+            node, rigorous = _slq.radau_node(lo, g, e)
+            r = _slq.radau_nodes(a, b, node)
             gap = max(float(_slq.bracket(g, r, e, f)[0]) for f in fns)
             ok = gap <= self.lanczos_tol
             if ok or deg >= self.max_lanczos_degree:
@@ -399,7 +400,8 @@ class MixedCorrelation(object):
         self.lanczos_degree_used = deg
         self._nodes = g
         self.last_slq_convergence = {'degree': deg, 'bracket': gap, 'converged': ok,
-                                     'eta': e[0]}
+                                     'eta': e[0], 'radau_node': node,
+                                     'rigorous_bound': rigorous}
         return self.last_slq_convergence
 
     def _slq(self, eta, what):
@@ -432,12 +434,21 @@ class MixedCorrelation(object):
         """Hutchinson probes [n, k]: the counter-based Rademacher set, with imate's
         ``orthogonalize`` (default True) orthonormalised and scaled by sqrt(n)
         (Householder QR: the first columns do not depend on later ones, so a
-        larger set extends a smaller one)."""
-        V = _slq.rademacher(self.n, offset + k, self.seed)
-        if self.orthogonalize and offset + k <= self.n:
-            Q, _ = numpy.linalg.qr(V)
-            V = Q * numpy.sqrt(self.n)
-        return V[:, offset:]
+        larger set extends a smaller one). The block depends only on (n, seed,
+        column count), so it is built once and kept (traceinv is called once per
+        eta): only a request for more columns than the cached block rebuilds it."""
+        m = offset + k
+        c = getattr(self, '_probe_cache', None)
+        if c is None or c[0] != self.seed or c[1] != bool(self.orthogonalize) or \
+                c[2].shape[1] < m:
+            V = _slq.rademacher(self.n, m, self.seed)
+            if self.orthogonalize and m <= self.n:
+                Q, _ = numpy.linalg.qr(V)
+                V = Q * numpy.sqrt(self.n)
+            V.setflags(write=False)
+            c = (self.seed, bool(self.orthogonalize), V)
+            self._probe_cache = c
+        return c[2][:, offset:m]
 
     def _hutchinson_traceinv(self, eta, exponent):
         """imate 'hutchinson' traceinv (:193-203): tr (K + eta I)^-p ~ mean_v

@@ -52,6 +52,14 @@ def nodes(alpha, beta):
     return out
 
 
+def _last_pivot(a, b, lower):
+    """Last pivot d_m of (T_m - lower I) = L D L^T (T_m: diagonal a, off-diagonal b)."""
+    d = a[0] - lower
+    for i in range(1, a.size):
+        d = (a[i] - lower) - b[i - 1] ** 2 / d
+    return d
+
+
 def radau_nodes(alpha, beta, lower):
     """Gauss-Radau rules with one node fixed at ``lower`` <= lambda_min(K)
     (Golub and Meurant, "Matrices, Moments and Quadrature with Applications",
@@ -60,7 +68,14 @@ def radau_nodes(alpha, beta, lower):
     For f with f^(2m) of constant sign on the spectrum (log(x + eta),
     (x + eta)^-p) the Gauss and Gauss-Radau values bracket the exact quadratic
     form, so their gap bounds the Lanczos quadrature error of each probe. A
-    probe whose tridiagonal broke down (exact rule) gets its Gauss rule."""
+    probe whose tridiagonal broke down (exact rule) gets its Gauss rule.
+
+    ``lower`` only a hair below a probe's smallest Ritz value can leave the
+    pivot d_m <= 0 from rounding alone (T_m - lower I is then numerically
+    singular): that probe's node moves down to its own smallest Ritz value minus
+    1e-8 max|T_m| (and 1e-6 max|T_m| if that still fails), a node still below its
+    rule's nodes. Nothing here raises, so a rank of a sharded sweep never leaves
+    the collectives alone (sweep.slq_sweep)."""
     out = []
     for a, b in zip(alpha, beta):
         a = numpy.asarray(a, dtype=float)
@@ -69,14 +84,48 @@ def radau_nodes(alpha, beta, lower):
         if k < len(b) or b[k - 1] == 0.0:
             out.append(_rule(a[:k], b[:k - 1]))
             continue
-        d = a[0] - lower
-        for i in range(1, k):
-            d = (a[i] - lower) - b[i - 1] ** 2 / d
+        node = float(lower)
+        d = _last_pivot(a[:k], b[:k - 1], node)
         if not d > 0.0:
-            raise ValueError('Gauss-Radau node %r is not below the Ritz values' % lower)
-        dd = numpy.append(a[:k], lower + b[k - 1] ** 2 / d)
+            theta = _rule(a[:k], b[:k - 1])[0]
+            scale = max(float(numpy.max(numpy.abs(a[:k]))),
+                        float(numpy.max(numpy.abs(b[:k]))), 1e-300)
+            for rel in (1e-8, 1e-6):
+                node = min(float(lower), float(theta.min()) - rel * scale)
+                d = _last_pivot(a[:k], b[:k - 1], node)
+                if d > 0.0:
+                    break
+        if not d > 0.0:
+            out.append(_rule(a[:k], b[:k - 1]))
+            continue
+        dd = numpy.append(a[:k], node + b[k - 1] ** 2 / d)
         out.append(_rule(dd, b[:k]))
     return out
+
+
+def radau_node(lower, node_list, etas):
+    """The fixed Gauss-Radau node for the quadratures of f(x + eta), eta >= min(etas).
+
+    ``lower`` (a proven lower bound of lambda_min(K): the user's
+    spectrum_lower_bound, 0 for a dense correlation matrix, a sparse K's Gershgorin
+    bound) is used while f stays finite there, i.e. lower + min(etas) > 0. A sparse
+    tapered K's Gershgorin bound is usually far below -min(eta) (log and the
+    inverse powers are NaN / infinite at such a node, so the bracket could never
+    close): the node is then the smallest Ritz value minus a margin (1e-8 of the
+    largest |Ritz value|), or half-way between -min(etas) and that Ritz value if
+    the margin would cross -min(etas). That node is a heuristic, not a proven
+    bound (lambda_min may lie below the smallest Ritz value); pass
+    ``spectrum_lower_bound`` for a rigorous bracket. Returns (node, rigorous)."""
+    e0 = float(numpy.min(etas))
+    tmin = min_ritz(node_list)
+    scale = max((float(numpy.max(numpy.abs(t))) for t, _ in node_list), default=1.0)
+    margin = 1e-8 * max(scale, 1e-300)
+    if lower + e0 > 0.0:
+        return min(float(lower), tmin - margin), True
+    node = tmin - margin
+    if not node + e0 > 0.0:
+        node = 0.5 * (tmin - e0)
+    return node, False
 
 
 def bracket(gauss, radau, etas, fn):

@@ -144,35 +144,51 @@ def slq_sweep(K_mixed, etas, group=None, converge=('logdet',)):
     lower = K_mixed._lower_bound() if tol else None
     deg = getattr(K_mixed, 'lanczos_degree_used', K_mixed.lanczos_degree)
     # per probe row: the quadratures, the smallest Ritz value (the SPD check runs
-    # after the all-gather, on every rank alike: no rank raises alone), then the
-    # Gauss / Gauss-Radau pair of each converge function at min(etas)
+    # after the all-gather, on every rank alike: no rank raises alone), the
+    # Gauss / Gauss-Radau pair of each converge function at min(etas), and an
+    # error flag (a host-side failure of this rank's rows is raised on every rank
+    # after the all-gather, not by this rank alone inside the collectives)
     nq = len(names) * etas.size
+    ncol = nq + 1 + 2 * len(conv) + 1
     seen = []
     while True:
-        local = numpy.zeros((per, nq + 1 + 2 * len(conv)))
+        local = numpy.zeros((per, ncol))
         local[:, nq] = numpy.inf
+        err = None
         if hi > lo:
             a, b = K_mixed.sop.lanczos(hi - lo, deg, K_mixed.seed, probe_offset=lo,
                                        orthogonalize=getattr(K_mixed, 'orthogonalize', 0))
-            nodes = _slq.nodes(a, b)
-            q = numpy.empty((hi - lo, len(names), etas.size))
-            for f, name in enumerate(names):
-                with numpy.errstate(invalid='ignore', divide='ignore'):
-                    q[:, f] = _slq.quadrature(nodes, etas, _slq.FUNCS[name], check=False)
-            local[:hi - lo, :nq] = q.reshape(hi - lo, nq)
-            local[:hi - lo, nq] = [float(t.min()) for t, _ in nodes]
-            if conv:
-                tmin = _slq.min_ritz(nodes)
-                radau = _slq.radau_nodes(a, b, min(lower, tmin - 1e-12 * abs(tmin)))
-                e = [float(etas.min())]
-                for i, fn in enumerate(conv):
+            try:
+                nodes = _slq.nodes(a, b)
+                q = numpy.empty((hi - lo, len(names), etas.size))
+                for f, name in enumerate(names):
                     with numpy.errstate(invalid='ignore', divide='ignore'):
-                        local[:hi - lo, nq + 1 + 2 * i] = _slq.quadrature(nodes, e, fn,
-                                                                          check=False)[:, 0]
-                        local[:hi - lo, nq + 2 + 2 * i] = _slq.quadrature(radau, e, fn,
-                                                                          check=False)[:, 0]
+                        q[:, f] = _slq.quadrature(nodes, etas, _slq.FUNCS[name], check=False)
+                local[:hi - lo, :nq] = q.reshape(hi - lo, nq)
+                local[:hi - lo, nq] = [float(t.min()) for t, _ in nodes]
+                if conv:
+                    # the node from this rank's Ritz values; radau_nodes never raises
+                    node, _ = _slq.radau_node(lower, nodes, etas)
+                    radau = _slq.radau_nodes(a, b, node)
+                    e = [float(etas.min())]
+                    for i, fn in enumerate(conv):
+                        with numpy.errstate(invalid='ignore', divide='ignore'):
+                            local[:hi - lo, nq + 1 + 2 * i] = _slq.quadrature(
+                                nodes, e, fn, check=False)[:, 0]
+                            local[:hi - lo, nq + 2 + 2 * i] = _slq.quadrature(
+                                radau, e, fn, check=False)[:, 0]
+            except (ValueError, numpy.linalg.LinAlgError) as exc:
+                if dist is None or world == 1:
+                    raise
+                err = exc
+                local[:, -1] = 1.0
         if dist is not None and world > 1:
             allv = _all_gather_rows(dist, group, local, world)[:s]
+            if err is not None:
+                raise err
+            if allv[:, -1].any():
+                raise numpy.linalg.LinAlgError(
+                    'slq_sweep: another rank\'s probe shard failed on the host')
         else:
             allv = local[:s]
         _slq.check_shifts(float(allv[:, nq].min()), etas)

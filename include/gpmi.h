@@ -243,6 +243,15 @@ int gpmi_sp_last_status(const gpmi_sp* sp, int* converged);
 /* Device-resident SpMM timing: reps launches of Y = (K + eta I) X with an
  * [n][s] block already in HBM; average ms per launch (HIP events). */
 int gpmi_sp_bench_spmm(gpmi_sp* sp, int s, int reps, double eta, double* avg_ms);
+/* In-step SpMM timing (measurement; no reference counterpart): while enabled,
+ * every SpMM this operator launches (Lanczos, CG, multi-shift CG; either
+ * stream) is bracketed by a HIP event pair on its own stream. set_timing clears
+ * the log (enable = 0 stops logging). spmm_timing sums the logged pairs by block
+ * width s: widths[k], launches[k], total_ms[k] for k < min(*n_widths, max_widths),
+ * ascending s (it waits for the logged launches to finish). */
+int gpmi_sp_set_timing(gpmi_sp* sp, int enable);
+int gpmi_sp_spmm_timing(gpmi_sp* sp, int max_widths, int* n_widths, int* widths,
+                        int* launches, double* total_ms);
 
 /* -------------------------------------------------------------------- band --
  * One-time orthogonal reduction of an operator's K to symmetric band form,

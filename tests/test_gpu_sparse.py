@@ -420,6 +420,39 @@ def test_sparse_operator_slq_vs_exact(gp):
     numpy.testing.assert_allclose(op.dot(0.5, x, 2), 2 * (Kd @ x + 0.5 * x), rtol=1e-13)
 
 
+def test_sparse_slq_lanczos_tol_converges(gp):
+    """imate's lanczos_tol on a SPARSE (tapered, indefinite) K: the Gauss-Radau
+    node is the smallest Ritz value minus a margin (the Gershgorin bound lies
+    below -eta, where log is NaN: ADVICE r4), so the bracket closes at a
+    moderate tolerance instead of running to max_lanczos_degree unconverged;
+    the logdet stays within 4 probe standard errors of the exact value."""
+    from gaussian_proc._mixed_correlation import MixedCorrelation
+    pts = data.generate_points(24, 2, True)
+    K, _ = osp.sparse_correlation(pts, 0.08, 1.5, 0.1)   # Gershgorin -9.3, lambda_min -0.79
+    n = K.shape[0]
+    Kd = K.toarray()
+    lam = numpy.linalg.eigvalsh(Kd)
+    op = MixedCorrelation(K, imate_method='slq',
+                          imate_options={'num_samples': 48, 'lanczos_degree': 8,
+                                         'lanczos_tol': 1e-7})
+    assert op._lower_bound() + 5.0 < 0.0     # the Gershgorin bound is useless here
+    for eta in (1.5, 5.0):
+        val = op.logdet(eta)
+        conv = op.last_slq_convergence
+        assert conv['converged'] and conv['bracket'] <= 1e-7, conv
+        assert conv['degree'] < op.max_lanczos_degree and not conv['rigorous_bound'], conv
+        assert conv['radau_node'] + eta > 0.0
+        ex = float(numpy.sum(numpy.log(lam + eta)))
+        q = n * _slq_probe_values(op, eta)
+        se = q.std(ddof=1) / numpy.sqrt(q.size)
+        assert abs(val - ex) < 4 * se + 1e-9 * abs(ex), (eta, val, ex, se)
+
+
+def _slq_probe_values(op, eta):
+    from gaussian_proc import _slq
+    return _slq.quadrature(op.slq_nodes(), [eta], numpy.log)[:, 0]
+
+
 def test_sparse_hutchinson_traceinv_exponent_3(gp):
     """Sparse 'hutchinson' traceinv of exponent 3: two chained device CG solves
     per probe (rtol 1e-10 here), within 4 standard errors of the eigenvalue sum."""

@@ -62,11 +62,57 @@ def test_radau_of_a_broken_down_probe_is_its_gauss_rule():
     assert _slq.bracket(g, r, [0.1], numpy.log)[0] == 0.0
 
 
-def test_radau_node_above_the_ritz_values_is_refused():
+def test_radau_node_above_the_ritz_values_moves_below_them():
+    """A node that is not below a probe's Ritz values (rounding puts a node a hair
+    below the smallest one on the wrong side: the last pivot d_m <= 0) is moved
+    to that probe's smallest Ritz value minus 1e-8 max|T|: radau_nodes never
+    raises (a rank raising alone inside slq_sweep's all-gather would
+    leave the other ranks blocked), and the rule still brackets."""
     a = numpy.array([[2.0, 2.0]])
     b = numpy.array([[1.0, 0.5]])
-    with pytest.raises(ValueError):
-        _slq.radau_nodes(a, b, 5.0)
+    g = _slq.nodes(a, b)
+    for lower in (5.0, float(g[0][0].min()), float(g[0][0].min()) * (1 - 1e-17)):
+        r = _slq.radau_nodes(a, b, lower)
+        assert r[0][0].size == 3
+        assert r[0][0].min() < g[0][0].min()
+        assert numpy.all(numpy.isfinite(r[0][1]))
+
+
+def test_stemr_failure_falls_back_to_dense_eigh():
+    """The tridiagonal on which LAPACK stemr stops with info = 22 (a plain Lanczos
+    at 130 steps: duplicated Ritz values; tests/golden/make_stemr_fixture.py):
+    _slq._rule returns numpy.linalg.eigh's nodes and squared first components."""
+    import os
+    import scipy.linalg
+    z = numpy.load(os.path.join(os.path.dirname(__file__), 'golden', 'stemr_info22.npz'))
+    d, e = z['d'], z['e']
+    with pytest.raises(numpy.linalg.LinAlgError):
+        scipy.linalg.eigh_tridiagonal(d, e)      # the failure the fallback exists for
+    theta, w = _slq._rule(d, e)
+    T = numpy.diag(d) + numpy.diag(e, 1) + numpy.diag(e, -1)
+    lam, U = numpy.linalg.eigh(T)
+    numpy.testing.assert_array_equal(theta, lam)
+    numpy.testing.assert_array_equal(w, U[0] ** 2)
+    assert abs(w.sum() - 1.0) < 1e-12
+    # nodes() goes through the same rule (one probe, beta padded to the steps)
+    nd = _slq.nodes(d[None, :], numpy.append(e, 1.0)[None, :])
+    numpy.testing.assert_array_equal(nd[0][0], lam)
+
+
+def test_radau_node_choice_keeps_f_finite():
+    """a sparse tapered K's Gershgorin bound lies far below -min(eta),
+    where log / inverse powers are NaN or infinite. radau_node then takes the
+    smallest Ritz value minus a margin (flagged not rigorous); a bound with
+    lower + min(eta) > 0 is kept (rigorous)."""
+    nodes = [(numpy.array([-0.2, 0.5, 3.0]), numpy.array([0.2, 0.3, 0.5]))]
+    node, rig = _slq.radau_node(-5.0, nodes, [0.3, 1.0])
+    assert not rig and -0.3 < node < -0.2
+    assert numpy.isfinite(numpy.log(node + 0.3))
+    node, rig = _slq.radau_node(-0.25, nodes, [0.3])
+    assert rig and node == -0.25
+    # the margin would cross -min(eta): half-way between
+    node, rig = _slq.radau_node(-5.0, nodes, [0.2 + 1e-12])
+    assert not rig and -0.2 - 1e-12 < node < -0.2
 
 
 @pytest.mark.parametrize('method,options', [

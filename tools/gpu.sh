@@ -99,7 +99,9 @@ for task in "$@"; do
     trace-sparse4|trace-sparse5)
       cfg=${task#trace-}
       run 400 $D/trace_$cfg.err rocprofv3 --kernel-trace --stats -d $D/prof_$cfg -o run --output-format csv -- python3 bench.py --config $cfg --steps 3 --warmup 1 --no-cpu-baseline --out-json $D/bench_under_rocprof_$cfg.json
-      python tools/bench_summary.py $D/bench_under_rocprof_$cfg.json ;;
+      python tools/bench_summary.py $D/bench_under_rocprof_$cfg.json
+      python tools/trace_summary.py --timed-spmm $D/prof_$cfg $D/bench_under_rocprof_$cfg.json > $D/spmm_timed_launches_$cfg.json
+      cat $D/spmm_timed_launches_$cfg.json ;;
     host)
       (nproc; cat /sys/fs/cgroup/cpu.max 2>/dev/null; python -c "import os; print('aff', len(os.sched_getaffinity(0)), 'omp', os.environ.get('OMP_NUM_THREADS'))"; lscpu | head -20) > $D/host.txt 2>&1 ;;
     py:*)

@@ -9,11 +9,15 @@ batch-B ``syrk_kernel`` dispatches (Grid_Size_Y = B, the eta batch) are
 (warmup + steps) x launches-per-step; the last steps x launches-per-step of them
 are the timed ones. Prints count / average / total against the bench line's
 HIP-event ``roofline.avg_launch_ms`` (JSON).
+
+``--timed-spmm <trace dir> <bench json> [sparse4|sparse5]``: the same for a sparse
+line's dominant SpMM (the launches between the timing marks; timed_spmm).
 """
 import csv
 import glob
 import json
 import os
+import re
 import sys
 from collections import defaultdict
 
@@ -51,9 +55,56 @@ def timed_syrk(trace_dir, bench_json):
     print(json.dumps(out, indent=1))
 
 
+def timed_spmm(trace_dir, bench_json, config=None):
+    """The sparse line's dominant SpMM in the timed steps of a trace of
+    ``bench.py --config sparseN``: the launches of that kernel instance (its block
+    width) that start between the two ``timing_mark_kernel`` launches bracketing the
+    timed loop (gpmi_sp_set_timing), against the bench line's in-step HIP-event
+    ``roofline.avg_launch_ms``."""
+    with open(bench_json) as fh:
+        line = json.loads([l for l in fh if l.startswith('{')][-1])
+    if config:
+        line = line['sparse_modes'][config]
+    roof = line['roofline']
+    kern, width = re.match(r'(\w+) \(s=(\d+) columns\)', roof['kernel']).groups()
+    files = glob.glob(os.path.join(trace_dir, '**', '*kernel_trace*.csv'), recursive=True)
+    marks, rows = [], []
+    for f in files:
+        with open(f) as fh:
+            for r in csv.DictReader(fh):
+                name = r['Kernel_Name']
+                t = (int(r['Start_Timestamp']), int(r['End_Timestamp']))
+                if 'timing_mark_kernel' in name:
+                    marks.append(t[0])
+                elif kern in name and re.search(r'%s<%s,' % (kern, width), name):
+                    rows.append(t)
+    marks.sort()
+    # the timed window: the last on/off pair of marks before the isolated launches
+    # (the line's set_timing(True) then set_timing(False); earlier pairs: none)
+    assert len(marks) >= 2, marks
+    lo, hi = marks[-2], marks[-1]
+    timed = sorted(t for t in rows if lo <= t[0] <= hi)
+    durs = [(e - s) / 1e6 for s, e in timed]
+    avg = sum(durs) / len(durs)
+    bench_n = roof['in_step_by_width'][width]['launches']
+    alg = roof['algorithmic_bytes_per_launch']
+    out = {'trace_files': [os.path.relpath(f) for f in files], 'kernel': '%s<%s>' % (kern, width),
+           'timed_launches_trace': len(timed), 'timed_launches_bench': bench_n,
+           'trace_avg_launch_ms': round(avg, 5), 'trace_total_ms': round(sum(durs), 3),
+           'bench_avg_launch_ms': roof['avg_launch_ms'],
+           'rel_diff_vs_bench': round(avg / roof['avg_launch_ms'] - 1.0, 5),
+           'algorithmic_bytes_per_launch': round(alg),
+           'trace_gbs': round(alg / (avg * 1e-3) / 1e9, 1),
+           'trace_frac_of_hbm_peak': round(alg / (avg * 1e-3) / 1e9 / roof['peak'], 4),
+           'bench_frac': roof['frac']}
+    print(json.dumps(out, indent=1))
+
+
 def main():
     if sys.argv[1] == '--timed-syrk':
         return timed_syrk(sys.argv[2], sys.argv[3])
+    if sys.argv[1] == '--timed-spmm':
+        return timed_spmm(sys.argv[2], sys.argv[3], sys.argv[4] if len(sys.argv) > 4 else None)
     path = sys.argv[1]
     window_ms = float(sys.argv[2]) if len(sys.argv) > 2 else 0.0
     rows = []
