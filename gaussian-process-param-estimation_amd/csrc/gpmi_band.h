@@ -98,6 +98,14 @@ __global__ void bcr_rhs_even_kernel(const double* W, int64_t sW, const double* Z
                                     int lvl, int m);
 __global__ void bcr_der_final_kernel(const double* g2part, const double* g3part, int nt,
                                      double* der);
+__global__ void bcr_sinv_x_kernel(const double* L, int64_t sL, const double* W, int64_t sW,
+                                  double* X, int64_t sX, int m, int lvl);
+__global__ void bcr_sinv_off_kernel(const double* Zd, int64_t sZd, double* Zo, int64_t sZo,
+                                    const double* X, int64_t sX, int m, int lvl);
+__global__ void bcr_sinv_diag_kernel(const double* L, int64_t sL, const double* X, int64_t sX,
+                                     const double* Zo, int64_t sZo, double* Zd, int64_t sZd,
+                                     double* trpart, int nt, int64_t n, int m, int lvl, int root);
+__global__ void bcr_sinv_final_kernel(const double* trpart, int nt, double* tr, int neta);
 __global__ void bcr_upd_kernel(const double* Ab, int64_t lda, const double* etas, int lvl,
                                const double* Din, int64_t sD, const double* Yin, int64_t sY,
                                const double* W, int64_t sW, const double* Zall, int64_t sZ,

@@ -71,7 +71,7 @@ struct gpmi_band {
   int64_t n = 0, n_pad = 0;
   int nt = 0;
   hipStream_t stream = nullptr;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
   double* Ab = nullptr;      // [n_pad][n_pad]: band (diagonal tiles, triu of subdiagonal
                              // tiles) + Householder vectors below the band
   double* U = nullptr;       // [n_pad][384] = [W | V | W] of the current panel
@@ -154,6 +154,13 @@ struct gpmi_band {
   double* bcrLd = nullptr;   // [bcap][nt]
   int* bcrFail = nullptr;    // [bcap][nt]
   double* bcrF0 = nullptr;   // [nt - 1][128][128]
+  // selected inversion down the reduction tree (traceinv without eigenvalues)
+  double* sinvZd = nullptr;  // [scap][nt][128][128]     diagonal blocks of (B + eta I)^-1
+  double* sinvZo = nullptr;  // [scap][nt][2][128][128]  Z_lp, Z_rp of every eliminated block
+  double* sinvX = nullptr;   // [scap][nt][2][128][128]  X_l, X_r
+  double* sinvTr = nullptr;  // [scap][nt] per-block traces, then [scap] sums
+  int scap = 0;
+  double sinv_ms = 0.0;
   double* cqMinv = nullptr;  // C = U^-T M3 of the current panel
   // T of a CholeskyQR panel from its reconstruction (cq_t_kernel) on the side stream
   // (not a stream of its own: the process's streams share GPU_MAX_HW_QUEUES hardware
@@ -199,7 +206,8 @@ int band_free(gpmi_band* b) {
                     b->cqMinv, b->cqS, b->cqscr, b->cqUS, b->cqW,
                     b->bcrD[0], b->bcrD[1], b->bcrF[0], b->bcrF[1], b->bcrY[0], b->bcrY[1],
                     b->bcrL, b->bcrW, b->bcrZ, b->bcrG, b->bcrLd, b->bcrF0, b->bcrX,
-                    b->bcrZp, b->bcrG2, b->bcrG3};
+                    b->bcrZp, b->bcrG2, b->bcrG3, b->sinvZd, b->sinvZo, b->sinvX,
+                    b->sinvTr};
   if (b->bcrFail) (void)hipFree(b->bcrFail);
   if (b->cqflag) (void)hipFree(b->cqflag);
   if (b->rorder) (void)hipFree(b->rorder);
@@ -211,6 +219,7 @@ int band_free(gpmi_band* b) {
   if (b->cmsg) (void)hipFree(b->cmsg);
   if (b->ev0) (void)hipEventDestroy(b->ev0);
   if (b->ev1) (void)hipEventDestroy(b->ev1);
+  if (b->ev2) (void)hipEventDestroy(b->ev2);
   if (b->stream) (void)hipStreamDestroy(b->stream);
   if (b->side) (void)hipStreamDestroy(b->side);
   if (b->s_pan) (void)hipStreamDestroy(b->s_pan);
@@ -684,6 +693,7 @@ int gpmi_band_create(gpmi_op* op, gpmi_band** out) {
     return fail(e, "stream");
   if ((e = hipEventCreate(&b->ev0)) != hipSuccess) return fail(e, "event");
   if ((e = hipEventCreate(&b->ev1)) != hipSuccess) return fail(e, "event");
+  if ((e = hipEventCreate(&b->ev2)) != hipSuccess) return fail(e, "event");
   if ((e = hipStreamCreateWithFlags(&b->side, hipStreamNonBlocking)) != hipSuccess)
     return fail(e, "side stream");
   if (const char* la = std::getenv("GPMI_BAND_LA")) b->lookahead = std::atoi(la);
@@ -1006,6 +1016,51 @@ int band_der_bcr(gpmi_band* b, int neta, hipStream_t s) {
   return 0;
 }
 
+// tr((B + eta_e I)^-1) for the neta etas whose cyclic-reduction factor band_loglik_bcr
+// left in bcrL / bcrW: selected inversion down the tree, top-down (gpmi_bcr.hip
+// bcr_sinv_*), into sinvTr[nt * scap + e] (device).
+int band_sinv_bcr(gpmi_band* b, int neta, hipStream_t s) {
+  const int nt = b->nt;
+  const size_t blk = (size_t)TS * TS;
+  if (b->scap < neta) {
+    for (double** q : {&b->sinvZd, &b->sinvZo, &b->sinvX, &b->sinvTr})
+      if (*q) {
+        BD_TRY(hipFree(*q));
+        *q = nullptr;
+      }
+    b->scap = 0;
+    BD_TRY(hipMalloc(&b->sinvZd, sizeof(double) * neta * nt * blk));
+    BD_TRY(hipMalloc(&b->sinvZo, sizeof(double) * neta * nt * 2 * blk));
+    BD_TRY(hipMalloc(&b->sinvX, sizeof(double) * neta * nt * 2 * blk));
+    BD_TRY(hipMalloc(&b->sinvTr, sizeof(double) * neta * (nt + 1)));
+    b->scap = neta;
+  }
+  const int64_t sL = (int64_t)nt * blk, sW = 2 * sL, sZd = sL, sZo = 2 * sL, sX = 2 * sL;
+  std::vector<int> ms;   // blocks per level; the last level has one
+  for (int m = nt; m > 1; m = (m + 1) / 2) ms.push_back(m);
+  const int L = (int)ms.size();
+  hipLaunchKernelGGL(bcr_sinv_diag_kernel, dim3(1, neta), dim3(256), 0, s, b->bcrL, sL, b->sinvX,
+                     sX, b->sinvZo, sZo, b->sinvZd, sZd, b->sinvTr, nt, b->n, 1, L, 1);
+  BD_LAUNCH("bcr_sinv_diag_kernel");
+  for (int l = L - 1; l >= 0; --l) {
+    const int nodd = ms[l] / 2;
+    hipLaunchKernelGGL(bcr_sinv_x_kernel, dim3(2 * nodd, neta), dim3(256), 0, s, b->bcrL, sL,
+                       b->bcrW, sW, b->sinvX, sX, ms[l], l);
+    BD_LAUNCH("bcr_sinv_x_kernel");
+    hipLaunchKernelGGL(bcr_sinv_off_kernel, dim3(2 * nodd, neta), dim3(256), 0, s, b->sinvZd, sZd,
+                       b->sinvZo, sZo, b->sinvX, sX, ms[l], l);
+    BD_LAUNCH("bcr_sinv_off_kernel");
+    hipLaunchKernelGGL(bcr_sinv_diag_kernel, dim3(nodd, neta), dim3(256), 0, s, b->bcrL, sL,
+                       b->sinvX, sX, b->sinvZo, sZo, b->sinvZd, sZd, b->sinvTr, nt, b->n, ms[l], l,
+                       0);
+    BD_LAUNCH("bcr_sinv_diag_kernel");
+  }
+  hipLaunchKernelGGL(bcr_sinv_final_kernel, dim3((neta + 63) / 64), dim3(64), 0, s, b->sinvTr, nt,
+                     b->sinvTr + (size_t)nt * neta, neta);
+  BD_LAUNCH("bcr_sinv_final_kernel");
+  return 0;
+}
+
 int gpmi_band_loglik(gpmi_band* b, const double* etas, int neta, double* logdet, double* gram,
                      int* info) {
   if (!b) return set_error(-1006, "null handle");
@@ -1048,6 +1103,11 @@ int gpmi_band_loglik(gpmi_band* b, const double* etas, int neta, double* logdet,
 
 int gpmi_band_der_terms(gpmi_band* b, const double* etas, int neta, double* logdet,
                         double* g1, double* g2, double* g3, int* info) {
+  return gpmi_band_der_terms_ex(b, etas, neta, logdet, g1, g2, g3, nullptr, info);
+}
+
+int gpmi_band_der_terms_ex(gpmi_band* b, const double* etas, int neta, double* logdet,
+                           double* g1, double* g2, double* g3, double* tr1, int* info) {
   if (!b) return set_error(-1006, "null handle");
   if (neta <= 0) return 0;
   if (neta > GPMI_BAND_DER_MAX)
@@ -1071,7 +1131,8 @@ int gpmi_band_der_terms(gpmi_band* b, const double* etas, int neta, double* logd
   hipStream_t s = b->stream;
   BD_TRY(hipMemcpyAsync(b->etas, etas, sizeof(double) * neta, hipMemcpyHostToDevice, s));
   BD_TRY(hipEventRecord(b->ev0, s));
-  if (b->bcr_mode == 1 || (b->bcr_mode == 2 && neta <= 64)) {
+  // tr1 needs the cyclic-reduction factor (the tree it inverts along)
+  if (tr1 || b->bcr_mode == 1 || (b->bcr_mode == 2 && neta <= 64)) {
     rc = band_der_bcr(b, neta, s);
     if (rc) return rc;
   } else {
@@ -1081,6 +1142,15 @@ int gpmi_band_der_terms(gpmi_band* b, const double* etas, int neta, double* logd
     hipLaunchKernelGGL(band_der_kernel, dim3(neta), dim3(256), 0, s, b->fac, nt, b->ysol,
                        b->der);
     BD_LAUNCH("band_der_kernel");
+  }
+  std::vector<double> htr;
+  if (tr1) {
+    BD_TRY(hipEventRecord(b->ev2, s));
+    rc = band_sinv_bcr(b, neta, s);
+    if (rc) return rc;
+    htr.resize(neta);
+    BD_TRY(hipMemcpyAsync(htr.data(), b->sinvTr + (size_t)nt * neta, sizeof(double) * neta,
+                          hipMemcpyDeviceToHost, s));
   }
   BD_TRY(hipEventRecord(b->ev1, s));
   std::vector<double> hout((size_t)neta * OUT_LD), hder((size_t)neta * 2 * RLD * RLD);
@@ -1094,6 +1164,12 @@ int gpmi_band_der_terms(gpmi_band* b, const double* etas, int neta, double* logd
   float ms = 0.f;
   BD_TRY(hipEventElapsedTime(&ms, b->ev0, b->ev1));
   b->der_ms = ms;
+  if (tr1) {
+    float ms2 = 0.f;
+    BD_TRY(hipEventElapsedTime(&ms2, b->ev2, b->ev1));
+    b->sinv_ms = ms2;
+    for (int e = 0; e < neta; ++e) tr1[e] = htr[e];
+  }
   const int m = b->nrhs;
   for (int e = 0; e < neta; ++e) {
     if (logdet) logdet[e] = hout[(size_t)e * OUT_LD];
@@ -1106,6 +1182,43 @@ int gpmi_band_der_terms(gpmi_band* b, const double* etas, int neta, double* logd
       }
     if (info) info[e] = hinfo[e];
   }
+  return 0;
+}
+
+int gpmi_band_traceinv(gpmi_band* b, const double* etas, int neta, double* tr, int* info) {
+  if (!b) return set_error(-1006, "null handle");
+  if (neta <= 0) return 0;
+  if (neta > GPMI_BAND_DER_MAX)
+    return set_error(-1203, "gpmi_band_traceinv: at most GPMI_BAND_DER_MAX etas per call");
+  Guard g(b->device);
+  int rc = ensure_cap(b, neta);
+  if (rc) return rc;
+  hipStream_t s = b->stream;
+  BD_TRY(hipMemcpyAsync(b->etas, etas, sizeof(double) * neta, hipMemcpyHostToDevice, s));
+  BD_TRY(hipEventRecord(b->ev0, s));
+  if ((rc = band_loglik_bcr(b, neta, s))) return rc;
+  BD_TRY(hipEventRecord(b->ev2, s));
+  if ((rc = band_sinv_bcr(b, neta, s))) return rc;
+  BD_TRY(hipEventRecord(b->ev1, s));
+  std::vector<double> htr(neta);
+  std::vector<int> hinfo(neta);
+  BD_TRY(hipMemcpyAsync(htr.data(), b->sinvTr + (size_t)b->nt * neta, sizeof(double) * neta,
+                        hipMemcpyDeviceToHost, s));
+  BD_TRY(hipMemcpyAsync(hinfo.data(), b->info, sizeof(int) * neta, hipMemcpyDeviceToHost, s));
+  BD_TRY(hipStreamSynchronize(s));
+  float ms = 0.f;
+  BD_TRY(hipEventElapsedTime(&ms, b->ev2, b->ev1));
+  b->sinv_ms = ms;
+  for (int e = 0; e < neta; ++e) {
+    tr[e] = htr[e];
+    if (info) info[e] = hinfo[e];
+  }
+  return 0;
+}
+
+int gpmi_band_sinv_ms(gpmi_band* b, double* ms) {
+  if (!b || !ms) return set_error(-1006, "null handle");
+  *ms = b->sinv_ms;
   return 0;
 }
 

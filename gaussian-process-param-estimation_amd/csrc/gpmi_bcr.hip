@@ -455,4 +455,146 @@ __global__ __launch_bounds__(256) void bcr_der_final_kernel(const double* __rest
   der[(int64_t)e * 2 * RLD * RLD + RLD * RLD + t] = b;
 }
 
+// ---------------------------------------------------------------------------
+// trace((B + eta I)^-1) by selected inversion down the reduction tree (round 5):
+// the factor above is a block Cholesky of the odd-even permuted matrix, in which
+// block p of level l (odd) is eliminated before its two neighbours l = p - 1,
+// r = p + 1 of that level, with L_{l,p} = W_l^T and L_{r,p} = W_r^T (bcr_w_kernel).
+// The Takahashi recurrences (Takahashi, Fagan and Chin 1973; Erisman and Tinney,
+// Comm. ACM 18 (1975) 177) need only the inverse's blocks on the factor's pattern:
+//   X_s  = W_s^T Linv_p                          s in {l, r}     bcr_sinv_x_kernel
+//   Z_sp = -(Z_sl X_l + Z_sr X_r)                                bcr_sinv_off_kernel
+//   Z_pp = Linv_p^T Linv_p - X_l^T Z_lp - X_r^T Z_rp              bcr_sinv_diag_kernel
+// top-down from the last level's single block (Z = Linv^T Linv), level by level,
+// every node of a level independent (numpy prototype tools/bcr_sinv_proto.py: the
+// diagonal blocks equal inv(A)'s to 1e-16). The parents' coupling Z_lr is the
+// off-diagonal block their own elimination produced one level up: l' = (p - 1) / 2
+// and r' = l' + 1 there; if r' is odd it is Z_{l', r'} = Zo[o_r][0], else l' is odd and
+// Z_lr = Zo[o_l][1]^T. tr Z_pp over the rows < n (the identity pad is decoupled) per
+// block, summed in block order by bcr_sinv_final_kernel. This replaces the eigenvalue
+// sums sum_i (lambda_i + eta)^-1 of the reference's 'eigenvalue' traceinv
+// (mixed_correlation.py:172-181) without the eigenvalues: O(n b^2) per eta.
+// Blocks by original index o = p << l: Zd[o] (diagonal), Zo[o][2] (Z_lp, Z_rp), X[o][2].
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256, 2) void bcr_sinv_x_kernel(const double* __restrict__ L,
+                                                            int64_t sL,
+                                                            const double* __restrict__ W,
+                                                            int64_t sW, double* __restrict__ X,
+                                                            int64_t sX, int m, int lvl) {
+  __shared__ double smem[4 * GSTAGE];
+  const int e = blockIdx.y;
+  const int h = blockIdx.x >> 1, side = blockIdx.x & 1;
+  const int p = 1 + 2 * h;
+  const int o = p << lvl;
+  if (side == 1 && p + 1 >= m) return;
+  d4 acc[4][4];
+  zero_tile(acc);
+  // X_s = W_s^T Linv_p
+  gemm_tile<KSLOW, KSLOW, false>(W + e * sW + ((int64_t)o * 2 + side) * TS * TS, TS,
+                                 L + e * sL + (int64_t)o * TS * TS, TS, TS, smem, acc);
+  store_tile(X + e * sX + ((int64_t)o * 2 + side) * TS * TS, TS, acc, 1.0);
+}
+
+// acc -= op(M) Xs, op(M) = M (KFAST) or M^T (KSLOW)
+__device__ __forceinline__ void sinv_sub(const double* M, bool trans, const double* Xs,
+                                         double* smem, d4 (&acc)[4][4]) {
+  if (trans)
+    gemm_tile<KSLOW, KSLOW, true>(M, TS, Xs, TS, TS, smem, acc);
+  else
+    gemm_tile<KFAST, KSLOW, true>(M, TS, Xs, TS, TS, smem, acc);
+}
+
+__global__ __launch_bounds__(256, 2) void bcr_sinv_off_kernel(
+    const double* __restrict__ Zd, int64_t sZd, double* __restrict__ Zo, int64_t sZo,
+    const double* __restrict__ X, int64_t sX, int m, int lvl) {
+  __shared__ double smem[4 * GSTAGE];
+  const int e = blockIdx.y;
+  const int h = blockIdx.x >> 1, side = blockIdx.x & 1;
+  const int p = 1 + 2 * h;
+  const bool right = p + 1 < m;
+  if (side == 1 && !right) return;
+  const int o = p << lvl, ol = (p - 1) << lvl, orr = (p + 1) << lvl;
+  const double* Zde = Zd + e * sZd;
+  const double* Zoe = Zo + e * sZo;
+  const double* Xe = X + e * sX;
+  const double* Xl = Xe + ((int64_t)o * 2 + 0) * TS * TS;
+  const double* Xr = Xe + ((int64_t)o * 2 + 1) * TS * TS;
+  // the parents' coupling: stored as Z_lr (r' odd one level up) or Z_rl (l' odd)
+  const double* Mlr = nullptr;
+  bool lr_direct = true;
+  if (right) {
+    const int lp = (p - 1) >> 1;
+    if ((lp + 1) & 1) {
+      Mlr = Zoe + ((int64_t)orr * 2 + 0) * TS * TS;   // Z_{l', r'}
+    } else {
+      Mlr = Zoe + ((int64_t)ol * 2 + 1) * TS * TS;    // Z_{r', l'}
+      lr_direct = false;
+    }
+  }
+  d4 acc[4][4];
+  zero_tile(acc);
+  if (side == 0) {
+    sinv_sub(Zde + (int64_t)ol * TS * TS, false, Xl, smem, acc);   // Z_ll X_l
+    if (right) sinv_sub(Mlr, !lr_direct, Xr, smem, acc);         // Z_lr X_r
+  } else {
+    sinv_sub(Mlr, lr_direct, Xl, smem, acc);                       // Z_rl X_l
+    sinv_sub(Zde + (int64_t)orr * TS * TS, false, Xr, smem, acc);  // Z_rr X_r
+  }
+  store_tile(Zo + e * sZo + ((int64_t)o * 2 + side) * TS * TS, TS, acc, 1.0);
+}
+
+// Z_pp and tr Z_pp (rows < n) of the odd blocks p = 1 + 2 blockIdx.x of level lvl, or
+// (root != 0) the last level's single block 0.
+__global__ __launch_bounds__(256, 2) void bcr_sinv_diag_kernel(
+    const double* __restrict__ L, int64_t sL, const double* __restrict__ X, int64_t sX,
+    const double* __restrict__ Zo, int64_t sZo, double* __restrict__ Zd, int64_t sZd,
+    double* __restrict__ trpart, int nt, int64_t n, int m, int lvl, int root) {
+  __shared__ double smem[4 * GSTAGE];
+  const int e = blockIdx.y;
+  const int p = root ? 0 : 1 + 2 * blockIdx.x;
+  const int o = p << lvl;
+  const double* Lo = L + e * sL + (int64_t)o * TS * TS;
+  d4 acc[4][4];
+  zero_tile(acc);
+  gemm_tile<KSLOW, KSLOW, false>(Lo, TS, Lo, TS, TS, smem, acc);   // Linv^T Linv
+  if (!root) {
+    const double* Xe = X + e * sX;
+    const double* Zoe = Zo + e * sZo;
+    gemm_tile<KSLOW, KSLOW, true>(Xe + ((int64_t)o * 2) * TS * TS, TS,
+                                  Zoe + ((int64_t)o * 2) * TS * TS, TS, TS, smem, acc);
+    if (p + 1 < m)
+      gemm_tile<KSLOW, KSLOW, true>(Xe + ((int64_t)o * 2 + 1) * TS * TS, TS,
+                                    Zoe + ((int64_t)o * 2 + 1) * TS * TS, TS, TS, smem, acc);
+  }
+  store_tile(Zd + e * sZd + (int64_t)o * TS * TS, TS, acc, 1.0);
+  // the trace: diagonal elements (row = wr 64 + a 16 + fk + 4 r == col = wc 64 + a 16 + fr)
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int wr = w >> 1, wc = w & 1, fr = lane & 15, fk = lane >> 4;
+  double v = 0.0;
+  if (wr == wc)
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wr * 64 + a * 16 + fk + 4 * r;
+        if (fk + 4 * r == fr && (int64_t)o * TS + row < n) v += acc[a][a][r];
+      }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  __syncthreads();
+  if (lane == 0) smem[w] = v;
+  __syncthreads();
+  if (t == 0) trpart[(int64_t)e * nt + o] = (smem[0] + smem[1]) + (smem[2] + smem[3]);
+}
+
+// tr[e] = sum_o trpart[e][o] in block order.
+__global__ void bcr_sinv_final_kernel(const double* __restrict__ trpart, int nt,
+                                      double* __restrict__ tr, int neta) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= neta) return;
+  double sum = 0.0;
+  for (int o = 0; o < nt; ++o) sum += trpart[(int64_t)e * nt + o];
+  tr[e] = sum;
+}
+
 }  // namespace gpmi

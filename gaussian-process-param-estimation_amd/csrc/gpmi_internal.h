@@ -89,6 +89,30 @@ struct MsState {
 // (block 0) straight into host-mapped pinned memory: the host reads it after an
 // event behind that kernel (no copy launches; round 4 copied the three fields with
 // three hipMemcpyAsync blits, ~75 us per batch with their gaps).
+// The Chronopoulos-Gear multi-shift CG (ms_cg2_update_kernel): the seed scalars,
+// double-buffered by iteration parity (every block of iteration k reads cur, block 0
+// writes nxt), and the shift state only block 0 touches.
+struct MsScal {
+  double* rr;      // [s] gamma_{k-1} = r_{k-1} . r_{k-1} (cur at iteration k)
+  double* a;       // [s] alpha_{k-1}
+  double* a_prev;  // [s] alpha_{k-2}
+  double* beta;    // [s] beta_{k-2}
+  int* active;     // [s] the column took step k-1
+};
+struct MsShift {
+  double* bn2;     // [s] ||b_c||^2
+  double* z;       // [S][s] zeta_j
+  double* z_prev;  // [S][s]
+  double* bp;      // [S][s'][s] b_c' . p_{j,c}
+  double* g;       // [S][s'][s] accumulated G_j[c'][c]
+  int* flags;      // [1] p^T (K + eta_0 I) p <= 0 in an active column
+  int* it_stop;    // [1] the first iteration with no active column (-1: none yet)
+};
+constexpr int MS_GRP_SP = 64;   // window-SpMM blocks per group of its in-launch dot sums
+constexpr int MS_UB = 512;      // vector blocks of ms_cg2_update_kernel
+constexpr int MS_GRP_U = 16;    // ... per group of its in-launch B^T r sums
+constexpr int MS_DOT_BLK = 64;  // blocks of ms_dots2_kernel (SpMM kinds without the epilogue)
+
 struct MsPin {
   int act[MS_MAXS];
   int flag;

@@ -314,6 +314,53 @@ __global__ __launch_bounds__(256) void csr_spmm_win_kernel(
   }
 }
 
+// Group last-arriver sum inside a launch (the in-launch split-K recipe of the HIP
+// guide, counter form): block `bid` has stored its row part[bid][0, ne) with plain
+// stores; blocks form groups of `grp` consecutive ids; each block drains its stores,
+// releases at agent scope and draws a ticket of its group's counter; the block
+// drawing the group's last ticket resets the counter (zeroed at allocation, so every
+// launch starts from 0), acquires at agent scope and sums the group's rows in
+// ascending id into gred[group][0, ne) (fixed order: deterministic for any
+// dispatch order or workgroup -> XCD placement). The summing block's own loads all
+// follow its acquire (no other block's bytes are read before it).
+__device__ __forceinline__ void group_reduce_rows(const double* part, int ne, int bid, int nblk,
+                                                  int grp, unsigned* gcnt, double* gred) {
+  __shared__ int last_flag;
+  const int t = threadIdx.x;
+  const int g = bid / grp, g0 = g * grp, gn = min(grp, nblk - g0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned old =
+        __hip_atomic_fetch_add(gcnt + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = old == (unsigned)(gn - 1);
+    if (last) {
+      __hip_atomic_store(gcnt + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    last_flag = last;
+  }
+  __syncthreads();
+  if (!last_flag) return;
+  for (int e = t; e < ne; e += blockDim.x) {
+    const double* pr = part + (int64_t)g0 * ne + e;
+    double sum = 0.0;
+    int q = 0;
+    for (; q + 8 <= gn; q += 8) {
+      double v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = pr[(int64_t)(q + u) * ne];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) sum += v[u];
+    }
+    for (; q < gn; ++q) sum += pr[(int64_t)q * ne];
+    gred[(int64_t)g * ne + e] = sum;
+  }
+}
+
 // The one-pass window with its staging latency hidden (round 3): the window rows of
 // X are gathered with NB loads in flight per thread (16-byte loads for even S; a
 // batch covers 8192 doubles, ~410 rows at S = 20), where the round-2 one-pass window
@@ -328,7 +375,7 @@ __global__ __launch_bounds__(64 * TPR) void csr_spmm_wing_kernel(
     const unsigned short* __restrict__ lidx, const double* __restrict__ data, int64_t n,
     const int* __restrict__ wcols, const int* __restrict__ ucount,
     const double* __restrict__ X, double* __restrict__ Y, double eta,
-    double* __restrict__ pqp) {
+    double* __restrict__ pqp, double* __restrict__ gred, unsigned* __restrict__ gcnt) {
   extern __shared__ double smem[];
   // TPR threads per row (4: 256-thread blocks, 8: 512), CG columns each
   constexpr int NT = 64 * TPR;
@@ -423,9 +470,9 @@ __global__ __launch_bounds__(64 * TPR) void csr_spmm_wing_kernel(
       }
     }
   }
-  double xy[CG];
+  double xy[CG], xx[CG];
 #pragma unroll
-  for (int j = 0; j < CG; ++j) xy[j] = 0.0;
+  for (int j = 0; j < CG; ++j) xy[j] = xx[j] = 0.0;
   if (r < nr) {
     const int64_t row = r0 + r;
 #pragma unroll
@@ -435,40 +482,53 @@ __global__ __launch_bounds__(64 * TPR) void csr_spmm_wing_kernel(
         const double y = acc[j] + eta * x;
         Y[row * S + c0 + j] = y;
         xy[j] = x * y;
+        xx[j] = x * x;
       }
   }
   if (pqp) {
     // the block's x . y per column (the multi-shift CG's p . q), rows summed in order:
-    // pqp[b][c]; the window's LDS is free once every thread is past its products
+    // pqp[b][c]; the window's LDS is free once every thread is past its products.
+    // With gred (the Chronopoulos-Gear multi-shift CG, x = r, y = A r): the row
+    // [x . y | x . x] of this block at pqp[blockIdx.x][2S], then the group
+    // last-arriver sum of MS_GRP_SP consecutive blocks' rows into gred[group][2S]
+    // (group_reduce_rows).
+    const int WD = gred ? 2 * S : S;
     __syncthreads();
-    double* red = smem;   // [64][S]
+    double* red = smem;   // [64][WD]
 #pragma unroll
     for (int j = 0; j < CG; ++j)
-      if (c0 + j < S) red[r * S + c0 + j] = xy[j];
+      if (c0 + j < S) {
+        red[r * WD + c0 + j] = xy[j];
+        if (gred) red[r * WD + S + c0 + j] = xx[j];
+      }
     __syncthreads();
-    if (t < S) {
+    if (t < WD) {
       double sum = 0.0;
-      for (int q = 0; q < nr; ++q) sum += red[q * S + t];
-      pqp[b * S + t] = sum;
+      for (int q = 0; q < nr; ++q) sum += red[q * WD + t];
+      if (gred)
+        pqp[(int64_t)blockIdx.x * WD + t] = sum;
+      else
+        pqp[b * S + t] = sum;
     }
+    if (gred) group_reduce_rows(pqp, WD, blockIdx.x, gridDim.x, MS_GRP_SP, gcnt, gred);
   }
 }
 
 template __global__ void csr_spmm_wing_kernel<20, 8, 4>(const int64_t*, const int*,
     const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
-    double*, double, double*);
+    double*, double, double*, double*, unsigned*);
 template __global__ void csr_spmm_wing_kernel<11, 8, 4>(const int64_t*, const int*,
     const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
-    double*, double, double*);
+    double*, double, double*, double*, unsigned*);
 template __global__ void csr_spmm_wing_kernel<12, 8, 4>(const int64_t*, const int*,
     const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
-    double*, double, double*);
+    double*, double, double*, double*, unsigned*);
 template __global__ void csr_spmm_wing_kernel<8, 8, 4>(const int64_t*, const int*,
     const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
-    double*, double, double*);
+    double*, double, double*, double*, unsigned*);
 template __global__ void csr_spmm_wing_kernel<7, 8, 4>(const int64_t*, const int*,
     const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
-    double*, double, double*);
+    double*, double, double*, double*, unsigned*);
 
 // partial[b][j][c] = sum over this block's rows of A_j[i][c] * B[i][c],
 // A_j = A + j * strideA, j = blockIdx.y; grid-stride over rows.
@@ -1458,6 +1518,218 @@ __global__ __launch_bounds__(256) void ms_tail_kernel(MsState cur, MsState nxt,
       pin->act[t] = act_n;
       if (t == 0) pin->flag = cur.flags[0];   // set by ms_rmfma_kernel, before this launch
     }
+  }
+}
+
+// Multi-shift CG, Chronopoulos-Gear form (round 5): ONE launch per iteration besides
+// the SpMM. Iteration k: the SpMM gave w_k = (K + eta_0 I) r_k and, in its epilogue
+// (csr_spmm_wing_kernel with gred, or ms_dots2_kernel), group sums of r_k . w_k and
+// r_k . r_k (dred[ndg][2s]). Every block reduces those rows in the same fixed order
+// and forms, per column (Chronopoulos and Gear, J. Comput. Appl. Math. 25 (1989) 153):
+//   gamma_k = r_k . r_k, delta_k = r_k . w_k, beta_{k-1} = gamma_k / gamma_{k-1}
+//   (0 at k = 0), alpha_k = gamma_k / (delta_k - beta_{k-1} gamma_k / alpha_{k-1}),
+// the denominator being p_k^T (K + eta_0 I) p_k (<= 0 flags the column), and the
+// stop test gamma_k <= rtol^2 ||b||^2. These equal standard CG's alpha, beta in exact
+// arithmetic. The vector blocks (1 .. MS_UB) then form, for active columns,
+//   p_k = r_k + beta_{k-1} p_{k-1},  s_k = w_k + beta_{k-1} s_{k-1}  (= A p_k),
+//   r_{k+1} = r_k - alpha_k s_k,
+// and B^T r_{k+1} on fp64 MFMA (as ms_rmfma_kernel), whose block rows are summed by
+// groups of MS_GRP_U in the launch (group_reduce_rows) into bred[nbg][nb s]. Block 0
+// does no vector work: it sums the previous launch's B^T r_k group rows and takes the
+// shift step k - 1 (the zeta / G / b . p recurrences of ms_tail_kernel, which need
+// beta_{k-1}, known only now), then writes the next scalar state (nxt), the batch end
+// state into pinned memory (pin) and the stopping iteration. One launch of vector
+// work (p, s, r) instead of ms_rmfma + ms_tail, and no separate reduction launches:
+// two dependent launches per iteration instead of five.
+__global__ __launch_bounds__(256) void ms_cg2_update_kernel(
+    const double* __restrict__ B, double* __restrict__ R, const double* __restrict__ W,
+    double* __restrict__ P, double* __restrict__ Sv, MsScal cur, MsScal nxt, MsShift sh,
+    const double* __restrict__ dred, int ndg, const double* __restrict__ bred_prev, int nbg,
+    double* __restrict__ bpart, double* __restrict__ bred, unsigned* __restrict__ bcnt,
+    const double* __restrict__ dshift, int S, int s, int nb, double rtol2, int k, int64_t n,
+    MsPin* __restrict__ pin) {
+  __shared__ double sd[2 * MS_MAXS];
+  __shared__ double sal[MS_MAXS], sbe[MS_MAXS];
+  __shared__ int sup[MS_MAXS], sneg[MS_MAXS];
+  __shared__ double red[4][16 * 16];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  // gamma_k, delta_k: the SpMM's group rows summed in ascending group order
+  if (t < 2 * s) {
+    const int e = t;   // [0, s): r . w, [s, 2s): r . r
+    double sum = 0.0;
+    int q = 0;
+    for (; q + 8 <= ndg; q += 8) {
+      double v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = dred[(int64_t)(q + u) * 2 * s + e];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) sum += v[u];
+    }
+    for (; q < ndg; ++q) sum += dred[(int64_t)q * 2 * s + e];
+    sd[e] = sum;
+  }
+  __syncthreads();
+  if (t < s) {
+    const double delta = sd[t], gamma = sd[s + t];
+    const int act = cur.active[t];
+    const bool upd = act && !(gamma <= rtol2 * sh.bn2[t]);
+    const double be = (k == 0 || !act) ? 0.0 : gamma / cur.rr[t];
+    const double den = be == 0.0 ? delta : delta - be * gamma / cur.a[t];
+    sbe[t] = be;
+    sal[t] = upd ? gamma / den : 0.0;
+    sup[t] = upd ? 1 : 0;
+    sneg[t] = upd && !(den > 0.0);
+  }
+  __syncthreads();
+  if (blockIdx.x != 0) {
+    // ---- vector blocks: p, s, r and the B^T r_{k+1} partials ----
+    const int vb = blockIdx.x - 1, nvb = gridDim.x - 1;
+    const int c = lane & 15, rq = lane >> 4;
+    const bool on = c < s, onb = c < nb;
+    const double al = on ? sal[c] : 0.0, be = on ? sbe[c] : 0.0;
+    const bool up = on && sup[c];
+    d4 acc = {0.0, 0.0, 0.0, 0.0};
+    constexpr int RG = 2;
+    const int64_t stride = (int64_t)nvb * 16;
+    for (int64_t base = (int64_t)vb * 16 + wv * 4; base < n; base += RG * stride) {
+      double bv[RG], rv[RG], wv_[RG], pv[RG], sv[RG];
+#pragma unroll
+      for (int u = 0; u < RG; ++u) {
+        const int64_t i = base + u * stride + rq;
+        const bool v = on && i < n, w = onb && i < n;
+        bv[u] = w ? B[i * nb + c] : 0.0;
+        rv[u] = v ? R[i * s + c] : 0.0;
+        wv_[u] = v ? W[i * s + c] : 0.0;
+        pv[u] = v ? P[i * s + c] : 0.0;
+        sv[u] = v ? Sv[i * s + c] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < RG; ++u) {
+        const int64_t i = base + u * stride + rq;
+        double rn = rv[u];
+        if (up && i < n) {
+          const double pn = rv[u] + be * pv[u];
+          const double sn = wv_[u] + be * sv[u];
+          rn = rv[u] - al * sn;
+          P[i * s + c] = pn;
+          Sv[i * s + c] = sn;
+          R[i * s + c] = rn;
+        }
+        acc = mfma64(bv[u], rn, acc);
+      }
+    }
+    // C map: row (c') = rq + 4 j, column (c) = lane & 15
+#pragma unroll
+    for (int j = 0; j < 4; ++j) red[wv][(rq + 4 * j) * 16 + c] = acc[j];
+    __syncthreads();
+    const int neb = nb * s;
+    for (int e = t; e < neb; e += 256) {
+      const int cp = e / s, cc = e - cp * s;
+      const int idx = cp * 16 + cc;
+      bpart[(int64_t)vb * neb + e] = (red[0][idx] + red[1][idx]) + (red[2][idx] + red[3][idx]);
+    }
+    group_reduce_rows(bpart, neb, vb, nvb, MS_GRP_U, bcnt, bred);
+    return;
+  }
+  // ---- block 0: shift step k - 1, the next scalar state ----
+  __shared__ double brd[MS_MAXS * MS_MAXS];
+  const int neb = nb * s;
+  if (k >= 1)
+    for (int e = t; e < neb; e += 256) {
+      double sum = 0.0;
+      for (int q = 0; q < nbg; ++q) sum += bred_prev[(int64_t)q * neb + e];
+      brd[e] = sum;
+    }
+  __syncthreads();
+  if (k >= 1)
+    for (int task = t; task < S * s; task += blockDim.x) {
+      const int j = task / s, c = task % s;
+      if (!cur.active[c]) continue;   // step k - 1 not taken by this column
+      const double a = cur.a[c], ap = cur.a_prev[c], bo = cur.beta[c];
+      const double z = sh.z[j * s + c], zp = sh.z_prev[j * s + c];
+      const double d = dshift[j];
+      const double zn = z * zp * ap / (a * bo * (zp - z) + zp * ap * (1.0 + d * a));
+      const double as = a * zn / z;
+      const double bs = sbe[c] * (zn / z) * (zn / z);
+      double bpv[MS_MAXS], gv[MS_MAXS];
+#pragma unroll
+      for (int cp = 0; cp < MS_MAXS; ++cp) {
+        const int e = (j * nb + cp) * s + c;
+        bpv[cp] = cp < nb ? sh.bp[e] : 0.0;
+        gv[cp] = cp < nb ? sh.g[e] : 0.0;
+      }
+#pragma unroll
+      for (int cp = 0; cp < MS_MAXS; ++cp) {
+        if (cp >= nb) break;
+        const int e = (j * nb + cp) * s + c;
+        sh.g[e] = gv[cp] + as * bpv[cp];
+        sh.bp[e] = zn * brd[cp * s + c] + bs * bpv[cp];
+      }
+      sh.z_prev[j * s + c] = z;
+      sh.z[j * s + c] = zn;
+    }
+  if (t < s) {
+    const int act = cur.active[t];
+    if (act) {
+      nxt.rr[t] = sd[s + t];
+      nxt.a[t] = sal[t];
+      nxt.a_prev[t] = cur.a[t];
+      nxt.beta[t] = sbe[t];
+    } else {
+      nxt.rr[t] = cur.rr[t];
+      nxt.a[t] = cur.a[t];
+      nxt.a_prev[t] = cur.a_prev[t];
+      nxt.beta[t] = cur.beta[t];
+    }
+    nxt.active[t] = sup[t];
+    if (sneg[t]) sh.flags[0] = 1;
+  }
+  __syncthreads();
+  if (t == 0) {
+    bool before = false, after = false;
+    for (int c = 0; c < s; ++c) {
+      before = before || cur.active[c];
+      after = after || sup[c];
+    }
+    if (before && !after && sh.it_stop[0] < 0) sh.it_stop[0] = k;
+  }
+  if (pin && t < s) {   // the batch's end state for the host (pinned, device-mapped)
+    pin->rr[t] = cur.active[t] ? sd[s + t] : cur.rr[t];
+    pin->act[t] = sup[t];
+    if (t == 0) pin->flag = sh.flags[0];
+  }
+}
+
+// Group rows of x . y and x . x per column ([blockIdx.x][2s]: x . y, then x . x) for
+// SpMM kinds without the dot epilogue: MS_DOT_BLK blocks, each a contiguous range of
+// rows, rows_per = 256 / s rows per block pass, summed in a fixed order.
+__global__ __launch_bounds__(256) void ms_dots2_kernel(const double* __restrict__ X,
+                                                       const double* __restrict__ Y, int64_t n,
+                                                       int s, double* __restrict__ out) {
+  __shared__ double red[2][256];
+  const int t = threadIdx.x;
+  const int rows_per = 256 / s;
+  const int c = t % s, r = t / s;
+  const int64_t chunk = (n + gridDim.x - 1) / gridDim.x;
+  const int64_t lo = (int64_t)blockIdx.x * chunk, hi = min(n, lo + chunk);
+  double xy = 0.0, xx = 0.0;
+  if (r < rows_per)
+    for (int64_t i = lo + r; i < hi; i += rows_per) {
+      const double x = X[i * s + c], y = Y[i * s + c];
+      xy += x * y;
+      xx += x * x;
+    }
+  red[0][t] = xy;
+  red[1][t] = xx;
+  __syncthreads();
+  if (t < s) {
+    double a = 0.0, b = 0.0;
+    for (int q = 0; q < rows_per; ++q) {
+      a += red[0][q * s + t];
+      b += red[1][q * s + t];
+    }
+    out[(int64_t)blockIdx.x * 2 * s + t] = a;
+    out[(int64_t)blockIdx.x * 2 * s + s + t] = b;
   }
 }
 

@@ -47,7 +47,8 @@ __global__ void csr_spmm_win_kernel(const int64_t*, const int*, const unsigned s
 template <int S, int U, int TPR>
 __global__ void csr_spmm_wing_kernel(const int64_t*, const int*, const unsigned short*,
                                      const double*, int64_t, const int*, const int*,
-                                     const double*, double*, double, double*);
+                                     const double*, double*, double, double*, double*,
+                                     unsigned*);
 constexpr int WING_MAX_LDS = 80 * 1024;   // two workgroups per CU
 // nonzeros in flight per thread and threads per row of csr_spmm_wing_kernel (measured:
 // 8 in flight best at cfg 5, within 0.3 us of 4 at cfg 4; 8 threads per row in
@@ -97,6 +98,11 @@ __global__ void ms_rmfma_kernel(const double*, double*, const double*, MsState, 
 __global__ void ms_tail_kernel(MsState, MsState, const double*, const double*, int, int, int, double,
                                double*, const double*, int64_t, MsPin*);
 __global__ void ms_init_kernel(MsState, const double*, int, int, int, int);
+__global__ void ms_cg2_update_kernel(const double*, double*, const double*, double*, double*,
+                                     MsScal, MsScal, MsShift, const double*, int, const double*,
+                                     int, double*, double*, unsigned*, const double*, int, int,
+                                     int, double, int, int64_t, MsPin*);
+__global__ void ms_dots2_kernel(const double*, const double*, int64_t, int, double*);
 template <int CT>
 __global__ void dense_mm_kernel(const double*, int64_t, int64_t, const double*, int, int, double*);
 __global__ void dense_mm_reduce_kernel(const double*, int, int64_t, const double*, double, double*);
@@ -181,6 +187,10 @@ struct gpmi_sp {
   double* ms_partial = nullptr;
   size_t ms_partial_doubles = 0;
   void* ms_pin = nullptr;                  // pinned flags / r.r of two CG batches
+  double* cg2_buf = nullptr;               // the Chronopoulos-Gear form's dot rows
+  size_t cg2_doubles = 0;
+  unsigned* cg2_cnt = nullptr;             // ... and its group counters (kept zero)
+  size_t cg2_cnt_n = 0;
   hipEvent_t ms_ev[2] = {nullptr, nullptr};
   std::mutex win_mu;           // the lazy X-window build (ensure_window)
   size_t msbuf_doubles = 0;
@@ -360,7 +370,7 @@ int spmm_kind(gpmi_sp* sp, int s, int* kind) {
 // X . Y per column (pqp[block][s], the multi-shift CG's p . q) and sets *pq_blocks to
 // their count; otherwise *pq_blocks = 0 and the caller forms them.
 int spmm_launch(gpmi_sp* sp, const double* X, double* Y, int s, double eta, hipStream_t st,
-                double* pqp, int* pq_blocks) {
+                double* pqp, int* pq_blocks, double* gred, unsigned* gcnt) {
   if (pq_blocks) *pq_blocks = 0;
   if (sp->dK) {
     // dense: split partials of K X on fp64 MFMA, summed in split order (+ eta X)
@@ -387,9 +397,11 @@ int spmm_launch(gpmi_sp* sp, const double* X, double* Y, int s, double eta, hipS
       ((reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(Y)) & 15) != 0)
     kind = 0;
   if (kind == 5) {
-    // the window, and the epilogue's [64][s] row partials of X . Y (pqp)
+    // the window, and the epilogue's [64][s] row partials of X . Y (pqp), or with gred
+    // the [64][2s] rows of X . Y and X . X and their group sums (the CG-CG form)
     const size_t lds = sizeof(double) * (size_t)s *
-                       (size_t)std::max(sp->win_maxu.load(std::memory_order_acquire), WIN_ROWS_HOST);
+                       (size_t)std::max(sp->win_maxu.load(std::memory_order_acquire),
+                                        (gred ? 2 : 1) * WIN_ROWS_HOST);
     auto kfn = s == 20   ? csr_spmm_wing_kernel<20, WING_U, WING_TPR>
                : s == 12 ? csr_spmm_wing_kernel<12, WING_U, WING_TPR>
                : s == 11 ? csr_spmm_wing_kernel<11, WING_U, WING_TPR>
@@ -398,9 +410,10 @@ int spmm_launch(gpmi_sp* sp, const double* X, double* Y, int s, double eta, hipS
     const int tpr = WING_TPR;
     hipLaunchKernelGGL(kfn, dim3((unsigned)sp->win_nblk), dim3(64 * tpr), lds, st, sp->indptr,
                        sp->indices, sp->win_lidx, sp->data, sp->n, sp->win_cols, sp->win_u, X, Y,
-                       eta, pqp);
+                       eta, pqp, gred, gcnt);
     SP_LAUNCH("csr_spmm_wing_kernel");
-    if (pqp && pq_blocks) *pq_blocks = (int)sp->win_nblk;
+    if (pqp && pq_blocks)
+      *pq_blocks = gred ? (int)((sp->win_nblk + MS_GRP_SP - 1) / MS_GRP_SP) : (int)sp->win_nblk;
     return 0;
   }
   if (kind == 1) {
@@ -444,9 +457,10 @@ int take_event(gpmi_sp* sp, hipEvent_t* e) {
 // Y = (K + eta I) X (spmm_launch), bracketed by a HIP event pair on its stream when
 // in-step timing is on (gpmi_sp_set_timing).
 int spmm(gpmi_sp* sp, const double* X, double* Y, int s, double eta, hipStream_t st = nullptr,
-         double* pqp = nullptr, int* pq_blocks = nullptr) {
+         double* pqp = nullptr, int* pq_blocks = nullptr, double* gred = nullptr,
+         unsigned* gcnt = nullptr) {
   if (!st) st = sp->stream;
-  if (!sp->timing) return spmm_launch(sp, X, Y, s, eta, st, pqp, pq_blocks);
+  if (!sp->timing) return spmm_launch(sp, X, Y, s, eta, st, pqp, pq_blocks, gred, gcnt);
   gpmi_sp::SpmmRec rec{nullptr, nullptr, s};
   {
     std::lock_guard<std::mutex> lock(sp->timing_mu);
@@ -454,7 +468,7 @@ int spmm(gpmi_sp* sp, const double* X, double* Y, int s, double eta, hipStream_t
     if (int rc = take_event(sp, &rec.e1)) return rc;
   }
   SP_TRY(hipEventRecord(rec.e0, st));
-  if (int rc = spmm_launch(sp, X, Y, s, eta, st, pqp, pq_blocks)) return rc;
+  if (int rc = spmm_launch(sp, X, Y, s, eta, st, pqp, pq_blocks, gred, gcnt)) return rc;
   SP_TRY(hipEventRecord(rec.e1, st));
   std::lock_guard<std::mutex> lock(sp->timing_mu);
   sp->spmm_log.push_back(rec);
@@ -1001,6 +1015,8 @@ int gpmi_sp_destroy(gpmi_sp* sp) {
   if (sp->rhs_dev) (void)hipFree(sp->rhs_dev);
   if (sp->ms_partial) (void)hipFree(sp->ms_partial);
   if (sp->ms_pin) (void)hipHostFree(sp->ms_pin);
+  if (sp->cg2_buf) (void)hipFree(sp->cg2_buf);
+  if (sp->cg2_cnt) (void)hipFree(sp->cg2_cnt);
   for (hipEvent_t e : sp->ev_pool) (void)hipEventDestroy(e);
   for (auto& r : sp->spmm_log) {
     (void)hipEventDestroy(r.e0);
@@ -1289,6 +1305,283 @@ int gpmi_sp_cg(gpmi_sp* sp, double eta, const double* rhs, int64_t ld, int nrhs,
   return 0;
 }
 
+// The multi-shift CG in the Chronopoulos-Gear form (round 5, the default;
+// GPMI_MS_CG=classic keeps the standard form below): per iteration the SpMM
+// w = (K + eta_0 I) r with the r . w / r . r group sums in its epilogue (window SpMM;
+// other kinds: + ms_dots2_kernel), then ms_cg2_update_kernel (the scalars, p, s, r,
+// B^T r, and the shift step of the previous iteration): two dependent launches per
+// iteration instead of five. Same arguments, results and polling as msgram_impl.
+static int msgram_cg2(gpmi_sp* sp, const double* etas, int neta, const double* rhs,
+                      int64_t ld, int nrhs, int c_lo, int c_hi, double rtol, int maxiter,
+                      double* G, int* iterations) {
+  const int nsub = c_hi - c_lo;
+  const bool full = nsub == nrhs;
+  Guard g(sp->device);
+  const int64_t n = sp->n;
+  const int S = neta;
+  int s = nsub;
+  int kind = 0;
+  {
+    int rc0 = spmm_kind(sp, s, &kind);
+    if (rc0) return rc0;
+    // the window SpMM stages 12-column rows with 16-byte loads (see msgram_impl)
+    if (full && kind == 5 && s == 11 && S * (s + 1) <= 1024) ++s;
+    if ((rc0 = spmm_kind(sp, s, &kind))) return rc0;
+  }
+  const int nbd = full ? s : nrhs;
+  const int64_t nsb = n * nbd;
+  if (!sp->ms_stream) SP_TRY(hipStreamCreateWithFlags(&sp->ms_stream, hipStreamNonBlocking));
+  const int64_t ns = n * s;
+  const double eta0 = *std::min_element(etas, etas + neta);
+  int rc = 0;
+  auto even = [](size_t d) { return (d + 1) & ~(size_t)1; };
+  // B [n][nbd], the host staging [n][nrhs], and R, W, P, S [n][s] (16-byte aligned)
+  const size_t wsn = even((size_t)nsb) + even((size_t)n * nrhs) + 4 * even((size_t)ns);
+  if (sp->ms_ws_doubles < wsn) {
+    if (sp->ms_ws) SP_TRY(hipFree(sp->ms_ws));
+    sp->ms_ws = nullptr;
+    SP_TRY(hipMalloc(&sp->ms_ws, sizeof(double) * wsn));
+    sp->ms_ws_doubles = wsn;
+  }
+  double* Bd = sp->ms_ws;
+  double* Hs = Bd + even((size_t)nsb);
+  double* Rd = Hs + even((size_t)n * nrhs);
+  double* Wd = Rd + even((size_t)ns);
+  double* Pd = Wd + even((size_t)ns);
+  double* Sd = Pd + even((size_t)ns);
+  // dot rows: the SpMM's per-block [nblk][2s] and group [ndg][2s]; the update's B^T r
+  // per-block [MS_UB][nbd s] and group rows [2][nbg][nbd s] (parity: iteration k + 1
+  // reads k's while writing its own); the init partials [MS_NBLK][ne]; the group
+  // counters (zeroed here once: every group's last arriver resets its own)
+  const int64_t nblk_sp = kind == 5 ? sp->win_nblk : MS_DOT_BLK;
+  const int ndg = kind == 5 ? (int)((nblk_sp + MS_GRP_SP - 1) / MS_GRP_SP) : MS_DOT_BLK;
+  const int neb = nbd * s;
+  const int nbg = (MS_UB + MS_GRP_U - 1) / MS_GRP_U;
+  const int ne0 = nbd * s + s;
+  const size_t c_sp = (size_t)nblk_sp * 2 * s, c_dg = (size_t)ndg * 2 * s;
+  const size_t c_bp = (size_t)MS_UB * neb, c_bg = (size_t)nbg * neb;
+  const size_t c_init = (size_t)MS_NBLK * ne0;
+  const size_t need = c_sp + c_dg + c_bp + 2 * c_bg + c_init;
+  if (sp->cg2_doubles < need) {
+    if (sp->cg2_buf) SP_TRY(hipFree(sp->cg2_buf));
+    sp->cg2_buf = nullptr;
+    SP_TRY(hipMalloc(&sp->cg2_buf, sizeof(double) * need));
+    sp->cg2_doubles = need;
+  }
+  // the group counters live in an allocation of their own, zeroed once: every
+  // launch's last arrivers leave them at zero again, whatever the layout above
+  const size_t n_cnt = (size_t)ndg + 1 + (size_t)nbg + 1;
+  if (sp->cg2_cnt_n < n_cnt) {
+    if (sp->cg2_cnt) SP_TRY(hipFree(sp->cg2_cnt));
+    sp->cg2_cnt = nullptr;
+    const size_t cap = std::max<size_t>(n_cnt, 2048);
+    SP_TRY(hipMalloc(&sp->cg2_cnt, sizeof(unsigned) * cap));
+    SP_TRY(hipMemset(sp->cg2_cnt, 0, sizeof(unsigned) * cap));
+    sp->cg2_cnt_n = cap;
+  }
+  double* spart = sp->cg2_buf;
+  double* dred = spart + c_sp;
+  double* bpart = dred + c_dg;
+  double* bred2[2] = {bpart + c_bp, bpart + c_bp + c_bg};
+  double* ipart = bred2[1] + c_bg;
+  unsigned* gcnt_sp = sp->cg2_cnt;
+  unsigned* gcnt_u = gcnt_sp + ndg + 1;
+  // scalar state: MsScal x 2, MsShift, and the old MsState view for ms_init_kernel
+  const size_t sneed = 2 * (4 * (size_t)s + s) + (size_t)s + 2 * (size_t)S * s +
+                       2 * (size_t)S * nbd * s + S + 4;
+  if (sp->msbuf_doubles < sneed) {
+    if (sp->msbuf) SP_TRY(hipFree(sp->msbuf));
+    sp->msbuf = nullptr;
+    SP_TRY(hipMalloc(&sp->msbuf, sizeof(double) * sneed));
+    sp->msbuf_doubles = sneed;
+  }
+  double* q = sp->msbuf;
+  MsScal sc[2];
+  for (int b = 0; b < 2; ++b) {
+    sc[b].rr = q; q += s;
+    sc[b].a = q; q += s;
+    sc[b].a_prev = q; q += s;
+    sc[b].beta = q; q += s;
+    sc[b].active = reinterpret_cast<int*>(q); q += s;
+  }
+  MsShift sh;
+  sh.bn2 = q; q += s;
+  sh.z = q; q += (size_t)S * s;
+  sh.z_prev = q; q += (size_t)S * s;
+  sh.bp = q; q += (size_t)S * nbd * s;
+  sh.g = q; q += (size_t)S * nbd * s;
+  double* dshift = q; q += S;
+  sh.flags = reinterpret_cast<int*>(q); q += 1;
+  sh.it_stop = reinterpret_cast<int*>(q); q += 1;
+  MsState st{};   // ms_init_kernel's view: cur[0] scalars + the shift state
+  st.rr = sc[0].rr;
+  st.a = sc[0].a;
+  st.a_prev = sc[0].a_prev;
+  st.beta = sc[0].beta;
+  st.active = sc[0].active;
+  st.bn2 = sh.bn2;
+  st.z = sh.z;
+  st.z_prev = sh.z_prev;
+  st.bp = sh.bp;
+  st.g = sh.g;
+  st.flags = sh.flags;
+  sp->last_converged = 0;
+  hipStream_t str = sp->ms_stream;
+  {
+    const double* Hsrc = Hs;
+    if (!rhs) {
+      Hsrc = sp->rhs_dev;
+    } else if (ld == nrhs) {
+      SP_TRY(hipMemcpyAsync(Hs, rhs, sizeof(double) * n * nrhs, hipMemcpyHostToDevice, str));
+    } else {
+      std::vector<double> h((size_t)n * nrhs);
+      for (int64_t i = 0; i < n; ++i)
+        for (int c = 0; c < nrhs; ++c) h[(size_t)i * nrhs + c] = rhs[i * ld + c];
+      SP_TRY(hipMemcpyAsync(Hs, h.data(), sizeof(double) * h.size(), hipMemcpyHostToDevice, str));
+      SP_TRY(hipStreamSynchronize(str));
+    }
+    hipLaunchKernelGGL(rows_gather_kernel, dim3(grid_ns(n, nbd)), dim3(256), 0, str, Hsrc, nrhs,
+                       (const int*)sp->perm_d, n, nbd, Bd);
+    SP_LAUNCH("rows_gather_kernel");
+    std::vector<double> hd(S);
+    for (int j = 0; j < S; ++j) hd[j] = etas[j] - eta0;
+    SP_TRY(hipMemcpyAsync(dshift, hd.data(), sizeof(double) * S, hipMemcpyHostToDevice, str));
+    if (full) {
+      SP_TRY(hipMemcpyAsync(Rd, Bd, sizeof(double) * ns, hipMemcpyDeviceToDevice, str));
+    } else {
+      hipLaunchKernelGGL(rows_gather_kernel, dim3(grid_ns(n, s)), dim3(256), 0, str, Bd + c_lo,
+                         nbd, (const int*)nullptr, n, s, Rd);
+      SP_LAUNCH("rows_gather_kernel");
+    }
+    // p_{-1} = s_{-1} = 0 (beta_{-1} = 0 multiplies them: no NaN may stand there)
+    SP_TRY(hipMemsetAsync(Pd, 0, sizeof(double) * 2 * even((size_t)ns), str));
+    const int minus1 = -1;
+    SP_TRY(hipMemcpyAsync(sh.it_stop, &minus1, sizeof(int), hipMemcpyHostToDevice, str));
+  }
+  launch_ms_dots(Bd, Rd, n, s, ipart, MS_NBLK, str, nbd);
+  SP_LAUNCH("ms_dots_partial_kernel");
+  hipLaunchKernelGGL(ms_init_kernel, dim3(1), dim3(1024), 0, str, st, ipart, MS_NBLK, S, s, nbd);
+  SP_LAUNCH("ms_init_kernel");
+  // alpha_{-1} = 1 (ms_init_kernel leaves a = 0, a_prev = 1: the standard form's
+  // state before its first iteration): a_prev into a
+  SP_TRY(hipMemcpyAsync(sc[0].a, sc[0].a_prev, sizeof(double) * s, hipMemcpyDeviceToDevice, str));
+  int it = 0;
+  // one iteration's launches on str (parity it & 1 picks the scalar and B^T r buffers)
+  auto iterate = [&](int k, MsPin* pin_out) -> int {
+    int ng = 0;
+    int rc1 = spmm(sp, Rd, Wd, s, eta0, str, spart, &ng, dred, gcnt_sp);
+    if (rc1) return rc1;
+    if (ng == 0) {
+      hipLaunchKernelGGL(ms_dots2_kernel, dim3(MS_DOT_BLK), dim3(256), 0, str, (const double*)Rd,
+                         (const double*)Wd, n, s, dred);
+      SP_LAUNCH("ms_dots2_kernel");
+      ng = MS_DOT_BLK;
+    }
+    hipLaunchKernelGGL(ms_cg2_update_kernel, dim3(MS_UB + 1), dim3(256), 0, str,
+                       (const double*)Bd, Rd, (const double*)Wd, Pd, Sd, sc[k & 1],
+                       sc[(k + 1) & 1], sh, (const double*)dred, ng,
+                       (const double*)bred2[(k + 1) & 1], nbg, bpart, bred2[k & 1], gcnt_u,
+                       (const double*)dshift, S, s, nbd, rtol * rtol, k, n, pin_out);
+    SP_LAUNCH("ms_cg2_update_kernel");
+    return 0;
+  };
+  if (!sp->ms_pin) {
+    SP_TRY(hipHostMalloc(reinterpret_cast<void**>(&sp->ms_pin), 2 * sizeof(MsPin),
+                         hipHostMallocCoherent | hipHostMallocMapped));
+    for (hipEvent_t* e : {&sp->ms_ev[0], &sp->ms_ev[1]})
+      SP_TRY(hipEventCreateWithFlags(e, hipEventDisableTiming));
+  }
+  MsPin* pin = reinterpret_cast<MsPin*>(sp->ms_pin);
+  MsPin* pin_dev = nullptr;
+  SP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&pin_dev), sp->ms_pin, 0));
+  std::vector<double> hbn2(s);
+  std::vector<int> hact(s);
+  SP_TRY(hipMemcpyAsync(hbn2.data(), sh.bn2, sizeof(double) * s, hipMemcpyDeviceToHost, str));
+  SP_TRY(hipMemcpyAsync(hact.data(), sc[0].active, sizeof(int) * s, hipMemcpyDeviceToHost, str));
+  SP_TRY(hipStreamSynchronize(str));
+  {
+    bool any = false;
+    for (int c = 0; c < s; ++c) any = any || hact[c];
+    if (!any) maxiter = 0;
+  }
+  // batches between host reads of the end state, sized from the residual decay (as
+  // msgram_impl); iteration k's end state is gamma_k (the residual entering it)
+  int slot_it[2] = {0, 0};
+  std::vector<double> rr_seen(s, -1.0);
+  int it_seen = 0;
+  bool prev = false;
+  int nb = MS_BATCH;
+  int kb = 0;
+  auto read_slot = [&](int qs, int* remaining_after) -> int {
+    SP_TRY(hipEventSynchronize(sp->ms_ev[qs]));
+    if (pin[qs].flag) {
+      SP_TRY(hipStreamSynchronize(str));
+      return set_error(1, "multi-shift CG: p^T (K + min(eta) I) p <= 0 (not positive definite)");
+    }
+    bool any = false;
+    double needm = 0.0;
+    const int at = slot_it[qs];
+    for (int c = 0; c < s; ++c) {
+      if (!pin[qs].act[c]) continue;
+      any = true;
+      const double r1 = pin[qs].rr[c], r0 = rr_seen[c], target = rtol * rtol * hbn2[c];
+      double m = (double)MS_BATCH;
+      if (r0 > 0.0 && r1 > 0.0 && r1 < r0 && at > it_seen && target > 0.0)
+        m = std::log(target / r1) / (std::log(r1 / r0) / (double)(at - it_seen));
+      needm = std::max(needm, m);
+      rr_seen[c] = r1;
+    }
+    it_seen = at;
+    // clamped before the conversion: a stagnating residual (r1 / r0 -> 1) gives a huge m
+    const double rem = std::min((double)maxiter, std::ceil((double)at + needm)) - (double)it;
+    *remaining_after = (int)std::max(-1.0, std::min(rem, (double)MS_BATCH));
+    return any ? 0 : 2;
+  };
+  while (it < maxiter) {
+    nb = std::max(1, std::min(nb, maxiter - it));
+    const int qs = kb & 1;
+    for (int i = 0; i < nb; ++i, ++it)
+      if ((rc = iterate(it, i + 1 == nb ? pin_dev + qs : nullptr))) return rc;
+    SP_TRY(hipEventRecord(sp->ms_ev[qs], str));
+    slot_it[qs] = it;
+    ++kb;
+    int rem = MS_BATCH;
+    if (prev) {
+      const int r = read_slot(qs ^ 1, &rem);
+      if (r == 2) break;
+      if (r) return r;
+    }
+    prev = true;
+    if (rem <= 0) {
+      int rem2 = 0;
+      const int r = read_slot(qs, &rem2);
+      if (r == 2) break;
+      if (r) return r;
+      prev = false;
+      rem = rem2;
+    }
+    nb = std::max(1, std::min(MS_BATCH, rem));
+  }
+  int flag = 0, it_stop = -1;
+  SP_TRY(hipMemcpyAsync(hact.data(), sc[it & 1].active, sizeof(int) * s, hipMemcpyDeviceToHost, str));
+  SP_TRY(hipMemcpyAsync(&flag, sh.flags, sizeof(int), hipMemcpyDeviceToHost, str));
+  SP_TRY(hipMemcpyAsync(&it_stop, sh.it_stop, sizeof(int), hipMemcpyDeviceToHost, str));
+  std::vector<double> hg((size_t)S * nbd * s);
+  SP_TRY(hipMemcpyAsync(hg.data(), sh.g, sizeof(double) * hg.size(), hipMemcpyDeviceToHost, str));
+  SP_TRY(hipStreamSynchronize(str));
+  if (flag)
+    return set_error(1, "multi-shift CG: p^T (K + min(eta) I) p <= 0 (not positive definite)");
+  bool any = false;
+  for (int c = 0; c < s; ++c) any = any || hact[c];
+  sp->last_converged = any ? 0 : 1;
+  for (int j = 0; j < S; ++j)
+    for (int a = 0; a < nrhs; ++a)
+      for (int c = 0; c < nsub; ++c)
+        G[((size_t)j * nrhs + a) * nsub + c] = hg[((size_t)j * nbd + a) * s + c];
+  if (iterations) *iterations = it_stop >= 0 ? it_stop : it;
+  return 0;
+}
+
 // Multi-shift CG Gram blocks for the right-hand sides B[:, c_lo:c_hi] of the nb-column
 // host block B (every eta): G[j][a][c] = b_a^T (K + eta_j I)^-1 b_{c_lo + c}, a < nb
 // (the dots run over all of B, so a shard of columns gives complete G columns).
@@ -1304,6 +1597,11 @@ static int msgram_impl(gpmi_sp* sp, const double* etas, int neta, const double* 
       neta * (c_hi - c_lo) > 1024)
     return set_error(-1104, "msgram: need 1 <= nrhs <= 16, 0 <= c_lo < c_hi <= nrhs and "
                             "neta * (c_hi - c_lo) <= 1024");
+  {
+    const char* ce = std::getenv("GPMI_MS_CG");
+    if (!(ce && std::strcmp(ce, "classic") == 0))
+      return msgram_cg2(sp, etas, neta, rhs, ld, nrhs, c_lo, c_hi, rtol, maxiter, G, iterations);
+  }
   const int nsub = c_hi - c_lo;
   const bool full = nsub == nrhs;
   Guard g(sp->device);

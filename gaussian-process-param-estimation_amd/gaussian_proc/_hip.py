@@ -99,6 +99,12 @@ SIGNATURES = {
     'gpmi_band_der_terms': (ctypes.c_int, [c_op_p, c_double_p, ctypes.c_int, c_double_p,
                                            c_double_p, c_double_p, c_double_p, c_int_p]),
     'gpmi_band_der_ms': (ctypes.c_int, [c_op_p, c_double_p]),
+    'gpmi_band_der_terms_ex': (ctypes.c_int, [c_op_p, c_double_p, ctypes.c_int, c_double_p,
+                                              c_double_p, c_double_p, c_double_p, c_double_p,
+                                              c_int_p]),
+    'gpmi_band_traceinv': (ctypes.c_int, [c_op_p, c_double_p, ctypes.c_int, c_double_p,
+                                          c_int_p]),
+    'gpmi_band_sinv_ms': (ctypes.c_int, [c_op_p, c_double_p]),
     'gpmi_band_stats': (ctypes.c_int, [c_op_p, c_int_p, c_int_p]),
     'gpmi_band_cq_stats': (ctypes.c_int, [c_op_p, c_int_p, c_int_p, c_int_p]),
     'gpmi_band_chase_info': (ctypes.c_int, [c_op_p, c_int_p, c_int_p, c_int_p]),
@@ -392,27 +398,67 @@ class Band(object):
 
     DER_CHUNK = 256   # GPMI_BAND_DER_MAX
 
-    def der_terms(self, etas):
+    TR_CHUNK = 64   # etas per selected-inversion call (its workspace: ~170 MB per eta
+    #                 at n = 16384, the cyclic-reduction factor and the inverse's blocks)
+
+    def der_terms(self, etas, traceinv=False):
         """-> (logdet[neta], g1, g2, g3 [neta, nrhs, nrhs], info[neta]) with
-        gp = R^T (K + eta I)^-p R for the resident RHS R."""
+        gp = R^T (K + eta I)^-p R for the resident RHS R; with ``traceinv`` also
+        tr1[neta] = trace((K + eta I)^-1) (selected inversion, no eigenvalues),
+        appended as the last-but-one item."""
         etas = as_c(numpy.atleast_1d(etas))
         ne, m = etas.shape[0], self.nrhs
         ld = numpy.empty(ne)
         g = [numpy.empty((ne, m, m)) for _ in range(3)]
+        tr = numpy.empty(ne)
         info = numpy.zeros(ne, dtype=numpy.int32)
-        for i in range(0, ne, self.DER_CHUNK):
-            e = as_c(etas[i:i + self.DER_CHUNK])
+        chunk = self.TR_CHUNK if traceinv else self.DER_CHUNK
+        for i in range(0, ne, chunk):
+            e = as_c(etas[i:i + chunk])
             k = e.shape[0]
             ldk = numpy.empty(k)
             gk = [numpy.empty((k, m, m)) for _ in range(3)]
             ik = numpy.zeros(k, dtype=numpy.int32)
-            check(self.lib.gpmi_band_der_terms(self.h, dptr(e), k, dptr(ldk), dptr(gk[0]),
-                                               dptr(gk[1]), dptr(gk[2]),
-                                               ik.ctypes.data_as(c_int_p)), 'gpmi_band_der_terms')
+            if traceinv:
+                tk = numpy.empty(k)
+                check(self.lib.gpmi_band_der_terms_ex(self.h, dptr(e), k, dptr(ldk),
+                                                      dptr(gk[0]), dptr(gk[1]), dptr(gk[2]),
+                                                      dptr(tk), ik.ctypes.data_as(c_int_p)),
+                      'gpmi_band_der_terms_ex')
+                tr[i:i + k] = tk
+            else:
+                check(self.lib.gpmi_band_der_terms(self.h, dptr(e), k, dptr(ldk), dptr(gk[0]),
+                                                   dptr(gk[1]), dptr(gk[2]),
+                                                   ik.ctypes.data_as(c_int_p)),
+                      'gpmi_band_der_terms')
             ld[i:i + k], info[i:i + k] = ldk, ik
             for q in range(3):
                 g[q][i:i + k] = gk[q]
+        if traceinv:
+            return ld, g[0], g[1], g[2], tr, info
         return ld, g[0], g[1], g[2], info
+
+    def traceinv(self, etas):
+        """-> (tr[neta], info[neta]): trace((K + eta I)^-1) by selected inversion of
+        the cyclic-reduction factor of B + eta I (gpmi_band_traceinv)."""
+        etas = as_c(numpy.atleast_1d(etas))
+        ne = etas.shape[0]
+        tr = numpy.empty(ne)
+        info = numpy.zeros(ne, dtype=numpy.int32)
+        for i in range(0, ne, self.TR_CHUNK):
+            e = as_c(etas[i:i + self.TR_CHUNK])
+            k = e.shape[0]
+            tk = numpy.empty(k)
+            ik = numpy.zeros(k, dtype=numpy.int32)
+            check(self.lib.gpmi_band_traceinv(self.h, dptr(e), k, dptr(tk),
+                                              ik.ctypes.data_as(c_int_p)), 'gpmi_band_traceinv')
+            tr[i:i + k], info[i:i + k] = tk, ik
+        return tr, info
+
+    def sinv_ms(self):
+        v = ctypes.c_double()
+        check(self.lib.gpmi_band_sinv_ms(self.h, ctypes.byref(v)), 'gpmi_band_sinv_ms')
+        return v.value
 
     def stats(self):
         """-> dict(panel_fallbacks, panel_maxg, panel, cholqr_fallbacks,

@@ -175,9 +175,8 @@ class DirectLikelihood(object):
         small = numpy.abs(sigma) < _TOL
         if not small and _use_band(K_mixed):
             eta = (sigma0 / sigma) ** 2
-            _, G1, G2, G3 = K_mixed.der_terms([eta], X, z)
-            jac = _jac_hess_from_terms(n, m, sigma, eta, G1[0], G2[0], G3[0],
-                                       K_mixed.traceinv(eta))[0]
+            _, G1, G2, G3, tr1 = K_mixed.der_terms([eta], X, z, traceinv=True)
+            jac = _jac_hess_from_terms(n, m, sigma, eta, G1[0], G2[0], G3[0], tr1[0])[0]
             if jac is not None:
                 return -jac if sign_switch else jac
         if small:
@@ -208,9 +207,9 @@ class DirectLikelihood(object):
         small = numpy.abs(sigma) < _TOL_HESS
         if not small and _use_band(K_mixed):
             eta = (sigma0 / sigma) ** 2
-            _, G1, G2, G3 = K_mixed.der_terms([eta], X, z)
-            hess = _jac_hess_from_terms(n, m, sigma, eta, G1[0], G2[0], G3[0],
-                                        K_mixed.traceinv(eta), K_mixed.traceinv(eta, 2))[1]
+            _, G1, G2, G3, tr1 = K_mixed.der_terms([eta], X, z, traceinv=True)
+            hess = _jac_hess_from_terms(n, m, sigma, eta, G1[0], G2[0], G3[0], tr1[0],
+                                        K_mixed.traceinv(eta, 2))[1]
             if hess is not None:
                 return -hess if sign_switch else hess
         if small:

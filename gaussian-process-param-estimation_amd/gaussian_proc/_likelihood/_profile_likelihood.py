@@ -108,17 +108,16 @@ class ProfileLikelihood(object):
                                 for le in log_etas])
         n, m = X.shape
         etas = numpy.where(numpy.isneginf(log_etas), 0.0, 10.0 ** log_etas)
-        _, G1, G2, G3 = K_mixed.der_terms(etas, X, z)
-        return numpy.array([_der_from_terms(n, m, G1[i], G2[i], G3[i],
-                                            K_mixed.traceinv(etas[i]))[0]
+        _, G1, G2, G3, tr1 = K_mixed.der_terms(etas, X, z, traceinv=True)
+        return numpy.array([_der_from_terms(n, m, G1[i], G2[i], G3[i], tr1[i])[0]
                             for i in range(etas.size)])
 
     @staticmethod
     def log_likelihood_der2_eta(z, X, K_mixed, eta):               # :138-192
         n, m = X.shape
         if _use_band(K_mixed):
-            _, G1, G2, G3 = K_mixed.der_terms([eta], X, z)
-            return float(_der_from_terms(n, m, G1[0], G2[0], G3[0], K_mixed.traceinv(eta),
+            _, G1, G2, G3, tr1 = K_mixed.der_terms([eta], X, z, traceinv=True)
+            return float(_der_from_terms(n, m, G1[0], G2[0], G3[0], tr1[0],
                                          K_mixed.traceinv(eta, exponent=2))[1])
         Y, Binv, Mz = ProfileLikelihood._mz(z, X, K_mixed, eta)
         V = K_mixed.solve(eta, Y)

@@ -288,13 +288,17 @@ class MixedCorrelation(object):
         self._check_info(etas, info)
         return ld, g
 
-    def der_terms(self, etas, X, z):
+    def der_terms(self, etas, X, z, traceinv=False):
         """The eigenvalue operator's eta-derivative terms: for each eta,
         logdet(K + eta I) and Gp = [X z]^T (K + eta I)^-p [X z] for p = 1, 2, 3,
-        from one banded Cholesky and two more banded triangular sweeps per eta
-        (csrc/gpmi_band.hip band_der_kernel). They replace the 2-5 dense solves
+        from one banded factorization and two more banded sweeps per eta
+        (csrc/gpmi_band.hip, gpmi_bcr.hip). They replace the 2-5 dense solves
         per eta of ProfileLikelihood.log_likelihood_der1_eta / der2_eta
-        (_profile_likelihood.py:91-192). Returns (logdet, G1, G2, G3)."""
+        (_profile_likelihood.py:91-192). Returns (logdet, G1, G2, G3); with
+        ``traceinv`` also tr1 = trace((K + eta I)^-1) per eta, appended: from the
+        eigenvalues when they are already computed (mixed_correlation.py:172-181),
+        else by selected inversion of the same cyclic-reduction factor on the
+        device (gpmi_band_der_terms_ex), without the one-time eigenvalue chase."""
         if self.imate_method != 'eigenvalue':
             raise NotImplementedError('der_terms needs the eigenvalue operator')
         etas = numpy.atleast_1d(numpy.asarray(etas, dtype=float))
@@ -302,12 +306,38 @@ class MixedCorrelation(object):
         c = getattr(self, '_der_cache', None)
         # the Jacobian and Hessian of one point ask for the same eta: reuse
         if c is not None and c[0] is self._band_rhs and c[1] is b and \
-                numpy.array_equal(c[2], etas):
-            return c[3]
-        ld, g1, g2, g3, info = b.der_terms(etas)
-        self._check_info(etas, info)
-        self._der_cache = (self._band_rhs, b, etas.copy(), (ld, g1, g2, g3))
-        return ld, g1, g2, g3
+                numpy.array_equal(c[2], etas) and (not traceinv or c[4] is not None or
+                                                   self._eig is not None):
+            res, tr1 = c[3], c[4]
+        elif traceinv and self._eig is None:
+            ld, g1, g2, g3, tr1, info = b.der_terms(etas, traceinv=True)
+            self._check_info(etas, info)
+            res = (ld, g1, g2, g3)
+            self._der_cache = (self._band_rhs, b, etas.copy(), res, tr1)
+        else:
+            ld, g1, g2, g3, info = b.der_terms(etas)
+            self._check_info(etas, info)
+            res, tr1 = (ld, g1, g2, g3), None
+            self._der_cache = (self._band_rhs, b, etas.copy(), res, None)
+        if not traceinv:
+            return res
+        if tr1 is None:
+            lam = self._eig
+            tr1 = numpy.array([float(numpy.sum(1.0 / (lam + e))) for e in etas])
+        return res + (tr1,)
+
+    # traceinv(eta) calls on the 'eigenvalue' operator answered by selected inversion
+    # (one cyclic-reduction factorization + the tree per call, ~ms) before the
+    # eigenvalues (one-time chase, ~0.15 s at n = 16384, then O(n) per eta) pay off
+    SINV_CALLS = 32
+
+    def _eig_traceinv1(self, eta):
+        if self._eig is None and getattr(self, '_sinv_calls', 0) < self.SINV_CALLS:
+            self._sinv_calls = getattr(self, '_sinv_calls', 0) + 1
+            tr, info = self.band().traceinv([eta])
+            self._check_info([eta], info)
+            return float(tr[0])
+        return float(numpy.sum(1.0 / (self.eigenvalues() + eta)))
 
     # ---- sparse K (tapered Matérn, CSR on the device) -------------------------
 
@@ -565,7 +595,10 @@ class MixedCorrelation(object):
         if exponent == 0:
             return float(self.n)
         if self.imate_method == 'eigenvalue':
-            # sum over the eigenvalues (imate 'eigenvalue', :172-181)
+            # sum over the eigenvalues (imate 'eigenvalue', :172-181); exponent 1 by
+            # selected inversion until the eigenvalues pay off (_eig_traceinv1)
+            if exponent == 1:
+                return self._eig_traceinv1(eta)
             return float(numpy.sum((self.eigenvalues() + eta) ** (-float(exponent))))
         if exponent in (1, 2):
             # exact, from the device triangular inverse of the cached factor

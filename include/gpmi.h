@@ -304,6 +304,24 @@ int gpmi_band_loglik(gpmi_band* b, const double* etas, int neta, double* logdet,
  * dense solves per eta. Any output pointer may be NULL. */
 int gpmi_band_der_terms(gpmi_band* b, const double* etas, int neta, double* logdet,
                         double* g1, double* g2, double* g3, int* info);
+/* gpmi_band_der_terms plus, when tr1 != NULL, tr1[e] = trace((K + eta_e I)^-1) =
+ * trace((B + eta_e I)^-1) by selected inversion of the block-cyclic-reduction
+ * factor down its reduction tree (the Takahashi recurrences: only the inverse's
+ * blocks on the factor's pattern, O(n 128^2) per eta, every block of a level in
+ * parallel). With these the profiled likelihood's der1
+ * (_profile_likelihood.py:91-132) needs no eigenvalues: it replaces the
+ * eigenvalue sums of MixedCorrelation.traceinv ('eigenvalue', exponent 1,
+ * mixed_correlation.py:172-181) and the eigh they come from (:76-79). */
+int gpmi_band_der_terms_ex(gpmi_band* b, const double* etas, int neta, double* logdet,
+                           double* g1, double* g2, double* g3, double* tr1, int* info);
+/* tr[e] = trace((K + eta_e I)^-1) for neta <= GPMI_BAND_DER_MAX etas by the same
+ * selected inversion (a cyclic-reduction factorization per eta first); info as
+ * gpmi_band_loglik. Replaces MixedCorrelation.traceinv(eta) on the 'eigenvalue'
+ * operator (mixed_correlation.py:172-181) without the eigenvalues. */
+int gpmi_band_traceinv(gpmi_band* b, const double* etas, int neta, double* tr, int* info);
+/* Device ms of the selected-inversion part of the last gpmi_band_traceinv /
+ * gpmi_band_der_terms_ex(tr1 != NULL) call. Diagnostic. */
+int gpmi_band_sinv_ms(gpmi_band* b, double* ms);
 
 /* Reduction diagnostics: how many reductions of this band fell back to the
  * per-column panel launches after a timed-out single-launch panel hand-off, and

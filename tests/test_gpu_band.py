@@ -601,3 +601,46 @@ def test_band_cyclic_reduction_not_spd(gp, monkeypatch):
     op = _mc(K)
     with pytest.raises(numpy.linalg.LinAlgError):
         op.loglik_terms([0.1, -lam[0] - 0.5 * (lam[1] - lam[0]) - 1e-3], X, z)
+
+
+@pytest.mark.parametrize('n', [1, 5, 128, 129, 300, 1000, 2177])
+def test_band_selected_inversion_traceinv(gp, n):
+    """trace((K + eta I)^-1) by selected inversion of the cyclic-reduction factor
+    down its reduction tree (gpmi_band_traceinv, no eigenvalues) vs numpy's
+    eigenvalue sums at ragged n (1 to 18 blocks, odd and even level sizes), rel
+    <= 1e-10; the same numbers from der_terms(traceinv=True) (one factorization
+    for the Gram blocks and the trace) and, once computed, from the device
+    eigenvalues."""
+    K, X, z = _inputs(n, n + 11, nu=2.5, scale=0.15)
+    lam = numpy.linalg.eigvalsh(K)
+    etas = numpy.array([1e-3, 0.05, 1.0, 30.0])
+    exact = numpy.array([numpy.sum(1.0 / (lam + e)) for e in etas])
+    op = _mc(K)
+    tr, info = op.band().traceinv(etas)
+    assert not numpy.any(info)
+    assert rel(tr, exact) < 1e-10, (tr, exact)
+    ld, G1, G2, G3, tr1 = op.der_terms(etas, X, z, traceinv=True)
+    assert rel(tr1, tr) < 1e-12
+    # MixedCorrelation.traceinv(eta) answers by selected inversion first
+    assert op._eig is None
+    assert rel(op.traceinv(0.05), exact[1]) < 1e-10 and op._eig is None
+    lam_d = op.eigenvalues()
+    assert rel(numpy.sum(1.0 / (lam_d + 0.05)), tr[1]) < 1e-10
+    # with the eigenvalues cached, der_terms takes its traces from them
+    tr1e = op.der_terms(etas[:2], X, z, traceinv=True)[4]
+    assert rel(tr1e, tr[:2]) < 1e-10
+
+
+def test_band_selected_inversion_not_spd_and_many_etas(gp):
+    """A non-SPD shift reports its pivot (LinAlgError through traceinv); 150 etas
+    in one call (three cyclic-reduction chunks of <= 64) equal the per-eta values."""
+    K, X, z = _inputs(600, 77)
+    lam = numpy.linalg.eigvalsh(K)
+    op = _mc(K)
+    with pytest.raises(numpy.linalg.LinAlgError):
+        op.traceinv(-lam[0] - 1.0)
+    etas = numpy.logspace(-2, 2, 150)
+    tr, info = op.band().traceinv(etas)
+    assert not numpy.any(info)
+    exact = numpy.array([numpy.sum(1.0 / (lam + e)) for e in etas])
+    assert rel(tr, exact) < 1e-10
