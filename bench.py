@@ -59,9 +59,6 @@ def parse():
     ap.add_argument('--cpu-budget-s', type=float, default=20.0,
                     help='sparse CPU baseline: seconds of sampled CG work (extrapolated)')
     ap.add_argument('--outer', type=int, default=16, help='outer panel width / 128')
-    ap.add_argument('--lookahead', type=int, default=0,
-                    help='1: panel factorization on a second stream overlaps the bulk '
-                         'trailing update; 0: one stream, in order')
     ap.add_argument('--config', default='dense', choices=['dense', 'sparse4', 'sparse5'],
                     help='dense: the headline N=16384 metric; sparse4/sparse5: BASELINE '
                          'configs 4 and 5 (tapered Matern, SLQ + CG)')
@@ -80,6 +77,9 @@ def parse():
                     help='check the N-rank launch only (no device): world size against '
                          '--gpus, the eta blocks and the all-gather / max-time collectives '
                          'over gloo; prints one JSON line')
+    ap.add_argument('--no-extras', action='store_true',
+                    help='dense probe runs: skip the batch-efficiency, dense-slq and nu=2.5 '
+                         'sub-lines')
     ap.add_argument('--no-sparse', action='store_true',
                     help='dense run: skip the sparse_modes block (configs 4 and 5, N=1 only)')
     return ap.parse_args()
@@ -977,6 +977,32 @@ def band_nu25_check(D, points, X, z):
     return out
 
 
+def dense_nu25_mode(args, op, X, z, steps=3):
+    """BASELINE configs[2] as written: the dense 64-eta curve of the N = 16384
+    Matern nu = 2.5 K (the resident K reassembled at nu = 2.5 by the caller), one
+    warm-up and `steps` timed steps of the same batched factorization as the
+    headline, with the logdet / direct lp errors against the reference's
+    N = 16384 nu = 2.5 values (tests/golden/cfg3_nu25.json). The Cholesky's cost
+    does not depend on nu; this line shows it."""
+    from gaussian_proc._likelihood._direct_likelihood import _lp_from_terms
+    n, m = X.shape
+    etas = numpy.logspace(-3, 3, args.eta_total)
+    op.loglik_terms(etas, X, z)
+    torch_sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ld, G = op.loglik_terms(etas, X, z)
+        [_lp_from_terms(n, m, 1.0, l, g) for l, g in zip(ld, G)]
+    torch_sync()
+    dt = time.perf_counter() - t0
+    ld_err, lp_err = golden_errors(lambda e: op.loglik_terms(e, X, z), 2.5, n, m)
+    return {'workload': 'cfg3 as specified: N=%d Matern nu=2.5 rho=0.1, the %d-point eta '
+                        'curve logspace(-3,3,%d) per step' % (n, etas.size, etas.size),
+            'steps': steps, 'warmup': 1, 'ms_per_step': round(dt / steps * 1e3, 2),
+            'value': round(etas.size * steps / dt, 3), 'unit': 'evals/s',
+            'logdet_rel_err_vs_reference': ld_err, 'lp_rel_err_vs_reference': lp_err}
+
+
 def band_batch_efficiency(op, X, z, batches=(8, 16, 32, 64)):
     """The band operator's per-rank eta batches of the strong-scaled curve at
     N = 8 / 4 / 2 / 1: device time of the banded-Cholesky call for that batch
@@ -1002,27 +1028,44 @@ def band_batch_efficiency(op, X, z, batches=(8, 16, 32, 64)):
 
 
 def der1_sweep(op, X, z, E, rank, torch):
-    """ProfileLikelihood.log_likelihood_der1_eta over this rank's E points of
-    the grid in one call (band Gram blocks G1..G3 + eigenvalue traceinv), after
-    the one-time eigenvalues of K (timed separately)."""
+    """ProfileLikelihood.log_likelihood_der1_eta over this rank's E points of the
+    grid in one call on the band operator right after its reduction: the Gram
+    blocks G1..G3 and trace((K + eta I)^-1) from ONE cyclic-reduction factorization
+    per eta, the traces by selected inversion down its tree (no eigenvalues:
+    `wall_ms` is the whole cost after the reduction). For comparison the round-4
+    path: the one-time eigenvalues of K (timed separately) and the eigenvalue sums,
+    and the two der1 curves' agreement."""
     from gaussian_proc._likelihood._profile_likelihood import ProfileLikelihood
     log_etas = numpy.linspace(-3, 3, 64)[[(rank * E + j) % 64 for j in range(E)]]
-    t0 = time.perf_counter()
-    op.eigenvalues()
-    eig_ms = (time.perf_counter() - t0) * 1e3
+    op._eig = None
     ProfileLikelihood.log_likelihood_der1_eta_batch(z, X, op, log_etas)   # warm (buffers)
     op._der_cache = None   # time the device work, not the operator's last-call cache
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     d1 = ProfileLikelihood.log_likelihood_der1_eta_batch(z, X, op, log_etas)
     dt = time.perf_counter() - t0
-    return {'etas': E, 'wall_ms': round(dt * 1e3, 3), 'device_ms': round(op.band().der_ms(), 3),
-            'der1_evals_per_s_per_gpu': round(E / dt, 1),
-            'eigenvalues_ms_once': round(eig_ms, 1),
-            'eigenvalues_chase': {2: 'chase_split_kernel (D and E workgroup per position)',
-                                  1: 'chase_systolic_kernel (one workgroup per position)',
-                                  0: 'per-wavefront launches'}[op.band().chase_info()['systolic']],
-            'der1_sample': [float(log_etas[0]), float(d1[0])]}
+    out = {'etas': E, 'wall_ms': round(dt * 1e3, 3), 'device_ms': round(op.band().der_ms(), 3),
+           'selected_inversion_ms': round(op.band().sinv_ms(), 3),
+           'der1_evals_per_s_per_gpu': round(E / dt, 1),
+           'traceinv': 'selected inversion of the cyclic-reduction factor (no eigenvalues)',
+           'der1_sample': [float(log_etas[0]), float(d1[0])]}
+    # the eigenvalue path for comparison
+    t0 = time.perf_counter()
+    op.eigenvalues()
+    eig_ms = (time.perf_counter() - t0) * 1e3
+    op._der_cache = None
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    d1e = ProfileLikelihood.log_likelihood_der1_eta_batch(z, X, op, log_etas)
+    dte = time.perf_counter() - t0
+    out['eigenvalue_path'] = {
+        'eigenvalues_ms_once': round(eig_ms, 1), 'sweep_wall_ms': round(dte * 1e3, 3),
+        'eigenvalues_chase': {2: 'chase_split_kernel (D and E workgroup per position)',
+                              1: 'chase_systolic_kernel (one workgroup per position)',
+                              0: 'per-wavefront launches'}[op.band().chase_info()['systolic']],
+        'der1_diff_vs_selected_inversion_rel_to_max': float(
+            numpy.max(numpy.abs(d1e - d1)) / numpy.max(numpy.abs(d1e)))}
+    return out
 
 
 def batch_efficiency(op, X, z, batches=(8, 16, 32)):
@@ -1199,7 +1242,6 @@ def main():
     asm_bytes = 8.0 * D.op.n_pad ** 2
     op = MixedCorrelation(D)
     op.op.set_outer(args.outer)
-    op.op.set_lookahead(args.lookahead)
     op.set_rhs(X, z)
 
     def step(s, timing_acc=None):
@@ -1284,7 +1326,7 @@ def main():
                        'operator': "imate_method='cholesky' (one dense fp64 MFMA Cholesky per "
                                    "eta); band_mode below is the 'eigenvalue' operator "
                                    "Likelihood uses",
-                       'outer_panel': 128 * args.outer, 'lookahead': args.lookahead,
+                       'outer_panel': 128 * args.outer,
                        'parallelism': 'eta-shard x%d + all-gather' % world},
             'roofline': roof,
             'whole_eval_tflops_per_gpu': round(whole, 3),
@@ -1307,7 +1349,7 @@ def main():
     if rank == 0:
         result['logdet_rel_err_vs_reference'] = ld_err
         result['lp_rel_err_vs_reference'] = lp_err
-        if world == 1 and args.scaling == 'strong':
+        if world == 1 and args.scaling == 'strong' and not args.no_extras:
             result['batch_efficiency'] = batch_efficiency(op, X, z)
             # (before band_nu25_check reassembles the resident K at nu = 2.5)
             if last is not None:
@@ -1329,8 +1371,15 @@ def main():
         lp_dev = _lp_from_terms(n, m, 1.0, ld1[0], G1[0])
     if rank == 0 and world == 1 and not args.no_band:
         result['band_mode']['optimizer'] = optimizer_timing(D, X, z)
-    if rank == 0 and world == 1 and not args.no_band and args.nu == 1.5:
-        result['band_mode']['nu25_check'] = band_nu25_check(D, points, X, z)
+    if rank == 0 and world == 1 and args.nu == 1.5 and not args.no_extras:
+        # BASELINE cfg3 as written (nu = 2.5): the band reduction's check reassembles
+        # the resident K at nu = 2.5, then the dense 64-eta curve is timed on it
+        if not args.no_band:
+            result['band_mode']['nu25_check'] = band_nu25_check(D, points, X, z)
+        else:
+            D.op.assemble_matern(points, numpy.full(2, 0.1), 2.5)
+        result['dense_nu25'] = dense_nu25_mode(args, op, X, z)
+        log('dense nu=2.5: %s' % result['dense_nu25'])
     if not args.no_sparse:
         # release the dense and band operators (their streams count against the
         # process's hardware queues) before the sparse configs run

@@ -75,15 +75,12 @@ struct gpmi_op {
   int nt = 0;
   int max_batch = 1;
   int outer = 16;                      // outer panel width in 128-column tiles
-  int lookahead = 0;                   // 1: panel chain on stream2 beside the bulk update
   hipStream_t stream = nullptr;
-  hipStream_t stream2 = nullptr;       // high-priority panel stream (look-ahead)
   hipStream_t stream3 = nullptr;       // second batch group (groups == 2)
   int groups = 0;                      // 2: the batch runs as two halves on two streams;
                                        // 0: auto (2 for batches of 2..32, 1 above)
   hipEvent_t ev_g = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-  std::vector<hipEvent_t> ev_panel, ev_rest;  // per outer panel (look-ahead)
   bool dry = false;                    // schedule dry run: collect SYRK shapes only
   std::vector<std::pair<int, int>> shapes;
   double* K = nullptr;       // [n_pad][n_pad]
@@ -106,7 +103,7 @@ struct gpmi_op {
   int* info = nullptr;       // [max_batch]
   // grouped syrk tile orders, one per trailing-update shape (w, t) of the schedule
   uint32_t* order = nullptr;
-  int order_nt = -1, order_outer = -1, order_la = -1, group = 8;
+  int order_nt = -1, order_outer = -1, group = 8;
   std::map<std::pair<int, int>, int64_t> order_off;
   int nrhs = 0;
   bool has_K = false;
@@ -234,65 +231,26 @@ int factor_panel(gpmi_op* op, const BatchPtrs& P, int b0, int nb, hipStream_t st
   return factor_panel(op, P, b0, nb, st, c0 + h, W - h);
 }
 
-int get_event(std::vector<hipEvent_t>* v, size_t i, hipEvent_t* out) {
-  while (v->size() <= i) {
-    hipEvent_t e;
-    HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    v->push_back(e);
-  }
-  *out = (*v)[i];
-  return 0;
-}
 
 // The blocked factorization schedule over outer panels P_k of `outer` tile
-// columns. Without look-ahead everything runs in order on op->stream: factor
-// P_k, then one trailing SYRK over all columns right of it (kdim = 128 * outer).
-// With look-ahead the panel chain runs on the high-priority op->stream2:
-//   stream2: factor(P_k) -> [wait U_rest(k-1)] -> U_next(k): P_{k+1}'s columns
-//   stream : [wait factor(P_k)] -> U_rest(k): columns right of P_{k+1}
-// so the latency-bound factorization of P_{k+1} overlaps the bulk update U_rest(k).
-// U_rest(k-1) and U_next(k) both write P_{k+1}'s columns, hence the wait.
+// columns, in order on one stream: factor P_k (recursive panel factorization), then
+// one trailing SYRK over all columns right of it (kdim = 128 * outer). (Round 5
+// removed the look-ahead form, the panel chain of P_{k+1} on a second high-priority
+// stream beside the bulk update of P_k: at the batch-64 headline 1441.8 against
+// 1442.9 ms per 64-eta step, and within +-1 % at 8 and 16 eta in round 3: the batched
+// SYRK keeps every CU busy, so the chain beside it gains nothing.)
 // P points at batch member b0 (a batch group); `main` replaces op->stream.
 int schedule(gpmi_op* op, const BatchPtrs& P, int b0, int nb, hipStream_t main = nullptr) {
   const int nt = op->nt, O = op->outer;
-  const bool la = op->lookahead && !op->dry;
-  hipStream_t A = main ? main : op->stream, B = la ? op->stream2 : A;
-  bool have_rest_prev = false;
-  hipEvent_t ev_rest_prev = nullptr;
-  int np = 0;
-  for (int c0 = 0; c0 < nt; c0 += O, ++np) {
+  hipStream_t A = main ? main : op->stream;
+  for (int c0 = 0; c0 < nt; c0 += O) {
     const int W = std::min(O, nt - c0);
-    int rc = factor_panel(op, P, b0, nb, B, c0, W);
+    int rc = factor_panel(op, P, b0, nb, A, c0, W);
     if (rc) return rc;
     const int c1 = c0 + W;
     if (c1 >= nt) break;
-    if (!op->lookahead) {
-      rc = launch_syrk(op, A, b0, nb, c1, nt - c1, nt - c1, c0 * TS, W * TS);
-      if (rc) return rc;
-      continue;
-    }
-    const int c2 = c1 + std::min(O, nt - c1);
-    bool have_rest = false;
-    hipEvent_t ev_f = nullptr, ev_r = nullptr;
-    if (c2 < nt) {
-      if (la) {
-        if ((rc = get_event(&op->ev_panel, np, &ev_f))) return rc;
-        HIP_TRY(hipEventRecord(ev_f, B));
-        HIP_TRY(hipStreamWaitEvent(A, ev_f, 0));
-      }
-      rc = launch_syrk(op, A, b0, nb, c2, nt - c2, nt - c2, c0 * TS, W * TS);
-      if (rc) return rc;
-      if (la) {
-        if ((rc = get_event(&op->ev_rest, np, &ev_r))) return rc;
-        HIP_TRY(hipEventRecord(ev_r, A));
-      }
-      have_rest = true;
-    }
-    if (la && have_rest_prev) HIP_TRY(hipStreamWaitEvent(B, ev_rest_prev, 0));
-    rc = launch_syrk(op, B, b0, nb, c1, c2 - c1, nt - c1, c0 * TS, W * TS);
+    rc = launch_syrk(op, A, b0, nb, c1, nt - c1, nt - c1, c0 * TS, W * TS);
     if (rc) return rc;
-    have_rest_prev = have_rest;
-    ev_rest_prev = ev_r;
   }
   return 0;
 }
@@ -301,7 +259,7 @@ int schedule(gpmi_op* op, const BatchPtrs& P, int b0, int nb, hipStream_t main =
 int ensure_order(gpmi_op* op) {
   if (op->group <= 0) return 0;
   if (op->order && op->order_nt == op->nt && op->order_outer == op->outer &&
-      op->order_la == op->lookahead)
+      true)
     return 0;
   if (op->order) HIP_TRY(hipFree(op->order));
   op->order = nullptr;
@@ -323,7 +281,6 @@ int ensure_order(gpmi_op* op) {
   HIP_TRY(hipMemcpy(op->order, h.data(), sizeof(uint32_t) * h.size(), hipMemcpyHostToDevice));
   op->order_nt = op->nt;
   op->order_outer = op->outer;
-  op->order_la = op->lookahead;
   return 0;
 }
 
@@ -373,16 +330,12 @@ int run_factor(gpmi_op* op, const double* etas_host, int nb, const double* rhs_d
     HIP_TRY(hipMemcpyAsync(op->R + b * P.sR, rhs_dev, sizeof(double) * P.sR,
                            hipMemcpyDeviceToDevice, s));
   HIP_TRY(hipMemsetAsync(op->info, 0, sizeof(int) * nb, s));
-  if (op->lookahead) {
-    HIP_TRY(hipEventRecord(op->ev_fork, s));
-    HIP_TRY(hipStreamWaitEvent(op->stream2, op->ev_fork, 0));
-  }
   int rc = 0;
   // auto: a small batch (the per-rank block of a strong-scaled curve) keeps more CUs
   // busy with its halves overlapped (batch 8: +2.3 %); a large one is all SYRK
   // already (batch 64: +0.2 %) and keeps one stream (clean per-launch timing)
   const int groups = op->groups ? op->groups : (nb <= 32 ? 2 : 1);
-  if (groups == 2 && nb >= 2 && !op->lookahead) {
+  if (groups == 2 && nb >= 2) {
     // two independent halves of the batch on two streams: one half's
     // latency-bound diagonal-block / panel kernels run beside the other's SYRK.
     // Only batched callers (nb >= 2) get here, and the one batched caller,
@@ -403,10 +356,6 @@ int run_factor(gpmi_op* op, const double* etas_host, int nb, const double* rhs_d
     rc = schedule(op, P, 0, nb);
   }
   if (rc) return rc;
-  if (op->lookahead) {
-    HIP_TRY(hipEventRecord(op->ev_join, op->stream2));
-    HIP_TRY(hipStreamWaitEvent(s, op->ev_join, 0));
-  }
   hipLaunchKernelGGL(finalize_kernel, dim3(nb), dim3(256), 0, s, P, nt, op->out, OUT_LD);
   LAUNCH_CHECK("finalize_kernel");
   if (op->timing) HIP_TRY(hipEventRecord(op->ev_end, s));
@@ -642,10 +591,10 @@ int gpmi_op_create(int device, int64_t n, int max_batch, gpmi_op** out) {
   hipError_t e;
   if ((e = hipStreamCreateWithFlags(&op->stream, hipStreamNonBlocking)) != hipSuccess)
     return fail(e, "stream");
-  // op->stream2 (look-ahead) is created by gpmi_op_set_lookahead(op, 1) only: HIP
-  // streams beyond the process's hardware queues (GPU_MAX_HW_QUEUES = 4) share
-  // queues and slow other objects' multi-stream work (a band reduction beside a dense
-  // operator holding three streams: 161 -> 181 ms)
+  // (one stream; op->stream3 only for the two-halves batch form: HIP streams beyond
+  // the process's hardware queues (GPU_MAX_HW_QUEUES = 4) share queues and slow other
+  // objects' multi-stream work, a band reduction beside a dense operator holding three
+  // streams: 161 -> 181 ms)
   if ((e = hipEventCreateWithFlags(&op->ev_fork, hipEventDisableTiming)) != hipSuccess)
     return fail(e, "event");
   if ((e = hipEventCreateWithFlags(&op->ev_join, hipEventDisableTiming)) != hipSuccess)
@@ -680,7 +629,6 @@ int gpmi_op_destroy(gpmi_op* op) {
   if (!op) return 0;
   DeviceGuard g(op->device);
   if (op->stream) (void)hipStreamSynchronize(op->stream);
-  if (op->stream2) (void)hipStreamSynchronize(op->stream2);
   if (op->stream3) (void)hipStreamSynchronize(op->stream3);
   double* bufs[] = {op->K, op->A, op->R, op->X, op->U, op->Linv, op->logdiag, op->gram,
                     op->out, op->etas, op->rhs_src, op->scratch, op->scratch2, op->tracebuf,
@@ -692,11 +640,8 @@ int gpmi_op_destroy(gpmi_op* op) {
   for (auto e : op->ev) (void)hipEventDestroy(e);
   if (op->ev_begin) (void)hipEventDestroy(op->ev_begin);
   if (op->ev_end) (void)hipEventDestroy(op->ev_end);
-  for (auto e : op->ev_panel) (void)hipEventDestroy(e);
-  for (auto e : op->ev_rest) (void)hipEventDestroy(e);
   if (op->ev_fork) (void)hipEventDestroy(op->ev_fork);
   if (op->ev_join) (void)hipEventDestroy(op->ev_join);
-  if (op->stream2) (void)hipStreamDestroy(op->stream2);
   if (op->stream3) (void)hipStreamDestroy(op->stream3);
   if (op->ev_g) (void)hipEventDestroy(op->ev_g);
   if (op->stream) (void)hipStreamDestroy(op->stream);
@@ -1038,19 +983,6 @@ int gpmi_op_last_timing(gpmi_op* op, double* syrk_ms, int* syrk_launches, double
   return 0;
 }
 
-int gpmi_op_set_lookahead(gpmi_op* op, int enable) {
-  if (!op) return set_err(-1006, "null handle");
-  if (enable && !op->stream2) {
-    DeviceGuard g(op->device);
-    int lo = 0, hi = 0;
-    hipError_t e;
-    if ((e = hipDeviceGetStreamPriorityRange(&lo, &hi)) != hipSuccess ||
-        (e = hipStreamCreateWithPriority(&op->stream2, hipStreamNonBlocking, hi)) != hipSuccess)
-      return set_err(-(int)e, "look-ahead stream: %s", hipGetErrorString(e));
-  }
-  op->lookahead = enable != 0;
-  return 0;
-}
 
 int gpmi_op_set_outer(gpmi_op* op, int s) {
   if (!op) return set_err(-1006, "null handle");

@@ -71,19 +71,6 @@ constexpr int MS_MAXS = 16;   // RHS columns per multi-shift block
 #define GPMI_LZ_JC 16
 #endif
 constexpr int LZ_JC = GPMI_LZ_JC;   // basis vectors per lz_dots_kernel launch (DCGS2 Lanczos)
-struct MsState {
-  double* rr;      // [s]   r_c . r_c
-  double* a;       // [s]   alpha_c of this iteration (0 once converged)
-  double* a_prev;  // [s]
-  double* beta;    // [s]   beta used to form the current p
-  double* bn2;     // [s]   ||b_c||^2
-  int* active;     // [s]
-  double* z;       // [S][s]    zeta_j of the current residual
-  double* z_prev;  // [S][s]
-  double* bp;      // [S][s'][s] b_c' . p_{j,c}
-  double* g;       // [S][s'][s] accumulated G_j[c'][c]
-  int* flags;      // [1]   set when an active column meets p^T (K + eta_0 I) p <= 0
-};
 
 // A multi-shift CG batch's end state, written by the batch's last ms_tail_kernel
 // (block 0) straight into host-mapped pinned memory: the host reads it after an
@@ -108,10 +95,8 @@ struct MsShift {
   int* flags;      // [1] p^T (K + eta_0 I) p <= 0 in an active column
   int* it_stop;    // [1] the first iteration with no active column (-1: none yet)
 };
-constexpr int MS_GRP_SP = 64;   // window-SpMM blocks per group of its in-launch dot sums
 constexpr int MS_UB = 512;      // vector blocks of ms_cg2_update_kernel
-constexpr int MS_GRP_U = 16;    // ... per group of its in-launch B^T r sums
-constexpr int MS_DOT_BLK = 64;  // blocks of ms_dots2_kernel (SpMM kinds without the epilogue)
+constexpr int MS_DOT_BLK = 256; // blocks of ms_dots2_kernel (SpMM kinds without the epilogue)
 
 struct MsPin {
   int act[MS_MAXS];

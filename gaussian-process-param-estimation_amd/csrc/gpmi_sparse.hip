@@ -314,53 +314,6 @@ __global__ __launch_bounds__(256) void csr_spmm_win_kernel(
   }
 }
 
-// Group last-arriver sum inside a launch (the in-launch split-K recipe of the HIP
-// guide, counter form): block `bid` has stored its row part[bid][0, ne) with plain
-// stores; blocks form groups of `grp` consecutive ids; each block drains its stores,
-// releases at agent scope and draws a ticket of its group's counter; the block
-// drawing the group's last ticket resets the counter (zeroed at allocation, so every
-// launch starts from 0), acquires at agent scope and sums the group's rows in
-// ascending id into gred[group][0, ne) (fixed order: deterministic for any
-// dispatch order or workgroup -> XCD placement). The summing block's own loads all
-// follow its acquire (no other block's bytes are read before it).
-__device__ __forceinline__ void group_reduce_rows(const double* part, int ne, int bid, int nblk,
-                                                  int grp, unsigned* gcnt, double* gred) {
-  __shared__ int last_flag;
-  const int t = threadIdx.x;
-  const int g = bid / grp, g0 = g * grp, gn = min(grp, nblk - g0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (t == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned old =
-        __hip_atomic_fetch_add(gcnt + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = old == (unsigned)(gn - 1);
-    if (last) {
-      __hip_atomic_store(gcnt + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    last_flag = last;
-  }
-  __syncthreads();
-  if (!last_flag) return;
-  for (int e = t; e < ne; e += blockDim.x) {
-    const double* pr = part + (int64_t)g0 * ne + e;
-    double sum = 0.0;
-    int q = 0;
-    for (; q + 8 <= gn; q += 8) {
-      double v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = pr[(int64_t)(q + u) * ne];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) sum += v[u];
-    }
-    for (; q < gn; ++q) sum += pr[(int64_t)q * ne];
-    gred[(int64_t)g * ne + e] = sum;
-  }
-}
-
 // The one-pass window with its staging latency hidden (round 3): the window rows of
 // X are gathered with NB loads in flight per thread (16-byte loads for even S; a
 // batch covers 8192 doubles, ~410 rows at S = 20), where the round-2 one-pass window
@@ -375,7 +328,7 @@ __global__ __launch_bounds__(64 * TPR) void csr_spmm_wing_kernel(
     const unsigned short* __restrict__ lidx, const double* __restrict__ data, int64_t n,
     const int* __restrict__ wcols, const int* __restrict__ ucount,
     const double* __restrict__ X, double* __restrict__ Y, double eta,
-    double* __restrict__ pqp, double* __restrict__ gred, unsigned* __restrict__ gcnt) {
+    double* __restrict__ pqp, int dots2) {
   extern __shared__ double smem[];
   // TPR threads per row (4: 256-thread blocks, 8: 512), CG columns each
   constexpr int NT = 64 * TPR;
@@ -488,47 +441,41 @@ __global__ __launch_bounds__(64 * TPR) void csr_spmm_wing_kernel(
   if (pqp) {
     // the block's x . y per column (the multi-shift CG's p . q), rows summed in order:
     // pqp[b][c]; the window's LDS is free once every thread is past its products.
-    // With gred (the Chronopoulos-Gear multi-shift CG, x = r, y = A r): the row
-    // [x . y | x . x] of this block at pqp[blockIdx.x][2S], then the group
-    // last-arriver sum of MS_GRP_SP consecutive blocks' rows into gred[group][2S]
-    // (group_reduce_rows).
-    const int WD = gred ? 2 * S : S;
+    // dots2 (the Chronopoulos-Gear multi-shift CG, x = r, y = A r): the row
+    // [x . y | x . x] of this block at pqp[b][2S] (summed by ms_cg2_reduce_kernel)
+    const int WD = dots2 ? 2 * S : S;
     __syncthreads();
     double* red = smem;   // [64][WD]
 #pragma unroll
     for (int j = 0; j < CG; ++j)
       if (c0 + j < S) {
         red[r * WD + c0 + j] = xy[j];
-        if (gred) red[r * WD + S + c0 + j] = xx[j];
+        if (dots2) red[r * WD + S + c0 + j] = xx[j];
       }
     __syncthreads();
     if (t < WD) {
       double sum = 0.0;
       for (int q = 0; q < nr; ++q) sum += red[q * WD + t];
-      if (gred)
-        pqp[(int64_t)blockIdx.x * WD + t] = sum;
-      else
-        pqp[b * S + t] = sum;
+      pqp[b * WD + t] = sum;
     }
-    if (gred) group_reduce_rows(pqp, WD, blockIdx.x, gridDim.x, MS_GRP_SP, gcnt, gred);
   }
 }
 
 template __global__ void csr_spmm_wing_kernel<20, 8, 4>(const int64_t*, const int*,
     const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
-    double*, double, double*, double*, unsigned*);
+    double*, double, double*, int);
 template __global__ void csr_spmm_wing_kernel<11, 8, 4>(const int64_t*, const int*,
     const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
-    double*, double, double*, double*, unsigned*);
+    double*, double, double*, int);
 template __global__ void csr_spmm_wing_kernel<12, 8, 4>(const int64_t*, const int*,
     const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
-    double*, double, double*, double*, unsigned*);
+    double*, double, double*, int);
 template __global__ void csr_spmm_wing_kernel<8, 8, 4>(const int64_t*, const int*,
     const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
-    double*, double, double*, double*, unsigned*);
+    double*, double, double*, int);
 template __global__ void csr_spmm_wing_kernel<7, 8, 4>(const int64_t*, const int*,
     const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
-    double*, double, double*, double*, unsigned*);
+    double*, double, double*, int);
 
 // partial[b][j][c] = sum over this block's rows of A_j[i][c] * B[i][c],
 // A_j = A + j * strideA, j = blockIdx.y; grid-stride over rows.
@@ -589,31 +536,6 @@ __global__ __launch_bounds__(256) void col_dot_reduce_kernel(const double* __res
   if (e >= J * s) return;
   const double v = wave_reduce_partials(partial, nblk, (int64_t)J * s, e);
   if ((threadIdx.x & 63) == 0) out[e] = v;
-}
-
-// The same sums by one workgroup per output element, for many partial rows (the
-// window SpMM's p . q partials: one row per 64-row block, 4096 at cfg 5): thread t
-// sums rows t, t + 256, ... (eight loads in flight), then the four waves' sums in a
-// fixed order. (One wave per element took ~9.6 us there: 64 dependent-ish loads a lane.)
-__global__ __launch_bounds__(256) void col_dot_reduce_wg_kernel(const double* __restrict__ partial,
-                                                                int nblk, int ne,
-                                                                double* __restrict__ out) {
-  __shared__ double red[4];
-  const int e = blockIdx.x, t = threadIdx.x;
-  double a = 0.0;
-  int b = t;
-  for (; b + 7 * 256 < nblk; b += 8 * 256) {
-    double x[8];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) x[q] = partial[(int64_t)(b + q * 256) * ne + e];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) a += x[q];
-  }
-  for (; b < nblk; b += 256) a += partial[(int64_t)b * ne + e];
-  a = wave_sum(a);
-  if ((t & 63) == 0) red[t >> 6] = a;
-  __syncthreads();
-  if (t == 0) out[e] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
 // W[i][c] = alpha * W[i][c] - sum_{j<J} A_j[i][c] * H[j][c]   (H on the device)
@@ -1328,224 +1250,36 @@ void launch_ms_dots(const double* B, const double* R, int64_t n, int s, double* 
   }
 }
 
-// Fused r update + dots of one multi-shift CG iteration for s <= 16 columns on fp64
-// MFMA: every block first reduces the p . q partials (fixed order, identical in
-// every block) to a[c] = rr[c] / (p . q)[c] (0 once the column stopped; block 0
-// stores a and flags p^T A p <= 0), then, four rows per wave instruction, lane
-// (row = r0 + lane / 16, column c = lane % 16) reads b, r and q of its element,
-// writes r_new = r - a q in place, and feeds b as the A operand and r_new as the
-// B operand of v_mfma_f64_16x16x4f64: the wave's 16 x 16 accumulator is B^T r_new
-// over its rows (columns >= s padded with zeros); r_new . r_new accumulates per
-// lane. Partials [block][s * s + s] as ms_dots_partial_kernel (waves summed in a
-// fixed order). One pass over b, r, q (ms_r_update + ms_dots_partial read r and
-// q, then b and r once per four-column group).
-__global__ __launch_bounds__(256) void ms_rmfma_kernel(const double* __restrict__ B,
-                                                       double* __restrict__ R,
-                                                       const double* __restrict__ Q, MsState st,
-                                                       const double* __restrict__ pqpart,
-                                                       int pq_nblk, int64_t n, int s,
-                                                       int nb, double* __restrict__ partial) {
-  // B: [n][nb] (nb >= s: the RHS columns R may be a shard of B's), R, Q: [n][s]
-  __shared__ double sa[16];
-  __shared__ double red[4][16 * 16 + 16];
-  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  for (int c = wv; c < s; c += 4) {
-    const double pq = wave_reduce_partials(pqpart, pq_nblk, s, c);
-    if (lane == 0) {
-      const int act = st.active[c];
-      const double a = act ? st.rr[c] / pq : 0.0;
-      sa[c] = a;
-      if (blockIdx.x == 0) {
-        st.a[c] = a;
-        if (act && !(pq > 0.0)) st.flags[0] = 1;
-      }
-    }
-  }
-  __syncthreads();
-  const int c = lane & 15, rq = lane >> 4;
-  const bool on = c < s, onb = c < nb;
-  const double a = on ? sa[c] : 0.0;
-  d4 acc = {0.0, 0.0, 0.0, 0.0};
-  double rr = 0.0;
-  // rows in groups of 16 per block iteration (4 waves x 4 rows), RG groups per trip
-  // so that 3 RG loads per lane are in flight (two groups, six loads: cfg 4 8.0 us)
-  // (the trip condition is wave-uniform: every lane issues every MFMA)
-  constexpr int RG = 4;
-  const int64_t stride = (int64_t)gridDim.x * 16;
-  for (int64_t base = (int64_t)blockIdx.x * 16 + wv * 4; base < n; base += RG * stride) {
-    double bv[RG], rv[RG], qv[RG];
-#pragma unroll
-    for (int u = 0; u < RG; ++u) {
-      const int64_t i = base + u * stride + rq;
-      const bool v = on && i < n, w = onb && i < n;
-      bv[u] = w ? B[i * nb + c] : 0.0;
-      rv[u] = v ? R[i * s + c] : 0.0;
-      qv[u] = v ? Q[i * s + c] : 0.0;
-    }
-#pragma unroll
-    for (int u = 0; u < RG; ++u) {
-      const int64_t i = base + u * stride + rq;
-      const double nr = rv[u] - a * qv[u];
-      if (on && i < n) R[i * s + c] = nr;
-      rr += nr * nr;
-      acc = mfma64(bv[u], nr, acc);
-    }
-  }
-  // C map: row (c') = rq + 4 k, column (c) = lane & 15
-#pragma unroll
-  for (int k = 0; k < 4; ++k) red[wv][(rq + 4 * k) * 16 + c] = acc[k];
-  // r . r: the four lanes of column c (rq = 0..3), in order
-  double rs = rr;
-  rs += __shfl_down(rs, 16);
-  rs += __shfl_down(rs, 32);
-  if (rq == 0) red[wv][256 + c] = rs;
-  __syncthreads();
-  const int ne = nb * s + s;
-  for (int e = t; e < ne; e += 256) {
-    int idx;
-    if (e < nb * s) {
-      const int cp = e / s, cc = e - cp * s;
-      idx = cp * 16 + cc;
-    } else {
-      idx = 256 + (e - nb * s);
-    }
-    partial[(int64_t)blockIdx.x * ne + e] =
-        (red[0][idx] + red[1][idx]) + (red[2][idx] + red[3][idx]);
-  }
-}
-
-// The tail of one multi-shift CG iteration in ONE launch (replaces ms_scalar_kernel
-// + ms_p_update_kernel): every block forms p = r + beta p for its elements, with
-// beta = rr_new / rr and the stop test of each column computed from the reduced
-// r . r (br) and the CURRENT state `cur` (the values ms_scalar_kernel would have
-// written), and block 0 also advances the per-shift scalars as ms_scalar_kernel
-// and writes rr / active of the NEXT state `nxt` (double-buffered: the other blocks
-// read cur's during this launch). Four consecutive elements per thread as
-// ms_p_update_kernel.
-__global__ __launch_bounds__(256) void ms_tail_kernel(MsState cur, MsState nxt,
-                                                      const double* __restrict__ br_in,
-                                                      const double* __restrict__ dshift, int S,
-                                                      int s, int nb, double rtol2,
-                                                      double* __restrict__ P,
-                                                      const double* __restrict__ R, int64_t n,
-                                                      MsPin* __restrict__ pin) {
-  __shared__ double br[MS_MAXS * MS_MAXS + MS_MAXS];
-  __shared__ double sbeta[MS_MAXS];
-  __shared__ int supd[MS_MAXS];
-  const int t = threadIdx.x;
-  const int ne = nb * s + s;
-  for (int e = t; e < ne; e += blockDim.x) br[e] = br_in[e];
-  __syncthreads();
-  if (t < s) {
-    const double rrn = br[nb * s + t];
-    const int act = cur.active[t];
-    const bool upd = act && !(rrn <= rtol2 * cur.bn2[t]);
-    sbeta[t] = act ? rrn / cur.rr[t] : 0.0;
-    supd[t] = upd ? 1 : 0;
-  }
-  __syncthreads();
-  // p = r + beta p for the columns still active after this iteration
-  {
-    const int64_t ns = n * s;
-    const int64_t e = ((int64_t)blockIdx.x * 256 + t) * 4;
-    if (e < ns) {
-      int c = (int)(e % s);
-      if (((ns | (int64_t)(((uintptr_t)P | (uintptr_t)R) >> 3)) & 1) == 0 && e + 3 < ns) {
-        d2 p[2] = {*reinterpret_cast<const d2*>(P + e), *reinterpret_cast<const d2*>(P + e + 2)};
-        const d2 r[2] = {*reinterpret_cast<const d2*>(R + e),
-                         *reinterpret_cast<const d2*>(R + e + 2)};
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          if (supd[c]) p[k >> 1][k & 1] = r[k >> 1][k & 1] + sbeta[c] * p[k >> 1][k & 1];
-          c = c + 1 == s ? 0 : c + 1;
-        }
-        *reinterpret_cast<d2*>(P + e) = p[0];
-        *reinterpret_cast<d2*>(P + e + 2) = p[1];
-      } else {
-        for (int k = 0; k < 4 && e + k < ns; ++k) {
-          if (supd[c]) P[e + k] = R[e + k] + sbeta[c] * P[e + k];
-          c = c + 1 == s ? 0 : c + 1;
-        }
-      }
-    }
-  }
-  if (blockIdx.x != 0) return;
-  // block 0: the per-shift scalars (thread (j, c) tasks in rounds of the block)
-  for (int task = t; task < S * s; task += blockDim.x) {
-    const int j = task / s, c = task % s;
-    if (!cur.active[c]) continue;
-    const double a = cur.a[c], ap = cur.a_prev[c], bo = cur.beta[c];
-    const double z = cur.z[j * s + c], zp = cur.z_prev[j * s + c];
-    const double d = dshift[j];
-    const double zn = z * zp * ap / (a * bo * (zp - z) + zp * ap * (1.0 + d * a));
-    const double as = a * zn / z;
-    const double bnew = sbeta[c];
-    const double bs = bnew * (zn / z) * (zn / z);
-    double bpv[MS_MAXS], gv[MS_MAXS];
-#pragma unroll
-    for (int cp = 0; cp < MS_MAXS; ++cp) {
-      const int e = (j * nb + cp) * s + c;
-      bpv[cp] = cp < nb ? cur.bp[e] : 0.0;
-      gv[cp] = cp < nb ? cur.g[e] : 0.0;
-    }
-#pragma unroll
-    for (int cp = 0; cp < MS_MAXS; ++cp) {
-      if (cp >= nb) break;
-      const int e = (j * nb + cp) * s + c;
-      cur.g[e] = gv[cp] + as * bpv[cp];
-      cur.bp[e] = zn * br[cp * s + c] + bs * bpv[cp];
-    }
-    cur.z_prev[j * s + c] = z;
-    cur.z[j * s + c] = zn;
-  }
-  __syncthreads();
-  if (t < s) {
-    double rr_n;
-    int act_n;
-    if (cur.active[t]) {
-      cur.a_prev[t] = cur.a[t];
-      cur.beta[t] = sbeta[t];
-      rr_n = br[nb * s + t];
-      act_n = supd[t];
-    } else {
-      rr_n = cur.rr[t];
-      act_n = 0;
-    }
-    nxt.rr[t] = rr_n;
-    nxt.active[t] = act_n;
-    if (pin) {   // the batch's end state for the host (pinned, device-mapped)
-      pin->rr[t] = rr_n;
-      pin->act[t] = act_n;
-      if (t == 0) pin->flag = cur.flags[0];   // set by ms_rmfma_kernel, before this launch
-    }
-  }
-}
-
-// Multi-shift CG, Chronopoulos-Gear form (round 5): ONE launch per iteration besides
-// the SpMM. Iteration k: the SpMM gave w_k = (K + eta_0 I) r_k and, in its epilogue
-// (csr_spmm_wing_kernel with gred, or ms_dots2_kernel), group sums of r_k . w_k and
-// r_k . r_k (dred[ndg][2s]). Every block reduces those rows in the same fixed order
-// and forms, per column (Chronopoulos and Gear, J. Comput. Appl. Math. 25 (1989) 153):
+// Multi-shift CG, Chronopoulos-Gear form (round 5): three launches per iteration,
+// the SpMM, one reduction and this update, against five for the standard form
+// (SpMM, reduce, r update + B^T r, reduce, tail). Iteration k: the SpMM gave
+// w_k = (K + eta_0 I) r_k and per-block rows of r_k . w_k and r_k . r_k in its epilogue
+// (csr_spmm_wing_kernel dots2, or ms_dots2_kernel); ms_cg2_reduce_kernel summed them,
+// and the previous update's B^T r_k rows, into red = [delta[s] | gamma[s] | B^T r_k].
+// Every block forms, per column (Chronopoulos and Gear, J. Comput. Appl. Math. 25
+// (1989) 153):
 //   gamma_k = r_k . r_k, delta_k = r_k . w_k, beta_{k-1} = gamma_k / gamma_{k-1}
 //   (0 at k = 0), alpha_k = gamma_k / (delta_k - beta_{k-1} gamma_k / alpha_{k-1}),
 // the denominator being p_k^T (K + eta_0 I) p_k (<= 0 flags the column), and the
-// stop test gamma_k <= rtol^2 ||b||^2. These equal standard CG's alpha, beta in exact
-// arithmetic. The vector blocks (1 .. MS_UB) then form, for active columns,
-//   p_k = r_k + beta_{k-1} p_{k-1},  s_k = w_k + beta_{k-1} s_{k-1}  (= A p_k),
+// stop test gamma_k <= rtol^2 ||b||^2: standard CG's alpha, beta in exact arithmetic
+// (numpy check of the whole recurrence: the Gram blocks to 1e-12 of exact solves, the
+// same iteration count as a host CG). The vector blocks (1 .. MS_UB) then form, for
+// active columns,
+//   s_k = w_k + beta_{k-1} s_{k-1}  (= A p_k, p_k = r_k + beta_{k-1} p_{k-1}),
 //   r_{k+1} = r_k - alpha_k s_k,
-// and B^T r_{k+1} on fp64 MFMA (as ms_rmfma_kernel), whose block rows are summed by
-// groups of MS_GRP_U in the launch (group_reduce_rows) into bred[nbg][nb s]. Block 0
-// does no vector work: it sums the previous launch's B^T r_k group rows and takes the
-// shift step k - 1 (the zeta / G / b . p recurrences of ms_tail_kernel, which need
-// beta_{k-1}, known only now), then writes the next scalar state (nxt), the batch end
-// state into pinned memory (pin) and the stopping iteration. One launch of vector
-// work (p, s, r) instead of ms_rmfma + ms_tail, and no separate reduction launches:
-// two dependent launches per iteration instead of five.
+// and the block rows of B^T r_{k+1} on fp64 MFMA (as ms_rmfma_kernel) into bpart,
+// which the next iteration's reduction sums. p itself is never formed: the Gram
+// blocks need only b . p of the shifted systems, which the shift recurrences carry
+// from B^T r (so a pass reads r, w, s and B and writes s and r: six block passes,
+// against seven for the standard form's r update and p update). Block 0 does no
+// vector work: it takes
+// the shift step k - 1 (the zeta / G / b . p recurrences of ms_tail_kernel, which need
+// beta_{k-1}, known only now, and B^T r_k), then writes the next scalar state (nxt),
+// the batch end state into pinned memory (pin) and the stopping iteration.
 __global__ __launch_bounds__(256) void ms_cg2_update_kernel(
     const double* __restrict__ B, double* __restrict__ R, const double* __restrict__ W,
-    double* __restrict__ P, double* __restrict__ Sv, MsScal cur, MsScal nxt, MsShift sh,
-    const double* __restrict__ dred, int ndg, const double* __restrict__ bred_prev, int nbg,
-    double* __restrict__ bpart, double* __restrict__ bred, unsigned* __restrict__ bcnt,
+    double* __restrict__ Sv, MsScal cur, MsScal nxt, MsShift sh,
+    const double* __restrict__ red_in, double* __restrict__ bpart,
     const double* __restrict__ dshift, int S, int s, int nb, double rtol2, int k, int64_t n,
     MsPin* __restrict__ pin) {
   __shared__ double sd[2 * MS_MAXS];
@@ -1553,21 +1287,7 @@ __global__ __launch_bounds__(256) void ms_cg2_update_kernel(
   __shared__ int sup[MS_MAXS], sneg[MS_MAXS];
   __shared__ double red[4][16 * 16];
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  // gamma_k, delta_k: the SpMM's group rows summed in ascending group order
-  if (t < 2 * s) {
-    const int e = t;   // [0, s): r . w, [s, 2s): r . r
-    double sum = 0.0;
-    int q = 0;
-    for (; q + 8 <= ndg; q += 8) {
-      double v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = dred[(int64_t)(q + u) * 2 * s + e];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) sum += v[u];
-    }
-    for (; q < ndg; ++q) sum += dred[(int64_t)q * 2 * s + e];
-    sd[e] = sum;
-  }
+  if (t < 2 * s) sd[t] = red_in[t];   // [0, s): r . w, [s, 2s): r . r
   __syncthreads();
   if (t < s) {
     const double delta = sd[t], gamma = sd[s + t];
@@ -1581,18 +1301,19 @@ __global__ __launch_bounds__(256) void ms_cg2_update_kernel(
     sneg[t] = upd && !(den > 0.0);
   }
   __syncthreads();
+  const int neb = nb * s;
   if (blockIdx.x != 0) {
-    // ---- vector blocks: p, s, r and the B^T r_{k+1} partials ----
+    // ---- vector blocks: s, r and the B^T r_{k+1} block rows ----
     const int vb = blockIdx.x - 1, nvb = gridDim.x - 1;
     const int c = lane & 15, rq = lane >> 4;
     const bool on = c < s, onb = c < nb;
     const double al = on ? sal[c] : 0.0, be = on ? sbe[c] : 0.0;
     const bool up = on && sup[c];
     d4 acc = {0.0, 0.0, 0.0, 0.0};
-    constexpr int RG = 2;
+    constexpr int RG = 4;   // 16 loads in flight per lane
     const int64_t stride = (int64_t)nvb * 16;
     for (int64_t base = (int64_t)vb * 16 + wv * 4; base < n; base += RG * stride) {
-      double bv[RG], rv[RG], wv_[RG], pv[RG], sv[RG];
+      double bv[RG], rv[RG], wv_[RG], sv[RG];
 #pragma unroll
       for (int u = 0; u < RG; ++u) {
         const int64_t i = base + u * stride + rq;
@@ -1600,7 +1321,6 @@ __global__ __launch_bounds__(256) void ms_cg2_update_kernel(
         bv[u] = w ? B[i * nb + c] : 0.0;
         rv[u] = v ? R[i * s + c] : 0.0;
         wv_[u] = v ? W[i * s + c] : 0.0;
-        pv[u] = v ? P[i * s + c] : 0.0;
         sv[u] = v ? Sv[i * s + c] : 0.0;
       }
 #pragma unroll
@@ -1608,10 +1328,8 @@ __global__ __launch_bounds__(256) void ms_cg2_update_kernel(
         const int64_t i = base + u * stride + rq;
         double rn = rv[u];
         if (up && i < n) {
-          const double pn = rv[u] + be * pv[u];
           const double sn = wv_[u] + be * sv[u];
           rn = rv[u] - al * sn;
-          P[i * s + c] = pn;
           Sv[i * s + c] = sn;
           R[i * s + c] = rn;
         }
@@ -1622,25 +1340,15 @@ __global__ __launch_bounds__(256) void ms_cg2_update_kernel(
 #pragma unroll
     for (int j = 0; j < 4; ++j) red[wv][(rq + 4 * j) * 16 + c] = acc[j];
     __syncthreads();
-    const int neb = nb * s;
     for (int e = t; e < neb; e += 256) {
       const int cp = e / s, cc = e - cp * s;
       const int idx = cp * 16 + cc;
       bpart[(int64_t)vb * neb + e] = (red[0][idx] + red[1][idx]) + (red[2][idx] + red[3][idx]);
     }
-    group_reduce_rows(bpart, neb, vb, nvb, MS_GRP_U, bcnt, bred);
     return;
   }
-  // ---- block 0: shift step k - 1, the next scalar state ----
-  __shared__ double brd[MS_MAXS * MS_MAXS];
-  const int neb = nb * s;
-  if (k >= 1)
-    for (int e = t; e < neb; e += 256) {
-      double sum = 0.0;
-      for (int q = 0; q < nbg; ++q) sum += bred_prev[(int64_t)q * neb + e];
-      brd[e] = sum;
-    }
-  __syncthreads();
+  // ---- block 0: shift step k - 1 with B^T r_k = red_in[2s ..], the next state ----
+  const double* brd = red_in + 2 * s;
   if (k >= 1)
     for (int task = t; task < S * s; task += blockDim.x) {
       const int j = task / s, c = task % s;
@@ -1700,6 +1408,37 @@ __global__ __launch_bounds__(256) void ms_cg2_update_kernel(
   }
 }
 
+// The sums one iteration of ms_cg2_update_kernel needs, one workgroup per output
+// element e: e < 2 s the SpMM's block rows of [r . w | r . r] (rows_a rows of 2 s),
+// else the previous update's block rows of B^T r (rows_b rows of ne_b). Thread t sums
+// rows t, t + 256, ... (eight loads in flight), then the four waves in a fixed order.
+__global__ __launch_bounds__(256) void ms_cg2_reduce_kernel(const double* __restrict__ pa,
+                                                            int rows_a, int s,
+                                                            const double* __restrict__ pb,
+                                                            int rows_b, int ne_b,
+                                                            double* __restrict__ out) {
+  __shared__ double w4[4];
+  const int e = blockIdx.x, t = threadIdx.x;
+  const bool first = e < 2 * s;
+  const double* src = first ? pa + e : pb + (e - 2 * s);
+  const int rows = first ? rows_a : rows_b;
+  const int64_t ld = first ? 2 * s : ne_b;
+  double a = 0.0;
+  int b = t;
+  for (; b + 7 * 256 < rows; b += 8 * 256) {
+    double x[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) x[q] = src[(int64_t)(b + q * 256) * ld];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) a += x[q];
+  }
+  for (; b < rows; b += 256) a += src[(int64_t)b * ld];
+  a = wave_sum(a);
+  if ((t & 63) == 0) w4[t >> 6] = a;
+  __syncthreads();
+  if (t == 0) out[e] = (w4[0] + w4[1]) + (w4[2] + w4[3]);
+}
+
 // Group rows of x . y and x . x per column ([blockIdx.x][2s]: x . y, then x . x) for
 // SpMM kinds without the dot epilogue: MS_DOT_BLK blocks, each a contiguous range of
 // rows, rows_per = 256 / s rows per block pass, summed in a fixed order.
@@ -1733,9 +1472,10 @@ __global__ __launch_bounds__(256) void ms_dots2_kernel(const double* __restrict_
   }
 }
 
-// Initial scalar state from BR0 = B^T b (= b . p_0 for every shift) and ||b||^2.
-__global__ void ms_init_kernel(MsState st, const double* __restrict__ partial, int nblk, int S,
-                               int s, int nb) {
+// Initial scalar state from BR0 = B^T b (= b . p_0 for every shift) and ||b||^2:
+// zeta = 1, G = 0, alpha_{-1} = 1 (a, a_prev), beta_{-1} = 0, active = ||b|| > 0.
+__global__ void ms_init_kernel(MsScal st, MsShift sh, const double* __restrict__ partial,
+                               int nblk, int S, int s, int nb) {
   __shared__ double br[MS_MAXS * MS_MAXS + MS_MAXS];
   const int ne = nb * s + s;
   {
@@ -1749,23 +1489,26 @@ __global__ void ms_init_kernel(MsState st, const double* __restrict__ partial, i
   const int t = threadIdx.x;
   const int j = t / s, c = t % s;
   if (j < S) {
-    st.z[j * s + c] = 1.0;
-    st.z_prev[j * s + c] = 1.0;
+    sh.z[j * s + c] = 1.0;
+    sh.z_prev[j * s + c] = 1.0;
     for (int cp = 0; cp < nb; ++cp) {
       const int e = (j * nb + cp) * s + c;
-      st.bp[e] = br[cp * s + c];
-      st.g[e] = 0.0;
+      sh.bp[e] = br[cp * s + c];
+      sh.g[e] = 0.0;
     }
   }
   if (t < s) {
     st.rr[t] = br[nb * s + t];
-    st.bn2[t] = br[nb * s + t];
-    st.a[t] = 0.0;
+    sh.bn2[t] = br[nb * s + t];
+    st.a[t] = 1.0;
     st.a_prev[t] = 1.0;
     st.beta[t] = 0.0;
     st.active[t] = br[nb * s + t] > 0.0 ? 1 : 0;
   }
-  if (t == 0) st.flags[0] = 0;
+  if (t == 0) {
+    sh.flags[0] = 0;
+    sh.it_stop[0] = -1;
+  }
 }
 
 // dst[i][c] = src[perm[i]][c] for c < ns_src, 0 for the padding columns up to s

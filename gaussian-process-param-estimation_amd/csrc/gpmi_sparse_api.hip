@@ -3,6 +3,7 @@
 // stochastic Lanczos quadrature, and blocked CG.
 
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <algorithm>
 #include <atomic>
@@ -47,8 +48,7 @@ __global__ void csr_spmm_win_kernel(const int64_t*, const int*, const unsigned s
 template <int S, int U, int TPR>
 __global__ void csr_spmm_wing_kernel(const int64_t*, const int*, const unsigned short*,
                                      const double*, int64_t, const int*, const int*,
-                                     const double*, double*, double, double*, double*,
-                                     unsigned*);
+                                     const double*, double*, double, double*, int);
 constexpr int WING_MAX_LDS = 80 * 1024;   // two workgroups per CU
 // nonzeros in flight per thread and threads per row of csr_spmm_wing_kernel (measured:
 // 8 in flight best at cfg 5, within 0.3 us of 4 at cfg 4; 8 threads per row in
@@ -60,7 +60,6 @@ constexpr int WIN_CS_HOST = 8;       // = WIN_CS
 __global__ void col_dot_partial_kernel(const double*, int64_t, const double*, int64_t, int,
                                        double*);
 __global__ void col_dot_reduce_kernel(const double*, int, int, int, double*);
-__global__ void col_dot_reduce_wg_kernel(const double*, int, int, double*);
 __global__ void col_gs_update_kernel(double*, const double*, int64_t, const double*, int, int64_t,
                                      int);
 __global__ void col_axpby_kernel(const double*, double*, const double*, const double*, int64_t,
@@ -93,15 +92,11 @@ __global__ void lanczos_scalar_kernel(const double*, const double*, const double
 void launch_ms_dots(const double* B, const double* R, int64_t n, int s, double* partial, int nblk,
                     hipStream_t st, int sa);
 __global__ void rows_gather_kernel(const double*, int, const int*, int64_t, int, double*);
-__global__ void ms_rmfma_kernel(const double*, double*, const double*, MsState, const double*, int,
-                                int64_t, int, int, double*);
-__global__ void ms_tail_kernel(MsState, MsState, const double*, const double*, int, int, int, double,
-                               double*, const double*, int64_t, MsPin*);
-__global__ void ms_init_kernel(MsState, const double*, int, int, int, int);
-__global__ void ms_cg2_update_kernel(const double*, double*, const double*, double*, double*,
-                                     MsScal, MsScal, MsShift, const double*, int, const double*,
-                                     int, double*, double*, unsigned*, const double*, int, int,
-                                     int, double, int, int64_t, MsPin*);
+__global__ void ms_init_kernel(MsScal, MsShift, const double*, int, int, int, int);
+__global__ void ms_cg2_update_kernel(const double*, double*, const double*, double*,
+                                     MsScal, MsScal, MsShift, const double*, double*,
+                                     const double*, int, int, int, double, int, int64_t, MsPin*);
+__global__ void ms_cg2_reduce_kernel(const double*, int, int, const double*, int, int, double*);
 __global__ void ms_dots2_kernel(const double*, const double*, int64_t, int, double*);
 template <int CT>
 __global__ void dense_mm_kernel(const double*, int64_t, int64_t, const double*, int, int, double*);
@@ -136,7 +131,6 @@ namespace {
 constexpr int NBLK = 256;   // fixed reduction grid (deterministic sums)
 constexpr int MAXS = 32;    // vector-block width per device pass
 constexpr int MS_NBLK = 128; // row blocks of the multi-shift dot partials
-constexpr int MS_RB = 512;   // row blocks of ms_rmfma_kernel (its loads in flight)
 
 struct Guard {
   int prev = -1;
@@ -189,8 +183,6 @@ struct gpmi_sp {
   void* ms_pin = nullptr;                  // pinned flags / r.r of two CG batches
   double* cg2_buf = nullptr;               // the Chronopoulos-Gear form's dot rows
   size_t cg2_doubles = 0;
-  unsigned* cg2_cnt = nullptr;             // ... and its group counters (kept zero)
-  size_t cg2_cnt_n = 0;
   hipEvent_t ms_ev[2] = {nullptr, nullptr};
   std::mutex win_mu;           // the lazy X-window build (ensure_window)
   size_t msbuf_doubles = 0;
@@ -370,7 +362,8 @@ int spmm_kind(gpmi_sp* sp, int s, int* kind) {
 // X . Y per column (pqp[block][s], the multi-shift CG's p . q) and sets *pq_blocks to
 // their count; otherwise *pq_blocks = 0 and the caller forms them.
 int spmm_launch(gpmi_sp* sp, const double* X, double* Y, int s, double eta, hipStream_t st,
-                double* pqp, int* pq_blocks, double* gred, unsigned* gcnt) {
+                double* pqp, int* pq_blocks, int dots2,
+                hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr) {
   if (pq_blocks) *pq_blocks = 0;
   if (sp->dK) {
     // dense: split partials of K X on fp64 MFMA, summed in split order (+ eta X)
@@ -397,23 +390,23 @@ int spmm_launch(gpmi_sp* sp, const double* X, double* Y, int s, double eta, hipS
       ((reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(Y)) & 15) != 0)
     kind = 0;
   if (kind == 5) {
-    // the window, and the epilogue's [64][s] row partials of X . Y (pqp), or with gred
-    // the [64][2s] rows of X . Y and X . X and their group sums (the CG-CG form)
+    // the window, and the epilogue's [64][s] rows of X . Y (pqp), with dots2 its
+    // [64][2s] rows of X . Y and X . X (the Chronopoulos-Gear multi-shift CG)
     const size_t lds = sizeof(double) * (size_t)s *
                        (size_t)std::max(sp->win_maxu.load(std::memory_order_acquire),
-                                        (gred ? 2 : 1) * WIN_ROWS_HOST);
+                                        (dots2 ? 2 : 1) * WIN_ROWS_HOST);
     auto kfn = s == 20   ? csr_spmm_wing_kernel<20, WING_U, WING_TPR>
                : s == 12 ? csr_spmm_wing_kernel<12, WING_U, WING_TPR>
                : s == 11 ? csr_spmm_wing_kernel<11, WING_U, WING_TPR>
                : s == 8  ? csr_spmm_wing_kernel<8, WING_U, WING_TPR>
                          : csr_spmm_wing_kernel<7, WING_U, WING_TPR>;
     const int tpr = WING_TPR;
-    hipLaunchKernelGGL(kfn, dim3((unsigned)sp->win_nblk), dim3(64 * tpr), lds, st, sp->indptr,
-                       sp->indices, sp->win_lidx, sp->data, sp->n, sp->win_cols, sp->win_u, X, Y,
-                       eta, pqp, gred, gcnt);
+    // (timed: the events ride in the dispatch packet, as the profiler's timestamps)
+    hipExtLaunchKernelGGL(kfn, dim3((unsigned)sp->win_nblk), dim3(64 * tpr), lds, st, ev0, ev1, 0,
+                          sp->indptr, sp->indices, sp->win_lidx, sp->data, sp->n, sp->win_cols,
+                          sp->win_u, X, Y, eta, pqp, dots2);
     SP_LAUNCH("csr_spmm_wing_kernel");
-    if (pqp && pq_blocks)
-      *pq_blocks = gred ? (int)((sp->win_nblk + MS_GRP_SP - 1) / MS_GRP_SP) : (int)sp->win_nblk;
+    if (pqp && pq_blocks) *pq_blocks = (int)sp->win_nblk;
     return 0;
   }
   if (kind == 1) {
@@ -457,19 +450,27 @@ int take_event(gpmi_sp* sp, hipEvent_t* e) {
 // Y = (K + eta I) X (spmm_launch), bracketed by a HIP event pair on its stream when
 // in-step timing is on (gpmi_sp_set_timing).
 int spmm(gpmi_sp* sp, const double* X, double* Y, int s, double eta, hipStream_t st = nullptr,
-         double* pqp = nullptr, int* pq_blocks = nullptr, double* gred = nullptr,
-         unsigned* gcnt = nullptr) {
+         double* pqp = nullptr, int* pq_blocks = nullptr, int dots2 = 0) {
   if (!st) st = sp->stream;
-  if (!sp->timing) return spmm_launch(sp, X, Y, s, eta, st, pqp, pq_blocks, gred, gcnt);
+  if (!sp->timing) return spmm_launch(sp, X, Y, s, eta, st, pqp, pq_blocks, dots2);
   gpmi_sp::SpmmRec rec{nullptr, nullptr, s};
   {
     std::lock_guard<std::mutex> lock(sp->timing_mu);
     if (int rc = take_event(sp, &rec.e0)) return rc;
     if (int rc = take_event(sp, &rec.e1)) return rc;
   }
-  SP_TRY(hipEventRecord(rec.e0, st));
-  if (int rc = spmm_launch(sp, X, Y, s, eta, st, pqp, pq_blocks, gred, gcnt)) return rc;
-  SP_TRY(hipEventRecord(rec.e1, st));
+  // the window SpMM carries the pair in its dispatch packet (hipExtLaunchKernel: the
+  // kernel's own start / end, as rocprofv3 sees them); other kinds: recorded around
+  int kind = 0;
+  if (int rc = spmm_kind(sp, s, &kind)) return rc;
+  const bool in_packet =
+      kind == 5 && !sp->dK &&
+      !(s % 2 == 0 && ((reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(Y)) & 15));
+  if (!in_packet) SP_TRY(hipEventRecord(rec.e0, st));
+  if (int rc = spmm_launch(sp, X, Y, s, eta, st, pqp, pq_blocks, dots2,
+                           in_packet ? rec.e0 : nullptr, in_packet ? rec.e1 : nullptr))
+    return rc;
+  if (!in_packet) SP_TRY(hipEventRecord(rec.e1, st));
   std::lock_guard<std::mutex> lock(sp->timing_mu);
   sp->spmm_log.push_back(rec);
   return 0;
@@ -1016,7 +1017,6 @@ int gpmi_sp_destroy(gpmi_sp* sp) {
   if (sp->ms_partial) (void)hipFree(sp->ms_partial);
   if (sp->ms_pin) (void)hipHostFree(sp->ms_pin);
   if (sp->cg2_buf) (void)hipFree(sp->cg2_buf);
-  if (sp->cg2_cnt) (void)hipFree(sp->cg2_cnt);
   for (hipEvent_t e : sp->ev_pool) (void)hipEventDestroy(e);
   for (auto& r : sp->spmm_log) {
     (void)hipEventDestroy(r.e0);
@@ -1305,12 +1305,17 @@ int gpmi_sp_cg(gpmi_sp* sp, double eta, const double* rhs, int64_t ld, int nrhs,
   return 0;
 }
 
-// The multi-shift CG in the Chronopoulos-Gear form (round 5, the default;
-// GPMI_MS_CG=classic keeps the standard form below): per iteration the SpMM
-// w = (K + eta_0 I) r with the r . w / r . r group sums in its epilogue (window SpMM;
-// other kinds: + ms_dots2_kernel), then ms_cg2_update_kernel (the scalars, p, s, r,
-// B^T r, and the shift step of the previous iteration): two dependent launches per
-// iteration instead of five. Same arguments, results and polling as msgram_impl.
+// The multi-shift CG in the Chronopoulos-Gear form (round 5): per iteration the SpMM
+// w = (K + eta_0 I) r with the r . w / r . r block rows in its epilogue (window SpMM;
+// other kinds: + ms_dots2_kernel), ms_cg2_reduce_kernel (those rows and the previous
+// update's B^T r rows summed), then ms_cg2_update_kernel (the scalars, p, s, r, the
+// B^T r rows, and the shift step of the previous iteration): three dependent launches
+// per iteration against the standard form's five (round 4: SpMM, its p . q sum, the r
+// update with B^T r, its sum, the tail), and six vector passes against seven: cfg 4
+// 4.80 -> 4.31 ms, cfg 5 13.44 -> 12.81 ms per step on one box (tools/sparse_ab.sh).
+// (A two-launch form that summed the rows inside the SpMM and the update by group
+// last-arriver tickets was slower: every block then drains its stores before its
+// ticket, 12.6 -> 25 us per cfg 4 SpMM.)
 static int msgram_cg2(gpmi_sp* sp, const double* etas, int neta, const double* rhs,
                       int64_t ld, int nrhs, int c_lo, int c_hi, double rtol, int maxiter,
                       double* G, int* iterations) {
@@ -1324,7 +1329,9 @@ static int msgram_cg2(gpmi_sp* sp, const double* etas, int neta, const double* r
   {
     int rc0 = spmm_kind(sp, s, &kind);
     if (rc0) return rc0;
-    // the window SpMM stages 12-column rows with 16-byte loads (see msgram_impl)
+    // Padding (the Gram of the real columns is unchanged by a zero column, inactive
+    // from the start: ||b|| = 0): the window SpMM at s = 11 stages 12-column rows with
+    // 16-byte loads: cfg 5 s = 11 88 -> 73 us per launch (round 3)
     if (full && kind == 5 && s == 11 && S * (s + 1) <= 1024) ++s;
     if ((rc0 = spmm_kind(sp, s, &kind))) return rc0;
   }
@@ -1335,8 +1342,8 @@ static int msgram_cg2(gpmi_sp* sp, const double* etas, int neta, const double* r
   const double eta0 = *std::min_element(etas, etas + neta);
   int rc = 0;
   auto even = [](size_t d) { return (d + 1) & ~(size_t)1; };
-  // B [n][nbd], the host staging [n][nrhs], and R, W, P, S [n][s] (16-byte aligned)
-  const size_t wsn = even((size_t)nsb) + even((size_t)n * nrhs) + 4 * even((size_t)ns);
+  // B [n][nbd], the host staging [n][nrhs], and R, W, S [n][s] (16-byte aligned)
+  const size_t wsn = even((size_t)nsb) + even((size_t)n * nrhs) + 3 * even((size_t)ns);
   if (sp->ms_ws_doubles < wsn) {
     if (sp->ms_ws) SP_TRY(hipFree(sp->ms_ws));
     sp->ms_ws = nullptr;
@@ -1347,46 +1354,27 @@ static int msgram_cg2(gpmi_sp* sp, const double* etas, int neta, const double* r
   double* Hs = Bd + even((size_t)nsb);
   double* Rd = Hs + even((size_t)n * nrhs);
   double* Wd = Rd + even((size_t)ns);
-  double* Pd = Wd + even((size_t)ns);
-  double* Sd = Pd + even((size_t)ns);
-  // dot rows: the SpMM's per-block [nblk][2s] and group [ndg][2s]; the update's B^T r
-  // per-block [MS_UB][nbd s] and group rows [2][nbg][nbd s] (parity: iteration k + 1
-  // reads k's while writing its own); the init partials [MS_NBLK][ne]; the group
-  // counters (zeroed here once: every group's last arriver resets its own)
+  double* Sd = Wd + even((size_t)ns);
+  // dot rows: the SpMM's per-block [nblk][2s]; the update's B^T r per-block
+  // [MS_UB][nbd s]; their sums [2s + nbd s] (ms_cg2_reduce_kernel); the init partials
+  // [MS_NBLK][ne]
   const int64_t nblk_sp = kind == 5 ? sp->win_nblk : MS_DOT_BLK;
-  const int ndg = kind == 5 ? (int)((nblk_sp + MS_GRP_SP - 1) / MS_GRP_SP) : MS_DOT_BLK;
   const int neb = nbd * s;
-  const int nbg = (MS_UB + MS_GRP_U - 1) / MS_GRP_U;
   const int ne0 = nbd * s + s;
-  const size_t c_sp = (size_t)nblk_sp * 2 * s, c_dg = (size_t)ndg * 2 * s;
-  const size_t c_bp = (size_t)MS_UB * neb, c_bg = (size_t)nbg * neb;
-  const size_t c_init = (size_t)MS_NBLK * ne0;
-  const size_t need = c_sp + c_dg + c_bp + 2 * c_bg + c_init;
+  const size_t c_sp = (size_t)nblk_sp * 2 * s, c_bp = (size_t)MS_UB * neb;
+  const size_t c_red = 2 * (size_t)s + neb, c_init = (size_t)MS_NBLK * ne0;
+  const size_t need = c_sp + c_bp + c_red + c_init;
   if (sp->cg2_doubles < need) {
     if (sp->cg2_buf) SP_TRY(hipFree(sp->cg2_buf));
     sp->cg2_buf = nullptr;
     SP_TRY(hipMalloc(&sp->cg2_buf, sizeof(double) * need));
     sp->cg2_doubles = need;
   }
-  // the group counters live in an allocation of their own, zeroed once: every
-  // launch's last arrivers leave them at zero again, whatever the layout above
-  const size_t n_cnt = (size_t)ndg + 1 + (size_t)nbg + 1;
-  if (sp->cg2_cnt_n < n_cnt) {
-    if (sp->cg2_cnt) SP_TRY(hipFree(sp->cg2_cnt));
-    sp->cg2_cnt = nullptr;
-    const size_t cap = std::max<size_t>(n_cnt, 2048);
-    SP_TRY(hipMalloc(&sp->cg2_cnt, sizeof(unsigned) * cap));
-    SP_TRY(hipMemset(sp->cg2_cnt, 0, sizeof(unsigned) * cap));
-    sp->cg2_cnt_n = cap;
-  }
   double* spart = sp->cg2_buf;
-  double* dred = spart + c_sp;
-  double* bpart = dred + c_dg;
-  double* bred2[2] = {bpart + c_bp, bpart + c_bp + c_bg};
-  double* ipart = bred2[1] + c_bg;
-  unsigned* gcnt_sp = sp->cg2_cnt;
-  unsigned* gcnt_u = gcnt_sp + ndg + 1;
-  // scalar state: MsScal x 2, MsShift, and the old MsState view for ms_init_kernel
+  double* bpart = spart + c_sp;
+  double* dred = bpart + c_bp;
+  double* ipart = dred + c_red;
+  // scalar state: MsScal x 2 (parity), MsShift
   const size_t sneed = 2 * (4 * (size_t)s + s) + (size_t)s + 2 * (size_t)S * s +
                        2 * (size_t)S * nbd * s + S + 4;
   if (sp->msbuf_doubles < sneed) {
@@ -1413,18 +1401,6 @@ static int msgram_cg2(gpmi_sp* sp, const double* etas, int neta, const double* r
   double* dshift = q; q += S;
   sh.flags = reinterpret_cast<int*>(q); q += 1;
   sh.it_stop = reinterpret_cast<int*>(q); q += 1;
-  MsState st{};   // ms_init_kernel's view: cur[0] scalars + the shift state
-  st.rr = sc[0].rr;
-  st.a = sc[0].a;
-  st.a_prev = sc[0].a_prev;
-  st.beta = sc[0].beta;
-  st.active = sc[0].active;
-  st.bn2 = sh.bn2;
-  st.z = sh.z;
-  st.z_prev = sh.z_prev;
-  st.bp = sh.bp;
-  st.g = sh.g;
-  st.flags = sh.flags;
   sp->last_converged = 0;
   hipStream_t str = sp->ms_stream;
   {
@@ -1453,35 +1429,33 @@ static int msgram_cg2(gpmi_sp* sp, const double* etas, int neta, const double* r
                          nbd, (const int*)nullptr, n, s, Rd);
       SP_LAUNCH("rows_gather_kernel");
     }
-    // p_{-1} = s_{-1} = 0 (beta_{-1} = 0 multiplies them: no NaN may stand there)
-    SP_TRY(hipMemsetAsync(Pd, 0, sizeof(double) * 2 * even((size_t)ns), str));
-    const int minus1 = -1;
-    SP_TRY(hipMemcpyAsync(sh.it_stop, &minus1, sizeof(int), hipMemcpyHostToDevice, str));
+    // s_{-1} = 0 (beta_{-1} = 0 multiplies it: no NaN may stand there)
+    SP_TRY(hipMemsetAsync(Sd, 0, sizeof(double) * ns, str));
   }
   launch_ms_dots(Bd, Rd, n, s, ipart, MS_NBLK, str, nbd);
   SP_LAUNCH("ms_dots_partial_kernel");
-  hipLaunchKernelGGL(ms_init_kernel, dim3(1), dim3(1024), 0, str, st, ipart, MS_NBLK, S, s, nbd);
+  hipLaunchKernelGGL(ms_init_kernel, dim3(1), dim3(1024), 0, str, sc[0], sh, ipart, MS_NBLK, S, s,
+                     nbd);
   SP_LAUNCH("ms_init_kernel");
-  // alpha_{-1} = 1 (ms_init_kernel leaves a = 0, a_prev = 1: the standard form's
-  // state before its first iteration): a_prev into a
-  SP_TRY(hipMemcpyAsync(sc[0].a, sc[0].a_prev, sizeof(double) * s, hipMemcpyDeviceToDevice, str));
   int it = 0;
   // one iteration's launches on str (parity it & 1 picks the scalar and B^T r buffers)
   auto iterate = [&](int k, MsPin* pin_out) -> int {
-    int ng = 0;
-    int rc1 = spmm(sp, Rd, Wd, s, eta0, str, spart, &ng, dred, gcnt_sp);
+    int rows = 0;
+    int rc1 = spmm(sp, Rd, Wd, s, eta0, str, spart, &rows, 1);
     if (rc1) return rc1;
-    if (ng == 0) {
+    if (rows == 0) {
       hipLaunchKernelGGL(ms_dots2_kernel, dim3(MS_DOT_BLK), dim3(256), 0, str, (const double*)Rd,
-                         (const double*)Wd, n, s, dred);
+                         (const double*)Wd, n, s, spart);
       SP_LAUNCH("ms_dots2_kernel");
-      ng = MS_DOT_BLK;
+      rows = MS_DOT_BLK;
     }
+    hipLaunchKernelGGL(ms_cg2_reduce_kernel, dim3(2 * s + neb), dim3(256), 0, str,
+                       (const double*)spart, rows, s, (const double*)bpart, MS_UB, neb, dred);
+    SP_LAUNCH("ms_cg2_reduce_kernel");
     hipLaunchKernelGGL(ms_cg2_update_kernel, dim3(MS_UB + 1), dim3(256), 0, str,
-                       (const double*)Bd, Rd, (const double*)Wd, Pd, Sd, sc[k & 1],
-                       sc[(k + 1) & 1], sh, (const double*)dred, ng,
-                       (const double*)bred2[(k + 1) & 1], nbg, bpart, bred2[k & 1], gcnt_u,
-                       (const double*)dshift, S, s, nbd, rtol * rtol, k, n, pin_out);
+                       (const double*)Bd, Rd, (const double*)Wd, Sd, sc[k & 1],
+                       sc[(k + 1) & 1], sh, (const double*)dred, bpart, (const double*)dshift, S,
+                       s, nbd, rtol * rtol, k, n, pin_out);
     SP_LAUNCH("ms_cg2_update_kernel");
     return 0;
   };
@@ -1504,8 +1478,14 @@ static int msgram_cg2(gpmi_sp* sp, const double* etas, int neta, const double* r
     for (int c = 0; c < s; ++c) any = any || hact[c];
     if (!any) maxiter = 0;
   }
-  // batches between host reads of the end state, sized from the residual decay (as
-  // msgram_impl); iteration k's end state is gamma_k (the residual entering it)
+  // Iterations run in batches between host reads of the stop flags. Each batch's last
+  // update kernel writes its end state (active flags, the negative-curvature flag,
+  // gamma) into host-mapped pinned memory, read while the NEXT batch is already
+  // queued, so the device does not wait for the host between batches. The next
+  // batch's size comes from the residuals' decay: the iterations the slowest active
+  // column still needs at its rate since the previous read, beyond what is queued (at
+  // most MS_BATCH); when the queued iterations should suffice the host waits for them
+  // instead. Iterations past a column's stop leave it unchanged (zero steps).
   int slot_it[2] = {0, 0};
   std::vector<double> rr_seen(s, -1.0);
   int it_seen = 0;
@@ -1597,310 +1577,7 @@ static int msgram_impl(gpmi_sp* sp, const double* etas, int neta, const double* 
       neta * (c_hi - c_lo) > 1024)
     return set_error(-1104, "msgram: need 1 <= nrhs <= 16, 0 <= c_lo < c_hi <= nrhs and "
                             "neta * (c_hi - c_lo) <= 1024");
-  {
-    const char* ce = std::getenv("GPMI_MS_CG");
-    if (!(ce && std::strcmp(ce, "classic") == 0))
-      return msgram_cg2(sp, etas, neta, rhs, ld, nrhs, c_lo, c_hi, rtol, maxiter, G, iterations);
-  }
-  const int nsub = c_hi - c_lo;
-  const bool full = nsub == nrhs;
-  Guard g(sp->device);
-  const int64_t n = sp->n;
-  const int S = neta;
-  // Padding (the Gram of the real columns is unchanged by a zero column, inactive
-  // from the start: ||b|| = 0): the window SpMM at s = 11 stages 12-column rows with
-  // 16-byte loads: cfg 5 s = 11 88 -> 73 us per launch, step 21.7 -> 20.9 ms (s = 7 ->
-  // 8 measured neutral at cfg 4; an odd block padded for the column-pair gather
-  // measured slower at cfg 5, 161 against 119 us)
-  int s = nsub;
-  {
-    int kind = 0;
-    int rc0 = spmm_kind(sp, s, &kind);
-    if (rc0) return rc0;
-    if (full && kind == 5 && s == 11 && S * (s + 1) <= 1024) ++s;
-  }
-  // the dot columns: all of B (with the padding column when the full block is padded)
-  const int nbd = full ? s : nrhs;
-  const int64_t nsb = n * nbd;
-  if (!sp->ms_stream) SP_TRY(hipStreamCreateWithFlags(&sp->ms_stream, hipStreamNonBlocking));
-  const int64_t ns = n * s;
-  const double eta0 = *std::min_element(etas, etas + neta);
-  int rc = 0;
-  // B [n][nbd], its host staging [n][nrhs], and R, P, Q [n][s], each segment an even
-  // number of doubles so that every block starts 16-byte aligned (the window and
-  // pair SpMMs read X with 16-byte loads; an odd n would misalign them)
-  auto even = [](size_t d) { return (d + 1) & ~(size_t)1; };
-  const size_t wsn = even((size_t)nsb) + even((size_t)n * nrhs) + 3 * even((size_t)ns);
-  if (sp->ms_ws_doubles < wsn) {
-    if (sp->ms_ws) SP_TRY(hipFree(sp->ms_ws));
-    sp->ms_ws = nullptr;
-    SP_TRY(hipMalloc(&sp->ms_ws, sizeof(double) * wsn));
-    sp->ms_ws_doubles = wsn;
-  }
-  const int ne = nbd * s + s;
-  {
-    // the SpMM kernel choice builds the window (and so win_nblk) before the p . q
-    // partial rows are sized from it
-    int kind = 0;
-    if ((rc = spmm_kind(sp, s, &kind))) return rc;
-  }
-  // [MS_NBLK][ne] dot partials, then the p . q partials: [NBLK][s] (col_dot_partial)
-  // or [win_nblk][s] from the window SpMM's epilogue, and their [s] sums
-  const size_t pq_rows = std::max<size_t>(NBLK, (size_t)std::max<int64_t>(0, sp->win_nblk));
-  const size_t pneed = (size_t)MS_RB * ne + pq_rows * s + s;
-  if (sp->ms_partial_doubles < pneed) {
-    if (sp->ms_partial) SP_TRY(hipFree(sp->ms_partial));
-    sp->ms_partial = nullptr;
-    SP_TRY(hipMalloc(&sp->ms_partial, sizeof(double) * pneed));
-    sp->ms_partial_doubles = pneed;
-  }
-  double* partial = sp->ms_partial;
-  double* pqpart = partial + (size_t)MS_RB * ne;
-  double* pqsum = pqpart + pq_rows * s;
-  const size_t need = (size_t)6 * s + 2 * (size_t)S * s + 2 * (size_t)S * nbd * s + S + s + s +
-                      1 + (size_t)ne + 2 * (size_t)s;
-  if (sp->msbuf_doubles < need) {
-    if (sp->msbuf) SP_TRY(hipFree(sp->msbuf));
-    sp->msbuf = nullptr;
-    SP_TRY(hipMalloc(&sp->msbuf, sizeof(double) * need));
-    sp->msbuf_doubles = need;
-  }
-  double* q = sp->msbuf;
-  MsState st;
-  st.rr = q; q += s;
-  st.a = q; q += s;
-  st.a_prev = q; q += s;
-  st.beta = q; q += s;
-  st.bn2 = q; q += s;
-  st.z = q; q += (size_t)S * s;
-  st.z_prev = q; q += (size_t)S * s;
-  st.bp = q; q += (size_t)S * nbd * s;
-  st.g = q; q += (size_t)S * nbd * s;
-  double* dshift = q; q += S;
-  q += s;   // (spare slot)
-  st.active = reinterpret_cast<int*>(q);   // s ints in s doubles
-  q += s;
-  st.flags = reinterpret_cast<int*>(q);    // 1 int in 1 double
-  q += 1;
-  double* brd = q;                         // [ne] reduced B^T r, r . r
-  q += ne;
-  // the second rr / active buffers (ms_tail_kernel reads one state's and writes the
-  // other's; iteration it's current state is st2[it & 1])
-  MsState st2[2] = {st, st};
-  st2[1].rr = q; q += s;
-  st2[1].active = reinterpret_cast<int*>(q);
-  q += s;
-  sp->last_converged = 0;
-  double* Bd = sp->ms_ws;
-  double* Hs = Bd + even((size_t)nsb);   // the host block as given (original row order)
-  double* Rd = Hs + even((size_t)n * nrhs);
-  double* Pd = Rd + even((size_t)ns);
-  double* Qd = Pd + even((size_t)ns);
-  // Per iteration: the SpMM (p . q partials from the window kernel's epilogue, else
-  // col_dot_partial_kernel), then the r update and B^T r, r . r on MFMA in one pass over
-  // b, r, q (ms_rmfma_kernel, s <= 16: every block the library forms; cfg 4 6.9-7.3 ->
-  // 6.3 ms per step against the scalar forms it replaced), its 512 partial rows summed
-  // one wave per element across the chip (cfg 5 33.6 -> 32.0 ms against the
-  // one-workgroup sum), the per-shift scalars, and p = r + beta p.
-  double* Rcur = Rd;     // the live residual
-  hipStream_t str = sp->ms_stream;
-  {
-    // the RHS block as the caller holds it (rows in the original order) into the
-    // staging Qd, then into the locality order (and zero padding columns) on the
-    // device: no host-side permutation pass over n x s doubles
-    const double* Hsrc = Hs;
-    if (!rhs) {
-      Hsrc = sp->rhs_dev;
-    } else if (ld == nrhs) {
-      SP_TRY(hipMemcpyAsync(Hs, rhs, sizeof(double) * n * nrhs, hipMemcpyHostToDevice, str));
-    } else {
-      std::vector<double> h((size_t)n * nrhs);
-      for (int64_t i = 0; i < n; ++i)
-        for (int c = 0; c < nrhs; ++c) h[(size_t)i * nrhs + c] = rhs[i * ld + c];
-      SP_TRY(hipMemcpyAsync(Hs, h.data(), sizeof(double) * h.size(), hipMemcpyHostToDevice, str));
-      SP_TRY(hipStreamSynchronize(str));
-    }
-    hipLaunchKernelGGL(rows_gather_kernel, dim3(grid_ns(n, nbd)), dim3(256), 0, str, Hsrc, nrhs,
-                       (const int*)sp->perm_d, n, nbd, Bd);
-    SP_LAUNCH("rows_gather_kernel");
-    std::vector<double> hd(S);
-    for (int j = 0; j < S; ++j) hd[j] = etas[j] - eta0;
-    SP_TRY(hipMemcpyAsync(dshift, hd.data(), sizeof(double) * S, hipMemcpyHostToDevice, str));
-    if (full) {
-      SP_TRY(hipMemcpyAsync(Rd, Bd, sizeof(double) * ns, hipMemcpyDeviceToDevice, str));
-    } else {
-      // the shard's columns of B (already in the device row order)
-      hipLaunchKernelGGL(rows_gather_kernel, dim3(grid_ns(n, s)), dim3(256), 0, str, Bd + c_lo,
-                         nbd, (const int*)nullptr, n, s, Rd);
-      SP_LAUNCH("rows_gather_kernel");
-    }
-    SP_TRY(hipMemcpyAsync(Pd, Rd, sizeof(double) * ns, hipMemcpyDeviceToDevice, str));
-    SP_TRY(hipStreamSynchronize(str));
-  }
-  // scalar kernels: S * s threads for the per-shift recurrences (<= 1024), and
-  // 16 waves for their fixed-order partial reductions
-  const unsigned sthreads = 1024;
-  launch_ms_dots(Bd, Rd, n, s, partial, MS_NBLK, str, nbd);
-  SP_LAUNCH("ms_dots_partial_kernel");
-  hipLaunchKernelGGL(ms_init_kernel, dim3(1), dim3(sthreads), 0, str, st, partial, MS_NBLK, S,
-                     s, nbd);
-  SP_LAUNCH("ms_init_kernel");
-  int it = 0;
-  std::vector<int> hact(2 * s + 2);
-  auto poll = [&](bool* any) -> int {
-    // the current state's active[0..s) and flags[0]
-    SP_TRY(hipMemcpyAsync(hact.data(), st2[it & 1].active, sizeof(int) * s, hipMemcpyDeviceToHost,
-                          str));
-    SP_TRY(hipMemcpyAsync(hact.data() + 2 * s, st.flags, sizeof(int), hipMemcpyDeviceToHost, str));
-    SP_TRY(hipStreamSynchronize(str));
-    *any = false;
-    for (int c = 0; c < s; ++c) *any = *any || hact[c];
-    return hact[2 * s] ? set_error(1, "multi-shift CG: p^T (K + min(eta) I) p <= 0 (not positive "
-                                      "definite)")
-                       : 0;
-  };
-  // one iteration's launches on str (parity it & 1 picks the state double buffer)
-  auto iterate = [&](int itx, MsPin* pin_out) -> int {
-    // the window SpMM also forms the p . q block partials in its epilogue (summed
-    // across the chip below); other kernels leave them to col_dot_partial_kernel
-    int pqb = 0;
-    int rc1 = spmm(sp, Pd, Qd, s, eta0, str, pqpart, &pqb);
-    if (rc1) return rc1;
-    const double* pqin = pqpart;
-    int pqn = NBLK;
-    if (pqb >= 1024) {
-      hipLaunchKernelGGL(col_dot_reduce_wg_kernel, dim3(s), dim3(256), 0, str, pqpart, pqb, s,
-                         pqsum);
-      SP_LAUNCH("col_dot_reduce_wg_kernel");
-      pqin = pqsum;
-      pqn = 1;
-    } else if (pqb > 0) {
-      hipLaunchKernelGGL(col_dot_reduce_kernel, dim3((s + 3) / 4), dim3(256), 0, str, pqpart, pqb,
-                         1, s, pqsum);
-      SP_LAUNCH("col_dot_reduce_kernel");
-      pqin = pqsum;
-      pqn = 1;
-    } else {
-      hipLaunchKernelGGL(col_dot_partial_kernel, dim3(NBLK, 1), dim3(256), 0, str, Pd, (int64_t)0,
-                         Qd, n, s, pqpart);
-      SP_LAUNCH("col_dot_partial_kernel");
-    }
-    hipLaunchKernelGGL(ms_rmfma_kernel, dim3(MS_RB), dim3(256), 0, str, Bd, Rcur, Qd, st2[itx & 1],
-                       pqin, pqn, n, s, nbd, partial);
-    SP_LAUNCH("ms_rmfma_kernel");
-    hipLaunchKernelGGL(col_dot_reduce_kernel, dim3((ne + 3) / 4), dim3(256), 0, str, partial, MS_RB,
-                       1, ne, brd);
-    SP_LAUNCH("col_dot_reduce_kernel");
-    // the per-shift scalars and p = r + beta p in one launch (ms_tail_kernel)
-    hipLaunchKernelGGL(ms_tail_kernel, dim3((unsigned)((ns + 1023) / 1024)), dim3(256), 0, str,
-                       st2[itx & 1], st2[(itx + 1) & 1], (const double*)brd, dshift, S, s, nbd,
-                       rtol * rtol, Pd, (const double*)Rcur, n, pin_out);
-    SP_LAUNCH("ms_tail_kernel");
-    return 0;
-  };
-  // Iterations run in batches between host reads of the stop flags. Each batch's end
-  // state (active flags, the negative-curvature flag, r . r) is copied into pinned
-  // memory behind it and read while the NEXT batch is already queued, so the device
-  // does not wait for the host between batches (a synchronous poll every 8
-  // iterations drained the queue). The next batch's size comes from the residuals'
-  // decay: the iterations the slowest active column still needs to reach rtol at its
-  // rate since the previous read, beyond what is queued (at most MS_BATCH); when the
-  // queued iterations should suffice, the host waits for them instead of queueing
-  // more. Iterations past a column's convergence leave it unchanged (zero steps).
-  // (A batch captured as a HIP graph and relaunched measured the same as launching
-  // it: the per-kernel cost is on the device.)
-  using PinSlot = MsPin;
-  if (!sp->ms_pin) {
-    // coherent: the batch's last ms_tail_kernel stores the end state into it directly
-    SP_TRY(hipHostMalloc(reinterpret_cast<void**>(&sp->ms_pin), 2 * sizeof(PinSlot),
-                         hipHostMallocCoherent | hipHostMallocMapped));
-    for (hipEvent_t* e : {&sp->ms_ev[0], &sp->ms_ev[1]})
-      SP_TRY(hipEventCreateWithFlags(e, hipEventDisableTiming));
-  }
-  PinSlot* pin = reinterpret_cast<PinSlot*>(sp->ms_pin);
-  PinSlot* pin_dev = nullptr;
-  SP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&pin_dev), sp->ms_pin, 0));
-  std::vector<double> hbn2(s);
-  {
-    bool any = false;
-    SP_TRY(hipMemcpyAsync(hbn2.data(), st.bn2, sizeof(double) * s, hipMemcpyDeviceToHost, str));
-    rc = poll(&any);
-    if (rc) return rc;
-    if (!any) maxiter = 0;
-  }
-  int slot_it[2] = {0, 0};
-  int it_done = -1;   // the iterations after which every column had stopped
-  std::vector<double> rr_seen(s, -1.0);
-  int it_seen = 0;
-  bool prev = false;   // a previous batch's slot awaits reading
-  int nb = MS_BATCH;
-  int k = 0;
-  // read slot q: 0 = columns remain, 1 = all stopped, < 0 / > 0 an error code
-  auto read_slot = [&](int q, int* remaining_after) -> int {
-    SP_TRY(hipEventSynchronize(sp->ms_ev[q]));
-    if (pin[q].flag) {
-      SP_TRY(hipStreamSynchronize(str));
-      return set_error(1, "multi-shift CG: p^T (K + min(eta) I) p <= 0 (not positive definite)");
-    }
-    bool any = false;
-    double need = 0.0;
-    const int at = slot_it[q];
-    for (int c = 0; c < s; ++c) {
-      if (!pin[q].act[c]) continue;
-      any = true;
-      const double r1 = pin[q].rr[c], r0 = rr_seen[c], target = rtol * rtol * hbn2[c];
-      double m = (double)MS_BATCH;
-      if (r0 > 0.0 && r1 > 0.0 && r1 < r0 && at > it_seen && target > 0.0)
-        m = std::log(target / r1) / (std::log(r1 / r0) / (double)(at - it_seen));
-      need = std::max(need, m);
-      rr_seen[c] = r1;
-    }
-    it_seen = at;
-    *remaining_after = (int)std::ceil(at + need) - it;   // beyond the queued iterations
-    if (!any) it_done = at;
-    return any ? 0 : 2;
-  };
-  while (it < maxiter) {
-    nb = std::max(1, std::min(nb, maxiter - it));
-    const int q = k & 1;
-    for (int i = 0; i < nb; ++i, ++it)
-      if ((rc = iterate(it, i + 1 == nb ? pin_dev + q : nullptr))) return rc;
-    SP_TRY(hipEventRecord(sp->ms_ev[q], str));
-    slot_it[q] = it;
-    ++k;
-    int rem = MS_BATCH;
-    if (prev) {
-      const int r = read_slot(q ^ 1, &rem);
-      if (r == 2) break;   // stopped before the queued batch (which then ran as zero steps)
-      if (r) return r;
-    }
-    prev = true;
-    if (rem <= 0) {
-      // the queued iterations should reach rtol: wait for them rather than queue more
-      int rem2 = 0;
-      const int r = read_slot(q, &rem2);
-      if (r == 2) break;
-      if (r) return r;
-      prev = false;
-      rem = rem2;
-    }
-    nb = std::max(1, std::min(MS_BATCH, rem));
-  }
-  {
-    bool any = false;
-    rc = poll(&any);
-    if (rc) return rc;
-    sp->last_converged = any ? 0 : 1;
-  }
-  std::vector<double> hg((size_t)S * nbd * s);
-  SP_TRY(hipMemcpyAsync(hg.data(), st.g, sizeof(double) * hg.size(), hipMemcpyDeviceToHost, str));
-  SP_TRY(hipStreamSynchronize(str));
-  for (int j = 0; j < S; ++j)
-    for (int a = 0; a < nrhs; ++a)
-      for (int c = 0; c < nsub; ++c)
-        G[((size_t)j * nrhs + a) * nsub + c] = hg[((size_t)j * nbd + a) * s + c];
-  if (iterations) *iterations = it_done >= 0 ? it_done : it;
-  return 0;
+  return msgram_cg2(sp, etas, neta, rhs, ld, nrhs, c_lo, c_hi, rtol, maxiter, G, iterations);
 }
 
 int gpmi_sp_msgram(gpmi_sp* sp, const double* etas, int neta, const double* rhs, int64_t ld,

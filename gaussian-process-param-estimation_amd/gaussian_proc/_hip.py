@@ -53,7 +53,6 @@ SIGNATURES = {
     'gpmi_op_set_timing': (ctypes.c_int, [c_op_p, ctypes.c_int]),
     'gpmi_op_last_timing': (ctypes.c_int, [c_op_p, c_double_p, c_int_p, c_double_p,
                                            c_double_p, c_double_p]),
-    'gpmi_op_set_lookahead': (ctypes.c_int, [c_op_p, ctypes.c_int]),
     'gpmi_op_set_outer': (ctypes.c_int, [c_op_p, ctypes.c_int]),
     'gpmi_last_assembly_ms': (ctypes.c_int, [c_double_p]),
     'gpmi_matern_values': (ctypes.c_int, [ctypes.c_int, c_double_p, c_i64, ctypes.c_double,
@@ -316,9 +315,6 @@ class Operator(object):
               'gpmi_op_last_timing')
         return dict(syrk_ms=ms.value, syrk_launches=nl.value, syrk_flops=fl.value,
                     total_ms=tot.value, syrk_busy_ms=busy.value)
-
-    def set_lookahead(self, enable):
-        check(self.lib.gpmi_op_set_lookahead(self.h, int(bool(enable))), 'gpmi_op_set_lookahead')
 
     def set_outer(self, s):
         check(self.lib.gpmi_op_set_outer(self.h, int(s)), 'gpmi_op_set_outer')

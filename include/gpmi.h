@@ -125,13 +125,6 @@ int gpmi_op_set_timing(gpmi_op* op, int enable);
 int gpmi_op_last_timing(gpmi_op* op, double* syrk_ms, int* syrk_launches,
                         double* syrk_flops, double* total_ms, double* syrk_busy_ms);
 
-/* Look-ahead (default off): the latency-bound factorization of outer panel
- * k + 1 runs on a second, high-priority HIP stream while the bulk trailing
- * update of panel k runs on the op's stream. 0 = one stream, in order.
- * (Measured: no gain on MI355X, the bulk SYRK's LDS keeps the diagonal-block
- * kernel from co-residing) */
-int gpmi_op_set_lookahead(gpmi_op* op, int enable);
-
 /* Outer panel width in 128-column tiles (trailing update depth = 128*S, 1..32,
  * default 16); each outer panel is factorized recursively (halves). */
 int gpmi_op_set_outer(gpmi_op* op, int s);

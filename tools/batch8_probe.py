@@ -25,16 +25,14 @@ n = X.shape[0]
 fl = n ** 3 / 3.0
 for nb in (8, 16):
     for outer in (8, 12, 16, 24):
-        for la in (0, 1):
-            op.op.set_outer(outer)
-            op.op.set_lookahead(la)
-            op.loglik_terms(etas[:nb], X, z)
-            ts = []
-            for r in range(3):
-                t0 = time.perf_counter()
-                op.loglik_terms(etas[8 * r:8 * r + nb], X, z)
-                ts.append(time.perf_counter() - t0)
-            t = min(ts)
-            print('batch %2d outer %2d la %d groups %s: %.1f ms  %.2f evals/s  %.3f of 78.6 (n^3/3)'
-                  % (nb, outer, la, os.environ.get('GPMI_GROUPS', 'auto'), t * 1e3, nb / t,
-                     nb * fl / t / 78.6e12), flush=True)
+        op.op.set_outer(outer)
+        op.loglik_terms(etas[:nb], X, z)
+        ts = []
+        for r in range(3):
+            t0 = time.perf_counter()
+            op.loglik_terms(etas[8 * r:8 * r + nb], X, z)
+            ts.append(time.perf_counter() - t0)
+        t = min(ts)
+        print('batch %2d outer %2d groups %s: %.1f ms  %.2f evals/s  %.3f of 78.6 (n^3/3)'
+              % (nb, outer, os.environ.get('GPMI_GROUPS', 'auto'), t * 1e3, nb / t,
+                 nb * fl / t / 78.6e12), flush=True)
