@@ -410,7 +410,7 @@ def sparse_measure(args, config, world, rank, local, dist, torch, cpu, exact, de
     also runs the exact 'cholesky' method on a dense copy (cfg 4: 34 GB)."""
     from gaussian_proc import generate_correlation, _data
     from gaussian_proc._mixed_correlation import MixedCorrelation
-    from gaussian_proc._likelihood._direct_likelihood import _lp_from_terms
+    from gaussian_proc._likelihood._direct_likelihood import _lp_from_terms_batch
     from gaussian_proc.sweep import slq_gram_sweep, shard
     npts, dim, rho, nu, dens, nprobe, steps, neta = SPARSE_CONFIGS[config]
     points = _data.generate_points(npts, dim, True)
@@ -449,9 +449,10 @@ def sparse_measure(args, config, world, rank, local, dist, torch, cpu, exact, de
         rows = numpy.zeros((per, 3))
         if hi > lo:
             holder['cg_iters'] = op.sop.last_cg_iterations
-            for i, e in enumerate(etas[lo:hi]):
-                rows[i] = [e, curves['logdet'][lo + i],
-                           _lp_from_terms(n, m, 1.0, curves['logdet'][lo + i], Gs[i])]
+            ld = curves['logdet'][lo:hi]
+            rows[:hi - lo, 0] = etas[lo:hi]
+            rows[:hi - lo, 1] = ld
+            rows[:hi - lo, 2] = _lp_from_terms_batch(n, m, 1.0, ld, Gs)
         return gather_rows(rows, world, dist, torch)
 
     for _ in range(args.warmup):
@@ -459,9 +460,6 @@ def sparse_measure(args, config, world, rank, local, dist, torch, cpu, exact, de
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
-    # in-step SpMM timing: a HIP event pair around every SpMM launch of the timed
-    # steps, on the stream it runs on (the Lanczos's and the multi-shift CG's)
-    op.sop.set_timing(True)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         last = step()
@@ -469,9 +467,21 @@ def sparse_measure(args, config, world, rank, local, dist, torch, cpu, exact, de
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    dt = max_over_ranks(dt, world, dist, torch)
+    # in-step SpMM timing: the same steps again, every SpMM launch timed by a HIP
+    # event pair on the stream it runs on (the window SpMM's in its dispatch packet),
+    # beside the other stream's work as in the timed steps; kept out of the timed
+    # steps above so that `value` carries no instrumentation
+    isteps = max(3, min(args.steps, 10))
+    op.sop.set_timing(True)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for _ in range(isteps):
+        step()
+    torch.cuda.synchronize()
+    dt_instr = (time.perf_counter() - t1) / isteps
     spmm_in_step = op.sop.spmm_timing()
     op.sop.set_timing(False)
-    dt = max_over_ranks(dt, world, dist, torch)
     # imate's `orthogonalize` option: this rank's probe block by the plain three-term
     # recurrence (0, imate's default, what the step uses) against full
     # reorthogonalisation (-1, DCGS2), Lanczos alone, and the two logdet curves in
@@ -553,9 +563,11 @@ def sparse_measure(args, config, world, rank, local, dist, torch, cpu, exact, de
                          'traffic_source': sp_tsrc,
                          'kernel': '%s (s=%d columns)' % (sp_kernel, s_blk),
                          'avg_launch_ms': round(ms, 4),
-                         'avg_launch_ms_source': 'HIP events around each SpMM launch of the '
-                                                 'timed steps (%d launches at s=%d)'
-                                                 % (n_launch, s_blk),
+                         'avg_launch_ms_source': 'HIP events of each SpMM launch of %d '
+                                                 'instrumented steps identical to the timed '
+                                                 'ones (%d launches at s=%d; %.3f ms per '
+                                                 'instrumented step)'
+                                                 % (isteps, n_launch, s_blk, dt_instr * 1e3),
                          'isolated_ms': round(ms_iso, 4),
                          'algorithmic_bytes_per_launch': alg_bytes,
                          'in_step_by_width': by_width,
@@ -786,7 +798,7 @@ def band_mode(args, D, X, z, world, rank, dist, torch, ld_ref=None):
     The reduction is the operator's one-time setup: every rank repeats it for
     its own K (it does not shard); only the per-eta banded Cholesky does."""
     from gaussian_proc._mixed_correlation import MixedCorrelation
-    from gaussian_proc._likelihood._direct_likelihood import _lp_from_terms
+    from gaussian_proc._likelihood._direct_likelihood import _lp_from_terms_batch
     n, m = X.shape
     op = MixedCorrelation(D, imate_method='eigenvalue')
     b = op.band()
@@ -801,7 +813,7 @@ def band_mode(args, D, X, z, world, rank, dist, torch, ld_ref=None):
         if record:
             for k, v in b.last_timing().items():
                 acc[k] += v
-        lp = numpy.array([_lp_from_terms(n, m, 1.0, l, g) for l, g in zip(ld, G)])
+        lp = _lp_from_terms_batch(n, m, 1.0, ld, G)
         return gather_rows(numpy.stack([etas, ld, lp], axis=1), world, dist, torch), own, \
             etas.size
 
@@ -984,7 +996,7 @@ def dense_nu25_mode(args, op, X, z, steps=3):
     headline, with the logdet / direct lp errors against the reference's
     N = 16384 nu = 2.5 values (tests/golden/cfg3_nu25.json). The Cholesky's cost
     does not depend on nu; this line shows it."""
-    from gaussian_proc._likelihood._direct_likelihood import _lp_from_terms
+    from gaussian_proc._likelihood._direct_likelihood import _lp_from_terms_batch
     n, m = X.shape
     etas = numpy.logspace(-3, 3, args.eta_total)
     op.loglik_terms(etas, X, z)
@@ -992,7 +1004,7 @@ def dense_nu25_mode(args, op, X, z, steps=3):
     t0 = time.perf_counter()
     for _ in range(steps):
         ld, G = op.loglik_terms(etas, X, z)
-        [_lp_from_terms(n, m, 1.0, l, g) for l, g in zip(ld, G)]
+        _lp_from_terms_batch(n, m, 1.0, ld, G)
     torch_sync()
     dt = time.perf_counter() - t0
     ld_err, lp_err = golden_errors(lambda e: op.loglik_terms(e, X, z), 2.5, n, m)
@@ -1225,7 +1237,7 @@ def main():
 
     from gaussian_proc import generate_correlation, _data
     from gaussian_proc._mixed_correlation import MixedCorrelation
-    from gaussian_proc._likelihood._direct_likelihood import _lp_from_terms
+    from gaussian_proc._likelihood._direct_likelihood import _lp_from_terms, _lp_from_terms_batch
 
     points = _data.generate_points(args.grid, 2, True)
     z = _data.generate_data(points, 0.2)
@@ -1251,7 +1263,7 @@ def main():
             t = op.op.last_timing()
             for k in ('syrk_ms', 'syrk_busy_ms', 'syrk_flops', 'syrk_launches', 'total_ms'):
                 timing_acc[k] += t[k]
-        lp = numpy.array([_lp_from_terms(n, m, 1.0, l, g) for l, g in zip(ld, G)])
+        lp = _lp_from_terms_batch(n, m, 1.0, ld, G)
         return gather_rows(numpy.stack([etas, ld, lp], axis=1), world, dist, torch)
 
     for s in range(args.warmup):

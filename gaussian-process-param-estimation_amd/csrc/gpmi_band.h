@@ -64,6 +64,8 @@ __global__ void tn_partial_kernel(const double* P1, int64_t ld1, const double* P
 __global__ void tn_reduce_kernel(const double* part, int nch, double* out, double scale,
                                  const int* only_if);
 __global__ void tbuild_kernel(const double* VtV, const double* tau, double* T, const int* only_if);
+__global__ void t_fallback_kernel(const double* V, int64_t ldv, int m, const double* tau,
+                                  double* VtV, double* T, const int* only_if);
 __global__ void symm_kernel(const double* A, int64_t lda, const double* U, int64_t ldu, int tr0,
                             int mt, int chunk, double* Xp);
 __global__ void psum_kernel(const double* Xp, int nch, double* X);

@@ -438,14 +438,10 @@ __global__ __launch_bounds__(256) void tn_reduce_kernel(const double* __restrict
 // Lm^-1 reuses the LDS block inverse of the Cholesky kernels (16 x 16 diagonal
 // blocks by forward substitution, then MFMA column blocks). An identity reflector
 // (tau_c = 0) is decoupled: unit diagonal, no coupling, and T_cc = 0.
-__global__ __launch_bounds__(256) void tbuild_kernel(const double* __restrict__ VtV,
-                                                     const double* __restrict__ tau,
-                                                     double* __restrict__ T,
-                                                     const int* __restrict__ only_if) {
-  __shared__ double Ls[TS * DL];
-  __shared__ double Aux[TS * RLD];
-  __shared__ double stau[TS];
-  if (only_if && *only_if == 0) return;
+__device__ __forceinline__ void tbuild_body(const double* __restrict__ VtV,
+                                            const double* __restrict__ tau,
+                                            double* __restrict__ T, double* Ls, double* Aux,
+                                            double* stau) {
   const int t = threadIdx.x;
   if (t < TS) stau[t] = tau[t];
   __syncthreads();
@@ -468,6 +464,45 @@ __global__ __launch_bounds__(256) void tbuild_kernel(const double* __restrict__ 
     if (r <= c && !(r == c && stau[c] == 0.0)) v = Ls[c * DL + r];
     T[e] = v;
   }
+}
+
+__global__ __launch_bounds__(256) void tbuild_kernel(const double* __restrict__ VtV,
+                                                     const double* __restrict__ tau,
+                                                     double* __restrict__ T,
+                                                     const int* __restrict__ only_if) {
+  __shared__ double Ls[TS * DL];
+  __shared__ double Aux[TS * RLD];
+  __shared__ double stau[TS];
+  if (only_if && *only_if == 0) return;
+  tbuild_body(VtV, tau, T, Ls, Aux, stau);
+}
+
+// T of a CholeskyQR panel that fell back to the Householder panel (flag set), in ONE
+// workgroup: V^T V over the m rows (the tn_partial products chunk by chunk into one
+// accumulator), then tbuild_body. Slow (one CU), but it runs only for a failed
+// panel; for every other panel it is one launch that exits at once (round 5: it
+// replaces the three guarded launches tn_partial / tn_reduce / tbuild, whose ~15 us
+// of no-op launches on the side stream delayed X T of the chain-bound late panels).
+__global__ __launch_bounds__(256) void t_fallback_kernel(const double* __restrict__ V,
+                                                         int64_t ldv, int m,
+                                                         const double* __restrict__ tau,
+                                                         double* __restrict__ VtV,
+                                                         double* __restrict__ T,
+                                                         const int* __restrict__ only_if) {
+  __shared__ double Ls[TS * DL];   // also the product's LDS stages (4 GSTAGE <= TS DL)
+  __shared__ double Aux[TS * RLD];
+  __shared__ double stau[TS];
+  static_assert(4 * GSTAGE <= TS * DL, "t_fallback_kernel: staging exceeds Ls");
+  if (*only_if == 0) return;
+  d4 acc[4][4];
+  zero_tile(acc);
+  for (int i0 = 0; i0 < m; i0 += TN_CH)
+    gemm_tile<KSLOW, KSLOW, false>(V + (int64_t)i0 * ldv, ldv, V + (int64_t)i0 * ldv, ldv,
+                                   min(TN_CH, m - i0), Ls, acc);
+  store_tile(VtV, TS, acc, 1.0);
+  __threadfence_block();
+  __syncthreads();
+  tbuild_body(VtV, tau, T, Ls, Aux, stau);
 }
 
 // Split-K symmetric product: Xp[il][ch] = sum_{J in chunk ch} A22_IJ V_J, with

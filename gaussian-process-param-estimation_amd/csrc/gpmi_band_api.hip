@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -450,6 +451,7 @@ int band_reduce_pass(gpmi_band* b, const double* K, const std::vector<double>* y
   BD_TRY(hipMemsetAsync(b->err, 0, 16, s));
   if (mode == 0) BD_TRY(hipMemsetAsync(b->cqflag, 0, sizeof(int) * 8 * nt, s));
   BD_TRY(hipEventRecord(b->ev0, s));
+  const auto host_t0 = std::chrono::steady_clock::now();
   if (yh) {
     BD_TRY(hipMemcpyAsync(b->Y, yh->data(), sizeof(double) * yh->size(), hipMemcpyHostToDevice,
                           b->side));
@@ -480,16 +482,22 @@ int band_reduce_pass(gpmi_band* b, const double* K, const std::vector<double>* y
     // T from V^T V on the side stream, beside the SYMM (which needs only V)
     BD_TRY(hipEventRecord(b->ev_v, s));
     BD_TRY(hipStreamWaitEvent(b->side, b->ev_v, 0));
-    // (a CholeskyQR panel's T comes from cq_t_kernel: these run only if it fell back)
-    const int* only_if = b->t_from_q[j] ? b->cqflag + 8 * j + 4 : nullptr;
-    hipLaunchKernelGGL(tn_partial_kernel, dim3(nch), dim3(256), 0, b->side, Ur + TS,
-                       (int64_t)BAND_ULD, Ur + TS, (int64_t)BAND_ULD, m, b->tnp2, only_if);
-    BD_LAUNCH("tn_partial_kernel");
-    hipLaunchKernelGGL(tn_reduce_kernel, dim3(TS * TS / 64), dim3(256), 0, b->side, b->tnp2,
-                       nch, b->VtV, 1.0, only_if);
-    BD_LAUNCH("tn_reduce_kernel");
-    hipLaunchKernelGGL(tbuild_kernel, dim3(1), dim3(256), 0, b->side, b->VtV, tau, T, only_if);
-    BD_LAUNCH("tbuild_kernel");
+    if (b->t_from_q[j]) {
+      // a CholeskyQR panel's T came from cq_t_kernel; only if it fell back does this
+      // one-workgroup launch form it (it exits at once otherwise)
+      hipLaunchKernelGGL(t_fallback_kernel, dim3(1), dim3(256), 0, b->side, Ur + TS,
+                         (int64_t)BAND_ULD, m, tau, b->VtV, T, b->cqflag + 8 * j + 4);
+      BD_LAUNCH("t_fallback_kernel");
+    } else {
+      hipLaunchKernelGGL(tn_partial_kernel, dim3(nch), dim3(256), 0, b->side, Ur + TS,
+                         (int64_t)BAND_ULD, Ur + TS, (int64_t)BAND_ULD, m, b->tnp2, nullptr);
+      BD_LAUNCH("tn_partial_kernel");
+      hipLaunchKernelGGL(tn_reduce_kernel, dim3(TS * TS / 64), dim3(256), 0, b->side, b->tnp2,
+                         nch, b->VtV, 1.0, nullptr);
+      BD_LAUNCH("tn_reduce_kernel");
+      hipLaunchKernelGGL(tbuild_kernel, dim3(1), dim3(256), 0, b->side, b->VtV, tau, T, nullptr);
+      BD_LAUNCH("tbuild_kernel");
+    }
     b->t_from_q[j] = 0;
     BD_TRY(hipEventRecord(b->ev_t, b->side));
     if (yh) {
@@ -534,38 +542,40 @@ int band_reduce_pass(gpmi_band* b, const double* K, const std::vector<double>* y
       BD_TRY(hipEventRecord(b->ev_col, s));
       BD_TRY(hipStreamWaitEvent(b->s_pan, b->ev_col, 0));
       const bool pipe = mode == 0;
-      bool guard = false;
-      int rc = panel_qr(b, j + 1, b->s_pan, mode, pipe ? &guard : nullptr);
-      if (rc) return rc;
       const int rest = (mt - 1) * mt / 2;
       const int la_free = mt < LA_LATE_MT ? LA_FREE_LATE : LA_FREE;
       const int nmain = std::min(rest, std::max(1, b->ncu - la_free));
       int* tcnt = pipe ? b->cqflag + 8 * j + 6 : nullptr;
-      if (tcnt && rest > nmain) {
-        // the chain's CUs join the update once the chain ends (tickets of tcnt;
-        // 139.2 against 141.0 ms at N = 16384; launched only from panels whose
-        // update outlasts the chain: no difference)
-        hipLaunchKernelGGL(syr2k_pipe_kernel, dim3(std::min(la_free, rest - nmain)), dim3(256),
-                           0, b->s_pan, b->Ab, np, b->U, (int64_t)BAND_ULD, j + 1, mt, tcnt,
-                           nmain, 1);
-        BD_LAUNCH("syr2k_pipe_kernel");
-      }
-      BD_TRY(hipEventRecord(b->ev_pan, b->s_pan));
+      // The rest of the update on s_pan, panel j + 1's QR on s right behind the tile
+      // column it needs (round 5: the chain used to run on s_pan between two cross-stream
+      // waits, ~12 us before it and ~10 us after it on every chain-bound late panel)
       if (pipe) {
         // one SYR2K workgroup per CU on all but la_free CUs, which the chain (its
         // single-workgroup kernels need a whole CU) has to itself
-        hipLaunchKernelGGL(syr2k_pipe_kernel, dim3(nmain), dim3(256), 0, s, b->Ab, np, b->U,
-                           (int64_t)BAND_ULD, j + 1, mt, tcnt, nmain, 0);
+        hipLaunchKernelGGL(syr2k_pipe_kernel, dim3(nmain), dim3(256), 0, b->s_pan, b->Ab, np,
+                           b->U, (int64_t)BAND_ULD, j + 1, mt, tcnt, nmain, 0);
         BD_LAUNCH("syr2k_pipe_kernel");
       } else {
         // the Householder panel (its workgroups must be co-resident) beside a capped
         // grid; la_grid 0: leave exactly the panel's workgroup count of CUs free
         // (measured: slower than a fixed 128-workgroup cap at N = 16384, 302 vs 262 ms)
         const int cap = b->la_grid > 0 ? b->la_grid : std::max(64, b->ncu - next_g);
-        hipLaunchKernelGGL(syr2k_rest_kernel, dim3(std::min(rest, cap)), dim3(256), 0, s, b->Ab,
-                           np, b->U, (int64_t)BAND_ULD, j + 1,
+        hipLaunchKernelGGL(syr2k_rest_kernel, dim3(std::min(rest, cap)), dim3(256), 0, b->s_pan,
+                           b->Ab, np, b->U, (int64_t)BAND_ULD, j + 1,
                            mt, b->rorder ? b->rorder + b->rorder_off[mt - 1] : nullptr);
         BD_LAUNCH("syr2k_rest_kernel");
+      }
+      BD_TRY(hipEventRecord(b->ev_pan, b->s_pan));
+      bool guard = false;
+      int rc = panel_qr(b, j + 1, s, mode, pipe ? &guard : nullptr);
+      if (rc) return rc;
+      if (tcnt && rest > nmain) {
+        // the chain's CUs join the update once the chain ends (tickets of tcnt;
+        // 139.2 against 141.0 ms at N = 16384; launched only from panels whose
+        // update outlasts the chain: no difference)
+        hipLaunchKernelGGL(syr2k_pipe_kernel, dim3(std::min(la_free, rest - nmain)), dim3(256),
+                           0, s, b->Ab, np, b->U, (int64_t)BAND_ULD, j + 1, mt, tcnt, nmain, 1);
+        BD_LAUNCH("syr2k_pipe_kernel");
       }
       BD_TRY(hipStreamWaitEvent(s, b->ev_pan, 0));
       if (guard) {
@@ -593,6 +603,10 @@ int band_reduce_pass(gpmi_band* b, const double* K, const std::vector<double>* y
     BD_LAUNCH("cq_top_kernel");
   }
   BD_TRY(hipEventRecord(b->ev1, s));
+  // host time to enqueue the whole reduction (GPMI_BAND_TRACE: against its device time,
+  // printed below; a device span not far above it would mean the host's launches bound it)
+  const double host_enqueue_ms =
+      std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - host_t0).count();
   int herr = 0;
   std::vector<int> hflag(mode == 0 ? 8 * nt : 0);
   BD_TRY(hipMemcpyAsync(&herr, b->err, sizeof(int), hipMemcpyDeviceToHost, s));
@@ -610,6 +624,9 @@ int band_reduce_pass(gpmi_band* b, const double* K, const std::vector<double>* y
   float ms = 0.f;
   BD_TRY(hipEventElapsedTime(&ms, b->ev0, b->ev1));
   b->reduce_ms = ms;
+  if (std::getenv("GPMI_BAND_TRACE"))
+    fprintf(stderr, "[gpmi band] reduction %.3f ms on the device, enqueued in %.3f ms\n", ms,
+            host_enqueue_ms);
   return 0;
 }
 

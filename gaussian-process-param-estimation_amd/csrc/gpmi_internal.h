@@ -103,6 +103,7 @@ struct MsPin {
   int flag;
   int pad;
   double rr[MS_MAXS];
+  double bn2[MS_MAXS];   // ||b_c||^2, written by ms_init_kernel into both slots
 };
 
 // Scatter a sparse operator's CSR (original point order) into a zeroed dense

@@ -1394,12 +1394,9 @@ __global__ __launch_bounds__(256) void ms_cg2_update_kernel(
   }
   __syncthreads();
   if (t == 0) {
-    bool before = false, after = false;
-    for (int c = 0; c < s; ++c) {
-      before = before || cur.active[c];
-      after = after || sup[c];
-    }
-    if (before && !after && sh.it_stop[0] < 0) sh.it_stop[0] = k;
+    bool after = false;
+    for (int c = 0; c < s; ++c) after = after || sup[c];
+    if (!after && sh.it_stop[0] < 0) sh.it_stop[0] = k;   // the first all-stopped iteration
   }
   if (pin && t < s) {   // the batch's end state for the host (pinned, device-mapped)
     pin->rr[t] = cur.active[t] ? sd[s + t] : cur.rr[t];
@@ -1475,7 +1472,7 @@ __global__ __launch_bounds__(256) void ms_dots2_kernel(const double* __restrict_
 // Initial scalar state from BR0 = B^T b (= b . p_0 for every shift) and ||b||^2:
 // zeta = 1, G = 0, alpha_{-1} = 1 (a, a_prev), beta_{-1} = 0, active = ||b|| > 0.
 __global__ void ms_init_kernel(MsScal st, MsShift sh, const double* __restrict__ partial,
-                               int nblk, int S, int s, int nb) {
+                               int nblk, int S, int s, int nb, MsPin* __restrict__ pin2) {
   __shared__ double br[MS_MAXS * MS_MAXS + MS_MAXS];
   const int ne = nb * s + s;
   {
@@ -1504,6 +1501,8 @@ __global__ void ms_init_kernel(MsScal st, MsShift sh, const double* __restrict__
     st.a_prev[t] = 1.0;
     st.beta[t] = 0.0;
     st.active[t] = br[nb * s + t] > 0.0 ? 1 : 0;
+    pin2[0].bn2[t] = br[nb * s + t];   // the host's stop-rate targets, no readback
+    pin2[1].bn2[t] = br[nb * s + t];
   }
   if (t == 0) {
     sh.flags[0] = 0;

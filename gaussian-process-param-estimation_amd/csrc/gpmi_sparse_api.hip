@@ -92,7 +92,7 @@ __global__ void lanczos_scalar_kernel(const double*, const double*, const double
 void launch_ms_dots(const double* B, const double* R, int64_t n, int s, double* partial, int nblk,
                     hipStream_t st, int sa);
 __global__ void rows_gather_kernel(const double*, int, const int*, int64_t, int, double*);
-__global__ void ms_init_kernel(MsScal, MsShift, const double*, int, int, int, int);
+__global__ void ms_init_kernel(MsScal, MsShift, const double*, int, int, int, int, MsPin*);
 __global__ void ms_cg2_update_kernel(const double*, double*, const double*, double*,
                                      MsScal, MsScal, MsShift, const double*, double*,
                                      const double*, int, int, int, double, int, int64_t, MsPin*);
@@ -1434,8 +1434,18 @@ static int msgram_cg2(gpmi_sp* sp, const double* etas, int neta, const double* r
   }
   launch_ms_dots(Bd, Rd, n, s, ipart, MS_NBLK, str, nbd);
   SP_LAUNCH("ms_dots_partial_kernel");
+  if (!sp->ms_pin) {
+    // coherent: the batch's last update kernel stores the end state into it directly
+    SP_TRY(hipHostMalloc(reinterpret_cast<void**>(&sp->ms_pin), 2 * sizeof(MsPin),
+                         hipHostMallocCoherent | hipHostMallocMapped));
+    for (hipEvent_t* e : {&sp->ms_ev[0], &sp->ms_ev[1]})
+      SP_TRY(hipEventCreateWithFlags(e, hipEventDisableTiming));
+  }
+  MsPin* pin = reinterpret_cast<MsPin*>(sp->ms_pin);
+  MsPin* pin_dev = nullptr;
+  SP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&pin_dev), sp->ms_pin, 0));
   hipLaunchKernelGGL(ms_init_kernel, dim3(1), dim3(1024), 0, str, sc[0], sh, ipart, MS_NBLK, S, s,
-                     nbd);
+                     nbd, pin_dev);
   SP_LAUNCH("ms_init_kernel");
   int it = 0;
   // one iteration's launches on str (parity it & 1 picks the scalar and B^T r buffers)
@@ -1459,25 +1469,7 @@ static int msgram_cg2(gpmi_sp* sp, const double* etas, int neta, const double* r
     SP_LAUNCH("ms_cg2_update_kernel");
     return 0;
   };
-  if (!sp->ms_pin) {
-    SP_TRY(hipHostMalloc(reinterpret_cast<void**>(&sp->ms_pin), 2 * sizeof(MsPin),
-                         hipHostMallocCoherent | hipHostMallocMapped));
-    for (hipEvent_t* e : {&sp->ms_ev[0], &sp->ms_ev[1]})
-      SP_TRY(hipEventCreateWithFlags(e, hipEventDisableTiming));
-  }
-  MsPin* pin = reinterpret_cast<MsPin*>(sp->ms_pin);
-  MsPin* pin_dev = nullptr;
-  SP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&pin_dev), sp->ms_pin, 0));
-  std::vector<double> hbn2(s);
   std::vector<int> hact(s);
-  SP_TRY(hipMemcpyAsync(hbn2.data(), sh.bn2, sizeof(double) * s, hipMemcpyDeviceToHost, str));
-  SP_TRY(hipMemcpyAsync(hact.data(), sc[0].active, sizeof(int) * s, hipMemcpyDeviceToHost, str));
-  SP_TRY(hipStreamSynchronize(str));
-  {
-    bool any = false;
-    for (int c = 0; c < s; ++c) any = any || hact[c];
-    if (!any) maxiter = 0;
-  }
   // Iterations run in batches between host reads of the stop flags. Each batch's last
   // update kernel writes its end state (active flags, the negative-curvature flag,
   // gamma) into host-mapped pinned memory, read while the NEXT batch is already
@@ -1504,7 +1496,7 @@ static int msgram_cg2(gpmi_sp* sp, const double* etas, int neta, const double* r
     for (int c = 0; c < s; ++c) {
       if (!pin[qs].act[c]) continue;
       any = true;
-      const double r1 = pin[qs].rr[c], r0 = rr_seen[c], target = rtol * rtol * hbn2[c];
+      const double r1 = pin[qs].rr[c], r0 = rr_seen[c], target = rtol * rtol * pin[qs].bn2[c];
       double m = (double)MS_BATCH;
       if (r0 > 0.0 && r1 > 0.0 && r1 < r0 && at > it_seen && target > 0.0)
         m = std::log(target / r1) / (std::log(r1 / r0) / (double)(at - it_seen));

@@ -49,6 +49,23 @@ def _lp_from_terms(n, m, sigma, logdet_kn, G):
         - 0.5 * logdet_B - 0.5 * zMz
 
 
+def _lp_from_terms_batch(n, m, sigma, logdet_kn, G):
+    """_lp_from_terms for a batch: logdet_kn [E], G [E, m+1, m+1] -> lp [E] (the
+    same formula with numpy's stacked det / solve: one call per step of a sweep
+    instead of E)."""
+    G = numpy.asarray(G, dtype=float)
+    s2 = sigma ** 2
+    Gxx = G[:, :m, :m]
+    gxz = G[:, :m, m]
+    gzz = G[:, m, m]
+    logdet_S = n * numpy.log(s2) + numpy.asarray(logdet_kn, dtype=float)
+    logdet_B = numpy.log(numpy.linalg.det(Gxx / s2))
+    zMz = (gzz - numpy.einsum('ei,ei->e', gxz,
+                              numpy.linalg.solve(Gxx, gxz[:, :, None])[:, :, 0])) / s2
+    return -0.5 * (n - m) * numpy.log(2.0 * numpy.pi) - 0.5 * logdet_S \
+        - 0.5 * logdet_B - 0.5 * zMz
+
+
 def _lp_small_sigma(z, X, sigma0):
     """|sigma| < tol branch (_direct_likelihood.py:50-55, M_dot :325-328)."""
     n, m = X.shape

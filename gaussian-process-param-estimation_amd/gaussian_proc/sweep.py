@@ -212,6 +212,20 @@ def slq_sweep(K_mixed, etas, group=None, converge=('logdet',)):
     return {name: n * allq[:, f].mean(axis=0) for f, name in enumerate(names)}
 
 
+_CG_POOL = None
+
+
+def _cg_worker():
+    """The one host thread that runs the multi-shift CG beside the Lanczos
+    (slq_gram_sweep), created once per process: a thread pool made per sweep cost a
+    thread start and join in every likelihood step."""
+    global _CG_POOL
+    if _CG_POOL is None:
+        from concurrent.futures import ThreadPoolExecutor
+        _CG_POOL = ThreadPoolExecutor(1, thread_name_prefix='gpmi-msgram')
+    return _CG_POOL
+
+
 def slq_gram_sweep(K_mixed, etas, R, rtol=1e-6, group=None, split='columns'):
     """One sparse likelihood sweep: slq_sweep (the Lanczos of this rank's probe
     shard, all-gathered quadratures) and the multi-shift CG Gram blocks
@@ -237,7 +251,6 @@ def slq_gram_sweep(K_mixed, etas, R, rtol=1e-6, group=None, split='columns'):
     the right-hand sides, so on several ranks it can fire on one rank only: that
     rank still joins the collectives with an error flag, and every rank raises
     after them (as der1_sweep)."""
-    from concurrent.futures import ThreadPoolExecutor
     etas = numpy.atleast_1d(numpy.asarray(etas, dtype=float))
     if R is None:
         # the block K_mixed.sop.set_rhs made resident in HBM (no upload per sweep)
@@ -254,21 +267,21 @@ def slq_gram_sweep(K_mixed, etas, R, rtol=1e-6, group=None, split='columns'):
     by_cols = multi and split == 'columns'
     clo, chi, cper = shard(s, world, rank)
     err = None
-    with ThreadPoolExecutor(1) as ex:
-        if by_cols:
-            fut = (ex.submit(K_mixed.sop.msgram, etas, R2, rtol, None, (clo, chi))
-                   if chi > clo else None)
-        else:
-            fut = ex.submit(K_mixed.sop.msgram, etas[lo:hi], R2, rtol) if hi > lo else None
+    ex = _cg_worker()
+    if by_cols:
+        fut = (ex.submit(K_mixed.sop.msgram, etas, R2, rtol, None, (clo, chi))
+               if chi > clo else None)
+    else:
+        fut = ex.submit(K_mixed.sop.msgram, etas[lo:hi], R2, rtol) if hi > lo else None
+    try:
+        curves = slq_sweep(K_mixed, etas, group=group)
+    finally:
         try:
-            curves = slq_sweep(K_mixed, etas, group=group)
-        finally:
-            try:
-                G = fut.result() if fut is not None else None
-            except numpy.linalg.LinAlgError as e:
-                if not multi:
-                    raise
-                err, G = e, None
+            G = fut.result() if fut is not None else None
+        except numpy.linalg.LinAlgError as e:
+            if not multi:
+                raise
+            err, G = e, None
     if by_cols:
         # one row per column c (its G[:, :, c] flattened) plus an error flag, cper
         # rows per rank; the all-gather runs after the Lanczos's (collectives in the

@@ -26,7 +26,7 @@ def main(path):
         if 'nu25_check' in bm:
             print('band nu25', bm['nu25_check'])
         if 'der1_sweep' in bm:
-            print('der1', {k: bm['der1_sweep'][k] for k in ('device_ms', 'eigenvalues_ms_once')})
+            print('der1', {k: bm['der1_sweep'].get(k) for k in ('wall_ms', 'device_ms', 'selected_inversion_ms')})
     ds = d.get('dense_slq_mode')
     if ds:
         print('dense slq', {k: ds[k] for k in ds if k != 'dense_mm'})
