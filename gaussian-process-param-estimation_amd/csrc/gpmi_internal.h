@@ -95,7 +95,8 @@ struct MsShift {
   int* flags;      // [1] p^T (K + eta_0 I) p <= 0 in an active column
   int* it_stop;    // [1] the first iteration with no active column (-1: none yet)
 };
-constexpr int MS_UB = 512;      // vector blocks of ms_cg2_update_kernel
+constexpr int MS_UB = 512;      // vector blocks of ms_cg2_update_kernel (256 / 1024: cfg 5
+                                // 12.37 / 12.12 against 11.91 ms per step)
 constexpr int MS_DOT_BLK = 256; // blocks of ms_dots2_kernel (SpMM kinds without the epilogue)
 
 struct MsPin {
