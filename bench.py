@@ -115,9 +115,10 @@ def pmc_traffic_sparse(config, kernel='gpmi::csr_spmm_kernel', width=None):
     instances appear as 'void gpmi::name<12, 8, 4>') from the newest committed PMC
     summary of this sparse config that holds it (profiles/r*/pmc_traffic_{config}.json,
     FETCH_SIZE / WRITE_SIZE passes over `bench.py --config <config> --steps 1`;
-    FETCH_SIZE doubled as in pmc_traffic). Per launch: 'per_dispatch_last' where the
-    summary has it (the last K dispatches), else the mean over every dispatch of
-    that instance (the step's launches of that width and the reference check's)."""
+    FETCH_SIZE doubled as in pmc_traffic). Per launch: 'per_dispatch_timed' where the
+    summary has it (the dispatches of the timed step, between its timing marks),
+    else 'per_dispatch_last' (the last K dispatches), else the mean over every
+    dispatch of that instance."""
     import glob
     files = sorted(glob.glob(os.path.join(REPO, 'profiles', 'r*',
                                           'pmc_traffic_%s.json' % config)),
@@ -135,7 +136,7 @@ def pmc_traffic_sparse(config, kernel='gpmi::csr_spmm_kernel', width=None):
         k = next((v for key, v in kernels.items() if match(key)), None)
         if not k:
             continue
-        pd = k.get('per_dispatch_last', k['per_dispatch'])
+        pd = k.get('per_dispatch_timed', k.get('per_dispatch_last', k['per_dispatch']))
         return (2.0 * pd['FETCH_SIZE'] + pd['WRITE_SIZE']) * 1024.0, os.path.relpath(f, REPO)
     return None, None
 
@@ -457,6 +458,11 @@ def sparse_measure(args, config, world, rank, local, dist, torch, cpu, exact, de
 
     for _ in range(args.warmup):
         step()
+    # in-step SpMM timing over the timed steps themselves: every window SpMM launch
+    # stamps its span (earliest workgroup start to latest workgroup end, the device's
+    # constant wall clock, two vector atomics per workgroup) into a slot of its own;
+    # the window is marked in a kernel trace by two timing_mark_kernel launches
+    op.sop.set_timing(True)
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
@@ -467,21 +473,9 @@ def sparse_measure(args, config, world, rank, local, dist, torch, cpu, exact, de
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    dt = max_over_ranks(dt, world, dist, torch)
-    # in-step SpMM timing: the same steps again, every SpMM launch timed by a HIP
-    # event pair on the stream it runs on (the window SpMM's in its dispatch packet),
-    # beside the other stream's work as in the timed steps; kept out of the timed
-    # steps above so that `value` carries no instrumentation
-    isteps = max(3, min(args.steps, 10))
-    op.sop.set_timing(True)
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    for _ in range(isteps):
-        step()
-    torch.cuda.synchronize()
-    dt_instr = (time.perf_counter() - t1) / isteps
-    spmm_in_step = op.sop.spmm_timing()
     op.sop.set_timing(False)
+    spmm_in_step = op.sop.spmm_timing()
+    dt = max_over_ranks(dt, world, dist, torch)
     # imate's `orthogonalize` option: this rank's probe block by the plain three-term
     # recurrence (0, imate's default, what the step uses) against full
     # reorthogonalisation (-1, DCGS2), Lanczos alone, and the two logdet curves in
@@ -508,7 +502,7 @@ def sparse_measure(args, config, world, rank, local, dist, torch, cpu, exact, de
                       "three-term recurrence); -1 is full reorthogonalisation (DCGS2)"}
     # SpMM roofline from the timed steps: the width whose SpMM launches took the most
     # device time (the multi-shift CG's s = 12, or the Lanczos's s = 20), its average
-    # in-step HIP-event launch time; the same kernel isolated (50 back-to-back
+    # in-step launch span; the same kernel isolated (50 back-to-back
     # launches on a resident block) is reported beside it as isolated_ms
     nnz = op.sop.nnz
     s_blk = max(spmm_in_step, key=lambda w: spmm_in_step[w][1])
@@ -563,11 +557,9 @@ def sparse_measure(args, config, world, rank, local, dist, torch, cpu, exact, de
                          'traffic_source': sp_tsrc,
                          'kernel': '%s (s=%d columns)' % (sp_kernel, s_blk),
                          'avg_launch_ms': round(ms, 4),
-                         'avg_launch_ms_source': 'HIP events of each SpMM launch of %d '
-                                                 'instrumented steps identical to the timed '
-                                                 'ones (%d launches at s=%d; %.3f ms per '
-                                                 'instrumented step)'
-                                                 % (isteps, n_launch, s_blk, dt_instr * 1e3),
+                         'avg_launch_ms_source': 'device wall-clock span of each SpMM '
+                                                 'launch of the %d timed steps (%d launches '
+                                                 'at s=%d)' % (args.steps, n_launch, s_blk),
                          'isolated_ms': round(ms_iso, 4),
                          'algorithmic_bytes_per_launch': alg_bytes,
                          'in_step_by_width': by_width,

@@ -161,7 +161,7 @@ void grouped_order(int w, int t, int G, std::vector<uint32_t>* out) {
 }
 
 int launch_syrk(gpmi_op* op, hipStream_t st, int b0, int nb, int tc0, int w, int t, int p0,
-                int kdim) {
+                int kdim, bool from_k = false) {
   // b0: first batch member of the launch (a batch group's offset)
   const int tri = w * (w + 1) / 2;
   const int tiles = tri + (t - w) * w;
@@ -189,7 +189,8 @@ int launch_syrk(gpmi_op* op, hipStream_t st, int b0, int nb, int tc0, int w, int
   }
   hipLaunchKernelGGL(syrk_kernel, dim3(tiles, nb), dim3(256), 0, st,
                      op->A + (int64_t)b0 * op->n_pad * op->n_pad, (int64_t)op->n_pad,
-                     op->n_pad * op->n_pad, tc0, w, t, p0, kdim, order);
+                     op->n_pad * op->n_pad, tc0, w, t, p0, kdim, order,
+                     from_k ? op->K : nullptr, op->etas + b0, (int64_t)op->n);
   LAUNCH_CHECK("syrk_kernel");
   if (op->timing) {
     HIP_TRY(hipEventRecord(op->ev[evi + 1], st));
@@ -249,7 +250,9 @@ int schedule(gpmi_op* op, const BatchPtrs& P, int b0, int nb, hipStream_t main =
     if (rc) return rc;
     const int c1 = c0 + W;
     if (c1 >= nt) break;
-    rc = launch_syrk(op, A, b0, nb, c1, nt - c1, nt - c1, c0 * TS, W * TS);
+    // the first trailing update reads its C tiles from K (run_factor copies only
+    // the first outer panel's tile columns into the members)
+    rc = launch_syrk(op, A, b0, nb, c1, nt - c1, nt - c1, c0 * TS, W * TS, c0 == 0);
     if (rc) return rc;
   }
   return 0;
@@ -323,8 +326,11 @@ int run_factor(gpmi_op* op, const double* etas_host, int nb, const double* rhs_d
     HIP_TRY(hipEventRecord(op->ev_begin, s));
   }
   HIP_TRY(hipMemcpyAsync(op->etas, etas_host, sizeof(double) * nb, hipMemcpyHostToDevice, s));
-  hipLaunchKernelGGL(shift_copy_kernel, dim3(nt * (nt + 1) / 2), dim3(256), 0, s, op->K, lda,
-                     op->A, lda, P.sA, op->etas, nb, op->n, nt);
+  // K + eta_b I into the members' tile columns of the first outer panel only; the
+  // rest is formed by the first trailing SYRK from K (schedule)
+  const int wc = std::min(op->outer, nt);
+  hipLaunchKernelGGL(shift_copy_kernel, dim3(wc * (wc + 1) / 2 + (nt - wc) * wc), dim3(256), 0,
+                     s, op->K, lda, op->A, lda, P.sA, op->etas, nb, op->n, wc);
   LAUNCH_CHECK("shift_copy_kernel");
   for (int b = 0; b < nb; ++b)
     HIP_TRY(hipMemcpyAsync(op->R + b * P.sR, rhs_dev, sizeof(double) * P.sR,

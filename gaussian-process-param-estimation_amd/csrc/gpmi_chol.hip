@@ -29,15 +29,16 @@
 namespace gpmi {
 
 // ---------------------------------------------------------------------------
-// A_b = K + eta_b * I on the lower-triangular 128-tiles (diagonal tiles whole).
-// K is read once per launch and written to every batch member. The shift is
-// applied only to the first n diagonal entries; pads stay identity.
+// A_b = K + eta_b * I on the lower-triangular 128-tiles (diagonal tiles whole) of
+// the first wc tile columns (tri_decode's band enumeration). K is read once per
+// launch and written to every batch member. The shift is applied only to the
+// first n diagonal entries; pads stay identity.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void shift_copy_kernel(
     const double* __restrict__ K, int64_t ldk, double* __restrict__ A, int64_t lda,
-    int64_t sA, const double* __restrict__ etas, int nb, int64_t n, int nt) {
+    int64_t sA, const double* __restrict__ etas, int nb, int64_t n, int wc) {
   int I, J;
-  tri_decode(blockIdx.x, nt, &I, &J);
+  tri_decode(blockIdx.x, wc, &I, &J);
   const int t = threadIdx.x;
   for (int e = t; e < TS * TS / 2; e += 256) {
     const int r = e >> 6, c = (e & 63) * 2;
@@ -109,9 +110,15 @@ __global__ __launch_bounds__(256, 2) void panel_kernel(BatchPtrs P, int64_t lda,
 // [tc0, tc0 + t): A_IJ -= sum_{p in [p0, p0+kdim)} A_Ip A_Jp^T, J <= I.
 // blockIdx.y = batch member.
 // ---------------------------------------------------------------------------
+// Ksrc (the first trailing update of a factorization): C is read from the shared K
+// instead of the member's copy, with eta_b added on the diagonal of its first n rows,
+// so A_b = K + eta_b I is never copied for the tiles right of the first outer panel.
 __global__ __launch_bounds__(256, 2) void syrk_kernel(double* A, int64_t lda, int64_t sA,
                                                       int tc0, int w, int t, int p0,
-                                                      int kdim, const uint32_t* order) {
+                                                      int kdim, const uint32_t* order,
+                                                      const double* __restrict__ Ksrc,
+                                                      const double* __restrict__ etas,
+                                                      int64_t n) {
   __shared__ double smem[4 * STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int wr = wv >> 1, wc = wv & 1, fr = lane & 15, fk = lane >> 4;
@@ -135,6 +142,7 @@ __global__ __launch_bounds__(256, 2) void syrk_kernel(double* A, int64_t lda, in
   // the first operand stage) and the update runs as acc += (-P1) P2^T, so the
   // epilogue is store-only.
   double* C = Ab + (int64_t)I * TS * lda + (int64_t)J * TS;
+  const double* Cin = Ksrc ? Ksrc + (int64_t)I * TS * lda + (int64_t)J * TS : C;
   d4 acc[4][4];
 #pragma unroll
   for (int a = 0; a < 4; ++a)
@@ -142,7 +150,16 @@ __global__ __launch_bounds__(256, 2) void syrk_kernel(double* A, int64_t lda, in
     for (int c = 0; c < 4; ++c)
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        acc[a][c][r] = C[(int64_t)(wr * 64 + a * 16 + fk + 4 * r) * lda + wc * 64 + c * 16 + fr];
+        acc[a][c][r] = Cin[(int64_t)(wr * 64 + a * 16 + fk + 4 * r) * lda + wc * 64 + c * 16 + fr];
+  if (Ksrc && I == J && wr == wc) {
+    // diagonal entries: a == c, row fk + 4 r == column fr
+    const double eta = etas[blockIdx.y];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (fk + 4 * r == fr && (int64_t)I * TS + wr * 64 + a * 16 + fr < n) acc[a][a][r] += eta;
+  }
   d4 dummy[2];
   tile_mma<false, true>(P1, lda, P2, lda, kdim, smem, smem + 2 * STAGE, acc, nullptr, dummy);
 #pragma unroll

@@ -43,11 +43,12 @@ struct BatchPtrs {
 
 __global__ void shift_copy_kernel(const double* K, int64_t ldk, double* A, int64_t lda,
                                   int64_t sA, const double* etas, int nb, int64_t n,
-                                  int nt);
+                                  int wc);
 __global__ void diag_block_kernel(BatchPtrs P, int64_t lda, int kb, int nt);
 __global__ void panel_kernel(BatchPtrs P, int64_t lda, int kb);
 __global__ void syrk_kernel(double* A, int64_t lda, int64_t sA, int tc0, int w, int t,
-                            int p0, int kdim, const uint32_t* order);
+                            int p0, int kdim, const uint32_t* order, const double* Ksrc,
+                            const double* etas, int64_t n);
 __global__ void finalize_kernel(BatchPtrs P, int nt, double* out, int out_ld);
 __global__ void bwd_step_kernel(BatchPtrs P, int64_t lda, int kb, double* X, int64_t sX);
 __global__ void fwd_step_kernel(BatchPtrs P, int64_t lda, int kb);

@@ -328,13 +328,16 @@ __global__ __launch_bounds__(64 * TPR) void csr_spmm_wing_kernel(
     const unsigned short* __restrict__ lidx, const double* __restrict__ data, int64_t n,
     const int* __restrict__ wcols, const int* __restrict__ ucount,
     const double* __restrict__ X, double* __restrict__ Y, double eta,
-    double* __restrict__ pqp, int dots2) {
+    double* __restrict__ pqp, int dots2, unsigned long long* __restrict__ stamp) {
   extern __shared__ double smem[];
   // TPR threads per row (4: 256-thread blocks, 8: 512), CG columns each
   constexpr int NT = 64 * TPR;
   constexpr int CG = (S + TPR - 1) / TPR;
   constexpr int NB = 4096 / NT;   // loads in flight per thread while staging
   const int t = threadIdx.x;
+  // in-step timing (gpmi_sp_set_timing): the launch's span on the constant wall
+  // clock, earliest workgroup start to latest workgroup end (vector atomics)
+  if (stamp && t == 0) atomicMin(stamp, (unsigned long long)wall_clock64());
   const int64_t b = xcd_remap(blockIdx.x, gridDim.x);
   const int64_t r0 = b * WIN_ROWS, r1 = min(r0 + WIN_ROWS, n);
   const int nr = (int)(r1 - r0);
@@ -459,23 +462,27 @@ __global__ __launch_bounds__(64 * TPR) void csr_spmm_wing_kernel(
       pqp[b * WD + t] = sum;
     }
   }
+  if (stamp) {
+    __syncthreads();
+    if (t == 0) atomicMax(stamp + 1, (unsigned long long)wall_clock64());
+  }
 }
 
 template __global__ void csr_spmm_wing_kernel<20, 8, 4>(const int64_t*, const int*,
     const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
-    double*, double, double*, int);
+    double*, double, double*, int, unsigned long long*);
 template __global__ void csr_spmm_wing_kernel<11, 8, 4>(const int64_t*, const int*,
     const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
-    double*, double, double*, int);
+    double*, double, double*, int, unsigned long long*);
 template __global__ void csr_spmm_wing_kernel<12, 8, 4>(const int64_t*, const int*,
     const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
-    double*, double, double*, int);
+    double*, double, double*, int, unsigned long long*);
 template __global__ void csr_spmm_wing_kernel<8, 8, 4>(const int64_t*, const int*,
     const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
-    double*, double, double*, int);
+    double*, double, double*, int, unsigned long long*);
 template __global__ void csr_spmm_wing_kernel<7, 8, 4>(const int64_t*, const int*,
     const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
-    double*, double, double*, int);
+    double*, double, double*, int, unsigned long long*);
 
 // partial[b][j][c] = sum over this block's rows of A_j[i][c] * B[i][c],
 // A_j = A + j * strideA, j = blockIdx.y; grid-stride over rows.

@@ -48,7 +48,8 @@ __global__ void csr_spmm_win_kernel(const int64_t*, const int*, const unsigned s
 template <int S, int U, int TPR>
 __global__ void csr_spmm_wing_kernel(const int64_t*, const int*, const unsigned short*,
                                      const double*, int64_t, const int*, const int*,
-                                     const double*, double*, double, double*, int);
+                                     const double*, double*, double, double*, int,
+                                     unsigned long long*);
 constexpr int WING_MAX_LDS = 80 * 1024;   // two workgroups per CU
 // nonzeros in flight per thread and threads per row of csr_spmm_wing_kernel (measured:
 // 8 in flight best at cfg 5, within 0.3 us of 4 at cfg 4; 8 threads per row in
@@ -211,16 +212,23 @@ struct gpmi_sp {
   int dsplit = 1, dkcs = 1;            // k splits of dense_mm_kernel, 64-column chunks each
   double* dYp = nullptr;               // split partials [dsplit][n][MAXS] of `stream`
   double* dYp_ms = nullptr;            // ... of ms_stream (the CG beside the Lanczos)
-  // In-step SpMM timing (gpmi_sp_set_timing): a HIP event pair around every SpMM
-  // launch on the stream it runs on (the Lanczos's and the CG's), logged with its
-  // width; gpmi_sp_spmm_timing sums the pairs per width. The two host threads of a
+  // In-step SpMM timing (gpmi_sp_set_timing), logged per launch with its width;
+  // gpmi_sp_spmm_timing sums the spans per width. The window SpMM (every SpMM of
+  // the sparse sweeps) stamps its own span on the device's constant wall clock into
+  // a slot of `stamps` (earliest workgroup start, latest workgroup end: two vector
+  // atomics per workgroup, so the timed steps themselves carry the timing); the
+  // other kinds get a HIP event pair on their stream. The two host threads of a
   // sweep both launch SpMMs: the log is under timing_mu.
   std::mutex timing_mu;
   bool timing = false;
   std::vector<hipEvent_t> ev_pool;     // free events
+  unsigned long long* stamps = nullptr;   // [STAMP_CAP][2]
+  int stamps_used = 0;
+  int wall_khz = 0;                    // wall clock rate (hipDeviceAttributeWallClockRate)
   struct SpmmRec {
     hipEvent_t e0, e1;
     int s;
+    int slot;                          // stamps slot, or -1 (events)
   };
   std::vector<SpmmRec> spmm_log;
 };
@@ -362,8 +370,7 @@ int spmm_kind(gpmi_sp* sp, int s, int* kind) {
 // X . Y per column (pqp[block][s], the multi-shift CG's p . q) and sets *pq_blocks to
 // their count; otherwise *pq_blocks = 0 and the caller forms them.
 int spmm_launch(gpmi_sp* sp, const double* X, double* Y, int s, double eta, hipStream_t st,
-                double* pqp, int* pq_blocks, int dots2,
-                hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr) {
+                double* pqp, int* pq_blocks, int dots2, unsigned long long* stamp = nullptr) {
   if (pq_blocks) *pq_blocks = 0;
   if (sp->dK) {
     // dense: split partials of K X on fp64 MFMA, summed in split order (+ eta X)
@@ -401,10 +408,9 @@ int spmm_launch(gpmi_sp* sp, const double* X, double* Y, int s, double eta, hipS
                : s == 8  ? csr_spmm_wing_kernel<8, WING_U, WING_TPR>
                          : csr_spmm_wing_kernel<7, WING_U, WING_TPR>;
     const int tpr = WING_TPR;
-    // (timed: the events ride in the dispatch packet, as the profiler's timestamps)
-    hipExtLaunchKernelGGL(kfn, dim3((unsigned)sp->win_nblk), dim3(64 * tpr), lds, st, ev0, ev1, 0,
-                          sp->indptr, sp->indices, sp->win_lidx, sp->data, sp->n, sp->win_cols,
-                          sp->win_u, X, Y, eta, pqp, dots2);
+    hipLaunchKernelGGL(kfn, dim3((unsigned)sp->win_nblk), dim3(64 * tpr), lds, st, sp->indptr,
+                       sp->indices, sp->win_lidx, sp->data, sp->n, sp->win_cols, sp->win_u, X, Y,
+                       eta, pqp, dots2, stamp);
     SP_LAUNCH("csr_spmm_wing_kernel");
     if (pqp && pq_blocks) *pq_blocks = (int)sp->win_nblk;
     return 0;
@@ -447,30 +453,35 @@ int take_event(gpmi_sp* sp, hipEvent_t* e) {
   return 0;
 }
 
-// Y = (K + eta I) X (spmm_launch), bracketed by a HIP event pair on its stream when
-// in-step timing is on (gpmi_sp_set_timing).
+constexpr int STAMP_CAP = 8192;   // stamped window-SpMM launches per timing window
+
+// Y = (K + eta I) X (spmm_launch); with in-step timing on (gpmi_sp_set_timing) the
+// window SpMM stamps its span into the next slot, other kinds are bracketed by a
+// HIP event pair on their stream.
 int spmm(gpmi_sp* sp, const double* X, double* Y, int s, double eta, hipStream_t st = nullptr,
          double* pqp = nullptr, int* pq_blocks = nullptr, int dots2 = 0) {
   if (!st) st = sp->stream;
   if (!sp->timing) return spmm_launch(sp, X, Y, s, eta, st, pqp, pq_blocks, dots2);
-  gpmi_sp::SpmmRec rec{nullptr, nullptr, s};
-  {
-    std::lock_guard<std::mutex> lock(sp->timing_mu);
-    if (int rc = take_event(sp, &rec.e0)) return rc;
-    if (int rc = take_event(sp, &rec.e1)) return rc;
-  }
-  // the window SpMM carries the pair in its dispatch packet (hipExtLaunchKernel: the
-  // kernel's own start / end, as rocprofv3 sees them); other kinds: recorded around
+  gpmi_sp::SpmmRec rec{nullptr, nullptr, s, -1};
   int kind = 0;
   if (int rc = spmm_kind(sp, s, &kind)) return rc;
-  const bool in_packet =
+  const bool stamped =
       kind == 5 && !sp->dK &&
       !(s % 2 == 0 && ((reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(Y)) & 15));
-  if (!in_packet) SP_TRY(hipEventRecord(rec.e0, st));
+  {
+    std::lock_guard<std::mutex> lock(sp->timing_mu);
+    if (stamped && sp->stamps_used < STAMP_CAP) {
+      rec.slot = sp->stamps_used++;
+    } else {
+      if (int rc = take_event(sp, &rec.e0)) return rc;
+      if (int rc = take_event(sp, &rec.e1)) return rc;
+    }
+  }
+  if (rec.slot < 0) SP_TRY(hipEventRecord(rec.e0, st));
   if (int rc = spmm_launch(sp, X, Y, s, eta, st, pqp, pq_blocks, dots2,
-                           in_packet ? rec.e0 : nullptr, in_packet ? rec.e1 : nullptr))
+                           rec.slot >= 0 ? sp->stamps + 2 * rec.slot : nullptr))
     return rc;
-  if (!in_packet) SP_TRY(hipEventRecord(rec.e1, st));
+  if (rec.slot < 0) SP_TRY(hipEventRecord(rec.e1, st));
   std::lock_guard<std::mutex> lock(sp->timing_mu);
   sp->spmm_log.push_back(rec);
   return 0;
@@ -1019,9 +1030,10 @@ int gpmi_sp_destroy(gpmi_sp* sp) {
   if (sp->cg2_buf) (void)hipFree(sp->cg2_buf);
   for (hipEvent_t e : sp->ev_pool) (void)hipEventDestroy(e);
   for (auto& r : sp->spmm_log) {
-    (void)hipEventDestroy(r.e0);
-    (void)hipEventDestroy(r.e1);
+    if (r.e0) (void)hipEventDestroy(r.e0);
+    if (r.e1) (void)hipEventDestroy(r.e1);
   }
+  if (sp->stamps) (void)hipFree(sp->stamps);
   for (hipEvent_t e : sp->ms_ev)
     if (e) (void)hipEventDestroy(e);
   if (sp->ms_stream) (void)hipStreamDestroy(sp->ms_stream);
@@ -1643,6 +1655,15 @@ namespace gpmi {
 // kernel trace (tools/trace_summary.py --timed-spmm takes the SpMM launches
 // between two marks as the timed ones).
 __global__ void timing_mark_kernel(int on) { (void)on; }
+
+// Every stamp slot to (start = max, end = 0) before a timing window.
+__global__ void stamp_init_kernel(unsigned long long* st, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    st[2 * i] = ~0ull;
+    st[2 * i + 1] = 0ull;
+  }
+}
 }  // namespace gpmi
 
 extern "C" {
@@ -1650,17 +1671,34 @@ extern "C" {
 int gpmi_sp_set_timing(gpmi_sp* sp, int enable) {
   if (!sp) return set_error(-1006, "null handle");
   Guard g(sp->device);
+  std::lock_guard<std::mutex> lock(sp->timing_mu);
+  if (enable) {
+    if (!sp->stamps) {
+      SP_TRY(hipMalloc(&sp->stamps, sizeof(unsigned long long) * 2 * STAMP_CAP));
+      SP_TRY(hipDeviceGetAttribute(&sp->wall_khz, hipDeviceAttributeWallClockRate, sp->device));
+    }
+    // a window starts with every slot reset, on the stream the caller orders its
+    // work on; synchronised, so that the side stream's launches find them reset too
+    hipLaunchKernelGGL(gpmi::stamp_init_kernel, dim3((STAMP_CAP + 255) / 256), dim3(256), 0,
+                       sp->stream, sp->stamps, STAMP_CAP);
+    SP_LAUNCH("stamp_init_kernel");
+    SP_TRY(hipStreamSynchronize(sp->stream));
+  }
   hipLaunchKernelGGL(gpmi::timing_mark_kernel, dim3(1), dim3(64), 0, sp->stream, enable);
   SP_LAUNCH("timing_mark_kernel");
-  std::lock_guard<std::mutex> lock(sp->timing_mu);
-  // the pairs of an earlier window go back to the pool (their streams are idle
-  // once the caller synchronised; wait for them anyway)
-  for (auto& r : sp->spmm_log) {
-    SP_TRY(hipEventSynchronize(r.e1));
-    sp->ev_pool.push_back(r.e0);
-    sp->ev_pool.push_back(r.e1);
+  if (enable) {
+    // the pairs of an earlier window go back to the pool (their streams are idle
+    // once the caller synchronised; wait for them anyway)
+    for (auto& r : sp->spmm_log) {
+      if (r.slot >= 0) continue;
+      SP_TRY(hipEventSynchronize(r.e1));
+      sp->ev_pool.push_back(r.e0);
+      sp->ev_pool.push_back(r.e1);
+    }
+    sp->spmm_log.clear();
+    sp->stamps_used = 0;
   }
-  sp->spmm_log.clear();
+  // (disabling keeps the window's log for gpmi_sp_spmm_timing)
   sp->timing = enable != 0;
   return 0;
 }
@@ -1671,10 +1709,25 @@ int gpmi_sp_spmm_timing(gpmi_sp* sp, int max_widths, int* n_widths, int* widths,
   Guard g(sp->device);
   std::lock_guard<std::mutex> lock(sp->timing_mu);
   std::map<int, std::pair<int, double>> acc;
+  std::vector<unsigned long long> st;
+  if (sp->stamps_used > 0) {
+    SP_TRY(hipDeviceSynchronize());
+    st.resize((size_t)2 * sp->stamps_used);
+    SP_TRY(hipMemcpy(st.data(), sp->stamps, sizeof(unsigned long long) * st.size(),
+                     hipMemcpyDeviceToHost));
+  }
   for (auto& r : sp->spmm_log) {
-    SP_TRY(hipEventSynchronize(r.e1));
-    float ms = 0.f;
-    SP_TRY(hipEventElapsedTime(&ms, r.e0, r.e1));
+    double ms = 0.0;
+    if (r.slot >= 0) {
+      const unsigned long long t0 = st[2 * r.slot], t1 = st[2 * r.slot + 1];
+      if (t1 < t0 || sp->wall_khz <= 0) return set_error(-1107, "SpMM timing: a stamp slot was not written");
+      ms = (double)(t1 - t0) / (double)sp->wall_khz;
+    } else {
+      SP_TRY(hipEventSynchronize(r.e1));
+      float fms = 0.f;
+      SP_TRY(hipEventElapsedTime(&fms, r.e0, r.e1));
+      ms = fms;
+    }
     auto& a = acc[r.s];
     a.first += 1;
     a.second += ms;

@@ -649,8 +649,10 @@ class SparseOperator(object):
         return a, b
 
     def set_timing(self, on):
-        """In-step SpMM timing: HIP event pairs around every SpMM launch of this
-        operator while on (the log is cleared on every call)."""
+        """In-step SpMM timing while on: every window SpMM launch of this operator
+        stamps its span on the device wall clock (other SpMM kinds: a HIP event pair
+        around it). set_timing(True) starts a new window (the log is cleared),
+        set_timing(False) ends it and keeps its log for spmm_timing()."""
         check(self.lib.gpmi_sp_set_timing(self.h, int(bool(on))), 'gpmi_sp_set_timing')
 
     def spmm_timing(self):

@@ -238,10 +238,12 @@ int gpmi_sp_last_status(const gpmi_sp* sp, int* converged);
 int gpmi_sp_bench_spmm(gpmi_sp* sp, int s, int reps, double eta, double* avg_ms);
 /* In-step SpMM timing (measurement; no reference counterpart): while enabled,
  * every SpMM this operator launches (Lanczos, CG, multi-shift CG; either
- * stream) is bracketed by a HIP event pair on its own stream. set_timing clears
- * the log (enable = 0 stops logging). spmm_timing sums the logged pairs by block
- * width s: widths[k], launches[k], total_ms[k] for k < min(*n_widths, max_widths),
- * ascending s (it waits for the logged launches to finish). */
+ * stream) is timed: the window SpMM stamps its own span (earliest workgroup start
+ * to latest workgroup end on the device wall clock, up to 8192 launches per
+ * window), other kinds get a HIP event pair on their stream. set_timing(1) starts
+ * a window (clears the log), set_timing(0) ends it and keeps the log. spmm_timing
+ * sums the logged spans by block width s: widths[k], launches[k], total_ms[k] for
+ * k < min(*n_widths, max_widths), ascending s (it waits for the device). */
 int gpmi_sp_set_timing(gpmi_sp* sp, int enable);
 int gpmi_sp_spmm_timing(gpmi_sp* sp, int max_widths, int* n_widths, int* widths,
                         int* launches, double* total_ms);

@@ -73,7 +73,7 @@ for task in "$@"; do
       run 900 $D/trace.err rocprofv3 --kernel-trace --stats -d $D/prof -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --out-json $D/bench_under_rocprof.json
       python tools/bench_summary.py $D/bench_under_rocprof.json ;;
     trace-dense)
-      run 600 $D/trace_dense.err rocprofv3 --kernel-trace --stats -d $D/prof_dense -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-band --no-sparse --out-json $D/bench_dense_under_rocprof.json
+      run 600 $D/trace_dense.err rocprofv3 --kernel-trace --stats -d $D/prof_dense -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-band --no-sparse --no-extras --out-json $D/bench_dense_under_rocprof.json
       python tools/trace_summary.py --timed-syrk $D/prof_dense $D/bench_dense_under_rocprof.json > $D/syrk_timed_launches.json
       cat $D/syrk_timed_launches.json ;;
     pmc-dense)

@@ -3,7 +3,9 @@
 usage: python tools/pmc_summary.py OUT.json NOTE dir1 [dir2 ...]
 PMC_FIRST=K (environment): also report, per kernel, the mean over its first K
 dispatches of each pass ('per_dispatch_first'), e.g. the timed call of a run
-that makes a second, differently sized call afterwards.
+that makes a second, differently sized call afterwards. PMC_MARKS=1: the mean over
+the dispatches between the last two timing_mark_kernel launches of each pass
+('per_dispatch_timed': bench.py's timed steps).
 Each dir holds one pass's *_counter_collection.csv. Per kernel name (template
 and argument list stripped) it reports dispatch count, the summed counter
 values and the per-dispatch mean; FETCH_SIZE / WRITE_SIZE are in KB as
@@ -55,6 +57,28 @@ def main():
             for did in sorted(by)[-last_k:]:
                 for c, v in by[did].items():
                     last[k][c] += v / last_k
+    # PMC_MARKS=1: the mean over the dispatches between the last two timing_mark_kernel
+    # dispatches of each pass (bench.py's timed steps, gpmi_sp_set_timing)
+    timed = defaultdict(lambda: defaultdict(float))
+    timed_n = {}
+    if os.environ.get('PMC_MARKS'):
+        files = {f for f, _ in rows_by}
+        for f in files:
+            marks = sorted(d for (g, k), by in rows_by.items() if g == f and
+                           'timing_mark_kernel' in k for d in by)
+            if len(marks) < 2:
+                continue
+            lo, hi = marks[-2], marks[-1]
+            for (g, k), by in rows_by.items():
+                if g != f:
+                    continue
+                ids = [d for d in by if lo < d < hi]
+                if not ids:
+                    continue
+                timed_n[k] = len(ids)
+                for d in ids:
+                    for c, v in by[d].items():
+                        timed[k][c] += v / len(ids)
     res = {'note': note, 'kernels': {}}
     for k, cs in acc.items():
         nd = max(1, len(disp[k]) // max(1, len(dirs)))
@@ -64,6 +88,9 @@ def main():
         if first_k and k in first:
             res['kernels'][k]['first_dispatches'] = first_k
             res['kernels'][k]['per_dispatch_first'] = dict(sorted(first[k].items()))
+        if k in timed:
+            res['kernels'][k]['timed_dispatches'] = timed_n[k]
+            res['kernels'][k]['per_dispatch_timed'] = dict(sorted(timed[k].items()))
         if last_k and k in last:
             res['kernels'][k]['last_dispatches'] = last_k
             res['kernels'][k]['per_dispatch_last'] = dict(sorted(last[k].items()))
