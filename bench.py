@@ -507,8 +507,18 @@ def sparse_measure(args, config, world, rank, local, dist, torch, cpu, exact, de
     nnz = op.sop.nnz
     s_blk = max(spmm_in_step, key=lambda w: spmm_in_step[w][1])
     n_launch, tot_ms = spmm_in_step[s_blk]
-    ms = tot_ms / n_launch
+    ms_span = tot_ms / n_launch
+    # the stamps span a launch's first workgroup start to its last workgroup end; a
+    # dispatch also costs the command processor's launch and the end-of-kernel
+    # release, which a kernel trace's dispatch interval includes. Measured here on
+    # the same kernel: 50 back-to-back launches' period per launch (HIP events
+    # around them) less their mean stamped span
+    op.sop.set_timing(True)
     ms_iso = op.sop.bench_spmm(s_blk, 50)
+    op.sop.set_timing(False)
+    iso_n, iso_tot = op.sop.spmm_timing()[s_blk]
+    dispatch_ms = max(0.0, ms_iso - iso_tot / iso_n)
+    ms = ms_span + dispatch_ms
     alg_bytes = 12.0 * nnz + 8.0 * (n + 1) + 16.0 * n * s_blk
     gbs = alg_bytes / (ms * 1e-3) / 1e9
     info = op.sop.spmm_info()
@@ -557,9 +567,19 @@ def sparse_measure(args, config, world, rank, local, dist, torch, cpu, exact, de
                          'traffic_source': sp_tsrc,
                          'kernel': '%s (s=%d columns)' % (sp_kernel, s_blk),
                          'avg_launch_ms': round(ms, 4),
-                         'avg_launch_ms_source': 'device wall-clock span of each SpMM '
-                                                 'launch of the %d timed steps (%d launches '
-                                                 'at s=%d)' % (args.steps, n_launch, s_blk),
+                         'avg_launch_ms_source': 'in_step_span_ms (device wall-clock span, '
+                                                 'first workgroup start to last workgroup '
+                                                 'end, of each SpMM launch of the %d timed '
+                                                 'steps: %d launches at s=%d) + '
+                                                 'dispatch_overhead_ms' % (args.steps, n_launch,
+                                                                           s_blk),
+                         'in_step_span_ms': round(ms_span, 5),
+                         'dispatch_overhead_ms': round(dispatch_ms, 5),
+                         'dispatch_overhead_source': '50 back-to-back launches of the same '
+                                                     'kernel: period per launch (HIP events) '
+                                                     'less their mean stamped span',
+                         'frac_of_span': round(alg_bytes / (ms_span * 1e-3) / 1e9 /
+                                               HBM_PEAK_GBS, 4),
                          'isolated_ms': round(ms_iso, 4),
                          'algorithmic_bytes_per_launch': alg_bytes,
                          'in_step_by_width': by_width,

@@ -39,16 +39,6 @@ __device__ __forceinline__ double readlane_d(double v, int lane) {
 __device__ int g_chol_calls;
 #endif
 
-// v broadcast from lane SG of each quad (DPP quad_perm [SG,SG,SG,SG], VALU only).
-template <int SG>
-__device__ __forceinline__ double quad_bcast(double v) {
-  const long long b = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_mov_dpp((int)(b & 0xffffffffLL), SG * 0x55, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), SG * 0x55, 0xF, 0xF, false);
-  return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) |
-                                          (unsigned)lo));
-}
-
 // Lanes of one wave exchanging values through LDS: the write must stay before the
 // read (the compiler, reasoning per lane, could otherwise forward or hoist). LDS
 // executes one wave's instructions in order, so no s_barrier is needed.
@@ -56,16 +46,6 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-// sg known after unrolling: the switch folds to one DPP pair
-__device__ __forceinline__ double quad_bcast_sel(double v, int sg) {
-  switch (sg) {
-    case 0: return quad_bcast<0>(v);
-    case 1: return quad_bcast<1>(v);
-    case 2: return quad_bcast<2>(v);
-    default: return quad_bcast<3>(v);
-  }
 }
 
 // 1/sqrt(d) to double precision: hardware estimate + two Newton steps.
@@ -118,69 +98,56 @@ __device__ __forceinline__ void store_colblock(double* Ls, const d4 (&Xc)[NDB - 
 
 // F1 of block jb (wave 0): factor the 16x16 diagonal block in registers and
 // invert it into Aux[jb][16][16]; diag(L) to sdiag, first bad pivot to *s_fail.
-// Lane (r, g) holds row r, columns 4g..4g+3. Pivot step j: column j to every lane
-// of quad r by DPP and across quads through the LDS line colbuf (one wave: LDS
-// order plus wave-scope fences, no barrier), overlapping the rsq chain; row j of
-// X = L^-1 is formed in the same step (rows above it are final) and passed
-// through xbuf, so the inverse chain runs in the shadow of the factor chain.
+// Lane r (and its mirrors r + 16, r + 32, r + 48, which only compute) holds row r
+// of the block and column r of X = L^-1. Pivot step j takes the pivot and the
+// column below it from the lanes that hold them by v_readlane (scalar registers:
+// every lane sees them, no LDS round trip, no barrier); row r's update and the
+// right-looking substitution of X's column r (s_i += L_ij X_jr, X_jr =
+// (delta_jr - s_j) / L_jj, in ascending j as the row-wise substitution) use the
+// same values. The arithmetic of every element is that of the round-4 quad /
+// LDS-exchange version: the same results.
 __device__ __forceinline__ void f1_factor(double* Ls, double* Aux, double* sdiag, int* s_fail,
-                                          int jb, double* colbuf, double* xbuf) {
+                                          int jb) {
   const int lane = threadIdx.x & 63;
   const int j0 = jb * DB;
-  const int r = lane >> 2, g = lane & 3;
-  double a[4];
+  const int r = lane & 15;
+  double a[DB];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) a[k] = Ls[(j0 + r) * DL + j0 + 4 * g + k];
-  double myrinv = 0.0;
-  double s[4] = {0.0, 0.0, 0.0, 0.0}, x[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int k = 0; k < DB; ++k) a[k] = Ls[(j0 + r) * DL + j0 + k];
+  double s[DB], x[DB];
+#pragma unroll
+  for (int k = 0; k < DB; ++k) s[k] = x[k] = 0.0;
   int fail = 0;
 #pragma unroll
   for (int j = 0; j < DB; ++j) {
-    const int sk = j & 3, sg = j >> 2;
-    const double d = readlane_d(a[sk], (j << 2) | sg);
-    const double crj = quad_bcast_sel(a[sk], sg);
-    if (g == 0) colbuf[r] = crj;
-    wave_lds_sync();
-    double lcj[4];
-    {
-      const d2 c01 = *reinterpret_cast<const d2*>(&colbuf[4 * g]);
-      const d2 c23 = *reinterpret_cast<const d2*>(&colbuf[4 * g + 2]);
-      lcj[0] = c01[0]; lcj[1] = c01[1]; lcj[2] = c23[0]; lcj[3] = c23[1];
-    }
+    const double d = readlane_d(a[j], j);
+    double col[DB];
+#pragma unroll
+    for (int c = j + 1; c < DB; ++c) col[c] = readlane_d(a[j], c);
     const double rinv = rsqrt_nr(d);
     const double ljj = d * rinv;
     if (!(d > 0.0) && fail == 0) fail = j0 + j + 1;   // d is wave-uniform
     if (lane == 0) sdiag[j0 + j] = ljj;
-    if (r == j) myrinv = rinv;
-    const double lrj = (r > j) ? crj * rinv : ((r == j) ? ljj : 0.0);
+    const double lrj = (r > j) ? a[j] * rinv : ((r == j) ? ljj : 0.0);
+    a[j] = lrj;
+    // X column r: row j final, then its contribution to the rows below
+    x[j] = ((r == j ? 1.0 : 0.0) - s[j]) * rinv;
+    // row r's update, unpredicated: the entries right of the diagonal (c > r) take
+    // garbage that nothing reads (they are zeroed when the block is stored)
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int c = 4 * g + k;
-      if (c > j && c <= r) a[k] -= lrj * (lcj[k] * rinv);
-    }
-    if (g == sg) a[sk] = lrj;
-    // row j of X: (e_j - sum_{p < j} L[j][p] X[p]) / L[j][j]; lrj = L[r][j] is final
-    if (r == j) {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) x[k] = (((4 * g + k) == j ? 1.0 : 0.0) - s[k]) * myrinv;
-      *reinterpret_cast<d2*>(&xbuf[4 * g]) = d2{x[0], x[1]};
-      *reinterpret_cast<d2*>(&xbuf[4 * g + 2]) = d2{x[2], x[3]};
-    }
-    wave_lds_sync();
-    if (r > j) {
-      const d2 c01 = *reinterpret_cast<const d2*>(&xbuf[4 * g]);
-      const d2 c23 = *reinterpret_cast<const d2*>(&xbuf[4 * g + 2]);
-      s[0] += lrj * c01[0];
-      s[1] += lrj * c01[1];
-      s[2] += lrj * c23[0];
-      s[3] += lrj * c23[1];
+    for (int c = j + 1; c < DB; ++c) {
+      const double lc = col[c] * rinv;
+      a[c] -= lrj * lc;
+      s[c] += lc * x[j];
     }
   }
   if (lane == 0 && fail && *s_fail == 0) *s_fail = fail;
+  if (lane < DB) {
 #pragma unroll
-  for (int k = 0; k < 4; ++k) Ls[(j0 + r) * DL + j0 + 4 * g + k] = a[k];
+    for (int k = 0; k < DB; ++k) Ls[(j0 + r) * DL + j0 + k] = k <= r ? a[k] : 0.0;
 #pragma unroll
-  for (int k = 0; k < 4; ++k) Aux[jb * 256 + r * 16 + 4 * g + k] = x[k];
+    for (int i = 0; i < DB; ++i) Aux[jb * 256 + i * 16 + r] = x[i];
+  }
 }
 
 // F3 tile q of the trailing update after block jb: (ti, tj), jb < tj <= ti < 8, K = 16.
@@ -211,19 +178,17 @@ __device__ __forceinline__ void lds_chol_block(double* Ls, double* Aux, double* 
                                                int* s_fail) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int fr = lane & 15, fk = lane >> 4;
-  __shared__ __attribute__((aligned(16))) double colbuf[DB];   // F1 column line (wave 0)
-  __shared__ __attribute__((aligned(16))) double xbuf[DB];     // F1 inverse-row line
 #if GPMI_CHOL_STAMPS
   unsigned long long cs[NDB + 1][3];
   bool cst = false;
-  if (t == 0 && blockIdx.x == 0) cst = atomicAdd(&g_chol_calls, 1) == 8;
+  if (t == 0 && blockIdx.x == 0) cst = atomicAdd(&g_chol_calls, 1) == 2;
 #define CHST(jb, i) \
   if (cst) cs[jb][i] = wall_clock64()
 #else
 #define CHST(jb, i)
 #endif
   CHST(0, 2);
-  if (w == 0) f1_factor(Ls, Aux, sdiag, s_fail, 0, colbuf, xbuf);
+  if (w == 0) f1_factor(Ls, Aux, sdiag, s_fail, 0);
   CHST(0, 1);
   for (int jb = 0; jb < NDB; ++jb) {
     const int j0 = jb * DB;
@@ -256,7 +221,7 @@ __device__ __forceinline__ void lds_chol_block(double* Ls, double* Aux, double* 
       if (ntile > 0) {
         f3_tile(Ls, jb, 0, fr, fk);
         wave_lds_sync();   // the tile written by other lanes of this wave
-        f1_factor(Ls, Aux, sdiag, s_fail, jb + 1, colbuf, xbuf);
+        f1_factor(Ls, Aux, sdiag, s_fail, jb + 1);
         CHST(jb + 1, 2);
       }
     } else {

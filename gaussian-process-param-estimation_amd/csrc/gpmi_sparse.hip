@@ -335,9 +335,10 @@ __global__ __launch_bounds__(64 * TPR) void csr_spmm_wing_kernel(
   constexpr int CG = (S + TPR - 1) / TPR;
   constexpr int NB = 4096 / NT;   // loads in flight per thread while staging
   const int t = threadIdx.x;
-  // in-step timing (gpmi_sp_set_timing): the launch's span on the constant wall
-  // clock, earliest workgroup start to latest workgroup end (vector atomics)
-  if (stamp && t == 0) atomicMin(stamp, (unsigned long long)wall_clock64());
+  // in-step timing (gpmi_sp_set_timing): this workgroup's start and end on the
+  // constant wall clock, stored at its end into its own pair of the launch's slot
+  // (no atomics, no wait inside the kernel; reduced to the launch's span afterwards)
+  const unsigned long long t_start = stamp ? (unsigned long long)wall_clock64() : 0ull;
   const int64_t b = xcd_remap(blockIdx.x, gridDim.x);
   const int64_t r0 = b * WIN_ROWS, r1 = min(r0 + WIN_ROWS, n);
   const int nr = (int)(r1 - r0);
@@ -464,7 +465,11 @@ __global__ __launch_bounds__(64 * TPR) void csr_spmm_wing_kernel(
   }
   if (stamp) {
     __syncthreads();
-    if (t == 0) atomicMax(stamp + 1, (unsigned long long)wall_clock64());
+    if (t == 0) {
+      const unsigned long long t_end = (unsigned long long)wall_clock64();
+      stamp[2 * blockIdx.x] = t_start;
+      stamp[2 * blockIdx.x + 1] = t_end;
+    }
   }
 }
 

@@ -214,15 +214,17 @@ struct gpmi_sp {
   double* dYp_ms = nullptr;            // ... of ms_stream (the CG beside the Lanczos)
   // In-step SpMM timing (gpmi_sp_set_timing), logged per launch with its width;
   // gpmi_sp_spmm_timing sums the spans per width. The window SpMM (every SpMM of
-  // the sparse sweeps) stamps its own span on the device's constant wall clock into
-  // a slot of `stamps` (earliest workgroup start, latest workgroup end: two vector
-  // atomics per workgroup, so the timed steps themselves carry the timing); the
-  // other kinds get a HIP event pair on their stream. The two host threads of a
-  // sweep both launch SpMMs: the log is under timing_mu.
+  // the sparse sweeps) stamps each workgroup's start and end on the device's
+  // constant wall clock into the launch's slot of `stamps` (win_nblk pairs, plain
+  // stores at the workgroup's end: the timed steps themselves carry the timing);
+  // stamp_span_kernel reduces a slot to the launch's span (earliest start, latest
+  // end). Other kinds get a HIP event pair on their stream. The two host threads
+  // of a sweep both launch SpMMs: the log is under timing_mu.
   std::mutex timing_mu;
   bool timing = false;
   std::vector<hipEvent_t> ev_pool;     // free events
-  unsigned long long* stamps = nullptr;   // [STAMP_CAP][2]
+  unsigned long long* stamps = nullptr;   // [stamp_cap][win_nblk][2]
+  int stamp_cap = 0;                   // launches the buffer holds
   int stamps_used = 0;
   int wall_khz = 0;                    // wall clock rate (hipDeviceAttributeWallClockRate)
   struct SpmmRec {
@@ -453,7 +455,8 @@ int take_event(gpmi_sp* sp, hipEvent_t* e) {
   return 0;
 }
 
-constexpr int STAMP_CAP = 8192;   // stamped window-SpMM launches per timing window
+constexpr int STAMP_CAP = 8192;            // stamped window-SpMM launches per timing window
+constexpr size_t STAMP_BYTES = 256u << 20;   // at most this much stamp buffer
 
 // Y = (K + eta I) X (spmm_launch); with in-step timing on (gpmi_sp_set_timing) the
 // window SpMM stamps its span into the next slot, other kinds are bracketed by a
@@ -470,7 +473,7 @@ int spmm(gpmi_sp* sp, const double* X, double* Y, int s, double eta, hipStream_t
       !(s % 2 == 0 && ((reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(Y)) & 15));
   {
     std::lock_guard<std::mutex> lock(sp->timing_mu);
-    if (stamped && sp->stamps_used < STAMP_CAP) {
+    if (stamped && sp->stamps_used < sp->stamp_cap) {
       rec.slot = sp->stamps_used++;
     } else {
       if (int rc = take_event(sp, &rec.e0)) return rc;
@@ -479,7 +482,7 @@ int spmm(gpmi_sp* sp, const double* X, double* Y, int s, double eta, hipStream_t
   }
   if (rec.slot < 0) SP_TRY(hipEventRecord(rec.e0, st));
   if (int rc = spmm_launch(sp, X, Y, s, eta, st, pqp, pq_blocks, dots2,
-                           rec.slot >= 0 ? sp->stamps + 2 * rec.slot : nullptr))
+                           rec.slot >= 0 ? sp->stamps + 2 * sp->win_nblk * rec.slot : nullptr))
     return rc;
   if (rec.slot < 0) SP_TRY(hipEventRecord(rec.e1, st));
   std::lock_guard<std::mutex> lock(sp->timing_mu);
@@ -1656,12 +1659,42 @@ namespace gpmi {
 // between two marks as the timed ones).
 __global__ void timing_mark_kernel(int on) { (void)on; }
 
-// Every stamp slot to (start = max, end = 0) before a timing window.
-__global__ void stamp_init_kernel(unsigned long long* st, int n) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) {
-    st[2 * i] = ~0ull;
-    st[2 * i + 1] = 0ull;
+// Holds its stream until the host sets *flag (pinned, coherent host memory), or at
+// most max_ticks of the wall clock: the launches queued behind it then run back to
+// back, not at the host's enqueue rate (gpmi_sp_bench_spmm).
+__global__ void gate_kernel(const int* flag, unsigned long long max_ticks) {
+  if (threadIdx.x != 0) return;
+  const unsigned long long t0 = wall_clock64();
+  while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0 &&
+         wall_clock64() - t0 < max_ticks)
+    __builtin_amdgcn_s_sleep(8);
+}
+
+// out[l] = (earliest start, latest end) over the nblk workgroup pairs of stamped
+// launch l (one workgroup per launch).
+__global__ void stamp_span_kernel(const unsigned long long* __restrict__ st, int64_t nblk,
+                                  unsigned long long* __restrict__ out) {
+  __shared__ unsigned long long s0[256], s1[256];
+  const int t = threadIdx.x;
+  const unsigned long long* p = st + 2 * nblk * blockIdx.x;
+  unsigned long long lo = ~0ull, hi = 0ull;
+  for (int64_t i = t; i < nblk; i += 256) {
+    lo = min(lo, p[2 * i]);
+    hi = max(hi, p[2 * i + 1]);
+  }
+  s0[t] = lo;
+  s1[t] = hi;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if (t < off) {
+      s0[t] = min(s0[t], s0[t + off]);
+      s1[t] = max(s1[t], s1[t + off]);
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    out[2 * blockIdx.x] = s0[0];
+    out[2 * blockIdx.x + 1] = s1[0];
   }
 }
 }  // namespace gpmi
@@ -1672,17 +1705,12 @@ int gpmi_sp_set_timing(gpmi_sp* sp, int enable) {
   if (!sp) return set_error(-1006, "null handle");
   Guard g(sp->device);
   std::lock_guard<std::mutex> lock(sp->timing_mu);
-  if (enable) {
-    if (!sp->stamps) {
-      SP_TRY(hipMalloc(&sp->stamps, sizeof(unsigned long long) * 2 * STAMP_CAP));
-      SP_TRY(hipDeviceGetAttribute(&sp->wall_khz, hipDeviceAttributeWallClockRate, sp->device));
-    }
-    // a window starts with every slot reset, on the stream the caller orders its
-    // work on; synchronised, so that the side stream's launches find them reset too
-    hipLaunchKernelGGL(gpmi::stamp_init_kernel, dim3((STAMP_CAP + 255) / 256), dim3(256), 0,
-                       sp->stream, sp->stamps, STAMP_CAP);
-    SP_LAUNCH("stamp_init_kernel");
-    SP_TRY(hipStreamSynchronize(sp->stream));
+  if (enable && !sp->stamps && !sp->dK) {
+    if (int rc = ensure_window(sp)) return rc;
+    const size_t per = sizeof(unsigned long long) * 2 * (size_t)std::max<int64_t>(1, sp->win_nblk);
+    sp->stamp_cap = (int)std::min<size_t>(STAMP_CAP, STAMP_BYTES / per);
+    SP_TRY(hipMalloc(&sp->stamps, per * sp->stamp_cap));
+    SP_TRY(hipDeviceGetAttribute(&sp->wall_khz, hipDeviceAttributeWallClockRate, sp->device));
   }
   hipLaunchKernelGGL(gpmi::timing_mark_kernel, dim3(1), dim3(64), 0, sp->stream, enable);
   SP_LAUNCH("timing_mark_kernel");
@@ -1711,10 +1739,18 @@ int gpmi_sp_spmm_timing(gpmi_sp* sp, int max_widths, int* n_widths, int* widths,
   std::map<int, std::pair<int, double>> acc;
   std::vector<unsigned long long> st;
   if (sp->stamps_used > 0) {
+    // every stamped launch's span, reduced on the device (after the logged work)
     SP_TRY(hipDeviceSynchronize());
+    unsigned long long* span = nullptr;
+    SP_TRY(hipMalloc(&span, sizeof(unsigned long long) * 2 * sp->stamps_used));
+    hipLaunchKernelGGL(gpmi::stamp_span_kernel, dim3(sp->stamps_used), dim3(256), 0, sp->stream,
+                       sp->stamps, sp->win_nblk, span);
+    SP_LAUNCH("stamp_span_kernel");
     st.resize((size_t)2 * sp->stamps_used);
-    SP_TRY(hipMemcpy(st.data(), sp->stamps, sizeof(unsigned long long) * st.size(),
-                     hipMemcpyDeviceToHost));
+    SP_TRY(hipMemcpyAsync(st.data(), span, sizeof(unsigned long long) * st.size(),
+                          hipMemcpyDeviceToHost, sp->stream));
+    SP_TRY(hipStreamSynchronize(sp->stream));
+    SP_TRY(hipFree(span));
   }
   for (auto& r : sp->spmm_log) {
     double ms = 0.0;
@@ -1759,13 +1795,26 @@ int gpmi_sp_bench_spmm(gpmi_sp* sp, int s, int reps, double eta, double* avg_ms)
   SP_TRY(hipEventCreate(&e1));
   rc = spmm(sp, sp->ws, sp->ws + ns, s, eta);   // warm-up
   if (rc) return rc;
+  // the timed launches wait behind a gate until all of them are queued (at most 2 s)
+  int* flag = nullptr;
+  SP_TRY(hipHostMalloc(&flag, sizeof(int), hipHostMallocCoherent));
+  *flag = 0;
+  int khz = 0;
+  SP_TRY(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, sp->device));
+  hipLaunchKernelGGL(gpmi::gate_kernel, dim3(1), dim3(64), 0, sp->stream, flag,
+                     (unsigned long long)std::max(khz, 1) * 2000ull);
+  SP_LAUNCH("gate_kernel");
   SP_TRY(hipEventRecord(e0, sp->stream));
-  for (int r = 0; r < reps; ++r) {
-    rc = spmm(sp, sp->ws, sp->ws + ns, s, eta);
-    if (rc) return rc;
+  for (int r = 0; r < reps && rc == 0; ++r) rc = spmm(sp, sp->ws, sp->ws + ns, s, eta);
+  __atomic_store_n(flag, 1, __ATOMIC_SEQ_CST);
+  if (rc) {
+    (void)hipStreamSynchronize(sp->stream);
+    (void)hipHostFree(flag);
+    return rc;
   }
   SP_TRY(hipEventRecord(e1, sp->stream));
   SP_TRY(hipEventSynchronize(e1));
+  SP_TRY(hipHostFree(flag));
   float ms = 0.f;
   SP_TRY(hipEventElapsedTime(&ms, e0, e1));
   *avg_ms = ms / reps;

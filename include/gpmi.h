@@ -234,7 +234,9 @@ int gpmi_sp_spmm_kernel(gpmi_sp* sp, int s, int* kind);
 int gpmi_sp_last_status(const gpmi_sp* sp, int* converged);
 
 /* Device-resident SpMM timing: reps launches of Y = (K + eta I) X with an
- * [n][s] block already in HBM; average ms per launch (HIP events). */
+ * [n][s] block already in HBM, queued behind a gate kernel that holds the stream
+ * until all of them are enqueued (so they run back to back, not at the host's
+ * launch rate); average ms per launch (HIP events). */
 int gpmi_sp_bench_spmm(gpmi_sp* sp, int s, int reps, double eta, double* avg_ms);
 /* In-step SpMM timing (measurement; no reference counterpart): while enabled,
  * every SpMM this operator launches (Lanczos, CG, multi-shift CG; either

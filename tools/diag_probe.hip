@@ -1,6 +1,7 @@
 // Phase timing of diag_block_kernel (diagnostic build with GPMI_DIAG_STAMPS).
-// Build: hipcc --offload-arch=gfx950 -O3 -DGPMI_DIAG_STAMPS -I../gaussian-process-param-estimation_amd/csrc \
-//        diag_probe.hip ../gaussian-process-param-estimation_amd/csrc/gpmi_diag.hip -o diag_probe
+// Build (from tools/): hipcc --offload-arch=gfx950 -O3 -DGPMI_DIAG_STAMPS -DGPMI_CHOL_STAMPS=1
+//        -I../gaussian-process-param-estimation_amd/csrc -I../include diag_probe.hip -o probe/diag_probe
+// (lds_chol_block's per-block phases print from the kernel, 10 ns units)
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
@@ -34,10 +35,9 @@ int main() {
     float ms; CK(hipEventElapsedTime(&ms, e0, e1));
     unsigned long long st[64];
     CK(hipMemcpyFromSymbol(st, HIP_SYMBOL(gpmi::g_diag_stamps), sizeof(st)));
-    printf("rep %d: %.1f us | load %llu", rep, ms * 1e3, st[1] - st[0]);
-    for (int jb = 0; jb < 8; ++jb)
-      printf(" | b%d F1 %llu F2 %llu F3 %llu", jb, st[2 + 3 * jb] - (jb ? st[1 + 3 * jb] : st[1]), st[3 + 3 * jb] - st[2 + 3 * jb], st[4 + 3 * jb] - st[3 + 3 * jb]);
-    printf(" | Lwrite %llu inv %llu Linvwrite %llu rhs %llu total %llu\n", st[26] - st[25], st[27] - st[26], st[28] - st[27], st[29] - st[28], st[29] - st[0]);
+    printf("rep %d: %.1f us (s_memtime cycles) load %llu chol %llu | Lwrite %llu inv+rhs-load %llu "
+           "Linvwrite %llu rhs %llu total %llu\n", rep, ms * 1e3, st[1] - st[0], st[26] - st[1],
+           st[26] - st[26], st[27] - st[26], st[28] - st[27], st[29] - st[28], st[29] - st[0]);
   }
   double hld[8]; CK(hipMemcpy(hld, ld, 64, hipMemcpyDeviceToHost));
   printf("logdet block0 %.12f\n", hld[0]);

@@ -23,7 +23,7 @@
 #   trace-band   kernel trace of two band reductions + the per-panel timeline
 #                (tools/band_timeline.py)
 #   host         the box's CPU / cgroup facts (host.txt)
-#   py:<file>    python -u <file> (a probe under tools/)
+#   py:<file>[:<arg>]   python -u <file> [<arg>] (a probe under tools/)
 set -o pipefail
 export TMPDIR=/tmp
 NAME=${1:?name}
@@ -105,9 +105,13 @@ for task in "$@"; do
     host)
       (nproc; cat /sys/fs/cgroup/cpu.max 2>/dev/null; python -c "import os; print('aff', len(os.sched_getaffinity(0)), 'omp', os.environ.get('OMP_NUM_THREADS'))"; lscpu | head -20) > $D/host.txt 2>&1 ;;
     py:*)
-      f=${task#py:}
-      run 900 $D/$(basename $f .py).log python -u $f
-      tail -30 $D/$(basename $f .py).log ;;
+      # py:<file>[:<arg>]
+      spec=${task#py:}
+      f=${spec%%:*}
+      arg=""
+      [ "$spec" != "$f" ] && arg=${spec#*:}
+      run 900 $D/$(basename $f .py)$arg.log python -u $f $arg
+      tail -30 $D/$(basename $f .py)$arg.log ;;
     *)
       echo "[gpu.sh] unknown task $task"; exit 2 ;;
   esac

@@ -4,7 +4,7 @@ usage: python tools/pmc_summary.py OUT.json NOTE dir1 [dir2 ...]
 PMC_FIRST=K (environment): also report, per kernel, the mean over its first K
 dispatches of each pass ('per_dispatch_first'), e.g. the timed call of a run
 that makes a second, differently sized call afterwards. PMC_MARKS=1: the mean over
-the dispatches between the last two timing_mark_kernel launches of each pass
+the dispatches between the first two timing_mark_kernel launches of each pass
 ('per_dispatch_timed': bench.py's timed steps).
 Each dir holds one pass's *_counter_collection.csv. Per kernel name (template
 and argument list stripped) it reports dispatch count, the summed counter
@@ -57,7 +57,7 @@ def main():
             for did in sorted(by)[-last_k:]:
                 for c, v in by[did].items():
                     last[k][c] += v / last_k
-    # PMC_MARKS=1: the mean over the dispatches between the last two timing_mark_kernel
+    # PMC_MARKS=1: the mean over the dispatches between the first two timing_mark_kernel
     # dispatches of each pass (bench.py's timed steps, gpmi_sp_set_timing)
     timed = defaultdict(lambda: defaultdict(float))
     timed_n = {}
@@ -68,7 +68,7 @@ def main():
                            'timing_mark_kernel' in k for d in by)
             if len(marks) < 2:
                 continue
-            lo, hi = marks[-2], marks[-1]
+            lo, hi = marks[0], marks[1]
             for (g, k), by in rows_by.items():
                 if g != f:
                     continue

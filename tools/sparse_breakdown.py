@@ -9,9 +9,12 @@ import numpy
 REPO = os.path.join(os.path.dirname(os.path.abspath(__file__)), '..')
 sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.join(REPO, 'gaussian-process-param-estimation_amd'))
+import torch  # noqa: E402
+torch.cuda.set_device(0)   # torch's HIP runtime first (as bench.py)
 import bench  # noqa: E402
 from gaussian_proc import generate_correlation, _data, _slq  # noqa: E402
 from gaussian_proc._mixed_correlation import MixedCorrelation  # noqa: E402
+from gaussian_proc.sweep import slq_gram_sweep  # noqa: E402
 
 cfg = sys.argv[1] if len(sys.argv) > 1 else 'sparse4'
 npts, dim, rho, nu, dens, nprobe, steps, neta = bench.SPARSE_CONFIGS[cfg]
@@ -26,7 +29,7 @@ etas = numpy.logspace(-2, 2, neta) + shift
 R = numpy.column_stack([X, z])
 for rep in range(4):
     t0 = time.perf_counter()
-    a, b = op.sop.lanczos(nprobe, steps, 0)
+    a, b = op.sop.lanczos(nprobe, steps, 0, orthogonalize=0)   # the step's (imate default)
     t1 = time.perf_counter()
     nodes = _slq.nodes(a, b)
     t2 = time.perf_counter()
@@ -34,6 +37,10 @@ for rep in range(4):
     t3 = time.perf_counter()
     G = op.sop.msgram(etas, R, rtol=1e-6)
     t4 = time.perf_counter()
+    slq_gram_sweep(op, etas, R, rtol=1e-6)
+    torch.cuda.synchronize()
+    t5 = time.perf_counter()
     print('%s rep %d: lanczos %.2f ms, nodes %.2f ms, quadrature %.2f ms, msgram %.2f ms '
-          '(%d CG iterations)' % (cfg, rep, (t1 - t0) * 1e3, (t2 - t1) * 1e3, (t3 - t2) * 1e3,
-                                  (t4 - t3) * 1e3, op.sop.last_cg_iterations))
+          '(%d CG iterations); both together (slq_gram_sweep) %.2f ms'
+          % (cfg, rep, (t1 - t0) * 1e3, (t2 - t1) * 1e3, (t3 - t2) * 1e3,
+             (t4 - t3) * 1e3, op.sop.last_cg_iterations, (t5 - t4) * 1e3))

@@ -81,10 +81,11 @@ def timed_spmm(trace_dir, bench_json, config=None):
                 elif kern in name and re.search(r'%s<%s,' % (kern, width), name):
                     rows.append(t)
     marks.sort()
-    # the timed window: the last on/off pair of marks before the isolated launches
-    # (the line's set_timing(True) then set_timing(False); earlier pairs: none)
+    # the timed window: the first on/off pair of marks (the line's set_timing(True)
+    # then set_timing(False) around the timed steps; the second pair brackets the
+    # isolated launches)
     assert len(marks) >= 2, marks
-    lo, hi = marks[-2], marks[-1]
+    lo, hi = marks[0], marks[1]
     timed = sorted(t for t in rows if lo <= t[0] <= hi)
     durs = [(e - s) / 1e6 for s, e in timed]
     avg = sum(durs) / len(durs)
