@@ -443,8 +443,8 @@ __global__ __launch_bounds__(64 * TPR) void csr_spmm_wing_kernel(
       }
   }
   if (pqp) {
-    // the block's x . y per column (the multi-shift CG's p . q), rows summed in order:
-    // pqp[b][c]; the window's LDS is free once every thread is past its products.
+    // the block's x . y per column (the Lanczos's u . Ku), rows summed in order:
+    // pqp[c][b]; the window's LDS is free once every thread is past its products.
     // dots2 (the Chronopoulos-Gear multi-shift CG, x = r, y = A r): the row
     // [x . y | x . x] of this block at pqp[b][2S] (summed by ms_cg2_reduce_kernel)
     const int WD = dots2 ? 2 * S : S;
@@ -460,7 +460,10 @@ __global__ __launch_bounds__(64 * TPR) void csr_spmm_wing_kernel(
     if (t < WD) {
       double sum = 0.0;
       for (int q = 0; q < nr; ++q) sum += red[q * WD + t];
-      pqp[b * WD + t] = sum;
+      // dots2: rows [b][2S] (ms_cg2_reduce_kernel); otherwise column-major [S][nblk]
+      // (lz0_alpha_kernel's per-column sums read it coalesced)
+      if (dots2) pqp[b * WD + t] = sum;
+      else pqp[(int64_t)t * gridDim.x + b] = sum;
     }
   }
   if (stamp) {
@@ -717,7 +720,8 @@ __global__ void lanczos_scalar_kernel(const double* __restrict__ H1k,
 // A last alpha launch (k = steps) forms beta_{steps-1}. Every reduction has a fixed
 // order (deterministic). st: [0, s) gamma_k, [s, 2s) gamma_{k-1}; coef [3][s].
 
-// out[b][c] = sum over the 64 rows of block b of X[i][c] Y[i][c] (fixed order).
+// out[c][b] = sum over the 64 rows of block b of X[i][c] Y[i][c] (fixed order;
+// column-major, as the window SpMM's epilogue).
 __global__ __launch_bounds__(256) void lz0_dot64_kernel(const double* __restrict__ X,
                                                         const double* __restrict__ Y, int64_t n,
                                                         int s, double* __restrict__ out) {
@@ -733,7 +737,7 @@ __global__ __launch_bounds__(256) void lz0_dot64_kernel(const double* __restrict
   if (t < s) {
     double a = 0.0;
     for (int i = 0; i < 64; ++i) a += sp[i * s + t];
-    out[(int64_t)blockIdx.x * s + t] = a;
+    out[(int64_t)t * gridDim.x + blockIdx.x] = a;
   }
 }
 
@@ -746,22 +750,26 @@ __global__ __launch_bounds__(256) void lz0_alpha_kernel(const double* __restrict
                                                         double* __restrict__ beta,
                                                         double* __restrict__ coef) {
   // one workgroup per column c: thread t sums blocks b = t, t + 256, ... of the three
-  // partial arrays (their loads in flight together, eight blocks at a time), then the
-  // four waves' sums combine in a fixed order (the round-3 form, one wave per column
-  // and one array after the other, took ~44 us at 4096 blocks)
+  // partial arrays (column-major [column][block]: coalesced; their loads in flight
+  // together, eight blocks at a time), then the four waves' sums combine in a fixed
+  // order (the round-3 form, one wave per column and one array after the other, took
+  // ~44 us at 4096 blocks; with [block][column] rows ~28 us in the cfg 5 step)
   const int c = blockIdx.x, t = threadIdx.x;
   __shared__ double red[3][4];
   const bool has1 = k < steps, has2 = k > 0;
+  const double* p1 = pq + (int64_t)c * nb;
+  const double* p2 = pv + (int64_t)c * nb;
+  const double* p3 = pv + (int64_t)(s + c) * nb;
   double a1 = 0.0, a2 = 0.0, a3 = 0.0;
   int b = t;
   for (; b + 7 * 256 < nb; b += 8 * 256) {
     double x1[8], x2[8], x3[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
-      const int64_t bq = b + q * 256;
-      x1[q] = has1 ? pq[bq * s + c] : 0.0;
-      x2[q] = has2 ? pv[bq * 2 * s + c] : 0.0;
-      x3[q] = has2 ? pv[bq * 2 * s + s + c] : 0.0;
+      const int bq = b + q * 256;
+      x1[q] = has1 ? p1[bq] : 0.0;
+      x2[q] = has2 ? p2[bq] : 0.0;
+      x3[q] = has2 ? p3[bq] : 0.0;
     }
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
@@ -771,10 +779,10 @@ __global__ __launch_bounds__(256) void lz0_alpha_kernel(const double* __restrict
     }
   }
   for (; b < nb; b += 256) {
-    if (has1) a1 += pq[(int64_t)b * s + c];
+    if (has1) a1 += p1[b];
     if (has2) {
-      a2 += pv[(int64_t)b * 2 * s + c];
-      a3 += pv[(int64_t)b * 2 * s + s + c];
+      a2 += p2[b];
+      a3 += p3[b];
     }
   }
   a1 = wave_sum(a1);
@@ -820,7 +828,7 @@ __global__ __launch_bounds__(256) void lz0_alpha_kernel(const double* __restrict
 }
 
 // u_{k+1} = c1 y - c2 u_{k-1} - c3 u_k per column, and per 64-row block b the partials
-// pv[b][0][c] = ||u_{k+1}||^2, pv[b][1][c] = u_{k+1} . u_k (fixed order).
+// pv[0][c][b] = ||u_{k+1}||^2, pv[1][c][b] = u_{k+1} . u_k (fixed order; column-major).
 __global__ __launch_bounds__(256) void lz0_update_kernel(const double* __restrict__ Y,
                                                          const double* __restrict__ Up,
                                                          const double* __restrict__ Uc,
@@ -830,20 +838,57 @@ __global__ __launch_bounds__(256) void lz0_update_kernel(const double* __restric
                                                          double* __restrict__ pv) {
   __shared__ double sq[64 * 32];
   __shared__ double sx[64 * 32];
+  __shared__ double sc[3 * 32];
   const int t = threadIdx.x;
   const int64_t r0 = (int64_t)blockIdx.x * 64;
   const int rows = (int)min((int64_t)64, n - r0);
-  for (int e = t; e < 64 * s; e += 256) {
-    const int i = e / s, c = e - i * s;
-    double w = 0.0, uc = 0.0;
-    if (i < rows) {
-      const int64_t g = r0 * s + e;
-      uc = Uc[g];
-      w = coef[c] * Y[g] - coef[s + c] * Up[g] - coef[2 * s + c] * uc;
-      Un[g] = w;
+  const int E = rows * s;   // the block's elements, contiguous from g0
+  const int64_t g0 = r0 * s;
+  if (t < 3 * s) sc[t] = coef[t];
+  for (int e = E + t; e < 64 * s; e += 256) sq[e] = sx[e] = 0.0;
+  __syncthreads();
+  const bool vec = ((reinterpret_cast<uintptr_t>(Y + g0) | reinterpret_cast<uintptr_t>(Up + g0) |
+                     reinterpret_cast<uintptr_t>(Uc + g0) | reinterpret_cast<uintptr_t>(Un + g0)) &
+                    15) == 0;
+  if (vec) {
+    // element pairs as 16-byte loads / stores; the pair's first column c advances by
+    // 512 mod s per iteration (no division in the loop)
+    const int step = 512 % s;
+    int c = (2 * t) % s;
+    for (int p = t; 2 * p + 1 < E; p += 256) {
+      const int e = 2 * p;
+      const d2 y = *reinterpret_cast<const d2*>(Y + g0 + e);
+      const d2 up = *reinterpret_cast<const d2*>(Up + g0 + e);
+      const d2 uc = *reinterpret_cast<const d2*>(Uc + g0 + e);
+      const int c1 = c + 1 == s ? 0 : c + 1;
+      const double w0 = sc[c] * y[0] - sc[s + c] * up[0] - sc[2 * s + c] * uc[0];
+      const double w1 = sc[c1] * y[1] - sc[s + c1] * up[1] - sc[2 * s + c1] * uc[1];
+      *reinterpret_cast<d2*>(Un + g0 + e) = d2{w0, w1};
+      sq[e] = w0 * w0;
+      sq[e + 1] = w1 * w1;
+      sx[e] = w0 * uc[0];
+      sx[e + 1] = w1 * uc[1];
+      c += step;
+      if (c >= s) c -= s;
     }
-    sq[e] = w * w;
-    sx[e] = w * uc;
+    if ((E & 1) && t == 0) {
+      const int e = E - 1, cc = e % s;
+      const double u = Uc[g0 + e];
+      const double w = sc[cc] * Y[g0 + e] - sc[s + cc] * Up[g0 + e] - sc[2 * s + cc] * u;
+      Un[g0 + e] = w;
+      sq[e] = w * w;
+      sx[e] = w * u;
+    }
+  } else {
+    for (int e = t; e < E; e += 256) {
+      const int c = e % s;
+      const int64_t g = g0 + e;
+      const double uc = Uc[g];
+      const double w = sc[c] * Y[g] - sc[s + c] * Up[g] - sc[2 * s + c] * uc;
+      Un[g] = w;
+      sq[e] = w * w;
+      sx[e] = w * uc;
+    }
   }
   __syncthreads();
   if (t < 2 * s) {
@@ -851,7 +896,7 @@ __global__ __launch_bounds__(256) void lz0_update_kernel(const double* __restric
     const int c = t < s ? t : t - s;
     double a = 0.0;
     for (int i = 0; i < 64; ++i) a += src[i * s + c];
-    pv[(int64_t)blockIdx.x * 2 * s + t] = a;
+    pv[(int64_t)t * gridDim.x + blockIdx.x] = a;
   }
 }
 
