@@ -500,12 +500,20 @@ def sparse_measure(args, config, world, rank, local, dist, torch, cpu, exact, de
               'logdet_diff_in_std_errors_max': round(float(numpy.max(numpy.abs(dz))), 3),
               'note': "the measured step uses imate's default orthogonalize=0 (plain "
                       "three-term recurrence); -1 is full reorthogonalisation (DCGS2)"}
-    # SpMM roofline from the timed steps: the width whose SpMM launches took the most
-    # device time (the multi-shift CG's s = 12, or the Lanczos's s = 20), its average
-    # in-step launch span; the same kernel isolated (50 back-to-back
-    # launches on a resident block) is reported beside it as isolated_ms
+    # SpMM roofline from the timed steps: the multi-shift CG's SpMM (its block width;
+    # the step's critical path: the step waits for the CG, which runs at the high
+    # dispatch priority, while the Lanczos beside it has slack and its launches' spans
+    # stretch around the CG's), else the width with the most device time; its
+    # average in-step launch span; the same kernel isolated (50 back-to-back launches
+    # on a resident block) is reported beside it as isolated_ms
     nnz = op.sop.nnz
-    s_blk = max(spmm_in_step, key=lambda w: spmm_in_step[w][1])
+    # the library pads a full 11-column block on the window SpMM to 12 (msgram_impl);
+    # a column shard (N > 1) runs unpadded: rank 0's shard width
+    clo0, chi0, _ = shard(R.shape[1], world, 0)
+    s_cg = (chi0 - clo0) + (1 if (world == 1 and R.shape[1] == 11 and
+                                  op.sop.spmm_kernel(11) == 'csr_spmm_wing_kernel') else 0)
+    s_blk = (s_cg if s_cg in spmm_in_step
+             else max(spmm_in_step, key=lambda w: spmm_in_step[w][1]))
     n_launch, tot_ms = spmm_in_step[s_blk]
     ms_span = tot_ms / n_launch
     # the stamps span a launch's first workgroup start to its last workgroup end; a
@@ -533,11 +541,6 @@ def sparse_measure(args, config, world, rank, local, dist, torch, cpu, exact, de
                                        (t / c * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
                 for w, (c, t) in sorted(spmm_in_step.items())}
     my_probes = shard(nprobe, world, rank)
-    # the library pads a full 11-column block on the window SpMM to 12 (msgram_impl);
-    # a column shard (N > 1) runs unpadded: rank 0's shard width
-    clo0, chi0, _ = shard(R.shape[1], world, 0)
-    s_cg = (chi0 - clo0) + (1 if (world == 1 and R.shape[1] == 11 and
-                                  op.sop.spmm_kernel(11) == 'csr_spmm_wing_kernel') else 0)
     sb = sparse_step_bytes(n, nnz, my_probes[1] - my_probes[0], steps, s_cg,
                            holder['cg_iters'], op.orthogonalize)
     step_s = dt / args.steps
