@@ -706,9 +706,6 @@ int gpmi_band_create(gpmi_op* op, gpmi_band** out) {
     snprintf(msg, sizeof(msg), "allocation of %s failed: %s", what, hipGetErrorString(err));
     return set_error(-(int)err, msg);
   };
-  // the three streams at the same (normal) dispatch priority: any of them high
-  // measured within +-0.4 ms of it (N = 16384: 135.5 ms all normal, 135.9-136.3 with
-  // the SYR2K's or the chain's stream high)
   if ((e = hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking)) != hipSuccess)
     return fail(e, "stream");
   if ((e = hipEventCreate(&b->ev0)) != hipSuccess) return fail(e, "event");
@@ -727,7 +724,15 @@ int gpmi_band_create(gpmi_op* op, gpmi_band** out) {
       hipSuccess)
     return fail(e, "CU count");
   if (b->lookahead) {
-    if ((e = hipStreamCreateWithFlags(&b->s_pan, hipStreamNonBlocking)) != hipSuccess)
+    // s_pan at the high dispatch priority. Alone, the priorities do not matter (135.5
+    // ms all normal, 135.9-136.3 with one stream high); in a process that holds other
+    // operators' streams (the bench line: the dense operator's) a high-priority stream
+    // gets a hardware queue of its own, while normal-priority streams beyond the
+    // process's GPU_MAX_HW_QUEUES (4) share queues and serialise: the bench line's
+    // reduction took 165.4 ms with all three at normal priority, 137 with this one high
+    int lo = 0, hi = 0;
+    if ((e = hipDeviceGetStreamPriorityRange(&lo, &hi)) != hipSuccess) return fail(e, "prio");
+    if ((e = hipStreamCreateWithPriority(&b->s_pan, hipStreamNonBlocking, hi)) != hipSuccess)
       return fail(e, "panel stream");
     for (hipEvent_t* ev : {&b->ev_col, &b->ev_pan})
       if ((e = hipEventCreateWithFlags(ev, hipEventDisableTiming)) != hipSuccess)
