@@ -141,6 +141,14 @@ def pmc_traffic_sparse(config, kernel='gpmi::csr_spmm_kernel', width=None):
     return None, None
 
 
+def curve_sha(rows):
+    """SHA-256 of the gathered [eta, logdet, lp] rows (float64, C order): equal digests
+    at N = 1 and N > 1 mean the curves agree bit for bit."""
+    import hashlib
+    return hashlib.sha256(numpy.ascontiguousarray(numpy.asarray(rows, dtype=numpy.float64))
+                          .tobytes()).hexdigest()
+
+
 def host_info():
     """The host the CPU baseline runs on: model, logical CPUs, physical cores,
     and the CPUs this job may use (affinity, cgroup quota, OMP_NUM_THREADS: the
@@ -609,6 +617,7 @@ def sparse_measure(args, config, world, rank, local, dist, torch, cpu, exact, de
                 'lanczos_orthogonalize': op.orthogonalize,
                 'model': 'bench.sparse_step_bytes (each vector block once per pass)'},
             'lp_sample': [float(v) for v in last[0].tolist()],
+            'curve_sha256': curve_sha(last),
             'cpu_baseline': None,
         }
         ref = sparse_reference_check(op, config, X, z, exact)
@@ -676,7 +685,7 @@ def sparse_modes(args, world, rank, local, dist, torch):
         out[cfg] = {k: r[k] for k in ('metric', 'value', 'unit', 'n_gpus', 'ms_per_step',
                                       'steps', 'warmup', 'scaling', 'roofline',
                                       'step_roofline', 'cpu_baseline', 'lp_sample',
-                                      'lanczos_orthogonalize') if k in r}
+                                      'curve_sha256', 'lanczos_orthogonalize') if k in r}
         out[cfg]['parallelism'] = r['config']['parallelism']
         out[cfg]['workload'] = r['config']['workload']
         out[cfg]['assembly_s'] = r['config']['assembly_s']
@@ -863,6 +872,7 @@ def band_mode(args, D, X, z, world, rank, dist, torch, ld_ref=None):
         'reduction_mfma_frac': round(flops_red / (red * 1e-3) / 1e12 / FP64_MFMA_PEAK_TFLOPS, 4),
         'panel': b.stats(),
         'lp_sample': [float(v) for v in last[0].tolist()],
+        'curve_sha256': curve_sha(last),
     }
     ld_err, lp_err = golden_errors(lambda e: op.loglik_terms(e, X, z), args.nu, n, m)
     out['logdet_rel_err_vs_reference'] = ld_err
@@ -1360,6 +1370,7 @@ def main():
             'whole_eval_mfma_frac': round(whole / FP64_MFMA_PEAK_TFLOPS, 4),
             'flops_per_eval': flops_eval,
             'lp_sample': [float(v) for v in last[0].tolist()] if last is not None else None,
+            'curve_sha256': curve_sha(last) if last is not None else None,
             'cpu_baseline': None,
             'devices': devices,
         }
