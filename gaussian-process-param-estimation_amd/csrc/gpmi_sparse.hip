@@ -446,7 +446,7 @@ __global__ __launch_bounds__(64 * TPR) void csr_spmm_wing_kernel(
     // the block's x . y per column (the Lanczos's u . Ku), rows summed in order:
     // pqp[c][b]; the window's LDS is free once every thread is past its products.
     // dots2 (the Chronopoulos-Gear multi-shift CG, x = r, y = A r): the row
-    // [x . y | x . x] of this block at pqp[b][2S] (summed by ms_cg2_reduce_kernel)
+    // [x . y | x . x] of this block at pqp[0 .. 2S)[b] (summed by ms_cg2_reduce_kernel)
     const int WD = dots2 ? 2 * S : S;
     __syncthreads();
     double* red = smem;   // [64][WD]
@@ -460,10 +460,9 @@ __global__ __launch_bounds__(64 * TPR) void csr_spmm_wing_kernel(
     if (t < WD) {
       double sum = 0.0;
       for (int q = 0; q < nr; ++q) sum += red[q * WD + t];
-      // dots2: rows [b][2S] (ms_cg2_reduce_kernel); otherwise column-major [S][nblk]
-      // (lz0_alpha_kernel's per-column sums read it coalesced)
-      if (dots2) pqp[b * WD + t] = sum;
-      else pqp[(int64_t)t * gridDim.x + b] = sum;
+      // column-major [WD][nblk]: the per-column sums (lz0_alpha_kernel,
+      // ms_cg2_reduce_kernel) read it coalesced
+      pqp[(int64_t)t * gridDim.x + b] = sum;
     }
   }
   if (stamp) {
@@ -1324,7 +1323,7 @@ void launch_ms_dots(const double* B, const double* R, int64_t n, int s, double* 
 // active columns,
 //   s_k = w_k + beta_{k-1} s_{k-1}  (= A p_k, p_k = r_k + beta_{k-1} p_{k-1}),
 //   r_{k+1} = r_k - alpha_k s_k,
-// and the block rows of B^T r_{k+1} on fp64 MFMA (as ms_rmfma_kernel) into bpart,
+// and the block partials of B^T r_{k+1} on fp64 MFMA into bpart ([neb][MS_UB]),
 // which the next iteration's reduction sums. p itself is never formed: the Gram
 // blocks need only b . p of the shifted systems, which the shift recurrences carry
 // from B^T r (so a pass reads r, w, s and B and writes s and r: six block passes,
@@ -1400,7 +1399,7 @@ __global__ __launch_bounds__(256) void ms_cg2_update_kernel(
     for (int e = t; e < neb; e += 256) {
       const int cp = e / s, cc = e - cp * s;
       const int idx = cp * 16 + cc;
-      bpart[(int64_t)vb * neb + e] = (red[0][idx] + red[1][idx]) + (red[2][idx] + red[3][idx]);
+      bpart[(int64_t)e * nvb + vb] = (red[0][idx] + red[1][idx]) + (red[2][idx] + red[3][idx]);
     }
     return;
   }
@@ -1463,9 +1462,10 @@ __global__ __launch_bounds__(256) void ms_cg2_update_kernel(
 }
 
 // The sums one iteration of ms_cg2_update_kernel needs, one workgroup per output
-// element e: e < 2 s the SpMM's block rows of [r . w | r . r] (rows_a rows of 2 s),
-// else the previous update's block rows of B^T r (rows_b rows of ne_b). Thread t sums
-// rows t, t + 256, ... (eight loads in flight), then the four waves in a fixed order.
+// element e: e < 2 s the SpMM's block partials of [r . w | r . r] ([2 s][rows_a]),
+// else the previous update's block partials of B^T r ([ne_b][rows_b]); column-major,
+// so element e's partials are contiguous. Thread t sums partials t, t + 256, ...
+// (eight loads in flight), then the four waves in a fixed order.
 __global__ __launch_bounds__(256) void ms_cg2_reduce_kernel(const double* __restrict__ pa,
                                                             int rows_a, int s,
                                                             const double* __restrict__ pb,
@@ -1474,26 +1474,27 @@ __global__ __launch_bounds__(256) void ms_cg2_reduce_kernel(const double* __rest
   __shared__ double w4[4];
   const int e = blockIdx.x, t = threadIdx.x;
   const bool first = e < 2 * s;
-  const double* src = first ? pa + e : pb + (e - 2 * s);
+  // column-major partials: element e's rows are contiguous (coalesced)
   const int rows = first ? rows_a : rows_b;
-  const int64_t ld = first ? 2 * s : ne_b;
+  const double* src = first ? pa + (int64_t)e * rows_a : pb + (int64_t)(e - 2 * s) * rows_b;
+  (void)ne_b;
   double a = 0.0;
   int b = t;
   for (; b + 7 * 256 < rows; b += 8 * 256) {
     double x[8];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) x[q] = src[(int64_t)(b + q * 256) * ld];
+    for (int q = 0; q < 8; ++q) x[q] = src[b + q * 256];
 #pragma unroll
     for (int q = 0; q < 8; ++q) a += x[q];
   }
-  for (; b < rows; b += 256) a += src[(int64_t)b * ld];
+  for (; b < rows; b += 256) a += src[b];
   a = wave_sum(a);
   if ((t & 63) == 0) w4[t >> 6] = a;
   __syncthreads();
   if (t == 0) out[e] = (w4[0] + w4[1]) + (w4[2] + w4[3]);
 }
 
-// Group rows of x . y and x . x per column ([blockIdx.x][2s]: x . y, then x . x) for
+// Group rows of x . y and x . x per column ([2s][gridDim.x]: x . y, then x . x) for
 // SpMM kinds without the dot epilogue: MS_DOT_BLK blocks, each a contiguous range of
 // rows, rows_per = 256 / s rows per block pass, summed in a fixed order.
 __global__ __launch_bounds__(256) void ms_dots2_kernel(const double* __restrict__ X,
@@ -1521,8 +1522,8 @@ __global__ __launch_bounds__(256) void ms_dots2_kernel(const double* __restrict_
       a += red[0][q * s + t];
       b += red[1][q * s + t];
     }
-    out[(int64_t)blockIdx.x * 2 * s + t] = a;
-    out[(int64_t)blockIdx.x * 2 * s + s + t] = b;
+    out[(int64_t)t * gridDim.x + blockIdx.x] = a;
+    out[(int64_t)(s + t) * gridDim.x + blockIdx.x] = b;
   }
 }
 
