@@ -93,6 +93,19 @@ __device__ __forceinline__ double fo_entry(double g, int r, int c) {
   return r > c ? -g : (r == c ? 1.0 - 0.5 * (g - 1.0) : 0.0);
 }
 
+// out (row-major 128 x 128) = the lower triangle of the LDS block S (row stride DL),
+// zeros above: two doubles per store, eight rows' LDS reads in flight together (one
+// element per iteration waited out each LDS read: ~4 us per block).
+__device__ __forceinline__ void store_lower_pairs(const double* S, double* __restrict__ out) {
+  const int t = threadIdx.x;
+#pragma unroll 8
+  for (int it = 0; it < 32; ++it) {
+    const int e = it * 256 + t, r = e >> 6, c = (e & 63) * 2;
+    const d2 v = *reinterpret_cast<const d2*>(&S[r * DL + c]);
+    *reinterpret_cast<d2*>(out + 2 * e) = d2{c <= r ? v[0] : 0.0, c + 1 <= r ? v[1] : 0.0};
+  }
+}
+
 // L = chol(G + shift I) (lower), L^-1 (lower), both row-major 128 x 128 with
 // zeros above the diagonal. pass 0 adds the shift coef * trace(G); pass 2
 // checks L against I.
@@ -109,7 +122,7 @@ __global__ __launch_bounds__(256) void cq_chol_kernel(const double* __restrict__
                                                       int* __restrict__ fo,
                                                       int* __restrict__ fail,
                                                       unsigned* __restrict__ ctr) {
-  __shared__ double Ls[TS * DL];
+  __shared__ __attribute__((aligned(16))) double Ls[TS * DL];
   __shared__ double Aux[TS * RLD];
   __shared__ double sdiag[TS];
   __shared__ double sred[4];
@@ -152,11 +165,15 @@ __global__ __launch_bounds__(256) void cq_chol_kernel(const double* __restrict__
   __syncthreads();
   int bad = s_fail;
   double dev = 0.0;
-  for (int e = t; e < TS * TS; e += 256) {
-    const int r = e >> 7, c = e & 127;
-    const double v = (c <= r) ? Ls[r * DL + c] : 0.0;
-    Lout[e] = v;
-    if (pass == 2) dev = fmax(dev, fabs(v - (c == r ? 1.0 : 0.0)));
+  // lower part out two doubles per store, eight rows' LDS reads in flight together
+#pragma unroll 8
+  for (int it = 0; it < 32; ++it) {
+    const int e = it * 256 + t, r = e >> 6, c = (e & 63) * 2;
+    const d2 v = *reinterpret_cast<const d2*>(&Ls[r * DL + c]);
+    const d2 o = {c <= r ? v[0] : 0.0, c + 1 <= r ? v[1] : 0.0};
+    *reinterpret_cast<d2*>(Lout + 2 * e) = o;
+    if (pass == 2)
+      dev = fmax(dev, fmax(fabs(o[0] - (c == r ? 1.0 : 0.0)), fabs(o[1] - (c + 1 == r ? 1.0 : 0.0))));
   }
   if (pass == 2) {
     // a NaN fails the test too (!(dev <= tol))
@@ -168,10 +185,7 @@ __global__ __launch_bounds__(256) void cq_chol_kernel(const double* __restrict__
   __syncthreads();   // every thread is done reading L before the inverse overwrites it
   lds_inv_block(Ls, Aux);
   __syncthreads();
-  for (int e = t; e < TS * TS; e += 256) {
-    const int r = e >> 7, c = e & 127;
-    Linv[e] = (c <= r) ? Ls[r * DL + c] : 0.0;
-  }
+  store_lower_pairs(Ls, Linv);
 }
 
 // Row tiles of 64: m / 64 workgroups of two per CU (67.6 KB of LDS each), so the
@@ -364,7 +378,7 @@ __global__ __launch_bounds__(256) void cq_recon_kernel(const double* __restrict_
                                                        int* __restrict__ fo,
                                                        int* __restrict__ fail,
                                                        double* __restrict__ US) {
-  __shared__ double A[TS * DL];
+  __shared__ __attribute__((aligned(16))) double A[TS * DL];
   __shared__ double Aux[TS * RLD];
   __shared__ double sS[TS];
   __shared__ double sdiag[TS];
@@ -429,10 +443,7 @@ __global__ __launch_bounds__(256) void cq_recon_kernel(const double* __restrict_
   }
   __syncthreads();
   CQST(1);
-  for (int e = t; e < TS * TS; e += 256) {
-    const int r = e >> 7, c = e & 127;
-    Linv3[e] = (c <= r) ? A[r * DL + c] : 0.0;
-  }
+  store_lower_pairs(A, Linv3);
   CQST(2);
   // ---- Q3t = Q2t M3^T (M3 lower: output column block cb needs k < 16 (cb + 1)): wave
   // w forms the column blocks w and 7 - w of all eight row blocks, 9 of the 36 units
@@ -571,11 +582,18 @@ __global__ __launch_bounds__(256) void cq_recon_kernel(const double* __restrict_
     __syncthreads();
   }
   CQST(4);
-  // V1 (strictly lower, into the panel's top block) and the signs / tau out
-  for (int e = t; e < TS * TS; e += 256) {
-    const int r = e >> 7, c = e & 127;
-    if (c < r) P[(int64_t)r * lda + c] = A[r * DL + c];
-    if (US) US[e] = c >= r ? A[r * DL + c] * sS[c] : 0.0;   // U S, for cq_t_kernel
+  // V1 (strictly lower, into the panel's top block) and U S (for cq_t_kernel) out, two
+  // doubles per store, eight rows' LDS reads in flight together; the signs / tau
+#pragma unroll 8
+  for (int it = 0; it < 32; ++it) {
+    const int e = it * 256 + t, r = e >> 6, c = (e & 63) * 2;
+    const d2 v = *reinterpret_cast<const d2*>(&A[r * DL + c]);
+    double* pr = P + (int64_t)r * lda + c;
+    if (c + 1 < r) *reinterpret_cast<d2*>(pr) = v;
+    else if (c < r) pr[0] = v[0];
+    if (US)
+      *reinterpret_cast<d2*>(US + 2 * e) =
+          d2{c >= r ? v[0] * sS[c] : 0.0, c + 1 >= r ? v[1] * sS[c + 1] : 0.0};
   }
   if (t < TS) {
     S[t] = sS[t];
@@ -585,9 +603,19 @@ __global__ __launch_bounds__(256) void cq_recon_kernel(const double* __restrict_
   __syncthreads();
   // U^T into the lower triangle (each lower slot is written by the one thread
   // that reads its mirror), then U^-T by the LDS triangular inverse
-  for (int e = t; e < TS * TS; e += 256) {
-    const int r = e >> 7, c = e & 127;
-    if (r > c) A[r * DL + c] = A[c * DL + r];
+  // (upper entries read, lower written: disjoint, so eight reads go out before the writes)
+  for (int it0 = 0; it0 < TS * TS / 256; it0 += 8) {
+    double u[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int e = (it0 + q) * 256 + t, r = e >> 7, c = e & 127;
+      u[q] = r > c ? A[c * DL + r] : 0.0;
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int e = (it0 + q) * 256 + t, r = e >> 7, c = e & 127;
+      if (r > c) A[r * DL + c] = u[q];
+    }
   }
   __syncthreads();
   CQST(5);
