@@ -350,7 +350,7 @@ int run_factor(gpmi_op* op, const double* etas_host, int nb, const double* rhs_d
     const int h = nb / 2;
     if (!op->stream3) {
       HIP_TRY(hipStreamCreateWithFlags(&op->stream3, hipStreamNonBlocking));
-      HIP_TRY(hipEventCreateWithFlags(&op->ev_g, hipEventDisableTiming));
+      HIP_TRY(hipEventCreateWithFlags(&op->ev_g, sync_event_flags()));
     }
     HIP_TRY(hipEventRecord(op->ev_fork, s));
     HIP_TRY(hipStreamWaitEvent(op->stream3, op->ev_fork, 0));
@@ -601,9 +601,9 @@ int gpmi_op_create(int device, int64_t n, int max_batch, gpmi_op** out) {
   // the process's hardware queues (GPU_MAX_HW_QUEUES = 4) share queues and slow other
   // objects' multi-stream work, a band reduction beside a dense operator holding three
   // streams: 161 -> 181 ms)
-  if ((e = hipEventCreateWithFlags(&op->ev_fork, hipEventDisableTiming)) != hipSuccess)
+  if ((e = hipEventCreateWithFlags(&op->ev_fork, sync_event_flags())) != hipSuccess)
     return fail(e, "event");
-  if ((e = hipEventCreateWithFlags(&op->ev_join, hipEventDisableTiming)) != hipSuccess)
+  if ((e = hipEventCreateWithFlags(&op->ev_join, sync_event_flags())) != hipSuccess)
     return fail(e, "event");
 #define ALLOC(ptr, count)                                                           \
   if ((e = hipMalloc(&op->ptr, sizeof(*op->ptr) * (size_t)(count))) != hipSuccess)  \

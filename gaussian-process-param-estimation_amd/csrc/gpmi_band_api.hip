@@ -735,13 +735,13 @@ int gpmi_band_create(gpmi_op* op, gpmi_band** out) {
     if ((e = hipStreamCreateWithPriority(&b->s_pan, hipStreamNonBlocking, hi)) != hipSuccess)
       return fail(e, "panel stream");
     for (hipEvent_t* ev : {&b->ev_col, &b->ev_pan})
-      if ((e = hipEventCreateWithFlags(ev, hipEventDisableTiming)) != hipSuccess)
+      if ((e = hipEventCreateWithFlags(ev, sync_event_flags())) != hipSuccess)
         return fail(e, "event");
   }
-  if ((e = hipEventCreateWithFlags(&b->ev_q, hipEventDisableTiming)) != hipSuccess)
+  if ((e = hipEventCreateWithFlags(&b->ev_q, sync_event_flags())) != hipSuccess)
     return fail(e, "event");
-  if ((e = hipEventCreateWithFlags(&b->ev_v, hipEventDisableTiming)) != hipSuccess ||
-      (e = hipEventCreateWithFlags(&b->ev_t, hipEventDisableTiming)) != hipSuccess)
+  if ((e = hipEventCreateWithFlags(&b->ev_v, sync_event_flags())) != hipSuccess ||
+      (e = hipEventCreateWithFlags(&b->ev_t, sync_event_flags())) != hipSuccess)
     return fail(e, "event");
 #define BALLOC(ptr, count)                                                          \
   if ((e = hipMalloc(&b->ptr, sizeof(double) * (size_t)(count))) != hipSuccess)     \
@@ -772,7 +772,7 @@ int gpmi_band_create(gpmi_op* op, gpmi_band** out) {
   BALLOC(cqMinv, TS * TS);
   BALLOC(cqUS, (int64_t)nt * TS * TS);
   BALLOC(cqW, (int64_t)nt * TS * TS);
-  if ((e = hipEventCreateWithFlags(&b->ev_rc, hipEventDisableTiming)) != hipSuccess)
+  if ((e = hipEventCreateWithFlags(&b->ev_rc, sync_event_flags())) != hipSuccess)
     return fail(e, "event");
   b->t_from_q.assign((size_t)nt, 0);
   b->v_in_u.assign((size_t)nt, 0);

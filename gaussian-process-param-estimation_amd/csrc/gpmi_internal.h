@@ -3,6 +3,7 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #define GPMI_MAX_DIM 8     // max point dimension handled by the assembly kernel
 #define GPMI_TS 128        // tile / diagonal-block size of the blocked Cholesky
@@ -11,6 +12,19 @@
 struct gpmi_sp;   // include/gpmi.h
 
 namespace gpmi {
+
+// Flags of the events that only order one device's streams (never read by the host):
+// no timing, and no system-scope fence on record (the default release writes back and
+// invalidates caches for host visibility, which a consumer kernel on the same device
+// does not need). GPMI_EV_SYSFENCE=1 restores the system-scope fence (A/B).
+inline unsigned sync_event_flags() {
+  static const unsigned f = [] {
+    const char* e = getenv("GPMI_EV_SYSFENCE");
+    return (unsigned)hipEventDisableTiming |
+           ((e && e[0] == '1') ? 0u : (unsigned)hipEventDisableSystemFence);
+  }();
+  return f;
+}
 
 enum MaternMode { MATERN_HALF = 0, MATERN_3HALF = 1, MATERN_5HALF = 2,
                   MATERN_GENERAL = 3, MATERN_GAUSS = 4 };
