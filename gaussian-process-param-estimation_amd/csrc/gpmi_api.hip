@@ -176,7 +176,7 @@ int launch_syrk(gpmi_op* op, hipStream_t st, int b0, int nb, int tc0, int w, int
     if ((int)op->ev.size() < evi + 2) {
       for (int k = 0; k < 64; ++k) {
         hipEvent_t e;
-        HIP_TRY(hipEventCreate(&e));
+        HIP_TRY(hipEventCreateWithFlags(&e, timing_event_flags()));
         op->ev.push_back(e);
       }
     }
@@ -320,8 +320,8 @@ int run_factor(gpmi_op* op, const double* etas_host, int nb, const double* rhs_d
   ++op->factor_gen;
   if (op->timing) {
     if (!op->ev_begin) {
-      HIP_TRY(hipEventCreate(&op->ev_begin));
-      HIP_TRY(hipEventCreate(&op->ev_end));
+      HIP_TRY(hipEventCreateWithFlags(&op->ev_begin, timing_event_flags()));
+      HIP_TRY(hipEventCreateWithFlags(&op->ev_end, timing_event_flags()));
     }
     HIP_TRY(hipEventRecord(op->ev_begin, s));
   }

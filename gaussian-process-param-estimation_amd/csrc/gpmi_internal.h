@@ -25,6 +25,11 @@ inline unsigned sync_event_flags() {
   }();
   return f;
 }
+// Timing events (elapsed time only; the host never reads memory behind them): timing
+// kept, the system-scope fence dropped the same way.
+inline unsigned timing_event_flags() {
+  return sync_event_flags() & ~(unsigned)hipEventDisableTiming;
+}
 
 enum MaternMode { MATERN_HALF = 0, MATERN_3HALF = 1, MATERN_5HALF = 2,
                   MATERN_GENERAL = 3, MATERN_GAUSS = 4 };

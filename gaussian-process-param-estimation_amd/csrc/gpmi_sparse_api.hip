@@ -451,7 +451,7 @@ int take_event(gpmi_sp* sp, hipEvent_t* e) {
     sp->ev_pool.pop_back();
     return 0;
   }
-  SP_TRY(hipEventCreate(e));
+  SP_TRY(hipEventCreateWithFlags(e, gpmi::timing_event_flags()));
   return 0;
 }
 
