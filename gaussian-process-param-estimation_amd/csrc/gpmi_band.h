@@ -74,13 +74,14 @@ __global__ void tn_partial_q_kernel(const double* P1, int64_t ld1, const double*
                                     int m, double* part);
 __global__ void z_q_kernel(const double* T, const double* M, double* Zh);
 __global__ void w_q_kernel(const double* X, double* U, int64_t ldu, const double* Zh);
-__global__ void syr2k_col_q_kernel(double* A, int64_t lda, const double* U, int64_t ldu, int tr0);
+__global__ void syr2k_col_q_kernel(double* A, int64_t lda, const double* U, int64_t ldu, int tr0,
+                                   const double* Ksrc);
 __global__ void syr2k_kernel(double* A, int64_t lda, const double* U, int64_t ldu, int tr0,
                              int mt);
 __global__ void syr2k_rest_kernel(double* A, int64_t lda, const double* U, int64_t ldu, int tr0,
                                   int mt, const uint32_t* order);
 __global__ void syr2k_pipe_kernel(double* A, int64_t lda, const double* U, int64_t ldu, int tr0,
-                                  int mt, int* cnt, int nmain, int filler);
+                                  int mt, int* cnt, int nmain, int filler, const double* Ksrc);
 __global__ void bcr_f0_kernel(const double* Ab, int64_t lda, double* F0);
 __global__ void bcr_chol_kernel(const double* Ab, int64_t lda, const double* etas, int lvl,
                                 int first, const double* Din, int64_t sD, const double* Yin,

@@ -615,14 +615,18 @@ __global__ __launch_bounds__(256, 2) void w_q_kernel(const double* __restrict__ 
 
 // Tile column 0 of the trailing update (the next panel's columns, look-ahead):
 // A_I0 -= [W_I V_I] [V_0 W_0]^T, one quadrant per workgroup.
+// Ksrc (the first panel's update): C is read from K, the reduction's source, instead of
+// A, so A never needs K's copy right of tile column 0.
 __global__ __launch_bounds__(256, 2) void syr2k_col_q_kernel(double* __restrict__ A, int64_t lda,
                                                              const double* __restrict__ U,
-                                                             int64_t ldu, int tr0) {
+                                                             int64_t ldu, int tr0,
+                                                             const double* __restrict__ Ksrc) {
   __shared__ double smem[Q2_SMEM];
   const int I = tr0 + blockIdx.x, q = blockIdx.y;
-  double* C = A + (int64_t)I * TS * lda + (int64_t)tr0 * TS;
+  const int64_t off = (int64_t)I * TS * lda + (int64_t)tr0 * TS;
+  double* C = A + off;
   d4 acc[2][2];
-  load_quad(C, lda, acc, q >> 1, q & 1);
+  load_quad((Ksrc ? Ksrc : A) + off, lda, acc, q >> 1, q & 1);
   gemm_quad2<KFAST, KFAST, true, 2 * TS>(U + (int64_t)I * TS * ldu, ldu,
                                          U + (int64_t)tr0 * TS * ldu + TS, ldu, smem, acc,
                                          q >> 1, q & 1);
@@ -705,7 +709,8 @@ __global__ __launch_bounds__(256, 1) void syr2k_pipe_kernel(double* __restrict__
                                                             const double* __restrict__ U,
                                                             int64_t ldu, int tr0, int mt,
                                                             int* __restrict__ cnt, int nmain,
-                                                            int filler) {
+                                                            int filler,
+                                                            const double* __restrict__ Ksrc) {
   __shared__ double smem[4 * GSTAGE + 2];
   int* stk = reinterpret_cast<int*>(smem + 4 * GSTAGE);   // [0] next ticket, [1] first
   constexpr int KD = 2 * TS;
@@ -741,11 +746,13 @@ __global__ __launch_bounds__(256, 1) void syr2k_pipe_kernel(double* __restrict__
   auto cidx = [&](int e) -> int64_t {   // e = a * 16 + c * 4 + r
     return (int64_t)((e >> 4) * 16 + 4 * (e & 3)) * lda + ((e >> 2) & 3) * 16;
   };
+  // C tiles are read from Ksrc when given (the first panel's update; the same offsets)
+  auto csrc = [&](const double* c) -> const double* { return Ksrc ? Ksrc + (c - A) : c; };
   d4 acc[4][4], cn[4][4], po[4][4];
   double* Cq;
   const double *P1, *P2;
   tile_ptrs(q, &Cq, &P1, &P2);
-  load_tile(Cq, lda, acc);
+  load_tile(csrc(Cq), lda, acc);
   d2 ra[4], rb[4];
   gl_op<KFAST>(P1, ldu, 0, ra);
   gl_op<KFAST>(P2, ldu, 0, rb);
@@ -760,6 +767,7 @@ __global__ __launch_bounds__(256, 1) void syr2k_pipe_kernel(double* __restrict__
     double* Cn = nullptr;
     const double *N1 = nullptr, *N2 = nullptr;
     if (has_n) tile_ptrs(qn, &Cn, &N1, &N2);
+    const double* Cns = has_n ? csrc(Cn) : nullptr;
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
       const int cur = s & 1;
@@ -783,7 +791,7 @@ __global__ __launch_bounds__(256, 1) void syr2k_pipe_kernel(double* __restrict__
 #pragma unroll
         for (int u = 0; u < PER; ++u) {
           const int e = s * PER + u;
-          if (e < 64) cn[e >> 4][(e >> 2) & 3][e & 3] = Cn[coff + cidx(e)];
+          if (e < 64) cn[e >> 4][(e >> 2) & 3][e & 3] = Cns[coff + cidx(e)];
         }
       }
       if (has_p) {

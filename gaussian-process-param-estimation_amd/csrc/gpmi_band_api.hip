@@ -127,6 +127,7 @@ struct gpmi_band {
   int* cqflag = nullptr;     // [nt][8]: [0..2] first-order flag per pass, [3] CholeskyQR
                              // succeeded, [4] failed (the guarded Householder panel ran),
                              // [6] the look-ahead SYR2K's tile tickets
+  bool poison = false;          // GPMI_BAND_POISON=1: Ab set to NaN before a K-first copy
   int cq_panel_fallbacks = 0;   // panels factored by the guarded Householder panel, or
                                 // (past its single-launch size) by per-column launches
   int cq_host_checks = 0;       // panels past the single-launch size whose flag the host read
@@ -456,10 +457,22 @@ int band_reduce_pass(gpmi_band* b, const double* K, const std::vector<double>* y
     BD_TRY(hipMemcpyAsync(b->Y, yh->data(), sizeof(double) * yh->size(), hipMemcpyHostToDevice,
                           b->side));
   }
-  BD_TRY(hipMemcpyAsync(b->Ab, K, sizeof(double) * np * np, hipMemcpyDeviceToDevice, s));
   std::fill(b->t_from_q.begin(), b->t_from_q.end(), 0);
   std::fill(b->v_in_u.begin(), b->v_in_u.end(), 0);
   const bool la = mode != 2 && b->lookahead && b->s_pan;
+  // The pipelined CholeskyQR form copies only tile column 0 of K into the working matrix:
+  // the first panel's SYMM reads A22 from K, and its update (the tile column and the
+  // pipelined SYR2K) reads its C tiles from K and writes them to Ab, which holds the
+  // lower triangle from then on (the upper one is never read). 2 GB -> 16 MB at N = 16384
+  // (the copy took 0.8 ms). Every other form copies all of K.
+  const bool k_first = mode == 0 && la && nt > 2;
+  if (k_first && b->poison)   // (tests: NaN wherever the reduction would read unwritten Ab)
+    BD_TRY(hipMemsetAsync(b->Ab, 0xff, sizeof(double) * np * np, s));
+  if (k_first)
+    BD_TRY(hipMemcpy2DAsync(b->Ab, sizeof(double) * np, K, sizeof(double) * np,
+                            sizeof(double) * TS, np, hipMemcpyDeviceToDevice, s));
+  else
+    BD_TRY(hipMemcpyAsync(b->Ab, K, sizeof(double) * np * np, hipMemcpyDeviceToDevice, s));
   bool ahead = false;   // panel j already factored by the previous look-ahead
   for (int j = 0; j + 1 < nt; ++j) {
     const int64_t r0 = (int64_t)(j + 1) * TS, c0 = (int64_t)j * TS;
@@ -508,8 +521,9 @@ int band_reduce_pass(gpmi_band* b, const double* K, const std::vector<double>* y
     }
     const int chunk = symm_chunk(mt, 2 * b->ncu);
     const int sch = (mt + chunk - 1) / chunk;
-    hipLaunchKernelGGL(symm_kernel, dim3(mt, sch), dim3(256), 0, s, b->Ab, np, b->U,
-                       (int64_t)BAND_ULD, j + 1, mt, chunk, b->Xp);
+    const double* ksrc = (k_first && j == 0) ? K : nullptr;   // panel 0: C and A22 from K
+    hipLaunchKernelGGL(symm_kernel, dim3(mt, sch), dim3(256), 0, s, ksrc ? ksrc : b->Ab, np,
+                       b->U, (int64_t)BAND_ULD, j + 1, mt, chunk, b->Xp);
     BD_LAUNCH("symm_kernel");
     hipLaunchKernelGGL(psum_kernel, dim3(TS * TS / 512, mt), dim3(256), 0, s, b->Xp, sch, b->X);
     BD_LAUNCH("psum_kernel");
@@ -537,7 +551,7 @@ int band_reduce_pass(gpmi_band* b, const double* K, const std::vector<double>* y
       // panel's QR beside the rest of the update on a grid capped to la_grid
       // workgroups, so that the panel's workgroups find free CUs
       hipLaunchKernelGGL(syr2k_col_q_kernel, dim3(mt, 4), dim3(256), 0, s, b->Ab, np, b->U,
-                         (int64_t)BAND_ULD, j + 1);
+                         (int64_t)BAND_ULD, j + 1, ksrc);
       BD_LAUNCH("syr2k_col_q_kernel");
       BD_TRY(hipEventRecord(b->ev_col, s));
       BD_TRY(hipStreamWaitEvent(b->s_pan, b->ev_col, 0));
@@ -553,7 +567,7 @@ int band_reduce_pass(gpmi_band* b, const double* K, const std::vector<double>* y
         // one SYR2K workgroup per CU on all but la_free CUs, which the chain (its
         // single-workgroup kernels need a whole CU) has to itself
         hipLaunchKernelGGL(syr2k_pipe_kernel, dim3(nmain), dim3(256), 0, b->s_pan, b->Ab, np,
-                           b->U, (int64_t)BAND_ULD, j + 1, mt, tcnt, nmain, 0);
+                           b->U, (int64_t)BAND_ULD, j + 1, mt, tcnt, nmain, 0, ksrc);
         BD_LAUNCH("syr2k_pipe_kernel");
       } else {
         // the Householder panel (its workgroups must be co-resident) beside a capped
@@ -574,7 +588,8 @@ int band_reduce_pass(gpmi_band* b, const double* K, const std::vector<double>* y
         // 139.2 against 141.0 ms at N = 16384; launched only from panels whose
         // update outlasts the chain: no difference)
         hipLaunchKernelGGL(syr2k_pipe_kernel, dim3(std::min(la_free, rest - nmain)), dim3(256),
-                           0, s, b->Ab, np, b->U, (int64_t)BAND_ULD, j + 1, mt, tcnt, nmain, 1);
+                           0, s, b->Ab, np, b->U, (int64_t)BAND_ULD, j + 1, mt, tcnt, nmain, 1,
+                           ksrc);
         BD_LAUNCH("syr2k_pipe_kernel");
       }
       BD_TRY(hipStreamWaitEvent(s, b->ev_pan, 0));
@@ -714,6 +729,7 @@ int gpmi_band_create(gpmi_op* op, gpmi_band** out) {
   if ((e = hipStreamCreateWithFlags(&b->side, hipStreamNonBlocking)) != hipSuccess)
     return fail(e, "side stream");
   if (const char* la = std::getenv("GPMI_BAND_LA")) b->lookahead = std::atoi(la);
+  if (const char* po = std::getenv("GPMI_BAND_POISON")) b->poison = std::atoi(po) != 0;
   if (const char* pm = std::getenv("GPMI_BAND_PANEL")) b->panel_mode = std::strcmp(pm, "hh") == 0;
   if (const char* bm = std::getenv("GPMI_BAND_BCR")) b->bcr_mode = std::max(0, std::min(2, std::atoi(bm)));
   // GPMI_CQ_FO=0: every CholeskyQR pass by an exact Cholesky (no first-order passes)
