@@ -566,6 +566,13 @@ def test_band_filler_tiles_bit_identical(gp, monkeypatch, n):
     K, X, z = _inputs(n, 7 * n + 1, nu=1.5, scale=0.1)
     etas = [1e-2, 1.0]
     ld0, G0 = _mc(K).loglik_terms(etas, X, z)
+    # the look-ahead form copies only tile column 0 of K (the first panel's update reads
+    # K): with the rest of the working matrix NaN beforehand, nothing may change
+    monkeypatch.setenv('GPMI_BAND_POISON', '1')
+    ldp, Gp = _mc(K).loglik_terms(etas, X, z)
+    numpy.testing.assert_array_equal(ld0, ldp)
+    numpy.testing.assert_array_equal(G0, Gp)
+    monkeypatch.delenv('GPMI_BAND_POISON')
     monkeypatch.setenv('GPMI_BAND_LA', '0')
     ld1, G1 = _mc(K).loglik_terms(etas, X, z)
     numpy.testing.assert_array_equal(ld0, ld1)
