@@ -127,6 +127,7 @@ struct gpmi_band {
   int* cqflag = nullptr;     // [nt][8]: [0..2] first-order flag per pass, [3] CholeskyQR
                              // succeeded, [4] failed (the guarded Householder panel ran),
                              // [6] the look-ahead SYR2K's tile tickets
+  int la_free = LA_FREE, la_free_late = LA_FREE_LATE, la_late_mt = LA_LATE_MT;   // GPMI_LA_*
   bool poison = false;          // GPMI_BAND_POISON=1: Ab set to NaN before a K-first copy
   int cq_panel_fallbacks = 0;   // panels factored by the guarded Householder panel, or
                                 // (past its single-launch size) by per-column launches
@@ -557,7 +558,7 @@ int band_reduce_pass(gpmi_band* b, const double* K, const std::vector<double>* y
       BD_TRY(hipStreamWaitEvent(b->s_pan, b->ev_col, 0));
       const bool pipe = mode == 0;
       const int rest = (mt - 1) * mt / 2;
-      const int la_free = mt < LA_LATE_MT ? LA_FREE_LATE : LA_FREE;
+      const int la_free = mt < b->la_late_mt ? b->la_free_late : b->la_free;
       const int nmain = std::min(rest, std::max(1, b->ncu - la_free));
       int* tcnt = pipe ? b->cqflag + 8 * j + 6 : nullptr;
       // The rest of the update on s_pan, panel j + 1's QR on s right behind the tile
@@ -730,6 +731,9 @@ int gpmi_band_create(gpmi_op* op, gpmi_band** out) {
     return fail(e, "side stream");
   if (const char* la = std::getenv("GPMI_BAND_LA")) b->lookahead = std::atoi(la);
   if (const char* po = std::getenv("GPMI_BAND_POISON")) b->poison = std::atoi(po) != 0;
+  if (const char* v = std::getenv("GPMI_LA_FREE")) b->la_free = std::max(1, std::atoi(v));
+  if (const char* v = std::getenv("GPMI_LA_FREE_LATE")) b->la_free_late = std::max(1, std::atoi(v));
+  if (const char* v = std::getenv("GPMI_LA_LATE_MT")) b->la_late_mt = std::atoi(v);
   if (const char* pm = std::getenv("GPMI_BAND_PANEL")) b->panel_mode = std::strcmp(pm, "hh") == 0;
   if (const char* bm = std::getenv("GPMI_BAND_BCR")) b->bcr_mode = std::max(0, std::min(2, std::atoi(bm)));
   // GPMI_CQ_FO=0: every CholeskyQR pass by an exact Cholesky (no first-order passes)
