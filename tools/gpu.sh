@@ -82,6 +82,13 @@ for task in "$@"; do
       done ;;
     pmc-mfma)
       run 300 $D/pmc_mfma.log rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F64 GRBM_GUI_ACTIVE --kernel-trace -d $D/pmc_mfma -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-timing --no-band --no-sparse ;;
+    pmc-peak)
+      # the fp64 MFMA microbenchmark (tools/fp64_peak, built in the container) under
+      # the same MFMA-busy / clock counters as pmc-mfma: the ceiling's own busy fraction
+      run 120 $D/fp64_peak_plain.log ./tools/fp64_peak
+      cat $D/fp64_peak_plain.log
+      run 200 $D/pmc_peak.log rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F64 GRBM_GUI_ACTIVE --kernel-trace -d $D/pmc_peak -o run --output-format csv -- ./tools/fp64_peak
+      python tools/pmc_summary.py $D/pmc_peak.json "fp64_peak under MFMA counters" $(dirname $(find $D/pmc_peak -name "*counter_collection.csv")) > /dev/null && cat $D/pmc_peak.json ;;
     pmc-band)
       run 200 $D/pmc_band_mfma.log rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F64 GRBM_GUI_ACTIVE --kernel-trace -d $D/pmc_band_mfma -o run --output-format csv -- python3 tools/band_refresh_probe.py 128 1
       for c in FETCH_SIZE WRITE_SIZE; do
