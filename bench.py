@@ -533,6 +533,7 @@ def sparse_measure(args, config, world, rank, local, dist, torch, cpu, exact, de
     ms_iso = op.sop.bench_spmm(s_blk, 50)
     op.sop.set_timing(False)
     iso_n, iso_tot = op.sop.spmm_timing()[s_blk]
+    # iso_n: the 50 gated launches only (gpmi_sp_bench_spmm keeps its warm-up out of the log)
     dispatch_ms = max(0.0, ms_iso - iso_tot / iso_n)
     ms = ms_span + dispatch_ms
     alg_bytes = 12.0 * nnz + 8.0 * (n + 1) + 16.0 * n * s_blk
@@ -892,15 +893,19 @@ def optimizer_timing(D, X, z):
     .maximize_log_likelihood(z) (likelihood.py:67-102) for 'direct' (trust-exact
     on lp, jacobian, hessian; _direct_likelihood.py:346-405) and 'profiled'
     (bracket search + Chandrupatla on der1; _profile_likelihood.py:244-415),
-    from the resident K: the operator's band reduction, its eigenvalues (traceinv)
-    and every evaluation included. Wall time and the optimum."""
+    from the resident K: the operator's band reduction and every evaluation
+    included (traceinv of exponents 1 and 2 by selected inversion of each
+    evaluation's factor, so no eigenvalue chase: band_eigenvalue_calls counts
+    them). Wall time and the optimum."""
     import contextlib
     import io
     from gaussian_proc._likelihood import Likelihood
     from gaussian_proc._likelihood._profile_likelihood import ProfileLikelihood
+    from gaussian_proc import _hip
     out = {}
     for method in ('direct', 'profiled'):
         torch_sync()
+        eig0 = _hip.Band.eigenvalue_calls
         t0 = time.perf_counter()
         lik = Likelihood(X, D, method)
         with contextlib.redirect_stdout(io.StringIO()) as buf:
@@ -908,7 +913,10 @@ def optimizer_timing(D, X, z):
         dt = time.perf_counter() - t0
         entry = {'wall_s': round(dt, 3),
                  'result': {k: (float(v) if not isinstance(v, bool) else v)
-                            for k, v in res.items()}}
+                            for k, v in res.items()},
+                 # traceinv of exponents 1 and 2 by selected inversion: no eigenvalue
+                 # chase on either optimizer's path (round 6)
+                 'band_eigenvalue_calls': _hip.Band.eigenvalue_calls - eig0}
         if method == 'profiled':
             calls, points, _ = ProfileLikelihood.last_der1_calls
             entry['der1_device_calls'] = calls

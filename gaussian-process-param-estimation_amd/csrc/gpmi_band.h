@@ -89,7 +89,27 @@ __global__ void bcr_chol_kernel(const double* Ab, int64_t lda, const double* eta
                                 int64_t sZ, double* logd, double* gpart, int* failv, int nt,
                                 int64_t n);
 __global__ void bcr_w_kernel(const double* Lin, int64_t sL, const double* Fin, int64_t sF,
-                             double* W, int64_t sW, int m, int lvl);
+                             double* W, int64_t sW, int m, int lvl, const double* dDin,
+                             int64_t sdD, double* scr, double* dL);
+__global__ void bcr_upd_kernel(const double* Ab, int64_t lda, const double* etas, int lvl,
+                               const double* Din, int64_t sD, const double* Yin, int64_t sY,
+                               const double* W, int64_t sW, const double* Zall, int64_t sZ,
+                               double* Dout, double* Fout, double* Yout, int64_t sO, int64_t sOY,
+                               int m, const double* L, const double* dL, int64_t sL,
+                               const double* Fin, int64_t sF, const double* dFin, int64_t sdF,
+                               double* dW);
+__global__ void bcr_sinv_pre_kernel(const double* L, const double* dL, int64_t sL, const double* W,
+                                    const double* dW, int64_t sW, double* X, double* dX,
+                                    int64_t sX, double* Zd, double* dZd, int64_t sZd,
+                                    double* trpart, double* dtrpart, int nt, int nlev, int64_t n,
+                                    int ntan);
+__global__ void bcr_sinv_off_kernel(const double* Zd, const double* dZd, int64_t sZd, double* Zo,
+                                    double* dZo, int64_t sZo, const double* X, const double* dX,
+                                    int64_t sX, int m, int lvl, int ntan);
+__global__ void bcr_sinv_diag_kernel(const double* X, const double* dX, int64_t sX,
+                                     const double* Zo, const double* dZo, int64_t sZo, double* Zd,
+                                     double* dZd, int64_t sZd, double* trpart, double* dtrpart,
+                                     int nt, int64_t n, int m, int lvl, int ntan);
 __global__ void bcr_back_kernel(const double* L, int64_t sL, const double* W, int64_t sW,
                                 const double* Zall, int64_t sZ, double* Xall, double* g2part,
                                 int nt, int lvl, int first, int m);
@@ -101,19 +121,10 @@ __global__ void bcr_rhs_even_kernel(const double* W, int64_t sW, const double* Z
                                     int lvl, int m);
 __global__ void bcr_der_final_kernel(const double* g2part, const double* g3part, int nt,
                                      double* der);
-__global__ void bcr_sinv_x_kernel(const double* L, int64_t sL, const double* W, int64_t sW,
-                                  double* X, int64_t sX, int m, int lvl);
-__global__ void bcr_sinv_off_kernel(const double* Zd, int64_t sZd, double* Zo, int64_t sZo,
-                                    const double* X, int64_t sX, int m, int lvl);
-__global__ void bcr_sinv_diag_kernel(const double* L, int64_t sL, const double* X, int64_t sX,
-                                     const double* Zo, int64_t sZo, double* Zd, int64_t sZd,
-                                     double* trpart, int nt, int64_t n, int m, int lvl, int root);
 __global__ void bcr_sinv_final_kernel(const double* trpart, int nt, double* tr, int neta);
-__global__ void bcr_upd_kernel(const double* Ab, int64_t lda, const double* etas, int lvl,
-                               const double* Din, int64_t sD, const double* Yin, int64_t sY,
-                               const double* W, int64_t sW, const double* Zall, int64_t sZ,
-                               double* Dout, double* Fout, double* Yout, int64_t sO, int64_t sOY,
-                               int m);
+__global__ void bcr_dupd_kernel(const double* W, const double* dW, int64_t sW, const double* dDin,
+                                int64_t sdD, double* dDout, double* dFout, int64_t sO, int m,
+                                int lvl);
 __global__ void bcr_final_kernel(const double* logd, const double* gpart, const int* failv, int nt,
                                  double* out, int out_ld, int* info);
 __global__ void qt_partial_kernel(const double* P, int64_t lda, int m, const double* Y,

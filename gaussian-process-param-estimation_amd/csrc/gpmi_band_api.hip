@@ -164,6 +164,18 @@ struct gpmi_band {
   double* sinvTr = nullptr;  // [scap][nt] per-block traces, then [scap] sums
   int scap = 0;
   double sinv_ms = 0.0;
+  // eta-tangents of the cyclic-reduction factor and of the selected inversion
+  // (traceinv of exponent 2, gpmi_bcr.hip bcr_d*): per eta of a chunk of at most
+  // BAND_TAN_MAX (tcap), strides per eta as the primal blocks
+  double* tanL = nullptr;    // [tcap][nt][128][128]     dLinv
+  double* tanW = nullptr;    // [tcap][nt][2][128][128]  dW_l, dW_r
+  double* tanX = nullptr;    // [tcap][nt][2][128][128]  dX_l, dX_r (bcr_dfac's scratch first)
+  double* tanZd = nullptr;   // [tcap][nt][128][128]
+  double* tanZo = nullptr;   // [tcap][nt][2][128][128]
+  double* tanD[2] = {nullptr, nullptr};   // [tcap][half][128][128]
+  double* tanF[2] = {nullptr, nullptr};
+  double* tanTr = nullptr;   // [tcap][nt] per-block -tr dZ_pp, then [tcap] sums
+  int tcap = 0;
   double* cqMinv = nullptr;  // C = U^-T M3 of the current panel
   // T of a CholeskyQR panel from its reconstruction (cq_t_kernel) on the side stream
   // (not a stream of its own: the process's streams share GPU_MAX_HW_QUEUES hardware
@@ -210,7 +222,8 @@ int band_free(gpmi_band* b) {
                     b->bcrD[0], b->bcrD[1], b->bcrF[0], b->bcrF[1], b->bcrY[0], b->bcrY[1],
                     b->bcrL, b->bcrW, b->bcrZ, b->bcrG, b->bcrLd, b->bcrF0, b->bcrX,
                     b->bcrZp, b->bcrG2, b->bcrG3, b->sinvZd, b->sinvZo, b->sinvX,
-                    b->sinvTr};
+                    b->sinvTr, b->tanL, b->tanW, b->tanX, b->tanZd, b->tanZo, b->tanD[0],
+                    b->tanD[1], b->tanF[0], b->tanF[1], b->tanTr};
   if (b->bcrFail) (void)hipFree(b->bcrFail);
   if (b->cqflag) (void)hipFree(b->cqflag);
   if (b->rorder) (void)hipFree(b->rorder);
@@ -934,9 +947,38 @@ int gpmi_band_set_rhs(gpmi_band* b, const double* rhs, int64_t ld, int nrhs) {
   return 0;
 }
 
+// Tangent buffers for neta <= BAND_TAN_MAX etas (band_loglik_bcr / band_sinv_bcr
+// with tan).
+int ensure_tan(gpmi_band* b, int neta) {
+  if (b->tcap >= neta) return 0;
+  for (double** q : {&b->tanL, &b->tanW, &b->tanX, &b->tanZd, &b->tanZo, &b->tanD[0],
+                     &b->tanD[1], &b->tanF[0], &b->tanF[1], &b->tanTr})
+    if (*q) {
+      BD_TRY(hipFree(*q));
+      *q = nullptr;
+    }
+  b->tcap = 0;
+  const int nt = b->nt, half = (nt + 1) / 2;
+  const size_t blk = (size_t)TS * TS;
+  BD_TRY(hipMalloc(&b->tanL, sizeof(double) * neta * nt * blk));
+  BD_TRY(hipMalloc(&b->tanW, sizeof(double) * neta * nt * 2 * blk));
+  BD_TRY(hipMalloc(&b->tanX, sizeof(double) * neta * nt * 2 * blk));
+  BD_TRY(hipMalloc(&b->tanZd, sizeof(double) * neta * nt * blk));
+  BD_TRY(hipMalloc(&b->tanZo, sizeof(double) * neta * nt * 2 * blk));
+  for (int q = 0; q < 2; ++q) {
+    BD_TRY(hipMalloc(&b->tanD[q], sizeof(double) * neta * half * blk));
+    BD_TRY(hipMalloc(&b->tanF[q], sizeof(double) * neta * half * blk));
+  }
+  BD_TRY(hipMalloc(&b->tanTr, sizeof(double) * neta * (nt + 1)));
+  b->tcap = neta;
+  return 0;
+}
+
 // The likelihood terms of neta eta (b->etas on the device) by block cyclic
-// reduction (gpmi_bcr.hip) into b->out / b->info, on stream s.
-int band_loglik_bcr(gpmi_band* b, int neta, hipStream_t s) {
+// reduction (gpmi_bcr.hip) into b->out / b->info, on stream s. With tan (neta <=
+// b->tcap), also every eliminated block's dLinv and dW (bcr_dfac / bcr_dw / bcr_dupd)
+// for band_sinv_bcr's exponent-2 trace.
+int band_loglik_bcr(gpmi_band* b, int neta, hipStream_t s, bool tan = false) {
   const int nt = b->nt;
   const int64_t np = b->n_pad;
   const int half = (nt + 1) / 2;
@@ -980,6 +1022,8 @@ int band_loglik_bcr(gpmi_band* b, int neta, hipStream_t s) {
   const double* Din = nullptr;
   const double* Yin = b->Y;
   const double* Fin = b->bcrF0;
+  const double* dDin = nullptr;   // tangents of the level's D, F (level 0: I, 0)
+  const double* dFin = nullptr;
   int64_t sD = 0, sY = 0, sF = 0;
   int m = nt, lvl = 0, cur = 0;
   while (m > 1) {
@@ -988,13 +1032,23 @@ int band_loglik_bcr(gpmi_band* b, int neta, hipStream_t s) {
                        lvl, 1, Din, sD, Yin, sY, b->bcrL, sL, 1, b->bcrZ, sZ, b->bcrLd, b->bcrG,
                        b->bcrFail, nt, b->n);
     BD_LAUNCH("bcr_chol_kernel");
-    hipLaunchKernelGGL(bcr_w_kernel, dim3(2 * nodd, neta), dim3(256), 0, s, b->bcrL, sL, Fin, sF,
-                       b->bcrW, sW, m, lvl);
+    // W (and with tangents the level's dLinv beside it), then D', F', Y' (and dW),
+    // then dD', dF'
+    hipLaunchKernelGGL(bcr_w_kernel, dim3(2 * nodd + (tan ? nodd : 0), neta), dim3(256), 0, s,
+                       b->bcrL, sL, Fin, sF, b->bcrW, sW, m, lvl, dDin, sH, b->tanX, b->tanL);
     BD_LAUNCH("bcr_w_kernel");
-    hipLaunchKernelGGL(bcr_upd_kernel, dim3(2 * neven, neta), dim3(256), 0, s, b->Ab, np, b->etas,
-                       lvl, Din, sD, Yin, sY, b->bcrW, sW, b->bcrZ, sZ, b->bcrD[cur], b->bcrF[cur],
-                       b->bcrY[cur], sH, sHY, m);
+    hipLaunchKernelGGL(bcr_upd_kernel, dim3(3 * neven + (tan ? 2 * nodd : 0), neta), dim3(256), 0,
+                       s, b->Ab, np, b->etas, lvl, Din, sD, Yin, sY, b->bcrW, sW, b->bcrZ, sZ,
+                       b->bcrD[cur], b->bcrF[cur], b->bcrY[cur], sH, sHY, m, b->bcrL, b->tanL, sL,
+                       Fin, sF, dFin, sH, b->tanW);
     BD_LAUNCH("bcr_upd_kernel");
+    if (tan) {
+      hipLaunchKernelGGL(bcr_dupd_kernel, dim3(2 * neven, neta), dim3(256), 0, s, b->bcrW,
+                         b->tanW, sW, dDin, sH, b->tanD[cur], b->tanF[cur], sH, m, lvl);
+      BD_LAUNCH("bcr_dupd_kernel");
+      dDin = b->tanD[cur];
+      dFin = b->tanF[cur];
+    }
     Din = b->bcrD[cur];
     Yin = b->bcrY[cur];
     Fin = b->bcrF[cur];
@@ -1009,6 +1063,11 @@ int band_loglik_bcr(gpmi_band* b, int neta, hipStream_t s) {
                      Din, sD, Yin, sY, b->bcrL, sL, 1, b->bcrZ, sZ, b->bcrLd, b->bcrG, b->bcrFail,
                      nt, b->n);
   BD_LAUNCH("bcr_chol_kernel");
+  if (tan) {   // the last level's dLinv (bcr_w_kernel with m = 1: its dfac role only)
+    hipLaunchKernelGGL(bcr_w_kernel, dim3(1, neta), dim3(256), 0, s, b->bcrL, sL, nullptr, 0,
+                       nullptr, sW, 1, lvl, dDin, sH, b->tanX, b->tanL);
+    BD_LAUNCH("bcr_w_kernel");
+  }
   hipLaunchKernelGGL(bcr_final_kernel, dim3(neta), dim3(256), 0, s, b->bcrLd, b->bcrG, b->bcrFail,
                      nt, b->out, OUT_LD, b->info);
   BD_LAUNCH("bcr_final_kernel");
@@ -1018,8 +1077,8 @@ int band_loglik_bcr(gpmi_band* b, int neta, hipStream_t s) {
 // Derivative terms by cyclic reduction (after band_loglik_bcr, whose levels stay
 // stored): X = (B + eta I)^-1 Y by back substitution from the last level down, then
 // the forward elimination of X; G2, G3 into b->der (gpmi_bcr.hip).
-int band_der_bcr(gpmi_band* b, int neta, hipStream_t s) {
-  int rc = band_loglik_bcr(b, neta, s);
+int band_der_bcr(gpmi_band* b, int neta, hipStream_t s, bool tan = false) {
+  int rc = band_loglik_bcr(b, neta, s, tan);
   if (rc) return rc;
   const int nt = b->nt;
   const int half = (nt + 1) / 2;
@@ -1061,8 +1120,10 @@ int band_der_bcr(gpmi_band* b, int neta, hipStream_t s) {
 
 // tr((B + eta_e I)^-1) for the neta etas whose cyclic-reduction factor band_loglik_bcr
 // left in bcrL / bcrW: selected inversion down the tree, top-down (gpmi_bcr.hip
-// bcr_sinv_*), into sinvTr[nt * scap + e] (device).
-int band_sinv_bcr(gpmi_band* b, int neta, hipStream_t s) {
+// bcr_sinv_*), into sinvTr[nt * neta + e] (device). With tan (the factor's tangents
+// computed by band_loglik_bcr(.., tan)) also tr((B + eta_e I)^-2) into
+// tanTr[nt * neta + e] (bcr_dsinv_*).
+int band_sinv_bcr(gpmi_band* b, int neta, hipStream_t s, bool tan = false) {
   const int nt = b->nt;
   const size_t blk = (size_t)TS * TS;
   if (b->scap < neta) {
@@ -1082,25 +1143,31 @@ int band_sinv_bcr(gpmi_band* b, int neta, hipStream_t s) {
   std::vector<int> ms;   // blocks per level; the last level has one
   for (int m = nt; m > 1; m = (m + 1) / 2) ms.push_back(m);
   const int L = (int)ms.size();
-  hipLaunchKernelGGL(bcr_sinv_diag_kernel, dim3(1, neta), dim3(256), 0, s, b->bcrL, sL, b->sinvX,
-                     sX, b->sinvZo, sZo, b->sinvZd, sZd, b->sinvTr, nt, b->n, 1, L, 1);
-  BD_LAUNCH("bcr_sinv_diag_kernel");
+  const int nt_ = tan ? 1 : 0;
+  // every block's X_l, X_r, Linv^T Linv (and tangents), the root's trace
+  hipLaunchKernelGGL(bcr_sinv_pre_kernel, dim3(nt * (3 + 3 * nt_), neta), dim3(256), 0, s,
+                     b->bcrL, b->tanL, sL, b->bcrW, b->tanW, sW, b->sinvX, b->tanX, sX, b->sinvZd,
+                     b->tanZd, sZd, b->sinvTr, b->tanTr, nt, L, b->n, nt_);
+  BD_LAUNCH("bcr_sinv_pre_kernel");
   for (int l = L - 1; l >= 0; --l) {
     const int nodd = ms[l] / 2;
-    hipLaunchKernelGGL(bcr_sinv_x_kernel, dim3(2 * nodd, neta), dim3(256), 0, s, b->bcrL, sL,
-                       b->bcrW, sW, b->sinvX, sX, ms[l], l);
-    BD_LAUNCH("bcr_sinv_x_kernel");
-    hipLaunchKernelGGL(bcr_sinv_off_kernel, dim3(2 * nodd, neta), dim3(256), 0, s, b->sinvZd, sZd,
-                       b->sinvZo, sZo, b->sinvX, sX, ms[l], l);
+    hipLaunchKernelGGL(bcr_sinv_off_kernel, dim3((2 + 2 * nt_) * nodd, neta), dim3(256), 0, s,
+                       b->sinvZd, b->tanZd, sZd, b->sinvZo, b->tanZo, sZo, b->sinvX, b->tanX, sX,
+                       ms[l], l, nt_);
     BD_LAUNCH("bcr_sinv_off_kernel");
-    hipLaunchKernelGGL(bcr_sinv_diag_kernel, dim3(nodd, neta), dim3(256), 0, s, b->bcrL, sL,
-                       b->sinvX, sX, b->sinvZo, sZo, b->sinvZd, sZd, b->sinvTr, nt, b->n, ms[l], l,
-                       0);
+    hipLaunchKernelGGL(bcr_sinv_diag_kernel, dim3((1 + nt_) * nodd, neta), dim3(256), 0, s,
+                       b->sinvX, b->tanX, sX, b->sinvZo, b->tanZo, sZo, b->sinvZd, b->tanZd, sZd,
+                       b->sinvTr, b->tanTr, nt, b->n, ms[l], l, nt_);
     BD_LAUNCH("bcr_sinv_diag_kernel");
   }
   hipLaunchKernelGGL(bcr_sinv_final_kernel, dim3((neta + 63) / 64), dim3(64), 0, s, b->sinvTr, nt,
                      b->sinvTr + (size_t)nt * neta, neta);
   BD_LAUNCH("bcr_sinv_final_kernel");
+  if (tan) {
+    hipLaunchKernelGGL(bcr_sinv_final_kernel, dim3((neta + 63) / 64), dim3(64), 0, s, b->tanTr,
+                       nt, b->tanTr + (size_t)nt * neta, neta);
+    BD_LAUNCH("bcr_sinv_final_kernel");
+  }
   return 0;
 }
 
@@ -1151,10 +1218,34 @@ int gpmi_band_der_terms(gpmi_band* b, const double* etas, int neta, double* logd
 
 int gpmi_band_der_terms_ex(gpmi_band* b, const double* etas, int neta, double* logdet,
                            double* g1, double* g2, double* g3, double* tr1, int* info) {
+  return gpmi_band_der_terms_ex2(b, etas, neta, logdet, g1, g2, g3, tr1, nullptr, info);
+}
+
+int gpmi_band_der_terms_ex2(gpmi_band* b, const double* etas, int neta, double* logdet,
+                            double* g1, double* g2, double* g3, double* tr1, double* tr2,
+                            int* info) {
   if (!b) return set_error(-1006, "null handle");
   if (neta <= 0) return 0;
   if (neta > GPMI_BAND_DER_MAX)
     return set_error(-1203, "gpmi_band_der_terms: at most GPMI_BAND_DER_MAX etas per call");
+  if (tr2 && neta > GPMI_BAND_TAN_MAX) {
+    // the tangent store is sized per chunk: chunks of GPMI_BAND_TAN_MAX etas
+    const size_t mm = (size_t)b->nrhs * b->nrhs;
+    for (int c = 0; c < neta; c += GPMI_BAND_TAN_MAX) {
+      const int k = std::min(GPMI_BAND_TAN_MAX, neta - c);
+      int rc = gpmi_band_der_terms_ex2(b, etas + c, k, logdet ? logdet + c : nullptr,
+                                       g1 ? g1 + c * mm : nullptr, g2 ? g2 + c * mm : nullptr,
+                                       g3 ? g3 + c * mm : nullptr, tr1 ? tr1 + c : nullptr,
+                                       tr2 + c, info ? info + c : nullptr);
+      if (rc) return rc;
+    }
+    return 0;
+  }
+  std::vector<double> tr1_scratch;
+  if (tr2 && !tr1) {
+    tr1_scratch.resize(neta);
+    tr1 = tr1_scratch.data();
+  }
   Guard g(b->device);
   int rc = ensure_cap(b, neta);
   if (rc) return rc;
@@ -1171,12 +1262,13 @@ int gpmi_band_der_terms_ex(gpmi_band* b, const double* etas, int neta, double* l
     BD_TRY(hipMalloc(&b->der, sizeof(double) * neta * 2 * RLD * RLD));
     b->dcap = neta;
   }
+  if (tr2 && (rc = ensure_tan(b, neta))) return rc;
   hipStream_t s = b->stream;
   BD_TRY(hipMemcpyAsync(b->etas, etas, sizeof(double) * neta, hipMemcpyHostToDevice, s));
   BD_TRY(hipEventRecord(b->ev0, s));
   // tr1 needs the cyclic-reduction factor (the tree it inverts along)
   if (tr1 || b->bcr_mode == 1 || (b->bcr_mode == 2 && neta <= 64)) {
-    rc = band_der_bcr(b, neta, s);
+    rc = band_der_bcr(b, neta, s, tr2 != nullptr);
     if (rc) return rc;
   } else {
     hipLaunchKernelGGL(band_chol_kernel, dim3(neta), dim3(256), 0, s, b->Ab, np, nt, b->n, b->Y,
@@ -1186,14 +1278,19 @@ int gpmi_band_der_terms_ex(gpmi_band* b, const double* etas, int neta, double* l
                        b->der);
     BD_LAUNCH("band_der_kernel");
   }
-  std::vector<double> htr;
+  std::vector<double> htr, htr2;
   if (tr1) {
     BD_TRY(hipEventRecord(b->ev2, s));
-    rc = band_sinv_bcr(b, neta, s);
+    rc = band_sinv_bcr(b, neta, s, tr2 != nullptr);
     if (rc) return rc;
     htr.resize(neta);
     BD_TRY(hipMemcpyAsync(htr.data(), b->sinvTr + (size_t)nt * neta, sizeof(double) * neta,
                           hipMemcpyDeviceToHost, s));
+    if (tr2) {
+      htr2.resize(neta);
+      BD_TRY(hipMemcpyAsync(htr2.data(), b->tanTr + (size_t)nt * neta, sizeof(double) * neta,
+                            hipMemcpyDeviceToHost, s));
+    }
   }
   BD_TRY(hipEventRecord(b->ev1, s));
   std::vector<double> hout((size_t)neta * OUT_LD), hder((size_t)neta * 2 * RLD * RLD);
@@ -1212,6 +1309,8 @@ int gpmi_band_der_terms_ex(gpmi_band* b, const double* etas, int neta, double* l
     BD_TRY(hipEventElapsedTime(&ms2, b->ev2, b->ev1));
     b->sinv_ms = ms2;
     for (int e = 0; e < neta; ++e) tr1[e] = htr[e];
+    if (tr2)
+      for (int e = 0; e < neta; ++e) tr2[e] = htr2[e];
   }
   const int m = b->nrhs;
   for (int e = 0; e < neta; ++e) {
@@ -1229,31 +1328,51 @@ int gpmi_band_der_terms_ex(gpmi_band* b, const double* etas, int neta, double* l
 }
 
 int gpmi_band_traceinv(gpmi_band* b, const double* etas, int neta, double* tr, int* info) {
+  return gpmi_band_traceinv2(b, etas, neta, tr, nullptr, info);
+}
+
+int gpmi_band_traceinv2(gpmi_band* b, const double* etas, int neta, double* tr1, double* tr2,
+                        int* info) {
   if (!b) return set_error(-1006, "null handle");
   if (neta <= 0) return 0;
   if (neta > GPMI_BAND_DER_MAX)
     return set_error(-1203, "gpmi_band_traceinv: at most GPMI_BAND_DER_MAX etas per call");
+  if (!tr1) return set_error(-1006, "gpmi_band_traceinv2: tr1 is required");
+  if (tr2 && neta > GPMI_BAND_TAN_MAX) {
+    for (int c = 0; c < neta; c += GPMI_BAND_TAN_MAX) {
+      const int k = std::min(GPMI_BAND_TAN_MAX, neta - c);
+      int rc = gpmi_band_traceinv2(b, etas + c, k, tr1 + c, tr2 + c, info ? info + c : nullptr);
+      if (rc) return rc;
+    }
+    return 0;
+  }
   Guard g(b->device);
   int rc = ensure_cap(b, neta);
   if (rc) return rc;
+  const bool tan = tr2 != nullptr;
+  if (tan && (rc = ensure_tan(b, neta))) return rc;
   hipStream_t s = b->stream;
   BD_TRY(hipMemcpyAsync(b->etas, etas, sizeof(double) * neta, hipMemcpyHostToDevice, s));
   BD_TRY(hipEventRecord(b->ev0, s));
-  if ((rc = band_loglik_bcr(b, neta, s))) return rc;
+  if ((rc = band_loglik_bcr(b, neta, s, tan))) return rc;
   BD_TRY(hipEventRecord(b->ev2, s));
-  if ((rc = band_sinv_bcr(b, neta, s))) return rc;
+  if ((rc = band_sinv_bcr(b, neta, s, tan))) return rc;
   BD_TRY(hipEventRecord(b->ev1, s));
-  std::vector<double> htr(neta);
+  std::vector<double> htr(neta), htr2(tan ? neta : 0);
   std::vector<int> hinfo(neta);
   BD_TRY(hipMemcpyAsync(htr.data(), b->sinvTr + (size_t)b->nt * neta, sizeof(double) * neta,
                         hipMemcpyDeviceToHost, s));
+  if (tan)
+    BD_TRY(hipMemcpyAsync(htr2.data(), b->tanTr + (size_t)b->nt * neta, sizeof(double) * neta,
+                          hipMemcpyDeviceToHost, s));
   BD_TRY(hipMemcpyAsync(hinfo.data(), b->info, sizeof(int) * neta, hipMemcpyDeviceToHost, s));
   BD_TRY(hipStreamSynchronize(s));
   float ms = 0.f;
   BD_TRY(hipEventElapsedTime(&ms, b->ev2, b->ev1));
   b->sinv_ms = ms;
   for (int e = 0; e < neta; ++e) {
-    tr[e] = htr[e];
+    tr1[e] = htr[e];
+    if (tan) tr2[e] = htr2[e];
     if (info) info[e] = hinfo[e];
   }
   return 0;

@@ -179,18 +179,17 @@ __global__ __launch_bounds__(256) void bcr_chol_kernel(
   }
 }
 
-// W of odd block p = 1 + 2 (blockIdx.x >> 1): which = blockIdx.x & 1:
+// W of odd block p = 1 + 2 (bx >> 1): which = bx & 1:
 //   0: W_l = Linv_p F_{p-1};  1: W_r = Linv_p F_p^T (only when p + 1 < m).
 // F: level 0 the shared F0 (sF = 0), else Fin. Linv and W are stored by the block's
 // original index (p << lvl): every level's factor survives for the solves of
 // bcr_back_kernel / bcr_rhs_*.
-__global__ __launch_bounds__(256, 2) void bcr_w_kernel(const double* __restrict__ Lin, int64_t sL,
-                                                       const double* __restrict__ Fin, int64_t sF,
-                                                       double* __restrict__ W, int64_t sW,
-                                                       int m, int lvl) {
-  __shared__ double smem[4 * GSTAGE];
+__device__ __forceinline__ void bcr_w_role(int bx, const double* __restrict__ Lin, int64_t sL,
+                                           const double* __restrict__ Fin, int64_t sF,
+                                           double* __restrict__ W, int64_t sW, int m, int lvl,
+                                           double* smem) {
   const int e = blockIdx.y;
-  const int h = blockIdx.x >> 1, which = blockIdx.x & 1;
+  const int h = bx >> 1, which = bx & 1;
   const int p = 1 + 2 * h;
   const int o = p << lvl;
   if (which == 1 && p + 1 >= m) return;
@@ -205,28 +204,97 @@ __global__ __launch_bounds__(256, 2) void bcr_w_kernel(const double* __restrict_
   store_tile(W + e * sW + ((int64_t)o * 2 + which) * TS * TS, TS, acc, 1.0);
 }
 
-// Even block j = 2 (blockIdx.x >> 1) of an m-block level: which = blockIdx.x & 1:
-//   0: D_j' (and Y_j'),  1: F_{j/2}' = -W_r(j+1)^T W_l(j+1)  (only when j + 2 < m).
+// Tangent of the eliminated block's inverse factor (defined with the tangent kernels
+// below): dLinv = -Phi(Linv dD Linv^T) Linv.
+__device__ void bcr_dfac_role(const double* __restrict__ L, int64_t sL,
+                              const double* __restrict__ dDin, int64_t sdD,
+                              double* __restrict__ scr, int64_t sS, double* __restrict__ dL,
+                              int lvl, int p, double* smem);
+
+// bcr_w_role for bx < 2 nodd (nodd = m / 2); with tangents (dL != nullptr) the
+// workgroups bx - 2 nodd < nodd form the same blocks' dLinv beside them (level m == 1:
+// the last level's single block, p = 0).
+__global__ __launch_bounds__(256, 2) void bcr_w_kernel(const double* __restrict__ Lin, int64_t sL,
+                                                       const double* __restrict__ Fin, int64_t sF,
+                                                       double* __restrict__ W, int64_t sW,
+                                                       int m, int lvl,
+                                                       const double* __restrict__ dDin,
+                                                       int64_t sdD, double* __restrict__ scr,
+                                                       double* __restrict__ dL) {
+  __shared__ double smem[4 * GSTAGE];
+  const int nodd = m / 2;
+  const int bx = blockIdx.x;
+  if (bx < 2 * nodd) {
+    bcr_w_role(bx, Lin, sL, Fin, sF, W, sW, m, lvl, smem);
+    return;
+  }
+  const int d = bx - 2 * nodd;
+  bcr_dfac_role(Lin, sL, dDin, sdD, scr, sW, dL, lvl, m == 1 ? 0 : 1 + 2 * d, smem);
+}
+
+// dW of odd block p = 1 + 2 (bx >> 1), which = bx & 1 as bcr_w_role (defined below).
+__device__ void bcr_dw_role(int bx, const double* __restrict__ L, const double* __restrict__ dL,
+                            int64_t sL, const double* __restrict__ Fin, int64_t sF,
+                            const double* __restrict__ dFin, int64_t sdF, double* __restrict__ dW,
+                            int64_t sW, int m, int lvl, double* smem);
+
+// Even block j = 2 (bx / 3) of an m-block level: which = bx % 3:
+//   0: D_j',  1: F_{j/2}' = -W_r(j+1)^T W_l(j+1)  (only when j + 2 < m),
+//   2: Y_j' = Y_j - W_r(j-1)^T Z_{j-1} - W_l(j+1)^T Z_{j+1} (its own workgroup: the
+//      scalar 128 x 16 update no longer follows the D' products).
 // W pairs of odd block i at W[(i << lvl) * 2 + {0: l, 1: r}]; Z of odd block i at
-// its original index (i << lvl) in Zall.
+// its original index (i << lvl) in Zall. With tangents (dW != nullptr) the workgroups
+// bx - 3 neven < 2 nodd form the level's dW (bcr_dw_role) beside them.
 __global__ __launch_bounds__(256, 2) void bcr_upd_kernel(
     const double* __restrict__ Ab, int64_t lda, const double* __restrict__ etas, int lvl,
     const double* __restrict__ Din, int64_t sD, const double* __restrict__ Yin, int64_t sY,
     const double* __restrict__ W, int64_t sW, const double* __restrict__ Zall, int64_t sZ,
     double* __restrict__ Dout, double* __restrict__ Fout, double* __restrict__ Yout, int64_t sO,
-    int64_t sOY, int m) {
+    int64_t sOY, int m, const double* __restrict__ L, const double* __restrict__ dL, int64_t sL,
+    const double* __restrict__ Fin, int64_t sF, const double* __restrict__ dFin, int64_t sdF,
+    double* __restrict__ dW) {
   __shared__ double smem[4 * GSTAGE];
+  const int neven = (m + 1) / 2;
+  if ((int)blockIdx.x >= 3 * neven) {
+    bcr_dw_role(blockIdx.x - 3 * neven, L, dL, sL, Fin, sF, dFin, sdF, dW, sW, m, lvl, smem);
+    return;
+  }
   const int e = blockIdx.y;
-  const int h = blockIdx.x >> 1, which = blockIdx.x & 1;
+  const int h = blockIdx.x / 3, which = blockIdx.x % 3;
   const int j = 2 * h;
   const double* We = W + e * sW;
+  const bool left = j >= 1, right = j + 1 < m;
+  if (which == 2) {
+    // Y_j' = Y_j - W_r(j-1)^T Z_{j-1} - W_l(j+1)^T Z_{j+1}: thread (row r, 8 columns)
+    const int t = threadIdx.x, r = t >> 1, c0 = (t & 1) * 8;
+    const double* ysrc = Yin + e * sY + (int64_t)j * TS * RLD;
+    double y[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) y[q] = ysrc[r * RLD + c0 + q];
+    for (int side = 0; side < 2; ++side) {
+      if (side == 0 && !left) continue;
+      if (side == 1 && !right) continue;
+      const int i = side == 0 ? j - 1 : j + 1;
+      const double* Wm = We + ((int64_t)(i << lvl) * 2 + (side == 0 ? 1 : 0)) * TS * TS;
+      const double* Z = Zall + e * sZ + (int64_t)(i << lvl) * TS * RLD;
+      for (int k = 0; k < TS; ++k) {
+        const double wv = Wm[k * TS + r];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) y[q] -= wv * Z[k * RLD + c0 + q];
+      }
+    }
+    double* ydst = Yout + e * sOY + (int64_t)h * TS * RLD;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) ydst[r * RLD + c0 + q] = y[q];
+    return;
+  }
   d4 acc[4][4];
   if (which == 1) {
     if (j + 2 >= m) return;
     const double* Wl = We + ((int64_t)((j + 1) << lvl) * 2 + 0) * TS * TS;
     const double* Wr = We + ((int64_t)((j + 1) << lvl) * 2 + 1) * TS * TS;
     zero_tile(acc);
-    gemm_tile<KSLOW, KSLOW, true>(Wr, TS, Wl, TS, TS, smem, acc);
+    gemm_tile_rr<true>(Wr, true, Wl, true, smem, acc);
     store_tile(Fout + e * sO + (int64_t)h * TS * TS, TS, acc, 1.0);
     return;
   }
@@ -245,37 +313,15 @@ __global__ __launch_bounds__(256, 2) void bcr_upd_kernel(
   } else {
     load_tile(Din + e * sD + (int64_t)j * TS * TS, TS, acc);
   }
-  const bool left = j >= 1, right = j + 1 < m;
-  if (left) {
-    const double* Wr = We + ((int64_t)((j - 1) << lvl) * 2 + 1) * TS * TS;
-    gemm_tile<KSLOW, KSLOW, true>(Wr, TS, Wr, TS, TS, smem, acc);
-  }
-  if (right) {
-    const double* Wl = We + ((int64_t)((j + 1) << lvl) * 2 + 0) * TS * TS;
-    gemm_tile<KSLOW, KSLOW, true>(Wl, TS, Wl, TS, TS, smem, acc);
+  // W_r(j-1)^T W_r(j-1), then W_l(j+1)^T W_l(j+1): a rolled loop (one inlined product)
+#pragma unroll 1
+  for (int q = 0; q < 2; ++q) {
+    if (q == 0 ? !left : !right) continue;
+    const double* Wm = We + ((int64_t)((q == 0 ? j - 1 : j + 1) << lvl) * 2 + (q == 0 ? 1 : 0)) *
+                                TS * TS;
+    gemm_tile_rr<true>(Wm, true, Wm, true, smem, acc);
   }
   store_tile(Dout + e * sO + (int64_t)h * TS * TS, TS, acc, 1.0);
-  // Y_j' = Y_j - W_r(j-1)^T Z_{j-1} - W_l(j+1)^T Z_{j+1}: thread (row r, 8 columns)
-  const int t = threadIdx.x, r = t >> 1, c0 = (t & 1) * 8;
-  const double* ysrc = Yin + e * sY + (int64_t)j * TS * RLD;
-  double y[8];
-#pragma unroll
-  for (int q = 0; q < 8; ++q) y[q] = ysrc[r * RLD + c0 + q];
-  for (int side = 0; side < 2; ++side) {
-    if (side == 0 && !left) continue;
-    if (side == 1 && !right) continue;
-    const int i = side == 0 ? j - 1 : j + 1;
-    const double* Wm = We + ((int64_t)(i << lvl) * 2 + (side == 0 ? 1 : 0)) * TS * TS;
-    const double* Z = Zall + e * sZ + (int64_t)(i << lvl) * TS * RLD;
-    for (int k = 0; k < TS; ++k) {
-      const double wv = Wm[k * TS + r];
-#pragma unroll
-      for (int q = 0; q < 8; ++q) y[q] -= wv * Z[k * RLD + c0 + q];
-    }
-  }
-  double* ydst = Yout + e * sOY + (int64_t)h * TS * RLD;
-#pragma unroll
-  for (int q = 0; q < 8; ++q) ydst[r * RLD + c0 + q] = y[q];
 }
 
 // out[e][0] = logdet (original block order), out[e][1 + a * 16 + c] = sum of the
@@ -462,12 +508,16 @@ __global__ __launch_bounds__(256) void bcr_der_final_kernel(const double* __rest
 // r = p + 1 of that level, with L_{l,p} = W_l^T and L_{r,p} = W_r^T (bcr_w_kernel).
 // The Takahashi recurrences (Takahashi, Fagan and Chin 1973; Erisman and Tinney,
 // Comm. ACM 18 (1975) 177) need only the inverse's blocks on the factor's pattern:
-//   X_s  = W_s^T Linv_p                          s in {l, r}     bcr_sinv_x_kernel
+//   X_s  = W_s^T Linv_p                          s in {l, r}
 //   Z_sp = -(Z_sl X_l + Z_sr X_r)                                bcr_sinv_off_kernel
 //   Z_pp = Linv_p^T Linv_p - X_l^T Z_lp - X_r^T Z_rp              bcr_sinv_diag_kernel
 // top-down from the last level's single block (Z = Linv^T Linv), level by level,
 // every node of a level independent (numpy prototype tools/bcr_sinv_proto.py: the
-// diagonal blocks equal inv(A)'s to 1e-16). The parents' coupling Z_lr is the
+// diagonal blocks equal inv(A)'s to 1e-16). X_s and Linv_p^T Linv_p depend on the
+// factor only, so ONE launch forms them for every block of every level before the
+// top-down pass (bcr_sinv_pre_kernel; round 6, with the tangents below: the level
+// loop keeps two launches of <= 2 products (<= 4 with tangents) per level, against
+// three of 1 / 2 / 3 (+ 2 / 4 / 6) before). The parents' coupling Z_lr is the
 // off-diagonal block their own elimination produced one level up: l' = (p - 1) / 2
 // and r' = l' + 1 there; if r' is odd it is Z_{l', r'} = Zo[o_r][0], else l' is odd and
 // Z_lr = Zo[o_l][1]^T. tr Z_pp over the rows < n (the identity pad is decoupled) per
@@ -475,99 +525,48 @@ __global__ __launch_bounds__(256) void bcr_der_final_kernel(const double* __rest
 // sums sum_i (lambda_i + eta)^-1 of the reference's 'eigenvalue' traceinv
 // (mixed_correlation.py:172-181) without the eigenvalues: O(n b^2) per eta.
 // Blocks by original index o = p << l: Zd[o] (diagonal), Zo[o][2] (Z_lp, Z_rp), X[o][2].
+//
+// trace((B + eta I)^-2) without eigenvalues (round 6): -d/deta trace((B + eta I)^-1)
+// by forward-mode differentiation of the factor and of the selected inversion
+// (numpy prototype tools/bcr_dsinv_proto.py). Every block carries its eta-tangent
+// (d/deta); level 0: dD = I, dF = 0.
+// Factor (with bcr_w / bcr_upd of the level, as extra workgroups of their launches):
+//   M_p     = Phi(Linv_p dD_p Linv_p^T)   Phi: strict lower + half diagonal   bcr_dfac_role
+//   dLinv_p = -M_p Linv_p                 (S = L L^T, dS = dL L^T + L dL^T)
+//   dW_l    = dLinv_p F_{p-1} + Linv_p dF_{p-1}                               bcr_dw_role
+//   dW_r    = dLinv_p F_p^T   + Linv_p dF_p^T
+//   dD_j'   = dD_j - (dW_r^T W_r + W_r^T dW_r)(j-1) - (dW_l^T W_l + W_l^T dW_l)(j+1)
+//   dF_j/2' = -(dW_r^T W_l + W_r^T dW_l)(j+1)                                 bcr_dupd
+// Selected inversion (extra workgroups of the launches above):
+//   dX_s  = dW_s^T Linv_p + W_s^T dLinv_p
+//   dZ_sp = -(dZ_sl X_l + Z_sl dX_l + dZ_sr X_r + Z_sr dX_r)
+//   dZ_pp = dLinv^T Linv + Linv^T dLinv - dX_l^T Z_lp - X_l^T dZ_lp
+//           - dX_r^T Z_rp - X_r^T dZ_rp
+// trace((B + eta I)^-2) = -sum_p tr dZ_pp over the rows < n. This replaces the
+// eigenvalue sums sum_i (lambda_i + eta)^-2 of the reference's 'eigenvalue'
+// traceinv(eta, exponent=2) (mixed_correlation.py:172-181), which the direct
+// Hessian (_direct_likelihood.py:224) and the profiled der2
+// (_profile_likelihood.py:168) call: O(n b^2) per eta, about three times the
+// selected inversion's products.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256, 2) void bcr_sinv_x_kernel(const double* __restrict__ L,
-                                                            int64_t sL,
-                                                            const double* __restrict__ W,
-                                                            int64_t sW, double* __restrict__ X,
-                                                            int64_t sX, int m, int lvl) {
-  __shared__ double smem[4 * GSTAGE];
-  const int e = blockIdx.y;
-  const int h = blockIdx.x >> 1, side = blockIdx.x & 1;
-  const int p = 1 + 2 * h;
-  const int o = p << lvl;
-  if (side == 1 && p + 1 >= m) return;
-  d4 acc[4][4];
-  zero_tile(acc);
-  // X_s = W_s^T Linv_p
-  gemm_tile<KSLOW, KSLOW, false>(W + e * sW + ((int64_t)o * 2 + side) * TS * TS, TS,
-                                 L + e * sL + (int64_t)o * TS * TS, TS, TS, smem, acc);
-  store_tile(X + e * sX + ((int64_t)o * 2 + side) * TS * TS, TS, acc, 1.0);
+
+// the diagonal elements of a 128 x 128 accumulator tile (C/D map of load_tile):
+// acc += v on the diagonal
+__device__ __forceinline__ void tile_add_diag(d4 (&acc)[4][4], double v) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int wr = w >> 1, wc = w & 1, fr = lane & 15, fk = lane >> 4;
+  if (wr != wc) return;
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (fk + 4 * r == fr) acc[a][a][r] += v;
 }
 
-// acc -= op(M) Xs, op(M) = M (KFAST) or M^T (KSLOW)
-__device__ __forceinline__ void sinv_sub(const double* M, bool trans, const double* Xs,
-                                         double* smem, d4 (&acc)[4][4]) {
-  if (trans)
-    gemm_tile<KSLOW, KSLOW, true>(M, TS, Xs, TS, TS, smem, acc);
-  else
-    gemm_tile<KFAST, KSLOW, true>(M, TS, Xs, TS, TS, smem, acc);
-}
-
-__global__ __launch_bounds__(256, 2) void bcr_sinv_off_kernel(
-    const double* __restrict__ Zd, int64_t sZd, double* __restrict__ Zo, int64_t sZo,
-    const double* __restrict__ X, int64_t sX, int m, int lvl) {
-  __shared__ double smem[4 * GSTAGE];
-  const int e = blockIdx.y;
-  const int h = blockIdx.x >> 1, side = blockIdx.x & 1;
-  const int p = 1 + 2 * h;
-  const bool right = p + 1 < m;
-  if (side == 1 && !right) return;
-  const int o = p << lvl, ol = (p - 1) << lvl, orr = (p + 1) << lvl;
-  const double* Zde = Zd + e * sZd;
-  const double* Zoe = Zo + e * sZo;
-  const double* Xe = X + e * sX;
-  const double* Xl = Xe + ((int64_t)o * 2 + 0) * TS * TS;
-  const double* Xr = Xe + ((int64_t)o * 2 + 1) * TS * TS;
-  // the parents' coupling: stored as Z_lr (r' odd one level up) or Z_rl (l' odd)
-  const double* Mlr = nullptr;
-  bool lr_direct = true;
-  if (right) {
-    const int lp = (p - 1) >> 1;
-    if ((lp + 1) & 1) {
-      Mlr = Zoe + ((int64_t)orr * 2 + 0) * TS * TS;   // Z_{l', r'}
-    } else {
-      Mlr = Zoe + ((int64_t)ol * 2 + 1) * TS * TS;    // Z_{r', l'}
-      lr_direct = false;
-    }
-  }
-  d4 acc[4][4];
-  zero_tile(acc);
-  if (side == 0) {
-    sinv_sub(Zde + (int64_t)ol * TS * TS, false, Xl, smem, acc);   // Z_ll X_l
-    if (right) sinv_sub(Mlr, !lr_direct, Xr, smem, acc);         // Z_lr X_r
-  } else {
-    sinv_sub(Mlr, lr_direct, Xl, smem, acc);                       // Z_rl X_l
-    sinv_sub(Zde + (int64_t)orr * TS * TS, false, Xr, smem, acc);  // Z_rr X_r
-  }
-  store_tile(Zo + e * sZo + ((int64_t)o * 2 + side) * TS * TS, TS, acc, 1.0);
-}
-
-// Z_pp and tr Z_pp (rows < n) of the odd blocks p = 1 + 2 blockIdx.x of level lvl, or
-// (root != 0) the last level's single block 0.
-__global__ __launch_bounds__(256, 2) void bcr_sinv_diag_kernel(
-    const double* __restrict__ L, int64_t sL, const double* __restrict__ X, int64_t sX,
-    const double* __restrict__ Zo, int64_t sZo, double* __restrict__ Zd, int64_t sZd,
-    double* __restrict__ trpart, int nt, int64_t n, int m, int lvl, int root) {
-  __shared__ double smem[4 * GSTAGE];
-  const int e = blockIdx.y;
-  const int p = root ? 0 : 1 + 2 * blockIdx.x;
-  const int o = p << lvl;
-  const double* Lo = L + e * sL + (int64_t)o * TS * TS;
-  d4 acc[4][4];
-  zero_tile(acc);
-  gemm_tile<KSLOW, KSLOW, false>(Lo, TS, Lo, TS, TS, smem, acc);   // Linv^T Linv
-  if (!root) {
-    const double* Xe = X + e * sX;
-    const double* Zoe = Zo + e * sZo;
-    gemm_tile<KSLOW, KSLOW, true>(Xe + ((int64_t)o * 2) * TS * TS, TS,
-                                  Zoe + ((int64_t)o * 2) * TS * TS, TS, TS, smem, acc);
-    if (p + 1 < m)
-      gemm_tile<KSLOW, KSLOW, true>(Xe + ((int64_t)o * 2 + 1) * TS * TS, TS,
-                                    Zoe + ((int64_t)o * 2 + 1) * TS * TS, TS, TS, smem, acc);
-  }
-  store_tile(Zd + e * sZd + (int64_t)o * TS * TS, TS, acc, 1.0);
-  // the trace: diagonal elements (row = wr 64 + a 16 + fk + 4 r == col = wc 64 + a 16 + fr)
+// sum over the rows < n of the tile's diagonal (block o), to trpart (scaled by sign);
+// smem: 4 doubles of scratch
+__device__ __forceinline__ void tile_trace(const d4 (&acc)[4][4], int o, int64_t n, double sign,
+                                           double* smem, double* trpart) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int wr = w >> 1, wc = w & 1, fr = lane & 15, fk = lane >> 4;
   double v = 0.0;
@@ -584,7 +583,152 @@ __global__ __launch_bounds__(256, 2) void bcr_sinv_diag_kernel(
   __syncthreads();
   if (lane == 0) smem[w] = v;
   __syncthreads();
-  if (t == 0) trpart[(int64_t)e * nt + o] = (smem[0] + smem[1]) + (smem[2] + smem[3]);
+  if (t == 0) *trpart = sign * ((smem[0] + smem[1]) + (smem[2] + smem[3]));
+}
+
+// Block o's level, its index p there and the level's block count (m0 = nt blocks at
+// level 0, ceil(m / 2) each level up; o = 0 is the root, at level L with m = 1).
+__device__ __forceinline__ void bcr_node(int o, int nt, int L, int& lvl, int& p, int& m) {
+  lvl = o == 0 ? L : __builtin_ctz(o);
+  p = o >> lvl;
+  m = nt;
+  for (int l = 0; l < lvl; ++l) m = (m + 1) >> 1;
+}
+
+// Every eliminated block's factor-only terms, before the top-down pass. Workgroup
+// bx: block o = bx / (3 + 3 ntan), role = bx % (3 + 3 ntan) (roles 3-5: tangents):
+//   0: X_l = W_l^T Linv   1: X_r = W_r^T Linv (p + 1 < m)   2: Zd = Linv^T Linv
+//   3: dX_l               4: dX_r                           5: dZd = dLinv^T Linv + Linv^T dLinv
+// The root (o = 0) has roles 2 and 5 only, and its trace (it is final).
+__global__ __launch_bounds__(256, 2) void bcr_sinv_pre_kernel(
+    const double* __restrict__ L, const double* __restrict__ dL, int64_t sL,
+    const double* __restrict__ W, const double* __restrict__ dW, int64_t sW,
+    double* __restrict__ X, double* __restrict__ dX, int64_t sX, double* __restrict__ Zd,
+    double* __restrict__ dZd, int64_t sZd, double* __restrict__ trpart,
+    double* __restrict__ dtrpart, int nt, int nlev, int64_t n, int ntan) {
+  __shared__ double smem[4 * GSTAGE];
+  const int e = blockIdx.y;
+  const int o = blockIdx.x / (3 + 3 * ntan), role = blockIdx.x % (3 + 3 * ntan);
+  int lvl, p, m;
+  bcr_node(o, nt, nlev, lvl, p, m);
+  if (o == 0 && role != 2 && role != 5) return;
+  if ((role == 1 || role == 4) && p + 1 >= m) return;
+  const int64_t lo = e * sL + (int64_t)o * TS * TS;
+  const double* Lo = L + lo;
+  const bool tan = role >= 3;
+  const int side = (role % 3) == 1 ? 1 : 0;
+  const int64_t wo = e * sW + ((int64_t)o * 2 + side) * TS * TS;
+  d4 acc[4][4];
+  zero_tile(acc);
+  const int nterm = tan ? 2 : 1;
+#pragma unroll 1
+  for (int t = 0; t < nterm; ++t) {
+    const double* A;
+    const double* Bm;
+    if (role % 3 == 2) {   // Linv^T Linv;  dLinv^T Linv + Linv^T dLinv
+      A = (tan && t == 0) ? dL + lo : Lo;
+      Bm = (tan && t == 1) ? dL + lo : Lo;
+    } else {               // W_s^T Linv;   dW_s^T Linv + W_s^T dLinv
+      A = (tan && t == 0) ? dW + wo : W + wo;
+      Bm = (tan && t == 1) ? dL + lo : Lo;
+    }
+    gemm_tile<KSLOW, KSLOW, false>(A, TS, Bm, TS, TS, smem, acc);
+  }
+  if (role % 3 == 2) {
+    store_tile((tan ? dZd : Zd) + e * sZd + (int64_t)o * TS * TS, TS, acc, 1.0);
+    if (o == 0)
+      tile_trace(acc, 0, n, tan ? -1.0 : 1.0, smem, (tan ? dtrpart : trpart) + (int64_t)e * nt);
+  } else {
+    store_tile((tan ? dX : X) + e * sX + ((int64_t)o * 2 + side) * TS * TS, TS, acc, 1.0);
+  }
+}
+
+// Z_sp (and with tangents, ntan = 1, dZ_sp) of the odd blocks p = 1 + 2 h of level
+// lvl: workgroup bx = (2 + 2 ntan) h + 2 tan + side (grid (2 + 2 ntan) nodd).
+//   Z_lp  = -(Z_ll X_l + Z_lr X_r)            Z_rp = -(Z_rl X_l + Z_rr X_r)
+//   dZ_lp = -(dZ_ll X_l + Z_ll dX_l + dZ_lr X_r + Z_lr dX_r), dZ_rp likewise.
+// The products run in a rolled loop on the runtime-layout product (the coupling Z_lr
+// is stored directly or transposed): one inlined product per kernel.
+__global__ __launch_bounds__(256, 2) void bcr_sinv_off_kernel(
+    const double* __restrict__ Zd, const double* __restrict__ dZd, int64_t sZd,
+    double* __restrict__ Zo, double* __restrict__ dZo, int64_t sZo,
+    const double* __restrict__ X, const double* __restrict__ dX, int64_t sX, int m, int lvl,
+    int ntan) {
+  __shared__ double smem[4 * GSTAGE];
+  const int e = blockIdx.y;
+  const int R = 2 + 2 * ntan;
+  const int h = blockIdx.x / R, tan = (blockIdx.x % R) >> 1, side = blockIdx.x & 1;
+  const int p = 1 + 2 * h;
+  const bool right = p + 1 < m;
+  if (side == 1 && !right) return;
+  const int o = p << lvl, ol = (p - 1) << lvl, orr = (p + 1) << lvl;
+  const double* Xl = X + e * sX + ((int64_t)o * 2 + 0) * TS * TS;
+  const double* Xr = Xl + TS * TS;
+  const double* dXl = dX + e * sX + ((int64_t)o * 2 + 0) * TS * TS;
+  const double* dXr = dXl + TS * TS;
+  // the parents' coupling: stored as Z_lr (r' odd one level up) or Z_rl (l' odd)
+  int64_t qlr = 0;
+  bool lr_direct = true;
+  if (right) {
+    const int lp = (p - 1) >> 1;
+    if ((lp + 1) & 1) {
+      qlr = ((int64_t)orr * 2 + 0) * TS * TS;   // Z_{l', r'}
+    } else {
+      qlr = ((int64_t)ol * 2 + 1) * TS * TS;    // Z_{r', l'}
+      lr_direct = false;
+    }
+  }
+  const double* Mlr = Zo + e * sZo + qlr;
+  const double* dMlr = dZo + e * sZo + qlr;
+  const int64_t qd = e * sZd + (int64_t)(side == 0 ? ol : orr) * TS * TS;
+  d4 acc[4][4];
+  zero_tile(acc);
+  // terms in order: the X_l pair, then the X_r pair; the primal has one term per pair
+  const int per = tan ? 2 : 1;
+#pragma unroll 1
+  for (int t = 0; t < 2 * per; ++t) {
+    const bool xl = t < per;
+    if (side == 0 && !xl && !right) break;
+    const bool diag = (side == 0) == xl;                // Z_ll (side 0) / Z_rr (side 1)
+    const bool dz = tan && ((t % per) == 0);            // the term with the Z tangent
+    const bool dx = tan && !dz;                         // the term with the X tangent
+    const double* M = diag ? (dz ? dZd : Zd) + qd : (dz ? dMlr : Mlr);
+    const bool trans = diag ? false : (side == 0 ? !lr_direct : lr_direct);
+    const double* Xs = xl ? (dx ? dXl : Xl) : (dx ? dXr : Xr);
+    gemm_tile_ra<true>(M, trans, Xs, smem, acc);
+  }
+  store_tile((tan ? dZo : Zo) + e * sZo + ((int64_t)o * 2 + side) * TS * TS, TS, acc, 1.0);
+}
+
+// Z_pp (and with ntan = 1 dZ_pp) of the odd blocks p = 1 + 2 h, workgroup
+// bx = (1 + ntan) h + tan, from the
+// pre-pass terms: Z_pp = Zd_pre - X_l^T Z_lp - X_r^T Z_rp, dZ_pp = dZd_pre
+// - dX_l^T Z_lp - X_l^T dZ_lp - dX_r^T Z_rp - X_r^T dZ_rp; their traces (rows < n;
+// the tangent's negated: -tr dZ_pp = tr (B + eta I)^-2 of the block).
+__global__ __launch_bounds__(256, 2) void bcr_sinv_diag_kernel(
+    const double* __restrict__ X, const double* __restrict__ dX, int64_t sX,
+    const double* __restrict__ Zo, const double* __restrict__ dZo, int64_t sZo,
+    double* __restrict__ Zd, double* __restrict__ dZd, int64_t sZd, double* __restrict__ trpart,
+    double* __restrict__ dtrpart, int nt, int64_t n, int m, int lvl, int ntan) {
+  __shared__ double smem[4 * GSTAGE];
+  const int e = blockIdx.y;
+  const int p = 1 + 2 * (blockIdx.x / (1 + ntan)), tan = blockIdx.x % (1 + ntan);
+  const int o = p << lvl;
+  double* Zdst = (tan ? dZd : Zd) + e * sZd + (int64_t)o * TS * TS;
+  d4 acc[4][4];
+  load_tile(Zdst, TS, acc);
+  const int per = tan ? 2 : 1;
+  const int nterm = (p + 1 < m ? 2 : 1) * per;
+#pragma unroll 1
+  for (int t = 0; t < nterm; ++t) {
+    const int64_t q = ((int64_t)o * 2 + t / per) * TS * TS;
+    const bool dxt = tan && (t % per) == 0;   // dX_s^T Z_sp, then X_s^T dZ_sp
+    const double* A = (dxt ? dX : X) + e * sX + q;
+    const double* Bm = ((tan && !dxt) ? dZo : Zo) + e * sZo + q;
+    gemm_tile<KSLOW, KSLOW, true>(A, TS, Bm, TS, TS, smem, acc);
+  }
+  store_tile(Zdst, TS, acc, 1.0);
+  tile_trace(acc, o, n, tan ? -1.0 : 1.0, smem, (tan ? dtrpart : trpart) + (int64_t)e * nt + o);
 }
 
 // tr[e] = sum_o trpart[e][o] in block order.
@@ -595,6 +739,126 @@ __global__ void bcr_sinv_final_kernel(const double* __restrict__ trpart, int nt,
   double sum = 0.0;
   for (int o = 0; o < nt; ++o) sum += trpart[(int64_t)e * nt + o];
   tr[e] = sum;
+}
+
+// ---------------------------------------------------------------------------
+// Factor tangents (the roles bcr_w_kernel / bcr_upd_kernel run beside the primal
+// workgroups, and bcr_dupd_kernel).
+// ---------------------------------------------------------------------------
+
+// dLinv of eliminated block p of level lvl. dD: level 0 the identity, else dDin's
+// blocks by level index. scr (per block 2 x 128^2, by original index) holds Linv dD
+// and M: the three products run in one workgroup, through global memory (written,
+// then read by the same workgroup after a barrier).
+__device__ void bcr_dfac_role(const double* __restrict__ L, int64_t sL,
+                              const double* __restrict__ dDin, int64_t sdD,
+                              double* __restrict__ scr, int64_t sS, double* __restrict__ dL,
+                              int lvl, int p, double* smem) {
+  const int e = blockIdx.y;
+  const int o = p << lvl;
+  const double* Lo = L + e * sL + (int64_t)o * TS * TS;
+  double* T = scr + e * sS + (int64_t)o * 2 * TS * TS;
+  double* Mm = T + TS * TS;
+  d4 acc[4][4];
+  const double* Tsrc = Lo;   // Linv dD (dD = I at level 0)
+  if (lvl > 0) {
+    zero_tile(acc);
+    gemm_tile<KFAST, KSLOW, false>(Lo, TS, dDin + e * sdD + (int64_t)p * TS * TS, TS, TS, smem,
+                                   acc);
+    store_tile(T, TS, acc, 1.0);
+    __syncthreads();
+    Tsrc = T;
+  }
+  zero_tile(acc);
+  gemm_tile<KFAST, KFAST, false>(Tsrc, TS, Lo, TS, TS, smem, acc);   // (Linv dD) Linv^T
+  {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int wr = w >> 1, wc = w & 1, fr = lane & 15, fk = lane >> 4;
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = wr * 64 + a * 16 + fk + 4 * r, col = wc * 64 + c * 16 + fr;
+          acc[a][c][r] = col > row ? 0.0 : (col == row ? 0.5 * acc[a][c][r] : acc[a][c][r]);
+        }
+  }
+  store_tile(Mm, TS, acc, 1.0);
+  __syncthreads();
+  zero_tile(acc);
+  gemm_tile<KFAST, KSLOW, true>(Mm, TS, Lo, TS, TS, smem, acc);     // -M Linv
+  store_tile(dL + e * sL + (int64_t)o * TS * TS, TS, acc, 1.0);
+}
+
+// dW of odd block p = 1 + 2 (bx >> 1), which = bx & 1 as bcr_w_role. F / dF: level 0
+// the shared F0 (sF = 0) and dF = 0 (dFin unused), else the level's.
+__device__ void bcr_dw_role(int bx, const double* __restrict__ L, const double* __restrict__ dL,
+                            int64_t sL, const double* __restrict__ Fin, int64_t sF,
+                            const double* __restrict__ dFin, int64_t sdF, double* __restrict__ dW,
+                            int64_t sW, int m, int lvl, double* smem) {
+  const int e = blockIdx.y;
+  const int h = bx >> 1, which = bx & 1;
+  const int p = 1 + 2 * h;
+  const int o = p << lvl;
+  if (which == 1 && p + 1 >= m) return;
+  const int64_t lo = e * sL + (int64_t)o * TS * TS;
+  const int fi = which == 0 ? p - 1 : p;
+  const double* F = Fin + e * sF + (int64_t)fi * TS * TS;
+  const double* dF = dFin + e * sdF + (int64_t)fi * TS * TS;
+  d4 acc[4][4];
+  zero_tile(acc);
+  const int nterm = lvl > 0 ? 2 : 1;
+  // (accumulated negated: the product form of bcr_upd_kernel's other roles, one
+  // inlined product per kernel; the sign is flipped at the store)
+#pragma unroll 1
+  for (int t = 0; t < nterm; ++t)   // . F_{p-1} (which 0) or . F_p^T (which 1)
+    gemm_tile_rr<true>(t == 0 ? dL + lo : L + lo, false, t == 0 ? F : dF, which == 0, smem, acc);
+  store_tile(dW + e * sW + ((int64_t)o * 2 + which) * TS * TS, TS, acc, -1.0);
+}
+
+// dD_j' / dF_{j/2}' of the even blocks j = 2 (bx >> 1), which = bx & 1.
+__global__ __launch_bounds__(256, 2) void bcr_dupd_kernel(
+    const double* __restrict__ W, const double* __restrict__ dW, int64_t sW,
+    const double* __restrict__ dDin, int64_t sdD, double* __restrict__ dDout,
+    double* __restrict__ dFout, int64_t sO, int m, int lvl) {
+  __shared__ double smem[4 * GSTAGE];
+  const int e = blockIdx.y;
+  const int h = blockIdx.x >> 1, which = blockIdx.x & 1;
+  const int j = 2 * h;
+  const double* We = W + e * sW;
+  const double* dWe = dW + e * sW;
+  d4 acc[4][4];
+  if (which == 1) {
+    if (j + 2 >= m) return;
+    const int64_t ol = ((int64_t)((j + 1) << lvl) * 2 + 0) * TS * TS;
+    const int64_t orr = ((int64_t)((j + 1) << lvl) * 2 + 1) * TS * TS;
+    zero_tile(acc);
+#pragma unroll 1
+    for (int t = 0; t < 2; ++t)   // -(dW_r^T W_l + W_r^T dW_l)
+      gemm_tile<KSLOW, KSLOW, true>((t == 0 ? dWe : We) + orr, TS, (t == 0 ? We : dWe) + ol, TS,
+                                    TS, smem, acc);
+    store_tile(dFout + e * sO + (int64_t)h * TS * TS, TS, acc, 1.0);
+    return;
+  }
+  if (lvl == 0) {
+    zero_tile(acc);
+    tile_add_diag(acc, 1.0);
+  } else {
+    load_tile(dDin + e * sdD + (int64_t)j * TS * TS, TS, acc);
+  }
+  // (dW_r^T W_r + W_r^T dW_r)(j - 1), then (dW_l^T W_l + W_l^T dW_l)(j + 1), in a
+  // rolled loop (straight-line, the four products spilled)
+  const int64_t ql = ((int64_t)((j - 1) << lvl) * 2 + 1) * TS * TS;
+  const int64_t qr = ((int64_t)((j + 1) << lvl) * 2 + 0) * TS * TS;
+#pragma unroll 1
+  for (int t = 0; t < 4; ++t) {
+    if (t < 2 ? j < 1 : j + 1 >= m) continue;
+    const int64_t q = t < 2 ? ql : qr;
+    gemm_tile<KSLOW, KSLOW, true>((t & 1) ? We + q : dWe + q, TS, (t & 1) ? dWe + q : We + q, TS,
+                                  TS, smem, acc);
+  }
+  store_tile(dDout + e * sO + (int64_t)h * TS * TS, TS, acc, 1.0);
 }
 
 }  // namespace gpmi

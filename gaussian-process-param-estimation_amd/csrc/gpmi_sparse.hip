@@ -1332,6 +1332,40 @@ void launch_ms_dots(const double* B, const double* R, int64_t n, int s, double* 
 // the shift step k - 1 (the zeta / G / b . p recurrences of ms_tail_kernel, which need
 // beta_{k-1}, known only now, and B^T r_k), then writes the next scalar state (nxt),
 // the batch end state into pinned memory (pin) and the stopping iteration.
+// zeta_k and alpha_{k-1} of shift j for column c (the shifted recurrence of step k - 1
+// from the unshifted alpha_{k-1}, alpha_{k-2}, beta_{k-1} in cur).
+__device__ __forceinline__ void ms_shift_step(const MsScal& cur, const MsShift& sh,
+                                              const double* __restrict__ dshift, int s, int j,
+                                              int c, double& zn, double& as) {
+  const double a = cur.a[c], ap = cur.a_prev[c], bo = cur.beta[c];
+  const double z = sh.z[j * s + c], zp = sh.z_prev[j * s + c];
+  const double d = dshift[j];
+  zn = z * zp * ap / (a * bo * (zp - z) + zp * ap * (1.0 + d * a));
+  as = a * zn / z;
+}
+
+// After the last iteration: ms_cg2_update_kernel applies shift step k - 1 during
+// iteration k (its b . p update needs beta_k), so a loop that ends at maxiter with
+// columns still active has not applied their last step's G update. This applies it
+// (G += alpha^s_{k-1} b . p^s for the columns that took step k - 1; one workgroup).
+// A no-op when every column had stopped.
+__global__ __launch_bounds__(256) void ms_cg2_close_kernel(MsScal cur, MsShift sh,
+                                                           const double* __restrict__ dshift,
+                                                           int S, int s, int nb) {
+  for (int task = threadIdx.x; task < S * s; task += blockDim.x) {
+    const int j = task / s, c = task % s;
+    if (!cur.active[c]) continue;
+    double zn, as;
+    ms_shift_step(cur, sh, dshift, s, j, c, zn, as);
+    for (int cp = 0; cp < nb; ++cp) {
+      const int e = (j * nb + cp) * s + c;
+      sh.g[e] += as * sh.bp[e];
+    }
+    sh.z_prev[j * s + c] = sh.z[j * s + c];
+    sh.z[j * s + c] = zn;
+  }
+}
+
 __global__ __launch_bounds__(256) void ms_cg2_update_kernel(
     const double* __restrict__ B, double* __restrict__ R, const double* __restrict__ W,
     double* __restrict__ Sv, MsScal cur, MsScal nxt, MsShift sh,
@@ -1409,11 +1443,9 @@ __global__ __launch_bounds__(256) void ms_cg2_update_kernel(
     for (int task = t; task < S * s; task += blockDim.x) {
       const int j = task / s, c = task % s;
       if (!cur.active[c]) continue;   // step k - 1 not taken by this column
-      const double a = cur.a[c], ap = cur.a_prev[c], bo = cur.beta[c];
-      const double z = sh.z[j * s + c], zp = sh.z_prev[j * s + c];
-      const double d = dshift[j];
-      const double zn = z * zp * ap / (a * bo * (zp - z) + zp * ap * (1.0 + d * a));
-      const double as = a * zn / z;
+      const double z = sh.z[j * s + c];
+      double zn, as;
+      ms_shift_step(cur, sh, dshift, s, j, c, zn, as);
       const double bs = sbe[c] * (zn / z) * (zn / z);
       double bpv[MS_MAXS], gv[MS_MAXS];
 #pragma unroll

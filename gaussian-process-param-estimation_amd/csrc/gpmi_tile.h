@@ -98,6 +98,97 @@ __device__ __forceinline__ void gemm_tile(const double* __restrict__ P1, int64_t
   }
 }
 
+// gemm_tile<AL, BL, NEG> with both operands' layouts chosen at run time (a_slow /
+// b_slow, uniform: KSLOW, else KFAST), leading dimensions 128: every layout is staged
+// k-major ([16][SLD], a KFAST operand by a transposing LDS store), so one MFMA loop
+// serves all four. For kernels whose products mix layouts (in a rolled loop, or in
+// different workgroup roles of one launch): one inlined product instead of one per
+// layout pair (two or three in one kernel spilled 92-136 VGPRs). The MFMA sequence
+// per output element is gemm_tile's: the same results.
+__device__ __forceinline__ void rt_load(const double* __restrict__ P, bool slow, int k0,
+                                        d2 (&r)[4]) {
+  if (slow) {
+    gl_op<KSLOW>(P, TS, k0, r);
+    return;
+  }
+  const int t = threadIdx.x;
+  const double* p = P + (int64_t)(t >> 1) * TS + k0 + (t & 1) * 8;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) r[q] = *reinterpret_cast<const d2*>(p + 2 * q);
+}
+
+__device__ __forceinline__ void rt_store(double* s, bool slow, const d2 (&r)[4]) {
+  if (slow) {
+    st_op<KSLOW>(s, r);
+    return;
+  }
+  const int t = threadIdx.x, row = t >> 1, kc = (t & 1) * 8;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    s[(kc + 2 * q) * SLD + row] = r[q][0];
+    s[(kc + 2 * q + 1) * SLD + row] = r[q][1];
+  }
+}
+
+template <bool NEG>
+__device__ __forceinline__ void gemm_tile_rr(const double* __restrict__ P1, bool a_slow,
+                                             const double* __restrict__ P2, bool b_slow,
+                                             double* smem, d4 (&acc)[4][4]) {
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int wr = w >> 1, wc = w & 1, fr = lane & 15, fk = lane >> 4;
+  double* sA = smem;
+  double* sB = smem + 2 * GSTAGE;
+  d2 ra[4], rb[4];
+  rt_load(P1, a_slow, 0, ra);
+  rt_load(P2, b_slow, 0, rb);
+  rt_store(sA, a_slow, ra);
+  rt_store(sB, b_slow, rb);
+  __syncthreads();
+  __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0) expcnt(7) lgkmcnt(15), as gemm_tile
+  constexpr int nsteps = TS / BK;
+  for (int s = 0; s < nsteps; ++s) {
+    const int cur = s & 1;
+    const double* cA = sA + cur * GSTAGE;
+    const double* cB = sB + cur * GSTAGE;
+    if (s + 1 < nsteps) {
+      rt_load(P1, a_slow, (s + 1) * BK, ra);
+      rt_load(P2, b_slow, (s + 1) * BK, rb);
+    }
+#pragma unroll
+    for (int kk = 0; kk < BK / 4; ++kk) {
+      double a[4], b[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = cA[(kk * 4 + fk) * SLD + wr * 64 + i * 16 + fr];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = cB[(kk * 4 + fk) * SLD + wc * 64 + j * 16 + fr];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = NEG ? mfma64_neg(a[i], b[j], acc[i][j]) : mfma64(a[i], b[j], acc[i][j]);
+    }
+    if (s + 1 < nsteps) {
+      rt_store(sA + (cur ^ 1) * GSTAGE, a_slow, ra);
+      rt_store(sB + (cur ^ 1) * GSTAGE, b_slow, rb);
+    }
+    __syncthreads();
+  }
+}
+
+template <bool NEG>
+__device__ __forceinline__ void gemm_tile_ra(const double* __restrict__ P1, bool a_slow,
+                                             const double* __restrict__ P2, double* smem,
+                                             d4 (&acc)[4][4]) {
+  gemm_tile_rr<NEG>(P1, a_slow, P2, true, smem, acc);
+}
+
+__device__ __forceinline__ void neg_tile(d4 (&acc)[4][4]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = -acc[i][j];
+}
+
 // One 64 x 64 quadrant (qr, qc) of the 128 x 128 product above, each wave a 32 x 32
 // piece (wave w: rows qr*64 + (w>>1)*32, columns qc*64 + (w&1)*32). Four workgroups
 // then cover one output tile with a quarter of the MFMA chain each: the band's serial

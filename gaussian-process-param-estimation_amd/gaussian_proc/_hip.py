@@ -103,6 +103,11 @@ SIGNATURES = {
                                               c_int_p]),
     'gpmi_band_traceinv': (ctypes.c_int, [c_op_p, c_double_p, ctypes.c_int, c_double_p,
                                           c_int_p]),
+    'gpmi_band_der_terms_ex2': (ctypes.c_int, [c_op_p, c_double_p, ctypes.c_int, c_double_p,
+                                               c_double_p, c_double_p, c_double_p, c_double_p,
+                                               c_double_p, c_int_p]),
+    'gpmi_band_traceinv2': (ctypes.c_int, [c_op_p, c_double_p, ctypes.c_int, c_double_p,
+                                           c_double_p, c_int_p]),
     'gpmi_band_sinv_ms': (ctypes.c_int, [c_op_p, c_double_p]),
     'gpmi_band_stats': (ctypes.c_int, [c_op_p, c_int_p, c_int_p]),
     'gpmi_band_cq_stats': (ctypes.c_int, [c_op_p, c_int_p, c_int_p, c_int_p]),
@@ -401,12 +406,14 @@ class Band(object):
         """-> (logdet[neta], g1, g2, g3 [neta, nrhs, nrhs], info[neta]) with
         gp = R^T (K + eta I)^-p R for the resident RHS R; with ``traceinv`` also
         tr1[neta] = trace((K + eta I)^-1) (selected inversion, no eigenvalues),
-        appended as the last-but-one item."""
+        appended as the last-but-one item; with ``traceinv=2`` also
+        tr2[neta] = trace((K + eta I)^-2) (its eta-tangent), after tr1."""
         etas = as_c(numpy.atleast_1d(etas))
         ne, m = etas.shape[0], self.nrhs
         ld = numpy.empty(ne)
         g = [numpy.empty((ne, m, m)) for _ in range(3)]
         tr = numpy.empty(ne)
+        tr2 = numpy.empty(ne)
         info = numpy.zeros(ne, dtype=numpy.int32)
         chunk = self.TR_CHUNK if traceinv else self.DER_CHUNK
         for i in range(0, ne, chunk):
@@ -417,11 +424,15 @@ class Band(object):
             ik = numpy.zeros(k, dtype=numpy.int32)
             if traceinv:
                 tk = numpy.empty(k)
-                check(self.lib.gpmi_band_der_terms_ex(self.h, dptr(e), k, dptr(ldk),
-                                                      dptr(gk[0]), dptr(gk[1]), dptr(gk[2]),
-                                                      dptr(tk), ik.ctypes.data_as(c_int_p)),
-                      'gpmi_band_der_terms_ex')
+                t2k = numpy.empty(k)
+                check(self.lib.gpmi_band_der_terms_ex2(self.h, dptr(e), k, dptr(ldk),
+                                                       dptr(gk[0]), dptr(gk[1]), dptr(gk[2]),
+                                                       dptr(tk),
+                                                       dptr(t2k) if traceinv == 2 else None,
+                                                       ik.ctypes.data_as(c_int_p)),
+                      'gpmi_band_der_terms_ex2')
                 tr[i:i + k] = tk
+                tr2[i:i + k] = t2k
             else:
                 check(self.lib.gpmi_band_der_terms(self.h, dptr(e), k, dptr(ldk), dptr(gk[0]),
                                                    dptr(gk[1]), dptr(gk[2]),
@@ -430,13 +441,19 @@ class Band(object):
             ld[i:i + k], info[i:i + k] = ldk, ik
             for q in range(3):
                 g[q][i:i + k] = gk[q]
+        if traceinv == 2:
+            return ld, g[0], g[1], g[2], tr, tr2, info
         if traceinv:
             return ld, g[0], g[1], g[2], tr, info
         return ld, g[0], g[1], g[2], info
 
-    def traceinv(self, etas):
-        """-> (tr[neta], info[neta]): trace((K + eta I)^-1) by selected inversion of
-        the cyclic-reduction factor of B + eta I (gpmi_band_traceinv)."""
+    def traceinv(self, etas, exponent=1):
+        """-> (tr[neta], info[neta]): trace((K + eta I)^-exponent), exponent 1 or 2,
+        by selected inversion of the cyclic-reduction factor of B + eta I (exponent
+        2: its eta-tangent, trace((B + eta I)^-2) = -d/deta trace((B + eta I)^-1);
+        gpmi_band_traceinv2)."""
+        if exponent not in (1, 2):
+            raise ValueError('selected inversion gives exponent 1 or 2')
         etas = as_c(numpy.atleast_1d(etas))
         ne = etas.shape[0]
         tr = numpy.empty(ne)
@@ -445,10 +462,14 @@ class Band(object):
             e = as_c(etas[i:i + self.TR_CHUNK])
             k = e.shape[0]
             tk = numpy.empty(k)
+            t2k = numpy.empty(k)
             ik = numpy.zeros(k, dtype=numpy.int32)
-            check(self.lib.gpmi_band_traceinv(self.h, dptr(e), k, dptr(tk),
-                                              ik.ctypes.data_as(c_int_p)), 'gpmi_band_traceinv')
-            tr[i:i + k], info[i:i + k] = tk, ik
+            check(self.lib.gpmi_band_traceinv2(self.h, dptr(e), k, dptr(tk),
+                                               dptr(t2k) if exponent == 2 else None,
+                                               ik.ctypes.data_as(c_int_p)),
+                  'gpmi_band_traceinv2')
+            tr[i:i + k] = tk if exponent == 1 else t2k
+            info[i:i + k] = ik
         return tr, info
 
     def sinv_ms(self):
@@ -482,8 +503,12 @@ class Band(object):
         check(self.lib.gpmi_band_der_ms(self.h, ctypes.byref(v)), 'gpmi_band_der_ms')
         return v.value
 
+    # gpmi_band_eigenvalues calls made by this process (bench: the optimizer's count)
+    eigenvalue_calls = 0
+
     def eigenvalues(self):
         """The n eigenvalues of K, ascending (device bulge chase + bisection)."""
+        Band.eigenvalue_calls += 1
         lam = numpy.empty(self.n)
         check(self.lib.gpmi_band_eigenvalues(self.h, dptr(lam)), 'gpmi_band_eigenvalues')
         return lam

@@ -19,7 +19,9 @@ as in the reference. The Jacobian / Hessian keep the reference formulas
 (derivatives w.r.t. sigma^2 and sigma0^2 — reference quirk) on top
 of the operator duck type; on the dense eigenvalue operator (sigma not ~ 0) the
 same quantities come from the band Gram blocks Gp = R^T (K + eta I)^-p R,
-p = 1..3, and the eigenvalue traces (_jac_hess_from_terms), with no dense solve.
+p = 1..3, and tr((K + eta I)^-1), tr((K + eta I)^-2) from the same factor
+(selected inversion and its eta-tangent; _jac_hess_from_terms), with no dense
+solve and no eigenvalues.
 """
 
 import numpy
@@ -224,9 +226,9 @@ class DirectLikelihood(object):
         small = numpy.abs(sigma) < _TOL_HESS
         if not small and _use_band(K_mixed):
             eta = (sigma0 / sigma) ** 2
-            _, G1, G2, G3, tr1 = K_mixed.der_terms([eta], X, z, traceinv=True)
+            _, G1, G2, G3, tr1, tr2 = K_mixed.der_terms([eta], X, z, traceinv=2)
             hess = _jac_hess_from_terms(n, m, sigma, eta, G1[0], G2[0], G3[0], tr1[0],
-                                        K_mixed.traceinv(eta, 2))[1]
+                                        tr2[0])[1]
             if hess is not None:
                 return -hess if sign_switch else hess
         if small:

@@ -11,8 +11,9 @@ The reference materialises Y B^-1 Y^T as an n x n matrix (:73); the value is the
 same. The eta-derivatives (:91-192) keep the reference formulas on the operator
 duck type; on the dense eigenvalue operator they come instead from the Gram
 blocks Gp = [X z]^T (K + eta I)^-p [X z], p = 1..3, of the band path
-(MixedCorrelation.der_terms, any number of eta per call) and traceinv from the
-eigenvalues, with the same algebra written in those blocks (_der_from_terms).
+(MixedCorrelation.der_terms, any number of eta per call) and traceinv of
+exponents 1 and 2 from the same factor (selected inversion and its eta-tangent),
+with the same algebra written in those blocks (_der_from_terms).
 """
 
 import numpy
@@ -116,9 +117,8 @@ class ProfileLikelihood(object):
     def log_likelihood_der2_eta(z, X, K_mixed, eta):               # :138-192
         n, m = X.shape
         if _use_band(K_mixed):
-            _, G1, G2, G3, tr1 = K_mixed.der_terms([eta], X, z, traceinv=True)
-            return float(_der_from_terms(n, m, G1[0], G2[0], G3[0], tr1[0],
-                                         K_mixed.traceinv(eta, exponent=2))[1])
+            _, G1, G2, G3, tr1, tr2 = K_mixed.der_terms([eta], X, z, traceinv=2)
+            return float(_der_from_terms(n, m, G1[0], G2[0], G3[0], tr1[0], tr2[0])[1])
         Y, Binv, Mz = ProfileLikelihood._mz(z, X, K_mixed, eta)
         V = K_mixed.solve(eta, Y)
         A = Binv @ (Y.T @ Y)

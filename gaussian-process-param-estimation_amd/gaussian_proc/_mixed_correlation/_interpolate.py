@@ -3,11 +3,21 @@
 The reference builds ``imate.InterpolateTraceInv(K, traceinv_options=...)``
 (mixed_correlation.py:52-66) and, when interpolating, answers every
 ``traceinv(eta, exponent)`` with the interpolant of tr((K + eta I)^-1)
-(:167-170; the exponent is ignored there, kept here). imate is absent from this
+(:167-170; the exponent is ignored there, and here). imate is absent from this
 environment (unpinned, requirements.txt:5), so its interpolation variants
-cannot be reproduced value for value: parity unpinned. This module restates
-the published idea behind them (Ameli and Shadden, interpolation of the trace
-of the inverse of A + t B): with tau(t) = tr((K + t I)^-1) / n,
+cannot be reproduced value for value: parity unpinned.
+
+A deliberate divergence ("Interpolation"): the reference
+requires ``interpolant_points`` to be given (:52-55, TypeError when None) but
+never passes them to imate (:65-66), so imate interpolates on its own default
+points. This build interpolates on the CALLER's ``interpolant_points`` (the
+exact traceinv at each of them is a node of the interpolant): the points a user
+chose are the ones used, and the result is exact there. imate's default point
+set is not restated (its version is unpinned and absent).
+
+This module restates the published idea behind imate's interpolants (Ameli and
+Shadden, interpolation of the trace of the inverse of A + t B): with
+tau(t) = tr((K + t I)^-1) / n,
 
     phi(t) = 1 / tau(t) - t
 

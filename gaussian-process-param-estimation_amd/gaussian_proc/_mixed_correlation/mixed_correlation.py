@@ -8,9 +8,12 @@ once per operator.
   :76-79, then cheap per-eta logdet, :239-248): the device reduces K once to
   band form K = Q B Q^T (bandwidth 128, csrc/gpmi_band.hip, on first use);
   logdet(eta) and the likelihood terms are then one banded Cholesky of
-  B + eta I per eta. traceinv / trace of any exponent are sums over the
-  eigenvalues of B (= those of K; device bulge chase + bisection, computed once
-  on first use, csrc/gpmi_chase.hip), as imate's 'eigenvalue' method (:172-181).
+  B + eta I per eta. traceinv of exponent 1 and 2 comes from selected inversion
+  of that factor (and its eta-tangent, gpmi_bcr.hip); trace / traceinv of other
+  exponents are sums over the eigenvalues of B (= those of K; device bulge chase
+  + bisection, computed once on first use, csrc/gpmi_chase.hip), as imate's
+  'eigenvalue' method (:172-181), which also serves exponents 1 and 2 once the
+  eigenvalues exist.
   solve(eta, Y) uses the dense Cholesky below.
 * 'cholesky' (and 'hutchinson' for logdet, which the reference maps to
   Cholesky at :250-261): one fp64 MFMA Cholesky of K + eta I
@@ -295,49 +298,54 @@ class MixedCorrelation(object):
         (csrc/gpmi_band.hip, gpmi_bcr.hip). They replace the 2-5 dense solves
         per eta of ProfileLikelihood.log_likelihood_der1_eta / der2_eta
         (_profile_likelihood.py:91-192). Returns (logdet, G1, G2, G3); with
-        ``traceinv`` also tr1 = trace((K + eta I)^-1) per eta, appended: from the
-        eigenvalues when they are already computed (mixed_correlation.py:172-181),
-        else by selected inversion of the same cyclic-reduction factor on the
-        device (gpmi_band_der_terms_ex), without the one-time eigenvalue chase."""
+        ``traceinv`` (True or 1) also tr1 = trace((K + eta I)^-1) per eta,
+        appended, and with ``traceinv=2`` tr1 and tr2 = trace((K + eta I)^-2):
+        from the eigenvalues when they are already computed
+        (mixed_correlation.py:172-181), else from the same cyclic-reduction factor
+        on the device (gpmi_band_der_terms_ex2: selected inversion, and for tr2
+        its eta-tangent), without the one-time eigenvalue chase."""
         if self.imate_method != 'eigenvalue':
             raise NotImplementedError('der_terms needs the eigenvalue operator')
         etas = numpy.atleast_1d(numpy.asarray(etas, dtype=float))
+        want = 0 if not traceinv else (2 if traceinv == 2 else 1)
         b = self._band_rhs_set(X, z)
         c = getattr(self, '_der_cache', None)
         # the Jacobian and Hessian of one point ask for the same eta: reuse
         if c is not None and c[0] is self._band_rhs and c[1] is b and \
-                numpy.array_equal(c[2], etas) and (not traceinv or c[4] is not None or
-                                                   self._eig is not None):
-            res, tr1 = c[3], c[4]
-        elif traceinv and self._eig is None:
-            ld, g1, g2, g3, tr1, info = b.der_terms(etas, traceinv=True)
+                numpy.array_equal(c[2], etas) and (c[5] >= want or self._eig is not None):
+            res, trs = c[3], c[4]
+        elif want and self._eig is None:
+            out = b.der_terms(etas, traceinv=want)
+            info = out[-1]
             self._check_info(etas, info)
-            res = (ld, g1, g2, g3)
-            self._der_cache = (self._band_rhs, b, etas.copy(), res, tr1)
+            res, trs = out[:4], out[4:-1]
+            self._der_cache = (self._band_rhs, b, etas.copy(), res, trs, want)
         else:
             ld, g1, g2, g3, info = b.der_terms(etas)
             self._check_info(etas, info)
-            res, tr1 = (ld, g1, g2, g3), None
-            self._der_cache = (self._band_rhs, b, etas.copy(), res, None)
-        if not traceinv:
+            res, trs = (ld, g1, g2, g3), ()
+            self._der_cache = (self._band_rhs, b, etas.copy(), res, trs, 0)
+        if not want:
             return res
-        if tr1 is None:
+        if len(trs) < want:
             lam = self._eig
-            tr1 = numpy.array([float(numpy.sum(1.0 / (lam + e))) for e in etas])
-        return res + (tr1,)
+            trs = tuple(numpy.array([float(numpy.sum((lam + e) ** -float(p))) for e in etas])
+                        for p in range(1, want + 1))
+        return res + tuple(trs[:want])
 
-    # traceinv(eta) calls on the 'eigenvalue' operator answered by selected inversion
-    # (one cyclic-reduction factorization + the tree per call, ~ms) before the
-    # eigenvalues (one-time chase, ~0.15 s at n = 16384, then O(n) per eta) pay off
-    SINV_CALLS = 32
-
-    def _eig_traceinv1(self, eta):
-        if self._eig is None and getattr(self, '_sinv_calls', 0) < self.SINV_CALLS:
-            self._sinv_calls = getattr(self, '_sinv_calls', 0) + 1
-            tr, info = self.band().traceinv([eta])
-            self._check_info([eta], info)
-            return float(tr[0])
-        return float(numpy.sum(1.0 / (self.eigenvalues() + eta)))
+    def _eig_traceinv(self, eta, exponent):
+        """traceinv(eta, 1 or 2) on the 'eigenvalue' operator: the sums over the
+        eigenvalues when they are already computed (imate 'eigenvalue',
+        :172-181), else selected inversion of the cyclic-reduction factor of
+        B + eta I (exponent 2: its eta-tangent) on the device, without the one-time
+        eigenvalue chase. The choice depends only on whether eigenvalues() has run.
+        A shift that leaves K + eta I indefinite takes the eigenvalue sums, as the
+        reference's eigenvalue traceinv does (it never raises)."""
+        if self._eig is None:
+            tr, info = self.band().traceinv([eta], exponent)
+            if not numpy.any(info):
+                return float(tr[0])
+        return float(numpy.sum((self.eigenvalues() + eta) ** (-float(exponent))))
 
     # ---- sparse K (tapered Matérn, CSR on the device) -------------------------
 
@@ -421,7 +429,7 @@ class MixedCorrelation(object):
             _slq.check_shifts(_slq.min_ritz(g), e)
             node, rigorous = _slq.radau_node(lo, g, e)
             r = _slq.radau_nodes(a, b, node)
-            gap = max(float(_slq.bracket(g, r, e, f)[0]) for f in fns)
+            gap = float(numpy.max([_slq.bracket(g, r, e, f)[0] for f in fns]))
             ok = gap <= self.lanczos_tol
             if ok or deg >= self.max_lanczos_degree:
                 break
@@ -595,10 +603,10 @@ class MixedCorrelation(object):
         if exponent == 0:
             return float(self.n)
         if self.imate_method == 'eigenvalue':
-            # sum over the eigenvalues (imate 'eigenvalue', :172-181); exponent 1 by
-            # selected inversion until the eigenvalues pay off (_eig_traceinv1)
-            if exponent == 1:
-                return self._eig_traceinv1(eta)
+            # sum over the eigenvalues (imate 'eigenvalue', :172-181); exponents 1
+            # and 2 by selected inversion unless the eigenvalues exist (_eig_traceinv)
+            if exponent in (1, 2):
+                return self._eig_traceinv(eta, exponent)
             return float(numpy.sum((self.eigenvalues() + eta) ** (-float(exponent))))
         if exponent in (1, 2):
             # exact, from the device triangular inverse of the cached factor

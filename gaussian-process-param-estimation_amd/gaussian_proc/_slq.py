@@ -49,13 +49,16 @@ def nodes(alpha, beta):
     a sweep, as a rule) are solved together by one batched dense symmetric
     eigensolver call (numpy.linalg.eigh on the [nprobe, k, k] stack: one call
     instead of one scipy call per probe, half the host time of a cfg 4 / cfg 5 step's
-    20 probes); the others one by one (_rule)."""
+    20 probes); the others one by one (_rule). The solver of a probe depends only
+    on its own tridiagonal, never on how many probes share the call (a rank's
+    shard of one probe, or the adaptive extra batches, get the nodes the whole set
+    gives it at N = 1)."""
     alpha = numpy.asarray(alpha, dtype=float)
     beta = numpy.asarray(beta, dtype=float)
     lens = [_length(b) for b in beta]
     out = [None] * len(lens)
     full = [p for p, k in enumerate(lens) if k == alpha.shape[1] and k > 1]
-    if len(full) > 1:
+    if full:
         k = alpha.shape[1]
         T = numpy.zeros((len(full), k, k))
         i = numpy.arange(k)
@@ -93,8 +96,12 @@ def radau_nodes(alpha, beta, lower):
     pivot d_m <= 0 from rounding alone (T_m - lower I is then numerically
     singular): that probe's node moves down to its own smallest Ritz value minus
     1e-8 max|T_m| (and 1e-6 max|T_m| if that still fails), a node still below its
-    rule's nodes. Nothing here raises, so a rank of a sharded sweep never leaves
-    the collectives alone (sweep.slq_sweep)."""
+    rule's nodes. If no node works the probe gets a NaN rule (one node, NaN): its
+    Radau quadrature, the probe mean and the bracket are then NaN, which the
+    degree searches read as "not converged" (a Gauss rule in its place would give
+    the probe a zero gap and could close the bracket falsely). Nothing here
+    raises, so a rank of a sharded sweep never leaves the collectives alone
+    (sweep.slq_sweep)."""
     out = []
     for a, b in zip(alpha, beta):
         a = numpy.asarray(a, dtype=float)
@@ -115,7 +122,7 @@ def radau_nodes(alpha, beta, lower):
                 if d > 0.0:
                     break
         if not d > 0.0:
-            out.append(_rule(a[:k], b[:k - 1]))
+            out.append((numpy.array([numpy.nan]), numpy.ones(1)))
             continue
         dd = numpy.append(a[:k], node + b[k - 1] ** 2 / d)
         out.append(_rule(dd, b[:k]))
@@ -147,14 +154,26 @@ def radau_node(lower, node_list, etas):
     return node, False
 
 
+def gap(g, r):
+    """Relative gap |g - r| / |g| of a Gauss / Gauss-Radau pair (|g - r| for g = 0);
+    inf when either is not finite (a probe without a valid Radau node, or f
+    undefined at a node): never read as converged."""
+    g = numpy.asarray(g, dtype=float)
+    r = numpy.asarray(r, dtype=float)
+    with numpy.errstate(divide='ignore', invalid='ignore'):
+        out = numpy.where(g != 0.0, numpy.abs(g - r) / numpy.abs(g), numpy.abs(g - r))
+    return numpy.where(numpy.isfinite(g) & numpy.isfinite(r), out, numpy.inf)
+
+
 def bracket(gauss, radau, etas, fn):
     """Relative gap |mean_p G_p - mean_p R_p| / |mean_p G_p| of the probe-mean
     Gauss and Gauss-Radau quadratures at each eta: a bound on the Lanczos
-    (quadrature) part of the SLQ error, as opposed to its Monte-Carlo part."""
-    g = quadrature(gauss, etas, fn, check=False).mean(axis=0)
-    r = quadrature(radau, etas, fn, check=False).mean(axis=0)
+    (quadrature) part of the SLQ error, as opposed to its Monte-Carlo part (inf
+    when a probe has no valid Radau rule, see radau_nodes)."""
     with numpy.errstate(divide='ignore', invalid='ignore'):
-        return numpy.where(g != 0.0, numpy.abs(g - r) / numpy.abs(g), numpy.abs(g - r))
+        g = quadrature(gauss, etas, fn, check=False).mean(axis=0)
+        r = quadrature(radau, etas, fn, check=False).mean(axis=0)
+    return gap(g, r)
 
 
 def min_ritz(node_list):

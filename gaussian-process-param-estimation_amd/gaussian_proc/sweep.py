@@ -198,15 +198,18 @@ def slq_sweep(K_mixed, etas, group=None, converge=('logdet',)):
         for i in range(len(conv)):
             g = allv[:, nq + 1 + 2 * i].mean()
             r = allv[:, nq + 2 + 2 * i].mean()
-            gap = max(gap, abs(g - r) / abs(g) if g != 0.0 else abs(g - r))
+            gap = max(gap, float(_slq.gap(g, r)))   # inf for a NaN rule: not converged
         if gap <= tol or deg >= K_mixed.max_lanczos_degree:
             break
         seen.append((deg, gap))
         deg = min(K_mixed.max_lanczos_degree, _next_degree(seen, tol))
     if conv:
         K_mixed.lanczos_degree_used = deg
+        # rigorous: the Radau node is the proven lower bound (_slq.radau_node's flag:
+        # lower + min(etas) > 0, the same on every rank), not a Ritz-value heuristic
+        rigorous = bool(lower + float(etas.min()) > 0.0)
         K_mixed.last_slq_convergence = {'degree': deg, 'bracket': gap, 'converged': gap <= tol,
-                                        'eta': float(etas.min())}
+                                        'eta': float(etas.min()), 'rigorous_bound': rigorous}
     allq = allv[:, :nq].reshape(s, len(names), etas.size)
     n = K_mixed.n
     return {name: n * allq[:, f].mean(axis=0) for f, name in enumerate(names)}

@@ -316,8 +316,33 @@ int gpmi_band_der_terms_ex(gpmi_band* b, const double* etas, int neta, double* l
  * gpmi_band_loglik. Replaces MixedCorrelation.traceinv(eta) on the 'eigenvalue'
  * operator (mixed_correlation.py:172-181) without the eigenvalues. */
 int gpmi_band_traceinv(gpmi_band* b, const double* etas, int neta, double* tr, int* info);
+/* Most etas per device chunk of the exponent-2 trace below (its eta-tangent store
+ * is 10 n_pad * 128 doubles per eta: 168 MB at n = 16384); larger calls run in
+ * chunks of this size. */
+#define GPMI_BAND_TAN_MAX 64
+
+/* gpmi_band_der_terms_ex plus, when tr2 != NULL, tr2[e] = trace((K + eta_e I)^-2)
+ * = -d/deta trace((B + eta_e I)^-1): the cyclic-reduction factor and the selected
+ * inversion above differentiated in eta in forward mode (every block carries its
+ * eta-tangent; about three times the selected inversion's products). tr2 needs tr1
+ * (the tangent rides on the primal recurrences); tr1 != NULL is then implied.
+ * With it the direct Hessian (_direct_likelihood.py:224) and the profiled der2
+ * (_profile_likelihood.py:168) need no eigenvalues: it replaces the eigenvalue
+ * sums of MixedCorrelation.traceinv(eta, exponent=2) on the 'eigenvalue' operator
+ * (mixed_correlation.py:172-181) and the eigh they come from (:76-79). */
+int gpmi_band_der_terms_ex2(gpmi_band* b, const double* etas, int neta, double* logdet,
+                            double* g1, double* g2, double* g3, double* tr1, double* tr2,
+                            int* info);
+/* tr1[e] = trace((K + eta_e I)^-1) and, when tr2 != NULL, tr2[e] =
+ * trace((K + eta_e I)^-2) for neta <= GPMI_BAND_DER_MAX etas (selected inversion
+ * and its eta-tangent, as gpmi_band_der_terms_ex2); info as gpmi_band_loglik.
+ * Replaces MixedCorrelation.traceinv(eta, exponent in {1, 2}) on the 'eigenvalue'
+ * operator (mixed_correlation.py:172-181). */
+int gpmi_band_traceinv2(gpmi_band* b, const double* etas, int neta, double* tr1, double* tr2,
+                        int* info);
 /* Device ms of the selected-inversion part of the last gpmi_band_traceinv /
- * gpmi_band_der_terms_ex(tr1 != NULL) call. Diagnostic. */
+ * gpmi_band_traceinv2 / gpmi_band_der_terms_ex(2) call (tr1 or tr2 requested).
+ * Diagnostic. */
 int gpmi_band_sinv_ms(gpmi_band* b, double* ms);
 
 /* Reduction diagnostics: how many reductions of this band fell back to the

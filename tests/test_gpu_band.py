@@ -266,6 +266,8 @@ def test_eigenvalue_operator_cfg2_golden(gp):
     g = cfg['operator']['eigenvalue']
     assert rel([op.traceinv(e) for e in cfg['etas']], g['traceinv']) < 1e-9
     assert rel([op.traceinv(e, 2) for e in cfg['etas']], g['traceinv_exp2']) < 1e-9
+    # exponents 1 and 2 by selected inversion and its eta-tangent: no eigenvalues
+    assert op._eig is None
     assert rel([op.logdet(e) for e in cfg['etas']], g['logdet']) < 1e-9
 
 
@@ -639,15 +641,50 @@ def test_band_selected_inversion_traceinv(gp, n):
 
 
 def test_band_selected_inversion_not_spd_and_many_etas(gp):
-    """A non-SPD shift reports its pivot (LinAlgError through traceinv); 150 etas
-    in one call (three cyclic-reduction chunks of <= 64) equal the per-eta values."""
+    """A non-SPD shift reports its pivot through the band's selected inversion;
+    MixedCorrelation.traceinv then answers from the eigenvalue sums, as the
+    reference's eigenvalue traceinv (which never raises) does, for exponents 1 and
+    2 alike. 150 etas in one call (three cyclic-reduction chunks of <= 64) equal
+    the per-eta values, for both exponents."""
     K, X, z = _inputs(600, 77)
     lam = numpy.linalg.eigvalsh(K)
     op = _mc(K)
-    with pytest.raises(numpy.linalg.LinAlgError):
-        op.traceinv(-lam[0] - 1.0)
+    bad = -lam[0] - 1.0
+    for p in (1, 2):
+        tr, info = op.band().traceinv([bad], p)
+        assert info[0] > 0
+    assert op._eig is None
+    for p in (1, 2):
+        assert rel(op.traceinv(bad, p), numpy.sum((lam + bad) ** -float(p))) < 1e-9
     etas = numpy.logspace(-2, 2, 150)
-    tr, info = op.band().traceinv(etas)
+    for p in (1, 2):
+        tr, info = op.band().traceinv(etas, p)
+        assert not numpy.any(info)
+        exact = numpy.array([numpy.sum((lam + e) ** -float(p)) for e in etas])
+        assert rel(tr, exact) < 1e-10, p
+
+
+@pytest.mark.parametrize('n', [1, 5, 128, 129, 300, 1000, 2177])
+def test_band_selected_inversion_traceinv_exponent_2(gp, n):
+    """trace((K + eta I)^-2) as -d/deta trace((K + eta I)^-1): the cyclic-reduction
+    factor and its selected inversion differentiated in eta in forward mode
+    (gpmi_band_traceinv2, no eigenvalues) vs numpy's eigenvalue sums at ragged n,
+    rel <= 1e-10; the same numbers from der_terms(traceinv=2) (one factorization
+    for the Gram blocks and both traces) and MixedCorrelation.traceinv(eta, 2)
+    without the eigenvalue chase."""
+    K, X, z = _inputs(n, n + 17, nu=2.5, scale=0.15)
+    lam = numpy.linalg.eigvalsh(K)
+    etas = numpy.array([1e-3, 0.05, 1.0, 30.0])
+    ex1 = numpy.array([numpy.sum(1.0 / (lam + e)) for e in etas])
+    ex2 = numpy.array([numpy.sum((lam + e) ** -2.0) for e in etas])
+    op = _mc(K)
+    tr2, info = op.band().traceinv(etas, 2)
     assert not numpy.any(info)
-    exact = numpy.array([numpy.sum(1.0 / (lam + e)) for e in etas])
-    assert rel(tr, exact) < 1e-10
+    assert rel(tr2, ex2) < 1e-10, (tr2, ex2)
+    ld, G1, G2, G3, tr1d, tr2d = op.der_terms(etas, X, z, traceinv=2)
+    assert rel(tr1d, ex1) < 1e-10 and rel(tr2d, tr2) < 1e-12
+    # the Gram blocks of the tangent-carrying call equal the plain call's
+    ld0, G10, G20, G30, info0 = op.band().der_terms(etas)
+    assert rel(ld, ld0) < 1e-13 and rel(G2, G20) < 1e-12 and rel(G3, G30) < 1e-12
+    assert rel(op.traceinv(0.05, 2), ex2[1]) < 1e-10
+    assert op._eig is None

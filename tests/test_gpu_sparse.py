@@ -686,6 +686,45 @@ def test_cg_unconverged_warns(gp):
         sop.msgram([3.0, 5.0], B, rtol=1e-14, maxiter=2)
 
 
+def test_msgram_at_maxiter_applies_the_last_step(gp):
+    """the multi-shift CG applies shift step k - 1 during iteration k,
+    so a loop ending at maxiter with active columns must still apply its last step
+    (ms_cg2_close_kernel). After k iterations each shifted solution equals plain CG
+    on K + eta_j I after k steps (same Krylov space, x0 = 0): G_j = B^T x_j^(k)
+    against a host CG truncated at k, for k = 1, 3, 7."""
+    from gaussian_proc import _hip
+    _, K = _small_sparse()
+    Kd = K.toarray()
+    n = Kd.shape[0]
+    B = numpy.random.RandomState(11).randn(n, 3)
+    etas = numpy.array([3.0, 4.5, 9.0])
+    sop = _hip.SparseOperator.from_csr(K)
+
+    def cg_steps(A, b, k):
+        x = numpy.zeros_like(b)
+        r = b.copy()
+        p = r.copy()
+        rr = r @ r
+        for _ in range(k):
+            Ap = A @ p
+            a = rr / (p @ Ap)
+            x += a * p
+            r -= a * Ap
+            rn = r @ r
+            p = r + (rn / rr) * p
+            rr = rn
+        return x
+
+    for k in (1, 3, 7):
+        with pytest.warns(RuntimeWarning):
+            G = sop.msgram(etas, B, rtol=1e-15, maxiter=k)
+        for j, eta in enumerate(etas):
+            A = Kd + eta * numpy.eye(n)
+            X = numpy.column_stack([cg_steps(A, B[:, c], k) for c in range(3)])
+            ref = B.T @ X
+            assert numpy.max(numpy.abs(G[j] - ref)) <= 1e-10 * numpy.abs(ref).max(), (k, j)
+
+
 def test_config5_full_size_vs_reference(gp):
     """BASELINE cfg5 at full size (N=262144, 3D 64^3 grid, rho=0.02, density
     6e-4) against tests/golden/sparse_cfg5.json (reference generator + the 2

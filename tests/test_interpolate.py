@@ -38,3 +38,23 @@ def test_interpolant_between_points():
     it2 = InterpolateTraceInv(tr, K.shape[0], numpy.trace(K), numpy.logspace(-3, 2, 41))
     err2 = max(abs(it2.interpolate(t) - tr(t)) / tr(t) for t in grid)
     assert err2 < err / 4, (err2, err)
+
+
+def test_interpolant_uses_the_callers_points():
+    """The chosen semantics ("Interpolation"): the interpolant's
+    nodes are the caller's interpolant_points (the reference requires them but
+    never forwards them to imate, which then uses its own defaults): its nodes are
+    exactly those points, it is exact at each, and a different point set gives a
+    different interpolant between them."""
+    K, lam, tr = _exact()
+    pts_a = [1e-2, 1.0, 100.0]
+    pts_b = [1e-3, 1e-1, 10.0]
+    ia = InterpolateTraceInv(tr, K.shape[0], numpy.trace(K), pts_a)
+    ib = InterpolateTraceInv(tr, K.shape[0], numpy.trace(K), pts_b)
+    numpy.testing.assert_array_equal(ia.points, pts_a)
+    numpy.testing.assert_array_equal(ib.points, pts_b)
+    for t in pts_a:
+        assert abs(ia.interpolate(t) - tr(t)) <= 1e-12 * tr(t)
+    for t in pts_b:
+        assert abs(ib.interpolate(t) - tr(t)) <= 1e-12 * tr(t)
+    assert abs(ia.interpolate(0.1) - ib.interpolate(0.1)) > 1e-9 * tr(0.1)

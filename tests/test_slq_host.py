@@ -78,6 +78,44 @@ def test_radau_node_above_the_ritz_values_moves_below_them():
         assert numpy.all(numpy.isfinite(r[0][1]))
 
 
+def test_radau_without_a_valid_node_never_reads_converged(monkeypatch):
+    """when no Radau node gives a positive last pivot, the probe gets a
+    NaN rule (not its Gauss rule, whose zero gap could close the bracket falsely):
+    the bracket is inf, so the lanczos_tol searches keep going or report
+    unconverged."""
+    rng = numpy.random.RandomState(3)
+    lam = numpy.sort(rng.gamma(0.3, 2.0, 200)) + 1e-3
+    K = numpy.diag(lam)
+    P = _slq.rademacher(lam.size, 3, 5)
+    ab = [_lanczos_with_last_beta(K, P[:, p], 10) for p in range(3)]
+    A = numpy.array([a for a, _ in ab])
+    B = numpy.array([b for _, b in ab])
+    g = _slq.nodes(A, B)
+    monkeypatch.setattr(_slq, '_last_pivot', lambda a, b, lower: -1.0)
+    r = _slq.radau_nodes(A, B, 0.0)
+    assert all(numpy.isnan(t).all() for t, _ in r)
+    gap = _slq.bracket(g, r, [0.1], numpy.log)[0]
+    assert gap == numpy.inf and not gap <= 1e-3
+    assert _slq.gap(1.0, numpy.nan) == numpy.inf and _slq.gap(2.0, 1.0) == 0.5
+
+
+def test_nodes_do_not_depend_on_the_probe_grouping():
+    """a probe's Ritz nodes are the same whether it is solved alone (a
+    rank's shard of one probe) or with others (the whole set at N = 1)."""
+    rng = numpy.random.RandomState(7)
+    lam = numpy.sort(rng.gamma(0.3, 2.0, 300)) + 1e-3
+    K = numpy.diag(lam)
+    P = _slq.rademacher(lam.size, 4, 1)
+    ab = [_lanczos_with_last_beta(K, P[:, p], 16) for p in range(4)]
+    A = numpy.array([a for a, _ in ab])
+    B = numpy.array([b for _, b in ab])
+    together = _slq.nodes(A, B)
+    for p in range(4):
+        alone = _slq.nodes(A[p:p + 1], B[p:p + 1])[0]
+        numpy.testing.assert_array_equal(alone[0], together[p][0])
+        numpy.testing.assert_array_equal(alone[1], together[p][1])
+
+
 def test_stemr_failure_falls_back_to_dense_eigh():
     """The tridiagonal on which LAPACK stemr stops with info = 22 (a plain Lanczos
     at 130 steps: duplicated Ritz values; tests/golden/make_stemr_fixture.py):

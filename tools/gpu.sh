@@ -24,6 +24,7 @@
 #                (tools/band_timeline.py)
 #   host         the box's CPU / cgroup facts (host.txt)
 #   py:<file>[:<arg>]   python -u <file> [<arg>] (a probe under tools/)
+#   trace-py:<file>[:<arg>]   the same under rocprofv3 --kernel-trace --stats
 set -o pipefail
 export TMPDIR=/tmp
 NAME=${1:?name}
@@ -111,6 +112,15 @@ for task in "$@"; do
       cat $D/spmm_timed_launches_$cfg.json ;;
     host)
       (nproc; cat /sys/fs/cgroup/cpu.max 2>/dev/null; python -c "import os; print('aff', len(os.sched_getaffinity(0)), 'omp', os.environ.get('OMP_NUM_THREADS'))"; lscpu | head -20) > $D/host.txt 2>&1 ;;
+    trace-py:*)
+      # trace-py:<file>[:<arg>]: kernel-trace stats of a probe under tools/
+      spec=${task#trace-py:}
+      f=${spec%%:*}
+      arg=""
+      [ "$spec" != "$f" ] && arg=${spec#*:}
+      b=$(basename $f .py)
+      run 600 $D/trace_$b.log rocprofv3 --kernel-trace --stats -d $D/prof_$b -o run --output-format csv -- python3 -u $f $arg
+      tail -12 $D/trace_$b.log ;;
     py:*)
       # py:<file>[:<arg>]
       spec=${task#py:}
