@@ -72,7 +72,7 @@ struct gpmi_band {
   int64_t n = 0, n_pad = 0;
   int nt = 0;
   hipStream_t stream = nullptr;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr;
   double* Ab = nullptr;      // [n_pad][n_pad]: band (diagonal tiles, triu of subdiagonal
                              // tiles) + Householder vectors below the band
   double* U = nullptr;       // [n_pad][384] = [W | V | W] of the current panel
@@ -236,6 +236,7 @@ int band_free(gpmi_band* b) {
   if (b->ev0) (void)hipEventDestroy(b->ev0);
   if (b->ev1) (void)hipEventDestroy(b->ev1);
   if (b->ev2) (void)hipEventDestroy(b->ev2);
+  if (b->ev3) (void)hipEventDestroy(b->ev3);
   if (b->stream) (void)hipStreamDestroy(b->stream);
   if (b->side) (void)hipStreamDestroy(b->side);
   if (b->s_pan) (void)hipStreamDestroy(b->s_pan);
@@ -740,6 +741,7 @@ int gpmi_band_create(gpmi_op* op, gpmi_band** out) {
   if ((e = hipEventCreate(&b->ev0)) != hipSuccess) return fail(e, "event");
   if ((e = hipEventCreate(&b->ev1)) != hipSuccess) return fail(e, "event");
   if ((e = hipEventCreate(&b->ev2)) != hipSuccess) return fail(e, "event");
+  if ((e = hipEventCreate(&b->ev3)) != hipSuccess) return fail(e, "event");
   if ((e = hipStreamCreateWithFlags(&b->side, hipStreamNonBlocking)) != hipSuccess)
     return fail(e, "side stream");
   if (const char* la = std::getenv("GPMI_BAND_LA")) b->lookahead = std::atoi(la);
@@ -1026,6 +1028,7 @@ int band_loglik_bcr(gpmi_band* b, int neta, hipStream_t s, bool tan = false) {
   const double* dFin = nullptr;
   int64_t sD = 0, sY = 0, sF = 0;
   int m = nt, lvl = 0, cur = 0;
+  bool dupd_pending = false;   // the last bcr_dupd_kernel (side stream) not yet waited for
   while (m > 1) {
     const int nodd = m / 2, neven = (m + 1) / 2;
     hipLaunchKernelGGL(bcr_chol_kernel, dim3(nodd, neta), dim3(256), 0, s, b->Ab, np, b->etas,
@@ -1033,7 +1036,10 @@ int band_loglik_bcr(gpmi_band* b, int neta, hipStream_t s, bool tan = false) {
                        b->bcrFail, nt, b->n);
     BD_LAUNCH("bcr_chol_kernel");
     // W (and with tangents the level's dLinv beside it), then D', F', Y' (and dW),
-    // then dD', dF'
+    // then dD', dF' on the side stream beside the next level's Cholesky (the dLinv of
+    // the next bcr_w_kernel launch waits for them)
+    if (dupd_pending) BD_TRY(hipStreamWaitEvent(s, b->ev_t, 0));
+    dupd_pending = false;
     hipLaunchKernelGGL(bcr_w_kernel, dim3(2 * nodd + (tan ? nodd : 0), neta), dim3(256), 0, s,
                        b->bcrL, sL, Fin, sF, b->bcrW, sW, m, lvl, dDin, sH, b->tanX, b->tanL);
     BD_LAUNCH("bcr_w_kernel");
@@ -1043,9 +1049,13 @@ int band_loglik_bcr(gpmi_band* b, int neta, hipStream_t s, bool tan = false) {
                        Fin, sF, dFin, sH, b->tanW);
     BD_LAUNCH("bcr_upd_kernel");
     if (tan) {
-      hipLaunchKernelGGL(bcr_dupd_kernel, dim3(2 * neven, neta), dim3(256), 0, s, b->bcrW,
+      BD_TRY(hipEventRecord(b->ev_v, s));
+      BD_TRY(hipStreamWaitEvent(b->side, b->ev_v, 0));
+      hipLaunchKernelGGL(bcr_dupd_kernel, dim3(2 * neven, neta), dim3(256), 0, b->side, b->bcrW,
                          b->tanW, sW, dDin, sH, b->tanD[cur], b->tanF[cur], sH, m, lvl);
       BD_LAUNCH("bcr_dupd_kernel");
+      BD_TRY(hipEventRecord(b->ev_t, b->side));
+      dupd_pending = true;
       dDin = b->tanD[cur];
       dFin = b->tanF[cur];
     }
@@ -1064,6 +1074,7 @@ int band_loglik_bcr(gpmi_band* b, int neta, hipStream_t s, bool tan = false) {
                      nt, b->n);
   BD_LAUNCH("bcr_chol_kernel");
   if (tan) {   // the last level's dLinv (bcr_w_kernel with m = 1: its dfac role only)
+    if (dupd_pending) BD_TRY(hipStreamWaitEvent(s, b->ev_t, 0));
     hipLaunchKernelGGL(bcr_w_kernel, dim3(1, neta), dim3(256), 0, s, b->bcrL, sL, nullptr, 0,
                        nullptr, sW, 1, lvl, dDin, sH, b->tanX, b->tanL);
     BD_LAUNCH("bcr_w_kernel");
@@ -1077,9 +1088,7 @@ int band_loglik_bcr(gpmi_band* b, int neta, hipStream_t s, bool tan = false) {
 // Derivative terms by cyclic reduction (after band_loglik_bcr, whose levels stay
 // stored): X = (B + eta I)^-1 Y by back substitution from the last level down, then
 // the forward elimination of X; G2, G3 into b->der (gpmi_bcr.hip).
-int band_der_bcr(gpmi_band* b, int neta, hipStream_t s, bool tan = false) {
-  int rc = band_loglik_bcr(b, neta, s, tan);
-  if (rc) return rc;
+int band_der_solves(gpmi_band* b, int neta, hipStream_t s) {
   const int nt = b->nt;
   const int half = (nt + 1) / 2;
   const int64_t sHY = (int64_t)half * TS * RLD;
@@ -1116,6 +1125,12 @@ int band_der_bcr(gpmi_band* b, int neta, hipStream_t s, bool tan = false) {
                      b->der);
   BD_LAUNCH("bcr_der_final_kernel");
   return 0;
+}
+
+int band_der_bcr(gpmi_band* b, int neta, hipStream_t s) {
+  int rc = band_loglik_bcr(b, neta, s);
+  if (rc) return rc;
+  return band_der_solves(b, neta, s);
 }
 
 // tr((B + eta_e I)^-1) for the neta etas whose cyclic-reduction factor band_loglik_bcr
@@ -1266,9 +1281,20 @@ int gpmi_band_der_terms_ex2(gpmi_band* b, const double* etas, int neta, double* 
   hipStream_t s = b->stream;
   BD_TRY(hipMemcpyAsync(b->etas, etas, sizeof(double) * neta, hipMemcpyHostToDevice, s));
   BD_TRY(hipEventRecord(b->ev0, s));
-  // tr1 needs the cyclic-reduction factor (the tree it inverts along)
-  if (tr1 || b->bcr_mode == 1 || (b->bcr_mode == 2 && neta <= 64)) {
-    rc = band_der_bcr(b, neta, s, tr2 != nullptr);
+  // tr1 needs the cyclic-reduction factor (the tree it inverts along); the selected
+  // inversion (side stream) and the G2 / G3 solves (s) both read only the factor, so
+  // they run side by side
+  if (tr1) {
+    if ((rc = band_loglik_bcr(b, neta, s, tr2 != nullptr))) return rc;
+    BD_TRY(hipEventRecord(b->ev_q, s));
+    BD_TRY(hipStreamWaitEvent(b->side, b->ev_q, 0));
+    BD_TRY(hipEventRecord(b->ev2, b->side));
+    if ((rc = band_sinv_bcr(b, neta, b->side, tr2 != nullptr))) return rc;
+    BD_TRY(hipEventRecord(b->ev3, b->side));
+    if ((rc = band_der_solves(b, neta, s))) return rc;
+    BD_TRY(hipStreamWaitEvent(s, b->ev3, 0));
+  } else if (b->bcr_mode == 1 || (b->bcr_mode == 2 && neta <= 64)) {
+    rc = band_der_bcr(b, neta, s);
     if (rc) return rc;
   } else {
     hipLaunchKernelGGL(band_chol_kernel, dim3(neta), dim3(256), 0, s, b->Ab, np, nt, b->n, b->Y,
@@ -1280,9 +1306,6 @@ int gpmi_band_der_terms_ex2(gpmi_band* b, const double* etas, int neta, double* 
   }
   std::vector<double> htr, htr2;
   if (tr1) {
-    BD_TRY(hipEventRecord(b->ev2, s));
-    rc = band_sinv_bcr(b, neta, s, tr2 != nullptr);
-    if (rc) return rc;
     htr.resize(neta);
     BD_TRY(hipMemcpyAsync(htr.data(), b->sinvTr + (size_t)nt * neta, sizeof(double) * neta,
                           hipMemcpyDeviceToHost, s));
@@ -1306,7 +1329,7 @@ int gpmi_band_der_terms_ex2(gpmi_band* b, const double* etas, int neta, double* 
   b->der_ms = ms;
   if (tr1) {
     float ms2 = 0.f;
-    BD_TRY(hipEventElapsedTime(&ms2, b->ev2, b->ev1));
+    BD_TRY(hipEventElapsedTime(&ms2, b->ev2, b->ev3));
     b->sinv_ms = ms2;
     for (int e = 0; e < neta; ++e) tr1[e] = htr[e];
     if (tr2)
