@@ -475,21 +475,19 @@ __global__ __launch_bounds__(64 * TPR) void csr_spmm_wing_kernel(
   }
 }
 
-template __global__ void csr_spmm_wing_kernel<20, 8, 4>(const int64_t*, const int*,
-    const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
-    double*, double, double*, int, unsigned long long*);
-template __global__ void csr_spmm_wing_kernel<11, 8, 4>(const int64_t*, const int*,
-    const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
-    double*, double, double*, int, unsigned long long*);
-template __global__ void csr_spmm_wing_kernel<12, 8, 4>(const int64_t*, const int*,
-    const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
-    double*, double, double*, int, unsigned long long*);
-template __global__ void csr_spmm_wing_kernel<8, 8, 4>(const int64_t*, const int*,
-    const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
-    double*, double, double*, int, unsigned long long*);
-template __global__ void csr_spmm_wing_kernel<7, 8, 4>(const int64_t*, const int*,
-    const unsigned short*, const double*, int64_t, const int*, const int*, const double*,
-    double*, double, double*, int, unsigned long long*);
+// every width 1 .. 20: the probe and column shards of an N-rank sweep run narrower
+// blocks than the single-GPU 20 (Lanczos) / 12 (multi-shift CG): at N = 8 a cfg 5
+// rank's 3 probes and 2 columns (round 6; the gather kernels they fell back to
+// made cfg 5's rank step 3x slower than the whole single-GPU step)
+#define GPMI_WING_INST(S)                                                                \
+  template __global__ void csr_spmm_wing_kernel<S, 8, 4>(                                 \
+      const int64_t*, const int*, const unsigned short*, const double*, int64_t, const int*, \
+      const int*, const double*, double*, double, double*, int, unsigned long long*);
+GPMI_WING_INST(1) GPMI_WING_INST(2) GPMI_WING_INST(3) GPMI_WING_INST(4) GPMI_WING_INST(5)
+GPMI_WING_INST(6) GPMI_WING_INST(7) GPMI_WING_INST(8) GPMI_WING_INST(9) GPMI_WING_INST(10)
+GPMI_WING_INST(11) GPMI_WING_INST(12) GPMI_WING_INST(13) GPMI_WING_INST(14) GPMI_WING_INST(15)
+GPMI_WING_INST(16) GPMI_WING_INST(17) GPMI_WING_INST(18) GPMI_WING_INST(19) GPMI_WING_INST(20)
+#undef GPMI_WING_INST
 
 // partial[b][j][c] = sum over this block's rows of A_j[i][c] * B[i][c],
 // A_j = A + j * strideA, j = blockIdx.y; grid-stride over rows.

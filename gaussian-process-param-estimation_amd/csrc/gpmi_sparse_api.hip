@@ -6,6 +6,8 @@
 #include <hip/hip_ext.h>
 
 #include <algorithm>
+#include <array>
+#include <utility>
 #include <atomic>
 #include <cmath>
 #include <cstdarg>
@@ -58,6 +60,15 @@ constexpr int WING_U = 8, WING_TPR = 4;
 constexpr int WIN_ROWS_HOST = 64;    // = WIN_ROWS (gpmi_sparse.hip)
 constexpr int WIN_MAXU_HOST = 1024;  // = WIN_MAXU
 constexpr int WIN_CS_HOST = 8;       // = WIN_CS
+constexpr int WING_MAXS = 20;        // widths 1 .. WING_MAXS have a window kernel
+
+// csr_spmm_wing_kernel<s> for s in [1, WING_MAXS] (index s - 1)
+template <int... I>
+constexpr std::array<decltype(&csr_spmm_wing_kernel<1, WING_U, WING_TPR>), sizeof...(I)>
+wing_table(std::integer_sequence<int, I...>) {
+  return {{&csr_spmm_wing_kernel<I + 1, WING_U, WING_TPR>...}};
+}
+const auto kWing = wing_table(std::make_integer_sequence<int, WING_MAXS>{});
 __global__ void col_dot_partial_kernel(const double*, int64_t, const double*, int64_t, int,
                                        double*);
 __global__ void col_dot_reduce_kernel(const double*, int, int, int, double*);
@@ -324,12 +335,9 @@ int build_window(gpmi_sp* sp) {
   if (lds > 64 * 1024)
     SP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&csr_spmm_win_kernel),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  for (const void* f : {reinterpret_cast<const void*>(&csr_spmm_wing_kernel<20, WING_U, WING_TPR>),
-                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<12, WING_U, WING_TPR>),
-                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<11, WING_U, WING_TPR>),
-                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<8, WING_U, WING_TPR>),
-                        reinterpret_cast<const void*>(&csr_spmm_wing_kernel<7, WING_U, WING_TPR>)})
-    SP_TRY(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, WING_MAX_LDS));
+  for (auto f : kWing)
+    SP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(f),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, WING_MAX_LDS));
   sp->win_nblk = nblk;
   sp->win_maxu.store(mu, std::memory_order_release);
   return 0;
@@ -352,11 +360,11 @@ int spmm_kind(gpmi_sp* sp, int s, int* kind) {
   if (wmode != 0)
     if (int rc = ensure_window(sp)) return rc;
   *kind = 0;
-  // the window with latency-hidden staging (csr_spmm_wing_kernel) at the Lanczos
-  // and multi-shift CG widths while the widest window fits two workgroups per CU
-  // (GPMI_SPMM_WING=0: off)
+  // the window with latency-hidden staging (csr_spmm_wing_kernel) at every width up to
+  // 20 (the Lanczos and multi-shift CG blocks and their N-rank shards) while the widest
+  // window fits two workgroups per CU (GPMI_SPMM_WING=0: off)
   const char* genv = std::getenv("GPMI_SPMM_WING");
-  if (wmode != 0 && !(genv && std::atoi(genv) == 0) && (s == 20 || s == 12 || s == 11 || s == 8 || s == 7) &&
+  if (wmode != 0 && !(genv && std::atoi(genv) == 0) && s >= 1 && s <= WING_MAXS &&
       sp->win_maxu.load(std::memory_order_acquire) > 0 &&
       sizeof(double) * (size_t)std::max(sp->win_maxu.load(std::memory_order_acquire),
                                         WIN_ROWS_HOST) * s <= (size_t)WING_MAX_LDS) {
@@ -405,11 +413,7 @@ int spmm_launch(gpmi_sp* sp, const double* X, double* Y, int s, double eta, hipS
     const size_t lds = sizeof(double) * (size_t)s *
                        (size_t)std::max(sp->win_maxu.load(std::memory_order_acquire),
                                         (dots2 ? 2 : 1) * WIN_ROWS_HOST);
-    auto kfn = s == 20   ? csr_spmm_wing_kernel<20, WING_U, WING_TPR>
-               : s == 12 ? csr_spmm_wing_kernel<12, WING_U, WING_TPR>
-               : s == 11 ? csr_spmm_wing_kernel<11, WING_U, WING_TPR>
-               : s == 8  ? csr_spmm_wing_kernel<8, WING_U, WING_TPR>
-                         : csr_spmm_wing_kernel<7, WING_U, WING_TPR>;
+    auto kfn = kWing[s - 1];
     const int tpr = WING_TPR;
     hipLaunchKernelGGL(kfn, dim3((unsigned)sp->win_nblk), dim3(64 * tpr), lds, st, sp->indptr,
                        sp->indices, sp->win_lidx, sp->data, sp->n, sp->win_cols, sp->win_u, X, Y,
