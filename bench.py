@@ -618,6 +618,8 @@ def sparse_measure(args, config, world, rank, local, dist, torch, cpu, exact, de
                 'lanczos_orthogonalize': op.orthogonalize,
                 'model': 'bench.sparse_step_bytes (each vector block once per pass)'},
             'lp_sample': [float(v) for v in last[0].tolist()],
+            # every eta of the curve finite (round 6: a large shift's Gram was NaN)
+            'lp_all_finite': bool(numpy.all(numpy.isfinite(last[:, 1:]))),
             'curve_sha256': curve_sha(last),
             'cpu_baseline': None,
         }

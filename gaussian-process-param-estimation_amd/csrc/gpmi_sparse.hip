@@ -1330,6 +1330,13 @@ void launch_ms_dots(const double* B, const double* R, int64_t n, int s, double* 
 // the shift step k - 1 (the zeta / G / b . p recurrences of ms_tail_kernel, which need
 // beta_{k-1}, known only now, and B^T r_k), then writes the next scalar state (nxt),
 // the batch end state into pinned memory (pin) and the stopping iteration.
+// A shift whose zeta fell below this is converged far past any tolerance (its residual
+// is zeta times the seed system's): its G is final and its recurrences stop. Without
+// the stop, a large shift's zeta (~ (1 + d alpha)^-k) underflows to 0 within the seed's
+// iterations and alpha^s = alpha zeta_k / zeta_{k-1} becomes 0 / 0 (round 6: the
+// largest eta of cfg 4's curve had a NaN Gram column for the data vector z).
+constexpr double MS_ZETA_MIN = 1e-250;
+
 // zeta_k and alpha_{k-1} of shift j for column c (the shifted recurrence of step k - 1
 // from the unshifted alpha_{k-1}, alpha_{k-2}, beta_{k-1} in cur).
 __device__ __forceinline__ void ms_shift_step(const MsScal& cur, const MsShift& sh,
@@ -1353,6 +1360,7 @@ __global__ __launch_bounds__(256) void ms_cg2_close_kernel(MsScal cur, MsShift s
   for (int task = threadIdx.x; task < S * s; task += blockDim.x) {
     const int j = task / s, c = task % s;
     if (!cur.active[c]) continue;
+    if (!(fabs(sh.z[j * s + c]) >= MS_ZETA_MIN)) continue;   // converged shift
     double zn, as;
     ms_shift_step(cur, sh, dshift, s, j, c, zn, as);
     for (int cp = 0; cp < nb; ++cp) {
@@ -1442,6 +1450,7 @@ __global__ __launch_bounds__(256) void ms_cg2_update_kernel(
       const int j = task / s, c = task % s;
       if (!cur.active[c]) continue;   // step k - 1 not taken by this column
       const double z = sh.z[j * s + c];
+      if (!(fabs(z) >= MS_ZETA_MIN)) continue;   // converged shift: G final
       double zn, as;
       ms_shift_step(cur, sh, dshift, s, j, c, zn, as);
       const double bs = sbe[c] * (zn / z) * (zn / z);

@@ -725,6 +725,26 @@ def test_msgram_at_maxiter_applies_the_last_step(gp):
             assert numpy.max(numpy.abs(G[j] - ref)) <= 1e-10 * numpy.abs(ref).max(), (k, j)
 
 
+def test_msgram_large_shifts_stay_finite(gp):
+    """A large shift's zeta decays like (1 + d alpha)^-k and underflows to 0 within
+    the seed system's iterations; alpha^s = alpha zeta_k / zeta_{k-1} was then 0 / 0
+    (round 6: the largest eta of cfg 4's curve had a NaN Gram column). Converged
+    shifts now stop (their zeta below 1e-250): every G finite and equal to the
+    exact solve, while the small shifts keep their accuracy."""
+    from gaussian_proc import _hip
+    _, K = _small_sparse()
+    Kd = K.toarray()
+    n = Kd.shape[0]
+    B = numpy.random.RandomState(5).randn(n, 3)
+    etas = numpy.array([3.0, 30.0, 1e3, 1e6, 1e9])
+    sop = _hip.SparseOperator.from_csr(K)
+    G = sop.msgram(etas, B, rtol=1e-13)
+    assert numpy.all(numpy.isfinite(G))
+    for j, eta in enumerate(etas):
+        ref = B.T @ numpy.linalg.solve(Kd + eta * numpy.eye(n), B)
+        assert numpy.max(numpy.abs(G[j] - ref)) <= 1e-10 * numpy.abs(ref).max(), (eta,)
+
+
 def test_config5_full_size_vs_reference(gp):
     """BASELINE cfg5 at full size (N=262144, 3D 64^3 grid, rho=0.02, density
     6e-4) against tests/golden/sparse_cfg5.json (reference generator + the 2
