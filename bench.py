@@ -688,7 +688,8 @@ def sparse_modes(args, world, rank, local, dist, torch):
         out[cfg] = {k: r[k] for k in ('metric', 'value', 'unit', 'n_gpus', 'ms_per_step',
                                       'steps', 'warmup', 'scaling', 'roofline',
                                       'step_roofline', 'cpu_baseline', 'lp_sample',
-                                      'curve_sha256', 'lanczos_orthogonalize') if k in r}
+                                      'curve_sha256', 'lp_all_finite',
+                                      'lanczos_orthogonalize') if k in r}
         out[cfg]['parallelism'] = r['config']['parallelism']
         out[cfg]['workload'] = r['config']['workload']
         out[cfg]['assembly_s'] = r['config']['assembly_s']
@@ -876,6 +877,7 @@ def band_mode(args, D, X, z, world, rank, dist, torch, ld_ref=None):
         'panel': b.stats(),
         'lp_sample': [float(v) for v in last[0].tolist()],
         'curve_sha256': curve_sha(last),
+        'lp_all_finite': bool(numpy.all(numpy.isfinite(last[:, 1:]))),
     }
     ld_err, lp_err = golden_errors(lambda e: op.loglik_terms(e, X, z), args.nu, n, m)
     out['logdet_rel_err_vs_reference'] = ld_err
@@ -1381,6 +1383,8 @@ def main():
             'flops_per_eval': flops_eval,
             'lp_sample': [float(v) for v in last[0].tolist()] if last is not None else None,
             'curve_sha256': curve_sha(last) if last is not None else None,
+            'lp_all_finite': (bool(numpy.all(numpy.isfinite(last[:, 1:])))
+                              if last is not None else None),
             'cpu_baseline': None,
             'devices': devices,
         }
