@@ -1607,6 +1607,28 @@ __global__ void ms_init_kernel(MsScal st, MsShift sh, const double* __restrict__
   }
 }
 
+// Active-column compaction of the multi-shift CG (round 6): dst[(r a + c') L + v] =
+// src[(r s + map[c']) L + v] for r < rows, c' < a, v < L: a column-indexed block of the
+// CG's state (vectors [n][s], scalars [s], shift state [S][nb][s], the B^T r block
+// partials [nb s][MS_UB]) restricted to the columns map[0 .. a).
+__global__ void ms_cols_gather_kernel(const double* __restrict__ src, int64_t rows, int s,
+                                      const int* __restrict__ map, int a, int L,
+                                      double* __restrict__ dst) {
+  const int64_t total = rows * a * L;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t v = i % L, rc = i / L;
+    const int c = (int)(rc % a);
+    const int64_t r = rc / a;
+    dst[i] = src[(r * s + map[c]) * L + v];
+  }
+}
+
+// act[0 .. a) = 1 (every column of a compacted block is active)
+__global__ void ms_set_active_kernel(int* __restrict__ act, int a) {
+  if ((int)threadIdx.x < a) act[threadIdx.x] = 1;
+}
+
 // dst[i][c] = src[perm[i]][c] for c < ns_src, 0 for the padding columns up to s
 // (perm null: identity): a host block in the caller's row order into the device's
 // locality order, on the device.

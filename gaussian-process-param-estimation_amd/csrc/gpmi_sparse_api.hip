@@ -110,6 +110,8 @@ __global__ void ms_cg2_update_kernel(const double*, double*, const double*, doub
                                      const double*, int, int, int, double, int, int64_t, MsPin*);
 __global__ void ms_cg2_reduce_kernel(const double*, int, int, const double*, int, int, double*);
 __global__ void ms_cg2_close_kernel(MsScal, MsShift, const double*, int, int, int);
+__global__ void ms_cols_gather_kernel(const double*, int64_t, int, const int*, int, int, double*);
+__global__ void ms_set_active_kernel(int*, int);
 __global__ void ms_dots2_kernel(const double*, const double*, int64_t, int, double*);
 template <int CT>
 __global__ void dense_mm_kernel(const double*, int64_t, int64_t, const double*, int, int, double*);
@@ -195,11 +197,14 @@ struct gpmi_sp {
   size_t ms_partial_doubles = 0;
   void* ms_pin = nullptr;                  // pinned flags / r.r of two CG batches
   double* cg2_buf = nullptr;               // the Chronopoulos-Gear form's dot rows
+  double* ms_cbuf = nullptr;               // its compacted state (active columns only)
+  size_t ms_cbuf_doubles = 0;
   size_t cg2_doubles = 0;
   hipEvent_t ms_ev[2] = {nullptr, nullptr};
   std::mutex win_mu;           // the lazy X-window build (ensure_window)
   size_t msbuf_doubles = 0;
   int last_converged = 1;      // last gpmi_sp_cg / gpmi_sp_msgram met rtol in every column
+  int last_compactions = 0;    // active-column compactions of the last multi-shift CG
   // Locality order (gpmi_sp_create_matern, d <= 3): device row r is original point
   // perm[r] (cells in Morton order), so the rows a CU streams through have their X
   // gathers in a compact window that stays in its XCD's L2. Host inputs and
@@ -1036,6 +1041,7 @@ int gpmi_sp_destroy(gpmi_sp* sp) {
   if (sp->ms_partial) (void)hipFree(sp->ms_partial);
   if (sp->ms_pin) (void)hipHostFree(sp->ms_pin);
   if (sp->cg2_buf) (void)hipFree(sp->cg2_buf);
+  if (sp->ms_cbuf) (void)hipFree(sp->ms_cbuf);
   for (hipEvent_t e : sp->ev_pool) (void)hipEventDestroy(e);
   for (auto& r : sp->spmm_log) {
     if (r.e0) (void)hipEventDestroy(r.e0);
@@ -1366,7 +1372,8 @@ static int msgram_cg2(gpmi_sp* sp, const double* etas, int neta, const double* r
     SP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
     SP_TRY(hipStreamCreateWithPriority(&sp->ms_stream, hipStreamNonBlocking, hi));
   }
-  const int64_t ns = n * s;
+  int64_t ns = n * s;
+  const int s0 = s;   // the block's width at the start (compaction narrows s)
   const double eta0 = *std::min_element(etas, etas + neta);
   int rc = 0;
   auto even = [](size_t d) { return (d + 1) & ~(size_t)1; };
@@ -1387,7 +1394,7 @@ static int msgram_cg2(gpmi_sp* sp, const double* etas, int neta, const double* r
   // [MS_UB][nbd s]; their sums [2s + nbd s] (ms_cg2_reduce_kernel); the init partials
   // [MS_NBLK][ne]
   const int64_t nblk_sp = kind == 5 ? sp->win_nblk : MS_DOT_BLK;
-  const int neb = nbd * s;
+  int neb = nbd * s;
   const int ne0 = nbd * s + s;
   const size_t c_sp = (size_t)nblk_sp * 2 * s, c_bp = (size_t)MS_UB * neb;
   const size_t c_red = 2 * (size_t)s + neb, c_init = (size_t)MS_NBLK * ne0;
@@ -1512,6 +1519,125 @@ static int msgram_cg2(gpmi_sp* sp, const double* etas, int neta, const double* r
   bool prev = false;
   int nb = MS_BATCH;
   int kb = 0;
+  // Active-column compaction (round 6). The block iterates until its slowest column
+  // converges, and a stopped column still costs its share of every SpMM and vector
+  // pass (zero steps). BASELINE cfg 5: the ten basis columns of [X z] stop at ~42
+  // iterations, the data column z runs to ~90. Once at most half of the columns are
+  // still active, their state (r, s, the scalars, the shift recurrences, the B^T r
+  // block partials) is gathered into a block of their width and the loop goes on
+  // there; the dropped columns' Grams are final and kept on the host. Every column's
+  // arithmetic is unchanged (the SpMM, the dots and the updates are per column): the
+  // Grams are bit-identical to the uncompacted block (test_msgram_compaction_*).
+  // GPMI_MS_COMPACT=0: off.
+  const char* cenv = std::getenv("GPMI_MS_COMPACT");
+  const bool compact_on = !(cenv && std::atoi(cenv) == 0);
+  std::vector<int> orig(s);   // each current column's index in the original block
+  for (int c = 0; c < s; ++c) orig[c] = c;
+  std::vector<double> g_final((size_t)S * nbd * s0, 0.0);   // [j][cp][c original]
+  int compactions = 0;
+  auto compact = [&]() -> int {
+    SP_TRY(hipStreamSynchronize(str));
+    std::vector<int> act(s);
+    SP_TRY(hipMemcpy(act.data(), sc[it & 1].active, sizeof(int) * s, hipMemcpyDeviceToHost));
+    std::vector<int> map;
+    for (int c = 0; c < s; ++c)
+      if (act[c]) map.push_back(c);
+    const int a = (int)map.size();
+    if (a == 0 || 2 * a > s) return 0;
+    {
+      std::vector<double> g((size_t)S * nbd * s);
+      SP_TRY(hipMemcpy(g.data(), sh.g, sizeof(double) * g.size(), hipMemcpyDeviceToHost));
+      for (int c = 0; c < s; ++c) {
+        if (act[c]) continue;
+        for (int jc = 0; jc < S * nbd; ++jc)
+          g_final[(size_t)jc * s0 + orig[c]] = g[(size_t)jc * s + c];
+      }
+    }
+    const size_t na = even((size_t)n * a);
+    const size_t cneed = 3 * na + (size_t)MS_UB * nbd * a + 2 * 5 * (size_t)a + (size_t)a +
+                         4 * (size_t)S * nbd * a + (size_t)a + 2;
+    if (sp->ms_cbuf_doubles < cneed) {
+      if (sp->ms_cbuf) SP_TRY(hipFree(sp->ms_cbuf));
+      sp->ms_cbuf = nullptr;
+      SP_TRY(hipMalloc(&sp->ms_cbuf, sizeof(double) * cneed));
+      sp->ms_cbuf_doubles = cneed;
+    }
+    double* cq = sp->ms_cbuf;
+    // the compacted block lives in ms_cbuf; the three vector slots rotate through it
+    // and the old block's buffers are left alone
+    double* Rn = cq; cq += na;
+    double* Wn = cq; cq += na;
+    double* Sn = cq; cq += na;
+    double* bpn = cq; cq += (size_t)MS_UB * nbd * a;
+    MsScal scn[2];
+    for (int b = 0; b < 2; ++b) {
+      scn[b].rr = cq; cq += a;
+      scn[b].a = cq; cq += a;
+      scn[b].a_prev = cq; cq += a;
+      scn[b].beta = cq; cq += a;
+      scn[b].active = reinterpret_cast<int*>(cq); cq += a;
+    }
+    MsShift shn = sh;   // flags, it_stop shared
+    shn.bn2 = cq; cq += a;
+    shn.z = cq; cq += (size_t)S * a;
+    shn.z_prev = cq; cq += (size_t)S * a;
+    shn.bp = cq; cq += (size_t)S * nbd * a;
+    shn.g = cq; cq += (size_t)S * nbd * a;
+    int* mapd = reinterpret_cast<int*>(cq);
+    SP_TRY(hipMemcpyAsync(mapd, map.data(), sizeof(int) * a, hipMemcpyHostToDevice, str));
+    auto gather = [&](const double* src, int64_t rows, int L, double* dst) {
+      const int64_t tot = rows * a * L;
+      const unsigned g = (unsigned)std::min<int64_t>(2048, (tot + 255) / 256);
+      hipLaunchKernelGGL(ms_cols_gather_kernel, dim3(std::max(1u, g)), dim3(256), 0, str, src,
+                         rows, s, (const int*)mapd, a, L, dst);
+    };
+    const MsScal& cur = sc[it & 1];
+    MsScal& ncur = scn[it & 1];
+    gather(Rd, n, 1, Rn);
+    gather(Sd, n, 1, Sn);
+    gather(bpart, nbd, MS_UB, bpn);   // [cp s + c][vb] -> [cp a + c'][vb]
+    gather(cur.rr, 1, 1, ncur.rr);
+    gather(cur.a, 1, 1, ncur.a);
+    gather(cur.a_prev, 1, 1, ncur.a_prev);
+    gather(cur.beta, 1, 1, ncur.beta);
+    gather(sh.bn2, 1, 1, shn.bn2);
+    gather(sh.z, S, 1, shn.z);
+    gather(sh.z_prev, S, 1, shn.z_prev);
+    gather(sh.bp, (int64_t)S * nbd, 1, shn.bp);
+    gather(sh.g, (int64_t)S * nbd, 1, shn.g);
+    SP_LAUNCH("ms_cols_gather_kernel");
+    hipLaunchKernelGGL(ms_set_active_kernel, dim3(1), dim3(64), 0, str, ncur.active, a);
+    SP_LAUNCH("ms_set_active_kernel");
+    SP_TRY(hipStreamSynchronize(str));
+    // host-side state in the new column order (no batch is in flight)
+    std::vector<int> norig(a);
+    std::vector<double> nrr(a);
+    for (int q = 0; q < a; ++q) {
+      norig[q] = orig[map[q]];
+      nrr[q] = rr_seen[map[q]];
+    }
+    for (int qs = 0; qs < 2; ++qs) {
+      double bn[MS_MAXS];
+      for (int q = 0; q < a; ++q) bn[q] = pin[qs].bn2[map[q]];
+      for (int q = 0; q < a; ++q) pin[qs].bn2[q] = bn[q];
+    }
+    orig.swap(norig);
+    rr_seen.swap(nrr);
+    Rd = Rn;
+    Wd = Wn;
+    Sd = Sn;
+    bpart = bpn;
+    sc[0] = scn[0];
+    sc[1] = scn[1];
+    sh = shn;
+    s = a;
+    ns = n * s;
+    neb = nbd * s;
+    hact.assign(s, 0);
+    prev = false;
+    ++compactions;
+    return 0;
+  };
   auto read_slot = [&](int qs, int* remaining_after) -> int {
     SP_TRY(hipEventSynchronize(sp->ms_ev[qs]));
     if (pin[qs].flag) {
@@ -1546,12 +1672,15 @@ static int msgram_cg2(gpmi_sp* sp, const double* etas, int neta, const double* r
     slot_it[qs] = it;
     ++kb;
     int rem = MS_BATCH;
+    int prev_read = -1;   // the slot read this round (its flags drive the compaction)
     if (prev) {
       const int r = read_slot(qs ^ 1, &rem);
       if (r == 2) break;
       if (r) return r;
+      prev_read = qs ^ 1;
     }
     prev = true;
+    int read = prev_read;
     if (rem <= 0) {
       int rem2 = 0;
       const int r = read_slot(qs, &rem2);
@@ -1559,6 +1688,13 @@ static int msgram_cg2(gpmi_sp* sp, const double* etas, int neta, const double* r
       if (r) return r;
       prev = false;
       rem = rem2;
+      read = qs;
+    }
+    if (compact_on && read >= 0 && s > 1 && it < maxiter) {
+      int nact = 0;
+      for (int c = 0; c < s; ++c) nact += pin[read].act[c] ? 1 : 0;
+      if (2 * nact <= s)
+        if ((rc = compact())) return rc;
     }
     nb = std::max(1, std::min(MS_BATCH, rem));
   }
@@ -1573,15 +1709,23 @@ static int msgram_cg2(gpmi_sp* sp, const double* etas, int neta, const double* r
   std::vector<double> hg((size_t)S * nbd * s);
   SP_TRY(hipMemcpyAsync(hg.data(), sh.g, sizeof(double) * hg.size(), hipMemcpyDeviceToHost, str));
   SP_TRY(hipStreamSynchronize(str));
+  sp->last_compactions = compactions;
   if (flag)
     return set_error(1, "multi-shift CG: p^T (K + min(eta) I) p <= 0 (not positive definite)");
   bool any = false;
   for (int c = 0; c < s; ++c) any = any || hact[c];
   sp->last_converged = any ? 0 : 1;
+  // each original column from the current block, or from the host copy its compaction
+  // kept when it stopped
+  std::vector<int> where(s0, -1);
+  for (int c = 0; c < s; ++c) where[orig[c]] = c;
   for (int j = 0; j < S; ++j)
     for (int a = 0; a < nrhs; ++a)
-      for (int c = 0; c < nsub; ++c)
-        G[((size_t)j * nrhs + a) * nsub + c] = hg[((size_t)j * nbd + a) * s + c];
+      for (int c = 0; c < nsub; ++c) {
+        const size_t jc = (size_t)j * nbd + a;
+        G[((size_t)j * nrhs + a) * nsub + c] =
+            where[c] >= 0 ? hg[jc * s + where[c]] : g_final[jc * s0 + c];
+      }
   if (iterations) *iterations = it_stop >= 0 ? it_stop : it;
   return 0;
 }
@@ -1665,6 +1809,12 @@ int gpmi_sp_spmm_kernel(gpmi_sp* sp, int s, int* kind) {
 int gpmi_sp_last_status(const gpmi_sp* sp, int* converged) {
   if (!sp) return set_error(-1006, "null handle");
   if (converged) *converged = sp->last_converged;
+  return 0;
+}
+
+int gpmi_sp_msgram_compactions(const gpmi_sp* sp, int* count) {
+  if (!sp || !count) return set_error(-1006, "null handle");
+  *count = sp->last_compactions;
   return 0;
 }
 

@@ -113,6 +113,7 @@ SIGNATURES = {
     'gpmi_band_cq_stats': (ctypes.c_int, [c_op_p, c_int_p, c_int_p, c_int_p]),
     'gpmi_band_chase_info': (ctypes.c_int, [c_op_p, c_int_p, c_int_p, c_int_p]),
     'gpmi_sp_last_status': (ctypes.c_int, [c_op_p, c_int_p]),
+    'gpmi_sp_msgram_compactions': (ctypes.c_int, [c_op_p, c_int_p]),
     'gpmi_sp_spmm_info': (ctypes.c_int, [c_op_p, c_int_p, c_double_p, c_int_p]),
     'gpmi_sp_spmm_kernel': (ctypes.c_int, [c_op_p, ctypes.c_int, c_int_p]),
     'gpmi_band_last_timing': (ctypes.c_int, [c_op_p, c_double_p, c_double_p, c_double_p]),
@@ -764,6 +765,13 @@ class SparseOperator(object):
             self._warn_unconverged('msgram', maxiter)
         self.last_cg_iterations = it.value
         return G
+
+    def msgram_compactions(self):
+        """Active-column compactions of the last msgram call (diagnostic)."""
+        v = ctypes.c_int(0)
+        check(self.lib.gpmi_sp_msgram_compactions(self.h, ctypes.byref(v)),
+              'gpmi_sp_msgram_compactions')
+        return v.value
 
     def _warn_unconverged(self, what, maxiter):
         """scipy's cg (the reference's sparse solve, _linear_solver.py:64,68)

@@ -232,6 +232,11 @@ int gpmi_sp_spmm_kernel(gpmi_sp* sp, int s, int* kind);
  * Python layer warns. (A non-positive p^T A p makes those calls return 1, "not
  * positive definite".) */
 int gpmi_sp_last_status(const gpmi_sp* sp, int* converged);
+/* Active-column compactions of the last gpmi_sp_msgram(_cols) call: once at most
+ * half of the block's columns still iterate, their state moves into a block of
+ * their width (the Grams are unchanged, bit for bit; GPMI_MS_COMPACT=0 disables
+ * it). Diagnostic. */
+int gpmi_sp_msgram_compactions(const gpmi_sp* sp, int* count);
 
 /* Device-resident SpMM timing: reps launches of Y = (K + eta I) X with an
  * [n][s] block already in HBM, queued behind a gate kernel that holds the stream
