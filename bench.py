@@ -363,7 +363,8 @@ def cpu_baseline_sparse(K, X, z, etas, nprobe, steps, seed, budget_s, workers=No
             'logdet': logdet.tolist(), 'gram_columns': cols}
 
 
-def sparse_step_bytes(n, nnz, s_lanczos, steps, s_cg, cg_iters, orthogonalize=0):
+def sparse_step_bytes(n, nnz, s_lanczos, steps, s_cg, cg_iters, orthogonalize=0,
+                      cg_segments=None):
     """Algorithmic bytes of one sparse step as implemented (each vector block
     read or written once per pass). Lanczos (block b_L = 8 n s_L): with
     orthogonalize = 0 (imate's default, the plain recurrence, gpmi_sparse.hip
@@ -375,7 +376,10 @@ def sparse_step_bytes(n, nnz, s_lanczos, steps, s_cg, cg_iters, orthogonalize=0)
     Multi-shift CG (b_C = 8 n s_C, s_C the device width: a full 11-column block on
     the window SpMM is padded by one zero column) per iteration: the SpMM (p . q in
     its epilogue), the r update with B^T r / r . r on MFMA (b, r, q read, r
-    written: 4 b_C) and p = r + beta p (3 b_C)."""
+    written: 4 b_C) and p = r + beta p (3 b_C). cg_segments: the CG's launch
+    segments [(device width, iterations), ...] (gpmi_sp_msgram_segments: the full
+    block, then the block its active-column compaction narrowed it to); without
+    them cg_iters iterations at width s_cg."""
     csr = 12.0 * nnz + 8.0 * (n + 1)
     bl, bc = 8.0 * n * s_lanczos, 8.0 * n * s_cg
     if orthogonalize == 0:
@@ -385,7 +389,9 @@ def sparse_step_bytes(n, nnz, s_lanczos, steps, s_cg, cg_iters, orthogonalize=0)
         lanczos = sum(csr + 2 * bl + (k + 2) * bl + (k + 4) * bl for k in range(steps)) + \
             (steps + 1) * bl
         basis = sum(2.0 * k * bl for k in range(steps)) + steps * bl
-    cg = cg_iters * (csr + 2 * bc + 7 * bc)
+    if cg_segments is None:
+        cg_segments = [(s_cg, cg_iters)]
+    cg = sum(k * (csr + 9 * 8.0 * n * w) for w, k in cg_segments)
     return {'lanczos': lanczos, 'lanczos_basis_reads': basis, 'cg': cg,
             'total': lanczos + cg}
 
@@ -447,7 +453,7 @@ def sparse_measure(args, config, world, rank, local, dist, torch, cpu, exact, de
     op.sop.set_rhs(R)
     lo, hi, per = shard(neta, world, rank)
 
-    holder = {'cg_iters': 0}
+    holder = {'cg_iters': 0, 'cg_segments': None}
 
     def step():
         # the SLQ Lanczos of the probe shard and the multi-shift CG Gram blocks of
@@ -458,6 +464,7 @@ def sparse_measure(args, config, world, rank, local, dist, torch, cpu, exact, de
         rows = numpy.zeros((per, 3))
         if hi > lo:
             holder['cg_iters'] = op.sop.last_cg_iterations
+            holder['cg_segments'] = op.sop.msgram_segments()
             ld = curves['logdet'][lo:hi]
             rows[:hi - lo, 0] = etas[lo:hi]
             rows[:hi - lo, 1] = ld
@@ -551,7 +558,7 @@ def sparse_measure(args, config, world, rank, local, dist, torch, cpu, exact, de
                 for w, (c, t) in sorted(spmm_in_step.items())}
     my_probes = shard(nprobe, world, rank)
     sb = sparse_step_bytes(n, nnz, my_probes[1] - my_probes[0], steps, s_cg,
-                           holder['cg_iters'], op.orthogonalize)
+                           holder['cg_iters'], op.orthogonalize, holder['cg_segments'])
     step_s = dt / args.steps
     res = None
     if rank == 0:
@@ -613,6 +620,9 @@ def sparse_measure(args, config, world, rank, local, dist, torch, cpu, exact, de
                 'lanczos_bytes': sb['lanczos'], 'lanczos_basis_read_bytes':
                     sb['lanczos_basis_reads'], 'cg_bytes': sb['cg'],
                 'cg_iterations': holder['cg_iters'],
+                # (device width, iterations launched) of the full block and of the
+                # block the active-column compaction narrowed it to
+                'cg_segments': holder['cg_segments'],
                 'lanczos_probes': my_probes[1] - my_probes[0], 'lanczos_steps': steps,
                 'cg_columns': R.shape[1], 'cg_device_width': s_cg,
                 'lanczos_orthogonalize': op.orthogonalize,

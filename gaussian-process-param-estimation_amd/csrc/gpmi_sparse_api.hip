@@ -205,6 +205,8 @@ struct gpmi_sp {
   size_t msbuf_doubles = 0;
   int last_converged = 1;      // last gpmi_sp_cg / gpmi_sp_msgram met rtol in every column
   int last_compactions = 0;    // active-column compactions of the last multi-shift CG
+  // its launch segments: (block width, iterations launched at that width), in order
+  std::vector<std::pair<int, int>> last_segments;
   // Locality order (gpmi_sp_create_matern, d <= 3): device row r is original point
   // perm[r] (cells in Morton order), so the rows a CU streams through have their X
   // gathers in a compact window that stays in its XCD's L2. Host inputs and
@@ -1535,6 +1537,8 @@ static int msgram_cg2(gpmi_sp* sp, const double* etas, int neta, const double* r
   for (int c = 0; c < s; ++c) orig[c] = c;
   std::vector<double> g_final((size_t)S * nbd * s0, 0.0);   // [j][cp][c original]
   int compactions = 0;
+  int seg_start = 0;   // the iteration the current block width began at
+  std::vector<std::pair<int, int>> segments;
   auto compact = [&]() -> int {
     SP_TRY(hipStreamSynchronize(str));
     std::vector<int> act(s);
@@ -1623,6 +1627,8 @@ static int msgram_cg2(gpmi_sp* sp, const double* etas, int neta, const double* r
     }
     orig.swap(norig);
     rr_seen.swap(nrr);
+    segments.emplace_back(s, it - seg_start);
+    seg_start = it;
     Rd = Rn;
     Wd = Wn;
     Sd = Sn;
@@ -1710,6 +1716,8 @@ static int msgram_cg2(gpmi_sp* sp, const double* etas, int neta, const double* r
   SP_TRY(hipMemcpyAsync(hg.data(), sh.g, sizeof(double) * hg.size(), hipMemcpyDeviceToHost, str));
   SP_TRY(hipStreamSynchronize(str));
   sp->last_compactions = compactions;
+  segments.emplace_back(s, it - seg_start);
+  sp->last_segments = segments;
   if (flag)
     return set_error(1, "multi-shift CG: p^T (K + min(eta) I) p <= 0 (not positive definite)");
   bool any = false;
@@ -1815,6 +1823,20 @@ int gpmi_sp_last_status(const gpmi_sp* sp, int* converged) {
 int gpmi_sp_msgram_compactions(const gpmi_sp* sp, int* count) {
   if (!sp || !count) return set_error(-1006, "null handle");
   *count = sp->last_compactions;
+  return 0;
+}
+
+int gpmi_sp_msgram_segments(const gpmi_sp* sp, int cap, int* widths, int* iterations,
+                            int* count) {
+  if (!sp || !count) return set_error(-1006, "null handle");
+  const int m = (int)sp->last_segments.size();
+  *count = m;
+  if (m > 0 && cap < m) return set_error(-1003, "gpmi_sp_msgram_segments: cap < segments");
+  if (m > 0 && (!widths || !iterations)) return set_error(-1006, "null output");
+  for (int q = 0; q < m; ++q) {
+    widths[q] = sp->last_segments[q].first;
+    iterations[q] = sp->last_segments[q].second;
+  }
   return 0;
 }
 

@@ -114,6 +114,8 @@ SIGNATURES = {
     'gpmi_band_chase_info': (ctypes.c_int, [c_op_p, c_int_p, c_int_p, c_int_p]),
     'gpmi_sp_last_status': (ctypes.c_int, [c_op_p, c_int_p]),
     'gpmi_sp_msgram_compactions': (ctypes.c_int, [c_op_p, c_int_p]),
+    'gpmi_sp_msgram_segments': (ctypes.c_int, [c_op_p, ctypes.c_int, c_int_p, c_int_p,
+                                               c_int_p]),
     'gpmi_sp_spmm_info': (ctypes.c_int, [c_op_p, c_int_p, c_double_p, c_int_p]),
     'gpmi_sp_spmm_kernel': (ctypes.c_int, [c_op_p, ctypes.c_int, c_int_p]),
     'gpmi_band_last_timing': (ctypes.c_int, [c_op_p, c_double_p, c_double_p, c_double_p]),
@@ -772,6 +774,17 @@ class SparseOperator(object):
         check(self.lib.gpmi_sp_msgram_compactions(self.h, ctypes.byref(v)),
               'gpmi_sp_msgram_compactions')
         return v.value
+
+    def msgram_segments(self):
+        """The last msgram call's launch segments [(block width, iterations), ...]:
+        the full block, then each compacted block (diagnostic)."""
+        cap = 64
+        w = (ctypes.c_int * cap)()
+        k = (ctypes.c_int * cap)()
+        m = ctypes.c_int(0)
+        check(self.lib.gpmi_sp_msgram_segments(self.h, cap, w, k, ctypes.byref(m)),
+              'gpmi_sp_msgram_segments')
+        return [(w[q], k[q]) for q in range(m.value)]
 
     def _warn_unconverged(self, what, maxiter):
         """scipy's cg (the reference's sparse solve, _linear_solver.py:64,68)

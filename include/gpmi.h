@@ -237,6 +237,13 @@ int gpmi_sp_last_status(const gpmi_sp* sp, int* converged);
  * their width (the Grams are unchanged, bit for bit; GPMI_MS_COMPACT=0 disables
  * it). Diagnostic. */
 int gpmi_sp_msgram_compactions(const gpmi_sp* sp, int* count);
+/* The launch segments of the last gpmi_sp_msgram(_cols) call, in order: segment q
+ * ran iterations[q] iterations (each one SpMM + reduce + update launch) at block
+ * width widths[q] (the full block, then each compacted block). count = segments
+ * (compactions + 1); cap = room in widths / iterations. Diagnostic (bench.py's
+ * algorithmic-byte count of the step). */
+int gpmi_sp_msgram_segments(const gpmi_sp* sp, int cap, int* widths, int* iterations,
+                            int* count);
 
 /* Device-resident SpMM timing: reps launches of Y = (K + eta I) X with an
  * [n][s] block already in HBM, queued behind a gate kernel that holds the stream

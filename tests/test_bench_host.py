@@ -63,6 +63,10 @@ def test_sparse_step_bytes_model():
     assert b['lanczos_basis_reads'] == sum(2 * k * bl for k in range(3)) + 3 * bl
     assert b['cg'] == 10 * (csr + 9 * bc)
     assert b['total'] == b['lanczos'] + b['cg']
+    # the compacted CG: each launch segment at its own width
+    c = bench.sparse_step_bytes(n, nnz, 4, 3, 12, 90, cg_segments=[(12, 42), (1, 49)])
+    assert c['cg'] == 42 * (csr + 9 * 8.0 * n * 12) + 49 * (csr + 9 * 8.0 * n * 1)
+    assert c['lanczos'] == p['lanczos']
 
 
 def _json_line(out):

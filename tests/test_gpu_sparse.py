@@ -747,9 +747,18 @@ def test_msgram_compaction_bit_identical(gp, monkeypatch, cols):
     monkeypatch.setenv('GPMI_MS_COMPACT', '0')
     G0 = sop.msgram(etas, B, rtol=1e-12, cols=cols)
     assert sop.msgram_compactions() == 0
+    seg0 = sop.msgram_segments()
+    assert len(seg0) == 1
     monkeypatch.setenv('GPMI_MS_COMPACT', '1')
     G1 = sop.msgram(etas, B, rtol=1e-12, cols=cols)
     assert sop.msgram_compactions() >= 1
+    # the launch segments: the full block's width, then narrower blocks, and at
+    # least the iterations to the last column's stop launched in all
+    seg1 = sop.msgram_segments()
+    assert len(seg1) == sop.msgram_compactions() + 1
+    assert seg1[0][0] == seg0[0][0]
+    assert all(seg1[q + 1][0] <= seg1[q][0] // 2 for q in range(len(seg1) - 1))
+    assert sum(k for _, k in seg1) >= sop.last_cg_iterations > 0
     numpy.testing.assert_array_equal(G1, G0)
     lo, hi = cols if cols else (0, 7)
     for j, eta in enumerate(etas):
