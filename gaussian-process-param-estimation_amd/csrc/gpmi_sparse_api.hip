@@ -197,8 +197,10 @@ struct gpmi_sp {
   size_t ms_partial_doubles = 0;
   void* ms_pin = nullptr;                  // pinned flags / r.r of two CG batches
   double* cg2_buf = nullptr;               // the Chronopoulos-Gear form's dot rows
-  double* ms_cbuf = nullptr;               // its compacted state (active columns only)
-  size_t ms_cbuf_doubles = 0;
+  // its compacted state (active columns only): two, alternating, so that a second
+  // compaction gathers from the first one's buffer into the other
+  double* ms_cbuf[2] = {nullptr, nullptr};
+  size_t ms_cbuf_doubles[2] = {0, 0};
   size_t cg2_doubles = 0;
   hipEvent_t ms_ev[2] = {nullptr, nullptr};
   std::mutex win_mu;           // the lazy X-window build (ensure_window)
@@ -1043,7 +1045,8 @@ int gpmi_sp_destroy(gpmi_sp* sp) {
   if (sp->ms_partial) (void)hipFree(sp->ms_partial);
   if (sp->ms_pin) (void)hipHostFree(sp->ms_pin);
   if (sp->cg2_buf) (void)hipFree(sp->cg2_buf);
-  if (sp->ms_cbuf) (void)hipFree(sp->ms_cbuf);
+  for (double* cb : sp->ms_cbuf)
+    if (cb) (void)hipFree(cb);
   for (hipEvent_t e : sp->ev_pool) (void)hipEventDestroy(e);
   for (auto& r : sp->spmm_log) {
     if (r.e0) (void)hipEventDestroy(r.e0);
@@ -1533,6 +1536,8 @@ static int msgram_cg2(gpmi_sp* sp, const double* etas, int neta, const double* r
   // GPMI_MS_COMPACT=0: off.
   const char* cenv = std::getenv("GPMI_MS_COMPACT");
   const bool compact_on = !(cenv && std::atoi(cenv) == 0);
+  // GPMI_MS_TRACE=1: each batch's size and each read's prediction on stderr (diagnostic)
+  const bool trace = std::getenv("GPMI_MS_TRACE") != nullptr;
   std::vector<int> orig(s);   // each current column's index in the original block
   for (int c = 0; c < s; ++c) orig[c] = c;
   std::vector<double> g_final((size_t)S * nbd * s0, 0.0);   // [j][cp][c original]
@@ -1560,13 +1565,14 @@ static int msgram_cg2(gpmi_sp* sp, const double* etas, int neta, const double* r
     const size_t na = even((size_t)n * a);
     const size_t cneed = 3 * na + (size_t)MS_UB * nbd * a + 2 * 5 * (size_t)a + (size_t)a +
                          4 * (size_t)S * nbd * a + (size_t)a + 2;
-    if (sp->ms_cbuf_doubles < cneed) {
-      if (sp->ms_cbuf) SP_TRY(hipFree(sp->ms_cbuf));
-      sp->ms_cbuf = nullptr;
-      SP_TRY(hipMalloc(&sp->ms_cbuf, sizeof(double) * cneed));
-      sp->ms_cbuf_doubles = cneed;
+    const int cb = compactions & 1;   // (the current block may live in the other one)
+    if (sp->ms_cbuf_doubles[cb] < cneed) {
+      if (sp->ms_cbuf[cb]) SP_TRY(hipFree(sp->ms_cbuf[cb]));
+      sp->ms_cbuf[cb] = nullptr;
+      SP_TRY(hipMalloc(&sp->ms_cbuf[cb], sizeof(double) * cneed));
+      sp->ms_cbuf_doubles[cb] = cneed;
     }
-    double* cq = sp->ms_cbuf;
+    double* cq = sp->ms_cbuf[cb];
     // the compacted block lives in ms_cbuf; the three vector slots rotate through it
     // and the old block's buffers are left alone
     double* Rn = cq; cq += na;
@@ -1644,7 +1650,19 @@ static int msgram_cg2(gpmi_sp* sp, const double* etas, int neta, const double* r
     ++compactions;
     return 0;
   };
-  auto read_slot = [&](int qs, int* remaining_after) -> int {
+  // Predictions from each read (round 6): need_after, the iterations the slowest active
+  // column still needs beyond those queued (it; unknown at first: a batch at a time), and
+  // compact_at, the iteration by which at most half of the block's columns should still
+  // iterate (each column's stop from its own rate; -1: none predicted). A batch sized to
+  // end where the prediction says the CG stops, or where the block can be compacted, is
+  // read as soon as it ends instead of after the next batch is queued: before, the
+  // iterations queued past the stop ran at full cost (cfg 4: 111 launched for 102) and
+  // the compaction waited a batch at the full width.
+  int need_after = maxiter;
+  int compact_at = -1;
+  int forced_reads = 0;   // compaction reads that found too few columns stopped
+  std::vector<double> stops;
+  auto read_slot = [&](int qs) -> int {
     SP_TRY(hipEventSynchronize(sp->ms_ev[qs]));
     if (pin[qs].flag) {
       SP_TRY(hipStreamSynchronize(str));
@@ -1653,20 +1671,39 @@ static int msgram_cg2(gpmi_sp* sp, const double* etas, int neta, const double* r
     bool any = false;
     double needm = 0.0;
     const int at = slot_it[qs];
+    int nact = 0;
+    stops.clear();
     for (int c = 0; c < s; ++c) {
       if (!pin[qs].act[c]) continue;
       any = true;
+      ++nact;
       const double r1 = pin[qs].rr[c], r0 = rr_seen[c], target = rtol * rtol * pin[qs].bn2[c];
       double m = (double)MS_BATCH;
-      if (r0 > 0.0 && r1 > 0.0 && r1 < r0 && at > it_seen && target > 0.0)
+      bool rated = false;
+      if (r0 > 0.0 && r1 > 0.0 && r1 < r0 && at > it_seen && target > 0.0) {
         m = std::log(target / r1) / (std::log(r1 / r0) / (double)(at - it_seen));
+        rated = true;
+      }
       needm = std::max(needm, m);
+      stops.push_back(rated ? (double)at + std::max(0.0, m) : 1e300);
       rr_seen[c] = r1;
     }
     it_seen = at;
     // clamped before the conversion: a stagnating residual (r1 / r0 -> 1) gives a huge m
     const double rem = std::min((double)maxiter, std::ceil((double)at + needm)) - (double)it;
-    *remaining_after = (int)std::max(-1.0, std::min(rem, (double)MS_BATCH));
+    need_after = (int)std::max(-1.0, rem);
+    compact_at = -1;
+    const int k = nact - s / 2;   // columns that must stop before the block can narrow
+    if (compact_on && s > 1 && any && k >= 1 && forced_reads < 2) {
+      std::nth_element(stops.begin(), stops.begin() + (k - 1), stops.end());
+      const double tk = stops[k - 1];
+      if (tk < (double)maxiter) compact_at = (int)std::ceil(tk);
+    }
+    if (trace)
+      std::fprintf(stderr,
+                   "[ms] read slot at %d (queued %d, width %d, active %d): need %.1f more, "
+                   "after %d, compact at %d%s\n",
+                   at, it, s, nact, needm, need_after, compact_at, any ? "" : " (all stopped)");
     return any ? 0 : 2;
   };
   while (it < maxiter) {
@@ -1677,34 +1714,42 @@ static int msgram_cg2(gpmi_sp* sp, const double* etas, int neta, const double* r
     SP_TRY(hipEventRecord(sp->ms_ev[qs], str));
     slot_it[qs] = it;
     ++kb;
-    int rem = MS_BATCH;
-    int prev_read = -1;   // the slot read this round (its flags drive the compaction)
+    need_after -= nb;
+    int read = -1;   // the slot read this round (its flags drive the compaction)
     if (prev) {
-      const int r = read_slot(qs ^ 1, &rem);
+      const int r = read_slot(qs ^ 1);
       if (r == 2) break;
       if (r) return r;
-      prev_read = qs ^ 1;
+      read = qs ^ 1;
     }
     prev = true;
-    int read = prev_read;
-    if (rem <= 0) {
-      int rem2 = 0;
-      const int r = read_slot(qs, &rem2);
+    auto compactable = [&](int q) {
+      int nact = 0;
+      for (int c = 0; c < s; ++c) nact += pin[q].act[c] ? 1 : 0;
+      return 2 * nact <= s;
+    };
+    const bool can_compact = compact_on && s > 1 && it < maxiter;
+    // the stop, or the compaction, predicted within the iterations queued: read them now
+    const bool due = can_compact && compact_at >= 0 && compact_at <= it &&
+                     !(read >= 0 && compactable(read));
+    if (need_after <= 0 || due) {
+      const int r = read_slot(qs);
       if (r == 2) break;
       if (r) return r;
       prev = false;
-      rem = rem2;
       read = qs;
+      if (due && !compactable(qs)) ++forced_reads;
     }
-    if (compact_on && read >= 0 && s > 1 && it < maxiter) {
-      int nact = 0;
-      for (int c = 0; c < s; ++c) nact += pin[read].act[c] ? 1 : 0;
-      if (2 * nact <= s)
-        if ((rc = compact())) return rc;
+    if (can_compact && read >= 0 && compactable(read)) {
+      if ((rc = compact())) return rc;
+      compact_at = -1;   // (a prediction for the old block)
     }
-    nb = std::max(1, std::min(MS_BATCH, rem));
+    nb = std::max(1, std::min(MS_BATCH, need_after));
+    // end the batch where the block is predicted to narrow
+    if (compact_on && s > 1 && compact_at > it && compact_at < it + nb) nb = compact_at - it;
   }
   // the last step of columns still active at maxiter (a no-op when all stopped)
+  if (trace) std::fprintf(stderr, "[ms] loop end: launched %d\n", it);
   hipLaunchKernelGGL(ms_cg2_close_kernel, dim3(1), dim3(256), 0, str, sc[it & 1], sh,
                      (const double*)dshift, S, s, nbd);
   SP_LAUNCH("ms_cg2_close_kernel");
@@ -1734,6 +1779,7 @@ static int msgram_cg2(gpmi_sp* sp, const double* etas, int neta, const double* r
         G[((size_t)j * nrhs + a) * nsub + c] =
             where[c] >= 0 ? hg[jc * s + where[c]] : g_final[jc * s0 + c];
       }
+  if (trace) std::fprintf(stderr, "[ms] all stopped at %d, %d compactions\n", it_stop, compactions);
   if (iterations) *iterations = it_stop >= 0 ? it_stop : it;
   return 0;
 }

@@ -766,6 +766,39 @@ def test_msgram_compaction_bit_identical(gp, monkeypatch, cols):
         assert numpy.max(numpy.abs(G1[j] - ref)) <= 1e-9 * numpy.abs(ref).max()
 
 
+def test_msgram_repeated_compactions_bit_identical(gp, monkeypatch):
+    """Columns that stop in three waves (four in the span of two eigenvectors, two in
+    the span of 24 spread over the spectrum, two random; ~2, ~21, ~35 iterations):
+    the block narrows more than once (8 -> 4 -> 2 ...). Each compaction gathers the state of the block the previous one made (round
+    6: both lived in one buffer, and the second gather overwrote what it read). The
+    Grams equal the uncompacted block's bit for bit, and the exact solves."""
+    from gaussian_proc import _hip
+    _, K = _small_sparse()
+    Kd = K.toarray()
+    n = Kd.shape[0]
+    lam, U = numpy.linalg.eigh(Kd)
+    rng = numpy.random.RandomState(11)
+    B = numpy.empty((n, 8))
+    for c in range(4):
+        B[:, c] = U[:, -1 - c] + 0.5 * U[:, -2 - c]
+    for c in range(4, 6):   # 24 eigenvectors across the spectrum: ~21 iterations
+        B[:, c] = U[:, ::24][:, :24] @ rng.randn(24)
+    B[:, 6:] = rng.randn(n, 2)
+    etas = numpy.array([3.0, 5.0, 40.0])
+    sop = _hip.SparseOperator.from_csr(K)
+    monkeypatch.setenv('GPMI_MS_COMPACT', '0')
+    G0 = sop.msgram(etas, B, rtol=1e-12)
+    it0 = sop.last_cg_iterations
+    monkeypatch.setenv('GPMI_MS_COMPACT', '1')
+    G1 = sop.msgram(etas, B, rtol=1e-12)
+    assert sop.msgram_compactions() >= 2, sop.msgram_segments()
+    assert sop.last_cg_iterations == it0
+    numpy.testing.assert_array_equal(G1, G0)
+    for j, eta in enumerate(etas):
+        ref = B.T @ numpy.linalg.solve(Kd + eta * numpy.eye(n), B)
+        assert numpy.max(numpy.abs(G1[j] - ref)) <= 1e-9 * numpy.abs(ref).max()
+
+
 def test_msgram_large_shifts_stay_finite(gp):
     """A large shift's zeta decays like (1 + d alpha)^-k and underflows to 0 within
     the seed system's iterations; alpha^s = alpha zeta_k / zeta_{k-1} was then 0 / 0
