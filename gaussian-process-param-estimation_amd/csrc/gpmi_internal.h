@@ -119,6 +119,32 @@ constexpr int MS_UB = 512;      // vector blocks of ms_cg2_update_kernel (256 / 
                                 // 12.37 / 12.12 against 11.91 ms per step)
 constexpr int MS_DOT_BLK = 256; // blocks of ms_dots2_kernel (SpMM kinds without the epilogue)
 
+// One active-column compaction of the multi-shift CG as ONE launch (round 6): up to
+// MS_CJOBS column gathers src[r][s][L] -> dst[r][a][L] by the map, the stopped columns'
+// Grams scattered into their final slots (gfin[jc][s0], by original column), and the
+// compacted block's active flags set. Everything by value: no host copy, no sync.
+constexpr int MS_CJOBS = 12;
+struct MsCompactJob {
+  const double* src;
+  double* dst;
+  int64_t rows;
+  int L;
+  int pad;
+};
+struct MsCompactArgs {
+  MsCompactJob job[MS_CJOBS];
+  int njob, s, a, nd, s0, pad;
+  int map[MS_MAXS];         // the kept columns (old block index), in order
+  int drop[MS_MAXS];        // the dropped columns (old block index)
+  int drop_orig[MS_MAXS];   // their original column
+  const double* g;          // [SN][s] the old block's Grams
+  double* gfin;             // [SN][s0]
+  int64_t SN;               // S * nbd
+  const int* act_src;       // [s] the old block's active flags at the compaction
+  int* act;                 // [a] the compacted block's (a kept column may have stopped
+                            //     since the slot the map came from was written)
+};
+
 struct MsPin {
   int act[MS_MAXS];
   int flag;

@@ -1607,26 +1607,42 @@ __global__ void ms_init_kernel(MsScal st, MsShift sh, const double* __restrict__
   }
 }
 
-// Active-column compaction of the multi-shift CG (round 6): dst[(r a + c') L + v] =
-// src[(r s + map[c']) L + v] for r < rows, c' < a, v < L: a column-indexed block of the
-// CG's state (vectors [n][s], scalars [s], shift state [S][nb][s], the B^T r block
-// partials [nb s][MS_UB]) restricted to the columns map[0 .. a).
-__global__ void ms_cols_gather_kernel(const double* __restrict__ src, int64_t rows, int s,
-                                      const int* __restrict__ map, int a, int L,
-                                      double* __restrict__ dst) {
-  const int64_t total = rows * a * L;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t v = i % L, rc = i / L;
-    const int c = (int)(rc % a);
-    const int64_t r = rc / a;
-    dst[i] = src[(r * s + map[c]) * L + v];
+// The compaction (MsCompactArgs): blockIdx.y < njob gathers job y, dst[r][c'][v] =
+// src[r][map[c']][v] (grid-stride over x); blockIdx.y == njob scatters the dropped
+// columns' Grams, gfin[jc][drop_orig[d]] = g[jc][drop[d]], and gathers the new block's
+// active flags.
+__global__ __launch_bounds__(256) void ms_compact_kernel(MsCompactArgs A) {
+  __shared__ int smap[MS_MAXS];
+  const int y = blockIdx.y, t = threadIdx.x;
+  if (y < A.njob) {
+    if (t < A.a) smap[t] = A.map[t];
+    __syncthreads();
+    const MsCompactJob J = A.job[y];
+    const int a = A.a, s = A.s, L = J.L;
+    const int64_t total = J.rows * a * L;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + t; i < total;
+         i += (int64_t)gridDim.x * blockDim.x) {
+      const int64_t v = i % L, rc = i / L;
+      const int c = (int)(rc % a);
+      const int64_t r = rc / a;
+      J.dst[i] = J.src[(r * s + smap[c]) * L + v];
+    }
+    return;
   }
-}
-
-// act[0 .. a) = 1 (every column of a compacted block is active)
-__global__ void ms_set_active_kernel(int* __restrict__ act, int a) {
-  if ((int)threadIdx.x < a) act[threadIdx.x] = 1;
+  __shared__ int sdrop[MS_MAXS], sorig[MS_MAXS];
+  if (t < A.nd) {
+    sdrop[t] = A.drop[t];
+    sorig[t] = A.drop_orig[t];
+  }
+  __syncthreads();
+  const int64_t total = A.SN * A.nd;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + t; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t jc = i / A.nd;
+    const int d = (int)(i - jc * A.nd);
+    A.gfin[jc * A.s0 + sorig[d]] = A.g[jc * A.s + sdrop[d]];
+  }
+  if (blockIdx.x == 0 && t < A.a) A.act[t] = A.act_src[A.map[t]];
 }
 
 // dst[i][c] = src[perm[i]][c] for c < ns_src, 0 for the padding columns up to s

@@ -110,8 +110,7 @@ __global__ void ms_cg2_update_kernel(const double*, double*, const double*, doub
                                      const double*, int, int, int, double, int, int64_t, MsPin*);
 __global__ void ms_cg2_reduce_kernel(const double*, int, int, const double*, int, int, double*);
 __global__ void ms_cg2_close_kernel(MsScal, MsShift, const double*, int, int, int);
-__global__ void ms_cols_gather_kernel(const double*, int64_t, int, const int*, int, int, double*);
-__global__ void ms_set_active_kernel(int*, int);
+__global__ void ms_compact_kernel(MsCompactArgs);
 __global__ void ms_dots2_kernel(const double*, const double*, int64_t, int, double*);
 template <int CT>
 __global__ void dense_mm_kernel(const double*, int64_t, int64_t, const double*, int, int, double*);
@@ -201,6 +200,8 @@ struct gpmi_sp {
   // compaction gathers from the first one's buffer into the other
   double* ms_cbuf[2] = {nullptr, nullptr};
   size_t ms_cbuf_doubles[2] = {0, 0};
+  double* ms_gfin = nullptr;   // the stopped columns' final Grams [S nb][s0]
+  size_t ms_gfin_doubles = 0;
   size_t cg2_doubles = 0;
   hipEvent_t ms_ev[2] = {nullptr, nullptr};
   std::mutex win_mu;           // the lazy X-window build (ensure_window)
@@ -1047,6 +1048,7 @@ int gpmi_sp_destroy(gpmi_sp* sp) {
   if (sp->cg2_buf) (void)hipFree(sp->cg2_buf);
   for (double* cb : sp->ms_cbuf)
     if (cb) (void)hipFree(cb);
+  if (sp->ms_gfin) (void)hipFree(sp->ms_gfin);
   for (hipEvent_t e : sp->ev_pool) (void)hipEventDestroy(e);
   for (auto& r : sp->spmm_log) {
     if (r.e0) (void)hipEventDestroy(r.e0);
@@ -1530,7 +1532,7 @@ static int msgram_cg2(gpmi_sp* sp, const double* etas, int neta, const double* r
   // iterations, the data column z runs to ~90. Once at most half of the columns are
   // still active, their state (r, s, the scalars, the shift recurrences, the B^T r
   // block partials) is gathered into a block of their width and the loop goes on
-  // there; the dropped columns' Grams are final and kept on the host. Every column's
+  // there; the dropped columns' Grams are final and kept in ms_gfin. Every column's
   // arithmetic is unchanged (the SpMM, the dots and the updates are per column): the
   // Grams are bit-identical to the uncompacted block (test_msgram_compaction_*).
   // GPMI_MS_COMPACT=0: off.
@@ -1540,31 +1542,39 @@ static int msgram_cg2(gpmi_sp* sp, const double* etas, int neta, const double* r
   const bool trace = std::getenv("GPMI_MS_TRACE") != nullptr;
   std::vector<int> orig(s);   // each current column's index in the original block
   for (int c = 0; c < s; ++c) orig[c] = c;
-  std::vector<double> g_final((size_t)S * nbd * s0, 0.0);   // [j][cp][c original]
+  // the dropped columns' final Grams, on the device until the end
+  if (compact_on && s0 > 1) {
+    const size_t gneed = (size_t)S * nbd * s0;
+    if (sp->ms_gfin_doubles < gneed) {
+      if (sp->ms_gfin) SP_TRY(hipFree(sp->ms_gfin));
+      sp->ms_gfin = nullptr;
+      SP_TRY(hipMalloc(&sp->ms_gfin, sizeof(double) * gneed));
+      sp->ms_gfin_doubles = gneed;
+    }
+  }
   int compactions = 0;
   int seg_start = 0;   // the iteration the current block width began at
   std::vector<std::pair<int, int>> segments;
-  auto compact = [&]() -> int {
-    SP_TRY(hipStreamSynchronize(str));
-    std::vector<int> act(s);
-    SP_TRY(hipMemcpy(act.data(), sc[it & 1].active, sizeof(int) * s, hipMemcpyDeviceToHost));
-    std::vector<int> map;
-    for (int c = 0; c < s; ++c)
-      if (act[c]) map.push_back(c);
-    const int a = (int)map.size();
-    if (a == 0 || 2 * a > s) return 0;
-    {
-      std::vector<double> g((size_t)S * nbd * s);
-      SP_TRY(hipMemcpy(g.data(), sh.g, sizeof(double) * g.size(), hipMemcpyDeviceToHost));
-      for (int c = 0; c < s; ++c) {
-        if (act[c]) continue;
-        for (int jc = 0; jc < S * nbd; ++jc)
-          g_final[(size_t)jc * s0 + orig[c]] = g[(size_t)jc * s + c];
-      }
+  // narrow the block once at most half of its columns still iterate (one column left
+  // always qualifies; waiting for three quarters measured the same at cfg 4 and 5)
+  auto keep_target = [&]() { return std::max(1, s / 2); };
+  // The compaction, asynchronous (round 6): the kept columns are those active in the
+  // pinned slot rd the host has just read (a column that stopped since idles in the new
+  // block until the next compaction or the end). One launch on the CG's stream gathers
+  // the state into the other compaction buffer and scatters the dropped columns' final
+  // Grams into gfin; the host only switches its pointers. The slot rd is behind every
+  // iteration queued so far, or the last batch's slot, either way the stream orders it.
+  auto compact = [&](int rd) -> int {
+    int map[MS_MAXS], drop[MS_MAXS];
+    int a = 0, nd = 0;
+    for (int c = 0; c < s; ++c) {
+      if (pin[rd].act[c]) map[a++] = c;
+      else drop[nd++] = c;
     }
+    if (a == 0 || a > keep_target() || nd == 0) return 0;
     const size_t na = even((size_t)n * a);
     const size_t cneed = 3 * na + (size_t)MS_UB * nbd * a + 2 * 5 * (size_t)a + (size_t)a +
-                         4 * (size_t)S * nbd * a + (size_t)a + 2;
+                         4 * (size_t)S * nbd * a + 2;
     const int cb = compactions & 1;   // (the current block may live in the other one)
     if (sp->ms_cbuf_doubles[cb] < cneed) {
       if (sp->ms_cbuf[cb]) SP_TRY(hipFree(sp->ms_cbuf[cb]));
@@ -1573,8 +1583,7 @@ static int msgram_cg2(gpmi_sp* sp, const double* etas, int neta, const double* r
       sp->ms_cbuf_doubles[cb] = cneed;
     }
     double* cq = sp->ms_cbuf[cb];
-    // the compacted block lives in ms_cbuf; the three vector slots rotate through it
-    // and the old block's buffers are left alone
+    // the compacted block lives in ms_cbuf; the old block's buffers are left alone
     double* Rn = cq; cq += na;
     double* Wn = cq; cq += na;
     double* Sn = cq; cq += na;
@@ -1593,33 +1602,47 @@ static int msgram_cg2(gpmi_sp* sp, const double* etas, int neta, const double* r
     shn.z_prev = cq; cq += (size_t)S * a;
     shn.bp = cq; cq += (size_t)S * nbd * a;
     shn.g = cq; cq += (size_t)S * nbd * a;
-    int* mapd = reinterpret_cast<int*>(cq);
-    SP_TRY(hipMemcpyAsync(mapd, map.data(), sizeof(int) * a, hipMemcpyHostToDevice, str));
-    auto gather = [&](const double* src, int64_t rows, int L, double* dst) {
-      const int64_t tot = rows * a * L;
-      const unsigned g = (unsigned)std::min<int64_t>(2048, (tot + 255) / 256);
-      hipLaunchKernelGGL(ms_cols_gather_kernel, dim3(std::max(1u, g)), dim3(256), 0, str, src,
-                         rows, s, (const int*)mapd, a, L, dst);
-    };
     const MsScal& cur = sc[it & 1];
     MsScal& ncur = scn[it & 1];
-    gather(Rd, n, 1, Rn);
-    gather(Sd, n, 1, Sn);
-    gather(bpart, nbd, MS_UB, bpn);   // [cp s + c][vb] -> [cp a + c'][vb]
-    gather(cur.rr, 1, 1, ncur.rr);
-    gather(cur.a, 1, 1, ncur.a);
-    gather(cur.a_prev, 1, 1, ncur.a_prev);
-    gather(cur.beta, 1, 1, ncur.beta);
-    gather(sh.bn2, 1, 1, shn.bn2);
-    gather(sh.z, S, 1, shn.z);
-    gather(sh.z_prev, S, 1, shn.z_prev);
-    gather(sh.bp, (int64_t)S * nbd, 1, shn.bp);
-    gather(sh.g, (int64_t)S * nbd, 1, shn.g);
-    SP_LAUNCH("ms_cols_gather_kernel");
-    hipLaunchKernelGGL(ms_set_active_kernel, dim3(1), dim3(64), 0, str, ncur.active, a);
-    SP_LAUNCH("ms_set_active_kernel");
-    SP_TRY(hipStreamSynchronize(str));
-    // host-side state in the new column order (no batch is in flight)
+    MsCompactArgs A{};
+    auto job = [&](const double* src, int64_t rows, int L, double* dst) {
+      A.job[A.njob++] = MsCompactJob{src, dst, rows, L, 0};
+    };
+    job(Rd, n, 1, Rn);
+    job(Sd, n, 1, Sn);
+    job(bpart, nbd, MS_UB, bpn);   // [cp s + c][vb] -> [cp a + c'][vb]
+    job(cur.rr, 1, 1, ncur.rr);
+    job(cur.a, 1, 1, ncur.a);
+    job(cur.a_prev, 1, 1, ncur.a_prev);
+    job(cur.beta, 1, 1, ncur.beta);
+    job(sh.bn2, 1, 1, shn.bn2);
+    job(sh.z, S, 1, shn.z);
+    job(sh.z_prev, S, 1, shn.z_prev);
+    job(sh.bp, (int64_t)S * nbd, 1, shn.bp);
+    job(sh.g, (int64_t)S * nbd, 1, shn.g);
+    A.s = s;
+    A.a = a;
+    A.nd = nd;
+    A.s0 = s0;
+    for (int q = 0; q < a; ++q) A.map[q] = map[q];
+    for (int d = 0; d < nd; ++d) {
+      A.drop[d] = drop[d];
+      A.drop_orig[d] = orig[drop[d]];
+    }
+    A.g = sh.g;
+    A.gfin = sp->ms_gfin;
+    A.SN = (int64_t)S * nbd;
+    A.act_src = cur.active;
+    A.act = ncur.active;
+    int64_t most = A.SN * nd;
+    for (int q = 0; q < A.njob; ++q)
+      most = std::max<int64_t>(most, A.job[q].rows * a * A.job[q].L);
+    const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>(1024, (most + 255) / 256));
+    hipLaunchKernelGGL(ms_compact_kernel, dim3(gx, A.njob + 1), dim3(256), 0, str, A);
+    SP_LAUNCH("ms_compact_kernel");
+    // host-side state in the new column order (pin's bn2 is written once, at the start;
+    // a batch still in flight writes its old-order end state into the slot after rd's,
+    // which is rewritten by the next batch before it is read)
     std::vector<int> norig(a);
     std::vector<double> nrr(a);
     for (int q = 0; q < a; ++q) {
@@ -1693,7 +1716,7 @@ static int msgram_cg2(gpmi_sp* sp, const double* etas, int neta, const double* r
     const double rem = std::min((double)maxiter, std::ceil((double)at + needm)) - (double)it;
     need_after = (int)std::max(-1.0, rem);
     compact_at = -1;
-    const int k = nact - s / 2;   // columns that must stop before the block can narrow
+    const int k = nact - keep_target();   // columns that must stop before the block narrows
     if (compact_on && s > 1 && any && k >= 1 && forced_reads < 2) {
       std::nth_element(stops.begin(), stops.begin() + (k - 1), stops.end());
       const double tk = stops[k - 1];
@@ -1726,7 +1749,7 @@ static int msgram_cg2(gpmi_sp* sp, const double* etas, int neta, const double* r
     auto compactable = [&](int q) {
       int nact = 0;
       for (int c = 0; c < s; ++c) nact += pin[q].act[c] ? 1 : 0;
-      return 2 * nact <= s;
+      return nact <= keep_target();
     };
     const bool can_compact = compact_on && s > 1 && it < maxiter;
     // the stop, or the compaction, predicted within the iterations queued: read them now
@@ -1741,7 +1764,7 @@ static int msgram_cg2(gpmi_sp* sp, const double* etas, int neta, const double* r
       if (due && !compactable(qs)) ++forced_reads;
     }
     if (can_compact && read >= 0 && compactable(read)) {
-      if ((rc = compact())) return rc;
+      if ((rc = compact(read))) return rc;
       compact_at = -1;   // (a prediction for the old block)
     }
     nb = std::max(1, std::min(MS_BATCH, need_after));
@@ -1759,6 +1782,12 @@ static int msgram_cg2(gpmi_sp* sp, const double* etas, int neta, const double* r
   SP_TRY(hipMemcpyAsync(&it_stop, sh.it_stop, sizeof(int), hipMemcpyDeviceToHost, str));
   std::vector<double> hg((size_t)S * nbd * s);
   SP_TRY(hipMemcpyAsync(hg.data(), sh.g, sizeof(double) * hg.size(), hipMemcpyDeviceToHost, str));
+  std::vector<double> g_final;   // [j][cp][c original], the dropped columns' entries
+  if (compactions > 0) {
+    g_final.resize((size_t)S * nbd * s0);
+    SP_TRY(hipMemcpyAsync(g_final.data(), sp->ms_gfin, sizeof(double) * g_final.size(),
+                          hipMemcpyDeviceToHost, str));
+  }
   SP_TRY(hipStreamSynchronize(str));
   sp->last_compactions = compactions;
   segments.emplace_back(s, it - seg_start);
@@ -1768,8 +1797,8 @@ static int msgram_cg2(gpmi_sp* sp, const double* etas, int neta, const double* r
   bool any = false;
   for (int c = 0; c < s; ++c) any = any || hact[c];
   sp->last_converged = any ? 0 : 1;
-  // each original column from the current block, or from the host copy its compaction
-  // kept when it stopped
+  // each original column from the current block, or from the final Grams its
+  // compaction scattered when it was dropped
   std::vector<int> where(s0, -1);
   for (int c = 0; c < s; ++c) where[orig[c]] = c;
   for (int j = 0; j < S; ++j)
