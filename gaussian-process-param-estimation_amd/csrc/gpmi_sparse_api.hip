@@ -1700,7 +1700,10 @@ static int msgram_cg2(gpmi_sp* sp, const double* etas, int neta, const double* r
       if (!pin[qs].act[c]) continue;
       any = true;
       ++nact;
-      const double r1 = pin[qs].rr[c], r0 = rr_seen[c], target = rtol * rtol * pin[qs].bn2[c];
+      // (at the first read the rate is from r_0 = b: ||r_0||^2 = ||b||^2, so the first
+      // batches need no wait for a second read)
+      const double r1 = pin[qs].rr[c], target = rtol * rtol * pin[qs].bn2[c];
+      const double r0 = rr_seen[c] < 0.0 && it_seen == 0 ? pin[qs].bn2[c] : rr_seen[c];
       double m = (double)MS_BATCH;
       bool rated = false;
       if (r0 > 0.0 && r1 > 0.0 && r1 < r0 && at > it_seen && target > 0.0) {
