@@ -1684,7 +1684,6 @@ static int msgram_cg2(gpmi_sp* sp, const double* etas, int neta, const double* r
   int need_after = maxiter;
   int compact_at = -1;
   int forced_reads = 0;   // compaction reads that found too few columns stopped
-  bool due_pending = false;   // the batch that reached compact_at is read next round
   std::vector<double> stops;
   auto read_slot = [&](int qs) -> int {
     SP_TRY(hipEventSynchronize(sp->ms_ev[qs]));
@@ -1743,42 +1742,37 @@ static int msgram_cg2(gpmi_sp* sp, const double* etas, int neta, const double* r
     ++kb;
     need_after -= nb;
     int read = -1;   // the slot read this round (its flags drive the compaction)
-    auto compactable = [&](int q) {
-      int nact = 0;
-      for (int c = 0; c < s; ++c) nact += pin[q].act[c] ? 1 : 0;
-      return nact <= keep_target();
-    };
     if (prev) {
       const int r = read_slot(qs ^ 1);
       if (r == 2) break;
       if (r) return r;
       read = qs ^ 1;
-      if (due_pending && !compactable(read)) ++forced_reads;
     }
-    due_pending = false;
     prev = true;
+    auto compactable = [&](int q) {
+      int nact = 0;
+      for (int c = 0; c < s; ++c) nact += pin[q].act[c] ? 1 : 0;
+      return nact <= keep_target();
+    };
     const bool can_compact = compact_on && s > 1 && it < maxiter;
-    // the stop predicted within the iterations queued: wait for them and read them now
-    if (need_after <= 0) {
+    // the stop, or the compaction, predicted within the iterations queued: read them now
+    const bool due = can_compact && compact_at >= 0 && compact_at <= it &&
+                     !(read >= 0 && compactable(read));
+    if (need_after <= 0 || due) {
       const int r = read_slot(qs);
       if (r == 2) break;
       if (r) return r;
       prev = false;
       read = qs;
+      if (due && !compactable(qs)) ++forced_reads;
     }
-    // the compaction predicted within them: queue ONE more iteration and read them next
-    // round, while it runs (a wait here would leave the device idle for the host's turn)
-    const bool due = can_compact && prev && compact_at >= 0 && compact_at <= it &&
-                     !(read >= 0 && compactable(read));
-    if (due) due_pending = true;
     if (can_compact && read >= 0 && compactable(read)) {
       if ((rc = compact(read))) return rc;
       compact_at = -1;   // (a prediction for the old block)
     }
     nb = std::max(1, std::min(MS_BATCH, need_after));
     // end the batch where the block is predicted to narrow
-    if (due_pending) nb = 1;
-    else if (compact_on && s > 1 && compact_at > it && compact_at < it + nb) nb = compact_at - it;
+    if (compact_on && s > 1 && compact_at > it && compact_at < it + nb) nb = compact_at - it;
   }
   // the last step of columns still active at maxiter (a no-op when all stopped)
   if (trace) std::fprintf(stderr, "[ms] loop end: launched %d\n", it);
