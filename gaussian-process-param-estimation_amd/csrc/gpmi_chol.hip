@@ -59,6 +59,9 @@ __global__ __launch_bounds__(256) void shift_copy_kernel(
 // Panel: for row tile I = kb + 1 + blockIdx.x of member b = blockIdx.y:
 //   L_Ik = A_Ik Linv_kk^T (in place)  and  r_I -= A_Ik u_k.
 // ---------------------------------------------------------------------------
+#ifndef GPMI_PROBE_PANEL_NO_RHS
+#define GPMI_PROBE_PANEL_NO_RHS 0
+#endif
 __global__ __launch_bounds__(256, 2) void panel_kernel(BatchPtrs P, int64_t lda, int kb) {
   __shared__ double smem[4 * STAGE + TS * RLD];
   double* sA = smem;
@@ -70,7 +73,7 @@ __global__ __launch_bounds__(256, 2) void panel_kernel(BatchPtrs P, int64_t lda,
   const int I = kb + 1 + blockIdx.x;
   double* A = P.A + b * P.sA;
   const double* U = P.U + b * P.sU;
-  {
+  if (!GPMI_PROBE_PANEL_NO_RHS) {
     d2 v[4];
 #pragma unroll
     for (int it = 0; it < 4; ++it)
@@ -87,7 +90,13 @@ __global__ __launch_bounds__(256, 2) void panel_kernel(BatchPtrs P, int64_t lda,
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = d4{0.0, 0.0, 0.0, 0.0};
   racc[0] = racc[1] = d4{0.0, 0.0, 0.0, 0.0};
+#if GPMI_PROBE_PANEL_NO_RHS
+  // timing probe only (wrong results): the panel without its RHS operand, the bound on
+  // what folding r_I -= L_Ik y_k into the SYRK could save (round 6, verdict item 7)
+  tile_mma<false>(Aik, lda, Li, TS, TS, sA, sB, acc, sU, racc);
+#else
   tile_mma<true>(Aik, lda, Li, TS, TS, sA, sB, acc, sU, racc);
+#endif
   // C/D map of v_mfma_f64_16x16x4f64: row = (lane>>4) + 4*r, col = lane&15.
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -98,6 +107,9 @@ __global__ __launch_bounds__(256, 2) void panel_kernel(BatchPtrs P, int64_t lda,
         Aik[(int64_t)(wr * 64 + i * 16 + fk + 4 * r) * lda + wc * 64 + j * 16 + fr] =
             acc[i][j][r];
   double* R = P.R + b * P.sR + (int64_t)I * TS * RLD;
+#if GPMI_PROBE_PANEL_NO_RHS
+  return;
+#endif
 #pragma unroll
   for (int h = 0; h < 2; ++h)
 #pragma unroll
