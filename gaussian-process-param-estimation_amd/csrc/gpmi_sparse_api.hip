@@ -13,7 +13,6 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
-#include <cstring>
 #include <mutex>
 #include <map>
 #include <vector>
@@ -1371,13 +1370,13 @@ static int msgram_cg2(gpmi_sp* sp, const double* etas, int neta, const double* r
   const int nbd = full ? s : nrhs;
   const int64_t nsb = n * nbd;
   if (!sp->ms_stream) {
-    // the CG's stream at the high dispatch priority: beside the Lanczos (the sweep's
-    // other stream, which has slack: its host-side quadrature waits for the CG
-    // anyway) the CG's dependent launches go first. cfg 5 step 11.85 -> 11.46 ms
-    // (low priority: 11.92), cfg 4 unchanged (3.21 ms)
-    int lo = 0, hi = 0;
-    SP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
-    SP_TRY(hipStreamCreateWithPriority(&sp->ms_stream, hipStreamNonBlocking, hi));
+    // the CG's own stream, at the same (normal) dispatch priority as the Lanczos's.
+    // Round 5 gave it the high priority (cfg 5 11.85 -> 11.46 ms, when the CG alone took
+    // 8.8 ms); since the compaction the CG alone takes 6.4 ms and a starved Lanczos (4.1
+    // ms alone) plus its host-side quadrature became the step's tail: round 6 alternating
+    // runs, high / normal / low: cfg 5 9.80-9.92 / 9.40-9.44 / 9.77-10.05 ms, cfg 4
+    // 2.86-2.90 / 2.80-2.82 / 2.83-2.86 ms.
+    SP_TRY(hipStreamCreateWithFlags(&sp->ms_stream, hipStreamNonBlocking));
   }
   int64_t ns = n * s;
   const int s0 = s;   // the block's width at the start (compaction narrows s)

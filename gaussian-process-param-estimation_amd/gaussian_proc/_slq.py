@@ -198,6 +198,14 @@ def quadrature(node_list, etas, fn, check=True):
     etas = numpy.atleast_1d(numpy.asarray(etas, dtype=float))
     if check:
         check_shifts(min_ritz(node_list), etas)
+    if node_list and len({theta.size for theta, _ in node_list}) == 1:
+        # every probe's rule has the same length (the rule): one array op over
+        # [probe, eta, node]; the node sums run along the contiguous last axis as in
+        # the per-probe form, so the values are the same bits (round 6: 0.38 -> 0.2 ms
+        # of host time per cfg 5 step)
+        th = numpy.stack([theta for theta, _ in node_list])
+        w = numpy.stack([w for _, w in node_list])
+        return numpy.sum(w[:, None, :] * fn(th[:, None, :] + etas[None, :, None]), axis=2)
     q = numpy.empty((len(node_list), etas.size))
     for p, (theta, w) in enumerate(node_list):   # all eta of a probe in one array op
         q[p] = numpy.sum(w[None, :] * fn(theta[None, :] + etas[:, None]), axis=1)

@@ -192,3 +192,23 @@ def test_next_lanczos_degree_extrapolates_the_gap():
     assert _next_degree([(40, 1e-3), (48, 2e-3)], 1e-6) == 96      # gap grew: double
     assert _next_degree([(40, 1e-5), (80, 1.01e-6)], 1e-6) == 96   # 1.1 x 80.2, rounded up
     assert _next_degree([(40, 1e-5), (41, 1e-12)], 1e-6) == 49     # at least 8 more
+
+
+def test_quadrature_batched_equals_per_probe_bits():
+    """_slq.quadrature forms every probe's sums in one array op when the rules have
+    one length (round 6); the values are the per-probe loop's bits. Ragged rules
+    (a probe that broke down early) take the per-probe loop."""
+    from gaussian_proc import _slq
+    rng = numpy.random.RandomState(4)
+    etas = numpy.logspace(-2, 2, 32)
+    for k in (1, 7, 30, 61):
+        nodes = [(numpy.sort(rng.rand(k) * 3 + 0.1), rng.rand(k)) for _ in range(20)]
+        for fn in _slq.FUNCS.values():
+            ref = numpy.array([numpy.sum(w[None, :] * fn(t[None, :] + etas[:, None]), axis=1)
+                               for t, w in nodes])
+            numpy.testing.assert_array_equal(_slq.quadrature(nodes, etas, fn, check=False), ref)
+    ragged = [(numpy.sort(rng.rand(k) * 3 + 0.1), rng.rand(k)) for k in (30, 12, 30)]
+    q = _slq.quadrature(ragged, etas, numpy.log, check=False)
+    for p, (t, w) in enumerate(ragged):
+        numpy.testing.assert_array_equal(
+            q[p], numpy.sum(w[None, :] * numpy.log(t[None, :] + etas[:, None]), axis=1))
