@@ -799,6 +799,37 @@ def test_msgram_repeated_compactions_bit_identical(gp, monkeypatch):
         assert numpy.max(numpy.abs(G1[j] - ref)) <= 1e-9 * numpy.abs(ref).max()
 
 
+def test_msgram_compaction_then_maxiter_bit_identical(gp, monkeypatch):
+    """A block that narrows (four columns stop within a few iterations) and then
+    reaches maxiter with its two random columns still active: the last step lands in
+    the compacted block (ms_cg2_close_kernel on it), the stopped columns' Grams come
+    from the device array their compaction wrote, and everything equals the
+    uncompacted block bit for bit."""
+    from gaussian_proc import _hip
+    _, K = _small_sparse()
+    Kd = K.toarray()
+    n = Kd.shape[0]
+    lam, U = numpy.linalg.eigh(Kd)
+    B = numpy.empty((n, 6))
+    for c in range(4):
+        B[:, c] = U[:, -1 - c] + 0.5 * U[:, -2 - c]
+    B[:, 4:] = numpy.random.RandomState(5).randn(n, 2)
+    etas = numpy.array([3.0, 6.0])
+    sop = _hip.SparseOperator.from_csr(K)
+    for maxiter in (17, 24):
+        monkeypatch.setenv('GPMI_MS_COMPACT', '0')
+        with pytest.warns(RuntimeWarning):
+            G0 = sop.msgram(etas, B, rtol=1e-13, maxiter=maxiter)
+        monkeypatch.setenv('GPMI_MS_COMPACT', '1')
+        with pytest.warns(RuntimeWarning):
+            G1 = sop.msgram(etas, B, rtol=1e-13, maxiter=maxiter)
+        assert sop.msgram_compactions() >= 1, sop.msgram_segments()
+        numpy.testing.assert_array_equal(G1, G0)
+        for j, eta in enumerate(etas):   # the quick columns are solved
+            ref = B.T @ numpy.linalg.solve(Kd + eta * numpy.eye(n), B[:, :4])
+            assert numpy.max(numpy.abs(G1[j][:, :4] - ref)) <= 1e-9 * numpy.abs(ref).max()
+
+
 def test_msgram_large_shifts_stay_finite(gp):
     """A large shift's zeta decays like (1 + d alpha)^-k and underflows to 0 within
     the seed system's iterations; alpha^s = alpha zeta_k / zeta_{k-1} was then 0 / 0
