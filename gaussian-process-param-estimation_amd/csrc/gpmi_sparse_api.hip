@@ -1562,8 +1562,9 @@ static int msgram_cg2(gpmi_sp* sp, const double* etas, int neta, const double* r
   // pinned slot rd the host has just read (a column that stopped since idles in the new
   // block until the next compaction or the end). One launch on the CG's stream gathers
   // the state into the other compaction buffer and scatters the dropped columns' final
-  // Grams into gfin; the host only switches its pointers. The slot rd is behind every
-  // iteration queued so far, or the last batch's slot, either way the stream orders it.
+  // Grams into gfin; the host only switches its pointers. The slot rd was written by the
+  // last batch or the one before it; the gathers are queued behind every iteration, so
+  // they see the state at iteration `it` whichever it was.
   auto compact = [&](int rd) -> int {
     int map[MS_MAXS], drop[MS_MAXS];
     int a = 0, nd = 0;
